@@ -1,0 +1,158 @@
+"""Synthetic 2-D jet meshes and their vertex-centred median dual.
+
+Host-side setup, not the hot path. Replicates the layout of the reference's jet combustor mesh
+(`Test_Cases/TURBOLENT/TURBOLENT_COMBUSTION/mesh_stretched.su2`: 0.125 x 0.006 m box; markers
+Oxidizer_Inlet (left), Outlet (right), upper_wall (top), and a bottom wall split 20:39:40 into
+lower_wall_pre / Fuel_Inlet / lower_wall_post) at any nx x ny resolution.
+
+The dual grid follows the reference construction:
+  * edges i<j, normal oriented from i to j, accumulated per element face from the edge midpoint to
+    the element centroid (`Common/src/dual_grid_structure.cpp:505-530`,
+    `Common/src/geometry_structure.cpp` CPhysicalGeometry::SetControlVolume, 2-D branch);
+  * dual volume = sum of the triangles (point, edge midpoint, element centroid);
+  * boundary vertex normals from the boundary line elements
+    (`Common/src/geometry_structure.cpp` CPhysicalGeometry::SetBoundControlVolume, 2-D branch).
+Edge order is lexicographic in (i, j) after the point ordering (reference `CGeometry::SetEdges`
+discovers edges point by point over sorted neighbour lists, `geometry_structure.cpp:223-252`).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+MARKERS = ("Oxidizer_Inlet", "Outlet", "upper_wall", "Fuel_Inlet", "lower_wall_pre", "lower_wall_post")
+# bottom split of the reference mesh: 20 : 39 : 40 elements out of 99
+BOTTOM_SPLIT = (20, 39, 40)
+
+
+def jet_points(nx: int, ny: int, length=0.125, height=0.006, stretch=1.5):
+    """Structured nx x ny points (x fastest), tanh-clustered towards both walls in y."""
+    x = np.linspace(0.0, length, nx)
+    s = np.linspace(-1.0, 1.0, ny)
+    y = 0.5 * height * (1.0 + np.tanh(stretch * s) / np.tanh(stretch))
+    y[0], y[-1] = 0.0, height
+    X, Y = np.meshgrid(x, y)  # (ny, nx)
+    return np.stack([X.ravel(), Y.ravel()], axis=1)
+
+
+def jet_mesh(nx: int, ny: int, **kw):
+    """Points, counter-clockwise quads and boundary line elements per marker."""
+    pts = jet_points(nx, ny, **kw)
+    pid = np.arange(nx * ny).reshape(ny, nx)
+    quads = np.stack([pid[:-1, :-1].ravel(), pid[:-1, 1:].ravel(), pid[1:, 1:].ravel(), pid[1:, :-1].ravel()], axis=1)
+    nxe = nx - 1
+    a = round(nxe * BOTTOM_SPLIT[0] / 99.0)
+    b = round(nxe * (BOTTOM_SPLIT[0] + BOTTOM_SPLIT[1]) / 99.0)
+    bottom = np.stack([pid[0, :-1], pid[0, 1:]], axis=1)
+    bnd = {
+        "Oxidizer_Inlet": np.stack([pid[1:, 0], pid[:-1, 0]], axis=1),
+        "Outlet": np.stack([pid[:-1, -1], pid[1:, -1]], axis=1),
+        "upper_wall": np.stack([pid[-1, 1:], pid[-1, :-1]], axis=1),
+        "Fuel_Inlet": bottom[a:b],
+        "lower_wall_pre": bottom[:a],
+        "lower_wall_post": bottom[b:],
+    }
+    return pts, quads, bnd
+
+
+def write_su2(path: str, pts, quads, bnd):
+    with open(path, "w") as f:
+        f.write("NDIME= 2\n")
+        f.write(f"NELEM= {len(quads)}\n")
+        for k, q in enumerate(quads):
+            f.write(f"9 {q[0]} {q[1]} {q[2]} {q[3]} {k}\n")
+        f.write(f"NPOIN= {len(pts)}\n")
+        for k, p in enumerate(pts):
+            f.write(f"{p[0]:.17g} {p[1]:.17g} {k}\n")
+        f.write(f"NMARK= {len(bnd)}\n")
+        for name in MARKERS:
+            lines = bnd[name]
+            f.write(f"MARKER_TAG= {name}\nMARKER_ELEMS= {len(lines)}\n")
+            for l in lines:
+                f.write(f"3 {l[0]} {l[1]}\n")
+
+
+def rcm_order(n, edges):
+    """Reverse Cuthill-McKee permutation (new -> old) of the point graph."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    i, j = edges[:, 0], edges[:, 1]
+    A = sp.coo_matrix((np.ones(2 * len(i)), (np.r_[i, j], np.r_[j, i])), shape=(n, n)).tocsr()
+    return np.asarray(reverse_cuthill_mckee(A, symmetric_mode=True), dtype=np.int64)
+
+
+def median_dual(pts, quads, bnd):
+    """Edges (i<j), edge normals, dual volumes, neighbour CSR and boundary vertices.
+
+    Vectorised restatement of the reference 2-D dual construction (see module docstring).
+    """
+    n = len(pts)
+    cg = pts[quads].mean(axis=1)  # element centroids
+    faces = np.stack([quads, np.roll(quads, -1, axis=1)], axis=2).reshape(-1, 2)  # (4*nelem, 2)
+    fcg = np.repeat(cg, 4, axis=0)
+    lo = np.minimum(faces[:, 0], faces[:, 1])
+    hi = np.maximum(faces[:, 0], faces[:, 1])
+    key = lo * n + hi
+    ukey, inv = np.unique(key, return_inverse=True)
+    edges = np.stack([ukey // n, ukey % n], axis=1).astype(np.int64)
+    emid = 0.5 * (pts[edges[:, 0]] + pts[edges[:, 1]])
+    # normal contribution: (Elem_CG - Edge_CG) rotated, oriented from lo to hi
+    d = fcg - emid[inv]
+    contrib = np.stack([d[:, 1], -d[:, 0]], axis=1)
+    flip = faces[:, 0] > faces[:, 1]
+    contrib[flip] *= -1.0
+    # orientation: the reference takes the element CG on the left of the oriented face; our quads
+    # are counter-clockwise, so the centroid is on the left of (face0 -> face1)
+    normal = np.zeros((len(edges), 2))
+    np.add.at(normal, inv, -contrib)
+    # dual volumes: triangles (point, edge midpoint, element centroid) on both face ends
+    vol = np.zeros(n)
+    for end in (0, 1):
+        p = pts[faces[:, end]]
+        a = emid[inv] - p
+        b = fcg - p
+        np.add.at(vol, faces[:, end], 0.5 * np.abs(a[:, 0] * b[:, 1] - a[:, 1] * b[:, 0]))
+    # neighbour CSR (sorted)
+    nb_i = np.r_[edges[:, 0], edges[:, 1]]
+    nb_j = np.r_[edges[:, 1], edges[:, 0]]
+    order = np.lexsort((nb_j, nb_i))
+    nb_i, nb_j = nb_i[order], nb_j[order]
+    nbr_ptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(nbr_ptr, nb_i + 1, 1)
+    nbr_ptr = np.cumsum(nbr_ptr)
+    # boundary vertex normals: each line element gives half its outward normal to each end
+    bverts = []
+    for m, name in enumerate(MARKERS):
+        lines = bnd[name]
+        acc = {}
+        for l in lines:
+            p0, p1 = pts[l[0]], pts[l[1]]
+            t = p1 - p0
+            half = 0.5 * np.array([t[1], -t[0]])
+            for v in (l[0], l[1]):
+                acc[v] = acc.get(v, 0.0) + half
+        for v in sorted(acc):
+            bverts.append((m, v, acc[v][0], acc[v][1]))
+    bv = np.array([(b[0], b[1]) for b in bverts], dtype=np.int64)
+    bn = np.array([(b[2], b[3]) for b in bverts], dtype=np.float64)
+    return dict(edges=edges, edge_normal=normal, volume=vol, nbr_ptr=nbr_ptr, nbr=nb_j.astype(np.int64),
+                bvertex=bv, bvertex_normal=bn)
+
+
+def renumber(pts, quads, bnd, perm):
+    """Apply a new->old permutation to points and connectivity."""
+    old2new = np.empty_like(perm)
+    old2new[perm] = np.arange(len(perm))
+    return pts[perm], old2new[quads], {k: old2new[v] for k, v in bnd.items()}, old2new
+
+
+def build_jet(nx: int, ny: int, rcm: bool = True, **kw):
+    """Synthetic jet mesh ready for the solver: RCM-ordered points + median dual."""
+    pts, quads, bnd = jet_mesh(nx, ny, **kw)
+    if rcm:
+        d0 = median_dual(pts, quads, bnd)
+        perm = rcm_order(len(pts), d0["edges"])
+        pts, quads, bnd, _ = renumber(pts, quads, bnd, perm)
+    dual = median_dual(pts, quads, bnd)
+    dual["coord"] = pts
+    dual["quads"] = quads
+    return dual

@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Generate golden vectors from the compiled reference (TEST INFRASTRUCTURE, runs only where
+/root/reference exists).
+
+Steps per case:
+  1. build oracle/_ref/harness (oracle/ref_build.mk: reference sources compiled as they lie);
+  2. lay out a work dir with a cfg written here, the mesh and the reference's own library data
+     files (Test_Cases/TURBOLENT/TURBOLENT_COMBUSTION/{Mixture,Chemistry,Thermo,Transp}, read in
+     place through symlinks, never copied into the repo);
+  3. write the state (conservatives + SST k, omega) from the reference's converged PaSR field
+     `PLOT/flow_second_chem.dat` (nearest-point sampling for coarser synthetic meshes);
+  4. run the harness, which drives the reference's own preprocessing and operators;
+  5. pack the dumped arrays into tests/golden/<case>.npz (+ the mechanism tables the oracle and the
+     HIP path need, parsed here by oracle/mech.py from the same files).
+
+Cases:
+  mini9 : 21 x 11 synthetic jet (same markers), 9 species, SST, implicit, full loops + BSR +
+          LU-SGS / ILU0 / FGMRES dumps.
+  jet9w : the reference's 9000-point mesh_stretched.su2 with the converged PaSR state, 2nd order
+          + Venkatakrishnan limiter enabled, implicit; a window of ~700 points around the flame
+          is kept (all inputs, per-edge residuals, sampled Jacobians).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = os.environ.get("RX_REFERENCE", "/root/reference")
+CASE_DIR = os.path.join(REF, "Test_Cases/TURBOLENT/TURBOLENT_COMBUSTION")
+PKG = os.path.join(REPO, "development-of-a-turbulent-numerical-solver-for-reactive-flows-in-su2_amd")
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+meshgen = _load("rx_meshgen", os.path.join(PKG, "meshgen.py"))
+
+CFG_TEMPLATE = """\
+% golden-vector cfg written by oracle/make_golden.py (keys of the reference's cfg grammar)
+CONFIG_LIB_FILE = test_chem_second.txt
+FREESTREAM_MASS_FRAC = (0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+SPECIES_ORDER = (C4H6, H2O, O2, CO, CO2, H2, O, OH, H)
+PHYSICAL_PROBLEM= REACTIVE_NAVIER_STOKES
+KIND_TURB_MODEL= SST
+MATH_PROBLEM= DIRECT
+RESTART_SOL= NO
+IGNITION = NO
+MACH_NUMBER= 0.01819
+FREESTREAM_TEMPERATURE= 300.0
+FREESTREAM_VELOCITY= (6.0, 0.0, 0.0)
+FREESTREAM_PRESSURE= 130000.0
+REYNOLDS_LENGTH= 0.125
+REF_DIMENSIONALIZATION= DIMENSIONAL
+REF_LENGTH= 0.125
+REF_AREA= 0
+MARKER_ISOTHERMAL = (upper_wall, 300.0, lower_wall_pre, 300.0, lower_wall_post, 600.0)
+INLET_TYPE = TEMPERATURE_IMPOSE
+MARKER_INLET= ( Oxidizer_Inlet, 300.0, 20.0, 1.0, 0.0, 0.0, Fuel_Inlet, 800.0, 0.87, 0.0, 1.0, 0.0)
+INLET_MASS_FRAC = (Oxidizer_Inlet, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0; Fuel_Inlet, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+MARKER_OUTLET= ( Outlet, 101325.0)
+NUM_METHOD_GRAD= WEIGHTED_LEAST_SQUARES
+CFL_NUMBER= {cfl}
+CFL_ADAPT= NO
+EXT_ITER= 1
+LINEAR_SOLVER= FGMRES
+LINEAR_SOLVER_PREC= {prec}
+LINEAR_SOLVER_ERROR= 1E-6
+LINEAR_SOLVER_ITER= 5
+MGLEVEL= 0
+CONV_NUM_METHOD_FLOW= AUSM
+SPATIAL_ORDER_FLOW= {order}
+SLOPE_LIMITER_FLOW= VENKATAKRISHNAN
+TIME_DISCRE_FLOW= EULER_IMPLICIT
+CONV_NUM_METHOD_TURB= SCALAR_UPWIND
+SLOPE_LIMITER_TURB= VENKATAKRISHNAN
+TIME_DISCRE_TURB= EULER_IMPLICIT
+PASR_LB = 0.2
+CONV_CRITERIA= RESIDUAL
+RESIDUAL_REDUCTION= 6
+RESIDUAL_MINVAL= -4
+MESH_FILENAME= {mesh}
+MESH_FORMAT= SU2
+OUTPUT_FORMAT= TECPLOT
+CONV_FILENAME= history
+WRT_SOL_FREQ= 100000
+WRT_CON_FREQ= 1
+"""
+
+
+def read_plot(path):
+    rows = []
+    with open(path) as f:
+        for line in f:
+            t = line.split()
+            if not t:
+                continue
+            try:
+                vals = [float(x) for x in t]
+            except ValueError:
+                continue
+            if len(vals) >= 17:
+                rows.append(vals)
+    a = np.array(rows)
+    return a[:, :2], a[:, 2:17]  # coords, 13 flow conservatives + k + omega
+
+
+def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS"):
+    wd = os.path.join("/tmp/rx_golden", case)
+    shutil.rmtree(wd, ignore_errors=True)
+    os.makedirs(os.path.join(wd, "out"))
+    for d in ("Mixture", "Chemistry", "Thermo", "Transp"):
+        os.symlink(os.path.join(CASE_DIR, d), os.path.join(wd, d))
+    os.symlink(os.path.join(CASE_DIR, "test_chem_second.txt"), os.path.join(wd, "test_chem_second.txt"))
+    mesh_name = mesh_writer(wd)
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec))
+    return wd
+
+
+def write_state(wd, U):
+    with open(os.path.join(wd, "state.txt"), "w") as f:
+        for g, row in enumerate(U):
+            f.write(str(g) + " " + " ".join(f"{v:.17g}" for v in row) + "\n")
+
+
+def run_harness(wd, bsr):
+    exe = os.path.join(HERE, "_ref", "harness")
+    cmd = [exe, "case.cfg", "state.txt", "out"] + (["--bsr"] if bsr else [])
+    r = subprocess.run(cmd, cwd=wd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout[-4000:] + r.stderr[-4000:])
+        raise SystemExit(f"harness failed for {wd}")
+    arrays = {}
+    with open(os.path.join(wd, "out", "manifest.txt")) as f:
+        for line in f:
+            t = line.split()
+            name, dt, shape = t[0], t[1], tuple(int(s) for s in t[2:])
+            arrays[name] = np.fromfile(os.path.join(wd, "out", name + ".bin"), dtype="<" + dt).reshape(shape)
+    return arrays
+
+
+def mech_arrays():
+    mech = _load("rx_oracle_mech", os.path.join(HERE, "mech.py"))
+    m = mech.load_mechanism(CASE_DIR, "test_chem_second.txt")
+    return {"mech_" + k: v for k, v in m.items()}
+
+
+def case_mini9(nx=21, ny=11):
+    pts, quads, bnd = meshgen.jet_mesh(nx, ny)
+    xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    # nearest-point sampling of the converged field
+    from scipy.spatial import cKDTree
+    scale = np.array([1.0 / 0.125, 1.0 / 0.006])
+    _, idx = cKDTree(xy * scale).query(pts * scale)
+    U = cons[idx]
+
+    def writer(wd):
+        meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, quads, bnd)
+        return "mesh.su2"
+
+    wd = make_workdir("mini9", writer, cfl=5.0, order="1ST_ORDER")
+    write_state(wd, U)
+    a = run_harness(wd, bsr=True)
+    wd = make_workdir("mini9_ilu", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    write_state(wd, U)
+    b = run_harness(wd, bsr=True)
+    for k in ("ilu_factor", "ilu_rhs", "fgmres_ilu_x", "fgmres_ilu_info"):
+        a[k] = b[k]
+    assert np.array_equal(a["bsr_system"], b["bsr_system"])
+    # keep the fixture small: the assembled system + ILU factor stay whole, per-edge Jacobians are
+    # sampled (the whole-matrix assembly is checked against bsr_system)
+    del a["bsr_jac_residual"]
+    rng = np.random.default_rng(7)
+    js = np.sort(rng.choice(len(a["edges"]), size=96, replace=False))
+    a["jac_edge_sample"] = js
+    for k in ("conv_jac_i", "conv_jac_j", "visc_jac_i", "visc_jac_j"):
+        a[k] = a[k][js]
+    ns = rng.choice(len(a["coord"]), size=64, replace=False)
+    a["src_jac_sample"] = np.sort(ns)
+    a["src_jac"] = a["src_jac"][a["src_jac_sample"]]
+    a.update(mech_arrays())
+    a["gen_points"] = pts
+    a["gen_quads"] = quads
+    return a
+
+
+def case_jet9w():
+    def writer(wd):
+        os.symlink(os.path.join(CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
+        return "mesh.su2"
+
+    xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    wd = make_workdir("jet9", writer, cfl=0.1, order="2ND_ORDER_LIMITER")
+    write_state(wd, cons)
+    a = run_harness(wd, bsr=False)
+    # window around the flame: strongest species gradients in the burning region
+    coord = a["coord"]
+    T = a["V"][:, 0]
+    c = coord[np.argmax(T)]
+    box = (np.abs(coord[:, 0] - c[0]) < 0.008) & (np.abs(coord[:, 1] - c[1]) < 0.0025)
+    keep = np.nonzero(box)[0]
+    loc = -np.ones(len(coord), dtype=np.int64)
+    loc[keep] = np.arange(len(keep))
+    e = a["edges"]
+    ekeep = np.nonzero((loc[e[:, 0]] >= 0) & (loc[e[:, 1]] >= 0))[0]
+    nb_ptr, nb = a["nbr_ptr"], a["nbr"]
+    interior = np.array([all(loc[nb[nb_ptr[i]:nb_ptr[i + 1]]] >= 0) for i in keep])
+    out = {}
+    node_keys = ["coord", "volume", "global_index", "U", "V", "dPdU", "dTdU", "mu", "kappa", "cp", "Dij",
+                 "grad_prim", "limiter", "turb_k", "turb_omega", "mu_t", "sigma_k", "grad_k", "src_res",
+                 "src_jac", "limiter_out", "grad_lsq_out", "wall_distance"]
+    for k in node_keys:
+        out[k] = a[k][keep]
+    out["interior"] = interior
+    # local neighbour CSR restricted to interior points' full lists
+    lp, ln = [0], []
+    for i in keep:
+        nbl = loc[nb[nb_ptr[i]:nb_ptr[i + 1]]]
+        ln.extend(int(x) for x in nbl if x >= 0)
+        lp.append(len(ln))
+    out["nbr_ptr"] = np.array(lp, dtype=np.int64)
+    out["nbr"] = np.array(ln, dtype=np.int64)
+    out["edges"] = loc[e[ekeep]]
+    out["edge_normal"] = a["edge_normal"][ekeep]
+    for k in ("conv_res", "visc_res"):
+        out[k] = a[k][ekeep]
+    rng = np.random.default_rng(12345)
+    js = np.sort(rng.choice(len(ekeep), size=min(256, len(ekeep)), replace=False))
+    out["jac_edge_sample"] = js
+    for k in ("conv_jac_i", "conv_jac_j", "visc_jac_i", "visc_jac_j"):
+        out[k] = a[k][ekeep][js]
+    for k in ("dims", "mach_inf", "visc_params", "src_params", "limiter_params"):
+        out[k] = a[k]
+    # limiter_out at window points needs neighbours' V/grad too: keep only interior as checked
+    out.update(mech_arrays())
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", default="mini9,jet9w")
+    args = ap.parse_args()
+    subprocess.run(["make", "-s", "-f", os.path.join(HERE, "ref_build.mk"), "-j8", "all", "harness"], check=True,
+                   cwd=REPO)
+    gold = os.path.join(REPO, "tests", "golden")
+    os.makedirs(gold, exist_ok=True)
+    for case in args.cases.split(","):
+        a = {"mini9": case_mini9, "jet9w": case_jet9w}[case]()
+        path = os.path.join(gold, case + ".npz")
+        np.savez_compressed(path, **a)
+        print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,495 @@
+// Golden-vector harness: TEST INFRASTRUCTURE ONLY.
+//
+// Links against the reference SU2 reactive fork compiled from /root/reference by
+// oracle/ref_build.mk (objects in oracle/_ref/, git-ignored). It builds the reference's own
+// CFluidDriver on a cfg + mesh, overwrites the flow/turbulence solution with a supplied state,
+// runs the reference's own preprocessing and then calls the reference's own operators
+// (CNumerics::ComputeResidual / ComputeChemistry, CSolver loops, CSysMatrix/CSysSolve) and dumps
+// their inputs and outputs as raw little-endian arrays + a manifest. oracle/make_golden.py packs
+// them into tests/golden/*.npz. Nothing in here ships or is measured.
+//
+// Reference call sites reproduced (file:line relative to /root/reference):
+//   per-edge AUSM setters/call       SU2_CFD/src/solver_direct_reactive.cpp:2546-2552,2731-2743
+//   per-edge viscous setters/call    SU2_CFD/src/solver_direct_reactive.cpp:5312-5355
+//   per-cell chemistry setters/call  SU2_CFD/src/solver_direct_reactive.cpp:2803-2817
+//   ImplicitEuler system build       SU2_CFD/src/solver_direct_reactive.cpp:2350-2390
+#include "../../SU2_CFD/include/driver_structure.hpp"
+#include "../../SU2_CFD/include/solver_reactive.hpp"
+#include "../../SU2_CFD/include/numerics_reactive.hpp"
+
+#include <cstdio>
+#include <cstdint>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace {
+
+std::string g_out;
+std::ofstream g_manifest;
+
+template <typename T>
+void dump(const std::string& name, const std::vector<T>& v, const std::vector<long>& shape, const char* dtype) {
+  std::string path = g_out + "/" + name + ".bin";
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) { std::perror(path.c_str()); std::exit(3); }
+  if (!v.empty()) std::fwrite(v.data(), sizeof(T), v.size(), f);
+  std::fclose(f);
+  g_manifest << name << " " << dtype;
+  for (long s : shape) g_manifest << " " << s;
+  g_manifest << "\n";
+  g_manifest.flush();
+}
+void dumpd(const std::string& n, const std::vector<double>& v, const std::vector<long>& s) { dump(n, v, s, "f8"); }
+void dumpi(const std::string& n, const std::vector<int64_t>& v, const std::vector<long>& s) { dump(n, v, s, "i8"); }
+
+// Expose the protected containers of the reference driver.
+class HarnessDriver : public CFluidDriver {
+ public:
+  HarnessDriver(char* cfg, unsigned short nZone, unsigned short nDim, SU2_Comm comm)
+      : CFluidDriver(cfg, nZone, nDim, comm) {}
+  CGeometry* geo() { return geometry_container[ZONE_0][MESH_0]; }
+  CSolver** sol() { return solver_container[ZONE_0][MESH_0]; }
+  CNumerics* num(unsigned short s, unsigned short t) { return numerics_container[ZONE_0][MESH_0][s][t]; }
+  CConfig* cfg() { return config_container[ZONE_0]; }
+};
+
+// sigma_k is a protected CNumerics member; Set_Sigmak has no return statement (UB,
+// SU2_CFD/include/numerics_structure.hpp:525-527), so set it through a derived accessor instead.
+struct SigmaSetter : public CNumerics {
+  static void set(CNumerics* n, double s) { static_cast<SigmaSetter*>(n)->sigma_k = s; }
+};
+
+double** alloc2(int n) {
+  double** a = new double*[n];
+  for (int i = 0; i < n; ++i) a[i] = new double[n]();
+  return a;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    std::fprintf(stderr, "usage: harness <cfg> <state.txt> <outdir> [--bsr]\n");
+    return 2;
+  }
+  char cfgname[MAX_STRING_SIZE];
+  std::strcpy(cfgname, argv[1]);
+  std::string state_file = argv[2];
+  g_out = argv[3];
+  bool do_bsr = (argc > 4 && std::string(argv[4]) == "--bsr");
+  g_manifest.open(g_out + "/manifest.txt");
+
+  SU2_Comm comm(0);
+  CConfig* c0 = new CConfig(cfgname, SU2_CFD);
+  unsigned short nZone = CConfig::GetnZone(c0->GetMesh_FileName(), c0->GetMesh_FileFormat(), c0);
+  unsigned short nDim = CConfig::GetnDim(c0->GetMesh_FileName(), c0->GetMesh_FileFormat());
+  delete c0;
+  HarnessDriver drv(cfgname, nZone, nDim, comm);
+
+  CGeometry* geo = drv.geo();
+  CSolver** sc = drv.sol();
+  CConfig* cfg = drv.cfg();
+  CSolver* flow = sc[FLOW_SOL];
+  CSolver* turb = sc[TURB_SOL];
+  const bool rans = (turb != NULL);
+
+  const unsigned long nPoint = geo->GetnPoint();
+  const unsigned long nEdge = geo->GetnEdge();
+  const unsigned short nVar = flow->GetnVar();
+  const unsigned short nPrimVar = flow->GetnPrimVar();
+  const unsigned short nPrimVarGrad = flow->GetnPrimVarGrad();
+  const unsigned short nSpecies = nVar - nDim - 2;
+  const unsigned short nPrimVarLim = nDim + 2;
+
+  // ---- load the state: lines "global_index U[0..nVar) [k omega]"
+  {
+    std::map<unsigned long, unsigned long> g2l;
+    for (unsigned long i = 0; i < nPoint; ++i) g2l[geo->node[i]->GetGlobalIndex()] = i;
+    std::ifstream sf(state_file);
+    std::string line;
+    unsigned long nset = 0;
+    while (std::getline(sf, line)) {
+      if (line.empty()) continue;
+      std::istringstream is(line);
+      unsigned long gidx;
+      is >> gidx;
+      auto it = g2l.find(gidx);
+      if (it == g2l.end()) continue;
+      unsigned long i = it->second;
+      for (unsigned short v = 0; v < nVar; ++v) {
+        double u;
+        is >> u;
+        flow->node[i]->SetSolution(v, u);
+        flow->node[i]->SetSolution_Old(v, u);
+      }
+      if (rans) {
+        double k, w;
+        is >> k >> w;
+        turb->node[i]->SetSolution(0, k);
+        turb->node[i]->SetSolution(1, w);
+        turb->node[i]->SetSolution_Old(0, k);
+        turb->node[i]->SetSolution_Old(1, w);
+      }
+      ++nset;
+    }
+    if (nset != nPoint) {
+      std::fprintf(stderr, "state covers %lu of %lu points\n", nset, nPoint);
+      return 4;
+    }
+  }
+
+  // ---- the reference's own preprocessing (flow, then turbulence mu_t, then flow again)
+  flow->Preprocessing(geo, sc, cfg, MESH_0, NO_RK_ITER, RUNTIME_FLOW_SYS, false);
+  if (rans) {
+    turb->Postprocessing(geo, sc, cfg, MESH_0);
+    flow->Preprocessing(geo, sc, cfg, MESH_0, NO_RK_ITER, RUNTIME_FLOW_SYS, false);
+    turb->Preprocessing(geo, sc, cfg, MESH_0, NO_RK_ITER, RUNTIME_TURB_SYS, false);
+    turb->Postprocessing(geo, sc, cfg, MESH_0);
+  }
+
+  const bool implicit = (cfg->GetKind_TimeIntScheme_Flow() == EULER_IMPLICIT);
+
+  // ---- geometry
+  {
+    std::vector<double> coord(nPoint * nDim), vol(nPoint);
+    std::vector<int64_t> gidx(nPoint), nb_ptr(nPoint + 1, 0), nb;
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      for (unsigned short d = 0; d < nDim; ++d) coord[i * nDim + d] = geo->node[i]->GetCoord(d);
+      vol[i] = geo->node[i]->GetVolume();
+      gidx[i] = geo->node[i]->GetGlobalIndex();
+      for (unsigned short k = 0; k < geo->node[i]->GetnPoint(); ++k) nb.push_back(geo->node[i]->GetPoint(k));
+      nb_ptr[i + 1] = nb.size();
+    }
+    dumpd("coord", coord, {(long)nPoint, nDim});
+    dumpd("volume", vol, {(long)nPoint});
+    dumpi("global_index", gidx, {(long)nPoint});
+    dumpi("nbr_ptr", nb_ptr, {(long)nPoint + 1});
+    dumpi("nbr", nb, {(long)nb.size()});
+    std::vector<int64_t> edges(nEdge * 2);
+    std::vector<double> normal(nEdge * nDim);
+    for (unsigned long e = 0; e < nEdge; ++e) {
+      edges[2 * e] = geo->edge[e]->GetNode(0);
+      edges[2 * e + 1] = geo->edge[e]->GetNode(1);
+      su2double* n = geo->edge[e]->GetNormal();
+      for (unsigned short d = 0; d < nDim; ++d) normal[e * nDim + d] = n[d];
+    }
+    dumpi("edges", edges, {(long)nEdge, 2});
+    dumpd("edge_normal", normal, {(long)nEdge, nDim});
+    // boundary vertices: marker id, node, dual-face normal (geometry_structure.cpp SetBoundControlVolume)
+    std::vector<int64_t> bv;
+    std::vector<double> bn;
+    for (unsigned short m = 0; m < geo->GetnMarker(); ++m)
+      for (unsigned long v = 0; v < geo->GetnVertex(m); ++v) {
+        bv.push_back(m);
+        bv.push_back(geo->vertex[m][v]->GetNode());
+        bv.push_back(cfg->GetMarker_All_KindBC(m));
+        su2double* n = geo->vertex[m][v]->GetNormal();
+        for (unsigned short d = 0; d < nDim; ++d) bn.push_back(n[d]);
+      }
+    dumpi("bvertex", bv, {(long)bv.size() / 3, 3});
+    dumpd("bvertex_normal", bn, {(long)bn.size() / nDim, nDim});
+    std::vector<double> wall(nPoint);
+    for (unsigned long i = 0; i < nPoint; ++i) wall[i] = geo->node[i]->GetWall_Distance();
+    dumpd("wall_distance", wall, {(long)nPoint});
+  }
+
+  // ---- node state after the reference's preprocessing
+  {
+    std::vector<double> U(nPoint * nVar), V(nPoint * nPrimVar), dPdU(nPoint * nVar), dTdU(nPoint * nVar);
+    std::vector<double> mu(nPoint), kap(nPoint), cp(nPoint), Dij(nPoint * nSpecies * nSpecies);
+    std::vector<double> grad(nPoint * nPrimVarGrad * nDim), lim(nPoint * nPrimVarLim);
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      CVariable* n = flow->node[i];
+      for (unsigned short v = 0; v < nVar; ++v) {
+        U[i * nVar + v] = n->GetSolution(v);
+        dPdU[i * nVar + v] = n->GetdPdU()[v];
+        dTdU[i * nVar + v] = n->GetdTdU()[v];
+      }
+      for (unsigned short v = 0; v < nPrimVar; ++v) V[i * nPrimVar + v] = n->GetPrimitive(v);
+      mu[i] = n->GetLaminarViscosity();
+      kap[i] = n->GetThermalConductivity();
+      cp[i] = n->GetSpecificHeatCp();
+      double* d = n->GetDiffusionCoeff();
+      for (int k = 0; k < nSpecies * nSpecies; ++k) Dij[i * nSpecies * nSpecies + k] = d[k];
+      su2double** g = n->GetGradient_Primitive();
+      for (unsigned short v = 0; v < nPrimVarGrad; ++v)
+        for (unsigned short dd = 0; dd < nDim; ++dd) grad[(i * nPrimVarGrad + v) * nDim + dd] = g[v][dd];
+      for (unsigned short v = 0; v < nPrimVarLim; ++v) lim[i * nPrimVarLim + v] = n->GetLimiter_Primitive(v);
+    }
+    dumpd("U", U, {(long)nPoint, nVar});
+    dumpd("V", V, {(long)nPoint, nPrimVar});
+    dumpd("dPdU", dPdU, {(long)nPoint, nVar});
+    dumpd("dTdU", dTdU, {(long)nPoint, nVar});
+    dumpd("mu", mu, {(long)nPoint});
+    dumpd("kappa", kap, {(long)nPoint});
+    dumpd("cp", cp, {(long)nPoint});
+    dumpd("Dij", Dij, {(long)nPoint, nSpecies, nSpecies});
+    dumpd("grad_prim", grad, {(long)nPoint, nPrimVarGrad, nDim});
+    dumpd("limiter", lim, {(long)nPoint, nPrimVarLim});
+    if (rans) {
+      std::vector<double> tk(nPoint), tw(nPoint), mut(nPoint), sk(nPoint), gk(nPoint * nDim);
+      for (unsigned long i = 0; i < nPoint; ++i) {
+        tk[i] = turb->node[i]->GetSolution(0);
+        tw[i] = turb->node[i]->GetSolution(1);
+        mut[i] = turb->node[i]->GetmuT();
+        sk[i] = turb->node[i]->Get_Sigmak();
+        for (unsigned short d = 0; d < nDim; ++d) gk[i * nDim + d] = turb->node[i]->GetGradient()[0][d];
+      }
+      dumpd("turb_k", tk, {(long)nPoint});
+      dumpd("turb_omega", tw, {(long)nPoint});
+      dumpd("mu_t", mut, {(long)nPoint});
+      dumpd("sigma_k", sk, {(long)nPoint});
+      dumpd("grad_k", gk, {(long)nPoint, nDim});
+    }
+  }
+
+  // ---- Venkatakrishnan limiter computed by the reference from the gradients above
+  //      (solver_direct_reactive.cpp:1328-1523). Forced on for the dump, independent of cfg.
+  {
+    flow->SetPrimitive_Limiter(geo, cfg);
+    std::vector<double> lim(nPoint * nPrimVarLim);
+    for (unsigned long i = 0; i < nPoint; ++i)
+      for (unsigned short v = 0; v < nPrimVarLim; ++v) lim[i * nPrimVarLim + v] = flow->node[i]->GetLimiter_Primitive(v);
+    dumpd("limiter_out", lim, {(long)nPoint, nPrimVarLim});
+    std::vector<double> prm = {cfg->GetRefElemLength(), cfg->GetLimiterCoeff()};
+    dumpd("limiter_params", prm, {2});
+  }
+
+  // ---- per-edge AUSM (1st order path, solver_direct_reactive.cpp:2731-2743)
+  CNumerics* conv = drv.num(FLOW_SOL, CONV_TERM);
+  double** Ji = alloc2(nVar);
+  double** Jj = alloc2(nVar);
+  {
+    std::vector<double> res(nEdge * nVar), ji, jj;
+    if (implicit) { ji.resize(nEdge * nVar * nVar); jj.resize(nEdge * nVar * nVar); }
+    double r[64];
+    for (unsigned long e = 0; e < nEdge; ++e) {
+      unsigned long i = geo->edge[e]->GetNode(0), j = geo->edge[e]->GetNode(1);
+      conv->SetNormal(geo->edge[e]->GetNormal());
+      conv->SetPrimitive(flow->node[i]->GetPrimitive(), flow->node[j]->GetPrimitive());
+      if (implicit) conv->SetSecondary(flow->node[i]->GetdPdU(), flow->node[j]->GetdPdU());
+      conv->ComputeResidual(r, Ji, Jj, cfg);
+      for (unsigned short v = 0; v < nVar; ++v) res[e * nVar + v] = r[v];
+      if (implicit)
+        for (unsigned short a = 0; a < nVar; ++a)
+          for (unsigned short b = 0; b < nVar; ++b) {
+            ji[(e * nVar + a) * nVar + b] = Ji[a][b];
+            jj[(e * nVar + a) * nVar + b] = Jj[a][b];
+          }
+    }
+    dumpd("conv_res", res, {(long)nEdge, nVar});
+    if (implicit) {
+      dumpd("conv_jac_i", ji, {(long)nEdge, nVar, nVar});
+      dumpd("conv_jac_j", jj, {(long)nEdge, nVar, nVar});
+    }
+    std::vector<double> minf = {cfg->GetMach()};
+    dumpd("mach_inf", minf, {1});
+  }
+
+  // ---- per-edge viscous flux (solver_direct_reactive.cpp:5312-5355)
+  CNumerics* visc = drv.num(FLOW_SOL, VISC_TERM);
+  {
+    std::vector<double> res(nEdge * nVar), ji, jj;
+    if (implicit) { ji.resize(nEdge * nVar * nVar); jj.resize(nEdge * nVar * nVar); }
+    double r[64];
+    for (unsigned long e = 0; e < nEdge; ++e) {
+      unsigned long i = geo->edge[e]->GetNode(0), j = geo->edge[e]->GetNode(1);
+      visc->SetCoord(geo->node[i]->GetCoord(), geo->node[j]->GetCoord());
+      visc->SetNormal(geo->edge[e]->GetNormal());
+      visc->SetPrimitive(flow->node[i]->GetPrimitive(), flow->node[j]->GetPrimitive());
+      visc->SetPrimVarGradient(flow->node[i]->GetGradient_Primitive(), flow->node[j]->GetGradient_Primitive());
+      if (implicit) visc->SetSecondary(flow->node[i]->GetdTdU(), flow->node[j]->GetdTdU());
+      visc->SetLaminarViscosity(flow->node[i]->GetLaminarViscosity(), flow->node[j]->GetLaminarViscosity());
+      visc->SetThermalConductivity(flow->node[i]->GetThermalConductivity(), flow->node[j]->GetThermalConductivity());
+      visc->SetDiffusionCoeff(flow->node[i]->GetDiffusionCoeff(), flow->node[j]->GetDiffusionCoeff());
+      if (rans) {
+        visc->SetTurbKineticEnergy(turb->node[i]->GetSolution(0), turb->node[j]->GetSolution(0));
+        visc->SetEddyViscosity(turb->node[i]->GetmuT(), turb->node[j]->GetmuT());
+        SigmaSetter::set(visc, turb->node[i]->Get_Sigmak());
+        visc->Set_GradTKE(turb->node[i]->GetGradient()[0], turb->node[j]->GetGradient()[0]);
+      }
+      visc->ComputeResidual(r, Ji, Jj, cfg);
+      for (unsigned short v = 0; v < nVar; ++v) res[e * nVar + v] = r[v];
+      if (implicit)
+        for (unsigned short a = 0; a < nVar; ++a)
+          for (unsigned short b = 0; b < nVar; ++b) {
+            ji[(e * nVar + a) * nVar + b] = Ji[a][b];
+            jj[(e * nVar + a) * nVar + b] = Jj[a][b];
+          }
+    }
+    dumpd("visc_res", res, {(long)nEdge, nVar});
+    if (implicit) {
+      dumpd("visc_jac_i", ji, {(long)nEdge, nVar, nVar});
+      dumpd("visc_jac_j", jj, {(long)nEdge, nVar, nVar});
+    }
+    std::vector<double> prm = {cfg->GetPrandtl_Lam(), cfg->GetPrandtl_Turb(), cfg->GetLewis_Turb()};
+    dumpd("visc_params", prm, {3});
+  }
+
+  // ---- per-cell chemistry source (solver_direct_reactive.cpp:2803-2817)
+  CNumerics* src = drv.num(FLOW_SOL, SOURCE_FIRST_TERM);
+  {
+    std::vector<double> res(nPoint * nVar), jac;
+    if (implicit) jac.resize(nPoint * nVar * nVar);
+    double r[64];
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      src->SetPrimitive(flow->node[i]->GetPrimitive(), flow->node[i]->GetPrimitive());
+      if (implicit) src->SetSecondary(flow->node[i]->GetdTdU(), flow->node[i]->GetdTdU());
+      src->SetVolume(geo->node[i]->GetVolume());
+      if (rans) src->SetOmegaParam(turb->node[i]->GetSolution(1));
+      src->ComputeChemistry(r, Ji, cfg);
+      for (unsigned short v = 0; v < nVar; ++v) res[i * nVar + v] = r[v];
+      if (implicit)
+        for (unsigned short a = 0; a < nVar; ++a)
+          for (unsigned short b = 0; b < nVar; ++b) jac[(i * nVar + a) * nVar + b] = Ji[a][b];
+    }
+    dumpd("src_res", res, {(long)nPoint, nVar});
+    if (implicit) dumpd("src_jac", jac, {(long)nPoint, nVar, nVar});
+    std::vector<double> prm = {cfg->Get_Cmu(), cfg->Get_PaSR_LB(), cfg->GetDensity_Ref(), cfg->GetTime_Ref(),
+                               cfg->GetTemperature_Ref()};
+    dumpd("src_params", prm, {5});
+  }
+
+  // ---- LSQ gradient recomputed by the reference (solver_direct_reactive.cpp:4887-5050)
+  {
+    CReactiveNSSolver* ns = dynamic_cast<CReactiveNSSolver*>(flow);
+    ns->SetPrimitive_Gradient_LS(geo, cfg);
+    std::vector<double> grad(nPoint * nPrimVarGrad * nDim);
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      su2double** g = flow->node[i]->GetGradient_Primitive();
+      for (unsigned short v = 0; v < nPrimVarGrad; ++v)
+        for (unsigned short dd = 0; dd < nDim; ++dd) grad[(i * nPrimVarGrad + v) * nDim + dd] = g[v][dd];
+    }
+    dumpd("grad_lsq_out", grad, {(long)nPoint, nPrimVarGrad, nDim});
+  }
+
+  // ---- whole loops (solver_direct_reactive.cpp Upwind/Viscous/Source) and the time step
+  if (do_bsr) {
+    CNumerics* visc_n = drv.num(FLOW_SOL, VISC_TERM);
+    CNumerics* conv_n = drv.num(FLOW_SOL, CONV_TERM);
+    CNumerics* src_n = drv.num(FLOW_SOL, SOURCE_FIRST_TERM);
+    CNumerics* src2_n = drv.num(FLOW_SOL, SOURCE_SECOND_TERM);
+    CSysVector& R = flow->LinSysRes;
+    auto dump_res = [&](const std::string& name) {
+      std::vector<double> r(nPoint * nVar);
+      for (unsigned long i = 0; i < nPoint * nVar; ++i) r[i] = R[i];
+      dumpd(name, r, {(long)nPoint, nVar});
+    };
+    R.SetValZero();
+    if (implicit) flow->Jacobian.SetValZero();
+    flow->Upwind_Residual(geo, sc, conv_n, cfg, MESH_0);
+    dump_res("loop_upwind_res");
+    flow->Viscous_Residual(geo, sc, visc_n, cfg, MESH_0, NO_RK_ITER);
+    dump_res("loop_upwind_visc_res");
+    flow->Source_Residual(geo, sc, src_n, src2_n, cfg, MESH_0);
+    dump_res("loop_total_res");
+
+    flow->SetTime_Step(geo, sc, cfg, MESH_0, 0);
+    std::vector<double> dt(nPoint), li(nPoint), lv(nPoint);
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      dt[i] = flow->node[i]->GetDelta_Time();
+      li[i] = flow->node[i]->GetMax_Lambda_Inv();
+      lv[i] = flow->node[i]->GetMax_Lambda_Visc();
+    }
+    dumpd("dt", dt, {(long)nPoint});
+    dumpd("lambda_inv", li, {(long)nPoint});
+    dumpd("lambda_visc", lv, {(long)nPoint});
+    std::vector<double> tprm = {cfg->GetCFL(MESH_0), cfg->GetMax_DeltaTime(), cfg->GetPrandtl_Lam(), cfg->GetPrandtl_Turb()};
+    dumpd("dt_params", tprm, {4});
+
+    if (implicit) {
+      CSysMatrix& A = flow->Jacobian;
+      // BSR of the assembled Jacobian (sorted neighbours + diagonal, matrix_structure.cpp:113-201)
+      std::vector<int64_t> row_ptr(nPoint + 1, 0), col;
+      for (unsigned long i = 0; i < nPoint; ++i) {
+        std::vector<unsigned long> cols;
+        cols.push_back(i);
+        for (unsigned short k = 0; k < geo->node[i]->GetnPoint(); ++k) cols.push_back(geo->node[i]->GetPoint(k));
+        std::sort(cols.begin(), cols.end());
+        for (auto c : cols) col.push_back(c);
+        row_ptr[i + 1] = col.size();
+      }
+      auto dump_bsr = [&](const std::string& name) {
+        std::vector<double> blocks(col.size() * nVar * nVar);
+        for (unsigned long i = 0; i < nPoint; ++i)
+          for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+            su2double* b = A.GetBlock(i, col[k]);
+            for (int q = 0; q < nVar * nVar; ++q) blocks[k * nVar * nVar + q] = b[q];
+          }
+        dumpd(name, blocks, {(long)col.size(), nVar, nVar});
+      };
+      dumpi("bsr_row_ptr", row_ptr, {(long)nPoint + 1});
+      dumpi("bsr_col", col, {(long)col.size()});
+      dump_bsr("bsr_jac_residual");
+
+      // ImplicitEuler system build (solver_direct_reactive.cpp:2350-2377), truncation error is zero here
+      CSysVector rhs(nPoint, nPoint, nVar, 0.0), x(nPoint, nPoint, nVar, 0.0);
+      for (unsigned long i = 0; i < nPoint; ++i) {
+        double Vol = geo->node[i]->GetVolume();
+        double Dt = flow->node[i]->GetDelta_Time();
+        if (Dt > EPS) A.AddVal2Diag(i, Vol / Dt);
+        else A.SetVal2Diag(i, 1.0);
+        for (unsigned short v = 0; v < nVar; ++v) rhs[i * nVar + v] = (Dt > EPS) ? -R[i * nVar + v] : -0.0;
+      }
+      dump_bsr("bsr_system");
+      std::vector<double> b(nPoint * nVar);
+      for (unsigned long i = 0; i < nPoint * nVar; ++i) b[i] = rhs[i];
+      dumpd("sys_rhs", b, {(long)nPoint, nVar});
+
+      CSysMatrixVectorProduct mv(A, geo, cfg);
+      CSysVector y(nPoint, nPoint, nVar, 0.0);
+      mv(rhs, y);
+      std::vector<double> yy(nPoint * nVar);
+      for (unsigned long i = 0; i < nPoint * nVar; ++i) yy[i] = y[i];
+      dumpd("spmv_rhs", yy, {(long)nPoint, nVar});
+
+      CSysVector z(nPoint, nPoint, nVar, 0.0);
+      CSysSolve solver;
+      double resid = 0.0;
+      const unsigned long m = cfg->GetLinear_Solver_Iter();
+      const double tol = cfg->GetLinear_Solver_Error();
+      if (cfg->GetKind_Linear_Solver_Prec() != ILU) {
+      CLU_SGSPreconditioner lusgs(A, geo, cfg);
+      lusgs(rhs, z);
+      for (unsigned long i = 0; i < nPoint * nVar; ++i) yy[i] = z[i];
+      dumpd("lusgs_rhs", yy, {(long)nPoint, nVar});
+
+      x.SetValZero();
+      unsigned long it1 = solver.FGMRES_LinSolver(rhs, x, mv, lusgs, tol, m, &resid, false);
+      for (unsigned long i = 0; i < nPoint * nVar; ++i) yy[i] = x[i];
+      dumpd("fgmres_lusgs_x", yy, {(long)nPoint, nVar});
+      std::vector<double> info = {(double)it1, resid, tol, (double)m};
+      dumpd("fgmres_lusgs_info", info, {4});
+      } else {
+
+      A.BuildILUPreconditioner();
+      std::vector<double> ilu(col.size() * nVar * nVar);
+      for (unsigned long i = 0; i < nPoint; ++i)
+        for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+          su2double* bb = A.GetBlock_ILUMatrix(i, col[k]);
+          for (int q = 0; q < nVar * nVar; ++q) ilu[k * nVar * nVar + q] = bb[q];
+        }
+      dumpd("ilu_factor", ilu, {(long)col.size(), nVar, nVar});
+      CILUPreconditioner ilup(A, geo, cfg);
+      ilup(rhs, z);
+      for (unsigned long i = 0; i < nPoint * nVar; ++i) yy[i] = z[i];
+      dumpd("ilu_rhs", yy, {(long)nPoint, nVar});
+      x.SetValZero();
+      unsigned long it2 = solver.FGMRES_LinSolver(rhs, x, mv, ilup, tol, m, &resid, false);
+      for (unsigned long i = 0; i < nPoint * nVar; ++i) yy[i] = x[i];
+      dumpd("fgmres_ilu_x", yy, {(long)nPoint, nVar});
+      std::vector<double> info = {(double)it2, resid, tol, (double)m};
+      dumpd("fgmres_ilu_info", info, {4});
+      }
+    }
+  }
+
+  std::vector<int64_t> dims = {nDim, nVar, nPrimVar, nPrimVarGrad, nSpecies, implicit ? 1 : 0, rans ? 1 : 0};
+  dumpi("dims", dims, {7});
+  g_manifest.close();
+  std::fprintf(stderr, "harness: done (%lu points, %lu edges)\n", nPoint, nEdge);
+  return 0;
+}
