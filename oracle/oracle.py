@@ -1,0 +1,221 @@
+"""ctypes wrapper of the CPU oracle (oracle/rx_oracle.cpp) — TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
+                os.path.join(HERE, "rx_oracle.cpp")):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_mech_create.restype = C.c_void_p
+        _lib.orc_spline.restype = C.c_double
+        _lib.orc_spline.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double]
+        _lib.orc_source_cells.restype = C.c_int
+        _lib.orc_visc_edges.restype = C.c_int
+        _lib.orc_fgmres.restype = C.c_int
+    return _lib
+
+
+_KEEP = []  # converted temporaries must outlive the foreign call that uses their pointers
+
+
+def _p(a, dt=np.float64):
+    if a is None:
+        return None
+    a = np.ascontiguousarray(a, dtype=dt)
+    _KEEP.append(a)
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _keepalive(fn):
+    import functools
+
+    @functools.wraps(fn)
+    def w(*args, **kw):
+        try:
+            return fn(*args, **kw)
+        finally:
+            _KEEP.clear()
+    return w
+
+
+class Mechanism:
+    """Oracle-side mechanism handle built from the `mech_*` arrays of a golden file."""
+
+    def __init__(self, arrays, prefix="mech_"):
+        g = {k[len(prefix):]: arrays[k] for k in arrays if k.startswith(prefix)}
+        self.arrays = {k: np.ascontiguousarray(v) for k, v in g.items()}
+        self.ns = int(g["n_species"])
+        self.nr = int(g["n_reactions"])
+        self.ntab = g["tab_x"].shape[2]
+        a = self.arrays
+        self._keep = [a[k] for k in ("mmass", "diff_vol", "stoich_reac", "stoich_prod", "exp_reac", "exp_prod", "A",
+                                     "beta", "Ta", "A_back", "beta_back", "Ta_back", "tab_x", "tab_y", "tab_y2")]
+        self._ikeep = [np.ascontiguousarray(a["reversible"], dtype=np.int64),
+                       np.ascontiguousarray(a["has_backward"], dtype=np.int64)]
+        L = lib()
+        self.h = C.c_void_p(L.orc_mech_create(
+            C.c_int(self.ns), C.c_int(self.nr), C.c_int(self.ntab),
+            *[_p(x) for x in self._keep[:12]], _p(self._ikeep[0], np.int64), _p(self._ikeep[1], np.int64),
+            *[_p(x) for x in self._keep[12:]]))
+
+    def __del__(self):
+        try:
+            lib().orc_mech_destroy(self.h)
+        except Exception:
+            pass
+
+    def spline(self, prop, s, T):
+        return lib().orc_spline(self.h, prop, s, T)
+
+
+@_keepalive
+def ausm_edges(nDim, ns, edges, normal, V, dPdU, mach_inf, implicit):
+    E = len(edges)
+    nVar = ns + nDim + 2
+    res = np.zeros((E, nVar))
+    Ji = np.zeros((E, nVar, nVar)) if implicit else None
+    Jj = np.zeros((E, nVar, nVar)) if implicit else None
+    edges = np.ascontiguousarray(edges, dtype=np.int64)
+    lib().orc_ausm_edges(C.c_int(nDim), C.c_int(ns), C.c_int64(E), _p(edges, np.int64), _p(normal), _p(V),
+                         _p(dPdU) if implicit else None, C.c_double(mach_inf), C.c_int(int(implicit)),
+                         res.ctypes.data_as(C.c_void_p), Ji.ctypes.data_as(C.c_void_p) if implicit else None,
+                         Jj.ctypes.data_as(C.c_void_p) if implicit else None)
+    return res, Ji, Jj
+
+
+@_keepalive
+def source_cells(mech, nDim, V, dTdU, vol, omega_turb, rans, implicit, params):
+    N = len(V)
+    nVar = mech.ns + nDim + 2
+    res = np.zeros((N, nVar))
+    J = np.zeros((N, nVar, nVar)) if implicit else None
+    rc = lib().orc_source_cells(mech.h, C.c_int(nDim), C.c_int64(N), _p(V), _p(dTdU) if implicit else None, _p(vol),
+                                _p(omega_turb) if rans else None, C.c_int(int(rans)), C.c_int(int(implicit)),
+                                _p(np.asarray(params, dtype=np.float64)), res.ctypes.data_as(C.c_void_p),
+                                J.ctypes.data_as(C.c_void_p) if implicit else None)
+    if rc != 0:
+        raise RuntimeError("oracle source failed (table range)")
+    return res, J
+
+
+@_keepalive
+def visc_edges(mech, nDim, edges, normal, coord, V, grad, mu, kappa, Dij, dTdU, tke, mut, sigma_k, gradk, rans,
+               implicit, vparams):
+    E = len(edges)
+    nVar = mech.ns + nDim + 2
+    res = np.zeros((E, nVar))
+    Ji = np.zeros((E, nVar, nVar)) if implicit else None
+    Jj = np.zeros((E, nVar, nVar)) if implicit else None
+    edges = np.ascontiguousarray(edges, dtype=np.int64)
+    rc = lib().orc_visc_edges(
+        mech.h, C.c_int(nDim), C.c_int64(E), _p(edges, np.int64), _p(normal), _p(coord), _p(V), _p(grad), _p(mu),
+        _p(kappa), _p(Dij), _p(dTdU) if implicit else None, _p(tke) if rans else None, _p(mut) if rans else None,
+        _p(sigma_k) if rans else None, _p(gradk) if rans else None, C.c_int(int(rans)), C.c_int(int(implicit)),
+        _p(np.asarray(vparams, dtype=np.float64)), res.ctypes.data_as(C.c_void_p),
+        Ji.ctypes.data_as(C.c_void_p) if implicit else None, Jj.ctypes.data_as(C.c_void_p) if implicit else None)
+    if rc != 0:
+        raise RuntimeError("oracle viscous flux failed")
+    return res, Ji, Jj
+
+
+@_keepalive
+def grad_lsq(mech, nDim, pts, coord, V, nbr_ptr, nbr, out=None):
+    N = len(coord)
+    nG = mech.ns + nDim + 2
+    g = np.zeros((N, nG, nDim)) if out is None else out
+    pts = np.ascontiguousarray(pts, dtype=np.int64)
+    lib().orc_grad_lsq(mech.h, C.c_int(nDim), C.c_int64(len(pts)), _p(pts, np.int64), _p(coord), _p(V),
+                       _p(nbr_ptr, np.int64), _p(nbr, np.int64), g.ctypes.data_as(C.c_void_p))
+    return g
+
+
+@_keepalive
+def limiter_venkat(nDim, ns, edges, coord, V, grad, ref_len, coeff):
+    N = len(coord)
+    lim = np.zeros((N, nDim + 2))
+    edges = np.ascontiguousarray(edges, dtype=np.int64)
+    lib().orc_limiter_venkat(C.c_int(nDim), C.c_int(ns), C.c_int64(N), C.c_int64(len(edges)), _p(edges, np.int64),
+                             _p(coord), _p(V), _p(grad), C.c_double(ref_len), C.c_double(coeff),
+                             lim.ctypes.data_as(C.c_void_p))
+    return lim
+
+
+@_keepalive
+def bsr_spmv(rp, col, A, x):
+    N, nb = len(rp) - 1, A.shape[1]
+    y = np.zeros(N * nb)
+    lib().orc_bsr_spmv(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A), _p(x),
+                       y.ctypes.data_as(C.c_void_p))
+    return y.reshape(N, nb)
+
+
+@_keepalive
+def lusgs(rp, col, A, b):
+    N, nb = len(rp) - 1, A.shape[1]
+    x = np.zeros(N * nb)
+    lib().orc_lusgs(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A), _p(b),
+                    x.ctypes.data_as(C.c_void_p))
+    return x.reshape(N, nb)
+
+
+@_keepalive
+def ilu_build(rp, col, A):
+    N, nb = len(rp) - 1, A.shape[1]
+    F = np.zeros_like(np.ascontiguousarray(A))
+    lib().orc_ilu_build(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
+                        F.ctypes.data_as(C.c_void_p))
+    return F
+
+
+@_keepalive
+def ilu_apply(rp, col, F, b):
+    N, nb = len(rp) - 1, F.shape[1]
+    x = np.zeros(N * nb)
+    lib().orc_ilu_apply(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(F), _p(b),
+                        x.ctypes.data_as(C.c_void_p))
+    return x.reshape(N, nb)
+
+
+@_keepalive
+def fgmres(rp, col, A, b, prec="lusgs", F=None, tol=1e-6, m=5, x0=None):
+    N, nb = len(rp) - 1, A.shape[1]
+    x = np.zeros(N * nb) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).ravel().copy()
+    resid = C.c_double(0.0)
+    it = lib().orc_fgmres(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
+                          _p(F) if F is not None else None, C.c_int(0 if prec == "lusgs" else 1), _p(b),
+                          x.ctypes.data_as(C.c_void_p), C.c_double(tol), C.c_int(m), C.byref(resid))
+    return x.reshape(N, nb), it, resid.value
+
+
+@_keepalive
+def time_step(nDim, ns, edges, normal, bverts, bnormal, V, dPdU, mu, eddy, vol, nbr_ptr, params):
+    N = len(V)
+    dt, li, lv = np.zeros(N), np.zeros(N), np.zeros(N)
+    bv = np.ascontiguousarray(np.asarray(bverts)[:, :2], dtype=np.int64)
+    edges = np.ascontiguousarray(edges, dtype=np.int64)
+    lib().orc_time_step(C.c_int(nDim), C.c_int(ns), C.c_int64(N), C.c_int64(len(edges)), _p(edges, np.int64),
+                        _p(normal), C.c_int64(len(bv)), _p(bv, np.int64), _p(bnormal), _p(V), _p(dPdU), _p(mu),
+                        _p(eddy), _p(vol), _p(nbr_ptr, np.int64), _p(np.asarray(params, dtype=np.float64)),
+                        dt.ctypes.data_as(C.c_void_p), li.ctypes.data_as(C.c_void_p), lv.ctypes.data_as(C.c_void_p))
+    return dt, li, lv

@@ -243,6 +243,9 @@ int main(int argc, char** argv) {
       dumpd("mu_t", mut, {(long)nPoint});
       dumpd("sigma_k", sk, {(long)nPoint});
       dumpd("grad_k", gk, {(long)nPoint, nDim});
+      std::vector<double> ev(nPoint);
+      for (unsigned long i = 0; i < nPoint; ++i) ev[i] = flow->node[i]->GetEddyViscosity();
+      dumpd("eddy_visc_flow", ev, {(long)nPoint});
     }
   }
 

@@ -1,0 +1,1679 @@
+// rx_oracle.cpp — CPU restatement of the reference hot path.
+//
+// TEST INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+// leg as the checker / CPU baseline. Never linked into, called by, or shipped with the product.
+// Parity of this restatement is pinned by tests/golden/*.npz, generated from the compiled
+// reference by oracle/make_golden.py (tests/test_oracle_golden.py).
+//
+// Every function follows the reference file:line it cites (paths relative to the reference root).
+// Arithmetic is plain sequential IEEE double (built with -ffp-contract=off: the x86-64 reference
+// has no FMA). Layouts (row-major, per node / per edge):
+//   V   [N][nPrimVar]   T, u, v, P, rho, h, a, Y_1..Y_Ns        (variable_direct_reactive.cpp:4-17)
+//   U   [N][nVar]       rho, rho u, rho v, rho E, rho_1..rho_Ns
+//   G   [N][nPrimVarGrad][nDim]  T, u, v, P, X_1..X_Ns
+//   Dij [N][Ns][Ns]     Eigen column-major copy (symmetric)
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+#include <vector>
+
+namespace {
+
+constexpr double EPS = 1.0e-16;                         // Common/include/option_structure.hpp:134
+constexpr double NA = 6.02214129 * 1.0e23;               // physical_chemical_library.hpp:571-579
+constexpr double KB = 1.3806488 * 1.0e-23;
+constexpr double R_UNGAS = NA * KB * 1.0e3;
+constexpr double R_UNGAS_ATM = 1.0e-3 * 0.082057338;
+constexpr double TWO3 = 2.0 / 3.0;
+enum { P_CP = 0, P_H = 1, P_S = 2, P_MU = 3, P_KAPPA = 4 };
+
+struct Mech {
+  int ns, nr, ntab;
+  std::vector<double> mm, ri, dv;
+  std::vector<double> sr, sp;  // [ns][nr]
+  std::vector<double> er, ep;  // [nr][ns]
+  std::vector<double> A, beta, Ta, Ab, betab, Tab;
+  std::vector<int> rev, hasb;
+  std::vector<double> tx, ty, ty2;  // [5][ns][ntab]
+  std::vector<std::vector<int>> neg_reac, neg_prod;
+  double mtot;
+};
+
+// spline.cpp:62-77 (GetSpline). Out of range -> std::out_of_range, as the reference.
+double spline(const Mech& m, int prop, int s, double T) {
+  const double* x = &m.tx[(prop * m.ns + s) * m.ntab];
+  const double* y = &m.ty[(prop * m.ns + s) * m.ntab];
+  const double* y2 = &m.ty2[(prop * m.ns + s) * m.ntab];
+  if (T < x[0] || T > x[m.ntab - 1]) throw std::out_of_range("temperature out of table range");
+  const double h = x[1] - x[0];
+  unsigned long klo = (unsigned long)((T - x[0]) / h + 1);
+  const double a = (x[klo] - T) / h;
+  const double b = (T - x[klo - 1]) / h;
+  return a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0;
+}
+
+// reacting_model_library.cpp:65-93 (SetMassFractions + SetMolarFromMass)
+void molar_from_mass(const Mech& m, const double* ys_in, double* ys_clamped, double* xs) {
+  double sy = 0.0, sx = 0.0;
+  for (int s = 0; s < m.ns; ++s) {
+    double y = ys_in[s];
+    if (y < 0.0) y = 1.0e-30;
+    ys_clamped[s] = y;
+    xs[s] = y / m.mm[s];
+  }
+  for (int s = 0; s < m.ns; ++s) sy += ys_clamped[s];
+  for (int s = 0; s < m.ns; ++s) sx += xs[s];
+  const double massTot = sy / sx;
+  for (int s = 0; s < m.ns; ++s) xs[s] = massTot * xs[s];
+}
+
+// ------------------------------------------------------------------------------------------------
+// a1: CUpwReactiveAUSM::ComputeResidual  (SU2_CFD/src/numerics_direct_reactive.cpp:53-378)
+// ------------------------------------------------------------------------------------------------
+void ausm(int nDim, int ns, const double* Vi, const double* Vj, const double* Normal, const double* Si,
+          const double* Sj, double mInfty, bool implicit, double* res, double* Ji, double* Jj) {
+  const int nVar = ns + nDim + 2;
+  const int T_ = 0, VX = 1, P_ = nDim + 1, RHO = nDim + 2, H_ = nDim + 3, A_ = nDim + 4, RHOS = nDim + 5;
+  const int RHO_S = 0, RHOVX_S = 1, RHOE_S = nDim + 1, RHOS_S = nDim + 2;
+  (void)T_;
+  double Area = 0.0;
+  for (int d = 0; d < nDim; ++d) Area += Normal[d] * Normal[d];
+  Area = std::sqrt(Area);
+  double UnitNormal[3];
+  for (int d = 0; d < nDim; ++d) UnitNormal[d] = Normal[d] / Area;
+  const double Density_i = Vi[RHO], Pressure_i = Vi[P_], Enthalpy_i = Vi[H_], SoundSpeed_i = Vi[A_];
+  const double Density_j = Vj[RHO], Pressure_j = Vj[P_], Enthalpy_j = Vj[H_], SoundSpeed_j = Vj[A_];
+  double ProjVelocity_i = 0.0, ProjVelocity_j = 0.0;
+  for (int d = 0; d < nDim; ++d) {
+    ProjVelocity_i += Vi[VX + d] * UnitNormal[d];
+    ProjVelocity_j += Vj[VX + d] * UnitNormal[d];
+  }
+  const double MeanSoundSpeed = 0.5 * (SoundSpeed_i + SoundSpeed_j);
+  const double mL = ProjVelocity_i / MeanSoundSpeed;
+  const double mR = ProjVelocity_j / MeanSoundSpeed;
+  const double mF2 = 0.5 * (mL * mL + mR * mR);
+  const double mRef2 = std::min(1.0, std::max(mF2, mInfty * mInfty));
+  const double mF = std::sqrt(mF2);
+  const double mRef = std::sqrt(mRef2);
+  const double fa = mRef * (2.0 - mRef);
+  const double alpha = 3.0 / 16.0 * (5.0 * fa * fa - 4.0);
+  const double beta = 0.125;
+  double mLP, mRM, pLP, pRM;
+  if (std::abs(mL) < 1.0) {
+    mLP = 0.25 * (mL + 1.0) * (mL + 1.0) + beta * (mL * mL - 1.0) * (mL * mL - 1.0);
+    pLP = 0.25 * (mL + 1.0) * (mL + 1.0) * (2.0 - mL) + alpha * mL * (mL * mL - 1.0) * (mL * mL - 1.0);
+  } else {
+    mLP = 0.5 * (mL + std::abs(mL));
+    pLP = 0.5 * (1.0 + std::abs(mL) / mL);
+  }
+  if (std::abs(mR) < 1.0) {
+    mRM = -0.25 * (mR - 1.0) * (mR - 1.0) - beta * (mR * mR - 1.0) * (mR * mR - 1.0);
+    pRM = 0.25 * (mR - 1.0) * (mR - 1.0) * (2.0 + mR) - alpha * mR * (mR * mR - 1.0) * (mR * mR - 1.0);
+  } else {
+    mRM = 0.5 * (mR - std::abs(mR));
+    pRM = 0.5 * (1.0 - std::abs(mR) / mR);
+  }
+  const double kP = 0.25, sigma = 1.0;
+  double m12 = mLP + mRM;
+  m12 -= kP / fa * std::max(1.0 - sigma * mF2, 0.0) * (Pressure_j - Pressure_i) /
+         (0.5 * (Density_i + Density_j) * MeanSoundSpeed * MeanSoundSpeed);
+  const double mLF = 0.5 * (m12 + std::abs(m12));
+  const double mRF = 0.5 * (m12 - std::abs(m12));
+  const double M12 = MeanSoundSpeed * (mLF * Density_i + mRF * Density_j);
+  double Phi_i[64], Phi_j[64];
+  Phi_i[RHO_S] = 1.0;
+  Phi_j[RHO_S] = 1.0;
+  for (int d = 0; d < nDim; ++d) {
+    Phi_i[RHOVX_S + d] = Vi[VX + d];
+    Phi_j[RHOVX_S + d] = Vj[VX + d];
+  }
+  Phi_i[RHOE_S] = Enthalpy_i;
+  Phi_j[RHOE_S] = Enthalpy_j;
+  for (int s = 0; s < ns; ++s) {
+    Phi_i[RHOS_S + s] = Vi[RHOS + s];
+    Phi_j[RHOS_S + s] = Vj[RHOS + s];
+  }
+  for (int v = 0; v < nVar; ++v)
+    res[v] = 0.5 * (M12 * (Phi_i[v] + Phi_j[v]) + std::abs(M12) * (Phi_i[v] - Phi_j[v])) * Area;
+  const double Ku = 0.75;
+  double pLF = pLP * Pressure_i + pRM * Pressure_j;
+  pLF -= Ku * pLP * pRM * (Density_i + Density_j) * fa * MeanSoundSpeed * (ProjVelocity_j - ProjVelocity_i);
+  for (int d = 0; d < nDim; ++d) res[RHOVX_S + d] += pLF * UnitNormal[d] * Area;
+  if (!implicit) return;
+
+  for (int k = 0; k < nVar * nVar; ++k) Ji[k] = Jj[k] = 0.0;
+  double MLD[64] = {0}, MRD[64] = {0};
+  MLD[RHO_S] = -mL / Density_i;
+  MRD[RHO_S] = -mR / Density_j;
+  for (int d = 0; d < nDim; ++d) {
+    MLD[RHOVX_S + d] = UnitNormal[d] / (Density_i * MeanSoundSpeed);
+    MRD[RHOVX_S + d] = UnitNormal[d] / (Density_j * MeanSoundSpeed);
+  }
+  double MPL[64], MPR[64];
+  if (std::abs(mL) < 1.0)
+    for (int v = 0; v < nVar; ++v) MPL[v] = MLD[v] * (0.5 * (mL + 1.0) + 4.0 * beta * mL * (mL * mL - 1.0));
+  else
+    for (int v = 0; v < nVar; ++v) MPL[v] = MLD[v] * (0.5 * (1.0 + std::abs(mL) / mL));
+  if (std::abs(mR) < 1.0)
+    for (int v = 0; v < nVar; ++v) MPR[v] = MRD[v] * (0.5 * (1.0 - mR) + 4.0 * beta * mR * (1.0 - mR * mR));
+  else
+    for (int v = 0; v < nVar; ++v) MPR[v] = MRD[v] * (0.5 * (1.0 - std::abs(mR) / mR));
+  double SL[64] = {0}, SR[64] = {0};
+  if (mF2 == mRef2) {
+    for (int v = 0; v < nVar; ++v) {
+      SL[v] = MLD[v] * mL * (1.0 - mF) / mF;
+      SR[v] = MRD[v] * mR * (1.0 - mF) / mF;
+    }
+  }
+  double MEL[64], MER[64];
+  const double MeanDensity = 0.5 * (Density_i + Density_j);
+  const double factor = std::max(1.0 - sigma * mF2, 0.0);
+  const double fpos = (factor > 0.0) ? 1.0 : 0.0;
+  for (int v = 0; v < nVar; ++v) {
+    MEL[v] = -kP / (MeanSoundSpeed * MeanSoundSpeed * fa * fa * MeanDensity * MeanDensity) *
+             ((fpos * sigma * mL * MLD[v] * (Pressure_j - Pressure_i) * fa * MeanDensity) +
+              (factor * Si[v] * fa * MeanDensity) + (factor * (Pressure_j - Pressure_i) * MeanDensity * SL[v]));
+    MER[v] = kP / (MeanSoundSpeed * MeanSoundSpeed * fa * fa * MeanDensity * MeanDensity) *
+             ((fpos * sigma * mR * MRD[v] * (Pressure_i - Pressure_j) * fa * MeanDensity) +
+              (factor * Sj[v] * fa * MeanDensity) - (factor * (Pressure_j - Pressure_i) * MeanDensity * SR[v]));
+  }
+  MEL[RHO_S] -= kP / (MeanSoundSpeed * MeanSoundSpeed * fa * MeanDensity * MeanDensity) * 0.5 * factor *
+                (Pressure_j - Pressure_i);
+  MER[RHO_S] -= kP / (MeanSoundSpeed * MeanSoundSpeed * fa * MeanDensity * MeanDensity) * 0.5 * factor *
+                (Pressure_j - Pressure_i);
+  double sign_m12 = 0.0;
+  if (m12 != 0.0) sign_m12 = std::abs(m12) / m12;
+  double MPlL[64], MMiL[64], MPlR[64], MMiR[64];
+  for (int v = 0; v < nVar; ++v) {
+    MPlL[v] = 0.5 * (MPL[v] - MEL[v]) * (1.0 + sign_m12);
+    MMiL[v] = 0.5 * (MPL[v] - MEL[v]) * (1.0 - sign_m12);
+    MPlR[v] = 0.5 * (MPR[v] - MER[v]) * (1.0 + sign_m12);
+    MMiR[v] = 0.5 * (MPR[v] - MER[v]) * (1.0 - sign_m12);
+  }
+  for (int a = 0; a < nVar; ++a)
+    for (int b = 0; b < nVar; ++b) {
+      Ji[a * nVar + b] += MeanSoundSpeed * ((MPlL[b] * Density_i * Phi_i[a]) + (MMiL[b] * Density_j * Phi_j[a]));
+      Jj[a * nVar + b] += MeanSoundSpeed * ((MPlR[b] * Density_i * Phi_i[a]) + (MMiR[b] * Density_j * Phi_j[a]));
+    }
+  for (int v = 0; v < nVar; ++v) {
+    Ji[v * nVar + v] += MeanSoundSpeed * mLF;
+    Jj[v * nVar + v] += MeanSoundSpeed * mRF;
+  }
+  for (int v = 0; v < nVar; ++v) {
+    Ji[RHOE_S * nVar + v] += MeanSoundSpeed * mLF * Si[v];
+    Jj[RHOE_S * nVar + v] += MeanSoundSpeed * mRF * Sj[v];
+  }
+  double PPL[64] = {0}, PPR[64] = {0};
+  if (std::abs(mL) < 1.0)
+    for (int v = 0; v < nVar; ++v)
+      PPL[v] = 0.25 * (mL + 1.0) * (3.0 * (1.0 - mL) + 4.0 * alpha * (5.0 * mL * mL - 1.0) * (mL - 1.0)) * MLD[v] +
+               15.0 / 8.0 * SL[v] * mL * (mL * mL - 1.0) * (mL * mL - 1.0);
+  if (std::abs(mR) < 1.0)
+    for (int v = 0; v < nVar; ++v)
+      PPR[v] = 0.25 * (mR - 1.0) * (3.0 * (1.0 + mR) + 4.0 * alpha * (1.0 - 5.0 * mR * mR) * (mR + 1.0)) * MRD[v] -
+               15.0 / 8.0 * SR[v] * mR * (mR * mR - 1.0) * (mR * mR - 1.0);
+  double PEL[64], PER[64];
+  for (int v = 0; v < nVar; ++v) {
+    PEL[v] = Ku * pRM * MeanSoundSpeed *
+             ((PPL[v] * (Density_i + Density_j) * fa * (ProjVelocity_j - ProjVelocity_i)) +
+              (pLP * (Density_i + Density_j) * (ProjVelocity_j - ProjVelocity_i) * SL[v]));
+    PER[v] = Ku * pLP * MeanSoundSpeed *
+             ((PPR[v] * (Density_i + Density_j) * fa * (ProjVelocity_j - ProjVelocity_i)) +
+              (pRM * (Density_i + Density_j) * (ProjVelocity_j - ProjVelocity_i) * SR[v]));
+  }
+  PEL[RHO_S] += Ku * pRM * MeanSoundSpeed * pLP * fa *
+                ((ProjVelocity_j - ProjVelocity_i) + (Density_i + Density_j) * ProjVelocity_i / Density_i);
+  PER[RHO_S] += Ku * pLP * MeanSoundSpeed * pRM * fa *
+                ((ProjVelocity_j - ProjVelocity_i) - (Density_i + Density_j) * ProjVelocity_j / Density_j);
+  for (int d = 0; d < nDim; ++d) {
+    PEL[RHOVX_S + d] -= Ku * pRM * MeanSoundSpeed * pLP * fa * (Density_i + Density_j) * UnitNormal[d] / Density_i;
+    PER[RHOVX_S + d] += Ku * pLP * MeanSoundSpeed * pRM * fa * (Density_i + Density_j) * UnitNormal[d] / Density_j;
+  }
+  double PDL[64], PDR[64];
+  for (int v = 0; v < nVar; ++v) {
+    PDL[v] = pLP * Si[v] + Pressure_i * PPL[v] - PEL[v];
+    PDR[v] = pRM * Sj[v] + Pressure_j * PPR[v] - PER[v];
+  }
+  for (int d = 0; d < nDim; ++d)
+    for (int b = 0; b < nVar; ++b) {
+      Ji[(RHOVX_S + d) * nVar + b] += UnitNormal[d] * PDL[b];
+      Jj[(RHOVX_S + d) * nVar + b] += UnitNormal[d] * PDR[b];
+    }
+  for (int k = 0; k < nVar * nVar; ++k) {
+    Ji[k] *= Area;
+    Jj[k] *= Area;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// a9/a10: kinetics + PaSR source  (numerics_direct_reactive.cpp:1728-1879,
+//          reacting_model_library.cpp:99-350, 701-705, 803-920)
+// ------------------------------------------------------------------------------------------------
+struct KinScratch {
+  double Ys[32], Cs[32], F[16], B[16], Kc[16], omega_ir[32 * 16], Df[32 * 16], k_pasr[16], Kcd[16];
+};
+
+double delta_gibbs(const Mech& m, int r, double T, double* dnu_out) {
+  double dG = 0.0, dnu = 0.0;
+  for (int s = 0; s < m.ns; ++s) {
+    const double dc = m.sp[s * m.nr + r] - m.sr[s * m.nr + r];
+    if (dc != 0.0) {
+      dG += dc * (spline(m, P_H, s, T) - T * spline(m, P_S, s, T));
+      dnu += dc;
+    }
+  }
+  *dnu_out = dnu;
+  return dG;
+}
+
+void set_source_term(const Mech& m, double T, double rho, const double* ys, KinScratch& k) {
+  for (int s = 0; s < m.ns; ++s) {
+    double y = ys[s];
+    if (y < 0.0) y = 1.0e-30;
+    k.Ys[s] = y;
+    k.Cs[s] = 1.0e3 * rho * y / m.mm[s];
+  }
+  for (int r = 0; r < m.nr; ++r) {
+    const double kf = m.A[r] * std::pow(T, m.beta[r]) * std::exp(-m.Ta[r] / T);
+    double kb;
+    if (!m.hasb[r]) {
+      double dnu;
+      const double dG = delta_gibbs(m, r, T, &dnu);
+      const double RT = R_UNGAS * T;
+      const double lnKp = -dG / RT;
+      const double lnKc = lnKp - dnu * std::log(R_UNGAS_ATM * T);
+      k.Kc[r] = std::exp(lnKc);
+      const bool complete = std::exp(lnKp) > 1.0e10;
+      if (!m.rev[r]) kb = 0.0;
+      else if (complete) kb = 0.0;
+      else kb = kf / k.Kc[r];
+    } else {
+      kb = m.Ab[r] * std::pow(T, m.betab[r]) * std::exp(-m.Tab[r] / T);
+      k.Kc[r] = kf / kb;
+    }
+    double fr = 0.0, br = 0.0;
+    bool zero = false;
+    for (int s : m.neg_reac[r]) if (k.Ys[s] < 1.0e-15) { zero = true; break; }
+    if (!zero) {
+      fr = 1.0;
+      for (int s = 0; s < m.ns; ++s) fr *= std::pow(k.Cs[s], m.er[r * m.ns + s]);
+      fr *= kf;
+    }
+    zero = false;
+    for (int s : m.neg_prod[r]) if (k.Ys[s] < 1.0e-15) { zero = true; break; }
+    if (!zero) {
+      br = 1.0;
+      for (int s = 0; s < m.ns; ++s) br *= std::pow(k.Cs[s], m.ep[r * m.ns + s]);
+      br *= kb;
+    }
+    k.F[r] = fr;
+    k.B[r] = br;
+  }
+  for (int r = 0; r < m.nr; ++r)
+    for (int s = 0; s < m.ns; ++s)
+      k.omega_ir[s * m.nr + r] = 1.0e-3 * m.mm[s] * (m.sp[s * m.nr + r] - m.sr[s * m.nr + r]) * (k.F[r] - k.B[r]);
+}
+
+void set_dfr_drhos(const Mech& m, double rho, KinScratch& k) {
+  for (int s = 0; s < m.ns; ++s)
+    for (int r = 0; r < m.nr; ++r) {
+      k.Df[s * m.nr + r] = 0.0;
+      if (k.Ys[s] > 1.0e-10)
+        k.Df[s * m.nr + r] = (k.F[r] * m.er[r * m.ns + s] - k.B[r] * m.ep[r * m.ns + s]) / (rho * k.Ys[s]);
+    }
+}
+
+void assemble_pasr(const Mech& m, double omega_turb, double C_mu, double lb, KinScratch& k) {
+  const double tau_mix = 1 / (C_mu * omega_turb);
+  for (int r = 0; r < m.nr; ++r) {
+    double hd = -1.0;
+    for (int s = 0; s < m.ns; ++s)
+      if (m.sp[s * m.nr + r] != 0.0 || m.sr[s * m.nr + r] != 0.0) {
+        const double v = std::fabs(k.Df[s * m.nr + r] * m.mm[s]);
+        if (hd < 0.0 || v > hd) hd = v;
+      }
+    const double tau_c = 1 / hd;
+    double kk;
+    if (std::isinf(tau_c)) kk = 1.0;
+    else if ((tau_c / (tau_c + tau_mix)) < lb) kk = lb;
+    else kk = tau_c / (tau_c + tau_mix);
+    k.k_pasr[r] = kk;
+  }
+}
+
+// Set_BackFor_Contr (:233-289): (back_contr, for_contr) per reaction
+void back_for_contr(const Mech& m, double T, KinScratch& k, double* bc, double* fc) {
+  const double epsilon = 1.0e-6;
+  const double Tp = T + epsilon * T;
+  const double RT = R_UNGAS * Tp;
+  const double lnRT = std::log(R_UNGAS_ATM * Tp);
+  for (int r = 0; r < m.nr; ++r) {
+    double Kcp;
+    if (!m.hasb[r]) {
+      if (k.B[r] > 0.0) {
+        double dnu;
+        const double dG = delta_gibbs(m, r, Tp, &dnu);
+        Kcp = std::exp(-dG / RT - dnu * lnRT);
+      } else {
+        Kcp = k.Kc[r];
+      }
+    } else {
+      const double kfp = m.A[r] * std::pow(Tp, m.beta[r]) * std::exp(-m.Ta[r] / Tp);
+      const double kbp = m.Ab[r] * std::pow(Tp, m.betab[r]) * std::exp(-m.Tab[r] / Tp);
+      Kcp = kfp / kbp;
+    }
+    k.Kcd[r] = (Kcp - k.Kc[r]) / (Tp - T);
+  }
+  for (int r = 0; r < m.nr; ++r) {
+    const double tmp = (m.beta[r] + m.Ta[r] / T) / T;
+    fc[r] = k.F[r] * tmp;
+    if (!m.hasb[r]) bc[r] = k.B[r] * (tmp - k.Kcd[r] / k.Kc[r]);
+    else bc[r] = k.B[r] * (m.betab[r] + m.Tab[r] / T) / T;
+  }
+}
+
+void source(const Mech& m, int nDim, const double* V, const double* S, double vol, double omega_turb, bool rans,
+            bool implicit, double C_mu, double lb, double rho_ref, double t_ref, double T_ref, double* res, double* J) {
+  const int ns = m.ns, nr = m.nr, nVar = ns + nDim + 2;
+  const int RHOS_P = nDim + 5, RHO_P = nDim + 2, RHOS_S = nDim + 2;
+  KinScratch k;
+  const double rho = V[RHO_P];
+  const double dim_temp = V[0] * T_ref;
+  const double dim_rho = rho * rho_ref;
+  set_source_term(m, dim_temp, dim_rho, V + RHOS_P, k);
+  double omega[32];
+  if (rans) {
+    set_dfr_drhos(m, dim_rho, k);
+    assemble_pasr(m, omega_turb, C_mu, lb, k);
+    for (int s = 0; s < ns; ++s) {
+      double o = 0.0;
+      for (int r = 0; r < nr; ++r) o += k.k_pasr[r] * k.omega_ir[s * nr + r];
+      omega[s] = o;
+    }
+  } else {
+    for (int s = 0; s < ns; ++s) {
+      double o = 0.0;
+      for (int r = 0; r < nr; ++r) o += k.omega_ir[s * nr + r];
+      omega[s] = o;
+    }
+  }
+  for (int v = 0; v < nVar; ++v) res[v] = 0.0;
+  for (int s = 0; s < ns; ++s) res[RHOS_S + s] = omega[s] * (-vol / (rho_ref / t_ref));
+  if (!implicit) return;
+  for (int q = 0; q < nVar * nVar; ++q) J[q] = 0.0;
+  double bc[16], fc[16];
+  back_for_contr(m, dim_temp, k, bc, fc);
+  // GetTurbSourceJacobian (:295-319) / GetSourceJacobian (:325-350): [ns][ns+1]
+  double sj[32 * 33];
+  for (int q = 0; q < ns * (ns + 1); ++q) sj[q] = 0.0;
+  for (int r = 0; r < nr; ++r)
+    for (int s = 0; s < ns; ++s) {
+      const double fixed = 1.0e-3 * m.mm[s] * (m.sp[s * nr + r] - m.sr[s * nr + r]);
+      if (rans) {
+        sj[s * (ns + 1)] += fixed * (fc[r] - bc[r]) * k.k_pasr[r];
+        for (int j = 0; j < ns; ++j)
+          if (k.Ys[j] > 1.0e-10) sj[s * (ns + 1) + j + 1] += fixed * k.k_pasr[r] * k.Df[j * nr + r];
+      } else {
+        sj[s * (ns + 1)] += fixed * (fc[r] - bc[r]);
+        for (int j = 0; j < ns; ++j)
+          if (k.Ys[j] > 1.0e-10)
+            sj[s * (ns + 1) + j + 1] +=
+                fixed * (k.F[r] * m.er[r * ns + j] - k.B[r] * m.ep[r * ns + j]) / (dim_rho * k.Ys[j]);
+      }
+    }
+  for (int s = 0; s < ns; ++s) {
+    const double fixed = sj[s * (ns + 1)] * t_ref * T_ref / rho_ref;
+    double* row = J + (RHOS_S + s) * nVar;
+    row[0] = -fixed * S[0] * vol;
+    for (int d = 0; d < nDim; ++d) row[1 + d] = -fixed * S[1 + d] * vol;
+    row[nDim + 1] = -fixed * S[nDim + 1] * vol;
+    for (int j = 0; j < ns; ++j)
+      row[RHOS_S + j] = -fixed * S[RHOS_S + j] * vol - sj[s * (ns + 1) + j + 1] * t_ref * vol;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Eigen 3.3.7 algorithms restated (externals/Eigen, parity dependency of the viscous flux):
+//   BiCGSTAB with DiagonalPreconditioner  src/IterativeLinearSolvers/BiCGSTAB.h:28-100
+//   ColPivHouseholderQR compute + solve    src/QR/ColPivHouseholderQR.h:480-611
+// Matrices here are row-major n x n.
+// ------------------------------------------------------------------------------------------------
+// Eigen's vectorised reduction order for a contiguous, 16-byte-aligned double vector
+// (Core/Redux.h LinearVectorizedTraversal, SSE2 packets of 2, two packet accumulators; no FMA).
+double eigen_redux_prod(int n, const double* a, const double* b) {
+  auto p = [&](int k) { return a[k] * b[k]; };
+  const int as2 = (n / 4) * 4, as = (n / 2) * 2;
+  double res;
+  if (as) {
+    double r0a = p(0), r0b = p(1);
+    if (as > 2) {
+      double r1a = p(2), r1b = p(3);
+      for (int k = 4; k < as2; k += 4) {
+        r0a += p(k); r0b += p(k + 1);
+        r1a += p(k + 2); r1b += p(k + 3);
+      }
+      r0a += r1a; r0b += r1b;
+      if (as > as2) { r0a += p(as2); r0b += p(as2 + 1); }
+    }
+    res = r0a + r0b;
+    for (int k = as; k < n; ++k) res += p(k);
+  } else {
+    res = p(0);
+    for (int k = 1; k < n; ++k) res += p(k);
+  }
+  return res;
+}
+double dot(int n, const double* a, const double* b) { return eigen_redux_prod(n, a, b); }
+
+// Eigen's column-major GEMV order for an n x n heap (16-byte aligned) matrix
+// (Core/products/GeneralMatrixVector.h:88-319): 4 columns at once, rows in packets of 2 as
+// res + ((a0 x0 + a1 x1) + (a2 x2 + a3 x3)), odd tail row by sequential multiply-adds, then the
+// leftover columns one by one. A is given row-major here; y = A x.
+void matvec(int n, const double* A, const double* x, double* y) {
+  for (int i = 0; i < n; ++i) y[i] = 0.0;
+  const int aligned = n & ~1;
+  const int bound = (n / 4) * 4;
+  for (int c = 0; c < bound; c += 4) {
+    for (int r = 0; r < aligned; ++r)
+      y[r] = y[r] + ((A[r * n + c] * x[c] + A[r * n + c + 1] * x[c + 1]) +
+                     (A[r * n + c + 2] * x[c + 2] + A[r * n + c + 3] * x[c + 3]));
+    for (int r = aligned; r < n; ++r) {
+      y[r] = A[r * n + c] * x[c] + y[r];
+      y[r] = A[r * n + c + 1] * x[c + 1] + y[r];
+      y[r] = A[r * n + c + 2] * x[c + 2] + y[r];
+      y[r] = A[r * n + c + 3] * x[c + 3] + y[r];
+    }
+  }
+  for (int c = bound; c < n; ++c) {
+    for (int r = 0; r < aligned; ++r) y[r] = A[r * n + c] * x[c] + y[r];
+    for (int r = aligned; r < n; ++r) y[r] += A[r * n + c] * x[c];
+  }
+}
+
+void bicgstab(int n, const double* A, const double* rhs, double* x, double tol) {
+  const int maxIters = 2 * n;
+  double invdiag[32];
+  for (int j = 0; j < n; ++j) invdiag[j] = (A[j * n + j] != 0.0) ? 1.0 / A[j * n + j] : 1.0;
+  for (int i = 0; i < n; ++i) x[i] = 0.0;
+  double r[32], r0[32], tmpv[32];
+  matvec(n, A, x, tmpv);
+  for (int i = 0; i < n; ++i) r[i] = rhs[i] - tmpv[i];
+  for (int i = 0; i < n; ++i) r0[i] = r[i];
+  double r0_sqnorm = dot(n, r0, r0);
+  const double rhs_sqnorm = dot(n, rhs, rhs);
+  if (rhs_sqnorm == 0) {
+    for (int i = 0; i < n; ++i) x[i] = 0.0;
+    return;
+  }
+  double rho = 1, alpha = 1, w = 1;
+  double v[32] = {0}, p[32] = {0}, y[32], z[32], s[32], t[32];
+  const double tol2 = tol * tol * rhs_sqnorm;
+  const double eps = std::numeric_limits<double>::epsilon();
+  const double eps2 = eps * eps;
+  int i = 0, restarts = 0;
+  while (dot(n, r, r) > tol2 && i < maxIters) {
+    const double rho_old = rho;
+    rho = dot(n, r0, r);
+    if (std::abs(rho) < eps2 * r0_sqnorm) {
+      matvec(n, A, x, tmpv);
+      for (int q = 0; q < n; ++q) r[q] = rhs[q] - tmpv[q];
+      for (int q = 0; q < n; ++q) r0[q] = r[q];
+      rho = r0_sqnorm = dot(n, r, r);
+      if (restarts++ == 0) i = 0;
+    }
+    const double beta = (rho / rho_old) * (alpha / w);
+    for (int q = 0; q < n; ++q) p[q] = r[q] + beta * (p[q] - w * v[q]);
+    for (int q = 0; q < n; ++q) y[q] = invdiag[q] * p[q];
+    matvec(n, A, y, v);
+    alpha = rho / dot(n, r0, v);
+    for (int q = 0; q < n; ++q) s[q] = r[q] - alpha * v[q];
+    for (int q = 0; q < n; ++q) z[q] = invdiag[q] * s[q];
+    matvec(n, A, z, t);
+    const double tmp = dot(n, t, t);
+    w = (tmp > 0.0) ? dot(n, t, s) / tmp : 0.0;
+    for (int q = 0; q < n; ++q) x[q] += alpha * y[q] + w * z[q];
+    for (int q = 0; q < n; ++q) r[q] = s[q] - w * t[q];
+    ++i;
+  }
+}
+
+struct ColPivQR {
+  int n;
+  double qr[32 * 32];  // row-major
+  double hc[32];
+  int perm[32];
+  int nonzero;
+};
+
+void qr_compute(int n, const double* M, ColPivQR& f) {
+  f.n = n;
+  std::memcpy(f.qr, M, sizeof(double) * n * n);
+  double* Q = f.qr;
+  auto at = [&](int i, int j) -> double& { return Q[i * n + j]; };
+  double normsU[32], normsD[32];
+  int trans[32];
+  for (int k = 0; k < n; ++k) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += at(i, k) * at(i, k);
+    normsD[k] = std::sqrt(s);
+    normsU[k] = normsD[k];
+  }
+  double mx = normsU[0];
+  for (int k = 1; k < n; ++k) mx = std::max(mx, normsU[k]);
+  const double epsm = std::numeric_limits<double>::epsilon();
+  const double threshold_helper = (mx * epsm) * (mx * epsm) / double(n);
+  const double norm_downdate_threshold = std::sqrt(epsm);
+  f.nonzero = n;
+  for (int k = 0; k < n; ++k) {
+    int big = k;
+    for (int j = k + 1; j < n; ++j)
+      if (normsU[j] > normsU[big]) big = j;
+    const double big_sq = normsU[big] * normsU[big];
+    if (f.nonzero == n && big_sq < threshold_helper * double(n - k)) f.nonzero = k;
+    trans[k] = big;
+    if (k != big) {
+      for (int i = 0; i < n; ++i) std::swap(at(i, k), at(i, big));
+      std::swap(normsU[k], normsU[big]);
+      std::swap(normsD[k], normsD[big]);
+    }
+    // makeHouseholderInPlace on column k rows k..n-1
+    double tailSq = 0.0;
+    for (int i = k + 1; i < n; ++i) tailSq += at(i, k) * at(i, k);
+    const double c0 = at(k, k);
+    double tau, beta;
+    if (tailSq <= std::numeric_limits<double>::min()) {
+      tau = 0.0;
+      beta = c0;
+      for (int i = k + 1; i < n; ++i) at(i, k) = 0.0;
+    } else {
+      beta = std::sqrt(c0 * c0 + tailSq);
+      if (c0 >= 0.0) beta = -beta;
+      for (int i = k + 1; i < n; ++i) at(i, k) = at(i, k) / (c0 - beta);
+      tau = (beta - c0) / beta;
+    }
+    f.hc[k] = tau;
+    at(k, k) = beta;
+    // applyHouseholderOnTheLeft to bottomRightCorner(n-k, n-k-1)
+    if (n - k == 1) {
+      for (int j = k + 1; j < n; ++j) at(k, j) *= (1.0 - tau);
+    } else if (tau != 0.0) {
+      for (int j = k + 1; j < n; ++j) {
+        double tmp = 0.0;
+        for (int i = k + 1; i < n; ++i) tmp += at(i, k) * at(i, j);
+        tmp += at(k, j);
+        at(k, j) -= tau * tmp;
+        for (int i = k + 1; i < n; ++i) at(i, j) -= tau * at(i, k) * tmp;
+      }
+    }
+    for (int j = k + 1; j < n; ++j) {
+      if (normsU[j] != 0.0) {
+        double temp = std::abs(at(k, j)) / normsU[j];
+        temp = (1.0 + temp) * (1.0 - temp);
+        temp = temp < 0.0 ? 0.0 : temp;
+        const double rr = normsU[j] / normsD[j];
+        const double temp2 = temp * (rr * rr);
+        if (temp2 <= norm_downdate_threshold) {
+          double s = 0.0;
+          for (int i = k + 1; i < n; ++i) s += at(i, j) * at(i, j);
+          normsD[j] = std::sqrt(s);
+          normsU[j] = normsD[j];
+        } else {
+          normsU[j] *= std::sqrt(temp);
+        }
+      }
+    }
+  }
+  for (int k = 0; k < n; ++k) f.perm[k] = k;
+  for (int k = 0; k < n; ++k) std::swap(f.perm[k], f.perm[trans[k]]);
+}
+
+void qr_solve(const ColPivQR& f, const double* rhs, double* dst) {
+  const int n = f.n, np = f.nonzero;
+  if (np == 0) {
+    for (int i = 0; i < n; ++i) dst[i] = 0.0;
+    return;
+  }
+  double c[32];
+  for (int i = 0; i < n; ++i) c[i] = rhs[i];
+  for (int k = 0; k < np; ++k) {
+    const double tau = f.hc[k];
+    if (n - k == 1) {
+      c[k] *= (1.0 - tau);
+    } else if (tau != 0.0) {
+      double tmp = 0.0;
+      for (int i = k + 1; i < n; ++i) tmp += f.qr[i * n + k] * c[i];
+      tmp += c[k];
+      c[k] -= tau * tmp;
+      for (int i = k + 1; i < n; ++i) c[i] -= tau * f.qr[i * n + k] * tmp;
+    }
+  }
+  for (int i = np - 1; i >= 0; --i) {  // column-oriented back substitution
+    c[i] /= f.qr[i * n + i];
+    for (int j = 0; j < i; ++j) c[j] -= c[i] * f.qr[j * n + i];
+  }
+  for (int i = 0; i < np; ++i) dst[f.perm[i]] = c[i];
+  for (int i = np; i < n; ++i) dst[f.perm[i]] = 0.0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// a3-a6: CAvgGradReactive_Flow::ComputeResidual (numerics_direct_reactive.cpp:1425-1678) with
+// SetLaminarTensorFlux (:1099-1190), Solve_SM (:451-470), GetGamma (library :771-798),
+// SST_Reactive_ResidualClosure (:656-852), Get_Molar2MassGrad_Operator (:861-880),
+// SetLaminarViscousProjJacs (:1200-1401), SST_Reactive_JacobianClosure (:891-1090).
+// ------------------------------------------------------------------------------------------------
+struct ViscParams {
+  double T_ref, E_ref, R_ref, Prandtl_Turb, Lewis_Turb;
+  int rans, implicit;
+};
+
+void visc_flux(const Mech& m, int nDim, const ViscParams& P, const double* Vi, const double* Vj, const double* Gi,
+               const double* Gj, double mu_i, double mu_j, double k_i, double k_j, const double* Dij_i,
+               const double* Dij_j, const double* Ci, const double* Cj, const double* Normal, const double* Si,
+               const double* Sj, double tke_i, double tke_j, double mut_i, double mut_j, double sigma_k,
+               const double* gk_i, const double* gk_j, double* res, double* Ji, double* Jj) {
+  const int ns = m.ns;
+  const int nVar = ns + nDim + 2, nPrimVar = ns + nDim + 5, nGrad = ns + nDim + 2;
+  const int T_P = 0, VX_P = 1, RHO_P = nDim + 2, RHOS_P = nDim + 5;
+  const int RHO_S = 0, RHOVX_S = 1, RHOE_S = nDim + 1, RHOS_S = nDim + 2;
+  const int T_G = 0, VX_G = 1, RHOS_G = nDim + 2;
+  const int T_A = 0, VX_A = 1, RHOS_A = 1 + nDim;  // avg-grad rows
+  const int nAvg = ns + nDim + 1;
+
+  const double Mean_mu = 2.0 / (1.0 / mu_i + 1.0 / mu_j);
+  const double Mean_k = 2.0 / (1.0 / k_i + 1.0 / k_j);
+  double Dm[32 * 32];  // [a][b] in the same (column-major) indexing as the input
+  double Dmax = -std::numeric_limits<double>::infinity();
+  for (int q = 0; q < ns * ns; ++q) {
+    Dm[q] = 2.0 / (1.0 / Dij_i[q] + 1.0 / Dij_j[q]);
+    Dmax = std::max(Dmax, Dm[q]);
+  }
+  auto D = [&](const double* d, int a, int b) { return d[b * ns + a]; };  // column-major (a,b)
+  double Vm[64];
+  for (int v = 0; v < nPrimVar; ++v) Vm[v] = 0.5 * (Vi[v] + Vj[v]);
+  double Xs_i[32], Xs_j[32], ytmp[32];
+  molar_from_mass(m, Vi + RHOS_P, ytmp, Xs_i);
+  molar_from_mass(m, Vj + RHOS_P, ytmp, Xs_j);
+  double Edge[3];
+  for (int d = 0; d < nDim; ++d) Edge[d] = Cj[d] - Ci[d];
+  double G[32][3];  // mean gradient [nAvg][nDim]
+  for (int d = 0; d < nDim; ++d) {
+    G[T_A][d] = 0.5 * (Gi[T_G * nDim + d] + Gj[T_G * nDim + d]);
+    for (int e = 0; e < nDim; ++e) G[VX_A + e][d] = 0.5 * (Gi[(VX_G + e) * nDim + d] + Gj[(VX_G + e) * nDim + d]);
+    for (int s = 0; s < ns; ++s) G[RHOS_A + s][d] = 0.5 * (Gi[(RHOS_G + s) * nDim + d] + Gj[(RHOS_G + s) * nDim + d]);
+  }
+  (void)nGrad;
+  double Proj[32];
+  for (int r = 0; r < nAvg; ++r) {
+    double s = 0.0;
+    for (int d = 0; d < nDim; ++d) s += G[r][d] * Edge[d];
+    Proj[r] = s;
+  }
+  double dist2 = 0.0;
+  for (int d = 0; d < nDim; ++d) dist2 += Edge[d] * Edge[d];
+  if (!(dist2 > EPS)) throw std::runtime_error("Error: You are trying to compute flux between a node and itself");
+  double Diff[32];
+  Diff[T_A] = Vj[T_P] - Vi[T_P];
+  for (int d = 0; d < nDim; ++d) Diff[VX_A + d] = Vj[VX_P + d] - Vi[VX_P + d];
+  for (int s = 0; s < ns; ++s) Diff[RHOS_A + s] = Xs_j[s] - Xs_i[s];
+  for (int r = 0; r < nAvg; ++r)
+    for (int d = 0; d < nDim; ++d) G[r][d] -= (Proj[r] - Diff[r]) * Edge[d] / dist2;
+
+  // --- SetLaminarTensorFlux
+  double Flux[32][3], PF[32];
+  for (int v = 0; v < nVar; ++v) {
+    PF[v] = 0.0;
+    for (int d = 0; d < nDim; ++d) Flux[v][d] = 0.0;
+  }
+  const double rho = Vm[RHO_P], T = Vm[T_P];
+  const double dim_temp = T * P.T_ref;
+  double hs[32], Ys[32], Xs[32], yc[32];
+  for (int s = 0; s < ns; ++s) hs[s] = spline(m, P_H, s, dim_temp) / m.mm[s] / P.E_ref;
+  for (int s = 0; s < ns; ++s) Ys[s] = Vm[RHOS_P + s];
+  molar_from_mass(m, Ys, yc, Xs);
+  double div_vel = 0.0;
+  for (int d = 0; d < nDim; ++d) div_vel += G[VX_A + d][d];
+  double tau[3][3];
+  for (int a = 0; a < nDim; ++a)
+    for (int b = 0; b < nDim; ++b) tau[a][b] = 0.0;
+  for (int a = 0; a < nDim; ++a) {
+    for (int b = 0; b < nDim; ++b) tau[a][b] += Mean_mu * (G[VX_A + b][a] + G[VX_A + a][b]);
+    tau[a][a] -= TWO3 * (Mean_mu * div_vel);
+  }
+  const double alpha = 1.0 / (rho * Dmax);
+  double Gxn[32];
+  for (int s = 0; s < ns; ++s) Gxn[s] = 0.0;
+  for (int a = 0; a < nDim; ++a) {
+    for (int b = 0; b < nDim; ++b) {
+      Flux[RHOVX_S + b][a] = tau[a][b];
+      Flux[RHOE_S][a] += tau[a][b] * Vm[VX_P + b];
+    }
+    Flux[RHOE_S][a] += Mean_k * G[T_A][a];
+    for (int s = 0; s < ns; ++s) Gxn[s] += G[RHOS_A + s][a] * Normal[a];
+  }
+  // Solve_SM: Gamma (GetGamma) + alpha*Y, BiCGSTAB tol 1e-11
+  double Gt[32 * 32];
+  {
+    double sigma = 0.0, massTot = 0.0;
+    for (int s = 0; s < ns; ++s) sigma += Ys[s];
+    for (int s = 0; s < ns; ++s) massTot += Ys[s] / m.mm[s];
+    massTot = 1.0 / massTot;
+    for (int a = 0; a < ns; ++a)
+      for (int b = 0; b < ns; ++b) {
+        double g;
+        if (a != b) {
+          g = -sigma * massTot * Xs[a] / (rho * m.mm[b] * D(Dm, a, b));
+        } else {
+          double tmp = 0.0;
+          for (int c = 0; c < ns; ++c)
+            if (c != a) tmp += Xs[c] / D(Dm, a, c);
+          g = sigma * massTot * tmp / (rho * m.mm[a]);
+        }
+        Gt[a * ns + b] = g + alpha * Ys[a];
+      }
+  }
+  double nGxn[32], Jd[32];
+  for (int s = 0; s < ns; ++s) nGxn[s] = -Gxn[s];
+  bicgstab(ns, Gt, nGxn, Jd, 1.0e-11);
+  {
+    double ones[32];
+    for (int s = 0; s < ns; ++s) ones[s] = 1.0;
+    PF[RHO_S] = -eigen_redux_prod(ns, Jd, ones);  // Jd.sum(): same packet order
+  }
+  for (int s = 0; s < ns; ++s) {
+    PF[RHOE_S] += -hs[s] * Jd[s];
+    PF[RHOS_S + s] = -Jd[s];
+  }
+
+  double Mean_mut = 0.0, Mean_tke = 0.0, Cps[32];
+  double MassGrads[32][3];
+  if (P.rans) {
+    Mean_mut = 2.0 / (1.0 / mut_i + 1.0 / mut_j);
+    Mean_tke = 0.5 * (tke_i + tke_j);
+    double gk[3];
+    for (int d = 0; d < nDim; ++d) gk[d] = 0.5 * (gk_i[d] + gk_j[d]);
+    for (int s = 0; s < ns; ++s) Cps[s] = spline(m, P_CP, s, dim_temp) / m.mm[s] / P.R_ref;
+    double dv = 0.0;
+    for (int d = 0; d < nDim; ++d) dv += G[VX_A + d][d];
+    double tt[3][3];
+    for (int a = 0; a < nDim; ++a)
+      for (int b = 0; b < nDim; ++b) tt[a][b] = 0.0;
+    for (int a = 0; a < nDim; ++a) {
+      for (int b = 0; b < nDim; ++b) tt[a][b] += Mean_mut * (G[VX_A + b][a] + G[VX_A + a][b]);
+      tt[a][a] -= TWO3 * (Mean_mut * dv + Mean_tke * rho);
+    }
+    // Get_Molar2MassGrad_Operator
+    double Mt[32 * 32];
+    {
+      double sig = 0.0;
+      for (int s = 0; s < ns; ++s) sig += Xs[s];
+      double mt = 0.0;
+      for (int s = 0; s < ns; ++s) mt += m.mm[s];
+      for (int a = 0; a < ns; ++a)
+        for (int b = 0; b < ns; ++b)
+          Mt[a * ns + b] = mt / m.mm[a] * (Ys[a] - Xs[a] + sig) * (a == b) +
+                           mt * (Ys[a] / m.mm[a] - Xs[a] / m.mm[b]) * (a != b);
+    }
+    ColPivQR qr;
+    qr_compute(ns, Mt, qr);
+    for (int d = 0; d < nDim; ++d) {
+      double rhs[32], sol[32];
+      for (int s = 0; s < ns; ++s) rhs[s] = G[RHOS_A + s][d];
+      qr_solve(qr, rhs, sol);
+      for (int s = 0; s < ns; ++s) MassGrads[s][d] = sol[s];
+    }
+    for (int s = 0; s < ns; ++s)
+      for (int d = 0; d < nDim; ++d)
+        if (std::abs(G[RHOS_A + s][d]) < 1e-8) MassGrads[s][d] = 0.0;
+    for (int a = 0; a < nDim; ++a) {
+      for (int b = 0; b < nDim; ++b) {
+        Flux[RHOVX_S + b][a] += tt[a][b];
+        Flux[RHOE_S][a] += tt[a][b] * Vm[VX_P + b];
+      }
+      for (int s = 0; s < ns; ++s)
+        PF[RHOS_S + s] += Mean_mut / (P.Prandtl_Turb * P.Lewis_Turb) * MassGrads[s][a] * Normal[a];
+      for (int s = 0; s < ns; ++s)
+        Flux[RHOE_S][a] += Mean_mut / (P.Prandtl_Turb * P.Lewis_Turb) * hs[s] * Ys[s] * MassGrads[s][a];
+      for (int s = 0; s < ns; ++s) Flux[RHOE_S][a] += Mean_mut / P.Prandtl_Turb * Cps[s] * Ys[s] * G[T_A][a];
+      Flux[RHOE_S][a] += (Mean_mu + Mean_mut / sigma_k) * gk[a];
+    }
+  }
+  for (int d = 0; d < nDim; ++d) {
+    for (int v = RHOVX_S; v < RHOVX_S + nDim; ++v) PF[v] += Flux[v][d] * Normal[d];
+    PF[RHOE_S] += Flux[RHOE_S][d] * Normal[d];
+  }
+  for (int v = 0; v < nVar; ++v) res[v] = PF[v];
+  if (!P.implicit) return;
+
+  // --- implicit part (:1576-1653)
+  double Ds_i[32], Ds_j[32], Ds[32];
+  for (int a = 0; a < ns; ++a) {
+    double di = 0.0, dj = 0.0;
+    for (int b = 0; b < ns; ++b)
+      if (b != a) {
+        di += Xs_i[b] / D(Dij_i, a, b);
+        dj += Xs_j[b] / D(Dij_j, a, b);
+      }
+    Ds_i[a] = (1.0 - Xs_i[a]) / di;
+    Ds_j[a] = (1.0 - Xs_j[a]) / dj;
+  }
+  for (int s = 0; s < ns; ++s) {
+    if (std::isnan(Ds_i[s]) || std::isinf(Ds_i[s])) Ds_i[s] = 0.0;
+    if (std::isnan(Ds_j[s]) || std::isinf(Ds_j[s])) Ds_j[s] = 0.0;
+    Ds[s] = 0.5 * (Ds_i[s] + Ds_j[s]);
+  }
+  double Area = 0.0;
+  for (int d = 0; d < nDim; ++d) Area += Normal[d] * Normal[d];
+  Area = std::sqrt(Area);
+  double UN[3];
+  for (int d = 0; d < nDim; ++d) UN[d] = Normal[d] / Area;
+  for (int s = 0; s < ns; ++s) Gxn[s] /= Area;
+  const double dij = std::sqrt(dist2), dS = Area;
+
+  static thread_local std::vector<double> buf;
+  buf.assign(4 * nVar * nVar, 0.0);
+  double* dFdVi = buf.data();
+  double* dFdVj = dFdVi + nVar * nVar;
+  double* dVdUi = dFdVj + nVar * nVar;
+  double* dVdUj = dVdUi + nVar * nVar;
+  auto FI = [&](int a, int b) -> double& { return dFdVi[a * nVar + b]; };
+  auto FJ = [&](int a, int b) -> double& { return dFdVj[a * nVar + b]; };
+  // SetLaminarViscousProjJacs
+  {
+    double theta = 0.0;
+    for (int d = 0; d < nDim; ++d) theta += UN[d] * UN[d];
+    const double rho_i = Vi[RHO_P], rho_j = Vj[RHO_P];
+    for (int s = 0; s < ns; ++s) Cps[s] = spline(m, P_CP, s, dim_temp) / m.mm[s] / P.R_ref;
+    static thread_local std::vector<double> djb;
+    djb.assign(2 * ns * (ns + 1), 0.0);
+    double* dJdr_j = djb.data();
+    double* dJdr_i = dJdr_j + ns * (ns + 1);
+    auto DJ = [&](double* a, int r, int c) -> double& { return a[r * (ns + 1) + c]; };
+    double totMass = 0.0, totMass_i = 0.0, totMass_j = 0.0, sigma_i = 0.0, sigma_j = 0.0;
+    for (int s = 0; s < ns; ++s) totMass += m.mm[s] * Xs[s];
+    for (int s = 0; s < ns; ++s) totMass_i += m.mm[s] * Xs_i[s];
+    for (int s = 0; s < ns; ++s) totMass_j += m.mm[s] * Xs_j[s];
+    for (int s = 0; s < ns; ++s) sigma_i += Xs_i[s];
+    for (int s = 0; s < ns; ++s) sigma_j += Xs_j[s];
+    for (int a = 0; a < ns; ++a)
+      for (int k = 0; k < ns; ++k) {
+        DJ(dJdr_j, a, k + 1) = -rho * m.mm[a] * Ds[a] * Xs_j[a] / (totMass * dij * sigma_j * rho_j);
+        DJ(dJdr_i, a, k + 1) = rho * m.mm[a] * Ds[a] * Xs_i[a] / (totMass * dij * sigma_i * rho_i);
+        for (int b = 0; b < ns; ++b) {
+          DJ(dJdr_j, a, k + 1) += rho * Ys[a] * m.mm[b] * Ds[b] * Xs_j[b] / (totMass * dij * sigma_j * rho_j);
+          DJ(dJdr_i, a, k + 1) -= rho * Ys[a] * m.mm[b] * Ds[b] * Xs_i[b] / (totMass * dij * sigma_i * rho_i);
+        }
+        DJ(dJdr_j, a, k + 1) += rho * Ys[a] * Ds[k] * totMass_j * sigma_j / (dij * totMass * rho_j);
+        DJ(dJdr_i, a, k + 1) -= rho * Ys[a] * Ds[k] * totMass_i * sigma_i / (dij * totMass * rho_i);
+        if (a == k) {
+          DJ(dJdr_j, a, k + 1) -= rho * Ds[a] * totMass_j * sigma_j / (dij * totMass * rho_j);
+          DJ(dJdr_i, a, k + 1) += rho * Ds[a] * totMass_i * sigma_i / (dij * totMass * rho_i);
+        }
+      }
+    for (int a = 0; a < ns; ++a)
+      for (int b = 0; b < ns; ++b) {
+        DJ(dJdr_j, a, a + 1) += 0.5 * rho * m.mm[b] * Ds[b] * Gxn[b] / (totMass * rho_j);
+        DJ(dJdr_i, a, a + 1) += 0.5 * rho * m.mm[b] * Ds[b] * Gxn[b] / (totMass * rho_i);
+      }
+    dVdUi[RHO_S * nVar + RHO_S] = 1.0;
+    dVdUj[RHO_S * nVar + RHO_S] = 1.0;
+    for (int s = 0; s < ns; ++s) {
+      dVdUi[(RHOS_S + s) * nVar + RHOS_S + s] = 1.0;
+      dVdUj[(RHOS_S + s) * nVar + RHOS_S + s] = 1.0;
+    }
+    for (int d = 0; d < nDim; ++d) {
+      dVdUi[(RHOVX_S + d) * nVar + RHO_S] = -Vi[VX_P + d] / Vi[RHO_P];
+      dVdUi[(RHOVX_S + d) * nVar + RHOVX_S + d] = 1.0 / Vi[RHO_P];
+      dVdUj[(RHOVX_S + d) * nVar + RHO_S] = -Vj[VX_P + d] / Vj[RHO_P];
+      dVdUj[(RHOVX_S + d) * nVar + RHOVX_S + d] = 1.0 / Vj[RHO_P];
+    }
+    for (int v = 0; v < nVar; ++v) {
+      dVdUi[RHOE_S * nVar + v] = Si[v];
+      dVdUj[RHOE_S * nVar + v] = Sj[v];
+    }
+    const double mu = Mean_mu, ktr = Mean_k;
+    if (nDim == 2) {
+      const double thetax = theta + UN[0] * UN[0] / 3.0, thetay = theta + UN[1] * UN[1] / 3.0;
+      const double etaz = UN[0] * UN[1] / 3.0;
+      const double pix = Vm[VX_P] * thetax + Vm[VX_P + 1] * etaz;
+      const double piy = Vm[VX_P] * etaz + Vm[VX_P + 1] * thetay;
+      FJ(RHOVX_S, RHOVX_S) = mu * thetax / dij * dS;
+      FJ(RHOVX_S, RHOVX_S + 1) = mu * etaz / dij * dS;
+      FJ(RHOVX_S + 1, RHOVX_S) = mu * etaz / dij * dS;
+      FJ(RHOVX_S + 1, RHOVX_S + 1) = mu * thetay / dij * dS;
+      FJ(RHOE_S, RHOVX_S) = pix * mu / dij * dS;
+      FJ(RHOE_S, RHOVX_S + 1) = piy * mu / dij * dS;
+      FJ(RHOE_S, RHOE_S) = ktr * theta / dij * dS;
+    } else {
+      const double thetax = theta + UN[0] * UN[0] / 3.0, thetay = theta + UN[1] * UN[1] / 3.0,
+                   thetaz = theta + UN[2] * UN[2] / 3.0;
+      const double etax = UN[1] * UN[2] / 3.0, etay = UN[0] * UN[2] / 3.0, etaz = UN[0] * UN[1] / 3.0;
+      const double pix = Vm[VX_P] * thetax + Vm[VX_P + 1] * etaz + Vm[VX_P + 2] * etay;
+      const double piy = Vm[VX_P] * etaz + Vm[VX_P + 1] * thetay + Vm[VX_P + 2] * etax;
+      const double piz = Vm[VX_P] * etay + Vm[VX_P + 1] * etax + Vm[VX_P + 2] * thetaz;
+      FJ(RHOVX_S, RHOVX_S) = mu * thetax / dij * dS;
+      FJ(RHOVX_S, RHOVX_S + 1) = mu * etaz / dij * dS;
+      FJ(RHOVX_S, RHOVX_S + 2) = mu * etay / dij * dS;
+      FJ(RHOVX_S + 1, RHOVX_S) = mu * etaz / dij * dS;
+      FJ(RHOVX_S + 1, RHOVX_S + 1) = mu * thetay / dij * dS;
+      FJ(RHOVX_S + 1, RHOVX_S + 2) = mu * etax / dij * dS;
+      FJ(RHOVX_S + 2, RHOVX_S) = mu * etay / dij * dS;
+      FJ(RHOVX_S + 2, RHOVX_S + 1) = mu * etax / dij * dS;
+      FJ(RHOVX_S + 2, RHOVX_S + 2) = mu * thetaz / dij * dS;
+      FJ(RHOE_S, RHOVX_S) = pix * mu / dij * dS;
+      FJ(RHOE_S, RHOVX_S + 1) = piy * mu / dij * dS;
+      FJ(RHOE_S, RHOVX_S + 2) = piz * mu / dij * dS;
+      FJ(RHOE_S, RHOE_S) = ktr * theta / dij * dS;
+    }
+    for (int a = 0; a < nVar; ++a)
+      for (int b = 0; b < nVar; ++b) FI(a, b) = -FJ(a, b);
+    for (int s = 0; s < ns; ++s) {
+      FI(RHOE_S, RHOE_S) += -0.5 * Jd[s] * Cps[s];
+      FJ(RHOE_S, RHOE_S) += -0.5 * Jd[s] * Cps[s];
+    }
+    for (int a = 0; a < ns; ++a) {
+      FJ(RHOS_S + a, RHO_S) = -DJ(dJdr_j, a, 0) * dS;
+      FI(RHOS_S + a, RHO_S) = -DJ(dJdr_i, a, 0) * dS;
+      FJ(RHO_S, RHO_S) += FJ(RHOS_S + a, RHO_S);
+      FI(RHO_S, RHO_S) += FI(RHOS_S + a, RHO_S);
+      FJ(RHOE_S, RHO_S) += -DJ(dJdr_j, a, 0) * hs[a] * dS;
+      FI(RHOE_S, RHO_S) += -DJ(dJdr_i, a, 0) * hs[a] * dS;
+      for (int b = 0; b < ns; ++b) {
+        FJ(RHOS_S + a, RHOS_S + b) = -DJ(dJdr_j, a, b + 1) * dS;
+        FI(RHOS_S + a, RHOS_S + b) = -DJ(dJdr_i, a, b + 1) * dS;
+        FJ(RHO_S, RHOS_S + b) += -DJ(dJdr_j, a, b + 1) * dS;
+        FI(RHO_S, RHOS_S + b) += -DJ(dJdr_i, a, b + 1) * dS;
+        FJ(RHOE_S, RHOS_S + a) += -DJ(dJdr_j, b, a + 1) * hs[b] * dS;
+        FI(RHOE_S, RHOS_S + a) += -DJ(dJdr_i, b, a + 1) * hs[b] * dS;
+      }
+    }
+  }
+  // SST_Reactive_JacobianClosure
+  if (P.rans) {
+    double theta = 0.0;
+    for (int d = 0; d < nDim; ++d) theta += UN[d] * UN[d];
+    const double sq = std::sqrt(dist2);
+    const double rho_i = Vi[RHO_P], rho_j = Vj[RHO_P];
+    const double mut = Mean_mut, PrT = P.Prandtl_Turb, LeT = P.Lewis_Turb;
+    if (nDim == 2) {
+      const double thetax = theta + UN[0] * UN[0] / 3.0, thetay = theta + UN[1] * UN[1] / 3.0;
+      const double etaz = UN[0] * UN[1] / 3.0;
+      const double pix = Vm[VX_P] * thetax + Vm[VX_P + 1] * etaz;
+      const double piy = Vm[VX_P] * etaz + Vm[VX_P + 1] * thetay;
+      FJ(RHOVX_S, RHOVX_S) += mut * thetax / sq * Area;
+      FJ(RHOVX_S, RHOVX_S + 1) += mut * etaz / sq * Area;
+      FI(RHOVX_S, RHOVX_S) -= mut * thetax / sq * Area;
+      FI(RHOVX_S, RHOVX_S + 1) -= mut * etaz / sq * Area;
+      FJ(RHOVX_S + 1, RHOVX_S) += mut * etaz / sq * Area;
+      FJ(RHOVX_S + 1, RHOVX_S + 1) += mut * thetay / sq * Area;
+      FI(RHOVX_S + 1, RHOVX_S) -= mut * etaz / sq * Area;
+      FI(RHOVX_S + 1, RHOVX_S + 1) -= mut * thetay / sq * Area;
+      FJ(RHOE_S, RHOVX_S) += pix * mut / sq * Area;
+      FJ(RHOE_S, RHOVX_S + 1) += piy * mut / sq * Area;
+      FI(RHOE_S, RHOVX_S) -= pix * mut / sq * Area;
+      FI(RHOE_S, RHOVX_S + 1) -= piy * mut / sq * Area;
+      for (int s = 0; s < ns; ++s) {
+        FJ(RHOE_S, RHOE_S) += mut / PrT * Cps[s] * Ys[s] * theta / sq * Area;
+        FI(RHOE_S, RHOE_S) -= mut / PrT * Cps[s] * Ys[s] * theta / sq * Area;
+        FJ(RHOE_S, RHOS_S + s) += mut / (PrT * LeT) * hs[s] * Ys[s] / rho_j * theta / sq * Area;
+        FI(RHOE_S, RHOS_S + s) -= mut / (PrT * LeT) * hs[s] * Ys[s] / rho_i * theta / sq * Area;
+      }
+    } else {
+      const double thetax = theta + UN[0] * UN[0] / 3.0, thetay = theta + UN[1] * UN[1] / 3.0,
+                   thetaz = theta + UN[2] * UN[2] / 3.0;
+      const double etax = UN[1] * UN[2] / 3.0, etay = UN[0] * UN[2] / 3.0, etaz = UN[0] * UN[1] / 3.0;
+      const double pix = Vm[VX_P] * thetax + Vm[VX_P + 1] * etaz + Vm[VX_P + 2] * etay;
+      const double piy = Vm[VX_P] * etaz + Vm[VX_P + 1] * thetay + Vm[VX_P + 2] * etax;
+      const double piz = Vm[VX_P] * etay + Vm[VX_P + 1] * etax + Vm[VX_P + 2] * thetaz;
+      const double th[3][3] = {{thetax, etaz, etay}, {etaz, thetay, etax}, {etay, etax, thetaz}};
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+          FJ(RHOVX_S + a, RHOVX_S + b) += mut * th[a][b] / sq * Area;
+          FI(RHOVX_S + a, RHOVX_S + b) -= mut * th[a][b] / sq * Area;
+        }
+      const double pi[3] = {pix, piy, piz};
+      for (int b = 0; b < 3; ++b) FJ(RHOE_S, RHOVX_S + b) += pi[b] * mut / sq * Area;
+      for (int b = 0; b < 3; ++b) FI(RHOE_S, RHOVX_S + b) -= pi[b] * mut / sq * Area;
+      for (int s = 0; s < ns; ++s) {
+        FJ(RHOE_S, RHOE_S) += mut / PrT * Cps[s] * Ys[s] * theta / sq * Area;
+        FI(RHOE_S, RHOE_S) -= mut / PrT * Cps[s] * Ys[s] * theta / sq * Area;
+        for (int b = 0; b < ns; ++b) {
+          FJ(RHOS_S + s, RHOS_S + b) += (s == b) * mut * Ys[s] / (PrT * LeT) / rho_j * theta / sq * Area;
+          FI(RHOS_S + s, RHOS_S + b) -= (s == b) * mut * Ys[s] / (PrT * LeT) / rho_i * theta / sq * Area;
+        }
+        FJ(RHOE_S, RHOS_S + s) += mut / (PrT * LeT) * hs[s] / rho_j * theta / sq * Area;
+        FI(RHOE_S, RHOS_S + s) -= mut / (PrT * LeT) * hs[s] / rho_i * theta / sq * Area;
+      }
+    }
+    // Quirk (numerics_direct_reactive.cpp:1083-1084): inner_product over
+    // Mean_Mass_Grads.row(s).data() .. +nDim walks the COLUMN-MAJOR storage, i.e. elements
+    // s, s+1, .. of the flattened [col][row] array, not the row. Reproduced, not fixed.
+    for (int s = 0; s < ns; ++s) {
+      double aux = 0.0;
+      for (int d = 0; d < nDim; ++d) {
+        const int flat = s + d;
+        aux += MassGrads[flat % ns][flat / ns] * UN[d];
+      }
+      FJ(RHOE_S, RHOE_S) += mut / (PrT * LeT) * Cps[s] * Ys[s] * aux * Area;
+      FI(RHOE_S, RHOE_S) += mut / (PrT * LeT) * Cps[s] * Ys[s] * aux * Area;
+    }
+  }
+  for (int d = 0; d < nDim; ++d) {
+    FI(RHOE_S, RHOVX_S + d) += 0.5 * PF[RHOVX_S + d];
+    FJ(RHOE_S, RHOVX_S + d) += 0.5 * PF[RHOVX_S + d];
+  }
+  for (int a = 0; a < nVar; ++a)
+    for (int b = 0; b < nVar; ++b) {
+      double si = 0.0, sj = 0.0;
+      for (int k = 0; k < nVar; ++k) {
+        si += dFdVi[a * nVar + k] * dVdUi[k * nVar + b];
+        sj += dFdVj[a * nVar + k] * dVdUj[k * nVar + b];
+      }
+      Ji[a * nVar + b] = si;
+      Jj[a * nVar + b] = sj;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// a12: CReactiveNSSolver::SetPrimitive_Gradient_LS (solver_direct_reactive.cpp:4887-5050)
+// ------------------------------------------------------------------------------------------------
+void grad_lsq_node(const Mech& m, int nDim, int i, const double* coord, const double* V, const int64_t* nptr,
+                   const int64_t* nbr, double* out) {
+  const int ns = m.ns, nPV = ns + nDim + 5, nG = ns + nDim + 2;
+  const int P_P = nDim + 1, RHOS_P = nDim + 5, P_G = nDim + 1, RHOS_G = nDim + 2;
+  auto prim = [&](int p, double* pv) {
+    const double* v = V + (size_t)p * nPV;
+    pv[0] = v[0];
+    pv[P_G] = v[P_P];
+    for (int d = 0; d < nDim; ++d) pv[1 + d] = v[1 + d];
+    double yc[32];
+    molar_from_mass(m, v + RHOS_P, yc, pv + RHOS_G);
+  };
+  double pi[32], pj[32], C[32][3];
+  prim(i, pi);
+  for (int v = 0; v < nG; ++v)
+    for (int d = 0; d < nDim; ++d) C[v][d] = 0.0;
+  double r11 = 0, r12 = 0, r13 = 0, r22 = 0, r23 = 0, r23_a = 0, r23_b = 0, r33 = 0;
+  const double* ci = coord + (size_t)i * nDim;
+  for (int64_t k = nptr[i]; k < nptr[i + 1]; ++k) {
+    const int64_t j = nbr[k];
+    const double* cj = coord + (size_t)j * nDim;
+    prim((int)j, pj);
+    double cij[3];
+    for (int d = 0; d < nDim; ++d) cij[d] = cj[d] - ci[d];
+    double w = 0.0;
+    for (int d = 0; d < nDim; ++d) w += cij[d] * cij[d];
+    if (w > EPS) {
+      r11 += cij[0] * cij[0] / w;
+      r12 += cij[0] * cij[1] / w;
+      r22 += cij[1] * cij[1] / w;
+      if (nDim == 3) {
+        r13 += cij[0] * cij[2] / w;
+        r23_a += cij[1] * cij[2] / w;
+        r23_b += cij[0] * cij[2] / w;
+        r33 += cij[2] * cij[2] / w;
+      }
+      for (int v = 0; v < nG; ++v)
+        for (int d = 0; d < nDim; ++d) C[v][d] += cij[d] * (pj[v] - pi[v]) / w;
+    }
+  }
+  r11 = (r11 > EPS) ? std::sqrt(r11) : 0.0;
+  r12 = (std::abs(r11) > EPS) ? r12 / r11 : 0.0;
+  r22 = (r22 - r12 * r12 > EPS) ? std::sqrt(r22 - r12 * r12) : 0.0;
+  if (nDim == 3) {
+    r13 = (std::abs(r11) > EPS) ? r13 / r11 : 0.0;
+    r23 = (std::abs(r22) > EPS && std::abs(r11 * r22) > EPS) ? r23_a / r22 - r23_b * r12 / (r11 * r22) : 0.0;
+    r33 = (r33 - r23 * r23 - r13 * r13 > EPS) ? std::sqrt(r33 - r23 * r23 - r13 * r13) : 0.0;
+  }
+  double detR2 = (nDim == 2) ? (r11 * r22) * (r11 * r22) : (r11 * r22 * r33) * (r11 * r22 * r33);
+  bool singular = false;
+  if (std::abs(detR2) < EPS) {
+    detR2 = 1.0;
+    singular = true;
+  }
+  double S[3][3] = {{0}};
+  if (!singular) {
+    if (nDim == 2) {
+      S[0][0] = (r12 * r12 + r22 * r22) / detR2;
+      S[0][1] = -r11 * r12 / detR2;
+      S[1][0] = S[0][1];
+      S[1][1] = r11 * r11 / detR2;
+    } else {
+      const double z11 = r22 * r33, z12 = -r12 * r33, z13 = r12 * r23 - r13 * r22;
+      const double z22 = r11 * r33, z23 = -r11 * r23, z33 = r11 * r22;
+      S[0][0] = (z11 * z11 + z12 * z12 + z13 * z13) / detR2;
+      S[0][1] = (z12 * z22 + z13 * z23) / detR2;
+      S[0][2] = (z13 * z33) / detR2;
+      S[1][0] = S[0][1];
+      S[1][1] = (z22 * z22 + z23 * z23) / detR2;
+      S[1][2] = (z23 * z33) / detR2;
+      S[2][0] = S[0][2];
+      S[2][1] = S[1][2];
+      S[2][2] = (z33 * z33) / detR2;
+    }
+  }
+  for (int v = 0; v < nG; ++v)
+    for (int d = 0; d < nDim; ++d) {
+      double r = 0.0;
+      for (int e = 0; e < nDim; ++e) r += C[v][e] * S[d][e];
+      out[v * nDim + d] = r;
+    }
+}
+
+std::vector<Mech*> g_mechs;
+
+}  // namespace
+
+// =================================================================================================
+// C ABI for the Python tests (ctypes).
+// =================================================================================================
+extern "C" {
+
+void* orc_mech_create(int ns, int nr, int ntab, const double* mm, const double* dv, const double* sr,
+                      const double* sp, const double* er, const double* ep, const double* A, const double* beta,
+                      const double* Ta, const double* Ab, const double* betab, const double* Tab,
+                      const int64_t* rev, const int64_t* hasb, const double* tx, const double* ty,
+                      const double* ty2) {
+  Mech* m = new Mech();
+  m->ns = ns;
+  m->nr = nr;
+  m->ntab = ntab;
+  m->mm.assign(mm, mm + ns);
+  m->dv.assign(dv, dv + ns);
+  m->ri.resize(ns);
+  for (int s = 0; s < ns; ++s) m->ri[s] = R_UNGAS / mm[s];
+  m->mtot = 0.0;
+  for (int s = 0; s < ns; ++s) m->mtot += mm[s];
+  m->sr.assign(sr, sr + ns * nr);
+  m->sp.assign(sp, sp + ns * nr);
+  m->er.assign(er, er + ns * nr);
+  m->ep.assign(ep, ep + ns * nr);
+  m->A.assign(A, A + nr);
+  m->beta.assign(beta, beta + nr);
+  m->Ta.assign(Ta, Ta + nr);
+  m->Ab.assign(Ab, Ab + nr);
+  m->betab.assign(betab, betab + nr);
+  m->Tab.assign(Tab, Tab + nr);
+  m->rev.assign(rev, rev + nr);
+  m->hasb.assign(hasb, hasb + nr);
+  m->tx.assign(tx, tx + 5 * ns * ntab);
+  m->ty.assign(ty, ty + 5 * ns * ntab);
+  m->ty2.assign(ty2, ty2 + 5 * ns * ntab);
+  m->neg_reac.resize(nr);
+  m->neg_prod.resize(nr);
+  for (int r = 0; r < nr; ++r)
+    for (int s = 0; s < ns; ++s) {
+      if (m->er[r * ns + s] < 0.0) m->neg_reac[r].push_back(s);
+      if (m->ep[r * ns + s] < 0.0) m->neg_prod[r].push_back(s);
+    }
+  return m;
+}
+
+void orc_mech_destroy(void* h) { delete static_cast<Mech*>(h); }
+
+double orc_spline(void* h, int prop, int s, double T) { return spline(*static_cast<Mech*>(h), prop, s, T); }
+
+// a1 over E edges. Outputs: res[E][nVar], Ji/Jj[E][nVar][nVar] (implicit only).
+void orc_ausm_edges(int nDim, int ns, int64_t E, const int64_t* edges, const double* normal, const double* V,
+                    const double* dPdU, double mach_inf, int implicit, double* res, double* Ji, double* Jj) {
+  const int nVar = ns + nDim + 2, nPV = ns + nDim + 5;
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    ausm(nDim, ns, V + i * nPV, V + j * nPV, normal + e * nDim, implicit ? dPdU + i * nVar : nullptr,
+         implicit ? dPdU + j * nVar : nullptr, mach_inf, implicit != 0, res + e * nVar,
+         implicit ? Ji + e * nVar * nVar : nullptr, implicit ? Jj + e * nVar * nVar : nullptr);
+  }
+}
+
+// a9 over N cells. params = {C_mu, PaSR_lb, rho_ref, t_ref, T_ref}
+int orc_source_cells(void* h, int nDim, int64_t N, const double* V, const double* dTdU, const double* vol,
+                     const double* omega_turb, int rans, int implicit, const double* params, double* res, double* J) {
+  const Mech& m = *static_cast<Mech*>(h);
+  const int nVar = m.ns + nDim + 2, nPV = m.ns + nDim + 5;
+  try {
+    for (int64_t i = 0; i < N; ++i)
+      source(m, nDim, V + i * nPV, implicit ? dTdU + i * nVar : nullptr, vol[i], rans ? omega_turb[i] : 0.0,
+             rans != 0, implicit != 0, params[0], params[1], params[2], params[3], params[4], res + i * nVar,
+             implicit ? J + i * nVar * nVar : nullptr);
+  } catch (const std::exception&) {
+    return 1;
+  }
+  return 0;
+}
+
+// a3-a6 over E edges. vparams = {T_ref, E_ref, R_ref, Prandtl_Turb, Lewis_Turb}
+int orc_visc_edges(void* h, int nDim, int64_t E, const int64_t* edges, const double* normal, const double* coord,
+                   const double* V, const double* grad, const double* mu, const double* kappa, const double* Dij,
+                   const double* dTdU, const double* tke, const double* mut, const double* sigma_k,
+                   const double* gradk, int rans, int implicit, const double* vparams, double* res, double* Ji,
+                   double* Jj) {
+  const Mech& m = *static_cast<Mech*>(h);
+  const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5, nG = ns + nDim + 2;
+  ViscParams P{vparams[0], vparams[1], vparams[2], vparams[3], vparams[4], rans, implicit};
+  try {
+    for (int64_t e = 0; e < E; ++e) {
+      const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+      visc_flux(m, nDim, P, V + i * nPV, V + j * nPV, grad + i * nG * nDim, grad + j * nG * nDim, mu[i], mu[j],
+                kappa[i], kappa[j], Dij + i * ns * ns, Dij + j * ns * ns, coord + i * nDim, coord + j * nDim,
+                normal + e * nDim, implicit ? dTdU + i * nVar : nullptr, implicit ? dTdU + j * nVar : nullptr,
+                rans ? tke[i] : 0.0, rans ? tke[j] : 0.0, rans ? mut[i] : 0.0, rans ? mut[j] : 0.0,
+                rans ? sigma_k[i] : 1.0, rans ? gradk + i * nDim : nullptr, rans ? gradk + j * nDim : nullptr,
+                res + e * nVar, implicit ? Ji + e * nVar * nVar : nullptr, implicit ? Jj + e * nVar * nVar : nullptr);
+    }
+  } catch (const std::exception&) {
+    return 1;
+  }
+  return 0;
+}
+
+// a12 for the listed points (pts), all others untouched.
+void orc_grad_lsq(void* h, int nDim, int64_t npts, const int64_t* pts, const double* coord, const double* V,
+                  const int64_t* nptr, const int64_t* nbr, double* grad) {
+  const Mech& m = *static_cast<Mech*>(h);
+  const int nG = m.ns + nDim + 2;
+  for (int64_t k = 0; k < npts; ++k) {
+    const int64_t i = pts[k];
+    grad_lsq_node(m, nDim, (int)i, coord, V, nptr, nbr, grad + i * nG * nDim);
+  }
+}
+
+// a13: Venkatakrishnan limiter (solver_direct_reactive.cpp:1328-1523), edge-loop form.
+void orc_limiter_venkat(int nDim, int ns, int64_t N, int64_t E, const int64_t* edges, const double* coord,
+                        const double* V, const double* grad, double ref_len, double lim_coeff, double* lim) {
+  const int nL = nDim + 2, nPV = ns + nDim + 5, nG = ns + nDim + 2;
+  std::vector<double> mx(N * nL, -EPS), mn(N * nL, EPS);
+  for (int64_t q = 0; q < N * nL; ++q) lim[q] = 2.0;
+  auto pl = [&](int64_t p, int v) {
+    const double* pv = V + p * nPV;
+    if (v == 0) return pv[0];
+    if (v == nL - 1) return pv[nDim + 1];
+    return pv[v];
+  };
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    for (int v = 0; v < nL; ++v) {
+      const double du = pl(j, v) - pl(i, v);
+      mn[i * nL + v] = std::min(mn[i * nL + v], du);
+      mx[i * nL + v] = std::max(mx[i * nL + v], du);
+      mn[j * nL + v] = std::min(mn[j * nL + v], -du);
+      mx[j * nL + v] = std::max(mx[j * nL + v], -du);
+    }
+  }
+  // gradient rows for the limited variables: T, u, v(, w), P are rows 0..nDim+1 of G
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    const double* Gi = grad + i * nG * nDim;
+    const double* Gj = grad + j * nG * nDim;
+    const double* ci = coord + i * nDim;
+    const double* cj = coord + j * nDim;
+    for (int v = 0; v < nL; ++v) {
+      const double eps1 = lim_coeff * ref_len;
+      const double eps2 = eps1 * eps1 * eps1;
+      double dm = 0.0;
+      for (int d = 0; d < nDim; ++d) dm += 0.5 * (cj[d] - ci[d]) * Gi[v * nDim + d];
+      double dp = (dm > 0.0) ? mx[i * nL + v] : mn[i * nL + v];
+      double lv = (dp * dp + 2.0 * dp * dm + eps2) / (dp * dp + dp * dm + 2.0 * dm * dm + eps2);
+      if (lv < lim[i * nL + v]) lim[i * nL + v] = lv;
+      dm = 0.0;
+      for (int d = 0; d < nDim; ++d) dm += 0.5 * (ci[d] - cj[d]) * Gj[v * nDim + d];
+      dp = (dm > 0.0) ? mx[j * nL + v] : mn[j * nL + v];
+      lv = (dp * dp + 2.0 * dp * dm + eps2) / (dp * dp + dp * dm + 2.0 * dm * dm + eps2);
+      if (lv < lim[j * nL + v]) lim[j * nL + v] = lv;
+    }
+  }
+}
+
+// a18: CReactiveNSSolver::SetTime_Step, RANS branch (solver_direct_reactive.cpp:5057-5298).
+// bverts[nb][2] = (marker, node) in marker/vertex order, bnormal[nb][nDim]. params = {CFL, Max_DeltaTime,
+// Prandtl_Lam, Prandtl_Turb}. Outputs dt, lambda_inv, lambda_visc per node.
+void orc_time_step(int nDim, int ns, int64_t N, int64_t E, const int64_t* edges, const double* normal, int64_t NB,
+                   const int64_t* bverts, const double* bnormal, const double* V, const double* dPdU,
+                   const double* mu, const double* eddy, const double* vol, const int64_t* nptr,
+                   const double* params, double* dt, double* li, double* lv) {
+  const int nPV = ns + nDim + 5, nVar = ns + nDim + 2;
+  const int RHO_P = nDim + 2, A_P = nDim + 4, RHOE_S = nDim + 1;
+  const double CFL = params[0], MaxDt = params[1], Pr_l = params[2], Pr_t = params[3];
+  const double K_v = 0.25;
+  for (int64_t i = 0; i < N; ++i) li[i] = lv[i] = 0.0;
+  auto projvel = [&](int64_t p, const double* n) {
+    double s = 0.0;
+    for (int d = 0; d < nDim; ++d) s += V[p * nPV + 1 + d] * n[d];
+    return s;
+  };
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    const double* n = normal + e * nDim;
+    double Area = 0.0;
+    for (int d = 0; d < nDim; ++d) Area += n[d] * n[d];
+    Area = std::sqrt(Area);
+    const double pv = 0.5 * (projvel(i, n) + projvel(j, n));
+    const double a = 0.5 * (V[i * nPV + A_P] + V[j * nPV + A_P]);
+    const double rho = 0.5 * (V[i * nPV + RHO_P] + V[j * nPV + RHO_P]);
+    const double m = 0.5 * (mu[i] + mu[j]);
+    double lam = (std::abs(pv) + a) * Area;
+    li[i] += lam;
+    li[j] += lam;
+    const double mt = 0.5 * (eddy[i] + eddy[j]);
+    const double gam = dPdU[i * nVar + RHOE_S] + 1;
+    const double l1 = 4.0 / 3.0 * (m + mt);
+    const double l2 = (1.0 + (Pr_l / Pr_t) * (mt / m)) * (gam * m / Pr_l);
+    lam = (l1 + l2) * Area * Area / rho;
+    lv[i] += lam;
+    lv[j] += lam;
+  }
+  for (int64_t b = 0; b < NB; ++b) {
+    const int64_t i = bverts[2 * b + 1];
+    const double* n = bnormal + b * nDim;
+    double Area = 0.0;
+    for (int d = 0; d < nDim; ++d) Area += n[d] * n[d];
+    Area = std::sqrt(Area);
+    const double pv = projvel(i, n);
+    const double a = V[i * nPV + A_P];
+    const double rho = V[i * nPV + RHO_P];
+    const double m = mu[i];
+    li[i] += (std::abs(pv) + a) * Area;
+    const double mt = eddy[i];
+    const double gam = dPdU[i * nVar + RHOE_S] + 1;
+    const double l1 = (4.0 / 3.0) * (m + mt);
+    const double l2 = (1.0 + (Pr_l / Pr_t) * (mt / m)) * (gam * m / Pr_l);
+    lv[i] += (l1 + l2) * Area * Area / rho;
+  }
+  double minDt = 1.0e6;
+  for (int64_t i = 0; i < N; ++i) {
+    if (vol[i] > EPS) {
+      double d = CFL * vol[i] / li[i];
+      const double dv = CFL * K_v * vol[i] * vol[i] / lv[i];
+      d = std::min(d, dv);
+      minDt = std::min(minDt, d);
+      if (d > MaxDt) d = MaxDt;
+      dt[i] = d;
+    } else {
+      dt[i] = 0.0;
+    }
+  }
+  for (int64_t i = 0; i < N; ++i)
+    if (nptr[i + 1] - nptr[i] == 1) dt[i] = minDt;
+}
+
+// ---- a15-a17: block-sparse linear algebra (Common/src/matrix_structure.cpp, linear_solvers_structure.cpp)
+// BSR: row_ptr[N+1], col[nnzb] sorted, blocks[nnzb][nb][nb] row-major. All N rows are domain rows.
+
+// MatrixVectorProduct (:997-1030)
+void orc_bsr_spmv(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* x,
+                  double* y) {
+  for (int64_t q = 0; q < N * nb; ++q) y[q] = 0.0;
+  for (int64_t i = 0; i < N; ++i)
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+      const double* b = A + k * nb * nb;
+      const double* xv = x + col[k] * nb;
+      for (int a = 0; a < nb; ++a)
+        for (int c = 0; c < nb; ++c) y[i * nb + a] += b[a * nb + c] * xv[c];
+    }
+}
+
+static void gauss_elim(int nb, const double* Block, double* rhs) {  // Gauss_Elimination (:594-643)
+  double blk[32 * 32];
+  std::memcpy(blk, Block, sizeof(double) * nb * nb);
+  if (nb == 1) {
+    rhs[0] /= blk[0];
+    return;
+  }
+  for (int i = 1; i < nb; ++i)
+    for (int j = 0; j < i; ++j) {
+      const double w = blk[i * nb + j] / blk[j * nb + j];
+      for (int k = j; k < nb; ++k) blk[i * nb + k] -= w * blk[j * nb + k];
+      rhs[i] -= w * rhs[j];
+    }
+  rhs[nb - 1] = rhs[nb - 1] / blk[nb * nb - 1];
+  for (int i = nb - 2; i >= 0; --i) {
+    double aux = 0.0;
+    for (int j = i + 1; j < nb; ++j) aux += blk[i * nb + j] * rhs[j];
+    rhs[i] = (rhs[i] - aux) / blk[i * nb + i];
+  }
+}
+
+static int64_t find_diag(const int64_t* rp, const int64_t* col, int64_t i) {
+  for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+    if (col[k] == i) return k;
+  return -1;
+}
+
+// ComputeLU_SGSPreconditioner (:1673-1709)
+void orc_lusgs(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* b,
+               double* x) {
+  std::vector<double> aux(nb), prv(nb);
+  for (int64_t i = 0; i < N; ++i) {
+    for (int a = 0; a < nb; ++a) prv[a] = 0.0;
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+      if (col[k] < i) {
+        const double* blk = A + k * nb * nb;
+        for (int a = 0; a < nb; ++a) {
+          double pb = 0.0;
+          for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * x[col[k] * nb + c];
+          prv[a] += pb;
+        }
+      }
+    for (int a = 0; a < nb; ++a) aux[a] = b[i * nb + a] - prv[a];
+    gauss_elim(nb, A + find_diag(rp, col, i) * nb * nb, aux.data());
+    for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+  }
+  for (int64_t i = N - 1; i >= 0; --i) {
+    const double* dblk = A + find_diag(rp, col, i) * nb * nb;
+    for (int a = 0; a < nb; ++a) {
+      double pb = 0.0;
+      for (int c = 0; c < nb; ++c) pb += dblk[a * nb + c] * x[i * nb + c];
+      aux[a] = pb;  // DiagonalProduct: prod_row_vector = 0 + block*x
+    }
+    for (int a = 0; a < nb; ++a) prv[a] = 0.0;
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+      if (col[k] > i) {
+        const double* blk = A + k * nb * nb;
+        for (int a = 0; a < nb; ++a) {
+          double pb = 0.0;
+          for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * x[col[k] * nb + c];
+          prv[a] += pb;
+        }
+      }
+    for (int a = 0; a < nb; ++a) aux[a] -= prv[a];
+    gauss_elim(nb, dblk, aux.data());
+    for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+  }
+}
+
+static void inverse_diag(int nb, const double* D, double* inv) {  // InverseDiagonalBlock_ILUMatrix (:1180-1228)
+  double v[32];
+  for (int i = 0; i < nb; ++i) {
+    for (int j = 0; j < nb; ++j) v[j] = 0.0;
+    v[i] = 1.0;
+    gauss_elim(nb, D, v);
+    for (int j = 0; j < nb; ++j) inv[j * nb + i] = v[j];
+  }
+}
+static void mat_mat(int nb, const double* a, const double* b, double* c) {  // MatrixMatrixProduct
+  for (int i = 0; i < nb; ++i)
+    for (int j = 0; j < nb; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < nb; ++k) s += a[i * nb + k] * b[k * nb + j];
+      c[i * nb + j] = s;
+    }
+}
+static void mat_vec(int nb, const double* a, const double* x, double* y) {
+  for (int i = 0; i < nb; ++i) {
+    double s = 0.0;
+    for (int k = 0; k < nb; ++k) s += a[i * nb + k] * x[k];
+    y[i] = s;
+  }
+}
+
+// BuildILUPreconditioner (:1368-1451), including the left-multiply quirk at :1432-1436.
+void orc_ilu_build(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, double* F) {
+  const int64_t nnzb = rp[N];
+  std::memcpy(F, A, sizeof(double) * nnzb * nb * nb);
+  std::vector<double> inv(nb * nb), w(nb * nb), blk(nb * nb);
+  auto findb = [&](int64_t i, int64_t j) -> double* {
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+      if (col[k] == j) return F + k * nb * nb;
+    return nullptr;
+  };
+  for (int64_t i = 1; i < N; ++i)
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+      const int64_t j = col[k];
+      if (j < i) {
+        double* Bij = F + k * nb * nb;
+        inverse_diag(nb, findb(j, j), inv.data());
+        mat_mat(nb, Bij, inv.data(), w.data());
+        for (int64_t kk = rp[j]; kk < rp[j + 1]; ++kk) {
+          const int64_t kp = col[kk];
+          if (kp >= j) {
+            const double* Bjk = F + kk * nb * nb;
+            mat_mat(nb, Bjk, w.data(), blk.data());
+            double* Bik = findb(i, kp);
+            if (Bik)  // SubtractBlock_ILUMatrix on a missing block is a no-op of the pattern
+              for (int q = 0; q < nb * nb; ++q) Bik[q] -= blk[q];
+          }
+        }
+        std::memcpy(Bij, w.data(), sizeof(double) * nb * nb);
+      }
+    }
+}
+
+// ComputeILUPreconditioner (:1453-1515)
+void orc_ilu_apply(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* F, const double* b,
+                   double* x) {
+  std::vector<double> aux(nb), sum(nb), inv(nb * nb);
+  for (int64_t q = 0; q < N * nb; ++q) x[q] = b[q];
+  for (int64_t i = 1; i < N; ++i)
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+      const int64_t j = col[k];
+      if (j < i) {
+        mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
+        for (int a = 0; a < nb; ++a) x[i * nb + a] -= aux[a];
+      }
+    }
+  auto diag = [&](int64_t i) { return F + find_diag(rp, col, i) * nb * nb; };
+  inverse_diag(nb, diag(N - 1), inv.data());
+  mat_vec(nb, inv.data(), x + (N - 1) * nb, aux.data());
+  for (int a = 0; a < nb; ++a) x[(N - 1) * nb + a] = aux[a];
+  for (int64_t i = N - 2; i >= 0; --i) {
+    for (int a = 0; a < nb; ++a) sum[a] = 0.0;
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+      const int64_t j = col[k];
+      if (j >= i + 1) {
+        mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
+        for (int a = 0; a < nb; ++a) sum[a] += aux[a];
+      }
+    }
+    for (int a = 0; a < nb; ++a) x[i * nb + a] = x[i * nb + a] - sum[a];
+    inverse_diag(nb, diag(i), inv.data());
+    mat_vec(nb, inv.data(), x + i * nb, aux.data());
+    for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+  }
+}
+
+// FGMRES_LinSolver (linear_solvers_structure.cpp:309-463) + ModGramSchmidt (:87-186), Givens (:37-71),
+// SolveReduced (:73-85). prec: 0 = LU-SGS on A, 1 = ILU0 with factor F. x in/out (initial guess).
+// Returns iterations; *resid = final beta. Returns -1 on divergence (MGS exit, :108-150).
+int orc_fgmres(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F, int prec,
+               const double* b, double* x, double tol, int m, double* resid) {
+  const int64_t n = N * nb;
+  auto dotp = [&](const double* a, const double* c) {
+    double s = 0.0;
+    for (int64_t q = 0; q < n; ++q) s += a[q] * c[q];
+    return s;
+  };
+  auto norm = [&](const double* a) { return std::sqrt(dotp(a, a)); };
+  std::vector<std::vector<double>> w(m + 1, std::vector<double>(n)), z(m + 1, std::vector<double>(n));
+  std::vector<double> g(m + 1, 0.0), sn(m + 1, 0.0), cs(m + 1, 0.0), y(m, 0.0);
+  std::vector<std::vector<double>> H(m + 1, std::vector<double>(m, 0.0));
+  double norm0 = norm(b);
+  orc_bsr_spmv(N, nb, rp, col, A, x, w[0].data());
+  for (int64_t q = 0; q < n; ++q) w[0][q] -= b[q];
+  double beta = norm(w[0].data());
+  const double epsm = std::numeric_limits<double>::epsilon();
+  if ((beta < tol * norm0) || (beta < epsm)) {
+    *resid = beta;
+    return 0;
+  }
+  for (int64_t q = 0; q < n; ++q) w[0][q] /= -beta;
+  g[0] = beta;
+  norm0 = beta;
+  int i = 0;
+  for (i = 0; i < m; ++i) {
+    if (beta < tol * norm0) break;
+    if (prec == 0) orc_lusgs(N, nb, rp, col, A, w[i].data(), z[i].data());
+    else orc_ilu_apply(N, nb, rp, col, F, w[i].data(), z[i].data());
+    orc_bsr_spmv(N, nb, rp, col, A, z[i].data(), w[i + 1].data());
+    // ModGramSchmidt
+    const double reorth = 0.98;
+    double nrm = dotp(w[i + 1].data(), w[i + 1].data());
+    double thr = nrm * reorth;
+    if ((nrm <= 0.0) || (nrm != nrm)) return -1;
+    for (int k = 0; k < i + 1; ++k) {
+      double prod = dotp(w[i + 1].data(), w[k].data());
+      H[k][i] = prod;
+      for (int64_t q = 0; q < n; ++q) w[i + 1][q] += -prod * w[k][q];
+      if (prod * prod > thr) {
+        prod = dotp(w[i + 1].data(), w[k].data());
+        H[k][i] += prod;
+        for (int64_t q = 0; q < n; ++q) w[i + 1][q] += -prod * w[k][q];
+      }
+      nrm -= H[k][i] * H[k][i];
+      if (nrm < 0.0) nrm = 0.0;
+      thr = nrm * reorth;
+    }
+    nrm = norm(w[i + 1].data());
+    H[i + 1][i] = nrm;
+    for (int64_t q = 0; q < n; ++q) w[i + 1][q] /= nrm;
+    auto applyG = [](double s, double c, double& h1, double& h2) {
+      const double t = c * h1 + s * h2;
+      h2 = c * h2 - s * h1;
+      h1 = t;
+    };
+    for (int k = 0; k < i; ++k) applyG(sn[k], cs[k], H[k][i], H[k + 1][i]);
+    {  // GenerateGivens(H[i][i], H[i+1][i], sn[i], cs[i])
+      double& dx = H[i][i];
+      double& dy = H[i + 1][i];
+      double& s = sn[i];
+      double& c = cs[i];
+      auto sgn = [](double a, double bb) { return bb == 0.0 ? 0.0 : (bb < 0 ? -std::fabs(a) : std::fabs(a)); };
+      if ((dx == 0.0) && (dy == 0.0)) {
+        c = 1.0;
+        s = 0.0;
+      } else if (std::fabs(dy) > std::fabs(dx)) {
+        const double tmp = dx / dy;
+        dx = std::sqrt(1.0 + tmp * tmp);
+        s = sgn(1.0 / dx, dy);
+        c = tmp * s;
+      } else if (std::fabs(dy) <= std::fabs(dx)) {
+        const double tmp = dy / dx;
+        dy = std::sqrt(1.0 + tmp * tmp);
+        c = sgn(1.0 / dy, dx);
+        s = tmp * c;
+      } else {
+        dx = 0.0;
+        dy = 0.0;
+        c = 1.0;
+        s = 0.0;
+      }
+      dx = std::fabs(dx * dy);
+      dy = 0.0;
+    }
+    applyG(sn[i], cs[i], g[i], g[i + 1]);
+    beta = std::fabs(g[i + 1]);
+  }
+  // SolveReduced
+  for (int k = 0; k < i; ++k) y[k] = g[k];
+  for (int k = i - 1; k >= 0; --k) {
+    y[k] /= H[k][k];
+    for (int j = k - 1; j >= 0; --j) y[j] -= H[j][k] * y[k];
+  }
+  for (int k = 0; k < i; ++k)
+    for (int64_t q = 0; q < n; ++q) x[q] += y[k] * z[k][q];
+  *resid = beta;
+  return i;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""Pin the CPU oracle (oracle/rx_oracle.cpp) against golden vectors produced by the compiled
+reference (oracle/make_golden.py). CPU only.
+
+Fixtures:
+  mini9.npz  21x11 synthetic jet, 9 species, SST, implicit: every operator + whole loops + BSR.
+  jet9w.npz  window of the reference's own 9000-point jet mesh around the flame, PaSR state.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.parity import assert_close
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+CASES = ["mini9", "jet9w"]
+
+
+def load(case):
+    g = dict(np.load(os.path.join(GOLD, case + ".npz")))
+    dims = [int(x) for x in g["dims"]]
+    return g, dims
+
+
+@pytest.fixture(scope="module", params=CASES)
+def case(request):
+    g, dims = load(request.param)
+    return request.param, g, dims, O.Mechanism(g)
+
+
+def test_mechanism_tables(case):
+    name, g, dims, mech = case
+    assert mech.ns == 9 and mech.nr == 2
+    # CGS -> SI conversion of the first reaction (reacting_model_library.cpp:1123-1132)
+    assert np.isclose(g["mech_A"][0], 8.80e11 * 1e-6)
+
+
+def test_ausm_edges(case):
+    name, g, (nDim, nVar, nPV, nG, ns, imp, rans), mech = case
+    r, Ji, Jj = O.ausm_edges(nDim, ns, g["edges"], g["edge_normal"], g["V"], g["dPdU"], g["mach_inf"][0], True)
+    js = g["jac_edge_sample"]
+    assert_close(r, g["conv_res"], what="AUSM residual")
+    assert_close(Ji[js], g["conv_jac_i"], floor=1e-9, what="AUSM Jac_i")
+    assert_close(Jj[js], g["conv_jac_j"], floor=1e-9, what="AUSM Jac_j")
+
+
+def test_source_cells(case):
+    name, g, (nDim, nVar, nPV, nG, ns, imp, rans), mech = case
+    r, J = O.source_cells(mech, nDim, g["V"], g["dTdU"], g["volume"], g["turb_omega"], True, True, g["src_params"])
+    sj = g["src_jac_sample"] if "src_jac_sample" in g else np.arange(len(g["V"]))
+    assert_close(r, g["src_res"], what="PaSR source")
+    assert_close(J[sj], g["src_jac"], floor=1e-9, what="PaSR source Jacobian")
+
+
+def test_grad_lsq(case):
+    name, g, (nDim, nVar, nPV, nG, ns, imp, rans), mech = case
+    pts = np.nonzero(g["interior"])[0] if "interior" in g else np.arange(len(g["V"]))
+    G = O.grad_lsq(mech, nDim, pts, g["coord"], g["V"], g["nbr_ptr"], g["nbr"])
+    assert_close(G[pts], g["grad_lsq_out"][pts], what="LSQ gradient")
+
+
+def test_viscous_edges(case):
+    name, g, (nDim, nVar, nPV, nG, ns, imp, rans), mech = case
+    vp = [1.0, 1.0, 1.0, g["visc_params"][1], g["visc_params"][2]]
+    r, Ji, Jj = O.visc_edges(mech, nDim, g["edges"], g["edge_normal"], g["coord"], g["V"], g["grad_prim"], g["mu"],
+                             g["kappa"], g["Dij"], g["dTdU"], g["turb_k"], g["mu_t"], g["sigma_k"], g["grad_k"], True,
+                             True, vp)
+    ref = g["visc_res"]
+    # momentum / energy rows: per-element relative
+    assert_close(r[:, 1:4], ref[:, 1:4], what="viscous momentum/energy")
+    # density + species rows: relative to each edge's species-flux block (the density row is
+    # -sum(J_s), zero up to the 1e-11 Stefan-Maxwell tolerance)
+    blk = np.abs(ref[:, 4:]).max(axis=1, keepdims=True)
+    blk = np.where(blk == 0.0, 1.0, blk)
+    err = np.abs(np.c_[r[:, :1], r[:, 4:]] - np.c_[ref[:, :1], ref[:, 4:]]) / blk
+    assert err.max() <= 1e-10, f"viscous species block err {err.max():.3e}"
+    js = g["jac_edge_sample"]
+    assert_close(Ji[js], g["visc_jac_i"], floor=1e-9, what="viscous Jac_i")
+    assert_close(Jj[js], g["visc_jac_j"], floor=1e-9, what="viscous Jac_j")
+
+
+def test_limiter_venkat():
+    g, (nDim, nVar, nPV, nG, ns, imp, rans) = load("jet9w")
+    lp = g["limiter_params"]
+    L = O.limiter_venkat(nDim, ns, g["edges"], g["coord"], g["V"], g["grad_prim"], lp[0], lp[1])
+    it = g["interior"]
+    assert_close(L[it], g["limiter_out"][it], what="Venkatakrishnan limiter")
+
+
+def test_loops_and_time_step():
+    g, (nDim, nVar, nPV, nG, ns, imp, rans) = load("mini9")
+    N = len(g["V"])
+    R = np.zeros((N, nVar))
+    for e, (i, j) in enumerate(g["edges"]):
+        R[i] += g["conv_res"][e]
+        R[j] -= g["conv_res"][e]
+    assert_close(R, g["loop_upwind_res"], what="Upwind_Residual loop")
+    for e, (i, j) in enumerate(g["edges"]):
+        R[i] -= g["visc_res"][e]
+        R[j] += g["visc_res"][e]
+    assert_close(R, g["loop_upwind_visc_res"], what="Viscous_Residual loop")
+    R += g["src_res"]
+    assert_close(R, g["loop_total_res"], what="Source_Residual loop")
+    dt, li, lv = O.time_step(nDim, ns, g["edges"], g["edge_normal"], g["bvertex"], g["bvertex_normal"], g["V"],
+                             g["dPdU"], g["mu"], g["eddy_visc_flow"], g["volume"], g["nbr_ptr"], g["dt_params"])
+    assert_close(dt, g["dt"], what="local time step")
+    assert_close(li, g["lambda_inv"], what="inviscid spectral radius")
+    assert_close(lv, g["lambda_visc"], what="viscous spectral radius")
+
+
+def test_block_sparse_linear_algebra():
+    g, _ = load("mini9")
+    rp, col, A, b = g["bsr_row_ptr"], g["bsr_col"], g["bsr_system"], g["sys_rhs"]
+    assert_close(O.bsr_spmv(rp, col, A, b), g["spmv_rhs"], what="BSR SpMV")
+    assert_close(O.lusgs(rp, col, A, b), g["lusgs_rhs"], what="LU-SGS apply")
+    F = O.ilu_build(rp, col, A)
+    assert_close(F, g["ilu_factor"], floor=1e-9, what="ILU(0) factor")
+    assert_close(O.ilu_apply(rp, col, F, b), g["ilu_rhs"], what="ILU(0) apply")
+    x, it, res = O.fgmres(rp, col, A, b, "lusgs", tol=g["fgmres_lusgs_info"][2], m=int(g["fgmres_lusgs_info"][3]))
+    assert it == int(g["fgmres_lusgs_info"][0])
+    assert_close(x, g["fgmres_lusgs_x"], what="FGMRES(LU-SGS)")
+    x, it, res = O.fgmres(rp, col, A, b, "ilu", F=F, tol=g["fgmres_ilu_info"][2], m=int(g["fgmres_ilu_info"][3]))
+    assert it == int(g["fgmres_ilu_info"][0])
+    assert_close(x, g["fgmres_ilu_x"], what="FGMRES(ILU0)")
