@@ -1,0 +1,291 @@
+"""Host-side Python mirror of the reactive-RANS hot path on MI355X.
+
+The compute lives in librx.so (hand-written HIP kernels for gfx950 behind the C ABI of
+include/rx.h). This module only marshals arrays through that ABI; it never computes physics and
+has no CPU fallback: on a machine without a HIP device the context creation fails loudly.
+
+The class and method names mirror the reference's CSolver / CNumerics call surface
+(SU2_CFD/include/solver_reactive.hpp): Preprocessing-time fields are uploaded, then
+Upwind_Residual / Viscous_Residual / Source_Residual / SetTime_Step / SetPrimitive_Gradient_LS /
+SetPrimitive_Limiter / ExplicitEuler_Iteration / ImplicitEuler_Iteration run on the device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librx.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "rx.h")
+
+# rx_status
+RX_OK, RX_ERR_ARG, RX_ERR_HIP, RX_ERR_NAN, RX_ERR_RANGE, RX_ERR_NONPHYS, RX_ERR_DIVERGED, RX_ERR_STATE = range(8)
+# rx_field
+FIELDS = ["U", "V", "DPDU", "DTDU", "MU", "KAPPA", "DIJ", "GRAD", "LIMITER", "TKE", "OMEGA", "MUT", "SIGMAK", "GRADK",
+          "EDDY", "RES", "DT", "LAMBDA_INV", "LAMBDA_VISC", "JAC", "ILU", "SOL", "RHS"]
+F = {name: k for k, name in enumerate(FIELDS)}
+# rx_kernel
+KERNELS = ["CONV", "VISC", "SOURCE", "GRAD", "LIMITER", "DT", "SPMV", "ILU_BUILD", "ILU_APPLY", "LUSGS", "KRYLOV",
+           "UPDATE"]
+K = {name: k for k, name in enumerate(KERNELS)}
+
+
+class RxError(RuntimeError):
+    pass
+
+
+class MechDesc(C.Structure):
+    _fields_ = [("n_species", C.c_int32), ("n_reactions", C.c_int32), ("n_tab", C.c_int32),
+                ("mmass", C.c_void_p), ("diff_vol", C.c_void_p),
+                ("stoich_reac", C.c_void_p), ("stoich_prod", C.c_void_p),
+                ("exp_reac", C.c_void_p), ("exp_prod", C.c_void_p),
+                ("A", C.c_void_p), ("beta", C.c_void_p), ("Ta", C.c_void_p),
+                ("A_back", C.c_void_p), ("beta_back", C.c_void_p), ("Ta_back", C.c_void_p),
+                ("reversible", C.c_void_p), ("has_backward", C.c_void_p),
+                ("tab_x", C.c_void_p), ("tab_y", C.c_void_p), ("tab_y2", C.c_void_p)]
+
+
+class MeshDesc(C.Structure):
+    _fields_ = [("n_dim", C.c_int32), ("n_point", C.c_int64), ("n_edge", C.c_int64), ("n_bvert", C.c_int64),
+                ("edges", C.c_void_p), ("edge_normal", C.c_void_p), ("coord", C.c_void_p), ("volume", C.c_void_p),
+                ("nbr_ptr", C.c_void_p), ("nbr", C.c_void_p), ("bvert", C.c_void_p), ("bvert_normal", C.c_void_p)]
+
+
+class Cfg(C.Structure):
+    _fields_ = [("mach_inf", C.c_double), ("T_ref", C.c_double), ("E_ref", C.c_double), ("R_ref", C.c_double),
+                ("rho_ref", C.c_double), ("t_ref", C.c_double), ("prandtl_lam", C.c_double),
+                ("prandtl_turb", C.c_double), ("lewis_turb", C.c_double), ("c_mu", C.c_double),
+                ("pasr_lb", C.c_double), ("cfl", C.c_double), ("max_delta_time", C.c_double),
+                ("ref_elem_length", C.c_double), ("limiter_coeff", C.c_double), ("lin_tol", C.c_double),
+                ("relaxation", C.c_double), ("implicit", C.c_int32), ("rans", C.c_int32), ("lin_iter", C.c_int32),
+                ("lin_prec", C.c_int32)]
+
+
+_lib = None
+
+
+def build():
+    """Compile librx.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-j4", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RxError(f"librx.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        _lib = C.CDLL(LIB_PATH)
+        _lib.rx_status_string.restype = C.c_char_p
+        _lib.rx_last_error_index.restype = C.c_int64
+        _lib.rx_ctx_create.argtypes = [C.POINTER(MeshDesc), C.POINTER(MechDesc), C.POINTER(Cfg), C.c_int,
+                                       C.POINTER(C.c_void_p)]
+        for name in ("rx_ctx_destroy", "rx_sync", "rx_residual_zero", "rx_edge_flux_conv", "rx_edge_flux_visc",
+                     "rx_cell_source_pasr", "rx_grad_lsq", "rx_limiter_venkat", "rx_time_step", "rx_ilu0_build"):
+            getattr(_lib, name).argtypes = [C.c_void_p]
+        _lib.rx_upload.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
+        _lib.rx_download.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
+        _lib.rx_field_size.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int64)]
+        _lib.rx_bsr_pattern.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib.rx_bsr_spmv.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        _lib.rx_ilu0_apply.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        _lib.rx_lusgs_apply.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        _lib.rx_fgmres.argtypes = [C.c_void_p, C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        _lib.rx_explicit_euler.argtypes = [C.c_void_p, C.c_void_p]
+        _lib.rx_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        _lib.rx_profile_enable.argtypes = [C.c_void_p, C.c_int]
+        _lib.rx_profile_read.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+        _lib.rx_last_error_index.argtypes = [C.c_void_p]
+    return _lib
+
+
+def header_symbols():
+    """Function names declared in include/rx.h (the ABI contract)."""
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(rx_[a-z0-9_]+)\s*\(", txt, re.M)))
+
+
+def _chk(rc, what, ctx=None):
+    if rc != RX_OK:
+        msg = lib().rx_status_string(rc).decode()
+        idx = lib().rx_last_error_index(ctx) if ctx is not None else -1
+        raise RxError(f"{what}: {msg} (status {rc}, index {idx})")
+
+
+class Mechanism:
+    """Flat mechanism arrays (same keys as oracle/mech.py / the golden files' mech_* arrays)."""
+
+    def __init__(self, arrays, prefix="mech_"):
+        g = {k[len(prefix):]: arrays[k] for k in arrays if k.startswith(prefix)}
+        f8 = lambda k: np.ascontiguousarray(g[k], dtype=np.float64)
+        i4 = lambda k: np.ascontiguousarray(g[k], dtype=np.int32)
+        self.ns = int(g["n_species"])
+        self.nr = int(g["n_reactions"])
+        self.ntab = int(g["tab_x"].shape[2])
+        self._keep = {k: f8(k) for k in ("mmass", "diff_vol", "stoich_reac", "stoich_prod", "exp_reac", "exp_prod",
+                                         "A", "beta", "Ta", "A_back", "beta_back", "Ta_back", "tab_x", "tab_y",
+                                         "tab_y2")}
+        self._keep["reversible"] = i4("reversible")
+        self._keep["has_backward"] = i4("has_backward")
+        d = MechDesc()
+        d.n_species, d.n_reactions, d.n_tab = self.ns, self.nr, self.ntab
+        for k, v in self._keep.items():
+            setattr(d, k, v.ctypes.data)
+        self.desc = d
+
+
+def default_cfg(**kw):
+    c = dict(mach_inf=0.01819, T_ref=1.0, E_ref=1.0, R_ref=1.0, rho_ref=1.0, t_ref=1.0, prandtl_lam=0.72,
+             prandtl_turb=0.9, lewis_turb=1.2, c_mu=0.09, pasr_lb=0.2, cfl=5.0, max_delta_time=1e6,
+             ref_elem_length=0.1, limiter_coeff=0.5, lin_tol=1e-6, relaxation=1.0, implicit=1, rans=1, lin_iter=5,
+             lin_prec=1)
+    c.update(kw)
+    cfg = Cfg()
+    for k, v in c.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+class ReactiveNSSolver:
+    """Device-resident reactive NS + SST flow state with the reference's per-phase entry points."""
+
+    def __init__(self, mesh, mech: Mechanism, cfg: Cfg, device=0):
+        self.mech = mech
+        self.cfg = cfg
+        self.nDim = int(mesh.get("n_dim", 2))
+        self.N = int(len(mesh["coord"]))
+        self.E = int(len(mesh["edges"]))
+        self.nVar = mech.ns + self.nDim + 2
+        self._mesh_keep = {
+            "edges": np.ascontiguousarray(mesh["edges"], dtype=np.int64),
+            "edge_normal": np.ascontiguousarray(mesh["edge_normal"], dtype=np.float64),
+            "coord": np.ascontiguousarray(mesh["coord"], dtype=np.float64),
+            "volume": np.ascontiguousarray(mesh["volume"], dtype=np.float64),
+            "nbr_ptr": np.ascontiguousarray(mesh["nbr_ptr"], dtype=np.int64),
+            "nbr": np.ascontiguousarray(mesh["nbr"], dtype=np.int64),
+            "bvert": np.ascontiguousarray(np.asarray(mesh["bvertex"])[:, :2], dtype=np.int64),
+            "bvert_normal": np.ascontiguousarray(mesh["bvertex_normal"], dtype=np.float64),
+        }
+        md = MeshDesc()
+        md.n_dim, md.n_point, md.n_edge = self.nDim, self.N, self.E
+        md.n_bvert = len(self._mesh_keep["bvert"])
+        for k, v in self._mesh_keep.items():
+            setattr(md, k, v.ctypes.data)
+        h = C.c_void_p()
+        _chk(lib().rx_ctx_create(C.byref(md), C.byref(mech.desc), C.byref(cfg), device, C.byref(h)), "rx_ctx_create")
+        self.h = h
+        self._mesh_keep = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- fields
+    def size(self, field):
+        n = C.c_int64()
+        _chk(lib().rx_field_size(self.h, F[field], C.byref(n)), "rx_field_size")
+        return n.value
+
+    def upload(self, field, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64).ravel()
+        _chk(lib().rx_upload(self.h, F[field], a.ctypes.data, a.size), f"rx_upload({field})", self.h)
+
+    def download(self, field):
+        n = self.size(field)
+        a = np.empty(n, dtype=np.float64)
+        _chk(lib().rx_download(self.h, F[field], a.ctypes.data, n), f"rx_download({field})", self.h)
+        return a
+
+    def bsr_pattern(self):
+        rp = np.empty(self.N + 1, dtype=np.int64)
+        lib().rx_bsr_pattern(self.h, rp.ctypes.data, None)
+        col = np.empty(int(rp[-1]), dtype=np.int64)
+        lib().rx_bsr_pattern(self.h, None, col.ctypes.data)
+        return rp, col
+
+    def set_state(self, st):
+        """Upload the node state produced by Preprocessing (primitives, transport, SST fields)."""
+        for key, field in (("V", "V"), ("dPdU", "DPDU"), ("dTdU", "DTDU"), ("mu", "MU"), ("kappa", "KAPPA"),
+                           ("Dij", "DIJ"), ("grad_prim", "GRAD"), ("turb_k", "TKE"), ("turb_omega", "OMEGA"),
+                           ("mu_t", "MUT"), ("sigma_k", "SIGMAK"), ("grad_k", "GRADK"), ("eddy_visc_flow", "EDDY"),
+                           ("U", "U")):
+            if key in st:
+                self.upload(field, st[key])
+
+    # ---- phases (reference CSolver names)
+    def _call(self, name, *args):
+        _chk(getattr(lib(), name)(self.h, *args), name, self.h)
+
+    def Preprocessing_zero(self):
+        self._call("rx_residual_zero")
+
+    def Upwind_Residual(self):
+        self._call("rx_edge_flux_conv")
+
+    def Viscous_Residual(self):
+        self._call("rx_edge_flux_visc")
+
+    def Source_Residual(self):
+        self._call("rx_cell_source_pasr")
+
+    def SetPrimitive_Gradient_LS(self):
+        self._call("rx_grad_lsq")
+
+    def SetPrimitive_Limiter(self):
+        self._call("rx_limiter_venkat")
+
+    def SetTime_Step(self):
+        self._call("rx_time_step")
+
+    def sync(self):
+        self._call("rx_sync")
+
+    def spmv(self, x="RHS", y="SOL"):
+        self._call("rx_bsr_spmv", F[x], F[y])
+
+    def ilu0_build(self):
+        self._call("rx_ilu0_build")
+
+    def ilu0_apply(self, b="RHS", x="SOL"):
+        self._call("rx_ilu0_apply", F[b], F[x])
+
+    def lusgs_apply(self, b="RHS", x="SOL"):
+        self._call("rx_lusgs_apply", F[b], F[x])
+
+    def fgmres(self, tol=None, m=None):
+        it = C.c_int()
+        res = C.c_double()
+        tol = self.cfg.lin_tol if tol is None else tol
+        m = self.cfg.lin_iter if m is None else m
+        _chk(lib().rx_fgmres(self.h, tol, m, C.byref(it), C.byref(res)), "rx_fgmres", self.h)
+        return it.value, res.value
+
+    def ExplicitEuler_Iteration(self):
+        rms = np.zeros(self.nVar)
+        _chk(lib().rx_explicit_euler(self.h, rms.ctypes.data), "rx_explicit_euler", self.h)
+        return rms
+
+    def ImplicitEuler_Iteration(self):
+        rms = np.zeros(self.nVar)
+        it = C.c_int()
+        _chk(lib().rx_implicit_euler(self.h, rms.ctypes.data, C.byref(it)), "rx_implicit_euler", self.h)
+        return rms, it.value
+
+    def profile(self, on=True):
+        _chk(lib().rx_profile_enable(self.h, int(on)), "rx_profile_enable")
+
+    def profile_read(self, kernel):
+        ms = C.c_double()
+        n = C.c_int64()
+        lib().rx_profile_read(self.h, K[kernel], C.byref(ms), C.byref(n))
+        return ms.value, n.value

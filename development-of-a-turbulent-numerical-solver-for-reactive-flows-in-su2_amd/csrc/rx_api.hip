@@ -1,0 +1,517 @@
+// rx_api.hip — C ABI (include/rx.h): context setup (dual-grid adjacency, BSR pattern, level
+// schedule, mechanism upload) and the phase entry points in the reference's call order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "rx_ctx.h"
+
+namespace {
+
+template <typename T>
+int dalloc(rx_ctx* ctx, T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  RX_HIP(hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)));
+  RX_HIP(hipMemsetAsync(*p, 0, n * sizeof(T), ctx->stream));
+  return RX_OK;
+}
+
+template <typename T>
+int dupload(rx_ctx* ctx, T** p, const T* h, size_t n) {
+  int rc = dalloc(ctx, p, n);
+  if (rc) return rc;
+  if (n) RX_HIP(hipMemcpy(*p, h, n * sizeof(T), hipMemcpyHostToDevice));
+  return RX_OK;
+}
+
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+int ensure_assembled(rx_ctx* ctx) {
+  if (!ctx->cfg.implicit || ctx->assembled) return RX_OK;
+  if (!ctx->phase_conv) return RX_ERR_STATE;
+  int rc = rx_launch_assemble(ctx, ctx->phase_visc, ctx->phase_src);
+  if (rc) return rc;
+  ctx->assembled = 1;
+  return RX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rx_status_string(int s) {
+  switch (s) {
+    case RX_OK: return "ok";
+    case RX_ERR_ARG: return "invalid argument";
+    case RX_ERR_HIP: return "HIP runtime error";
+    case RX_ERR_NAN: return "NaN found in the residual";
+    case RX_ERR_RANGE: return "temperature out of the property-table range";
+    case RX_ERR_NONPHYS: return "non-physical state";
+    case RX_ERR_DIVERGED: return "linear solver diverged";
+    case RX_ERR_STATE: return "call sequence error";
+    default: return "unknown";
+  }
+}
+
+int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg* cfg, int device, rx_ctx** out) {
+  if (!mesh || !mech || !cfg || !out) return RX_ERR_ARG;
+  if (mesh->n_dim != 2) return RX_ERR_ARG;  // 3-D dual grids: next round
+  const int ns = mech->n_species;
+  if (!(ns == 3 || ns == 4 || ns == 7 || ns == 9)) return RX_ERR_ARG;
+  if (mech->n_reactions > rx::kMaxNR) return RX_ERR_ARG;
+  if (mesh->n_point >= (1LL << 31) || 2 * mesh->n_edge >= (1LL << 31)) return RX_ERR_ARG;
+  rx_ctx* ctx = new rx_ctx();
+  *out = nullptr;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete ctx;
+    return RX_ERR_HIP;
+  }
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return RX_ERR_HIP;
+  }
+  ctx->cfg = *cfg;
+  ctx->nDim = mesh->n_dim;
+  ctx->ns = ns;
+  ctx->nr = mech->n_reactions;
+  ctx->nVar = ns + ctx->nDim + 2;
+  ctx->nPV = ns + ctx->nDim + 5;
+  ctx->nG = ns + ctx->nDim + 2;
+  ctx->nL = ctx->nDim + 2;
+  const int64_t N = mesh->n_point, E = mesh->n_edge, NB = mesh->n_bvert;
+  ctx->N = N;
+  ctx->E = E;
+  ctx->NB = NB;
+  const int nd = ctx->nDim, nv = ctx->nVar;
+  int rc = RX_OK;
+#define CK(x)        \
+  do {               \
+    rc = (x);        \
+    if (rc) {        \
+      rx_ctx_destroy(ctx); \
+      return rc;     \
+    }                \
+  } while (0)
+
+  // ---- edges, incident-edge adjacency (sorted by edge id), BSR pattern
+  std::vector<int32_t> e32(2 * E);
+  for (int64_t q = 0; q < 2 * E; ++q) {
+    if (mesh->edges[q] < 0 || mesh->edges[q] >= N) {
+      rx_ctx_destroy(ctx);
+      return RX_ERR_ARG;
+    }
+    e32[q] = (int32_t)mesh->edges[q];
+  }
+  std::vector<int32_t> adj_ptr(N + 1, 0), adj(2 * E);
+  for (int64_t e = 0; e < E; ++e) {
+    adj_ptr[e32[2 * e] + 1]++;
+    adj_ptr[e32[2 * e + 1] + 1]++;
+  }
+  for (int64_t i = 0; i < N; ++i) adj_ptr[i + 1] += adj_ptr[i];
+  {
+    std::vector<int32_t> fill(adj_ptr.begin(), adj_ptr.end() - 1);
+    for (int64_t e = 0; e < E; ++e) {  // increasing e => sorted
+      adj[fill[e32[2 * e]]++] = (int32_t)(e << 1);
+      adj[fill[e32[2 * e + 1]]++] = (int32_t)((e << 1) | 1);
+    }
+  }
+  // BSR: neighbours + diagonal, sorted (matrix_structure.cpp:113-201)
+  ctx->h_rp.assign(N + 1, 0);
+  std::vector<std::vector<int32_t>> rows(N);
+  for (int64_t i = 0; i < N; ++i) {
+    rows[i].push_back((int32_t)i);
+    for (int32_t k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+      const int e = adj[k] >> 1, side = adj[k] & 1;
+      rows[i].push_back(e32[2 * e + (side ^ 1)]);
+    }
+    std::sort(rows[i].begin(), rows[i].end());
+    rows[i].erase(std::unique(rows[i].begin(), rows[i].end()), rows[i].end());
+    ctx->h_rp[i + 1] = ctx->h_rp[i] + (int64_t)rows[i].size();
+  }
+  ctx->nnzb = ctx->h_rp[N];
+  ctx->h_col.resize(ctx->nnzb);
+  std::vector<int32_t> rp32(N + 1), col32(ctx->nnzb);
+  std::vector<int64_t> diag(N), adj_blk(2 * E);
+  for (int64_t i = 0; i < N; ++i) {
+    rp32[i] = (int32_t)ctx->h_rp[i];
+    for (size_t q = 0; q < rows[i].size(); ++q) {
+      ctx->h_col[ctx->h_rp[i] + q] = rows[i][q];
+      col32[ctx->h_rp[i] + q] = rows[i][q];
+      if (rows[i][q] == i) diag[i] = ctx->h_rp[i] + (int64_t)q;
+    }
+    for (int32_t k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+      const int e = adj[k] >> 1, side = adj[k] & 1;
+      const int32_t o = e32[2 * e + (side ^ 1)];
+      const auto it = std::lower_bound(rows[i].begin(), rows[i].end(), o);
+      adj_blk[k] = ctx->h_rp[i] + (it - rows[i].begin());
+    }
+  }
+  rp32[N] = (int32_t)ctx->nnzb;
+  // level schedules of the lower / upper triangular dependency graphs
+  {
+    std::vector<int32_t> lv(N, 0), bl(N, 0);
+    int32_t maxl = 0, maxb = 0;
+    for (int64_t i = 0; i < N; ++i) {
+      int32_t l = 0;
+      for (auto j : rows[i])
+        if (j < i) l = std::max(l, lv[j] + 1);
+      lv[i] = l;
+      maxl = std::max(maxl, l);
+    }
+    for (int64_t i = N - 1; i >= 0; --i) {
+      int32_t l = 0;
+      for (auto j : rows[i])
+        if (j > i) l = std::max(l, bl[j] + 1);
+      bl[i] = l;
+      maxb = std::max(maxb, l);
+    }
+    auto bucket = [&](const std::vector<int32_t>& lev, int32_t maxlev, std::vector<int32_t>& ptr,
+                      std::vector<int32_t>& order) {
+      ptr.assign(maxlev + 2, 0);
+      for (int64_t i = 0; i < N; ++i) ptr[lev[i] + 1]++;
+      for (int32_t l = 0; l <= maxlev; ++l) ptr[l + 1] += ptr[l];
+      order.resize(N);
+      std::vector<int32_t> f(ptr.begin(), ptr.end() - 1);
+      for (int64_t i = 0; i < N; ++i) order[f[lev[i]]++] = (int32_t)i;
+    };
+    std::vector<int32_t> fo, bo;
+    bucket(lv, maxl, ctx->h_lvl_ptr, fo);
+    bucket(bl, maxb, ctx->h_blvl_ptr, bo);
+    CK(dupload(ctx, &ctx->lvl_rows, fo.data(), N));
+    CK(dupload(ctx, &ctx->blvl_rows, bo.data(), N));
+  }
+  // LSQ neighbour lists (reference order) and boundary vertices per node
+  std::vector<int32_t> nptr(N + 1), nbr(mesh->nbr_ptr[N]);
+  for (int64_t i = 0; i <= N; ++i) nptr[i] = (int32_t)mesh->nbr_ptr[i];
+  for (int64_t q = 0; q < mesh->nbr_ptr[N]; ++q) nbr[q] = (int32_t)mesh->nbr[q];
+  std::vector<int32_t> bvp(N + 1, 0);
+  std::vector<double> bvn((size_t)std::max<int64_t>(NB, 1) * nd);
+  {
+    for (int64_t b = 0; b < NB; ++b) bvp[mesh->bvert[2 * b + 1] + 1]++;
+    for (int64_t i = 0; i < N; ++i) bvp[i + 1] += bvp[i];
+    std::vector<int32_t> f(bvp.begin(), bvp.end() - 1);
+    for (int64_t b = 0; b < NB; ++b) {  // input is in (marker, vertex) order: stable per node
+      const int64_t p = mesh->bvert[2 * b + 1];
+      const int32_t slot = f[p]++;
+      for (int d = 0; d < nd; ++d) bvn[(size_t)slot * nd + d] = mesh->bvert_normal[b * nd + d];
+    }
+  }
+  CK(dupload(ctx, &ctx->edges, e32.data(), 2 * E));
+  CK(dupload(ctx, &ctx->normal, mesh->edge_normal, E * nd));
+  CK(dupload(ctx, &ctx->coord, mesh->coord, N * nd));
+  CK(dupload(ctx, &ctx->vol, mesh->volume, N));
+  CK(dupload(ctx, &ctx->adj_ptr, adj_ptr.data(), N + 1));
+  CK(dupload(ctx, &ctx->adj, adj.data(), 2 * E));
+  CK(dupload(ctx, &ctx->adj_blk, adj_blk.data(), 2 * E));
+  CK(dupload(ctx, &ctx->nbr_ptr, nptr.data(), N + 1));
+  CK(dupload(ctx, &ctx->nbr, nbr.data(), nbr.size()));
+  CK(dupload(ctx, &ctx->bv_ptr, bvp.data(), N + 1));
+  CK(dupload(ctx, &ctx->bv_normal, bvn.data(), bvn.size()));
+  CK(dupload(ctx, &ctx->rp, rp32.data(), N + 1));
+  CK(dupload(ctx, &ctx->col, col32.data(), ctx->nnzb));
+  CK(dupload(ctx, &ctx->diag, diag.data(), N));
+
+  // ---- mechanism
+  {
+    rx::DevMech& m = ctx->mech;
+    const int nr = mech->n_reactions, nt = mech->n_tab;
+    m.ns = ns;
+    m.nr = nr;
+    m.ntab = nt;
+    auto up = [&](const double* h, size_t n) -> const double* {
+      double* d = nullptr;
+      if (dupload(ctx, &d, h, n)) return nullptr;
+      ctx->mech_bufs.push_back(d);
+      return d;
+    };
+    auto upi = [&](const int32_t* h, size_t n) -> const int* {
+      int32_t* d = nullptr;
+      if (dupload(ctx, &d, h, n)) return nullptr;
+      ctx->mech_bufs.push_back(d);
+      return d;
+    };
+    m.mm = up(mech->mmass, ns);
+    m.sr = up(mech->stoich_reac, (size_t)ns * nr);
+    m.sp = up(mech->stoich_prod, (size_t)ns * nr);
+    m.er = up(mech->exp_reac, (size_t)ns * nr);
+    m.ep = up(mech->exp_prod, (size_t)ns * nr);
+    m.A = up(mech->A, nr);
+    m.beta = up(mech->beta, nr);
+    m.Ta = up(mech->Ta, nr);
+    m.Ab = up(mech->A_back, nr);
+    m.betab = up(mech->beta_back, nr);
+    m.Tab = up(mech->Ta_back, nr);
+    m.rev = upi(mech->reversible, nr);
+    m.hasb = upi(mech->has_backward, nr);
+    m.tx = up(mech->tab_x, (size_t)5 * ns * nt);
+    m.ty = up(mech->tab_y, (size_t)5 * ns * nt);
+    m.ty2 = up(mech->tab_y2, (size_t)5 * ns * nt);
+    m.mtot = 0.0;
+    for (int s = 0; s < ns; ++s) m.mtot += mech->mmass[s];
+    for (int r = 0; r < rx::kMaxNR; ++r) m.neg_reac[r] = m.neg_prod[r] = 0;
+    for (int r = 0; r < nr; ++r)
+      for (int s = 0; s < ns; ++s) {
+        if (mech->exp_reac[r * ns + s] < 0.0) m.neg_reac[r] |= (1u << s);
+        if (mech->exp_prod[r * ns + s] < 0.0) m.neg_prod[r] |= (1u << s);
+      }
+    if (!m.mm || !m.tx || !m.ty2) CK(RX_ERR_HIP);
+  }
+
+  // ---- fields
+  const int64_t nb2 = ctx->nnzb * (int64_t)nv * nv;
+  const int64_t sizes[RX_F_COUNT] = {
+      N * nv,                 // U
+      N * ctx->nPV,           // V
+      N * nv, N * nv,         // dPdU, dTdU
+      N, N,                   // mu, kappa
+      N * ns * ns,            // Dij
+      N * ctx->nG * nd,       // grad
+      N * ctx->nL,            // limiter
+      N, N, N, N,             // tke, omega, mut, sigmak
+      N * nd,                 // gradk
+      N,                      // eddy
+      N * nv,                 // res
+      N, N, N,                // dt, lambda_inv, lambda_visc
+      ctx->cfg.implicit ? nb2 : 0,                       // jac
+      ctx->cfg.implicit ? nb2 + N * (int64_t)nv * nv : 0, // ilu (+ inverse diagonals)
+      N * nv, N * nv          // sol, rhs
+  };
+  for (int q = 0; q < RX_F_COUNT; ++q) {
+    ctx->fcount[q] = sizes[q];
+    CK(dalloc(ctx, &ctx->f[q], sizes[q]));
+  }
+  ctx->fcount[RX_F_ILU] = ctx->cfg.implicit ? nb2 : 0;
+  if (ctx->cfg.implicit) {
+    CK(dalloc(ctx, &ctx->fconv, E * nv));
+    CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
+    CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
+    CK(dalloc(ctx, &ctx->jsrc, N * (int64_t)nv * nv));
+    CK(dalloc(ctx, &ctx->rsrc, N * nv));
+  }
+  CK(dalloc(ctx, &ctx->fvisc, E * nv));
+  CK(dalloc(ctx, &ctx->lim_mn, N * ctx->nL));
+  CK(dalloc(ctx, &ctx->lim_mx, N * ctx->nL));
+  CK(dalloc(ctx, &ctx->red, 256 * 32 + 1024));
+  CK(dalloc(ctx, &ctx->err, 2));
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), sizeof(double) * (256 * 32 + 1024)) != hipSuccess)
+    CK(RX_ERR_HIP);
+  if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) CK(RX_ERR_HIP);
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) CK(RX_ERR_HIP);
+#undef CK
+  *out = ctx;
+  return RX_OK;
+}
+
+int rx_ctx_destroy(rx_ctx* ctx) {
+  if (!ctx) return RX_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->nbr_ptr,
+                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->lvl_rows, ctx->blvl_rows,
+                  ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->jsrc, ctx->rsrc, ctx->lim_mn, ctx->lim_mx,
+                  ctx->red, ctx->err, ctx->kw, ctx->kz};
+  for (void* p : ptrs) dfree(p);
+  for (void* p : ctx->mech_bufs) dfree(p);
+  for (int q = 0; q < RX_F_COUNT; ++q) dfree(ctx->f[q]);
+  if (ctx->h_red) (void)hipHostFree(ctx->h_red);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return RX_OK;
+}
+
+int rx_field_size(const rx_ctx* ctx, rx_field f, int64_t* count) {
+  if (!ctx || f < 0 || f >= RX_F_COUNT || !count) return RX_ERR_ARG;
+  *count = ctx->fcount[f];
+  return RX_OK;
+}
+
+int rx_upload(rx_ctx* ctx, rx_field f, const double* host, int64_t count) {
+  if (!ctx || f < 0 || f >= RX_F_COUNT || count != ctx->fcount[f] || !host) return RX_ERR_ARG;
+  RX_HIP(hipMemcpyAsync(ctx->f[f], host, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  RX_HIP(hipStreamSynchronize(ctx->stream));
+  return RX_OK;
+}
+
+int rx_download(rx_ctx* ctx, rx_field f, double* host, int64_t count) {
+  if (!ctx || f < 0 || f >= RX_F_COUNT || count != ctx->fcount[f] || !host) return RX_ERR_ARG;
+  if (f == RX_F_RES || f == RX_F_JAC) {
+    int rc = ensure_assembled(ctx);
+    if (rc && rc != RX_ERR_STATE) return rc;
+  }
+  RX_HIP(hipMemcpyAsync(host, ctx->f[f], count * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  RX_HIP(hipStreamSynchronize(ctx->stream));
+  return RX_OK;
+}
+
+int rx_bsr_pattern(const rx_ctx* ctx, int64_t* row_ptr, int64_t* col) {
+  if (!ctx) return RX_ERR_ARG;
+  if (row_ptr) std::memcpy(row_ptr, ctx->h_rp.data(), sizeof(int64_t) * (ctx->N + 1));
+  if (col) std::memcpy(col, ctx->h_col.data(), sizeof(int64_t) * ctx->nnzb);
+  return RX_OK;
+}
+
+int rx_sync(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RX_HIP(hipStreamSynchronize(ctx->stream));
+  return rx_check_error(ctx);
+}
+
+int64_t rx_last_error_index(const rx_ctx* ctx) { return ctx ? ctx->last_err_index : -1; }
+
+int rx_residual_zero(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
+  ctx->phase_conv = ctx->phase_visc = ctx->phase_src = 0;
+  ctx->assembled = ctx->cfg.implicit ? 0 : 1;
+  return RX_OK;
+}
+
+int rx_edge_flux_conv(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_CONV);
+  int rc = ctx->cfg.implicit ? rx_launch_ausm_edge(ctx) : rx_launch_ausm_node(ctx);
+  if (rc) return rc;
+  ctx->phase_conv = 1;
+  ctx->assembled = ctx->cfg.implicit ? 0 : 1;
+  return RX_OK;
+}
+
+int rx_edge_flux_visc(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_VISC);
+  int rc = rx_launch_visc_edge(ctx);
+  if (rc) return rc;
+  if (!ctx->cfg.implicit) {
+    rc = rx_launch_gather_edge_flux(ctx, ctx->fvisc, -1.0);  // R[i] -= Fv, R[j] += Fv
+    if (rc) return rc;
+  }
+  ctx->phase_visc = 1;
+  ctx->assembled = ctx->cfg.implicit ? 0 : 1;
+  return RX_OK;
+}
+
+int rx_cell_source_pasr(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_SOURCE);
+  int rc = rx_launch_source(ctx);
+  if (rc) return rc;
+  ctx->phase_src = 1;
+  ctx->assembled = ctx->cfg.implicit ? 0 : 1;
+  return RX_OK;
+}
+
+int rx_grad_lsq(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_GRAD);
+  return rx_launch_grad(ctx);
+}
+
+int rx_limiter_venkat(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_LIMITER);
+  return rx_launch_limiter(ctx);
+}
+
+int rx_time_step(rx_ctx* ctx) {
+  if (!ctx) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_DT);
+  return rx_launch_time_step(ctx);
+}
+
+int rx_bsr_spmv(rx_ctx* ctx, rx_field x, rx_field y) {
+  if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
+  int rc = ensure_assembled(ctx);
+  if (rc) return rc;
+  RxPhase ph(ctx, RX_K_SPMV);
+  return rx_la_spmv(ctx, ctx->f[RX_F_JAC], ctx->f[x], ctx->f[y]);
+}
+
+int rx_ilu0_build(rx_ctx* ctx) {
+  if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
+  int rc = ensure_assembled(ctx);
+  if (rc) return rc;
+  RxPhase ph(ctx, RX_K_ILU_BUILD);
+  return rx_la_ilu_build(ctx);
+}
+
+int rx_ilu0_apply(rx_ctx* ctx, rx_field b, rx_field x) {
+  if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_ILU_APPLY);
+  return rx_la_ilu_apply(ctx, ctx->f[b], ctx->f[x]);
+}
+
+int rx_lusgs_apply(rx_ctx* ctx, rx_field b, rx_field x) {
+  if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
+  int rc = ensure_assembled(ctx);
+  if (rc) return rc;
+  RxPhase ph(ctx, RX_K_LUSGS);
+  return rx_la_lusgs(ctx, ctx->f[RX_F_JAC], ctx->f[b], ctx->f[x]);
+}
+
+int rx_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
+  if (!ctx || !ctx->cfg.implicit || !iters || !resid) return RX_ERR_ARG;
+  int rc = ensure_assembled(ctx);
+  if (rc) return rc;
+  RxPhase ph(ctx, RX_K_KRYLOV);
+  return rx_la_fgmres(ctx, tol, m, iters, resid);
+}
+
+int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
+  if (!ctx) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_UPDATE);
+  return rx_la_explicit_update(ctx, res_rms);
+}
+
+// ImplicitEuler_Iteration (solver_direct_reactive.cpp:2336-2407): system build, ILU0 build if
+// selected (CSysSolve::Solve :601-653), FGMRES, clipped relaxed update.
+int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
+  if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
+  int rc = ensure_assembled(ctx);
+  if (rc) return rc;
+  {
+    RxPhase ph(ctx, RX_K_UPDATE);
+    if ((rc = rx_la_build_system(ctx))) return rc;
+  }
+  if (ctx->cfg.lin_prec == 1) {
+    RxPhase ph(ctx, RX_K_ILU_BUILD);
+    if ((rc = rx_la_ilu_build(ctx))) return rc;
+  }
+  int it = 0;
+  double resid = 0.0;
+  {
+    RxPhase ph(ctx, RX_K_KRYLOV);
+    if ((rc = rx_la_fgmres(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter, &it, &resid))) return rc;
+  }
+  if (lin_iters) *lin_iters = it;
+  RxPhase ph(ctx, RX_K_UPDATE);
+  return rx_la_implicit_update(ctx, res_rms);
+}
+
+int rx_profile_enable(rx_ctx* ctx, int on) {
+  if (!ctx) return RX_ERR_ARG;
+  ctx->prof = on != 0;
+  for (int k = 0; k < RX_K_COUNT; ++k) {
+    ctx->prof_ms[k] = 0.0;
+    ctx->prof_n[k] = 0;
+  }
+  return RX_OK;
+}
+
+int rx_profile_read(rx_ctx* ctx, rx_kernel k, double* total_ms, int64_t* launches) {
+  if (!ctx || k < 0 || k >= RX_K_COUNT) return RX_ERR_ARG;
+  if (total_ms) *total_ms = ctx->prof_ms[k];
+  if (launches) *launches = ctx->prof_n[k];
+  return RX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+// rx_ctx.h — the device-resident state behind the C ABI (include/rx.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rx.h"
+#include "rx_device.h"
+
+#define RX_HIP(call)                                     \
+  do {                                                   \
+    hipError_t _e = (call);                              \
+    if (_e != hipSuccess) return rx_fail_hip(ctx, _e);   \
+  } while (0)
+
+struct rx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int nDim = 2, ns = 0, nr = 0, nVar = 0, nPV = 0, nG = 0, nL = 0;
+  int64_t N = 0, E = 0, NB = 0, nnzb = 0;
+  rx_cfg cfg{};
+
+  // ---- dual grid (device)
+  int32_t* edges = nullptr;     // [E][2]
+  double* normal = nullptr;     // [E][nDim]
+  double* coord = nullptr;      // [N][nDim]
+  double* vol = nullptr;        // [N]
+  int32_t* adj_ptr = nullptr;   // [N+1] incident edges per node, increasing edge id
+  int32_t* adj = nullptr;       // [2E] (edge << 1) | (node is the edge's second node)
+  int64_t* adj_blk = nullptr;   // [2E] BSR block index of (node, other)
+  int32_t* nbr_ptr = nullptr;   // [N+1] LSQ neighbours in the reference order
+  int32_t* nbr = nullptr;
+  int32_t* bv_ptr = nullptr;    // [N+1] boundary vertices per node in (marker, vertex) order
+  double* bv_normal = nullptr;  // [NB][nDim]
+  // ---- BSR pattern (device + host copy)
+  int32_t* rp = nullptr;        // [N+1]
+  int32_t* col = nullptr;       // [nnzb]
+  int64_t* diag = nullptr;      // [N] block index of the diagonal
+  std::vector<int64_t> h_rp, h_col;
+  // level schedule for the triangular sweeps (rows grouped by dependency level)
+  int32_t* lvl_rows = nullptr;  // [N] rows sorted by forward level
+  std::vector<int32_t> h_lvl_ptr;   // [nLevels+1]
+  int32_t* blvl_rows = nullptr; // [N] rows sorted by backward level
+  std::vector<int32_t> h_blvl_ptr;
+
+  // ---- mechanism
+  rx::DevMech mech{};
+  std::vector<void*> mech_bufs;
+
+  // ---- fields (device), see rx_field
+  double* f[RX_F_COUNT] = {};
+  int64_t fcount[RX_F_COUNT] = {};
+
+  // ---- scratch
+  double* fconv = nullptr;   // [E][nVar]   convective edge fluxes (implicit path)
+  double* fvisc = nullptr;   // [E][nVar]   viscous edge fluxes
+  double* jconv = nullptr;   // [E][2][nVar*nVar]
+  double* jvisc = nullptr;   // [E][2][nVar*nVar]
+  double* jsrc = nullptr;    // [N][nVar*nVar]
+  double* rsrc = nullptr;    // [N][nVar] source residual (implicit path)
+  int phase_conv = 0, phase_visc = 0, phase_src = 0, assembled = 1;
+  double* lim_mn = nullptr;  // [N][nL]
+  double* lim_mx = nullptr;
+  double* red = nullptr;     // reduction scratch
+  double* h_red = nullptr;   // pinned host mirror
+  int* err = nullptr;        // [2] code, index (device)
+  int64_t last_err_index = -1;
+  // Krylov workspace
+  int krylov_m = 0;
+  double* kw = nullptr;      // [(m+1)][N*nVar]
+  double* kz = nullptr;      // [(m+1)][N*nVar]
+
+  // ---- profiling
+  bool prof = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double prof_ms[RX_K_COUNT] = {};
+  int64_t prof_n[RX_K_COUNT] = {};
+};
+
+int rx_fail_hip(rx_ctx* ctx, hipError_t e);
+
+// Phase timer: records HIP events around a phase on the context stream when profiling is on.
+struct RxPhase {
+  rx_ctx* c;
+  rx_kernel k;
+  RxPhase(rx_ctx* ctx, rx_kernel kk) : c(ctx), k(kk) {
+    if (c->prof) (void)hipEventRecord(c->ev0, c->stream);
+  }
+  ~RxPhase() {
+    if (c->prof) {
+      (void)hipEventRecord(c->ev1, c->stream);
+      (void)hipEventSynchronize(c->ev1);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+      c->prof_ms[k] += ms;
+      c->prof_n[k] += 1;
+    }
+  }
+};
+
+// kernel launchers (rx_kernels.hip)
+int rx_launch_ausm_node(rx_ctx* ctx);
+int rx_launch_ausm_edge(rx_ctx* ctx);
+int rx_launch_visc_edge(rx_ctx* ctx);
+int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);
+int rx_launch_source(rx_ctx* ctx);
+int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src);
+int rx_launch_grad(rx_ctx* ctx);
+int rx_launch_limiter(rx_ctx* ctx);
+int rx_launch_time_step(rx_ctx* ctx);
+int rx_check_error(rx_ctx* ctx);
+// linear algebra (rx_linalg.hip)
+int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y);
+int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x);
+int rx_la_ilu_build(rx_ctx* ctx);
+int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x);
+int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid);
+int rx_la_implicit_update(rx_ctx* ctx, double* rms);
+int rx_la_explicit_update(rx_ctx* ctx, double* rms);
+int rx_la_build_system(rx_ctx* ctx);

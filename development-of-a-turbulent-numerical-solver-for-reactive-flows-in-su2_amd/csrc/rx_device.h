@@ -1,0 +1,273 @@
+// rx_device.h — device-side physics of the reactive-RANS hot path (gfx950, FP64).
+//
+// Restates, for one edge / one cell, the reference operators cited per function (paths relative to
+// the reference root). Compiled with -ffp-contract=off so every expression rounds exactly as the
+// x86-64 reference (no FMA contraction); only transcendental calls (exp, pow, log, sqrt, cbrt) may
+// differ by an ulp from glibc.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rx {
+
+constexpr double kEPS = 1.0e-16;  // Common/include/option_structure.hpp:134
+constexpr double kNA = 6.02214129 * 1.0e23;
+constexpr double kKB = 1.3806488 * 1.0e-23;
+constexpr double kR = kNA * kKB * 1.0e3;           // physical_chemical_library.hpp:575
+constexpr double kRatm = 1.0e-3 * 0.082057338;     // :579
+constexpr double kTWO3 = 2.0 / 3.0;
+enum { P_CP = 0, P_H = 1, P_S = 2, P_MU = 3, P_KAPPA = 4 };
+enum { ERR_NONE = 0, ERR_RANGE = 1, ERR_NAN = 2, ERR_GEOM = 3 };
+
+constexpr int kMaxNS = 12;
+constexpr int kMaxNR = 8;
+
+// Mechanism + spline tables resident in HBM (~1 MB at Ns = 9: L2 / MALL resident).
+struct DevMech {
+  int ns, nr, ntab;
+  const double *mm;             // [ns]
+  const double *sr, *sp;        // [ns][nr]
+  const double *er, *ep;        // [nr][ns]
+  const double *A, *beta, *Ta, *Ab, *betab, *Tab;
+  const int *rev, *hasb;
+  const double *tx, *ty, *ty2;  // [5][ns][ntab]
+  double mtot;                  // sum of molar masses
+  uint32_t neg_reac[kMaxNR], neg_prod[kMaxNR];  // species masks with negative rate exponents
+};
+
+// MathTools::GetSpline (Common/src/Tools/spline.cpp:62-77). Out of range sets *err (the reference
+// throws std::out_of_range).
+__device__ __host__ inline double spline(const DevMech& m, int prop, int s, double T, int* err) {
+  const size_t off = (size_t)(prop * m.ns + s) * m.ntab;
+  const double* x = m.tx + off;
+  const double* y = m.ty + off;
+  const double* y2 = m.ty2 + off;
+  const double x0 = x[0], xn = x[m.ntab - 1];
+  if (T < x0 || T > xn) {
+    *err = ERR_RANGE;
+    return 0.0;
+  }
+  const double h = x[1] - x0;
+  unsigned long klo = (unsigned long)((T - x0) / h + 1);
+  if (klo > (unsigned long)(m.ntab - 1)) klo = m.ntab - 1;  // T == Tmax reads x[n] in the reference
+  const double a = (x[klo] - T) / h;
+  const double b = (T - x[klo - 1]) / h;
+  return a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0;
+}
+
+// ReactingModelLibrary::SetMassFractions + SetMolarFromMass (reacting_model_library.cpp:65-93)
+template <int NS>
+__device__ __host__ inline void molar_from_mass(const DevMech& m, const double* ys, double* xs) {
+  double yc[NS];
+  double sy = 0.0, sx = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    double y = ys[s];
+    if (y < 0.0) y = 1.0e-30;
+    yc[s] = y;
+    xs[s] = y / m.mm[s];
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sy += yc[s];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sx += xs[s];
+  const double tot = sy / sx;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) xs[s] = tot * xs[s];
+}
+
+// ------------------------------------------------------------------------------------------------
+// AUSM+-up, CUpwReactiveAUSM::ComputeResidual (SU2_CFD/src/numerics_direct_reactive.cpp:53-378).
+// The per-edge scalars are computed once; the residual and the Jacobian entries are evaluated
+// from them in exactly the reference's operation order.
+// ------------------------------------------------------------------------------------------------
+struct AusmEdge {
+  double Area, UN[3];
+  double rho_i, rho_j, p_i, p_j, pv_i, pv_j;
+  double mss, mL, mR, mF, mF2, mRef2, fa, alpha, m12, mLF, mRF, M12, pLP, pRM, factor, fpos, sign_m12;
+  double pLF;
+};
+
+template <int NDIM>
+__device__ __host__ inline void ausm_scalars(const double* Vi, const double* Vj, const double* Normal, double mInfty,
+                                             AusmEdge& s) {
+  constexpr int VX = 1, P_ = NDIM + 1, RHO = NDIM + 2, A_ = NDIM + 4;
+  double Area = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) Area += Normal[d] * Normal[d];
+  Area = sqrt(Area);
+  s.Area = Area;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) s.UN[d] = Normal[d] / Area;
+  s.rho_i = Vi[RHO];
+  s.rho_j = Vj[RHO];
+  s.p_i = Vi[P_];
+  s.p_j = Vj[P_];
+  double pvi = 0.0, pvj = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    pvi += Vi[VX + d] * s.UN[d];
+    pvj += Vj[VX + d] * s.UN[d];
+  }
+  s.pv_i = pvi;
+  s.pv_j = pvj;
+  const double mss = 0.5 * (Vi[A_] + Vj[A_]);
+  s.mss = mss;
+  const double mL = pvi / mss, mR = pvj / mss;
+  s.mL = mL;
+  s.mR = mR;
+  const double mF2 = 0.5 * (mL * mL + mR * mR);
+  const double mRef2 = fmin(1.0, fmax(mF2, mInfty * mInfty));
+  s.mF2 = mF2;
+  s.mRef2 = mRef2;
+  s.mF = sqrt(mF2);
+  const double mRef = sqrt(mRef2);
+  const double fa = mRef * (2.0 - mRef);
+  s.fa = fa;
+  const double alpha = 3.0 / 16.0 * (5.0 * fa * fa - 4.0);
+  s.alpha = alpha;
+  const double beta = 0.125;
+  double mLP, mRM, pLP, pRM;
+  if (fabs(mL) < 1.0) {
+    mLP = 0.25 * (mL + 1.0) * (mL + 1.0) + beta * (mL * mL - 1.0) * (mL * mL - 1.0);
+    pLP = 0.25 * (mL + 1.0) * (mL + 1.0) * (2.0 - mL) + alpha * mL * (mL * mL - 1.0) * (mL * mL - 1.0);
+  } else {
+    mLP = 0.5 * (mL + fabs(mL));
+    pLP = 0.5 * (1.0 + fabs(mL) / mL);
+  }
+  if (fabs(mR) < 1.0) {
+    mRM = -0.25 * (mR - 1.0) * (mR - 1.0) - beta * (mR * mR - 1.0) * (mR * mR - 1.0);
+    pRM = 0.25 * (mR - 1.0) * (mR - 1.0) * (2.0 + mR) - alpha * mR * (mR * mR - 1.0) * (mR * mR - 1.0);
+  } else {
+    mRM = 0.5 * (mR - fabs(mR));
+    pRM = 0.5 * (1.0 - fabs(mR) / mR);
+  }
+  s.pLP = pLP;
+  s.pRM = pRM;
+  const double kP = 0.25, sigma = 1.0;
+  double m12 = mLP + mRM;
+  m12 -= kP / fa * fmax(1.0 - sigma * mF2, 0.0) * (s.p_j - s.p_i) / (0.5 * (s.rho_i + s.rho_j) * mss * mss);
+  s.m12 = m12;
+  s.mLF = 0.5 * (m12 + fabs(m12));
+  s.mRF = 0.5 * (m12 - fabs(m12));
+  s.M12 = mss * (s.mLF * s.rho_i + s.mRF * s.rho_j);
+  const double Ku = 0.75;
+  double pLF = pLP * s.p_i + pRM * s.p_j;
+  pLF -= Ku * pLP * pRM * (s.rho_i + s.rho_j) * fa * mss * (pvj - pvi);
+  s.pLF = pLF;
+  s.factor = fmax(1.0 - sigma * mF2, 0.0);
+  s.fpos = (s.factor > 0.0) ? 1.0 : 0.0;
+  s.sign_m12 = (m12 != 0.0) ? fabs(m12) / m12 : 0.0;
+}
+
+// Phi (the convected state) for index v of the conservative vector.
+template <int NDIM>
+__device__ __host__ inline double ausm_phi(const double* V, double h, int v) {
+  // RHO: 1, momentum: velocity, RHOE: enthalpy, species: mass fraction
+  if (v == 0) return 1.0;
+  if (v <= NDIM) return V[v];
+  if (v == NDIM + 1) return h;
+  return V[NDIM + 5 + (v - NDIM - 2)];
+}
+
+// Residual component v (:180-188).
+template <int NDIM>
+__device__ __host__ inline double ausm_res(const AusmEdge& s, const double* Vi, const double* Vj, int v) {
+  constexpr int H_ = NDIM + 3;
+  const double pi = ausm_phi<NDIM>(Vi, Vi[H_], v), pj = ausm_phi<NDIM>(Vj, Vj[H_], v);
+  double r = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
+  if (v >= 1 && v <= NDIM) r += s.pLF * s.UN[v - 1] * s.Area;
+  return r;
+}
+
+// Per-column (b) derivative vectors of the Jacobian (:216-358).
+struct AusmCol {
+  double PlL, MiL, PlR, MiR, PDL, PDR;
+};
+
+template <int NDIM>
+__device__ __host__ inline AusmCol ausm_col(const AusmEdge& s, const double* Si, const double* Sj, int b) {
+  const double kP = 0.25, sigma = 1.0, beta = 0.125, Ku = 0.75;
+  const double mL = s.mL, mR = s.mR, mss = s.mss, fa = s.fa, alpha = s.alpha;
+  const double rho_i = s.rho_i, rho_j = s.rho_j;
+  double MLD = 0.0, MRD = 0.0;
+  if (b == 0) {
+    MLD = -mL / rho_i;
+    MRD = -mR / rho_j;
+  } else if (b <= NDIM) {
+    MLD = s.UN[b - 1] / (rho_i * mss);
+    MRD = s.UN[b - 1] / (rho_j * mss);
+  }
+  double MPL, MPR;
+  if (fabs(mL) < 1.0) MPL = MLD * (0.5 * (mL + 1.0) + 4.0 * beta * mL * (mL * mL - 1.0));
+  else MPL = MLD * (0.5 * (1.0 + fabs(mL) / mL));
+  if (fabs(mR) < 1.0) MPR = MRD * (0.5 * (1.0 - mR) + 4.0 * beta * mR * (1.0 - mR * mR));
+  else MPR = MRD * (0.5 * (1.0 - fabs(mR) / mR));
+  double SL = 0.0, SR = 0.0;
+  if (s.mF2 == s.mRef2) {
+    SL = MLD * mL * (1.0 - s.mF) / s.mF;
+    SR = MRD * mR * (1.0 - s.mF) / s.mF;
+  }
+  const double MD = 0.5 * (rho_i + rho_j);
+  const double dp = s.p_j - s.p_i;
+  double MEL = -kP / (mss * mss * fa * fa * MD * MD) *
+               ((s.fpos * sigma * mL * MLD * dp * fa * MD) + (s.factor * Si[b] * fa * MD) + (s.factor * dp * MD * SL));
+  double MER = kP / (mss * mss * fa * fa * MD * MD) *
+               ((s.fpos * sigma * mR * MRD * (s.p_i - s.p_j) * fa * MD) + (s.factor * Sj[b] * fa * MD) -
+                (s.factor * dp * MD * SR));
+  if (b == 0) {
+    MEL -= kP / (mss * mss * fa * MD * MD) * 0.5 * s.factor * dp;
+    MER -= kP / (mss * mss * fa * MD * MD) * 0.5 * s.factor * dp;
+  }
+  AusmCol c;
+  c.PlL = 0.5 * (MPL - MEL) * (1.0 + s.sign_m12);
+  c.MiL = 0.5 * (MPL - MEL) * (1.0 - s.sign_m12);
+  c.PlR = 0.5 * (MPR - MER) * (1.0 + s.sign_m12);
+  c.MiR = 0.5 * (MPR - MER) * (1.0 - s.sign_m12);
+  double PPL = 0.0, PPR = 0.0;
+  if (fabs(mL) < 1.0)
+    PPL = 0.25 * (mL + 1.0) * (3.0 * (1.0 - mL) + 4.0 * alpha * (5.0 * mL * mL - 1.0) * (mL - 1.0)) * MLD +
+          15.0 / 8.0 * SL * mL * (mL * mL - 1.0) * (mL * mL - 1.0);
+  if (fabs(mR) < 1.0)
+    PPR = 0.25 * (mR - 1.0) * (3.0 * (1.0 + mR) + 4.0 * alpha * (1.0 - 5.0 * mR * mR) * (mR + 1.0)) * MRD -
+          15.0 / 8.0 * SR * mR * (mR * mR - 1.0) * (mR * mR - 1.0);
+  const double dvn = s.pv_j - s.pv_i;
+  double PEL = Ku * s.pRM * mss * ((PPL * (rho_i + rho_j) * fa * dvn) + (s.pLP * (rho_i + rho_j) * dvn * SL));
+  double PER = Ku * s.pLP * mss * ((PPR * (rho_i + rho_j) * fa * dvn) + (s.pRM * (rho_i + rho_j) * dvn * SR));
+  if (b == 0) {
+    PEL += Ku * s.pRM * mss * s.pLP * fa * (dvn + (rho_i + rho_j) * s.pv_i / rho_i);
+    PER += Ku * s.pLP * mss * s.pRM * fa * (dvn - (rho_i + rho_j) * s.pv_j / rho_j);
+  } else if (b <= NDIM) {
+    PEL -= Ku * s.pRM * mss * s.pLP * fa * (rho_i + rho_j) * s.UN[b - 1] / rho_i;
+    PER += Ku * s.pLP * mss * s.pRM * fa * (rho_i + rho_j) * s.UN[b - 1] / rho_j;
+  }
+  c.PDL = s.pLP * Si[b] + s.p_i * PPL - PEL;
+  c.PDR = s.pRM * Sj[b] + s.p_j * PPR - PER;
+  return c;
+}
+
+// Jacobian entry (a, b) of Jac_i (left) and Jac_j (right), accumulation order of :295-374.
+template <int NDIM>
+__device__ __host__ inline void ausm_jac_entry(const AusmEdge& s, const AusmCol& c, double phia_i, double phia_j,
+                                               double Sib, double Sjb, int a, int b, double* ji, double* jj) {
+  double vi = 0.0, vj = 0.0;
+  vi += s.mss * ((c.PlL * s.rho_i * phia_i) + (c.MiL * s.rho_j * phia_j));
+  vj += s.mss * ((c.PlR * s.rho_i * phia_i) + (c.MiR * s.rho_j * phia_j));
+  if (a == b) {
+    vi += s.mss * s.mLF;
+    vj += s.mss * s.mRF;
+  }
+  if (a == NDIM + 1) {
+    vi += s.mss * s.mLF * Sib;
+    vj += s.mss * s.mRF * Sjb;
+  }
+  if (a >= 1 && a <= NDIM) {
+    vi += s.UN[a - 1] * c.PDL;
+    vj += s.UN[a - 1] * c.PDR;
+  }
+  *ji = vi * s.Area;
+  *jj = vj * s.Area;
+}
+
+}  // namespace rx

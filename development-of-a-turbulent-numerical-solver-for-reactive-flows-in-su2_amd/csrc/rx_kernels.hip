@@ -1,0 +1,691 @@
+// rx_kernels.hip — residual-side kernels of the reactive-RANS hot path for gfx950.
+//
+// Determinism: every per-node accumulation is a gather over the node's incident edges in
+// increasing edge id, which is exactly the order the reference's sequential edge loop applies
+// its scatters (LinSysRes.AddBlock(i) / SubtractBlock(j), solver_direct_reactive.cpp:2759-2772,
+// 5374-5381). No atomics: results are bitwise reproducible run to run.
+#include <hip/hip_runtime.h>
+
+#include "rx_chem.h"
+#include "rx_ctx.h"
+#include "rx_visc.h"
+
+using namespace rx;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ inline void set_err(int* err, int code, int64_t idx) {
+  if (atomicCAS(err, 0, code) == 0) err[1] = (int)idx;
+}
+
+// ------------------------------------------------------------------------------------------------
+// a1/a2 explicit: node-centric AUSM gather. Each node recomputes the flux of its incident edges
+// (with the edge's own node order, so both endpoints see bitwise-identical fluxes) and applies
+// +F (first node) / -F (second node) in edge order.
+// ------------------------------------------------------------------------------------------------
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) void k_ausm_node(int N, const int32_t* __restrict__ adj_ptr,
+                                                      const int32_t* __restrict__ adj,
+                                                      const int32_t* __restrict__ edges,
+                                                      const double* __restrict__ normal, const double* __restrict__ V,
+                                                      double mInfty, double* __restrict__ R, int* err) {
+  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double acc[nVar];
+#pragma unroll
+  for (int v = 0; v < nVar; ++v) acc[v] = R[(size_t)i * nVar + v];
+  double Vs[nPV], Vo[nPV];
+#pragma unroll
+  for (int v = 0; v < nPV; ++v) Vs[v] = V[(size_t)i * nPV + v];
+  const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  bool bad = false;
+  for (int k = k0; k < k1; ++k) {
+    const int a = adj[k];
+    const int e = a >> 1;
+    const int side = a & 1;
+    const int other = edges[2 * e + (side ^ 1)];
+#pragma unroll
+    for (int v = 0; v < nPV; ++v) Vo[v] = V[(size_t)other * nPV + v];
+    double nrm[NDIM];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
+    const double* V0 = side ? Vo : Vs;
+    const double* V1 = side ? Vs : Vo;
+    AusmEdge s;
+    ausm_scalars<NDIM>(V0, V1, nrm, mInfty, s);
+#pragma unroll
+    for (int v = 0; v < nVar; ++v) {
+      const double r = ausm_res<NDIM>(s, V0, V1, v);
+      bad |= isnan(r);
+      acc[v] = side ? acc[v] - r : acc[v] + r;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < nVar; ++v) R[(size_t)i * nVar + v] = acc[v];
+  if (bad) set_err(err, ERR_NAN, i);
+}
+
+// a1 implicit: edge-parallel flux + both Jacobians into per-edge scratch.
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) void k_ausm_edge(int E, const int32_t* __restrict__ edges,
+                                                      const double* __restrict__ normal, const double* __restrict__ V,
+                                                      const double* __restrict__ dPdU, double mInfty,
+                                                      double* __restrict__ F, double* __restrict__ Jac, int* err) {
+  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nVar2 = nVar * nVar;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+  double Vi[nPV], Vj[nPV], Si[nVar], Sj[nVar];
+#pragma unroll
+  for (int v = 0; v < nPV; ++v) {
+    Vi[v] = V[(size_t)n0 * nPV + v];
+    Vj[v] = V[(size_t)n1 * nPV + v];
+  }
+#pragma unroll
+  for (int v = 0; v < nVar; ++v) {
+    Si[v] = dPdU[(size_t)n0 * nVar + v];
+    Sj[v] = dPdU[(size_t)n1 * nVar + v];
+  }
+  double nrm[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
+  AusmEdge s;
+  ausm_scalars<NDIM>(Vi, Vj, nrm, mInfty, s);
+  bool bad = false;
+#pragma unroll
+  for (int v = 0; v < nVar; ++v) {
+    const double r = ausm_res<NDIM>(s, Vi, Vj, v);
+    bad |= isnan(r);
+    F[(size_t)e * nVar + v] = r;
+  }
+  double* Ji = Jac + (size_t)e * 2 * nVar2;
+  double* Jj = Ji + nVar2;
+  for (int b = 0; b < nVar; ++b) {
+    const AusmCol c = ausm_col<NDIM>(s, Si, Sj, b);
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) {
+      double ji, jj;
+      ausm_jac_entry<NDIM>(s, c, ausm_phi<NDIM>(Vi, Vi[NDIM + 3], a), ausm_phi<NDIM>(Vj, Vj[NDIM + 3], a), Si[b],
+                           Sj[b], a, b, &ji, &jj);
+      bad |= isnan(ji) || isnan(jj);
+      Ji[a * nVar + b] = ji;
+      Jj[a * nVar + b] = jj;
+    }
+  }
+  if (bad) set_err(err, ERR_NAN, e);
+}
+
+// a3-a6: viscous flux (+ Jacobians) per edge into scratch.
+template <int NS, int NDIM>
+__global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restrict__ edges,
+                                                  const double* __restrict__ normal, const double* __restrict__ coord,
+                                                  const double* __restrict__ V, const double* __restrict__ G,
+                                                  const double* __restrict__ mu, const double* __restrict__ kappa,
+                                                  const double* __restrict__ Dij, const double* __restrict__ dTdU,
+                                                  const double* __restrict__ tke, const double* __restrict__ mut,
+                                                  const double* __restrict__ sigk, const double* __restrict__ gk,
+                                                  DevMech m, ViscParams P, double* __restrict__ F,
+                                                  double* __restrict__ Jac, int* err) {
+  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nG = NS + NDIM + 2, nVar2 = nVar * nVar;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+  ViscNode<NS, NDIM> a, b;
+  a.V = V + (size_t)n0 * nPV;
+  b.V = V + (size_t)n1 * nPV;
+  a.G = G + (size_t)n0 * nG * NDIM;
+  b.G = G + (size_t)n1 * nG * NDIM;
+  a.Dij = Dij + (size_t)n0 * NS * NS;
+  b.Dij = Dij + (size_t)n1 * NS * NS;
+  a.S = P.implicit ? dTdU + (size_t)n0 * nVar : nullptr;
+  b.S = P.implicit ? dTdU + (size_t)n1 * nVar : nullptr;
+  a.coord = coord + (size_t)n0 * NDIM;
+  b.coord = coord + (size_t)n1 * NDIM;
+  a.mu = mu[n0];
+  b.mu = mu[n1];
+  a.kappa = kappa[n0];
+  b.kappa = kappa[n1];
+  double sk = 1.0;
+  if (P.rans) {
+    a.tke = tke[n0];
+    b.tke = tke[n1];
+    a.mut = mut[n0];
+    b.mut = mut[n1];
+    a.gk = gk + (size_t)n0 * NDIM;
+    b.gk = gk + (size_t)n1 * NDIM;
+    sk = sigk[n0];  // Set_Sigmak(node i), solver_direct_reactive.cpp:5345
+  } else {
+    a.tke = b.tke = a.mut = b.mut = 0.0;
+    a.gk = b.gk = nullptr;
+  }
+  double nrm[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
+  double res[nVar];
+  double* Ji = P.implicit ? Jac + (size_t)e * 2 * nVar2 : nullptr;
+  double* Jj = P.implicit ? Ji + nVar2 : nullptr;
+  const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, Ji, Jj);
+  bool bad = false;
+#pragma unroll
+  for (int v = 0; v < nVar; ++v) {
+    bad |= isnan(res[v]);
+    F[(size_t)e * nVar + v] = res[v];
+  }
+  if (rc != ERR_NONE) set_err(err, rc == ERR_RANGE ? ERR_RANGE : ERR_NAN, e);
+  else if (bad) set_err(err, ERR_NAN, e);
+}
+
+// Generic node gather of an edge flux array: node0 += sign*F, node1 -= sign*F (edge order).
+__global__ __launch_bounds__(kBlock) void k_gather_flux(int N, int nVar, const int32_t* __restrict__ adj_ptr,
+                                                        const int32_t* __restrict__ adj, const double* __restrict__ F,
+                                                        double sign_first, double* __restrict__ R) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * nVar) return;
+  const int i = t / nVar, v = t - i * nVar;
+  double acc = R[t];
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k];
+    const double f = F[(size_t)(a >> 1) * nVar + v];
+    // node0: acc (+/-) f ; node1: the opposite sign (R[j] -= F for conv, += F for visc)
+    const bool plus = ((a & 1) == 0) == (sign_first > 0.0);
+    acc = plus ? acc + f : acc - f;
+  }
+  R[t] = acc;
+}
+
+// a9: PaSR source per cell: R[i] += S; implicit: cell Jacobian into scratch.
+template <int NS, int NDIM>
+__global__ __launch_bounds__(128) void k_source(int N, const double* __restrict__ V, const double* __restrict__ dTdU,
+                                                const double* __restrict__ vol, const double* __restrict__ omega,
+                                                DevMech m, SourceParams P, double* __restrict__ R, int add,
+                                                double* __restrict__ Js, int* err) {
+  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double Vl[nPV];
+#pragma unroll
+  for (int v = 0; v < nPV; ++v) Vl[v] = V[(size_t)i * nPV + v];
+  double res[nVar];
+  const int rc = source_cell<NS, NDIM>(m, P, Vl, P.implicit ? dTdU + (size_t)i * nVar : nullptr, vol[i],
+                                       P.rans ? omega[i] : 0.0, res,
+                                       P.implicit ? Js + (size_t)i * nVar * nVar : nullptr);
+  bool bad = false;
+#pragma unroll
+  for (int v = 0; v < nVar; ++v) {
+    bad |= isnan(res[v]);
+    if (add) R[(size_t)i * nVar + v] += res[v];
+    else R[(size_t)i * nVar + v] = res[v];
+  }
+  if (rc != ERR_NONE) set_err(err, ERR_RANGE, i);
+  else if (bad) set_err(err, ERR_NAN, i);
+}
+
+// Implicit assembly: one thread per (node i, block row a). Residual component a and block row a
+// of every block in BSR row i, in the reference's accumulation order:
+//   R  = 0 + conv(edge order) - visc(edge order) + source
+//   Aii = 0 + conv(edge order) + visc(edge order) + source     (AddVal2Diag comes later)
+//   A(n0,n1) = (0 + Jc_j) - Jv_j ;  A(n1,n0) = (0 - Jc_i) + Jv_i
+template <int NVAR>
+__global__ __launch_bounds__(kBlock) void k_assemble(int N, const int32_t* __restrict__ adj_ptr,
+                                                     const int32_t* __restrict__ adj,
+                                                     const int64_t* __restrict__ adj_blk,
+                                                     const int64_t* __restrict__ diag, const double* __restrict__ Fc,
+                                                     const double* __restrict__ Fv, const double* __restrict__ Jc,
+                                                     const double* __restrict__ Jv, const double* __restrict__ Js,
+                                                     const double* __restrict__ Rsrc, double* __restrict__ R,
+                                                     double* __restrict__ A, int visc, int src) {
+  constexpr int nVar2 = NVAR * NVAR;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * NVAR) return;
+  const int i = t / NVAR, a = t - i * NVAR;
+  double r = 0.0;
+  double D[NVAR];
+#pragma unroll
+  for (int b = 0; b < NVAR; ++b) D[b] = 0.0;
+  const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  for (int k = k0; k < k1; ++k) {
+    const int ad = adj[k];
+    const size_t e = (size_t)(ad >> 1);
+    const int side = ad & 1;
+    const double f = Fc[e * NVAR + a];
+    r = side ? r - f : r + f;
+    const double* jd = Jc + (e * 2 + side) * nVar2 + (size_t)a * NVAR;       // own-side block: Ji for n0, Jj for n1
+    const double* jo = Jc + (e * 2 + (side ^ 1)) * nVar2 + (size_t)a * NVAR; // other-side block
+    double* off = A + adj_blk[k] * nVar2 + (size_t)a * NVAR;
+#pragma unroll
+    for (int b = 0; b < NVAR; ++b) {
+      D[b] = side ? D[b] - jd[b] : D[b] + jd[b];
+      off[b] = side ? 0.0 - jo[b] : 0.0 + jo[b];
+    }
+  }
+  if (visc) {
+    for (int k = k0; k < k1; ++k) {
+      const int ad = adj[k];
+      const size_t e = (size_t)(ad >> 1);
+      const int side = ad & 1;
+      const double f = Fv[e * NVAR + a];
+      r = side ? r + f : r - f;
+      const double* jd = Jv + (e * 2 + side) * nVar2 + (size_t)a * NVAR;
+      const double* jo = Jv + (e * 2 + (side ^ 1)) * nVar2 + (size_t)a * NVAR;
+      double* off = A + adj_blk[k] * nVar2 + (size_t)a * NVAR;
+#pragma unroll
+      for (int b = 0; b < NVAR; ++b) {
+        D[b] = side ? D[b] + jd[b] : D[b] - jd[b];
+        off[b] = side ? off[b] + jo[b] : off[b] - jo[b];
+      }
+    }
+  }
+  if (src) {
+    r += Rsrc[(size_t)i * NVAR + a];
+    const double* js = Js + (size_t)i * nVar2 + (size_t)a * NVAR;
+#pragma unroll
+    for (int b = 0; b < NVAR; ++b) D[b] += js[b];
+  }
+  R[(size_t)i * NVAR + a] = r;
+  double* dd = A + diag[i] * nVar2 + (size_t)a * NVAR;
+#pragma unroll
+  for (int b = 0; b < NVAR; ++b) dd[b] = D[b];
+}
+
+// a12: weighted least-squares gradient of (T, u, v, P, X_s) per node.
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) void k_grad_lsq(int N, const int32_t* __restrict__ nptr,
+                                                     const int32_t* __restrict__ nbr, const double* __restrict__ coord,
+                                                     const double* __restrict__ V, DevMech m, double* __restrict__ Gout) {
+  constexpr int nPV = NS + NDIM + 5, nG = NS + NDIM + 2, P_P = NDIM + 1, RHOS_P = NDIM + 5, P_G = NDIM + 1,
+                RHOS_G = NDIM + 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double pi[nG], pj[nG], C[nG][NDIM];
+  {
+    const double* v = V + (size_t)i * nPV;
+    pi[0] = v[0];
+    pi[P_G] = v[P_P];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) pi[1 + d] = v[1 + d];
+    double ys[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ys[s] = v[RHOS_P + s];
+    molar_from_mass<NS>(m, ys, pi + RHOS_G);
+  }
+#pragma unroll
+  for (int g = 0; g < nG; ++g)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) C[g][d] = 0.0;
+  double r11 = 0, r12 = 0, r13 = 0, r22 = 0, r23 = 0, r23_a = 0, r23_b = 0, r33 = 0;
+  double ci[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) ci[d] = coord[(size_t)i * NDIM + d];
+  for (int k = nptr[i]; k < nptr[i + 1]; ++k) {
+    const int j = nbr[k];
+    const double* v = V + (size_t)j * nPV;
+    pj[0] = v[0];
+    pj[P_G] = v[P_P];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) pj[1 + d] = v[1 + d];
+    double ys[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ys[s] = v[RHOS_P + s];
+    molar_from_mass<NS>(m, ys, pj + RHOS_G);
+    double cij[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) cij[d] = coord[(size_t)j * NDIM + d] - ci[d];
+    double w = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) w += cij[d] * cij[d];
+    if (w > kEPS) {
+      r11 += cij[0] * cij[0] / w;
+      r12 += cij[0] * cij[1] / w;
+      r22 += cij[1] * cij[1] / w;
+      if (NDIM == 3) {
+        r13 += cij[0] * cij[2] / w;
+        r23_a += cij[1] * cij[2] / w;
+        r23_b += cij[0] * cij[2] / w;
+        r33 += cij[2] * cij[2] / w;
+      }
+#pragma unroll
+      for (int g = 0; g < nG; ++g)
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) C[g][d] += cij[d] * (pj[g] - pi[g]) / w;
+    }
+  }
+  r11 = (r11 > kEPS) ? sqrt(r11) : 0.0;
+  r12 = (fabs(r11) > kEPS) ? r12 / r11 : 0.0;
+  r22 = (r22 - r12 * r12 > kEPS) ? sqrt(r22 - r12 * r12) : 0.0;
+  if (NDIM == 3) {
+    r13 = (fabs(r11) > kEPS) ? r13 / r11 : 0.0;
+    r23 = (fabs(r22) > kEPS && fabs(r11 * r22) > kEPS) ? r23_a / r22 - r23_b * r12 / (r11 * r22) : 0.0;
+    r33 = (r33 - r23 * r23 - r13 * r13 > kEPS) ? sqrt(r33 - r23 * r23 - r13 * r13) : 0.0;
+  }
+  double detR2 = (NDIM == 2) ? (r11 * r22) * (r11 * r22) : (r11 * r22 * r33) * (r11 * r22 * r33);
+  bool singular = false;
+  if (fabs(detR2) < kEPS) {
+    detR2 = 1.0;
+    singular = true;
+  }
+  double S[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+  if (!singular) {
+    if (NDIM == 2) {
+      S[0][0] = (r12 * r12 + r22 * r22) / detR2;
+      S[0][1] = -r11 * r12 / detR2;
+      S[1][0] = S[0][1];
+      S[1][1] = r11 * r11 / detR2;
+    } else {
+      const double z11 = r22 * r33, z12 = -r12 * r33, z13 = r12 * r23 - r13 * r22;
+      const double z22 = r11 * r33, z23 = -r11 * r23, z33 = r11 * r22;
+      S[0][0] = (z11 * z11 + z12 * z12 + z13 * z13) / detR2;
+      S[0][1] = (z12 * z22 + z13 * z23) / detR2;
+      S[0][2] = (z13 * z33) / detR2;
+      S[1][0] = S[0][1];
+      S[1][1] = (z22 * z22 + z23 * z23) / detR2;
+      S[1][2] = (z23 * z33) / detR2;
+      S[2][0] = S[0][2];
+      S[2][1] = S[1][2];
+      S[2][2] = (z33 * z33) / detR2;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < nG; ++g)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+      double r = 0.0;
+#pragma unroll
+      for (int e = 0; e < NDIM; ++e) r += C[g][e] * S[d][e];
+      Gout[((size_t)i * nG + g) * NDIM + d] = r;
+    }
+}
+
+// a13: Venkatakrishnan limiter, node-centric (min over incident edges is order independent).
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_limiter_minmax(int N, int nPV, const int32_t* __restrict__ adj_ptr,
+                                                           const int32_t* __restrict__ adj,
+                                                           const int32_t* __restrict__ edges,
+                                                           const double* __restrict__ V, double* __restrict__ mn,
+                                                           double* __restrict__ mx) {
+  constexpr int nL = NDIM + 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double lo[nL], hi[nL];
+#pragma unroll
+  for (int v = 0; v < nL; ++v) {
+    lo[v] = kEPS;
+    hi[v] = -kEPS;
+  }
+  auto pl = [&](int p, int v) {
+    const double* pv = V + (size_t)p * nPV;
+    return v == 0 ? pv[0] : (v == nL - 1 ? pv[NDIM + 1] : pv[v]);
+  };
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k];
+    const int e = a >> 1, side = a & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+#pragma unroll
+    for (int v = 0; v < nL; ++v) {
+      const double du = pl(n1, v) - pl(n0, v);
+      const double d = side ? -du : du;
+      lo[v] = fmin(lo[v], d);
+      hi[v] = fmax(hi[v], d);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < nL; ++v) {
+    mn[(size_t)i * nL + v] = lo[v];
+    mx[(size_t)i * nL + v] = hi[v];
+  }
+}
+
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_limiter_venkat(int N, int nG, const int32_t* __restrict__ adj_ptr,
+                                                           const int32_t* __restrict__ adj,
+                                                           const int32_t* __restrict__ edges,
+                                                           const double* __restrict__ coord,
+                                                           const double* __restrict__ G, const double* __restrict__ mn,
+                                                           const double* __restrict__ mx, double eps2,
+                                                           double* __restrict__ lim) {
+  constexpr int nL = NDIM + 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double l[nL];
+#pragma unroll
+  for (int v = 0; v < nL; ++v) l[v] = 2.0;
+  double ci[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) ci[d] = coord[(size_t)i * NDIM + d];
+  const double* Gi = G + (size_t)i * nG * NDIM;
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k];
+    const int e = a >> 1, side = a & 1;
+    const int other = edges[2 * e + (side ^ 1)];
+#pragma unroll
+    for (int v = 0; v < nL; ++v) {
+      double dm = 0.0;
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) dm += 0.5 * (coord[(size_t)other * NDIM + d] - ci[d]) * Gi[v * NDIM + d];
+      const double dp = (dm > 0.0) ? mx[(size_t)i * nL + v] : mn[(size_t)i * nL + v];
+      const double lv = (dp * dp + 2.0 * dp * dm + eps2) / (dp * dp + dp * dm + 2.0 * dm * dm + eps2);
+      if (lv < l[v]) l[v] = lv;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < nL; ++v) lim[(size_t)i * nL + v] = l[v];
+}
+
+// a18: SetTime_Step (RANS branch), node-centric over incident edges then boundary vertices.
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_time_step(int N, int nPV, int nVar, const int32_t* __restrict__ adj_ptr,
+                                                      const int32_t* __restrict__ adj,
+                                                      const int32_t* __restrict__ edges,
+                                                      const double* __restrict__ normal,
+                                                      const int32_t* __restrict__ bv_ptr,
+                                                      const double* __restrict__ bv_normal,
+                                                      const double* __restrict__ V, const double* __restrict__ dPdU,
+                                                      const double* __restrict__ mu, const double* __restrict__ eddy,
+                                                      const double* __restrict__ vol,
+                                                      const int32_t* __restrict__ nptr, double CFL, double maxdt,
+                                                      double Pr_l, double Pr_t, double* __restrict__ dt,
+                                                      double* __restrict__ li_out, double* __restrict__ lv_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int RHO_P = NDIM + 2, A_P = NDIM + 4, RHOE_S = NDIM + 1;
+  double li = 0.0, lv = 0.0;
+  auto pvel = [&](int p, const double* n) {
+    double s = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) s += V[(size_t)p * nPV + 1 + d] * n[d];
+    return s;
+  };
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int e = adj[k] >> 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    double n[NDIM];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) n[d] = normal[(size_t)e * NDIM + d];
+    double Area = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) Area += n[d] * n[d];
+    Area = sqrt(Area);
+    const double pv = 0.5 * (pvel(n0, n) + pvel(n1, n));
+    const double a = 0.5 * (V[(size_t)n0 * nPV + A_P] + V[(size_t)n1 * nPV + A_P]);
+    const double rho = 0.5 * (V[(size_t)n0 * nPV + RHO_P] + V[(size_t)n1 * nPV + RHO_P]);
+    const double m = 0.5 * (mu[n0] + mu[n1]);
+    li += (fabs(pv) + a) * Area;
+    const double mt = 0.5 * (eddy[n0] + eddy[n1]);
+    const double gam = dPdU[(size_t)n0 * nVar + RHOE_S] + 1;
+    const double l1 = 4.0 / 3.0 * (m + mt);
+    const double l2 = (1.0 + (Pr_l / Pr_t) * (mt / m)) * (gam * m / Pr_l);
+    lv += (l1 + l2) * Area * Area / rho;
+  }
+  for (int b = bv_ptr[i]; b < bv_ptr[i + 1]; ++b) {
+    double n[NDIM];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) n[d] = bv_normal[(size_t)b * NDIM + d];
+    double Area = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) Area += n[d] * n[d];
+    Area = sqrt(Area);
+    const double pv = pvel(i, n);
+    li += (fabs(pv) + V[(size_t)i * nPV + A_P]) * Area;
+    const double m = mu[i], mt = eddy[i];
+    const double gam = dPdU[(size_t)i * nVar + RHOE_S] + 1;
+    const double l1 = (4.0 / 3.0) * (m + mt);
+    const double l2 = (1.0 + (Pr_l / Pr_t) * (mt / m)) * (gam * m / Pr_l);
+    lv += (l1 + l2) * Area * Area / V[(size_t)i * nPV + RHO_P];
+  }
+  li_out[i] = li;
+  lv_out[i] = lv;
+  double d = 0.0;
+  if (vol[i] > kEPS) {
+    d = CFL * vol[i] / li;
+    const double dv = CFL * 0.25 * vol[i] * vol[i] / lv;
+    d = fmin(d, dv);
+    if (d > maxdt) d = maxdt;
+  }
+  dt[i] = d;
+  // points with a single neighbour take the global minimum (rare; fixed up on the host path)
+  (void)nptr;
+}
+
+inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
+
+#define RX_NS_SWITCH(ns, CALL)                                 \
+  switch (ns) {                                                \
+    case 3: { constexpr int NS_ = 3; CALL; } break;            \
+    case 4: { constexpr int NS_ = 4; CALL; } break;            \
+    case 7: { constexpr int NS_ = 7; CALL; } break;            \
+    case 9: { constexpr int NS_ = 9; CALL; } break;            \
+    default: return RX_ERR_ARG;                                \
+  }
+
+}  // namespace
+
+int rx_fail_hip(rx_ctx* ctx, hipError_t e) {
+  (void)ctx;
+  (void)e;
+  return RX_ERR_HIP;
+}
+
+int rx_check_error(rx_ctx* ctx) {
+  int h[2] = {0, 0};
+  RX_HIP(hipMemcpyAsync(h, ctx->err, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  RX_HIP(hipStreamSynchronize(ctx->stream));
+  if (h[0] != 0) {
+    ctx->last_err_index = h[1];
+    RX_HIP(hipMemsetAsync(ctx->err, 0, 2 * sizeof(int), ctx->stream));
+    return h[0] == ERR_RANGE ? RX_ERR_RANGE : RX_ERR_NAN;
+  }
+  return RX_OK;
+}
+
+int rx_launch_ausm_node(rx_ctx* ctx) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  RX_NS_SWITCH(ctx->ns, (k_ausm_node<NS_, 2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+                            (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->f[RX_F_V],
+                            ctx->cfg.mach_inf, ctx->f[RX_F_RES], ctx->err)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_ausm_edge(rx_ctx* ctx) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  RX_NS_SWITCH(ctx->ns, (k_ausm_edge<NS_, 2><<<blocks(ctx->E), kBlock, 0, ctx->stream>>>(
+                            (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
+                            ctx->cfg.mach_inf, ctx->fconv, ctx->jconv, ctx->err)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_visc_edge(rx_ctx* ctx) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
+               ctx->cfg.rans, ctx->cfg.implicit};
+  RX_NS_SWITCH(ctx->ns, (k_visc_edge<NS_, 2><<<blocks(ctx->E, 64), 64, 0, ctx->stream>>>(
+                            (int)ctx->E, ctx->edges, ctx->normal, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_GRAD],
+                            ctx->f[RX_F_MU], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_DTDU],
+                            ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_SIGMAK], ctx->f[RX_F_GRADK], ctx->mech,
+                            P, ctx->fvisc, ctx->jvisc, ctx->err)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first) {
+  k_gather_flux<<<blocks(ctx->N * ctx->nVar), kBlock, 0, ctx->stream>>>(
+      (int)ctx->N, ctx->nVar, ctx->adj_ptr, ctx->adj, flux, sign_first, ctx->f[RX_F_RES]);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_source(rx_ctx* ctx) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  SourceParams P{ctx->cfg.c_mu, ctx->cfg.pasr_lb, ctx->cfg.rho_ref, ctx->cfg.t_ref, ctx->cfg.T_ref, ctx->cfg.rans,
+                 ctx->cfg.implicit};
+  // explicit: R += S directly; implicit: S and its Jacobian go to scratch, folded in by k_assemble
+  double* Rdst = ctx->cfg.implicit ? ctx->rsrc : ctx->f[RX_F_RES];
+  const int add = ctx->cfg.implicit ? 0 : 1;
+  RX_NS_SWITCH(ctx->ns, (k_source<NS_, 2><<<blocks(ctx->N, 128), 128, 0, ctx->stream>>>(
+                            (int)ctx->N, ctx->f[RX_F_V], ctx->f[RX_F_DTDU], ctx->vol, ctx->f[RX_F_OMEGA], ctx->mech,
+                            P, Rdst, add, ctx->jsrc, ctx->err)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
+  const int nv = ctx->nVar;
+  const int nb = blocks(ctx->N * nv);
+  switch (nv) {
+#define RX_ASM(NV)                                                                                          \
+  case NV:                                                                                                  \
+    k_assemble<NV><<<nb, kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk,        \
+                                                   ctx->diag, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, \
+                                                   ctx->jsrc, ctx->rsrc, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], \
+                                                   with_visc, with_src);                                      \
+    break;
+    RX_ASM(7)
+    RX_ASM(8)
+    RX_ASM(11)
+    RX_ASM(13)
+#undef RX_ASM
+    default:
+      return RX_ERR_ARG;
+  }
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_grad(rx_ctx* ctx) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  RX_NS_SWITCH(ctx->ns, (k_grad_lsq<NS_, 2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+                            (int)ctx->N, ctx->nbr_ptr, ctx->nbr, ctx->coord, ctx->f[RX_F_V], ctx->mech,
+                            ctx->f[RX_F_GRAD])));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_limiter(rx_ctx* ctx) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  k_limiter_minmax<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nPV, ctx->adj_ptr, ctx->adj,
+                                                                  ctx->edges, ctx->f[RX_F_V], ctx->lim_mn,
+                                                                  ctx->lim_mx);
+  RX_HIP(hipGetLastError());
+  const double eps1 = ctx->cfg.limiter_coeff * ctx->cfg.ref_elem_length;
+  const double eps2 = eps1 * eps1 * eps1;
+  k_limiter_venkat<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->adj_ptr, ctx->adj,
+                                                                  ctx->edges, ctx->coord, ctx->f[RX_F_GRAD],
+                                                                  ctx->lim_mn, ctx->lim_mx, eps2,
+                                                                  ctx->f[RX_F_LIMITER]);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_launch_time_step(rx_ctx* ctx) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  k_time_step<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+      (int)ctx->N, ctx->nPV, ctx->nVar, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->bv_ptr, ctx->bv_normal,
+      ctx->f[RX_F_V], ctx->f[RX_F_DPDU], ctx->f[RX_F_MU], ctx->f[RX_F_EDDY], ctx->vol, ctx->nbr_ptr, ctx->cfg.cfl,
+      ctx->cfg.max_delta_time, ctx->cfg.prandtl_lam, ctx->cfg.prandtl_turb, ctx->f[RX_F_DT], ctx->f[RX_F_LAMBDA_INV],
+      ctx->f[RX_F_LAMBDA_VISC]);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}

@@ -100,10 +100,8 @@ def median_dual(pts, quads, bnd):
     contrib = np.stack([d[:, 1], -d[:, 0]], axis=1)
     flip = faces[:, 0] > faces[:, 1]
     contrib[flip] *= -1.0
-    # orientation: the reference takes the element CG on the left of the oriented face; our quads
-    # are counter-clockwise, so the centroid is on the left of (face0 -> face1)
     normal = np.zeros((len(edges), 2))
-    np.add.at(normal, inv, -contrib)
+    np.add.at(normal, inv, contrib)
     # dual volumes: triangles (point, edge midpoint, element centroid) on both face ends
     vol = np.zeros(n)
     for end in (0, 1):
@@ -127,7 +125,7 @@ def median_dual(pts, quads, bnd):
         for l in lines:
             p0, p1 = pts[l[0]], pts[l[1]]
             t = p1 - p0
-            half = 0.5 * np.array([t[1], -t[0]])
+            half = 0.5 * np.array([-t[1], t[0]])  # CVertex::SetNodes_Coord, both line ends
             for v in (l[0], l[1]):
                 acc[v] = acc.get(v, 0.0) + half
         for v in sorted(acc):

@@ -1,0 +1,148 @@
+/* rx.h — C ABI of the MI355X reactive-RANS hot path (librx.so).
+ *
+ * Drop-in boundary for the loops the reference runs inside its CSolver overrides. Each entry point
+ * replaces one reference loop / operator (paths relative to the reference root):
+ *
+ *   rx_edge_flux_conv    CReactiveEulerSolver::Upwind_Residual, 1st-order branch
+ *                        SU2_CFD/src/solver_direct_reactive.cpp:2535-2785 with
+ *                        CUpwReactiveAUSM::ComputeResidual SU2_CFD/src/numerics_direct_reactive.cpp:53-378
+ *   rx_edge_flux_visc    CReactiveNSSolver::Viscous_Residual solver_direct_reactive.cpp:5305-5386 with
+ *                        CAvgGradReactive_Flow::ComputeResidual numerics_direct_reactive.cpp:1425-1678
+ *   rx_cell_source_pasr  CReactiveEulerSolver::Source_Residual solver_direct_reactive.cpp:2792-2874 with
+ *                        CSourceReactive::ComputeChemistry numerics_direct_reactive.cpp:1728-1879
+ *   rx_grad_lsq          CReactiveNSSolver::SetPrimitive_Gradient_LS solver_direct_reactive.cpp:4887-5050
+ *   rx_limiter_venkat    CReactiveEulerSolver::SetPrimitive_Limiter solver_direct_reactive.cpp:1328-1523
+ *   rx_time_step         CReactiveNSSolver::SetTime_Step solver_direct_reactive.cpp:5057-5298
+ *   rx_bsr_spmv          CSysMatrix::MatrixVectorProduct Common/src/matrix_structure.cpp:997-1030
+ *   rx_ilu0_build        CSysMatrix::BuildILUPreconditioner matrix_structure.cpp:1368-1451
+ *   rx_ilu0_apply        CSysMatrix::ComputeILUPreconditioner matrix_structure.cpp:1453-1515
+ *   rx_lusgs_apply       CSysMatrix::ComputeLU_SGSPreconditioner matrix_structure.cpp:1673-1709
+ *   rx_fgmres            CSysSolve::FGMRES_LinSolver Common/src/linear_solvers_structure.cpp:309-463
+ *   rx_implicit_euler    CReactiveEulerSolver::ImplicitEuler_Iteration solver_direct_reactive.cpp:2336-2407
+ *   rx_explicit_euler    CReactiveEulerSolver::ExplicitEuler_Iteration solver_direct_reactive.cpp:2414-2449
+ *
+ * Ownership: all device buffers belong to the rx_ctx. Host arrays passed in are copied at the
+ * call; no pointer is retained. Every function returns an rx_status; on RX_ERR_NAN /
+ * RX_ERR_RANGE the index of the first offending edge/cell is available from rx_last_error_index
+ * (reference behaviour: std::runtime_error "NaN found in the ... residual").
+ * Layouts are the reference's (row-major per node):
+ *   V   [N][nPrimVar]  T, u, v, P, rho, h, a, Y_1..Y_Ns   (nPrimVar = Ns + nDim + 5)
+ *   U   [N][nVar]      rho, rho u, rho v, rho E, rho Y_s   (nVar = Ns + nDim + 2)
+ *   grad[N][nPrimVarGrad][nDim]  T, u, v, P, X_1..X_Ns    (nPrimVarGrad = Ns + nDim + 2)
+ *   Dij [N][Ns][Ns], BSR blocks [nnzb][nVar][nVar] row-major, columns sorted per row, diagonal included.
+ */
+#ifndef RX_H
+#define RX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  RX_OK = 0,
+  RX_ERR_ARG = 1,
+  RX_ERR_HIP = 2,
+  RX_ERR_NAN = 3,
+  RX_ERR_RANGE = 4,
+  RX_ERR_NONPHYS = 5,
+  RX_ERR_DIVERGED = 6,
+  RX_ERR_STATE = 7
+} rx_status;
+
+typedef struct rx_ctx rx_ctx;
+
+/* Mechanism + property tables (reacting_model_library.cpp Setup/readers output). Tables are
+ * [5][Ns][nTab] in property order cp, h, s, mu, kappa with the spline second derivatives. */
+typedef struct {
+  int32_t n_species, n_reactions, n_tab;
+  const double *mmass, *diff_vol;
+  const double *stoich_reac, *stoich_prod; /* [Ns][nR] */
+  const double *exp_reac, *exp_prod;       /* [nR][Ns] */
+  const double *A, *beta, *Ta, *A_back, *beta_back, *Ta_back;
+  const int32_t *reversible, *has_backward;
+  const double *tab_x, *tab_y, *tab_y2;
+} rx_mech_desc;
+
+/* Dual grid (CGeometry edges / dual volumes / boundary vertices). Edge order is the reference's
+ * (i < j), normals oriented i -> j. nbr = point neighbour lists in the reference's order. */
+typedef struct {
+  int32_t n_dim;
+  int64_t n_point, n_edge, n_bvert;
+  const int64_t *edges;      /* [E][2] */
+  const double *edge_normal; /* [E][nDim] */
+  const double *coord;       /* [N][nDim] */
+  const double *volume;      /* [N] */
+  const int64_t *nbr_ptr;    /* [N+1] */
+  const int64_t *nbr;        /* [nbr_ptr[N]] */
+  const int64_t *bvert;      /* [nB][2] (marker, point) in marker / vertex order */
+  const double *bvert_normal;/* [nB][nDim] */
+} rx_mesh_desc;
+
+typedef struct {
+  double mach_inf;                               /* CUpwReactiveAUSM mInfty */
+  double T_ref, E_ref, R_ref, rho_ref, t_ref;    /* non-dimensionalisation (all 1 when DIMENSIONAL) */
+  double prandtl_lam, prandtl_turb, lewis_turb;  /* CNumerics / config */
+  double c_mu, pasr_lb;                          /* PaSR closure */
+  double cfl, max_delta_time;                    /* SetTime_Step */
+  double ref_elem_length, limiter_coeff;         /* Venkatakrishnan */
+  double lin_tol, relaxation;                    /* LINEAR_SOLVER_ERROR, RELAXATION_FACTOR_FLOW */
+  int32_t implicit, rans, lin_iter, lin_prec;    /* lin_prec: 0 = LU_SGS, 1 = ILU0 */
+} rx_cfg;
+
+typedef enum {
+  RX_F_U = 0, RX_F_V, RX_F_DPDU, RX_F_DTDU, RX_F_MU, RX_F_KAPPA, RX_F_DIJ, RX_F_GRAD, RX_F_LIMITER,
+  RX_F_TKE, RX_F_OMEGA, RX_F_MUT, RX_F_SIGMAK, RX_F_GRADK, RX_F_EDDY,
+  RX_F_RES,        /* LinSysRes [N][nVar] */
+  RX_F_DT,         /* local time step [N] */
+  RX_F_LAMBDA_INV, RX_F_LAMBDA_VISC,
+  RX_F_JAC,        /* BSR blocks [nnzb][nVar][nVar] */
+  RX_F_ILU,        /* ILU(0) factor, same layout */
+  RX_F_SOL,        /* LinSysSol [N][nVar] */
+  RX_F_RHS,        /* linear-system right-hand side [N][nVar] */
+  RX_F_COUNT
+} rx_field;
+
+int rx_ctx_create(const rx_mesh_desc *mesh, const rx_mech_desc *mech, const rx_cfg *cfg, int device, rx_ctx **out);
+int rx_ctx_destroy(rx_ctx *ctx);
+int rx_field_size(const rx_ctx *ctx, rx_field f, int64_t *count);
+int rx_upload(rx_ctx *ctx, rx_field f, const double *host, int64_t count);
+int rx_download(rx_ctx *ctx, rx_field f, double *host, int64_t count);
+int rx_bsr_pattern(const rx_ctx *ctx, int64_t *row_ptr, int64_t *col); /* host copies, [N+1], [nnzb] */
+int rx_sync(rx_ctx *ctx);
+int64_t rx_last_error_index(const rx_ctx *ctx);
+const char *rx_status_string(int status);
+
+/* Residual / Jacobian phases (Space_Integration order). */
+int rx_residual_zero(rx_ctx *ctx);      /* LinSysRes = 0, Jacobian = 0 (Preprocessing) */
+int rx_edge_flux_conv(rx_ctx *ctx);     /* R[i] += F, R[j] -= F (+ Jacobian blocks) */
+int rx_edge_flux_visc(rx_ctx *ctx);     /* R[i] -= Fv, R[j] += Fv (+ Jacobian blocks) */
+int rx_cell_source_pasr(rx_ctx *ctx);   /* R[i] += S (+ diagonal block) */
+int rx_grad_lsq(rx_ctx *ctx);           /* grad from V */
+int rx_limiter_venkat(rx_ctx *ctx);     /* limiter from V, grad */
+int rx_time_step(rx_ctx *ctx);          /* dt, lambda_inv, lambda_visc */
+
+/* Linear algebra on the context's BSR Jacobian (all on device vectors of the context). */
+int rx_bsr_spmv(rx_ctx *ctx, rx_field x, rx_field y);
+int rx_ilu0_build(rx_ctx *ctx);
+int rx_ilu0_apply(rx_ctx *ctx, rx_field b, rx_field x);
+int rx_lusgs_apply(rx_ctx *ctx, rx_field b, rx_field x);
+int rx_fgmres(rx_ctx *ctx, double tol, int m, int *iters, double *resid); /* solves JAC * SOL = RHS */
+
+/* Time integration (updates RX_F_U). */
+int rx_explicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */);
+int rx_implicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */, int *lin_iters);
+
+/* Per-phase device timing with HIP events on the context stream (for bench roofline). */
+typedef enum {
+  RX_K_CONV = 0, RX_K_VISC, RX_K_SOURCE, RX_K_GRAD, RX_K_LIMITER, RX_K_DT, RX_K_SPMV, RX_K_ILU_BUILD,
+  RX_K_ILU_APPLY, RX_K_LUSGS, RX_K_KRYLOV, RX_K_UPDATE, RX_K_COUNT
+} rx_kernel;
+int rx_profile_enable(rx_ctx *ctx, int on);
+int rx_profile_read(rx_ctx *ctx, rx_kernel k, double *total_ms, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RX_H */
