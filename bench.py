@@ -1,0 +1,201 @@
+"""Throughput of the reactive RANS hot path on MI355X: Mcells*iters/s (BASELINE.json metric).
+
+One step = one outer implicit iteration of the device-resident hot path over the whole mesh
+(the order CIntegration drives them):
+  SetPrimitive_Gradient_LS -> SetTime_Step -> residual zero -> Upwind_Residual (AUSM + Jacobians)
+  -> Viscous_Residual (reactive viscous + SST closure + Jacobians) -> Source_Residual (PaSR + Jacobian)
+  -> ImplicitEuler_Iteration (assembly, Vol/dt, ILU(0) build, FGMRES(5), clipped update, RMS).
+
+Default workload (N=1): BASELINE configs[1] — synthetic 2-D reactive jet, 500x200 = 100k points,
+7 species PaSR + SST, implicit FGMRES+ILU0. `--workload c3` runs configs[2] (2000x500, 1M points).
+Inputs are resident in HBM before the timed region. Data are synthetic: the mesh replicates the
+reference jet geometry, node records are resampled from the reference's converged PaSR jet state
+(tests/golden/jet9w.npz, see synth.py).
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): every rank runs its own copy of the workload
+(weak scaling, no data-path collective yet); timing = max over ranks; value = all ranks' cells.
+
+Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel and `cpu_baseline` from the
+CPU restatement (oracle/) timed on one host core over one step of the same mesh.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+WORKLOADS = {
+    "c1": dict(nx=100, ny=90, ns=4, desc="configs[0]: 2-D jet 100x90, 4 species"),
+    "c2": dict(nx=500, ny=200, ns=7, desc="configs[1]: 2-D reactive jet 500x200 (100k cells), implicit FGMRES+ILU0"),
+    "c3": dict(nx=2000, ny=500, ns=7, desc="configs[2]: 2-D reactive jet 2000x500 (1M cells), 7 species PaSR+SST"),
+}
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFS = 78.6       # MI355X FP64 vector spec
+
+
+def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
+    """Algorithmic bytes per launch (each unique datum once per sweep)."""
+    nVar, nPV, nG = ns + nDim + 2, ns + nDim + 5, ns + nDim + 2
+    d = 8
+    blk = nVar * nVar * d
+    return {
+        # k_ausm_edge: V_i,V_j (nPV), dPdU (nVar) per node once; edge (2 int32 + normal); out flux + 2 Jacobians
+        "CONV": dict(bound="hbm", bytes=N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk)),
+        # k_visc_edge: node record V, grad, mu, kappa, Dij, dTdU, k, mu_t, sigma_k, grad_k, coord
+        "VISC": dict(bound="hbm", bytes=N * (nPV + nG * nDim + 2 + ns * ns + nVar + 3 + nDim + nDim) * d
+                     + E * (8 + nDim * d) + E * (nVar * d + 2 * blk)),
+        "GRAD": dict(bound="hbm", bytes=N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4),
+        "SOURCE": dict(bound="hbm", bytes=N * (nPV + nVar + 2) * d + N * (nVar * d + blk)),
+        "SPMV": dict(bound="hbm", bytes=nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d),
+        "ILU_BUILD": dict(bound="hbm", bytes=2 * nnzb * blk + N * blk),
+        "ILU_APPLY": dict(bound="hbm", bytes=nnzb * blk + N * blk + 3 * N * nVar * d),
+    }
+
+
+def build_workload(nx, ny, ns):
+    from tests.rxpkg import synth
+    mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=ns)
+    return mesh, st, mech, kw
+
+
+def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg):
+    """One implicit step of the CPU restatement (oracle/, one core) on the same mesh."""
+    from oracle import oracle as O
+    om = O.Mechanism(mech_arrays)
+    c = dict(cfl=cfg.cfl, max_delta_time=cfg.max_delta_time, prandtl_lam=cfg.prandtl_lam,
+             prandtl_turb=cfg.prandtl_turb, lewis_turb=cfg.lewis_turb, mach_inf=cfg.mach_inf, c_mu=cfg.c_mu,
+             pasr_lb=cfg.pasr_lb, lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter, relaxation=cfg.relaxation)
+    pattern = O.bsr_pattern(len(st["V"]), mesh["edges"])
+    t0 = time.perf_counter()
+    O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern)
+    dt = time.perf_counter() - t0
+    N = len(st["V"])
+    return dict(value=N / dt / 1e6, unit="Mcells*iters/s", cores=1, kind="port",
+                sample=f"1 implicit step of the same {N}-cell mesh on 1 host core ({dt:.2f} s)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--nx", type=int, default=0)
+    ap.add_argument("--ny", type=int, default=0)
+    ap.add_argument("--species", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from tests.rxpkg import rx
+
+    wl = dict(WORKLOADS[args.workload])
+    nx, ny, ns = args.nx or wl["nx"], args.ny or wl["ny"], args.species or wl["ns"]
+    mesh, st, mech_arrays, kw = build_workload(nx, ny, ns)
+    mech = rx.Mechanism(mech_arrays)
+    cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
+    s = rx.ReactiveNSSolver(mesh, mech, cfg, device=local)
+    s.set_state(st)
+    N, E = s.N, s.E
+    rp, col = s.bsr_pattern()
+    nnzb = int(rp[-1])
+
+    lin_its = []
+
+    def step():
+        s.SetPrimitive_Gradient_LS()
+        s.SetTime_Step()
+        s.Preprocessing_zero()
+        s.Upwind_Residual()
+        s.Viscous_Residual()
+        s.Source_Residual()
+        _, it = s.ImplicitEuler_Iteration()
+        lin_its.append(it)
+
+    for _ in range(args.warmup):
+        step()
+    s.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    s.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    s.sync()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    prof = {k: s.profile_read(k) for k in rx.K}
+    s.profile(False)
+
+    models = kernel_models(N, E, nnzb, ns, 2, 5)
+    phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0}
+    # dominant single-launch kernel among the modelled ones (phase == one kernel launch for these)
+    single = [k for k in ("CONV", "VISC", "GRAD", "SOURCE") if prof[k][1] > 0]
+    dom = max(single, key=lambda k: prof[k][0])
+
+    def roof(k):
+        ms, n = prof[k]
+        avg_s = ms / n / 1e3
+        m = models[k]
+        ach = m["bytes"] / avg_s / 1e9
+        return dict(kernel=k, bound=m["bound"], achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=None, avg_launch_us=round(avg_s * 1e6, 2),
+                    algorithmic_bytes=int(m["bytes"]))
+
+    cells = N * world
+    out = {
+        "metric": "Mcells*iters/s (reactive RANS)",
+        "value": round(cells * args.steps / el / 1e6, 4),
+        "unit": "Mcells*iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (reference jet geometry; node records resampled from the reference PaSR jet state)",
+        "config": {"workload": f"{args.workload}: 2-D reactive jet {nx}x{ny}", "cells_per_gpu": N, "edges": E,
+                   "species": ns, "nVar": ns + 4, "nnz_blocks": nnzb, "time": "EULER_IMPLICIT",
+                   "linear_solver": "FGMRES(5)+ILU0", "parallelism": f"replicas x{world}" if world > 1 else "1 GPU",
+                   "lin_iters_mean": float(np.mean(lin_its[-args.steps:]))},
+        "roofline": roof(dom),
+        "roofline_edge_flux": roof("CONV"),
+        "phase_ms_per_step": {k: round(v, 4) for k, v in phase_ms.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg)
+    else:
+        out["cpu_baseline"] = None
+    s.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -303,7 +303,6 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
   CK(dalloc(ctx, &ctx->err, 2));
   if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), sizeof(double) * (256 * 32 + 1024)) != hipSuccess)
     CK(RX_ERR_HIP);
-  if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) CK(RX_ERR_HIP);
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) CK(RX_ERR_HIP);
 #undef CK
   *out = ctx;
@@ -322,8 +321,8 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   for (void* p : ctx->mech_bufs) dfree(p);
   for (int q = 0; q < RX_F_COUNT; ++q) dfree(ctx->f[q]);
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
-  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  ctx->prof_drain();
+  for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RX_OK;
@@ -497,8 +496,35 @@ int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   return rx_la_implicit_update(ctx, res_rms);
 }
 
+hipEvent_t rx_ctx::prof_event() {
+  if (ev_pool.empty()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  hipEvent_t e = ev_pool.back();
+  ev_pool.pop_back();
+  return e;
+}
+
+void rx_ctx::prof_drain() {
+  if (prof_pending.empty()) return;
+  (void)hipEventSynchronize(prof_pending.back().b);
+  for (const ProfRec& r : prof_pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      prof_ms[r.k] += ms;
+      prof_n[r.k] += 1;
+    }
+    ev_pool.push_back(r.a);
+    ev_pool.push_back(r.b);
+  }
+  prof_pending.clear();
+}
+
 int rx_profile_enable(rx_ctx* ctx, int on) {
   if (!ctx) return RX_ERR_ARG;
+  ctx->prof_drain();
   ctx->prof = on != 0;
   for (int k = 0; k < RX_K_COUNT; ++k) {
     ctx->prof_ms[k] = 0.0;
@@ -509,6 +535,7 @@ int rx_profile_enable(rx_ctx* ctx, int on) {
 
 int rx_profile_read(rx_ctx* ctx, rx_kernel k, double* total_ms, int64_t* launches) {
   if (!ctx || k < 0 || k >= RX_K_COUNT) return RX_ERR_ARG;
+  ctx->prof_drain();
   if (total_ms) *total_ms = ctx->prof_ms[k];
   if (launches) *launches = ctx->prof_n[k];
   return RX_OK;

@@ -73,10 +73,16 @@ struct rx_ctx {
   double* kz = nullptr;      // [(m+1)][N*nVar]
 
   // ---- profiling
+  // Phases record an event pair on the context stream without blocking; pairs are resolved
+  // (elapsed time accumulated per rx_kernel) when rx_profile_read / rx_sync drain the queue.
   bool prof = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  struct ProfRec { hipEvent_t a, b; int k; };
+  std::vector<hipEvent_t> ev_pool;   // free events
+  std::vector<ProfRec> prof_pending;
   double prof_ms[RX_K_COUNT] = {};
   int64_t prof_n[RX_K_COUNT] = {};
+  hipEvent_t prof_event();
+  void prof_drain();
 };
 
 int rx_fail_hip(rx_ctx* ctx, hipError_t e);
@@ -85,17 +91,19 @@ int rx_fail_hip(rx_ctx* ctx, hipError_t e);
 struct RxPhase {
   rx_ctx* c;
   rx_kernel k;
+  hipEvent_t a = nullptr;
   RxPhase(rx_ctx* ctx, rx_kernel kk) : c(ctx), k(kk) {
-    if (c->prof) (void)hipEventRecord(c->ev0, c->stream);
+    if (c->prof) {
+      a = c->prof_event();
+      (void)hipEventRecord(a, c->stream);
+    }
   }
   ~RxPhase() {
-    if (c->prof) {
-      (void)hipEventRecord(c->ev1, c->stream);
-      (void)hipEventSynchronize(c->ev1);
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
-      c->prof_ms[k] += ms;
-      c->prof_n[k] += 1;
+    if (a) {
+      hipEvent_t b = c->prof_event();
+      (void)hipEventRecord(b, c->stream);
+      c->prof_pending.push_back({a, b, (int)k});
+      if (c->prof_pending.size() > 4096) c->prof_drain();
     }
   }
 };

@@ -37,11 +37,46 @@ def load_records(name="jet9w"):
     return g
 
 
-def jet_case(nx, ny, records="jet9w", seed=12345):
-    """Mesh (RCM-ordered median dual) + node records for an nx x ny jet."""
+def species_subset(g, keep, nDim=2):
+    """Restrict records + mechanism to the species indices `keep` (7 species =
+    C4H6, H2O, O2, CO, CO2, H2, O; 4 species = reaction 1 only). Reactions touching a dropped species
+    are removed. The dropped species carry zero mass in the jet records, so the restricted records stay
+    consistent (rho, mixture properties unchanged)."""
+    keep = np.asarray(keep, dtype=np.int64)
+    ns0 = int(g["mech_n_species"])
+    drop = np.setdiff1d(np.arange(ns0), keep)
+    sr, sp = g["mech_stoich_reac"], g["mech_stoich_prod"]
+    rk = np.nonzero(np.all(sr[drop] == 0, axis=0) & np.all(sp[drop] == 0, axis=0))[0]
+    out = dict(g)
+    fl = nDim + 2  # [rho, rho u, rho v, rho E] then species in U / dPdU / dTdU
+    pv = nDim + 5  # [T, u, v, P, rho, h, a] then Y_s in V
+    out["V"] = np.concatenate([g["V"][:, :pv], g["V"][:, pv + keep]], axis=1)
+    for k in ("U", "dPdU", "dTdU"):
+        out[k] = np.concatenate([g[k][:, :fl], g[k][:, fl + keep]], axis=1)
+    out["Dij"] = g["Dij"][:, keep][:, :, keep]
+    for k in ("mmass", "diff_vol", "form_enthalpy", "species"):
+        out["mech_" + k] = g["mech_" + k][keep]
+    for k in ("tab_x", "tab_y", "tab_y2"):
+        out["mech_" + k] = g["mech_" + k][:, keep]
+    out["mech_stoich_reac"] = sr[keep][:, rk]
+    out["mech_stoich_prod"] = sp[keep][:, rk]
+    out["mech_exp_reac"] = g["mech_exp_reac"][rk][:, keep]
+    out["mech_exp_prod"] = g["mech_exp_prod"][rk][:, keep]
+    for k in ("A", "beta", "Ta", "A_back", "beta_back", "Ta_back", "reversible", "has_backward"):
+        out["mech_" + k] = g["mech_" + k][rk]
+    out["mech_n_species"] = np.array(len(keep))
+    out["mech_n_reactions"] = np.array(len(rk))
+    return out
+
+
+def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9):
+    """Mesh (RCM-ordered median dual) + node records for an nx x ny jet with 9 (reference-native), 7
+    or 4 species."""
     mg = _meshgen()
     mesh = mg.build_jet(nx, ny)
     g = load_records(records)
+    if n_species != int(g["mech_n_species"]):
+        g = species_subset(g, np.arange(n_species))
     src = g["coord"]
     lo, hi = src.min(axis=0), src.max(axis=0)
     sn = (src - lo) / np.where(hi > lo, hi - lo, 1.0)

@@ -219,3 +219,64 @@ def time_step(nDim, ns, edges, normal, bverts, bnormal, V, dPdU, mu, eddy, vol, 
                         _p(eddy), _p(vol), _p(nbr_ptr, np.int64), _p(np.asarray(params, dtype=np.float64)),
                         dt.ctypes.data_as(C.c_void_p), li.ctypes.data_as(C.c_void_p), lv.ctypes.data_as(C.c_void_p))
     return dt, li, lv
+
+
+@_keepalive
+def assemble(rp, col, edges, Fc, Jci, Jcj, Fv, Jvi, Jvj, Rs, Js, vol, dt, nb):
+    """Reference-order residual/Jacobian assembly + AddVal2Diag(Vol/dt) + rhs (orc_assemble)."""
+    N, E = len(rp) - 1, len(edges)
+    R = np.zeros(N * nb)
+    A = np.zeros(int(rp[-1]) * nb * nb) if Jci is not None else None
+    rhs = np.zeros(N * nb)
+    lib().orc_assemble(C.c_int64(N), C.c_int64(E), C.c_int(nb), _p(edges, np.int64), _p(rp, np.int64),
+                       _p(col, np.int64), _p(Fc), _p(Jci), _p(Jcj), _p(Fv), _p(Jvi), _p(Jvj), _p(Rs), _p(Js), _p(vol),
+                       _p(dt), R.ctypes.data_as(C.c_void_p), A.ctypes.data_as(C.c_void_p) if A is not None else None,
+                       rhs.ctypes.data_as(C.c_void_p))
+    return R.reshape(N, nb), (A.reshape(-1, nb, nb) if A is not None else None), rhs.reshape(N, nb)
+
+
+@_keepalive
+def update(U, d, nDim, mode, relax, vol, dt):
+    """AddClippedSolution: mode 0 implicit (relax * d), mode 1 explicit (-d * dt / Vol)."""
+    U = np.ascontiguousarray(U, dtype=np.float64).copy()
+    N, nb = U.shape
+    lib().orc_update(C.c_int64(N), C.c_int(nb), C.c_int(nDim), C.c_int(mode), _p(d), C.c_double(relax), _p(vol),
+                     _p(dt), U.ctypes.data_as(C.c_void_p))
+    return U
+
+
+def bsr_pattern(N, edges):
+    """Edge-connected BSR sparsity with the diagonal, columns sorted (CSysMatrix::Initialize)."""
+    e = np.asarray(edges, dtype=np.int64)
+    r = np.r_[np.arange(N), e[:, 0], e[:, 1]]
+    c = np.r_[np.arange(N), e[:, 1], e[:, 0]]
+    o = np.lexsort((c, r))
+    r, c = r[o], c[o]
+    rp = np.zeros(N + 1, dtype=np.int64)
+    np.add.at(rp, r + 1, 1)
+    return np.cumsum(rp), c
+
+
+def implicit_step(mech, nDim, ns, mesh, st, cfg, pattern=None):
+    """One outer iteration of the implicit reactive RANS hot path, restated on the CPU in the order
+    bench.py runs it on the device: LSQ gradient, SetTime_Step, Upwind/Viscous/Source residuals with
+    Jacobians, assembly, ILU(0) build, FGMRES(m) and the clipped relaxed update
+    (solver_direct_reactive.cpp:2336-2407). Returns (U_new, info dict)."""
+    N = len(st["V"])
+    nb = ns + nDim + 2
+    rp, col = pattern if pattern is not None else bsr_pattern(N, mesh["edges"])
+    G = grad_lsq(mech, nDim, np.arange(N), mesh["coord"], st["V"], mesh["nbr_ptr"], mesh["nbr"])
+    dt, _, _ = time_step(nDim, ns, mesh["edges"], mesh["edge_normal"], mesh["bvertex"], mesh["bvertex_normal"],
+                         st["V"], st["dPdU"], st["mu"], st["eddy_visc_flow"], mesh["volume"], mesh["nbr_ptr"],
+                         [cfg["cfl"], cfg["max_delta_time"], cfg["prandtl_lam"], cfg["prandtl_turb"]])
+    rc, Jci, Jcj = ausm_edges(nDim, ns, mesh["edges"], mesh["edge_normal"], st["V"], st["dPdU"], cfg["mach_inf"], True)
+    rv, Jvi, Jvj = visc_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], st["V"], G, st["mu"],
+                              st["kappa"], st["Dij"], st["dTdU"], st["turb_k"], st["mu_t"], st["sigma_k"], st["grad_k"],
+                              True, True, [1, 1, 1, cfg["prandtl_turb"], cfg["lewis_turb"]])
+    rs, Js = source_cells(mech, nDim, st["V"], st["dTdU"], mesh["volume"], st["turb_omega"], True, True,
+                          [cfg["c_mu"], cfg["pasr_lb"], 1, 1, 1])
+    R, A, rhs = assemble(rp, col, mesh["edges"], rc, Jci, Jcj, rv, Jvi, Jvj, rs, Js, mesh["volume"], dt, nb)
+    F = ilu_build(rp, col, A)
+    x, it, res = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"])
+    U = update(st["U"], x, nDim, 0, cfg["relaxation"], mesh["volume"], dt)
+    return U, dict(grad=G, dt=dt, res=R, jac=A, rhs=rhs, sol=x, lin_iters=it, lin_resid=res)

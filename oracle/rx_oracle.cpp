@@ -1676,4 +1676,96 @@ int orc_fgmres(int64_t N, int nb, const int64_t* rp, const int64_t* col, const d
   return i;
 }
 
+static int64_t blk_of(const int64_t* rp, const int64_t* col, int64_t i, int64_t j) {
+  const int64_t* lo = col + rp[i];
+  const int64_t* hi = col + rp[i + 1];
+  const int64_t* p = std::lower_bound(lo, hi, j);
+  return (p != hi && *p == j) ? (p - col) : -1;
+}
+
+// Residual + Jacobian assembly in the reference's loop order: Upwind_Residual scatter
+// (solver_direct_reactive.cpp:2759-2772: R_i += F, R_j -= F; A_ii += Ji, A_ij += Jj, A_ji -= Ji,
+// A_jj -= Jj), Viscous_Residual with the opposite signs (:5374-5381), Source_Residual (R_i += S,
+// A_ii += Js), then ImplicitEuler_Iteration (:2336-2380): A_ii += Vol/dt (or A_ii = I, R_i = 0 when
+// dt <= EPS), rhs = -(R + 0). Any of the Jacobian pointers may be null (explicit assembly of R only).
+void orc_assemble(int64_t N, int64_t E, int nb, const int64_t* edges, const int64_t* rp, const int64_t* col,
+                  const double* Fc, const double* Jci, const double* Jcj, const double* Fv, const double* Jvi,
+                  const double* Jvj, const double* Rs, const double* Js, const double* vol, const double* dt,
+                  double* R, double* A, double* rhs) {
+  const int nb2 = nb * nb;
+  std::fill(R, R + N * nb, 0.0);
+  if (A) std::fill(A, A + rp[N] * nb2, 0.0);
+  auto add = [&](int64_t b, const double* J, double sgn) {
+    double* d = A + b * nb2;
+    if (sgn > 0)
+      for (int q = 0; q < nb2; ++q) d[q] += J[q];
+    else
+      for (int q = 0; q < nb2; ++q) d[q] -= J[q];
+  };
+  for (int pass = 0; pass < 2; ++pass) {
+    const double* F = pass ? Fv : Fc;
+    const double* Ji = pass ? Jvi : Jci;
+    const double* Jj = pass ? Jvj : Jcj;
+    if (!F) continue;
+    const double s = pass ? -1.0 : 1.0;
+    for (int64_t e = 0; e < E; ++e) {
+      const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+      for (int v = 0; v < nb; ++v) {
+        if (s > 0) {
+          R[i * nb + v] += F[e * nb + v];
+          R[j * nb + v] -= F[e * nb + v];
+        } else {
+          R[i * nb + v] -= F[e * nb + v];
+          R[j * nb + v] += F[e * nb + v];
+        }
+      }
+      if (A && Ji) {
+        add(blk_of(rp, col, i, i), Ji + e * nb2, s);
+        add(blk_of(rp, col, i, j), Jj + e * nb2, s);
+        add(blk_of(rp, col, j, i), Ji + e * nb2, -s);
+        add(blk_of(rp, col, j, j), Jj + e * nb2, -s);
+      }
+    }
+  }
+  if (Rs)
+    for (int64_t i = 0; i < N; ++i) {
+      for (int v = 0; v < nb; ++v) R[i * nb + v] += Rs[i * nb + v];
+      if (A && Js) add(blk_of(rp, col, i, i), Js + i * nb2, 1.0);
+    }
+  if (!A) return;
+  for (int64_t i = 0; i < N; ++i) {
+    double* D = A + blk_of(rp, col, i, i) * nb2;
+    if (dt[i] > EPS) {
+      const double delta = vol[i] / dt[i];
+      for (int a = 0; a < nb; ++a) D[a * nb + a] += delta;
+    } else {
+      for (int a = 0; a < nb; ++a)
+        for (int c = 0; c < nb; ++c) D[a * nb + c] = (a == c) ? 1.0 : 0.0;
+      for (int a = 0; a < nb; ++a) R[i * nb + a] = 0.0;
+    }
+    for (int a = 0; a < nb; ++a) rhs[i * nb + a] = -(R[i * nb + a] + 0.0);
+  }
+}
+
+// CReactiveEulerVariable::AddClippedSolution (variable_reactive.hpp) as called by
+// ImplicitEuler_Iteration (:2390-2400, relax * LinSysSol) and ExplicitEuler_Iteration (:2430-2440,
+// -Res * dt / Vol). Lower bound 0 for density/species/… and -1/EPS for momentum/energy, upper 1/EPS.
+void orc_update(int64_t N, int nb, int nDim, int mode, const double* d, double relax, const double* vol,
+                const double* dt, double* U) {
+  for (int64_t i = 0; i < N; ++i)
+    for (int v = 0; v < nb; ++v) {
+      double delta;
+      if (mode == 0) {
+        delta = relax * d[i * nb + v];
+      } else {
+        double Delta = 0.0;
+        if (vol[i] > EPS) Delta = dt[i] / vol[i];
+        delta = -(d[i * nb + v] + 0.0) * Delta;
+      }
+      const double lo = (v >= 1 && v <= nDim + 1) ? -1.0 / EPS : 0.0;
+      const double hi = 1.0 / EPS;
+      U[i * nb + v] = std::fmin(std::fmax(U[i * nb + v] + delta, lo), hi);
+    }
+}
+
 }  // extern "C"
