@@ -32,7 +32,10 @@ def main():
     print("| kernel | calls | total ms | % | avg us | min us | max us |")
     print("|---|---:|---:|---:|---:|---:|---:|")
     for name, n, s, a, mn, mx in rows:
-        short = name.split("(")[0].replace("(anonymous namespace)::", "")
+        short = name.replace("(anonymous namespace)::", "")
+        if short.startswith("void "):
+            short = short[5:]
+        short = short.split("(")[0]
         print(f"| `{short}` | {n} | {s / 1e6:.3f} | {100 * s / tot:.1f} | {a / 1e3:.2f} | {mn / 1e3:.2f} | {mx / 1e3:.2f} |")
 
 
