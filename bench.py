@@ -12,6 +12,10 @@ Inputs are resident in HBM before the timed region. Data are synthetic: the mesh
 reference jet geometry, node records are resampled from the reference's converged PaSR jet state
 (tests/golden/jet9w.npz, see synth.py).
 
+The preconditioner is partitioned like the reference run on `--parts` MPI ranks (RCB partition,
+local RCM per part, ILU(0) per rank; default 256 = one rank per CU); `--parts 1` is the serial
+reference.
+
 Multi-GPU (`torch.distributed.run --nproc-per-node N`): every rank runs its own copy of the workload
 (weak scaling, no data-path collective yet); timing = max over ranks; value = all ranks' cells.
 
@@ -59,9 +63,9 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
     }
 
 
-def build_workload(nx, ny, ns):
+def build_workload(nx, ny, ns, n_part=1):
     from tests.rxpkg import synth
-    mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=ns)
+    mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=ns, n_part=n_part)
     return mesh, st, mech, kw
 
 
@@ -74,7 +78,7 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg):
              pasr_lb=cfg.pasr_lb, lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter, relaxation=cfg.relaxation)
     pattern = O.bsr_pattern(len(st["V"]), mesh["edges"])
     t0 = time.perf_counter()
-    O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern)
+    O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern, part_ptr=mesh.get("part_ptr"))
     dt = time.perf_counter() - t0
     N = len(st["V"])
     return dict(value=N / dt / 1e6, unit="Mcells*iters/s", cores=1, kind="port",
@@ -90,6 +94,8 @@ def main():
     ap.add_argument("--nx", type=int, default=0)
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--species", type=int, default=0)
+    ap.add_argument("--parts", type=int, default=256,
+                    help="partitions (= the reference's MPI ranks) of the ILU(0)/LU-SGS preconditioner")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
     args = ap.parse_args()
@@ -107,7 +113,7 @@ def main():
 
     wl = dict(WORKLOADS[args.workload])
     nx, ny, ns = args.nx or wl["nx"], args.ny or wl["ny"], args.species or wl["ns"]
-    mesh, st, mech_arrays, kw = build_workload(nx, ny, ns)
+    mesh, st, mech_arrays, kw = build_workload(nx, ny, ns, args.parts)
     mech = rx.Mechanism(mech_arrays)
     cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
     s = rx.ReactiveNSSolver(mesh, mech, cfg, device=local)
@@ -180,7 +186,9 @@ def main():
         "data": "synthetic (reference jet geometry; node records resampled from the reference PaSR jet state)",
         "config": {"workload": f"{args.workload}: 2-D reactive jet {nx}x{ny}", "cells_per_gpu": N, "edges": E,
                    "species": ns, "nVar": ns + 4, "nnz_blocks": nnzb, "time": "EULER_IMPLICIT",
-                   "linear_solver": "FGMRES(5)+ILU0", "parallelism": f"replicas x{world}" if world > 1 else "1 GPU",
+                   "linear_solver": "FGMRES(5)+ILU0",
+                   "partitions": args.parts,
+                   "parallelism": f"replicas x{world}" if world > 1 else "1 GPU",
                    "lin_iters_mean": float(np.mean(lin_its[-args.steps:]))},
         "roofline": roof(dom),
         "roofline_edge_flux": roof("CONV"),

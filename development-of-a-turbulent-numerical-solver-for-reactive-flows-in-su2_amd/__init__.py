@@ -29,7 +29,7 @@ FIELDS = ["U", "V", "DPDU", "DTDU", "MU", "KAPPA", "DIJ", "GRAD", "LIMITER", "TK
 F = {name: k for k, name in enumerate(FIELDS)}
 # rx_kernel
 KERNELS = ["CONV", "VISC", "SOURCE", "GRAD", "LIMITER", "DT", "SPMV", "ILU_BUILD", "ILU_APPLY", "LUSGS", "KRYLOV",
-           "UPDATE"]
+           "UPDATE", "SOLVE"]
 K = {name: k for k, name in enumerate(KERNELS)}
 
 
@@ -51,7 +51,8 @@ class MechDesc(C.Structure):
 class MeshDesc(C.Structure):
     _fields_ = [("n_dim", C.c_int32), ("n_point", C.c_int64), ("n_edge", C.c_int64), ("n_bvert", C.c_int64),
                 ("edges", C.c_void_p), ("edge_normal", C.c_void_p), ("coord", C.c_void_p), ("volume", C.c_void_p),
-                ("nbr_ptr", C.c_void_p), ("nbr", C.c_void_p), ("bvert", C.c_void_p), ("bvert_normal", C.c_void_p)]
+                ("nbr_ptr", C.c_void_p), ("nbr", C.c_void_p), ("bvert", C.c_void_p), ("bvert_normal", C.c_void_p),
+                ("n_part", C.c_int64), ("part_ptr", C.c_void_p)]
 
 
 class Cfg(C.Structure):
@@ -169,9 +170,14 @@ class ReactiveNSSolver:
             "bvert": np.ascontiguousarray(np.asarray(mesh["bvertex"])[:, :2], dtype=np.int64),
             "bvert_normal": np.ascontiguousarray(mesh["bvertex_normal"], dtype=np.float64),
         }
+        pp = mesh.get("part_ptr")
+        if pp is not None and len(pp) > 2:
+            self._mesh_keep["part_ptr"] = np.ascontiguousarray(pp, dtype=np.int64)
+        self.n_part = len(pp) - 1 if pp is not None else 1
         md = MeshDesc()
         md.n_dim, md.n_point, md.n_edge = self.nDim, self.N, self.E
         md.n_bvert = len(self._mesh_keep["bvert"])
+        md.n_part = len(self._mesh_keep["part_ptr"]) - 1 if "part_ptr" in self._mesh_keep else 0
         for k, v in self._mesh_keep.items():
             setattr(md, k, v.ctypes.data)
         h = C.c_void_p()

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -21,11 +22,16 @@ int dalloc(rx_ctx* ctx, T** p, size_t n) {
   return RX_OK;
 }
 
+// Allocate + copy on the context stream (ordered after dalloc's memset on the same stream; the
+// context stream does not synchronise with the null stream) and wait, so the host buffer may go.
 template <typename T>
 int dupload(rx_ctx* ctx, T** p, const T* h, size_t n) {
   int rc = dalloc(ctx, p, n);
   if (rc) return rc;
-  if (n) RX_HIP(hipMemcpy(*p, h, n * sizeof(T), hipMemcpyHostToDevice));
+  if (n) {
+    RX_HIP(hipMemcpyAsync(*p, h, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+    RX_HIP(hipStreamSynchronize(ctx->stream));
+  }
   return RX_OK;
 }
 
@@ -155,38 +161,79 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
     }
   }
   rp32[N] = (int32_t)ctx->nnzb;
-  // level schedules of the lower / upper triangular dependency graphs
+  // partitions (ranks), per-row intra-partition column ranges and per-partition level schedules
   {
-    std::vector<int32_t> lv(N, 0), bl(N, 0);
-    int32_t maxl = 0, maxb = 0;
-    for (int64_t i = 0; i < N; ++i) {
-      int32_t l = 0;
-      for (auto j : rows[i])
-        if (j < i) l = std::max(l, lv[j] + 1);
-      lv[i] = l;
-      maxl = std::max(maxl, l);
+    const int64_t np = (mesh->part_ptr && mesh->n_part > 0) ? mesh->n_part : 1;
+    ctx->h_part_ptr.assign(np + 1, 0);
+    if (mesh->part_ptr && mesh->n_part > 0) {
+      for (int64_t p = 0; p <= np; ++p) ctx->h_part_ptr[p] = mesh->part_ptr[p];
+      bool ok = ctx->h_part_ptr[0] == 0 && ctx->h_part_ptr[np] == N;
+      for (int64_t p = 0; p < np && ok; ++p) ok = ctx->h_part_ptr[p + 1] > ctx->h_part_ptr[p];
+      if (!ok) CK(RX_ERR_ARG);
+    } else {
+      ctx->h_part_ptr[1] = N;
     }
-    for (int64_t i = N - 1; i >= 0; --i) {
-      int32_t l = 0;
-      for (auto j : rows[i])
-        if (j > i) l = std::max(l, bl[j] + 1);
-      bl[i] = l;
-      maxb = std::max(maxb, l);
+    ctx->npart = (int)np;
+    std::vector<int32_t> klo(N), khi(N);
+    int rowmax = 1;
+    for (int64_t p = 0; p < np; ++p) {
+      const int64_t lo = ctx->h_part_ptr[p], hi = ctx->h_part_ptr[p + 1];
+      for (int64_t i = lo; i < hi; ++i) {
+        const auto& r = rows[i];
+        klo[i] = (int32_t)(ctx->h_rp[i] + (std::lower_bound(r.begin(), r.end(), (int32_t)lo) - r.begin()));
+        khi[i] = (int32_t)(ctx->h_rp[i] + (std::lower_bound(r.begin(), r.end(), (int32_t)hi) - r.begin()));
+        rowmax = std::max(rowmax, khi[i] - klo[i]);
+      }
     }
-    auto bucket = [&](const std::vector<int32_t>& lev, int32_t maxlev, std::vector<int32_t>& ptr,
-                      std::vector<int32_t>& order) {
-      ptr.assign(maxlev + 2, 0);
-      for (int64_t i = 0; i < N; ++i) ptr[lev[i] + 1]++;
-      for (int32_t l = 0; l <= maxlev; ++l) ptr[l + 1] += ptr[l];
-      order.resize(N);
-      std::vector<int32_t> f(ptr.begin(), ptr.end() - 1);
-      for (int64_t i = 0; i < N; ++i) order[f[lev[i]]++] = (int32_t)i;
+    ctx->rowmax = rowmax;
+    auto schedule = [&](bool fwd, rx_ctx::Sched& S) -> int {
+      std::vector<int32_t> lv(N, 0), part_lvl(np + 1, 0), lvl_ptr(1, 0), order;
+      order.reserve(N);
+      for (int64_t p = 0; p < np; ++p) {
+        const int64_t lo = ctx->h_part_ptr[p], hi = ctx->h_part_ptr[p + 1];
+        int32_t maxl = 0;
+        if (fwd) {
+          for (int64_t i = lo; i < hi; ++i) {
+            int32_t l = 0;
+            for (int32_t k = klo[i]; k < (int32_t)diag[i]; ++k) l = std::max(l, lv[col32[k]] + 1);
+            lv[i] = l;
+            maxl = std::max(maxl, l);
+          }
+        } else {
+          for (int64_t i = hi - 1; i >= lo; --i) {
+            int32_t l = 0;
+            for (int32_t k = (int32_t)diag[i] + 1; k < khi[i]; ++k) l = std::max(l, lv[col32[k]] + 1);
+            lv[i] = l;
+            maxl = std::max(maxl, l);
+          }
+        }
+        std::vector<int32_t> cnt(maxl + 2, 0);
+        for (int64_t i = lo; i < hi; ++i) cnt[lv[i] + 1]++;
+        for (int32_t l = 0; l <= maxl; ++l) cnt[l + 1] += cnt[l];
+        std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1), loc(hi - lo);
+        for (int64_t i = lo; i < hi; ++i) loc[fill[lv[i]]++] = (int32_t)i;
+        const int32_t base = (int32_t)order.size();
+        for (int32_t l = 0; l <= maxl; ++l) {
+          lvl_ptr.push_back(base + cnt[l + 1]);
+          S.maxwidth = std::max(S.maxwidth, cnt[l + 1] - cnt[l]);
+        }
+        order.insert(order.end(), loc.begin(), loc.end());
+        part_lvl[p + 1] = part_lvl[p] + maxl + 1;
+      }
+      S.nlevels = part_lvl[np];
+      int rc2 = dupload(ctx, &S.part_lvl, part_lvl.data(), part_lvl.size());
+      if (!rc2) rc2 = dupload(ctx, &S.lvl_ptr, lvl_ptr.data(), lvl_ptr.size());
+      if (!rc2) rc2 = dupload(ctx, &S.rows, order.data(), order.size());
+      return rc2;
     };
-    std::vector<int32_t> fo, bo;
-    bucket(lv, maxl, ctx->h_lvl_ptr, fo);
-    bucket(bl, maxb, ctx->h_blvl_ptr, bo);
-    CK(dupload(ctx, &ctx->lvl_rows, fo.data(), N));
-    CK(dupload(ctx, &ctx->blvl_rows, bo.data(), N));
+    CK(schedule(true, ctx->fs));
+    CK(schedule(false, ctx->bs));
+    CK(dupload(ctx, &ctx->klo, klo.data(), N));
+    CK(dupload(ctx, &ctx->khi, khi.data(), N));
+    const size_t per_wave = sizeof(double) * (size_t)(rowmax + 2) * nv * nv;
+    if (per_wave > 64 * 1024) CK(RX_ERR_ARG);  // a row with more blocks than one wave's LDS slice
+    ctx->ilu_waves = (int)std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1, ctx->fs.maxwidth),
+                                                                (64 * 1024) / per_wave}));
   }
   // LSQ neighbour lists (reference order) and boundary vertices per node
   std::vector<int32_t> nptr(N + 1), nbr(mesh->nbr_ptr[N]);
@@ -295,6 +342,8 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
     CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->jsrc, N * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->rsrc, N * nv));
+    CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
+    CK(dalloc(ctx, &ctx->xstar, N * nv));
   }
   CK(dalloc(ctx, &ctx->fvisc, E * nv));
   CK(dalloc(ctx, &ctx->lim_mn, N * ctx->nL));
@@ -314,9 +363,13 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->nbr_ptr,
-                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->lvl_rows, ctx->blvl_rows,
-                  ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->jsrc, ctx->rsrc, ctx->lim_mn, ctx->lim_mx,
-                  ctx->red, ctx->err, ctx->kw, ctx->kz};
+                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi,
+                  ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
+                  ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
+                  ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
+  if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
+  if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
+  rx_la_krylov_free(ctx);
   for (void* p : ptrs) dfree(p);
   for (void* p : ctx->mech_bufs) dfree(p);
   for (int q = 0; q < RX_F_COUNT; ++q) dfree(ctx->f[q]);
@@ -432,7 +485,7 @@ int rx_bsr_spmv(rx_ctx* ctx, rx_field x, rx_field y) {
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
   RxPhase ph(ctx, RX_K_SPMV);
-  return rx_la_spmv(ctx, ctx->f[RX_F_JAC], ctx->f[x], ctx->f[y]);
+  return rx_la_spmv(ctx, ctx->f[RX_F_JAC], ctx->f[x], ctx->f[y], nullptr);
 }
 
 int rx_ilu0_build(rx_ctx* ctx) {
@@ -446,7 +499,7 @@ int rx_ilu0_build(rx_ctx* ctx) {
 int rx_ilu0_apply(rx_ctx* ctx, rx_field b, rx_field x) {
   if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_ILU_APPLY);
-  return rx_la_ilu_apply(ctx, ctx->f[b], ctx->f[x]);
+  return rx_la_ilu_apply(ctx, ctx->f[b], ctx->f[x], nullptr);
 }
 
 int rx_lusgs_apply(rx_ctx* ctx, rx_field b, rx_field x) {
@@ -454,7 +507,8 @@ int rx_lusgs_apply(rx_ctx* ctx, rx_field b, rx_field x) {
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
   RxPhase ph(ctx, RX_K_LUSGS);
-  return rx_la_lusgs(ctx, ctx->f[RX_F_JAC], ctx->f[b], ctx->f[x]);
+  if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
+  return rx_la_lusgs(ctx, ctx->f[RX_F_JAC], ctx->f[b], ctx->f[x], nullptr);
 }
 
 int rx_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
@@ -462,14 +516,42 @@ int rx_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
   RxPhase ph(ctx, RX_K_KRYLOV);
+  if (ctx->cfg.lin_prec == 0 && (rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
   return rx_la_fgmres(ctx, tol, m, iters, resid);
 }
 
 int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
   if (!ctx) return RX_ERR_ARG;
-  RxPhase ph(ctx, RX_K_UPDATE);
-  return rx_la_explicit_update(ctx, res_rms);
+  int rc;
+  {
+    RxPhase ph(ctx, RX_K_UPDATE);
+    if (res_rms && (rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RES]))) return rc;
+    if ((rc = rx_la_explicit_update(ctx))) return rc;
+  }
+  return res_rms ? rx_la_rms_read(ctx, res_rms) : RX_OK;
 }
+
+namespace {
+// System build (Vol/dt, rhs), preconditioner build, FGMRES, RMS partials and the clipped update:
+// a fixed kernel sequence with no host decision (rx_krylov.hip), recorded once as a hipGraph.
+int enqueue_solve(rx_ctx* ctx) {
+  int rc;
+  if ((rc = rx_la_build_system(ctx))) return rc;
+  if (ctx->cfg.lin_prec == 1) {
+    if ((rc = rx_la_ilu_build(ctx))) return rc;
+  } else {
+    if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
+  }
+  if ((rc = rx_la_fgmres_enqueue(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter))) return rc;
+  if ((rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RHS]))) return rc;
+  return rx_la_implicit_update(ctx);
+}
+
+bool graphs_enabled() {
+  const char* e = getenv("RX_NO_GRAPH");
+  return !(e && e[0] == '1');
+}
+}  // namespace
 
 // ImplicitEuler_Iteration (solver_direct_reactive.cpp:2336-2407): system build, ILU0 build if
 // selected (CSysSolve::Solve :601-653), FGMRES, clipped relaxed update.
@@ -477,23 +559,36 @@ int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
+  if ((rc = rx_la_krylov_alloc(ctx, ctx->cfg.lin_iter))) return rc;
   {
-    RxPhase ph(ctx, RX_K_UPDATE);
-    if ((rc = rx_la_build_system(ctx))) return rc;
+    RxPhase ph(ctx, RX_K_SOLVE);
+    if (graphs_enabled()) {
+      if (!ctx->solve_exec) {
+        RX_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        ctx->capturing = true;
+        rc = enqueue_solve(ctx);
+        ctx->capturing = false;
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (rc) {
+          if (g) (void)hipGraphDestroy(g);
+          return rc;
+        }
+        if (e != hipSuccess) return rx_fail_hip(ctx, e);
+        ctx->solve_graph = g;
+        RX_HIP(hipGraphInstantiate(&ctx->solve_exec, g, nullptr, nullptr, 0));
+      }
+      RX_HIP(hipGraphLaunch(ctx->solve_exec, ctx->stream));
+    } else {
+      if ((rc = enqueue_solve(ctx))) return rc;
+    }
   }
-  if (ctx->cfg.lin_prec == 1) {
-    RxPhase ph(ctx, RX_K_ILU_BUILD);
-    if ((rc = rx_la_ilu_build(ctx))) return rc;
-  }
+  if (res_rms && (rc = rx_la_rms_read(ctx, res_rms))) return rc;
   int it = 0;
   double resid = 0.0;
-  {
-    RxPhase ph(ctx, RX_K_KRYLOV);
-    if ((rc = rx_la_fgmres(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter, &it, &resid))) return rc;
-  }
+  if ((rc = rx_la_fgmres_result(ctx, &it, &resid))) return rc;
   if (lin_iters) *lin_iters = it;
-  RxPhase ph(ctx, RX_K_UPDATE);
-  return rx_la_implicit_update(ctx, res_rms);
+  return RX_OK;
 }
 
 hipEvent_t rx_ctx::prof_event() {

@@ -39,11 +39,24 @@ struct rx_ctx {
   int32_t* col = nullptr;       // [nnzb]
   int64_t* diag = nullptr;      // [N] block index of the diagonal
   std::vector<int64_t> h_rp, h_col;
-  // level schedule for the triangular sweeps (rows grouped by dependency level)
-  int32_t* lvl_rows = nullptr;  // [N] rows sorted by forward level
-  std::vector<int32_t> h_lvl_ptr;   // [nLevels+1]
-  int32_t* blvl_rows = nullptr; // [N] rows sorted by backward level
-  std::vector<int32_t> h_blvl_ptr;
+  // partitions (the reference's MPI ranks): contiguous row ranges; per row the BSR index range of
+  // the columns inside its own partition [klo, khi) (columns are sorted, partitions contiguous)
+  int npart = 1;
+  std::vector<int64_t> h_part_ptr;
+  int32_t* klo = nullptr;       // [N]
+  int32_t* khi = nullptr;       // [N]
+  int rowmax = 1;               // max khi - klo
+  int ilu_waves = 1;            // wavefronts per workgroup of the ILU factorisation
+  // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
+  // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])
+  struct Sched {
+    int32_t* part_lvl = nullptr;
+    int32_t* lvl_ptr = nullptr;
+    int32_t* rows = nullptr;
+    int nlevels = 0, maxwidth = 0;
+  } fs, bs;
+  double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)
+  double* xstar = nullptr;      // [N][nVar] LU-SGS forward-sweep result (halo values)
 
   // ---- mechanism
   rx::DevMech mech{};
@@ -67,10 +80,16 @@ struct rx_ctx {
   double* h_red = nullptr;   // pinned host mirror
   int* err = nullptr;        // [2] code, index (device)
   int64_t last_err_index = -1;
-  // Krylov workspace
+  // Krylov workspace (device-resident FGMRES, rx_krylov.hip)
   int krylov_m = 0;
   double* kw = nullptr;      // [(m+1)][N*nVar]
   double* kz = nullptr;      // [(m+1)][N*nVar]
+  void* kstate = nullptr;    // device KState
+  void* h_kstate = nullptr;  // pinned host mirror
+  // captured implicit solve (system build + preconditioner build + FGMRES + update)
+  hipGraphExec_t solve_exec = nullptr;
+  hipGraph_t solve_graph = nullptr;
+  bool capturing = false;
 
   // ---- profiling
   // Phases record an event pair on the context stream without blocking; pairs are resolved
@@ -93,7 +112,7 @@ struct RxPhase {
   rx_kernel k;
   hipEvent_t a = nullptr;
   RxPhase(rx_ctx* ctx, rx_kernel kk) : c(ctx), k(kk) {
-    if (c->prof) {
+    if (c->prof && !c->capturing) {
       a = c->prof_event();
       (void)hipEventRecord(a, c->stream);
     }
@@ -120,11 +139,19 @@ int rx_launch_limiter(rx_ctx* ctx);
 int rx_launch_time_step(rx_ctx* ctx);
 int rx_check_error(rx_ctx* ctx);
 // linear algebra (rx_linalg.hip)
-int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y);
-int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x);
+int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y, const int* skip);
+int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, const int* skip);
+int rx_la_diag_factor(rx_ctx* ctx, const double* A);
 int rx_la_ilu_build(rx_ctx* ctx);
-int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x);
+int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, const int* skip);
+double* rx_invd_buf(rx_ctx* ctx);
+int rx_la_krylov_alloc(rx_ctx* ctx, int m);
+int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m);
+int rx_la_fgmres_result(rx_ctx* ctx, int* iters, double* resid);
 int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid);
-int rx_la_implicit_update(rx_ctx* ctx, double* rms);
-int rx_la_explicit_update(rx_ctx* ctx, double* rms);
+void rx_la_krylov_free(rx_ctx* ctx);
+int rx_la_rms_enqueue(rx_ctx* ctx, const double* r);
+int rx_la_rms_read(rx_ctx* ctx, double* rms);
+int rx_la_implicit_update(rx_ctx* ctx);
+int rx_la_explicit_update(rx_ctx* ctx);
 int rx_la_build_system(rx_ctx* ctx);

@@ -6,9 +6,7 @@
 //   ComputeILUPreconditioner :1453-1515, ComputeLU_SGSPreconditioner :1673-1709,
 //   FGMRES_LinSolver / ModGramSchmidt / Givens / SolveReduced :37-186, 309-463,
 //   ImplicitEuler_Iteration SU2_CFD/src/solver_direct_reactive.cpp:2336-2407.
-// The triangular sweeps keep the reference's exact sequential semantics by processing rows in
-// dependency levels (rows of one level are independent); within a row the arithmetic order is the
-// reference's. Dot products use a fixed-order tree reduction (bitwise reproducible run to run).
+// Triangular sweeps: rx_sweeps.hip; FGMRES: rx_krylov.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -26,7 +24,8 @@ inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_spmv(int N, const int32_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                  const double* __restrict__ A, const double* __restrict__ x,
-                                                 double* __restrict__ y) {
+                                                 double* __restrict__ y, const int* __restrict__ skip) {
+  if (skip && *skip) return;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * NV) return;
   const int i = t / NV, a = t - i * NV;
@@ -38,256 +37,6 @@ __global__ __launch_bounds__(kBlock) void k_spmv(int N, const int32_t* __restric
     for (int c = 0; c < NV; ++c) acc += blk[c] * xv[c];
   }
   y[t] = acc;
-}
-
-// Gauss_Elimination on a private copy (matrix_structure.cpp:594-643).
-template <int NV>
-__device__ inline void gauss(const double* __restrict__ Block, double* rhs) {
-  double blk[NV * NV];
-#pragma unroll
-  for (int q = 0; q < NV * NV; ++q) blk[q] = Block[q];
-  for (int i = 1; i < NV; ++i)
-    for (int j = 0; j < i; ++j) {
-      const double w = blk[i * NV + j] / blk[j * NV + j];
-      for (int k = j; k < NV; ++k) blk[i * NV + k] -= w * blk[j * NV + k];
-      rhs[i] -= w * rhs[j];
-    }
-  rhs[NV - 1] = rhs[NV - 1] / blk[NV * NV - 1];
-  for (int i = NV - 2; i >= 0; --i) {
-    double aux = 0.0;
-    for (int j = i + 1; j < NV; ++j) aux += blk[i * NV + j] * rhs[j];
-    rhs[i] = (rhs[i] - aux) / blk[i * NV + i];
-  }
-}
-
-// LU-SGS forward sweep for the rows of one level: (D+L) x* = b.
-template <int NV>
-__global__ __launch_bounds__(64) void k_lusgs_fwd(int n, const int32_t* __restrict__ rows, const int32_t* __restrict__ rp,
-                                                  const int32_t* __restrict__ col, const int64_t* __restrict__ diag,
-                                                  const double* __restrict__ A, const double* __restrict__ b,
-                                                  double* __restrict__ x) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int i = rows[t];
-  double prv[NV];
-#pragma unroll
-  for (int a = 0; a < NV; ++a) prv[a] = 0.0;
-  for (int k = rp[i]; k < rp[i + 1]; ++k) {
-    const int j = col[k];
-    if (j < i) {
-      const double* blk = A + (size_t)k * NV * NV;
-#pragma unroll
-      for (int a = 0; a < NV; ++a) {
-        double pb = 0.0;
-#pragma unroll
-        for (int c = 0; c < NV; ++c) pb += blk[a * NV + c] * x[(size_t)j * NV + c];
-        prv[a] += pb;
-      }
-    }
-  }
-  double aux[NV];
-#pragma unroll
-  for (int a = 0; a < NV; ++a) aux[a] = b[(size_t)i * NV + a] - prv[a];
-  gauss<NV>(A + diag[i] * NV * NV, aux);
-#pragma unroll
-  for (int a = 0; a < NV; ++a) x[(size_t)i * NV + a] = aux[a];
-}
-
-// LU-SGS backward sweep: (D+U) x = D x*.
-template <int NV>
-__global__ __launch_bounds__(64) void k_lusgs_bwd(int n, const int32_t* __restrict__ rows, const int32_t* __restrict__ rp,
-                                                  const int32_t* __restrict__ col, const int64_t* __restrict__ diag,
-                                                  const double* __restrict__ A, double* __restrict__ x) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int i = rows[t];
-  const double* D = A + diag[i] * NV * NV;
-  double aux[NV], prv[NV];
-#pragma unroll
-  for (int a = 0; a < NV; ++a) {
-    double pb = 0.0;
-#pragma unroll
-    for (int c = 0; c < NV; ++c) pb += D[a * NV + c] * x[(size_t)i * NV + c];
-    aux[a] = 0.0 + pb;
-    prv[a] = 0.0;
-  }
-  for (int k = rp[i]; k < rp[i + 1]; ++k) {
-    const int j = col[k];
-    if (j > i) {
-      const double* blk = A + (size_t)k * NV * NV;
-#pragma unroll
-      for (int a = 0; a < NV; ++a) {
-        double pb = 0.0;
-#pragma unroll
-        for (int c = 0; c < NV; ++c) pb += blk[a * NV + c] * x[(size_t)j * NV + c];
-        prv[a] += pb;
-      }
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < NV; ++a) aux[a] -= prv[a];
-  gauss<NV>(D, aux);
-#pragma unroll
-  for (int a = 0; a < NV; ++a) x[(size_t)i * NV + a] = aux[a];
-}
-
-// inv(D) by Gauss elimination of each unit column (InverseDiagonalBlock_ILUMatrix): one row.
-template <int NV>
-__device__ inline void block_inverse(const double* __restrict__ D, double* __restrict__ inv) {
-  for (int c = 0; c < NV; ++c) {
-    double v[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) v[j] = 0.0;
-    v[c] = 1.0;
-    gauss<NV>(D, v);
-#pragma unroll
-    for (int j = 0; j < NV; ++j) inv[j * NV + c] = v[j];
-  }
-}
-
-// ILU(0) factorisation of the rows of one level (row-sequential semantics of :1387-1449). The
-// inverse of each finished diagonal is stored (the reference recomputes the same inverse from the
-// same finished block every time it needs it, so storing it is bitwise identical).
-template <int NV>
-__global__ __launch_bounds__(64) void k_ilu_build(int n, const int32_t* __restrict__ rows, const int32_t* __restrict__ rp,
-                                                  const int32_t* __restrict__ col, const int64_t* __restrict__ diag,
-                                                  double* __restrict__ F, double* __restrict__ invD) {
-  constexpr int NV2 = NV * NV;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int i = rows[t];
-  for (int k = rp[i]; k < rp[i + 1]; ++k) {
-    const int j = col[k];
-    if (j >= i) break;  // columns are sorted: lower part first
-    double* Bij = F + (size_t)k * NV2;
-    const double* inv = invD + (size_t)j * NV2;
-    double w[NV2];
-    for (int a = 0; a < NV; ++a)
-      for (int c = 0; c < NV; ++c) {
-        double s = 0.0;
-        for (int q = 0; q < NV; ++q) s += Bij[a * NV + q] * inv[q * NV + c];
-        w[a * NV + c] = s;
-      }
-    for (int kk = rp[j]; kk < rp[j + 1]; ++kk) {
-      const int kp = col[kk];
-      if (kp < j) continue;
-      // find block (i, kp) in row i
-      int pos = -1;
-      for (int q = rp[i]; q < rp[i + 1]; ++q)
-        if (col[q] == kp) {
-          pos = q;
-          break;
-        }
-      if (pos < 0) continue;
-      const double* Bjk = F + (size_t)kk * NV2;
-      double* Bik = F + (size_t)pos * NV2;
-      // left multiply quirk: block = A_jk * (A_ij inv(A_jj))
-      for (int a = 0; a < NV; ++a)
-        for (int c = 0; c < NV; ++c) {
-          double s = 0.0;
-          for (int q = 0; q < NV; ++q) s += Bjk[a * NV + q] * w[q * NV + c];
-          Bik[a * NV + c] -= s;
-        }
-    }
-    for (int q = 0; q < NV2; ++q) Bij[q] = w[q];
-  }
-  block_inverse<NV>(F + diag[i] * NV2, invD + (size_t)i * NV2);
-}
-
-// ILU apply, forward substitution on one level: x_i = b_i - sum_{j<i} L_ij x_j (row order).
-template <int NV>
-__global__ __launch_bounds__(kBlock) void k_ilu_fwd(int n, const int32_t* __restrict__ rows,
-                                                    const int32_t* __restrict__ rp, const int32_t* __restrict__ col,
-                                                    const double* __restrict__ F, const double* __restrict__ b,
-                                                    double* __restrict__ x) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n * NV) return;
-  const int i = rows[t / NV], a = t % NV;
-  double xi = b[(size_t)i * NV + a];
-  for (int k = rp[i]; k < rp[i + 1]; ++k) {
-    const int j = col[k];
-    if (j >= i) break;
-    const double* blk = F + (size_t)k * NV * NV + a * NV;
-    double s = 0.0;
-#pragma unroll
-    for (int c = 0; c < NV; ++c) s += blk[c] * x[(size_t)j * NV + c];
-    xi -= s;
-  }
-  x[(size_t)i * NV + a] = xi;
-}
-
-// ILU apply, backward substitution on one level: x_i = inv(D_i) (x_i - sum_{j>i} U_ij x_j).
-template <int NV>
-__global__ __launch_bounds__(64) void k_ilu_bwd(int n, const int32_t* __restrict__ rows, const int32_t* __restrict__ rp,
-                                                const int32_t* __restrict__ col, const double* __restrict__ F,
-                                                const double* __restrict__ invD, int last, double* __restrict__ x) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int i = rows[t];
-  double v[NV];
-  if (i == last) {
-#pragma unroll
-    for (int a = 0; a < NV; ++a) v[a] = x[(size_t)i * NV + a];
-  } else {
-    double sum[NV];
-#pragma unroll
-    for (int a = 0; a < NV; ++a) sum[a] = 0.0;
-    for (int k = rp[i]; k < rp[i + 1]; ++k) {
-      const int j = col[k];
-      if (j >= i + 1) {
-        const double* blk = F + (size_t)k * NV * NV;
-#pragma unroll
-        for (int a = 0; a < NV; ++a) {
-          double s = 0.0;
-#pragma unroll
-          for (int c = 0; c < NV; ++c) s += blk[a * NV + c] * x[(size_t)j * NV + c];
-          sum[a] += s;
-        }
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < NV; ++a) v[a] = x[(size_t)i * NV + a] - sum[a];
-  }
-  const double* inv = invD + (size_t)i * NV * NV;
-#pragma unroll
-  for (int a = 0; a < NV; ++a) {
-    double s = 0.0;
-#pragma unroll
-    for (int c = 0; c < NV; ++c) s += inv[a * NV + c] * v[c];
-    x[(size_t)i * NV + a] = s;
-  }
-}
-
-// ---- vector kernels for FGMRES (deterministic fixed-order reductions)
-constexpr int kRedBlocks = 512;
-
-__global__ __launch_bounds__(kBlock) void k_dot_partial(int64_t n, const double* __restrict__ a,
-                                                        const double* __restrict__ b, double* __restrict__ part) {
-  __shared__ double sh[kBlock];
-  double s = 0.0;
-  for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < n; q += (int64_t)gridDim.x * kBlock)
-    s += a[q] * b[q];
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  for (int w = kBlock / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
-}
-
-__global__ __launch_bounds__(kBlock) void k_axpy(int64_t n, double alpha, const double* __restrict__ x,
-                                                 double* __restrict__ y) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q < n) y[q] += alpha * x[q];
-}
-__global__ __launch_bounds__(kBlock) void k_scale_div(int64_t n, double d, double* __restrict__ y) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q < n) y[q] /= d;
-}
-__global__ __launch_bounds__(kBlock) void k_sub(int64_t n, const double* __restrict__ b, double* __restrict__ y) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q < n) y[q] -= b[q];
 }
 
 // ImplicitEuler system build: Aii += V/dt (or identity row when dt <= EPS), rhs = -R, x = 0.
@@ -368,197 +117,13 @@ __global__ __launch_bounds__(kBlock) void k_sumsq_cols(int N, int nVar, const do
     default: return RX_ERR_ARG;                      \
   }
 
-double* invd_buf(rx_ctx* ctx) { return ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)ctx->nVar * ctx->nVar; }
 
 }  // namespace
 
-int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y) {
+int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y, const int* skip) {
   RX_NV_SWITCH(ctx->nVar, (k_spmv<NV_><<<blocks(ctx->N * NV_), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->rp,
-                                                                                          ctx->col, A, x, y)));
+                                                                                          ctx->col, A, x, y, skip)));
   RX_HIP(hipGetLastError());
-  return RX_OK;
-}
-
-int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x) {
-  const int nl = (int)ctx->h_lvl_ptr.size() - 1;
-  for (int l = 0; l < nl; ++l) {
-    const int s = ctx->h_lvl_ptr[l], n = ctx->h_lvl_ptr[l + 1] - s;
-    RX_NV_SWITCH(ctx->nVar, (k_lusgs_fwd<NV_><<<blocks(n, 64), 64, 0, ctx->stream>>>(
-                                n, ctx->lvl_rows + s, ctx->rp, ctx->col, ctx->diag, A, b, x)));
-  }
-  const int nb = (int)ctx->h_blvl_ptr.size() - 1;
-  for (int l = 0; l < nb; ++l) {
-    const int s = ctx->h_blvl_ptr[l], n = ctx->h_blvl_ptr[l + 1] - s;
-    RX_NV_SWITCH(ctx->nVar, (k_lusgs_bwd<NV_><<<blocks(n, 64), 64, 0, ctx->stream>>>(
-                                n, ctx->blvl_rows + s, ctx->rp, ctx->col, ctx->diag, A, x)));
-  }
-  RX_HIP(hipGetLastError());
-  return RX_OK;
-}
-
-int rx_la_ilu_build(rx_ctx* ctx) {
-  const int64_t nb = ctx->nnzb * (int64_t)ctx->nVar * ctx->nVar;
-  RX_HIP(hipMemcpyAsync(ctx->f[RX_F_ILU], ctx->f[RX_F_JAC], nb * sizeof(double), hipMemcpyDeviceToDevice,
-                        ctx->stream));
-  const int nl = (int)ctx->h_lvl_ptr.size() - 1;
-  for (int l = 0; l < nl; ++l) {
-    const int s = ctx->h_lvl_ptr[l], n = ctx->h_lvl_ptr[l + 1] - s;
-    RX_NV_SWITCH(ctx->nVar, (k_ilu_build<NV_><<<blocks(n, 64), 64, 0, ctx->stream>>>(
-                                n, ctx->lvl_rows + s, ctx->rp, ctx->col, ctx->diag, ctx->f[RX_F_ILU],
-                                invd_buf(ctx))));
-  }
-  RX_HIP(hipGetLastError());
-  return RX_OK;
-}
-
-int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x) {
-  const int nl = (int)ctx->h_lvl_ptr.size() - 1;
-  for (int l = 0; l < nl; ++l) {
-    const int s = ctx->h_lvl_ptr[l], n = ctx->h_lvl_ptr[l + 1] - s;
-    RX_NV_SWITCH(ctx->nVar, (k_ilu_fwd<NV_><<<blocks((int64_t)n * NV_), kBlock, 0, ctx->stream>>>(
-                                n, ctx->lvl_rows + s, ctx->rp, ctx->col, ctx->f[RX_F_ILU], b, x)));
-  }
-  const int nb = (int)ctx->h_blvl_ptr.size() - 1;
-  for (int l = 0; l < nb; ++l) {
-    const int s = ctx->h_blvl_ptr[l], n = ctx->h_blvl_ptr[l + 1] - s;
-    RX_NV_SWITCH(ctx->nVar, (k_ilu_bwd<NV_><<<blocks(n, 64), 64, 0, ctx->stream>>>(
-                                n, ctx->blvl_rows + s, ctx->rp, ctx->col, ctx->f[RX_F_ILU], invd_buf(ctx),
-                                (int)ctx->N - 1, x)));
-  }
-  RX_HIP(hipGetLastError());
-  return RX_OK;
-}
-
-namespace {
-int dev_dot(rx_ctx* ctx, const double* a, const double* b, int64_t n, double* out) {
-  k_dot_partial<<<kRedBlocks, kBlock, 0, ctx->stream>>>(n, a, b, ctx->red);
-  RX_HIP(hipGetLastError());
-  RX_HIP(hipMemcpyAsync(ctx->h_red, ctx->red, kRedBlocks * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-  RX_HIP(hipStreamSynchronize(ctx->stream));
-  double s = 0.0;
-  for (int q = 0; q < kRedBlocks; ++q) s += ctx->h_red[q];
-  *out = s;
-  return RX_OK;
-}
-int dev_axpy(rx_ctx* ctx, int64_t n, double alpha, const double* x, double* y) {
-  k_axpy<<<blocks(n), kBlock, 0, ctx->stream>>>(n, alpha, x, y);
-  RX_HIP(hipGetLastError());
-  return RX_OK;
-}
-}  // namespace
-
-// FGMRES (linear_solvers_structure.cpp:309-463) on JAC * SOL = RHS, SOL holds the initial guess.
-int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
-  const int64_t n = ctx->N * ctx->nVar;
-  if (m < 1 || m > 1000) return RX_ERR_ARG;
-  if (ctx->krylov_m < m) {
-    if (ctx->kw) (void)hipFree(ctx->kw);
-    if (ctx->kz) (void)hipFree(ctx->kz);
-    RX_HIP(hipMalloc(&ctx->kw, sizeof(double) * n * (m + 1)));
-    RX_HIP(hipMalloc(&ctx->kz, sizeof(double) * n * (m + 1)));
-    ctx->krylov_m = m;
-  }
-  double* A = ctx->f[RX_F_JAC];
-  double* b = ctx->f[RX_F_RHS];
-  double* x = ctx->f[RX_F_SOL];
-  auto W = [&](int k) { return ctx->kw + (int64_t)k * n; };
-  auto Z = [&](int k) { return ctx->kz + (int64_t)k * n; };
-  std::vector<double> g(m + 1, 0.0), sn(m + 1, 0.0), cs(m + 1, 0.0), y(m, 0.0);
-  std::vector<std::vector<double>> H(m + 1, std::vector<double>(m, 0.0));
-  int rc;
-  double norm0;
-  if ((rc = dev_dot(ctx, b, b, n, &norm0))) return rc;
-  norm0 = std::sqrt(norm0);
-  if ((rc = rx_la_spmv(ctx, A, x, W(0)))) return rc;
-  k_sub<<<blocks(n), kBlock, 0, ctx->stream>>>(n, b, W(0));
-  double beta;
-  if ((rc = dev_dot(ctx, W(0), W(0), n, &beta))) return rc;
-  beta = std::sqrt(beta);
-  const double epsm = 2.220446049250313e-16;
-  if ((beta < tol * norm0) || (beta < epsm)) {
-    *iters = 0;
-    *resid = beta;
-    return RX_OK;
-  }
-  k_scale_div<<<blocks(n), kBlock, 0, ctx->stream>>>(n, -beta, W(0));
-  g[0] = beta;
-  norm0 = beta;
-  int i = 0;
-  for (i = 0; i < m; ++i) {
-    if (beta < tol * norm0) break;
-    if (ctx->cfg.lin_prec == 1) {
-      if ((rc = rx_la_ilu_apply(ctx, W(i), Z(i)))) return rc;
-    } else {
-      if ((rc = rx_la_lusgs(ctx, A, W(i), Z(i)))) return rc;
-    }
-    if ((rc = rx_la_spmv(ctx, A, Z(i), W(i + 1)))) return rc;
-    // ModGramSchmidt (:87-186)
-    const double reorth = 0.98;
-    double nrm;
-    if ((rc = dev_dot(ctx, W(i + 1), W(i + 1), n, &nrm))) return rc;
-    double thr = nrm * reorth;
-    if ((nrm <= 0.0) || (nrm != nrm)) return RX_ERR_DIVERGED;
-    for (int k = 0; k < i + 1; ++k) {
-      double prod;
-      if ((rc = dev_dot(ctx, W(i + 1), W(k), n, &prod))) return rc;
-      H[k][i] = prod;
-      if ((rc = dev_axpy(ctx, n, -prod, W(k), W(i + 1)))) return rc;
-      if (prod * prod > thr) {
-        if ((rc = dev_dot(ctx, W(i + 1), W(k), n, &prod))) return rc;
-        H[k][i] += prod;
-        if ((rc = dev_axpy(ctx, n, -prod, W(k), W(i + 1)))) return rc;
-      }
-      nrm -= H[k][i] * H[k][i];
-      if (nrm < 0.0) nrm = 0.0;
-      thr = nrm * reorth;
-    }
-    if ((rc = dev_dot(ctx, W(i + 1), W(i + 1), n, &nrm))) return rc;
-    nrm = std::sqrt(nrm);
-    H[i + 1][i] = nrm;
-    k_scale_div<<<blocks(n), kBlock, 0, ctx->stream>>>(n, nrm, W(i + 1));
-    auto applyG = [](double s, double c, double& h1, double& h2) {
-      const double t = c * h1 + s * h2;
-      h2 = c * h2 - s * h1;
-      h1 = t;
-    };
-    for (int k = 0; k < i; ++k) applyG(sn[k], cs[k], H[k][i], H[k + 1][i]);
-    {
-      double& dx = H[i][i];
-      double& dy = H[i + 1][i];
-      auto sgn = [](double a, double bb) { return bb == 0.0 ? 0.0 : (bb < 0 ? -std::fabs(a) : std::fabs(a)); };
-      if ((dx == 0.0) && (dy == 0.0)) {
-        cs[i] = 1.0;
-        sn[i] = 0.0;
-      } else if (std::fabs(dy) > std::fabs(dx)) {
-        const double tmp = dx / dy;
-        dx = std::sqrt(1.0 + tmp * tmp);
-        sn[i] = sgn(1.0 / dx, dy);
-        cs[i] = tmp * sn[i];
-      } else if (std::fabs(dy) <= std::fabs(dx)) {
-        const double tmp = dy / dx;
-        dy = std::sqrt(1.0 + tmp * tmp);
-        cs[i] = sgn(1.0 / dy, dx);
-        sn[i] = tmp * cs[i];
-      } else {
-        dx = dy = 0.0;
-        cs[i] = 1.0;
-        sn[i] = 0.0;
-      }
-      dx = std::fabs(dx * dy);
-      dy = 0.0;
-    }
-    applyG(sn[i], cs[i], g[i], g[i + 1]);
-    beta = std::fabs(g[i + 1]);
-  }
-  for (int k = 0; k < i; ++k) y[k] = g[k];
-  for (int k = i - 1; k >= 0; --k) {
-    y[k] /= H[k][k];
-    for (int j = k - 1; j >= 0; --j) y[j] -= H[j][k] * y[k];
-  }
-  for (int k = 0; k < i; ++k)
-    if ((rc = dev_axpy(ctx, n, y[k], Z(k), x))) return rc;
-  *iters = i;
-  *resid = beta;
   return RX_OK;
 }
 
@@ -570,40 +135,40 @@ int rx_la_build_system(rx_ctx* ctx) {
   return RX_OK;
 }
 
-namespace {
-int rms_of(rx_ctx* ctx, const double* r, double* rms) {
-  const int nb = 256, nv = ctx->nVar;
-  k_sumsq_cols<<<nb, kBlock, 0, ctx->stream>>>((int)ctx->N, nv, r, ctx->red);
+// SetResidual_RMS (solver_structure.cpp:184): per-variable partial sums of r^2 (fixed order), read
+// back and finished on the host by rx_la_rms_read.
+constexpr int kRmsBlocks = 256;
+constexpr int64_t kRmsOff = 1024;  // ctx->red[0..1023] is the inner-product scratch
+
+int rx_la_rms_enqueue(rx_ctx* ctx, const double* r) {
+  k_sumsq_cols<<<kRmsBlocks, kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nVar, r, ctx->red + kRmsOff);
   RX_HIP(hipGetLastError());
-  RX_HIP(hipMemcpyAsync(ctx->h_red, ctx->red, sizeof(double) * nb * nv, hipMemcpyDeviceToHost, ctx->stream));
+  return RX_OK;
+}
+
+int rx_la_rms_read(rx_ctx* ctx, double* rms) {
+  const int nv = ctx->nVar;
+  RX_HIP(hipMemcpyAsync(ctx->h_red, ctx->red + kRmsOff, sizeof(double) * kRmsBlocks * nv, hipMemcpyDeviceToHost,
+                        ctx->stream));
   RX_HIP(hipStreamSynchronize(ctx->stream));
   for (int v = 0; v < nv; ++v) {
     double s = 0.0;
-    for (int q = 0; q < nb; ++q) s += ctx->h_red[q * nv + v];
+    for (int q = 0; q < kRmsBlocks; ++q) s += ctx->h_red[q * nv + v];
     rms[v] = std::max(rx::kEPS * rx::kEPS, std::sqrt(s / (double)ctx->N));
   }
   return RX_OK;
 }
-}  // namespace
 
-int rx_la_implicit_update(rx_ctx* ctx, double* rms) {
+int rx_la_implicit_update(rx_ctx* ctx) {
   const int64_t n = ctx->N * ctx->nVar;
-  if (rms) {
-    int rc = rms_of(ctx, ctx->f[RX_F_RHS], rms);
-    if (rc) return rc;
-  }
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nVar, ctx->nDim, ctx->f[RX_F_SOL],
                                                   ctx->cfg.relaxation, ctx->vol, ctx->f[RX_F_DT], 0, ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
 
-int rx_la_explicit_update(rx_ctx* ctx, double* rms) {
+int rx_la_explicit_update(rx_ctx* ctx) {
   const int64_t n = ctx->N * ctx->nVar;
-  if (rms) {
-    int rc = rms_of(ctx, ctx->f[RX_F_RES], rms);
-    if (rc) return rc;
-  }
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], 1.0,
                                                   ctx->vol, ctx->f[RX_F_DT], 1, ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());

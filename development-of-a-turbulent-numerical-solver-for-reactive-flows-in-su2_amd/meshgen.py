@@ -143,14 +143,65 @@ def renumber(pts, quads, bnd, perm):
     return pts[perm], old2new[quads], {k: old2new[v] for k, v in bnd.items()}, old2new
 
 
-def build_jet(nx: int, ny: int, rcm: bool = True, **kw):
-    """Synthetic jet mesh ready for the solver: RCM-ordered points + median dual."""
+def partition_rcb(coord, n_part: int):
+    """Recursive coordinate bisection into n_part balanced parts (stand-in for the reference's METIS
+    k-way call, geometry_structure.cpp:11465-11530: any partition is valid input, the solver records
+    it). Returns the part id of every point."""
+    part = np.zeros(len(coord), dtype=np.int64)
+
+    def split(idx, p0, np_):
+        if np_ == 1:
+            part[idx] = p0
+            return
+        left = np_ // 2
+        ext = coord[idx].max(axis=0) - coord[idx].min(axis=0)
+        # split along the longer extent, normalised by the domain aspect so slabs stay square-ish
+        ax = int(np.argmax(ext / np.maximum(dom, 1e-300)))
+        o = idx[np.argsort(coord[idx, ax], kind="stable")]
+        cut = int(round(len(o) * left / np_))
+        split(o[:cut], p0, left)
+        split(o[cut:], p0 + left, np_ - left)
+
+    dom = coord.max(axis=0) - coord.min(axis=0)
+    split(np.arange(len(coord)), 0, int(n_part))
+    return part
+
+
+def partition_order(n, edges, part):
+    """New->old permutation: partitions in order, each one RCM-ordered on its own subgraph (the
+    reference renumbers every rank's domain points with RCM, CPhysicalGeometry::SetRCM_Ordering)."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    i, j = edges[:, 0], edges[:, 1]
+    same = part[i] == part[j]
+    A = sp.coo_matrix((np.ones(2 * same.sum()), (np.r_[i[same], j[same]], np.r_[j[same], i[same]])),
+                      shape=(n, n)).tocsr()
+    perm, ptr = [], [0]
+    for p in range(int(part.max()) + 1):
+        idx = np.nonzero(part == p)[0]
+        sub = A[idx][:, idx]
+        perm.append(idx[np.asarray(reverse_cuthill_mckee(sub, symmetric_mode=True), dtype=np.int64)])
+        ptr.append(ptr[-1] + len(idx))
+    return np.concatenate(perm), np.asarray(ptr, dtype=np.int64)
+
+
+def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, **kw):
+    """Synthetic jet mesh ready for the solver: RCM-ordered points + median dual.
+
+    n_part > 1: points are split into n_part RCB parts (the reference's MPI ranks), numbered part by
+    part with a local RCM; `part_ptr` gives the row range of every part."""
     pts, quads, bnd = jet_mesh(nx, ny, **kw)
-    if rcm:
+    part_ptr = np.array([0, len(pts)], dtype=np.int64)
+    if n_part > 1:
+        d0 = median_dual(pts, quads, bnd)
+        perm, part_ptr = partition_order(len(pts), d0["edges"], partition_rcb(pts, n_part))
+        pts, quads, bnd, _ = renumber(pts, quads, bnd, perm)
+    elif rcm:
         d0 = median_dual(pts, quads, bnd)
         perm = rcm_order(len(pts), d0["edges"])
         pts, quads, bnd, _ = renumber(pts, quads, bnd, perm)
     dual = median_dual(pts, quads, bnd)
     dual["coord"] = pts
     dual["quads"] = quads
+    dual["part_ptr"] = part_ptr
     return dual

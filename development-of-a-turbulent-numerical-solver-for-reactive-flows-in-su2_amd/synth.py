@@ -69,11 +69,11 @@ def species_subset(g, keep, nDim=2):
     return out
 
 
-def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9):
+def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1):
     """Mesh (RCM-ordered median dual) + node records for an nx x ny jet with 9 (reference-native), 7
     or 4 species."""
     mg = _meshgen()
-    mesh = mg.build_jet(nx, ny)
+    mesh = mg.build_jet(nx, ny, n_part=n_part)
     g = load_records(records)
     if n_species != int(g["mech_n_species"]):
         g = species_subset(g, np.arange(n_species))

@@ -78,6 +78,13 @@ typedef struct {
   const int64_t *nbr;        /* [nbr_ptr[N]] */
   const int64_t *bvert;      /* [nB][2] (marker, point) in marker / vertex order */
   const double *bvert_normal;/* [nB][nDim] */
+  /* Partitions standing for the reference's MPI ranks (CGeometry partitioning,
+   * geometry_structure.cpp:11465-11530): points are numbered partition by partition and
+   * part_ptr[p]..part_ptr[p+1] is partition p. The ILU(0)/LU-SGS preconditioners act per partition
+   * exactly as each rank's CSysMatrix does (matrix_structure.cpp:1397/1416/1472 skip halo columns;
+   * LU-SGS's backward sweep reads halo x*). n_part = 0 or part_ptr = NULL: one partition. */
+  int64_t n_part;
+  const int64_t *part_ptr;   /* [n_part+1] */
 } rx_mesh_desc;
 
 typedef struct {
@@ -137,7 +144,9 @@ int rx_implicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */, int *li
 /* Per-phase device timing with HIP events on the context stream (for bench roofline). */
 typedef enum {
   RX_K_CONV = 0, RX_K_VISC, RX_K_SOURCE, RX_K_GRAD, RX_K_LIMITER, RX_K_DT, RX_K_SPMV, RX_K_ILU_BUILD,
-  RX_K_ILU_APPLY, RX_K_LUSGS, RX_K_KRYLOV, RX_K_UPDATE, RX_K_COUNT
+  RX_K_ILU_APPLY, RX_K_LUSGS, RX_K_KRYLOV, RX_K_UPDATE,
+  RX_K_SOLVE, /* rx_implicit_euler's captured solve: system build + preconditioner build + FGMRES + update */
+  RX_K_COUNT
 } rx_kernel;
 int rx_profile_enable(rx_ctx *ctx, int on);
 int rx_profile_read(rx_ctx *ctx, rx_kernel k, double *total_ms, int64_t *launches);

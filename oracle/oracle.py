@@ -33,6 +33,8 @@ def lib():
         _lib.orc_source_cells.restype = C.c_int
         _lib.orc_visc_edges.restype = C.c_int
         _lib.orc_fgmres.restype = C.c_int
+        _lib.orc_fgmres_p.restype = C.c_int
+        _lib.orc_dot.restype = C.c_double
     return _lib
 
 
@@ -170,41 +172,66 @@ def bsr_spmv(rp, col, A, x):
     return y.reshape(N, nb)
 
 
+class dot_order:
+    """Context manager: FGMRES inner products in the device's reduction order (mode "device") instead
+    of the reference's sequential sum (mode "reference", the default)."""
+
+    def __init__(self, mode="device"):
+        self.mode = 1 if mode == "device" else 0
+
+    def __enter__(self):
+        lib().orc_set_dot_mode(C.c_int(self.mode))
+        return self
+
+    def __exit__(self, *a):
+        lib().orc_set_dot_mode(C.c_int(0))
+
+
+def _parts(N, part_ptr):
+    if part_ptr is None:
+        return C.c_int64(1), None
+    pp = np.asarray(part_ptr, dtype=np.int64)
+    assert pp[0] == 0 and pp[-1] == N
+    return C.c_int64(len(pp) - 1), _p(pp, np.int64)
+
+
 @_keepalive
-def lusgs(rp, col, A, b):
+def lusgs(rp, col, A, b, part_ptr=None):
+    """LU-SGS apply; `part_ptr` splits the rows into ranks (see Parts in rx_oracle.cpp)."""
     N, nb = len(rp) - 1, A.shape[1]
     x = np.zeros(N * nb)
-    lib().orc_lusgs(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A), _p(b),
-                    x.ctypes.data_as(C.c_void_p))
+    lib().orc_lusgs_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A), _p(b),
+                      x.ctypes.data_as(C.c_void_p), *_parts(N, part_ptr))
     return x.reshape(N, nb)
 
 
 @_keepalive
-def ilu_build(rp, col, A):
+def ilu_build(rp, col, A, part_ptr=None):
     N, nb = len(rp) - 1, A.shape[1]
     F = np.zeros_like(np.ascontiguousarray(A))
-    lib().orc_ilu_build(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
-                        F.ctypes.data_as(C.c_void_p))
+    lib().orc_ilu_build_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
+                          F.ctypes.data_as(C.c_void_p), *_parts(N, part_ptr))
     return F
 
 
 @_keepalive
-def ilu_apply(rp, col, F, b):
+def ilu_apply(rp, col, F, b, part_ptr=None):
     N, nb = len(rp) - 1, F.shape[1]
     x = np.zeros(N * nb)
-    lib().orc_ilu_apply(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(F), _p(b),
-                        x.ctypes.data_as(C.c_void_p))
+    lib().orc_ilu_apply_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(F), _p(b),
+                          x.ctypes.data_as(C.c_void_p), *_parts(N, part_ptr))
     return x.reshape(N, nb)
 
 
 @_keepalive
-def fgmres(rp, col, A, b, prec="lusgs", F=None, tol=1e-6, m=5, x0=None):
+def fgmres(rp, col, A, b, prec="lusgs", F=None, tol=1e-6, m=5, x0=None, part_ptr=None):
     N, nb = len(rp) - 1, A.shape[1]
     x = np.zeros(N * nb) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).ravel().copy()
     resid = C.c_double(0.0)
-    it = lib().orc_fgmres(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
-                          _p(F) if F is not None else None, C.c_int(0 if prec == "lusgs" else 1), _p(b),
-                          x.ctypes.data_as(C.c_void_p), C.c_double(tol), C.c_int(m), C.byref(resid))
+    it = lib().orc_fgmres_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
+                            _p(F) if F is not None else None, C.c_int(0 if prec == "lusgs" else 1), _p(b),
+                            x.ctypes.data_as(C.c_void_p), C.c_double(tol), C.c_int(m), C.byref(resid),
+                            *_parts(N, part_ptr))
     return x.reshape(N, nb), it, resid.value
 
 
@@ -257,7 +284,7 @@ def bsr_pattern(N, edges):
     return np.cumsum(rp), c
 
 
-def implicit_step(mech, nDim, ns, mesh, st, cfg, pattern=None):
+def implicit_step(mech, nDim, ns, mesh, st, cfg, pattern=None, part_ptr=None):
     """One outer iteration of the implicit reactive RANS hot path, restated on the CPU in the order
     bench.py runs it on the device: LSQ gradient, SetTime_Step, Upwind/Viscous/Source residuals with
     Jacobians, assembly, ILU(0) build, FGMRES(m) and the clipped relaxed update
@@ -276,7 +303,7 @@ def implicit_step(mech, nDim, ns, mesh, st, cfg, pattern=None):
     rs, Js = source_cells(mech, nDim, st["V"], st["dTdU"], mesh["volume"], st["turb_omega"], True, True,
                           [cfg["c_mu"], cfg["pasr_lb"], 1, 1, 1])
     R, A, rhs = assemble(rp, col, mesh["edges"], rc, Jci, Jcj, rv, Jvi, Jvj, rs, Js, mesh["volume"], dt, nb)
-    F = ilu_build(rp, col, A)
-    x, it, res = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"])
+    F = ilu_build(rp, col, A, part_ptr)
+    x, it, res = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"], part_ptr=part_ptr)
     U = update(st["U"], x, nDim, 0, cfg["relaxation"], mesh["volume"], dt)
     return U, dict(grad=G, dt=dt, res=R, jac=A, rhs=rhs, sol=x, lin_iters=it, lin_resid=res)

@@ -1441,26 +1441,55 @@ static int64_t find_diag(const int64_t* rp, const int64_t* col, int64_t i) {
   return -1;
 }
 
+// Partitions: rows are grouped in contiguous ranges [part_ptr[p], part_ptr[p+1]) that stand for the
+// reference's MPI ranks (each rank's domain points, in the same relative order). A rank's matrix has
+// its domain rows with columns on domain AND halo points; the preconditioners see the halo as follows
+// (matrix_structure.cpp):
+//   ILU(0) build/apply (:1397, :1416, :1472, :1489-1492): halo columns are skipped (block Jacobi);
+//   LU-SGS (:1673-1709): LowerProduct only ever meets domain columns (halos are numbered after the
+//   domain points), UpperProduct (:743-757) meets every halo column and reads the halo copy of x*
+//   exchanged after the forward sweep (SendReceive_Solution :1687). The halo columns of a row come
+//   after its domain columns, in increasing global index.
+// np = 1, part_ptr = {0, N} is the serial reference.
+struct Parts {
+  std::vector<int64_t> lo, hi;
+  Parts(int64_t N, int64_t np, const int64_t* pp) : lo(N), hi(N) {
+    if (!pp || np <= 1) {
+      std::fill(lo.begin(), lo.end(), 0);
+      std::fill(hi.begin(), hi.end(), N);
+      return;
+    }
+    for (int64_t p = 0; p < np; ++p)
+      for (int64_t i = pp[p]; i < pp[p + 1]; ++i) {
+        lo[i] = pp[p];
+        hi[i] = pp[p + 1];
+      }
+  }
+};
+
 // ComputeLU_SGSPreconditioner (:1673-1709)
-void orc_lusgs(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* b,
-               double* x) {
-  std::vector<double> aux(nb), prv(nb);
-  for (int64_t i = 0; i < N; ++i) {
+void orc_lusgs_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* b,
+                 double* x, int64_t np, const int64_t* part_ptr) {
+  Parts P(N, np, part_ptr);
+  std::vector<double> aux(nb), prv(nb), xs(N * nb);
+  auto blockprod = [&](int64_t k, const double* xv) {
+    const double* blk = A + k * nb * nb;
+    for (int a = 0; a < nb; ++a) {
+      double pb = 0.0;
+      for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * xv[c];
+      prv[a] += pb;
+    }
+  };
+  for (int64_t i = 0; i < N; ++i) {  // (D+L) x* = b, per rank
     for (int a = 0; a < nb; ++a) prv[a] = 0.0;
     for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
-      if (col[k] < i) {
-        const double* blk = A + k * nb * nb;
-        for (int a = 0; a < nb; ++a) {
-          double pb = 0.0;
-          for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * x[col[k] * nb + c];
-          prv[a] += pb;
-        }
-      }
+      if (col[k] < i && col[k] >= P.lo[i]) blockprod(k, x + col[k] * nb);
     for (int a = 0; a < nb; ++a) aux[a] = b[i * nb + a] - prv[a];
     gauss_elim(nb, A + find_diag(rp, col, i) * nb * nb, aux.data());
     for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
   }
-  for (int64_t i = N - 1; i >= 0; --i) {
+  std::memcpy(xs.data(), x, sizeof(double) * N * nb);  // halo copies of x*
+  for (int64_t i = N - 1; i >= 0; --i) {  // (D+U) x = D x*
     const double* dblk = A + find_diag(rp, col, i) * nb * nb;
     for (int a = 0; a < nb; ++a) {
       double pb = 0.0;
@@ -1469,18 +1498,18 @@ void orc_lusgs(int64_t N, int nb, const int64_t* rp, const int64_t* col, const d
     }
     for (int a = 0; a < nb; ++a) prv[a] = 0.0;
     for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
-      if (col[k] > i) {
-        const double* blk = A + k * nb * nb;
-        for (int a = 0; a < nb; ++a) {
-          double pb = 0.0;
-          for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * x[col[k] * nb + c];
-          prv[a] += pb;
-        }
-      }
+      if (col[k] > i && col[k] < P.hi[i]) blockprod(k, x + col[k] * nb);
+    for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+      if (col[k] < P.lo[i] || col[k] >= P.hi[i]) blockprod(k, xs.data() + col[k] * nb);
     for (int a = 0; a < nb; ++a) aux[a] -= prv[a];
     gauss_elim(nb, dblk, aux.data());
     for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
   }
+}
+
+void orc_lusgs(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* b,
+               double* x) {
+  orc_lusgs_p(N, nb, rp, col, A, b, x, 1, nullptr);
 }
 
 static void inverse_diag(int nb, const double* D, double* inv) {  // InverseDiagonalBlock_ILUMatrix (:1180-1228)
@@ -1508,8 +1537,10 @@ static void mat_vec(int nb, const double* a, const double* x, double* y) {
   }
 }
 
-// BuildILUPreconditioner (:1368-1451), including the left-multiply quirk at :1432-1436.
-void orc_ilu_build(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, double* F) {
+// BuildILUPreconditioner (:1368-1451), including the left-multiply quirk at :1432-1436; per rank.
+void orc_ilu_build_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, double* F,
+                     int64_t np, const int64_t* part_ptr) {
+  Parts P(N, np, part_ptr);
   const int64_t nnzb = rp[N];
   std::memcpy(F, A, sizeof(double) * nnzb * nb * nb);
   std::vector<double> inv(nb * nb), w(nb * nb), blk(nb * nb);
@@ -1518,16 +1549,17 @@ void orc_ilu_build(int64_t N, int nb, const int64_t* rp, const int64_t* col, con
       if (col[k] == j) return F + k * nb * nb;
     return nullptr;
   };
-  for (int64_t i = 1; i < N; ++i)
+  for (int64_t i = 0; i < N; ++i) {
+    if (i == P.lo[i]) continue;  // the loop of each rank starts at its second row
     for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
       const int64_t j = col[k];
-      if (j < i) {
+      if (j < i && j >= P.lo[i]) {
         double* Bij = F + k * nb * nb;
         inverse_diag(nb, findb(j, j), inv.data());
         mat_mat(nb, Bij, inv.data(), w.data());
         for (int64_t kk = rp[j]; kk < rp[j + 1]; ++kk) {
           const int64_t kp = col[kk];
-          if (kp >= j) {
+          if (kp >= j && kp < P.hi[i]) {
             const double* Bjk = F + kk * nb * nb;
             mat_mat(nb, Bjk, w.data(), blk.data());
             double* Bik = findb(i, kp);
@@ -1538,30 +1570,41 @@ void orc_ilu_build(int64_t N, int nb, const int64_t* rp, const int64_t* col, con
         std::memcpy(Bij, w.data(), sizeof(double) * nb * nb);
       }
     }
+  }
 }
 
-// ComputeILUPreconditioner (:1453-1515)
-void orc_ilu_apply(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* F, const double* b,
-                   double* x) {
+void orc_ilu_build(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, double* F) {
+  orc_ilu_build_p(N, nb, rp, col, A, F, 1, nullptr);
+}
+
+// ComputeILUPreconditioner (:1453-1515), per rank.
+void orc_ilu_apply_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* F, const double* b,
+                     double* x, int64_t np, const int64_t* part_ptr) {
+  Parts P(N, np, part_ptr);
   std::vector<double> aux(nb), sum(nb), inv(nb * nb);
   for (int64_t q = 0; q < N * nb; ++q) x[q] = b[q];
-  for (int64_t i = 1; i < N; ++i)
+  for (int64_t i = 0; i < N; ++i) {
+    if (i == P.lo[i]) continue;
     for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
       const int64_t j = col[k];
-      if (j < i) {
+      if (j < i && j >= P.lo[i]) {
         mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
         for (int a = 0; a < nb; ++a) x[i * nb + a] -= aux[a];
       }
     }
+  }
   auto diag = [&](int64_t i) { return F + find_diag(rp, col, i) * nb * nb; };
-  inverse_diag(nb, diag(N - 1), inv.data());
-  mat_vec(nb, inv.data(), x + (N - 1) * nb, aux.data());
-  for (int a = 0; a < nb; ++a) x[(N - 1) * nb + a] = aux[a];
-  for (int64_t i = N - 2; i >= 0; --i) {
+  for (int64_t i = N - 1; i >= 0; --i) {
+    if (i == P.hi[i] - 1) {  // last row of the rank
+      inverse_diag(nb, diag(i), inv.data());
+      mat_vec(nb, inv.data(), x + i * nb, aux.data());
+      for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+      continue;
+    }
     for (int a = 0; a < nb; ++a) sum[a] = 0.0;
     for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
       const int64_t j = col[k];
-      if (j >= i + 1) {
+      if (j >= i + 1 && j < P.hi[i]) {
         mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
         for (int a = 0; a < nb; ++a) sum[a] += aux[a];
       }
@@ -1573,17 +1616,49 @@ void orc_ilu_apply(int64_t N, int nb, const int64_t* rp, const int64_t* col, con
   }
 }
 
+void orc_ilu_apply(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* F, const double* b,
+                   double* x) {
+  orc_ilu_apply_p(N, nb, rp, col, F, b, x, 1, nullptr);
+}
+
 // FGMRES_LinSolver (linear_solvers_structure.cpp:309-463) + ModGramSchmidt (:87-186), Givens (:37-71),
 // SolveReduced (:73-85). prec: 0 = LU-SGS on A, 1 = ILU0 with factor F. x in/out (initial guess).
 // Returns iterations; *resid = final beta. Returns -1 on divergence (MGS exit, :108-150).
-int orc_fgmres(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F, int prec,
-               const double* b, double* x, double tol, int m, double* resid) {
-  const int64_t n = N * nb;
-  auto dotp = [&](const double* a, const double* c) {
+// Inner product used by FGMRES. Mode 0 (default): CSysVector dotProd (vector_structure.cpp:397-419),
+// a sequential sum. Mode 1: the summation order of the device kernels (rx_krylov.hip k_dot_part /
+// k_dot_fin: 512 x 256 grid-stride partial sums, pairwise tree in each block, then a pairwise tree
+// over the 512 partials) — lets tests separate algorithmic parity (bitwise) from reduction order.
+static int g_dot_mode = 0;
+void orc_set_dot_mode(int mode) { g_dot_mode = mode; }
+double orc_dot(int64_t n, const double* a, const double* c) {
+  if (g_dot_mode == 0) {
     double s = 0.0;
     for (int64_t q = 0; q < n; ++q) s += a[q] * c[q];
     return s;
-  };
+  }
+  const int NB = 512, BS = 256;
+  std::vector<double> part(NB), sh(BS);
+  for (int b = 0; b < NB; ++b) {
+    for (int t = 0; t < BS; ++t) {
+      double s = 0.0;
+      for (int64_t q = (int64_t)b * BS + t; q < n; q += (int64_t)NB * BS) s += a[q] * c[q];
+      sh[t] = s;
+    }
+    for (int w = BS / 2; w > 0; w >>= 1)
+      for (int t = 0; t < w; ++t) sh[t] += sh[t + w];
+    part[b] = sh[0];
+  }
+  for (int t = 0; t < BS; ++t) sh[t] = part[t] + part[t + BS];
+  for (int w = BS / 2; w > 0; w >>= 1)
+    for (int t = 0; t < w; ++t) sh[t] += sh[t + w];
+  return sh[0];
+}
+
+int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F,
+                 int prec, const double* b, double* x, double tol, int m, double* resid, int64_t np,
+                 const int64_t* part_ptr) {
+  const int64_t n = N * nb;
+  auto dotp = [&](const double* a, const double* c) { return orc_dot(n, a, c); };
   auto norm = [&](const double* a) { return std::sqrt(dotp(a, a)); };
   std::vector<std::vector<double>> w(m + 1, std::vector<double>(n)), z(m + 1, std::vector<double>(n));
   std::vector<double> g(m + 1, 0.0), sn(m + 1, 0.0), cs(m + 1, 0.0), y(m, 0.0);
@@ -1603,8 +1678,8 @@ int orc_fgmres(int64_t N, int nb, const int64_t* rp, const int64_t* col, const d
   int i = 0;
   for (i = 0; i < m; ++i) {
     if (beta < tol * norm0) break;
-    if (prec == 0) orc_lusgs(N, nb, rp, col, A, w[i].data(), z[i].data());
-    else orc_ilu_apply(N, nb, rp, col, F, w[i].data(), z[i].data());
+    if (prec == 0) orc_lusgs_p(N, nb, rp, col, A, w[i].data(), z[i].data(), np, part_ptr);
+    else orc_ilu_apply_p(N, nb, rp, col, F, w[i].data(), z[i].data(), np, part_ptr);
     orc_bsr_spmv(N, nb, rp, col, A, z[i].data(), w[i + 1].data());
     // ModGramSchmidt
     const double reorth = 0.98;
@@ -1674,6 +1749,11 @@ int orc_fgmres(int64_t N, int nb, const int64_t* rp, const int64_t* col, const d
     for (int64_t q = 0; q < n; ++q) x[q] += y[k] * z[k][q];
   *resid = beta;
   return i;
+}
+
+int orc_fgmres(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F, int prec,
+               const double* b, double* x, double tol, int m, double* resid) {
+  return orc_fgmres_p(N, nb, rp, col, A, F, prec, b, x, tol, m, resid, 1, nullptr);
 }
 
 static int64_t blk_of(const int64_t* rp, const int64_t* col, int64_t i, int64_t j) {
