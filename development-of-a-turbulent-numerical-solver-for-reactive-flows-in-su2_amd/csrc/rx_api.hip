@@ -221,19 +221,72 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
         part_lvl[p + 1] = part_lvl[p] + maxl + 1;
       }
       S.nlevels = part_lvl[np];
+      std::vector<int32_t> slot(4 * order.size());
+      for (size_t r = 0; r < order.size(); ++r) {
+        const int32_t i = order[r];
+        slot[4 * r] = i;
+        slot[4 * r + 1] = klo[i];
+        slot[4 * r + 2] = (int32_t)diag[i];
+        slot[4 * r + 3] = khi[i];
+      }
       int rc2 = dupload(ctx, &S.part_lvl, part_lvl.data(), part_lvl.size());
       if (!rc2) rc2 = dupload(ctx, &S.lvl_ptr, lvl_ptr.data(), lvl_ptr.size());
       if (!rc2) rc2 = dupload(ctx, &S.rows, order.data(), order.size());
+      if (!rc2) rc2 = dupload(ctx, &S.slot, slot.data(), slot.size());
       return rc2;
     };
+    {
+      std::vector<int32_t> pp32(np + 1);
+      int maxpart = 1;
+      for (int64_t p = 0; p <= np; ++p) pp32[p] = (int32_t)ctx->h_part_ptr[p];
+      int maxnz = 1;
+      for (int64_t p = 0; p < np; ++p) {
+        maxpart = std::max(maxpart, pp32[p + 1] - pp32[p]);
+        maxnz = std::max(maxnz, (int)(ctx->h_rp[pp32[p + 1]] - ctx->h_rp[pp32[p]]));
+      }
+      ctx->maxpart = maxpart;
+      ctx->maxpart_nnzb = maxnz;
+      CK(dupload(ctx, &ctx->part_ptr, pp32.data(), pp32.size()));
+      int v = 0;
+      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && v > 0)
+        ctx->lds_max = v;
+      CK(rx_la_prepare(ctx));
+    }
     CK(schedule(true, ctx->fs));
     CK(schedule(false, ctx->bs));
     CK(dupload(ctx, &ctx->klo, klo.data(), N));
     CK(dupload(ctx, &ctx->khi, khi.data(), N));
-    const size_t per_wave = sizeof(double) * (size_t)(rowmax + 2) * nv * nv;
-    if (per_wave > 64 * 1024) CK(RX_ERR_ARG);  // a row with more blocks than one wave's LDS slice
+    // ILU(0) update plan: for each intra lower block k = (i, j): upper blocks kk = (j, kp), kp > j
+    // inside row i's partition and present in row i, with their BSR index pos in row i
+    {
+      std::vector<int32_t> uptr(ctx->nnzb + 1, 0), upd;
+      for (int64_t i = 0; i < N; ++i) {
+        for (int32_t k = (int32_t)ctx->h_rp[i]; k < (int32_t)ctx->h_rp[i + 1]; ++k) {
+          if (k >= klo[i] && k < (int32_t)diag[i]) {
+            const int32_t j = col32[k];
+            for (int32_t kk = (int32_t)diag[j] + 1; kk < khi[j]; ++kk) {
+              const int32_t kp = col32[kk];
+              const auto& r = rows[i];
+              const auto it = std::lower_bound(r.begin(), r.end(), kp);
+              if (it != r.end() && *it == kp) {
+                const int32_t pos = (int32_t)(ctx->h_rp[i] + (it - r.begin()));
+                if (pos >= klo[i] && pos < khi[i]) {
+                  upd.push_back(kk);
+                  upd.push_back(pos);
+                }
+              }
+            }
+          }
+          uptr[k + 1] = (int32_t)(upd.size() / 2);
+        }
+      }
+      CK(dupload(ctx, &ctx->upd_ptr, uptr.data(), uptr.size()));
+      CK(dupload(ctx, &ctx->upd, upd.data(), upd.size()));
+    }
+    const size_t per_wave = sizeof(double) * (size_t)(rowmax + 7) * nv * nv;
+    if (per_wave > (size_t)ctx->lds_max) CK(RX_ERR_ARG);  // a row with more blocks than one wave's LDS slice
     ctx->ilu_waves = (int)std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1, ctx->fs.maxwidth),
-                                                                (64 * 1024) / per_wave}));
+                                                                (size_t)ctx->lds_max / per_wave}));
   }
   // LSQ neighbour lists (reference order) and boundary vertices per node
   std::vector<int32_t> nptr(N + 1), nbr(mesh->nbr_ptr[N]);
@@ -363,8 +416,9 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->nbr_ptr,
-                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi,
+                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
+                  ctx->fs.slot, ctx->bs.slot,
                   ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
@@ -499,7 +553,7 @@ int rx_ilu0_build(rx_ctx* ctx) {
 int rx_ilu0_apply(rx_ctx* ctx, rx_field b, rx_field x) {
   if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_ILU_APPLY);
-  return rx_la_ilu_apply(ctx, ctx->f[b], ctx->f[x], nullptr);
+  return rx_la_ilu_apply(ctx, ctx->f[b], ctx->f[x], nullptr, nullptr);
 }
 
 int rx_lusgs_apply(rx_ctx* ctx, rx_field b, rx_field x) {
@@ -508,7 +562,7 @@ int rx_lusgs_apply(rx_ctx* ctx, rx_field b, rx_field x) {
   if (rc) return rc;
   RxPhase ph(ctx, RX_K_LUSGS);
   if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
-  return rx_la_lusgs(ctx, ctx->f[RX_F_JAC], ctx->f[b], ctx->f[x], nullptr);
+  return rx_la_lusgs(ctx, ctx->f[RX_F_JAC], ctx->f[b], ctx->f[x], nullptr, nullptr);
 }
 
 int rx_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {

@@ -43,9 +43,15 @@ struct rx_ctx {
   // the columns inside its own partition [klo, khi) (columns are sorted, partitions contiguous)
   int npart = 1;
   std::vector<int64_t> h_part_ptr;
+  int32_t* part_ptr = nullptr;  // [npart+1] device copy
+  int maxpart = 1;              // rows of the largest partition
+  int maxpart_nnzb = 1;         // BSR blocks of the largest partition's rows
+  int lds_max = 65536;          // dynamic LDS bytes a workgroup may use on this device
   int32_t* klo = nullptr;       // [N]
   int32_t* khi = nullptr;       // [N]
   int rowmax = 1;               // max khi - klo
+  int32_t* upd_ptr = nullptr;   // [nnzb+1] ILU update plan per lower block (rx_sweeps.hip)
+  int32_t* upd = nullptr;       // [2 * n_upd] (kk, pos) pairs
   int ilu_waves = 1;            // wavefronts per workgroup of the ILU factorisation
   // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
   // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])
@@ -53,10 +59,12 @@ struct rx_ctx {
     int32_t* part_lvl = nullptr;
     int32_t* lvl_ptr = nullptr;
     int32_t* rows = nullptr;
+    int32_t* slot = nullptr;      // [rows][4] {row, klo, diag, khi} in schedule order
     int nlevels = 0, maxwidth = 0;
   } fs, bs;
   double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)
   double* xstar = nullptr;      // [N][nVar] LU-SGS forward-sweep result (halo values)
+  long long* ilu_trace = nullptr;  // debug phase trace of the ILU factorisation (rx_debug_ilu_trace)
 
   // ---- mechanism
   rx::DevMech mech{};
@@ -140,10 +148,11 @@ int rx_launch_time_step(rx_ctx* ctx);
 int rx_check_error(rx_ctx* ctx);
 // linear algebra (rx_linalg.hip)
 int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y, const int* skip);
-int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, const int* skip);
+int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, int* done, const int* conv);
 int rx_la_diag_factor(rx_ctx* ctx, const double* A);
 int rx_la_ilu_build(rx_ctx* ctx);
-int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, const int* skip);
+int rx_la_prepare(rx_ctx* ctx);
+int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv);
 double* rx_invd_buf(rx_ctx* ctx);
 int rx_la_krylov_alloc(rx_ctx* ctx, int m);
 int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m);

@@ -82,6 +82,15 @@ __device__ __host__ inline void molar_from_mass(const DevMech& m, const double* 
 // The per-edge scalars are computed once; the residual and the Jacobian entries are evaluated
 // from them in exactly the reference's operation order.
 // ------------------------------------------------------------------------------------------------
+// Runtime index into a small register array without dynamic indexing (keeps it out of scratch).
+template <int N>
+__device__ __host__ inline double pick(const double* a, int idx) {
+  double v = a[0];
+#pragma unroll
+  for (int q = 1; q < N; ++q) v = (idx == q) ? a[q] : v;
+  return v;
+}
+
 struct AusmEdge {
   double Area, UN[3];
   double rho_i, rho_j, p_i, p_j, pv_i, pv_j;
@@ -187,7 +196,7 @@ struct AusmCol {
 };
 
 template <int NDIM>
-__device__ __host__ inline AusmCol ausm_col(const AusmEdge& s, const double* Si, const double* Sj, int b) {
+__device__ __host__ inline AusmCol ausm_col_impl(const AusmEdge& s, double Sib, double Sjb, int b) {
   const double kP = 0.25, sigma = 1.0, beta = 0.125, Ku = 0.75;
   const double mL = s.mL, mR = s.mR, mss = s.mss, fa = s.fa, alpha = s.alpha;
   const double rho_i = s.rho_i, rho_j = s.rho_j;
@@ -196,8 +205,9 @@ __device__ __host__ inline AusmCol ausm_col(const AusmEdge& s, const double* Si,
     MLD = -mL / rho_i;
     MRD = -mR / rho_j;
   } else if (b <= NDIM) {
-    MLD = s.UN[b - 1] / (rho_i * mss);
-    MRD = s.UN[b - 1] / (rho_j * mss);
+    const double unb = pick<NDIM>(s.UN, b - 1);
+    MLD = unb / (rho_i * mss);
+    MRD = unb / (rho_j * mss);
   }
   double MPL, MPR;
   if (fabs(mL) < 1.0) MPL = MLD * (0.5 * (mL + 1.0) + 4.0 * beta * mL * (mL * mL - 1.0));
@@ -212,9 +222,9 @@ __device__ __host__ inline AusmCol ausm_col(const AusmEdge& s, const double* Si,
   const double MD = 0.5 * (rho_i + rho_j);
   const double dp = s.p_j - s.p_i;
   double MEL = -kP / (mss * mss * fa * fa * MD * MD) *
-               ((s.fpos * sigma * mL * MLD * dp * fa * MD) + (s.factor * Si[b] * fa * MD) + (s.factor * dp * MD * SL));
+               ((s.fpos * sigma * mL * MLD * dp * fa * MD) + (s.factor * Sib * fa * MD) + (s.factor * dp * MD * SL));
   double MER = kP / (mss * mss * fa * fa * MD * MD) *
-               ((s.fpos * sigma * mR * MRD * (s.p_i - s.p_j) * fa * MD) + (s.factor * Sj[b] * fa * MD) -
+               ((s.fpos * sigma * mR * MRD * (s.p_i - s.p_j) * fa * MD) + (s.factor * Sjb * fa * MD) -
                 (s.factor * dp * MD * SR));
   if (b == 0) {
     MEL -= kP / (mss * mss * fa * MD * MD) * 0.5 * s.factor * dp;
@@ -239,12 +249,24 @@ __device__ __host__ inline AusmCol ausm_col(const AusmEdge& s, const double* Si,
     PEL += Ku * s.pRM * mss * s.pLP * fa * (dvn + (rho_i + rho_j) * s.pv_i / rho_i);
     PER += Ku * s.pLP * mss * s.pRM * fa * (dvn - (rho_i + rho_j) * s.pv_j / rho_j);
   } else if (b <= NDIM) {
-    PEL -= Ku * s.pRM * mss * s.pLP * fa * (rho_i + rho_j) * s.UN[b - 1] / rho_i;
-    PER += Ku * s.pLP * mss * s.pRM * fa * (rho_i + rho_j) * s.UN[b - 1] / rho_j;
+    const double unb = pick<NDIM>(s.UN, b - 1);
+    PEL -= Ku * s.pRM * mss * s.pLP * fa * (rho_i + rho_j) * unb / rho_i;
+    PER += Ku * s.pLP * mss * s.pRM * fa * (rho_i + rho_j) * unb / rho_j;
   }
-  c.PDL = s.pLP * Si[b] + s.p_i * PPL - PEL;
-  c.PDR = s.pRM * Sj[b] + s.p_j * PPR - PER;
+  c.PDL = s.pLP * Sib + s.p_i * PPL - PEL;
+  c.PDR = s.pRM * Sjb + s.p_j * PPR - PER;
   return c;
+}
+
+template <int NDIM>
+__device__ __host__ inline AusmCol ausm_col(const AusmEdge& s, const double* Si, const double* Sj, int b) {
+  return ausm_col_impl<NDIM>(s, Si[b], Sj[b], b);
+}
+
+// ausm_col for one column b given Si[b], Sj[b] (same arithmetic as ausm_col).
+template <int NDIM>
+__device__ __host__ inline AusmCol ausm_col_b(const AusmEdge& s, double Sib, double Sjb, int b) {
+  return ausm_col_impl<NDIM>(s, Sib, Sjb, b);
 }
 
 // Jacobian entry (a, b) of Jac_i (left) and Jac_j (right), accumulation order of :295-374.

@@ -68,52 +68,57 @@ __global__ __launch_bounds__(kBlock) void k_ausm_node(int N, const int32_t* __re
   if (bad) set_err(err, ERR_NAN, i);
 }
 
-// a1 implicit: edge-parallel flux + both Jacobians into per-edge scratch.
+// a1 implicit: flux + both Jacobians into per-edge scratch. A team of 16 lanes per edge (4 edges
+// per wavefront): every lane evaluates the edge scalars, lane v < nVar owns residual component v and
+// Jacobian column b = v, so for every row a the team stores one contiguous row segment of Ji and Jj.
+constexpr int kAusmTeam = 16;
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) void k_ausm_edge(int E, const int32_t* __restrict__ edges,
                                                       const double* __restrict__ normal, const double* __restrict__ V,
                                                       const double* __restrict__ dPdU, double mInfty,
                                                       double* __restrict__ F, double* __restrict__ Jac, int* err) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nVar2 = nVar * nVar;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  static_assert(nVar <= kAusmTeam, "team too small");
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = gt / kAusmTeam, b = gt % kAusmTeam;
   if (e >= E) return;
   const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
-  double Vi[nPV], Vj[nPV], Si[nVar], Sj[nVar];
+  double Vi[nPV], Vj[nPV];
 #pragma unroll
   for (int v = 0; v < nPV; ++v) {
     Vi[v] = V[(size_t)n0 * nPV + v];
     Vj[v] = V[(size_t)n1 * nPV + v];
-  }
-#pragma unroll
-  for (int v = 0; v < nVar; ++v) {
-    Si[v] = dPdU[(size_t)n0 * nVar + v];
-    Sj[v] = dPdU[(size_t)n1 * nVar + v];
   }
   double nrm[NDIM];
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
   AusmEdge s;
   ausm_scalars<NDIM>(Vi, Vj, nrm, mInfty, s);
+  if (b >= nVar) return;
   bool bad = false;
-#pragma unroll
-  for (int v = 0; v < nVar; ++v) {
-    const double r = ausm_res<NDIM>(s, Vi, Vj, v);
+  {
+    // ausm_res for the runtime component b, with phi read by index (no dynamic register indexing)
+    const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
+    const double pi = b == 0 ? 1.0 : V[(size_t)n0 * nPV + pidx];
+    const double pj = b == 0 ? 1.0 : V[(size_t)n1 * nPV + pidx];
+    double r = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
+    if (b >= 1 && b <= NDIM) r += s.pLF * pick<NDIM>(s.UN, b - 1) * s.Area;
     bad |= isnan(r);
-    F[(size_t)e * nVar + v] = r;
+    F[(size_t)e * nVar + b] = r;
   }
+  // dP/dU of both nodes: only column b is needed by this lane's Jacobian column
+  const double sib = dPdU[(size_t)n0 * nVar + b], sjb = dPdU[(size_t)n1 * nVar + b];
+  const AusmCol c = ausm_col_b<NDIM>(s, sib, sjb, b);
   double* Ji = Jac + (size_t)e * 2 * nVar2;
   double* Jj = Ji + nVar2;
-  for (int b = 0; b < nVar; ++b) {
-    const AusmCol c = ausm_col<NDIM>(s, Si, Sj, b);
 #pragma unroll
-    for (int a = 0; a < nVar; ++a) {
-      double ji, jj;
-      ausm_jac_entry<NDIM>(s, c, ausm_phi<NDIM>(Vi, Vi[NDIM + 3], a), ausm_phi<NDIM>(Vj, Vj[NDIM + 3], a), Si[b],
-                           Sj[b], a, b, &ji, &jj);
-      bad |= isnan(ji) || isnan(jj);
-      Ji[a * nVar + b] = ji;
-      Jj[a * nVar + b] = jj;
-    }
+  for (int a = 0; a < nVar; ++a) {
+    double ji, jj;
+    ausm_jac_entry<NDIM>(s, c, ausm_phi<NDIM>(Vi, Vi[NDIM + 3], a), ausm_phi<NDIM>(Vj, Vj[NDIM + 3], a), sib, sjb,
+                         a, b, &ji, &jj);
+    bad |= isnan(ji) || isnan(jj);
+    Ji[a * nVar + b] = ji;
+    Jj[a * nVar + b] = jj;
   }
   if (bad) set_err(err, ERR_NAN, e);
 }
@@ -223,11 +228,16 @@ __global__ __launch_bounds__(128) void k_source(int N, const double* __restrict_
   else if (bad) set_err(err, ERR_NAN, i);
 }
 
-// Implicit assembly: one thread per (node i, block row a). Residual component a and block row a
-// of every block in BSR row i, in the reference's accumulation order:
+// Implicit assembly: a team of 128 lanes per node, lane t < nVar^2 owns entry t of every block of
+// the node's BSR row (coalesced block reads and writes), lane t < nVar also owns residual component
+// t. Reference accumulation order:
 //   R  = 0 + conv(edge order) - visc(edge order) + source
 //   Aii = 0 + conv(edge order) + visc(edge order) + source     (AddVal2Diag comes later)
 //   A(n0,n1) = (0 + Jc_j) - Jv_j ;  A(n1,n0) = (0 - Jc_i) + Jv_i
+template <int NVAR>
+constexpr int asm_team() {
+  return NVAR * NVAR <= 64 ? 64 : (NVAR * NVAR <= 128 ? 128 : 256);
+}
 template <int NVAR>
 __global__ __launch_bounds__(kBlock) void k_assemble(int N, const int32_t* __restrict__ adj_ptr,
                                                      const int32_t* __restrict__ adj,
@@ -237,57 +247,50 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int N, const int32_t* __res
                                                      const double* __restrict__ Jv, const double* __restrict__ Js,
                                                      const double* __restrict__ Rsrc, double* __restrict__ R,
                                                      double* __restrict__ A, int visc, int src) {
-  constexpr int nVar2 = NVAR * NVAR;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N * NVAR) return;
-  const int i = t / NVAR, a = t - i * NVAR;
-  double r = 0.0;
-  double D[NVAR];
-#pragma unroll
-  for (int b = 0; b < NVAR; ++b) D[b] = 0.0;
+  constexpr int nVar2 = NVAR * NVAR, kTeam = asm_team<NVAR>();
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = gt / kTeam, t = gt % kTeam;
+  if (i >= N || t >= nVar2) return;
+  const bool res = t < NVAR;
+  double r = 0.0, D = 0.0;
   const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  // convective pass: residual and diagonal (own-side blocks)
   for (int k = k0; k < k1; ++k) {
     const int ad = adj[k];
     const size_t e = (size_t)(ad >> 1);
     const int side = ad & 1;
-    const double f = Fc[e * NVAR + a];
-    r = side ? r - f : r + f;
-    const double* jd = Jc + (e * 2 + side) * nVar2 + (size_t)a * NVAR;       // own-side block: Ji for n0, Jj for n1
-    const double* jo = Jc + (e * 2 + (side ^ 1)) * nVar2 + (size_t)a * NVAR; // other-side block
-    double* off = A + adj_blk[k] * nVar2 + (size_t)a * NVAR;
-#pragma unroll
-    for (int b = 0; b < NVAR; ++b) {
-      D[b] = side ? D[b] - jd[b] : D[b] + jd[b];
-      off[b] = side ? 0.0 - jo[b] : 0.0 + jo[b];
+    if (res) {
+      const double f = Fc[e * NVAR + t];
+      r = side ? r - f : r + f;
     }
+    const double jd = Jc[(e * 2 + side) * nVar2 + t];  // own side: Ji for n0, Jj for n1
+    D = side ? D - jd : D + jd;
   }
-  if (visc) {
-    for (int k = k0; k < k1; ++k) {
-      const int ad = adj[k];
-      const size_t e = (size_t)(ad >> 1);
-      const int side = ad & 1;
-      const double f = Fv[e * NVAR + a];
-      r = side ? r + f : r - f;
-      const double* jd = Jv + (e * 2 + side) * nVar2 + (size_t)a * NVAR;
-      const double* jo = Jv + (e * 2 + (side ^ 1)) * nVar2 + (size_t)a * NVAR;
-      double* off = A + adj_blk[k] * nVar2 + (size_t)a * NVAR;
-#pragma unroll
-      for (int b = 0; b < NVAR; ++b) {
-        D[b] = side ? D[b] + jd[b] : D[b] - jd[b];
-        off[b] = side ? off[b] + jo[b] : off[b] - jo[b];
+  // viscous pass: residual, diagonal, and each off-diagonal block written once as (0 +- Jc) -+ Jv
+  for (int k = k0; k < k1; ++k) {
+    const int ad = adj[k];
+    const size_t e = (size_t)(ad >> 1);
+    const int side = ad & 1;
+    const double joc = Jc[(e * 2 + (side ^ 1)) * nVar2 + t];  // other side
+    double off = side ? 0.0 - joc : 0.0 + joc;
+    if (visc) {
+      if (res) {
+        const double f = Fv[e * NVAR + t];
+        r = side ? r + f : r - f;
       }
+      const double jd = Jv[(e * 2 + side) * nVar2 + t];
+      const double jov = Jv[(e * 2 + (side ^ 1)) * nVar2 + t];
+      D = side ? D + jd : D - jd;
+      off = side ? off + jov : off - jov;
     }
+    A[adj_blk[k] * nVar2 + t] = off;
   }
   if (src) {
-    r += Rsrc[(size_t)i * NVAR + a];
-    const double* js = Js + (size_t)i * nVar2 + (size_t)a * NVAR;
-#pragma unroll
-    for (int b = 0; b < NVAR; ++b) D[b] += js[b];
+    if (res) r += Rsrc[(size_t)i * NVAR + t];
+    D += Js[(size_t)i * nVar2 + t];
   }
-  R[(size_t)i * NVAR + a] = r;
-  double* dd = A + diag[i] * nVar2 + (size_t)a * NVAR;
-#pragma unroll
-  for (int b = 0; b < NVAR; ++b) dd[b] = D[b];
+  if (res) R[(size_t)i * NVAR + t] = r;
+  A[diag[i] * nVar2 + t] = D;
 }
 
 // a12: weighted least-squares gradient of (T, u, v, P, X_s) per node.
@@ -590,7 +593,7 @@ int rx_launch_ausm_node(rx_ctx* ctx) {
 
 int rx_launch_ausm_edge(rx_ctx* ctx) {
   if (ctx->nDim != 2) return RX_ERR_ARG;
-  RX_NS_SWITCH(ctx->ns, (k_ausm_edge<NS_, 2><<<blocks(ctx->E), kBlock, 0, ctx->stream>>>(
+  RX_NS_SWITCH(ctx->ns, (k_ausm_edge<NS_, 2><<<blocks(ctx->E * kAusmTeam), kBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
                             ctx->cfg.mach_inf, ctx->fconv, ctx->jconv, ctx->err)));
   RX_HIP(hipGetLastError());
@@ -633,11 +636,10 @@ int rx_launch_source(rx_ctx* ctx) {
 
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   const int nv = ctx->nVar;
-  const int nb = blocks(ctx->N * nv);
   switch (nv) {
 #define RX_ASM(NV)                                                                                          \
   case NV:                                                                                                  \
-    k_assemble<NV><<<nb, kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk,        \
+    k_assemble<NV><<<blocks(ctx->N * asm_team<NV>()), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk,        \
                                                    ctx->diag, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, \
                                                    ctx->jsrc, ctx->rsrc, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], \
                                                    with_visc, with_src);                                      \

@@ -1,14 +1,21 @@
 // rx_krylov.hip — device-resident FGMRES (CSysSolve::FGMRES_LinSolver,
 // Common/src/linear_solvers_structure.cpp:309-463, ModGramSchmidt :87-186, ApplyGivens /
-// GenerateGivens :37-71, SolveReduced :73-85) and the captured implicit solve.
+// GenerateGivens :37-71, SolveReduced :73-85).
 //
 // Every scalar of the Krylov recurrence (norms, Hessenberg entries, Givens rotations, the
 // stop/breakdown decisions and the re-orthogonalisation test of MGS) lives in device memory and is
-// updated by single-lane kernels in the reference's operation order, so the whole solve is a fixed
-// sequence of kernels with no host round trip: the host launches it (or replays it as one hipGraph)
-// and reads the iteration count / residual once at the end. Kernels after a stop decision see the
-// `done` flag and return immediately. Inner products are fixed-order tree reductions (bitwise
-// reproducible); the reference sums sequentially, so results agree to rounding.
+// updated by the lead lane of the kernel that produces it, in the reference's operation order; the
+// other lanes evaluate the same decisions from the same inputs. The solve is therefore a fixed
+// sequence of kernels with no host round trip (replayed as one hipGraph by rx_implicit_euler), and
+// kernels after a stop decision see the `done` flag and return.
+//
+// Fusion: every vector kernel also produces the inner product the recurrence needs next
+// (SpMV -> |w|^2 and <w, w_0>; projection k -> <w, w_{k+1}> or |w|^2 or, when MGS re-orthogonalises,
+// <w, w_k>), reduced inside the launch: each of the 512 blocks reduces its grid-stride partial with a
+// fixed tree, publishes it with a write-through (sc1) store, takes an arrival ticket, and the last
+// block to arrive sums the partials in a fixed tree (MI355X_MICROARCH.md, inter-workgroup hand-off
+// with sc1 stores/loads). The summation order is fixed (independent of arrival order); the oracle's
+// orc_dot mode 1 restates it. The reference sums sequentially, so results agree to rounding.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -18,151 +25,244 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kRedBlocks = 512;
+constexpr int kRedBlocks = 512;  // every reducing kernel runs exactly this grid (grid-stride loops)
 constexpr int kMaxM = 64;
 inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 
 struct KState {
-  double tol, norm0, beta, nrm, thr, prod, dot, resid;
-  int done, noreo, iters, diverged;
+  double tol, norm0, beta, nrm, thr2[2], prod, dot, resid;  // thr2: read thr2[k&1], write thr2[(k+1)&1]
+  double norm0_in, dotn, dot2;  // inner-product landing slots
+  int done, noreo, iters, diverged, conv;
+  unsigned int ticket;          // arrival counter of the in-launch reductions
   double H[(kMaxM + 1) * kMaxM];  // H[k][i] at k * kMaxM + i
   double g[kMaxM + 1], cs[kMaxM + 1], sn[kMaxM + 1], y[kMaxM];
 };
 
 __device__ inline double& Hk(KState* s, int k, int i) { return s->H[k * kMaxM + i]; }
+__device__ inline bool lead() { return blockIdx.x == 0 && threadIdx.x == 0; }
 
-// ---- vector kernels (skip when *skip != 0)
-__global__ __launch_bounds__(kBlock) void k_dot_part(int64_t n, const double* __restrict__ a,
-                                                     const double* __restrict__ b, double* __restrict__ part,
-                                                     const int* __restrict__ skip) {
-  if (skip && *skip) return;
-  __shared__ double sh[kBlock];
-  double s = 0.0;
-  for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < n; q += (int64_t)gridDim.x * kBlock)
-    s += a[q] * b[q];
-  sh[threadIdx.x] = s;
+// Block tree (256 lanes, halving) of NR values; results in sh[r * kBlock].
+template <int NR>
+__device__ inline void block_tree(double* sh) {
   __syncthreads();
   for (int w = kBlock / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    if ((int)threadIdx.x < w) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) sh[r * kBlock + threadIdx.x] += sh[r * kBlock + threadIdx.x + w];
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
 }
 
-__global__ __launch_bounds__(kBlock) void k_dot_fin(const double* __restrict__ part, double* __restrict__ out,
-                                                    const int* __restrict__ skip) {
-  if (skip && *skip) return;
-  __shared__ double sh[kBlock];
-  sh[threadIdx.x] = part[threadIdx.x] + part[threadIdx.x + kBlock];
+// In-launch grid reduction of NR partial sums into *out[r] (see header). part: [NR][kRedBlocks].
+template <int NR>
+__device__ inline void grid_reduce(const double (&v)[NR], double* __restrict__ part, unsigned int* ticket,
+                                   double* const (&out)[NR]) {
+  __shared__ double sh[NR * kBlock + 1];
+  int* last = reinterpret_cast<int*>(sh + NR * kBlock);
+#pragma unroll
+  for (int r = 0; r < NR; ++r) sh[r * kBlock + threadIdx.x] = v[r];
+  block_tree<NR>(sh);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      __hip_atomic_store(part + r * kRedBlocks + blockIdx.x, sh[r * kBlock], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = (t == kRedBlocks - 1);
+  }
   __syncthreads();
-  for (int w = kBlock / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-    __syncthreads();
+  if (!*last) return;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const double a =
+        __hip_atomic_load(part + r * kRedBlocks + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double b =
+        __hip_atomic_load(part + r * kRedBlocks + kBlock + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[r * kBlock + threadIdx.x] = a + b;
   }
-  if (threadIdx.x == 0) *out = sh[0];
+  block_tree<NR>(sh);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) *out[r] = sh[r * kBlock];
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-// y += sign * (*alpha) * x
-__global__ __launch_bounds__(kBlock) void k_axpy_dev(int64_t n, const double* __restrict__ alpha, double sign,
-                                                     const double* __restrict__ x, double* __restrict__ y,
-                                                     const int* __restrict__ skip) {
-  if (skip && *skip) return;
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q < n) y[q] += (sign * *alpha) * x[q];
-}
-// y /= *d
-__global__ __launch_bounds__(kBlock) void k_div_dev(int64_t n, const double* __restrict__ d, double* __restrict__ y,
-                                                    const int* __restrict__ skip) {
-  if (skip && *skip) return;
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q < n) y[q] /= *d;
-}
-__global__ __launch_bounds__(kBlock) void k_sub_vec(int64_t n, const double* __restrict__ b, double* __restrict__ y) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q < n) y[q] -= b[q];
-}
-// x += sum_k y_k z_k, k ascending (the reference's per-k vector updates, element by element)
-__global__ __launch_bounds__(kBlock) void k_fg_update_x(int64_t n, const KState* __restrict__ s,
-                                                        const double* __restrict__ Z, double* __restrict__ x) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int it = s->iters;
-  if (q >= n || it == 0 || s->diverged) return;
-  double v = x[q];
-  for (int k = 0; k < it; ++k) v += s->y[k] * Z[(int64_t)k * n + q];
-  x[q] = v;
+#define GRID_LOOP(q, n) \
+  for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < (n); q += (int64_t)kRedBlocks * kBlock)
+
+// <a, b> (standalone)
+__global__ __launch_bounds__(kBlock) void k_dot(int64_t n, const double* __restrict__ a, const double* __restrict__ b,
+                                                double* __restrict__ part, KState* __restrict__ s,
+                                                double* __restrict__ out) {
+  double v[1] = {0.0};
+  GRID_LOOP(q, n) v[0] += a[q] * b[q];
+  double* const o[1] = {out};
+  grid_reduce<1>(v, part, &s->ticket, o);
 }
 
-// ---- single-lane recurrence kernels
-__global__ void k_fg_reset(KState* s, double tol) {
-  s->tol = tol;
-  s->done = 0;
-  s->noreo = 1;
-  s->iters = 0;
-  s->diverged = 0;
-  s->resid = 0.0;
+// Row-block product of y = A x for element q = (row i, component a): the reference's
+// MatrixVectorProduct order (blocks of the row in column order, columns c ascending).
+template <int NV>
+__device__ inline double spmv_elem(int64_t q, const int32_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                   const double* __restrict__ A, const double* __restrict__ x) {
+  const int i = (int)(q / NV), a = (int)(q - (int64_t)i * NV);
+  double acc = 0.0;
+  for (int k = rp[i]; k < rp[i + 1]; ++k) {
+    const double* blk = A + (size_t)k * NV * NV + a * NV;
+    const double* xv = x + (size_t)col[k] * NV;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) acc += blk[c] * xv[c];
+  }
+  return acc;
 }
-// after dot(b,b) -> norm0 slot and dot(w0,w0) -> dot slot
-__global__ void k_fg_start(KState* s) {
-  s->norm0 = sqrt(s->norm0);
-  s->beta = sqrt(s->dot);
+
+// w0 = A x - b and |w0|^2 -> dot
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_fg_residual(int N, const int32_t* __restrict__ rp,
+                                                        const int32_t* __restrict__ col, const double* __restrict__ A,
+                                                        const double* __restrict__ x, const double* __restrict__ b,
+                                                        double* __restrict__ w, double* __restrict__ part,
+                                                        KState* __restrict__ s) {
+  const int64_t n = (int64_t)N * NV;
+  double v[1] = {0.0};
+  GRID_LOOP(q, n) {
+    double y = spmv_elem<NV>(q, rp, col, A, x);
+    y -= b[q];
+    w[q] = y;
+    v[0] += y * y;
+  }
+  double* const o[1] = {&s->dot};
+  grid_reduce<1>(v, part, &s->ticket, o);
+}
+
+// w_{i+1} = A z_i with |w_{i+1}|^2 -> dotn and <w_{i+1}, w_0> -> dot
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_fg_spmv(int N, const int32_t* __restrict__ rp,
+                                                    const int32_t* __restrict__ col, const double* __restrict__ A,
+                                                    const double* __restrict__ z, const double* __restrict__ w0,
+                                                    double* __restrict__ w, double* __restrict__ part,
+                                                    KState* __restrict__ s) {
+  if (s->done) return;
+  const int64_t n = (int64_t)N * NV;
+  double v[2] = {0.0, 0.0};
+  GRID_LOOP(q, n) {
+    const double y = spmv_elem<NV>(q, rp, col, A, z);
+    w[q] = y;
+    v[0] += y * y;
+    v[1] += y * w0[q];
+  }
+  double* const o[2] = {&s->dotn, &s->dot};
+  grid_reduce<2>(v, part, &s->ticket, o);
+}
+
+// w0 = w0 / (-beta) after the start decision (:318-330), evaluated identically by every lane.
+__global__ __launch_bounds__(kBlock) void k_fg_start_div(int64_t n, KState* __restrict__ s, double* __restrict__ w0) {
+  const double norm0 = sqrt(s->norm0_in);
+  const double beta = sqrt(s->dot);
   const double epsm = 2.220446049250313e-16;
-  if ((s->beta < s->tol * s->norm0) || (s->beta < epsm)) {
-    s->done = 1;
-    s->resid = s->beta;
+  const bool early = (beta < s->tol * norm0) || (beta < epsm);
+  if (early) {
+    if (lead()) {
+      s->done = 1;
+      s->resid = beta;
+      s->beta = beta;
+      s->norm0 = norm0;
+    }
     return;
   }
-  s->prod = -s->beta;  // w0 /= -beta
-  s->g[0] = s->beta;
-  s->norm0 = s->beta;
-}
-__global__ void k_fg_begin(KState* s) {
-  if (s->done) return;
-  if (s->beta < s->tol * s->norm0) s->done = 1;
-}
-// after dot(w_{i+1}, w_{i+1}) -> dot
-__global__ void k_fg_mgs_begin(KState* s) {
-  if (s->done) return;
-  s->nrm = s->dot;
-  s->thr = s->nrm * 0.98;
-  if ((s->nrm <= 0.0) || (s->nrm != s->nrm)) {
-    s->diverged = 1;
-    s->done = 1;
+  if (lead()) {
+    s->g[0] = beta;
+    s->norm0 = beta;
+    s->beta = beta;
   }
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q < n) w0[q] /= -beta;
 }
-// after dot(w_{i+1}, w_k) -> dot: H[k][i] = prod, decide re-orthogonalisation
-__global__ void k_fg_proj(KState* s, int k, int i) {
-  if (s->done) {
-    s->noreo = 1;
-    return;
-  }
-  s->prod = s->dot;
-  Hk(s, k, i) = s->prod;
-  s->noreo = (s->prod * s->prod > s->thr) ? 0 : 1;
-}
-// after the optional second projection (dot -> dot when it ran)
-__global__ void k_fg_reo(KState* s, int k, int i) {
+
+// ModGramSchmidt (:87-186) projection k of iteration i: H[k][i] = prod = <w, w_k> (in s->dot),
+// w -= prod w_k, the re-orthogonalisation test prod^2 > thr, and the inner product the recurrence
+// needs next: <w, w_k> (re-orthogonalise), else <w, w_{k+1}> (k < i) or |w|^2 (k == i).
+// For k = 0 also ModGramSchmidt's entry: nrm = |w|^2 (s->dotn), thr = 0.98 nrm, breakdown test.
+__global__ __launch_bounds__(kBlock) void k_fg_proj(int64_t n, KState* __restrict__ s, int k, int i,
+                                                    double* __restrict__ W, double* __restrict__ part) {
   if (s->done) return;
-  if (!s->noreo) {
-    s->prod = s->dot;
-    Hk(s, k, i) += s->prod;
+  double nrm0 = 0.0;
+  if (k == 0) {
+    nrm0 = s->dotn;
+    if ((nrm0 <= 0.0) || (nrm0 != nrm0)) {
+      if (lead()) {
+        s->diverged = 1;
+        s->done = 1;
+      }
+      return;
+    }
   }
+  const double prod = s->dot;
+  const double thr = (k == 0) ? nrm0 * 0.98 : s->thr2[k & 1];
+  const bool reo = prod * prod > thr;
+  const double* wk = W + (int64_t)k * n;
+  double* w = W + (int64_t)(i + 1) * n;
+  const double* wn = reo ? wk : (k < i ? W + (int64_t)(k + 1) * n : nullptr);
+  double v[1] = {0.0};
+  GRID_LOOP(q, n) {
+    const double y = w[q] + (-1.0 * prod) * wk[q];
+    w[q] = y;
+    v[0] += y * (wn ? wn[q] : y);
+  }
+  if (lead()) {
+    if (k == 0) s->nrm = nrm0;
+    Hk(s, k, i) = prod;
+    s->prod = prod;
+    s->noreo = reo ? 0 : 1;
+    if (!reo) {
+      s->nrm -= Hk(s, k, i) * Hk(s, k, i);
+      if (s->nrm < 0.0) s->nrm = 0.0;
+      s->thr2[(k + 1) & 1] = s->nrm * 0.98;
+    }
+  }
+  double* const o[1] = {reo ? &s->dot2 : (k < i ? &s->dot : &s->dotn)};
+  grid_reduce<1>(v, part, &s->ticket, o);
 }
-__global__ void k_fg_nrm_update(KState* s, int k, int i) {
-  if (s->done) return;
-  s->nrm -= Hk(s, k, i) * Hk(s, k, i);
-  if (s->nrm < 0.0) s->nrm = 0.0;
-  s->thr = s->nrm * 0.98;
+
+// Second projection when the test fired: H[k][i] += prod2, w -= prod2 w_k, norm update, and the
+// next inner product (<w, w_{k+1}> or |w|^2).
+__global__ __launch_bounds__(kBlock) void k_fg_reo(int64_t n, KState* __restrict__ s, int k, int i,
+                                                   double* __restrict__ W, double* __restrict__ part) {
+  if (s->done || s->noreo) return;
+  const double prod = s->dot2;
+  const double* wk = W + (int64_t)k * n;
+  double* w = W + (int64_t)(i + 1) * n;
+  const double* wn = k < i ? W + (int64_t)(k + 1) * n : nullptr;
+  double v[1] = {0.0};
+  GRID_LOOP(q, n) {
+    const double y = w[q] + (-1.0 * prod) * wk[q];
+    w[q] = y;
+    v[0] += y * (wn ? wn[q] : y);
+  }
+  if (lead()) {
+    Hk(s, k, i) += prod;
+    s->nrm -= Hk(s, k, i) * Hk(s, k, i);
+    if (s->nrm < 0.0) s->nrm = 0.0;
+    s->thr2[(k + 1) & 1] = s->nrm * 0.98;
+  }
+  double* const o[1] = {k < i ? &s->dot : &s->dotn};
+  grid_reduce<1>(v, part, &s->ticket, o);
 }
+
 __device__ inline void apply_givens(double sn, double cs, double& h1, double& h2) {
   const double t = cs * h1 + sn * h2;
   h2 = cs * h2 - sn * h1;
   h1 = t;
 }
 __device__ inline double sign_of(double a, double b) { return b == 0.0 ? 0.0 : (b < 0 ? -fabs(a) : fabs(a)); }
-// after dot(w_{i+1}, w_{i+1}) -> dot: H[i+1][i], Givens, beta
-__global__ void k_fg_close(KState* s, int i) {
-  if (s->done) return;
-  s->nrm = sqrt(s->dot);
+
+// H[i+1][i] = |w|, Givens rotations (:37-71), beta = |g[i+1]|, and the stop test of the next
+// iteration's top (:339), published in `conv` (the next iteration's first kernel turns it into done).
+__device__ void fg_close(KState* s, int i) {
+  s->nrm = sqrt(s->dotn);
   Hk(s, i + 1, i) = s->nrm;
   for (int k = 0; k < i; ++k) apply_givens(s->sn[k], s->cs[k], Hk(s, k, i), Hk(s, k + 1, i));
   double& dx = Hk(s, i, i);
@@ -190,17 +290,63 @@ __global__ void k_fg_close(KState* s, int i) {
   apply_givens(s->sn[i], s->cs[i], s->g[i], s->g[i + 1]);
   s->beta = fabs(s->g[i + 1]);
   s->iters = i + 1;
+  if (s->beta < s->tol * s->norm0) s->conv = 1;
 }
-__global__ void k_fg_solve(KState* s) {
+
+// w_{i+1} /= |w_{i+1}| (all lanes) and fg_close (lead lane).
+__global__ __launch_bounds__(kBlock) void k_fg_close_div(int64_t n, KState* __restrict__ s, int i,
+                                                         double* __restrict__ w) {
+  if (s->done) return;
+  const double nrm = sqrt(s->dotn);
+  GRID_LOOP(q, n) w[q] /= nrm;
+  if (lead()) fg_close(s, i);
+}
+
+__global__ void k_fg_reset(KState* s, double tol) {
+  s->tol = tol;
+  s->done = 0;
+  s->conv = 0;
+  s->noreo = 1;
+  s->iters = 0;
+  s->diverged = 0;
+  s->resid = 0.0;
+}
+
+// SolveReduced (:73-85) and x += sum_k y_k z_k (k ascending, element by element as the reference's
+// per-k vector updates). Every block solves the small triangular system itself.
+__global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, KState* __restrict__ s, const double* __restrict__ Z,
+                                                      double* __restrict__ x) {
   if (s->diverged) return;
+  __shared__ double y[kMaxM];
   const int it = s->iters;
-  if (it > 0 || !s->done) s->resid = s->beta;
-  for (int k = 0; k < it; ++k) s->y[k] = s->g[k];
-  for (int k = it - 1; k >= 0; --k) {
-    s->y[k] /= Hk(s, k, k);
-    for (int j = k - 1; j >= 0; --j) s->y[j] -= Hk(s, j, k) * s->y[k];
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < it; ++k) y[k] = s->g[k];
+    for (int k = it - 1; k >= 0; --k) {
+      y[k] /= Hk(s, k, k);
+      for (int j = k - 1; j >= 0; --j) y[j] -= Hk(s, j, k) * y[k];
+    }
+  }
+  __syncthreads();
+  if (lead()) {
+    if (it > 0 || !s->done) s->resid = s->beta;
+    for (int k = 0; k < it; ++k) s->y[k] = y[k];
+  }
+  if (it == 0) return;
+  GRID_LOOP(q, n) {
+    double v = x[q];
+    for (int k = 0; k < it; ++k) v += y[k] * Z[(int64_t)k * n + q];
+    x[q] = v;
   }
 }
+
+#define RX_NV_SWITCH(nv, CALL)                       \
+  switch (nv) {                                      \
+    case 7: { constexpr int NV_ = 7; CALL; } break;   \
+    case 8: { constexpr int NV_ = 8; CALL; } break;   \
+    case 11: { constexpr int NV_ = 11; CALL; } break; \
+    case 13: { constexpr int NV_ = 13; CALL; } break; \
+    default: return RX_ERR_ARG;                      \
+  }
 
 }  // namespace
 
@@ -228,53 +374,35 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m) {
   int rc = rx_la_krylov_alloc(ctx, m);
   if (rc) return rc;
   const int64_t n = ctx->N * ctx->nVar;
+  const int nb = blocks(n);
   hipStream_t st = ctx->stream;
   KState* s = static_cast<KState*>(ctx->kstate);
   double* A = ctx->f[RX_F_JAC];
   double* b = ctx->f[RX_F_RHS];
   double* x = ctx->f[RX_F_SOL];
-  double* part = ctx->red;
+  double* part = ctx->red;  // [2][kRedBlocks]
   auto W = [&](int k) { return ctx->kw + (int64_t)k * n; };
   auto Z = [&](int k) { return ctx->kz + (int64_t)k * n; };
-  const int* done = &s->done;
-  const int* noreo = &s->noreo;
-  auto dot = [&](const double* a, const double* c, double* out, const int* skip) -> int {
-    k_dot_part<<<kRedBlocks, kBlock, 0, st>>>(n, a, c, part, skip);
-    k_dot_fin<<<1, kBlock, 0, st>>>(part, out, skip);
-    return RX_OK;
-  };
   k_fg_reset<<<1, 1, 0, st>>>(s, tol);
-  dot(b, b, &s->norm0, nullptr);
-  if ((rc = rx_la_spmv(ctx, A, x, W(0), nullptr))) return rc;
-  k_sub_vec<<<blocks(n), kBlock, 0, st>>>(n, b, W(0));
-  dot(W(0), W(0), &s->dot, nullptr);
-  k_fg_start<<<1, 1, 0, st>>>(s);
-  k_div_dev<<<blocks(n), kBlock, 0, st>>>(n, &s->prod, W(0), done);
+  k_dot<<<kRedBlocks, kBlock, 0, st>>>(n, b, b, part, s, &s->norm0_in);
+  RX_NV_SWITCH(ctx->nVar, (k_fg_residual<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->N, ctx->rp, ctx->col, A, x, b,
+                                                                             W(0), part, s)));
+  k_fg_start_div<<<nb, kBlock, 0, st>>>(n, s, W(0));
   for (int i = 0; i < m; ++i) {
-    k_fg_begin<<<1, 1, 0, st>>>(s);
     if (ctx->cfg.lin_prec == 1) {
-      if ((rc = rx_la_ilu_apply(ctx, W(i), Z(i), done))) return rc;
+      if ((rc = rx_la_ilu_apply(ctx, W(i), Z(i), &s->done, &s->conv))) return rc;
     } else {
-      if ((rc = rx_la_lusgs(ctx, A, W(i), Z(i), done))) return rc;
+      if ((rc = rx_la_lusgs(ctx, A, W(i), Z(i), &s->done, &s->conv))) return rc;
     }
-    if ((rc = rx_la_spmv(ctx, A, Z(i), W(i + 1), done))) return rc;
-    dot(W(i + 1), W(i + 1), &s->dot, done);
-    k_fg_mgs_begin<<<1, 1, 0, st>>>(s);
+    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->N, ctx->rp, ctx->col, A, Z(i),
+                                                                           W(0), W(i + 1), part, s)));
     for (int k = 0; k <= i; ++k) {
-      dot(W(i + 1), W(k), &s->dot, done);
-      k_fg_proj<<<1, 1, 0, st>>>(s, k, i);
-      k_axpy_dev<<<blocks(n), kBlock, 0, st>>>(n, &s->prod, -1.0, W(k), W(i + 1), done);
-      dot(W(i + 1), W(k), &s->dot, noreo);
-      k_fg_reo<<<1, 1, 0, st>>>(s, k, i);
-      k_axpy_dev<<<blocks(n), kBlock, 0, st>>>(n, &s->prod, -1.0, W(k), W(i + 1), noreo);
-      k_fg_nrm_update<<<1, 1, 0, st>>>(s, k, i);
+      k_fg_proj<<<kRedBlocks, kBlock, 0, st>>>(n, s, k, i, ctx->kw, part);
+      k_fg_reo<<<kRedBlocks, kBlock, 0, st>>>(n, s, k, i, ctx->kw, part);
     }
-    dot(W(i + 1), W(i + 1), &s->dot, done);
-    k_fg_close<<<1, 1, 0, st>>>(s, i);
-    k_div_dev<<<blocks(n), kBlock, 0, st>>>(n, &s->nrm, W(i + 1), done);
+    k_fg_close_div<<<kRedBlocks, kBlock, 0, st>>>(n, s, i, W(i + 1));
   }
-  k_fg_solve<<<1, 1, 0, st>>>(s);
-  k_fg_update_x<<<blocks(n), kBlock, 0, st>>>(n, s, ctx->kz, x);
+  k_fg_finish<<<kRedBlocks, kBlock, 0, st>>>(n, s, ctx->kz, x);
   RX_HIP(hipGetLastError());
   return RX_OK;
 }

@@ -34,6 +34,18 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// FGMRES hooks of the sweeps: skip when the solve is done; the first kernel of an iteration also
+// turns the previous iteration's convergence flag into `done` (rx_krylov.hip).
+__device__ __forceinline__ bool skip_sweep(int* done, const int* conv) {
+  if (!done) return false;
+  if (*done) return true;
+  if (conv && *conv) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *done = 1;
+    return true;
+  }
+  return false;
+}
+
 __device__ __forceinline__ double bcast(double v, int lane) {
   const unsigned long long u = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), lane);
@@ -93,6 +105,43 @@ __device__ __forceinline__ void lu_solve(const double* __restrict__ LU, double (
   }
 }
 
+// Right-looking form of the same elimination, lane r holding ROW r: for every pivot jj the rows
+// ii > jj compute their multiplier LU[ii][jj] / LU[jj][jj] and update LU[ii][kk] -= w * LU[jj][kk]
+// (kk > jj) in parallel. Each (ii, jj) step sees exactly the operands of the reference's row-by-row
+// loop (row jj is final when pivot jj is used, row ii has had steps 0..jj-1), so the result is bitwise
+// the same while the dependent chain shrinks from NV(NV-1)/2 divisions to NV-1.
+// On exit row[kk] holds U[r][kk] (kk >= r) or the multiplier w[r][kk] (kk < r).
+template <int NV>
+__device__ __forceinline__ void wave_factor_rows(double (&row)[NV], int lane) {
+#pragma unroll
+  for (int jj = 0; jj < NV - 1; ++jj) {
+    const double piv = bcast(row[jj], jj);
+    const double w = row[jj] / piv;
+    if (lane > jj) {
+#pragma unroll
+      for (int kk = jj + 1; kk < NV; ++kk) row[kk] -= w * bcast(row[kk], jj);
+      row[jj] = w;
+    }
+  }
+}
+
+// Solve with a factorisation held as in wave_factor_rows (lane r holds row r); one rhs per lane.
+template <int NV>
+__device__ __forceinline__ void wave_solve_rows(const double (&row)[NV], double (&rhs)[NV]) {
+#pragma unroll
+  for (int ii = 1; ii < NV; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < ii; ++jj) rhs[ii] -= bcast(row[jj], ii) * rhs[jj];
+  rhs[NV - 1] = rhs[NV - 1] / bcast(row[NV - 1], NV - 1);
+#pragma unroll
+  for (int ii = NV - 2; ii >= 0; --ii) {
+    double aux = 0.0;
+#pragma unroll
+    for (int jj = ii + 1; jj < NV; ++jj) aux += bcast(row[jj], ii) * rhs[jj];
+    rhs[ii] = (rhs[ii] - aux) / bcast(row[ii], ii);
+  }
+}
+
 // Factorise every diagonal block once (LU-SGS uses Gauss_Elimination on the same, unchanged diagonal
 // block for every row and every call, so one factorisation per matrix is bitwise equivalent).
 // One wavefront per row.
@@ -103,106 +152,158 @@ __global__ __launch_bounds__(256) void k_diag_factor(int N, const int64_t* __res
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= N) return;
   const double* D = A + diag[i] * (NV * NV);
-  double col[NV];
+  double row[NV];
 #pragma unroll
-  for (int r = 0; r < NV; ++r) col[r] = lane < NV ? D[r * NV + lane] : 1.0;
-  wave_factor<NV>(col, lane);
+  for (int k = 0; k < NV; ++k) row[k] = lane < NV ? D[lane * NV + k] : 1.0;
+  wave_factor_rows<NV>(row, lane);
   if (lane < NV) {
 #pragma unroll
-    for (int r = 0; r < NV; ++r) LU[(size_t)i * NV * NV + r * NV + lane] = col[r];
+    for (int k = 0; k < NV; ++k) LU[(size_t)i * NV * NV + lane * NV + k] = row[k];
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // ILU(0) factorisation, one workgroup per partition, one wavefront per row.
-// F holds a copy of A on entry. invD receives inv(D_i) of every finished row (the reference recomputes
+// Reads A, writes the factor F (the reference's copy into ILU_matrix is fused). invD receives inv(D_i) of every finished row (the reference recomputes
 // exactly this inverse from the same finished block whenever it needs it).
-// LDS per wave: row blocks [rowmax][NV2] + W [NV2] + staging [NV2].
+// The update plan is static (host-built in rx_ctx_create): for every intra-partition lower block k =
+// (i, j) the list upd[upd_ptr[k] .. upd_ptr[k+1]) of (kk, pos) pairs, kk = (j, kp) an upper block of
+// row j with kp inside row i at BSR index pos, in increasing kk (the reference's loop order :1421-1443;
+// the diagonal kp = j is left out since it only touches A_ij, which is then overwritten by W).
+// A row stages everything it reads from finished rows (inv(A_jj) and the A_jk of the plan) in one
+// round trip together with its own blocks when it fits kStage blocks; otherwise per lower block.
+// LDS per wave: row blocks [rowmax][NV2] + W + staging [kStage][NV2].
+constexpr int kStage = 6;
 template <int NV>
 __global__ __launch_bounds__(1024) void k_ilu_build_part(const int32_t* __restrict__ part_lvl,
                                                          const int32_t* __restrict__ lvl_ptr,
-                                                         const int32_t* __restrict__ rows,
+                                                         const int4* __restrict__ slot,
                                                          const int32_t* __restrict__ col,
-                                                         const int32_t* __restrict__ klo,
-                                                         const int32_t* __restrict__ khi,
-                                                         const int64_t* __restrict__ diag, double* __restrict__ F,
-                                                         double* __restrict__ invD, int rowmax) {
+                                                         const int32_t* __restrict__ upd_ptr,
+                                                         const int2* __restrict__ upd,
+                                                         const int32_t* __restrict__ rp, const double* __restrict__ A,
+                                                         double* __restrict__ F, double* __restrict__ invD,
+                                                         int rowmax, long long* __restrict__ trace) {
   constexpr int NV2 = NV * NV;
   extern __shared__ double lds[];
+  // optional phase trace of block 0 (tools/ilu_trace.py): per row of wave w: 5 stamps
+  long long* tr = (trace && blockIdx.x == 0 && (threadIdx.x & 63) == 0) ? trace + 1 + (threadIdx.x >> 6) * 5 * 64
+                                                                          : nullptr;
+  int trow = 0;
+#define RX_STAMP(ph)                                                            \
+  do {                                                                          \
+    if (tr && trow < 64) tr[trow * 5 + (ph)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
-  double* rowbuf = lds + (size_t)wave * (rowmax + 2) * NV2;
+  double* rowbuf = lds + (size_t)wave * (rowmax + 1 + kStage) * NV2;
   double* Wb = rowbuf + (size_t)rowmax * NV2;
   double* S = Wb + NV2;
   const int p = blockIdx.x;
   for (int l = part_lvl[p]; l < part_lvl[p + 1]; ++l) {
     for (int r = lvl_ptr[l] + wave; r < lvl_ptr[l + 1]; r += nwave) {
-      const int i = rows[r];
-      const int k0 = klo[i], k1 = khi[i], kd = (int)diag[i];
+      RX_STAMP(0);
+      const int4 sl = slot[r];
+      const int i = sl.x, k0 = sl.y, kd = sl.z, k1 = sl.w;
       const int nbk = k1 - k0;
-      for (int q = lane; q < nbk * NV2; q += 64) rowbuf[q] = F[(size_t)k0 * NV2 + q];
+      const int ua = upd_ptr[k0], ub = upd_ptr[kd];
+      const bool all = (kd - k0) + (ub - ua) <= kStage;  // stage the whole row at once
+      for (int q = lane; q < nbk * NV2; q += 64) rowbuf[q] = A[(size_t)k0 * NV2 + q];
+      {  // blocks of the row outside the partition are copied unchanged (SetBlock_ILUMatrix :1378-1389)
+        const int ra = rp[i], rb = rp[i + 1];
+        for (int q = lane; q < (k0 - ra) * NV2; q += 64) F[(size_t)ra * NV2 + q] = A[(size_t)ra * NV2 + q];
+        for (int q = lane; q < (rb - k1) * NV2; q += 64) F[(size_t)k1 * NV2 + q] = A[(size_t)k1 * NV2 + q];
+      }
+      if (all) {
+        // staging order: for each lower k: inv(A_jj), then its plan blocks
+        int slotn = 0;
+        for (int k = k0; k < kd; ++k) {
+          const int j = col[k];
+          for (int q = lane; q < NV2; q += 64) S[slotn * NV2 + q] = invD[(size_t)j * NV2 + q];
+          ++slotn;
+          for (int u = upd_ptr[k]; u < upd_ptr[k + 1]; ++u, ++slotn) {
+            const int kk = upd[u].x;
+            for (int q = lane; q < NV2; q += 64) S[slotn * NV2 + q] = F[(size_t)kk * NV2 + q];
+          }
+        }
+      }
       wave_sync();
+      RX_STAMP(1);
+      int slotn = 0;
       for (int k = k0; k < kd; ++k) {
-        const int j = col[k];
-        for (int q = lane; q < NV2; q += 64) S[q] = invD[(size_t)j * NV2 + q];
-        wave_sync();
+        const int u0 = upd_ptr[k], u1 = upd_ptr[k + 1];
+        const double* Sinv;
+        if (all) {
+          Sinv = S + (size_t)slotn * NV2;
+          ++slotn;
+        } else {
+          const int j = col[k];
+          for (int q = lane; q < NV2; q += 64) S[q] = invD[(size_t)j * NV2 + q];
+          wave_sync();
+          Sinv = S;
+        }
         const double* Bij = rowbuf + (size_t)(k - k0) * NV2;
         // W = A_ij * inv(A_jj)  (MatrixMatrixProduct, sum from 0.0 over q ascending)
         for (int e = lane; e < NV2; e += 64) {
           const int a = e / NV, c = e - a * NV;
           double s = 0.0;
 #pragma unroll
-          for (int q = 0; q < NV; ++q) s += Bij[a * NV + q] * S[q * NV + c];
+          for (int q = 0; q < NV; ++q) s += Bij[a * NV + q] * Sinv[q * NV + c];
           Wb[e] = s;
         }
         wave_sync();
-        // A_ik -= A_jk * W for the upper blocks of row j (left-multiply quirk). The diagonal of row j
-        // would update A_ij, which is overwritten by W below, so it is skipped.
-        const int kdj = (int)diag[j], k1j = khi[j];
-        for (int kk = kdj + 1; kk < k1j; ++kk) {
-          const int kp = col[kk];
-          int pos = -1;
-          for (int q = k0; q < k1; ++q)
-            if (col[q] == kp) {
-              pos = q;
-              break;
-            }
-          if (pos < 0) continue;
-          for (int q = lane; q < NV2; q += 64) S[q] = F[(size_t)kk * NV2 + q];
-          wave_sync();
-          double* Bik = rowbuf + (size_t)(pos - k0) * NV2;
+        // A_ik -= A_jk * W (left-multiply quirk), in increasing kk
+        for (int u = u0; u < u1; ++u) {
+          const int2 h = upd[u];
+          const double* Bjk;
+          if (all) {
+            Bjk = S + (size_t)slotn * NV2;
+            ++slotn;
+          } else {
+            wave_sync();
+            for (int q = lane; q < NV2; q += 64) S[NV2 + q] = F[(size_t)h.x * NV2 + q];
+            wave_sync();
+            Bjk = S + NV2;
+          }
+          double* Bik = rowbuf + (size_t)(h.y - k0) * NV2;
           for (int e = lane; e < NV2; e += 64) {
             const int a = e / NV, c = e - a * NV;
             double s = 0.0;
 #pragma unroll
-            for (int q = 0; q < NV; ++q) s += S[a * NV + q] * Wb[q * NV + c];
+            for (int q = 0; q < NV; ++q) s += Bjk[a * NV + q] * Wb[q * NV + c];
             Bik[e] -= s;
           }
-          wave_sync();
         }
+        wave_sync();
         double* dst = rowbuf + (size_t)(k - k0) * NV2;
         for (int e = lane; e < NV2; e += 64) dst[e] = Wb[e];
         wave_sync();
       }
+      RX_STAMP(2);
       // inv(D_i): Gauss elimination of each unit column (InverseDiagonalBlock_ILUMatrix)
       {
         const double* D = rowbuf + (size_t)(kd - k0) * NV2;
-        double cl[NV], rhs[NV];
+        double rw[NV], rhs[NV];
 #pragma unroll
-        for (int rr = 0; rr < NV; ++rr) cl[rr] = lane < NV ? D[rr * NV + lane] : 1.0;
-        wave_factor<NV>(cl, lane);
+        for (int kk = 0; kk < NV; ++kk) rw[kk] = lane < NV ? D[lane * NV + kk] : 1.0;
+        wave_factor_rows<NV>(rw, lane);
 #pragma unroll
         for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == lane) ? 1.0 : 0.0;
-        wave_solve<NV>(cl, rhs);
+        wave_solve_rows<NV>(rw, rhs);
         if (lane < NV) {
 #pragma unroll
           for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + lane] = rhs[rr];
         }
       }
+      RX_STAMP(3);
       for (int q = lane; q < nbk * NV2; q += 64) F[(size_t)k0 * NV2 + q] = rowbuf[q];
       wave_sync();
+      RX_STAMP(4);
+      ++trow;
     }
     __syncthreads();
   }
+  if (trace && blockIdx.x == 0 && threadIdx.x == 0) trace[0] = (long long)__builtin_amdgcn_s_memtime();
+#undef RX_STAMP
 }
 
 // ILU(0) forward substitution x = b - L x per partition; one thread per (row, component).
@@ -215,8 +316,8 @@ __global__ __launch_bounds__(256) void k_ilu_fwd_part(const int32_t* __restrict_
                                                       const int64_t* __restrict__ diag,
                                                       const double* __restrict__ F, const double* __restrict__ b,
                                                       double* __restrict__ x,
-    const int* __restrict__ skip) {
-  if (skip && *skip) return;
+    int* __restrict__ done, const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
   constexpr int NV2 = NV * NV, RPB = 256 / NV;
   const int p = blockIdx.x;
   const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
@@ -250,8 +351,8 @@ __global__ __launch_bounds__(256) void k_ilu_bwd_part(const int32_t* __restrict_
                                                       const int64_t* __restrict__ diag,
                                                       const double* __restrict__ F,
                                                       const double* __restrict__ invD, double* __restrict__ x,
-    const int* __restrict__ skip) {
-  if (skip && *skip) return;
+    int* __restrict__ done, const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
   constexpr int NV2 = NV * NV, RPB = 256 / NV;
   __shared__ double v[RPB * NV];
   const int p = blockIdx.x;
@@ -289,6 +390,173 @@ __global__ __launch_bounds__(256) void k_ilu_bwd_part(const int32_t* __restrict_
   }
 }
 
+// ILU(0) application with the partition's vector resident in LDS: b is loaded once, the forward
+// and backward substitutions run level by level on the LDS copy, and x is stored once. The row
+// metadata of both schedules and the partition's column indices (local) are staged in LDS too, so the
+// only global loads inside a level are the factor blocks, and those of level l+1 are issued before
+// level l is computed (register double buffer, kPF blocks per row; longer rows load the rest
+// directly). Same arithmetic as k_ilu_fwd_part / k_ilu_bwd_part.
+// LDS: xs[rows][NV] + v[RPB][NV] + fslot/bslot[rows][4] + colL[partition nnzb].
+constexpr int kPF = 3;
+template <int NV>
+struct RowPF {
+  double f[kPF][NV];
+};
+template <int NV>
+__device__ __forceinline__ void pf_load(RowPF<NV>& d, const double* __restrict__ F, int k0, int k1, int a) {
+#pragma unroll
+  for (int t = 0; t < kPF; ++t)
+    if (k0 + t < k1) {
+      const double* blk = F + (size_t)(k0 + t) * NV * NV + a * NV;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) d.f[t][c] = blk[c];
+    }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict__ part_ptr,
+                                                       const int32_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ f_part_lvl,
+                                                       const int32_t* __restrict__ f_lvl_ptr,
+                                                       const int4* __restrict__ f_slot,
+                                                       const int32_t* __restrict__ b_part_lvl,
+                                                       const int32_t* __restrict__ b_lvl_ptr,
+                                                       const int4* __restrict__ b_slot,
+                                                       const int32_t* __restrict__ col, const double* __restrict__ F,
+                                                       const double* __restrict__ invD, const double* __restrict__ b,
+                                                       double* __restrict__ x, int* __restrict__ done,
+                                                       const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  constexpr int NV2 = NV * NV, RPB = 256 / NV;
+  extern __shared__ double lds[];
+  const int p = blockIdx.x;
+  const int lo = part_ptr[p], hi = part_ptr[p + 1], nr = hi - lo;
+  const int kb = rp[lo], ke = rp[hi];
+  double* xs = lds;
+  double* v = xs + (size_t)nr * NV;
+  int4* fsl = reinterpret_cast<int4*>(lds + (((size_t)nr * NV + RPB * NV + 1) & ~(size_t)1));  // 16-B aligned
+  int4* bsl = fsl + nr;
+  int* colL = reinterpret_cast<int*>(bsl + nr);
+  // rows of partition p occupy slots [f_lvl_ptr[f_part_lvl[p]], +nr) in both schedules
+  const int fl0 = f_part_lvl[p], fl1 = f_part_lvl[p + 1], bl0 = b_part_lvl[p], bl1 = b_part_lvl[p + 1];
+  const int fr0 = f_lvl_ptr[fl0], br0 = b_lvl_ptr[bl0];
+  const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
+  const bool lane_ok = rl < RPB;
+  RowPF<NV> cur, nxt;
+  // first forward level's factor rows straight from the global slot table
+  if (lane_ok && fr0 + rl < f_lvl_ptr[fl0 + 1]) {
+    const int4 sl = f_slot[fr0 + rl];
+    pf_load<NV>(cur, F, sl.y, sl.z, a);
+  }
+  for (int q = threadIdx.x; q < nr * NV; q += blockDim.x) xs[q] = b[(size_t)lo * NV + q];
+  for (int q = threadIdx.x; q < nr; q += blockDim.x) {
+    fsl[q] = f_slot[fr0 + q];
+    bsl[q] = b_slot[br0 + q];
+  }
+  for (int q = threadIdx.x; q < ke - kb; q += blockDim.x) colL[q] = col[kb + q] - lo;
+  __syncthreads();
+  for (int l = fl0; l < fl1; ++l) {
+    const int r0 = f_lvl_ptr[l], r1 = f_lvl_ptr[l + 1];
+    if (lane_ok && l + 1 < fl1 && r1 + rl < f_lvl_ptr[l + 2]) {
+      const int4 sl = fsl[r1 + rl - fr0];
+      pf_load<NV>(nxt, F, sl.y, sl.z, a);
+    }
+    for (int r = r0 + rl; r < r1 && lane_ok; r += RPB) {
+      const int4 sl = fsl[r - fr0];
+      const int li = sl.x - lo;
+      double xi = xs[li * NV + a];
+      for (int k = sl.y; k < sl.z; ++k) {
+        const int t = k - sl.y;
+        const double* xj = xs + colL[k - kb] * NV;
+        double s = 0.0;
+        if (r == r0 + rl && t < kPF) {
+#pragma unroll
+          for (int tt = 0; tt < kPF; ++tt)
+            if (tt == t) {
+#pragma unroll
+              for (int c = 0; c < NV; ++c) s += cur.f[tt][c] * xj[c];
+            }
+        } else {
+          const double* blk = F + (size_t)k * NV2 + a * NV;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
+        }
+        xi -= s;
+      }
+      xs[li * NV + a] = xi;
+    }
+    __syncthreads();
+    cur = nxt;
+  }
+  // backward: upper blocks + the row of inv(D_i)
+  RowPF<NV> ucur, unxt;
+  double icur[NV], inxt[NV];
+  if (lane_ok && br0 + rl < b_lvl_ptr[bl0 + 1]) {
+    const int4 sl = bsl[rl];
+    pf_load<NV>(ucur, F, sl.z + 1, sl.w, a);
+#pragma unroll
+    for (int c = 0; c < NV; ++c) icur[c] = invD[(size_t)sl.x * NV2 + a * NV + c];
+  }
+  for (int l = bl0; l < bl1; ++l) {
+    const int r0 = b_lvl_ptr[l], r1 = b_lvl_ptr[l + 1];
+    if (lane_ok && l + 1 < bl1 && r1 + rl < b_lvl_ptr[l + 2]) {
+      const int4 sl = bsl[r1 + rl - br0];
+      pf_load<NV>(unxt, F, sl.z + 1, sl.w, a);
+#pragma unroll
+      for (int c = 0; c < NV; ++c) inxt[c] = invD[(size_t)sl.x * NV2 + a * NV + c];
+    }
+    for (int base = r0; base < r1; base += RPB) {
+      const int r = base + rl;
+      const bool act = lane_ok && r < r1;
+      const bool first = base == r0;
+      int i = 0, li = 0;
+      if (act) {
+        const int4 sl = bsl[r - br0];
+        i = sl.x;
+        li = i - lo;
+        double sum = 0.0;
+        for (int k = sl.z + 1; k < sl.w; ++k) {
+          const int t = k - sl.z - 1;
+          const double* xj = xs + colL[k - kb] * NV;
+          double s = 0.0;
+          if (first && t < kPF) {
+#pragma unroll
+            for (int tt = 0; tt < kPF; ++tt)
+              if (tt == t) {
+#pragma unroll
+                for (int c = 0; c < NV; ++c) s += ucur.f[tt][c] * xj[c];
+              }
+          } else {
+            const double* blk = F + (size_t)k * NV2 + a * NV;
+#pragma unroll
+            for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
+          }
+          sum += s;
+        }
+        v[rl * NV + a] = xs[li * NV + a] - sum;
+      }
+      __syncthreads();
+      if (act) {
+        double s = 0.0;
+        if (first) {
+#pragma unroll
+          for (int c = 0; c < NV; ++c) s += icur[c] * v[rl * NV + c];
+        } else {
+          const double* inv = invD + (size_t)i * NV2 + a * NV;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
+        }
+        xs[li * NV + a] = s;
+      }
+      __syncthreads();
+    }
+    ucur = unxt;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) icur[c] = inxt[c];
+  }
+  for (int q = threadIdx.x; q < nr * NV; q += blockDim.x) x[(size_t)lo * NV + q] = xs[q];
+}
+
 // LU-SGS forward sweep (D+L) x* = b per partition: products per (row, component), then one thread
 // per row solves with the stored factorisation of D.
 template <int NV>
@@ -300,8 +568,8 @@ __global__ __launch_bounds__(256) void k_lusgs_fwd_part(const int32_t* __restric
                                                         const int64_t* __restrict__ diag,
                                                         const double* __restrict__ A, const double* __restrict__ DLU,
                                                         const double* __restrict__ b, double* __restrict__ xs,
-    const int* __restrict__ skip) {
-  if (skip && *skip) return;
+    int* __restrict__ done, const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
   constexpr int NV2 = NV * NV, RPB = 256 / NV;
   __shared__ double v[RPB * NV];
   const int p = blockIdx.x;
@@ -352,8 +620,8 @@ __global__ __launch_bounds__(256) void k_lusgs_bwd_part(const int32_t* __restric
                                                         const int64_t* __restrict__ diag,
                                                         const double* __restrict__ A, const double* __restrict__ DLU,
                                                         const double* __restrict__ xs, double* __restrict__ x,
-    const int* __restrict__ skip) {
-  if (skip && *skip) return;
+    int* __restrict__ done, const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
   constexpr int NV2 = NV * NV, RPB = 256 / NV;
   __shared__ double v[RPB * NV];
   const int p = blockIdx.x;
@@ -419,27 +687,48 @@ __global__ __launch_bounds__(256) void k_lusgs_bwd_part(const int32_t* __restric
 
 double* rx_invd_buf(rx_ctx* ctx) { return ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)ctx->nVar * ctx->nVar; }
 
+// Raise the dynamic-LDS limit of the LDS-resident kernels to what the device allows (once).
+int rx_la_prepare(rx_ctx* ctx) {
+  RX_NV_SWITCH(ctx->nVar, {
+    RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_lds<NV_>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_part<NV_>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+  });
+  return RX_OK;
+}
+
 int rx_la_ilu_build(rx_ctx* ctx) {
   const int nv = ctx->nVar;
-  const int64_t nb = ctx->nnzb * (int64_t)nv * nv;
-  RX_HIP(hipMemcpyAsync(ctx->f[RX_F_ILU], ctx->f[RX_F_JAC], nb * sizeof(double), hipMemcpyDeviceToDevice,
-                        ctx->stream));
   const int waves = ctx->ilu_waves;
-  const size_t shm = sizeof(double) * (size_t)waves * (ctx->rowmax + 2) * nv * nv;
+  const size_t shm = sizeof(double) * (size_t)waves * (ctx->rowmax + 1 + kStage) * nv * nv;
   RX_NV_SWITCH(nv, (k_ilu_build_part<NV_><<<ctx->npart, 64 * waves, shm, ctx->stream>>>(
-                       ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->khi, ctx->diag,
-                       ctx->f[RX_F_ILU], rx_invd_buf(ctx), ctx->rowmax)));
+                       ctx->fs.part_lvl, ctx->fs.lvl_ptr, reinterpret_cast<const int4*>(ctx->fs.slot), ctx->col,
+                       ctx->upd_ptr, reinterpret_cast<const int2*>(ctx->upd), ctx->rp, ctx->f[RX_F_JAC],
+                       ctx->f[RX_F_ILU], rx_invd_buf(ctx), ctx->rowmax, ctx->ilu_trace)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
 
-int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, const int* skip) {
+int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv) {
+  const int nv = ctx->nVar;
+  const size_t shm = sizeof(double) * ((size_t)ctx->maxpart * nv + (size_t)(256 / nv) * nv + 1) +
+                     sizeof(int32_t) * (8 * (size_t)ctx->maxpart + (size_t)ctx->maxpart_nnzb);
+  if (shm <= (size_t)ctx->lds_max) {
+    RX_NV_SWITCH(nv, (k_ilu_apply_lds<NV_><<<ctx->npart, 256, shm, ctx->stream>>>(
+                         ctx->part_ptr, ctx->rp, ctx->fs.part_lvl, ctx->fs.lvl_ptr,
+                         reinterpret_cast<const int4*>(ctx->fs.slot), ctx->bs.part_lvl, ctx->bs.lvl_ptr,
+                         reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx),
+                         b, x, done, conv)));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
   RX_NV_SWITCH(ctx->nVar, (k_ilu_fwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->diag,
-                              ctx->f[RX_F_ILU], b, x, skip)));
+                              ctx->f[RX_F_ILU], b, x, done, conv)));
   RX_NV_SWITCH(ctx->nVar, (k_ilu_bwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows, ctx->col, ctx->khi, ctx->diag,
-                              ctx->f[RX_F_ILU], rx_invd_buf(ctx), x, skip)));
+                              ctx->f[RX_F_ILU], rx_invd_buf(ctx), x, done, conv)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
@@ -451,13 +740,30 @@ int rx_la_diag_factor(rx_ctx* ctx, const double* A) {
   return RX_OK;
 }
 
-int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, const int* skip) {
+int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, int* done, const int* conv) {
   RX_NV_SWITCH(ctx->nVar, (k_lusgs_fwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->diag, A,
-                              ctx->dlu, b, ctx->xstar, skip)));
+                              ctx->dlu, b, ctx->xstar, done, conv)));
   RX_NV_SWITCH(ctx->nVar, (k_lusgs_bwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows, ctx->rp, ctx->col, ctx->klo, ctx->khi,
-                              ctx->diag, A, ctx->dlu, ctx->xstar, x, skip)));
+                              ctx->diag, A, ctx->dlu, ctx->xstar, x, done, conv)));
   RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+// Debug: trace the phases of the ILU(0) factorisation of partition 0 (see tools/ilu_trace.py).
+extern "C" int rx_debug_ilu_trace(rx_ctx* ctx, long long* host, int64_t n) {
+  const int64_t need = 1 + 16 * 5 * 64;
+  if (!ctx || n < need) return RX_ERR_ARG;
+  if (!ctx->ilu_trace) {
+    RX_HIP(hipMalloc(&ctx->ilu_trace, sizeof(long long) * need));
+  }
+  RX_HIP(hipMemsetAsync(ctx->ilu_trace, 0, sizeof(long long) * need, ctx->stream));
+  int rc = rx_la_ilu_build(ctx);
+  if (rc) return rc;
+  RX_HIP(hipMemcpyAsync(host, ctx->ilu_trace, sizeof(long long) * need, hipMemcpyDeviceToHost, ctx->stream));
+  RX_HIP(hipStreamSynchronize(ctx->stream));
+  (void)hipFree(ctx->ilu_trace);
+  ctx->ilu_trace = nullptr;
   return RX_OK;
 }

@@ -1,0 +1,36 @@
+"""Debug: phase timing of the ILU(0) factorisation kernel (partition 0) on the GPU.
+
+python tools/ilu_trace.py [nx ny parts]  — prints median shader-clock cycles per row phase:
+  0-1 row/staging loads, 1-2 lower-block products and updates, 2-3 inverse of D_i, 3-4 write-back.
+"""
+import ctypes as C
+import sys
+
+import numpy as np
+
+sys.path.insert(0, ".")
+from tests.rxpkg import rx, synth  # noqa: E402
+
+nx, ny, P = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (500, 200, 256)))
+mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=7, n_part=P)
+s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), rx.default_cfg(implicit=1, lin_prec=1, **kw))
+s.set_state(st)
+s.SetPrimitive_Gradient_LS()
+s.SetTime_Step()
+s.Preprocessing_zero()
+s.Upwind_Residual()
+s.Viscous_Residual()
+s.Source_Residual()
+s.ImplicitEuler_Iteration()
+n = 1 + 16 * 5 * 64
+buf = np.zeros(n, dtype=np.int64)
+rc = rx.lib().rx_debug_ilu_trace(s.h, buf.ctypes.data_as(C.c_void_p), C.c_int64(n))
+assert rc == 0, rc
+t = buf[1:].reshape(16, 64, 5)
+rows = t[(t[:, :, 0] > 0) & (t[:, :, 4] > 0)]
+t0 = rows[:, 0].min()
+d = np.diff(rows, axis=1)
+print("rows traced", len(rows), "kernel span (cycles)", buf[0] - t0)
+for k, name in enumerate(["loads", "products", "inverse", "writeback"]):
+    print(f"{name:10s} median {np.median(d[:, k]):8.0f}  mean {d[:, k].mean():8.0f}  max {d[:, k].max():8.0f}")
+print("row total median", np.median(rows[:, 4] - rows[:, 0]))
