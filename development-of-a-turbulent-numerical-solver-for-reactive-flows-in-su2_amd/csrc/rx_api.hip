@@ -282,10 +282,62 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
       }
       CK(dupload(ctx, &ctx->upd_ptr, uptr.data(), uptr.size()));
       CK(dupload(ctx, &ctx->upd, upd.data(), upd.size()));
+      // compact row plans in forward-schedule order (layout: rx_sweeps.hip, k_ilu_build_part); the
+      // order is recomputed exactly as schedule() builds it
+      std::vector<int32_t> fo(N);
+      {
+        std::vector<int32_t> lv(N, 0);
+        for (int64_t p = 0; p < np; ++p) {
+          const int64_t lo = ctx->h_part_ptr[p], hi = ctx->h_part_ptr[p + 1];
+          int32_t maxl = 0;
+          for (int64_t i = lo; i < hi; ++i) {
+            int32_t l = 0;
+            for (int32_t k = klo[i]; k < (int32_t)diag[i]; ++k) l = std::max(l, lv[col32[k]] + 1);
+            lv[i] = l;
+            maxl = std::max(maxl, l);
+          }
+          std::vector<int32_t> cnt(maxl + 2, 0);
+          for (int64_t i = lo; i < hi; ++i) cnt[lv[i] + 1]++;
+          for (int32_t l = 0; l <= maxl; ++l) cnt[l + 1] += cnt[l];
+          for (int64_t i = lo; i < hi; ++i) fo[lo + cnt[lv[i]]++] = (int32_t)i;
+        }
+      }
+      std::vector<int32_t> plan((size_t)N * 32, 0);
+      for (int64_t r = 0; r < N; ++r) {
+        const int32_t i = fo[r];
+        int32_t* rec = plan.data() + r * 32;
+        rec[0] = i;
+        rec[1] = klo[i];
+        rec[2] = (int32_t)diag[i];
+        rec[3] = khi[i];
+        rec[4] = (int32_t)ctx->h_rp[i];
+        rec[5] = (int32_t)ctx->h_rp[i + 1];
+        const int32_t nlow = (int32_t)diag[i] - klo[i];
+        int32_t npair = 0;
+        bool ok = nlow <= 3;
+        for (int32_t t = 0; t < nlow && ok; ++t) {
+          const int32_t k = klo[i] + t;
+          const int32_t nu = uptr[k + 1] - uptr[k];
+          if (nu > 3 || npair + nu > 9) {
+            ok = false;
+            break;
+          }
+          rec[8 + t] = col32[k];
+          rec[11 + t] = nu;
+          for (int32_t u = uptr[k]; u < uptr[k + 1]; ++u, ++npair) {
+            rec[14 + 2 * npair] = upd[2 * u];
+            rec[14 + 2 * npair + 1] = upd[2 * u + 1];
+          }
+        }
+        rec[6] = ok ? nlow : -1;
+        rec[7] = ok ? npair : 0;
+      }
+      CK(dupload(ctx, &ctx->ilu_plan, plan.data(), plan.size()));
     }
-    const size_t per_wave = sizeof(double) * (size_t)(rowmax + 7) * nv * nv;
+
+    const size_t per_wave = sizeof(double) * ((size_t)(rowmax + 7) * nv * nv + 16);
     if (per_wave > (size_t)ctx->lds_max) CK(RX_ERR_ARG);  // a row with more blocks than one wave's LDS slice
-    ctx->ilu_waves = (int)std::max<size_t>(1, std::min<size_t>({16, (size_t)std::max(1, ctx->fs.maxwidth),
+    ctx->ilu_waves = (int)std::max<size_t>(1, std::min<size_t>({12, (size_t)std::max(1, ctx->fs.maxwidth),
                                                                 (size_t)ctx->lds_max / per_wave}));
   }
   // LSQ neighbour lists (reference order) and boundary vertices per node
@@ -416,7 +468,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->nbr_ptr,
-                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd,
+                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.slot, ctx->bs.slot,
                   ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,

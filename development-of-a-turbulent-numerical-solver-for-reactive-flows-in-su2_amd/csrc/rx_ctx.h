@@ -52,6 +52,7 @@ struct rx_ctx {
   int rowmax = 1;               // max khi - klo
   int32_t* upd_ptr = nullptr;   // [nnzb+1] ILU update plan per lower block (rx_sweeps.hip)
   int32_t* upd = nullptr;       // [2 * n_upd] (kk, pos) pairs
+  int32_t* ilu_plan = nullptr;  // [N][32] per forward-schedule slot row plan (rx_sweeps.hip)
   int ilu_waves = 1;            // wavefronts per workgroup of the ILU factorisation
   // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
   // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])

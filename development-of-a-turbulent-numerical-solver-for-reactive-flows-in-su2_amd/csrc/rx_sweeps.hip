@@ -27,11 +27,19 @@ struct Blk {
   static constexpr int N2 = NV * NV;
 };
 
-// Lanes of one wavefront exchanging data through LDS: order the LDS traffic at wavefront scope.
+// LDS-only synchronisation. Lanes of one wavefront exchanging data through LDS need their LDS
+// operations complete (lgkmcnt(0)); outstanding global loads (prefetches into registers) are left in
+// flight — a fence would also wait vmcnt(0). The empty asm keeps the compiler from moving LDS
+// accesses across. lds_barrier() is the same for all waves of the workgroup (s_barrier); it is only
+// used where the data shared between waves lives in LDS.
 __device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // FGMRES hooks of the sweeps: skip when the solve is done; the first kernel of an iteration also
@@ -164,84 +172,199 @@ __global__ __launch_bounds__(256) void k_diag_factor(int N, const int64_t* __res
 
 // ---------------------------------------------------------------------------------------------
 // ILU(0) factorisation, one workgroup per partition, one wavefront per row.
-// Reads A, writes the factor F (the reference's copy into ILU_matrix is fused). invD receives inv(D_i) of every finished row (the reference recomputes
-// exactly this inverse from the same finished block whenever it needs it).
-// The update plan is static (host-built in rx_ctx_create): for every intra-partition lower block k =
-// (i, j) the list upd[upd_ptr[k] .. upd_ptr[k+1]) of (kk, pos) pairs, kk = (j, kp) an upper block of
-// row j with kp inside row i at BSR index pos, in increasing kk (the reference's loop order :1421-1443;
-// the diagonal kp = j is left out since it only touches A_ij, which is then overwritten by W).
-// A row stages everything it reads from finished rows (inv(A_jj) and the A_jk of the plan) in one
-// round trip together with its own blocks when it fits kStage blocks; otherwise per lower block.
-// LDS per wave: row blocks [rowmax][NV2] + W + staging [kStage][NV2].
+// Reads A, writes the factor F (the reference's copy into ILU_matrix is fused). invD receives inv(D_i)
+// of every finished row (the reference recomputes exactly this inverse from the same finished block
+// whenever it needs it).
+//
+// Row plan (host-built, rx_ctx_create; one 32-int record per forward-schedule slot):
+//   [0] i [1] k0=klo [2] kd=diag [3] k1=khi [4] rp[i] [5] rp[i+1] [6] nlow (-1: use the general plan)
+//   [7] npair [8..10] j of the lower blocks k0.. [11..13] update count per lower block
+//   [14..31] (kk, pos) pairs: kk = (j, kp) an upper block of row j with kp in row i at BSR index pos,
+//   in the reference's loop order (:1421-1443; kp = j is left out: it only touches A_ij, which is
+//   then overwritten by W). The general plan is upd_ptr/upd per lower block.
+// Per row: its own A blocks and plan were prefetched during the previous row; one round trip stages
+// inv(A_jj) and every A_jk it reads from finished rows; the products run from LDS; inv(D_i) is the
+// right-looking Gauss elimination with pivot rows broadcast through LDS.
+// LDS per wave: row blocks [rowmax][NV2] + W + staging [kStage][NV2] + plan[32].
 constexpr int kStage = 6;
+constexpr int kPlan = 32;
+constexpr int kPrefA = 10;  // doubles per lane of the next row's A blocks held in registers
+
+// inv(D) of the block in LDS at D (row-major), written to out (global) — Gauss elimination of every
+// unit column (InverseDiagonalBlock_ILUMatrix :1180-1228 via Gauss_Elimination :594-643), right-looking
+// as wave_factor_rows, pivot rows and the factors exchanged through the LDS scratch L (NV2 doubles).
 template <int NV>
-__global__ __launch_bounds__(1024) void k_ilu_build_part(const int32_t* __restrict__ part_lvl,
+__device__ __forceinline__ void wave_inverse_lds(const double* D, double* L, double* __restrict__ out, int lane) {
+  constexpr int NV2 = NV * NV;
+  double row[NV];
+#pragma unroll
+  for (int kk = 0; kk < NV; ++kk) row[kk] = lane < NV ? D[lane * NV + kk] : 1.0;
+#pragma unroll
+  for (int jj = 0; jj < NV - 1; ++jj) {
+    if (lane == jj) {
+#pragma unroll
+      for (int kk = jj; kk < NV; ++kk) L[jj * NV + kk] = row[kk];
+    }
+    wave_sync();
+    const double w = row[jj] / L[jj * NV + jj];
+    if (lane > jj && lane < NV) {
+#pragma unroll
+      for (int kk = jj + 1; kk < NV; ++kk) row[kk] -= w * L[jj * NV + kk];
+      row[jj] = w;
+    }
+    wave_sync();
+  }
+  if (lane < NV) {
+#pragma unroll
+    for (int kk = 0; kk < NV; ++kk) L[lane * NV + kk] = row[kk];
+  }
+  wave_sync();
+  // lane c: column c of the inverse
+  double rhs[NV];
+#pragma unroll
+  for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == lane) ? 1.0 : 0.0;
+#pragma unroll
+  for (int ii = 1; ii < NV; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < ii; ++jj) rhs[ii] -= L[ii * NV + jj] * rhs[jj];
+  rhs[NV - 1] = rhs[NV - 1] / L[NV2 - 1];
+#pragma unroll
+  for (int ii = NV - 2; ii >= 0; --ii) {
+    double aux = 0.0;
+#pragma unroll
+    for (int jj = ii + 1; jj < NV; ++jj) aux += L[ii * NV + jj] * rhs[jj];
+    rhs[ii] = (rhs[ii] - aux) / L[ii * NV + ii];
+  }
+  if (lane < NV) {
+#pragma unroll
+    for (int rr = 0; rr < NV; ++rr) out[rr * NV + lane] = rhs[rr];
+  }
+  wave_sync();
+}
+
+template <int NV>
+__global__ __launch_bounds__(768) void k_ilu_build_part(const int32_t* __restrict__ part_lvl,
                                                          const int32_t* __restrict__ lvl_ptr,
-                                                         const int4* __restrict__ slot,
+                                                         const int32_t* __restrict__ plan,
                                                          const int32_t* __restrict__ col,
                                                          const int32_t* __restrict__ upd_ptr,
-                                                         const int2* __restrict__ upd,
-                                                         const int32_t* __restrict__ rp, const double* __restrict__ A,
+                                                         const int2* __restrict__ upd, const double* __restrict__ A,
                                                          double* __restrict__ F, double* __restrict__ invD,
                                                          int rowmax, long long* __restrict__ trace) {
   constexpr int NV2 = NV * NV;
+  constexpr int PA = NV <= 11 ? kPrefA : 8;
   extern __shared__ double lds[];
   // optional phase trace of block 0 (tools/ilu_trace.py): per row of wave w: 5 stamps
   long long* tr = (trace && blockIdx.x == 0 && (threadIdx.x & 63) == 0) ? trace + 1 + (threadIdx.x >> 6) * 5 * 64
                                                                           : nullptr;
   int trow = 0;
-#define RX_STAMP(ph)                                                            \
-  do {                                                                          \
+#define RX_STAMP(ph)                                                                        \
+  do {                                                                                      \
     if (tr && trow < 64) tr[trow * 5 + (ph)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
-  double* rowbuf = lds + (size_t)wave * (rowmax + 1 + kStage) * NV2;
+  double* rowbuf = lds + (size_t)wave * ((rowmax + 1 + kStage) * NV2 + kPlan / 2);
   double* Wb = rowbuf + (size_t)rowmax * NV2;
   double* S = Wb + NV2;
+  int* rec = reinterpret_cast<int*>(S + kStage * NV2);
   const int p = blockIdx.x;
-  for (int l = part_lvl[p]; l < part_lvl[p + 1]; ++l) {
+  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  // next row of this wave after slot r of level l (same level, else a later level), -1 if none
+  auto next_slot = [&](int r, int l) -> int {
+    if (r + nwave < lvl_ptr[l + 1]) return r + nwave;
+    for (int ll = l + 1; ll < l1; ++ll)
+      if (lvl_ptr[ll] + wave < lvl_ptr[ll + 1]) return lvl_ptr[ll] + wave;
+    return -1;
+  };
+  int pr = -1;  // first slot of this wave
+  for (int ll = l0; ll < l1 && pr < 0; ++ll)
+    if (lvl_ptr[ll] + wave < lvl_ptr[ll + 1]) pr = lvl_ptr[ll] + wave;
+  int prec = 0;
+  double pa[PA];
+#pragma unroll
+  for (int t = 0; t < PA; ++t) pa[t] = 0.0;
+  if (pr >= 0) {
+    if (lane < kPlan) prec = plan[(size_t)pr * kPlan + lane];
+    const int k0 = __builtin_amdgcn_readlane(prec, 1), k1 = __builtin_amdgcn_readlane(prec, 3);
+#pragma unroll
+    for (int t = 0; t < PA; ++t) {
+      const int q = lane + 64 * t;
+      if (q < (k1 - k0) * NV2) pa[t] = A[(size_t)k0 * NV2 + q];
+    }
+  }
+  for (int l = l0; l < l1; ++l) {
     for (int r = lvl_ptr[l] + wave; r < lvl_ptr[l + 1]; r += nwave) {
       RX_STAMP(0);
-      const int4 sl = slot[r];
-      const int i = sl.x, k0 = sl.y, kd = sl.z, k1 = sl.w;
+      // this row's plan and A blocks (prefetched)
+      if (lane < kPlan) rec[lane] = prec;
+      const int i = __builtin_amdgcn_readlane(prec, 0), k0 = __builtin_amdgcn_readlane(prec, 1),
+                kd = __builtin_amdgcn_readlane(prec, 2), k1 = __builtin_amdgcn_readlane(prec, 3),
+                ra = __builtin_amdgcn_readlane(prec, 4), rb = __builtin_amdgcn_readlane(prec, 5),
+                nlow = __builtin_amdgcn_readlane(prec, 6), npair = __builtin_amdgcn_readlane(prec, 7);
       const int nbk = k1 - k0;
-      const int ua = upd_ptr[k0], ub = upd_ptr[kd];
-      const bool all = (kd - k0) + (ub - ua) <= kStage;  // stage the whole row at once
-      for (int q = lane; q < nbk * NV2; q += 64) rowbuf[q] = A[(size_t)k0 * NV2 + q];
-      {  // blocks of the row outside the partition are copied unchanged (SetBlock_ILUMatrix :1378-1389)
-        const int ra = rp[i], rb = rp[i + 1];
-        for (int q = lane; q < (k0 - ra) * NV2; q += 64) F[(size_t)ra * NV2 + q] = A[(size_t)ra * NV2 + q];
-        for (int q = lane; q < (rb - k1) * NV2; q += 64) F[(size_t)k1 * NV2 + q] = A[(size_t)k1 * NV2 + q];
+#pragma unroll
+      for (int t = 0; t < PA; ++t) {
+        const int q = lane + 64 * t;
+        if (q < nbk * NV2) rowbuf[q] = pa[t];
       }
-      if (all) {
-        // staging order: for each lower k: inv(A_jj), then its plan blocks
-        int slotn = 0;
-        for (int k = k0; k < kd; ++k) {
-          const int j = col[k];
-          for (int q = lane; q < NV2; q += 64) S[slotn * NV2 + q] = invD[(size_t)j * NV2 + q];
-          ++slotn;
-          for (int u = upd_ptr[k]; u < upd_ptr[k + 1]; ++u, ++slotn) {
-            const int kk = upd[u].x;
-            for (int q = lane; q < NV2; q += 64) S[slotn * NV2 + q] = F[(size_t)kk * NV2 + q];
+      for (int q = lane + 64 * PA; q < nbk * NV2; q += 64) rowbuf[q] = A[(size_t)k0 * NV2 + q];
+      // blocks of the row outside the partition are copied unchanged (SetBlock_ILUMatrix :1378-1389)
+      for (int q = lane; q < (k0 - ra) * NV2; q += 64) F[(size_t)ra * NV2 + q] = A[(size_t)ra * NV2 + q];
+      for (int q = lane; q < (rb - k1) * NV2; q += 64) F[(size_t)k1 * NV2 + q] = A[(size_t)k1 * NV2 + q];
+      const bool fast = nlow >= 0 && nlow + npair <= kStage;
+      if (fast) {  // one round trip: inv(A_jj) of every lower block, then the plan's A_jk blocks
+        constexpr int PER = (NV2 + 63) / 64;
+        double stg[kStage][PER];
+#pragma unroll
+        for (int t = 0; t < kStage; ++t) {
+          const double* src = nullptr;
+          if (t < nlow) src = invD + (size_t)__builtin_amdgcn_readlane(prec, 8 + (t < 3 ? t : 0)) * NV2;
+          else if (t < nlow + npair) src = F + (size_t)__builtin_amdgcn_readlane(prec, 14 + 2 * (t - nlow)) * NV2;
+#pragma unroll
+          for (int u = 0; u < PER; ++u) {
+            const int q = lane + 64 * u;
+            if (src && q < NV2) stg[t][u] = src[q];
           }
+        }
+#pragma unroll
+        for (int t = 0; t < kStage; ++t)
+          if (t < nlow + npair) {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+              const int q = lane + 64 * u;
+              if (q < NV2) S[t * NV2 + q] = stg[t][u];
+            }
+          }
+      }
+      // prefetch the next row's plan and A blocks (inputs only)
+      const int nr = next_slot(r, l);
+      if (nr >= 0) {
+        if (lane < kPlan) prec = plan[(size_t)nr * kPlan + lane];
+        const int nk0 = __builtin_amdgcn_readlane(prec, 1), nk1 = __builtin_amdgcn_readlane(prec, 3);
+#pragma unroll
+        for (int t = 0; t < PA; ++t) {
+          const int q = lane + 64 * t;
+          if (q < (nk1 - nk0) * NV2) pa[t] = A[(size_t)nk0 * NV2 + q];
         }
       }
       wave_sync();
       RX_STAMP(1);
-      int slotn = 0;
+      int pcur = 0;
       for (int k = k0; k < kd; ++k) {
-        const int u0 = upd_ptr[k], u1 = upd_ptr[k + 1];
+        const int t = k - k0;
         const double* Sinv;
-        if (all) {
-          Sinv = S + (size_t)slotn * NV2;
-          ++slotn;
+        int u0 = 0, u1 = 0;
+        if (fast) {
+          Sinv = S + (size_t)t * NV2;
         } else {
           const int j = col[k];
+          u0 = upd_ptr[k];
+          u1 = upd_ptr[k + 1];
           for (int q = lane; q < NV2; q += 64) S[q] = invD[(size_t)j * NV2 + q];
           wave_sync();
           Sinv = S;
         }
-        const double* Bij = rowbuf + (size_t)(k - k0) * NV2;
+        const double* Bij = rowbuf + (size_t)t * NV2;
         // W = A_ij * inv(A_jj)  (MatrixMatrixProduct, sum from 0.0 over q ascending)
         for (int e = lane; e < NV2; e += 64) {
           const int a = e / NV, c = e - a * NV;
@@ -252,19 +375,23 @@ __global__ __launch_bounds__(1024) void k_ilu_build_part(const int32_t* __restri
         }
         wave_sync();
         // A_ik -= A_jk * W (left-multiply quirk), in increasing kk
-        for (int u = u0; u < u1; ++u) {
-          const int2 h = upd[u];
+        const int nu = fast ? rec[11 + t] : (u1 - u0);
+        for (int h = 0; h < nu; ++h) {
           const double* Bjk;
-          if (all) {
-            Bjk = S + (size_t)slotn * NV2;
-            ++slotn;
+          int pos;
+          if (fast) {
+            Bjk = S + (size_t)(nlow + pcur) * NV2;
+            pos = rec[14 + 2 * pcur + 1];
+            ++pcur;
           } else {
+            const int2 hh = upd[u0 + h];
             wave_sync();
-            for (int q = lane; q < NV2; q += 64) S[NV2 + q] = F[(size_t)h.x * NV2 + q];
+            for (int q = lane; q < NV2; q += 64) S[NV2 + q] = F[(size_t)hh.x * NV2 + q];
             wave_sync();
             Bjk = S + NV2;
+            pos = hh.y;
           }
-          double* Bik = rowbuf + (size_t)(h.y - k0) * NV2;
+          double* Bik = rowbuf + (size_t)(pos - k0) * NV2;
           for (int e = lane; e < NV2; e += 64) {
             const int a = e / NV, c = e - a * NV;
             double s = 0.0;
@@ -274,26 +401,12 @@ __global__ __launch_bounds__(1024) void k_ilu_build_part(const int32_t* __restri
           }
         }
         wave_sync();
-        double* dst = rowbuf + (size_t)(k - k0) * NV2;
+        double* dst = rowbuf + (size_t)t * NV2;
         for (int e = lane; e < NV2; e += 64) dst[e] = Wb[e];
         wave_sync();
       }
       RX_STAMP(2);
-      // inv(D_i): Gauss elimination of each unit column (InverseDiagonalBlock_ILUMatrix)
-      {
-        const double* D = rowbuf + (size_t)(kd - k0) * NV2;
-        double rw[NV], rhs[NV];
-#pragma unroll
-        for (int kk = 0; kk < NV; ++kk) rw[kk] = lane < NV ? D[lane * NV + kk] : 1.0;
-        wave_factor_rows<NV>(rw, lane);
-#pragma unroll
-        for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == lane) ? 1.0 : 0.0;
-        wave_solve_rows<NV>(rw, rhs);
-        if (lane < NV) {
-#pragma unroll
-          for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + lane] = rhs[rr];
-        }
-      }
+      wave_inverse_lds<NV>(rowbuf + (size_t)(kd - k0) * NV2, Wb, invD + (size_t)i * NV2, lane);
       RX_STAMP(3);
       for (int q = lane; q < nbk * NV2; q += 64) F[(size_t)k0 * NV2 + q] = rowbuf[q];
       wave_sync();
@@ -454,7 +567,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
     bsl[q] = b_slot[br0 + q];
   }
   for (int q = threadIdx.x; q < ke - kb; q += blockDim.x) colL[q] = col[kb + q] - lo;
-  __syncthreads();
+  lds_barrier();
   for (int l = fl0; l < fl1; ++l) {
     const int r0 = f_lvl_ptr[l], r1 = f_lvl_ptr[l + 1];
     if (lane_ok && l + 1 < fl1 && r1 + rl < f_lvl_ptr[l + 2]) {
@@ -485,7 +598,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
       }
       xs[li * NV + a] = xi;
     }
-    __syncthreads();
+    lds_barrier();
     cur = nxt;
   }
   // backward: upper blocks + the row of inv(D_i)
@@ -535,7 +648,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
         }
         v[rl * NV + a] = xs[li * NV + a] - sum;
       }
-      __syncthreads();
+      lds_barrier();
       if (act) {
         double s = 0.0;
         if (first) {
@@ -548,7 +661,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
         }
         xs[li * NV + a] = s;
       }
-      __syncthreads();
+      lds_barrier();
     }
     ucur = unxt;
 #pragma unroll
@@ -701,11 +814,11 @@ int rx_la_prepare(rx_ctx* ctx) {
 int rx_la_ilu_build(rx_ctx* ctx) {
   const int nv = ctx->nVar;
   const int waves = ctx->ilu_waves;
-  const size_t shm = sizeof(double) * (size_t)waves * (ctx->rowmax + 1 + kStage) * nv * nv;
+  const size_t shm = sizeof(double) * (size_t)waves * ((ctx->rowmax + 1 + kStage) * nv * nv + kPlan / 2);
   RX_NV_SWITCH(nv, (k_ilu_build_part<NV_><<<ctx->npart, 64 * waves, shm, ctx->stream>>>(
-                       ctx->fs.part_lvl, ctx->fs.lvl_ptr, reinterpret_cast<const int4*>(ctx->fs.slot), ctx->col,
-                       ctx->upd_ptr, reinterpret_cast<const int2*>(ctx->upd), ctx->rp, ctx->f[RX_F_JAC],
-                       ctx->f[RX_F_ILU], rx_invd_buf(ctx), ctx->rowmax, ctx->ilu_trace)));
+                       ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_plan, ctx->col, ctx->upd_ptr,
+                       reinterpret_cast<const int2*>(ctx->upd), ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
+                       rx_invd_buf(ctx), ctx->rowmax, ctx->ilu_trace)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }

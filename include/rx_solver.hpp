@@ -1,0 +1,98 @@
+/* rx_solver.hpp — C++ host mirror of the reference's CReactiveNSSolver phase surface over the C ABI
+ * of rx.h (header-only; link with librx.so).
+ *
+ * The methods keep the reference's names, call order and error behaviour
+ * (SU2_CFD/include/solver_reactive.hpp:141-363, 476-554):
+ *   Preprocessing residual reset  -> rx_residual_zero            (LinSysRes.SetValZero, Jacobian.SetValZero)
+ *   SetPrimitive_Gradient_LS      -> rx_grad_lsq                 (solver_direct_reactive.cpp:4887-5050)
+ *   SetPrimitive_Limiter          -> rx_limiter_venkat           (:1328-1523)
+ *   SetTime_Step                  -> rx_time_step                (:5057-5298)
+ *   Upwind_Residual               -> rx_edge_flux_conv           (:2535-2785)  throws "NaN found in the upwind residual"
+ *   Viscous_Residual              -> rx_edge_flux_visc           (:5305-5386)  throws "NaN found in the viscous residual"
+ *   Source_Residual               -> rx_cell_source_pasr         (:2792-2874)  throws "NaN found in the source residual"
+ *   ExplicitEuler_Iteration       -> rx_explicit_euler           (:2414-2449)
+ *   ImplicitEuler_Iteration       -> rx_implicit_euler           (:2336-2407)
+ * A spline lookup outside the property tables throws std::out_of_range (MathTools::GetSpline,
+ * Common/src/spline.cpp:62-77); any other failure throws std::runtime_error with rx_status_string.
+ * Ownership: the solver owns one rx_ctx (device state); host arrays are copied at construction /
+ * upload and never retained.
+ */
+#ifndef RX_SOLVER_HPP
+#define RX_SOLVER_HPP
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rx.h"
+
+namespace rx {
+
+class ReactiveNSSolver {
+ public:
+  ReactiveNSSolver(const rx_mesh_desc& mesh, const rx_mech_desc& mech, const rx_cfg& cfg, int device = 0)
+      : cfg_(cfg) {
+    check(rx_ctx_create(&mesh, &mech, &cfg, device, &ctx_), "rx_ctx_create");
+    nvar_ = mech.n_species + mesh.n_dim + 2;
+  }
+  ~ReactiveNSSolver() { rx_ctx_destroy(ctx_); }
+  ReactiveNSSolver(const ReactiveNSSolver&) = delete;
+  ReactiveNSSolver& operator=(const ReactiveNSSolver&) = delete;
+
+  rx_ctx* context() const { return ctx_; }
+  int nVar() const { return nvar_; }
+
+  // ---- node state (Preprocessing output of the reference: primitives, transport, SST fields)
+  void Upload(rx_field f, const std::vector<double>& host) {
+    check(rx_upload(ctx_, f, host.data(), (int64_t)host.size()), "rx_upload");
+  }
+  std::vector<double> Download(rx_field f) const {
+    int64_t n = 0;
+    check(rx_field_size(ctx_, f, &n), "rx_field_size");
+    std::vector<double> h((size_t)n);
+    check(rx_download(ctx_, f, h.data(), n), "rx_download");
+    return h;
+  }
+
+  // ---- phases, reference names
+  void Preprocessing() { check(rx_residual_zero(ctx_), "Preprocessing"); }
+  void SetPrimitive_Gradient_LS() { check(rx_grad_lsq(ctx_), "SetPrimitive_Gradient_LS"); }
+  void SetPrimitive_Limiter() { check(rx_limiter_venkat(ctx_), "SetPrimitive_Limiter"); }
+  void SetTime_Step() { check(rx_time_step(ctx_), "SetTime_Step"); }
+  void Upwind_Residual() { phase(rx_edge_flux_conv(ctx_), "NaN found in the upwind residual"); }
+  void Viscous_Residual() { phase(rx_edge_flux_visc(ctx_), "NaN found in the viscous residual"); }
+  void Source_Residual() { phase(rx_cell_source_pasr(ctx_), "NaN found in the source residual"); }
+  std::vector<double> ExplicitEuler_Iteration() {
+    std::vector<double> rms((size_t)nvar_);
+    check(rx_explicit_euler(ctx_, rms.data()), "ExplicitEuler_Iteration");
+    return rms;
+  }
+  std::vector<double> ImplicitEuler_Iteration(int* lin_iters = nullptr) {
+    std::vector<double> rms((size_t)nvar_);
+    int it = 0;
+    check(rx_implicit_euler(ctx_, rms.data(), &it), "ImplicitEuler_Iteration");
+    if (lin_iters) *lin_iters = it;
+    return rms;
+  }
+  void Synchronize() { check(rx_sync(ctx_), "rx_sync"); }
+
+ private:
+  void phase(int rc, const char* nan_msg) {
+    if (rc == RX_OK) rc = rx_sync(ctx_);
+    if (rc == RX_ERR_NAN) throw std::runtime_error(nan_msg);
+    check(rc, nan_msg);
+  }
+  void check(int rc, const char* what) const {
+    if (rc == RX_OK) return;
+    if (rc == RX_ERR_RANGE) throw std::out_of_range(std::string(what) + ": " + rx_status_string(rc));
+    throw std::runtime_error(std::string(what) + ": " + rx_status_string(rc) + " (index " +
+                             std::to_string((long long)rx_last_error_index(ctx_)) + ")");
+  }
+  rx_ctx* ctx_ = nullptr;
+  rx_cfg cfg_;
+  int nvar_ = 0;
+};
+
+}  // namespace rx
+
+#endif

@@ -1,0 +1,136 @@
+// rx_driver.cpp — C++ host driver in the reference's CIntegration call order over include/rx_solver.hpp.
+// Test harness (tests/test_cpp_driver.py): reads a case directory of raw little-endian arrays
+// (<name>.f64 / <name>.i64 / <name>.i32), runs one explicit residual evaluation and one implicit
+// iteration, writes the results back as <name>.f64.
+//
+//   rx_driver <case_dir> <implicit 0|1>
+#include <cstdint>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "rx_solver.hpp"
+
+template <typename T>
+static std::vector<T> load(const std::string& dir, const std::string& name, const char* ext) {
+  std::ifstream f(dir + "/" + name + ext, std::ios::binary | std::ios::ate);
+  if (!f) throw std::runtime_error("missing " + name + ext);
+  const std::streamsize n = f.tellg();
+  f.seekg(0);
+  std::vector<T> v((size_t)n / sizeof(T));
+  f.read(reinterpret_cast<char*>(v.data()), n);
+  return v;
+}
+static std::vector<double> f64(const std::string& d, const std::string& n) { return load<double>(d, n, ".f64"); }
+static std::vector<int64_t> i64(const std::string& d, const std::string& n) { return load<int64_t>(d, n, ".i64"); }
+static std::vector<int32_t> i32(const std::string& d, const std::string& n) { return load<int32_t>(d, n, ".i32"); }
+static void save(const std::string& dir, const std::string& name, const std::vector<double>& v) {
+  std::ofstream f(dir + "/" + name + ".f64", std::ios::binary);
+  f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(double)));
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    std::cerr << "usage: rx_driver <case_dir> <implicit>\n";
+    return 2;
+  }
+  const std::string d = argv[1];
+  const int implicit = std::atoi(argv[2]);
+  try {
+    // mesh
+    auto edges = i64(d, "edges"), nbr_ptr = i64(d, "nbr_ptr"), nbr = i64(d, "nbr"), bvert = i64(d, "bvertex");
+    auto normal = f64(d, "edge_normal"), coord = f64(d, "coord"), vol = f64(d, "volume"), bn = f64(d, "bvertex_normal");
+    rx_mesh_desc mesh{};
+    mesh.n_dim = 2;
+    mesh.n_point = (int64_t)vol.size();
+    mesh.n_edge = (int64_t)edges.size() / 2;
+    mesh.n_bvert = (int64_t)bvert.size() / 2;
+    mesh.edges = edges.data();
+    mesh.edge_normal = normal.data();
+    mesh.coord = coord.data();
+    mesh.volume = vol.data();
+    mesh.nbr_ptr = nbr_ptr.data();
+    mesh.nbr = nbr.data();
+    mesh.bvert = bvert.data();
+    mesh.bvert_normal = bn.data();
+    // mechanism
+    auto mm = f64(d, "mech_mmass"), dv = f64(d, "mech_diff_vol"), sr = f64(d, "mech_stoich_reac"),
+         sp = f64(d, "mech_stoich_prod"), er = f64(d, "mech_exp_reac"), ep = f64(d, "mech_exp_prod"), A = f64(d, "mech_A"),
+         be = f64(d, "mech_beta"), Ta = f64(d, "mech_Ta"), Ab = f64(d, "mech_A_back"), beb = f64(d, "mech_beta_back"),
+         Tab = f64(d, "mech_Ta_back"), tx = f64(d, "mech_tab_x"), ty = f64(d, "mech_tab_y"), ty2 = f64(d, "mech_tab_y2");
+    auto rev = i32(d, "mech_reversible"), hb = i32(d, "mech_has_backward");
+    rx_mech_desc mech{};
+    mech.n_species = (int32_t)mm.size();
+    mech.n_reactions = (int32_t)A.size();
+    mech.n_tab = (int32_t)(tx.size() / (5 * mm.size()));
+    mech.mmass = mm.data();
+    mech.diff_vol = dv.data();
+    mech.stoich_reac = sr.data();
+    mech.stoich_prod = sp.data();
+    mech.exp_reac = er.data();
+    mech.exp_prod = ep.data();
+    mech.A = A.data();
+    mech.beta = be.data();
+    mech.Ta = Ta.data();
+    mech.A_back = Ab.data();
+    mech.beta_back = beb.data();
+    mech.Ta_back = Tab.data();
+    mech.reversible = rev.data();
+    mech.has_backward = hb.data();
+    mech.tab_x = tx.data();
+    mech.tab_y = ty.data();
+    mech.tab_y2 = ty2.data();
+    // configuration: [mach_inf, Pr_t, Le_t, c_mu, pasr_lb, cfl]
+    auto c = f64(d, "cfg");
+    rx_cfg cfg{};
+    cfg.mach_inf = c[0];
+    cfg.T_ref = cfg.E_ref = cfg.R_ref = cfg.rho_ref = cfg.t_ref = 1.0;
+    cfg.prandtl_lam = 0.72;
+    cfg.prandtl_turb = c[1];
+    cfg.lewis_turb = c[2];
+    cfg.c_mu = c[3];
+    cfg.pasr_lb = c[4];
+    cfg.cfl = c[5];
+    cfg.max_delta_time = 1e6;
+    cfg.ref_elem_length = 0.1;
+    cfg.limiter_coeff = 0.5;
+    cfg.lin_tol = 1e-6;
+    cfg.relaxation = 1.0;
+    cfg.implicit = implicit;
+    cfg.rans = 1;
+    cfg.lin_iter = 5;
+    cfg.lin_prec = 1;
+
+    rx::ReactiveNSSolver solver(mesh, mech, cfg, 0);
+    const struct {
+      const char* name;
+      rx_field f;
+    } state[] = {{"U", RX_F_U},          {"V", RX_F_V},         {"dPdU", RX_F_DPDU},   {"dTdU", RX_F_DTDU},
+                 {"mu", RX_F_MU},        {"kappa", RX_F_KAPPA}, {"Dij", RX_F_DIJ},     {"grad_prim", RX_F_GRAD},
+                 {"turb_k", RX_F_TKE},   {"turb_omega", RX_F_OMEGA}, {"mu_t", RX_F_MUT}, {"sigma_k", RX_F_SIGMAK},
+                 {"grad_k", RX_F_GRADK}, {"eddy_visc_flow", RX_F_EDDY}};
+    for (const auto& s : state) solver.Upload(s.f, f64(d, s.name));
+
+    // CIntegration::Space_Integration order (integration_structure.cpp:72-193), then Time_Integration
+    solver.SetTime_Step();
+    solver.Preprocessing();
+    solver.Upwind_Residual();
+    solver.Viscous_Residual();
+    solver.Source_Residual();
+    save(d, "out_res", solver.Download(RX_F_RES));
+    save(d, "out_dt", solver.Download(RX_F_DT));
+    std::vector<double> rms;
+    int lin_iters = 0;
+    if (implicit) rms = solver.ImplicitEuler_Iteration(&lin_iters);
+    else rms = solver.ExplicitEuler_Iteration();
+    save(d, "out_u", solver.Download(RX_F_U));
+    save(d, "out_rms", rms);
+    std::printf("ok lin_iters=%d\n", lin_iters);
+  } catch (const std::exception& e) {
+    std::printf("exception: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -1,0 +1,11 @@
+#!/bin/bash
+# One GPU verification cycle (run through gpurun from the repo root): GPU parity tests, the ILU
+# phase trace, a bench line and a rocprofv3 kernel-trace summary. Every GPU step has its own time
+# limit; a failing step ends the script (set -e semantics via &&).
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -q -m gpu -rA --tb=short > gpurun_out/gpu_tests.log 2>&1
+echo "pytest rc=$?"
+timeout -k 10 300 python tools/ilu_trace.py > gpurun_out/trace.log 2>&1 && echo "trace ok" &&
+timeout -k 10 400 python bench.py --steps 20 --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} > gpurun_out/bench.log 2>&1 && echo "bench ok" &&
+R=$PWD && cd /tmp && export TMPDIR=/tmp &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof.log 2>&1 && echo "prof ok"
