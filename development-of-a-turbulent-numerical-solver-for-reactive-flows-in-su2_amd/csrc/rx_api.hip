@@ -445,6 +445,7 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
     CK(dalloc(ctx, &ctx->fconv, E * nv));
     CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
+    CK(dalloc(ctx, &ctx->vsumm, E * (int64_t)(24 + 9 * ns)));
     CK(dalloc(ctx, &ctx->jsrc, N * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->rsrc, N * nv));
     CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
@@ -471,7 +472,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.slot, ctx->bs.slot,
-                  ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
+                  ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
   if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);

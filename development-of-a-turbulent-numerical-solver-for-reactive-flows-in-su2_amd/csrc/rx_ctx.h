@@ -80,6 +80,7 @@ struct rx_ctx {
   double* fvisc = nullptr;   // [E][nVar]   viscous edge fluxes
   double* jconv = nullptr;   // [E][2][nVar*nVar]
   double* jvisc = nullptr;   // [E][2][nVar*nVar]
+  double* vsumm = nullptr;   // [E][visc_summary_size] per-edge viscous summary (implicit)
   double* jsrc = nullptr;    // [N][nVar*nVar]
   double* rsrc = nullptr;    // [N][nVar] source residual (implicit path)
   int phase_conv = 0, phase_visc = 0, phase_src = 0, assembled = 1;

@@ -133,8 +133,8 @@ __global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restri
                                                   const double* __restrict__ tke, const double* __restrict__ mut,
                                                   const double* __restrict__ sigk, const double* __restrict__ gk,
                                                   DevMech m, ViscParams P, double* __restrict__ F,
-                                                  double* __restrict__ Jac, int* err) {
-  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nG = NS + NDIM + 2, nVar2 = nVar * nVar;
+                                                  double* __restrict__ Summ, int* err) {
+  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nG = NS + NDIM + 2;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
   const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
@@ -170,9 +170,8 @@ __global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restri
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
   double res[nVar];
-  double* Ji = P.implicit ? Jac + (size_t)e * 2 * nVar2 : nullptr;
-  double* Jj = P.implicit ? Ji + nVar2 : nullptr;
-  const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, Ji, Jj);
+  double* summ = P.implicit ? Summ + (size_t)e * visc_summary_size<NS>() : nullptr;
+  const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ);
   bool bad = false;
 #pragma unroll
   for (int v = 0; v < nVar; ++v) {
@@ -181,6 +180,23 @@ __global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restri
   }
   if (rc != ERR_NONE) set_err(err, rc == ERR_RANGE ? ERR_RANGE : ERR_NAN, e);
   else if (bad) set_err(err, ERR_NAN, e);
+}
+
+// a6: viscous Jacobians from the per-edge summary; a team of 16 lanes per edge, lane b = column b,
+// so every row of Ji / Jj is stored as one contiguous segment per team.
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) void k_visc_jac(int E, const int32_t* __restrict__ edges,
+                                                     const double* __restrict__ dTdU, const double* __restrict__ Summ,
+                                                     DevMech m, ViscParams P, double* __restrict__ Jac) {
+  constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = gt / 16, b = gt % 16;
+  if (e >= E) return;  // whole teams exit together (E * 16 threads)
+  const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+  const int bc = b < nVar ? b : 0;
+  const double sib = dTdU[(size_t)n0 * nVar + bc], sjb = dTdU[(size_t)n1 * nVar + bc];
+  double* Ji = Jac + (size_t)e * 2 * nVar2;
+  visc_jac_column<NS, NDIM>(m, P, Summ + (size_t)e * visc_summary_size<NS>(), sib, sjb, b, b, Ji, Ji + nVar2);
 }
 
 // Generic node gather of an edge flux array: node0 += sign*F, node1 -= sign*F (edge order).
@@ -608,8 +624,13 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_GRAD],
                             ctx->f[RX_F_MU], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_DTDU],
                             ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_SIGMAK], ctx->f[RX_F_GRADK], ctx->mech,
-                            P, ctx->fvisc, ctx->jvisc, ctx->err)));
+                            P, ctx->fvisc, ctx->vsumm, ctx->err)));
   RX_HIP(hipGetLastError());
+  if (ctx->cfg.implicit) {
+    RX_NS_SWITCH(ctx->ns, (k_visc_jac<NS_, 2><<<blocks(ctx->E * 16), kBlock, 0, ctx->stream>>>(
+                              (int)ctx->E, ctx->edges, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->mech, P, ctx->jvisc)));
+    RX_HIP(hipGetLastError());
+  }
   return RX_OK;
 }
 

@@ -268,6 +268,15 @@ __device__ inline void colpiv_qr_solve(double* Q, const double (*rhs)[NDIM], dou
   }
 }
 
+// Per-edge summary written by visc_edge (implicit) for the Jacobian kernel: scalars, then nine
+// species arrays (Xs_i, Xs_j, Ys, hs, Cps, Jd, Gxn/|n|, Ds, quirk aux).
+enum {
+  VS_MU = 0, VS_K, VS_MUT, VS_RHO, VS_VM, VS_RHOI = 6, VS_RHOJ, VS_VI, VS_VJ = 10, VS_THETA = 12, VS_DIJ, VS_DS,
+  VS_UN, VS_PF = 17, VS_TM = 19, VS_TMI, VS_TMJ, VS_SGI, VS_SGJ, VS_ARR
+};
+template <int NS>
+constexpr int visc_summary_size() { return VS_ARR + 9 * NS; }
+
 // Per-edge inputs gathered from the two node records.
 template <int NS, int NDIM>
 struct ViscNode {
@@ -279,7 +288,7 @@ struct ViscNode {
 template <int NS, int NDIM>
 __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const ViscNode<NS, NDIM>& ni,
                                 const ViscNode<NS, NDIM>& nj, double sigma_k, const double* Normal, double* res,
-                                double* Ji, double* Jj) {
+                                double* summ) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
   constexpr int T_P = 0, VX_P = 1, RHO_P = NDIM + 2, RHOS_P = NDIM + 5;
   constexpr int RHO_S = 0, RHOVX_S = 1, RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
@@ -490,7 +499,7 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   for (int v = 0; v < nVar; ++v) res[v] = PF[v];
   if (!P.implicit) return err;
 
-  // ---- implicit part (:1576-1653): dF/dV (sparse structure built explicitly) times dV/dU
+  // ---- implicit part: the per-edge summary the Jacobian kernel (visc_jac_column) needs
   double Ds[NS];
   {
     double Ds_i[NS], Ds_j[NS];
@@ -522,180 +531,267 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   for (int d = 0; d < NDIM; ++d) UN[d] = Normal[d] / Area;
 #pragma unroll
   for (int s = 0; s < NS; ++s) Gxn[s] /= Area;
-  const double dij = sqrt(dist2), dS = Area;
   double theta = 0.0;
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) theta += UN[d] * UN[d];
-  const double rho_i = Vi[RHO_P], rho_j = Vj[RHO_P];
+  if (!P.rans) {
 #pragma unroll
-  for (int s = 0; s < NS; ++s) Cps[s] = spline(m, P_CP, s, dim_temp, &err) / m.mm[s] / P.R_ref;
-
-  // dF/dV for both sides, full nVar x nVar (zero-initialised, as the reference).
-  double FI[nVar][nVar], FJ[nVar][nVar];
-#pragma unroll
-  for (int a = 0; a < nVar; ++a)
-#pragma unroll
-    for (int b = 0; b < nVar; ++b) FI[a][b] = FJ[a][b] = 0.0;
-  {
-    // dJ/drho for the Stefan-Maxwell diffusion, [NS][NS+1] (column 0 never set: quirk :1249-1252)
-    double totMass = 0.0, totMass_i = 0.0, totMass_j = 0.0, sigma_i = 0.0, sigma_j = 0.0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) totMass += m.mm[s] * Xs[s];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) totMass_i += m.mm[s] * Xs_i[s];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) totMass_j += m.mm[s] * Xs_j[s];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) sigma_i += Xs_i[s];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) sigma_j += Xs_j[s];
-    const double mu = Mean_mu, ktr = Mean_k;
-    if (NDIM == 2) {
-      const double thetax = theta + UN[0] * UN[0] / 3.0, thetay = theta + UN[NDIM - 1] * UN[NDIM - 1] / 3.0;
-      const double etaz = UN[0] * UN[NDIM - 1] / 3.0;
-      const double pix = Vm[VX_P] * thetax + Vm[VX_P + 1] * etaz;
-      const double piy = Vm[VX_P] * etaz + Vm[VX_P + 1] * thetay;
-      FJ[RHOVX_S][RHOVX_S] = mu * thetax / dij * dS;
-      FJ[RHOVX_S][RHOVX_S + 1] = mu * etaz / dij * dS;
-      FJ[RHOVX_S + 1][RHOVX_S] = mu * etaz / dij * dS;
-      FJ[RHOVX_S + 1][RHOVX_S + 1] = mu * thetay / dij * dS;
-      FJ[RHOE_S][RHOVX_S] = pix * mu / dij * dS;
-      FJ[RHOE_S][RHOVX_S + 1] = piy * mu / dij * dS;
-      FJ[RHOE_S][RHOE_S] = ktr * theta / dij * dS;
-    }
-#pragma unroll
-    for (int a = 0; a < nVar; ++a)
-#pragma unroll
-      for (int b = 0; b < nVar; ++b) FI[a][b] = -FJ[a][b];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      FI[RHOE_S][RHOE_S] += -0.5 * Jd[s] * Cps[s];
-      FJ[RHOE_S][RHOE_S] += -0.5 * Jd[s] * Cps[s];
-    }
-    // species rows: dJdr[a][k+1]
-    double dj_[NS][NS], di_[NS][NS];
-#pragma unroll
-    for (int a = 0; a < NS; ++a)
-#pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        double vj = -rho * m.mm[a] * Ds[a] * Xs_j[a] / (totMass * dij * sigma_j * rho_j);
-        double vi = rho * m.mm[a] * Ds[a] * Xs_i[a] / (totMass * dij * sigma_i * rho_i);
-#pragma unroll
-        for (int b = 0; b < NS; ++b) {
-          vj += rho * Ys[a] * m.mm[b] * Ds[b] * Xs_j[b] / (totMass * dij * sigma_j * rho_j);
-          vi -= rho * Ys[a] * m.mm[b] * Ds[b] * Xs_i[b] / (totMass * dij * sigma_i * rho_i);
-        }
-        vj += rho * Ys[a] * Ds[k] * totMass_j * sigma_j / (dij * totMass * rho_j);
-        vi -= rho * Ys[a] * Ds[k] * totMass_i * sigma_i / (dij * totMass * rho_i);
-        if (a == k) {
-          vj -= rho * Ds[a] * totMass_j * sigma_j / (dij * totMass * rho_j);
-          vi += rho * Ds[a] * totMass_i * sigma_i / (dij * totMass * rho_i);
-        }
-        dj_[a][k] = vj;
-        di_[a][k] = vi;
-      }
-#pragma unroll
-    for (int a = 0; a < NS; ++a)
-#pragma unroll
-      for (int b = 0; b < NS; ++b) {
-        dj_[a][a] += 0.5 * rho * m.mm[b] * Ds[b] * Gxn[b] / (totMass * rho_j);
-        di_[a][a] += 0.5 * rho * m.mm[b] * Ds[b] * Gxn[b] / (totMass * rho_i);
-      }
-#pragma unroll
-    for (int a = 0; a < NS; ++a) {
-      // column 0 of dJdr is never set in the reference (stays 0.0): -0.0 * dS etc.
-      FJ[RHOS_S + a][RHO_S] = -0.0 * dS;
-      FI[RHOS_S + a][RHO_S] = -0.0 * dS;
-      FJ[RHO_S][RHO_S] += FJ[RHOS_S + a][RHO_S];
-      FI[RHO_S][RHO_S] += FI[RHOS_S + a][RHO_S];
-      FJ[RHOE_S][RHO_S] += -0.0 * hs[a] * dS;
-      FI[RHOE_S][RHO_S] += -0.0 * hs[a] * dS;
-#pragma unroll
-      for (int b = 0; b < NS; ++b) {
-        FJ[RHOS_S + a][RHOS_S + b] = -dj_[a][b] * dS;
-        FI[RHOS_S + a][RHOS_S + b] = -di_[a][b] * dS;
-        FJ[RHO_S][RHOS_S + b] += -dj_[a][b] * dS;
-        FI[RHO_S][RHOS_S + b] += -di_[a][b] * dS;
-        FJ[RHOE_S][RHOS_S + a] += -dj_[b][a] * hs[b] * dS;
-        FI[RHOE_S][RHOS_S + a] += -di_[b][a] * hs[b] * dS;
-      }
-    }
+    for (int s = 0; s < NS; ++s) Cps[s] = spline(m, P_CP, s, dim_temp, &err) / m.mm[s] / P.R_ref;
   }
-  if (P.rans) {
-    const double sq = sqrt(dist2);
-    const double mut = Mean_mut, PrT = P.Pr_t, LeT = P.Le_t;
-    if (NDIM == 2) {
-      const double thetax = theta + UN[0] * UN[0] / 3.0, thetay = theta + UN[NDIM - 1] * UN[NDIM - 1] / 3.0;
-      const double etaz = UN[0] * UN[NDIM - 1] / 3.0;
-      const double pix = Vm[VX_P] * thetax + Vm[VX_P + 1] * etaz;
-      const double piy = Vm[VX_P] * etaz + Vm[VX_P + 1] * thetay;
-      FJ[RHOVX_S][RHOVX_S] += mut * thetax / sq * Area;
-      FJ[RHOVX_S][RHOVX_S + 1] += mut * etaz / sq * Area;
-      FI[RHOVX_S][RHOVX_S] -= mut * thetax / sq * Area;
-      FI[RHOVX_S][RHOVX_S + 1] -= mut * etaz / sq * Area;
-      FJ[RHOVX_S + 1][RHOVX_S] += mut * etaz / sq * Area;
-      FJ[RHOVX_S + 1][RHOVX_S + 1] += mut * thetay / sq * Area;
-      FI[RHOVX_S + 1][RHOVX_S] -= mut * etaz / sq * Area;
-      FI[RHOVX_S + 1][RHOVX_S + 1] -= mut * thetay / sq * Area;
-      FJ[RHOE_S][RHOVX_S] += pix * mut / sq * Area;
-      FJ[RHOE_S][RHOVX_S + 1] += piy * mut / sq * Area;
-      FI[RHOE_S][RHOVX_S] -= pix * mut / sq * Area;
-      FI[RHOE_S][RHOVX_S + 1] -= piy * mut / sq * Area;
+  double totMass = 0.0, totMass_i = 0.0, totMass_j = 0.0, sigma_i = 0.0, sigma_j = 0.0;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        FJ[RHOE_S][RHOE_S] += mut / PrT * Cps[s] * Ys[s] * theta / sq * Area;
-        FI[RHOE_S][RHOE_S] -= mut / PrT * Cps[s] * Ys[s] * theta / sq * Area;
-        FJ[RHOE_S][RHOS_S + s] += mut / (PrT * LeT) * hs[s] * Ys[s] / rho_j * theta / sq * Area;
-        FI[RHOE_S][RHOS_S + s] -= mut / (PrT * LeT) * hs[s] * Ys[s] / rho_i * theta / sq * Area;
-      }
-    }
-    // quirk :1083-1084 — row(s).data() walks the column-major storage of Mean_Mass_Grads
+  for (int s = 0; s < NS; ++s) totMass += m.mm[s] * Xs[s];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      double aux = 0.0;
+  for (int s = 0; s < NS; ++s) totMass_i += m.mm[s] * Xs_i[s];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) totMass_j += m.mm[s] * Xs_j[s];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sigma_i += Xs_i[s];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sigma_j += Xs_j[s];
+  // quirk :1083-1084 — row(s).data() walks the column-major storage of Mean_Mass_Grads
+  double qaux[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    double aux = 0.0;
+    if (P.rans) {
 #pragma unroll
       for (int d = 0; d < NDIM; ++d) {
         const int flat = s + d;
         aux += MG[flat % NS][flat / NS] * UN[d];
       }
-      FJ[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[s] * Ys[s] * aux * Area;
-      FI[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[s] * Ys[s] * aux * Area;
     }
+    qaux[s] = aux;
   }
+  double* o = summ;
+  o[VS_MU] = Mean_mu;
+  o[VS_K] = Mean_k;
+  o[VS_MUT] = Mean_mut;
+  o[VS_RHO] = rho;
+  o[VS_VM] = Vm[VX_P];
+  o[VS_VM + 1] = Vm[VX_P + 1];
+  o[VS_RHOI] = Vi[RHO_P];
+  o[VS_RHOJ] = Vj[RHO_P];
+  o[VS_VI] = Vi[VX_P];
+  o[VS_VI + 1] = Vi[VX_P + 1];
+  o[VS_VJ] = Vj[VX_P];
+  o[VS_VJ + 1] = Vj[VX_P + 1];
+  o[VS_THETA] = theta;
+  o[VS_DIJ] = sqrt(dist2);
+  o[VS_DS] = Area;
+  o[VS_UN] = UN[0];
+  o[VS_UN + 1] = UN[NDIM - 1];
+  o[VS_PF] = PF[RHOVX_S];
+  o[VS_PF + 1] = PF[RHOVX_S + 1];
+  o[VS_TM] = totMass;
+  o[VS_TMI] = totMass_i;
+  o[VS_TMJ] = totMass_j;
+  o[VS_SGI] = sigma_i;
+  o[VS_SGJ] = sigma_j;
 #pragma unroll
-  for (int d = 0; d < NDIM; ++d) {
-    FI[RHOE_S][RHOVX_S + d] += 0.5 * PF[RHOVX_S + d];
-    FJ[RHOE_S][RHOVX_S + d] += 0.5 * PF[RHOVX_S + d];
+  for (int s = 0; s < NS; ++s) {
+    o[VS_ARR + 0 * NS + s] = Xs_i[s];
+    o[VS_ARR + 1 * NS + s] = Xs_j[s];
+    o[VS_ARR + 2 * NS + s] = Ys[s];
+    o[VS_ARR + 3 * NS + s] = hs[s];
+    o[VS_ARR + 4 * NS + s] = Cps[s];
+    o[VS_ARR + 5 * NS + s] = Jd[s];
+    o[VS_ARR + 6 * NS + s] = Gxn[s];
+    o[VS_ARR + 7 * NS + s] = Ds[s];
+    o[VS_ARR + 8 * NS + s] = qaux[s];
   }
-  // J = dF/dV * dV/dU; dV/dU rows: rho e0; momentum (-u/rho) e0 + (1/rho) e_d; energy S; species e_s.
-  // Summation over k in index order with only the non-zero dV/dU terms (x + 0*y == x).
-#pragma unroll
-  for (int a = 0; a < nVar; ++a)
-#pragma unroll
-    for (int b = 0; b < nVar; ++b) {
-      double si = 0.0, sj = 0.0;
-      // k = 0 (rho row of dV/dU = e0)
-      if (b == 0) { si += FI[a][0] * 1.0; sj += FJ[a][0] * 1.0; }
-      else { si += FI[a][0] * 0.0; sj += FJ[a][0] * 0.0; }
-#pragma unroll
-      for (int d = 0; d < NDIM; ++d) {
-        const double ci = (b == 0) ? -Vi[VX_P + d] / Vi[RHO_P] : ((b == 1 + d) ? 1.0 / Vi[RHO_P] : 0.0);
-        const double cj = (b == 0) ? -Vj[VX_P + d] / Vj[RHO_P] : ((b == 1 + d) ? 1.0 / Vj[RHO_P] : 0.0);
-        si += FI[a][1 + d] * ci;
-        sj += FJ[a][1 + d] * cj;
-      }
-      si += FI[a][RHOE_S] * ni.S[b];
-      sj += FJ[a][RHOE_S] * nj.S[b];
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const double c = (b == RHOS_S + s) ? 1.0 : 0.0;
-        si += FI[a][RHOS_S + s] * c;
-        sj += FJ[a][RHOS_S + s] * c;
-      }
-      Ji[a * nVar + b] = si;
-      Jj[a * nVar + b] = sj;
-    }
   return err;
+}
+
+// Jacobian column b (0 <= b < nVar) of Jac_i and Jac_j for one edge, from the visc_edge summary:
+// SetLaminarViscousProjJacs (:1200-1401) + SST_Reactive_JacobianClosure (:891-1090, 2-D branch)
+// build dF/dV (FI for node i, FJ for node j); J = dF/dV * dV/dU (:1637-1653). A team of lanes owns
+// the columns of one edge; every dF/dV entry is accumulated in the reference's order, and J's sum over
+// k keeps the reference's order (the F*0 terms of dV/dU's zero entries are dropped: they can only
+// change the sign of an exact zero). base_i/base_j: the column-independent part of row a of dJ/drho
+// (this lane's a = lane index in the team), shared through shuffles. Only 2-D.
+template <int NS, int NDIM>
+__device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, const double* __restrict__ sm,
+                                       double Sib, double Sjb, int b, int tl, double* __restrict__ Ji,
+                                       double* __restrict__ Jj) {
+  constexpr int nVar = NS + NDIM + 2;
+  constexpr int RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
+  const double mu = sm[VS_MU], ktr = sm[VS_K], mut = sm[VS_MUT], rho = sm[VS_RHO];
+  const double rho_i = sm[VS_RHOI], rho_j = sm[VS_RHOJ];
+  const double theta = sm[VS_THETA], dij = sm[VS_DIJ], dS = sm[VS_DS], sq = sm[VS_DIJ], Area = sm[VS_DS];
+  const double totMass = sm[VS_TM], totMass_i = sm[VS_TMI], totMass_j = sm[VS_TMJ];
+  const double sigma_i = sm[VS_SGI], sigma_j = sm[VS_SGJ];
+  const double* Xs_i = sm + VS_ARR;
+  const double* Xs_j = Xs_i + NS;
+  const double* Ys = Xs_j + NS;
+  const double* hs = Ys + NS;
+  const double* Cps = hs + NS;
+  const double* Jd = Cps + NS;
+  const double* Gxn = Jd + NS;
+  const double* Ds = Gxn + NS;
+  const double* qaux = Ds + NS;
+  const double PrT = P.Pr_t, LeT = P.Le_t;
+  // ---- column-independent part of dJ/drho rows (lane tl < NS owns row a = tl)
+  double bj = 0.0, bi = 0.0;
+  if (tl < NS) {
+    const int a = tl;
+    double vj = -rho * m.mm[a] * Ds[a] * Xs_j[a] / (totMass * dij * sigma_j * rho_j);
+    double vi = rho * m.mm[a] * Ds[a] * Xs_i[a] / (totMass * dij * sigma_i * rho_i);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      vj += rho * Ys[a] * m.mm[q] * Ds[q] * Xs_j[q] / (totMass * dij * sigma_j * rho_j);
+      vi -= rho * Ys[a] * m.mm[q] * Ds[q] * Xs_i[q] / (totMass * dij * sigma_i * rho_i);
+    }
+    bj = vj;
+    bi = vi;
+  }
+  double colj[NS], coli[NS];  // dJ/drho column k = b - RHOS_S (species columns only)
+  const int k = b - RHOS_S;
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    const double baj = __shfl(bj, a, 16), bai = __shfl(bi, a, 16);
+    double vj = baj, vi = bai;
+    if (k >= 0) {
+      vj += rho * Ys[a] * Ds[k] * totMass_j * sigma_j / (dij * totMass * rho_j);
+      vi -= rho * Ys[a] * Ds[k] * totMass_i * sigma_i / (dij * totMass * rho_i);
+      if (a == k) {
+        vj -= rho * Ds[a] * totMass_j * sigma_j / (dij * totMass * rho_j);
+        vi += rho * Ds[a] * totMass_i * sigma_i / (dij * totMass * rho_i);
+      }
+    }
+    colj[a] = vj;
+    coli[a] = vi;
+  }
+  if (b >= nVar) return;
+  if (k >= 0) {  // diagonal increments of dJ/drho (:1369-1374)
+#pragma unroll
+    for (int a = 0; a < NS; ++a)
+      if (a == k) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+          colj[a] += 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_j);
+          coli[a] += 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_i);
+        }
+      }
+  }
+  // ---- dF/dV flow block rows 0..3, columns 0..3 (index [row][col]); zero-initialised
+  double FJ[4][4], FI[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) FJ[r][c] = FI[r][c] = 0.0;
+  const double UN0 = sm[VS_UN], UN1 = sm[VS_UN + 1];
+  const double thetax = theta + UN0 * UN0 / 3.0, thetay = theta + UN1 * UN1 / 3.0;
+  const double etaz = UN0 * UN1 / 3.0;
+  const double pix = sm[VS_VM] * thetax + sm[VS_VM + 1] * etaz;
+  const double piy = sm[VS_VM] * etaz + sm[VS_VM + 1] * thetay;
+  FJ[1][1] = mu * thetax / dij * dS;
+  FJ[1][2] = mu * etaz / dij * dS;
+  FJ[2][1] = mu * etaz / dij * dS;
+  FJ[2][2] = mu * thetay / dij * dS;
+  FJ[3][1] = pix * mu / dij * dS;
+  FJ[3][2] = piy * mu / dij * dS;
+  FJ[3][3] = ktr * theta / dij * dS;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) FI[r][c] = -FJ[r][c];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    FI[3][3] += -0.5 * Jd[q] * Cps[q];
+    FJ[3][3] += -0.5 * Jd[q] * Cps[q];
+  }
+  // species column of rows 0 (rho) and 3 (rho E), accumulated over the species rows in order
+  double FJ0k = 0.0, FI0k = 0.0, FJ3k = 0.0, FI3k = 0.0;
+  if (k >= 0) {
+#pragma unroll
+    for (int a = 0; a < NS; ++a) {
+      FJ0k += -colj[a] * dS;
+      FI0k += -coli[a] * dS;
+      FJ3k += -colj[a] * hs[a] * dS;
+      FI3k += -coli[a] * hs[a] * dS;
+    }
+  }
+  if (P.rans) {
+    FJ[1][1] += mut * thetax / sq * Area;
+    FJ[1][2] += mut * etaz / sq * Area;
+    FI[1][1] -= mut * thetax / sq * Area;
+    FI[1][2] -= mut * etaz / sq * Area;
+    FJ[2][1] += mut * etaz / sq * Area;
+    FJ[2][2] += mut * thetay / sq * Area;
+    FI[2][1] -= mut * etaz / sq * Area;
+    FI[2][2] -= mut * thetay / sq * Area;
+    FJ[3][1] += pix * mut / sq * Area;
+    FJ[3][2] += piy * mut / sq * Area;
+    FI[3][1] -= pix * mut / sq * Area;
+    FI[3][2] -= piy * mut / sq * Area;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      FJ[3][3] += mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
+      FI[3][3] -= mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
+      if (q == k) {
+        FJ3k += mut / (PrT * LeT) * hs[q] * Ys[q] / rho_j * theta / sq * Area;
+        FI3k -= mut / (PrT * LeT) * hs[q] * Ys[q] / rho_i * theta / sq * Area;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      FJ[3][3] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
+      FI[3][3] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
+    }
+  }
+  FI[3][1] += 0.5 * sm[VS_PF];
+  FJ[3][1] += 0.5 * sm[VS_PF];
+  FI[3][2] += 0.5 * sm[VS_PF + 1];
+  FJ[3][2] += 0.5 * sm[VS_PF + 1];
+  // ---- J[a][b] = sum_k F[a][k] dV/dU[k][b]
+  const double ui = sm[VS_VI], vvi = sm[VS_VI + 1], uj = sm[VS_VJ], vvj = sm[VS_VJ + 1];
+  double ci1, ci2, cj1, cj2;  // dV/dU velocity rows, column b
+  if (b == 0) {
+    ci1 = -ui / rho_i;
+    ci2 = -vvi / rho_i;
+    cj1 = -uj / rho_j;
+    cj2 = -vvj / rho_j;
+  } else {
+    ci1 = (b == 1) ? 1.0 / rho_i : 0.0;
+    ci2 = (b == 2) ? 1.0 / rho_i : 0.0;
+    cj1 = (b == 1) ? 1.0 / rho_j : 0.0;
+    cj2 = (b == 2) ? 1.0 / rho_j : 0.0;
+  }
+  const double d0 = (b == 0) ? 1.0 : 0.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double si = 0.0, sj = 0.0;
+    si += FI[r][0] * d0;
+    sj += FJ[r][0] * d0;
+    si += FI[r][1] * ci1;
+    sj += FJ[r][1] * cj1;
+    si += FI[r][2] * ci2;
+    sj += FJ[r][2] * cj2;
+    si += FI[r][RHOE_S] * Sib;
+    sj += FJ[r][RHOE_S] * Sjb;
+    if (k >= 0) {
+      if (r == 0) {
+        si += FI0k;
+        sj += FJ0k;
+      } else if (r == RHOE_S) {
+        si += FI3k;
+        sj += FJ3k;
+      }
+    }
+    Ji[r * nVar + b] = si;
+    Jj[r * nVar + b] = sj;
+  }
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    double si = 0.0, sj = 0.0;
+    if (k >= 0) {
+      si = -coli[a] * dS;
+      sj = -colj[a] * dS;
+    }
+    Ji[(RHOS_S + a) * nVar + b] = si;
+    Jj[(RHOS_S + a) * nVar + b] = sj;
+  }
 }
 
 }  // namespace rx
