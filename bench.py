@@ -45,22 +45,44 @@ FP64_PEAK_TFS = 78.6       # MI355X FP64 vector spec
 
 
 def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
-    """Algorithmic bytes per launch (each unique datum once per sweep)."""
+    """Algorithmic bytes (or flops) per launch of the single-launch kernels timed per phase
+    (each unique datum once per sweep)."""
     nVar, nPV, nG = ns + nDim + 2, ns + nDim + 5, ns + nDim + 2
     d = 8
     blk = nVar * nVar * d
+    summ = (24 + 9 * ns) * d
+    hbm = lambda b, name: dict(bound="hbm", work=float(b), unit="GB/s", peak=HBM_PEAK_GBS, kernel=name)
     return {
-        # k_ausm_edge: V_i,V_j (nPV), dPdU (nVar) per node once; edge (2 int32 + normal); out flux + 2 Jacobians
-        "CONV": dict(bound="hbm", bytes=N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk)),
-        # k_visc_edge: node record V, grad, mu, kappa, Dij, dTdU, k, mu_t, sigma_k, grad_k, coord
-        "VISC": dict(bound="hbm", bytes=N * (nPV + nG * nDim + 2 + ns * ns + nVar + 3 + nDim + nDim) * d
-                     + E * (8 + nDim * d) + E * (nVar * d + 2 * blk)),
-        "GRAD": dict(bound="hbm", bytes=N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4),
-        "SOURCE": dict(bound="hbm", bytes=N * (nPV + nVar + 2) * d + N * (nVar * d + blk)),
-        "SPMV": dict(bound="hbm", bytes=nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d),
-        "ILU_BUILD": dict(bound="hbm", bytes=2 * nnzb * blk + N * blk),
-        "ILU_APPLY": dict(bound="hbm", bytes=nnzb * blk + N * blk + 3 * N * nVar * d),
+        # k_ausm_edge: V (nPV) and dPdU (nVar) per node once; edge (2 int32 + normal); flux + 2 Jacobians
+        "CONV": hbm(N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk), "k_ausm_edge"),
+        # k_visc_edge: FP64-compute bound, SURVEY §8(d): ~8-10 kflop per edge for flux + closures
+        "VISC": dict(bound="fp64", work=9000.0 * E, unit="TFLOP/s", peak=FP64_PEAK_TFS, kernel="k_visc_edge"),
+        # k_visc_jac: per-edge summary + dT/dU in, two Jacobian blocks out
+        "VISC_JAC": hbm(E * summ + N * nVar * d + E * 2 * blk, "k_visc_jac"),
+        # k_assemble: 4 scratch blocks per edge + source block per node in; BSR + residual out
+        "ASSEMBLE": hbm((4 * E + N + nnzb) * blk + (2 * E + 2 * N) * nVar * d, "k_assemble"),
+        "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq"),
+        "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar * d + blk), "k_source"),
+        # k_ilu_build_part: A in, factor + inv(D) out
+        "ILU_BUILD": hbm((2 * nnzb + N) * blk, "k_ilu_build_part"),
     }
+
+
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc.json")
+
+
+def pmc_traffic(kernel, workload_key):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (tools/pmc_summary.py),
+    when they were taken on this workload; else None."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload_key:
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes")
 
 
 def build_workload(nx, ny, ns, n_part=1):
@@ -157,18 +179,30 @@ def main():
 
     models = kernel_models(N, E, nnzb, ns, 2, 5)
     phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0}
-    # dominant single-launch kernel among the modelled ones (phase == one kernel launch for these)
-    single = [k for k in ("CONV", "VISC", "GRAD", "SOURCE") if prof[k][1] > 0]
-    dom = max(single, key=lambda k: prof[k][0])
+    wkey = f"{args.workload} {nx}x{ny} ns{ns} parts{args.parts}"
 
     def roof(k):
         ms, n = prof[k]
         avg_s = ms / n / 1e3
         m = models[k]
-        ach = m["bytes"] / avg_s / 1e9
-        return dict(kernel=k, bound=m["bound"], achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=None, avg_launch_us=round(avg_s * 1e6, 2),
-                    algorithmic_bytes=int(m["bytes"]))
+        scale = 1e9 if m["unit"] == "GB/s" else 1e12
+        ach = m["work"] / avg_s / scale
+        out = dict(kernel=m["kernel"], phase=k, bound=m["bound"], achieved=round(ach, 2), peak=m["peak"],
+                   unit=m["unit"], frac=round(ach / m["peak"], 4), avg_launch_us=round(avg_s * 1e6, 2),
+                   launches=int(n))
+        if m["unit"] == "GB/s":
+            t = pmc_traffic(m["kernel"], wkey)
+            out["algorithmic_bytes"] = int(m["work"])
+            out["traffic"] = None if t is None else int(t)
+        else:
+            out["algorithmic_flops"] = int(m["work"])
+            out["traffic"] = None
+        return out
+
+    timed = [k for k in models if prof[k][1] > 0]
+    kernels = {k: roof(k) for k in timed}
+    # dominant kernel: the longest average launch among the single-launch phases
+    dom = max(timed, key=lambda k: prof[k][0] / prof[k][1])
 
     cells = N * world
     out = {
@@ -190,8 +224,9 @@ def main():
                    "partitions": args.parts,
                    "parallelism": f"replicas x{world}" if world > 1 else "1 GPU",
                    "lin_iters_mean": float(np.mean(lin_its[-args.steps:]))},
-        "roofline": roof(dom),
-        "roofline_edge_flux": roof("CONV"),
+        "roofline": kernels[dom],
+        "roofline_edge_flux": kernels.get("CONV"),
+        "roofline_kernels": kernels,
         "phase_ms_per_step": {k: round(v, 4) for k, v in phase_ms.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

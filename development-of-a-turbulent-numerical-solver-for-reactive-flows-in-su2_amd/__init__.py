@@ -29,7 +29,7 @@ FIELDS = ["U", "V", "DPDU", "DTDU", "MU", "KAPPA", "DIJ", "GRAD", "LIMITER", "TK
 F = {name: k for k, name in enumerate(FIELDS)}
 # rx_kernel
 KERNELS = ["CONV", "VISC", "SOURCE", "GRAD", "LIMITER", "DT", "SPMV", "ILU_BUILD", "ILU_APPLY", "LUSGS", "KRYLOV",
-           "UPDATE", "SOLVE"]
+           "UPDATE", "SOLVE", "VISC_JAC", "ASSEMBLE"]
 K = {name: k for k, name in enumerate(KERNELS)}
 
 

@@ -42,6 +42,7 @@ void dfree(void* p) {
 int ensure_assembled(rx_ctx* ctx) {
   if (!ctx->cfg.implicit || ctx->assembled) return RX_OK;
   if (!ctx->phase_conv) return RX_ERR_STATE;
+  RxPhase ph(ctx, RX_K_ASSEMBLE);
   int rc = rx_launch_assemble(ctx, ctx->phase_visc, ctx->phase_src);
   if (rc) return rc;
   ctx->assembled = 1;
@@ -547,7 +548,6 @@ int rx_edge_flux_conv(rx_ctx* ctx) {
 
 int rx_edge_flux_visc(rx_ctx* ctx) {
   if (!ctx) return RX_ERR_ARG;
-  RxPhase ph(ctx, RX_K_VISC);
   int rc = rx_launch_visc_edge(ctx);
   if (rc) return rc;
   if (!ctx->cfg.implicit) {
@@ -639,16 +639,11 @@ int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
 }
 
 namespace {
-// System build (Vol/dt, rhs), preconditioner build, FGMRES, RMS partials and the clipped update:
-// a fixed kernel sequence with no host decision (rx_krylov.hip), recorded once as a hipGraph.
+// FGMRES, RMS partials and the clipped update: a fixed kernel sequence with no host decision
+// (rx_krylov.hip), recorded once as a hipGraph. System and preconditioner builds are launched
+// before it as single kernels (timed per phase).
 int enqueue_solve(rx_ctx* ctx) {
   int rc;
-  if ((rc = rx_la_build_system(ctx))) return rc;
-  if (ctx->cfg.lin_prec == 1) {
-    if ((rc = rx_la_ilu_build(ctx))) return rc;
-  } else {
-    if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
-  }
   if ((rc = rx_la_fgmres_enqueue(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter))) return rc;
   if ((rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RHS]))) return rc;
   return rx_la_implicit_update(ctx);
@@ -667,6 +662,17 @@ int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
   if ((rc = rx_la_krylov_alloc(ctx, ctx->cfg.lin_iter))) return rc;
+  {
+    RxPhase ph(ctx, RX_K_UPDATE);
+    if ((rc = rx_la_build_system(ctx))) return rc;
+  }
+  if (ctx->cfg.lin_prec == 1) {
+    RxPhase ph(ctx, RX_K_ILU_BUILD);
+    if ((rc = rx_la_ilu_build(ctx))) return rc;
+  } else {
+    RxPhase ph(ctx, RX_K_LUSGS);
+    if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
+  }
   {
     RxPhase ph(ctx, RX_K_SOLVE);
     if (graphs_enabled()) {

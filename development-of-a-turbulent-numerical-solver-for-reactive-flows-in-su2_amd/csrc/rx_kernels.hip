@@ -620,13 +620,17 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
   if (ctx->nDim != 2) return RX_ERR_ARG;
   ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
                ctx->cfg.rans, ctx->cfg.implicit};
-  RX_NS_SWITCH(ctx->ns, (k_visc_edge<NS_, 2><<<blocks(ctx->E, 64), 64, 0, ctx->stream>>>(
-                            (int)ctx->E, ctx->edges, ctx->normal, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_GRAD],
-                            ctx->f[RX_F_MU], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_DTDU],
-                            ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_SIGMAK], ctx->f[RX_F_GRADK], ctx->mech,
-                            P, ctx->fvisc, ctx->vsumm, ctx->err)));
-  RX_HIP(hipGetLastError());
+  {
+    RxPhase ph(ctx, RX_K_VISC);
+    RX_NS_SWITCH(ctx->ns, (k_visc_edge<NS_, 2><<<blocks(ctx->E, 64), 64, 0, ctx->stream>>>(
+                              (int)ctx->E, ctx->edges, ctx->normal, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_GRAD],
+                              ctx->f[RX_F_MU], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_DTDU],
+                              ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_SIGMAK], ctx->f[RX_F_GRADK],
+                              ctx->mech, P, ctx->fvisc, ctx->vsumm, ctx->err)));
+    RX_HIP(hipGetLastError());
+  }
   if (ctx->cfg.implicit) {
+    RxPhase ph(ctx, RX_K_VISC_JAC);
     RX_NS_SWITCH(ctx->ns, (k_visc_jac<NS_, 2><<<blocks(ctx->E * 16), kBlock, 0, ctx->stream>>>(
                               (int)ctx->E, ctx->edges, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->mech, P, ctx->jvisc)));
     RX_HIP(hipGetLastError());

@@ -145,7 +145,9 @@ int rx_implicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */, int *li
 typedef enum {
   RX_K_CONV = 0, RX_K_VISC, RX_K_SOURCE, RX_K_GRAD, RX_K_LIMITER, RX_K_DT, RX_K_SPMV, RX_K_ILU_BUILD,
   RX_K_ILU_APPLY, RX_K_LUSGS, RX_K_KRYLOV, RX_K_UPDATE,
-  RX_K_SOLVE, /* rx_implicit_euler's captured solve: system build + preconditioner build + FGMRES + update */
+  RX_K_SOLVE,    /* rx_implicit_euler's captured solve: FGMRES + RMS + clipped update (one hipGraph) */
+  RX_K_VISC_JAC, /* viscous Jacobian kernel (implicit) */
+  RX_K_ASSEMBLE, /* residual + BSR Jacobian assembly */
   RX_K_COUNT
 } rx_kernel;
 int rx_profile_enable(rx_ctx *ctx, int on);

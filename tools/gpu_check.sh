@@ -9,3 +9,9 @@ timeout -k 10 300 python tools/ilu_trace.py > gpurun_out/trace.log 2>&1 && echo 
 timeout -k 10 400 python bench.py --steps 20 --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} > gpurun_out/bench.log 2>&1 && echo "bench ok" &&
 R=$PWD && cd /tmp && export TMPDIR=/tmp &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof.log 2>&1 && echo "prof ok"
+if [ "${PMC:-0}" = "1" ]; then
+  R=$GRAFT_REPO_ROOT; [ -z "$R" ] && R=/root/repo
+  cd /tmp && export TMPDIR=/tmp &&
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/pmc_fetch.log 2>&1 && echo "pmc fetch ok" &&
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/pmc_write.log 2>&1 && echo "pmc write ok"
+fi
