@@ -16,8 +16,15 @@ The preconditioner is partitioned like the reference run on `--parts` MPI ranks 
 local RCM per part, ILU(0) per rank; default 256 = one rank per CU); `--parts 1` is the serial
 reference.
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`): every rank runs its own copy of the workload
-(weak scaling, no data-path collective yet); timing = max over ranks; value = all ranks' cells.
+Multi-GPU (`torch.distributed.run --nproc-per-node N`, one rank per GPU): weak scaling by domain
+decomposition like the reference's MPI run. The global jet is N times taller (nx x ny*N points,
+parts*N partitions); every rank owns a contiguous block of `parts` partitions plus one halo layer
+(meshgen.shard) and exchanges halos over RCCL where the reference calls SendReceive / Set_MPI_*,
+with every FGMRES inner product and the RMS all-reduced (rx_comm_init). The first warm-up step runs
+eagerly and must give bitwise the RMS of the next (graph-replayed) one, else the graph is disabled.
+If the communicator cannot be set up, every rank falls back to an independent replica of the
+single-GPU workload and `config.parallelism` says so. Timing = max over ranks; value = all ranks'
+owned cells.
 
 Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel and `cpu_baseline` from the
 CPU restatement (oracle/) timed on one host core over one step of the same mesh.
@@ -107,6 +114,21 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg):
                 sample=f"1 implicit step of the same {N}-cell mesh on 1 host core ({dt:.2f} s)")
 
 
+def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist):
+    """Build the rank's shard of the N-times-taller jet and attach the RCCL communicator."""
+    from tests.rxpkg import meshgen
+    mesh, st, mech_arrays, kw = build_workload(nx, ny * world, ns, args.parts * world)
+    sh = meshgen.shard(mesh, world, rank)
+    st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
+    cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
+    s = rx.ReactiveNSSolver(sh, rx.Mechanism(mech_arrays), cfg, device=local)
+    uid = [rx.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    s.comm_init(world, rank, uid[0])
+    s.set_state(st_l)
+    return s, mesh, st_l, mech_arrays, kw, cfg, int(sh["n_domain"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,22 +151,46 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())  # rehearsal with more ranks than GPUs
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # host-side control only (uid broadcast, barrier, max of the timings): gloo; the data path
+        # is the context's own RCCL communicator
+        dist.init_process_group("gloo")
     from tests.rxpkg import rx
 
     wl = dict(WORKLOADS[args.workload])
     nx, ny, ns = args.nx or wl["nx"], args.ny or wl["ny"], args.species or wl["ns"]
-    mesh, st, mech_arrays, kw = build_workload(nx, ny, ns, args.parts)
-    mech = rx.Mechanism(mech_arrays)
-    cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
-    s = rx.ReactiveNSSolver(mesh, mech, cfg, device=local)
-    s.set_state(st)
+    s = None
+    parallelism = "1 GPU"
+    n_owned = 0
+    if world > 1:
+        err = ""
+        try:
+            s, mesh, st, mech_arrays, kw, cfg, n_owned = setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            err = repr(e)[:200]
+        flags = [None] * world
+        dist.all_gather_object(flags, err)
+        bad = [f for f in flags if f]
+        if bad:
+            if s is not None:
+                s.close()
+            s = None
+            parallelism = f"replicas x{world} (sharded setup failed: {bad[0]})"
+        else:
+            parallelism = f"sharded x{world} (RCCL halo exchange + all-reduce)"
+    if s is None:
+        mesh, st, mech_arrays, kw = build_workload(nx, ny, ns, args.parts)
+        cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
+        s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg, device=local)
+        s.set_state(st)
+        n_owned = s.N
     N, E = s.N, s.E
     rp, col = s.bsr_pattern()
     nnzb = int(rp[-1])
 
     lin_its = []
+    rms_log = []
 
     def step():
         s.SetPrimitive_Gradient_LS()
@@ -153,9 +199,23 @@ def main():
         s.Upwind_Residual()
         s.Viscous_Residual()
         s.Source_Residual()
-        _, it = s.ImplicitEuler_Iteration()
+        rms, it = s.ImplicitEuler_Iteration()
         lin_its.append(it)
+        rms_log.append(rms)
 
+    graph = True
+    if parallelism.startswith("sharded"):
+        # eager step, then a graph-replayed step: same system (node records fixed), same RMS bitwise
+        os.environ["RX_NO_GRAPH"] = "1"
+        step()
+        os.environ.pop("RX_NO_GRAPH")
+        step()
+        ok = bool(np.array_equal(rms_log[0], rms_log[1]) and lin_its[0] == lin_its[1])
+        oks = [None] * world
+        dist.all_gather_object(oks, ok)
+        if not all(oks):
+            os.environ["RX_NO_GRAPH"] = "1"
+            graph = False
     for _ in range(args.warmup):
         step()
     s.sync()
@@ -171,7 +231,7 @@ def main():
     el = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     prof = {k: s.profile_read(k) for k in rx.K}
@@ -204,7 +264,12 @@ def main():
     # dominant kernel: the longest average launch among the single-launch phases
     dom = max(timed, key=lambda k: prof[k][0] / prof[k][1])
 
-    cells = N * world
+    if world > 1:
+        tot = [None] * world
+        dist.all_gather_object(tot, n_owned)
+        cells = int(sum(tot)) if parallelism.startswith("sharded") else N * world
+    else:
+        cells = N
     out = {
         "metric": "Mcells*iters/s (reactive RANS)",
         "value": round(cells * args.steps / el / 1e6, 4),
@@ -218,11 +283,13 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference jet geometry; node records resampled from the reference PaSR jet state)",
-        "config": {"workload": f"{args.workload}: 2-D reactive jet {nx}x{ny}", "cells_per_gpu": N, "edges": E,
+        "config": {"workload": f"{args.workload}: 2-D reactive jet {nx}x{ny}" + (
+                       f" per GPU (global {nx}x{ny * world})" if parallelism.startswith("sharded") else ""),
+                   "cells_per_gpu": n_owned, "halo_points": N - n_owned, "edges": E,
                    "species": ns, "nVar": ns + 4, "nnz_blocks": nnzb, "time": "EULER_IMPLICIT",
                    "linear_solver": "FGMRES(5)+ILU0",
                    "partitions": args.parts,
-                   "parallelism": f"replicas x{world}" if world > 1 else "1 GPU",
+                   "parallelism": parallelism, "solve_graph": graph, "cells_total": cells,
                    "lin_iters_mean": float(np.mean(lin_its[-args.steps:]))},
         "roofline": kernels[dom],
         "roofline_edge_flux": kernels.get("CONV"),

@@ -52,7 +52,19 @@ class MeshDesc(C.Structure):
     _fields_ = [("n_dim", C.c_int32), ("n_point", C.c_int64), ("n_edge", C.c_int64), ("n_bvert", C.c_int64),
                 ("edges", C.c_void_p), ("edge_normal", C.c_void_p), ("coord", C.c_void_p), ("volume", C.c_void_p),
                 ("nbr_ptr", C.c_void_p), ("nbr", C.c_void_p), ("bvert", C.c_void_p), ("bvert_normal", C.c_void_p),
-                ("n_part", C.c_int64), ("part_ptr", C.c_void_p)]
+                ("n_part", C.c_int64), ("part_ptr", C.c_void_p),
+                ("n_domain", C.c_int64), ("n_neigh", C.c_int32), ("neigh", C.c_void_p), ("send_ptr", C.c_void_p),
+                ("send_idx", C.c_void_p), ("recv_ptr", C.c_void_p)]
+
+
+SENDRECV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                          C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_double), C.c_int32)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32)
+
+
+class HostComm(C.Structure):
+    """rx_host_comm: the host-staged transport (the reference's MPI SendReceive / Allreduce pattern)."""
+    _fields_ = [("user", C.c_void_p), ("sendrecv", SENDRECV_FN), ("allreduce", ALLREDUCE_FN)]
 
 
 class Cfg(C.Structure):
@@ -99,7 +111,62 @@ def lib():
         _lib.rx_profile_enable.argtypes = [C.c_void_p, C.c_int]
         _lib.rx_profile_read.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         _lib.rx_last_error_index.argtypes = [C.c_void_p]
+        _lib.rx_comm_unique_id.argtypes = [C.c_void_p]
+        _lib.rx_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        _lib.rx_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(HostComm)]
+        _lib.rx_halo_exchange.argtypes = [C.c_void_p, C.c_int]
     return _lib
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (128 bytes) for rx_comm_init; create on one rank and broadcast."""
+    buf = C.create_string_buffer(128)
+    _chk(lib().rx_comm_unique_id(buf), "rx_comm_unique_id")
+    return buf.raw
+
+
+class TorchHostTransport:
+    """rx_host_comm over torch.distributed point-to-point and all_reduce (gloo on CPU tensors): the
+    reference's MPI_Isend/Irecv halo exchange and MPI_Allreduce, for ranks that cannot share RCCL
+    (several ranks on one GPU, CPU-side validation)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.error = None
+
+        def sendrecv(user, n_neigh, neigh, send_ptr, send, recv_ptr, recv, stride):
+            try:
+                reqs = []
+                for k in range(n_neigh):
+                    s0, s1 = send_ptr[k] * stride, send_ptr[k + 1] * stride
+                    r0, r1 = recv_ptr[k] * stride, recv_ptr[k + 1] * stride
+                    if s1 > s0:
+                        sb = torch.from_numpy(np.ctypeslib.as_array(send, shape=(s1,))[s0:s1])
+                        reqs.append(dist.isend(sb, int(neigh[k]), group=self.group))
+                    if r1 > r0:
+                        rb = torch.from_numpy(np.ctypeslib.as_array(recv, shape=(r1,))[r0:r1])
+                        reqs.append(dist.irecv(rb, int(neigh[k]), group=self.group))
+                for r in reqs:
+                    r.wait()
+                return 0
+            except Exception as e:  # surfaced as RX_ERR_COMM
+                self.error = e
+                return 1
+
+        def allreduce(user, inp, out, count):
+            try:
+                t = torch.from_numpy(np.ctypeslib.as_array(inp, shape=(count,)).copy())
+                dist.all_reduce(t, group=self.group)
+                np.ctypeslib.as_array(out, shape=(count,))[:] = t.numpy()
+                return 0
+            except Exception as e:
+                self.error = e
+                return 1
+
+        self._cb = (SENDRECV_FN(sendrecv), ALLREDUCE_FN(allreduce))  # keep alive
+        self.desc = HostComm(None, self._cb[0], self._cb[1])
 
 
 def header_symbols():
@@ -174,16 +241,38 @@ class ReactiveNSSolver:
         if pp is not None and len(pp) > 2:
             self._mesh_keep["part_ptr"] = np.ascontiguousarray(pp, dtype=np.int64)
         self.n_part = len(pp) - 1 if pp is not None else 1
+        self.Nd = int(mesh.get("n_domain", self.N))
+        if "n_domain" in mesh:
+            self._mesh_keep["neigh"] = np.ascontiguousarray(mesh["neigh"], dtype=np.int32)
+            for k in ("send_ptr", "send_idx", "recv_ptr"):
+                self._mesh_keep[k] = np.ascontiguousarray(mesh[k], dtype=np.int64)
         md = MeshDesc()
         md.n_dim, md.n_point, md.n_edge = self.nDim, self.N, self.E
         md.n_bvert = len(self._mesh_keep["bvert"])
         md.n_part = len(self._mesh_keep["part_ptr"]) - 1 if "part_ptr" in self._mesh_keep else 0
+        if "n_domain" in mesh:
+            md.n_domain = self.Nd
+            md.n_neigh = len(self._mesh_keep["neigh"])
         for k, v in self._mesh_keep.items():
             setattr(md, k, v.ctypes.data)
         h = C.c_void_p()
         _chk(lib().rx_ctx_create(C.byref(md), C.byref(mech.desc), C.byref(cfg), device, C.byref(h)), "rx_ctx_create")
         self.h = h
         self._mesh_keep = None
+
+    # ---- distributed (one rank per GPU)
+    def comm_init(self, nranks, rank, uid: bytes):
+        """Attach an RCCL communicator (uid from comm_unique_id() on one rank)."""
+        buf = C.create_string_buffer(uid, 128)
+        _chk(lib().rx_comm_init(self.h, nranks, rank, buf), "rx_comm_init", self.h)
+
+    def comm_init_host(self, nranks, rank, transport):
+        """Attach a host-staged transport (e.g. TorchHostTransport over gloo)."""
+        self._transport = transport
+        _chk(lib().rx_comm_init_host(self.h, nranks, rank, C.byref(transport.desc)), "rx_comm_init_host", self.h)
+
+    def halo_exchange(self, field):
+        _chk(lib().rx_halo_exchange(self.h, F[field]), f"rx_halo_exchange({field})", self.h)
 
     def close(self):
         if getattr(self, "h", None):

@@ -63,6 +63,7 @@ const char* rx_status_string(int s) {
     case RX_ERR_NONPHYS: return "non-physical state";
     case RX_ERR_DIVERGED: return "linear solver diverged";
     case RX_ERR_STATE: return "call sequence error";
+    case RX_ERR_COMM: return "RCCL communication error";
     default: return "unknown";
   }
 }
@@ -97,6 +98,12 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
   ctx->N = N;
   ctx->E = E;
   ctx->NB = NB;
+  ctx->Nd = (mesh->n_domain > 0) ? mesh->n_domain : N;
+  if (ctx->Nd > N) {
+    rx_ctx_destroy(ctx);
+    return RX_ERR_ARG;
+  }
+  ctx->n_global = ctx->Nd;
   const int nd = ctx->nDim, nv = ctx->nVar;
   int rc = RX_OK;
 #define CK(x)        \
@@ -168,14 +175,15 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
     ctx->h_part_ptr.assign(np + 1, 0);
     if (mesh->part_ptr && mesh->n_part > 0) {
       for (int64_t p = 0; p <= np; ++p) ctx->h_part_ptr[p] = mesh->part_ptr[p];
-      bool ok = ctx->h_part_ptr[0] == 0 && ctx->h_part_ptr[np] == N;
+      bool ok = ctx->h_part_ptr[0] == 0 && ctx->h_part_ptr[np] == ctx->Nd;
       for (int64_t p = 0; p < np && ok; ++p) ok = ctx->h_part_ptr[p + 1] > ctx->h_part_ptr[p];
       if (!ok) CK(RX_ERR_ARG);
     } else {
-      ctx->h_part_ptr[1] = N;
+      ctx->h_part_ptr[1] = ctx->Nd;
     }
     ctx->npart = (int)np;
     std::vector<int32_t> klo(N), khi(N);
+    for (int64_t i = ctx->Nd; i < N; ++i) klo[i] = khi[i] = (int32_t)diag[i];  // halo rows: no solve
     int rowmax = 1;
     for (int64_t p = 0; p < np; ++p) {
       const int64_t lo = ctx->h_part_ptr[p], hi = ctx->h_part_ptr[p + 1];
@@ -285,7 +293,8 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
       CK(dupload(ctx, &ctx->upd, upd.data(), upd.size()));
       // compact row plans in forward-schedule order (layout: rx_sweeps.hip, k_ilu_build_part); the
       // order is recomputed exactly as schedule() builds it
-      std::vector<int32_t> fo(N);
+      const int64_t Nd = ctx->Nd;
+      std::vector<int32_t> fo(Nd);
       {
         std::vector<int32_t> lv(N, 0);
         for (int64_t p = 0; p < np; ++p) {
@@ -303,8 +312,8 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
           for (int64_t i = lo; i < hi; ++i) fo[lo + cnt[lv[i]]++] = (int32_t)i;
         }
       }
-      std::vector<int32_t> plan((size_t)N * 32, 0);
-      for (int64_t r = 0; r < N; ++r) {
+      std::vector<int32_t> plan((size_t)Nd * 32, 0);
+      for (int64_t r = 0; r < Nd; ++r) {
         const int32_t i = fo[r];
         int32_t* rec = plan.data() + r * 32;
         rec[0] = i;
@@ -341,6 +350,24 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
     ctx->ilu_waves = (int)std::max<size_t>(1, std::min<size_t>({12, (size_t)std::max(1, ctx->fs.maxwidth),
                                                                 (size_t)ctx->lds_max / per_wave}));
   }
+  // halo exchange plan (distributed mesh)
+  if (mesh->n_neigh > 0) {
+    if (!mesh->neigh || !mesh->send_ptr || !mesh->send_idx || !mesh->recv_ptr) CK(RX_ERR_ARG);
+    ctx->n_neigh = mesh->n_neigh;
+    ctx->h_neigh.assign(mesh->neigh, mesh->neigh + mesh->n_neigh);
+    ctx->h_send_ptr.assign(mesh->send_ptr, mesh->send_ptr + mesh->n_neigh + 1);
+    ctx->h_recv_ptr.assign(mesh->recv_ptr, mesh->recv_ptr + mesh->n_neigh + 1);
+    if (ctx->h_recv_ptr.back() != N - ctx->Nd) CK(RX_ERR_ARG);
+    ctx->n_send = ctx->h_send_ptr.back();
+    std::vector<int32_t> si(ctx->n_send);
+    for (int64_t q = 0; q < ctx->n_send; ++q) {
+      if (mesh->send_idx[q] < 0 || mesh->send_idx[q] >= ctx->Nd) CK(RX_ERR_ARG);
+      si[q] = (int32_t)mesh->send_idx[q];
+    }
+    CK(dupload(ctx, &ctx->send_idx, si.data(), si.size()));
+    CK(dalloc(ctx, &ctx->sendbuf, (size_t)std::max<int64_t>(1, ctx->n_send) * kHaloMaxStride));
+  }
+  CK(dalloc(ctx, &ctx->rms_sum, 32));
   // LSQ neighbour lists (reference order) and boundary vertices per node
   std::vector<int32_t> nptr(N + 1), nbr(mesh->nbr_ptr[N]);
   for (int64_t i = 0; i <= N; ++i) nptr[i] = (int32_t)mesh->nbr_ptr[i];
@@ -472,9 +499,10 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
-                  ctx->fs.slot, ctx->bs.slot,
+                  ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->sendbuf, ctx->rms_sum,
                   ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
+  rx_comm_free(ctx);
   if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
   if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
   rx_la_krylov_free(ctx);
@@ -572,13 +600,19 @@ int rx_cell_source_pasr(rx_ctx* ctx) {
 int rx_grad_lsq(rx_ctx* ctx) {
   if (!ctx) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_GRAD);
-  return rx_launch_grad(ctx);
+  const int rc = rx_launch_grad(ctx);
+  if (rc) return rc;
+  // Set_MPI_Primitive_Gradient (solver_direct_reactive.cpp:5049)
+  return rx_la_exchange(ctx, ctx->f[RX_F_GRAD], (int)(ctx->fcount[RX_F_GRAD] / ctx->N));
 }
 
 int rx_limiter_venkat(rx_ctx* ctx) {
   if (!ctx) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_LIMITER);
-  return rx_launch_limiter(ctx);
+  const int rc = rx_launch_limiter(ctx);
+  if (rc) return rc;
+  // Set_MPI_Primitive_Limiter (:1522)
+  return rx_la_exchange(ctx, ctx->f[RX_F_LIMITER], (int)(ctx->fcount[RX_F_LIMITER] / ctx->N));
 }
 
 int rx_time_step(rx_ctx* ctx) {
@@ -649,9 +683,11 @@ int enqueue_solve(rx_ctx* ctx) {
   return rx_la_implicit_update(ctx);
 }
 
-bool graphs_enabled() {
+// The solve is replayed as a graph unless RX_NO_GRAPH=1 or a host-staged transport is attached
+// (its exchanges synchronise with the host).
+bool graphs_enabled(const rx_ctx* ctx) {
   const char* e = getenv("RX_NO_GRAPH");
-  return !(e && e[0] == '1');
+  return !(e && e[0] == '1') && !ctx->has_hcomm;
 }
 }  // namespace
 
@@ -675,7 +711,7 @@ int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   }
   {
     RxPhase ph(ctx, RX_K_SOLVE);
-    if (graphs_enabled()) {
+    if (graphs_enabled(ctx)) {
       if (!ctx->solve_exec) {
         RX_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
         ctx->capturing = true;

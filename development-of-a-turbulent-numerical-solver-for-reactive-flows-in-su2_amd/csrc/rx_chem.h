@@ -55,7 +55,8 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
     k.Ys[s] = y;
     Cs[s] = 1.0e3 * drho * y / m.mm[s];
   }
-  for (int r = 0; r < nr; ++r) {
+  _Pragma("unroll") for (int r = 0; r < kMaxNR; ++r) {
+    if (r >= nr) break;
     const double kf = m.A[r] * pow(T, m.beta[r]) * exp(-m.Ta[r] / T);
     double kb;
     if (!m.hasb[r]) {
@@ -97,7 +98,8 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
   // PaSR constants (Set_DfrDrhos + AssemblePaSRConstant)
   if (P.rans) {
     const double tau_mix = 1 / (P.C_mu * omega_turb);
-    for (int r = 0; r < nr; ++r) {
+    _Pragma("unroll") for (int r = 0; r < kMaxNR; ++r) {
+    if (r >= nr) break;
       double hd = -1.0;
 #pragma unroll
       for (int s = 0; s < NS; ++s)
@@ -121,7 +123,8 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     double o = 0.0;
-    for (int r = 0; r < nr; ++r) {
+    _Pragma("unroll") for (int r = 0; r < kMaxNR; ++r) {
+    if (r >= nr) break;
       const double wir = 1.0e-3 * m.mm[s] * (m.sp[s * nr + r] - m.sr[s * nr + r]) * (k.F[r] - k.B[r]);
       o += P.rans ? k.k[r] * wir : wir;
     }
@@ -135,7 +138,8 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
     const double Tp = T + 1.0e-6 * T;
     const double RT = kR * Tp;
     const double lnRT = log(kRatm * Tp);
-    for (int r = 0; r < nr; ++r) {
+    _Pragma("unroll") for (int r = 0; r < kMaxNR; ++r) {
+    if (r >= nr) break;
       double Kcp;
       if (!m.hasb[r]) {
         if (k.B[r] > 0.0) {
@@ -160,7 +164,8 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
   for (int s = 0; s < NS; ++s) {
     // column 0 (temperature) of the [Ns][Ns+1] source Jacobian, reaction-ordered accumulation
     double sj0 = 0.0;
-    for (int r = 0; r < nr; ++r) {
+    _Pragma("unroll") for (int r = 0; r < kMaxNR; ++r) {
+    if (r >= nr) break;
       const double fixed = 1.0e-3 * m.mm[s] * (m.sp[s * nr + r] - m.sr[s * nr + r]);
       sj0 += P.rans ? fixed * (fc[r] - bc[r]) * k.k[r] : fixed * (fc[r] - bc[r]);
     }
@@ -173,7 +178,8 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       double sjj = 0.0;
-      for (int r = 0; r < nr; ++r) {
+      _Pragma("unroll") for (int r = 0; r < kMaxNR; ++r) {
+    if (r >= nr) break;
         const double fixed = 1.0e-3 * m.mm[s] * (m.sp[s * nr + r] - m.sr[s * nr + r]);
         if (k.Ys[j] > 1.0e-10) {
           const double num = k.F[r] * m.er[r * NS + j] - k.B[r] * m.ep[r * NS + j];

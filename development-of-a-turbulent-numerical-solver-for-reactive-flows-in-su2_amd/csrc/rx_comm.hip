@@ -1,0 +1,174 @@
+// rx_comm.hip — multi-GPU plumbing: halo exchange and all-reduce on the context stream, over RCCL
+// (graph-capturable: the FGMRES graph contains them) or over a caller-provided host transport.
+//
+// Halo exchange = the reference's SendReceive_Solution / Set_MPI_Solution / Set_MPI_Primitive_*
+// (Common/src/matrix_structure.cpp:794-880; SU2_CFD/src/solver_direct_reactive.cpp:1530-1640,
+// 1756-1990): owned values are packed per neighbour and received straight into the halo block
+// (halo points are contiguous per owning rank). Inner products and the RMS: dotProd's
+// MPI_Allreduce (Common/src/vector_structure.cpp:397-419), SetResidual_RMS (solver_structure.cpp:184-230).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "rx_ctx.h"
+
+namespace {
+
+__global__ void k_pack(int64_t n, int stride, const int32_t* __restrict__ idx, const double* __restrict__ f,
+                       double* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * stride) return;
+  const int64_t k = t / stride;
+  const int c = (int)(t - k * stride);
+  out[t] = f[(int64_t)idx[k] * stride + c];
+}
+
+int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? RX_OK : RX_ERR_COMM; }
+
+int stage_alloc(rx_ctx* ctx) {
+  if (ctx->h_stage) return RX_OK;
+  const size_t n = (size_t)(ctx->n_send + (ctx->N - ctx->Nd)) * kHaloMaxStride + 64;
+  RX_HIP(hipHostMalloc(&ctx->h_stage, n * sizeof(double)));
+  return RX_OK;
+}
+
+}  // namespace
+
+int rx_la_exchange(rx_ctx* ctx, double* f, int stride) {
+  if (!ctx->distributed() || ctx->n_neigh == 0) return RX_OK;
+  if (stride > kHaloMaxStride) return RX_ERR_ARG;
+  if (ctx->n_send > 0) {
+    const int64_t n = ctx->n_send * stride;
+    k_pack<<<(int)((n + 255) / 256), 256, 0, ctx->stream>>>(ctx->n_send, stride, ctx->send_idx, f, ctx->sendbuf);
+    RX_HIP(hipGetLastError());
+  }
+  double* halo = f + ctx->Nd * stride;
+  const int64_t n_recv = ctx->N - ctx->Nd;
+  if (ctx->has_hcomm) {
+    double* hs = ctx->h_stage;
+    double* hr = ctx->h_stage + ctx->n_send * stride;
+    RX_HIP(hipMemcpyAsync(hs, ctx->sendbuf, sizeof(double) * ctx->n_send * stride, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    RX_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->hcomm.sendrecv(ctx->hcomm.user, ctx->n_neigh, ctx->h_neigh.data(), ctx->h_send_ptr.data(), hs,
+                            ctx->h_recv_ptr.data(), hr, stride) != 0)
+      return RX_ERR_COMM;
+    RX_HIP(hipMemcpyAsync(halo, hr, sizeof(double) * n_recv * stride, hipMemcpyHostToDevice, ctx->stream));
+    return RX_OK;
+  }
+  ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
+  int rc = nccl_rc(ncclGroupStart());
+  for (int k = 0; k < ctx->n_neigh && !rc; ++k) {
+    const int64_t s0 = ctx->h_send_ptr[k], s1 = ctx->h_send_ptr[k + 1];
+    const int64_t r0 = ctx->h_recv_ptr[k], r1 = ctx->h_recv_ptr[k + 1];
+    if (s1 > s0)
+      rc = nccl_rc(ncclSend(ctx->sendbuf + s0 * stride, (size_t)((s1 - s0) * stride), ncclDouble, ctx->h_neigh[k],
+                            comm, ctx->stream));
+    if (!rc && r1 > r0)
+      rc = nccl_rc(ncclRecv(halo + r0 * stride, (size_t)((r1 - r0) * stride), ncclDouble, ctx->h_neigh[k], comm,
+                            ctx->stream));
+  }
+  const int rc2 = nccl_rc(ncclGroupEnd());
+  return rc ? rc : rc2;
+}
+
+int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count) {
+  if (!ctx->distributed()) return RX_OK;
+  if (ctx->has_hcomm) {
+    if (count > 64) return RX_ERR_ARG;
+    double* h = ctx->h_stage + (ctx->n_send + (ctx->N - ctx->Nd)) * kHaloMaxStride;
+    RX_HIP(hipMemcpyAsync(h, in, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
+    RX_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->hcomm.allreduce(ctx->hcomm.user, h, h, count) != 0) return RX_ERR_COMM;
+    RX_HIP(hipMemcpyAsync(out, h, sizeof(double) * count, hipMemcpyHostToDevice, ctx->stream));
+    return RX_OK;
+  }
+  return nccl_rc(ncclAllReduce(in, out, (size_t)count, ncclDouble, ncclSum, static_cast<ncclComm_t>(ctx->comm),
+                               ctx->stream));
+}
+
+namespace {
+
+// global owned-point count (RMS normalisation) and a fresh solve graph once a transport is attached
+int comm_attached(rx_ctx* ctx) {
+  double* d = nullptr;
+  RX_HIP(hipMalloc(&d, sizeof(double)));
+  double h = (double)ctx->Nd;
+  int rc = RX_OK;
+  if (hipMemcpyAsync(d, &h, sizeof(double), hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    rc = RX_ERR_HIP;
+  if (!rc) rc = rx_la_allreduce(ctx, d, d, 1);
+  if (!rc && (hipMemcpyAsync(&h, d, sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+              hipStreamSynchronize(ctx->stream) != hipSuccess))
+    rc = RX_ERR_HIP;
+  if (!rc) ctx->n_global = (int64_t)h;
+  (void)hipFree(d);
+  if (ctx->solve_exec) {
+    (void)hipGraphExecDestroy(ctx->solve_exec);
+    ctx->solve_exec = nullptr;
+  }
+  if (ctx->solve_graph) {
+    (void)hipGraphDestroy(ctx->solve_graph);
+    ctx->solve_graph = nullptr;
+  }
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rx_comm_unique_id(void* id128) {
+  if (!id128) return RX_ERR_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return RX_ERR_COMM;
+  std::memcpy(id128, &id, sizeof(id));
+  return RX_OK;
+}
+
+int rx_comm_init(rx_ctx* ctx, int nranks, int rank, const void* id128) {
+  if (!ctx || !id128 || nranks < 1 || rank < 0 || rank >= nranks || ctx->distributed()) return RX_ERR_ARG;
+  RX_HIP(hipSetDevice(ctx->device));
+  ncclUniqueId id;
+  std::memcpy(&id, id128, sizeof(id));
+  ncclComm_t comm = nullptr;
+  if (ncclCommInitRank(&comm, nranks, id, rank) != ncclSuccess) return RX_ERR_COMM;
+  ctx->comm = comm;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return comm_attached(ctx);
+}
+
+int rx_comm_init_host(rx_ctx* ctx, int nranks, int rank, const rx_host_comm* ops) {
+  if (!ctx || !ops || !ops->sendrecv || !ops->allreduce || nranks < 1 || rank < 0 || rank >= nranks ||
+      ctx->distributed())
+    return RX_ERR_ARG;
+  int rc = stage_alloc(ctx);
+  if (rc) return rc;
+  ctx->hcomm = *ops;
+  ctx->has_hcomm = true;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return comm_attached(ctx);
+}
+
+int rx_halo_exchange(rx_ctx* ctx, rx_field f) {
+  if (!ctx || f < 0 || f >= RX_F_COUNT || ctx->fcount[f] % ctx->N != 0) return RX_ERR_ARG;
+  if (f == RX_F_JAC || f == RX_F_ILU) return RX_ERR_ARG;
+  const int rc = rx_la_exchange(ctx, ctx->f[f], (int)(ctx->fcount[f] / ctx->N));
+  if (rc) return rc;
+  RX_HIP(hipStreamSynchronize(ctx->stream));
+  return RX_OK;
+}
+
+}  // extern "C"
+
+void rx_comm_free(rx_ctx* ctx) {
+  if (ctx->comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
+  ctx->comm = nullptr;
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  ctx->h_stage = nullptr;
+  ctx->has_hcomm = false;
+}

@@ -20,6 +20,22 @@ struct rx_ctx {
   hipStream_t stream = nullptr;
   int nDim = 2, ns = 0, nr = 0, nVar = 0, nPV = 0, nG = 0, nL = 0;
   int64_t N = 0, E = 0, NB = 0, nnzb = 0;
+  int64_t Nd = 0;               // owned (domain) points; N - Nd halo points follow them
+  // ---- distributed: halo plan and RCCL communicator (rx_comm.hip)
+  int n_neigh = 0;
+  std::vector<int> h_neigh;
+  std::vector<int64_t> h_send_ptr, h_recv_ptr;
+  int32_t* send_idx = nullptr;  // [n_send] owned points to send, grouped per neighbour
+  int64_t n_send = 0;
+  double* sendbuf = nullptr;    // [n_send * kHaloMaxStride]
+  void* comm = nullptr;         // ncclComm_t
+  bool has_hcomm = false;       // host-staged transport (rx_comm_init_host)
+  rx_host_comm hcomm{};
+  double* h_stage = nullptr;    // pinned [(n_send + N - Nd) * kHaloMaxStride + 64]
+  int nranks = 1, rank = 0;
+  bool distributed() const { return comm != nullptr || has_hcomm; }
+  int64_t n_global = 0;         // owned points over all ranks
+  double* rms_sum = nullptr;    // [32] per-variable sums of squares (device)
   rx_cfg cfg{};
 
   // ---- dual grid (device)
@@ -115,6 +131,13 @@ struct rx_ctx {
 };
 
 int rx_fail_hip(rx_ctx* ctx, hipError_t e);
+constexpr int kHaloMaxStride = 64;  // doubles per point of the largest exchanged field (gradient)
+// halo exchange of a device array with `stride` doubles per point (no-op without communicator)
+int rx_la_exchange(rx_ctx* ctx, double* f, int stride);
+// out[i] = sum over ranks of in[i] (in == out allowed), ordered on the context stream; no-op
+// without communicator
+int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count);
+void rx_comm_free(rx_ctx* ctx);
 
 // Phase timer: records HIP events around a phase on the context stream when profiling is on.
 struct RxPhase {

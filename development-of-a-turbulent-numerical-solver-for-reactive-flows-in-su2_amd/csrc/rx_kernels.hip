@@ -171,7 +171,8 @@ __global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restri
   for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
   double res[nVar];
   double* summ = P.implicit ? Summ + (size_t)e * visc_summary_size<NS>() : nullptr;
-  const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ);
+  __shared__ double scr_all[64 * NS * NS];  // dense Stefan-Maxwell / QR matrices, one slice per lane
+  const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ, scr_all + threadIdx.x * NS * NS);
   bool bad = false;
 #pragma unroll
   for (int v = 0; v < nVar; ++v) {

@@ -16,6 +16,16 @@
 // block to arrive sums the partials in a fixed tree (MI355X_MICROARCH.md, inter-workgroup hand-off
 // with sc1 stores/loads). The summation order is fixed (independent of arrival order); the oracle's
 // orc_dot mode 1 restates it. The reference sums sequentially, so results agree to rounding.
+//
+// Distributed (one rank per GPU): every reducing kernel publishes its rank-local sums in
+// KState::loc[4] (slots not produced are zero), and an out-of-place all-reduce loc -> the landing
+// slots {norm0_in, dot, dotn, dot2} follows each reducing launch (dotProd's MPI_Allreduce,
+// Common/src/vector_structure.cpp:397-419). A skipped kernel leaves loc unchanged, so the
+// all-reduce after it is idempotent and every rank takes the same decisions. Single rank: the
+// reducer writes the landing slots itself and no collective is issued. Vectors have N*nVar rows;
+// inner products and updates run over the owned prefix Nd*nVar, the preconditioned vector z_i gets
+// its halo from the neighbours before the SpMV reads it (MatrixVectorProduct :997-1029 +
+// SendReceive_Solution :794).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -30,8 +40,9 @@ constexpr int kMaxM = 64;
 inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 
 struct KState {
-  double tol, norm0, beta, nrm, thr2[2], prod, dot, resid;  // thr2: read thr2[k&1], write thr2[(k+1)&1]
-  double norm0_in, dotn, dot2;  // inner-product landing slots
+  double tol, norm0, beta, nrm, thr2[2], prod, resid;  // thr2: read thr2[k&1], write thr2[(k+1)&1]
+  double norm0_in, dot, dotn, dot2;  // inner-product landing slots (all-reduced), contiguous
+  double loc[4];                     // rank-local sums in landing-slot order
   int done, noreo, iters, diverged, conv;
   unsigned int ticket;          // arrival counter of the in-launch reductions
   double H[(kMaxM + 1) * kMaxM];  // H[k][i] at k * kMaxM + i
@@ -54,10 +65,15 @@ __device__ inline void block_tree(double* sh) {
   }
 }
 
-// In-launch grid reduction of NR partial sums into *out[r] (see header). part: [NR][kRedBlocks].
+enum Slot { kNorm0In = 0, kDot = 1, kDotN = 2, kDot2 = 3 };
+__device__ inline double* land(KState* s) { return &s->norm0_in; }
+
+// In-launch grid reduction of NR partial sums into landing slots slot[r] (see header); the other
+// landing slots are zeroed in loc. part: [NR][kRedBlocks].
 template <int NR>
-__device__ inline void grid_reduce(const double (&v)[NR], double* __restrict__ part, unsigned int* ticket,
-                                   double* const (&out)[NR]) {
+__device__ inline void grid_reduce(const double (&v)[NR], double* __restrict__ part, KState* __restrict__ s,
+                                   const int (&slot)[NR], bool dist) {
+  unsigned int* ticket = &s->ticket;
   __shared__ double sh[NR * kBlock + 1];
   int* last = reinterpret_cast<int*>(sh + NR * kBlock);
 #pragma unroll
@@ -84,24 +100,16 @@ __device__ inline void grid_reduce(const double (&v)[NR], double* __restrict__ p
   }
   block_tree<NR>(sh);
   if (threadIdx.x == 0) {
+    double* dst = dist ? s->loc : land(s);
+    for (int r = 0; r < 4; ++r) dst[r] = 0.0;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) *out[r] = sh[r * kBlock];
+    for (int r = 0; r < NR; ++r) dst[slot[r]] = sh[r * kBlock];
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 #define GRID_LOOP(q, n) \
   for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < (n); q += (int64_t)kRedBlocks * kBlock)
-
-// <a, b> (standalone)
-__global__ __launch_bounds__(kBlock) void k_dot(int64_t n, const double* __restrict__ a, const double* __restrict__ b,
-                                                double* __restrict__ part, KState* __restrict__ s,
-                                                double* __restrict__ out) {
-  double v[1] = {0.0};
-  GRID_LOOP(q, n) v[0] += a[q] * b[q];
-  double* const o[1] = {out};
-  grid_reduce<1>(v, part, &s->ticket, o);
-}
 
 // Row-block product of y = A x for element q = (row i, component a): the reference's
 // MatrixVectorProduct order (blocks of the row in column order, columns c ascending).
@@ -119,34 +127,36 @@ __device__ inline double spmv_elem(int64_t q, const int32_t* __restrict__ rp, co
   return acc;
 }
 
-// w0 = A x - b and |w0|^2 -> dot
+// |b|^2 -> norm0_in, w0 = A x - b and |w0|^2 -> dot (owned rows Nd)
 template <int NV>
-__global__ __launch_bounds__(kBlock) void k_fg_residual(int N, const int32_t* __restrict__ rp,
+__global__ __launch_bounds__(kBlock) void k_fg_residual(int Nd, const int32_t* __restrict__ rp,
                                                         const int32_t* __restrict__ col, const double* __restrict__ A,
                                                         const double* __restrict__ x, const double* __restrict__ b,
                                                         double* __restrict__ w, double* __restrict__ part,
-                                                        KState* __restrict__ s) {
-  const int64_t n = (int64_t)N * NV;
-  double v[1] = {0.0};
+                                                        KState* __restrict__ s, bool dist) {
+  const int64_t n = (int64_t)Nd * NV;
+  double v[2] = {0.0, 0.0};
   GRID_LOOP(q, n) {
+    const double bq = b[q];
+    v[0] += bq * bq;
     double y = spmv_elem<NV>(q, rp, col, A, x);
-    y -= b[q];
+    y -= bq;
     w[q] = y;
-    v[0] += y * y;
+    v[1] += y * y;
   }
-  double* const o[1] = {&s->dot};
-  grid_reduce<1>(v, part, &s->ticket, o);
+  const int sl[2] = {kNorm0In, kDot};
+  grid_reduce<2>(v, part, s, sl, dist);
 }
 
 // w_{i+1} = A z_i with |w_{i+1}|^2 -> dotn and <w_{i+1}, w_0> -> dot
 template <int NV>
-__global__ __launch_bounds__(kBlock) void k_fg_spmv(int N, const int32_t* __restrict__ rp,
+__global__ __launch_bounds__(kBlock) void k_fg_spmv(int Nd, const int32_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col, const double* __restrict__ A,
                                                     const double* __restrict__ z, const double* __restrict__ w0,
                                                     double* __restrict__ w, double* __restrict__ part,
-                                                    KState* __restrict__ s) {
+                                                    KState* __restrict__ s, bool dist) {
   if (s->done) return;
-  const int64_t n = (int64_t)N * NV;
+  const int64_t n = (int64_t)Nd * NV;
   double v[2] = {0.0, 0.0};
   GRID_LOOP(q, n) {
     const double y = spmv_elem<NV>(q, rp, col, A, z);
@@ -154,8 +164,8 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv(int N, const int32_t* __rest
     v[0] += y * y;
     v[1] += y * w0[q];
   }
-  double* const o[2] = {&s->dotn, &s->dot};
-  grid_reduce<2>(v, part, &s->ticket, o);
+  const int sl[2] = {kDotN, kDot};
+  grid_reduce<2>(v, part, s, sl, dist);
 }
 
 // w0 = w0 / (-beta) after the start decision (:318-330), evaluated identically by every lane.
@@ -186,8 +196,8 @@ __global__ __launch_bounds__(kBlock) void k_fg_start_div(int64_t n, KState* __re
 // w -= prod w_k, the re-orthogonalisation test prod^2 > thr, and the inner product the recurrence
 // needs next: <w, w_k> (re-orthogonalise), else <w, w_{k+1}> (k < i) or |w|^2 (k == i).
 // For k = 0 also ModGramSchmidt's entry: nrm = |w|^2 (s->dotn), thr = 0.98 nrm, breakdown test.
-__global__ __launch_bounds__(kBlock) void k_fg_proj(int64_t n, KState* __restrict__ s, int k, int i,
-                                                    double* __restrict__ W, double* __restrict__ part) {
+__global__ __launch_bounds__(kBlock) void k_fg_proj(int64_t n, int64_t ld, KState* __restrict__ s, int k, int i,
+                                                    double* __restrict__ W, double* __restrict__ part, bool dist) {
   if (s->done) return;
   double nrm0 = 0.0;
   if (k == 0) {
@@ -203,9 +213,9 @@ __global__ __launch_bounds__(kBlock) void k_fg_proj(int64_t n, KState* __restric
   const double prod = s->dot;
   const double thr = (k == 0) ? nrm0 * 0.98 : s->thr2[k & 1];
   const bool reo = prod * prod > thr;
-  const double* wk = W + (int64_t)k * n;
-  double* w = W + (int64_t)(i + 1) * n;
-  const double* wn = reo ? wk : (k < i ? W + (int64_t)(k + 1) * n : nullptr);
+  const double* wk = W + (int64_t)k * ld;
+  double* w = W + (int64_t)(i + 1) * ld;
+  const double* wn = reo ? wk : (k < i ? W + (int64_t)(k + 1) * ld : nullptr);
   double v[1] = {0.0};
   GRID_LOOP(q, n) {
     const double y = w[q] + (-1.0 * prod) * wk[q];
@@ -223,19 +233,19 @@ __global__ __launch_bounds__(kBlock) void k_fg_proj(int64_t n, KState* __restric
       s->thr2[(k + 1) & 1] = s->nrm * 0.98;
     }
   }
-  double* const o[1] = {reo ? &s->dot2 : (k < i ? &s->dot : &s->dotn)};
-  grid_reduce<1>(v, part, &s->ticket, o);
+  const int sl[1] = {reo ? kDot2 : (k < i ? kDot : kDotN)};
+  grid_reduce<1>(v, part, s, sl, dist);
 }
 
 // Second projection when the test fired: H[k][i] += prod2, w -= prod2 w_k, norm update, and the
 // next inner product (<w, w_{k+1}> or |w|^2).
-__global__ __launch_bounds__(kBlock) void k_fg_reo(int64_t n, KState* __restrict__ s, int k, int i,
-                                                   double* __restrict__ W, double* __restrict__ part) {
+__global__ __launch_bounds__(kBlock) void k_fg_reo(int64_t n, int64_t ld, KState* __restrict__ s, int k, int i,
+                                                   double* __restrict__ W, double* __restrict__ part, bool dist) {
   if (s->done || s->noreo) return;
   const double prod = s->dot2;
-  const double* wk = W + (int64_t)k * n;
-  double* w = W + (int64_t)(i + 1) * n;
-  const double* wn = k < i ? W + (int64_t)(k + 1) * n : nullptr;
+  const double* wk = W + (int64_t)k * ld;
+  double* w = W + (int64_t)(i + 1) * ld;
+  const double* wn = k < i ? W + (int64_t)(k + 1) * ld : nullptr;
   double v[1] = {0.0};
   GRID_LOOP(q, n) {
     const double y = w[q] + (-1.0 * prod) * wk[q];
@@ -248,8 +258,8 @@ __global__ __launch_bounds__(kBlock) void k_fg_reo(int64_t n, KState* __restrict
     if (s->nrm < 0.0) s->nrm = 0.0;
     s->thr2[(k + 1) & 1] = s->nrm * 0.98;
   }
-  double* const o[1] = {k < i ? &s->dot : &s->dotn};
-  grid_reduce<1>(v, part, &s->ticket, o);
+  const int sl[1] = {k < i ? kDot : kDotN};
+  grid_reduce<1>(v, part, s, sl, dist);
 }
 
 __device__ inline void apply_givens(double sn, double cs, double& h1, double& h2) {
@@ -302,7 +312,11 @@ __global__ __launch_bounds__(kBlock) void k_fg_close_div(int64_t n, KState* __re
   if (lead()) fg_close(s, i);
 }
 
+// Per-solve initialisation; g = 0 as the reference's std::vector<su2double> g(m+1, 0.0) (:349):
+// the Givens update of column i reads g[i+1] before writing it.
 __global__ void k_fg_reset(KState* s, double tol) {
+  for (int k = threadIdx.x; k <= kMaxM; k += blockDim.x) s->g[k] = 0.0;
+  if (threadIdx.x != 0) return;
   s->tol = tol;
   s->done = 0;
   s->conv = 0;
@@ -314,8 +328,8 @@ __global__ void k_fg_reset(KState* s, double tol) {
 
 // SolveReduced (:73-85) and x += sum_k y_k z_k (k ascending, element by element as the reference's
 // per-k vector updates). Every block solves the small triangular system itself.
-__global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, KState* __restrict__ s, const double* __restrict__ Z,
-                                                      double* __restrict__ x) {
+__global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, int64_t ld, KState* __restrict__ s,
+                                                      const double* __restrict__ Z, double* __restrict__ x) {
   if (s->diverged) return;
   __shared__ double y[kMaxM];
   const int it = s->iters;
@@ -334,7 +348,7 @@ __global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, KState* __restr
   if (it == 0) return;
   GRID_LOOP(q, n) {
     double v = x[q];
-    for (int k = 0; k < it; ++k) v += y[k] * Z[(int64_t)k * n + q];
+    for (int k = 0; k < it; ++k) v += y[k] * Z[(int64_t)k * ld + q];
     x[q] = v;
   }
 }
@@ -347,6 +361,9 @@ __global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, KState* __restr
     case 13: { constexpr int NV_ = 13; CALL; } break; \
     default: return RX_ERR_ARG;                      \
   }
+
+// device address of the landing slots (host-side pointer arithmetic on the device KState)
+double* land_host(KState* s) { return &s->norm0_in; }
 
 }  // namespace
 
@@ -373,20 +390,23 @@ int rx_la_krylov_alloc(rx_ctx* ctx, int m) {
 int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m) {
   int rc = rx_la_krylov_alloc(ctx, m);
   if (rc) return rc;
-  const int64_t n = ctx->N * ctx->nVar;
+  const int64_t ld = ctx->N * ctx->nVar;  // vector length (owned + halo)
+  const int64_t n = ctx->Nd * ctx->nVar;  // owned prefix
   const int nb = blocks(n);
+  const bool dist = ctx->distributed();
   hipStream_t st = ctx->stream;
   KState* s = static_cast<KState*>(ctx->kstate);
   double* A = ctx->f[RX_F_JAC];
   double* b = ctx->f[RX_F_RHS];
   double* x = ctx->f[RX_F_SOL];
   double* part = ctx->red;  // [2][kRedBlocks]
-  auto W = [&](int k) { return ctx->kw + (int64_t)k * n; };
-  auto Z = [&](int k) { return ctx->kz + (int64_t)k * n; };
-  k_fg_reset<<<1, 1, 0, st>>>(s, tol);
-  k_dot<<<kRedBlocks, kBlock, 0, st>>>(n, b, b, part, s, &s->norm0_in);
-  RX_NV_SWITCH(ctx->nVar, (k_fg_residual<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->N, ctx->rp, ctx->col, A, x, b,
-                                                                             W(0), part, s)));
+  auto W = [&](int k) { return ctx->kw + (int64_t)k * ld; };
+  auto Z = [&](int k) { return ctx->kz + (int64_t)k * ld; };
+  auto reduce = [&]() { return dist ? rx_la_allreduce(ctx, s->loc, land_host(s), 4) : RX_OK; };
+  k_fg_reset<<<1, 64, 0, st>>>(s, tol);
+  RX_NV_SWITCH(ctx->nVar, (k_fg_residual<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, x,
+                                                                             b, W(0), part, s, dist)));
+  if ((rc = reduce())) return rc;
   k_fg_start_div<<<nb, kBlock, 0, st>>>(n, s, W(0));
   for (int i = 0; i < m; ++i) {
     if (ctx->cfg.lin_prec == 1) {
@@ -394,15 +414,18 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m) {
     } else {
       if ((rc = rx_la_lusgs(ctx, A, W(i), Z(i), &s->done, &s->conv))) return rc;
     }
-    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->N, ctx->rp, ctx->col, A, Z(i),
-                                                                           W(0), W(i + 1), part, s)));
+    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, Z(i),
+                                                                           W(0), W(i + 1), part, s, dist)));
+    if ((rc = reduce())) return rc;
     for (int k = 0; k <= i; ++k) {
-      k_fg_proj<<<kRedBlocks, kBlock, 0, st>>>(n, s, k, i, ctx->kw, part);
-      k_fg_reo<<<kRedBlocks, kBlock, 0, st>>>(n, s, k, i, ctx->kw, part);
+      k_fg_proj<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, k, i, ctx->kw, part, dist);
+      if ((rc = reduce())) return rc;
+      k_fg_reo<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, k, i, ctx->kw, part, dist);
+      if ((rc = reduce())) return rc;
     }
     k_fg_close_div<<<kRedBlocks, kBlock, 0, st>>>(n, s, i, W(i + 1));
   }
-  k_fg_finish<<<kRedBlocks, kBlock, 0, st>>>(n, s, ctx->kz, x);
+  k_fg_finish<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, ctx->kz, x);
   RX_HIP(hipGetLastError());
   return RX_OK;
 }

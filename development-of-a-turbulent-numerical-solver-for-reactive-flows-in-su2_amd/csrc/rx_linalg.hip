@@ -39,14 +39,23 @@ __global__ __launch_bounds__(kBlock) void k_spmv(int N, const int32_t* __restric
   y[t] = acc;
 }
 
-// ImplicitEuler system build: Aii += V/dt (or identity row when dt <= EPS), rhs = -R, x = 0.
+// ImplicitEuler system build over the owned rows: Aii += V/dt (or identity row when dt <= EPS),
+// rhs = -R, x = 0; halo rows get rhs = x = 0 (solver_direct_reactive.cpp:2336-2387).
 template <int NV>
-__global__ __launch_bounds__(kBlock) void k_build_system(int N, const int64_t* __restrict__ diag,
+__global__ __launch_bounds__(kBlock) void k_build_system(int Nd, int N, const int64_t* __restrict__ diag,
                                                          const double* __restrict__ vol, const double* __restrict__ dt,
                                                          double* __restrict__ A, double* __restrict__ R,
                                                          double* __restrict__ rhs, double* __restrict__ x) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
+  if (i >= Nd) {
+#pragma unroll
+    for (int a = 0; a < NV; ++a) {
+      rhs[(size_t)i * NV + a] = 0.0;
+      x[(size_t)i * NV + a] = 0.0;
+    }
+    return;
+  }
   double* D = A + diag[i] * NV * NV;
   const bool ok = dt[i] > rx::kEPS;
   if (ok) {
@@ -108,6 +117,15 @@ __global__ __launch_bounds__(kBlock) void k_sumsq_cols(int N, int nVar, const do
   }
 }
 
+// Per-variable totals of the block partials, summed in block order (one lane per variable).
+__global__ void k_sumsq_total(int nVar, int nblk, const double* __restrict__ part, double* __restrict__ out) {
+  const int v = threadIdx.x;
+  if (v >= nVar) return;
+  double s = 0.0;
+  for (int q = 0; q < nblk; ++q) s += part[q * nVar + v];
+  out[v] = s;
+}
+
 #define RX_NV_SWITCH(nv, CALL)                       \
   switch (nv) {                                      \
     case 7: { constexpr int NV_ = 7; CALL; } break;   \
@@ -120,57 +138,58 @@ __global__ __launch_bounds__(kBlock) void k_sumsq_cols(int N, int nVar, const do
 
 }  // namespace
 
+// MatrixVectorProduct (:997-1029): owned rows, then the halo of the product from the neighbours.
 int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y, const int* skip) {
-  RX_NV_SWITCH(ctx->nVar, (k_spmv<NV_><<<blocks(ctx->N * NV_), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->rp,
-                                                                                          ctx->col, A, x, y, skip)));
+  RX_NV_SWITCH(ctx->nVar, (k_spmv<NV_><<<blocks(ctx->Nd * NV_), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->rp,
+                                                                                           ctx->col, A, x, y, skip)));
   RX_HIP(hipGetLastError());
-  return RX_OK;
+  return rx_la_exchange(ctx, y, ctx->nVar);
 }
 
 int rx_la_build_system(rx_ctx* ctx) {
   RX_NV_SWITCH(ctx->nVar, (k_build_system<NV_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
-                              (int)ctx->N, ctx->diag, ctx->vol, ctx->f[RX_F_DT], ctx->f[RX_F_JAC], ctx->f[RX_F_RES],
+                              (int)ctx->Nd, (int)ctx->N, ctx->diag, ctx->vol, ctx->f[RX_F_DT], ctx->f[RX_F_JAC], ctx->f[RX_F_RES],
                               ctx->f[RX_F_RHS], ctx->f[RX_F_SOL])));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
 
-// SetResidual_RMS (solver_structure.cpp:184): per-variable partial sums of r^2 (fixed order), read
-// back and finished on the host by rx_la_rms_read.
+// SetResidual_RMS (solver_structure.cpp:184-230): per-variable sums of r^2 over the owned rows
+// (fixed order), all-reduced over ranks into rms_sum[16..), read back and finished on the host by
+// rx_la_rms_read with the global owned-point count.
 constexpr int kRmsBlocks = 256;
 constexpr int64_t kRmsOff = 1024;  // ctx->red[0..1023] is the inner-product scratch
 
 int rx_la_rms_enqueue(rx_ctx* ctx, const double* r) {
-  k_sumsq_cols<<<kRmsBlocks, kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nVar, r, ctx->red + kRmsOff);
+  k_sumsq_cols<<<kRmsBlocks, kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, r, ctx->red + kRmsOff);
+  k_sumsq_total<<<1, 64, 0, ctx->stream>>>(ctx->nVar, kRmsBlocks, ctx->red + kRmsOff, ctx->rms_sum);
   RX_HIP(hipGetLastError());
-  return RX_OK;
+  return rx_la_allreduce(ctx, ctx->rms_sum, ctx->rms_sum + 16, ctx->nVar);
 }
 
 int rx_la_rms_read(rx_ctx* ctx, double* rms) {
   const int nv = ctx->nVar;
-  RX_HIP(hipMemcpyAsync(ctx->h_red, ctx->red + kRmsOff, sizeof(double) * kRmsBlocks * nv, hipMemcpyDeviceToHost,
-                        ctx->stream));
+  const double* src = ctx->rms_sum + (ctx->distributed() ? 16 : 0);
+  RX_HIP(hipMemcpyAsync(ctx->h_red, src, sizeof(double) * nv, hipMemcpyDeviceToHost, ctx->stream));
   RX_HIP(hipStreamSynchronize(ctx->stream));
-  for (int v = 0; v < nv; ++v) {
-    double s = 0.0;
-    for (int q = 0; q < kRmsBlocks; ++q) s += ctx->h_red[q * nv + v];
-    rms[v] = std::max(rx::kEPS * rx::kEPS, std::sqrt(s / (double)ctx->N));
-  }
+  for (int v = 0; v < nv; ++v)
+    rms[v] = std::max(rx::kEPS * rx::kEPS, std::sqrt(ctx->h_red[v] / (double)ctx->n_global));
   return RX_OK;
 }
 
+// Owned points, then Set_MPI_Solution (solver_direct_reactive.cpp:2403, 2445).
 int rx_la_implicit_update(rx_ctx* ctx) {
-  const int64_t n = ctx->N * ctx->nVar;
-  k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nVar, ctx->nDim, ctx->f[RX_F_SOL],
+  const int64_t n = ctx->Nd * ctx->nVar;
+  k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_SOL],
                                                   ctx->cfg.relaxation, ctx->vol, ctx->f[RX_F_DT], 0, ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());
-  return RX_OK;
+  return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }
 
 int rx_la_explicit_update(rx_ctx* ctx) {
-  const int64_t n = ctx->N * ctx->nVar;
-  k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], 1.0,
+  const int64_t n = ctx->Nd * ctx->nVar;
+  k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], 1.0,
                                                   ctx->vol, ctx->f[RX_F_DT], 1, ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());
-  return RX_OK;
+  return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }

@@ -834,7 +834,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                          reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx),
                          b, x, done, conv)));
     RX_HIP(hipGetLastError());
-    return RX_OK;
+    return rx_la_exchange(ctx, x, nv);  // ComputeILUPreconditioner's closing SendReceive_Solution (:1513)
   }
   RX_NV_SWITCH(ctx->nVar, (k_ilu_fwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->diag,
@@ -843,12 +843,12 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                               ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows, ctx->col, ctx->khi, ctx->diag,
                               ctx->f[RX_F_ILU], rx_invd_buf(ctx), x, done, conv)));
   RX_HIP(hipGetLastError());
-  return RX_OK;
+  return rx_la_exchange(ctx, x, nv);
 }
 
 int rx_la_diag_factor(rx_ctx* ctx, const double* A) {
-  RX_NV_SWITCH(ctx->nVar, (k_diag_factor<NV_><<<(int)((ctx->N + 3) / 4), 256, 0, ctx->stream>>>(
-                              (int)ctx->N, ctx->diag, A, ctx->dlu)));
+  RX_NV_SWITCH(ctx->nVar, (k_diag_factor<NV_><<<(int)((ctx->Nd + 3) / 4), 256, 0, ctx->stream>>>(
+                              (int)ctx->Nd, ctx->diag, A, ctx->dlu)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
@@ -857,11 +857,14 @@ int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, int* d
   RX_NV_SWITCH(ctx->nVar, (k_lusgs_fwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->diag, A,
                               ctx->dlu, b, ctx->xstar, done, conv)));
+  // halo x* between the sweeps (ComputeLU_SGSPreconditioner :1689)
+  int rc = rx_la_exchange(ctx, ctx->xstar, ctx->nVar);
+  if (rc) return rc;
   RX_NV_SWITCH(ctx->nVar, (k_lusgs_bwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows, ctx->rp, ctx->col, ctx->klo, ctx->khi,
                               ctx->diag, A, ctx->dlu, ctx->xstar, x, done, conv)));
   RX_HIP(hipGetLastError());
-  return RX_OK;
+  return rx_la_exchange(ctx, x, ctx->nVar);  // :1707
 }
 
 // Debug: trace the phases of the ILU(0) factorisation of partition 0 (see tools/ilu_trace.py).

@@ -288,7 +288,7 @@ struct ViscNode {
 template <int NS, int NDIM>
 __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const ViscNode<NS, NDIM>& ni,
                                 const ViscNode<NS, NDIM>& nj, double sigma_k, const double* Normal, double* res,
-                                double* summ) {
+                                double* summ, double* scr) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
   constexpr int T_P = 0, VX_P = 1, RHO_P = NDIM + 2, RHOS_P = NDIM + 5;
   constexpr int RHO_S = 0, RHOVX_S = 1, RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
@@ -299,13 +299,11 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   const double* Vj = nj.V;
   const double Mean_mu = 2.0 / (1.0 / ni.mu + 1.0 / nj.mu);
   const double Mean_k = 2.0 / (1.0 / ni.kappa + 1.0 / nj.kappa);
-  double Dm[NS * NS];
+  // harmonic means of the binary diffusion coefficients (recomputed where used: same arithmetic)
+  auto Dm = [&](int q) { return 2.0 / (1.0 / ni.Dij[q] + 1.0 / nj.Dij[q]); };
   double Dmax = -INFINITY;
 #pragma unroll
-  for (int q = 0; q < NS * NS; ++q) {
-    Dm[q] = 2.0 / (1.0 / ni.Dij[q] + 1.0 / nj.Dij[q]);
-    Dmax = fmax(Dmax, Dm[q]);
-  }
+  for (int q = 0; q < NS * NS; ++q) Dmax = fmax(Dmax, Dm(q));
   double Vm[nPV];
 #pragma unroll
   for (int v = 0; v < nPV; ++v) Vm[v] = 0.5 * (Vi[v] + Vj[v]);
@@ -391,7 +389,7 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   }
   double Jd[NS];
   {
-    double Gt[NS * NS];
+    double* Gt = scr;  // LDS scratch of this lane (NS*NS)
     double sigma = 0.0, massTot = 0.0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) sigma += Ys[s];
@@ -404,12 +402,12 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
       for (int b = 0; b < NS; ++b) {
         double g;
         if (a != b) {
-          g = -sigma * massTot * Xs[a] / (rho * m.mm[b] * Dm[b * NS + a]);
+          g = -sigma * massTot * Xs[a] / (rho * m.mm[b] * Dm(b * NS + a));
         } else {
           double tmp = 0.0;
 #pragma unroll
           for (int c = 0; c < NS; ++c)
-            if (c != a) tmp += Xs[c] / Dm[c * NS + a];
+            if (c != a) tmp += Xs[c] / Dm(c * NS + a);
           g = sigma * massTot * tmp / (rho * m.mm[a]);
         }
         Gt[a * NS + b] = g + alpha * Ys[a];
@@ -451,7 +449,7 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
       tt[a][a] -= kTWO3 * (Mean_mut * dv + Mean_tke * rho);
     }
     {
-      double Mt[NS * NS];
+      double* Mt = scr;  // LDS scratch of this lane (NS*NS), Gt is dead here
       double sig = 0.0;
 #pragma unroll
       for (int s = 0; s < NS; ++s) sig += Xs[s];
@@ -647,30 +645,40 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
   }
   double colj[NS], coli[NS];  // dJ/drho column k = b - RHOS_S (species columns only)
   const int k = b - RHOS_S;
+  const int kk = (k >= 0 && k < NS) ? k : 0;
+  // the a == k term of :1352-1357, evaluated once for this lane's column (no divergent divisions)
+  const double dkj = rho * Ds[kk] * totMass_j * sigma_j / (dij * totMass * rho_j);
+  const double dki = rho * Ds[kk] * totMass_i * sigma_i / (dij * totMass * rho_i);
 #pragma unroll
   for (int a = 0; a < NS; ++a) {
     const double baj = __shfl(bj, a, 16), bai = __shfl(bi, a, 16);
     double vj = baj, vi = bai;
     if (k >= 0) {
-      vj += rho * Ys[a] * Ds[k] * totMass_j * sigma_j / (dij * totMass * rho_j);
-      vi -= rho * Ys[a] * Ds[k] * totMass_i * sigma_i / (dij * totMass * rho_i);
+      vj += rho * Ys[a] * Ds[kk] * totMass_j * sigma_j / (dij * totMass * rho_j);
+      vi -= rho * Ys[a] * Ds[kk] * totMass_i * sigma_i / (dij * totMass * rho_i);
       if (a == k) {
-        vj -= rho * Ds[a] * totMass_j * sigma_j / (dij * totMass * rho_j);
-        vi += rho * Ds[a] * totMass_i * sigma_i / (dij * totMass * rho_i);
+        vj -= dkj;
+        vi += dki;
       }
     }
     colj[a] = vj;
     coli[a] = vi;
   }
   if (b >= nVar) return;
-  if (k >= 0) {  // diagonal increments of dJ/drho (:1369-1374)
+  if (k >= 0) {  // diagonal increments of dJ/drho (:1369-1374): the same sequence for every diagonal entry
+    double tj[NS], ti[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      tj[q] = 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_j);
+      ti[q] = 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_i);
+    }
 #pragma unroll
     for (int a = 0; a < NS; ++a)
       if (a == k) {
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
-          colj[a] += 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_j);
-          coli[a] += 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_i);
+          colj[a] += tj[q];
+          coli[a] += ti[q];
         }
       }
   }
@@ -729,10 +737,10 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
     for (int q = 0; q < NS; ++q) {
       FJ[3][3] += mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
       FI[3][3] -= mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
-      if (q == k) {
-        FJ3k += mut / (PrT * LeT) * hs[q] * Ys[q] / rho_j * theta / sq * Area;
-        FI3k -= mut / (PrT * LeT) * hs[q] * Ys[q] / rho_i * theta / sq * Area;
-      }
+    }
+    if (k >= 0) {
+      FJ3k += mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_j * theta / sq * Area;
+      FI3k -= mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_i * theta / sq * Area;
     }
 #pragma unroll
     for (int q = 0; q < NS; ++q) {

@@ -205,3 +205,76 @@ def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, **kw):
     dual["quads"] = quads
     dual["part_ptr"] = part_ptr
     return dual
+
+
+def shard(mesh, n_ranks: int, rank: int):
+    """The local mesh of one MPI rank / GPU: the rank owns a contiguous block of the global partitions
+    (points [g0, g1) of the partition-major numbering) plus one halo layer, like the reference's
+    partitioned CGeometry (geometry_structure.cpp:11465-11530: domain points, then halo points).
+
+    Local numbering: own points in global order, then halo points in global order (so the halo is
+    contiguous per owning rank). Local edges: every global edge with an own endpoint, oriented low ->
+    high local id (normal negated when the orientation flips), sorted by (i, j). LSQ neighbour lists of
+    own points keep the global order; halo points keep only their local neighbours (their gradients
+    are overwritten by the halo exchange). Returns the local mesh dict plus the exchange plan
+    (`neigh`, `send_ptr`, `send_idx`, `recv_ptr`, `n_domain`) and `l2g`.
+    """
+    pp = np.asarray(mesh["part_ptr"], dtype=np.int64)
+    P = len(pp) - 1
+    assert P % n_ranks == 0 or P >= n_ranks, "need at least one partition per rank"
+    pr = np.array_split(np.arange(P), n_ranks)
+    rank_ptr = np.array([pp[c[0]] for c in pr] + [pp[-1]], dtype=np.int64)
+    g0, g1 = int(rank_ptr[rank]), int(rank_ptr[rank + 1])
+    owner = np.searchsorted(rank_ptr, np.arange(pp[-1]), side="right") - 1
+    e = np.asarray(mesh["edges"], dtype=np.int64)
+    own_e = ((e[:, 0] >= g0) & (e[:, 0] < g1)) | ((e[:, 1] >= g0) & (e[:, 1] < g1))
+    ends = np.unique(e[own_e].ravel())
+    halo = ends[(ends < g0) | (ends >= g1)]
+    n_own = g1 - g0
+    l2g = np.concatenate([np.arange(g0, g1, dtype=np.int64), halo])
+    g2l = np.full(int(pp[-1]), -1, dtype=np.int64)
+    g2l[l2g] = np.arange(len(l2g))
+    le = g2l[e[own_e]]
+    ln = np.asarray(mesh["edge_normal"])[own_e].copy()
+    flip = le[:, 0] > le[:, 1]
+    le[flip] = le[flip][:, ::-1]
+    ln[flip] *= -1.0
+    o = np.lexsort((le[:, 1], le[:, 0]))
+    le, ln = le[o], ln[o]
+    # LSQ neighbours
+    nptr_g, nbr_g = np.asarray(mesh["nbr_ptr"]), np.asarray(mesh["nbr"])
+    cnt = nptr_g[l2g + 1] - nptr_g[l2g]
+    idx = np.repeat(nptr_g[l2g], cnt) + (np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+    row = np.repeat(np.arange(len(l2g)), cnt)
+    lj = g2l[nbr_g[idx]]
+    ok = lj >= 0  # own points have every neighbour locally; halo points keep their local ones
+    nbr_l = lj[ok]
+    nptr_l = np.zeros(len(l2g) + 1, dtype=np.int64)
+    np.add.at(nptr_l, row[ok] + 1, 1)
+    nptr_l = np.cumsum(nptr_l)
+    # boundary vertices of own points
+    bv = np.asarray(mesh["bvertex"])[:, :2]
+    keep = (bv[:, 1] >= g0) & (bv[:, 1] < g1)
+    lbv = np.stack([bv[keep, 0], bv[keep, 1] - g0], axis=1).astype(np.int64) if keep.any() else np.zeros((0, 2),
+                                                                                                         np.int64)
+    # exchange plan with every neighbouring rank
+    neigh = sorted({int(owner[h]) for h in halo})
+    recv_ptr = [0]
+    for q in neigh:
+        recv_ptr.append(recv_ptr[-1] + int(np.sum(owner[halo] == q)))
+    send_ptr, send_idx = [0], []
+    for q in neigh:
+        # points of mine in rank q's halo, in global order (= q's halo order)
+        qa, qb = rank_ptr[q], rank_ptr[q + 1]
+        q_e = ((e[:, 0] >= qa) & (e[:, 0] < qb)) | ((e[:, 1] >= qa) & (e[:, 1] < qb))
+        qe = np.unique(e[q_e].ravel())
+        mine = qe[(qe >= g0) & (qe < g1)]
+        send_idx.extend((mine - g0).tolist())
+        send_ptr.append(len(send_idx))
+    lpp = pp[pr[rank][0]:pr[rank][-1] + 2] - g0
+    return dict(edges=le, edge_normal=ln, coord=np.asarray(mesh["coord"])[l2g],
+                volume=np.asarray(mesh["volume"])[l2g], nbr_ptr=nptr_l, nbr=nbr_l.astype(np.int64), bvertex=lbv,
+                bvertex_normal=np.asarray(mesh["bvertex_normal"])[keep], part_ptr=lpp.astype(np.int64),
+                n_domain=n_own, l2g=l2g, neigh=np.asarray(neigh, dtype=np.int32),
+                send_ptr=np.asarray(send_ptr, dtype=np.int64), send_idx=np.asarray(send_idx, dtype=np.int64),
+                recv_ptr=np.asarray(recv_ptr, dtype=np.int64), rank_ptr=rank_ptr)

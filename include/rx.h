@@ -48,7 +48,8 @@ typedef enum {
   RX_ERR_RANGE = 4,
   RX_ERR_NONPHYS = 5,
   RX_ERR_DIVERGED = 6,
-  RX_ERR_STATE = 7
+  RX_ERR_STATE = 7,
+  RX_ERR_COMM = 8     /* RCCL error */
 } rx_status;
 
 typedef struct rx_ctx rx_ctx;
@@ -85,6 +86,17 @@ typedef struct {
    * LU-SGS's backward sweep reads halo x*). n_part = 0 or part_ptr = NULL: one partition. */
   int64_t n_part;
   const int64_t *part_ptr;   /* [n_part+1] */
+  /* Distributed mesh (one rank per GPU, geometry_structure.cpp:11465-11530 partitioning): the first
+   * n_domain points are owned, the rest are halo points grouped by owning rank. n_neigh neighbour
+   * ranks; to neighbour k this rank sends its points send_idx[send_ptr[k]..send_ptr[k+1]) and
+   * receives halo points n_domain + recv_ptr[k] .. n_domain + recv_ptr[k+1]. n_domain = 0: all
+   * points are owned (single rank). Partitions must then cover exactly [0, n_domain). */
+  int64_t n_domain;
+  int32_t n_neigh;
+  const int32_t *neigh;      /* [n_neigh] ranks */
+  const int64_t *send_ptr;   /* [n_neigh+1] */
+  const int64_t *send_idx;   /* [send_ptr[n_neigh]] local owned point ids */
+  const int64_t *recv_ptr;   /* [n_neigh+1] offsets into the halo block */
 } rx_mesh_desc;
 
 typedef struct {
@@ -136,6 +148,33 @@ int rx_ilu0_build(rx_ctx *ctx);
 int rx_ilu0_apply(rx_ctx *ctx, rx_field b, rx_field x);
 int rx_lusgs_apply(rx_ctx *ctx, rx_field b, rx_field x);
 int rx_fgmres(rx_ctx *ctx, double tol, int m, int *iters, double *resid); /* solves JAC * SOL = RHS */
+
+/* Multi-GPU (RCCL over xGMI). rx_comm_unique_id on one rank, broadcast the 128 bytes, then
+ * rx_comm_init on every rank. With a communicator the context exchanges halo values where the
+ * reference calls SendReceive / Set_MPI_* (after the gradient and the limiter, before every SpMV,
+ * the LU-SGS halo x*) and all-reduces every FGMRES inner product and the RMS. */
+int rx_comm_unique_id(void *id128);
+int rx_comm_init(rx_ctx *ctx, int nranks, int rank, const void *id128);
+
+/* Host-staged transport: the reference's own MPI pattern (CSysMatrix::SendReceive_Solution,
+ * Common/src/matrix_structure.cpp:794-880, point-to-point host buffers; dotProd's MPI_Allreduce,
+ * Common/src/vector_structure.cpp:397-419). Halo values and inner products are staged through pinned
+ * host memory and handed to the caller's transport (MPI, gloo, ...). Synchronous: a context with a
+ * host transport runs its solve eagerly (no graph).
+ *   sendrecv: for every neighbour k, send points [send_ptr[k], send_ptr[k+1]) of `send` (stride
+ *             doubles each) to rank neigh[k] and receive points [recv_ptr[k], recv_ptr[k+1]) of
+ *             `recv` from it.
+ *   allreduce: out[i] = sum over ranks of in[i], i < count (in == out allowed).
+ * Both return 0 on success. */
+typedef struct {
+  void *user;
+  int (*sendrecv)(void *user, int32_t n_neigh, const int32_t *neigh, const int64_t *send_ptr, const double *send,
+                  const int64_t *recv_ptr, double *recv, int32_t stride);
+  int (*allreduce)(void *user, const double *in, double *out, int32_t count);
+} rx_host_comm;
+int rx_comm_init_host(rx_ctx *ctx, int nranks, int rank, const rx_host_comm *ops);
+
+int rx_halo_exchange(rx_ctx *ctx, rx_field f); /* owned -> halo copies of a node field */
 
 /* Time integration (updates RX_F_U). */
 int rx_explicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */);

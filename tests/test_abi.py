@@ -27,3 +27,26 @@ def test_gfx950_code_object_present():
         rx.build()
     data = open(rx.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_ctypes_structs_match_header_layout(tmp_path):
+    """The Python mirror's structs have the C header's field offsets (gcc on include/rx.h)."""
+    import subprocess
+    structs = {"rx_mesh_desc": rx.MeshDesc, "rx_host_comm": rx.HostComm, "rx_cfg": rx.Cfg}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rx.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    inc = os.path.dirname(rx.HEADER)
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)

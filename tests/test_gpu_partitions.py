@@ -126,4 +126,8 @@ def test_implicit_step_vs_oracle(n_part):
     s.Source_Residual()
     rms2, it2 = s.ImplicitEuler_Iteration()
     assert it2 == it and np.all(np.isfinite(rms2))
+    # the node records did not change, so the replayed solve is the same linear system: same
+    # solution bitwise (no state may leak from one solve into the next)
+    assert np.array_equal(rms2, rms)
+    assert np.array_equal(s.download("SOL"), sol.ravel())
     s.close()

@@ -1,0 +1,139 @@
+"""Distributed path on the device: one context per rank, halo exchange + all-reduced inner products
+(include/rx.h rx_comm_init / rx_comm_init_host). Requires an MI355X.
+
+- World size 1 with an RCCL communicator: the all-reduce path of FGMRES (rank-local sums -> landing
+  slots) and the RCCL calls inside the captured solve graph give bitwise the single-context result.
+- World size 2 on the one GPU of the test box (RCCL refuses two ranks on one device, so the ranks use
+  the host-staged transport over gloo, the reference's own MPI pattern): gradients are bitwise the
+  global ones on every local row (owned rows recomputed in the same neighbour order, halo rows
+  received from their owner); one implicit step agrees with the single-context run on the same
+  partitions to the FGMRES bar (edge order differs per rank, so fluxes agree to rounding).
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from tests.parity import assert_close, per_column_close
+from tests.rxpkg import meshgen, rx, synth
+
+pytestmark = pytest.mark.gpu
+
+NX, NY, NPART, NS = 48, 20, 8, 7
+
+
+def _case():
+    mesh, st, mech_arrays, kw = synth.jet_case(NX, NY, n_species=NS, n_part=NPART)
+    cfg = rx.default_cfg(implicit=1, lin_prec=1, cfl=5.0, max_delta_time=1e6, prandtl_lam=0.72,
+                         prandtl_turb=kw["prandtl_turb"], lewis_turb=kw["lewis_turb"], mach_inf=kw["mach_inf"],
+                         c_mu=kw["c_mu"], pasr_lb=kw["pasr_lb"], lin_tol=1e-6, lin_iter=5, relaxation=1.0)
+    return mesh, st, mech_arrays, cfg
+
+
+def _step(s):
+    s.SetPrimitive_Gradient_LS()
+    grad = s.download("GRAD")
+    s.SetTime_Step()
+    s.Preprocessing_zero()
+    s.Upwind_Residual()
+    s.Viscous_Residual()
+    s.Source_Residual()
+    rms, it = s.ImplicitEuler_Iteration()
+    return grad, rms, it
+
+
+def _global_run():
+    mesh, st, mech_arrays, cfg = _case()
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg)
+    s.set_state(st)
+    U0 = s.download("U")
+    grad, rms, it = _step(s)
+    U = s.download("U")
+    s.close()
+    return grad, rms, it, U0, U
+
+
+def test_rccl_world1_matches_single_context():
+    g0, rms0, it0, _, U0 = _global_run()
+    mesh, st, mech_arrays, cfg = _case()
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg)
+    s.comm_init(1, 0, rx.comm_unique_id())
+    s.set_state(st)
+    for rep in range(2):  # second step replays the captured graph with the collectives in it
+        s.set_state(st)
+        g, rms, it = _step(s)
+        U = s.download("U")
+        assert it == it0
+        assert np.array_equal(g, g0)
+        assert np.array_equal(rms, rms0), f"rep {rep}"
+        assert np.array_equal(U, U0), f"rep {rep}"
+    s.close()
+
+
+def _rank_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mesh, st, mech_arrays, cfg = _case()
+        sh = meshgen.shard(mesh, world, rank)
+        st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
+        s = rx.ReactiveNSSolver(sh, rx.Mechanism(mech_arrays), cfg)
+        s.comm_init_host(world, rank, rx.TorchHostTransport())
+        s.set_state(st_l)
+        grad, rms, it = _step(s)
+        U = s.download("U")
+        s.close()
+        q.put((rank, dict(l2g=sh["l2g"], nd=sh["n_domain"], grad=grad, rms=rms, it=it, U=U)))
+    except Exception as e:  # reported to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_host_transport_match_single_context():
+    g0, rms0, it0, U_init, U0 = _global_run()
+    nvar = NS + 4
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        res = dict(q.get(timeout=600) for _ in ps)
+    finally:
+        for p in ps:
+            p.join(timeout=120)
+    for r in range(2):
+        assert isinstance(res[r], dict), res[r]
+    g0 = g0.reshape(len(U0) // nvar, -1)
+    U0 = U0.reshape(-1, nvar)
+    U_init = U_init.reshape(-1, nvar)
+    U_sh = np.zeros_like(U0)
+    for r in range(2):
+        d = res[r]
+        l2g, nd = d["l2g"], d["nd"]
+        assert d["it"] == it0
+        # every local row (owned recomputed, halo received) equals the global gradient
+        assert np.array_equal(d["grad"].reshape(len(l2g), -1), g0[l2g])
+        # the all-reduced RMS is the same number on every rank
+        assert np.array_equal(d["rms"], res[0]["rms"])
+        U_l = d["U"].reshape(len(l2g), nvar)
+        U_sh[l2g[:nd]] = U_l[:nd]
+        # halo rows of U hold the owner's updated values after Set_MPI_Solution
+        U_sh_halo = U_l[nd:]
+        res[r]["halo"] = (l2g[nd:], U_sh_halo)
+    for r in range(2):
+        hg, hv = res[r]["halo"]
+        assert np.array_equal(hv, U_sh[hg])
+    assert_close(res[0]["rms"], rms0, rtol=1e-10, what="RMS (two ranks vs one context)")
+    # Each rank orders its local edges by local ids (halo points last), as the reference's partitioned
+    # CGeometry does, so residual/Jacobian sums round differently from the one-context run (RMS above
+    # agrees to 1e-10); FGMRES(5)+ILU(0) amplifies that to ~1e-8 in the update (measured 1.1e-8).
+    per_column_close(U_sh - U_init, U0 - U_init, rtol=5e-8, floor=1e-14, what="dU (two ranks vs one context)")
