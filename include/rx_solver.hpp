@@ -76,6 +76,15 @@ class ReactiveNSSolver {
   }
   void Synchronize() { check(rx_sync(ctx_), "rx_sync"); }
 
+  // ---- distributed (one rank per GPU): RCCL communicator or host-staged transport (rx.h)
+  void CommInit(int nranks, int rank, const void* unique_id128) {
+    check(rx_comm_init(ctx_, nranks, rank, unique_id128), "rx_comm_init");
+  }
+  void CommInitHost(int nranks, int rank, const rx_host_comm& ops) {
+    check(rx_comm_init_host(ctx_, nranks, rank, &ops), "rx_comm_init_host");
+  }
+  void HaloExchange(rx_field f) { check(rx_halo_exchange(ctx_, f), "rx_halo_exchange"); }
+
  private:
   void phase(int rc, const char* nan_msg) {
     if (rc == RX_OK) rc = rx_sync(ctx_);
