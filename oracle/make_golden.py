@@ -178,6 +178,11 @@ def case_mini9(nx=21, ny=11):
     b = run_harness(wd, bsr=True)
     for k in ("ilu_factor", "ilu_rhs", "fgmres_ilu_x", "fgmres_ilu_info"):
         a[k] = b[k]
+    # the SST implicit step solved with ILU0 (same system, other preconditioner)
+    assert np.array_equal(a["sst_bsr_system"], b["sst_bsr_system"])
+    for k in ("sst_lin_sol", "sst_new_sol", "sst_rms", "sst_post_mut", "sst_post_F1", "sst_post_F2",
+              "sst_post_CDkw", "sst_post_grad"):
+        a[k + "_ilu"] = b[k]
     assert np.array_equal(a["bsr_system"], b["bsr_system"])
     # keep the fixture small: the assembled system + ILU factor stay whole, per-edge Jacobians are
     # sampled (the whole-matrix assembly is checked against bsr_system)
@@ -220,7 +225,9 @@ def case_jet9w():
     out = {}
     node_keys = ["coord", "volume", "global_index", "U", "V", "dPdU", "dTdU", "mu", "kappa", "cp", "Dij",
                  "grad_prim", "limiter", "turb_k", "turb_omega", "mu_t", "sigma_k", "grad_k", "src_res",
-                 "src_jac", "limiter_out", "grad_lsq_out", "wall_distance"]
+                 "src_jac", "limiter_out", "grad_lsq_out", "wall_distance",
+                 "eddy_visc_flow", "sst_sol", "sst_grad", "sst_F1", "sst_F2", "sst_CDkw", "strain_mag",
+                 "sst_src_res", "sst_src_jac"]
     for k in node_keys:
         out[k] = a[k][keep]
     out["interior"] = interior
@@ -234,7 +241,8 @@ def case_jet9w():
     out["nbr"] = np.array(ln, dtype=np.int64)
     out["edges"] = loc[e[ekeep]]
     out["edge_normal"] = a["edge_normal"][ekeep]
-    for k in ("conv_res", "visc_res"):
+    for k in ("conv_res", "visc_res", "sst_upw_res", "sst_upw_jac_i", "sst_upw_jac_j", "sst_visc_res",
+              "sst_visc_jac_i", "sst_visc_jac_j"):
         out[k] = a[k][ekeep]
     rng = np.random.default_rng(12345)
     js = np.sort(rng.choice(len(ekeep), size=min(256, len(ekeep)), replace=False))

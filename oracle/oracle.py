@@ -307,3 +307,118 @@ def implicit_step(mech, nDim, ns, mesh, st, cfg, pattern=None, part_ptr=None):
     x, it, res = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"], part_ptr=part_ptr)
     U = update(st["U"], x, nDim, 0, cfg["relaxation"], mesh["volume"], dt)
     return U, dict(grad=G, dt=dt, res=R, jac=A, rhs=rhs, sol=x, lin_iters=it, lin_resid=res)
+
+
+# ---- a14 + next-2: Menter SST turbulence solver (rx_oracle.cpp, "a14 + next-2" section) ----------
+
+def _f(x):
+    return x.ctypes.data_as(C.c_void_p)
+
+
+@_keepalive
+def sol_grad_ls(nDim, coord, sol, nbr_ptr, nbr):
+    """CSolver::SetSolution_Gradient_LS (solver_structure.cpp:580-720) of an [N][nVar] solution."""
+    sol = np.ascontiguousarray(sol, dtype=np.float64)
+    N, nv = sol.shape
+    g = np.zeros((N, nv, nDim))
+    lib().orc_sol_grad_ls(C.c_int(nDim), C.c_int(nv), C.c_int64(N), _p(coord), _p(sol), _p(nbr_ptr, np.int64),
+                          _p(nbr, np.int64), _f(g))
+    return g
+
+
+@_keepalive
+def strain_mag(nDim, G):
+    """CReactiveNSVariable::SetStrainMag (variable_direct_reactive.cpp:1060-1095)."""
+    G = np.ascontiguousarray(G, dtype=np.float64)
+    out = np.zeros(len(G))
+    lib().orc_strain_mag(C.c_int(nDim), C.c_int(G.shape[1]), C.c_int64(len(G)), _p(G), _f(out))
+    return out
+
+
+@_keepalive
+def sst_blending(nDim, T, TG, rho, mu, dist, strain):
+    """SetBlendingFunc + mu_t of CTurbSSTSolver::Postprocessing -> (F1, F2, CDkw, muT)."""
+    N = len(T)
+    F1, F2, CD, mt = (np.zeros(N) for _ in range(4))
+    lib().orc_sst_blending(C.c_int(nDim), C.c_int64(N), _p(T), _p(TG), _p(rho), _p(mu), _p(dist), _p(strain),
+                           _f(F1), _f(F2), _f(CD), _f(mt))
+    return F1, F2, CD, mt
+
+
+@_keepalive
+def sst_upwind(nDim, edges, normal, V, T):
+    E = len(edges)
+    res, Ji, Jj = np.zeros((E, 2)), np.zeros((E, 2, 2)), np.zeros((E, 2, 2))
+    lib().orc_sst_upwind(C.c_int(nDim), C.c_int(V.shape[1]), C.c_int64(E), _p(edges, np.int64), _p(normal), _p(V),
+                         _p(T), _f(res), _f(Ji), _f(Jj))
+    return res, Ji, Jj
+
+
+@_keepalive
+def sst_visc(nDim, edges, normal, coord, V, T, TG, F1, mu, eddy):
+    E = len(edges)
+    res, Ji, Jj = np.zeros((E, 2)), np.zeros((E, 2, 2)), np.zeros((E, 2, 2))
+    lib().orc_sst_visc(C.c_int(nDim), C.c_int(V.shape[1]), C.c_int64(E), _p(edges, np.int64), _p(normal),
+                       _p(coord), _p(V), _p(T), _p(TG), _p(F1), _p(mu), _p(eddy), _f(res), _f(Ji), _f(Jj))
+    return res, Ji, Jj
+
+
+@_keepalive
+def sst_source(nDim, V, G, T, vol, dist, F1, F2, CDkw, strain, eddy):
+    N = len(V)
+    res, J = np.zeros((N, 2)), np.zeros((N, 2, 2))
+    lib().orc_sst_source(C.c_int(nDim), C.c_int(V.shape[1]), C.c_int(G.shape[1]), C.c_int64(N), _p(V), _p(G), _p(T),
+                         _p(vol), _p(dist), _p(F1), _p(F2), _p(CDkw), _p(strain), _p(eddy), _f(res), _f(J))
+    return res, J
+
+
+@_keepalive
+def sst_assemble(rp, col, edges, Fu, Jui, Juj, Fv, Jvi, Jvj, Rs, Js, vol, dt, cfl_red):
+    N, E = len(rp) - 1, len(edges)
+    R, rhs = np.zeros(N * 2), np.zeros(N * 2)
+    A = np.zeros(int(rp[-1]) * 4) if Jui is not None else None
+    lib().orc_sst_assemble(C.c_int64(N), C.c_int64(E), _p(edges, np.int64), _p(rp, np.int64), _p(col, np.int64),
+                           _p(Fu), _p(Jui), _p(Juj), _p(Fv), _p(Jvi), _p(Jvj), _p(Rs), _p(Js), _p(vol), _p(dt),
+                           C.c_double(cfl_red), _f(R), _f(A) if A is not None else None, _f(rhs))
+    return R.reshape(N, 2), (A.reshape(-1, 2, 2) if A is not None else None), rhs.reshape(N, 2)
+
+
+@_keepalive
+def sst_update(T, x, relax, rho, rho_old):
+    T = np.ascontiguousarray(T, dtype=np.float64).copy()
+    lib().orc_sst_update(C.c_int64(len(T)), _p(x), C.c_double(relax), _p(rho), _p(rho_old), _f(T))
+    return T
+
+
+def sst_step(nDim, mesh, flow, T, TG, F1, F2, CDkw, dt, cfg, pattern=None, part_ptr=None, prec="ilu"):
+    """One iteration of the SST solver after the flow's (CSingleGridIntegration::SingleGrid_Iteration,
+    integration_time.cpp:777-810): Preprocessing (zero + LS gradient of (k, omega)), upwind / viscous /
+    source residuals with Jacobians, ImplicitEuler_Iteration (system, preconditioned FGMRES, conservative
+    clipped update, RMS), Postprocessing (gradient, blending, mu_t).
+    flow: dict with V, grad (flow primitive gradient), mu, eddy (flow eddy viscosity), strain.
+    Returns (T_new, info)."""
+    N = len(T)
+    rp, col = pattern if pattern is not None else bsr_pattern(N, mesh["edges"])
+    V = flow["V"]
+    rho = np.ascontiguousarray(V[:, nDim + 2])
+    TG0 = sol_grad_ls(nDim, mesh["coord"], T, mesh["nbr_ptr"], mesh["nbr"])
+    ru, Jui, Juj = sst_upwind(nDim, mesh["edges"], mesh["edge_normal"], V, T)
+    rv, Jvi, Jvj = sst_visc(nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], V, T, TG0, F1, flow["mu"],
+                            flow["eddy"])
+    rs, Js = sst_source(nDim, V, flow["grad"], T, mesh["volume"], mesh["wall_distance"], F1, F2, CDkw,
+                        flow["strain"], flow["eddy"])
+    R, A, rhs = sst_assemble(rp, col, mesh["edges"], ru, Jui, Juj, rv, Jvi, Jvj, rs, Js, mesh["volume"], dt,
+                             cfg.get("cfl_red_turb", 1.0))
+    if prec == "ilu":
+        F = ilu_build(rp, col, A, part_ptr)
+        x, it, res = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                            part_ptr=part_ptr)
+    else:
+        x, it, res = fgmres(rp, col, A, rhs.ravel(), "lusgs", tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                            part_ptr=part_ptr)
+    Tn = sst_update(T, x.ravel(), cfg.get("relaxation_turb", 1.0), rho, rho)
+    rms = np.maximum(1e-32, np.sqrt(np.sum(rhs * rhs, axis=0) / N))
+    TG1 = sol_grad_ls(nDim, mesh["coord"], Tn, mesh["nbr_ptr"], mesh["nbr"])
+    F1n, F2n, CDn, mut = sst_blending(nDim, Tn, TG1, rho, flow["mu"], mesh["wall_distance"], flow["strain"])
+    return Tn, dict(grad_pre=TG0, res=R, jac=A, rhs=rhs, sol=x, lin_iters=it, lin_resid=res, rms=rms, grad=TG1,
+                    F1=F1n, F2=F2n, CDkw=CDn, mut=mut)

@@ -356,6 +356,94 @@ int main(int argc, char** argv) {
     dumpd("src_params", prm, {5});
   }
 
+  // ---- SST turbulence operators (a14): the turbulent solver's own numerics on the same state.
+  //      Per-edge setters as CTurbSolver::Upwind_Residual / Viscous_Residual
+  //      (solver_direct_turbulent.cpp:429-600), per-node as CTurbSSTSolver::Source_Residual (:3018-3080).
+  double** Ti = alloc2(2);
+  double** Tj = alloc2(2);
+  if (rans) {
+    std::vector<double> tg(nPoint * 2 * nDim), f1(nPoint), f2(nPoint), cd(nPoint), sm(nPoint), ts(nPoint * 2);
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      su2double** g = turb->node[i]->GetGradient();
+      for (unsigned short v = 0; v < 2; ++v)
+        for (unsigned short d = 0; d < nDim; ++d) tg[(i * 2 + v) * nDim + d] = g[v][d];
+      f1[i] = turb->node[i]->GetF1blending();
+      f2[i] = turb->node[i]->GetF2blending();
+      cd[i] = turb->node[i]->GetCrossDiff();
+      sm[i] = flow->node[i]->GetStrainMag();
+      ts[2 * i] = turb->node[i]->GetSolution(0);
+      ts[2 * i + 1] = turb->node[i]->GetSolution(1);
+    }
+    dumpd("sst_sol", ts, {(long)nPoint, 2});
+    dumpd("sst_grad", tg, {(long)nPoint, 2, nDim});
+    dumpd("sst_F1", f1, {(long)nPoint});
+    dumpd("sst_F2", f2, {(long)nPoint});
+    dumpd("sst_CDkw", cd, {(long)nPoint});
+    dumpd("strain_mag", sm, {(long)nPoint});
+
+    CNumerics* tconv = drv.num(TURB_SOL, CONV_TERM);
+    CNumerics* tvisc = drv.num(TURB_SOL, VISC_TERM);
+    CNumerics* tsrc = drv.num(TURB_SOL, SOURCE_FIRST_TERM);
+    std::vector<double> ur(nEdge * 2), uji(nEdge * 4), ujj(nEdge * 4), vr(nEdge * 2), vji(nEdge * 4), vjj(nEdge * 4);
+    double r[8];
+    auto put = [&](std::vector<double>& dst, size_t at, double** J) {
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) dst[at * 4 + a * 2 + b] = J[a][b];
+    };
+    for (unsigned long e = 0; e < nEdge; ++e) {
+      unsigned long i = geo->edge[e]->GetNode(0), j = geo->edge[e]->GetNode(1);
+      tconv->SetNormal(geo->edge[e]->GetNormal());
+      tconv->SetPrimitive(flow->node[i]->GetPrimitive(), flow->node[j]->GetPrimitive());
+      tconv->SetTurbVar(turb->node[i]->GetSolution(), turb->node[j]->GetSolution());
+      tconv->ComputeResidual(r, Ti, Tj, cfg);
+      ur[2 * e] = r[0];
+      ur[2 * e + 1] = r[1];
+      put(uji, e, Ti);
+      put(ujj, e, Tj);
+      tvisc->SetCoord(geo->node[i]->GetCoord(), geo->node[j]->GetCoord());
+      tvisc->SetNormal(geo->edge[e]->GetNormal());
+      tvisc->SetPrimitive(flow->node[i]->GetPrimitive(), flow->node[j]->GetPrimitive());
+      tvisc->SetTurbVar(turb->node[i]->GetSolution(), turb->node[j]->GetSolution());
+      tvisc->SetTurbVarGradient(turb->node[i]->GetGradient(), turb->node[j]->GetGradient());
+      tvisc->SetF1blending(turb->node[i]->GetF1blending(), turb->node[j]->GetF1blending());
+      tvisc->SetLaminarViscosity(flow->node[i]->GetLaminarViscosity(), flow->node[j]->GetLaminarViscosity());
+      tvisc->SetEddyViscosity(flow->node[i]->GetEddyViscosity(), flow->node[j]->GetEddyViscosity());
+      tvisc->ComputeResidual(r, Ti, Tj, cfg);
+      vr[2 * e] = r[0];
+      vr[2 * e + 1] = r[1];
+      put(vji, e, Ti);
+      put(vjj, e, Tj);
+    }
+    dumpd("sst_upw_res", ur, {(long)nEdge, 2});
+    dumpd("sst_upw_jac_i", uji, {(long)nEdge, 2, 2});
+    dumpd("sst_upw_jac_j", ujj, {(long)nEdge, 2, 2});
+    dumpd("sst_visc_res", vr, {(long)nEdge, 2});
+    dumpd("sst_visc_jac_i", vji, {(long)nEdge, 2, 2});
+    dumpd("sst_visc_jac_j", vjj, {(long)nEdge, 2, 2});
+    std::vector<double> sr(nPoint * 2), sj(nPoint * 4);
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      tsrc->SetPrimitive(flow->node[i]->GetPrimitive(), NULL);
+      tsrc->SetPrimVarGradient(flow->node[i]->GetGradient_Primitive(), NULL);
+      tsrc->SetTurbVar(turb->node[i]->GetSolution(), NULL);
+      tsrc->SetTurbVarGradient(turb->node[i]->GetGradient(), NULL);
+      tsrc->SetVolume(geo->node[i]->GetVolume());
+      tsrc->SetDistance(geo->node[i]->GetWall_Distance(), 0.0);
+      tsrc->SetF1blending(turb->node[i]->GetF1blending(), 0.0);
+      tsrc->SetF2blending(turb->node[i]->GetF2blending(), 0.0);
+      tsrc->SetVorticity(flow->node[i]->GetVorticity(), NULL);
+      tsrc->SetStrainMag(flow->node[i]->GetStrainMag(), 0.0);
+      tsrc->SetCrossDiff(turb->node[i]->GetCrossDiff(), 0.0);
+      tsrc->SetLaminarViscosity(flow->node[i]->GetLaminarViscosity(), flow->node[i]->GetLaminarViscosity());
+      tsrc->SetEddyViscosity(flow->node[i]->GetEddyViscosity(), flow->node[i]->GetEddyViscosity());
+      tsrc->ComputeResidual(r, Ti, NULL, cfg);
+      sr[2 * i] = r[0];
+      sr[2 * i + 1] = r[1];
+      put(sj, i, Ti);
+    }
+    dumpd("sst_src_res", sr, {(long)nPoint, 2});
+    dumpd("sst_src_jac", sj, {(long)nPoint, 2, 2});
+  }
+
   // ---- LSQ gradient recomputed by the reference (solver_direct_reactive.cpp:4887-5050)
   {
     CReactiveNSSolver* ns = dynamic_cast<CReactiveNSSolver*>(flow);
@@ -486,6 +574,85 @@ int main(int argc, char** argv) {
       dumpd("fgmres_ilu_x", yy, {(long)nPoint, nVar});
       std::vector<double> info = {(double)it2, resid, tol, (double)m};
       dumpd("fgmres_ilu_info", info, {4});
+      }
+    }
+    // ---- SST loops and the turbulent implicit step (CTurbSSTSolver::Preprocessing :2923-2946,
+    //      CTurbSolver::Upwind/Viscous_Residual :429-600, Source_Residual :3018-3080,
+    //      CTurbSolver::ImplicitEuler_Iteration :615-728, CTurbSSTSolver::Postprocessing :2948-3016)
+    if (rans) {
+      CNumerics* tconv = drv.num(TURB_SOL, CONV_TERM);
+      CNumerics* tvisc = drv.num(TURB_SOL, VISC_TERM);
+      CNumerics* tsrc = drv.num(TURB_SOL, SOURCE_FIRST_TERM);
+      CNumerics* tsrc2 = drv.num(TURB_SOL, SOURCE_SECOND_TERM);
+      CSysVector& TR = turb->LinSysRes;
+      auto dump_tres = [&](const std::string& name) {
+        std::vector<double> rr(nPoint * 2);
+        for (unsigned long i = 0; i < nPoint * 2; ++i) rr[i] = TR[i];
+        dumpd(name, rr, {(long)nPoint, 2});
+      };
+      turb->Preprocessing(geo, sc, cfg, MESH_0, 0, RUNTIME_TURB_SYS, false);
+      {
+        std::vector<double> tg(nPoint * 2 * nDim);
+        for (unsigned long i = 0; i < nPoint; ++i)
+          for (unsigned short v = 0; v < 2; ++v)
+            for (unsigned short d = 0; d < nDim; ++d) tg[(i * 2 + v) * nDim + d] = turb->node[i]->GetGradient()[v][d];
+        dumpd("sst_grad_ls", tg, {(long)nPoint, 2, nDim});
+      }
+      turb->Upwind_Residual(geo, sc, tconv, cfg, MESH_0);
+      dump_tres("sst_loop_upw_res");
+      turb->Viscous_Residual(geo, sc, tvisc, cfg, MESH_0, NO_RK_ITER);
+      dump_tres("sst_loop_upw_visc_res");
+      turb->Source_Residual(geo, sc, tsrc, tsrc2, cfg, MESH_0);
+      dump_tres("sst_loop_total_res");
+      if (implicit) {
+        CSysMatrix& TA = turb->Jacobian;
+        std::vector<int64_t> trp(nPoint + 1, 0), tcol;
+        for (unsigned long i = 0; i < nPoint; ++i) {
+          std::vector<unsigned long> cols;
+          cols.push_back(i);
+          for (unsigned short k = 0; k < geo->node[i]->GetnPoint(); ++k) cols.push_back(geo->node[i]->GetPoint(k));
+          std::sort(cols.begin(), cols.end());
+          for (auto c : cols) tcol.push_back(c);
+          trp[i + 1] = tcol.size();
+        }
+        auto dump_tbsr = [&](const std::string& name) {
+          std::vector<double> blocks(tcol.size() * 4);
+          for (unsigned long i = 0; i < nPoint; ++i)
+            for (int64_t k = trp[i]; k < trp[i + 1]; ++k) {
+              su2double* b = TA.GetBlock(i, tcol[k]);
+              for (int q = 0; q < 4; ++q) blocks[k * 4 + q] = b[q];
+            }
+          dumpd(name, blocks, {(long)tcol.size(), 2, 2});
+        };
+        dump_tbsr("sst_bsr_jac_residual");
+        turb->ImplicitEuler_Iteration(geo, sc, cfg);
+        dump_tbsr("sst_bsr_system");
+        dump_tres("sst_sys_rhs");
+        std::vector<double> xs(nPoint * 2), ns2(nPoint * 2);
+        for (unsigned long i = 0; i < nPoint * 2; ++i) xs[i] = turb->LinSysSol[i];
+        for (unsigned long i = 0; i < nPoint; ++i) {
+          ns2[2 * i] = turb->node[i]->GetSolution(0);
+          ns2[2 * i + 1] = turb->node[i]->GetSolution(1);
+        }
+        dumpd("sst_lin_sol", xs, {(long)nPoint, 2});
+        dumpd("sst_new_sol", ns2, {(long)nPoint, 2});
+        std::vector<double> rms = {turb->GetRes_RMS(0), turb->GetRes_RMS(1)};
+        dumpd("sst_rms", rms, {2});
+        turb->Postprocessing(geo, sc, cfg, MESH_0);
+        std::vector<double> mt(nPoint), f1(nPoint), f2(nPoint), cd(nPoint), tg(nPoint * 2 * nDim);
+        for (unsigned long i = 0; i < nPoint; ++i) {
+          mt[i] = turb->node[i]->GetmuT();
+          f1[i] = turb->node[i]->GetF1blending();
+          f2[i] = turb->node[i]->GetF2blending();
+          cd[i] = turb->node[i]->GetCrossDiff();
+          for (unsigned short v = 0; v < 2; ++v)
+            for (unsigned short d = 0; d < nDim; ++d) tg[(i * 2 + v) * nDim + d] = turb->node[i]->GetGradient()[v][d];
+        }
+        dumpd("sst_post_mut", mt, {(long)nPoint});
+        dumpd("sst_post_F1", f1, {(long)nPoint});
+        dumpd("sst_post_F2", f2, {(long)nPoint});
+        dumpd("sst_post_CDkw", cd, {(long)nPoint});
+        dumpd("sst_post_grad", tg, {(long)nPoint, 2, nDim});
       }
     }
   }

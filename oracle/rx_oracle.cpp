@@ -1848,4 +1848,328 @@ void orc_update(int64_t N, int nb, int nDim, int mode, const double* d, double r
     }
 }
 
+// =================================================================================================
+// a14 + next-2: Menter SST turbulence solver on the flow state (CTurbSSTSolver / CTurbSolver,
+// SU2_CFD/src/solver_direct_turbulent.cpp; numerics SU2_CFD/src/numerics_direct_turbulent.cpp;
+// node record CTurbSSTVariable SU2_CFD/src/variable_direct_turbulent.cpp). Turbulent solution
+// T[N][2] = (k, omega); std::min/std::max are restated as the ternaries they are.
+// =================================================================================================
+struct SSTConst {
+  double sk1, sk2, so1, so2, b1, b2, bs, a1, al1, al2;
+};
+// CTurbSSTSolver constructor, solver_direct_turbulent.cpp:2716-2725
+static SSTConst sst_const() {
+  SSTConst c;
+  c.sk1 = 0.85;
+  c.sk2 = 1.0;
+  c.so1 = 0.5;
+  c.so2 = 0.856;
+  c.b1 = 0.075;
+  c.b2 = 0.0828;
+  c.bs = 0.09;
+  c.a1 = 0.31;
+  c.al1 = c.b1 / c.bs - c.so1 * 0.41 * 0.41 / std::sqrt(c.bs);
+  c.al2 = c.b2 / c.bs - c.so2 * 0.41 * 0.41 / std::sqrt(c.bs);
+  return c;
+}
+static inline double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+static inline double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+
+// CSolver::SetSolution_Gradient_LS (Common solver base, SU2_CFD/src/solver_structure.cpp:580-720)
+// for an nVar-component solution: weight != 0 test, r11 >= 0 / r11 != 0 guards, |detR2| <= EPS.
+void orc_sol_grad_ls(int nDim, int nVar, int64_t N, const double* coord, const double* sol, const int64_t* nptr,
+                     const int64_t* nbr, double* grad) {
+  double Cv[8][3];
+  for (int64_t i = 0; i < N; ++i) {
+    bool singular = false;
+    const double* ci = coord + i * nDim;
+    const double* si = sol + i * nVar;
+    for (int v = 0; v < nVar; ++v)
+      for (int d = 0; d < nDim; ++d) Cv[v][d] = 0.0;
+    double r11 = 0, r12 = 0, r13 = 0, r22 = 0, r23 = 0, r23_a = 0, r23_b = 0, r33 = 0;
+    for (int64_t k = nptr[i]; k < nptr[i + 1]; ++k) {
+      const int64_t j = nbr[k];
+      const double* cj = coord + j * nDim;
+      const double* sj = sol + j * nVar;
+      double w = 0.0;
+      for (int d = 0; d < nDim; ++d) w += (cj[d] - ci[d]) * (cj[d] - ci[d]);
+      if (w != 0.0) {
+        r11 += (cj[0] - ci[0]) * (cj[0] - ci[0]) / w;
+        r12 += (cj[0] - ci[0]) * (cj[1] - ci[1]) / w;
+        r22 += (cj[1] - ci[1]) * (cj[1] - ci[1]) / w;
+        if (nDim == 3) {
+          r13 += (cj[0] - ci[0]) * (cj[2] - ci[2]) / w;
+          r23_a += (cj[1] - ci[1]) * (cj[2] - ci[2]) / w;
+          r23_b += (cj[0] - ci[0]) * (cj[2] - ci[2]) / w;
+          r33 += (cj[2] - ci[2]) * (cj[2] - ci[2]) / w;
+        }
+        for (int v = 0; v < nVar; ++v)
+          for (int d = 0; d < nDim; ++d) Cv[v][d] += (cj[d] - ci[d]) * (sj[v] - si[v]) / w;
+      }
+    }
+    if (r11 >= 0.0) r11 = std::sqrt(r11); else r11 = 0.0;
+    if (r11 != 0.0) r12 = r12 / r11; else r12 = 0.0;
+    if (r22 - r12 * r12 >= 0.0) r22 = std::sqrt(r22 - r12 * r12); else r22 = 0.0;
+    if (nDim == 3) {
+      if (r11 != 0.0) r13 = r13 / r11; else r13 = 0.0;
+      if ((r22 != 0.0) && (r11 * r22 != 0.0)) r23 = r23_a / r22 - r23_b * r12 / (r11 * r22); else r23 = 0.0;
+      if (r33 - r23 * r23 - r13 * r13 >= 0.0) r33 = std::sqrt(r33 - r23 * r23 - r13 * r13); else r33 = 0.0;
+    }
+    double detR2 = (nDim == 2) ? (r11 * r22) * (r11 * r22) : (r11 * r22 * r33) * (r11 * r22 * r33);
+    if (std::fabs(detR2) <= EPS) {
+      detR2 = 1.0;
+      singular = true;
+    }
+    double S[3][3] = {{0}};
+    if (!singular) {
+      if (nDim == 2) {
+        S[0][0] = (r12 * r12 + r22 * r22) / detR2;
+        S[0][1] = -r11 * r12 / detR2;
+        S[1][0] = S[0][1];
+        S[1][1] = r11 * r11 / detR2;
+      } else {
+        const double z11 = r22 * r33, z12 = -r12 * r33, z13 = r12 * r23 - r13 * r22;
+        const double z22 = r11 * r33, z23 = -r11 * r23, z33 = r11 * r22;
+        S[0][0] = (z11 * z11 + z12 * z12 + z13 * z13) / detR2;
+        S[0][1] = (z12 * z22 + z13 * z23) / detR2;
+        S[0][2] = (z13 * z33) / detR2;
+        S[1][0] = S[0][1];
+        S[1][1] = (z22 * z22 + z23 * z23) / detR2;
+        S[1][2] = (z23 * z33) / detR2;
+        S[2][0] = S[0][2];
+        S[2][1] = S[1][2];
+        S[2][2] = (z33 * z33) / detR2;
+      }
+    }
+    for (int v = 0; v < nVar; ++v)
+      for (int d = 0; d < nDim; ++d) {
+        double product = 0.0;
+        for (int e = 0; e < nDim; ++e) product += S[d][e] * Cv[v][e];
+        grad[(i * nVar + v) * nDim + d] = product;
+      }
+  }
+}
+
+// CReactiveNSVariable::SetStrainMag (variable_direct_reactive.cpp:1060-1095) from the flow primitive
+// gradient G[N][nG][nDim] (rows 1..nDim = velocity).
+void orc_strain_mag(int nDim, int nG, int64_t N, const double* G, double* out) {
+  for (int64_t i = 0; i < N; ++i) {
+    const double* g = G + i * nG * nDim;
+    auto gr = [&](int v, int d) { return g[v * nDim + d]; };
+    double Div = 0.0;
+    for (int d = 0; d < nDim; ++d) Div += gr(d + 1, d);
+    double S = 0.0;
+    for (int d = 0; d < nDim; ++d) S += std::pow(gr(d + 1, d) - 1.0 / 3.0 * Div, 2.0);
+    S += 2.0 * std::pow(0.5 * (gr(1, 1) + gr(2, 0)), 2.0);
+    if (nDim == 3) {
+      S += 2.0 * std::pow(0.5 * (gr(1, 2) + gr(3, 0)), 2.0);
+      S += 2.0 * std::pow(0.5 * (gr(2, 2) + gr(3, 1)), 2.0);
+    }
+    out[i] = std::sqrt(2.0 * S);
+  }
+}
+
+// CTurbSSTSolver::Postprocessing (solver_direct_turbulent.cpp:2953-3000) after its gradient:
+// CTurbSSTVariable::SetBlendingFunc (variable_direct_turbulent.cpp:178-203) and mu_t.
+// rho, mu: flow density V[nDim+2] and laminar viscosity; strain: flow StrainMag.
+void orc_sst_blending(int nDim, int64_t N, const double* T, const double* TG, const double* rho, const double* mu,
+                      const double* dist, const double* strain, double* F1, double* F2, double* CDkw, double* muT) {
+  const SSTConst c = sst_const();
+  for (int64_t i = 0; i < N; ++i) {
+    const double* t = T + 2 * i;
+    const double* g = TG + i * 2 * nDim;
+    double cd = 0.0;
+    for (int d = 0; d < nDim; ++d) cd += g[d] * g[nDim + d];
+    cd *= 2.0 * rho[i] * c.so2 / t[1];
+    cd = smax(cd, std::pow(10.0, -20.0));
+    const double arg2A = std::sqrt(t[0]) / (c.bs * t[1] * dist[i] + EPS * EPS);
+    const double arg2B = 500.0 * mu[i] / (rho[i] * dist[i] * dist[i] * t[1] + EPS * EPS);
+    double arg2 = smax(arg2A, arg2B);
+    const double arg1 = smin(arg2, 4.0 * rho[i] * c.so2 * t[0] / (cd * dist[i] * dist[i] + EPS * EPS));
+    F1[i] = std::tanh(std::pow(arg1, 4.0));
+    arg2 = smax(2.0 * arg2A, arg2B);
+    F2[i] = std::tanh(std::pow(arg2, 2.0));
+    CDkw[i] = cd;
+    const double zeta = smin(1.0 / t[1], c.a1 / (strain[i] * F2[i]));
+    muT[i] = smin(smax(rho[i] * t[0] * zeta, 0.0), 1.0);
+  }
+}
+
+// CUpwSca_TurbSST::ComputeResidual (numerics_direct_turbulent.cpp:865-922), 1st order, fixed grid.
+void orc_sst_upwind(int nDim, int nPV, int64_t E, const int64_t* edges, const double* normal, const double* V,
+                    const double* T, double* res, double* Ji, double* Jj) {
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    const double* vi = V + i * nPV;
+    const double* vj = V + j * nPV;
+    const double* n = normal + e * nDim;
+    double q = 0.0;
+    for (int d = 0; d < nDim; ++d) q += 0.5 * (vi[d + 1] + vj[d + 1]) * n[d];
+    const double a0 = 0.5 * (q + std::fabs(q)), a1 = 0.5 * (q - std::fabs(q));
+    const double ri = vi[nDim + 2], rj = vj[nDim + 2];
+    res[2 * e] = a0 * ri * T[2 * i] + a1 * rj * T[2 * j];
+    res[2 * e + 1] = a0 * ri * T[2 * i + 1] + a1 * rj * T[2 * j + 1];
+    if (Ji) {
+      double* A = Ji + 4 * e;
+      double* B = Jj + 4 * e;
+      A[0] = a0; A[1] = 0.0; A[2] = 0.0; A[3] = a0;
+      B[0] = a1; B[1] = 0.0; B[2] = 0.0; B[3] = a1;
+    }
+  }
+}
+
+// CAvgGradCorrected_TurbSST::ComputeResidual (numerics_direct_turbulent.cpp:1080-1163) with the
+// setters of CTurbSolver::Viscous_Residual (solver_direct_turbulent.cpp:545-600): laminar and
+// eddy viscosity of the flow nodes, F1 of the turbulent nodes.
+void orc_sst_visc(int nDim, int nPV, int64_t E, const int64_t* edges, const double* normal, const double* coord,
+                  const double* V, const double* T, const double* TG, const double* F1, const double* mu,
+                  const double* eddy, double* res, double* Ji, double* Jj) {
+  const SSTConst c = sst_const();
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    const double* n = normal + e * nDim;
+    const double ri = V[i * nPV + nDim + 2], rj = V[j * nPV + nDim + 2];
+    const double ski = F1[i] * c.sk1 + (1.0 - F1[i]) * c.sk2;
+    const double skj = F1[j] * c.sk1 + (1.0 - F1[j]) * c.sk2;
+    const double soi = F1[i] * c.so1 + (1.0 - F1[i]) * c.so2;
+    const double soj = F1[j] * c.so1 + (1.0 - F1[j]) * c.so2;
+    const double dik = mu[i] + ski * eddy[i], djk = mu[j] + skj * eddy[j];
+    const double dio = mu[i] + soi * eddy[i], djo = mu[j] + soj * eddy[j];
+    const double dk = 0.5 * (dik + djk), dw = 0.5 * (dio + djo);
+    double ev[3], dist2 = 0.0, proj = 0.0;
+    for (int d = 0; d < nDim; ++d) {
+      ev[d] = coord[j * nDim + d] - coord[i * nDim + d];
+      dist2 += ev[d] * ev[d];
+      proj += ev[d] * n[d];
+    }
+    if (dist2 == 0.0) proj = 0.0; else proj = proj / dist2;
+    double corr[2];
+    for (int v = 0; v < 2; ++v) {
+      double pn = 0.0, pe = 0.0;
+      for (int d = 0; d < nDim; ++d) {
+        const double m = 0.5 * (TG[(i * 2 + v) * nDim + d] + TG[(j * 2 + v) * nDim + d]);
+        pn += m * n[d];
+        pe += m * ev[d];
+      }
+      corr[v] = pn;
+      corr[v] -= pe * proj - (T[2 * j + v] - T[2 * i + v]) * proj;
+    }
+    res[2 * e] = dk * corr[0];
+    res[2 * e + 1] = dw * corr[1];
+    if (Ji) {
+      double* A = Ji + 4 * e;
+      double* B = Jj + 4 * e;
+      A[0] = -dk * proj / ri; A[1] = 0.0; A[2] = 0.0; A[3] = -dw * proj / ri;
+      B[0] = dk * proj / rj; B[1] = 0.0; B[2] = 0.0; B[3] = dw * proj / rj;
+    }
+  }
+}
+
+// CSourcePieceWise_TurbSST::ComputeResidual (numerics_direct_turbulent.cpp:1183-1256) with the setters
+// of CTurbSSTSolver::Source_Residual (solver_direct_turbulent.cpp:3018-3080).
+// G: flow primitive gradient [N][nG][nDim].
+void orc_sst_source(int nDim, int nPV, int nG, int64_t N, const double* V, const double* G, const double* T,
+                    const double* vol, const double* dist, const double* F1, const double* F2, const double* CDkw,
+                    const double* strain, const double* eddy, double* res, double* J) {
+  const SSTConst c = sst_const();
+  for (int64_t i = 0; i < N; ++i) {
+    double* r = res + 2 * i;
+    double* A = J ? J + 4 * i : nullptr;
+    r[0] = 0.0;
+    r[1] = 0.0;
+    if (A) A[0] = A[1] = A[2] = A[3] = 0.0;
+    const double rho = V[i * nPV + nDim + 2];
+    const double k = T[2 * i], w = T[2 * i + 1], S = strain[i], Vol = vol[i];
+    const double ab = F1[i] * c.al1 + (1.0 - F1[i]) * c.al2;
+    const double bb = F1[i] * c.b1 + (1.0 - F1[i]) * c.b2;
+    if (dist[i] > 1e-10) {
+      double diverg = 0.0;
+      for (int d = 0; d < nDim; ++d) diverg += G[(i * nG + d + 1) * nDim + d];
+      double pk = eddy[i] * S * S - 2.0 / 3.0 * rho * k * diverg;
+      pk = smin(pk, 20.0 * c.bs * rho * w * k);
+      pk = smax(pk, 0.0);
+      const double zeta = smax(w, S * F2[i] / c.a1);
+      double pw = S * S - 2.0 / 3.0 * zeta * diverg;
+      pw = smax(pw, 0.0);
+      r[0] += pk * Vol;
+      r[1] += ab * rho * pw * Vol;
+      r[0] -= c.bs * rho * w * k * Vol;
+      r[1] -= bb * rho * w * w * Vol;
+      r[1] += (1.0 - F1[i]) * CDkw[i] * Vol;
+      if (A) {
+        A[0] = -c.bs * w * Vol;
+        A[3] = -2.0 * bb * w * Vol;
+      }
+    }
+  }
+}
+
+// SST residual / Jacobian assembly in the reference's loop order: CTurbSolver::Upwind_Residual
+// (solver_direct_turbulent.cpp:525-538: R_i += F, R_j -= F; A_ii += Ji, A_ij += Jj, A_ji -= Ji, A_jj -= Jj),
+// Viscous_Residual (:587-595, opposite signs), CTurbSSTSolver::Source_Residual (:3074-3075: R_i -= S,
+// A_ii -= Js); then CTurbSolver::ImplicitEuler_Iteration (:630-655): A_ii += Vol/(CFLRedCoeff_Turb*dt),
+// rhs = -R. Jacobian pointers may be null (residual only).
+void orc_sst_assemble(int64_t N, int64_t E, const int64_t* edges, const int64_t* rp, const int64_t* col,
+                      const double* Fu, const double* Jui, const double* Juj, const double* Fv, const double* Jvi,
+                      const double* Jvj, const double* Rs, const double* Js, const double* vol, const double* dt,
+                      double cfl_red, double* R, double* A, double* rhs) {
+  std::fill(R, R + N * 2, 0.0);
+  if (A) std::fill(A, A + rp[N] * 4, 0.0);
+  auto add = [&](int64_t b, const double* J, bool plus) {
+    double* d = A + b * 4;
+    for (int q = 0; q < 4; ++q) {
+      if (plus) d[q] += J[q]; else d[q] -= J[q];
+    }
+  };
+  for (int pass = 0; pass < 2; ++pass) {
+    const double* F = pass ? Fv : Fu;
+    const double* Ji = pass ? Jvi : Jui;
+    const double* Jj = pass ? Jvj : Juj;
+    if (!F) continue;
+    const bool up = pass == 0;
+    for (int64_t e = 0; e < E; ++e) {
+      const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+      for (int v = 0; v < 2; ++v) {
+        if (up) {
+          R[i * 2 + v] += F[e * 2 + v];
+          R[j * 2 + v] -= F[e * 2 + v];
+        } else {
+          R[i * 2 + v] -= F[e * 2 + v];
+          R[j * 2 + v] += F[e * 2 + v];
+        }
+      }
+      if (A && Ji) {
+        add(blk_of(rp, col, i, i), Ji + e * 4, up);
+        add(blk_of(rp, col, i, j), Jj + e * 4, up);
+        add(blk_of(rp, col, j, i), Ji + e * 4, !up);
+        add(blk_of(rp, col, j, j), Jj + e * 4, !up);
+      }
+    }
+  }
+  if (Rs)
+    for (int64_t i = 0; i < N; ++i) {
+      for (int v = 0; v < 2; ++v) R[i * 2 + v] -= Rs[i * 2 + v];
+      if (A && Js) add(blk_of(rp, col, i, i), Js + i * 4, false);
+    }
+  if (!A) return;
+  for (int64_t i = 0; i < N; ++i) {
+    double* D = A + blk_of(rp, col, i, i) * 4;
+    const double delta = vol[i] / (cfl_red * dt[i]);
+    D[0] += delta;
+    D[3] += delta;
+    for (int v = 0; v < 2; ++v) rhs[i * 2 + v] = -R[i * 2 + v];
+  }
+}
+
+// CTurbSolver::ImplicitEuler_Iteration SST branch (solver_direct_turbulent.cpp:698-713) through
+// CVariable::AddConservativeSolution (variable_structure.cpp:214-219): limits from the CTurbSSTSolver
+// constructor (solver_direct_turbulent.cpp:2731-2735). rho_old = rho (Cons2PrimVar sets V[rho] = U[rho],
+// variable_direct_reactive.cpp:579-584, and the flow's Solution_Old is the U the primitives came from).
+void orc_sst_update(int64_t N, const double* x, double relax, const double* rho, const double* rho_old, double* T) {
+  const double lo[2] = {1.0e-10, 1.0e-4}, hi[2] = {1.0e10, 1.0e15};
+  for (int64_t i = 0; i < N; ++i)
+    for (int v = 0; v < 2; ++v)
+      T[2 * i + v] = smin(smax((T[2 * i + v] * rho_old[i] + relax * x[2 * i + v]) / rho[i], lo[v]), hi[v]);
+}
+
 }  // extern "C"
