@@ -25,11 +25,13 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "rx.h")
 RX_OK, RX_ERR_ARG, RX_ERR_HIP, RX_ERR_NAN, RX_ERR_RANGE, RX_ERR_NONPHYS, RX_ERR_DIVERGED, RX_ERR_STATE = range(8)
 # rx_field
 FIELDS = ["U", "V", "DPDU", "DTDU", "MU", "KAPPA", "DIJ", "GRAD", "LIMITER", "TKE", "OMEGA", "MUT", "SIGMAK", "GRADK",
-          "EDDY", "RES", "DT", "LAMBDA_INV", "LAMBDA_VISC", "JAC", "ILU", "SOL", "RHS"]
+          "EDDY", "RES", "DT", "LAMBDA_INV", "LAMBDA_VISC", "JAC", "ILU", "SOL", "RHS", "STRAIN", "F1", "F2", "CDKW",
+          "WALLDIST"]
 F = {name: k for k, name in enumerate(FIELDS)}
 # rx_kernel
 KERNELS = ["CONV", "VISC", "SOURCE", "GRAD", "LIMITER", "DT", "SPMV", "ILU_BUILD", "ILU_APPLY", "LUSGS", "KRYLOV",
-           "UPDATE", "SOLVE", "VISC_JAC", "ASSEMBLE"]
+           "UPDATE", "SOLVE", "VISC_JAC", "ASSEMBLE", "STRAIN", "SST_GRAD", "SST_UPW", "SST_VISC", "SST_SOURCE",
+           "SST_SYSTEM", "SST_SOLVE", "SST_POST"]
 K = {name: k for k, name in enumerate(KERNELS)}
 
 
@@ -115,6 +117,11 @@ def lib():
         _lib.rx_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         _lib.rx_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(HostComm)]
         _lib.rx_halo_exchange.argtypes = [C.c_void_p, C.c_int]
+        _lib.rx_sst_create.argtypes = [C.POINTER(MeshDesc), C.c_void_p, C.POINTER(Cfg), C.POINTER(C.c_void_p)]
+        for name in ("rx_strain_mag", "rx_sst_preprocessing", "rx_sst_upwind", "rx_sst_viscous", "rx_sst_source",
+                     "rx_sst_postprocessing"):
+            getattr(_lib, name).argtypes = [C.c_void_p]
+        _lib.rx_sst_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
     return _lib
 
 
@@ -217,6 +224,39 @@ def default_cfg(**kw):
     return cfg
 
 
+def mesh_desc(mesh):
+    """rx_mesh_desc over contiguous copies of the mesh arrays (kept alive by the returned dict)."""
+    nDim = int(mesh.get("n_dim", 2))
+    keep = {
+        "edges": np.ascontiguousarray(mesh["edges"], dtype=np.int64),
+        "edge_normal": np.ascontiguousarray(mesh["edge_normal"], dtype=np.float64),
+        "coord": np.ascontiguousarray(mesh["coord"], dtype=np.float64),
+        "volume": np.ascontiguousarray(mesh["volume"], dtype=np.float64),
+        "nbr_ptr": np.ascontiguousarray(mesh["nbr_ptr"], dtype=np.int64),
+        "nbr": np.ascontiguousarray(mesh["nbr"], dtype=np.int64),
+        "bvert": np.ascontiguousarray(np.asarray(mesh["bvertex"])[:, :2], dtype=np.int64),
+        "bvert_normal": np.ascontiguousarray(mesh["bvertex_normal"], dtype=np.float64),
+    }
+    pp = mesh.get("part_ptr")
+    if pp is not None and len(pp) > 2:
+        keep["part_ptr"] = np.ascontiguousarray(pp, dtype=np.int64)
+    N = len(keep["coord"])
+    if "n_domain" in mesh:
+        keep["neigh"] = np.ascontiguousarray(mesh["neigh"], dtype=np.int32)
+        for k in ("send_ptr", "send_idx", "recv_ptr"):
+            keep[k] = np.ascontiguousarray(mesh[k], dtype=np.int64)
+    md = MeshDesc()
+    md.n_dim, md.n_point, md.n_edge = nDim, N, len(keep["edges"])
+    md.n_bvert = len(keep["bvert"])
+    md.n_part = len(keep["part_ptr"]) - 1 if "part_ptr" in keep else 0
+    if "n_domain" in mesh:
+        md.n_domain = int(mesh["n_domain"])
+        md.n_neigh = len(keep["neigh"])
+    for k, v in keep.items():
+        setattr(md, k, v.ctypes.data)
+    return keep, md
+
+
 class ReactiveNSSolver:
     """Device-resident reactive NS + SST flow state with the reference's per-phase entry points."""
 
@@ -227,38 +267,14 @@ class ReactiveNSSolver:
         self.N = int(len(mesh["coord"]))
         self.E = int(len(mesh["edges"]))
         self.nVar = mech.ns + self.nDim + 2
-        self._mesh_keep = {
-            "edges": np.ascontiguousarray(mesh["edges"], dtype=np.int64),
-            "edge_normal": np.ascontiguousarray(mesh["edge_normal"], dtype=np.float64),
-            "coord": np.ascontiguousarray(mesh["coord"], dtype=np.float64),
-            "volume": np.ascontiguousarray(mesh["volume"], dtype=np.float64),
-            "nbr_ptr": np.ascontiguousarray(mesh["nbr_ptr"], dtype=np.int64),
-            "nbr": np.ascontiguousarray(mesh["nbr"], dtype=np.int64),
-            "bvert": np.ascontiguousarray(np.asarray(mesh["bvertex"])[:, :2], dtype=np.int64),
-            "bvert_normal": np.ascontiguousarray(mesh["bvertex_normal"], dtype=np.float64),
-        }
-        pp = mesh.get("part_ptr")
-        if pp is not None and len(pp) > 2:
-            self._mesh_keep["part_ptr"] = np.ascontiguousarray(pp, dtype=np.int64)
-        self.n_part = len(pp) - 1 if pp is not None else 1
+        self._mesh_keep, md = mesh_desc(mesh)
+        self.n_part = md.n_part if md.n_part > 0 else 1
         self.Nd = int(mesh.get("n_domain", self.N))
-        if "n_domain" in mesh:
-            self._mesh_keep["neigh"] = np.ascontiguousarray(mesh["neigh"], dtype=np.int32)
-            for k in ("send_ptr", "send_idx", "recv_ptr"):
-                self._mesh_keep[k] = np.ascontiguousarray(mesh[k], dtype=np.int64)
-        md = MeshDesc()
-        md.n_dim, md.n_point, md.n_edge = self.nDim, self.N, self.E
-        md.n_bvert = len(self._mesh_keep["bvert"])
-        md.n_part = len(self._mesh_keep["part_ptr"]) - 1 if "part_ptr" in self._mesh_keep else 0
-        if "n_domain" in mesh:
-            md.n_domain = self.Nd
-            md.n_neigh = len(self._mesh_keep["neigh"])
-        for k, v in self._mesh_keep.items():
-            setattr(md, k, v.ctypes.data)
         h = C.c_void_p()
         _chk(lib().rx_ctx_create(C.byref(md), C.byref(mech.desc), C.byref(cfg), device, C.byref(h)), "rx_ctx_create")
         self.h = h
         self._mesh_keep = None
+        self._children = []
 
     # ---- distributed (one rank per GPU)
     def comm_init(self, nranks, rank, uid: bytes):
@@ -275,6 +291,8 @@ class ReactiveNSSolver:
         _chk(lib().rx_halo_exchange(self.h, F[field]), f"rx_halo_exchange({field})", self.h)
 
     def close(self):
+        for c in getattr(self, "_children", []):
+            c.close()
         if getattr(self, "h", None):
             lib().rx_ctx_destroy(self.h)
             self.h = None
@@ -342,6 +360,9 @@ class ReactiveNSSolver:
     def SetTime_Step(self):
         self._call("rx_time_step")
 
+    def SetStrainMag(self):
+        self._call("rx_strain_mag")
+
     def sync(self):
         self._call("rx_sync")
 
@@ -384,3 +405,67 @@ class ReactiveNSSolver:
         n = C.c_int64()
         lib().rx_profile_read(self.h, K[kernel], C.byref(ms), C.byref(n))
         return ms.value, n.value
+
+
+def sst_cfg(implicit=1, lin_tol=1e-6, lin_iter=5, lin_prec=1, relaxation_turb=1.0, cfl_red_turb=1.0):
+    """rx_cfg for the SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl."""
+    return default_cfg(implicit=implicit, lin_tol=lin_tol, lin_iter=lin_iter, lin_prec=lin_prec,
+                       relaxation=relaxation_turb, cfl=cfl_red_turb)
+
+
+class TurbSSTSolver:
+    """Device-resident Menter SST solver (CTurbSSTSolver / CTurbSolver surface) bound to a flow solver:
+    a second context (k, omega) on the flow context's stream, reading the flow's primitives, laminar and
+    eddy viscosity, primitive gradient, StrainMag and time step, and writing back the turbulent fields the
+    flow's viscous flux reads (TKE, OMEGA, MUT, GRADK, SIGMAK, EDDY) in Postprocessing."""
+
+    def __init__(self, mesh, flow: ReactiveNSSolver, cfg: Cfg):
+        self.flow = flow
+        self.cfg = cfg
+        self.N, self.nDim, self.nVar = flow.N, flow.nDim, 2
+        keep, md = mesh_desc(mesh)
+        h = C.c_void_p()
+        _chk(lib().rx_sst_create(C.byref(md), flow.h, C.byref(cfg), C.byref(h)), "rx_sst_create")
+        self.h = h
+        flow._children.append(self)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rx_ctx_destroy(self.h)
+            self.h = None
+
+    size = ReactiveNSSolver.size
+    upload = ReactiveNSSolver.upload
+    download = ReactiveNSSolver.download
+    _call = ReactiveNSSolver._call
+    sync = ReactiveNSSolver.sync
+    profile = ReactiveNSSolver.profile
+    profile_read = ReactiveNSSolver.profile_read
+
+    def set_state(self, T, wall_distance, F1=None, F2=None, CDkw=None):
+        self.upload("U", T)
+        self.upload("WALLDIST", wall_distance)
+        for k, v in (("F1", F1), ("F2", F2), ("CDKW", CDkw)):
+            if v is not None:
+                self.upload(k, v)
+
+    def Preprocessing(self):
+        self._call("rx_sst_preprocessing")
+
+    def Upwind_Residual(self):
+        self._call("rx_sst_upwind")
+
+    def Viscous_Residual(self):
+        self._call("rx_sst_viscous")
+
+    def Source_Residual(self):
+        self._call("rx_sst_source")
+
+    def ImplicitEuler_Iteration(self):
+        rms = np.zeros(2)
+        it = C.c_int()
+        _chk(lib().rx_sst_implicit_euler(self.h, rms.ctypes.data, C.byref(it)), "rx_sst_implicit_euler", self.h)
+        return rms, it.value
+
+    def Postprocessing(self):
+        self._call("rx_sst_postprocessing")

@@ -68,32 +68,55 @@ const char* rx_status_string(int s) {
   }
 }
 
-int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg* cfg, int device, rx_ctx** out) {
-  if (!mesh || !mech || !cfg || !out) return RX_ERR_ARG;
-  if (mesh->n_dim != 2) return RX_ERR_ARG;  // 3-D dual grids: next round
-  const int ns = mech->n_species;
-  if (!(ns == 3 || ns == 4 || ns == 7 || ns == 9)) return RX_ERR_ARG;
-  if (mech->n_reactions > rx::kMaxNR) return RX_ERR_ARG;
-  if (mesh->n_point >= (1LL << 31) || 2 * mesh->n_edge >= (1LL << 31)) return RX_ERR_ARG;
-  rx_ctx* ctx = new rx_ctx();
+}  // extern "C"
+
+namespace {
+
+// Context construction shared by the flow context (mech != null) and the SST context (flow != null,
+// nVar = 2, borrows the flow context's stream and communicator).
+int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg* cfg, int device, rx_ctx* flow,
+                rx_ctx** out) {
+  if (!mesh || !cfg || !out || (!mech && !flow)) return RX_ERR_ARG;
   *out = nullptr;
-  ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess) {
+  if (mesh->n_dim != 2) return RX_ERR_ARG;  // 3-D dual grids: next round
+  const bool sst = flow != nullptr;
+  const int ns = sst ? 0 : mech->n_species;
+  if (!sst && !(ns == 3 || ns == 4 || ns == 7 || ns == 9)) return RX_ERR_ARG;
+  if (!sst && mech->n_reactions > rx::kMaxNR) return RX_ERR_ARG;
+  if (mesh->n_point >= (1LL << 31) || 2 * mesh->n_edge >= (1LL << 31)) return RX_ERR_ARG;
+  if (sst && (mesh->n_point != flow->N || mesh->n_edge != flow->E)) return RX_ERR_ARG;
+  rx_ctx* ctx = new rx_ctx();
+  ctx->device = sst ? flow->device : device;
+  if (hipSetDevice(ctx->device) != hipSuccess) {
     delete ctx;
     return RX_ERR_HIP;
   }
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (sst) {
+    ctx->kind = RX_KIND_SST;
+    ctx->flow = flow;
+    ctx->stream = flow->stream;
+    ctx->own_stream = false;
+  } else if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return RX_ERR_HIP;
   }
   ctx->cfg = *cfg;
   ctx->nDim = mesh->n_dim;
   ctx->ns = ns;
-  ctx->nr = mech->n_reactions;
-  ctx->nVar = ns + ctx->nDim + 2;
-  ctx->nPV = ns + ctx->nDim + 5;
-  ctx->nG = ns + ctx->nDim + 2;
-  ctx->nL = ctx->nDim + 2;
+  if (sst) {  // (k, omega); the gradient has the same two rows
+    ctx->cfg.rans = 1;
+    ctx->nr = 0;
+    ctx->nVar = 2;
+    ctx->nPV = 0;
+    ctx->nG = 2;
+    ctx->nL = 0;
+  } else {
+    ctx->nr = mech->n_reactions;
+    ctx->nVar = ns + ctx->nDim + 2;
+    ctx->nPV = ns + ctx->nDim + 5;
+    ctx->nG = ns + ctx->nDim + 2;
+    ctx->nL = ctx->nDim + 2;
+  }
   const int64_t N = mesh->n_point, E = mesh->n_edge, NB = mesh->n_bvert;
   ctx->N = N;
   ctx->E = E;
@@ -400,7 +423,7 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
   CK(dupload(ctx, &ctx->diag, diag.data(), N));
 
   // ---- mechanism
-  {
+  if (!sst) {
     rx::DevMech& m = ctx->mech;
     const int nr = mech->n_reactions, nt = mech->n_tab;
     m.ns = ns;
@@ -447,49 +470,85 @@ int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_c
 
   // ---- fields
   const int64_t nb2 = ctx->nnzb * (int64_t)nv * nv;
-  const int64_t sizes[RX_F_COUNT] = {
-      N * nv,                 // U
-      N * ctx->nPV,           // V
-      N * nv, N * nv,         // dPdU, dTdU
-      N, N,                   // mu, kappa
-      N * ns * ns,            // Dij
-      N * ctx->nG * nd,       // grad
-      N * ctx->nL,            // limiter
-      N, N, N, N,             // tke, omega, mut, sigmak
-      N * nd,                 // gradk
-      N,                      // eddy
-      N * nv,                 // res
-      N, N, N,                // dt, lambda_inv, lambda_visc
-      ctx->cfg.implicit ? nb2 : 0,                       // jac
-      ctx->cfg.implicit ? nb2 + N * (int64_t)nv * nv : 0, // ilu (+ inverse diagonals)
-      N * nv, N * nv          // sol, rhs
-  };
+  const int64_t imp = ctx->cfg.implicit ? 1 : 0;
+  int64_t sizes[RX_F_COUNT] = {};
+  if (!sst) {
+    const int64_t fl[RX_F_COUNT] = {
+        N * nv,                 // U
+        N * ctx->nPV,           // V
+        N * nv, N * nv,         // dPdU, dTdU
+        N, N,                   // mu, kappa
+        N * ns * ns,            // Dij
+        N * ctx->nG * nd,       // grad
+        N * ctx->nL,            // limiter
+        N, N, N, N,             // tke, omega, mut, sigmak
+        N * nd,                 // gradk
+        N,                      // eddy
+        N * nv,                 // res
+        N, N, N,                // dt, lambda_inv, lambda_visc
+        imp * nb2,                       // jac
+        imp * (nb2 + N * (int64_t)nv * nv), // ilu (+ inverse diagonals)
+        N * nv, N * nv,         // sol, rhs
+        N,                      // strain
+        0, 0, 0, 0              // SST-only
+    };
+    std::copy(fl, fl + RX_F_COUNT, sizes);
+  } else {
+    sizes[RX_F_U] = N * 2;
+    sizes[RX_F_GRAD] = N * 2 * nd;
+    sizes[RX_F_MUT] = N;
+    sizes[RX_F_RES] = N * 2;
+    sizes[RX_F_JAC] = imp * nb2;
+    sizes[RX_F_ILU] = imp * (nb2 + N * 4);
+    sizes[RX_F_SOL] = N * 2;
+    sizes[RX_F_RHS] = N * 2;
+    sizes[RX_F_F1] = sizes[RX_F_F2] = sizes[RX_F_CDKW] = sizes[RX_F_WALLDIST] = N;
+  }
   for (int q = 0; q < RX_F_COUNT; ++q) {
     ctx->fcount[q] = sizes[q];
     CK(dalloc(ctx, &ctx->f[q], sizes[q]));
   }
-  ctx->fcount[RX_F_ILU] = ctx->cfg.implicit ? nb2 : 0;
-  if (ctx->cfg.implicit) {
+  ctx->fcount[RX_F_ILU] = imp * nb2;
+  if (ctx->cfg.implicit && !sst) {
     CK(dalloc(ctx, &ctx->fconv, E * nv));
     CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->vsumm, E * (int64_t)(24 + 9 * ns)));
     CK(dalloc(ctx, &ctx->jsrc, N * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->rsrc, N * nv));
+  }
+  if (ctx->cfg.implicit) {
     CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->xstar, N * nv));
   }
-  CK(dalloc(ctx, &ctx->fvisc, E * nv));
-  CK(dalloc(ctx, &ctx->lim_mn, N * ctx->nL));
-  CK(dalloc(ctx, &ctx->lim_mx, N * ctx->nL));
+  if (!sst) {
+    CK(dalloc(ctx, &ctx->fvisc, E * nv));
+    CK(dalloc(ctx, &ctx->lim_mn, N * ctx->nL));
+    CK(dalloc(ctx, &ctx->lim_mx, N * ctx->nL));
+  }
   CK(dalloc(ctx, &ctx->red, 256 * 32 + 1024));
   CK(dalloc(ctx, &ctx->err, 2));
   if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), sizeof(double) * (256 * 32 + 1024)) != hipSuccess)
     CK(RX_ERR_HIP);
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) CK(RX_ERR_HIP);
+  if (sst && flow->distributed()) CK(rx_comm_borrow(ctx, flow));
 #undef CK
   *out = ctx;
   return RX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rx_ctx_create(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg* cfg, int device, rx_ctx** out) {
+  if (!mech) return RX_ERR_ARG;
+  return create_impl(mesh, mech, cfg, device, nullptr, out);
+}
+
+int rx_sst_create(const rx_mesh_desc* mesh, rx_ctx* flow, const rx_cfg* cfg, rx_ctx** out) {
+  if (!flow || flow->kind != RX_KIND_FLOW) return RX_ERR_ARG;
+  return create_impl(mesh, nullptr, cfg, 0, flow, out);
 }
 
 int rx_ctx_destroy(rx_ctx* ctx) {
@@ -512,7 +571,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   if (ctx->h_red) (void)hipHostFree(ctx->h_red);
   ctx->prof_drain();
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RX_OK;
 }
@@ -557,7 +616,7 @@ int rx_sync(rx_ctx* ctx) {
 int64_t rx_last_error_index(const rx_ctx* ctx) { return ctx ? ctx->last_err_index : -1; }
 
 int rx_residual_zero(rx_ctx* ctx) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
   ctx->phase_conv = ctx->phase_visc = ctx->phase_src = 0;
   ctx->assembled = ctx->cfg.implicit ? 0 : 1;
@@ -565,7 +624,7 @@ int rx_residual_zero(rx_ctx* ctx) {
 }
 
 int rx_edge_flux_conv(rx_ctx* ctx) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_CONV);
   int rc = ctx->cfg.implicit ? rx_launch_ausm_edge(ctx) : rx_launch_ausm_node(ctx);
   if (rc) return rc;
@@ -575,7 +634,7 @@ int rx_edge_flux_conv(rx_ctx* ctx) {
 }
 
 int rx_edge_flux_visc(rx_ctx* ctx) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   int rc = rx_launch_visc_edge(ctx);
   if (rc) return rc;
   if (!ctx->cfg.implicit) {
@@ -588,7 +647,7 @@ int rx_edge_flux_visc(rx_ctx* ctx) {
 }
 
 int rx_cell_source_pasr(rx_ctx* ctx) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_SOURCE);
   int rc = rx_launch_source(ctx);
   if (rc) return rc;
@@ -598,7 +657,7 @@ int rx_cell_source_pasr(rx_ctx* ctx) {
 }
 
 int rx_grad_lsq(rx_ctx* ctx) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_GRAD);
   const int rc = rx_launch_grad(ctx);
   if (rc) return rc;
@@ -607,7 +666,7 @@ int rx_grad_lsq(rx_ctx* ctx) {
 }
 
 int rx_limiter_venkat(rx_ctx* ctx) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_LIMITER);
   const int rc = rx_launch_limiter(ctx);
   if (rc) return rc;
@@ -616,7 +675,7 @@ int rx_limiter_venkat(rx_ctx* ctx) {
 }
 
 int rx_time_step(rx_ctx* ctx) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_DT);
   return rx_launch_time_step(ctx);
 }
@@ -662,7 +721,7 @@ int rx_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
 }
 
 int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
-  if (!ctx) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   int rc;
   {
     RxPhase ph(ctx, RX_K_UPDATE);
@@ -680,7 +739,7 @@ int enqueue_solve(rx_ctx* ctx) {
   int rc;
   if ((rc = rx_la_fgmres_enqueue(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter))) return rc;
   if ((rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RHS]))) return rc;
-  return rx_la_implicit_update(ctx);
+  return ctx->kind == RX_KIND_SST ? rx_sst_update(ctx) : rx_la_implicit_update(ctx);
 }
 
 // The solve is replayed as a graph unless RX_NO_GRAPH=1 or a host-staged transport is attached
@@ -689,28 +748,27 @@ bool graphs_enabled(const rx_ctx* ctx) {
   const char* e = getenv("RX_NO_GRAPH");
   return !(e && e[0] == '1') && !ctx->has_hcomm;
 }
-}  // namespace
 
-// ImplicitEuler_Iteration (solver_direct_reactive.cpp:2336-2407): system build, ILU0 build if
-// selected (CSysSolve::Solve :601-653), FGMRES, clipped relaxed update.
-int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
-  if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
+// Shared by the flow and the SST context: system build, preconditioner build (CSysSolve::Solve
+// :601-653), then FGMRES + RMS + update replayed as one hipGraph.
+int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
+  const bool sst = ctx->kind == RX_KIND_SST;
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
   if ((rc = rx_la_krylov_alloc(ctx, ctx->cfg.lin_iter))) return rc;
   {
-    RxPhase ph(ctx, RX_K_UPDATE);
-    if ((rc = rx_la_build_system(ctx))) return rc;
+    RxPhase ph(ctx, sst ? RX_K_SST_SYSTEM : RX_K_UPDATE);
+    if ((rc = sst ? rx_sst_build_system(ctx) : rx_la_build_system(ctx))) return rc;
   }
   if (ctx->cfg.lin_prec == 1) {
-    RxPhase ph(ctx, RX_K_ILU_BUILD);
+    RxPhase ph(ctx, sst ? RX_K_SST_SYSTEM : RX_K_ILU_BUILD);
     if ((rc = rx_la_ilu_build(ctx))) return rc;
   } else {
-    RxPhase ph(ctx, RX_K_LUSGS);
+    RxPhase ph(ctx, sst ? RX_K_SST_SYSTEM : RX_K_LUSGS);
     if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
   }
   {
-    RxPhase ph(ctx, RX_K_SOLVE);
+    RxPhase ph(ctx, sst ? RX_K_SST_SOLVE : RX_K_SOLVE);
     if (graphs_enabled(ctx)) {
       if (!ctx->solve_exec) {
         RX_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
@@ -738,6 +796,21 @@ int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   if ((rc = rx_la_fgmres_result(ctx, &it, &resid))) return rc;
   if (lin_iters) *lin_iters = it;
   return RX_OK;
+}
+}  // namespace
+
+// ImplicitEuler_Iteration (solver_direct_reactive.cpp:2336-2407): system build, ILU0 build if
+// selected (CSysSolve::Solve :601-653), FGMRES, clipped relaxed update.
+int rx_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
+  if (!ctx || !ctx->cfg.implicit || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
+  return implicit_solve(ctx, res_rms, lin_iters);
+}
+
+// CTurbSolver::ImplicitEuler_Iteration (solver_direct_turbulent.cpp:615-728): A_ii += Vol/(CFLRed*dt),
+// rhs = -R, the same preconditioned FGMRES, AddConservativeSolution, Set_MPI_Solution, RMS.
+int rx_sst_implicit_euler(rx_ctx* ctx, double* res_rms, int* lin_iters) {
+  if (!ctx || !ctx->cfg.implicit || ctx->kind != RX_KIND_SST) return RX_ERR_ARG;
+  return implicit_solve(ctx, res_rms, lin_iters);
 }
 
 hipEvent_t rx_ctx::prof_event() {

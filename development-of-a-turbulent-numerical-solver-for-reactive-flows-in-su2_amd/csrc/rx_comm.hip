@@ -165,8 +165,24 @@ int rx_halo_exchange(rx_ctx* ctx, rx_field f) {
 
 }  // extern "C"
 
+// An SST context shares its flow context's transport (same ranks, same halo plan).
+int rx_comm_borrow(rx_ctx* ctx, const rx_ctx* from) {
+  ctx->comm = from->comm;
+  ctx->comm_owned = false;
+  ctx->nranks = from->nranks;
+  ctx->rank = from->rank;
+  if (from->has_hcomm) {
+    const int rc = stage_alloc(ctx);
+    if (rc) return rc;
+    ctx->hcomm = from->hcomm;
+    ctx->has_hcomm = true;
+  }
+  ctx->n_global = from->n_global;
+  return RX_OK;
+}
+
 void rx_comm_free(rx_ctx* ctx) {
-  if (ctx->comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
+  if (ctx->comm && ctx->comm_owned) (void)ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
   ctx->comm = nullptr;
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   ctx->h_stage = nullptr;

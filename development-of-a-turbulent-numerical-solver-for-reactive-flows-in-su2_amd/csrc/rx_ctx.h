@@ -15,9 +15,14 @@
     if (_e != hipSuccess) return rx_fail_hip(ctx, _e);   \
   } while (0)
 
+enum rx_kind { RX_KIND_FLOW = 0, RX_KIND_SST = 1 };
+
 struct rx_ctx {
   int device = 0;
+  int kind = RX_KIND_FLOW;
+  rx_ctx* flow = nullptr;       // SST context: the flow context it reads (V, MU, EDDY, GRAD, STRAIN, DT)
   hipStream_t stream = nullptr;
+  bool own_stream = true;       // SST contexts run on their flow context's stream
   int nDim = 2, ns = 0, nr = 0, nVar = 0, nPV = 0, nG = 0, nL = 0;
   int64_t N = 0, E = 0, NB = 0, nnzb = 0;
   int64_t Nd = 0;               // owned (domain) points; N - Nd halo points follow them
@@ -29,6 +34,7 @@ struct rx_ctx {
   int64_t n_send = 0;
   double* sendbuf = nullptr;    // [n_send * kHaloMaxStride]
   void* comm = nullptr;         // ncclComm_t
+  bool comm_owned = true;       // SST contexts borrow the flow context's communicator
   bool has_hcomm = false;       // host-staged transport (rx_comm_init_host)
   rx_host_comm hcomm{};
   double* h_stage = nullptr;    // pinned [(n_send + N - Nd) * kHaloMaxStride + 64]
@@ -138,6 +144,7 @@ int rx_la_exchange(rx_ctx* ctx, double* f, int stride);
 // without communicator
 int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count);
 void rx_comm_free(rx_ctx* ctx);
+int rx_comm_borrow(rx_ctx* ctx, const rx_ctx* from);
 
 // Phase timer: records HIP events around a phase on the context stream when profiling is on.
 struct RxPhase {
@@ -189,3 +196,6 @@ int rx_la_rms_read(rx_ctx* ctx, double* rms);
 int rx_la_implicit_update(rx_ctx* ctx);
 int rx_la_explicit_update(rx_ctx* ctx);
 int rx_la_build_system(rx_ctx* ctx);
+// SST (rx_sst.hip)
+int rx_sst_build_system(rx_ctx* ctx);
+int rx_sst_update(rx_ctx* ctx);

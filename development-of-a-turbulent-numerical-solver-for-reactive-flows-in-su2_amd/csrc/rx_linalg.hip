@@ -128,6 +128,7 @@ __global__ void k_sumsq_total(int nVar, int nblk, const double* __restrict__ par
 
 #define RX_NV_SWITCH(nv, CALL)                       \
   switch (nv) {                                      \
+    case 2: { constexpr int NV_ = 2; CALL; } break;   \
     case 7: { constexpr int NV_ = 7; CALL; } break;   \
     case 8: { constexpr int NV_ = 8; CALL; } break;   \
     case 11: { constexpr int NV_ = 11; CALL; } break; \

@@ -1,0 +1,575 @@
+// rx_sst.hip — Menter SST turbulence solver of the reactive RANS iteration on gfx950 (SURVEY §8 a14 +
+// next-2), and the flow-side StrainMag it reads.
+//
+// Reference (paths relative to the reference root):
+//   CTurbSSTSolver::Preprocessing / Postprocessing / Source_Residual   SU2_CFD/src/solver_direct_turbulent.cpp:2923-3080
+//   CTurbSolver::Upwind_Residual / Viscous_Residual / ImplicitEuler     solver_direct_turbulent.cpp:429-728
+//   CUpwSca_TurbSST / CAvgGradCorrected_TurbSST / CSourcePieceWise_TurbSST
+//                                                  SU2_CFD/src/numerics_direct_turbulent.cpp:865-922, 1080-1256
+//   CSolver::SetSolution_Gradient_LS               SU2_CFD/src/solver_structure.cpp:580-720
+//   CTurbSSTVariable::SetBlendingFunc              SU2_CFD/src/variable_direct_turbulent.cpp:178-203
+//   CReactiveNSVariable::SetStrainMag              SU2_CFD/src/variable_direct_reactive.cpp:1060-1095
+//
+// The SST context is a second rx_ctx (nVar = 2) on the flow context's stream: its linear system reuses
+// the BSR / ILU(0) / LU-SGS / FGMRES kernels with 2x2 blocks. Residual loops are node-centric gathers:
+// each node recomputes the flux of its incident edges in increasing edge id (the reference's scatter
+// order) and applies the row's own residual and Jacobian-block updates, so every block of row i is
+// written by one thread only and the accumulation order is the reference's. The per-edge operators are
+// cheap (tens of flops), so recomputing each edge from both ends costs less than a scratch round trip.
+// std::min / std::max are restated as their ternaries (NaN / signed-zero behaviour included).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "rx_ctx.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
+
+struct SSTC {
+  double sk1, sk2, so1, so2, b1, b2, bs, a1, al1, al2;
+};
+// CTurbSSTSolver constructor (solver_direct_turbulent.cpp:2716-2725), evaluated on the host as there.
+SSTC sst_constants() {
+  SSTC c;
+  c.sk1 = 0.85;
+  c.sk2 = 1.0;
+  c.so1 = 0.5;
+  c.so2 = 0.856;
+  c.b1 = 0.075;
+  c.b2 = 0.0828;
+  c.bs = 0.09;
+  c.a1 = 0.31;
+  c.al1 = c.b1 / c.bs - c.so1 * 0.41 * 0.41 / std::sqrt(c.bs);
+  c.al2 = c.b2 / c.bs - c.so2 * 0.41 * 0.41 / std::sqrt(c.bs);
+  return c;
+}
+
+__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }
+
+// CSolver::SetSolution_Gradient_LS for the two turbulent variables, one thread per owned point.
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_sol_grad_ls(int Nd, const double* __restrict__ coord,
+                                                        const int32_t* __restrict__ nptr,
+                                                        const int32_t* __restrict__ nbr,
+                                                        const double* __restrict__ sol, double* __restrict__ grad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Nd) return;
+  double ci[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) ci[d] = coord[(size_t)i * NDIM + d];
+  const double s0 = sol[2 * (size_t)i], s1 = sol[2 * (size_t)i + 1];
+  double Cv[2][NDIM];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) Cv[v][d] = 0.0;
+  double r11 = 0, r12 = 0, r13 = 0, r22 = 0, r23 = 0, r23_a = 0, r23_b = 0, r33 = 0;
+  for (int k = nptr[i]; k < nptr[i + 1]; ++k) {
+    const int j = nbr[k];
+    double dx[NDIM];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) dx[d] = coord[(size_t)j * NDIM + d] - ci[d];
+    double w = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) w += dx[d] * dx[d];
+    if (w != 0.0) {
+      r11 += dx[0] * dx[0] / w;
+      r12 += dx[0] * dx[1] / w;
+      r22 += dx[1] * dx[1] / w;
+      if constexpr (NDIM == 3) {
+        r13 += dx[0] * dx[NDIM - 1] / w;
+        r23_a += dx[1] * dx[NDIM - 1] / w;
+        r23_b += dx[0] * dx[NDIM - 1] / w;
+        r33 += dx[NDIM - 1] * dx[NDIM - 1] / w;
+      }
+      const double d0 = sol[2 * (size_t)j] - s0, d1 = sol[2 * (size_t)j + 1] - s1;
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) {
+        Cv[0][d] += dx[d] * d0 / w;
+        Cv[1][d] += dx[d] * d1 / w;
+      }
+    }
+  }
+  if (r11 >= 0.0) r11 = sqrt(r11); else r11 = 0.0;
+  if (r11 != 0.0) r12 = r12 / r11; else r12 = 0.0;
+  if (r22 - r12 * r12 >= 0.0) r22 = sqrt(r22 - r12 * r12); else r22 = 0.0;
+  if constexpr (NDIM == 3) {
+    if (r11 != 0.0) r13 = r13 / r11; else r13 = 0.0;
+    if ((r22 != 0.0) && (r11 * r22 != 0.0)) r23 = r23_a / r22 - r23_b * r12 / (r11 * r22); else r23 = 0.0;
+    if (r33 - r23 * r23 - r13 * r13 >= 0.0) r33 = sqrt(r33 - r23 * r23 - r13 * r13); else r33 = 0.0;
+  }
+  double detR2 = (NDIM == 2) ? (r11 * r22) * (r11 * r22) : (r11 * r22 * r33) * (r11 * r22 * r33);
+  bool singular = false;
+  if (fabs(detR2) <= rx::kEPS) {
+    detR2 = 1.0;
+    singular = true;
+  }
+  double S[NDIM][NDIM];
+#pragma unroll
+  for (int a = 0; a < NDIM; ++a)
+#pragma unroll
+    for (int b = 0; b < NDIM; ++b) S[a][b] = 0.0;
+  if (!singular) {
+    if constexpr (NDIM == 2) {
+      S[0][0] = (r12 * r12 + r22 * r22) / detR2;
+      S[0][1] = -r11 * r12 / detR2;
+      S[1][0] = S[0][1];
+      S[1][1] = r11 * r11 / detR2;
+    } else {
+      const double z11 = r22 * r33, z12 = -r12 * r33, z13 = r12 * r23 - r13 * r22;
+      const double z22 = r11 * r33, z23 = -r11 * r23, z33 = r11 * r22;
+      double* s = &S[0][0];
+      s[0] = (z11 * z11 + z12 * z12 + z13 * z13) / detR2;
+      s[1] = (z12 * z22 + z13 * z23) / detR2;
+      s[NDIM - 1] = (z13 * z33) / detR2;
+      s[NDIM] = s[1];
+      s[NDIM + 1] = (z22 * z22 + z23 * z23) / detR2;
+      s[2 * NDIM - 1] = (z23 * z33) / detR2;
+      s[2 * NDIM] = s[NDIM - 1];
+      s[2 * NDIM + 1] = s[2 * NDIM - 1];
+      s[NDIM * NDIM - 1] = (z33 * z33) / detR2;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+      double product = 0.0;
+#pragma unroll
+      for (int e = 0; e < NDIM; ++e) product += S[d][e] * Cv[v][e];
+      grad[((size_t)i * 2 + v) * NDIM + d] = product;
+    }
+}
+
+// SetStrainMag from the flow primitive gradient (rows 1..NDIM = velocity); pow(x, 2.0) -> x * x.
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_strain(int N, int nG, const double* __restrict__ G,
+                                                   double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const double* g = G + (size_t)i * nG * NDIM;
+  double Div = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) Div += g[(d + 1) * NDIM + d];
+  double S = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    const double x = g[(d + 1) * NDIM + d] - 1.0 / 3.0 * Div;
+    S += x * x;
+  }
+  {
+    const double x = 0.5 * (g[1 * NDIM + 1] + g[2 * NDIM + 0]);
+    S += 2.0 * (x * x);
+  }
+  if constexpr (NDIM == 3) {
+    const double x = 0.5 * (g[1 * NDIM + NDIM - 1] + g[3 * NDIM + 0]);
+    S += 2.0 * (x * x);
+    const double y = 0.5 * (g[2 * NDIM + NDIM - 1] + g[3 * NDIM + 1]);
+    S += 2.0 * (y * y);
+  }
+  out[i] = sqrt(2.0 * S);
+}
+
+// Residual loops: each node updates its residual, its diagonal block and the off-diagonal block of
+// (i, other) per incident edge. Blocks are 2x2 row-major; the reference adds/subtracts whole blocks,
+// zeros included (CSysMatrix::AddBlock / SubtractBlock, matrix_structure.cpp:327-357).
+// CTurbSolver::Upwind_Residual (solver_direct_turbulent.cpp:429-543) + CUpwSca_TurbSST (:865-922):
+// R_i += F, R_j -= F; A_ii += Ji, A_ij += Jj, A_ji -= Ji, A_jj -= Jj.
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_sst_upwind(int N, const int32_t* __restrict__ adj_ptr,
+                                                       const int32_t* __restrict__ adj,
+                                                       const int64_t* __restrict__ adj_blk,
+                                                       const int64_t* __restrict__ diag,
+                                                       const int32_t* __restrict__ edges,
+                                                       const double* __restrict__ normal,
+                                                       const double* __restrict__ V, int nPV,
+                                                       const double* __restrict__ T, double* __restrict__ R,
+                                                       double* __restrict__ A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  constexpr int RHO = NDIM + 2;
+  double r0 = R[2 * (size_t)i], r1 = R[2 * (size_t)i + 1];
+  double* Dp = A ? A + diag[i] * 4 : nullptr;
+  double D[4] = {0, 0, 0, 0};
+  if (Dp)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) D[q] = Dp[q];
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k];
+    const int e = a >> 1, side = a & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    const double* v0 = V + (size_t)n0 * nPV;
+    const double* v1 = V + (size_t)n1 * nPV;
+    double q = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) q += 0.5 * (v0[d + 1] + v1[d + 1]) * normal[(size_t)e * NDIM + d];
+    const double a0 = 0.5 * (q + fabs(q)), a1 = 0.5 * (q - fabs(q));
+    const double rho0 = v0[RHO], rho1 = v1[RHO];
+    const double f0 = a0 * rho0 * T[2 * (size_t)n0] + a1 * rho1 * T[2 * (size_t)n1];
+    const double f1 = a0 * rho0 * T[2 * (size_t)n0 + 1] + a1 * rho1 * T[2 * (size_t)n1 + 1];
+    // Ji = diag(a0), Jj = diag(a1) with explicit zeros
+    const double Ji[4] = {a0, 0.0, 0.0, a0}, Jj[4] = {a1, 0.0, 0.0, a1};
+    if (side == 0) {
+      r0 += f0;
+      r1 += f1;
+      if (Dp) {
+        double* O = A + adj_blk[k] * 4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          D[t] += Ji[t];
+          O[t] += Jj[t];
+        }
+      }
+    } else {
+      r0 -= f0;
+      r1 -= f1;
+      if (Dp) {
+        double* O = A + adj_blk[k] * 4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          O[t] -= Ji[t];
+          D[t] -= Jj[t];
+        }
+      }
+    }
+  }
+  R[2 * (size_t)i] = r0;
+  R[2 * (size_t)i + 1] = r1;
+  if (Dp)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Dp[q] = D[q];
+}
+
+// CTurbSolver::Viscous_Residual (:545-600) + CAvgGradCorrected_TurbSST (:1080-1163):
+// R_i -= F, R_j += F; A_ii -= Ji, A_ij -= Jj, A_ji += Ji, A_jj += Jj.
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_sst_visc(int N, SSTC c, const int32_t* __restrict__ adj_ptr,
+                                                     const int32_t* __restrict__ adj,
+                                                     const int64_t* __restrict__ adj_blk,
+                                                     const int64_t* __restrict__ diag,
+                                                     const int32_t* __restrict__ edges,
+                                                     const double* __restrict__ normal,
+                                                     const double* __restrict__ coord, const double* __restrict__ V,
+                                                     int nPV, const double* __restrict__ mu,
+                                                     const double* __restrict__ eddy, const double* __restrict__ T,
+                                                     const double* __restrict__ TG, const double* __restrict__ F1,
+                                                     double* __restrict__ R, double* __restrict__ A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  constexpr int RHO = NDIM + 2;
+  double r0 = R[2 * (size_t)i], r1 = R[2 * (size_t)i + 1];
+  double* Dp = A ? A + diag[i] * 4 : nullptr;
+  double D[4] = {0, 0, 0, 0};
+  if (Dp)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) D[q] = Dp[q];
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k];
+    const int e = a >> 1, side = a & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    const double F1i = F1[n0], F1j = F1[n1];
+    const double ski = F1i * c.sk1 + (1.0 - F1i) * c.sk2;
+    const double skj = F1j * c.sk1 + (1.0 - F1j) * c.sk2;
+    const double soi = F1i * c.so1 + (1.0 - F1i) * c.so2;
+    const double soj = F1j * c.so1 + (1.0 - F1j) * c.so2;
+    const double mui = mu[n0], muj = mu[n1], eti = eddy[n0], etj = eddy[n1];
+    const double dik = mui + ski * eti, djk = muj + skj * etj;
+    const double dio = mui + soi * eti, djo = muj + soj * etj;
+    const double dk = 0.5 * (dik + djk), dw = 0.5 * (dio + djo);
+    double ev[NDIM], nrm[NDIM], dist2 = 0.0, proj = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+      nrm[d] = normal[(size_t)e * NDIM + d];
+      ev[d] = coord[(size_t)n1 * NDIM + d] - coord[(size_t)n0 * NDIM + d];
+      dist2 += ev[d] * ev[d];
+      proj += ev[d] * nrm[d];
+    }
+    if (dist2 == 0.0) proj = 0.0; else proj = proj / dist2;
+    double corr[2];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      double pn = 0.0, pe = 0.0;
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) {
+        const double m = 0.5 * (TG[((size_t)n0 * 2 + v) * NDIM + d] + TG[((size_t)n1 * 2 + v) * NDIM + d]);
+        pn += m * nrm[d];
+        pe += m * ev[d];
+      }
+      corr[v] = pn;
+      corr[v] -= pe * proj - (T[2 * (size_t)n1 + v] - T[2 * (size_t)n0 + v]) * proj;
+    }
+    const double f0 = dk * corr[0], f1 = dw * corr[1];
+    if (side == 0) {
+      r0 -= f0;
+      r1 -= f1;
+    } else {
+      r0 += f0;
+      r1 += f1;
+    }
+    if (Dp) {
+      const double ri = V[(size_t)n0 * nPV + RHO], rj = V[(size_t)n1 * nPV + RHO];
+      const double Ji[4] = {-dk * proj / ri, 0.0, 0.0, -dw * proj / ri};
+      const double Jj[4] = {dk * proj / rj, 0.0, 0.0, dw * proj / rj};
+      double* O = A + adj_blk[k] * 4;
+      if (side == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          D[t] -= Ji[t];
+          O[t] -= Jj[t];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          O[t] += Ji[t];
+          D[t] += Jj[t];
+        }
+      }
+    }
+  }
+  R[2 * (size_t)i] = r0;
+  R[2 * (size_t)i + 1] = r1;
+  if (Dp)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Dp[q] = D[q];
+}
+
+// CTurbSSTSolver::Source_Residual (:3018-3080) + CSourcePieceWise_TurbSST (:1183-1256) over the owned
+// points: R_i -= S, A_ii -= Js.
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_sst_source(int Nd, SSTC c, const int64_t* __restrict__ diag,
+                                                       const double* __restrict__ V, int nPV,
+                                                       const double* __restrict__ G, int nG,
+                                                       const double* __restrict__ eddy,
+                                                       const double* __restrict__ strain,
+                                                       const double* __restrict__ T, const double* __restrict__ vol,
+                                                       const double* __restrict__ dist,
+                                                       const double* __restrict__ F1, const double* __restrict__ F2,
+                                                       const double* __restrict__ CDkw, double* __restrict__ R,
+                                                       double* __restrict__ A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Nd) return;
+  const double rho = V[(size_t)i * nPV + NDIM + 2];
+  const double k = T[2 * (size_t)i], w = T[2 * (size_t)i + 1], S = strain[i], Vol = vol[i], f1 = F1[i];
+  const double ab = f1 * c.al1 + (1.0 - f1) * c.al2;
+  const double bb = f1 * c.b1 + (1.0 - f1) * c.b2;
+  double s0 = 0.0, s1 = 0.0, j00 = 0.0, j11 = 0.0;
+  if (dist[i] > 1e-10) {
+    double diverg = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) diverg += G[((size_t)i * nG + d + 1) * NDIM + d];
+    double pk = eddy[i] * S * S - 2.0 / 3.0 * rho * k * diverg;
+    pk = smin(pk, 20.0 * c.bs * rho * w * k);
+    pk = smax(pk, 0.0);
+    const double zeta = smax(w, S * F2[i] / c.a1);
+    double pw = S * S - 2.0 / 3.0 * zeta * diverg;
+    pw = smax(pw, 0.0);
+    s0 += pk * Vol;
+    s1 += ab * rho * pw * Vol;
+    s0 -= c.bs * rho * w * k * Vol;
+    s1 -= bb * rho * w * w * Vol;
+    s1 += (1.0 - f1) * CDkw[i] * Vol;
+    j00 = -c.bs * w * Vol;
+    j11 = -2.0 * bb * w * Vol;
+  }
+  R[2 * (size_t)i] -= s0;
+  R[2 * (size_t)i + 1] -= s1;
+  if (A) {
+    double* D = A + diag[i] * 4;
+    D[0] -= j00;
+    D[1] -= 0.0;
+    D[2] -= 0.0;
+    D[3] -= j11;
+  }
+}
+
+// CTurbSolver::ImplicitEuler_Iteration system build (:630-668): owned rows A_ii += Vol/(CFLRed*dt_flow),
+// rhs = -R, x = 0; ghost rows rhs = x = 0.
+__global__ __launch_bounds__(kBlock) void k_sst_build_system(int Nd, int N, const int64_t* __restrict__ diag,
+                                                             const double* __restrict__ vol,
+                                                             const double* __restrict__ dt, double cfl_red,
+                                                             double* __restrict__ A, const double* __restrict__ R,
+                                                             double* __restrict__ rhs, double* __restrict__ x) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  if (i >= Nd) {
+    rhs[2 * (size_t)i] = rhs[2 * (size_t)i + 1] = 0.0;
+    x[2 * (size_t)i] = x[2 * (size_t)i + 1] = 0.0;
+    return;
+  }
+  const double delta = vol[i] / (cfl_red * dt[i]);
+  double* D = A + diag[i] * 4;
+  D[0] += delta;
+  D[3] += delta;
+  rhs[2 * (size_t)i] = -R[2 * (size_t)i];
+  rhs[2 * (size_t)i + 1] = -R[2 * (size_t)i + 1];
+  x[2 * (size_t)i] = x[2 * (size_t)i + 1] = 0.0;
+}
+
+// SST branch of the update (:698-713): AddConservativeSolution (variable_structure.cpp:214-219) with
+// the flow density (rho_old = rho: Cons2PrimVar sets V[rho] = U[rho], variable_direct_reactive.cpp:579-584,
+// and Solution_Old is the U the primitives were computed from). Limits: constructor :2731-2735.
+__global__ __launch_bounds__(kBlock) void k_sst_update(int Nd, const double* __restrict__ x, double relax,
+                                                       const double* __restrict__ V, int nPV, int rho_idx,
+                                                       double* __restrict__ T) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * Nd) return;
+  const int i = t >> 1, v = t & 1;
+  const double rho = V[(size_t)i * nPV + rho_idx];
+  const double lo = v ? 1.0e-4 : 1.0e-10, hi = v ? 1.0e15 : 1.0e10;
+  T[t] = smin(smax((T[t] * rho + relax * x[t]) / rho, lo), hi);
+}
+
+// CTurbSSTSolver::Postprocessing after its gradient (:2966-3000): SetBlendingFunc, mu_t, over every
+// point; then the MANGOTURB coupling the flow reads (turb node k, omega, mu_t, grad k, sigma_k, and the
+// flow eddy viscosity SetPrimVar copies from mu_t, variable_direct_reactive.cpp:1188-1193).
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_sst_post(int N, SSTC c, const double* __restrict__ T,
+                                                     const double* __restrict__ TG, const double* __restrict__ V,
+                                                     int nPV, const double* __restrict__ mu,
+                                                     const double* __restrict__ dist,
+                                                     const double* __restrict__ strain, double* __restrict__ F1,
+                                                     double* __restrict__ F2, double* __restrict__ CDkw,
+                                                     double* __restrict__ muT, double* __restrict__ fl_tke,
+                                                     double* __restrict__ fl_omega, double* __restrict__ fl_mut,
+                                                     double* __restrict__ fl_eddy, double* __restrict__ fl_sigmak,
+                                                     double* __restrict__ fl_gradk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const double k = T[2 * (size_t)i], w = T[2 * (size_t)i + 1];
+  const double rho = V[(size_t)i * nPV + NDIM + 2], m = mu[i], ds = dist[i];
+  const double* g = TG + (size_t)i * 2 * NDIM;
+  double cd = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) cd += g[d] * g[NDIM + d];
+  cd *= 2.0 * rho * c.so2 / w;
+  cd = smax(cd, 1.0e-20);  // pow(10.0, -20.0): glibc's correctly rounded result is the literal
+  const double eps2 = rx::kEPS * rx::kEPS;
+  const double arg2A = sqrt(k) / (c.bs * w * ds + eps2);
+  const double arg2B = 500.0 * m / (rho * ds * ds * w + eps2);
+  double arg2 = smax(arg2A, arg2B);
+  const double arg1 = smin(arg2, 4.0 * rho * c.so2 * k / (cd * ds * ds + eps2));
+  const double f1 = tanh(pow(arg1, 4.0));
+  arg2 = smax(2.0 * arg2A, arg2B);
+  const double f2 = tanh(pow(arg2, 2.0));
+  const double zeta = smin(1.0 / w, c.a1 / (strain[i] * f2));
+  const double mt = smin(smax(rho * k * zeta, 0.0), 1.0);
+  F1[i] = f1;
+  F2[i] = f2;
+  CDkw[i] = cd;
+  muT[i] = mt;
+  fl_tke[i] = k;
+  fl_omega[i] = w;
+  fl_mut[i] = mt;
+  fl_eddy[i] = mt;
+  fl_sigmak[i] = c.sk1;  // CTurbSSTVariable::Get_Sigmak = constants[0] (variable_direct_turbulent.cpp:151)
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) fl_gradk[(size_t)i * NDIM + d] = g[d];
+}
+
+bool is_sst(const rx_ctx* ctx) { return ctx && ctx->kind == RX_KIND_SST && ctx->flow; }
+
+int sst_gradient(rx_ctx* ctx) {
+  if (ctx->Nd > 0)
+    k_sol_grad_ls<2><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->coord, ctx->nbr_ptr, ctx->nbr,
+                                                                   ctx->f[RX_F_U], ctx->f[RX_F_GRAD]);
+  RX_HIP(hipGetLastError());
+  return rx_la_exchange(ctx, ctx->f[RX_F_GRAD], 2 * ctx->nDim);  // Set_MPI_Solution_Gradient
+}
+
+}  // namespace
+
+int rx_sst_build_system(rx_ctx* ctx) {
+  k_sst_build_system<<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->Nd, (int)ctx->N, ctx->diag, ctx->vol,
+                                                                 ctx->flow->f[RX_F_DT], ctx->cfg.cfl,
+                                                                 ctx->f[RX_F_JAC], ctx->f[RX_F_RES], ctx->f[RX_F_RHS],
+                                                                 ctx->f[RX_F_SOL]);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_sst_update(rx_ctx* ctx) {
+  const rx_ctx* fl = ctx->flow;
+  if (ctx->Nd > 0)
+    k_sst_update<<<blocks(2 * ctx->Nd), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->f[RX_F_SOL], ctx->cfg.relaxation,
+                                                                  fl->f[RX_F_V], fl->nPV, fl->nDim + 2, ctx->f[RX_F_U]);
+  RX_HIP(hipGetLastError());
+  return rx_la_exchange(ctx, ctx->f[RX_F_U], 2);  // Set_MPI_Solution (:718)
+}
+
+extern "C" {
+
+int rx_strain_mag(rx_ctx* ctx) {
+  if (!ctx || ctx->kind != RX_KIND_FLOW || ctx->nDim != 2) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_STRAIN);
+  k_strain<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->f[RX_F_GRAD],
+                                                          ctx->f[RX_F_STRAIN]);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_sst_preprocessing(rx_ctx* ctx) {
+  if (!is_sst(ctx)) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_SST_GRAD);
+  RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
+  if (ctx->cfg.implicit)
+    RX_HIP(hipMemsetAsync(ctx->f[RX_F_JAC], 0, sizeof(double) * ctx->fcount[RX_F_JAC], ctx->stream));
+  ctx->assembled = 1;
+  return sst_gradient(ctx);
+}
+
+int rx_sst_upwind(rx_ctx* ctx) {
+  if (!is_sst(ctx)) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_SST_UPW);
+  const rx_ctx* fl = ctx->flow;
+  k_sst_upwind<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+      (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->diag, ctx->edges, ctx->normal, fl->f[RX_F_V], fl->nPV,
+      ctx->f[RX_F_U], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_sst_viscous(rx_ctx* ctx) {
+  if (!is_sst(ctx)) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_SST_VISC);
+  const rx_ctx* fl = ctx->flow;
+  k_sst_visc<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+      (int)ctx->N, sst_constants(), ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->diag, ctx->edges, ctx->normal,
+      ctx->coord, fl->f[RX_F_V], fl->nPV, fl->f[RX_F_MU], fl->f[RX_F_EDDY], ctx->f[RX_F_U], ctx->f[RX_F_GRAD],
+      ctx->f[RX_F_F1], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_sst_source(rx_ctx* ctx) {
+  if (!is_sst(ctx)) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_SST_SOURCE);
+  const rx_ctx* fl = ctx->flow;
+  if (ctx->Nd > 0)
+    k_sst_source<2><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
+        (int)ctx->Nd, sst_constants(), ctx->diag, fl->f[RX_F_V], fl->nPV, fl->f[RX_F_GRAD], fl->nG, fl->f[RX_F_EDDY],
+        fl->f[RX_F_STRAIN], ctx->f[RX_F_U], ctx->vol, ctx->f[RX_F_WALLDIST], ctx->f[RX_F_F1], ctx->f[RX_F_F2],
+        ctx->f[RX_F_CDKW], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_sst_postprocessing(rx_ctx* ctx) {
+  if (!is_sst(ctx)) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_SST_POST);
+  int rc = sst_gradient(ctx);
+  if (rc) return rc;
+  rx_ctx* fl = ctx->flow;
+  k_sst_post<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+      (int)ctx->N, sst_constants(), ctx->f[RX_F_U], ctx->f[RX_F_GRAD], fl->f[RX_F_V], fl->nPV, fl->f[RX_F_MU],
+      ctx->f[RX_F_WALLDIST], fl->f[RX_F_STRAIN], ctx->f[RX_F_F1], ctx->f[RX_F_F2], ctx->f[RX_F_CDKW],
+      ctx->f[RX_F_MUT], fl->f[RX_F_TKE], fl->f[RX_F_OMEGA], fl->f[RX_F_MUT], fl->f[RX_F_EDDY], fl->f[RX_F_SIGMAK],
+      fl->f[RX_F_GRADK]);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+}  // extern "C"

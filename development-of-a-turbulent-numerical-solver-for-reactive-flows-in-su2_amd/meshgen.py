@@ -204,7 +204,20 @@ def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, **kw):
     dual["coord"] = pts
     dual["quads"] = quads
     dual["part_ptr"] = part_ptr
+    dual["wall_distance"] = wall_distance(pts, bnd)
     return dual
+
+
+WALLS = ("upper_wall", "lower_wall_pre", "lower_wall_post")  # the cfg's MARKER_ISOTHERMAL
+
+
+def wall_distance(pts, bnd):
+    """Distance of every point to the nearest wall vertex (CGeometry::ComputeWall_Distance: points of the
+    viscous-wall markers; wall points get 0)."""
+    from scipy.spatial import cKDTree
+    wp = np.unique(np.concatenate([np.asarray(bnd[m]).ravel() for m in WALLS]))
+    d, _ = cKDTree(pts[wp]).query(pts)
+    return np.ascontiguousarray(d, dtype=np.float64)
 
 
 def shard(mesh, n_ranks: int, rank: int):
@@ -272,7 +285,8 @@ def shard(mesh, n_ranks: int, rank: int):
         send_idx.extend((mine - g0).tolist())
         send_ptr.append(len(send_idx))
     lpp = pp[pr[rank][0]:pr[rank][-1] + 2] - g0
-    return dict(edges=le, edge_normal=ln, coord=np.asarray(mesh["coord"])[l2g],
+    extra = {"wall_distance": np.asarray(mesh["wall_distance"])[l2g]} if "wall_distance" in mesh else {}
+    return dict(**extra, edges=le, edge_normal=ln, coord=np.asarray(mesh["coord"])[l2g],
                 volume=np.asarray(mesh["volume"])[l2g], nbr_ptr=nptr_l, nbr=nbr_l.astype(np.int64), bvertex=lbv,
                 bvertex_normal=np.asarray(mesh["bvertex_normal"])[keep], part_ptr=lpp.astype(np.int64),
                 n_domain=n_own, l2g=l2g, neigh=np.asarray(neigh, dtype=np.int32),

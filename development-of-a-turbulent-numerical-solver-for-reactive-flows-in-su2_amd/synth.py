@@ -20,7 +20,7 @@ REPO = os.path.dirname(HERE)
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 NODE_KEYS = ("V", "U", "dPdU", "dTdU", "mu", "kappa", "Dij", "turb_k", "turb_omega", "mu_t", "sigma_k", "grad_k",
-             "eddy_visc_flow")
+             "eddy_visc_flow", "sst_F1", "sst_F2", "sst_CDkw")
 
 
 def _meshgen():
@@ -88,6 +88,7 @@ def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1):
     from scipy.spatial import cKDTree
     _, idx = cKDTree(sn).query(dn)
     state = {k: np.ascontiguousarray(g[k][idx]) for k in NODE_KEYS if k in g}
+    state["sst_sol"] = np.ascontiguousarray(np.stack([state["turb_k"], state["turb_omega"]], axis=1))
     mesh["n_dim"] = 2
     mech = {k: g[k] for k in g if k.startswith("mech_")}
     return mesh, state, mech, {"mach_inf": float(g["mach_inf"][0]), "prandtl_turb": float(g["visc_params"][1]),

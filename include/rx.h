@@ -120,6 +120,11 @@ typedef enum {
   RX_F_ILU,        /* ILU(0) factor, same layout */
   RX_F_SOL,        /* LinSysSol [N][nVar] */
   RX_F_RHS,        /* linear-system right-hand side [N][nVar] */
+  RX_F_STRAIN,     /* flow: StrainMag [N] (CReactiveNSVariable::SetStrainMag) */
+  RX_F_F1,         /* SST: Menter blending F1 [N] */
+  RX_F_F2,         /* SST: Menter blending F2 [N] */
+  RX_F_CDKW,       /* SST: cross diffusion CDkw [N] */
+  RX_F_WALLDIST,   /* SST: wall distance [N] (CGeometry::ComputeWall_Distance output) */
   RX_F_COUNT
 } rx_field;
 
@@ -180,6 +185,35 @@ int rx_halo_exchange(rx_ctx *ctx, rx_field f); /* owned -> halo copies of a node
 int rx_explicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */);
 int rx_implicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */, int *lin_iters);
 
+/* Menter SST turbulence solver (SURVEY.md §8 a14 + next-2): CTurbSSTSolver / CTurbSolver
+ * (SU2_CFD/src/solver_direct_turbulent.cpp) on the flow context's state. A second context with
+ * nVar = 2, U = (k, omega) [N][2], GRAD [N][2][nDim], its own BSR Jacobian (2x2 blocks), ILU / LU-SGS
+ * and FGMRES, sharing the flow context's stream (and communicator, which must be attached to the flow
+ * context before rx_sst_create). rx_cfg fields read: implicit, lin_tol, lin_iter, lin_prec,
+ * relaxation (= RELAXATION_FACTOR_TURB), cfl (= CFL_REDUCTION_TURB). Upload RX_F_U, RX_F_WALLDIST and,
+ * before the first Upwind, RX_F_F1/F2/CDKW (or run rx_sst_postprocessing). Reads the flow's V, MU,
+ * EDDY, GRAD, STRAIN, DT.
+ *   rx_strain_mag        (flow ctx) CReactiveNSVariable::SetStrainMag variable_direct_reactive.cpp:1060-1095,
+ *                        called from CReactiveNSSolver::Preprocessing solver_direct_reactive.cpp:4720-4735
+ *   rx_sst_preprocessing CTurbSSTSolver::Preprocessing solver_direct_turbulent.cpp:2923-2951 (zero +
+ *                        CSolver::SetSolution_Gradient_LS solver_structure.cpp:580-720)
+ *   rx_sst_upwind        CTurbSolver::Upwind_Residual :429-543 + CUpwSca_TurbSST::ComputeResidual
+ *                        numerics_direct_turbulent.cpp:865-922
+ *   rx_sst_viscous       CTurbSolver::Viscous_Residual :545-600 + CAvgGradCorrected_TurbSST :1080-1163
+ *   rx_sst_source        CTurbSSTSolver::Source_Residual :3018-3080 + CSourcePieceWise_TurbSST :1183-1256
+ *   rx_sst_implicit_euler CTurbSolver::ImplicitEuler_Iteration :615-728 (CSysSolve::Solve)
+ *   rx_sst_postprocessing CTurbSSTSolver::Postprocessing :2953-3016 (gradient, SetBlendingFunc
+ *                        variable_direct_turbulent.cpp:178-203, mu_t); then writes the flow context's
+ *                        TKE, OMEGA, MUT, GRADK, SIGMAK and EDDY (the MANGOTURB coupling getters). */
+int rx_sst_create(const rx_mesh_desc *mesh, rx_ctx *flow, const rx_cfg *cfg, rx_ctx **out);
+int rx_strain_mag(rx_ctx *flow);
+int rx_sst_preprocessing(rx_ctx *turb);
+int rx_sst_upwind(rx_ctx *turb);
+int rx_sst_viscous(rx_ctx *turb);
+int rx_sst_source(rx_ctx *turb);
+int rx_sst_implicit_euler(rx_ctx *turb, double *res_rms /* [2] or NULL */, int *lin_iters);
+int rx_sst_postprocessing(rx_ctx *turb);
+
 /* Per-phase device timing with HIP events on the context stream (for bench roofline). */
 typedef enum {
   RX_K_CONV = 0, RX_K_VISC, RX_K_SOURCE, RX_K_GRAD, RX_K_LIMITER, RX_K_DT, RX_K_SPMV, RX_K_ILU_BUILD,
@@ -187,6 +221,12 @@ typedef enum {
   RX_K_SOLVE,    /* rx_implicit_euler's captured solve: FGMRES + RMS + clipped update (one hipGraph) */
   RX_K_VISC_JAC, /* viscous Jacobian kernel (implicit) */
   RX_K_ASSEMBLE, /* residual + BSR Jacobian assembly */
+  RX_K_STRAIN,   /* flow StrainMag */
+  RX_K_SST_GRAD, /* SST: least-squares gradient of (k, omega) */
+  RX_K_SST_UPW, RX_K_SST_VISC, RX_K_SST_SOURCE, /* SST residual + Jacobian loops */
+  RX_K_SST_SYSTEM, /* SST: system build + preconditioner build */
+  RX_K_SST_SOLVE,  /* SST: FGMRES + RMS + conservative clipped update */
+  RX_K_SST_POST,   /* SST: Postprocessing (gradient, blending, mu_t, flow coupling fields) */
   RX_K_COUNT
 } rx_kernel;
 int rx_profile_enable(rx_ctx *ctx, int on);

@@ -50,3 +50,22 @@ def test_ctypes_structs_match_header_layout(tmp_path):
         assert got[(cname, "size")] == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def test_python_enums_match_header():
+    """rx_field / rx_kernel order in the Python mirror is the header's."""
+    import re
+    txt = open(rx.HEADER).read()
+
+    def names(enum, prefix):
+        body = re.search(r"typedef enum \{([^{}]*)\}\s*%s;" % enum, txt).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        out = []
+        for tok in body.split(","):
+            tok = tok.strip().split("=")[0].strip()
+            if tok:
+                out.append(tok[len(prefix):])
+        return [n for n in out if n != "COUNT"]
+
+    assert names("rx_field", "RX_F_") == rx.FIELDS
+    assert names("rx_kernel", "RX_K_") == rx.KERNELS
