@@ -1,10 +1,15 @@
 """Throughput of the reactive RANS hot path on MI355X: Mcells*iters/s (BASELINE.json metric).
 
-One step = one outer implicit iteration of the device-resident hot path over the whole mesh
-(the order CIntegration drives them):
-  SetPrimitive_Gradient_LS -> SetTime_Step -> residual zero -> Upwind_Residual (AUSM + Jacobians)
-  -> Viscous_Residual (reactive viscous + SST closure + Jacobians) -> Source_Residual (PaSR + Jacobian)
-  -> ImplicitEuler_Iteration (assembly, Vol/dt, ILU(0) build, FGMRES(5), clipped update, RMS).
+One step = one outer implicit iteration (flow + SST, as CMeanFlowIteration::Iterate runs them) of the
+device-resident hot path over the whole mesh (the order CIntegration drives
+them):
+  flow: SetPrimitive_Gradient_LS -> SetStrainMag -> SetTime_Step -> residual zero -> Upwind_Residual
+        (AUSM + Jacobians) -> Viscous_Residual (reactive viscous + SST closure + Jacobians) ->
+        Source_Residual (PaSR + Jacobian) -> ImplicitEuler_Iteration (assembly, Vol/dt, ILU(0) build,
+        FGMRES(5), clipped update, RMS);
+  SST:  Preprocessing (LS gradient) -> Upwind / Viscous / Source residuals with 2x2 Jacobians ->
+        ImplicitEuler_Iteration (system, ILU(0), FGMRES(5), conservative clipped update, RMS) ->
+        Postprocessing (gradient, F1/F2/CDkw, mu_t, coupling fields the flow reads next step).
 
 Default workload (N=1): BASELINE configs[1] — synthetic 2-D reactive jet, 500x200 = 100k points,
 7 species PaSR + SST, implicit FGMRES+ILU0. `--workload c3` runs configs[2] (2000x500, 1M points).
@@ -99,7 +104,8 @@ def build_workload(nx, ny, ns, n_part=1):
 
 
 def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg):
-    """One implicit step of the CPU restatement (oracle/, one core) on the same mesh."""
+    """One outer iteration (flow implicit step + SST step) of the CPU restatement (oracle/, one core) on
+    the same mesh."""
     from oracle import oracle as O
     om = O.Mechanism(mech_arrays)
     c = dict(cfl=cfg.cfl, max_delta_time=cfg.max_delta_time, prandtl_lam=cfg.prandtl_lam,
@@ -107,11 +113,16 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg):
              pasr_lb=cfg.pasr_lb, lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter, relaxation=cfg.relaxation)
     pattern = O.bsr_pattern(len(st["V"]), mesh["edges"])
     t0 = time.perf_counter()
-    O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern, part_ptr=mesh.get("part_ptr"))
+    _, info = O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern, part_ptr=mesh.get("part_ptr"))
+    flow = dict(V=st["V"], grad=info["grad"], mu=st["mu"], eddy=st["eddy_visc_flow"],
+                strain=O.strain_mag(2, info["grad"]))
+    O.sst_step(2, mesh, flow, st["sst_sol"], None, st["sst_F1"], st["sst_F2"], st["sst_CDkw"], info["dt"],
+               dict(lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter), pattern=pattern, part_ptr=mesh.get("part_ptr"))
     dt = time.perf_counter() - t0
     N = len(st["V"])
     return dict(value=N / dt / 1e6, unit="Mcells*iters/s", cores=1, kind="port",
-                sample=f"1 implicit step of the same {N}-cell mesh on 1 host core ({dt:.2f} s)")
+                sample=f"1 outer iteration (flow implicit step + SST step) of the same {N}-cell mesh on 1 host "
+                       f"core ({dt:.2f} s)")
 
 
 def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist):
@@ -125,8 +136,13 @@ def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist):
     uid = [rx.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     s.comm_init(world, rank, uid[0])
-    s.set_state(st_l)
-    return s, mesh, st_l, mech_arrays, kw, cfg, int(sh["n_domain"])
+    t = rx.TurbSSTSolver(sh, s, rx.sst_cfg())
+    return s, t, sh, st_l, mech_arrays, kw, cfg, int(sh["n_domain"])
+
+
+def set_states(s, t, mesh, st):
+    s.set_state(st)
+    t.set_state(st["sst_sol"], mesh["wall_distance"], st["sst_F1"], st["sst_F2"], st["sst_CDkw"])
 
 
 def main():
@@ -166,7 +182,9 @@ def main():
     if world > 1:
         err = ""
         try:
-            s, mesh, st, mech_arrays, kw, cfg, n_owned = setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist)
+            s, t, mesh, st, mech_arrays, kw, cfg, n_owned = setup_sharded(rx, args, nx, ny, ns, world, rank, local,
+                                                                          dist)
+            set_states(s, t, mesh, st)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             err = repr(e)[:200]
         flags = [None] * world
@@ -183,7 +201,8 @@ def main():
         mesh, st, mech_arrays, kw = build_workload(nx, ny, ns, args.parts)
         cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
         s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg, device=local)
-        s.set_state(st)
+        t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+        set_states(s, t, mesh, st)
         n_owned = s.N
     N, E = s.N, s.E
     rp, col = s.bsr_pattern()
@@ -194,21 +213,29 @@ def main():
 
     def step():
         s.SetPrimitive_Gradient_LS()
+        s.SetStrainMag()
         s.SetTime_Step()
         s.Preprocessing_zero()
         s.Upwind_Residual()
         s.Viscous_Residual()
         s.Source_Residual()
         rms, it = s.ImplicitEuler_Iteration()
-        lin_its.append(it)
-        rms_log.append(rms)
+        t.Preprocessing()
+        t.Upwind_Residual()
+        t.Viscous_Residual()
+        t.Source_Residual()
+        trms, tit = t.ImplicitEuler_Iteration()
+        t.Postprocessing()
+        lin_its.append((it, tit))
+        rms_log.append(np.r_[rms, trms])
 
     graph = True
     if parallelism.startswith("sharded"):
-        # eager step, then a graph-replayed step: same system (node records fixed), same RMS bitwise
+        # eager step, then a graph-replayed step from the same state: same systems, same RMS bitwise
         os.environ["RX_NO_GRAPH"] = "1"
         step()
         os.environ.pop("RX_NO_GRAPH")
+        set_states(s, t, mesh, st)
         step()
         ok = bool(np.array_equal(rms_log[0], rms_log[1]) and lin_its[0] == lin_its[1])
         oks = [None] * world
@@ -223,6 +250,7 @@ def main():
     if dist:
         dist.barrier()
     s.profile(True)
+    t.profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -231,11 +259,14 @@ def main():
     el = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        tel = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tel, op=dist.ReduceOp.MAX)
+        el = float(tel.item())
     prof = {k: s.profile_read(k) for k in rx.K}
+    tprof = {k: t.profile_read(k) for k in rx.K}
+    prof = {k: (prof[k][0] + tprof[k][0], prof[k][1] + tprof[k][1]) for k in rx.K}
     s.profile(False)
+    t.profile(False)
 
     models = kernel_models(N, E, nnzb, ns, 2, 5)
     phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0}
@@ -286,11 +317,13 @@ def main():
         "config": {"workload": f"{args.workload}: 2-D reactive jet {nx}x{ny}" + (
                        f" per GPU (global {nx}x{ny * world})" if parallelism.startswith("sharded") else ""),
                    "cells_per_gpu": n_owned, "halo_points": N - n_owned, "edges": E,
-                   "species": ns, "nVar": ns + 4, "nnz_blocks": nnzb, "time": "EULER_IMPLICIT",
-                   "linear_solver": "FGMRES(5)+ILU0",
+                   "species": ns, "nVar": ns + 4, "nnz_blocks": nnzb,
+                   "time": "EULER_IMPLICIT flow + SST (one outer iteration per step)",
+                   "linear_solver": "FGMRES(5)+ILU0 (flow 11x11 and SST 2x2 systems)",
                    "partitions": args.parts,
                    "parallelism": parallelism, "solve_graph": graph, "cells_total": cells,
-                   "lin_iters_mean": float(np.mean(lin_its[-args.steps:]))},
+                   "lin_iters_mean": float(np.mean([a for a, _ in lin_its[-args.steps:]])),
+                   "sst_lin_iters_mean": float(np.mean([b for _, b in lin_its[-args.steps:]]))},
         "roofline": kernels[dom],
         "roofline_edge_flux": kernels.get("CONV"),
         "roofline_kernels": kernels,

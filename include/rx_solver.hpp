@@ -12,6 +12,15 @@
  *   Source_Residual               -> rx_cell_source_pasr         (:2792-2874)  throws "NaN found in the source residual"
  *   ExplicitEuler_Iteration       -> rx_explicit_euler           (:2414-2449)
  *   ImplicitEuler_Iteration       -> rx_implicit_euler           (:2336-2407)
+ *   SetStrainMag                  -> rx_strain_mag               (variable_direct_reactive.cpp:1060-1095)
+ * TurbSSTSolver mirrors CTurbSSTSolver / CTurbSolver (SU2_CFD/include/solver_structure.hpp, turbulent
+ * classes; SU2_CFD/src/solver_direct_turbulent.cpp):
+ *   Preprocessing                 -> rx_sst_preprocessing        (:2923-2951)
+ *   Upwind_Residual               -> rx_sst_upwind               (:429-543)
+ *   Viscous_Residual              -> rx_sst_viscous              (:545-600)
+ *   Source_Residual               -> rx_sst_source               (:3018-3080)
+ *   ImplicitEuler_Iteration       -> rx_sst_implicit_euler       (:615-728)
+ *   Postprocessing                -> rx_sst_postprocessing       (:2953-3016)
  * A spline lookup outside the property tables throws std::out_of_range (MathTools::GetSpline,
  * Common/src/spline.cpp:62-77); any other failure throws std::runtime_error with rx_status_string.
  * Ownership: the solver owns one rx_ctx (device state); host arrays are copied at construction /
@@ -59,6 +68,7 @@ class ReactiveNSSolver {
   void SetPrimitive_Gradient_LS() { check(rx_grad_lsq(ctx_), "SetPrimitive_Gradient_LS"); }
   void SetPrimitive_Limiter() { check(rx_limiter_venkat(ctx_), "SetPrimitive_Limiter"); }
   void SetTime_Step() { check(rx_time_step(ctx_), "SetTime_Step"); }
+  void SetStrainMag() { check(rx_strain_mag(ctx_), "SetStrainMag"); }
   void Upwind_Residual() { phase(rx_edge_flux_conv(ctx_), "NaN found in the upwind residual"); }
   void Viscous_Residual() { phase(rx_edge_flux_visc(ctx_), "NaN found in the viscous residual"); }
   void Source_Residual() { phase(rx_cell_source_pasr(ctx_), "NaN found in the source residual"); }
@@ -100,6 +110,49 @@ class ReactiveNSSolver {
   rx_ctx* ctx_ = nullptr;
   rx_cfg cfg_;
   int nvar_ = 0;
+};
+
+// Menter SST solver bound to a flow solver: its own device context (k, omega), on the flow context's
+// stream and communicator (attach the flow's communicator first).
+class TurbSSTSolver {
+ public:
+  TurbSSTSolver(const rx_mesh_desc& mesh, ReactiveNSSolver& flow, const rx_cfg& cfg) {
+    check(rx_sst_create(&mesh, flow.context(), &cfg, &ctx_), "rx_sst_create");
+  }
+  ~TurbSSTSolver() { rx_ctx_destroy(ctx_); }
+  TurbSSTSolver(const TurbSSTSolver&) = delete;
+  TurbSSTSolver& operator=(const TurbSSTSolver&) = delete;
+
+  rx_ctx* context() const { return ctx_; }
+  void Upload(rx_field f, const std::vector<double>& host) {
+    check(rx_upload(ctx_, f, host.data(), (int64_t)host.size()), "rx_upload");
+  }
+  std::vector<double> Download(rx_field f) const {
+    int64_t n = 0;
+    check(rx_field_size(ctx_, f, &n), "rx_field_size");
+    std::vector<double> h((size_t)n);
+    check(rx_download(ctx_, f, h.data(), n), "rx_download");
+    return h;
+  }
+  void Preprocessing() { check(rx_sst_preprocessing(ctx_), "Preprocessing"); }
+  void Upwind_Residual() { check(rx_sst_upwind(ctx_), "Upwind_Residual"); }
+  void Viscous_Residual() { check(rx_sst_viscous(ctx_), "Viscous_Residual"); }
+  void Source_Residual() { check(rx_sst_source(ctx_), "Source_Residual"); }
+  std::vector<double> ImplicitEuler_Iteration(int* lin_iters = nullptr) {
+    std::vector<double> rms(2);
+    int it = 0;
+    check(rx_sst_implicit_euler(ctx_, rms.data(), &it), "ImplicitEuler_Iteration");
+    if (lin_iters) *lin_iters = it;
+    return rms;
+  }
+  void Postprocessing() { check(rx_sst_postprocessing(ctx_), "Postprocessing"); }
+
+ private:
+  void check(int rc, const char* what) const {
+    if (rc == RX_OK) return;
+    throw std::runtime_error(std::string(what) + ": " + rx_status_string(rc));
+  }
+  rx_ctx* ctx_ = nullptr;
 };
 
 }  // namespace rx

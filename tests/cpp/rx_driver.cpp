@@ -113,7 +113,9 @@ int main(int argc, char** argv) {
                  {"grad_k", RX_F_GRADK}, {"eddy_visc_flow", RX_F_EDDY}};
     for (const auto& s : state) solver.Upload(s.f, f64(d, s.name));
 
+    // CReactiveNSSolver::Preprocessing tail (StrainMag from the gradient, solver_direct_reactive.cpp:4720-4735),
     // CIntegration::Space_Integration order (integration_structure.cpp:72-193), then Time_Integration
+    solver.SetStrainMag();
     solver.SetTime_Step();
     solver.Preprocessing();
     solver.Upwind_Residual();
@@ -128,6 +130,31 @@ int main(int argc, char** argv) {
     save(d, "out_u", solver.Download(RX_F_U));
     save(d, "out_rms", rms);
     std::printf("ok lin_iters=%d\n", lin_iters);
+    if (implicit) {
+      // CSingleGridIntegration::SingleGrid_Iteration for TURB_SOL (integration_time.cpp:777-810)
+      rx_cfg tcfg = cfg;
+      tcfg.relaxation = 1.0;  // RELAXATION_FACTOR_TURB
+      tcfg.cfl = 1.0;         // CFL_REDUCTION_TURB
+      auto wall = f64(d, "wall_distance");
+      mesh.n_bvert = (int64_t)bvert.size() / 2;
+      rx::TurbSSTSolver turb(mesh, solver, tcfg);
+      turb.Upload(RX_F_U, f64(d, "sst_sol"));
+      turb.Upload(RX_F_WALLDIST, wall);
+      turb.Upload(RX_F_F1, f64(d, "sst_F1"));
+      turb.Upload(RX_F_F2, f64(d, "sst_F2"));
+      turb.Upload(RX_F_CDKW, f64(d, "sst_CDkw"));
+      turb.Preprocessing();
+      turb.Upwind_Residual();
+      turb.Viscous_Residual();
+      turb.Source_Residual();
+      int tit = 0;
+      auto trms = turb.ImplicitEuler_Iteration(&tit);
+      turb.Postprocessing();
+      save(d, "out_sst_u", turb.Download(RX_F_U));
+      save(d, "out_sst_rms", trms);
+      save(d, "out_sst_mut", turb.Download(RX_F_MUT));
+      std::printf("ok sst lin_iters=%d\n", tit);
+    }
   } catch (const std::exception& e) {
     std::printf("exception: %s\n", e.what());
     return 1;

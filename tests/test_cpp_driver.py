@@ -37,7 +37,8 @@ def write_case(d, g):
         w(k, g[k], np.int64)
     w("bvertex", np.asarray(g["bvertex"])[:, :2], np.int64)
     for k in ("edge_normal", "coord", "volume", "bvertex_normal", "U", "V", "dPdU", "dTdU", "mu", "kappa", "Dij",
-              "grad_prim", "turb_k", "turb_omega", "mu_t", "sigma_k", "grad_k"):
+              "grad_prim", "turb_k", "turb_omega", "mu_t", "sigma_k", "grad_k", "wall_distance", "sst_sol", "sst_F1",
+              "sst_F2", "sst_CDkw"):
         w(k, g[k], np.float64)
     w("eddy_visc_flow", g.get("eddy_visc_flow", g["mu_t"]), np.float64)
     for k in ("mmass", "diff_vol", "stoich_reac", "stoich_prod", "exp_reac", "exp_prod", "A", "beta", "Ta", "A_back",
@@ -71,3 +72,9 @@ def test_cpp_driver_matches_reference(tmp_path, implicit):
         assert_close(U, U_ref, what="C++ driver explicit update")
     else:
         assert np.all(np.isfinite(U)) and "lin_iters=5" in r.stdout
+        # the SST iteration (TurbSSTSolver, ILU0) against the reference's own turbulent step
+        T = np.fromfile(os.path.join(d, "out_sst_u.f64")).reshape(-1, 2)
+        for v in range(2):
+            assert_close(T[:, v], g["sst_new_sol_ilu"][:, v], what=f"C++ driver SST (k, omega)[{v}]")
+        assert_close(np.fromfile(os.path.join(d, "out_sst_rms.f64")), g["sst_rms_ilu"], what="C++ driver SST RMS")
+        assert_close(np.fromfile(os.path.join(d, "out_sst_mut.f64")), g["sst_post_mut_ilu"], what="C++ driver mu_t")

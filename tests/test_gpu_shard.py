@@ -6,8 +6,9 @@
 - World size 2 on the one GPU of the test box (RCCL refuses two ranks on one device, so the ranks use
   the host-staged transport over gloo, the reference's own MPI pattern): gradients are bitwise the
   global ones on every local row (owned rows recomputed in the same neighbour order, halo rows
-  received from their owner); one implicit step agrees with the single-context run on the same
-  partitions to the FGMRES bar (edge order differs per rank, so fluxes agree to rounding).
+  received from their owner); one outer iteration (flow implicit step + SST step) agrees with the
+  single-context run on the same partitions to the FGMRES bar (edge order differs per rank, so fluxes
+  agree to rounding).
 """
 import multiprocessing as mp
 import os
@@ -32,43 +33,59 @@ def _case():
     return mesh, st, mech_arrays, cfg
 
 
-def _step(s):
+def _step(s, t):
+    """One outer iteration: flow implicit step, then the SST step on the same ranks / communicator."""
     s.SetPrimitive_Gradient_LS()
     grad = s.download("GRAD")
+    s.SetStrainMag()
     s.SetTime_Step()
     s.Preprocessing_zero()
     s.Upwind_Residual()
     s.Viscous_Residual()
     s.Source_Residual()
     rms, it = s.ImplicitEuler_Iteration()
-    return grad, rms, it
+    t.Preprocessing()
+    t.Upwind_Residual()
+    t.Viscous_Residual()
+    t.Source_Residual()
+    trms, tit = t.ImplicitEuler_Iteration()
+    t.Postprocessing()
+    return grad, np.r_[rms, trms], (it, tit)
+
+
+def _set(s, t, mesh, st):
+    s.set_state(st)
+    t.set_state(st["sst_sol"], mesh["wall_distance"], st["sst_F1"], st["sst_F2"], st["sst_CDkw"])
 
 
 def _global_run():
     mesh, st, mech_arrays, cfg = _case()
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg)
-    s.set_state(st)
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+    _set(s, t, mesh, st)
     U0 = s.download("U")
-    grad, rms, it = _step(s)
+    grad, rms, it = _step(s, t)
     U = s.download("U")
+    T = t.download("U")
     s.close()
-    return grad, rms, it, U0, U
+    return grad, rms, it, U0, U, T
 
 
 def test_rccl_world1_matches_single_context():
-    g0, rms0, it0, _, U0 = _global_run()
+    g0, rms0, it0, _, U0, T0 = _global_run()
     mesh, st, mech_arrays, cfg = _case()
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg)
     s.comm_init(1, 0, rx.comm_unique_id())
-    s.set_state(st)
-    for rep in range(2):  # second step replays the captured graph with the collectives in it
-        s.set_state(st)
-        g, rms, it = _step(s)
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())  # borrows the flow context's communicator
+    for rep in range(2):  # second step replays the captured graphs with the collectives in them
+        _set(s, t, mesh, st)
+        g, rms, it = _step(s, t)
         U = s.download("U")
         assert it == it0
         assert np.array_equal(g, g0)
         assert np.array_equal(rms, rms0), f"rep {rep}"
         assert np.array_equal(U, U0), f"rep {rep}"
+        assert np.array_equal(t.download("U"), T0), f"rep {rep}"
     s.close()
 
 
@@ -83,11 +100,13 @@ def _rank_worker(rank, world, port, q):
         st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
         s = rx.ReactiveNSSolver(sh, rx.Mechanism(mech_arrays), cfg)
         s.comm_init_host(world, rank, rx.TorchHostTransport())
-        s.set_state(st_l)
-        grad, rms, it = _step(s)
+        t = rx.TurbSSTSolver(sh, s, rx.sst_cfg())
+        _set(s, t, sh, st_l)
+        grad, rms, it = _step(s, t)
         U = s.download("U")
+        T = t.download("U")
         s.close()
-        q.put((rank, dict(l2g=sh["l2g"], nd=sh["n_domain"], grad=grad, rms=rms, it=it, U=U)))
+        q.put((rank, dict(l2g=sh["l2g"], nd=sh["n_domain"], grad=grad, rms=rms, it=it, U=U, T=T)))
     except Exception as e:  # reported to the parent
         q.put((rank, repr(e)))
     finally:
@@ -95,7 +114,7 @@ def _rank_worker(rank, world, port, q):
 
 
 def test_two_ranks_host_transport_match_single_context():
-    g0, rms0, it0, U_init, U0 = _global_run()
+    g0, rms0, it0, U_init, U0, T0 = _global_run()
     nvar = NS + 4
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -116,6 +135,8 @@ def test_two_ranks_host_transport_match_single_context():
     U0 = U0.reshape(-1, nvar)
     U_init = U_init.reshape(-1, nvar)
     U_sh = np.zeros_like(U0)
+    T0 = T0.reshape(-1, 2)
+    T_sh = np.zeros_like(T0)
     for r in range(2):
         d = res[r]
         l2g, nd = d["l2g"], d["nd"]
@@ -126,14 +147,21 @@ def test_two_ranks_host_transport_match_single_context():
         assert np.array_equal(d["rms"], res[0]["rms"])
         U_l = d["U"].reshape(len(l2g), nvar)
         U_sh[l2g[:nd]] = U_l[:nd]
+        T_l = d["T"].reshape(len(l2g), 2)
+        T_sh[l2g[:nd]] = T_l[:nd]
+        res[r]["thalo"] = (l2g[nd:], T_l[nd:])
         # halo rows of U hold the owner's updated values after Set_MPI_Solution
         U_sh_halo = U_l[nd:]
         res[r]["halo"] = (l2g[nd:], U_sh_halo)
     for r in range(2):
         hg, hv = res[r]["halo"]
         assert np.array_equal(hv, U_sh[hg])
+        hg, hv = res[r]["thalo"]
+        assert np.array_equal(hv, T_sh[hg])
     assert_close(res[0]["rms"], rms0, rtol=1e-10, what="RMS (two ranks vs one context)")
     # Each rank orders its local edges by local ids (halo points last), as the reference's partitioned
     # CGeometry does, so residual/Jacobian sums round differently from the one-context run (RMS above
     # agrees to 1e-10); FGMRES(5)+ILU(0) amplifies that to ~1e-8 in the update (measured 1.1e-8).
     per_column_close(U_sh - U_init, U0 - U_init, rtol=5e-8, floor=1e-14, what="dU (two ranks vs one context)")
+    # the SST step on the same shards (RMS all-reduced, (k, omega) halos exchanged after the update)
+    per_column_close(T_sh, T0, rtol=5e-8, floor=1e-14, what="(k, omega) (two ranks vs one context)")

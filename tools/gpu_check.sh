@@ -6,6 +6,7 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests -q -m gpu -rA --tb=short > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"
 case $rc in 0|1) ;; *) exit $rc;; esac
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo "smoke ok" &&
 timeout -k 10 300 python tools/ilu_trace.py > gpurun_out/trace.log 2>&1 && echo "trace ok" &&
 timeout -k 10 400 python bench.py --steps 20 --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} > gpurun_out/bench.log 2>&1 && echo "bench ok" &&
 R=$PWD && cd /tmp && export TMPDIR=/tmp &&
