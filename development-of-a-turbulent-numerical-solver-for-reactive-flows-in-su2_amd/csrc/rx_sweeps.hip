@@ -406,7 +406,21 @@ __global__ __launch_bounds__(768) void k_ilu_build_part(const int32_t* __restric
         wave_sync();
       }
       RX_STAMP(2);
-      wave_inverse_lds<NV>(rowbuf + (size_t)(kd - k0) * NV2, Wb, invD + (size_t)i * NV2, lane);
+      {  // inv(D_i): right-looking elimination with register broadcasts, then one unit column per lane
+        const double* D = rowbuf + (size_t)(kd - k0) * NV2;
+        double row[NV];
+#pragma unroll
+        for (int kk = 0; kk < NV; ++kk) row[kk] = lane < NV ? D[lane * NV + kk] : 1.0;
+        wave_factor_rows<NV>(row, lane);
+        double rhs[NV];
+#pragma unroll
+        for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == lane) ? 1.0 : 0.0;
+        wave_solve_rows<NV>(row, rhs);
+        if (lane < NV) {
+#pragma unroll
+          for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + lane] = rhs[rr];
+        }
+      }
       RX_STAMP(3);
       for (int q = lane; q < nbk * NV2; q += 64) F[(size_t)k0 * NV2 + q] = rowbuf[q];
       wave_sync();
@@ -417,6 +431,91 @@ __global__ __launch_bounds__(768) void k_ilu_build_part(const int32_t* __restric
   }
   if (trace && blockIdx.x == 0 && threadIdx.x == 0) trace[0] = (long long)__builtin_amdgcn_s_memtime();
 #undef RX_STAMP
+}
+
+// ILU(0) factorisation for small blocks (NV <= 4, the SST system's 2x2): one thread per row, rows of a
+// dependency level spread over the workgroup. Same arithmetic as k_ilu_build_part: W = A_ij inv(A_jj)
+// (sums from 0.0, q ascending), A_ik -= A_jk W over the update plan in the reference's order, then
+// inv(D_i) by Gauss elimination of every unit column (the factor computed once, left-looking per row:
+// each (ii, jj) step sees the operands of Gauss_Elimination :594-643). The thread updates its row in F
+// directly; rows of later levels read finished rows after the level barrier.
+template <int NV>
+__global__ __launch_bounds__(256) void k_ilu_build_small(const int32_t* __restrict__ part_lvl,
+                                                         const int32_t* __restrict__ lvl_ptr,
+                                                         const int4* __restrict__ slot,
+                                                         const int32_t* __restrict__ rp,
+                                                         const int32_t* __restrict__ col,
+                                                         const int32_t* __restrict__ upd_ptr,
+                                                         const int2* __restrict__ upd, const double* __restrict__ A,
+                                                         double* __restrict__ F, double* __restrict__ invD) {
+  constexpr int NV2 = NV * NV;
+  const int p = blockIdx.x;
+  for (int l = part_lvl[p]; l < part_lvl[p + 1]; ++l) {
+    for (int r = lvl_ptr[l] + threadIdx.x; r < lvl_ptr[l + 1]; r += blockDim.x) {
+      const int4 sl = slot[r];
+      const int i = sl.x, k0 = sl.y, kd = sl.z, k1 = sl.w;
+      const int ra = rp[i], rb = rp[i + 1];
+      for (int q = ra * NV2; q < rb * NV2; ++q) F[q] = A[q];
+      for (int k = k0; k < kd; ++k) {
+        const int j = col[k];
+        double Sinv[NV2], Bij[NV2], W[NV2];
+#pragma unroll
+        for (int q = 0; q < NV2; ++q) {
+          Sinv[q] = invD[(size_t)j * NV2 + q];
+          Bij[q] = F[(size_t)k * NV2 + q];
+        }
+#pragma unroll
+        for (int a = 0; a < NV; ++a)
+#pragma unroll
+          for (int c = 0; c < NV; ++c) {
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) s += Bij[a * NV + q] * Sinv[q * NV + c];
+            W[a * NV + c] = s;
+          }
+        for (int u = upd_ptr[k]; u < upd_ptr[k + 1]; ++u) {
+          const int2 h = upd[u];
+          double Bjk[NV2];
+#pragma unroll
+          for (int q = 0; q < NV2; ++q) Bjk[q] = F[(size_t)h.x * NV2 + q];
+          double* Bik = F + (size_t)h.y * NV2;
+#pragma unroll
+          for (int a = 0; a < NV; ++a)
+#pragma unroll
+            for (int c = 0; c < NV; ++c) {
+              double s = 0.0;
+#pragma unroll
+              for (int q = 0; q < NV; ++q) s += Bjk[a * NV + q] * W[q * NV + c];
+              Bik[a * NV + c] -= s;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NV2; ++q) F[(size_t)k * NV2 + q] = W[q];
+      }
+      double L[NV2];
+#pragma unroll
+      for (int q = 0; q < NV2; ++q) L[q] = F[(size_t)kd * NV2 + q];
+#pragma unroll
+      for (int ii = 1; ii < NV; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < ii; ++jj) {
+          const double w = L[ii * NV + jj] / L[jj * NV + jj];
+#pragma unroll
+          for (int kk = jj + 1; kk < NV; ++kk) L[ii * NV + kk] -= w * L[jj * NV + kk];
+          L[ii * NV + jj] = w;
+        }
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        double rhs[NV];
+#pragma unroll
+        for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == c) ? 1.0 : 0.0;
+        lu_solve<NV>(L, rhs);
+#pragma unroll
+        for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + c] = rhs[rr];
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // ILU(0) forward substitution x = b - L x per partition; one thread per (row, component).
@@ -814,6 +913,14 @@ int rx_la_prepare(rx_ctx* ctx) {
 
 int rx_la_ilu_build(rx_ctx* ctx) {
   const int nv = ctx->nVar;
+  if (nv <= 4 && !ctx->ilu_trace) {
+    RX_NV_SWITCH(nv, (k_ilu_build_small<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
+                         ctx->fs.part_lvl, ctx->fs.lvl_ptr, reinterpret_cast<const int4*>(ctx->fs.slot), ctx->rp,
+                         ctx->col, ctx->upd_ptr, reinterpret_cast<const int2*>(ctx->upd), ctx->f[RX_F_JAC],
+                         ctx->f[RX_F_ILU], rx_invd_buf(ctx))));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
   const int waves = ctx->ilu_waves;
   const size_t shm = sizeof(double) * (size_t)waves * ((ctx->rowmax + 1 + kStage) * nv * nv + kPlan / 2);
   RX_NV_SWITCH(nv, (k_ilu_build_part<NV_><<<ctx->npart, 64 * waves, shm, ctx->stream>>>(

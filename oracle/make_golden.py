@@ -249,8 +249,26 @@ def case_jet9w():
     out["jac_edge_sample"] = js
     for k in ("conv_jac_i", "conv_jac_j", "visc_jac_i", "visc_jac_j"):
         out[k] = a[k][ekeep][js]
-    for k in ("dims", "mach_inf", "visc_params", "src_params", "limiter_params"):
+    for k in ("dims", "mach_inf", "visc_params", "src_params", "limiter_params", "muscl_params"):
         out[k] = a[k]
+    # a2 MUSCL branch: whole-loop residual at the window points (compared at interior points, whose
+    # incident edges are all in the window) and the Jacobian rows of a sample of interior points
+    out["muscl_loop_res"] = a["muscl_loop_res"][keep]
+    irows = np.nonzero(interior)[0]
+    rs = np.sort(rng.choice(irows, size=min(48, len(irows)), replace=False))
+    rp, cl, blk = a["muscl_bsr_row_ptr"], a["muscl_bsr_col"], a["muscl_bsr"]
+    deg = max(int(rp[keep[r] + 1] - rp[keep[r]]) for r in rs)
+    nv = blk.shape[1]
+    mc = -np.ones((len(rs), deg), dtype=np.int64)
+    mb = np.zeros((len(rs), deg, nv, nv))
+    for q, r in enumerate(rs):
+        g = keep[r]
+        cols = loc[cl[rp[g]:rp[g + 1]]]
+        mc[q, :len(cols)] = cols
+        mb[q, :len(cols)] = blk[rp[g]:rp[g + 1]]
+    out["muscl_jac_rows"] = rs
+    out["muscl_jac_cols"] = mc
+    out["muscl_jac"] = mb
     # limiter_out at window points needs neighbours' V/grad too: keep only interior as checked
     out.update(mech_arrays())
     return out

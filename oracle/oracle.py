@@ -35,6 +35,7 @@ def lib():
         _lib.orc_fgmres.restype = C.c_int
         _lib.orc_fgmres_p.restype = C.c_int
         _lib.orc_dot.restype = C.c_double
+        _lib.orc_muscl_edges.restype = C.c_int
     return _lib
 
 
@@ -103,6 +104,25 @@ def ausm_edges(nDim, ns, edges, normal, V, dPdU, mach_inf, implicit):
                          _p(dPdU) if implicit else None, C.c_double(mach_inf), C.c_int(int(implicit)),
                          res.ctypes.data_as(C.c_void_p), Ji.ctypes.data_as(C.c_void_p) if implicit else None,
                          Jj.ctypes.data_as(C.c_void_p) if implicit else None)
+    return res, Ji, Jj
+
+
+@_keepalive
+def muscl_edges(mech, nDim, edges, normal, coord, V, dPdU, grad, limiter, refs, mach_inf, implicit):
+    """a2 second-order branch: MUSCL reconstruction + AUSM per edge (limiter None: SECOND_ORDER)."""
+    E = len(edges)
+    nVar = mech.ns + nDim + 2
+    res = np.zeros((E, nVar))
+    Ji = np.zeros((E, nVar, nVar)) if implicit else None
+    Jj = np.zeros((E, nVar, nVar)) if implicit else None
+    rc = lib().orc_muscl_edges(mech.h, C.c_int(nDim), C.c_int64(E), _p(edges, np.int64), _p(normal), _p(coord),
+                               _p(V), _p(dPdU) if implicit else None, _p(grad),
+                               _p(limiter) if limiter is not None else None,
+                               _p(np.asarray(refs, dtype=np.float64)), C.c_double(mach_inf), C.c_int(int(implicit)),
+                               res.ctypes.data_as(C.c_void_p), Ji.ctypes.data_as(C.c_void_p) if implicit else None,
+                               Jj.ctypes.data_as(C.c_void_p) if implicit else None)
+    if rc != 0:
+        raise RuntimeError("oracle MUSCL failed (table range)")
     return res, Ji, Jj
 
 

@@ -657,6 +657,41 @@ int main(int argc, char** argv) {
     }
   }
 
+  // ---- a2 second-order branch: Upwind_Residual with the MUSCL reconstruction on the cfg's spatial
+  //      order (jet9: 2ND_ORDER_LIMITER), solver_direct_reactive.cpp:2554-2729. Whole residual and the
+  //      BSR Jacobian it assembles (make_golden keeps a window / a row sample).
+  if (!do_bsr) {
+    CNumerics* conv_n = drv.num(FLOW_SOL, CONV_TERM);
+    flow->LinSysRes.SetValZero();
+    if (implicit) flow->Jacobian.SetValZero();
+    flow->Upwind_Residual(geo, sc, conv_n, cfg, MESH_0);
+    std::vector<double> r(nPoint * nVar);
+    for (unsigned long i = 0; i < nPoint * nVar; ++i) r[i] = flow->LinSysRes[i];
+    dumpd("muscl_loop_res", r, {(long)nPoint, nVar});
+    if (implicit) {
+      std::vector<int64_t> rp(nPoint + 1, 0), cl;
+      std::vector<double> blocks;
+      for (unsigned long i = 0; i < nPoint; ++i) {
+        std::vector<unsigned long> cols;
+        cols.push_back(i);
+        for (unsigned short k = 0; k < geo->node[i]->GetnPoint(); ++k) cols.push_back(geo->node[i]->GetPoint(k));
+        std::sort(cols.begin(), cols.end());
+        for (auto c : cols) {
+          cl.push_back(c);
+          su2double* b = flow->Jacobian.GetBlock(i, c);
+          blocks.insert(blocks.end(), b, b + nVar * nVar);
+        }
+        rp[i + 1] = cl.size();
+      }
+      dumpi("muscl_bsr_row_ptr", rp, {(long)nPoint + 1});
+      dumpi("muscl_bsr_col", cl, {(long)cl.size()});
+      dumpd("muscl_bsr", blocks, {(long)cl.size(), nVar, nVar});
+    }
+    std::vector<double> prm = {(double)cfg->GetSpatialOrder_Flow(), cfg->GetTemperature_Ref(), cfg->GetEnergy_Ref(),
+                               cfg->GetGas_Constant_Ref()};
+    dumpd("muscl_params", prm, {4});
+  }
+
   std::vector<int64_t> dims = {nDim, nVar, nPrimVar, nPrimVarGrad, nSpecies, implicit ? 1 : 0, rans ? 1 : 0};
   dumpi("dims", dims, {7});
   g_manifest.close();

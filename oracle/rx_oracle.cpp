@@ -1163,6 +1163,60 @@ void grad_lsq_node(const Mech& m, int nDim, int i, const double* coord, const do
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// a2: second-order branch of CReactiveEulerSolver::Upwind_Residual (solver_direct_reactive.cpp:2554-2729):
+// MUSCL reconstruction of (T, u, v, P) with the (optional) limiter, then a thermodynamically consistent
+// state rebuilt through the library (ComputeDensity :457-460 with SetRgas :26-31, ComputeEnthalpy
+// :519-523, ComputeFrozenGamma :398-403 via ComputeCP :612-619, ComputedP_dYs :591-596). Reference
+// quirk kept: side j's pressure check reads Prim_Recon_i[P] (:2617).
+// refs = {Temperature_Ref, Energy_Ref, Gas_Constant_Ref}.
+// ------------------------------------------------------------------------------------------------
+void muscl_side(const Mech& m, int nDim, const double* V, const double* dPdU, const double* recon, bool non_phys,
+                const double* refs, double* Prim, double* Sec, bool implicit) {
+  const int ns = m.ns, nPV = ns + nDim + 5, nVar = ns + nDim + 2;
+  const int T_ = 0, VX = 1, P_ = nDim + 1, RHO = nDim + 2, H_ = nDim + 3, A_ = nDim + 4, RHOS = nDim + 5;
+  if (non_phys) {
+    for (int v = 0; v < nPV; ++v) Prim[v] = V[v];
+    if (implicit)
+      for (int v = 0; v < nVar; ++v) Sec[v] = dPdU[v];
+    return;
+  }
+  Prim[T_] = recon[0];
+  Prim[P_] = recon[nDim + 1];
+  for (int d = 0; d < nDim; ++d) Prim[VX + d] = recon[1 + d];
+  double Ys[32];
+  for (int s = 0; s < ns; ++s) {
+    Prim[RHOS + s] = V[RHOS + s];
+    Ys[s] = V[RHOS + s] < 0.0 ? 1.0e-30 : V[RHOS + s];  // SetMassFractions clamp
+  }
+  double Rgas = 0.0;
+  for (int s = 0; s < ns; ++s) Rgas += Ys[s] * m.ri[s];
+  double rho = Prim[P_] / (Prim[T_] * Rgas);
+  rho *= refs[2];
+  Prim[RHO] = rho;
+  const double dim_temp = Prim[T_] * refs[0];
+  double h = 0.0;
+  for (int s = 0; s < ns; ++s) h += Ys[s] * (spline(m, P_H, s, dim_temp) / m.mm[s]);
+  Prim[H_] = h / refs[1];
+  double sq = 0.0;
+  for (int d = 0; d < nDim; ++d) sq += Prim[VX + d] * Prim[VX + d];
+  Prim[H_] += 0.5 * sq;
+  double Cp = 0.0;
+  for (int s = 0; s < ns; ++s) Cp += Ys[s] * (spline(m, P_CP, s, dim_temp) / m.mm[s]);
+  double Rg2 = 0.0;
+  for (int s = 0; s < ns; ++s) Rg2 += Ys[s] * m.ri[s];
+  const double Gamma = Cp / (Cp - Rg2);
+  Prim[A_] = std::sqrt(Gamma * Prim[P_] / rho);
+  if (!implicit) return;
+  Sec[0] = (Gamma - 1.0) * 0.5 * sq;
+  for (int d = 0; d < nDim; ++d) Sec[1 + d] = (1.0 - Gamma) * Prim[VX + d];
+  Sec[nDim + 1] = Gamma - 1.0;
+  for (int s = 0; s < ns; ++s) {
+    const double e_s = spline(m, P_H, s, dim_temp) / m.mm[s] - m.ri[s] * dim_temp;
+    Sec[nDim + 2 + s] = (m.ri[s] * dim_temp - (Gamma - 1.0) * e_s) / refs[1];
+  }
+}
+
 std::vector<Mech*> g_mechs;
 
 }  // namespace
@@ -1226,6 +1280,63 @@ void orc_ausm_edges(int nDim, int ns, int64_t E, const int64_t* edges, const dou
          implicit ? dPdU + j * nVar : nullptr, mach_inf, implicit != 0, res + e * nVar,
          implicit ? Ji + e * nVar * nVar : nullptr, implicit ? Jj + e * nVar * nVar : nullptr);
   }
+}
+
+// a2 second-order: reconstruction + AUSM over E edges. grad [N][nG][nDim] (rows T, u, v, P first),
+// limiter [N][nDim+2] or null (SECOND_ORDER without limiter). Returns 1 on a table-range error.
+int orc_muscl_edges(void* h, int nDim, int64_t E, const int64_t* edges, const double* normal, const double* coord,
+                    const double* V, const double* dPdU, const double* grad, const double* limiter,
+                    const double* refs, double mach_inf, int implicit, double* res, double* Ji, double* Jj) {
+  const Mech& m = *static_cast<Mech*>(h);
+  const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5, nG = ns + nDim + 2, nL = nDim + 2;
+  try {
+    for (int64_t e = 0; e < E; ++e) {
+      const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+      const double* Vi = V + i * nPV;
+      const double* Vj = V + j * nPV;
+      double vec_i[3], vec_j[3];
+      for (int d = 0; d < nDim; ++d) {
+        vec_i[d] = 0.5 * (coord[j * nDim + d] - coord[i * nDim + d]);
+        vec_j[d] = -vec_i[d];
+      }
+      double ri[8], rj[8];
+      ri[0] = Vi[0];
+      rj[0] = Vj[0];
+      ri[nDim + 1] = Vi[nDim + 1];
+      rj[nDim + 1] = Vj[nDim + 1];
+      for (int d = 0; d < nDim; ++d) {
+        ri[1 + d] = Vi[1 + d];
+        rj[1 + d] = Vj[1 + d];
+      }
+      for (int v = 0; v < nL; ++v) {
+        double pgi = 0.0, pgj = 0.0;
+        for (int d = 0; d < nDim; ++d) {
+          pgi += vec_i[d] * grad[(i * nG + v) * nDim + d];
+          pgj += vec_j[d] * grad[(j * nG + v) * nDim + d];
+        }
+        if (limiter) {
+          ri[v] += limiter[i * nL + v] * pgi;
+          rj[v] += limiter[j * nL + v] * pgj;
+        } else {
+          ri[v] += pgi;
+          rj[v] += pgj;
+        }
+      }
+      bool npi = !(ri[0] > EPS);
+      if (!npi) npi = !(ri[nDim + 1] > EPS);
+      bool npj = !(rj[0] > EPS);
+      if (!npj) npj = !(ri[nDim + 1] > EPS);  // :2617 checks side i's reconstructed pressure
+      double Pi[32], Pj[32], Si[32], Sj[32];
+      muscl_side(m, nDim, Vi, implicit ? dPdU + i * nVar : nullptr, ri, npi, refs, Pi, Si, implicit != 0);
+      muscl_side(m, nDim, Vj, implicit ? dPdU + j * nVar : nullptr, rj, npj, refs, Pj, Sj, implicit != 0);
+      ausm(nDim, ns, Pi, Pj, normal + e * nDim, implicit ? Si : nullptr, implicit ? Sj : nullptr, mach_inf,
+           implicit != 0, res + e * nVar, implicit ? Ji + e * nVar * nVar : nullptr,
+           implicit ? Jj + e * nVar * nVar : nullptr);
+    }
+  } catch (const std::out_of_range&) {
+    return 1;
+  }
+  return 0;
 }
 
 // a9 over N cells. params = {C_mu, PaSR_lb, rho_ref, t_ref, T_ref}
