@@ -76,7 +76,7 @@ class Cfg(C.Structure):
                 ("pasr_lb", C.c_double), ("cfl", C.c_double), ("max_delta_time", C.c_double),
                 ("ref_elem_length", C.c_double), ("limiter_coeff", C.c_double), ("lin_tol", C.c_double),
                 ("relaxation", C.c_double), ("implicit", C.c_int32), ("rans", C.c_int32), ("lin_iter", C.c_int32),
-                ("lin_prec", C.c_int32)]
+                ("lin_prec", C.c_int32), ("spatial_order", C.c_int32)]
 
 
 _lib = None
@@ -110,6 +110,7 @@ def lib():
         _lib.rx_fgmres.argtypes = [C.c_void_p, C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         _lib.rx_explicit_euler.argtypes = [C.c_void_p, C.c_void_p]
         _lib.rx_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        _lib.rx_explicit_rk.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p]
         _lib.rx_profile_enable.argtypes = [C.c_void_p, C.c_int]
         _lib.rx_profile_read.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         _lib.rx_last_error_index.argtypes = [C.c_void_p]
@@ -216,7 +217,7 @@ def default_cfg(**kw):
     c = dict(mach_inf=0.01819, T_ref=1.0, E_ref=1.0, R_ref=1.0, rho_ref=1.0, t_ref=1.0, prandtl_lam=0.72,
              prandtl_turb=0.9, lewis_turb=1.2, c_mu=0.09, pasr_lb=0.2, cfl=5.0, max_delta_time=1e6,
              ref_elem_length=0.1, limiter_coeff=0.5, lin_tol=1e-6, relaxation=1.0, implicit=1, rans=1, lin_iter=5,
-             lin_prec=1)
+             lin_prec=1, spatial_order=0)
     c.update(kw)
     cfg = Cfg()
     for k, v in c.items():
@@ -389,6 +390,11 @@ class ReactiveNSSolver:
     def ExplicitEuler_Iteration(self):
         rms = np.zeros(self.nVar)
         _chk(lib().rx_explicit_euler(self.h, rms.ctypes.data), "rx_explicit_euler", self.h)
+        return rms
+
+    def ExplicitRK_Iteration(self, rk_step, alpha):
+        rms = np.zeros(self.nVar)
+        _chk(lib().rx_explicit_rk(self.h, int(rk_step), float(alpha), rms.ctypes.data), "rx_explicit_rk", self.h)
         return rms
 
     def ImplicitEuler_Iteration(self):

@@ -77,6 +77,7 @@ namespace {
 int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg* cfg, int device, rx_ctx* flow,
                 rx_ctx** out) {
   if (!mesh || !cfg || !out || (!mech && !flow)) return RX_ERR_ARG;
+  if (cfg->spatial_order < 0 || cfg->spatial_order > 2) return RX_ERR_ARG;
   *out = nullptr;
   if (mesh->n_dim != 2) return RX_ERR_ARG;  // 3-D dual grids: next round
   const bool sst = flow != nullptr;
@@ -521,7 +522,9 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->xstar, N * nv));
   }
+  if (!sst && ctx->cfg.spatial_order) CK(dalloc(ctx, &ctx->recon, E * 2 * (int64_t)(ctx->nPV + nv)));
   if (!sst) {
+    CK(dalloc(ctx, &ctx->uold, N * nv));
     CK(dalloc(ctx, &ctx->fvisc, E * nv));
     CK(dalloc(ctx, &ctx->lim_mn, N * ctx->nL));
     CK(dalloc(ctx, &ctx->lim_mx, N * ctx->nL));
@@ -559,7 +562,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->sendbuf, ctx->rms_sum,
-                  ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
+                  ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   rx_comm_free(ctx);
   if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
@@ -626,7 +629,9 @@ int rx_residual_zero(rx_ctx* ctx) {
 int rx_edge_flux_conv(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_CONV);
-  int rc = ctx->cfg.implicit ? rx_launch_ausm_edge(ctx) : rx_launch_ausm_node(ctx);
+  int rc = RX_OK;
+  if (ctx->cfg.spatial_order && (rc = rx_launch_muscl(ctx))) return rc;
+  rc = ctx->cfg.implicit ? rx_launch_ausm_edge(ctx) : rx_launch_ausm_node(ctx);
   if (rc) return rc;
   ctx->phase_conv = 1;
   ctx->assembled = ctx->cfg.implicit ? 0 : 1;
@@ -727,6 +732,18 @@ int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
     RxPhase ph(ctx, RX_K_UPDATE);
     if (res_rms && (rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RES]))) return rc;
     if ((rc = rx_la_explicit_update(ctx))) return rc;
+  }
+  return res_rms ? rx_la_rms_read(ctx, res_rms) : RX_OK;
+}
+
+// ExplicitRK_Iteration (solver_direct_reactive.cpp:2456-2493): stage iRKStep with RK_ALPHA_COEFF[iRKStep].
+int rx_explicit_rk(rx_ctx* ctx, int rk_step, double alpha, double* res_rms) {
+  if (!ctx || ctx->kind != RX_KIND_FLOW || rk_step < 0) return RX_ERR_ARG;
+  int rc;
+  {
+    RxPhase ph(ctx, RX_K_UPDATE);
+    if (res_rms && (rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RES]))) return rc;
+    if ((rc = rx_la_rk_update(ctx, rk_step, alpha))) return rc;
   }
   return res_rms ? rx_la_rms_read(ctx, res_rms) : RX_OK;
 }

@@ -105,6 +105,8 @@ struct rx_ctx {
   double* vsumm = nullptr;   // [E][visc_summary_size] per-edge viscous summary (implicit)
   double* jsrc = nullptr;    // [N][nVar*nVar]
   double* rsrc = nullptr;    // [N][nVar] source residual (implicit path)
+  double* uold = nullptr;    // [N][nVar] Solution_Old of the RK stages
+  double* recon = nullptr;   // [E][2][nPV] reconstructed edge states + [E][2][nVar] their dP/dU (2nd order)
   int phase_conv = 0, phase_visc = 0, phase_src = 0, assembled = 1;
   double* lim_mn = nullptr;  // [N][nL]
   double* lim_mx = nullptr;
@@ -169,6 +171,7 @@ struct RxPhase {
 
 // kernel launchers (rx_kernels.hip)
 int rx_launch_ausm_node(rx_ctx* ctx);
+int rx_launch_muscl(rx_ctx* ctx);
 int rx_launch_ausm_edge(rx_ctx* ctx);
 int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);
@@ -195,6 +198,7 @@ int rx_la_rms_enqueue(rx_ctx* ctx, const double* r);
 int rx_la_rms_read(rx_ctx* ctx, double* rms);
 int rx_la_implicit_update(rx_ctx* ctx);
 int rx_la_explicit_update(rx_ctx* ctx);
+int rx_la_rk_update(rx_ctx* ctx, int stage, double alpha);
 int rx_la_build_system(rx_ctx* ctx);
 // SST (rx_sst.hip)
 int rx_sst_build_system(rx_ctx* ctx);

@@ -30,7 +30,8 @@ __global__ __launch_bounds__(kBlock) void k_ausm_node(int N, const int32_t* __re
                                                       const int32_t* __restrict__ adj,
                                                       const int32_t* __restrict__ edges,
                                                       const double* __restrict__ normal, const double* __restrict__ V,
-                                                      double mInfty, double* __restrict__ R, int* err) {
+                                                      const double* __restrict__ VR, double mInfty,
+                                                      double* __restrict__ R, int* err) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
@@ -47,8 +48,16 @@ __global__ __launch_bounds__(kBlock) void k_ausm_node(int N, const int32_t* __re
     const int e = a >> 1;
     const int side = a & 1;
     const int other = edges[2 * e + (side ^ 1)];
+    if (VR) {  // second order: the edge's reconstructed states (k_muscl_edge), [2e] node 0, [2e+1] node 1
 #pragma unroll
-    for (int v = 0; v < nPV; ++v) Vo[v] = V[(size_t)other * nPV + v];
+      for (int v = 0; v < nPV; ++v) {
+        Vs[v] = VR[(2 * (size_t)e + side) * nPV + v];
+        Vo[v] = VR[(2 * (size_t)e + (side ^ 1)) * nPV + v];
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < nPV; ++v) Vo[v] = V[(size_t)other * nPV + v];
+    }
     double nrm[NDIM];
 #pragma unroll
     for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
@@ -68,6 +77,120 @@ __global__ __launch_bounds__(kBlock) void k_ausm_node(int N, const int32_t* __re
   if (bad) set_err(err, ERR_NAN, i);
 }
 
+// a2 second order: MUSCL reconstruction of (T, u, v, P) per edge side with the optional limiter, and the
+// thermodynamically consistent state + pressure derivatives rebuilt through the library
+// (CReactiveEulerSolver::Upwind_Residual, solver_direct_reactive.cpp:2554-2729; ComputeDensity :457-460,
+// ComputeEnthalpy :519-523, ComputeFrozenGamma :398-403, ComputedP_dYs :591-596 of
+// reacting_model_library.cpp). One thread per (edge, side); [2e + side] of VR / SR. Quirk kept: side j's
+// pressure check reads side i's reconstructed pressure (:2617). Table range -> ERR_RANGE.
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) void k_muscl_edge(int E, const int32_t* __restrict__ edges,
+                                                       const double* __restrict__ coord,
+                                                       const double* __restrict__ V, const double* __restrict__ dPdU,
+                                                       const double* __restrict__ G, const double* __restrict__ lim,
+                                                       DevMech m, double T_ref, double E_ref, double R_ref,
+                                                       int implicit, double* __restrict__ VR,
+                                                       double* __restrict__ SR, int* err) {
+  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nG = NS + NDIM + 2, nL = NDIM + 2;
+  constexpr int VX = 1, P_ = NDIM + 1, RHO = NDIM + 2, H_ = NDIM + 3, A_ = NDIM + 4, RHOS = NDIM + 5;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * E) return;
+  const int e = t >> 1, side = t & 1;
+  const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+  const int me = side ? n1 : n0;
+  // Vector_i = 0.5 (x_j - x_i), Vector_j = -Vector_i
+  double vec[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    const double vi = 0.5 * (coord[(size_t)n1 * NDIM + d] - coord[(size_t)n0 * NDIM + d]);
+    vec[d] = side ? -vi : vi;
+  }
+  const double* Vm = V + (size_t)me * nPV;
+  double rc[nL];
+  rc[0] = Vm[0];
+  rc[P_] = Vm[P_];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) rc[VX + d] = Vm[VX + d];
+#pragma unroll
+  for (int v = 0; v < nL; ++v) {
+    double pg = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) pg += vec[d] * G[((size_t)me * nG + v) * NDIM + d];
+    if (lim) rc[v] += lim[(size_t)me * nL + v] * pg;
+    else rc[v] += pg;
+  }
+  // side i's reconstructed pressure (the j-side check of :2617 reads it)
+  double p_i = rc[P_];
+  if (side) {
+    double pg = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) pg += -vec[d] * G[((size_t)n0 * nG + P_) * NDIM + d];
+    p_i = V[(size_t)n0 * nPV + P_];
+    if (lim) p_i += lim[(size_t)n0 * nL + P_] * pg;
+    else p_i += pg;
+  }
+  bool np = !(rc[0] > kEPS);
+  if (!np) np = !(p_i > kEPS);
+  double* out = VR + (size_t)t * nPV;
+  double* sout = SR ? SR + (size_t)t * nVar : nullptr;
+  if (np) {
+#pragma unroll
+    for (int v = 0; v < nPV; ++v) out[v] = Vm[v];
+    if (implicit)
+#pragma unroll
+      for (int v = 0; v < nVar; ++v) sout[v] = dPdU[(size_t)me * nVar + v];
+    return;
+  }
+  double Ys[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const double y = Vm[RHOS + s];
+    out[RHOS + s] = y;
+    Ys[s] = y < 0.0 ? 1.0e-30 : y;
+  }
+  const double T = rc[0], P = rc[P_];
+  double Rgas = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) Rgas += Ys[s] * (kR / m.mm[s]);
+  double rho = P / (T * Rgas);
+  rho *= R_ref;
+  const double dim_temp = T * T_ref;
+  int ierr = ERR_NONE;
+  double hs[NS], h = 0.0, Cp = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    hs[s] = spline(m, P_H, s, dim_temp, &ierr) / m.mm[s];
+    h += Ys[s] * hs[s];
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) Cp += Ys[s] * (spline(m, P_CP, s, dim_temp, &ierr) / m.mm[s]);
+  if (ierr != ERR_NONE) set_err(err, ERR_RANGE, e);
+  double sq = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) sq += rc[VX + d] * rc[VX + d];
+  const double Gamma = Cp / (Cp - Rgas);
+  out[0] = T;
+  out[P_] = P;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) out[VX + d] = rc[VX + d];
+  out[RHO] = rho;
+  double hh = h / E_ref;
+  hh += 0.5 * sq;
+  out[H_] = hh;
+  out[A_] = sqrt(Gamma * P / rho);
+  if (!implicit) return;
+  sout[0] = (Gamma - 1.0) * 0.5 * sq;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) sout[1 + d] = (1.0 - Gamma) * rc[VX + d];
+  sout[NDIM + 1] = Gamma - 1.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const double ri = kR / m.mm[s];
+    const double es = hs[s] - ri * dim_temp;
+    sout[NDIM + 2 + s] = (ri * dim_temp - (Gamma - 1.0) * es) / E_ref;
+  }
+}
+
 // a1 implicit: flux + both Jacobians into per-edge scratch. A team of 16 lanes per edge (4 edges
 // per wavefront): every lane evaluates the edge scalars, lane v < nVar owns residual component v and
 // Jacobian column b = v, so for every row a the team stores one contiguous row segment of Ji and Jj.
@@ -75,7 +198,8 @@ constexpr int kAusmTeam = 16;
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) void k_ausm_edge(int E, const int32_t* __restrict__ edges,
                                                       const double* __restrict__ normal, const double* __restrict__ V,
-                                                      const double* __restrict__ dPdU, double mInfty,
+                                                      const double* __restrict__ dPdU, const double* __restrict__ VR,
+                                                      const double* __restrict__ SR, double mInfty,
                                                       double* __restrict__ F, double* __restrict__ Jac, int* err) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nVar2 = nVar * nVar;
   static_assert(nVar <= kAusmTeam, "team too small");
@@ -83,11 +207,16 @@ __global__ __launch_bounds__(kBlock) void k_ausm_edge(int E, const int32_t* __re
   const int e = gt / kAusmTeam, b = gt % kAusmTeam;
   if (e >= E) return;
   const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+  // node states (1st order) or the edge's reconstructed states and pressure derivatives (2nd order)
+  const double* Vsi = VR ? VR + 2 * (size_t)e * nPV : V + (size_t)n0 * nPV;
+  const double* Vsj = VR ? VR + (2 * (size_t)e + 1) * nPV : V + (size_t)n1 * nPV;
+  const double* Ssi = VR ? SR + 2 * (size_t)e * nVar : dPdU + (size_t)n0 * nVar;
+  const double* Ssj = VR ? SR + (2 * (size_t)e + 1) * nVar : dPdU + (size_t)n1 * nVar;
   double Vi[nPV], Vj[nPV];
 #pragma unroll
   for (int v = 0; v < nPV; ++v) {
-    Vi[v] = V[(size_t)n0 * nPV + v];
-    Vj[v] = V[(size_t)n1 * nPV + v];
+    Vi[v] = Vsi[v];
+    Vj[v] = Vsj[v];
   }
   double nrm[NDIM];
 #pragma unroll
@@ -99,15 +228,15 @@ __global__ __launch_bounds__(kBlock) void k_ausm_edge(int E, const int32_t* __re
   {
     // ausm_res for the runtime component b, with phi read by index (no dynamic register indexing)
     const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
-    const double pi = b == 0 ? 1.0 : V[(size_t)n0 * nPV + pidx];
-    const double pj = b == 0 ? 1.0 : V[(size_t)n1 * nPV + pidx];
+    const double pi = b == 0 ? 1.0 : Vsi[pidx];
+    const double pj = b == 0 ? 1.0 : Vsj[pidx];
     double r = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
     if (b >= 1 && b <= NDIM) r += s.pLF * pick<NDIM>(s.UN, b - 1) * s.Area;
     bad |= isnan(r);
     F[(size_t)e * nVar + b] = r;
   }
   // dP/dU of both nodes: only column b is needed by this lane's Jacobian column
-  const double sib = dPdU[(size_t)n0 * nVar + b], sjb = dPdU[(size_t)n1 * nVar + b];
+  const double sib = Ssi[b], sjb = Ssj[b];
   const AusmCol c = ausm_col_b<NDIM>(s, sib, sjb, b);
   double* Ji = Jac + (size_t)e * 2 * nVar2;
   double* Jj = Ji + nVar2;
@@ -599,11 +728,24 @@ int rx_check_error(rx_ctx* ctx) {
   return RX_OK;
 }
 
+int rx_launch_muscl(rx_ctx* ctx) {
+  if (ctx->nDim != 2 || !ctx->recon) return RX_ERR_ARG;
+  const double* lim = ctx->cfg.spatial_order == 2 ? ctx->f[RX_F_LIMITER] : nullptr;
+  double* SR = ctx->cfg.implicit ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
+  RX_NS_SWITCH(ctx->ns, (k_muscl_edge<NS_, 2><<<blocks(2 * ctx->E), kBlock, 0, ctx->stream>>>(
+                            (int)ctx->E, ctx->edges, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_DPDU], ctx->f[RX_F_GRAD],
+                            lim, ctx->mech, ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.implicit,
+                            ctx->recon, SR, ctx->err)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
 int rx_launch_ausm_node(rx_ctx* ctx) {
   if (ctx->nDim != 2) return RX_ERR_ARG;
   RX_NS_SWITCH(ctx->ns, (k_ausm_node<NS_, 2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->f[RX_F_V],
-                            ctx->cfg.mach_inf, ctx->f[RX_F_RES], ctx->err)));
+                            ctx->cfg.spatial_order ? ctx->recon : nullptr, ctx->cfg.mach_inf, ctx->f[RX_F_RES],
+                            ctx->err)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
@@ -612,6 +754,8 @@ int rx_launch_ausm_edge(rx_ctx* ctx) {
   if (ctx->nDim != 2) return RX_ERR_ARG;
   RX_NS_SWITCH(ctx->ns, (k_ausm_edge<NS_, 2><<<blocks(ctx->E * kAusmTeam), kBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
+                            ctx->cfg.spatial_order ? ctx->recon : nullptr,
+                            ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr,
                             ctx->cfg.mach_inf, ctx->fconv, ctx->jconv, ctx->err)));
   RX_HIP(hipGetLastError());
   return RX_OK;

@@ -76,24 +76,32 @@ __global__ __launch_bounds__(kBlock) void k_build_system(int Nd, int N, const in
   }
 }
 
-// U = clip(U + relax*x) and per-block partial sums of res^2 (RMS monitor).
+// AddClippedSolution: U = clip(U_old + delta) (variable_structure.cpp:207-211) with
+//   mode 0 implicit  delta = relax * LinSysSol                          (:2390-2400)
+//   mode 1 explicit  delta = -(Res + 0) * dt / Vol                       (:2430-2440)
+//   mode 2 RK stage  delta = -(Res + 0) * dt / Vol * alpha_RK, U_old = U0 (ExplicitRK_Iteration :2456-2493)
 __global__ __launch_bounds__(kBlock) void k_update(int N, int nVar, int nDim, const double* __restrict__ dx,
                                                    double scale, const double* __restrict__ vol,
-                                                   const double* __restrict__ dt, int mode, double* __restrict__ U) {
+                                                   const double* __restrict__ dt, int mode,
+                                                   const double* __restrict__ U0, double* __restrict__ U) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * nVar) return;
   const int i = t / nVar, v = t - i * nVar;
   double delta;
-  if (mode == 0) {  // implicit: relax * LinSysSol
+  if (mode == 0) {
     delta = scale * dx[t];
-  } else {  // explicit: -Res * dt / Vol
+  } else {
     double Delta = 0.0;
     if (vol[i] > rx::kEPS) Delta = dt[i] / vol[i];
     delta = -(dx[t] + 0.0) * Delta;
+    if (mode == 2) delta = delta * scale;
   }
   const double lo = (v >= 1 && v <= nDim + 1) ? -1.0 / rx::kEPS : 0.0;
   const double hi = 1.0 / rx::kEPS;
-  U[t] = fmin(fmax(U[t] + delta, lo), hi);
+  const double base = U0 ? U0[t] : U[t];
+  const double x = base + delta;
+  const double mx = (x < lo) ? lo : x;  // std::min(std::max(x, lo), hi), NaN and signed zeros included
+  U[t] = (hi < mx) ? hi : mx;
 }
 
 __global__ __launch_bounds__(kBlock) void k_sumsq_cols(int N, int nVar, const double* __restrict__ r,
@@ -182,7 +190,8 @@ int rx_la_rms_read(rx_ctx* ctx, double* rms) {
 int rx_la_implicit_update(rx_ctx* ctx) {
   const int64_t n = ctx->Nd * ctx->nVar;
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_SOL],
-                                                  ctx->cfg.relaxation, ctx->vol, ctx->f[RX_F_DT], 0, ctx->f[RX_F_U]);
+                                                  ctx->cfg.relaxation, ctx->vol, ctx->f[RX_F_DT], 0, nullptr,
+                                                  ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }
@@ -190,7 +199,20 @@ int rx_la_implicit_update(rx_ctx* ctx) {
 int rx_la_explicit_update(rx_ctx* ctx) {
   const int64_t n = ctx->Nd * ctx->nVar;
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], 1.0,
-                                                  ctx->vol, ctx->f[RX_F_DT], 1, ctx->f[RX_F_U]);
+                                                  ctx->vol, ctx->f[RX_F_DT], 1, nullptr, ctx->f[RX_F_U]);
+  RX_HIP(hipGetLastError());
+  return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
+}
+
+// ExplicitRK_Iteration stage: Set_OldSolution at stage 0 (integration_time.cpp:162), then
+// U = clip(U_old - Res dt/Vol alpha), Set_MPI_Solution (:2488).
+int rx_la_rk_update(rx_ctx* ctx, int stage, double alpha) {
+  const int64_t n = ctx->Nd * ctx->nVar;
+  if (stage == 0)
+    RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[RX_F_U], sizeof(double) * ctx->N * ctx->nVar, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], alpha,
+                                                  ctx->vol, ctx->f[RX_F_DT], 2, ctx->uold, ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }

@@ -3,7 +3,8 @@
  * Drop-in boundary for the loops the reference runs inside its CSolver overrides. Each entry point
  * replaces one reference loop / operator (paths relative to the reference root):
  *
- *   rx_edge_flux_conv    CReactiveEulerSolver::Upwind_Residual, 1st-order branch
+ *   rx_edge_flux_conv    CReactiveEulerSolver::Upwind_Residual (1st order, or the MUSCL 2nd-order branch
+ *                        :2554-2729 when rx_cfg.spatial_order > 0)
  *                        SU2_CFD/src/solver_direct_reactive.cpp:2535-2785 with
  *                        CUpwReactiveAUSM::ComputeResidual SU2_CFD/src/numerics_direct_reactive.cpp:53-378
  *   rx_edge_flux_visc    CReactiveNSSolver::Viscous_Residual solver_direct_reactive.cpp:5305-5386 with
@@ -20,6 +21,7 @@
  *   rx_fgmres            CSysSolve::FGMRES_LinSolver Common/src/linear_solvers_structure.cpp:309-463
  *   rx_implicit_euler    CReactiveEulerSolver::ImplicitEuler_Iteration solver_direct_reactive.cpp:2336-2407
  *   rx_explicit_euler    CReactiveEulerSolver::ExplicitEuler_Iteration solver_direct_reactive.cpp:2414-2449
+ *   rx_explicit_rk       CReactiveEulerSolver::ExplicitRK_Iteration solver_direct_reactive.cpp:2456-2493
  *
  * Ownership: all device buffers belong to the rx_ctx. Host arrays passed in are copied at the
  * call; no pointer is retained. Every function returns an rx_status; on RX_ERR_NAN /
@@ -108,6 +110,8 @@ typedef struct {
   double ref_elem_length, limiter_coeff;         /* Venkatakrishnan */
   double lin_tol, relaxation;                    /* LINEAR_SOLVER_ERROR, RELAXATION_FACTOR_FLOW */
   int32_t implicit, rans, lin_iter, lin_prec;    /* lin_prec: 0 = LU_SGS, 1 = ILU0 */
+  int32_t spatial_order;  /* SPATIAL_ORDER_FLOW: 0 = 1ST_ORDER, 1 = 2ND_ORDER (MUSCL), 2 = 2ND_ORDER_LIMITER
+                             (MUSCL with RX_F_LIMITER), Upwind_Residual :2554-2729 */
 } rx_cfg;
 
 typedef enum {
@@ -184,6 +188,10 @@ int rx_halo_exchange(rx_ctx *ctx, rx_field f); /* owned -> halo copies of a node
 /* Time integration (updates RX_F_U). */
 int rx_explicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */);
 int rx_implicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */, int *lin_iters);
+/* CReactiveEulerSolver::ExplicitRK_Iteration (solver_direct_reactive.cpp:2456-2493): stage rk_step with
+ * alpha = RK_ALPHA_COEFF[rk_step]; stage 0 also stores Solution_Old (Set_OldSolution,
+ * integration_time.cpp:162). U = clip(U_old - Res dt/Vol alpha). */
+int rx_explicit_rk(rx_ctx *ctx, int rk_step, double alpha, double *res_rms /* [nVar] or NULL */);
 
 /* Menter SST turbulence solver (SURVEY.md §8 a14 + next-2): CTurbSSTSolver / CTurbSolver
  * (SU2_CFD/src/solver_direct_turbulent.cpp) on the flow context's state. A second context with

@@ -11,6 +11,7 @@
  *   Viscous_Residual              -> rx_edge_flux_visc           (:5305-5386)  throws "NaN found in the viscous residual"
  *   Source_Residual               -> rx_cell_source_pasr         (:2792-2874)  throws "NaN found in the source residual"
  *   ExplicitEuler_Iteration       -> rx_explicit_euler           (:2414-2449)
+ *   ExplicitRK_Iteration          -> rx_explicit_rk              (:2456-2493)
  *   ImplicitEuler_Iteration       -> rx_implicit_euler           (:2336-2407)
  *   SetStrainMag                  -> rx_strain_mag               (variable_direct_reactive.cpp:1060-1095)
  * TurbSSTSolver mirrors CTurbSSTSolver / CTurbSolver (SU2_CFD/include/solver_structure.hpp, turbulent
@@ -75,6 +76,11 @@ class ReactiveNSSolver {
   std::vector<double> ExplicitEuler_Iteration() {
     std::vector<double> rms((size_t)nvar_);
     check(rx_explicit_euler(ctx_, rms.data()), "ExplicitEuler_Iteration");
+    return rms;
+  }
+  std::vector<double> ExplicitRK_Iteration(int rk_step, double alpha) {
+    std::vector<double> rms((size_t)nvar_);
+    check(rx_explicit_rk(ctx_, rk_step, alpha, rms.data()), "ExplicitRK_Iteration");
     return rms;
   }
   std::vector<double> ImplicitEuler_Iteration(int* lin_iters = nullptr) {

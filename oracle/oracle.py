@@ -292,6 +292,17 @@ def update(U, d, nDim, mode, relax, vol, dt):
     return U
 
 
+@_keepalive
+def update_rk(Uold, R, nDim, alpha, vol, dt):
+    """ExplicitRK_Iteration stage from Solution_Old (orc_update_rk)."""
+    Uold = np.ascontiguousarray(Uold, dtype=np.float64)
+    N, nb = Uold.shape
+    U = np.zeros_like(Uold)
+    lib().orc_update_rk(C.c_int64(N), C.c_int(nb), C.c_int(nDim), _p(R), C.c_double(alpha), _p(vol), _p(dt),
+                        _p(Uold), U.ctypes.data_as(C.c_void_p))
+    return U
+
+
 def bsr_pattern(N, edges):
     """Edge-connected BSR sparsity with the diagonal, columns sorted (CSysMatrix::Initialize)."""
     e = np.asarray(edges, dtype=np.int64)

@@ -1955,8 +1955,24 @@ void orc_update(int64_t N, int nb, int nDim, int mode, const double* d, double r
       }
       const double lo = (v >= 1 && v <= nDim + 1) ? -1.0 / EPS : 0.0;
       const double hi = 1.0 / EPS;
-      U[i * nb + v] = std::fmin(std::fmax(U[i * nb + v] + delta, lo), hi);
+      U[i * nb + v] = std::min(std::max(U[i * nb + v] + delta, lo), hi);
     }
+}
+
+// CReactiveEulerSolver::ExplicitRK_Iteration (solver_direct_reactive.cpp:2456-2493): one stage,
+// U = clip(U_old + (-(Res + 0) * dt / Vol) * alpha) via AddClippedSolution (variable_structure.cpp:207-211).
+void orc_update_rk(int64_t N, int nb, int nDim, const double* Res, double alpha, const double* vol, const double* dt,
+                   const double* Uold, double* U) {
+  for (int64_t i = 0; i < N; ++i) {
+    double Delta = 0.0;
+    if (vol[i] > EPS) Delta = dt[i] / vol[i];
+    for (int v = 0; v < nb; ++v) {
+      const double r = Res[i * nb + v] + 0.0;
+      const double lo = (v >= 1 && v <= nDim + 1) ? -1.0 / EPS : 0.0;
+      const double hi = 1.0 / EPS;
+      U[i * nb + v] = std::min(std::max(Uold[i * nb + v] + -r * Delta * alpha, lo), hi);
+    }
+  }
 }
 
 // =================================================================================================

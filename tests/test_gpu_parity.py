@@ -23,7 +23,7 @@ def golden(case):
     return g
 
 
-def make_solver(g, implicit, lin_prec=1, cfl=None):
+def make_solver(g, implicit, lin_prec=1, cfl=None, spatial_order=0):
     nDim, nVar, nPV, nG, ns, imp, rans = [int(x) for x in g["dims"]]
     mesh = {k: g[k] for k in ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr")}
     mesh["bvertex"] = g.get("bvertex", np.zeros((0, 3), dtype=np.int64))
@@ -31,7 +31,8 @@ def make_solver(g, implicit, lin_prec=1, cfl=None):
     mech = rx.Mechanism(g)
     kw = dict(mach_inf=float(g["mach_inf"][0]), prandtl_turb=float(g["visc_params"][1]),
               lewis_turb=float(g["visc_params"][2]), c_mu=float(g["src_params"][0]),
-              pasr_lb=float(g["src_params"][1]), implicit=int(implicit), lin_prec=lin_prec)
+              pasr_lb=float(g["src_params"][1]), implicit=int(implicit), lin_prec=lin_prec,
+              spatial_order=spatial_order)
     if "limiter_params" in g:
         kw.update(ref_elem_length=float(g["limiter_params"][0]), limiter_coeff=float(g["limiter_params"][1]))
     if "dt_params" in g:
