@@ -227,7 +227,8 @@ def case_jet9w():
                  "grad_prim", "limiter", "turb_k", "turb_omega", "mu_t", "sigma_k", "grad_k", "src_res",
                  "src_jac", "limiter_out", "grad_lsq_out", "wall_distance",
                  "eddy_visc_flow", "sst_sol", "sst_grad", "sst_F1", "sst_F2", "sst_CDkw", "strain_mag",
-                 "sst_src_res", "sst_src_jac"]
+                 "sst_src_res", "sst_src_jac", "p2v_U", "p2v_V_before", "p2v_tke", "p2v_mut", "p2v_U_after", "p2v_V",
+                 "p2v_dPdU", "p2v_dTdU", "p2v_mu", "p2v_kappa", "p2v_cp", "p2v_eddy", "p2v_Dij"]
     for k in node_keys:
         out[k] = a[k][keep]
     out["interior"] = interior
@@ -249,7 +250,7 @@ def case_jet9w():
     out["jac_edge_sample"] = js
     for k in ("conv_jac_i", "conv_jac_j", "visc_jac_i", "visc_jac_j"):
         out[k] = a[k][ekeep][js]
-    for k in ("dims", "mach_inf", "visc_params", "src_params", "limiter_params", "muscl_params"):
+    for k in ("dims", "mach_inf", "visc_params", "src_params", "limiter_params", "muscl_params", "p2v_params"):
         out[k] = a[k]
     # a2 MUSCL branch: whole-loop residual at the window points (compared at interior points, whose
     # incident edges are all in the window) and the Jacobian rows of a sample of interior points

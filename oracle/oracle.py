@@ -36,6 +36,7 @@ def lib():
         _lib.orc_fgmres_p.restype = C.c_int
         _lib.orc_dot.restype = C.c_double
         _lib.orc_muscl_edges.restype = C.c_int
+        _lib.orc_set_primitive.restype = C.c_int
     return _lib
 
 
@@ -301,6 +302,32 @@ def update_rk(Uold, R, nDim, alpha, vol, dt):
     lib().orc_update_rk(C.c_int64(N), C.c_int(nb), C.c_int(nDim), _p(R), C.c_double(alpha), _p(vol), _p(dt),
                         _p(Uold), U.ctypes.data_as(C.c_void_p))
     return U
+
+
+@_keepalive
+def set_primitive(mech, nDim, U, V_before, tke, mut, prm, Uold=None):
+    """next-1: SetPrimitive_Variables per point (orc_set_primitive). Returns dict of the node record and the
+    non-physical count (-1: bisection failure)."""
+    U = np.ascontiguousarray(U, dtype=np.float64).copy()
+    V = np.ascontiguousarray(V_before, dtype=np.float64).copy()
+    N, nVar = U.shape
+    ns = mech.ns
+    out = dict(dPdU=np.zeros((N, nVar)), dTdU=np.zeros((N, nVar)), mu=np.zeros(N), kappa=np.zeros(N),
+               Dij=np.zeros((N, ns, ns)), eddy=np.zeros(N), cp=np.zeros(N))
+    n = lib().orc_set_primitive(mech.h, C.c_int(nDim), C.c_int64(N), U.ctypes.data_as(C.c_void_p),
+                                V.ctypes.data_as(C.c_void_p), _p(Uold) if Uold is not None else None,
+                                _p(tke) if tke is not None else None, _p(mut) if mut is not None else None,
+                                _p(np.asarray(prm, dtype=np.float64)),
+                                *[out[k].ctypes.data_as(C.c_void_p) for k in ("dPdU", "dTdU", "mu", "kappa", "Dij",
+                                                                              "eddy", "cp")])
+    out.update(U=U, V=V, nonphys=n)
+    return out
+
+
+def p2v_params(g):
+    """orc_set_primitive's prm from a golden file's p2v_params (+ CLIPPING_TEMPRATURE = NO)."""
+    p = g["p2v_params"]
+    return [p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9], p[10], p[11], 0.0]
 
 
 def bsr_pattern(N, edges):

@@ -692,6 +692,80 @@ int main(int argc, char** argv) {
     dumpd("muscl_params", prm, {4});
   }
 
+  // ---- next-1: one reference update (residual loops, time step, Euler update) followed by
+  //      CReactiveEulerSolver::SetPrimitive_Variables (solver_direct_reactive.cpp:985-1040):
+  //      Cons2PrimVar from the updated U with the previous T as the secant's start, Cp, dT/dU, dP/dU,
+  //      mu, kappa, Dij, eddy viscosity (variable_direct_reactive.cpp:550-853, 1188-1228).
+  {
+    CNumerics* conv_n = drv.num(FLOW_SOL, CONV_TERM);
+    CNumerics* visc_n = drv.num(FLOW_SOL, VISC_TERM);
+    CNumerics* src_n = drv.num(FLOW_SOL, SOURCE_FIRST_TERM);
+    CNumerics* src2_n = drv.num(FLOW_SOL, SOURCE_SECOND_TERM);
+    flow->LinSysRes.SetValZero();
+    if (implicit) flow->Jacobian.SetValZero();
+    flow->Upwind_Residual(geo, sc, conv_n, cfg, MESH_0);
+    flow->Viscous_Residual(geo, sc, visc_n, cfg, MESH_0, NO_RK_ITER);
+    flow->Source_Residual(geo, sc, src_n, src2_n, cfg, MESH_0);
+    flow->SetTime_Step(geo, sc, cfg, MESH_0, 0);
+    std::vector<double> Uprev(nPoint * nVar);
+    for (unsigned long i = 0; i < nPoint; ++i)
+      for (unsigned short v = 0; v < nVar; ++v) Uprev[i * nVar + v] = flow->node[i]->GetSolution(v);
+    if (implicit) flow->ImplicitEuler_Iteration(geo, sc, cfg);
+    else flow->ExplicitEuler_Iteration(geo, sc, cfg);
+    // mini9 (CFL 5 on a 21x11 mesh without boundary conditions): a fraction of the reference's update
+    // keeps every point inside the property tables; jet9 takes the whole update.
+    const double frac = do_bsr ? 0.05 : 1.0;
+    if (frac != 1.0)
+      for (unsigned long i = 0; i < nPoint; ++i)
+        for (unsigned short v = 0; v < nVar; ++v) {
+          const double u0 = Uprev[i * nVar + v];
+          flow->node[i]->SetSolution(v, u0 + frac * (flow->node[i]->GetSolution(v) - u0));
+        }
+    std::vector<double> U(nPoint * nVar), V0(nPoint * nPrimVar), tk(nPoint), mt(nPoint);
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      for (unsigned short v = 0; v < nVar; ++v) U[i * nVar + v] = flow->node[i]->GetSolution(v);
+      for (unsigned short v = 0; v < nPrimVar; ++v) V0[i * nPrimVar + v] = flow->node[i]->GetPrimitive(v);
+      tk[i] = rans ? turb->node[i]->GetSolution(0) : 0.0;
+      mt[i] = rans ? turb->node[i]->GetmuT() : 0.0;
+    }
+    dumpd("p2v_U", U, {(long)nPoint, nVar});
+    dumpd("p2v_V_before", V0, {(long)nPoint, nPrimVar});
+    dumpd("p2v_tke", tk, {(long)nPoint});
+    dumpd("p2v_mut", mt, {(long)nPoint});
+    const unsigned long nerr = flow->SetPrimitive_Variables(sc, cfg, false);
+    std::vector<double> U1(nPoint * nVar), V(nPoint * nPrimVar), dPdU(nPoint * nVar), dTdU(nPoint * nVar);
+    std::vector<double> mu(nPoint), kap(nPoint), cp(nPoint), ed(nPoint), Dij(nPoint * nSpecies * nSpecies);
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      CVariable* n = flow->node[i];
+      for (unsigned short v = 0; v < nVar; ++v) {
+        U1[i * nVar + v] = n->GetSolution(v);
+        dPdU[i * nVar + v] = n->GetdPdU()[v];
+        dTdU[i * nVar + v] = n->GetdTdU()[v];
+      }
+      for (unsigned short v = 0; v < nPrimVar; ++v) V[i * nPrimVar + v] = n->GetPrimitive(v);
+      mu[i] = n->GetLaminarViscosity();
+      kap[i] = n->GetThermalConductivity();
+      cp[i] = n->GetSpecificHeatCp();
+      ed[i] = n->GetEddyViscosity();
+      double* d = n->GetDiffusionCoeff();
+      for (int k = 0; k < nSpecies * nSpecies; ++k) Dij[i * nSpecies * nSpecies + k] = d[k];
+    }
+    dumpd("p2v_U_after", U1, {(long)nPoint, nVar});
+    dumpd("p2v_V", V, {(long)nPoint, nPrimVar});
+    dumpd("p2v_dPdU", dPdU, {(long)nPoint, nVar});
+    dumpd("p2v_dTdU", dTdU, {(long)nPoint, nVar});
+    dumpd("p2v_mu", mu, {(long)nPoint});
+    dumpd("p2v_kappa", kap, {(long)nPoint});
+    dumpd("p2v_cp", cp, {(long)nPoint});
+    dumpd("p2v_eddy", ed, {(long)nPoint});
+    dumpd("p2v_Dij", Dij, {(long)nPoint, nSpecies, nSpecies});
+    std::vector<double> prm = {(double)nerr, cfg->GetTemperatureMin(), cfg->GetTemperatureMax(),
+                               cfg->GetTemperature_Ref(), cfg->GetEnergy_Ref(), cfg->GetGas_Constant_Ref(),
+                               cfg->GetPressure_Ref(), cfg->GetViscosity_Ref(), cfg->GetConductivity_Ref(),
+                               cfg->GetVelocity_Ref(), cfg->GetLength_Ref(), (double)cfg->GetExtIter()};
+    dumpd("p2v_params", prm, {(long)prm.size()});
+  }
+
   std::vector<int64_t> dims = {nDim, nVar, nPrimVar, nPrimVarGrad, nSpecies, implicit ? 1 : 0, rans ? 1 : 0};
   dumpi("dims", dims, {7});
   g_manifest.close();

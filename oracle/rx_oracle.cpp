@@ -1976,6 +1976,257 @@ void orc_update_rk(int64_t N, int nb, int nDim, const double* Res, double alpha,
 }
 
 // =================================================================================================
+// next-1: CReactiveEulerSolver::SetPrimitive_Variables (solver_direct_reactive.cpp:985-1040) per point:
+// CReactiveNSVariable::SetPrimVar(eddy, k) (variable_direct_reactive.cpp:1188-1228) ->
+// CReactiveEulerVariable::SetPrimVar (:292-330) -> Cons2PrimVar (:550-778), Cp from the sound speed,
+// CalcdTdU (:786-823), CalcdPdU (:829-853); transport: ComputeEta (reacting_model_library.cpp:634-656),
+// ComputeLambda (:671-696), GetDij_SM (:751-766).
+// prm = {Tmin, Tmax, T_ref, E_ref, R_ref, P_ref, Visc_ref, Cond_ref, Vel_ref, Len_ref, ExtIter, clip_temp}.
+// U is updated in place (the reference clamps negative partial densities / density in Solution).
+// Returns -1 when the bisection fails (std::runtime_error in the reference), else the non-physical count.
+// =================================================================================================
+namespace {
+double mix_enthalpy(const Mech& m, double T, const double* Ys) {  // ComputeEnthalpy :519-523
+  double h = 0.0;
+  for (int s = 0; s < m.ns; ++s) {
+    const double y = Ys[s] < 0.0 ? 1.0e-30 : Ys[s];
+    h += y * (spline(m, P_H, s, T) / m.mm[s]);
+  }
+  return h;
+}
+double mix_rgas(const Mech& m, const double* Ys) {  // SetRgas :26-31
+  double r = 0.0;
+  for (int s = 0; s < m.ns; ++s) r += (Ys[s] < 0.0 ? 1.0e-30 : Ys[s]) * m.ri[s];
+  return r;
+}
+// Cons2PrimVar (:550-778); V[T] on entry is the secant's start. Throws std::runtime_error on failure.
+bool cons2prim(const Mech& m, int nDim, double* U, double* V, double val_ke, const double* prm) {
+  const int ns = m.ns;
+  const int T_ = 0, VX = 1, P_ = nDim + 1, RHO = nDim + 2, H_ = nDim + 3, A_ = nDim + 4, RHOS = nDim + 5;
+  const int RHO_S = 0, RHOVX_S = 1, RHOE_S = nDim + 1, RHOS_S = nDim + 2;
+  bool nonPhys = false;
+  for (int s = 0; s < ns; ++s)
+    if (U[RHOS_S + s] < 0.0) {
+      U[RHOS_S + s] = 1.0e-30;
+      nonPhys = true;
+    }
+  if (U[RHO_S] < EPS) {
+    V[RHO] = U[RHO_S] = EPS;
+    nonPhys = true;
+  } else {
+    V[RHO] = U[RHO_S];
+  }
+  for (int s = 0; s < ns; ++s) V[RHOS + s] = U[RHOS_S + s] / U[RHO_S];
+  double Ys[32];
+  for (int s = 0; s < ns; ++s) Ys[s] = V[RHOS + s];
+  double sy = 0.0;
+  for (int s = 0; s < ns; ++s) sy += Ys[s];
+  nonPhys = nonPhys || (std::abs(sy - 1.0) > 0.1);
+  const double rho = U[RHO_S];
+  const double rhoE = U[RHOE_S] - rho * val_ke;
+  double sqvel = 0.0;
+  for (int d = 0; d < nDim; ++d) {
+    V[VX + d] = U[RHOVX_S + d] / rho;
+    sqvel += V[VX + d] * V[VX + d];
+  }
+  const double T_ref = prm[2], E_ref = prm[3], R_ref = prm[4];
+  const double Tmin = prm[0] / T_ref, Tmax = prm[1] / T_ref;
+  const double NRtol = 1.0e-6, Btol = 1.0e-4;
+  const int maxNIter = 7, maxBIter = 32;
+  bool NRconvg = false, Bconvg;
+  const double Rgas = mix_rgas(m, Ys) / R_ref;
+  const double C1 = (-rhoE + 0.5 * rho * sqvel) / (rho * Rgas);
+  const double C2 = 1.0 / Rgas;
+  const double old_temp = V[T_];
+  double T = V[T_], Told = T + 1.0, Tnew, f, df, hs, hs_old;
+  for (int iIter = 0; iIter < maxNIter; ++iIter) {
+    try {
+      const double dim_temp = T * T_ref, dim_temp_old = Told * T_ref;
+      hs_old = mix_enthalpy(m, dim_temp_old, Ys) / E_ref;
+      hs = mix_enthalpy(m, dim_temp, Ys) / E_ref;
+      f = T - C1 - C2 * hs;
+      df = T - Told + C2 * (hs_old - hs);
+      Tnew = T - f * (T - Told) / df;
+      if (std::abs(Tnew - T) < NRtol) {
+        NRconvg = true;
+        break;
+      } else {
+        Told = T;
+        T = Tnew;
+      }
+    } catch (const std::out_of_range&) {
+      double Ta = Tmin, Tb = Tmax;
+      for (int b = 0; b < 10000; ++b) {
+        T = (Ta + Tb) / 2.0;
+        hs = mix_enthalpy(m, T * T_ref, Ys) / E_ref;
+        f = T - C1 - C2 * hs;
+        if (std::abs(f) < Btol) {
+          NRconvg = true;
+          break;
+        } else {
+          if (f > 0) Ta = T;
+          else Tb = T;
+        }
+      }
+      if (NRconvg) break;
+      throw std::runtime_error("Convergence not achieved for bisection method after catching out of range");
+    }
+  }
+  if (NRconvg) {
+    V[T_] = T;
+  } else {
+    Bconvg = false;
+    double Ta = Tmin, Tb = Tmax;
+    for (int b = 0; b < maxBIter; ++b) {
+      T = (Ta + Tb) / 2.0;
+      hs = mix_enthalpy(m, T * T_ref, Ys) / E_ref;
+      f = T - C1 - C2 * hs;
+      if (std::abs(f) < Btol) {
+        V[T_] = T;
+        Bconvg = true;
+        break;
+      } else {
+        if (f > 0) Ta = T;
+        else Tb = T;
+      }
+    }
+    if (!Bconvg) throw std::runtime_error("Convergence not achieved for bisection method");
+  }
+  if (prm[10] > 0 && prm[11] != 0) V[T_] = std::min(std::max(V[T_], 0.95 * old_temp), 1.05 * old_temp);
+  if (V[T_] < Tmin) {
+    V[T_] = Tmin;
+    nonPhys = true;
+  } else if (V[T_] > Tmax) {
+    V[T_] = Tmax;
+    nonPhys = true;
+  }
+  T = V[T_];
+  V[P_] = rho * Rgas * T;
+  if (V[P_] < EPS) {
+    V[P_] = EPS;
+    nonPhys = true;
+  }
+  const double dim_temp = T * T_ref;
+  double Cp = 0.0;  // ComputeFrozenSoundSpeed(T, ys, P, rho) :432-436 via ComputeFrozenGamma :398-403
+  for (int s = 0; s < ns; ++s) Cp += (Ys[s] < 0.0 ? 1.0e-30 : Ys[s]) * (spline(m, P_CP, s, dim_temp) / m.mm[s]);
+  const double Rg = mix_rgas(m, Ys);
+  const double gamma = Cp / (Cp - Rg);
+  V[A_] = std::sqrt(gamma * V[P_] / rho);
+  if (V[A_] < EPS) {
+    V[A_] = EPS;
+    nonPhys = true;
+  }
+  V[H_] = (U[RHOE_S] + V[P_]) / rho;
+  return nonPhys;
+}
+}  // namespace
+
+int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const double* Uold, const double* tke,
+                      const double* mut, const double* prm, double* dPdU, double* dTdU, double* mu, double* kappa,
+                      double* Dij, double* eddy, double* cp_out) {
+  const Mech& m = *static_cast<Mech*>(h);
+  const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5;
+  const int T_ = 0, VX = 1, P_ = nDim + 1, RHO = nDim + 2, A_ = nDim + 4, RHOS = nDim + 5;
+  const double T_ref = prm[2], E_ref = prm[3], R_ref = prm[4], P_ref = prm[5], Visc_ref = prm[6],
+               Cond_ref = prm[7], Vel_ref = prm[8], Len_ref = prm[9];
+  int64_t count = 0;
+  try {
+    for (int64_t i = 0; i < N; ++i) {
+      double* u = U + i * nVar;
+      double* v = V + i * nPV;
+      const double ke = tke ? tke[i] : 0.0;
+      const double vT0 = v[T_];
+      bool nonPhys = cons2prim(m, nDim, u, v, ke, prm);
+      if (nonPhys && prm[10] > 0 && Uold) {  // SetPrimVar :297-301: back to Solution_Old
+        for (int q = 0; q < nVar; ++q) u[q] = Uold[i * nVar + q];
+        (void)vT0;
+        const bool np_old = cons2prim(m, nDim, u, v, ke, prm);
+        if (np_old) return -1;
+      }
+      // Cp = ComputeCP_FromSoundSpeed(T, a, Ys) / R_ref (:304-311)
+      const double dim_temp = v[T_] * T_ref, dim_a = v[A_] * Vel_ref;
+      double Ys[32];
+      for (int s = 0; s < ns; ++s) Ys[s] = v[RHOS + s];
+      const double Rg = mix_rgas(m, Ys);
+      const double Cp = (dim_a * dim_a * Rg) / (dim_a * dim_a - Rg * dim_temp) / R_ref;
+      if (cp_out) cp_out[i] = Cp;
+      // CalcdTdU (:786-823)
+      const double rhov = v[RHO], T = v[T_];
+      const double dim_cp = Cp * R_ref;
+      const double Cv = (dim_cp - mix_rgas(m, Ys)) / R_ref;
+      const double rhoCv = rhov * Cv;
+      double sq = 0.0;
+      for (int d = 0; d < nDim; ++d) sq += v[VX + d] * v[VX + d];
+      double dTdYs[32];
+      for (int s = 0; s < ns; ++s) dTdYs[s] = (spline(m, P_H, s, dim_temp) / m.mm[s] - m.ri[s] * dim_temp) / E_ref;
+      double* dt = dTdU + i * nVar;
+      dt[0] = 0.5 * sq / rhoCv;
+      for (int d = 0; d < nDim; ++d) dt[1 + d] = -v[VX + d] / rhoCv;
+      dt[nDim + 1] = 1.0 / rhoCv;
+      for (int s = 0; s < ns; ++s) dt[nDim + 2 + s] = -dTdYs[s] / rhoCv;
+      // CalcdPdU (:829-853)
+      const double Gamma = dim_cp / (dim_cp - mix_rgas(m, Ys));
+      double* dp = dPdU + i * nVar;
+      dp[0] = (Gamma - 1.0) * 0.5 * sq;
+      for (int d = 0; d < nDim; ++d) dp[1 + d] = (1.0 - Gamma) * v[VX + d];
+      dp[nDim + 1] = Gamma - 1.0;
+      for (int s = 0; s < ns; ++s) dp[nDim + 2 + s] = m.ri[s] / R_ref * T - (Gamma - 1.0) * dTdYs[s];
+      // CReactiveNSVariable::SetPrimVar transport (:1188-1228)
+      eddy[i] = mut ? mut[i] : 0.0;
+      const double dim_press = v[P_] * P_ref / 101325.0;
+      double visc[32], cond[32], yom[32];
+      for (int s = 0; s < ns; ++s) {
+        visc[s] = spline(m, P_MU, s, dim_temp);
+        cond[s] = spline(m, P_KAPPA, s, dim_temp);
+      }
+      // ComputeEta: clamped mass fractions
+      for (int s = 0; s < ns; ++s) yom[s] = (Ys[s] < 0.0 ? 1.0e-30 : Ys[s]) / m.mm[s];
+      double eta = 0.0;
+      for (int a = 0; a < ns; ++a) {
+        double phi = 0.0;
+        for (int b = 0; b < ns; ++b)
+          phi += yom[b] / std::sqrt(8.0 * (1.0 + m.mm[a] / m.mm[b])) *
+                 (1.0 + std::sqrt(visc[a] / visc[b]) * std::pow(m.mm[b] / m.mm[a], 0.25)) *
+                 (1.0 + std::sqrt(visc[a] / visc[b]) * std::pow(m.mm[b] / m.mm[a], 0.25));
+        eta += visc[a] * yom[a] / phi;
+      }
+      mu[i] = eta / Visc_ref;
+      // ComputeLambda: the argument (unclamped) mass fractions
+      for (int s = 0; s < ns; ++s) yom[s] = Ys[s] / m.mm[s];
+      double lam = 0.0;
+      for (int a = 0; a < ns; ++a) {
+        double phi = 0.0;
+        for (int b = 0; b < ns; ++b)
+          if (b != a)
+            phi += 1.065 * yom[b] / std::sqrt(8.0 * (1.0 + m.mm[a] / m.mm[b])) *
+                   (1.0 + std::sqrt(visc[a] / visc[b]) * std::pow(m.mm[b] / m.mm[a], 0.25)) *
+                   (1.0 + std::sqrt(visc[a] / visc[b]) * std::pow(m.mm[b] / m.mm[a], 0.25));
+        phi += yom[a];
+        lam += cond[a] * yom[a] / phi;
+      }
+      kappa[i] = lam / Cond_ref;
+      // GetDij_SM / (Vel_ref * Len_ref * 1e4), symmetric
+      double* D = Dij + i * ns * ns;
+      const double scale = Vel_ref * Len_ref * 1.0e4;
+      for (int a = 0; a < ns; ++a) {
+        const double mi = m.mm[a], dvi = std::cbrt(m.dv[a]);
+        for (int b = a; b < ns; ++b) {
+          const double Mij = std::sqrt((mi * m.mm[b]) / (mi + m.mm[b]));
+          const double dvj = std::cbrt(m.dv[b]);
+          const double d = 1.0e-3 * std::pow(dim_temp, 1.75) / (dim_press * Mij * (dvi + dvj) * (dvi + dvj));
+          D[a * ns + b] = d / scale;
+          D[b * ns + a] = d / scale;
+        }
+      }
+      if (nonPhys) ++count;
+    }
+  } catch (const std::exception&) {
+    return -1;
+  }
+  return (int)count;
+}
+
+// =================================================================================================
 // a14 + next-2: Menter SST turbulence solver on the flow state (CTurbSSTSolver / CTurbSolver,
 // SU2_CFD/src/solver_direct_turbulent.cpp; numerics SU2_CFD/src/numerics_direct_turbulent.cpp;
 // node record CTurbSSTVariable SU2_CFD/src/variable_direct_turbulent.cpp). Turbulent solution
