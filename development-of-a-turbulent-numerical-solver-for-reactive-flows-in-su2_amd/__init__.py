@@ -30,7 +30,7 @@ FIELDS = ["U", "V", "DPDU", "DTDU", "MU", "KAPPA", "DIJ", "GRAD", "LIMITER", "TK
 F = {name: k for k, name in enumerate(FIELDS)}
 # rx_kernel
 KERNELS = ["CONV", "VISC", "SOURCE", "GRAD", "LIMITER", "DT", "SPMV", "ILU_BUILD", "ILU_APPLY", "LUSGS", "KRYLOV",
-           "UPDATE", "SOLVE", "VISC_JAC", "ASSEMBLE", "STRAIN", "SST_GRAD", "SST_UPW", "SST_VISC", "SST_SOURCE",
+           "UPDATE", "SOLVE", "VISC_JAC", "ASSEMBLE", "STRAIN", "PRIMITIVE", "SST_GRAD", "SST_UPW", "SST_VISC", "SST_SOURCE",
            "SST_SYSTEM", "SST_SOLVE", "SST_POST"]
 K = {name: k for k, name in enumerate(KERNELS)}
 
@@ -76,7 +76,9 @@ class Cfg(C.Structure):
                 ("pasr_lb", C.c_double), ("cfl", C.c_double), ("max_delta_time", C.c_double),
                 ("ref_elem_length", C.c_double), ("limiter_coeff", C.c_double), ("lin_tol", C.c_double),
                 ("relaxation", C.c_double), ("implicit", C.c_int32), ("rans", C.c_int32), ("lin_iter", C.c_int32),
-                ("lin_prec", C.c_int32), ("spatial_order", C.c_int32)]
+                ("lin_prec", C.c_int32), ("spatial_order", C.c_int32), ("clip_temp", C.c_int32),
+                ("t_min", C.c_double), ("t_max", C.c_double), ("p_ref", C.c_double), ("visc_ref", C.c_double),
+                ("cond_ref", C.c_double), ("vel_ref", C.c_double), ("len_ref", C.c_double)]
 
 
 _lib = None
@@ -111,6 +113,7 @@ def lib():
         _lib.rx_explicit_euler.argtypes = [C.c_void_p, C.c_void_p]
         _lib.rx_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         _lib.rx_explicit_rk.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p]
+        _lib.rx_set_primitive.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int64)]
         _lib.rx_profile_enable.argtypes = [C.c_void_p, C.c_int]
         _lib.rx_profile_read.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         _lib.rx_last_error_index.argtypes = [C.c_void_p]
@@ -217,7 +220,8 @@ def default_cfg(**kw):
     c = dict(mach_inf=0.01819, T_ref=1.0, E_ref=1.0, R_ref=1.0, rho_ref=1.0, t_ref=1.0, prandtl_lam=0.72,
              prandtl_turb=0.9, lewis_turb=1.2, c_mu=0.09, pasr_lb=0.2, cfl=5.0, max_delta_time=1e6,
              ref_elem_length=0.1, limiter_coeff=0.5, lin_tol=1e-6, relaxation=1.0, implicit=1, rans=1, lin_iter=5,
-             lin_prec=1, spatial_order=0)
+             lin_prec=1, spatial_order=0, clip_temp=0, t_min=200.0, t_max=6000.0, p_ref=1.0, visc_ref=1.0,
+             cond_ref=1.0, vel_ref=1.0, len_ref=1.0)
     c.update(kw)
     cfg = Cfg()
     for k, v in c.items():
@@ -363,6 +367,13 @@ class ReactiveNSSolver:
 
     def SetStrainMag(self):
         self._call("rx_strain_mag")
+
+    def SetPrimitive_Variables(self, ext_iter=0, count=False):
+        """Cons2Prim + transport on the device; returns the non-physical count when count=True (syncs)."""
+        n = C.c_int64(0)
+        _chk(lib().rx_set_primitive(self.h, int(ext_iter), C.byref(n) if count else None), "rx_set_primitive",
+             self.h)
+        return n.value if count else None
 
     def sync(self):
         self._call("rx_sync")

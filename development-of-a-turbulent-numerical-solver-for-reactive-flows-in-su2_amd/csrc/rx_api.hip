@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -460,6 +461,21 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     m.ty2 = up(mech->tab_y2, (size_t)5 * ns * nt);
     m.mtot = 0.0;
     for (int s = 0; s < ns; ++s) m.mtot += mech->mmass[s];
+    {
+      std::vector<double> phic(ns * ns), pw(ns * ns), mij(ns * ns), dvs(ns * ns);
+      const double* M = mech->mmass;
+      for (int a = 0; a < ns; ++a)
+        for (int b = 0; b < ns; ++b) {
+          phic[a * ns + b] = std::sqrt(8.0 * (1.0 + M[a] / M[b]));
+          pw[a * ns + b] = std::pow(M[b] / M[a], 0.25);
+          mij[a * ns + b] = std::sqrt((M[a] * M[b]) / (M[a] + M[b]));
+          dvs[a * ns + b] = std::cbrt(mech->diff_vol[a]) + std::cbrt(mech->diff_vol[b]);
+        }
+      m.phic = up(phic.data(), phic.size());
+      m.pw25 = up(pw.data(), pw.size());
+      m.mij = up(mij.data(), mij.size());
+      m.dvs = up(dvs.data(), dvs.size());
+    }
     for (int r = 0; r < rx::kMaxNR; ++r) m.neg_reac[r] = m.neg_prod[r] = 0;
     for (int r = 0; r < nr; ++r)
       for (int s = 0; s < ns; ++s) {
@@ -530,7 +546,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     CK(dalloc(ctx, &ctx->lim_mx, N * ctx->nL));
   }
   CK(dalloc(ctx, &ctx->red, 256 * 32 + 1024));
-  CK(dalloc(ctx, &ctx->err, 2));
+  CK(dalloc(ctx, &ctx->err, 4));
   if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_red), sizeof(double) * (256 * 32 + 1024)) != hipSuccess)
     CK(RX_ERR_HIP);
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) CK(RX_ERR_HIP);
@@ -734,6 +750,24 @@ int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
     if ((rc = rx_la_explicit_update(ctx))) return rc;
   }
   return res_rms ? rx_la_rms_read(ctx, res_rms) : RX_OK;
+}
+
+// SetPrimitive_Variables (solver_direct_reactive.cpp:985-1040); the residual reset it also does is
+// rx_residual_zero.
+int rx_set_primitive(rx_ctx* ctx, int ext_iter, int64_t* n_nonphys) {
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
+  {
+    RxPhase ph(ctx, RX_K_PRIMITIVE);
+    RX_HIP(hipMemsetAsync(ctx->err + 2, 0, sizeof(int), ctx->stream));
+    const int rc = rx_launch_set_primitive(ctx, ext_iter);
+    if (rc) return rc;
+  }
+  if (!n_nonphys) return RX_OK;
+  int h = 0;
+  RX_HIP(hipMemcpyAsync(&h, ctx->err + 2, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  const int rc = rx_sync(ctx);
+  *n_nonphys = h;
+  return rc;
 }
 
 // ExplicitRK_Iteration (solver_direct_reactive.cpp:2456-2493): stage iRKStep with RK_ALPHA_COEFF[iRKStep].

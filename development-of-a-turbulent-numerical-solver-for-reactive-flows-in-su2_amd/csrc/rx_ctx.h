@@ -172,6 +172,7 @@ struct RxPhase {
 // kernel launchers (rx_kernels.hip)
 int rx_launch_ausm_node(rx_ctx* ctx);
 int rx_launch_muscl(rx_ctx* ctx);
+int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter);
 int rx_launch_ausm_edge(rx_ctx* ctx);
 int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);

@@ -18,7 +18,7 @@ constexpr double kR = kNA * kKB * 1.0e3;           // physical_chemical_library.
 constexpr double kRatm = 1.0e-3 * 0.082057338;     // :579
 constexpr double kTWO3 = 2.0 / 3.0;
 enum { P_CP = 0, P_H = 1, P_S = 2, P_MU = 3, P_KAPPA = 4 };
-enum { ERR_NONE = 0, ERR_RANGE = 1, ERR_NAN = 2, ERR_GEOM = 3 };
+enum { ERR_NONE = 0, ERR_RANGE = 1, ERR_NAN = 2, ERR_GEOM = 3, ERR_CONV = 4 };
 
 constexpr int kMaxNS = 12;
 constexpr int kMaxNR = 8;
@@ -33,6 +33,12 @@ struct DevMech {
   const int *rev, *hasb;
   const double *tx, *ty, *ty2;  // [5][ns][ntab]
   double mtot;                  // sum of molar masses
+  // transport constants of the mechanism, evaluated once on the host with the reference's expressions
+  // (ComputeEta / ComputeLambda :634-696, GetDij_SM :751-766 of reacting_model_library.cpp):
+  const double *phic;           // [ns][ns] sqrt(8 (1 + M_a / M_b))
+  const double *pw25;           // [ns][ns] pow(M_b / M_a, 0.25)
+  const double *mij;            // [ns][ns] sqrt(M_a M_b / (M_a + M_b))
+  const double *dvs;            // [ns][ns] cbrt(V_a) + cbrt(V_b)
   uint32_t neg_reac[kMaxNR], neg_prod[kMaxNR];  // species masks with negative rate exponents
 };
 

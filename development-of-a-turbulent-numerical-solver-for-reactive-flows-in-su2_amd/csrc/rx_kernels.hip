@@ -77,6 +77,290 @@ __global__ __launch_bounds__(kBlock) void k_ausm_node(int N, const int32_t* __re
   if (bad) set_err(err, ERR_NAN, i);
 }
 
+// next-1: CReactiveEulerSolver::SetPrimitive_Variables (solver_direct_reactive.cpp:985-1040), one thread per
+// point: CReactiveNSVariable::SetPrimVar(eddy, k) (variable_direct_reactive.cpp:1188-1228) ->
+// CReactiveEulerVariable::SetPrimVar (:292-330): Cons2PrimVar (:550-778; secant from the previous T, then
+// the bisection fallbacks), Cp from the sound speed, CalcdTdU (:786-823), CalcdPdU (:829-853); transport
+// ComputeEta / ComputeLambda / GetDij_SM (reacting_model_library.cpp:634-766) with the mechanism
+// constants of DevMech. std::min/max as ternaries. ERR_CONV: the reference's "Convergence not achieved
+// for bisection method" runtime_error.
+struct PrimParams {
+  double Tmin, Tmax, T_ref, E_ref, R_ref, P_ref, Visc_ref, Cond_ref, Vel_ref, Len_ref;
+  int ext_iter, clip_temp, rans;
+};
+
+template <int NS>
+__device__ inline double mix_h(const DevMech& m, double T, const double* Yc, int* err) {
+  double h = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) h += Yc[s] * (spline(m, P_H, s, T, err) / m.mm[s]);
+  return h;
+}
+
+// Cons2PrimVar on one point; V[T] holds the secant's start. Returns nonPhys; *fail on bisection failure.
+template <int NS, int NDIM>
+__device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, double* U, double* V, double val_ke,
+                                     bool* fail) {
+  constexpr int VX = 1, P_ = NDIM + 1, RHO = NDIM + 2, H_ = NDIM + 3, A_ = NDIM + 4, RHOS = NDIM + 5;
+  constexpr int RHOVX_S = 1, RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
+  bool nonPhys = false;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (U[RHOS_S + s] < 0.0) {
+      U[RHOS_S + s] = 1.0e-30;
+      nonPhys = true;
+    }
+  if (U[0] < kEPS) {
+    V[RHO] = U[0] = kEPS;
+    nonPhys = true;
+  } else {
+    V[RHO] = U[0];
+  }
+  double Ys[NS], Yc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    V[RHOS + s] = U[RHOS_S + s] / U[0];
+    Ys[s] = V[RHOS + s];
+    Yc[s] = Ys[s] < 0.0 ? 1.0e-30 : Ys[s];
+  }
+  double sy = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) sy += Ys[s];
+  nonPhys = nonPhys || (fabs(sy - 1.0) > 0.1);
+  const double rho = U[0];
+  const double rhoE = U[RHOE_S] - rho * val_ke;
+  double sqvel = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    V[VX + d] = U[RHOVX_S + d] / rho;
+    sqvel += V[VX + d] * V[VX + d];
+  }
+  const double Tmin = P.Tmin / P.T_ref, Tmax = P.Tmax / P.T_ref;
+  double Rg = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) Rg += Yc[s] * (kR / m.mm[s]);
+  const double Rgas = Rg / P.R_ref;
+  const double C1 = (-rhoE + 0.5 * rho * sqvel) / (rho * Rgas);
+  const double C2 = 1.0 / Rgas;
+  const double old_temp = V[0];
+  double T = V[0], Told = T + 1.0;
+  bool conv = false;
+  for (int it = 0; it < 7; ++it) {
+    int e1 = ERR_NONE;
+    const double hs_old = mix_h<NS>(m, Told * P.T_ref, Yc, &e1) / P.E_ref;
+    const double hs = mix_h<NS>(m, T * P.T_ref, Yc, &e1) / P.E_ref;
+    if (e1 != ERR_NONE) {  // std::out_of_range inside the secant: bisection on [Tmin, Tmax], 10000 steps
+      double Ta = Tmin, Tb = Tmax;
+      for (int b = 0; b < 10000; ++b) {
+        T = (Ta + Tb) / 2.0;
+        int e2 = ERR_NONE;
+        const double h2 = mix_h<NS>(m, T * P.T_ref, Yc, &e2) / P.E_ref;
+        const double f = T - C1 - C2 * h2;
+        if (fabs(f) < 1.0e-4) {
+          conv = true;
+          break;
+        }
+        if (f > 0) Ta = T;
+        else Tb = T;
+      }
+      if (!conv) *fail = true;
+      break;
+    }
+    const double f = T - C1 - C2 * hs;
+    const double df = T - Told + C2 * (hs_old - hs);
+    const double Tnew = T - f * (T - Told) / df;
+    if (fabs(Tnew - T) < 1.0e-6) {
+      conv = true;
+      break;
+    }
+    Told = T;
+    T = Tnew;
+  }
+  if (*fail) return nonPhys;
+  if (conv) {
+    V[0] = T;
+  } else {
+    bool bconv = false;
+    double Ta = Tmin, Tb = Tmax;
+    for (int b = 0; b < 32; ++b) {
+      T = (Ta + Tb) / 2.0;
+      int e2 = ERR_NONE;
+      const double h2 = mix_h<NS>(m, T * P.T_ref, Yc, &e2) / P.E_ref;
+      const double f = T - C1 - C2 * h2;
+      if (fabs(f) < 1.0e-4) {
+        V[0] = T;
+        bconv = true;
+        break;
+      }
+      if (f > 0) Ta = T;
+      else Tb = T;
+    }
+    if (!bconv) {
+      *fail = true;
+      return nonPhys;
+    }
+  }
+  if (P.ext_iter > 0 && P.clip_temp) {
+    const double lo = 0.95 * old_temp, hi = 1.05 * old_temp;
+    const double mx = (V[0] < lo) ? lo : V[0];
+    V[0] = (hi < mx) ? hi : mx;
+  }
+  if (V[0] < Tmin) {
+    V[0] = Tmin;
+    nonPhys = true;
+  } else if (V[0] > Tmax) {
+    V[0] = Tmax;
+    nonPhys = true;
+  }
+  T = V[0];
+  V[P_] = rho * Rgas * T;
+  if (V[P_] < kEPS) {
+    V[P_] = kEPS;
+    nonPhys = true;
+  }
+  const double dim_temp = T * P.T_ref;
+  int e3 = ERR_NONE;
+  double Cp = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) Cp += Yc[s] * (spline(m, P_CP, s, dim_temp, &e3) / m.mm[s]);
+  const double gamma = Cp / (Cp - Rg);
+  V[A_] = sqrt(gamma * V[P_] / rho);
+  if (V[A_] < kEPS) {
+    V[A_] = kEPS;
+    nonPhys = true;
+  }
+  V[H_] = (U[RHOE_S] + V[P_]) / rho;
+  if (e3 != ERR_NONE) *fail = true;
+  return nonPhys;
+}
+
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) void k_set_primitive(int N, DevMech m, PrimParams P, double* __restrict__ Ug,
+                                                          double* __restrict__ Vg, const double* __restrict__ Uold,
+                                                          const double* __restrict__ tke,
+                                                          const double* __restrict__ mut, double* __restrict__ dPdU,
+                                                          double* __restrict__ dTdU, double* __restrict__ mu,
+                                                          double* __restrict__ kappa, double* __restrict__ Dij,
+                                                          double* __restrict__ eddy, int* __restrict__ err) {
+  constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
+  constexpr int VX = 1, P_ = NDIM + 1, RHO = NDIM + 2, A_ = NDIM + 4, RHOS = NDIM + 5;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double U[nVar], V[nPV];
+#pragma unroll
+  for (int q = 0; q < nVar; ++q) U[q] = Ug[(size_t)i * nVar + q];
+  V[0] = Vg[(size_t)i * nPV];
+  const double ke = P.rans ? tke[i] : 0.0;
+  bool fail = false;
+  bool nonPhys = cons2prim_dev<NS, NDIM>(m, P, U, V, ke, &fail);
+  if (!fail && nonPhys && P.ext_iter > 0 && Uold) {  // SetPrimVar :297-301: restart from Solution_Old
+#pragma unroll
+    for (int q = 0; q < nVar; ++q) U[q] = Uold[(size_t)i * nVar + q];
+    if (cons2prim_dev<NS, NDIM>(m, P, U, V, ke, &fail)) fail = true;
+  }
+  if (fail) {
+    if (atomicCAS(err, 0, ERR_CONV) == 0) err[1] = i;
+    return;
+  }
+  if (nonPhys) atomicAdd(err + 2, 1);
+#pragma unroll
+  for (int q = 0; q < nVar; ++q) Ug[(size_t)i * nVar + q] = U[q];
+#pragma unroll
+  for (int q = 0; q < nPV; ++q) Vg[(size_t)i * nPV + q] = V[q];
+  // Cp = ComputeCP_FromSoundSpeed(T, a, Ys) / R_ref
+  const double dim_temp = V[0] * P.T_ref, dim_a = V[A_] * P.Vel_ref;
+  double Ys[NS], Yc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    Ys[s] = V[RHOS + s];
+    Yc[s] = Ys[s] < 0.0 ? 1.0e-30 : Ys[s];
+  }
+  double Rg = 0.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) Rg += Yc[s] * (kR / m.mm[s]);
+  const double Cp = (dim_a * dim_a * Rg) / (dim_a * dim_a - Rg * dim_temp) / P.R_ref;
+  // CalcdTdU / CalcdPdU
+  const double dim_cp = Cp * P.R_ref;
+  const double Cv = (dim_cp - Rg) / P.R_ref;
+  const double rhoCv = V[RHO] * Cv;
+  double sq = 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) sq += V[VX + d] * V[VX + d];
+  int e4 = ERR_NONE;
+  double dTdYs[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    dTdYs[s] = (spline(m, P_H, s, dim_temp, &e4) / m.mm[s] - (kR / m.mm[s]) * dim_temp) / P.E_ref;
+  double* dt = dTdU + (size_t)i * nVar;
+  dt[0] = 0.5 * sq / rhoCv;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) dt[1 + d] = -V[VX + d] / rhoCv;
+  dt[NDIM + 1] = 1.0 / rhoCv;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) dt[NDIM + 2 + s] = -dTdYs[s] / rhoCv;
+  const double Gamma = dim_cp / (dim_cp - Rg);
+  double* dp = dPdU + (size_t)i * nVar;
+  dp[0] = (Gamma - 1.0) * 0.5 * sq;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) dp[1 + d] = (1.0 - Gamma) * V[VX + d];
+  dp[NDIM + 1] = Gamma - 1.0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) dp[NDIM + 2 + s] = (kR / m.mm[s]) / P.R_ref * V[0] - (Gamma - 1.0) * dTdYs[s];
+  // transport (CReactiveNSVariable::SetPrimVar)
+  eddy[i] = P.rans ? mut[i] : 0.0;
+  const double dim_press = V[P_] * P.P_ref / 101325.0;
+  double visc[NS], cond[NS], yom[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    visc[s] = spline(m, P_MU, s, dim_temp, &e4);
+    cond[s] = spline(m, P_KAPPA, s, dim_temp, &e4);
+    yom[s] = Yc[s] / m.mm[s];
+  }
+  double eta = 0.0;
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    double phi = 0.0;
+#pragma unroll
+    for (int b = 0; b < NS; ++b) {
+      const double f = 1.0 + sqrt(visc[a] / visc[b]) * m.pw25[a * NS + b];
+      phi += yom[b] / m.phic[a * NS + b] * f * f;
+    }
+    eta += visc[a] * yom[a] / phi;
+  }
+  mu[i] = eta / P.Visc_ref;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) yom[s] = Ys[s] / m.mm[s];  // ComputeLambda: the unclamped argument
+  double lam = 0.0;
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    double phi = 0.0;
+#pragma unroll
+    for (int b = 0; b < NS; ++b)
+      if (b != a) {
+        const double f = 1.0 + sqrt(visc[a] / visc[b]) * m.pw25[a * NS + b];
+        phi += 1.065 * yom[b] / m.phic[a * NS + b] * f * f;
+      }
+    phi += yom[a];
+    lam += cond[a] * yom[a] / phi;
+  }
+  kappa[i] = lam / P.Cond_ref;
+  const double pT = 1.0e-3 * pow(dim_temp, 1.75);
+  const double scale = P.Vel_ref * P.Len_ref * 1.0e4;
+  double* D = Dij + (size_t)i * NS * NS;
+#pragma unroll
+  for (int a = 0; a < NS; ++a)
+#pragma unroll
+    for (int b = a; b < NS; ++b) {
+      const double sv = m.dvs[a * NS + b];
+      const double d = pT / (dim_press * m.mij[a * NS + b] * sv * sv);
+      D[a * NS + b] = d / scale;
+      D[b * NS + a] = d / scale;
+    }
+  if (e4 != ERR_NONE) {
+    if (atomicCAS(err, 0, ERR_RANGE) == 0) err[1] = i;
+  }
+}
+
 // a2 second order: MUSCL reconstruction of (T, u, v, P) per edge side with the optional limiter, and the
 // thermodynamically consistent state + pressure derivatives rebuilt through the library
 // (CReactiveEulerSolver::Upwind_Residual, solver_direct_reactive.cpp:2554-2729; ComputeDensity :457-460,
@@ -723,8 +1007,21 @@ int rx_check_error(rx_ctx* ctx) {
   if (h[0] != 0) {
     ctx->last_err_index = h[1];
     RX_HIP(hipMemsetAsync(ctx->err, 0, 2 * sizeof(int), ctx->stream));
-    return h[0] == ERR_RANGE ? RX_ERR_RANGE : RX_ERR_NAN;
+    return h[0] == ERR_RANGE ? RX_ERR_RANGE : (h[0] == ERR_CONV ? RX_ERR_NONPHYS : RX_ERR_NAN);
   }
+  return RX_OK;
+}
+
+int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter) {
+  if (ctx->nDim != 2) return RX_ERR_ARG;
+  const rx_cfg& c = ctx->cfg;
+  PrimParams P{c.t_min, c.t_max, c.T_ref, c.E_ref, c.R_ref, c.p_ref, c.visc_ref, c.cond_ref, c.vel_ref, c.len_ref,
+               ext_iter, c.clip_temp, c.rans};
+  RX_NS_SWITCH(ctx->ns, (k_set_primitive<NS_, 2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+                            (int)ctx->N, ctx->mech, P, ctx->f[RX_F_U], ctx->f[RX_F_V], ext_iter > 0 ? ctx->uold : nullptr,
+                            ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_DPDU], ctx->f[RX_F_DTDU], ctx->f[RX_F_MU],
+                            ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_EDDY], ctx->err)));
+  RX_HIP(hipGetLastError());
   return RX_OK;
 }
 

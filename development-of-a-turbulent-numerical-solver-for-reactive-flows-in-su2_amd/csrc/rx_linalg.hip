@@ -189,6 +189,9 @@ int rx_la_rms_read(rx_ctx* ctx, double* rms) {
 // Owned points, then Set_MPI_Solution (solver_direct_reactive.cpp:2403, 2445).
 int rx_la_implicit_update(rx_ctx* ctx) {
   const int64_t n = ctx->Nd * ctx->nVar;
+  // Solution_Old (Set_OldSolution) for SetPrimVar's non-physical restart
+  RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[RX_F_U], sizeof(double) * ctx->N * ctx->nVar, hipMemcpyDeviceToDevice,
+                        ctx->stream));
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_SOL],
                                                   ctx->cfg.relaxation, ctx->vol, ctx->f[RX_F_DT], 0, nullptr,
                                                   ctx->f[RX_F_U]);
@@ -198,6 +201,8 @@ int rx_la_implicit_update(rx_ctx* ctx) {
 
 int rx_la_explicit_update(rx_ctx* ctx) {
   const int64_t n = ctx->Nd * ctx->nVar;
+  RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[RX_F_U], sizeof(double) * ctx->N * ctx->nVar, hipMemcpyDeviceToDevice,
+                        ctx->stream));
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], 1.0,
                                                   ctx->vol, ctx->f[RX_F_DT], 1, nullptr, ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());

@@ -112,6 +112,9 @@ typedef struct {
   int32_t implicit, rans, lin_iter, lin_prec;    /* lin_prec: 0 = LU_SGS, 1 = ILU0 */
   int32_t spatial_order;  /* SPATIAL_ORDER_FLOW: 0 = 1ST_ORDER, 1 = 2ND_ORDER (MUSCL), 2 = 2ND_ORDER_LIMITER
                              (MUSCL with RX_F_LIMITER), Upwind_Residual :2554-2729 */
+  int32_t clip_temp;      /* CLIPPING_TEMPRATURE (Cons2PrimVar :711-712) */
+  double t_min, t_max;    /* TEMPERATURE_MIN / TEMPERATURE_MAX (Cons2PrimVar secant / bisection bounds) */
+  double p_ref, visc_ref, cond_ref, vel_ref, len_ref;  /* Pressure/Viscosity/Conductivity/Velocity/Length_Ref */
 } rx_cfg;
 
 typedef enum {
@@ -185,6 +188,15 @@ int rx_comm_init_host(rx_ctx *ctx, int nranks, int rank, const rx_host_comm *ops
 
 int rx_halo_exchange(rx_ctx *ctx, rx_field f); /* owned -> halo copies of a node field */
 
+/* CReactiveEulerSolver::SetPrimitive_Variables (solver_direct_reactive.cpp:985-1040) on every point:
+ * CReactiveNSVariable::SetPrimVar(eddy = MUT, k = TKE) (variable_direct_reactive.cpp:1188-1228) — Cons2PrimVar
+ * (:550-778) from RX_F_U with the secant started at the current RX_F_V temperature, Cp, dT/dU, dP/dU
+ * (:786-853), mu, kappa, Dij (reacting_model_library.cpp:634-766), eddy viscosity. Writes RX_F_V, DPDU,
+ * DTDU, MU, KAPPA, DIJ, EDDY (and clamps RX_F_U as the reference does). ext_iter > 0 enables the reference's
+ * restart from Solution_Old (kept by the last update) and CLIPPING_TEMPRATURE. n_nonphys (optional, syncs):
+ * the reference's ErrorCounter. A failed bisection returns RX_ERR_NONPHYS (the reference throws). */
+int rx_set_primitive(rx_ctx *ctx, int ext_iter, int64_t *n_nonphys);
+
 /* Time integration (updates RX_F_U). */
 int rx_explicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */);
 int rx_implicit_euler(rx_ctx *ctx, double *res_rms /* [nVar] or NULL */, int *lin_iters);
@@ -230,6 +242,7 @@ typedef enum {
   RX_K_VISC_JAC, /* viscous Jacobian kernel (implicit) */
   RX_K_ASSEMBLE, /* residual + BSR Jacobian assembly */
   RX_K_STRAIN,   /* flow StrainMag */
+  RX_K_PRIMITIVE, /* SetPrimitive_Variables */
   RX_K_SST_GRAD, /* SST: least-squares gradient of (k, omega) */
   RX_K_SST_UPW, RX_K_SST_VISC, RX_K_SST_SOURCE, /* SST residual + Jacobian loops */
   RX_K_SST_SYSTEM, /* SST: system build + preconditioner build */

@@ -102,6 +102,9 @@ int main(int argc, char** argv) {
     cfg.rans = 1;
     cfg.lin_iter = 5;
     cfg.lin_prec = 1;
+    cfg.t_min = 200.0;   // TEMPERATURE_MIN / MAX
+    cfg.t_max = 6000.0;
+    cfg.p_ref = cfg.visc_ref = cfg.cond_ref = cfg.vel_ref = cfg.len_ref = 1.0;  // DIMENSIONAL
 
     rx::ReactiveNSSolver solver(mesh, mech, cfg, 0);
     const struct {
