@@ -131,6 +131,8 @@ def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist):
     mesh, st, mech_arrays, kw = build_workload(nx, ny * world, ns, args.parts * world)
     sh = meshgen.shard(mesh, world, rank)
     st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
+    if args.cfl:
+        kw["cfl"] = args.cfl
     cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
     s = rx.ReactiveNSSolver(sh, rx.Mechanism(mech_arrays), cfg, device=local)
     uid = [rx.comm_unique_id() if rank == 0 else None]
@@ -157,6 +159,9 @@ def main():
     ap.add_argument("--parts", type=int, default=256,
                     help="partitions (= the reference's MPI ranks) of the ILU(0)/LU-SGS preconditioner")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--frozen", action="store_true",
+                    help="skip SetPrimitive_Variables: every step re-evaluates the same flow node records")
+    ap.add_argument("--cfl", type=float, default=0.0, help="CFL_NUMBER (default: the case's)")
     ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
     args = ap.parse_args()
 
@@ -199,6 +204,8 @@ def main():
             parallelism = f"sharded x{world} (RCCL halo exchange + all-reduce)"
     if s is None:
         mesh, st, mech_arrays, kw = build_workload(nx, ny, ns, args.parts)
+        if args.cfl:
+            kw["cfl"] = args.cfl
         cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
         s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg, device=local)
         t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
@@ -212,6 +219,8 @@ def main():
     rms_log = []
 
     def step():
+        if not args.frozen:
+            s.SetPrimitive_Variables()  # Cons2Prim + transport from the U of the previous update (next-1)
         s.SetPrimitive_Gradient_LS()
         s.SetStrainMag()
         s.SetTime_Step()
