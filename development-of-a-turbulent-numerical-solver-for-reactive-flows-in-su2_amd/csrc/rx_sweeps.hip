@@ -518,6 +518,251 @@ __global__ __launch_bounds__(256) void k_ilu_build_small(const int32_t* __restri
   }
 }
 
+// 2x2 fast path of k_ilu_build_small driven by the compact row plan (ilu_plan, nlow <= 3, npair <= 9): every
+// load a row needs (its A blocks, inv(D_j) of its lower neighbours, the A_jk of the plan) is issued at once,
+// the row lives in registers (runtime block indices resolved by selects), and the row is stored once. Rows
+// without a compact plan take the general per-block path. Same arithmetic as k_ilu_build_small.
+constexpr int kSmallMaxB = 12;
+__global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__ part_lvl,
+                                                     const int32_t* __restrict__ lvl_ptr,
+                                                     const int32_t* __restrict__ plan, const int4* __restrict__ slot,
+                                                     const int32_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                     const int32_t* __restrict__ upd_ptr,
+                                                     const int2* __restrict__ upd, const double* __restrict__ A,
+                                                     double* __restrict__ F, double* __restrict__ invD) {
+  constexpr int NV = 2, NV2 = 4;
+  const int p = blockIdx.x;
+  for (int l = part_lvl[p]; l < part_lvl[p + 1]; ++l) {
+    for (int r = lvl_ptr[l] + threadIdx.x; r < lvl_ptr[l + 1]; r += blockDim.x) {
+      const int4* pr = reinterpret_cast<const int4*>(plan + (size_t)r * 32);
+      int rec[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int4 v = pr[q];
+        rec[4 * q] = v.x;
+        rec[4 * q + 1] = v.y;
+        rec[4 * q + 2] = v.z;
+        rec[4 * q + 3] = v.w;
+      }
+      const int i = rec[0], k0 = rec[1], kd = rec[2], k1 = rec[3], ra = rec[4], rb = rec[5];
+      const int nlow = rec[6], npair = rec[7], nbk = k1 - k0;
+      for (int q = ra * NV2; q < k0 * NV2; ++q) F[q] = A[q];
+      for (int q = k1 * NV2; q < rb * NV2; ++q) F[q] = A[q];
+      if (nlow < 0 || nbk > kSmallMaxB) {  // general per-block path
+        for (int q = k0 * NV2; q < k1 * NV2; ++q) F[q] = A[q];
+        for (int k = k0; k < kd; ++k) {
+          const int j = col[k];
+          double Sinv[NV2], Bij[NV2], W[NV2];
+#pragma unroll
+          for (int q = 0; q < NV2; ++q) {
+            Sinv[q] = invD[(size_t)j * NV2 + q];
+            Bij[q] = F[(size_t)k * NV2 + q];
+          }
+#pragma unroll
+          for (int a = 0; a < NV; ++a)
+#pragma unroll
+            for (int c = 0; c < NV; ++c) {
+              double sm = 0.0;
+#pragma unroll
+              for (int q = 0; q < NV; ++q) sm += Bij[a * NV + q] * Sinv[q * NV + c];
+              W[a * NV + c] = sm;
+            }
+          for (int u = upd_ptr[k]; u < upd_ptr[k + 1]; ++u) {
+            const int2 h = upd[u];
+            double* Bik = F + (size_t)h.y * NV2;
+            const double* Bjk = F + (size_t)h.x * NV2;
+#pragma unroll
+            for (int a = 0; a < NV; ++a)
+#pragma unroll
+              for (int c = 0; c < NV; ++c) {
+                double sm = 0.0;
+#pragma unroll
+                for (int q = 0; q < NV; ++q) sm += Bjk[a * NV + q] * W[q * NV + c];
+                Bik[a * NV + c] -= sm;
+              }
+          }
+#pragma unroll
+          for (int q = 0; q < NV2; ++q) F[(size_t)k * NV2 + q] = W[q];
+        }
+      } else {
+        double B[kSmallMaxB][NV2], S[3][NV2], J[9][NV2];
+#pragma unroll
+        for (int b = 0; b < kSmallMaxB; ++b)
+          if (b < nbk)
+#pragma unroll
+            for (int q = 0; q < NV2; ++q) B[b][q] = A[(size_t)(k0 + b) * NV2 + q];
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          if (t < nlow)
+#pragma unroll
+            for (int q = 0; q < NV2; ++q) S[t][q] = invD[(size_t)rec[8 + t] * NV2 + q];
+#pragma unroll
+        for (int u = 0; u < 9; ++u)
+          if (u < npair)
+#pragma unroll
+            for (int q = 0; q < NV2; ++q) J[u][q] = F[(size_t)rec[14 + 2 * u] * NV2 + q];
+        int pc = 0;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          if (t < nlow) {
+            double W[NV2];
+#pragma unroll
+            for (int a = 0; a < NV; ++a)
+#pragma unroll
+              for (int c = 0; c < NV; ++c) {
+                double sm = 0.0;
+#pragma unroll
+                for (int q = 0; q < NV; ++q) sm += B[t][a * NV + q] * S[t][q * NV + c];
+                W[a * NV + c] = sm;
+              }
+            const int nu = rec[11 + t];
+#pragma unroll
+            for (int u = 0; u < 9; ++u) {
+              if (u >= pc && u < pc + nu) {
+                const int pos = rec[14 + 2 * u + 1] - k0;
+                double prod[NV2];
+#pragma unroll
+                for (int a = 0; a < NV; ++a)
+#pragma unroll
+                  for (int c = 0; c < NV; ++c) {
+                    double sm = 0.0;
+#pragma unroll
+                    for (int q = 0; q < NV; ++q) sm += J[u][a * NV + q] * W[q * NV + c];
+                    prod[a * NV + c] = sm;
+                  }
+#pragma unroll
+                for (int b = 0; b < kSmallMaxB; ++b)
+                  if (b == pos)
+#pragma unroll
+                    for (int q = 0; q < NV2; ++q) B[b][q] -= prod[q];
+              }
+            }
+            pc += nu;
+#pragma unroll
+            for (int q = 0; q < NV2; ++q) B[t][q] = W[q];
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < kSmallMaxB; ++b)
+          if (b < nbk)
+#pragma unroll
+            for (int q = 0; q < NV2; ++q) F[(size_t)(k0 + b) * NV2 + q] = B[b][q];
+      }
+      // inv(D_i) (Gauss elimination per unit column, factor once)
+      double L[NV2];
+#pragma unroll
+      for (int q = 0; q < NV2; ++q) L[q] = F[(size_t)kd * NV2 + q];
+      {
+        const double w = L[2] / L[0];
+        L[3] -= w * L[1];
+        L[2] = w;
+      }
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        double rhs[NV] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0};
+        lu_solve<NV>(L, rhs);
+        invD[(size_t)i * NV2 + c] = rhs[0];
+        invD[(size_t)i * NV2 + NV + c] = rhs[1];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Small-block ILU(0) with the whole partition resident in LDS (the SST system's 2x2 blocks: a 390-row
+// partition is ~2 000 blocks = 64 KB). The workgroup loads the partition rows' A blocks once, every
+// dependency level then reads finished rows' blocks and inverses from LDS (no global round trip between
+// levels), and the factor and inv(D) are stored once at the end. One thread per row of a level; the row
+// plan of the thread's next-level row is prefetched during the current level. Arithmetic as
+// k_ilu_build_small (general per-block update plan, reference order).
+template <int NV>
+__global__ __launch_bounds__(256) void k_ilu_build_lds(const int32_t* __restrict__ part_ptr,
+                                                       const int32_t* __restrict__ part_lvl,
+                                                       const int32_t* __restrict__ lvl_ptr,
+                                                       const int4* __restrict__ slot, const int32_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ col,
+                                                       const int32_t* __restrict__ upd_ptr,
+                                                       const int2* __restrict__ upd, const double* __restrict__ A,
+                                                       double* __restrict__ F, double* __restrict__ invD) {
+  constexpr int NV2 = NV * NV;
+  extern __shared__ double lds[];
+  const int p = blockIdx.x;
+  const int lo = part_ptr[p], hi = part_ptr[p + 1];
+  const int kb = rp[lo], ke = rp[hi];
+  double* Fl = lds;                                // [ke - kb][NV2]
+  double* Il = lds + (size_t)(ke - kb) * NV2;      // [hi - lo][NV2]
+  for (int q = threadIdx.x; q < (ke - kb) * NV2; q += blockDim.x) Fl[q] = A[(size_t)kb * NV2 + q];
+  __syncthreads();
+  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  int4 nxt = make_int4(-1, 0, 0, 0);
+  if (l0 < l1 && lvl_ptr[l0] + (int)threadIdx.x < lvl_ptr[l0 + 1]) nxt = slot[lvl_ptr[l0] + threadIdx.x];
+  for (int l = l0; l < l1; ++l) {
+    const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
+    int4 cur = nxt;
+    nxt = make_int4(-1, 0, 0, 0);
+    if (l + 1 < l1 && lvl_ptr[l + 1] + (int)threadIdx.x < lvl_ptr[l + 2]) nxt = slot[lvl_ptr[l + 1] + threadIdx.x];
+    for (int r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+      const int4 sl = (r == r0 + (int)threadIdx.x) ? cur : slot[r];
+      const int i = sl.x, k0 = sl.y, kd = sl.z;
+      for (int k = k0; k < kd; ++k) {
+        const int j = col[k];
+        const double* Sinv = Il + (size_t)(j - lo) * NV2;
+        double* Bij = Fl + (size_t)(k - kb) * NV2;
+        double W[NV2];
+#pragma unroll
+        for (int a = 0; a < NV; ++a)
+#pragma unroll
+          for (int c = 0; c < NV; ++c) {
+            double sm = 0.0;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) sm += Bij[a * NV + q] * Sinv[q * NV + c];
+            W[a * NV + c] = sm;
+          }
+        for (int u = upd_ptr[k]; u < upd_ptr[k + 1]; ++u) {
+          const int2 h = upd[u];
+          const double* Bjk = Fl + (size_t)(h.x - kb) * NV2;
+          double* Bik = Fl + (size_t)(h.y - kb) * NV2;
+#pragma unroll
+          for (int a = 0; a < NV; ++a)
+#pragma unroll
+            for (int c = 0; c < NV; ++c) {
+              double sm = 0.0;
+#pragma unroll
+              for (int q = 0; q < NV; ++q) sm += Bjk[a * NV + q] * W[q * NV + c];
+              Bik[a * NV + c] -= sm;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NV2; ++q) Bij[q] = W[q];
+      }
+      double L[NV2];
+#pragma unroll
+      for (int q = 0; q < NV2; ++q) L[q] = Fl[(size_t)(kd - kb) * NV2 + q];
+#pragma unroll
+      for (int ii = 1; ii < NV; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < ii; ++jj) {
+          const double w = L[ii * NV + jj] / L[jj * NV + jj];
+#pragma unroll
+          for (int kk = jj + 1; kk < NV; ++kk) L[ii * NV + kk] -= w * L[jj * NV + kk];
+          L[ii * NV + jj] = w;
+        }
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        double rhs[NV];
+#pragma unroll
+        for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == c) ? 1.0 : 0.0;
+        lu_solve<NV>(L, rhs);
+#pragma unroll
+        for (int rr = 0; rr < NV; ++rr) Il[(size_t)(i - lo) * NV2 + rr * NV + c] = rhs[rr];
+      }
+    }
+    __syncthreads();
+  }
+  for (int q = threadIdx.x; q < (ke - kb) * NV2; q += blockDim.x) F[(size_t)kb * NV2 + q] = Fl[q];
+  for (int q = threadIdx.x; q < (hi - lo) * NV2; q += blockDim.x) invD[(size_t)lo * NV2 + q] = Il[q];
+}
+
 // ILU(0) forward substitution x = b - L x per partition; one thread per (row, component).
 template <int NV>
 __global__ __launch_bounds__(256) void k_ilu_fwd_part(const int32_t* __restrict__ part_lvl,
@@ -907,12 +1152,32 @@ int rx_la_prepare(rx_ctx* ctx) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_part<NV_>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    if (NV_ <= 4)
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_lds<NV_>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
   });
   return RX_OK;
 }
 
 int rx_la_ilu_build(rx_ctx* ctx) {
   const int nv = ctx->nVar;
+  const size_t shm_small = sizeof(double) * (size_t)nv * nv * (ctx->maxpart_nnzb + ctx->maxpart);
+  if (nv <= 4 && !ctx->ilu_trace && shm_small <= (size_t)ctx->lds_max) {
+    RX_NV_SWITCH(nv, (k_ilu_build_lds<NV_><<<ctx->npart, 256, shm_small, ctx->stream>>>(
+                         ctx->part_ptr, ctx->fs.part_lvl, ctx->fs.lvl_ptr, reinterpret_cast<const int4*>(ctx->fs.slot),
+                         ctx->rp, ctx->col, ctx->upd_ptr, reinterpret_cast<const int2*>(ctx->upd), ctx->f[RX_F_JAC],
+                         ctx->f[RX_F_ILU], rx_invd_buf(ctx))));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
+  if (nv == 2 && !ctx->ilu_trace) {
+    k_ilu_build_2<<<ctx->npart, 256, 0, ctx->stream>>>(ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_plan,
+                                                       reinterpret_cast<const int4*>(ctx->fs.slot), ctx->rp, ctx->col,
+                                                       ctx->upd_ptr, reinterpret_cast<const int2*>(ctx->upd),
+                                                       ctx->f[RX_F_JAC], ctx->f[RX_F_ILU], rx_invd_buf(ctx));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
   if (nv <= 4 && !ctx->ilu_trace) {
     RX_NV_SWITCH(nv, (k_ilu_build_small<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                          ctx->fs.part_lvl, ctx->fs.lvl_ptr, reinterpret_cast<const int4*>(ctx->fs.slot), ctx->rp,
