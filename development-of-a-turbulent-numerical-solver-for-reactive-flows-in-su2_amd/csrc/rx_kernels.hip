@@ -475,27 +475,41 @@ __global__ __launch_bounds__(kBlock) void k_muscl_edge(int E, const int32_t* __r
   }
 }
 
-// a1 implicit: flux + both Jacobians into per-edge scratch. A team of 16 lanes per edge (4 edges
-// per wavefront): every lane evaluates the edge scalars, lane v < nVar owns residual component v and
-// Jacobian column b = v, so for every row a the team stores one contiguous row segment of Ji and Jj.
-constexpr int kAusmTeam = 16;
+// a1 implicit: flux + both Jacobians into per-edge scratch. An edge is shared by a team of 4 lanes
+// (16 edges per wavefront): every lane evaluates the edge scalars (~15 divisions / square roots) once
+// and owns the residual components and Jacobian columns b = t, t + 4, t + 8 (t = lane in team), in the
+// reference's operation order per entry. The 16 edges of a wavefront own one contiguous scratch range
+// ([e][Ji|Jj], edge-major), so Ji and then Jj of the 16 edges are staged in LDS and stored as whole
+// 512-byte rows (full cache lines).
+constexpr int kAusmTeam = 4;
+constexpr int kAusmBlock = 128;
 template <int NS, int NDIM>
-__global__ __launch_bounds__(kBlock) void k_ausm_edge(int E, const int32_t* __restrict__ edges,
-                                                      const double* __restrict__ normal, const double* __restrict__ V,
-                                                      const double* __restrict__ dPdU, const double* __restrict__ VR,
-                                                      const double* __restrict__ SR, double mInfty,
-                                                      double* __restrict__ F, double* __restrict__ Jac, int* err) {
+__global__ __launch_bounds__(kAusmBlock) void k_ausm_edge(int E, const int32_t* __restrict__ edges,
+                                                          const double* __restrict__ normal,
+                                                          const double* __restrict__ V,
+                                                          const double* __restrict__ dPdU,
+                                                          const double* __restrict__ VR,
+                                                          const double* __restrict__ SR, double mInfty,
+                                                          double* __restrict__ F, double* __restrict__ Jac,
+                                                          int* err) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nVar2 = nVar * nVar;
-  static_assert(nVar <= kAusmTeam, "team too small");
+  constexpr int CPL = (nVar + kAusmTeam - 1) / kAusmTeam;
+  constexpr int EW = 64 / kAusmTeam;
+  __shared__ double stage[kAusmBlock / 64][EW * nVar2];
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-  const int e = gt / kAusmTeam, b = gt % kAusmTeam;
-  if (e >= E) return;
-  const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+  const int lane = threadIdx.x & 63, k = lane / kAusmTeam, t = lane % kAusmTeam;
+  const int e0 = (gt >> 6) * EW;  // first edge of this wavefront
+  if (e0 >= E) return;            // whole wavefronts exit together
+  const int e = e0 + k;
+  const bool live = e < E;
+  const int ee = live ? e : e0;
+  double* sj = stage[threadIdx.x >> 6];
+  const int n0 = edges[2 * ee], n1 = edges[2 * ee + 1];
   // node states (1st order) or the edge's reconstructed states and pressure derivatives (2nd order)
-  const double* Vsi = VR ? VR + 2 * (size_t)e * nPV : V + (size_t)n0 * nPV;
-  const double* Vsj = VR ? VR + (2 * (size_t)e + 1) * nPV : V + (size_t)n1 * nPV;
-  const double* Ssi = VR ? SR + 2 * (size_t)e * nVar : dPdU + (size_t)n0 * nVar;
-  const double* Ssj = VR ? SR + (2 * (size_t)e + 1) * nVar : dPdU + (size_t)n1 * nVar;
+  const double* Vsi = VR ? VR + 2 * (size_t)ee * nPV : V + (size_t)n0 * nPV;
+  const double* Vsj = VR ? VR + (2 * (size_t)ee + 1) * nPV : V + (size_t)n1 * nPV;
+  const double* Ssi = VR ? SR + 2 * (size_t)ee * nVar : dPdU + (size_t)n0 * nVar;
+  const double* Ssj = VR ? SR + (2 * (size_t)ee + 1) * nVar : dPdU + (size_t)n1 * nVar;
   double Vi[nPV], Vj[nPV];
 #pragma unroll
   for (int v = 0; v < nPV; ++v) {
@@ -504,36 +518,60 @@ __global__ __launch_bounds__(kBlock) void k_ausm_edge(int E, const int32_t* __re
   }
   double nrm[NDIM];
 #pragma unroll
-  for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
+  for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)ee * NDIM + d];
   AusmEdge s;
   ausm_scalars<NDIM>(Vi, Vj, nrm, mInfty, s);
-  if (b >= nVar) return;
   bool bad = false;
-  {
-    // ausm_res for the runtime component b, with phi read by index (no dynamic register indexing)
-    const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
-    const double pi = b == 0 ? 1.0 : Vsi[pidx];
-    const double pj = b == 0 ? 1.0 : Vsj[pidx];
-    double r = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
-    if (b >= 1 && b <= NDIM) r += s.pLF * pick<NDIM>(s.UN, b - 1) * s.Area;
-    bad |= isnan(r);
-    F[(size_t)e * nVar + b] = r;
-  }
-  // dP/dU of both nodes: only column b is needed by this lane's Jacobian column
-  const double sib = Ssi[b], sjb = Ssj[b];
-  const AusmCol c = ausm_col_b<NDIM>(s, sib, sjb, b);
-  double* Ji = Jac + (size_t)e * 2 * nVar2;
-  double* Jj = Ji + nVar2;
+  double jjr[CPL][nVar];
 #pragma unroll
-  for (int a = 0; a < nVar; ++a) {
-    double ji, jj;
-    ausm_jac_entry<NDIM>(s, c, ausm_phi<NDIM>(Vi, Vi[NDIM + 3], a), ausm_phi<NDIM>(Vj, Vj[NDIM + 3], a), sib, sjb,
-                         a, b, &ji, &jj);
-    bad |= isnan(ji) || isnan(jj);
-    Ji[a * nVar + b] = ji;
-    Jj[a * nVar + b] = jj;
+  for (int c = 0; c < CPL; ++c) {
+    const int b = t + kAusmTeam * c;
+    if (b < nVar) {
+      // ausm_res for the runtime component b, with phi read by index (no dynamic register indexing)
+      const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
+      const double pi = b == 0 ? 1.0 : Vsi[pidx];
+      const double pj = b == 0 ? 1.0 : Vsj[pidx];
+      double r = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
+      if (b >= 1 && b <= NDIM) r += s.pLF * pick<NDIM>(s.UN, b - 1) * s.Area;
+      bad |= isnan(r);
+      if (live) F[(size_t)e * nVar + b] = r;
+      // dP/dU of both nodes: only column b is needed by this lane's Jacobian column
+      const double sib = Ssi[b], sjb = Ssj[b];
+      const AusmCol col = ausm_col_b<NDIM>(s, sib, sjb, b);
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) {
+        double ji, jj;
+        ausm_jac_entry<NDIM>(s, col, ausm_phi<NDIM>(Vi, Vi[NDIM + 3], a), ausm_phi<NDIM>(Vj, Vj[NDIM + 3], a), sib,
+                             sjb, a, b, &ji, &jj);
+        bad |= isnan(ji) || isnan(jj);
+        sj[k * nVar2 + a * nVar + b] = ji;
+        jjr[c][a] = jj;
+      }
+    }
   }
-  if (bad) set_err(err, ERR_NAN, e);
+  const int ne = min(EW, E - e0);
+  double* Jo = Jac + (size_t)e0 * 2 * nVar2;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    if (side) {
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int b = t + kAusmTeam * c;
+        if (b < nVar)
+#pragma unroll
+          for (int a = 0; a < nVar; ++a) sj[k * nVar2 + a * nVar + b] = jjr[c][a];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    for (int q = lane; q < ne * nVar2; q += 64) {
+      const int kk = q / nVar2, r = q - kk * nVar2;
+      Jo[(size_t)kk * 2 * nVar2 + side * nVar2 + r] = sj[q];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (live && bad) set_err(err, ERR_NAN, e);
 }
 
 // a3-a6: viscous flux (+ Jacobians) per edge into scratch.
@@ -1049,7 +1087,7 @@ int rx_launch_ausm_node(rx_ctx* ctx) {
 
 int rx_launch_ausm_edge(rx_ctx* ctx) {
   if (ctx->nDim != 2) return RX_ERR_ARG;
-  RX_NS_SWITCH(ctx->ns, (k_ausm_edge<NS_, 2><<<blocks(ctx->E * kAusmTeam), kBlock, 0, ctx->stream>>>(
+  RX_NS_SWITCH(ctx->ns, (k_ausm_edge<NS_, 2><<<blocks(ctx->E * kAusmTeam, kAusmBlock), kAusmBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
                             ctx->cfg.spatial_order ? ctx->recon : nullptr,
                             ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr,
