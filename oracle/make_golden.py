@@ -135,9 +135,9 @@ def write_state(wd, U):
             f.write(str(g) + " " + " ".join(f"{v:.17g}" for v in row) + "\n")
 
 
-def run_harness(wd, bsr):
+def run_harness(wd, bsr, extra=None):
     exe = os.path.join(HERE, "_ref", "harness")
-    cmd = [exe, "case.cfg", "state.txt", "out"] + (["--bsr"] if bsr else [])
+    cmd = [exe, "case.cfg", "state.txt", "out"] + (["--bsr"] if bsr else []) + list(extra or [])
     r = subprocess.run(cmd, cwd=wd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout[-4000:] + r.stderr[-4000:])
@@ -198,6 +198,54 @@ def case_mini9(nx=21, ny=11):
     a.update(mech_arrays())
     a["gen_points"] = pts
     a["gen_quads"] = quads
+    return a
+
+
+def mini9_inputs(nx=21, ny=11):
+    pts, quads, bnd = meshgen.jet_mesh(nx, ny)
+    xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    from scipy.spatial import cKDTree
+    scale = np.array([1.0 / 0.125, 1.0 / 0.006])
+    _, idx = cKDTree(xy * scale).query(pts * scale)
+
+    def writer(wd):
+        meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, quads, bnd)
+        return "mesh.su2"
+
+    return pts, quads, cons[idx], writer
+
+
+GEOM_KEYS = ("coord", "volume", "global_index", "nbr_ptr", "nbr", "edges", "edge_normal", "bvertex", "bvertex_normal",
+             "wall_distance")
+
+
+def case_bc9():
+    """next-3 / a8: the reference's Space_Integration with its boundary conditions (inlets TEMPERATURE_IMPOSE,
+    outlet, isothermal walls; SST inlet / outlet / wall) on the mini9 jet, flow + SST, ILU0 cfg."""
+    pts, quads, U, writer = mini9_inputs()
+    wd = make_workdir("bc9", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--bc"])
+    # keep the BSR rows of the boundary points only (the interior rows are the plain assembly)
+    rp = a["bsr_row_ptr"]
+    rows = np.unique(a["bvertex"][:, 1])
+    blk = np.concatenate([np.arange(rp[i], rp[i + 1]) for i in rows])
+    a["bc_rows"] = rows
+    a["bc_blk"] = blk
+    for k in ("bc_pre_bsr", "bc_bsr", "sst_bc_pre_bsr", "sst_bc_bsr"):
+        a[k] = a[k][blk]
+    a.update(mech_arrays())
+    return a
+
+
+def case_it9():
+    """Whole reference outer iterations (CMeanFlowIteration::Iterate: flow MultiGrid_Iteration + SST
+    SingleGrid_Iteration, boundary conditions included) from the mini9 state: 3 iterations, ILU0."""
+    pts, quads, U, writer = mini9_inputs()
+    wd = make_workdir("it9", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--iters", "3"])
+    a.update(mech_arrays())
     return a
 
 
@@ -284,7 +332,7 @@ def main():
     gold = os.path.join(REPO, "tests", "golden")
     os.makedirs(gold, exist_ok=True)
     for case in args.cases.split(","):
-        a = {"mini9": case_mini9, "jet9w": case_jet9w}[case]()
+        a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

@@ -480,3 +480,145 @@ def sst_step(nDim, mesh, flow, T, TG, F1, F2, CDkw, dt, cfg, pattern=None, part_
     F1n, F2n, CDn, mut = sst_blending(nDim, Tn, TG1, rho, flow["mu"], mesh["wall_distance"], flow["strain"])
     return Tn, dict(grad_pre=TG0, res=R, jac=A, rhs=rhs, sol=x, lin_iters=it, lin_resid=res, rms=rms, grad=TG1,
                     F1=F1n, F2=F2n, CDkw=CDn, mut=mut)
+
+
+def bc_prm(bc_params, mach_inf, prandtl_turb, lewis_turb):
+    """Oracle BC parameter vector: the harness's bc_params[:18] (inlet kind, Tke_Inf, kine_Inf, omega_Inf, beta_1,
+    reference values, the reference's marker / inlet enum values) + (Mach_inf, Pr_t, Le_t)."""
+    p = np.zeros(21)
+    p[:18] = np.asarray(bc_params, dtype=np.float64)[:18]
+    p[18:] = (mach_inf, prandtl_turb, lewis_turb)
+    return p
+
+
+@_keepalive
+def bc_flow(mech, nDim, mesh, bc_marker, prm, st, rp, col, R, A, Uold, implicit, rans):
+    """Weak + strong flow BCs of one Space_Integration (next-3 + a8). R [N][nVar], A (BSR blocks or None) and
+    Uold are updated in place; returns the ghost states (CharacPrimVar) [NB][nPV]."""
+    ns = mech.ns
+    nPV = ns + nDim + 5
+    bv = np.ascontiguousarray(mesh["bvertex"], dtype=np.int64)
+    NB = len(bv)
+    charac = np.zeros((NB, nPV))
+    for a in (R, Uold) + ((A,) if A is not None else ()):
+        assert a.flags.c_contiguous and a.dtype == np.float64
+    rc = lib().orc_bc_flow(
+        mech.h, C.c_int(nDim), C.c_int64(NB), _p(bv, np.int64), _p(mesh["bvertex_normal"]),
+        _p(mesh["bvertex_pn"], np.int64), C.c_int(len(bc_marker)), _p(bc_marker), C.c_int(bc_marker.shape[1]), _p(prm),
+        C.c_int(int(implicit)), C.c_int(int(rans)), _p(mesh["coord"]), _p(st["U"]), _p(st["V"]), _p(st["dPdU"]),
+        _p(st["dTdU"]), _p(st["grad_prim"]), _p(st["mu"]), _p(st["kappa"]), _p(st["Dij"]), _p(st["turb_k"]),
+        _p(st["mu_t"]), _p(st["sigma_k"]), _p(st["grad_k"]), _p(st["eddy_visc_flow"]), _p(rp, np.int64),
+        _p(col, np.int64), _f(R), _f(A) if A is not None else None, _f(Uold), _f(charac))
+    if rc:
+        raise RuntimeError("reference exception in a flow boundary condition")
+    return charac
+
+
+@_keepalive
+def bc_sst(nDim, mesh, bc_marker, prm, V, mu, eddy, charac, TG, F1, rp, col, T, R, A, implicit):
+    """SST inlet / outlet / isothermal-wall BCs; T [N][2], R [N][2], A (2x2 BSR or None) updated in place."""
+    bv = np.ascontiguousarray(mesh["bvertex"], dtype=np.int64)
+    for a in (T, R) + ((A,) if A is not None else ()):
+        assert a.flags.c_contiguous and a.dtype == np.float64
+    lib().orc_bc_sst(C.c_int(nDim), C.c_int(V.shape[1]), C.c_int64(len(bv)), _p(bv, np.int64),
+                     _p(mesh["bvertex_normal"]), _p(mesh["bvertex_pn"], np.int64), C.c_int(len(bc_marker)),
+                     _p(bc_marker), C.c_int(bc_marker.shape[1]), _p(prm), C.c_int(int(implicit)), _p(mesh["coord"]),
+                     _p(V), _p(mu), _p(eddy), _p(charac), _p(TG), _p(F1), _p(rp, np.int64), _p(col, np.int64), _f(T),
+                     _f(R), _f(A) if A is not None else None)
+
+
+def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=None):
+    """One reference outer iteration for REACTIVE_RANS, restated on the CPU in the reference's order
+    (CMeanFlowIteration::Iterate iteration_structure.cpp:486-560 -> CMultiGridIntegration::MultiGrid_Iteration
+    integration_time.cpp:40-140 with MGLEVEL = 0, then CSingleGridIntegration::SingleGrid_Iteration :770-810):
+      flow  Preprocessing (SetPrimitive_Variables, LSQ gradient, StrainMag), Set_OldSolution, SetTime_Step,
+            Space_Integration (upwind, viscous, source, weak then strong BCs), ImplicitEuler_Iteration (ILU0 FGMRES),
+            Preprocessing(Output = true) on the updated solution;
+      SST   Preprocessing (gradient), Space_Integration (loops + BCs), ImplicitEuler_Iteration, Postprocessing.
+    s: state dict (U, V, Uold, T = (k, omega), TG, F1, F2, CDkw, mut) — returned updated with the iteration's
+    RMS (rms, sst_rms) and linear-solver counts. bc: dict(marker, prm) of the golden's bc_marker / oracle bc_prm."""
+    ns = mech.ns
+    nb = ns + nDim + 2
+    N = len(s["U"])
+    rp, col = pattern
+    vol = mesh["volume"]
+    sig = np.full(N, 0.85)  # CTurbSSTVariable::Get_Sigmak = constants[0]
+
+    def preprocess(U, V, Uold, T, mut):
+        prm = list(cfg["p2v"])
+        prm[10] = float(ext_iter)
+        o = set_primitive(mech, nDim, U, V, T[:, 0].copy(), mut, prm, Uold=Uold)
+        if o["nonphys"] < 0:
+            raise RuntimeError("SetPrimitive_Variables: bisection failed")
+        G = grad_lsq(mech, nDim, np.arange(N), mesh["coord"], o["V"], mesh["nbr_ptr"], mesh["nbr"])
+        return o, G, strain_mag(nDim, G)
+
+    T, TG, mut = s["T"], s["TG"], s["mut"]
+    o, G, strain = preprocess(s["U"], s["V"], s["Uold"], T, mut)
+    U = o["U"]
+    Uold = U.copy()  # Set_OldSolution (integration_time.cpp:162)
+    dt, _, _ = time_step(nDim, ns, mesh["edges"], mesh["edge_normal"], mesh["bvertex"], mesh["bvertex_normal"], o["V"],
+                         o["dPdU"], o["mu"], o["eddy"], vol, mesh["nbr_ptr"],
+                         [cfg["cfl"], cfg["max_delta_time"], cfg["prandtl_lam"], cfg["prandtl_turb"]])
+    gk = np.ascontiguousarray(TG[:, 0, :])
+    rc, Jci, Jcj = ausm_edges(nDim, ns, mesh["edges"], mesh["edge_normal"], o["V"], o["dPdU"], cfg["mach_inf"], True)
+    rv, Jvi, Jvj = visc_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], o["V"], G, o["mu"],
+                              o["kappa"], o["Dij"], o["dTdU"], T[:, 0].copy(), mut, sig, gk, True, True,
+                              [1, 1, 1, cfg["prandtl_turb"], cfg["lewis_turb"]])
+    rs, Js = source_cells(mech, nDim, o["V"], o["dTdU"], vol, T[:, 1].copy(), True, True,
+                          [cfg["c_mu"], cfg["pasr_lb"], 1, 1, 1])
+    R, A, _ = assemble(rp, col, mesh["edges"], rc, Jci, Jcj, rv, Jvi, Jvj, rs, Js, vol, np.full(N, np.inf), nb)
+    R = np.ascontiguousarray(R)
+    A = np.ascontiguousarray(A)
+    st = dict(U=U, V=o["V"], dPdU=o["dPdU"], dTdU=o["dTdU"], grad_prim=G, mu=o["mu"], kappa=o["kappa"], Dij=o["Dij"],
+              turb_k=T[:, 0].copy(), mu_t=mut, sigma_k=sig, grad_k=gk, eddy_visc_flow=o["eddy"])
+    charac = bc_flow(mech, nDim, mesh, bc["marker"], bc["prm"], st, rp, col, R, A, Uold, True, True)
+    diag = np.array([rp[i] + np.searchsorted(col[rp[i]:rp[i + 1]], i) for i in range(N)])
+    ok = dt > 1e-16
+    D = A[diag]
+    idx = np.arange(nb)
+    for i in np.nonzero(ok)[0]:
+        D[i][idx, idx] += vol[i] / dt[i]
+    for i in np.nonzero(~ok)[0]:
+        D[i] = np.eye(nb)
+        R[i] = 0.0
+    A[diag] = D
+    rhs = -(R + 0.0)
+    F = ilu_build(rp, col, A, part_ptr)
+    x, it, _ = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"], part_ptr=part_ptr)
+    Un = update(Uold, x, nDim, 0, cfg["relaxation"], vol, dt)
+    rms = np.maximum(1e-32, np.sqrt(np.sum(rhs * rhs, axis=0) / N))
+    # MultiGrid_Iteration's Preprocessing(Output = true) on the updated solution (integration_time.cpp:127-129)
+    o2, G2, strain2 = preprocess(Un, o["V"], Uold, T, mut)
+    Un = o2["U"]
+    V2 = o2["V"]
+    rho = np.ascontiguousarray(V2[:, nDim + 2])
+    # SST SingleGrid_Iteration
+    TG0 = sol_grad_ls(nDim, mesh["coord"], T, mesh["nbr_ptr"], mesh["nbr"])
+    ru, Jui, Juj = sst_upwind(nDim, mesh["edges"], mesh["edge_normal"], V2, T)
+    rv2, Jvi2, Jvj2 = sst_visc(nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], V2, T, TG0, s["F1"], o2["mu"],
+                               o2["eddy"])
+    rs2, Js2 = sst_source(nDim, V2, G2, T, vol, mesh["wall_distance"], s["F1"], s["F2"], s["CDkw"], strain2, o2["eddy"])
+    R2, A2, _ = sst_assemble(rp, col, mesh["edges"], ru, Jui, Juj, rv2, Jvi2, Jvj2, rs2, Js2, vol, np.full(N, np.inf),
+                             cfg.get("cfl_red_turb", 1.0))
+    R2 = np.ascontiguousarray(R2)
+    A2 = np.ascontiguousarray(A2)
+    T = np.ascontiguousarray(T).copy()
+    bc_sst(nDim, mesh, bc["marker"], bc["prm"], V2, o2["mu"], o2["eddy"], charac, TG0, s["F1"], rp, col, T, R2, A2,
+           True)
+    D2 = A2[diag]
+    for i in range(N):
+        delta = vol[i] / (cfg.get("cfl_red_turb", 1.0) * dt[i])
+        D2[i][0, 0] += delta
+        D2[i][1, 1] += delta
+    A2[diag] = D2
+    rhs2 = -R2
+    F2 = ilu_build(rp, col, A2, part_ptr)
+    x2, it2, _ = fgmres(rp, col, A2, rhs2.ravel(), "ilu", F=F2, tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                        part_ptr=part_ptr)
+    Tn = sst_update(T, x2.ravel(), cfg.get("relaxation_turb", 1.0), rho, np.ascontiguousarray(Uold[:, 0]))
+    sst_rms = np.maximum(1e-32, np.sqrt(np.sum(rhs2 * rhs2, axis=0) / N))
+    TG1 = sol_grad_ls(nDim, mesh["coord"], Tn, mesh["nbr_ptr"], mesh["nbr"])
+    F1n, F2n, CDn, mutn = sst_blending(nDim, Tn, TG1, rho, o2["mu"], mesh["wall_distance"], strain2)
+    return dict(U=Un, V=V2, Uold=Uold, T=Tn, TG=TG1, F1=F1n, F2=F2n, CDkw=CDn, mut=mutn, rms=rms, sst_rms=sst_rms,
+                lin_iters=it, sst_lin_iters=it2, dt=dt)

@@ -54,6 +54,14 @@ class HarnessDriver : public CFluidDriver {
   CSolver** sol() { return solver_container[ZONE_0][MESH_0]; }
   CNumerics* num(unsigned short s, unsigned short t) { return numerics_container[ZONE_0][MESH_0][s][t]; }
   CConfig* cfg() { return config_container[ZONE_0]; }
+  CIntegration* integ(unsigned short s) { return integration_container[ZONE_0][s]; }
+  CNumerics** nums(unsigned short s) { return numerics_container[ZONE_0][MESH_0][s]; }
+  // one outer iteration of the reference (CMeanFlowIteration::Iterate, iteration_structure.cpp:486-560)
+  void iterate() {
+    iteration_container[ZONE_0]->Iterate(output, integration_container, geometry_container, solver_container,
+                                         numerics_container, config_container, surface_movement, grid_movement,
+                                         FFDBox, ZONE_0);
+  }
 };
 
 // sigma_k is a protected CNumerics member; Set_Sigmak has no return statement (UB,
@@ -68,6 +76,21 @@ double** alloc2(int n) {
   return a;
 }
 
+// CTurbSSTSolver's kine_Inf / omega_Inf are private: recomputed with the constructor's own expressions
+// (solver_direct_turbulent.cpp:2740-2752).
+void sst_inf(CConfig* config, unsigned short nDim, double& kine, double& omega) {
+  su2double rhoInf = config->GetDensity_FreeStreamND();
+  su2double* VelInf = config->GetVelocity_FreeStreamND();
+  su2double muLamInf = config->GetViscosity_FreeStreamND();
+  su2double Intensity = config->GetTurbulenceIntensity_FreeStream();
+  su2double viscRatio = config->GetTurb2LamViscRatio_FreeStream();
+  su2double VelMag = 0;
+  for (unsigned short iDim = 0; iDim < nDim; iDim++) VelMag += VelInf[iDim] * VelInf[iDim];
+  VelMag = sqrt(VelMag);
+  kine = 3.0 / 2.0 * (VelMag * VelMag * Intensity * Intensity);
+  omega = rhoInf * kine / (muLamInf * viscRatio);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -80,6 +103,9 @@ int main(int argc, char** argv) {
   std::string state_file = argv[2];
   g_out = argv[3];
   bool do_bsr = (argc > 4 && std::string(argv[4]) == "--bsr");
+  // --bc: boundary conditions of one Space_Integration (flow + SST); --iters K: K reference outer iterations
+  const bool do_bc = (argc > 4 && std::string(argv[4]) == "--bc");
+  const int n_iters = (argc > 5 && std::string(argv[4]) == "--iters") ? std::atoi(argv[5]) : 0;
   g_manifest.open(g_out + "/manifest.txt");
 
   SU2_Comm comm(0);
@@ -247,6 +273,217 @@ int main(int argc, char** argv) {
       for (unsigned long i = 0; i < nPoint; ++i) ev[i] = flow->node[i]->GetEddyViscosity();
       dumpd("eddy_visc_flow", ev, {(long)nPoint});
     }
+  }
+
+  // ---- boundary conditions (--bc) and whole reference iterations (--iters K)
+  if (do_bc || n_iters > 0) {
+    const unsigned short nMarker = geo->GetnMarker();
+    const unsigned short kind_solver = cfg->GetKind_Solver();
+    // per-vertex normal neighbour (CVertex::GetNormal_Neighbor), in bvertex order
+    std::vector<int64_t> pn;
+    for (unsigned short m = 0; m < nMarker; ++m)
+      for (unsigned long v = 0; v < geo->GetnVertex(m); ++v) pn.push_back(geo->vertex[m][v]->GetNormal_Neighbor());
+    dumpi("bvertex_pn", pn, {(long)pn.size()});
+    // marker data rows [kind, a, b, dir0, dir1, dir2, Y_1..Y_Ns]: inlet (Ttotal, Ptotal, flow dir, mass fractions),
+    // outlet (pressure), isothermal (wall temperature), heat flux (wall heat flux)
+    const int W = 6 + nSpecies;
+    std::vector<double> md((size_t)nMarker * W, 0.0);
+    for (unsigned short m = 0; m < nMarker; ++m) {
+      std::string tag = cfg->GetMarker_All_TagBound(m);
+      const unsigned short kind = cfg->GetMarker_All_KindBC(m);
+      double* r = md.data() + (size_t)m * W;
+      r[0] = kind;
+      if (kind == INLET_FLOW) {
+        r[1] = cfg->GetInlet_Ttotal(tag);
+        r[2] = cfg->GetInlet_Ptotal(tag);
+        su2double* fd = cfg->GetInlet_FlowDir(tag);
+        for (unsigned short d = 0; d < nDim; ++d) r[3 + d] = fd[d];
+        const su2double* ys = cfg->GetInlet_MassFrac(tag);
+        for (unsigned short s = 0; s < nSpecies; ++s) r[6 + s] = ys[s];
+      } else if (kind == OUTLET_FLOW) {
+        r[1] = cfg->GetOutlet_Pressure(tag);
+      } else if (kind == ISOTHERMAL) {
+        r[1] = cfg->GetIsothermal_Temperature(tag);
+      } else if (kind == HEAT_FLUX) {
+        r[1] = cfg->GetWall_HeatFlux(tag);
+      }
+    }
+    dumpd("bc_marker", md, {(long)nMarker, W});
+    double kine_inf = 0.0, omega_inf = 0.0;
+    if (rans) sst_inf(cfg, nDim, kine_inf, omega_inf);
+    std::vector<double> bp = {(double)cfg->GetKind_Inlet(), flow->GetTke_Inf(), kine_inf, omega_inf,
+                              rans ? turb->GetConstants()[4] : 0.0,
+                              cfg->GetPressure_Ref(), cfg->GetVelocity_Ref(), cfg->GetTemperature_Ref(),
+                              cfg->GetEnergy_Ref(), cfg->GetGas_Constant_Ref(), cfg->GetDensity_Ref(),
+                              (double)INLET_FLOW, (double)OUTLET_FLOW, (double)ISOTHERMAL, (double)HEAT_FLUX,
+                              (double)TOTAL_CONDITIONS, (double)MASS_FLOW, (double)TEMPERATURE_IMPOSE,
+                              cfg->GetCFL(MESH_0), cfg->GetLinear_Solver_Error(), (double)cfg->GetLinear_Solver_Iter(),
+                              (double)cfg->GetKind_Linear_Solver_Prec(), cfg->GetRelaxation_Factor_Flow(),
+                              cfg->GetRelaxation_Factor_Turb(), cfg->GetCFLRedCoeff_Turb(), cfg->GetMax_DeltaTime()};
+    dumpd("bc_params", bp, {(long)bp.size()});
+    // the cfg values the other modes dump with their operators, same layouts
+    dumpd("mach_inf", std::vector<double>{cfg->GetMach()}, {1});
+    dumpd("visc_params", std::vector<double>{cfg->GetPrandtl_Lam(), cfg->GetPrandtl_Turb(), cfg->GetLewis_Turb()}, {3});
+    dumpd("src_params", std::vector<double>{cfg->Get_Cmu(), cfg->Get_PaSR_LB(), cfg->GetDensity_Ref(), cfg->GetTime_Ref(),
+                                            cfg->GetTemperature_Ref()}, {5});
+    dumpd("dt_params", std::vector<double>{cfg->GetCFL(MESH_0), cfg->GetMax_DeltaTime(), cfg->GetPrandtl_Lam(),
+                                           cfg->GetPrandtl_Turb()}, {4});
+    dumpd("limiter_params", std::vector<double>{cfg->GetRefElemLength(), cfg->GetLimiterCoeff()}, {2});
+    dumpd("p2v_params", std::vector<double>{0.0, cfg->GetTemperatureMin(), cfg->GetTemperatureMax(),
+                                            cfg->GetTemperature_Ref(), cfg->GetEnergy_Ref(), cfg->GetGas_Constant_Ref(),
+                                            cfg->GetPressure_Ref(), cfg->GetViscosity_Ref(), cfg->GetConductivity_Ref(),
+                                            cfg->GetVelocity_Ref(), cfg->GetLength_Ref(), (double)cfg->GetExtIter()},
+          {12});
+    // sorted BSR pattern (neighbours + diagonal, matrix_structure.cpp:113-201)
+    std::vector<int64_t> brp(nPoint + 1, 0), bcol;
+    for (unsigned long i = 0; i < nPoint; ++i) {
+      std::vector<unsigned long> cols;
+      cols.push_back(i);
+      for (unsigned short k = 0; k < geo->node[i]->GetnPoint(); ++k) cols.push_back(geo->node[i]->GetPoint(k));
+      std::sort(cols.begin(), cols.end());
+      for (auto c : cols) bcol.push_back(c);
+      brp[i + 1] = bcol.size();
+    }
+    auto dump_mat = [&](CSysMatrix& A, int nb, const std::string& name) {
+      std::vector<double> blocks(bcol.size() * nb * nb);
+      for (unsigned long i = 0; i < nPoint; ++i)
+        for (int64_t k = brp[i]; k < brp[i + 1]; ++k) {
+          su2double* b = A.GetBlock(i, bcol[k]);
+          for (int q = 0; q < nb * nb; ++q) blocks[k * nb * nb + q] = b[q];
+        }
+      dumpd(name, blocks, {(long)bcol.size(), nb, nb});
+    };
+    auto dump_vec = [&](CSysVector& R, int nb, const std::string& name) {
+      std::vector<double> r(nPoint * nb);
+      for (unsigned long i = 0; i < nPoint * nb; ++i) r[i] = R[i];
+      dumpd(name, r, {(long)nPoint, nb});
+    };
+    auto dump_sol = [&](CSolver* s, int nb, bool old, const std::string& name) {
+      std::vector<double> u(nPoint * nb);
+      for (unsigned long i = 0; i < nPoint; ++i)
+        for (int v = 0; v < nb; ++v) u[i * nb + v] = old ? s->node[i]->GetSolution_Old(v) : s->node[i]->GetSolution(v);
+      dumpd(name, u, {(long)nPoint, nb});
+    };
+    dumpi("bsr_row_ptr", brp, {(long)nPoint + 1});
+    dumpi("bsr_col", bcol, {(long)bcol.size()});
+
+    if (do_bc) {
+      if (rans) {  // SST node records after the reference's preprocessing
+        std::vector<double> tg(nPoint * 2 * nDim), f1(nPoint), f2(nPoint), cd(nPoint), ts(nPoint * 2);
+        for (unsigned long i = 0; i < nPoint; ++i) {
+          for (unsigned short v = 0; v < 2; ++v)
+            for (unsigned short d = 0; d < nDim; ++d) tg[(i * 2 + v) * nDim + d] = turb->node[i]->GetGradient()[v][d];
+          f1[i] = turb->node[i]->GetF1blending();
+          f2[i] = turb->node[i]->GetF2blending();
+          cd[i] = turb->node[i]->GetCrossDiff();
+          ts[2 * i] = turb->node[i]->GetSolution(0);
+          ts[2 * i + 1] = turb->node[i]->GetSolution(1);
+        }
+        dumpd("sst_sol", ts, {(long)nPoint, 2});
+        dumpd("sst_grad", tg, {(long)nPoint, 2, nDim});
+        dumpd("sst_F1", f1, {(long)nPoint});
+        dumpd("sst_F2", f2, {(long)nPoint});
+        dumpd("sst_CDkw", cd, {(long)nPoint});
+      }
+      // flow: the interior loops alone, then the reference's whole Space_Integration (loops + weak and strong
+      // BCs, integration_structure.cpp:72-193) from zero, after Set_OldSolution as in MultiGrid_Cycle (:162)
+      CNumerics** fn = drv.nums(FLOW_SOL);
+      cfg->SetGlobalParam(kind_solver, RUNTIME_REACTIVE_SYS, 0);
+      flow->Set_OldSolution(geo);
+      flow->LinSysRes.SetValZero();
+      if (implicit) flow->Jacobian.SetValZero();
+      flow->Upwind_Residual(geo, sc, fn[CONV_TERM], cfg, MESH_0);
+      flow->Viscous_Residual(geo, sc, fn[VISC_TERM], cfg, MESH_0, NO_RK_ITER);
+      flow->Source_Residual(geo, sc, fn[SOURCE_FIRST_TERM], fn[SOURCE_SECOND_TERM], cfg, MESH_0);
+      dump_vec(flow->LinSysRes, nVar, "bc_pre_res");
+      if (implicit) dump_mat(flow->Jacobian, nVar, "bc_pre_bsr");
+      flow->LinSysRes.SetValZero();
+      if (implicit) flow->Jacobian.SetValZero();
+      drv.integ(FLOW_SOL)->Space_Integration(geo, sc, fn, cfg, MESH_0, NO_RK_ITER, RUNTIME_REACTIVE_SYS);
+      dump_vec(flow->LinSysRes, nVar, "bc_res");
+      if (implicit) dump_mat(flow->Jacobian, nVar, "bc_bsr");
+      dump_sol(flow, nVar, true, "bc_sol_old");
+      std::vector<double> ch;
+      for (unsigned short m = 0; m < nMarker; ++m)
+        for (unsigned long v = 0; v < geo->GetnVertex(m); ++v) {
+          su2double* c = flow->GetCharacPrimVar(m, v);
+          ch.insert(ch.end(), c, c + nPrimVar);
+        }
+      dumpd("bc_charac", ch, {(long)ch.size() / nPrimVar, nPrimVar});
+      if (rans) {
+        // SST: CTurbSSTSolver::Preprocessing (zero + gradient), Set_OldSolution, loops, then Space_Integration
+        CNumerics** tn = drv.nums(TURB_SOL);
+        cfg->SetGlobalParam(kind_solver, RUNTIME_TURB_SYS, 0);
+        turb->Preprocessing(geo, sc, cfg, MESH_0, 0, RUNTIME_TURB_SYS, false);
+        turb->Set_OldSolution(geo);
+        turb->LinSysRes.SetValZero();
+        if (implicit) turb->Jacobian.SetValZero();
+        turb->Upwind_Residual(geo, sc, tn[CONV_TERM], cfg, MESH_0);
+        turb->Viscous_Residual(geo, sc, tn[VISC_TERM], cfg, MESH_0, NO_RK_ITER);
+        turb->Source_Residual(geo, sc, tn[SOURCE_FIRST_TERM], tn[SOURCE_SECOND_TERM], cfg, MESH_0);
+        dump_vec(turb->LinSysRes, 2, "sst_bc_pre_res");
+        if (implicit) dump_mat(turb->Jacobian, 2, "sst_bc_pre_bsr");
+        turb->LinSysRes.SetValZero();
+        if (implicit) turb->Jacobian.SetValZero();
+        drv.integ(TURB_SOL)->Space_Integration(geo, sc, tn, cfg, MESH_0, NO_RK_ITER, RUNTIME_TURB_SYS);
+        dump_vec(turb->LinSysRes, 2, "sst_bc_res");
+        if (implicit) dump_mat(turb->Jacobian, 2, "sst_bc_bsr");
+        dump_sol(turb, 2, false, "sst_bc_sol");
+        dump_sol(turb, 2, true, "sst_bc_sol_old");
+      }
+    } else {
+      // initial node records the first Iterate reads (flow U / V / Solution_Old, SST solution, mu_t, blending,
+      // cross diffusion and gradient from the last Postprocessing)
+      dump_sol(flow, nVar, false, "it_U0");
+      dump_sol(flow, nVar, true, "it_Uold0");
+      {
+        std::vector<double> V0(nPoint * nPrimVar);
+        for (unsigned long i = 0; i < nPoint; ++i)
+          for (unsigned short v = 0; v < nPrimVar; ++v) V0[i * nPrimVar + v] = flow->node[i]->GetPrimitive(v);
+        dumpd("it_V0", V0, {(long)nPoint, nPrimVar});
+      }
+      if (rans) {
+        dump_sol(turb, 2, false, "it_sst0");
+        std::vector<double> mt(nPoint), f1(nPoint), f2(nPoint), cd(nPoint), tg(nPoint * 2 * nDim);
+        for (unsigned long i = 0; i < nPoint; ++i) {
+          mt[i] = turb->node[i]->GetmuT();
+          f1[i] = turb->node[i]->GetF1blending();
+          f2[i] = turb->node[i]->GetF2blending();
+          cd[i] = turb->node[i]->GetCrossDiff();
+          for (unsigned short v = 0; v < 2; ++v)
+            for (unsigned short d = 0; d < nDim; ++d) tg[(i * 2 + v) * nDim + d] = turb->node[i]->GetGradient()[v][d];
+        }
+        dumpd("it_mut0", mt, {(long)nPoint});
+        dumpd("it_F1_0", f1, {(long)nPoint});
+        dumpd("it_F2_0", f2, {(long)nPoint});
+        dumpd("it_CDkw0", cd, {(long)nPoint});
+        dumpd("it_sstgrad0", tg, {(long)nPoint, 2, nDim});
+      }
+      for (int k = 0; k < n_iters; ++k) {
+        cfg->SetExtIter(k);
+        drv.iterate();
+        const std::string p = "it" + std::to_string(k + 1) + "_";
+        dump_sol(flow, nVar, false, p + "U");
+        std::vector<double> V(nPoint * nPrimVar), rms(nVar);
+        for (unsigned long i = 0; i < nPoint; ++i)
+          for (unsigned short v = 0; v < nPrimVar; ++v) V[i * nPrimVar + v] = flow->node[i]->GetPrimitive(v);
+        dumpd(p + "V", V, {(long)nPoint, nPrimVar});
+        for (unsigned short v = 0; v < nVar; ++v) rms[v] = flow->GetRes_RMS(v);
+        dumpd(p + "rms", rms, {(long)nVar});
+        if (rans) {
+          dump_sol(turb, 2, false, p + "sst");
+          std::vector<double> mt(nPoint), trms = {turb->GetRes_RMS(0), turb->GetRes_RMS(1)};
+          for (unsigned long i = 0; i < nPoint; ++i) mt[i] = turb->node[i]->GetmuT();
+          dumpd(p + "mut", mt, {(long)nPoint});
+          dumpd(p + "sst_rms", trms, {2});
+        }
+      }
+    }
+    std::vector<int64_t> dims = {nDim, nVar, nPrimVar, nPrimVarGrad, nSpecies, implicit ? 1 : 0, rans ? 1 : 0};
+    dumpi("dims", dims, {7});
+    g_manifest.close();
+    std::fprintf(stderr, "harness: bc/iters done (%lu points)\n", nPoint);
+    return 0;
   }
 
   // ---- Venkatakrishnan limiter computed by the reference from the gradients above

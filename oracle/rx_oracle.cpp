@@ -674,7 +674,9 @@ void visc_flux(const Mech& m, int nDim, const ViscParams& P, const double* Vi, c
                const double* Gj, double mu_i, double mu_j, double k_i, double k_j, const double* Dij_i,
                const double* Dij_j, const double* Ci, const double* Cj, const double* Normal, const double* Si,
                const double* Sj, double tke_i, double tke_j, double mut_i, double mut_j, double sigma_k,
-               const double* gk_i, const double* gk_j, double* res, double* Ji, double* Jj) {
+               const double* gk_i, const double* gk_j, double* res, double* Ji, double* Jj, bool corrected = true) {
+  // corrected = false: CAvgGradReactive_Boundary::ComputeResidual (numerics_direct_reactive.cpp:478-648, a8) —
+  // the plain mean gradient, no edge correction and no coincident-point check.
   const int ns = m.ns;
   const int nVar = ns + nDim + 2, nPrimVar = ns + nDim + 5, nGrad = ns + nDim + 2;
   const int T_P = 0, VX_P = 1, RHO_P = nDim + 2, RHOS_P = nDim + 5;
@@ -714,13 +716,15 @@ void visc_flux(const Mech& m, int nDim, const ViscParams& P, const double* Vi, c
   }
   double dist2 = 0.0;
   for (int d = 0; d < nDim; ++d) dist2 += Edge[d] * Edge[d];
-  if (!(dist2 > EPS)) throw std::runtime_error("Error: You are trying to compute flux between a node and itself");
-  double Diff[32];
-  Diff[T_A] = Vj[T_P] - Vi[T_P];
-  for (int d = 0; d < nDim; ++d) Diff[VX_A + d] = Vj[VX_P + d] - Vi[VX_P + d];
-  for (int s = 0; s < ns; ++s) Diff[RHOS_A + s] = Xs_j[s] - Xs_i[s];
-  for (int r = 0; r < nAvg; ++r)
-    for (int d = 0; d < nDim; ++d) G[r][d] -= (Proj[r] - Diff[r]) * Edge[d] / dist2;
+  if (corrected) {
+    if (!(dist2 > EPS)) throw std::runtime_error("Error: You are trying to compute flux between a node and itself");
+    double Diff[32];
+    Diff[T_A] = Vj[T_P] - Vi[T_P];
+    for (int d = 0; d < nDim; ++d) Diff[VX_A + d] = Vj[VX_P + d] - Vi[VX_P + d];
+    for (int s = 0; s < ns; ++s) Diff[RHOS_A + s] = Xs_j[s] - Xs_i[s];
+    for (int r = 0; r < nAvg; ++r)
+      for (int d = 0; d < nDim; ++d) G[r][d] -= (Proj[r] - Diff[r]) * Edge[d] / dist2;
+  }
 
   // --- SetLaminarTensorFlux
   double Flux[32][3], PF[32];
@@ -2548,6 +2552,496 @@ void orc_sst_update(int64_t N, const double* x, double relax, const double* rho,
   for (int64_t i = 0; i < N; ++i)
     for (int v = 0; v < 2; ++v)
       T[2 * i + v] = smin(smax((T[2 * i + v] * rho_old[i] + relax * x[2 * i + v]) / rho[i], lo[v]), hi[v]);
+}
+
+}  // extern "C"
+
+// =================================================================================================
+// next-3 + a8: boundary conditions of one Space_Integration (integration_structure.cpp:95-193): the weak
+// BCs in marker order, then the strong ones.
+//   flow  CReactiveEulerSolver::BC_Inlet    SU2_CFD/src/solver_direct_reactive.cpp:3226-3674
+//         CReactiveEulerSolver::BC_Outlet   :3808-4123
+//         CReactiveNSSolver::BC_Isothermal_Wall :5393-5711 (no grid motion)
+//         boundary viscous numerics CAvgGradReactive_Boundary::ComputeResidual numerics_direct_reactive.cpp:478-648
+//   SST   CTurbSSTSolver::BC_Inlet / BC_Outlet / BC_Isothermal_Wall solver_direct_turbulent.cpp:3142-3450
+// Library calls restated: ComputeDensity / ComputeTemperature / ComputeRgas (SetRgas on the clamped mass
+// fractions), ComputeEnthalpy, ComputeFrozenGamma / ComputeFrozenSoundSpeed, ComputeCV, ComputePartialEnergy,
+// ComputedP_dYs, ComputeCps (reacting_model_library.cpp:26-41, 398-470, 519-619, reacting_model_library.hpp:368).
+// =================================================================================================
+namespace {
+
+struct BCPrm {
+  int kind_inlet;             // TOTAL_CONDITIONS / MASS_FLOW / TEMPERATURE_IMPOSE
+  double tke_inf, kine_inf, omega_inf, beta1;
+  double P_ref, vel_ref, T_ref, E_ref, R_ref, rho_ref;
+  int k_inlet, k_outlet, k_iso, k_hf, k_total, k_massflow, k_timpose;  // the reference's enum values
+  double mach_inf, Pr_t, Le_t;
+  int implicit, rans;
+};
+
+double mix_cp(const Mech& m, double T, const double* Ys) {  // ComputeCP :612-619
+  double c = 0.0;
+  for (int s = 0; s < m.ns; ++s) c += (Ys[s] < 0.0 ? 1.0e-30 : Ys[s]) * (spline(m, P_CP, s, T) / m.mm[s]);
+  return c;
+}
+double frozen_gamma(const Mech& m, double T, const double* Ys) {  // ComputeFrozenGamma :398-403
+  const double Cp = mix_cp(m, T, Ys);
+  const double Cv = Cp - mix_rgas(m, Ys);
+  return Cp / Cv;
+}
+double partial_energy(const Mech& m, double T, int s) {  // ComputePartialEnergy(T, s) :583-588
+  return spline(m, P_H, s, T) / m.mm[s] - m.ri[s] * T;
+}
+
+// Secondary (dP/dU) of a ghost state (BC_Inlet :3510-3533 / BC_Outlet :3941-3962)
+void ghost_dpdu(const Mech& m, int nDim, const double* Vg, double Gamma, double vel2, const BCPrm& P, double* S) {
+  const int ns = m.ns;
+  S[0] = (Gamma - 1.0) * 0.5 * vel2;
+  for (int d = 0; d < nDim; ++d) S[1 + d] = (1.0 - Gamma) * Vg[1 + d];
+  S[nDim + 1] = Gamma - 1.0;
+  const double dim_temp = Vg[0] * P.T_ref;
+  for (int s = 0; s < ns; ++s) S[nDim + 2 + s] = (m.ri[s] * dim_temp - (Gamma - 1.0) * partial_energy(m, dim_temp, s)) / P.E_ref;
+}
+// Secondary (dT/dU) of a ghost state for the boundary viscous numerics (:3573-3595 / :4021-4044)
+void ghost_dtdu(const Mech& m, int nDim, const double* Vg, const double* Ys, const BCPrm& P, double* S) {
+  const int ns = m.ns;
+  const double dim_temp = Vg[0] * P.T_ref;
+  const double Cv = (mix_cp(m, dim_temp, Ys) - mix_rgas(m, Ys)) / P.R_ref;
+  const double rhoCv = Vg[nDim + 2] * Cv;
+  double sq_vel = 0.0;
+  for (int d = 0; d < nDim; ++d) sq_vel += Vg[1 + d] * Vg[1 + d];
+  S[0] = 0.5 * sq_vel / rhoCv;
+  for (int d = 0; d < nDim; ++d) S[1 + d] = -Vg[1 + d] / rhoCv;
+  S[nDim + 1] = 1.0 / rhoCv;
+  for (int s = 0; s < ns; ++s) S[nDim + 2 + s] = -partial_energy(m, dim_temp, s) / (P.E_ref * rhoCv);
+}
+
+struct BCField {
+  const double *coord, *U, *V, *dPdU, *dTdU, *G, *mu, *kappa, *Dij, *tke, *mut, *sigk, *gk, *eddy;
+  const int64_t *rp, *col;
+  double *R, *A, *Uold;
+};
+
+// The weak flow BC of one vertex: ghost state, then R += Fc, A_ii += Jc_i, R -= Fv, A_ii -= Jv_i.
+void flow_weak_vertex(const Mech& m, int nDim, const BCPrm& P, int kind, const double* md, int64_t i, int64_t pn,
+                      const double* bn, BCField& f, double* Vg) {
+  const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5, nG = ns + nDim + 2;
+  const int T_ = 0, VX = 1, P_ = nDim + 1, RHO = nDim + 2, H_ = nDim + 3, A_ = nDim + 4, RHOS = nDim + 5;
+  double Normal[3], UnitNormal[3];
+  double Area = 0.0;
+  for (int d = 0; d < nDim; ++d) Area += bn[d] * bn[d];
+  Area = std::sqrt(Area);
+  for (int d = 0; d < nDim; ++d) {
+    Normal[d] = -bn[d];
+    UnitNormal[d] = Normal[d] / Area;
+  }
+  const double* Vd = f.V + i * nPV;
+  const double* Sd = f.dPdU + i * nVar;
+  double Sc[32], Sv[32], Ys[32];
+  bool sup = false;  // supersonic outlet: the node's own secondaries
+  if (kind == P.k_inlet) {
+    for (int s = 0; s < ns; ++s) Ys[s] = md[6 + s];
+    const double* dir = md + 3;
+    double Gamma = Sd[nDim + 1] + 1.0, vel_mag = 0.0;
+    if (P.kind_inlet == P.k_timpose) {
+      const double T = md[1] / P.T_ref;
+      vel_mag = md[2] / P.vel_ref;
+      Vg[T_] = T;
+      for (int d = 0; d < nDim; ++d) Vg[VX + d] = vel_mag * dir[d];
+      Vg[P_] = Vd[P_];
+      Vg[RHO] = Vg[P_] / (T * mix_rgas(m, Ys)) * P.R_ref;
+      const double dim_temp = T * P.T_ref;
+      Vg[H_] = mix_enthalpy(m, dim_temp, Ys) / P.E_ref + (P.rans ? 1.0 : 0.0) * P.tke_inf;
+      Vg[H_] += 0.5 * vel_mag * vel_mag;
+      Vg[A_] = std::sqrt(frozen_gamma(m, dim_temp, Ys) * mix_rgas(m, Ys) * dim_temp) / P.vel_ref;
+      // Gamma is left uninitialised by the reference in this branch (:3236, :3515); it only enters the
+      // ghost's dP/dU, i.e. Jacobian_j, which the BC discards. The domain value stands in.
+    } else if (P.kind_inlet == P.k_massflow) {
+      const double Density = md[1] / P.rho_ref;
+      vel_mag = md[2] / P.vel_ref;
+      double SoundSpeed = Vd[A_];
+      const double GM1 = Gamma - 1.0;
+      double Vn = 0.0;
+      for (int d = 0; d < nDim; ++d) Vn += Vd[VX + d] * UnitNormal[d];
+      const double Riemann = Vn + 2.0 * SoundSpeed / GM1;
+      double alpha = 0.0;
+      for (int d = 0; d < nDim; ++d) alpha += UnitNormal[d] * dir[d];
+      SoundSpeed = Riemann - vel_mag * alpha;
+      SoundSpeed = std::max(0.0, 0.5 * GM1 * SoundSpeed);
+      const double Pressure = SoundSpeed * SoundSpeed * Density / Gamma;
+      Vg[T_] = Pressure / (Density * mix_rgas(m, Ys)) * P.R_ref;
+      for (int d = 0; d < nDim; ++d) Vg[VX + d] = vel_mag * dir[d];
+      Vg[P_] = Pressure;
+      Vg[RHO] = Density;
+      const double dim_temp = Vg[T_] * P.T_ref;
+      double aux = mix_enthalpy(m, dim_temp, Ys) / P.E_ref;
+      if (P.rans) aux += P.tke_inf;
+      Vg[H_] = aux;
+      Vg[H_] += 0.5 * vel_mag * vel_mag;
+      Vg[A_] = SoundSpeed;
+    } else {  // TOTAL_CONDITIONS :3283-3408
+      const double Ttot = md[1] / P.T_ref, Ptot = md[2] / P.P_ref;
+      double Velocity2 = 0.0, Vn = 0.0;
+      for (int d = 0; d < nDim; ++d) {
+        Velocity2 += Vd[VX + d] * Vd[VX + d];
+        Vn += Vd[VX + d] * UnitNormal[d];
+      }
+      const double SoundSpeed = Vd[A_];
+      const double dim_temp = Ttot * P.T_ref;
+      const double Gamma_Tot = frozen_gamma(m, dim_temp, Ys);
+      Gamma = 2.0 / (1.0 / Gamma + 1.0 / Gamma_Tot);
+      const double GM1 = Gamma - 1.0;
+      const double Riemann = Vn + 2.0 * SoundSpeed / GM1;
+      double Tot_Enthalpy = mix_enthalpy(m, dim_temp, Ys);
+      double alpha = 0.0;
+      for (int d = 0; d < nDim; ++d) alpha += UnitNormal[d] * dir[d];
+      const double Rgas = mix_rgas(m, Ys) / P.R_ref;
+      auto fT = [&](double T) {
+        const double hb = mix_enthalpy(m, T, Ys);
+        const double cb = std::sqrt(Gamma * Rgas * T);
+        const double Vb = (Riemann - 2.0 * cb / GM1) / alpha;
+        return hb + 0.5 * Vb * Vb;
+      };
+      double Told = Ttot + 1.0, Tcurr = Ttot, Tnew;
+      bool conv = false;
+      for (int it = 0; it < 15; ++it) {
+        const double tmp = fT(Tcurr);
+        const double F = tmp - Tot_Enthalpy;
+        const double dF = tmp - fT(Told);
+        Tnew = Tcurr - F * (Tcurr - Told) / dF;
+        if (std::abs(Tnew - Tcurr) < 1.0e-9) {
+          conv = true;
+          break;
+        }
+        Told = Tcurr;
+        Tcurr = Tnew;
+      }
+      if (conv) {
+        Vg[T_] = Tcurr;
+      } else {
+        double Ta = 300.0 / P.T_ref, Tb = Ttot;
+        bool bconv = false;
+        for (int it = 0; it < 100; ++it) {
+          Tcurr = (Ta + Tb) / 2.0;
+          const double F = fT(Tcurr) - Tot_Enthalpy;
+          if (std::abs(F) < 1.0e-6) {
+            Vg[T_] = Tcurr;
+            bconv = true;
+            break;
+          }
+          if (F > 0.0) Ta = Tcurr; else Tb = Tcurr;
+        }
+        if (!bconv) throw std::runtime_error("Convergence not achieved for bisection method in inlet boundary condition");
+      }
+      if (P.rans) Tot_Enthalpy += P.tke_inf;
+      Vg[H_] = Tot_Enthalpy;
+      const double rho_tot = Ptot / (Rgas * Ttot);
+      Vg[RHO] = rho_tot * std::pow(Vg[T_] / Ttot, 1.0 / GM1);
+      Vg[P_] = Vg[RHO] * Rgas * Vg[T_];
+      Vg[A_] = std::sqrt(Vg[T_] * Gamma * Rgas);
+      vel_mag = std::abs((Riemann - 2.0 * Vg[A_] / GM1) / alpha);
+      for (int d = 0; d < nDim; ++d) Vg[VX + d] = vel_mag * dir[d];
+      (void)Velocity2;
+    }
+    for (int s = 0; s < ns; ++s) Vg[RHOS + s] = Ys[s];
+    if (P.implicit) ghost_dpdu(m, nDim, Vg, Gamma, vel_mag * vel_mag, P, Sc);
+  } else {  // OUTLET_FLOW :3826-3930
+    const double Density = Vd[RHO];
+    double Velocity[3], Velocity2 = 0.0;
+    for (int d = 0; d < nDim; ++d) {
+      Velocity[d] = Vd[VX + d];
+      Velocity2 += Velocity[d] * Velocity[d];
+    }
+    const double Pressure = Vd[P_];
+    const double Gamma = Sd[nDim + 1] + 1.0;
+    double SoundSpeed = std::sqrt(Gamma * Pressure / Density);
+    const double Mach_Exit = std::sqrt(Velocity2) / SoundSpeed;
+    if (Mach_Exit >= 1.0) {
+      for (int v = 0; v < nPV; ++v) Vg[v] = Vd[v];
+      sup = true;
+    } else {
+      const double Entropy = Pressure * std::pow(1.0 / Density, Gamma);
+      double Vn = 0.0;
+      for (int d = 0; d < nDim; ++d) Vn += Velocity[d] * UnitNormal[d];
+      const double GM1 = Gamma - 1.0;
+      const double Riemann = Vn + 2.0 * SoundSpeed / GM1;
+      const double P_Exit = md[1] / P.P_ref;
+      Vg[P_] = P_Exit;
+      Vg[RHO] = std::pow(P_Exit / Entropy, 1.0 / Gamma);
+      SoundSpeed = std::sqrt(Gamma * P_Exit / Vg[RHO]);
+      const double Vn_Exit = Riemann - 2.0 * SoundSpeed / GM1;
+      Velocity2 = 0.0;
+      for (int d = 0; d < nDim; ++d) {
+        Velocity[d] += (Vn_Exit - Vn) * UnitNormal[d];
+        Velocity2 += Velocity[d] * Velocity[d];
+        Vg[VX + d] = Velocity[d];
+      }
+      for (int s = 0; s < ns; ++s) Ys[s] = Vd[RHOS + s];
+      Vg[T_] = P_Exit / (Vg[RHO] * mix_rgas(m, Ys)) * P.R_ref;
+      const double dim_temp = Vg[T_] * P.T_ref;
+      Vg[H_] = mix_enthalpy(m, dim_temp, Ys) / P.E_ref + (P.rans ? 1.0 : 0.0) * P.tke_inf;
+      Vg[H_] += 0.5 * Velocity2;
+      Vg[A_] = SoundSpeed;
+      for (int s = 0; s < ns; ++s) Vg[RHOS + s] = Ys[s];
+      if (P.implicit) ghost_dpdu(m, nDim, Vg, Gamma, Velocity2, P, Sc);
+    }
+  }
+  // convective part (CUpwReactiveAUSM on V_domain | V_ghost)
+  double res[32], Ji[32 * 32], Jj[32 * 32];
+  ausm(nDim, ns, Vd, Vg, Normal, Sd, sup ? Sd : Sc, P.mach_inf, P.implicit != 0, res, Ji, Jj);
+  bool err = false;
+  for (int v = 0; v < nVar; ++v) err |= std::isnan(res[v]);
+  if (P.implicit && !err)
+    for (int q = 0; q < nVar * nVar; ++q) err |= std::isnan(Ji[q]);
+  if (err) throw std::runtime_error("NaN found in the convective residual of a boundary condition");
+  double* Ri = f.R + i * nVar;
+  double* D = P.implicit ? f.A + find_diag(f.rp, f.col, i) * nVar * nVar : nullptr;
+  for (int v = 0; v < nVar; ++v) Ri[v] += res[v];
+  if (D)
+    for (int q = 0; q < nVar * nVar; ++q) D[q] += Ji[q];
+  // viscous part (CAvgGradReactive_Boundary: both gradients / transport coefficients of the domain node)
+  if (P.implicit) {
+    if (sup) {
+      for (int v = 0; v < nVar; ++v) Sv[v] = f.dTdU[i * nVar + v];
+    } else {
+      ghost_dtdu(m, nDim, Vg, Ys, P, Sv);
+    }
+  }
+  ViscParams vp{P.T_ref, P.E_ref, P.R_ref, P.Pr_t, P.Le_t, P.rans, P.implicit};
+  const double* Gi = f.G + i * nG * nDim;
+  visc_flux(m, nDim, vp, Vd, Vg, Gi, Gi, f.mu[i], f.mu[i], f.kappa[i], f.kappa[i], f.Dij + i * ns * ns,
+            f.Dij + i * ns * ns, f.coord + i * nDim, f.coord + pn * nDim, Normal,
+            P.implicit ? f.dTdU + i * nVar : nullptr, P.implicit ? Sv : nullptr, P.rans ? f.tke[i] : 0.0,
+            P.rans ? f.tke[i] : 0.0, P.rans ? f.mut[i] : 0.0, P.rans ? f.mut[i] : 0.0, P.rans ? f.sigk[i] : 1.0,
+            P.rans ? f.gk + i * nDim : nullptr, P.rans ? f.gk + i * nDim : nullptr, res, P.implicit ? Ji : nullptr,
+            P.implicit ? Jj : nullptr, false);
+  err = false;
+  for (int v = 0; v < nVar; ++v) err |= std::isnan(res[v]);
+  if (P.implicit && !err)
+    for (int q = 0; q < nVar * nVar; ++q) err |= std::isnan(Ji[q]);
+  if (err) throw std::runtime_error("NaN found in the viscous residual of a boundary condition");
+  for (int v = 0; v < nVar; ++v) Ri[v] -= res[v];
+  if (D)
+    for (int q = 0; q < nVar * nVar; ++q) D[q] -= Ji[q];
+}
+
+// CSysMatrix::DeleteValsRowi (matrix_structure.cpp:483-495) for scalar row r of block row i.
+void delete_row(int64_t i, int r, int nb, const int64_t* rp, const int64_t* col, double* A) {
+  for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+    for (int c = 0; c < nb; ++c) A[k * nb * nb + r * nb + c] = 0.0;
+    if (col[k] == i) A[k * nb * nb + r * nb + r] = 1.0;
+  }
+}
+
+// CReactiveNSSolver::BC_Isothermal_Wall (:5393-5711), no grid motion.
+void flow_wall_vertex(const Mech& m, int nDim, const BCPrm& P, const double* md, int64_t i, int64_t pn,
+                      const double* bn, BCField& f) {
+  const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5;
+  const double Twall = md[1] / P.T_ref;
+  const double dim_temp = Twall * P.T_ref;
+  double aux_Cp[32];
+  for (int s = 0; s < ns; ++s) aux_Cp[s] = spline(m, P_CP, s, dim_temp) / m.mm[s];
+  double Area = 0.0;
+  for (int d = 0; d < nDim; ++d) Area += bn[d] * bn[d];
+  Area = std::sqrt(Area);
+  double dij = 0.0;
+  for (int d = 0; d < nDim; ++d) {
+    const double x = f.coord[pn * nDim + d] - f.coord[i * nDim + d];
+    dij += x * x;
+  }
+  dij = std::sqrt(dij);
+  double Res_Conv[32], Res_Visc[32];
+  for (int v = 0; v < nVar; ++v) Res_Conv[v] = Res_Visc[v] = 0.0;
+  for (int d = 0; d < nDim; ++d) f.Uold[i * nVar + 1 + d] = 0.0 * f.V[i * nPV + nDim + 2];  // SetVelocity_Old
+  double* Ri = f.R + i * nVar;
+  for (int d = 0; d < nDim; ++d) Ri[1 + d] = 0.0;  // LinSysRes.SetBlock_Zero(iPoint, RHOVX + iDim)
+  const double Tj = f.V[pn * nPV];
+  const double ktr = f.kappa[i];
+  double turb_closure = 0.0, turb_ktr = 0.0;
+  if (P.rans) {
+    const double eddy_v = f.eddy[i];
+    for (int s = 0; s < ns; ++s) {
+      const double aux_ys = f.U[i * nVar + nDim + 2 + s];
+      turb_closure += eddy_v / P.Pr_t * aux_Cp[s] * aux_ys * (Twall - Tj) / dij;
+    }
+    for (int s = 0; s < ns; ++s) {
+      const double aux_ys = f.U[i * nVar + nDim + 2 + s];
+      turb_ktr += eddy_v / (P.Pr_t) * aux_Cp[s] * aux_ys;
+    }
+  }
+  const double dTdn = +(Twall - Tj) / dij;
+  Res_Visc[nDim + 1] = ktr * dTdn * Area + turb_closure * Area;
+  if (P.implicit) {
+    double J[32 * 32];
+    for (int q = 0; q < nVar * nVar; ++q) J[q] = 0.0;
+    for (int d = 0; d < nDim; ++d) delete_row(i, 1 + d, nVar, f.rp, f.col, f.A);
+    const double* dTdU = f.dTdU + pn * nVar;
+    const int E = nDim + 1;
+    J[E * nVar + 0] = -ktr * dTdU[0] / dij * Area;
+    J[E * nVar + E] = -ktr * dTdU[E] / dij * Area - turb_ktr * dTdU[E] / dij * Area;
+    for (int s = 0; s < ns; ++s) J[E * nVar + nDim + 2 + s] = -ktr * dTdU[nDim + 2 + s] / dij * Area;
+    double* D = f.A + find_diag(f.rp, f.col, i) * nVar * nVar;
+    for (int q = 0; q < nVar * nVar; ++q) D[q] -= J[q];
+  }
+  for (int v = 0; v < nVar; ++v) Ri[v] += Res_Conv[v];
+  for (int v = 0; v < nVar; ++v) Ri[v] -= Res_Visc[v];
+  if (P.implicit)
+    for (int d = 0; d < nDim; ++d) delete_row(i, 1 + d, nVar, f.rp, f.col, f.A);
+}
+
+BCPrm bc_params(const double* p, int implicit, int rans) {
+  BCPrm P;
+  P.kind_inlet = (int)p[0];
+  P.tke_inf = p[1];
+  P.kine_inf = p[2];
+  P.omega_inf = p[3];
+  P.beta1 = p[4];
+  P.P_ref = p[5];
+  P.vel_ref = p[6];
+  P.T_ref = p[7];
+  P.E_ref = p[8];
+  P.R_ref = p[9];
+  P.rho_ref = p[10];
+  P.k_inlet = (int)p[11];
+  P.k_outlet = (int)p[12];
+  P.k_iso = (int)p[13];
+  P.k_hf = (int)p[14];
+  P.k_total = (int)p[15];
+  P.k_massflow = (int)p[16];
+  P.k_timpose = (int)p[17];
+  P.mach_inf = p[18];
+  P.Pr_t = p[19];
+  P.Le_t = p[20];
+  P.implicit = implicit;
+  P.rans = rans;
+  return P;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Flow BCs of one Space_Integration. bvert [NB][3] = (marker, node, kind) in marker / vertex order, pn [NB]
+// normal neighbours, mdata [nMarker][W] = (kind, a, b, dir[3], Y[Ns]), prm: bc_params layout (see oracle.py).
+// R [N][nVar] and A (BSR, may be null) are updated in place; Uold gets SetVelocity_Old; charac [NB][nPV] the
+// ghost states (CharacPrimVar) of the weak BCs. Returns 0, or 1 on a reference exception.
+int orc_bc_flow(void* h, int nDim, int64_t NB, const int64_t* bvert, const double* bnormal, const int64_t* pn,
+                int nMarker, const double* mdata, int W, const double* prm, int implicit, int rans,
+                const double* coord, const double* U, const double* V, const double* dPdU, const double* dTdU,
+                const double* G, const double* mu, const double* kappa, const double* Dij, const double* tke,
+                const double* mut, const double* sigk, const double* gk, const double* eddy, const int64_t* rp,
+                const int64_t* col, double* R, double* A, double* Uold, double* charac) {
+  const Mech& m = *static_cast<Mech*>(h);
+  const int nPV = m.ns + nDim + 5;
+  const BCPrm P = bc_params(prm, implicit, rans);
+  BCField f{coord, U, V, dPdU, dTdU, G, mu, kappa, Dij, tke, mut, sigk, gk, eddy, rp, col, R, A, Uold};
+  try {
+    for (int pass = 0; pass < 2; ++pass)
+      for (int mk = 0; mk < nMarker; ++mk) {
+        const double* md = mdata + (size_t)mk * W;
+        const int kind = (int)md[0];
+        const bool weak = kind == P.k_inlet || kind == P.k_outlet;
+        const bool strong = kind == P.k_iso;
+        if ((pass == 0 && !weak) || (pass == 1 && !strong)) continue;
+        for (int64_t b = 0; b < NB; ++b) {
+          if (bvert[3 * b] != mk) continue;
+          const int64_t i = bvert[3 * b + 1];
+          if (pass == 0)
+            flow_weak_vertex(m, nDim, P, kind, md, i, pn[b], bnormal + b * nDim, f, charac + b * nPV);
+          else
+            flow_wall_vertex(m, nDim, P, md, i, pn[b], bnormal + b * nDim, f);
+        }
+      }
+  } catch (const std::exception&) {
+    return 1;
+  }
+  return 0;
+}
+
+// SST BCs of one Space_Integration (CTurbSSTSolver::BC_Inlet / BC_Outlet :3264-3450, BC_Isothermal_Wall
+// :3142-3196; numerics CUpwSca_TurbSST / CAvgGrad_TurbSST) on the flow's V, mu, eddy viscosity and the ghost states charac of the flow BCs. T [N][2] (and
+// its Solution_Old: the same array) is set at the walls.
+void orc_bc_sst(int nDim, int nPV, int64_t NB, const int64_t* bvert, const double* bnormal, const int64_t* pn,
+                int nMarker, const double* mdata, int W, const double* prm, int implicit, const double* coord,
+                const double* V, const double* mu, const double* eddy, const double* charac, const double* TG,
+                const double* F1, const int64_t* rp, const int64_t* col, double* T, double* R, double* A) {
+  const BCPrm P = bc_params(prm, implicit, 1);
+  const SSTConst c = sst_const();
+  for (int pass = 0; pass < 2; ++pass)
+    for (int mk = 0; mk < nMarker; ++mk) {
+      const int kind = (int)mdata[(size_t)mk * W];
+      const bool weak = kind == P.k_inlet || kind == P.k_outlet;
+      const bool strong = kind == P.k_iso;
+      if ((pass == 0 && !weak) || (pass == 1 && !strong)) continue;
+      for (int64_t b = 0; b < NB; ++b) {
+        if (bvert[3 * b] != mk) continue;
+        const int64_t i = bvert[3 * b + 1], j = pn[b];
+        if (pass == 1) {
+          double distance = 0.0;
+          for (int d = 0; d < nDim; ++d)
+            distance += (coord[i * nDim + d] - coord[j * nDim + d]) * (coord[i * nDim + d] - coord[j * nDim + d]);
+          distance = std::sqrt(distance);
+          const double density = V[j * nPV + nDim + 2], lam = mu[j];
+          T[2 * i] = 0.0;
+          T[2 * i + 1] = 60.0 * lam / (density * P.beta1 * distance * distance);
+          R[2 * i] = R[2 * i + 1] = 0.0;
+          if (implicit)
+            for (int v = 0; v < 2; ++v) delete_row(i, v, 2, rp, col, A);
+          continue;
+        }
+        double Normal[3];
+        for (int d = 0; d < nDim; ++d) Normal[d] = -bnormal[b * nDim + d];
+        const double* Vi = V + i * nPV;
+        const double* Vg = charac + b * nPV;
+        const double Ti[2] = {T[2 * i], T[2 * i + 1]};
+        double Tg[2] = {Ti[0], Ti[1]};
+        if (kind == P.k_inlet) {
+          Tg[0] = P.kine_inf;
+          Tg[1] = P.omega_inf;
+        }
+        double* D = implicit ? A + find_diag(rp, col, i) * 4 : nullptr;
+        // CUpwSca_TurbSST (numerics_direct_turbulent.cpp:865-922)
+        double q = 0.0;
+        for (int d = 0; d < nDim; ++d) q += 0.5 * (Vi[d + 1] + Vg[d + 1]) * Normal[d];
+        const double a0 = 0.5 * (q + std::fabs(q)), a1 = 0.5 * (q - std::fabs(q));
+        const double ri = Vi[nDim + 2], rj = Vg[nDim + 2];
+        R[2 * i] += a0 * ri * Ti[0] + a1 * rj * Tg[0];
+        R[2 * i + 1] += a0 * ri * Ti[1] + a1 * rj * Tg[1];
+        if (D) {
+          D[0] += a0;
+          D[1] += 0.0;
+          D[2] += 0.0;
+          D[3] += a0;
+        }
+        // CAvgGrad_TurbSST (numerics_direct_turbulent.cpp:966-1040, the TURB_SOL VISC_BOUND_TERM of
+        // driver_structure.cpp:1610): plain mean normal gradient; both gradients, F1, mu, eddy of node i
+        const double sk = F1[i] * c.sk1 + (1.0 - F1[i]) * c.sk2;
+        const double so = F1[i] * c.so1 + (1.0 - F1[i]) * c.so2;
+        const double dik = mu[i] + sk * eddy[i], dio = mu[i] + so * eddy[i];
+        const double dk = 0.5 * (dik + dik), dw = 0.5 * (dio + dio);
+        double ev[3], dist2 = 0.0, proj = 0.0;
+        for (int d = 0; d < nDim; ++d) {
+          ev[d] = coord[j * nDim + d] - coord[i * nDim + d];
+          dist2 += ev[d] * ev[d];
+          proj += ev[d] * Normal[d];
+        }
+        if (dist2 == 0.0) proj = 0.0; else proj = proj / dist2;
+        double corr[2];
+        for (int v = 0; v < 2; ++v) {
+          double pnv = 0.0;
+          for (int d = 0; d < nDim; ++d) pnv += 0.5 * (TG[(i * 2 + v) * nDim + d] + TG[(i * 2 + v) * nDim + d]) * Normal[d];
+          corr[v] = pnv;
+        }
+        R[2 * i] -= dk * corr[0];
+        R[2 * i + 1] -= dw * corr[1];
+        if (D) {
+          D[0] -= -dk * proj / ri;
+          D[1] -= 0.0;
+          D[2] -= 0.0;
+          D[3] -= -dw * proj / ri;
+        }
+      }
+    }
 }
 
 }  // extern "C"

@@ -1,0 +1,110 @@
+"""next-3 + a8: the CPU oracle's boundary conditions and whole outer iteration against the reference's own
+(golden bc9 / it9 from oracle/ref_harness --bc / --iters, see oracle/make_golden.py).
+
+bc9: one Space_Integration of the reference (integration_structure.cpp:72-193) on the mini9 jet — interior loops,
+then the weak BCs (BC_Inlet TEMPERATURE_IMPOSE, BC_Outlet with the boundary viscous numerics
+CAvgGradReactive_Boundary) and the strong BC_Isothermal_Wall, for the flow and the SST solver.
+it9: three whole reference outer iterations (CMeanFlowIteration::Iterate) from the mini9 state.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def golden(case):
+    return dict(np.load(os.path.join(GOLD, case + ".npz")))
+
+
+@pytest.fixture(scope="module")
+def bc9():
+    return golden("bc9")
+
+
+@pytest.fixture(scope="module")
+def it9():
+    return golden("it9")
+
+
+def _bc_setup(g):
+    nDim, nVar = int(g["dims"][0]), int(g["dims"][1])
+    rp, col = g["bsr_row_ptr"], g["bsr_col"]
+    prm = O.bc_prm(g["bc_params"], g["mach_inf"][0], g["visc_params"][1], g["visc_params"][2])
+    return nDim, nVar, rp, col, prm
+
+
+def test_flow_bc_vs_reference(bc9):
+    g = bc9
+    nDim, nVar, rp, col, prm = _bc_setup(g)
+    m = O.Mechanism(g)
+    R = g["bc_pre_res"].copy()
+    A = np.zeros((int(rp[-1]), nVar, nVar))
+    A[g["bc_blk"]] = g["bc_pre_bsr"]
+    Uold = g["U"].copy()
+    ch = O.bc_flow(m, nDim, g, g["bc_marker"], prm, g, rp, col, R, A, Uold, True, True)
+    # ghost states (CharacPrimVar), Jacobian rows, Solution_Old (SetVelocity_Old at the walls): bitwise
+    assert np.array_equal(ch, g["bc_charac"])
+    assert np.array_equal(A[g["bc_blk"]], g["bc_bsr"])
+    assert np.array_equal(Uold, g["bc_sol_old"])
+    # residual: bitwise except the Stefan-Maxwell BiCGSTAB rounding of the boundary viscous flux
+    ref = g["bc_res"]
+    scale = np.maximum(np.abs(ref).max(axis=0), 1e-300)
+    assert (np.abs(R - ref).max(axis=0) / scale).max() < 1e-13
+    flow_rows = np.abs(R[:, :3] - ref[:, :3]).max()
+    assert flow_rows == 0.0
+
+
+def test_sst_bc_vs_reference(bc9):
+    g = bc9
+    nDim, nVar, rp, col, prm = _bc_setup(g)
+    charac = g["bc_charac"]
+    T = g["sst_sol"].copy()
+    R = g["sst_bc_pre_res"].copy()
+    A = np.zeros((int(rp[-1]), 2, 2))
+    A[g["bc_blk"]] = g["sst_bc_pre_bsr"]
+    O.bc_sst(nDim, g, g["bc_marker"], prm, g["V"], g["mu"], g["eddy_visc_flow"], charac, g["sst_grad"], g["sst_F1"],
+             rp, col, T, R, A, True)
+    assert np.array_equal(R, g["sst_bc_res"])
+    assert np.array_equal(A[g["bc_blk"]], g["sst_bc_bsr"])
+    assert np.array_equal(T, g["sst_bc_sol"])
+
+
+def iteration_cfg(g):
+    bp = g["bc_params"]
+    cfg = dict(p2v=O.p2v_params(g), cfl=g["dt_params"][0], max_delta_time=g["dt_params"][1],
+               prandtl_lam=g["dt_params"][2], prandtl_turb=g["dt_params"][3], lewis_turb=g["visc_params"][2],
+               mach_inf=g["mach_inf"][0], c_mu=g["src_params"][0], pasr_lb=g["src_params"][1], lin_tol=bp[19],
+               lin_iter=int(bp[20]), relaxation=bp[22], relaxation_turb=bp[23], cfl_red_turb=bp[24])
+    bc = dict(marker=g["bc_marker"], prm=O.bc_prm(bp, g["mach_inf"][0], g["visc_params"][1], g["visc_params"][2]))
+    state = dict(U=g["it_U0"], V=g["it_V0"], Uold=g["it_Uold0"], T=g["it_sst0"], TG=g["it_sstgrad0"],
+                 F1=g["it_F1_0"], F2=g["it_F2_0"], CDkw=g["it_CDkw0"], mut=g["it_mut0"])
+    return cfg, bc, state
+
+
+def colrel(a, ref):
+    return (np.abs(a - ref).max(axis=0) / np.maximum(np.abs(ref).max(axis=0), 1e-300)).max()
+
+
+# per-iteration bars: last-bit differences of the Stefan-Maxwell solve grow through FGMRES
+ITER_TOL = {1: 1e-13, 2: 1e-11, 3: 1e-9}
+
+
+def test_outer_iterations_vs_reference(it9):
+    g = it9
+    nDim = int(g["dims"][0])
+    m = O.Mechanism(g)
+    cfg, bc, s = iteration_cfg(g)
+    pat = (g["bsr_row_ptr"], g["bsr_col"])
+    for k in range(3):
+        s = O.outer_iteration(m, nDim, g, s, bc, cfg, k, pat)
+        p, tol = f"it{k + 1}_", ITER_TOL[k + 1]
+        assert colrel(s["U"], g[p + "U"]) < tol, k
+        assert colrel(s["V"], g[p + "V"]) < tol, k
+        assert colrel(s["T"], g[p + "sst"]) < tol, k
+        assert np.abs(s["mut"] - g[p + "mut"]).max() / np.abs(g[p + "mut"]).max() < tol * 100
+        np.testing.assert_allclose(s["rms"], g[p + "rms"], rtol=tol * 100)
+        np.testing.assert_allclose(s["sst_rms"], g[p + "sst_rms"], rtol=tol * 100)
