@@ -103,31 +103,49 @@ def build_workload(nx, ny, ns, n_part=1):
     return mesh, st, mech, kw
 
 
-def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg):
-    """One outer iteration (flow implicit step + SST step) of the CPU restatement (oracle/, one core) on
-    the same mesh."""
+def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
+    """One reference outer iteration of the CPU restatement (oracle/, one core) on the same mesh and state:
+    O.outer_iteration (flow Preprocessing, time step, loops + boundary conditions, FGMRES(5)+ILU0 update,
+    Preprocessing(Output), SST iteration) — or, with bc None (--no-bc), the legacy flow + SST step."""
     from oracle import oracle as O
     om = O.Mechanism(mech_arrays)
     c = dict(cfl=cfg.cfl, max_delta_time=cfg.max_delta_time, prandtl_lam=cfg.prandtl_lam,
              prandtl_turb=cfg.prandtl_turb, lewis_turb=cfg.lewis_turb, mach_inf=cfg.mach_inf, c_mu=cfg.c_mu,
              pasr_lb=cfg.pasr_lb, lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter, relaxation=cfg.relaxation)
-    pattern = O.bsr_pattern(len(st["V"]), mesh["edges"])
-    t0 = time.perf_counter()
-    _, info = O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern, part_ptr=mesh.get("part_ptr"))
-    flow = dict(V=st["V"], grad=info["grad"], mu=st["mu"], eddy=st["eddy_visc_flow"],
-                strain=O.strain_mag(2, info["grad"]))
-    O.sst_step(2, mesh, flow, st["sst_sol"], None, st["sst_F1"], st["sst_F2"], st["sst_CDkw"], info["dt"],
-               dict(lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter), pattern=pattern, part_ptr=mesh.get("part_ptr"))
-    dt = time.perf_counter() - t0
     N = len(st["V"])
+    pattern = O.bsr_pattern(N, mesh["edges"])
+    if bc is not None:
+        from tests.rxpkg import synth
+        bp = np.asarray(dict(np.load(os.path.join(ROOT, "tests", "golden", "bc9.npz")))["bc_params"])
+        md = np.array(bc["data"], dtype=np.float64)
+        md[:, 0] = [{1: bp[11], 2: bp[12], 3: bp[13]}.get(int(k), -1.0) for k in bc["kind"]]
+        mesh_o = dict(mesh, bvertex=np.c_[np.asarray(mesh["bvertex"])[:, :2], np.zeros(len(mesh["bvertex"]))])
+        bco = dict(marker=md, prm=O.bc_prm(bp, cfg.mach_inf, cfg.prandtl_turb, cfg.lewis_turb))
+        c.update(p2v=[cfg.t_min, cfg.t_max, cfg.T_ref, cfg.E_ref, cfg.R_ref, cfg.p_ref, cfg.visc_ref, cfg.cond_ref,
+                      cfg.vel_ref, cfg.len_ref, 0.0, float(cfg.clip_temp)])
+        T = np.ascontiguousarray(st["sst_sol"])
+        state = dict(U=st["U"], V=st["V"], Uold=st["U"], T=T, TG=O.sol_grad_ls(2, mesh["coord"], T, mesh["nbr_ptr"],
+                                                                             mesh["nbr"]),
+                     F1=st["sst_F1"], F2=st["sst_F2"], CDkw=st["sst_CDkw"], mut=st["mu_t"])
+        t0 = time.perf_counter()
+        O.outer_iteration(om, 2, mesh_o, state, bco, c, 0, pattern, part_ptr=mesh.get("part_ptr"))
+        what = "1 reference outer iteration (flow + SST, jet boundary conditions)"
+    else:
+        t0 = time.perf_counter()
+        _, info = O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern, part_ptr=mesh.get("part_ptr"))
+        flow = dict(V=st["V"], grad=info["grad"], mu=st["mu"], eddy=st["eddy_visc_flow"],
+                    strain=O.strain_mag(2, info["grad"]))
+        O.sst_step(2, mesh, flow, st["sst_sol"], None, st["sst_F1"], st["sst_F2"], st["sst_CDkw"], info["dt"],
+                   dict(lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter), pattern=pattern, part_ptr=mesh.get("part_ptr"))
+        what = "1 outer iteration (flow implicit step + SST step, no boundary conditions)"
+    dt = time.perf_counter() - t0
     return dict(value=N / dt / 1e6, unit="Mcells*iters/s", cores=1, kind="port",
-                sample=f"1 outer iteration (flow implicit step + SST step) of the same {N}-cell mesh on 1 host "
-                       f"core ({dt:.2f} s)")
+                sample=f"{what} of the same {N}-cell mesh on 1 host core ({dt:.2f} s)")
 
 
 def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist):
     """Build the rank's shard of the N-times-taller jet and attach the RCCL communicator."""
-    from tests.rxpkg import meshgen
+    from tests.rxpkg import meshgen, synth
     mesh, st, mech_arrays, kw = build_workload(nx, ny * world, ns, args.parts * world)
     sh = meshgen.shard(mesh, world, rank)
     st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
@@ -138,6 +156,8 @@ def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist):
     uid = [rx.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     s.comm_init(world, rank, uid[0])
+    if not args.no_bc:
+        s.set_bc(synth.jet_bc(sh, ns))
     t = rx.TurbSSTSolver(sh, s, rx.sst_cfg())
     return s, t, sh, st_l, mech_arrays, kw, cfg, int(sh["n_domain"])
 
@@ -159,8 +179,8 @@ def main():
     ap.add_argument("--parts", type=int, default=256,
                     help="partitions (= the reference's MPI ranks) of the ILU(0)/LU-SGS preconditioner")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--frozen", action="store_true",
-                    help="skip SetPrimitive_Variables: every step re-evaluates the same flow node records")
+    ap.add_argument("--no-bc", action="store_true",
+                    help="legacy step without boundary conditions and without the post-update Preprocessing")
     ap.add_argument("--cfl", type=float, default=0.0, help="CFL_NUMBER (default: the case's)")
     ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
     args = ap.parse_args()
@@ -208,6 +228,10 @@ def main():
             kw["cfl"] = args.cfl
         cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
         s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg, device=local)
+        if not args.no_bc:
+            from tests.rxpkg import synth
+            synth_bc = synth.jet_bc(mesh, ns)
+            s.set_bc(synth_bc)
         t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
         set_states(s, t, mesh, st)
         n_owned = s.N
@@ -218,23 +242,30 @@ def main():
     lin_its = []
     rms_log = []
 
+    ext_iter = [0]
+
     def step():
-        if not args.frozen:
+        if not args.no_bc:
+            # the reference's outer iteration (CMeanFlowIteration::Iterate): flow Preprocessing, time step,
+            # loops + boundary conditions, implicit solve, Preprocessing(Output) on the update, SST iteration
+            rms, trms, (it, tit) = rx.Iterate(s, t, ext_iter=ext_iter[0])
+            ext_iter[0] += 1
+        else:
             s.SetPrimitive_Variables()  # Cons2Prim + transport from the U of the previous update (next-1)
-        s.SetPrimitive_Gradient_LS()
-        s.SetStrainMag()
-        s.SetTime_Step()
-        s.Preprocessing_zero()
-        s.Upwind_Residual()
-        s.Viscous_Residual()
-        s.Source_Residual()
-        rms, it = s.ImplicitEuler_Iteration()
-        t.Preprocessing()
-        t.Upwind_Residual()
-        t.Viscous_Residual()
-        t.Source_Residual()
-        trms, tit = t.ImplicitEuler_Iteration()
-        t.Postprocessing()
+            s.SetPrimitive_Gradient_LS()
+            s.SetStrainMag()
+            s.SetTime_Step()
+            s.Preprocessing_zero()
+            s.Upwind_Residual()
+            s.Viscous_Residual()
+            s.Source_Residual()
+            rms, it = s.ImplicitEuler_Iteration()
+            t.Preprocessing()
+            t.Upwind_Residual()
+            t.Viscous_Residual()
+            t.Source_Residual()
+            trms, tit = t.ImplicitEuler_Iteration()
+            t.Postprocessing()
         lin_its.append((it, tit))
         rms_log.append(np.r_[rms, trms])
 
@@ -327,7 +358,8 @@ def main():
                        f" per GPU (global {nx}x{ny * world})" if parallelism.startswith("sharded") else ""),
                    "cells_per_gpu": n_owned, "halo_points": N - n_owned, "edges": E,
                    "species": ns, "nVar": ns + 4, "nnz_blocks": nnzb,
-                   "time": "EULER_IMPLICIT flow + SST (one outer iteration per step)",
+                   "time": "EULER_IMPLICIT flow + SST (one reference outer iteration per step" +
+                           (", no boundary conditions)" if args.no_bc else ", jet boundary conditions)"),
                    "linear_solver": "FGMRES(5)+ILU0 (flow 11x11 and SST 2x2 systems)",
                    "partitions": args.parts,
                    "parallelism": parallelism, "solve_graph": graph, "cells_total": cells,
@@ -339,7 +371,8 @@ def main():
         "phase_ms_per_step": {k: round(v, 4) for k, v in phase_ms.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg)
+        out["cpu_baseline"] = cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg,
+                                           None if args.no_bc else synth_bc)
     else:
         out["cpu_baseline"] = None
     s.close()

@@ -31,7 +31,7 @@ F = {name: k for k, name in enumerate(FIELDS)}
 # rx_kernel
 KERNELS = ["CONV", "VISC", "SOURCE", "GRAD", "LIMITER", "DT", "SPMV", "ILU_BUILD", "ILU_APPLY", "LUSGS", "KRYLOV",
            "UPDATE", "SOLVE", "VISC_JAC", "ASSEMBLE", "STRAIN", "PRIMITIVE", "SST_GRAD", "SST_UPW", "SST_VISC", "SST_SOURCE",
-           "SST_SYSTEM", "SST_SOLVE", "SST_POST"]
+           "SST_SYSTEM", "SST_SOLVE", "SST_POST", "BC", "SST_BC"]
 K = {name: k for k, name in enumerate(KERNELS)}
 
 
@@ -81,6 +81,31 @@ class Cfg(C.Structure):
                 ("cond_ref", C.c_double), ("vel_ref", C.c_double), ("len_ref", C.c_double)]
 
 
+class BcDesc(C.Structure):
+    """rx_bc_desc: boundary markers of Space_Integration (next-3)."""
+    _fields_ = [("n_marker", C.c_int32), ("kind", C.c_void_p), ("data", C.c_void_p), ("normal_neighbor", C.c_void_p),
+                ("inlet_kind", C.c_int32), ("tke_inf", C.c_double), ("kine_inf", C.c_double),
+                ("omega_inf", C.c_double)]
+
+
+BC_NONE, BC_INLET, BC_OUTLET, BC_ISOTHERMAL = 0, 1, 2, 3
+INLET_TOTAL_CONDITIONS, INLET_MASS_FLOW, INLET_TEMPERATURE_IMPOSE = 0, 1, 2
+
+
+def bc_from_reference(bc_marker, bc_params, normal_neighbor):
+    """rx_bc_desc inputs from the reference's marker table (oracle/ref_harness bc_marker / bc_params: rows
+    [KindBC, a, b, dir[3], Y[Ns]]; bc_params[11:18] = the reference's INLET_FLOW, OUTLET_FLOW, ISOTHERMAL,
+    HEAT_FLUX, TOTAL_CONDITIONS, MASS_FLOW, TEMPERATURE_IMPOSE enum values)."""
+    p = np.asarray(bc_params, dtype=np.float64)
+    k_in, k_out, k_iso, k_hf, k_tot, k_mf, k_ti = (int(x) for x in p[11:18])
+    kmap = {k_in: BC_INLET, k_out: BC_OUTLET, k_iso: BC_ISOTHERMAL}
+    md = np.ascontiguousarray(bc_marker, dtype=np.float64)
+    kinds = np.array([kmap.get(int(k), BC_NONE) for k in md[:, 0]], dtype=np.int32)
+    inlet = {k_tot: INLET_TOTAL_CONDITIONS, k_mf: INLET_MASS_FLOW, k_ti: INLET_TEMPERATURE_IMPOSE}[int(p[0])]
+    return dict(kind=kinds, data=md, normal_neighbor=np.ascontiguousarray(normal_neighbor, dtype=np.int64),
+                inlet_kind=inlet, tke_inf=float(p[1]), kine_inf=float(p[2]), omega_inf=float(p[3]))
+
+
 _lib = None
 
 
@@ -126,6 +151,9 @@ def lib():
                      "rx_sst_postprocessing"):
             getattr(_lib, name).argtypes = [C.c_void_p]
         _lib.rx_sst_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        _lib.rx_bc_set.argtypes = [C.c_void_p, C.POINTER(BcDesc)]
+        _lib.rx_bc_flow.argtypes = [C.c_void_p]
+        _lib.rx_bc_sst.argtypes = [C.c_void_p]
     return _lib
 
 
@@ -375,6 +403,20 @@ class ReactiveNSSolver:
              self.h)
         return n.value if count else None
 
+    def set_bc(self, bc):
+        """Boundary markers (dict from bc_from_reference or the same keys)."""
+        keep = dict(kind=np.ascontiguousarray(bc["kind"], dtype=np.int32),
+                    data=np.ascontiguousarray(bc["data"], dtype=np.float64),
+                    nn=np.ascontiguousarray(bc["normal_neighbor"], dtype=np.int64))
+        d = BcDesc(len(keep["kind"]), keep["kind"].ctypes.data, keep["data"].ctypes.data, keep["nn"].ctypes.data,
+                   int(bc["inlet_kind"]), float(bc.get("tke_inf", 0.0)), float(bc.get("kine_inf", 0.0)),
+                   float(bc.get("omega_inf", 0.0)))
+        _chk(lib().rx_bc_set(self.h, C.byref(d)), "rx_bc_set", self.h)
+
+    def BC(self):
+        """Space_Integration's boundary-condition loops (weak markers, then strong)."""
+        self._call("rx_bc_flow")
+
     def sync(self):
         self._call("rx_sync")
 
@@ -486,3 +528,41 @@ class TurbSSTSolver:
 
     def Postprocessing(self):
         self._call("rx_sst_postprocessing")
+
+    def BC(self):
+        """The SST boundary-condition loops (after the flow's BC of the same iteration)."""
+        self._call("rx_bc_sst")
+
+
+def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=False):
+    """One reference outer iteration for REACTIVE_RANS on the device, in the reference's order
+    (CMeanFlowIteration::Iterate iteration_structure.cpp:486-560; CMultiGridIntegration::MultiGrid_Iteration
+    integration_time.cpp:40-140 with MGLEVEL = 0; CSingleGridIntegration::SingleGrid_Iteration :770-810):
+    flow Preprocessing, SetTime_Step, Space_Integration (loops + BCs), ImplicitEuler_Iteration, the flow
+    Preprocessing(Output = true) on the updated solution; then the SST iteration. Nothing leaves the device
+    except the two RMS vectors and the linear-solver counts. Returns (rms_flow, rms_turb, lin_iters)."""
+
+    def preprocess(output):
+        flow.SetPrimitive_Variables(ext_iter)
+        flow.SetPrimitive_Gradient_LS()
+        flow.SetStrainMag()
+        if limiter and not output:
+            flow.SetPrimitive_Limiter()
+
+    preprocess(False)
+    flow.SetTime_Step()
+    flow.Preprocessing_zero()
+    flow.Upwind_Residual()
+    flow.Viscous_Residual()
+    flow.Source_Residual()
+    flow.BC()
+    rms, it = flow.ImplicitEuler_Iteration()
+    preprocess(True)
+    turb.Preprocessing()
+    turb.Upwind_Residual()
+    turb.Viscous_Residual()
+    turb.Source_Residual()
+    turb.BC()
+    rms_t, it_t = turb.ImplicitEuler_Iteration()
+    turb.Postprocessing()
+    return rms, rms_t, (it, it_t)

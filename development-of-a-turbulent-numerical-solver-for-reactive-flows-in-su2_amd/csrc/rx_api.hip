@@ -52,6 +52,8 @@ int ensure_assembled(rx_ctx* ctx) {
 
 }  // namespace
 
+int rx_ensure_assembled(rx_ctx* ctx) { return ensure_assembled(ctx); }
+
 extern "C" {
 
 const char* rx_status_string(int s) {
@@ -397,6 +399,8 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   std::vector<int32_t> nptr(N + 1), nbr(mesh->nbr_ptr[N]);
   for (int64_t i = 0; i <= N; ++i) nptr[i] = (int32_t)mesh->nbr_ptr[i];
   for (int64_t q = 0; q < mesh->nbr_ptr[N]; ++q) nbr[q] = (int32_t)mesh->nbr[q];
+  ctx->h_bvert.assign(mesh->bvert, mesh->bvert + 2 * NB);
+  ctx->h_bnormal.assign(mesh->bvert_normal, mesh->bvert_normal + NB * nd);
   std::vector<int32_t> bvp(N + 1, 0);
   std::vector<double> bvn((size_t)std::max<int64_t>(NB, 1) * nd);
   {
@@ -581,6 +585,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   rx_comm_free(ctx);
+  if (ctx->kind == RX_KIND_FLOW) rx_bc_free(ctx);
   if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
   if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
   rx_la_krylov_free(ctx);
@@ -604,6 +609,9 @@ int rx_field_size(const rx_ctx* ctx, rx_field f, int64_t* count) {
 int rx_upload(rx_ctx* ctx, rx_field f, const double* host, int64_t count) {
   if (!ctx || f < 0 || f >= RX_F_COUNT || count != ctx->fcount[f] || !host) return RX_ERR_ARG;
   RX_HIP(hipMemcpyAsync(ctx->f[f], host, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  // a loaded solution is also the Solution_Old (CVariable construction / LoadRestart)
+  if (f == RX_F_U && ctx->kind == RX_KIND_FLOW && ctx->uold)
+    RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[f], count * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
   RX_HIP(hipStreamSynchronize(ctx->stream));
   return RX_OK;
 }
@@ -639,6 +647,15 @@ int rx_residual_zero(rx_ctx* ctx) {
   RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
   ctx->phase_conv = ctx->phase_visc = ctx->phase_src = 0;
   ctx->assembled = ctx->cfg.implicit ? 0 : 1;
+  if (ctx->bc_on && ctx->bc_stream && !ctx->capturing) {
+    // the boundary fluxes of the current node records, overlapped with the interior sweeps (rx_bc.hip)
+    RX_HIP(hipEventRecord(ctx->bc_fork, ctx->stream));
+    RX_HIP(hipStreamWaitEvent(ctx->bc_stream, ctx->bc_fork, 0));
+    const int rc = rx_bc_launch_weak(ctx, ctx->bc_stream);
+    if (rc) return rc;
+    RX_HIP(hipEventRecord(ctx->bc_join, ctx->bc_stream));
+    ctx->bc_pending = true;
+  }
   return RX_OK;
 }
 

@@ -125,6 +125,36 @@ struct rx_ctx {
   hipGraph_t solve_graph = nullptr;
   bool capturing = false;
 
+  // ---- boundary conditions (rx_bc.hip, rx_bc_set); the SST context reads its flow context's
+  std::vector<int64_t> h_bvert;  // [NB][2] (marker, point) of the mesh, vertex order
+  std::vector<double> h_bnormal; // [NB][nDim]
+  bool bc_on = false;
+  int bc_nmark = 0, bc_W = 0, bc_inlet_kind = 0, bc_nweak = 0, bc_nbn = 0;
+  double bc_tke_inf = 0.0, bc_kine_inf = 0.0, bc_omega_inf = 0.0;
+  int32_t* bc_mkind = nullptr;   // [n_marker] rx_bc_kind
+  double* bc_mdata = nullptr;    // [n_marker][W]
+  int32_t* bc_node = nullptr;    // [NB] per vertex: point, normal neighbour, marker
+  int32_t* bc_pn = nullptr;
+  int32_t* bc_mark = nullptr;
+  double* bc_nrm = nullptr;      // [NB][nDim] vertex normals (vertex order)
+  int32_t* bc_weak = nullptr;    // [nweak] vertices of the weak (inlet / outlet) markers
+  int32_t* bc_bn = nullptr;      // [nbn] owned boundary points
+  int32_t* bc_bn_ptr = nullptr;  // [nbn+1] their vertices (bc_bn_vtx) in (marker, vertex) order
+  int32_t* bc_bn_vtx = nullptr;
+  uint8_t* bc_wall = nullptr;    // [N] isothermal-wall points (SetVelocity_Old in the update)
+  double* bc_charac = nullptr;   // [NB][nPV] ghost states (CharacPrimVar)
+  double* bc_resc = nullptr;     // [NB][nVar] convective / viscous boundary fluxes
+  double* bc_resv = nullptr;
+  double* bc_jacc = nullptr;     // [NB][nVar^2] convective Jacobian_i
+  double* bc_jacv = nullptr;     // [NB][2][nVar^2] viscous Jacobians (i, j)
+  double* bc_summ = nullptr;     // [NB][visc summary]
+  double* bc_sv = nullptr;       // [NB][nVar] ghost dT/dU
+  // the boundary fluxes (weak markers) only read the node records, so rx_residual_zero launches them on a
+  // side stream where they overlap the interior edge sweeps; rx_bc_flow joins before applying them
+  hipStream_t bc_stream = nullptr;
+  hipEvent_t bc_fork = nullptr, bc_join = nullptr;
+  bool bc_pending = false;
+
   // ---- profiling
   // Phases record an event pair on the context stream without blocking; pairs are resolved
   // (elapsed time accumulated per rx_kernel) when rx_profile_read / rx_sync drain the queue.
@@ -201,6 +231,10 @@ int rx_la_implicit_update(rx_ctx* ctx);
 int rx_la_explicit_update(rx_ctx* ctx);
 int rx_la_rk_update(rx_ctx* ctx, int stage, double alpha);
 int rx_la_build_system(rx_ctx* ctx);
+// boundary conditions (rx_bc.hip)
+void rx_bc_free(rx_ctx* ctx);
+int rx_bc_launch_weak(rx_ctx* ctx, hipStream_t st);  // ghost states + boundary fluxes (+ Jacobians)
+int rx_ensure_assembled(rx_ctx* ctx);  // implicit: assemble the residual / BSR Jacobian now (rx_api.hip)
 // SST (rx_sst.hip)
 int rx_sst_build_system(rx_ctx* ctx);
 int rx_sst_update(rx_ctx* ctx);

@@ -80,10 +80,13 @@ __global__ __launch_bounds__(kBlock) void k_build_system(int Nd, int N, const in
 //   mode 0 implicit  delta = relax * LinSysSol                          (:2390-2400)
 //   mode 1 explicit  delta = -(Res + 0) * dt / Vol                       (:2430-2440)
 //   mode 2 RK stage  delta = -(Res + 0) * dt / Vol * alpha_RK, U_old = U0 (ExplicitRK_Iteration :2456-2493)
+// wall (optional): isothermal-wall points, whose momentum Solution_Old BC_Isothermal_Wall sets to zero
+// (SetVelocity_Old, solver_direct_reactive.cpp:5477, variable_direct_reactive.cpp:950-957); uold mirrors it.
 __global__ __launch_bounds__(kBlock) void k_update(int N, int nVar, int nDim, const double* __restrict__ dx,
                                                    double scale, const double* __restrict__ vol,
                                                    const double* __restrict__ dt, int mode,
-                                                   const double* __restrict__ U0, double* __restrict__ U) {
+                                                   const double* __restrict__ U0, double* __restrict__ U,
+                                                   const uint8_t* __restrict__ wall, double* __restrict__ uold) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * nVar) return;
   const int i = t / nVar, v = t - i * nVar;
@@ -98,7 +101,11 @@ __global__ __launch_bounds__(kBlock) void k_update(int N, int nVar, int nDim, co
   }
   const double lo = (v >= 1 && v <= nDim + 1) ? -1.0 / rx::kEPS : 0.0;
   const double hi = 1.0 / rx::kEPS;
-  const double base = U0 ? U0[t] : U[t];
+  double base = U0 ? U0[t] : U[t];
+  if (wall && wall[i] && v >= 1 && v <= nDim) {
+    base = 0.0;
+    uold[t] = 0.0;
+  }
   const double x = base + delta;
   const double mx = (x < lo) ? lo : x;  // std::min(std::max(x, lo), hi), NaN and signed zeros included
   U[t] = (hi < mx) ? hi : mx;
@@ -194,7 +201,7 @@ int rx_la_implicit_update(rx_ctx* ctx) {
                         ctx->stream));
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_SOL],
                                                   ctx->cfg.relaxation, ctx->vol, ctx->f[RX_F_DT], 0, nullptr,
-                                                  ctx->f[RX_F_U]);
+                                                  ctx->f[RX_F_U], ctx->bc_wall, ctx->uold);
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }
@@ -204,7 +211,8 @@ int rx_la_explicit_update(rx_ctx* ctx) {
   RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[RX_F_U], sizeof(double) * ctx->N * ctx->nVar, hipMemcpyDeviceToDevice,
                         ctx->stream));
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], 1.0,
-                                                  ctx->vol, ctx->f[RX_F_DT], 1, nullptr, ctx->f[RX_F_U]);
+                                                  ctx->vol, ctx->f[RX_F_DT], 1, nullptr, ctx->f[RX_F_U], ctx->bc_wall,
+                                                  ctx->uold);
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }
@@ -217,7 +225,8 @@ int rx_la_rk_update(rx_ctx* ctx, int stage, double alpha) {
     RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[RX_F_U], sizeof(double) * ctx->N * ctx->nVar, hipMemcpyDeviceToDevice,
                           ctx->stream));
   k_update<<<blocks(n), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->nVar, ctx->nDim, ctx->f[RX_F_RES], alpha,
-                                                  ctx->vol, ctx->f[RX_F_DT], 2, ctx->uold, ctx->f[RX_F_U]);
+                                                  ctx->vol, ctx->f[RX_F_DT], 2, ctx->uold, ctx->f[RX_F_U], ctx->bc_wall,
+                                                  ctx->uold);
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }

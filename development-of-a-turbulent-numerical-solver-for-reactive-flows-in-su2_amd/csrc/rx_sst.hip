@@ -410,17 +410,19 @@ __global__ __launch_bounds__(kBlock) void k_sst_build_system(int Nd, int N, cons
 }
 
 // SST branch of the update (:698-713): AddConservativeSolution (variable_structure.cpp:214-219) with
-// the flow density (rho_old = rho: Cons2PrimVar sets V[rho] = U[rho], variable_direct_reactive.cpp:579-584,
-// and Solution_Old is the U the primitives were computed from). Limits: constructor :2731-2735.
+// density = the flow primitive density and density_old = the flow's Solution_Old(0) (the U before the flow
+// update, kept by its update kernel). Limits: constructor :2731-2735.
 __global__ __launch_bounds__(kBlock) void k_sst_update(int Nd, const double* __restrict__ x, double relax,
                                                        const double* __restrict__ V, int nPV, int rho_idx,
+                                                       const double* __restrict__ Uold, int nVarF,
                                                        double* __restrict__ T) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * Nd) return;
   const int i = t >> 1, v = t & 1;
   const double rho = V[(size_t)i * nPV + rho_idx];
+  const double rho_old = Uold[(size_t)i * nVarF];
   const double lo = v ? 1.0e-4 : 1.0e-10, hi = v ? 1.0e15 : 1.0e10;
-  T[t] = smin(smax((T[t] * rho + relax * x[t]) / rho, lo), hi);
+  T[t] = smin(smax((T[t] * rho_old + relax * x[t]) / rho, lo), hi);
 }
 
 // CTurbSSTSolver::Postprocessing after its gradient (:2966-3000): SetBlendingFunc, mu_t, over every
@@ -495,7 +497,8 @@ int rx_sst_update(rx_ctx* ctx) {
   const rx_ctx* fl = ctx->flow;
   if (ctx->Nd > 0)
     k_sst_update<<<blocks(2 * ctx->Nd), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->f[RX_F_SOL], ctx->cfg.relaxation,
-                                                                  fl->f[RX_F_V], fl->nPV, fl->nDim + 2, ctx->f[RX_F_U]);
+                                                                  fl->f[RX_F_V], fl->nPV, fl->nDim + 2, fl->uold,
+                                                                  fl->nVar, ctx->f[RX_F_U]);
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_U], 2);  // Set_MPI_Solution (:718)
 }

@@ -288,7 +288,9 @@ struct ViscNode {
 template <int NS, int NDIM>
 __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const ViscNode<NS, NDIM>& ni,
                                 const ViscNode<NS, NDIM>& nj, double sigma_k, const double* Normal, double* res,
-                                double* summ, double* scr) {
+                                double* summ, double* scr, bool corrected = true) {
+  // corrected = false: CAvgGradReactive_Boundary::ComputeResidual (numerics_direct_reactive.cpp:478-648, a8):
+  // the plain mean gradient — no edge correction, no coincident-point check.
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
   constexpr int T_P = 0, VX_P = 1, RHO_P = NDIM + 2, RHOS_P = NDIM + 5;
   constexpr int RHO_S = 0, RHOVX_S = 1, RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
@@ -326,8 +328,8 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   double dist2 = 0.0;
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) dist2 += Edge[d] * Edge[d];
-  if (!(dist2 > kEPS)) return ERR_GEOM;
-  {
+  if (corrected && !(dist2 > kEPS)) return ERR_GEOM;
+  if (corrected) {
     double Diff[nAvg], Proj[nAvg];
 #pragma unroll
     for (int r = 0; r < nAvg; ++r) {

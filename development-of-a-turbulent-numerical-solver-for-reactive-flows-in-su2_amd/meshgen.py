@@ -205,7 +205,33 @@ def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, **kw):
     dual["quads"] = quads
     dual["part_ptr"] = part_ptr
     dual["wall_distance"] = wall_distance(pts, bnd)
+    dual["bvertex_pn"] = normal_neighbor(pts, dual["nbr_ptr"], dual["nbr"], dual["bvertex"], dual["bvertex_normal"])
     return dual
+
+
+def normal_neighbor(coord, nbr_ptr, nbr, bvertex, bvertex_normal):
+    """CPhysicalGeometry::FindNormal_Neighbor (Common/src/geometry_structure.cpp:12610-12652): for every boundary
+    vertex the neighbour whose edge makes the largest cosine with the vertex normal (the last one on ties, the
+    reference's `>=`), with the reference's arithmetic."""
+    coord = np.asarray(coord, dtype=np.float64)
+    bv = np.asarray(bvertex)
+    out = np.zeros(len(bv), dtype=np.int64)
+    for b in range(len(bv)):
+        i = int(bv[b, 1])
+        n = np.asarray(bvertex_normal[b], dtype=np.float64)
+        best, cmax = 0, -1.0
+        for j in nbr[nbr_ptr[i]:nbr_ptr[i + 1]]:
+            sp = nv = nn = 0.0
+            for d in range(coord.shape[1]):
+                dc = coord[j, d] - coord[i, d]
+                sp += dc * n[d]
+                nv += dc * dc
+                nn += n[d] * n[d]
+            c = sp / (np.sqrt(nv) * np.sqrt(nn))
+            if c >= cmax:
+                best, cmax = int(j), c
+        out[b] = best
+    return out
 
 
 WALLS = ("upper_wall", "lower_wall_pre", "lower_wall_post")  # the cfg's MARKER_ISOTHERMAL
@@ -286,6 +312,8 @@ def shard(mesh, n_ranks: int, rank: int):
         send_ptr.append(len(send_idx))
     lpp = pp[pr[rank][0]:pr[rank][-1] + 2] - g0
     extra = {"wall_distance": np.asarray(mesh["wall_distance"])[l2g]} if "wall_distance" in mesh else {}
+    if "bvertex_pn" in mesh:  # normal neighbours: neighbours of own points, hence local
+        extra["bvertex_pn"] = g2l[np.asarray(mesh["bvertex_pn"])[keep]]
     return dict(**extra, edges=le, edge_normal=ln, coord=np.asarray(mesh["coord"])[l2g],
                 volume=np.asarray(mesh["volume"])[l2g], nbr_ptr=nptr_l, nbr=nbr_l.astype(np.int64), bvertex=lbv,
                 bvertex_normal=np.asarray(mesh["bvertex_normal"])[keep], part_ptr=lpp.astype(np.int64),

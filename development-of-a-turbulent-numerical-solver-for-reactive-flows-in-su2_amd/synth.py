@@ -94,3 +94,37 @@ def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1):
     return mesh, state, mech, {"mach_inf": float(g["mach_inf"][0]), "prandtl_turb": float(g["visc_params"][1]),
                                "lewis_turb": float(g["visc_params"][2]), "c_mu": float(g["src_params"][0]),
                                "pasr_lb": float(g["src_params"][1])}
+
+
+# MARKER_* of the reference's jet cfg (Test_Cases/TURBOLENT/TURBOLENT_COMBUSTION/*.cfg, oracle/make_golden.py):
+# INLET_TYPE = TEMPERATURE_IMPOSE, MARKER_INLET = (Oxidizer_Inlet, 300 K, 20 m/s, (1, 0, 0); Fuel_Inlet, 800 K,
+# 0.87 m/s, (0, 1, 0)), INLET_MASS_FRAC pure O2 / pure C4H6, MARKER_OUTLET = (Outlet, 101325 Pa),
+# MARKER_ISOTHERMAL = (upper_wall 300 K, lower_wall_pre 300 K, lower_wall_post 600 K).
+JET_MARKERS = {  # in meshgen.MARKERS order: (kind, a, b, flow direction, inlet species)
+    "Oxidizer_Inlet": ("inlet", 300.0, 20.0, (1.0, 0.0, 0.0), "O2"),
+    "Outlet": ("outlet", 101325.0, 0.0, (0.0, 0.0, 0.0), None),
+    "upper_wall": ("isothermal", 300.0, 0.0, (0.0, 0.0, 0.0), None),
+    "Fuel_Inlet": ("inlet", 800.0, 0.87, (0.0, 1.0, 0.0), "C4H6"),
+    "lower_wall_pre": ("isothermal", 300.0, 0.0, (0.0, 0.0, 0.0), None),
+    "lower_wall_post": ("isothermal", 600.0, 0.0, (0.0, 0.0, 0.0), None),
+}
+SPECIES_ORDER = ("C4H6", "H2O", "O2", "CO", "CO2", "H2", "O", "OH", "H")  # the golden cfg's SPECIES_ORDER
+
+
+def jet_bc(mesh, n_species):
+    """rx_bc_desc inputs of the jet's markers for a meshgen mesh (bvertex markers in meshgen.MARKERS order), with
+    the free-stream turbulence values the reference derives from the same cfg (golden bc9 bc_params)."""
+    mg = _meshgen()
+    g = dict(np.load(os.path.join(GOLDEN, "bc9.npz")))
+    bp = g["bc_params"]
+    kinds = {"inlet": 1, "outlet": 2, "isothermal": 3}
+    rows, kk = [], []
+    for name in mg.MARKERS:
+        kind, a, b, d, sp = JET_MARKERS[name]
+        y = np.zeros(n_species)
+        if sp is not None:
+            y[SPECIES_ORDER.index(sp)] = 1.0
+        rows.append(np.r_[0.0, a, b, d, y])
+        kk.append(kinds[kind])
+    return dict(kind=np.array(kk, dtype=np.int32), data=np.array(rows), normal_neighbor=mesh["bvertex_pn"],
+                inlet_kind=2, tke_inf=float(bp[1]), kine_inf=float(bp[2]), omega_inf=float(bp[3]))

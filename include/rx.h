@@ -234,6 +234,33 @@ int rx_sst_source(rx_ctx *turb);
 int rx_sst_implicit_euler(rx_ctx *turb, double *res_rms /* [2] or NULL */, int *lin_iters);
 int rx_sst_postprocessing(rx_ctx *turb);
 
+/* Boundary conditions of Space_Integration (SURVEY.md §8 next-3 + a8; integration_structure.cpp:95-193: the weak
+ * BCs in marker order, then the strong ones), restricted to the markers of the reference's reactive jet:
+ *   RX_BC_INLET       CReactiveEulerSolver::BC_Inlet solver_direct_reactive.cpp:3226-3674 (INLET_TYPE TOTAL_CONDITIONS,
+ *                     MASS_FLOW, TEMPERATURE_IMPOSE) / CTurbSSTSolver::BC_Inlet solver_direct_turbulent.cpp:3264-3358
+ *   RX_BC_OUTLET      CReactiveEulerSolver::BC_Outlet :3808-4123 / CTurbSSTSolver::BC_Outlet :3360-3450
+ *   RX_BC_ISOTHERMAL  CReactiveNSSolver::BC_Isothermal_Wall :5393-5711 (strong no-slip, DeleteValsRowi) /
+ *                     CTurbSSTSolver::BC_Isothermal_Wall :3142-3196
+ * with the boundary numerics CUpwReactiveAUSM + CAvgGradReactive_Boundary::ComputeResidual
+ * (numerics_direct_reactive.cpp:478-648, a8) and CUpwSca_TurbSST + CAvgGrad_TurbSST. Marker m of a mesh bvert is
+ * rx_mesh_desc.bvert[2b]. data rows [n_marker][6 + Ns]: inlet (Ttotal | density | T, Ptotal | velocity, flow
+ * direction[3], mass fractions[Ns]) as MARKER_INLET / INLET_MASS_FRAC, outlet (back pressure), isothermal (wall
+ * temperature). */
+typedef enum { RX_BC_NONE = 0, RX_BC_INLET = 1, RX_BC_OUTLET = 2, RX_BC_ISOTHERMAL = 3 } rx_bc_kind;
+typedef enum { RX_INLET_TOTAL_CONDITIONS = 0, RX_INLET_MASS_FLOW = 1, RX_INLET_TEMPERATURE_IMPOSE = 2 } rx_inlet_kind;
+typedef struct {
+  int32_t n_marker;
+  const int32_t *kind;             /* [n_marker] rx_bc_kind */
+  const double *data;              /* [n_marker][6 + Ns] */
+  const int64_t *normal_neighbor;  /* [n_bvert] CVertex::GetNormal_Neighbor */
+  int32_t inlet_kind;              /* rx_inlet_kind (INLET_TYPE) */
+  double tke_inf;                  /* CReactiveEulerSolver Tke_Inf (Tke_FreeStreamND; 0 without SST) */
+  double kine_inf, omega_inf;      /* CTurbSSTSolver free-stream k, omega (solver_direct_turbulent.cpp:2740-2752) */
+} rx_bc_desc;
+int rx_bc_set(rx_ctx *flow, const rx_bc_desc *bc);
+int rx_bc_flow(rx_ctx *flow); /* after the interior residual loops; implicit: on the assembled Jacobian */
+int rx_bc_sst(rx_ctx *turb);  /* after the SST loops, reads the ghost states of the flow's last rx_bc_flow */
+
 /* Per-phase device timing with HIP events on the context stream (for bench roofline). */
 typedef enum {
   RX_K_CONV = 0, RX_K_VISC, RX_K_SOURCE, RX_K_GRAD, RX_K_LIMITER, RX_K_DT, RX_K_SPMV, RX_K_ILU_BUILD,
@@ -248,6 +275,8 @@ typedef enum {
   RX_K_SST_SYSTEM, /* SST: system build + preconditioner build */
   RX_K_SST_SOLVE,  /* SST: FGMRES + RMS + conservative clipped update */
   RX_K_SST_POST,   /* SST: Postprocessing (gradient, blending, mu_t, flow coupling fields) */
+  RX_K_BC,         /* flow boundary conditions (rx_bc_flow) */
+  RX_K_SST_BC,     /* SST boundary conditions (rx_bc_sst) */
   RX_K_COUNT
 } rx_kernel;
 int rx_profile_enable(rx_ctx *ctx, int on);

@@ -572,6 +572,7 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     A = np.ascontiguousarray(A)
     st = dict(U=U, V=o["V"], dPdU=o["dPdU"], dTdU=o["dTdU"], grad_prim=G, mu=o["mu"], kappa=o["kappa"], Dij=o["Dij"],
               turb_k=T[:, 0].copy(), mu_t=mut, sigma_k=sig, grad_k=gk, eddy_visc_flow=o["eddy"])
+    A_loops, R_loops = A.copy(), R.copy()
     charac = bc_flow(mech, nDim, mesh, bc["marker"], bc["prm"], st, rp, col, R, A, Uold, True, True)
     diag = np.array([rp[i] + np.searchsorted(col[rp[i]:rp[i + 1]], i) for i in range(N)])
     ok = dt > 1e-16
@@ -621,4 +622,4 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     TG1 = sol_grad_ls(nDim, mesh["coord"], Tn, mesh["nbr_ptr"], mesh["nbr"])
     F1n, F2n, CDn, mutn = sst_blending(nDim, Tn, TG1, rho, o2["mu"], mesh["wall_distance"], strain2)
     return dict(U=Un, V=V2, Uold=Uold, T=Tn, TG=TG1, F1=F1n, F2=F2n, CDkw=CDn, mut=mutn, rms=rms, sst_rms=sst_rms,
-                lin_iters=it, sst_lin_iters=it2, dt=dt)
+                lin_iters=it, sst_lin_iters=it2, dt=dt, pre=o, pre_grad=G, jac_loops=A_loops, res_loops=R_loops, sys=A, rhs=rhs, sol=x, sst_sys=A2, sst_rhs=rhs2, sst_sol=x2)

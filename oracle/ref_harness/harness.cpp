@@ -470,12 +470,25 @@ int main(int argc, char** argv) {
         dumpd(p + "V", V, {(long)nPoint, nPrimVar});
         for (unsigned short v = 0; v < nVar; ++v) rms[v] = flow->GetRes_RMS(v);
         dumpd(p + "rms", rms, {(long)nVar});
+        dump_sol(flow, nVar, true, p + "Uold");
         if (rans) {
           dump_sol(turb, 2, false, p + "sst");
           std::vector<double> mt(nPoint), trms = {turb->GetRes_RMS(0), turb->GetRes_RMS(1)};
-          for (unsigned long i = 0; i < nPoint; ++i) mt[i] = turb->node[i]->GetmuT();
+          std::vector<double> f1(nPoint), f2(nPoint), cd(nPoint), tg(nPoint * 2 * nDim);
+          for (unsigned long i = 0; i < nPoint; ++i) {
+            mt[i] = turb->node[i]->GetmuT();
+            f1[i] = turb->node[i]->GetF1blending();
+            f2[i] = turb->node[i]->GetF2blending();
+            cd[i] = turb->node[i]->GetCrossDiff();
+            for (unsigned short v = 0; v < 2; ++v)
+              for (unsigned short d = 0; d < nDim; ++d) tg[(i * 2 + v) * nDim + d] = turb->node[i]->GetGradient()[v][d];
+          }
           dumpd(p + "mut", mt, {(long)nPoint});
           dumpd(p + "sst_rms", trms, {2});
+          dumpd(p + "F1", f1, {(long)nPoint});
+          dumpd(p + "F2", f2, {(long)nPoint});
+          dumpd(p + "CDkw", cd, {(long)nPoint});
+          dumpd(p + "sstgrad", tg, {(long)nPoint, 2, nDim});
         }
       }
     }
