@@ -14,6 +14,9 @@
  *   ExplicitRK_Iteration          -> rx_explicit_rk              (:2456-2493)
  *   ImplicitEuler_Iteration       -> rx_implicit_euler           (:2336-2407)
  *   SetStrainMag                  -> rx_strain_mag               (variable_direct_reactive.cpp:1060-1095)
+ *   SetPrimitive_Variables        -> rx_set_primitive            (:985-1040)
+ *   BC_Inlet / BC_Outlet / BC_Isothermal_Wall (Space_Integration's marker loops,
+ *                                 integration_structure.cpp:95-193) -> rx_bc_flow (:3226-4123, 5393-5711)
  * TurbSSTSolver mirrors CTurbSSTSolver / CTurbSolver (SU2_CFD/include/solver_structure.hpp, turbulent
  * classes; SU2_CFD/src/solver_direct_turbulent.cpp):
  *   Preprocessing                 -> rx_sst_preprocessing        (:2923-2951)
@@ -22,6 +25,8 @@
  *   Source_Residual               -> rx_sst_source               (:3018-3080)
  *   ImplicitEuler_Iteration       -> rx_sst_implicit_euler       (:615-728)
  *   Postprocessing                -> rx_sst_postprocessing       (:2953-3016)
+ *   BC_Inlet / BC_Outlet / BC_Isothermal_Wall -> rx_bc_sst       (:3142-3450)
+ * Iterate(flow, turb, ext_iter) is CMeanFlowIteration::Iterate for REACTIVE_RANS (iteration_structure.cpp:486-560).
  * A spline lookup outside the property tables throws std::out_of_range (MathTools::GetSpline,
  * Common/src/spline.cpp:62-77); any other failure throws std::runtime_error with rx_status_string.
  * Ownership: the solver owns one rx_ctx (device state); host arrays are copied at construction /
@@ -91,6 +96,17 @@ class ReactiveNSSolver {
     return rms;
   }
   void Synchronize() { check(rx_sync(ctx_), "rx_sync"); }
+  // CReactiveEulerSolver::SetPrimitive_Variables; returns the non-physical point count (syncs)
+  long long SetPrimitive_Variables(int ext_iter) {
+    int64_t n = 0;
+    const int rc = rx_set_primitive(ctx_, ext_iter, &n);
+    if (rc == RX_ERR_NONPHYS) throw std::runtime_error("Convergence not achieved for bisection method");
+    check(rc, "SetPrimitive_Variables");
+    return (long long)n;
+  }
+  // boundary markers, then Space_Integration's weak + strong BC loops
+  void SetBoundaryConditions(const rx_bc_desc& bc) { check(rx_bc_set(ctx_, &bc), "rx_bc_set"); }
+  void BC_Apply() { phase(rx_bc_flow(ctx_), "NaN found in the residual of a boundary condition"); }
 
   // ---- distributed (one rank per GPU): RCCL communicator or host-staged transport (rx.h)
   void CommInit(int nranks, int rank, const void* unique_id128) {
@@ -152,6 +168,7 @@ class TurbSSTSolver {
     return rms;
   }
   void Postprocessing() { check(rx_sst_postprocessing(ctx_), "Postprocessing"); }
+  void BC_Apply() { check(rx_bc_sst(ctx_), "BC_Apply"); }
 
  private:
   void check(int rc, const char* what) const {
@@ -160,6 +177,35 @@ class TurbSSTSolver {
   }
   rx_ctx* ctx_ = nullptr;
 };
+
+// One outer iteration in the reference's order (CMultiGridIntegration::MultiGrid_Iteration with MGLEVEL = 0,
+// integration_time.cpp:40-140, then CSingleGridIntegration::SingleGrid_Iteration :770-810 for the SST solver).
+// Returns the flow RMS; turb_rms gets the SST one.
+inline std::vector<double> Iterate(ReactiveNSSolver& flow, TurbSSTSolver& turb, int ext_iter,
+                                   std::vector<double>* turb_rms = nullptr) {
+  flow.SetPrimitive_Variables(ext_iter);
+  flow.SetPrimitive_Gradient_LS();
+  flow.SetStrainMag();
+  flow.SetTime_Step();
+  flow.Preprocessing();
+  flow.Upwind_Residual();
+  flow.Viscous_Residual();
+  flow.Source_Residual();
+  flow.BC_Apply();
+  std::vector<double> rms = flow.ImplicitEuler_Iteration();
+  flow.SetPrimitive_Variables(ext_iter);  // Preprocessing(Output = true) on the updated solution
+  flow.SetPrimitive_Gradient_LS();
+  flow.SetStrainMag();
+  turb.Preprocessing();
+  turb.Upwind_Residual();
+  turb.Viscous_Residual();
+  turb.Source_Residual();
+  turb.BC_Apply();
+  std::vector<double> trms = turb.ImplicitEuler_Iteration();
+  turb.Postprocessing();
+  if (turb_rms) *turb_rms = trms;
+  return rms;
+}
 
 }  // namespace rx
 

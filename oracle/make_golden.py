@@ -66,8 +66,8 @@ REF_DIMENSIONALIZATION= DIMENSIONAL
 REF_LENGTH= 0.125
 REF_AREA= 0
 MARKER_ISOTHERMAL = (upper_wall, 300.0, lower_wall_pre, 300.0, lower_wall_post, 600.0)
-INLET_TYPE = TEMPERATURE_IMPOSE
-MARKER_INLET= ( Oxidizer_Inlet, 300.0, 20.0, 1.0, 0.0, 0.0, Fuel_Inlet, 800.0, 0.87, 0.0, 1.0, 0.0)
+INLET_TYPE = {inlet_type}
+MARKER_INLET= ( Oxidizer_Inlet, {inlet_ox}, 1.0, 0.0, 0.0, Fuel_Inlet, {inlet_fuel}, 0.0, 1.0, 0.0)
 INLET_MASS_FRAC = (Oxidizer_Inlet, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0; Fuel_Inlet, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
 MARKER_OUTLET= ( Outlet, 101325.0)
 NUM_METHOD_GRAD= WEIGHTED_LEAST_SQUARES
@@ -116,7 +116,16 @@ def read_plot(path):
     return a[:, :2], a[:, 2:17]  # coords, 13 flow conservatives + k + omega
 
 
-def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS"):
+# INLET_TYPE variants: (a, b) of MARKER_INLET per inlet — TEMPERATURE_IMPOSE (T, |u|) as the shipped jet cfgs,
+# TOTAL_CONDITIONS (T_total, P_total), MASS_FLOW (rho, |u|)
+INLETS = {
+    "TEMPERATURE_IMPOSE": ("300.0, 20.0", "800.0, 0.87"),
+    "TOTAL_CONDITIONS": ("340.0, 195000.0", "900.0, 195000.0"),
+    "MASS_FLOW": ("2.37, 20.0", "1.49, 0.87"),
+}
+
+
+def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATURE_IMPOSE"):
     wd = os.path.join("/tmp/rx_golden", case)
     shutil.rmtree(wd, ignore_errors=True)
     os.makedirs(os.path.join(wd, "out"))
@@ -125,7 +134,8 @@ def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS"):
     os.symlink(os.path.join(CASE_DIR, "test_chem_second.txt"), os.path.join(wd, "test_chem_second.txt"))
     mesh_name = mesh_writer(wd)
     with open(os.path.join(wd, "case.cfg"), "w") as f:
-        f.write(CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec))
+        f.write(CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec, inlet_type=inlet,
+                                    inlet_ox=INLETS[inlet][0], inlet_fuel=INLETS[inlet][1]))
     return wd
 
 
@@ -219,11 +229,11 @@ GEOM_KEYS = ("coord", "volume", "global_index", "nbr_ptr", "nbr", "edges", "edge
              "wall_distance")
 
 
-def case_bc9():
-    """next-3 / a8: the reference's Space_Integration with its boundary conditions (inlets TEMPERATURE_IMPOSE,
-    outlet, isothermal walls; SST inlet / outlet / wall) on the mini9 jet, flow + SST, ILU0 cfg."""
+def case_bc9(inlet="TEMPERATURE_IMPOSE"):
+    """next-3 / a8: the reference's Space_Integration with its boundary conditions (inlets of the given
+    INLET_TYPE, outlet, isothermal walls; SST inlet / outlet / wall) on the mini9 jet, flow + SST, ILU0 cfg."""
     pts, quads, U, writer = mini9_inputs()
-    wd = make_workdir("bc9", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    wd = make_workdir("bc9_" + inlet, writer, cfl=5.0, order="1ST_ORDER", prec="ILU0", inlet=inlet)
     write_state(wd, U)
     a = run_harness(wd, bsr=False, extra=["--bc"])
     # keep the BSR rows of the boundary points only (the interior rows are the plain assembly)
@@ -234,6 +244,10 @@ def case_bc9():
     a["bc_blk"] = blk
     for k in ("bc_pre_bsr", "bc_bsr", "sst_bc_pre_bsr", "sst_bc_bsr"):
         a[k] = a[k][blk]
+    if inlet != "TEMPERATURE_IMPOSE":
+        # same mesh, state and interior loops as bc9: keep only what the inlet kind changes
+        return {k: a[k] for k in ("bc_res", "bc_bsr", "bc_charac", "bc_sol_old", "sst_bc_res", "sst_bc_bsr",
+                                  "sst_bc_sol", "bc_marker", "bc_params")}
     a.update(mech_arrays())
     return a
 
@@ -332,7 +346,8 @@ def main():
     gold = os.path.join(REPO, "tests", "golden")
     os.makedirs(gold, exist_ok=True)
     for case in args.cases.split(","):
-        a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9}[case]()
+        a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
+             "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW")}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

@@ -1,9 +1,10 @@
 // rx_driver.cpp — C++ host driver in the reference's CIntegration call order over include/rx_solver.hpp.
 // Test harness (tests/test_cpp_driver.py): reads a case directory of raw little-endian arrays
 // (<name>.f64 / <name>.i64 / <name>.i32), runs one explicit residual evaluation and one implicit
-// iteration, writes the results back as <name>.f64.
+// iteration (mode 0 / 1), or one whole reference outer iteration with the boundary conditions (mode 2,
+// rx::Iterate), writes the results back as <name>.f64.
 //
-//   rx_driver <case_dir> <implicit 0|1>
+//   rx_driver <case_dir> <mode 0|1|2>
 #include <cstdint>
 #include <cstdio>
 #include <fstream>
@@ -105,6 +106,74 @@ int main(int argc, char** argv) {
     cfg.t_min = 200.0;   // TEMPERATURE_MIN / MAX
     cfg.t_max = 6000.0;
     cfg.p_ref = cfg.visc_ref = cfg.cond_ref = cfg.vel_ref = cfg.len_ref = 1.0;  // DIMENSIONAL
+
+    if (implicit == 2) {
+      // CMeanFlowIteration::Iterate from the reference's records (cfg_it: mach, Pr_lam, Pr_t, Le_t, C_mu, PaSR_LB,
+      // CFL, max dt, lin tol, lin iter, relax flow, T_min, T_max, relax turb, CFL reduction turb)
+      auto ci = f64(d, "cfg_it");
+      cfg.mach_inf = ci[0];
+      cfg.prandtl_lam = ci[1];
+      cfg.prandtl_turb = ci[2];
+      cfg.lewis_turb = ci[3];
+      cfg.c_mu = ci[4];
+      cfg.pasr_lb = ci[5];
+      cfg.cfl = ci[6];
+      cfg.max_delta_time = ci[7];
+      cfg.lin_tol = ci[8];
+      cfg.lin_iter = (int32_t)ci[9];
+      cfg.relaxation = ci[10];
+      cfg.t_min = ci[11];
+      cfg.t_max = ci[12];
+      cfg.implicit = 1;
+      rx::ReactiveNSSolver flow(mesh, mech, cfg, 0);
+      auto pn = i64(d, "bvertex_pn");
+      auto kind = i32(d, "bc_kind");
+      auto bdata = f64(d, "bc_data"), bsc = f64(d, "bc_scalars");
+      rx_bc_desc bc{};
+      bc.n_marker = (int32_t)kind.size();
+      bc.kind = kind.data();
+      bc.data = bdata.data();
+      bc.normal_neighbor = pn.data();
+      bc.inlet_kind = (int32_t)bsc[0];
+      bc.tke_inf = bsc[1];
+      bc.kine_inf = bsc[2];
+      bc.omega_inf = bsc[3];
+      flow.SetBoundaryConditions(bc);
+      rx_cfg tcfg = cfg;
+      tcfg.relaxation = ci[13];
+      tcfg.cfl = ci[14];
+      rx::TurbSSTSolver turb(mesh, flow, tcfg);
+      auto T = f64(d, "it_sst0");
+      std::vector<double> k(T.size() / 2), w(T.size() / 2), gk(T.size());
+      auto tg = f64(d, "it_sstgrad0");
+      for (size_t i = 0; i < k.size(); ++i) {
+        k[i] = T[2 * i];
+        w[i] = T[2 * i + 1];
+        gk[2 * i] = tg[4 * i];
+        gk[2 * i + 1] = tg[4 * i + 1];
+      }
+      flow.Upload(RX_F_V, f64(d, "it_V0"));
+      flow.Upload(RX_F_U, f64(d, "it_U0"));
+      flow.Upload(RX_F_TKE, k);
+      flow.Upload(RX_F_OMEGA, w);
+      flow.Upload(RX_F_MUT, f64(d, "it_mut0"));
+      flow.Upload(RX_F_SIGMAK, std::vector<double>(k.size(), 0.85));
+      flow.Upload(RX_F_GRADK, gk);
+      turb.Upload(RX_F_U, T);
+      turb.Upload(RX_F_WALLDIST, f64(d, "wall_distance"));
+      turb.Upload(RX_F_F1, f64(d, "it_F1_0"));
+      turb.Upload(RX_F_F2, f64(d, "it_F2_0"));
+      turb.Upload(RX_F_CDKW, f64(d, "it_CDkw0"));
+      std::vector<double> trms;
+      auto rms = rx::Iterate(flow, turb, 0, &trms);
+      flow.Synchronize();
+      save(d, "out_u", flow.Download(RX_F_U));
+      save(d, "out_sst_u", turb.Download(RX_F_U));
+      save(d, "out_rms", rms);
+      save(d, "out_sst_rms", trms);
+      std::printf("ok iterate\n");
+      return 0;
+    }
 
     rx::ReactiveNSSolver solver(mesh, mech, cfg, 0);
     const struct {

@@ -78,3 +78,46 @@ def test_cpp_driver_matches_reference(tmp_path, implicit):
             assert_close(T[:, v], g["sst_new_sol_ilu"][:, v], what=f"C++ driver SST (k, omega)[{v}]")
         assert_close(np.fromfile(os.path.join(d, "out_sst_rms.f64")), g["sst_rms_ilu"], what="C++ driver SST RMS")
         assert_close(np.fromfile(os.path.join(d, "out_sst_mut.f64")), g["sst_post_mut_ilu"], what="C++ driver mu_t")
+
+
+@pytest.mark.gpu
+def test_cpp_driver_reference_iteration(tmp_path):
+    """rx::Iterate (the reference's outer iteration with the jet's boundary conditions) from the C++ mirror, against
+    the reference's own iteration (golden it9)."""
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "it9.npz")))
+    d = str(tmp_path)
+
+    def w(name, arr, dt):
+        np.ascontiguousarray(arr, dtype=dt).tofile(os.path.join(d, name + {np.float64: ".f64", np.int64: ".i64",
+                                                                             np.int32: ".i32"}[dt]))
+    for k in ("edges", "nbr_ptr", "nbr", "bvertex_pn"):
+        w(k, g[k], np.int64)
+    w("bvertex", np.asarray(g["bvertex"])[:, :2], np.int64)
+    for k in ("edge_normal", "coord", "volume", "bvertex_normal", "wall_distance", "it_U0", "it_V0", "it_sst0",
+              "it_mut0", "it_F1_0", "it_F2_0", "it_CDkw0", "it_sstgrad0"):
+        w(k, g[k], np.float64)
+    for k in ("mmass", "diff_vol", "stoich_reac", "stoich_prod", "exp_reac", "exp_prod", "A", "beta", "Ta", "A_back",
+              "beta_back", "Ta_back", "tab_x", "tab_y", "tab_y2"):
+        w("mech_" + k, g["mech_" + k], np.float64)
+    for k in ("reversible", "has_backward"):
+        w("mech_" + k, g["mech_" + k], np.int32)
+    w("cfg", [0.0] * 6, np.float64)
+    bp, p2v = g["bc_params"], g["p2v_params"]
+    w("cfg_it", [g["mach_inf"][0], g["visc_params"][0], g["visc_params"][1], g["visc_params"][2], g["src_params"][0],
+                 g["src_params"][1], g["dt_params"][0], g["dt_params"][1], bp[19], bp[20], bp[22], p2v[1], p2v[2],
+                 bp[23], bp[24]], np.float64)
+    bc = rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"])
+    w("bc_kind", bc["kind"], np.int32)
+    w("bc_data", bc["data"], np.float64)
+    w("bc_scalars", [bc["inlet_kind"], bc["tke_inf"], bc["kine_inf"], bc["omega_inf"]], np.float64)
+    exe = os.path.join(d, "rx_driver")
+    build_driver(exe)
+    r = subprocess.run([exe, d, "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    N, nVar = g["it_U0"].shape
+    U = np.fromfile(os.path.join(d, "out_u.f64")).reshape(N, nVar)
+    T = np.fromfile(os.path.join(d, "out_sst_u.f64")).reshape(N, 2)
+    from tests.parity import per_column_close
+    per_column_close(U, g["it1_U"], floor=1e-3, what="C++ Iterate U")
+    per_column_close(T, g["it1_sst"], floor=1e-3, what="C++ Iterate (k, omega)")
+    assert_close(np.fromfile(os.path.join(d, "out_rms.f64")), g["it1_rms"], what="C++ Iterate RMS")

@@ -50,9 +50,17 @@ def rows(g, A, nb):
     return A.reshape(-1, nb, nb)[g["bc_blk"]]
 
 
-@pytest.mark.parametrize("implicit", [1, 0])
-def test_flow_bc_vs_reference(implicit):
+def bc_case(name):
     g = golden("bc9")
+    if name != "bc9":
+        g.update(golden(name))
+    return g
+
+
+@pytest.mark.parametrize("case", ["bc9", "bc9t", "bc9m"])
+@pytest.mark.parametrize("implicit", [1, 0])
+def test_flow_bc_vs_reference(implicit, case):
+    g = bc_case(case)
     nVar = int(g["dims"][1])
     N = len(g["V"])
     s, t = solvers(g, implicit)
@@ -83,8 +91,9 @@ def test_flow_bc_vs_reference(implicit):
     s.close()
 
 
-def test_sst_bc_vs_reference():
-    g = golden("bc9")
+@pytest.mark.parametrize("case", ["bc9", "bc9t", "bc9m"])
+def test_sst_bc_vs_reference(case):
+    g = bc_case(case)
     N = len(g["V"])
     s, t = solvers(g, 1)
     s.set_state(g)
