@@ -54,21 +54,106 @@ def jet_mesh(nx: int, ny: int, **kw):
     return pts, quads, bnd
 
 
+# 3-D extrusion (config C5): the 2-D markers become side walls / inlets / outlet of the slab, the two z planes are
+# symmetry planes (MARKER_SYM; the reactive solvers leave them to CSolver::BC_Sym_Plane, a no-op)
+MARKERS3 = MARKERS + ("sym_back", "sym_front")
+# CHexahedron::Faces (Common/src/primal_grid_structure.cpp:395), CQuadrilateral::Neighbor_Nodes (:260)
+HEX_FACES = np.array([[0, 1, 5, 4], [1, 2, 6, 5], [2, 3, 7, 6], [3, 0, 4, 7], [0, 3, 2, 1], [4, 5, 6, 7]])
+QUAD_NEIGHBORS = np.array([[1, 3], [2, 0], [3, 1], [0, 2]])
+
+
+def jet_mesh3d(nx: int, ny: int, nz: int, depth=0.003, **kw):
+    """The 2-D jet extruded over nz planes in z: points (plane-major), VTK-ordered hexahedra and boundary quads per
+    marker, ordered counter-clockwise seen from the interior (the orientation CPhysicalGeometry::
+    Check_BoundElem_Orientation, geometry_structure.cpp:8825-8960, leaves unflipped)."""
+    p2, q2, b2 = jet_mesh(nx, ny, **kw)
+    n2 = len(p2)
+    z = np.linspace(0.0, depth, nz)
+    pts = np.concatenate([np.c_[p2, np.full(n2, zk)] for zk in z])
+    hexes = np.concatenate([np.c_[q2 + k * n2, q2 + (k + 1) * n2] for k in range(nz - 1)]).astype(np.int64)
+    bnd = {}
+    for name in MARKERS:
+        l = np.asarray(b2[name], dtype=np.int64)
+        bnd[name] = np.concatenate([np.c_[l[:, 0] + k * n2, l[:, 0] + (k + 1) * n2, l[:, 1] + (k + 1) * n2,
+                                          l[:, 1] + k * n2] for k in range(nz - 1)])
+    bnd["sym_back"] = q2.astype(np.int64)
+    bnd["sym_front"] = q2[:, ::-1].astype(np.int64) + (nz - 1) * n2
+    return pts, hexes, bnd
+
+
+def median_dual3d(pts, hexes, bnd):
+    """3-D median dual of a hexahedral mesh, vectorised restatement of CPhysicalGeometry::SetControlVolume
+    (geometry_structure.cpp:10457-10560, 3-D branch): for every face edge (i, j) of every element the triangle
+    (edge midpoint, face centroid, element centroid) adds 1/2 (E - e) x (F - e) to the edge normal, negated when
+    i > j (CEdge::SetNodes_Coord, dual_grid_structure.cpp:479-505), and the tetrahedra (point, e, F, E) add to
+    both dual volumes (CEdge::GetVolume :425-453). Boundary vertex normals: CPhysicalGeometry::SetBoundControlVolume
+    (:9595-9660, 3-D branch) with CVertex::SetNodes_Coord (dual_grid_structure.cpp:589-616). Sums are taken in
+    numpy order (the reference's element order gives the same values up to rounding)."""
+    n = len(pts)
+    ecg = pts[hexes].mean(axis=1)                                     # (nE, 3)
+    fnodes = hexes[:, HEX_FACES]                                      # (nE, 6, 4)
+    fcg = pts[fnodes].mean(axis=2)                                    # (nE, 6, 3)
+    fi = fnodes.reshape(-1, 4)
+    fj = np.roll(fnodes, -1, axis=2).reshape(-1, 4)
+    fi, fj = fi.ravel(), fj.ravel()                                   # (nE*24,)
+    F = np.repeat(fcg.reshape(-1, 3), 4, axis=0)
+    E = np.repeat(ecg, 24, axis=0)
+    lo, hi = np.minimum(fi, fj), np.maximum(fi, fj)
+    ukey, inv = np.unique(lo * n + hi, return_inverse=True)
+    edges = np.stack([ukey // n, ukey % n], axis=1).astype(np.int64)
+    emid = 0.5 * (pts[edges[:, 0]] + pts[edges[:, 1]])
+    e = emid[inv]
+    contrib = 0.5 * np.cross(E - e, F - e)
+    contrib[fi > fj] *= -1.0
+    normal = np.zeros((len(edges), 3))
+    np.add.at(normal, inv, contrib)
+    vol = np.zeros(n)
+    for P_ in (fi, fj):
+        P = pts[P_]
+        np.add.at(vol, P_, np.abs(np.einsum("ij,ij->i", E - P, np.cross(e - P, F - P))) / 6.0)
+    nb_i = np.r_[edges[:, 0], edges[:, 1]]
+    nb_j = np.r_[edges[:, 1], edges[:, 0]]
+    order = np.lexsort((nb_j, nb_i))
+    nb_i, nb_j = nb_i[order], nb_j[order]
+    nbr_ptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(nbr_ptr, nb_i + 1, 1)
+    nbr_ptr = np.cumsum(nbr_ptr)
+    bv, bn = [], []
+    for m, name in enumerate(bnd.keys()):
+        q = np.asarray(bnd[name], dtype=np.int64)
+        C = pts[q].mean(axis=1)
+        acc = np.zeros((n, 3))
+        for k in range(4):
+            V = pts[q[:, k]]
+            e0 = 0.5 * (V + pts[q[:, QUAD_NEIGHBORS[k, 0]]])
+            e1 = 0.5 * (V + pts[q[:, QUAD_NEIGHBORS[k, 1]]])
+            np.add.at(acc, q[:, k], 0.5 * np.cross(V - C, e0 - C) + 0.5 * np.cross(V - e1, C - e1))
+        verts = np.unique(q)
+        bv.append(np.c_[np.full(len(verts), m), verts])
+        bn.append(acc[verts])
+    return dict(edges=edges, edge_normal=normal, volume=vol, nbr_ptr=nbr_ptr, nbr=nb_j.astype(np.int64),
+                bvertex=np.concatenate(bv).astype(np.int64), bvertex_normal=np.concatenate(bn))
+
+
 def write_su2(path: str, pts, quads, bnd):
+    """SU2 native mesh file: quads (VTK 9) + boundary lines (VTK 3) in 2-D, hexahedra (VTK 12) + boundary quads
+    (VTK 9) in 3-D; markers in the order of `bnd`."""
+    nd = pts.shape[1]
+    elem_t, bnd_t = (9, 3) if nd == 2 else (12, 9)
     with open(path, "w") as f:
-        f.write("NDIME= 2\n")
+        f.write(f"NDIME= {nd}\n")
         f.write(f"NELEM= {len(quads)}\n")
         for k, q in enumerate(quads):
-            f.write(f"9 {q[0]} {q[1]} {q[2]} {q[3]} {k}\n")
+            f.write(f"{elem_t} " + " ".join(str(int(v)) for v in q) + f" {k}\n")
         f.write(f"NPOIN= {len(pts)}\n")
         for k, p in enumerate(pts):
-            f.write(f"{p[0]:.17g} {p[1]:.17g} {k}\n")
+            f.write(" ".join(f"{c:.17g}" for c in p) + f" {k}\n")
         f.write(f"NMARK= {len(bnd)}\n")
-        for name in MARKERS:
+        for name in (MARKERS if nd == 2 else bnd.keys()):
             lines = bnd[name]
             f.write(f"MARKER_TAG= {name}\nMARKER_ELEMS= {len(lines)}\n")
             for l in lines:
-                f.write(f"3 {l[0]} {l[1]}\n")
+                f.write(f"{bnd_t} " + " ".join(str(int(v)) for v in l) + "\n")
 
 
 def rcm_order(n, edges):
@@ -80,7 +165,7 @@ def rcm_order(n, edges):
     return np.asarray(reverse_cuthill_mckee(A, symmetric_mode=True), dtype=np.int64)
 
 
-def median_dual(pts, quads, bnd):
+def median_dual2d(pts, quads, bnd):
     """Edges (i<j), edge normals, dual volumes, neighbour CSR and boundary vertices.
 
     Vectorised restatement of the reference 2-D dual construction (see module docstring).
@@ -136,6 +221,11 @@ def median_dual(pts, quads, bnd):
                 bvertex=bv, bvertex_normal=bn)
 
 
+def median_dual(pts, elems, bnd):
+    """Median dual of a 2-D quad or 3-D hexahedral mesh."""
+    return median_dual3d(pts, elems, bnd) if pts.shape[1] == 3 else median_dual2d(pts, elems, bnd)
+
+
 def renumber(pts, quads, bnd, perm):
     """Apply a new->old permutation to points and connectivity."""
     old2new = np.empty_like(perm)
@@ -185,12 +275,13 @@ def partition_order(n, edges, part):
     return np.concatenate(perm), np.asarray(ptr, dtype=np.int64)
 
 
-def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, **kw):
-    """Synthetic jet mesh ready for the solver: RCM-ordered points + median dual.
+def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, nz: int = 0, **kw):
+    """Synthetic jet mesh ready for the solver: RCM-ordered points + median dual (nz > 1: the 3-D extrusion).
 
     n_part > 1: points are split into n_part RCB parts (the reference's MPI ranks), numbered part by
     part with a local RCM; `part_ptr` gives the row range of every part."""
-    pts, quads, bnd = jet_mesh(nx, ny, **kw)
+    pts, quads, bnd = jet_mesh3d(nx, ny, nz, **kw) if nz > 1 else jet_mesh(nx, ny, **kw)
+    median_dual = median_dual3d if nz > 1 else median_dual2d
     part_ptr = np.array([0, len(pts)], dtype=np.int64)
     if n_part > 1:
         d0 = median_dual(pts, quads, bnd)

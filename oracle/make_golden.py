@@ -70,7 +70,7 @@ INLET_TYPE = {inlet_type}
 MARKER_INLET= ( Oxidizer_Inlet, {inlet_ox}, 1.0, 0.0, 0.0, Fuel_Inlet, {inlet_fuel}, 0.0, 1.0, 0.0)
 INLET_MASS_FRAC = (Oxidizer_Inlet, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0; Fuel_Inlet, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
 MARKER_OUTLET= ( Outlet, 101325.0)
-NUM_METHOD_GRAD= WEIGHTED_LEAST_SQUARES
+{extra}NUM_METHOD_GRAD= WEIGHTED_LEAST_SQUARES
 CFL_NUMBER= {cfl}
 CFL_ADAPT= NO
 EXT_ITER= 1
@@ -125,7 +125,7 @@ INLETS = {
 }
 
 
-def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATURE_IMPOSE"):
+def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATURE_IMPOSE", extra=""):
     wd = os.path.join("/tmp/rx_golden", case)
     shutil.rmtree(wd, ignore_errors=True)
     os.makedirs(os.path.join(wd, "out"))
@@ -135,7 +135,7 @@ def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATUR
     mesh_name = mesh_writer(wd)
     with open(os.path.join(wd, "case.cfg"), "w") as f:
         f.write(CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec, inlet_type=inlet,
-                                    inlet_ox=INLETS[inlet][0], inlet_fuel=INLETS[inlet][1]))
+                                    inlet_ox=INLETS[inlet][0], inlet_fuel=INLETS[inlet][1], extra=extra))
     return wd
 
 
@@ -263,6 +263,92 @@ def case_it9():
     return a
 
 
+# 3-D (config C5's extruded jet): 13 x 7 x 4 points, z planes as symmetry planes
+MINI3D = (13, 7, 4)
+SYM3D = "MARKER_SYM= ( sym_back, sym_front )\n"
+
+
+def mini3d_inputs():
+    """The extruded jet and a 3-D state: the converged 2-D field sampled at (x, y), plus a spanwise velocity
+    w = 0.8 sin(pi z / depth) sin(pi x / L) m/s (zero on the symmetry planes) so that every third-component term of
+    the operators is exercised; rho E gains the matching kinetic energy (T unchanged)."""
+    nx, ny, nz = MINI3D
+    pts, hexes, bnd = meshgen.jet_mesh3d(nx, ny, nz)
+    xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    from scipy.spatial import cKDTree
+    scale = np.array([1.0 / 0.125, 1.0 / 0.006])
+    _, idx = cKDTree(xy * scale).query(pts[:, :2] * scale)
+    c2 = cons[idx]  # [rho, rho u, rho v, rho E, rho Y x9, k, omega]
+    depth = pts[:, 2].max()
+    w = 0.8 * np.sin(np.pi * pts[:, 2] / depth) * np.sin(np.pi * pts[:, 0] / 0.125)
+    rho = c2[:, 0]
+    U = np.c_[c2[:, :3], rho * w, c2[:, 3] + 0.5 * rho * w * w, c2[:, 4:]]
+
+    def writer(wd):
+        meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, hexes, bnd)
+        return "mesh.su2"
+
+    return pts, hexes, U, writer
+
+
+def case_mini3d():
+    """mini9's dumps on the 3-D extruded jet (every operator, whole loops, BSR, LU-SGS / ILU0 / FGMRES, SST)."""
+    pts, hexes, U, writer = mini3d_inputs()
+    wd = make_workdir("mini3d", writer, cfl=5.0, order="1ST_ORDER", extra=SYM3D)
+    write_state(wd, U)
+    a = run_harness(wd, bsr=True)
+    wd = make_workdir("mini3d_ilu", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0", extra=SYM3D)
+    write_state(wd, U)
+    b = run_harness(wd, bsr=True)
+    for k in ("ilu_factor", "ilu_rhs", "fgmres_ilu_x", "fgmres_ilu_info"):
+        a[k] = b[k]
+    assert np.array_equal(a["sst_bsr_system"], b["sst_bsr_system"])
+    for k in ("sst_lin_sol", "sst_new_sol", "sst_rms", "sst_post_mut", "sst_post_F1", "sst_post_F2",
+              "sst_post_CDkw", "sst_post_grad"):
+        a[k + "_ilu"] = b[k]
+    assert np.array_equal(a["bsr_system"], b["bsr_system"])
+    del a["bsr_jac_residual"]
+    rng = np.random.default_rng(7)
+    js = np.sort(rng.choice(len(a["edges"]), size=96, replace=False))
+    a["jac_edge_sample"] = js
+    for k in ("conv_jac_i", "conv_jac_j", "visc_jac_i", "visc_jac_j"):
+        a[k] = a[k][js]
+    ns = rng.choice(len(a["coord"]), size=64, replace=False)
+    a["src_jac_sample"] = np.sort(ns)
+    a["src_jac"] = a["src_jac"][a["src_jac_sample"]]
+    a.update(mech_arrays())
+    a["gen_points"] = pts
+    a["gen_quads"] = hexes
+    return a
+
+
+def case_bc3d():
+    """case_bc9 on the 3-D extruded jet (symmetry planes: no-op markers)."""
+    pts, hexes, U, writer = mini3d_inputs()
+    wd = make_workdir("bc3d", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0", extra=SYM3D)
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--bc"])
+    rp = a["bsr_row_ptr"]
+    rows = np.unique(a["bvertex"][:, 1])
+    blk = np.concatenate([np.arange(rp[i], rp[i + 1]) for i in rows])
+    a["bc_rows"] = rows
+    a["bc_blk"] = blk
+    for k in ("bc_pre_bsr", "bc_bsr", "sst_bc_pre_bsr", "sst_bc_bsr"):
+        a[k] = a[k][blk]
+    a.update(mech_arrays())
+    return a
+
+
+def case_it3d():
+    """Whole reference outer iterations on the 3-D extruded jet: 2 iterations, ILU0."""
+    pts, hexes, U, writer = mini3d_inputs()
+    wd = make_workdir("it3d", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0", extra=SYM3D)
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--iters", "2"])
+    a.update(mech_arrays())
+    return a
+
+
 def case_jet9w():
     def writer(wd):
         os.symlink(os.path.join(CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
@@ -347,7 +433,8 @@ def main():
     os.makedirs(gold, exist_ok=True)
     for case in args.cases.split(","):
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
-             "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW")}[case]()
+             "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
+             "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

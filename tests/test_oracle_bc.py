@@ -5,6 +5,9 @@ bc9: one Space_Integration of the reference (integration_structure.cpp:72-193) o
 then the weak BCs (BC_Inlet TEMPERATURE_IMPOSE, BC_Outlet with the boundary viscous numerics
 CAvgGradReactive_Boundary) and the strong BC_Isothermal_Wall, for the flow and the SST solver.
 it9: three whole reference outer iterations (CMeanFlowIteration::Iterate) from the mini9 state.
+bc3d / it3d: the same on the 3-D extruded jet (symmetry planes in z: CSolver::BC_Sym_Plane is a no-op for the
+reactive solvers, solver_structure.inl:731-732, and CTurbSolver::BC_Sym_Plane, solver_direct_turbulent.cpp:602-606),
+two iterations.
 """
 import os
 
@@ -23,20 +26,26 @@ def golden(case):
 def bc_case(name):
     """bc9 (INLET_TYPE = TEMPERATURE_IMPOSE, the shipped jet cfgs), bc9t (TOTAL_CONDITIONS), bc9m (MASS_FLOW): the
     variants hold only the outputs their inlet kind changes, over bc9's mesh and state."""
+    if name == "bc3d":
+        return golden(name)
     g = golden("bc9")
     if name != "bc9":
         g.update(golden(name))
     return g
 
 
-@pytest.fixture(scope="module", params=["bc9", "bc9t", "bc9m"])
+@pytest.fixture(scope="module", params=["bc9", "bc9t", "bc9m", "bc3d"])
 def bc9(request):
     return bc_case(request.param)
 
 
-@pytest.fixture(scope="module")
-def it9():
-    return golden("it9")
+@pytest.fixture(scope="module", params=["it9", "it3d"])
+def it9(request):
+    return golden(request.param)
+
+
+def n_iters(g):
+    return sum(1 for k in g if k.startswith("it") and k.endswith("_U") and k[2:-2].isdigit())
 
 
 def _bc_setup(g):
@@ -55,6 +64,8 @@ def test_flow_bc_vs_reference(bc9):
     A[g["bc_blk"]] = g["bc_pre_bsr"]
     Uold = g["U"].copy()
     ch = O.bc_flow(m, nDim, g, g["bc_marker"], prm, g, rp, col, R, A, Uold, True, True)
+    if nDim == 3:  # the symmetry planes are markers with no action
+        assert int(g["bc_params"][26]) in g["bc_marker"][:, 0]
     # ghost states (CharacPrimVar), Jacobian rows, Solution_Old (SetVelocity_Old at the walls): bitwise
     assert np.array_equal(ch, g["bc_charac"])
     assert np.array_equal(A[g["bc_blk"]], g["bc_bsr"])
@@ -100,25 +111,31 @@ def colrel(a, ref):
 
 # chained iterations: last-bit differences of the Stefan-Maxwell solve grow through FGMRES
 ITER_TOL = {1: 1e-13, 2: 1e-11, 3: 1e-9}
+# 3-D: the small spanwise / wall-normal momentum columns carry the FGMRES-amplified rounding of the large ones.
+# Chained, the second 3-D iteration already crosses the Ds discontinuity of the viscous Jacobian (DESIGN.md §2:
+# an energy-row species entry moves by 8e-7 relative for a 4e-12 state difference), so only the first is chained;
+# every iteration is checked from the reference's own state in test_each_iteration_from_reference_state.
+ITER_TOL3 = {1: 1e-11}
 
 
 def test_each_iteration_from_reference_state(it9):
     """Every iteration restarted from the reference's own records after the previous one."""
     g = it9
+    nDim = int(g["dims"][0])
     m = O.Mechanism(g)
     cfg, bc, s0 = iteration_cfg(g)
     pat = (g["bsr_row_ptr"], g["bsr_col"])
-    for k in range(3):
+    for k in range(n_iters(g)):
         if k == 0:
             s = s0
         else:
             p = f"it{k}_"
             s = dict(U=g[p + "U"], V=g[p + "V"], Uold=g[p + "Uold"], T=g[p + "sst"], TG=g[p + "sstgrad"], F1=g[p + "F1"],
                      F2=g[p + "F2"], CDkw=g[p + "CDkw"], mut=g[p + "mut"])
-        s = O.outer_iteration(m, 2, g, s, bc, cfg, k, pat)
+        s = O.outer_iteration(m, nDim, g, s, bc, cfg, k, pat)
         p = f"it{k + 1}_"
         for key, ref in (("U", "U"), ("V", "V"), ("T", "sst")):
-            assert colrel(s[key], g[p + ref]) < 1e-12, (k, key)
+            assert colrel(s[key], g[p + ref]) < (1e-12 if nDim == 2 else 1e-10), (k, key)
         np.testing.assert_allclose(s["rms"], g[p + "rms"], rtol=1e-12)
 
 
@@ -128,9 +145,9 @@ def test_outer_iterations_vs_reference(it9):
     m = O.Mechanism(g)
     cfg, bc, s = iteration_cfg(g)
     pat = (g["bsr_row_ptr"], g["bsr_col"])
-    for k in range(3):
+    for k in range(n_iters(g) if nDim == 2 else len(ITER_TOL3)):
         s = O.outer_iteration(m, nDim, g, s, bc, cfg, k, pat)
-        p, tol = f"it{k + 1}_", ITER_TOL[k + 1]
+        p, tol = f"it{k + 1}_", (ITER_TOL if nDim == 2 else ITER_TOL3)[k + 1]
         assert colrel(s["U"], g[p + "U"]) < tol, k
         assert colrel(s["V"], g[p + "V"]) < tol, k
         assert colrel(s["T"], g[p + "sst"]) < tol, k

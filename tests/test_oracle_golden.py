@@ -4,6 +4,7 @@ reference (oracle/make_golden.py). CPU only.
 Fixtures:
   mini9.npz  21x11 synthetic jet, 9 species, SST, implicit: every operator + whole loops + BSR.
   jet9w.npz  window of the reference's own 9000-point jet mesh around the flame, PaSR state.
+  mini3d.npz the 3-D extruded jet (13x7x4 points, symmetry planes in z, spanwise velocity), mini9's dumps.
 """
 import os
 
@@ -14,7 +15,7 @@ from oracle import oracle as O
 from tests.parity import assert_close
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-CASES = ["mini9", "jet9w"]
+CASES = ["mini9", "jet9w", "mini3d"]
 
 
 def load(case):
@@ -88,8 +89,9 @@ def test_limiter_venkat():
     assert_close(L[it], g["limiter_out"][it], what="Venkatakrishnan limiter")
 
 
-def test_loops_and_time_step():
-    g, (nDim, nVar, nPV, nG, ns, imp, rans) = load("mini9")
+@pytest.mark.parametrize("name", ["mini9", "mini3d"])
+def test_loops_and_time_step(name):
+    g, (nDim, nVar, nPV, nG, ns, imp, rans) = load(name)
     N = len(g["V"])
     R = np.zeros((N, nVar))
     for e, (i, j) in enumerate(g["edges"]):
@@ -109,8 +111,9 @@ def test_loops_and_time_step():
     assert_close(lv, g["lambda_visc"], what="viscous spectral radius")
 
 
-def test_block_sparse_linear_algebra():
-    g, _ = load("mini9")
+@pytest.mark.parametrize("name", ["mini9", "mini3d"])
+def test_block_sparse_linear_algebra(name):
+    g, _ = load(name)
     rp, col, A, b = g["bsr_row_ptr"], g["bsr_col"], g["bsr_system"], g["sys_rhs"]
     assert_close(O.bsr_spmv(rp, col, A, b), g["spmv_rhs"], what="BSR SpMV")
     assert_close(O.lusgs(rp, col, A, b), g["lusgs_rhs"], what="LU-SGS apply")
@@ -125,12 +128,15 @@ def test_block_sparse_linear_algebra():
     assert_close(x, g["fgmres_ilu_x"], what="FGMRES(ILU0)")
 
 
-def test_meshgen_dual_matches_reference_geometry():
-    """Our median-dual builder reproduces the reference's edges, normals, dual volumes and boundary
-    normals on the same quads (mini9 was meshed by the reference from meshgen's SU2 file)."""
+@pytest.mark.parametrize("name", ["mini9", "mini3d"])
+def test_meshgen_dual_matches_reference_geometry(name):
+    """Our median-dual builder reproduces the reference's edges, normals, dual volumes, boundary
+    normals and wall distances on the same elements (mini9 / mini3d were meshed by the reference from
+    meshgen's SU2 file)."""
     from tests.rxpkg import meshgen
-    g, _ = load("mini9")
-    pts, quads, bnd = meshgen.jet_mesh(21, 11)
+    g, _ = load(name)
+    pts, quads, bnd = meshgen.jet_mesh(21, 11) if name == "mini9" else meshgen.jet_mesh3d(13, 7, 4)
+    nd = pts.shape[1]
     d = meshgen.median_dual(pts, quads, bnd)
     gi = g["global_index"]
     re = gi[g["edges"]]
@@ -145,11 +151,14 @@ def test_meshgen_dual_matches_reference_geometry():
     vol = np.zeros(len(pts))
     vol[gi] = g["volume"]
     assert np.max(np.abs(vol - d["volume"])) <= 1e-15 * vol.max()
-    bn = np.zeros((len(pts), 2))
+    bn = np.zeros((len(pts), nd))
     np.add.at(bn, gi[g["bvertex"][:, 1]], g["bvertex_normal"])
-    mn = np.zeros((len(pts), 2))
+    mn = np.zeros((len(pts), nd))
     np.add.at(mn, d["bvertex"][:, 1], d["bvertex_normal"])
     assert np.max(np.abs(bn - mn)) <= 1e-15
+    wd = np.zeros(len(pts))
+    wd[gi] = g["wall_distance"]
+    assert np.array_equal(wd, meshgen.wall_distance(pts, bnd))
 
 
 def test_partitioned_ilu_is_block_jacobi():

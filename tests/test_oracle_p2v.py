@@ -13,11 +13,11 @@ KEYS = (("V", "p2v_V"), ("dPdU", "p2v_dPdU"), ("dTdU", "p2v_dTdU"), ("mu", "p2v_
         ("Dij", "p2v_Dij"), ("eddy", "p2v_eddy"), ("cp", "p2v_cp"), ("U", "p2v_U_after"))
 
 
-@pytest.mark.parametrize("case", ["mini9", "jet9w"])
+@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d"])
 def test_set_primitive_bitwise(case):
     g = dict(np.load(os.path.join(GOLD, case + ".npz")))
     m = O.Mechanism(g)
-    o = O.set_primitive(m, 2, g["p2v_U"], g["p2v_V_before"], g["p2v_tke"], g["p2v_mut"], O.p2v_params(g))
+    o = O.set_primitive(m, int(g["dims"][0]), g["p2v_U"], g["p2v_V_before"], g["p2v_tke"], g["p2v_mut"], O.p2v_params(g))
     assert o["nonphys"] == int(g["p2v_params"][0])
     for k, gk in KEYS:
         assert np.array_equal(o[k], g[gk]), k

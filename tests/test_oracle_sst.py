@@ -17,7 +17,7 @@ def load(case):
     return g, [int(x) for x in g["dims"]]
 
 
-@pytest.fixture(scope="module", params=["mini9", "jet9w"])
+@pytest.fixture(scope="module", params=["mini9", "jet9w", "mini3d"])
 def case(request):
     g, dims = load(request.param)
     return request.param, g, dims
@@ -50,8 +50,9 @@ def test_sst_source(case):
     assert np.array_equal(r, g["sst_src_res"]) and np.array_equal(J, g["sst_src_jac"])
 
 
-def test_sst_gradient_and_blending():
-    g, (nDim, *_r) = load("mini9")
+@pytest.mark.parametrize("name", ["mini9", "mini3d"])
+def test_sst_gradient_and_blending(name):
+    g, (nDim, *_r) = load(name)
     TG = O.sol_grad_ls(nDim, g["coord"], g["sst_sol"], g["nbr_ptr"], g["nbr"])
     assert np.array_equal(TG, g["sst_grad_ls"])
     assert np.array_equal(TG, g["sst_grad"])
@@ -61,10 +62,11 @@ def test_sst_gradient_and_blending():
         assert np.array_equal(a, g[k]), k
 
 
+@pytest.mark.parametrize("name", ["mini9", "mini3d"])
 @pytest.mark.parametrize("prec", ["lusgs", "ilu"])
-def test_sst_implicit_step(prec):
+def test_sst_implicit_step(prec, name):
     """Loops, system and the whole turbulent implicit step + Postprocessing against the reference."""
-    g, (nDim, *_r) = load("mini9")
+    g, (nDim, *_r) = load(name)
     mesh = {k: g[k] for k in ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr", "wall_distance")}
     flow = dict(V=g["V"], grad=g["grad_prim"], mu=g["mu"], eddy=g["eddy_visc_flow"], strain=g["strain_mag"])
     cfg = dict(lin_tol=1e-6, lin_iter=5)
