@@ -259,7 +259,7 @@ def default_cfg(**kw):
 
 def mesh_desc(mesh):
     """rx_mesh_desc over contiguous copies of the mesh arrays (kept alive by the returned dict)."""
-    nDim = int(mesh.get("n_dim", 2))
+    nDim = int(mesh.get("n_dim", np.shape(mesh["coord"])[1]))
     keep = {
         "edges": np.ascontiguousarray(mesh["edges"], dtype=np.int64),
         "edge_normal": np.ascontiguousarray(mesh["edge_normal"], dtype=np.float64),
@@ -296,7 +296,7 @@ class ReactiveNSSolver:
     def __init__(self, mesh, mech: Mechanism, cfg: Cfg, device=0):
         self.mech = mech
         self.cfg = cfg
-        self.nDim = int(mesh.get("n_dim", 2))
+        self.nDim = int(mesh.get("n_dim", np.shape(mesh["coord"])[1]))
         self.N = int(len(mesh["coord"]))
         self.E = int(len(mesh["edges"]))
         self.nVar = mech.ns + self.nDim + 2

@@ -82,10 +82,11 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   if (!mesh || !cfg || !out || (!mech && !flow)) return RX_ERR_ARG;
   if (cfg->spatial_order < 0 || cfg->spatial_order > 2) return RX_ERR_ARG;
   *out = nullptr;
-  if (mesh->n_dim != 2) return RX_ERR_ARG;  // 3-D dual grids: next round
+  if (mesh->n_dim != 2 && mesh->n_dim != 3) return RX_ERR_ARG;
   const bool sst = flow != nullptr;
   const int ns = sst ? 0 : mech->n_species;
   if (!sst && !(ns == 3 || ns == 4 || ns == 7 || ns == 9)) return RX_ERR_ARG;
+  if (!sst && mesh->n_dim == 3 && !(ns == 7 || ns == 9)) return RX_ERR_ARG;  // 3-D instantiations (rx_kernels.hip)
   if (!sst && mech->n_reactions > rx::kMaxNR) return RX_ERR_ARG;
   if (mesh->n_point >= (1LL << 31) || 2 * mesh->n_edge >= (1LL << 31)) return RX_ERR_ARG;
   if (sst && (mesh->n_point != flow->N || mesh->n_edge != flow->E)) return RX_ERR_ARG;
@@ -534,7 +535,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     CK(dalloc(ctx, &ctx->fconv, E * nv));
     CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
-    CK(dalloc(ctx, &ctx->vsumm, E * (int64_t)(24 + 9 * ns)));
+    CK(dalloc(ctx, &ctx->vsumm, E * (int64_t)(14 + 5 * ctx->nDim + 9 * ns)));  // visc_summary_size<NS, NDIM>
     CK(dalloc(ctx, &ctx->jsrc, N * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->rsrc, N * nv));
   }

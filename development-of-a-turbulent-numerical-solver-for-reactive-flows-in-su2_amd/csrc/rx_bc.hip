@@ -395,7 +395,7 @@ __global__ __launch_bounds__(64) void k_bc_weak(int NW, const int32_t* __restric
     a.gk = g.gk = nullptr;
   }
   double res[nVar];
-  double* sm = B.implicit ? summ + (size_t)b * visc_summary_size<NS>() : nullptr;
+  double* sm = B.implicit ? summ + (size_t)b * visc_summary_size<NS, NDIM>() : nullptr;
   const int rc = visc_edge<NS, NDIM>(m, B.vp, a, g, sk, Normal, res, sm, scr_all + threadIdx.x * NS * NS, false);
   bad = false;
 #pragma unroll
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void k_bc_visc_jac(int NW, const int32_t* _
   const int cc = c < nVar ? c : 0;
   const double sib = dTdU[(size_t)i * nVar + cc], sjb = sv[(size_t)b * nVar + cc];
   double* Ji = jacv + (size_t)b * 2 * nVar2;
-  visc_jac_column<NS, NDIM>(m, P, summ + (size_t)b * visc_summary_size<NS>(), sib, sjb, c, c, Ji, Ji + nVar2);
+  visc_jac_column<NS, NDIM>(m, P, summ + (size_t)b * visc_summary_size<NS, NDIM>(), sib, sjb, c, c, Ji, Ji + nVar2);
 }
 
 // CSysMatrix::DeleteValsRowi (Common/src/matrix_structure.cpp:483-495) for scalar row r of block row i.
@@ -438,7 +438,7 @@ __device__ inline void delete_row(int i, int r, int nb, const int32_t* rp, const
 // residual entries): the reference's per-vertex updates in Space_Integration order. Every entry sees its own
 // sequence of AddBlock / SubtractBlock operations, so the lanes are independent except around DeleteValsRowi,
 // which spans the whole BSR row.
-constexpr int kApplyBlock = 192;  // >= nVar^2 for Ns <= 9
+constexpr int kApplyBlock = 256;  // >= nVar^2 (nVar <= 14: Ns = 9 in 3-D)
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kApplyBlock) void k_bc_apply(const int32_t* __restrict__ bn,
                                                           const int32_t* __restrict__ bn_ptr,
@@ -462,6 +462,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_bc_apply(const int32_t* __restr
                                                           const double* __restrict__ jacv, double* __restrict__ R,
                                                           double* __restrict__ A, int* err) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nVar2 = nVar * nVar, E_ = NDIM + 1;
+  static_assert(nVar2 <= kApplyBlock, "one lane per diagonal-block entry");
   const int t = blockIdx.x, q = threadIdx.x;
   const int i = bn[t];
   const int a = q / nVar, c = q - a * nVar;
@@ -659,13 +660,34 @@ __global__ __launch_bounds__(kBlock) void k_sst_bc(int nbn, const int32_t* __res
   }
 }
 
-#define RX_NS_SWITCH(ns, CALL)                                 \
-  switch (ns) {                                                \
-    case 3: { constexpr int NS_ = 3; CALL; } break;            \
-    case 4: { constexpr int NS_ = 4; CALL; } break;            \
-    case 7: { constexpr int NS_ = 7; CALL; } break;            \
-    case 9: { constexpr int NS_ = 9; CALL; } break;            \
-    default: return RX_ERR_ARG;                                \
+#define RX_DNS_SWITCH(nd, ns, CALL)                                        \
+  if ((nd) == 2) {                                                         \
+    switch (ns) {                                                          \
+      case 3: { constexpr int NS_ = 3, ND_ = 2; CALL; } break;             \
+      case 4: { constexpr int NS_ = 4, ND_ = 2; CALL; } break;             \
+      case 7: { constexpr int NS_ = 7, ND_ = 2; CALL; } break;             \
+      case 9: { constexpr int NS_ = 9, ND_ = 2; CALL; } break;             \
+      default: return RX_ERR_ARG;                                          \
+    }                                                                      \
+  } else if ((nd) == 3) { /* 3-D: the 7-species C5 mechanism, 9 (golden) */ \
+    switch (ns) {                                                          \
+      case 7: { constexpr int NS_ = 7, ND_ = 3; CALL; } break;             \
+      case 9: { constexpr int NS_ = 9, ND_ = 3; CALL; } break;             \
+      default: return RX_ERR_ARG;                                          \
+    }                                                                      \
+  } else {                                                                 \
+    return RX_ERR_ARG;                                                     \
+  }
+
+#define RX_ND_SWITCH(nd, CALL)                   \
+  if ((nd) == 2) {                               \
+    constexpr int ND_ = 2;                       \
+    CALL;                                        \
+  } else if ((nd) == 3) {                        \
+    constexpr int ND_ = 3;                       \
+    CALL;                                        \
+  } else {                                       \
+    return RX_ERR_ARG;                           \
   }
 
 template <typename T>
@@ -711,7 +733,7 @@ BCDev bc_dev(const rx_ctx* fl) {
 int rx_bc_launch_weak(rx_ctx* ctx, hipStream_t st) {
   if (ctx->bc_nweak <= 0) return RX_OK;
   const BCDev B = bc_dev(ctx);
-  RX_NS_SWITCH(ctx->ns, (k_bc_weak<NS_, 2><<<blocks(ctx->bc_nweak, 64), 64, 0, st>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_bc_weak<NS_, ND_><<<blocks(ctx->bc_nweak, 64), 64, 0, st>>>(
                             ctx->bc_nweak, ctx->bc_weak, ctx->bc_node, ctx->bc_pn, ctx->bc_mark, ctx->bc_nrm,
                             ctx->bc_mkind, ctx->bc_mdata, B, ctx->mech, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
                             ctx->f[RX_F_DTDU], ctx->f[RX_F_GRAD], ctx->f[RX_F_MU], ctx->f[RX_F_KAPPA],
@@ -720,7 +742,7 @@ int rx_bc_launch_weak(rx_ctx* ctx, hipStream_t st) {
                             ctx->bc_summ, ctx->bc_sv, ctx->err)));
   RX_HIP(hipGetLastError());
   if (ctx->cfg.implicit) {
-    RX_NS_SWITCH(ctx->ns, (k_bc_visc_jac<NS_, 2><<<blocks((int64_t)ctx->bc_nweak * 16), kBlock, 0, st>>>(
+    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_bc_visc_jac<NS_, ND_><<<blocks((int64_t)ctx->bc_nweak * 16), kBlock, 0, st>>>(
                               ctx->bc_nweak, ctx->bc_weak, ctx->bc_node, ctx->f[RX_F_DTDU], ctx->bc_sv, ctx->bc_summ,
                               ctx->mech, B.vp, ctx->bc_jacv)));
     RX_HIP(hipGetLastError());
@@ -755,7 +777,6 @@ extern "C" {
 
 int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
   if (!ctx || ctx->kind != RX_KIND_FLOW || !bc || bc->n_marker <= 0 || !bc->kind || !bc->data) return RX_ERR_ARG;
-  if (ctx->nDim != 2) return RX_ERR_ARG;
   const int64_t NB = ctx->NB;
   if (NB > 0 && !bc->normal_neighbor) return RX_ERR_ARG;
   if (bc->inlet_kind < RX_INLET_TOTAL_CONDITIONS || bc->inlet_kind > RX_INLET_TEMPERATURE_IMPOSE) return RX_ERR_ARG;
@@ -848,7 +869,7 @@ int rx_bc_flow(rx_ctx* ctx) {
     return rc;
   }
   if (ctx->bc_nbn > 0) {
-    RX_NS_SWITCH(ctx->ns, (k_bc_apply<NS_, 2><<<ctx->bc_nbn, kApplyBlock, 0, ctx->stream>>>(
+    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_bc_apply<NS_, ND_><<<ctx->bc_nbn, kApplyBlock, 0, ctx->stream>>>(
                               ctx->bc_bn, ctx->bc_bn_ptr, ctx->bc_bn_vtx, ctx->bc_mark, ctx->bc_pn,
                               ctx->bc_nrm, ctx->bc_mkind, ctx->bc_mdata, B, ctx->mech, ctx->coord, ctx->f[RX_F_U],
                               ctx->f[RX_F_V], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DTDU], ctx->f[RX_F_EDDY], ctx->rp,
@@ -866,11 +887,11 @@ int rx_bc_sst(rx_ctx* ctx) {
   if (fl->bc_pending) RX_HIP(hipStreamWaitEvent(ctx->stream, fl->bc_join, 0));  // ghost states of this iteration
   if (fl->bc_nbn > 0) {
     const double sk1 = 0.85, sk2 = 1.0, so1 = 0.5, so2 = 0.856, beta1 = 0.075;  // CTurbSSTSolver constants
-    k_sst_bc<2><<<blocks(fl->bc_nbn), kBlock, 0, ctx->stream>>>(
+    RX_ND_SWITCH(ctx->nDim, (k_sst_bc<ND_><<<blocks(fl->bc_nbn), kBlock, 0, ctx->stream>>>(
         fl->bc_nbn, fl->bc_bn, fl->bc_bn_ptr, fl->bc_bn_vtx, fl->bc_mark, fl->bc_pn, fl->bc_nrm, fl->bc_mkind,
         fl->bc_kine_inf, fl->bc_omega_inf, sk1, sk2, so1, so2, beta1, ctx->coord, fl->f[RX_F_V], fl->nPV,
         fl->f[RX_F_MU], fl->f[RX_F_EDDY], fl->bc_charac, ctx->f[RX_F_GRAD], ctx->f[RX_F_F1], ctx->rp, ctx->col,
-        ctx->diag, ctx->f[RX_F_U], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr);
+        ctx->diag, ctx->f[RX_F_U], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr)));
     RX_HIP(hipGetLastError());
   }
   return RX_OK;

@@ -344,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_set_primitive(int N, DevMech m, Prim
     lam += cond[a] * yom[a] / phi;
   }
   kappa[i] = lam / P.Cond_ref;
-  const double pT = 1.0e-3 * pow(dim_temp, 1.75);
+  const double pT = 1.0e-3 * pow175_cr(dim_temp);
   const double scale = P.Vel_ref * P.Len_ref * 1.0e4;
   double* D = Dij + (size_t)i * NS * NS;
 #pragma unroll
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restri
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
   double res[nVar];
-  double* summ = P.implicit ? Summ + (size_t)e * visc_summary_size<NS>() : nullptr;
+  double* summ = P.implicit ? Summ + (size_t)e * visc_summary_size<NS, NDIM>() : nullptr;
   __shared__ double scr_all[64 * NS * NS];  // dense Stefan-Maxwell / QR matrices, one slice per lane
   const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ, scr_all + threadIdx.x * NS * NS);
   bool bad = false;
@@ -648,7 +648,7 @@ __global__ __launch_bounds__(kBlock) void k_visc_jac(int E, const int32_t* __res
   const int bc = b < nVar ? b : 0;
   const double sib = dTdU[(size_t)n0 * nVar + bc], sjb = dTdU[(size_t)n1 * nVar + bc];
   double* Ji = Jac + (size_t)e * 2 * nVar2;
-  visc_jac_column<NS, NDIM>(m, P, Summ + (size_t)e * visc_summary_size<NS>(), sib, sjb, b, b, Ji, Ji + nVar2);
+  visc_jac_column<NS, NDIM>(m, P, Summ + (size_t)e * visc_summary_size<NS, NDIM>(), sib, sjb, b, b, Ji, Ji + nVar2);
 }
 
 // Generic node gather of an edge flux array: node0 += sign*F, node1 -= sign*F (edge order).
@@ -1021,13 +1021,34 @@ __global__ __launch_bounds__(kBlock) void k_time_step(int N, int nPV, int nVar, 
 
 inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 
-#define RX_NS_SWITCH(ns, CALL)                                 \
-  switch (ns) {                                                \
-    case 3: { constexpr int NS_ = 3; CALL; } break;            \
-    case 4: { constexpr int NS_ = 4; CALL; } break;            \
-    case 7: { constexpr int NS_ = 7; CALL; } break;            \
-    case 9: { constexpr int NS_ = 9; CALL; } break;            \
-    default: return RX_ERR_ARG;                                \
+#define RX_DNS_SWITCH(nd, ns, CALL)                                        \
+  if ((nd) == 2) {                                                         \
+    switch (ns) {                                                          \
+      case 3: { constexpr int NS_ = 3, ND_ = 2; CALL; } break;             \
+      case 4: { constexpr int NS_ = 4, ND_ = 2; CALL; } break;             \
+      case 7: { constexpr int NS_ = 7, ND_ = 2; CALL; } break;             \
+      case 9: { constexpr int NS_ = 9, ND_ = 2; CALL; } break;             \
+      default: return RX_ERR_ARG;                                          \
+    }                                                                      \
+  } else if ((nd) == 3) { /* 3-D: the 7-species C5 mechanism, 9 (golden) */ \
+    switch (ns) {                                                          \
+      case 7: { constexpr int NS_ = 7, ND_ = 3; CALL; } break;             \
+      case 9: { constexpr int NS_ = 9, ND_ = 3; CALL; } break;             \
+      default: return RX_ERR_ARG;                                          \
+    }                                                                      \
+  } else {                                                                 \
+    return RX_ERR_ARG;                                                     \
+  }
+
+#define RX_ND_SWITCH(nd, CALL)                   \
+  if ((nd) == 2) {                               \
+    constexpr int ND_ = 2;                       \
+    CALL;                                        \
+  } else if ((nd) == 3) {                        \
+    constexpr int ND_ = 3;                       \
+    CALL;                                        \
+  } else {                                       \
+    return RX_ERR_ARG;                           \
   }
 
 }  // namespace
@@ -1051,11 +1072,10 @@ int rx_check_error(rx_ctx* ctx) {
 }
 
 int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
   const rx_cfg& c = ctx->cfg;
   PrimParams P{c.t_min, c.t_max, c.T_ref, c.E_ref, c.R_ref, c.p_ref, c.visc_ref, c.cond_ref, c.vel_ref, c.len_ref,
                ext_iter, c.clip_temp, c.rans};
-  RX_NS_SWITCH(ctx->ns, (k_set_primitive<NS_, 2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_set_primitive<NS_, ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->mech, P, ctx->f[RX_F_U], ctx->f[RX_F_V], ext_iter > 0 ? ctx->uold : nullptr,
                             ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_DPDU], ctx->f[RX_F_DTDU], ctx->f[RX_F_MU],
                             ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_EDDY], ctx->err)));
@@ -1064,10 +1084,10 @@ int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter) {
 }
 
 int rx_launch_muscl(rx_ctx* ctx) {
-  if (ctx->nDim != 2 || !ctx->recon) return RX_ERR_ARG;
+  if (!ctx->recon) return RX_ERR_ARG;
   const double* lim = ctx->cfg.spatial_order == 2 ? ctx->f[RX_F_LIMITER] : nullptr;
   double* SR = ctx->cfg.implicit ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
-  RX_NS_SWITCH(ctx->ns, (k_muscl_edge<NS_, 2><<<blocks(2 * ctx->E), kBlock, 0, ctx->stream>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_muscl_edge<NS_, ND_><<<blocks(2 * ctx->E), kBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_DPDU], ctx->f[RX_F_GRAD],
                             lim, ctx->mech, ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.implicit,
                             ctx->recon, SR, ctx->err)));
@@ -1076,8 +1096,7 @@ int rx_launch_muscl(rx_ctx* ctx) {
 }
 
 int rx_launch_ausm_node(rx_ctx* ctx) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
-  RX_NS_SWITCH(ctx->ns, (k_ausm_node<NS_, 2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_ausm_node<NS_, ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->f[RX_F_V],
                             ctx->cfg.spatial_order ? ctx->recon : nullptr, ctx->cfg.mach_inf, ctx->f[RX_F_RES],
                             ctx->err)));
@@ -1086,8 +1105,7 @@ int rx_launch_ausm_node(rx_ctx* ctx) {
 }
 
 int rx_launch_ausm_edge(rx_ctx* ctx) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
-  RX_NS_SWITCH(ctx->ns, (k_ausm_edge<NS_, 2><<<blocks(ctx->E * kAusmTeam, kAusmBlock), kAusmBlock, 0, ctx->stream>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_ausm_edge<NS_, ND_><<<blocks(ctx->E * kAusmTeam, kAusmBlock), kAusmBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
                             ctx->cfg.spatial_order ? ctx->recon : nullptr,
                             ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr,
@@ -1097,12 +1115,11 @@ int rx_launch_ausm_edge(rx_ctx* ctx) {
 }
 
 int rx_launch_visc_edge(rx_ctx* ctx) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
   ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
                ctx->cfg.rans, ctx->cfg.implicit};
   {
     RxPhase ph(ctx, RX_K_VISC);
-    RX_NS_SWITCH(ctx->ns, (k_visc_edge<NS_, 2><<<blocks(ctx->E, 64), 64, 0, ctx->stream>>>(
+    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_visc_edge<NS_, ND_><<<blocks(ctx->E, 64), 64, 0, ctx->stream>>>(
                               (int)ctx->E, ctx->edges, ctx->normal, ctx->coord, ctx->f[RX_F_V], ctx->f[RX_F_GRAD],
                               ctx->f[RX_F_MU], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_DTDU],
                               ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_SIGMAK], ctx->f[RX_F_GRADK],
@@ -1111,7 +1128,7 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
   }
   if (ctx->cfg.implicit) {
     RxPhase ph(ctx, RX_K_VISC_JAC);
-    RX_NS_SWITCH(ctx->ns, (k_visc_jac<NS_, 2><<<blocks(ctx->E * 16), kBlock, 0, ctx->stream>>>(
+    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_visc_jac<NS_, ND_><<<blocks(ctx->E * 16), kBlock, 0, ctx->stream>>>(
                               (int)ctx->E, ctx->edges, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->mech, P, ctx->jvisc)));
     RX_HIP(hipGetLastError());
   }
@@ -1126,13 +1143,12 @@ int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_firs
 }
 
 int rx_launch_source(rx_ctx* ctx) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
   SourceParams P{ctx->cfg.c_mu, ctx->cfg.pasr_lb, ctx->cfg.rho_ref, ctx->cfg.t_ref, ctx->cfg.T_ref, ctx->cfg.rans,
                  ctx->cfg.implicit};
   // explicit: R += S directly; implicit: S and its Jacobian go to scratch, folded in by k_assemble
   double* Rdst = ctx->cfg.implicit ? ctx->rsrc : ctx->f[RX_F_RES];
   const int add = ctx->cfg.implicit ? 0 : 1;
-  RX_NS_SWITCH(ctx->ns, (k_source<NS_, 2><<<blocks(ctx->N, 128), 128, 0, ctx->stream>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_source<NS_, ND_><<<blocks(ctx->N, 128), 128, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->f[RX_F_V], ctx->f[RX_F_DTDU], ctx->vol, ctx->f[RX_F_OMEGA], ctx->mech,
                             P, Rdst, add, ctx->jsrc, ctx->err)));
   RX_HIP(hipGetLastError());
@@ -1152,7 +1168,9 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
     RX_ASM(7)
     RX_ASM(8)
     RX_ASM(11)
+    RX_ASM(12)
     RX_ASM(13)
+    RX_ASM(14)
 #undef RX_ASM
     default:
       return RX_ERR_ARG;
@@ -1162,8 +1180,7 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
 }
 
 int rx_launch_grad(rx_ctx* ctx) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
-  RX_NS_SWITCH(ctx->ns, (k_grad_lsq<NS_, 2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_grad_lsq<NS_, ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->nbr_ptr, ctx->nbr, ctx->coord, ctx->f[RX_F_V], ctx->mech,
                             ctx->f[RX_F_GRAD])));
   RX_HIP(hipGetLastError());
@@ -1171,28 +1188,26 @@ int rx_launch_grad(rx_ctx* ctx) {
 }
 
 int rx_launch_limiter(rx_ctx* ctx) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
-  k_limiter_minmax<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nPV, ctx->adj_ptr, ctx->adj,
+  RX_ND_SWITCH(ctx->nDim, (k_limiter_minmax<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nPV, ctx->adj_ptr, ctx->adj,
                                                                   ctx->edges, ctx->f[RX_F_V], ctx->lim_mn,
-                                                                  ctx->lim_mx);
+                                                                  ctx->lim_mx)));
   RX_HIP(hipGetLastError());
   const double eps1 = ctx->cfg.limiter_coeff * ctx->cfg.ref_elem_length;
   const double eps2 = eps1 * eps1 * eps1;
-  k_limiter_venkat<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->adj_ptr, ctx->adj,
+  RX_ND_SWITCH(ctx->nDim, (k_limiter_venkat<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->adj_ptr, ctx->adj,
                                                                   ctx->edges, ctx->coord, ctx->f[RX_F_GRAD],
                                                                   ctx->lim_mn, ctx->lim_mx, eps2,
-                                                                  ctx->f[RX_F_LIMITER]);
+                                                                  ctx->f[RX_F_LIMITER])));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
 
 int rx_launch_time_step(rx_ctx* ctx) {
-  if (ctx->nDim != 2) return RX_ERR_ARG;
-  k_time_step<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+  RX_ND_SWITCH(ctx->nDim, (k_time_step<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
       (int)ctx->N, ctx->nPV, ctx->nVar, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->bv_ptr, ctx->bv_normal,
       ctx->f[RX_F_V], ctx->f[RX_F_DPDU], ctx->f[RX_F_MU], ctx->f[RX_F_EDDY], ctx->vol, ctx->nbr_ptr, ctx->cfg.cfl,
       ctx->cfg.max_delta_time, ctx->cfg.prandtl_lam, ctx->cfg.prandtl_turb, ctx->f[RX_F_DT], ctx->f[RX_F_LAMBDA_INV],
-      ctx->f[RX_F_LAMBDA_VISC]);
+      ctx->f[RX_F_LAMBDA_VISC])));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }

@@ -26,6 +26,17 @@
 namespace {
 
 constexpr int kBlock = 256;
+#define RX_ND_SWITCH(nd, CALL)                   \
+  if ((nd) == 2) {                               \
+    constexpr int ND_ = 2;                       \
+    CALL;                                        \
+  } else if ((nd) == 3) {                        \
+    constexpr int ND_ = 3;                       \
+    CALL;                                        \
+  } else {                                       \
+    return RX_ERR_ARG;                           \
+  }
+
 inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 
 struct SSTC {
@@ -476,8 +487,8 @@ bool is_sst(const rx_ctx* ctx) { return ctx && ctx->kind == RX_KIND_SST && ctx->
 
 int sst_gradient(rx_ctx* ctx) {
   if (ctx->Nd > 0)
-    k_sol_grad_ls<2><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->coord, ctx->nbr_ptr, ctx->nbr,
-                                                                   ctx->f[RX_F_U], ctx->f[RX_F_GRAD]);
+    RX_ND_SWITCH(ctx->nDim, (k_sol_grad_ls<ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->coord, ctx->nbr_ptr, ctx->nbr,
+                                                                   ctx->f[RX_F_U], ctx->f[RX_F_GRAD])));
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_GRAD], 2 * ctx->nDim);  // Set_MPI_Solution_Gradient
 }
@@ -506,10 +517,10 @@ int rx_sst_update(rx_ctx* ctx) {
 extern "C" {
 
 int rx_strain_mag(rx_ctx* ctx) {
-  if (!ctx || ctx->kind != RX_KIND_FLOW || ctx->nDim != 2) return RX_ERR_ARG;
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_STRAIN);
-  k_strain<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->f[RX_F_GRAD],
-                                                          ctx->f[RX_F_STRAIN]);
+  RX_ND_SWITCH(ctx->nDim, (k_strain<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->f[RX_F_GRAD],
+                                                          ctx->f[RX_F_STRAIN])));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
@@ -528,9 +539,9 @@ int rx_sst_upwind(rx_ctx* ctx) {
   if (!is_sst(ctx)) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_SST_UPW);
   const rx_ctx* fl = ctx->flow;
-  k_sst_upwind<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+  RX_ND_SWITCH(ctx->nDim, (k_sst_upwind<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
       (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->diag, ctx->edges, ctx->normal, fl->f[RX_F_V], fl->nPV,
-      ctx->f[RX_F_U], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr);
+      ctx->f[RX_F_U], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
@@ -539,10 +550,10 @@ int rx_sst_viscous(rx_ctx* ctx) {
   if (!is_sst(ctx)) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_SST_VISC);
   const rx_ctx* fl = ctx->flow;
-  k_sst_visc<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+  RX_ND_SWITCH(ctx->nDim, (k_sst_visc<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
       (int)ctx->N, sst_constants(), ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->diag, ctx->edges, ctx->normal,
       ctx->coord, fl->f[RX_F_V], fl->nPV, fl->f[RX_F_MU], fl->f[RX_F_EDDY], ctx->f[RX_F_U], ctx->f[RX_F_GRAD],
-      ctx->f[RX_F_F1], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr);
+      ctx->f[RX_F_F1], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
@@ -552,10 +563,10 @@ int rx_sst_source(rx_ctx* ctx) {
   RxPhase ph(ctx, RX_K_SST_SOURCE);
   const rx_ctx* fl = ctx->flow;
   if (ctx->Nd > 0)
-    k_sst_source<2><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
+    RX_ND_SWITCH(ctx->nDim, (k_sst_source<ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
         (int)ctx->Nd, sst_constants(), ctx->diag, fl->f[RX_F_V], fl->nPV, fl->f[RX_F_GRAD], fl->nG, fl->f[RX_F_EDDY],
         fl->f[RX_F_STRAIN], ctx->f[RX_F_U], ctx->vol, ctx->f[RX_F_WALLDIST], ctx->f[RX_F_F1], ctx->f[RX_F_F2],
-        ctx->f[RX_F_CDKW], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr);
+        ctx->f[RX_F_CDKW], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
@@ -566,11 +577,11 @@ int rx_sst_postprocessing(rx_ctx* ctx) {
   int rc = sst_gradient(ctx);
   if (rc) return rc;
   rx_ctx* fl = ctx->flow;
-  k_sst_post<2><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+  RX_ND_SWITCH(ctx->nDim, (k_sst_post<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
       (int)ctx->N, sst_constants(), ctx->f[RX_F_U], ctx->f[RX_F_GRAD], fl->f[RX_F_V], fl->nPV, fl->f[RX_F_MU],
       ctx->f[RX_F_WALLDIST], fl->f[RX_F_STRAIN], ctx->f[RX_F_F1], ctx->f[RX_F_F2], ctx->f[RX_F_CDKW],
       ctx->f[RX_F_MUT], fl->f[RX_F_TKE], fl->f[RX_F_OMEGA], fl->f[RX_F_MUT], fl->f[RX_F_EDDY], fl->f[RX_F_SIGMAK],
-      fl->f[RX_F_GRADK]);
+      fl->f[RX_F_GRADK])));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }

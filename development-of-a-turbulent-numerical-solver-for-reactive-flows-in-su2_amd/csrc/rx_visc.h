@@ -268,14 +268,17 @@ __device__ inline void colpiv_qr_solve(double* Q, const double (*rhs)[NDIM], dou
   }
 }
 
-// Per-edge summary written by visc_edge (implicit) for the Jacobian kernel: scalars, then nine
-// species arrays (Xs_i, Xs_j, Ys, hs, Cps, Jd, Gxn/|n|, Ds, quirk aux).
-enum {
-  VS_MU = 0, VS_K, VS_MUT, VS_RHO, VS_VM, VS_RHOI = 6, VS_RHOJ, VS_VI, VS_VJ = 10, VS_THETA = 12, VS_DIJ, VS_DS,
-  VS_UN, VS_PF = 17, VS_TM = 19, VS_TMI, VS_TMJ, VS_SGI, VS_SGJ, VS_ARR
+// Per-edge summary written by visc_edge (implicit) for the Jacobian kernel: scalars and NDIM-vectors (mean
+// velocity, both velocities, unit normal, projected flux momentum rows), then nine species arrays (Xs_i, Xs_j, Ys,
+// hs, Cps, Jd, Gxn/|n|, Ds, quirk aux).
+template <int NDIM>
+struct VSL {
+  static constexpr int MU = 0, K = 1, MUT = 2, RHO = 3, VM = 4, RHOI = VM + NDIM, RHOJ = RHOI + 1, VI = RHOJ + 1,
+                       VJ = VI + NDIM, THETA = VJ + NDIM, DIJ = THETA + 1, DS = DIJ + 1, UN = DS + 1, PF = UN + NDIM,
+                       TM = PF + NDIM, TMI = TM + 1, TMJ = TMI + 1, SGI = TMJ + 1, SGJ = SGI + 1, ARR = SGJ + 1;
 };
-template <int NS>
-constexpr int visc_summary_size() { return VS_ARR + 9 * NS; }
+template <int NS, int NDIM>
+constexpr int visc_summary_size() { return VSL<NDIM>::ARR + 9 * NS; }
 
 // Per-edge inputs gathered from the two node records.
 template <int NS, int NDIM>
@@ -563,65 +566,66 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     }
     qaux[s] = aux;
   }
+  using L = VSL<NDIM>;
   double* o = summ;
-  o[VS_MU] = Mean_mu;
-  o[VS_K] = Mean_k;
-  o[VS_MUT] = Mean_mut;
-  o[VS_RHO] = rho;
-  o[VS_VM] = Vm[VX_P];
-  o[VS_VM + 1] = Vm[VX_P + 1];
-  o[VS_RHOI] = Vi[RHO_P];
-  o[VS_RHOJ] = Vj[RHO_P];
-  o[VS_VI] = Vi[VX_P];
-  o[VS_VI + 1] = Vi[VX_P + 1];
-  o[VS_VJ] = Vj[VX_P];
-  o[VS_VJ + 1] = Vj[VX_P + 1];
-  o[VS_THETA] = theta;
-  o[VS_DIJ] = sqrt(dist2);
-  o[VS_DS] = Area;
-  o[VS_UN] = UN[0];
-  o[VS_UN + 1] = UN[NDIM - 1];
-  o[VS_PF] = PF[RHOVX_S];
-  o[VS_PF + 1] = PF[RHOVX_S + 1];
-  o[VS_TM] = totMass;
-  o[VS_TMI] = totMass_i;
-  o[VS_TMJ] = totMass_j;
-  o[VS_SGI] = sigma_i;
-  o[VS_SGJ] = sigma_j;
+  o[L::MU] = Mean_mu;
+  o[L::K] = Mean_k;
+  o[L::MUT] = Mean_mut;
+  o[L::RHO] = rho;
+  o[L::RHOI] = Vi[RHO_P];
+  o[L::RHOJ] = Vj[RHO_P];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    o[L::VM + d] = Vm[VX_P + d];
+    o[L::VI + d] = Vi[VX_P + d];
+    o[L::VJ + d] = Vj[VX_P + d];
+    o[L::UN + d] = UN[d];
+    o[L::PF + d] = PF[RHOVX_S + d];
+  }
+  o[L::THETA] = theta;
+  o[L::DIJ] = sqrt(dist2);
+  o[L::DS] = Area;
+  o[L::TM] = totMass;
+  o[L::TMI] = totMass_i;
+  o[L::TMJ] = totMass_j;
+  o[L::SGI] = sigma_i;
+  o[L::SGJ] = sigma_j;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    o[VS_ARR + 0 * NS + s] = Xs_i[s];
-    o[VS_ARR + 1 * NS + s] = Xs_j[s];
-    o[VS_ARR + 2 * NS + s] = Ys[s];
-    o[VS_ARR + 3 * NS + s] = hs[s];
-    o[VS_ARR + 4 * NS + s] = Cps[s];
-    o[VS_ARR + 5 * NS + s] = Jd[s];
-    o[VS_ARR + 6 * NS + s] = Gxn[s];
-    o[VS_ARR + 7 * NS + s] = Ds[s];
-    o[VS_ARR + 8 * NS + s] = qaux[s];
+    o[L::ARR + 0 * NS + s] = Xs_i[s];
+    o[L::ARR + 1 * NS + s] = Xs_j[s];
+    o[L::ARR + 2 * NS + s] = Ys[s];
+    o[L::ARR + 3 * NS + s] = hs[s];
+    o[L::ARR + 4 * NS + s] = Cps[s];
+    o[L::ARR + 5 * NS + s] = Jd[s];
+    o[L::ARR + 6 * NS + s] = Gxn[s];
+    o[L::ARR + 7 * NS + s] = Ds[s];
+    o[L::ARR + 8 * NS + s] = qaux[s];
   }
   return err;
 }
 
 // Jacobian column b (0 <= b < nVar) of Jac_i and Jac_j for one edge, from the visc_edge summary:
-// SetLaminarViscousProjJacs (:1200-1401) + SST_Reactive_JacobianClosure (:891-1090, 2-D branch)
+// SetLaminarViscousProjJacs (:1200-1401) + SST_Reactive_JacobianClosure (:891-1090; the 2-D branch :891-1000, the
+// 3-D branch :1001-1090 with its species-species diagonal term and hs/rho instead of hs*Ys/rho in the energy row)
 // build dF/dV (FI for node i, FJ for node j); J = dF/dV * dV/dU (:1637-1653). A team of lanes owns
 // the columns of one edge; every dF/dV entry is accumulated in the reference's order, and J's sum over
 // k keeps the reference's order (the F*0 terms of dV/dU's zero entries are dropped: they can only
 // change the sign of an exact zero). base_i/base_j: the column-independent part of row a of dJ/drho
-// (this lane's a = lane index in the team), shared through shuffles. Only 2-D.
+// (this lane's a = lane index in the team), shared through shuffles.
 template <int NS, int NDIM>
 __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, const double* __restrict__ sm,
                                        double Sib, double Sjb, int b, int tl, double* __restrict__ Ji,
                                        double* __restrict__ Jj) {
-  constexpr int nVar = NS + NDIM + 2;
+  using L = VSL<NDIM>;
+  constexpr int nVar = NS + NDIM + 2, NF = NDIM + 2;
   constexpr int RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
-  const double mu = sm[VS_MU], ktr = sm[VS_K], mut = sm[VS_MUT], rho = sm[VS_RHO];
-  const double rho_i = sm[VS_RHOI], rho_j = sm[VS_RHOJ];
-  const double theta = sm[VS_THETA], dij = sm[VS_DIJ], dS = sm[VS_DS], sq = sm[VS_DIJ], Area = sm[VS_DS];
-  const double totMass = sm[VS_TM], totMass_i = sm[VS_TMI], totMass_j = sm[VS_TMJ];
-  const double sigma_i = sm[VS_SGI], sigma_j = sm[VS_SGJ];
-  const double* Xs_i = sm + VS_ARR;
+  const double mu = sm[L::MU], ktr = sm[L::K], mut = sm[L::MUT], rho = sm[L::RHO];
+  const double rho_i = sm[L::RHOI], rho_j = sm[L::RHOJ];
+  const double theta = sm[L::THETA], dij = sm[L::DIJ], dS = sm[L::DS], sq = sm[L::DIJ], Area = sm[L::DS];
+  const double totMass = sm[L::TM], totMass_i = sm[L::TMI], totMass_j = sm[L::TMJ];
+  const double sigma_i = sm[L::SGI], sigma_j = sm[L::SGJ];
+  const double* Xs_i = sm + L::ARR;
   const double* Xs_j = Xs_i + NS;
   const double* Ys = Xs_j + NS;
   const double* hs = Ys + NS;
@@ -684,34 +688,44 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
         }
       }
   }
-  // ---- dF/dV flow block rows 0..3, columns 0..3 (index [row][col]); zero-initialised
-  double FJ[4][4], FI[4][4];
+  // ---- dF/dV flow block rows / columns 0..RHOE (index [row][col]); zero-initialised
+  double FJ[NF][NF], FI[NF][NF];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < NF; ++r)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) FJ[r][c] = FI[r][c] = 0.0;
-  const double UN0 = sm[VS_UN], UN1 = sm[VS_UN + 1];
-  const double thetax = theta + UN0 * UN0 / 3.0, thetay = theta + UN1 * UN1 / 3.0;
-  const double etaz = UN0 * UN1 / 3.0;
-  const double pix = sm[VS_VM] * thetax + sm[VS_VM + 1] * etaz;
-  const double piy = sm[VS_VM] * etaz + sm[VS_VM + 1] * thetay;
-  FJ[1][1] = mu * thetax / dij * dS;
-  FJ[1][2] = mu * etaz / dij * dS;
-  FJ[2][1] = mu * etaz / dij * dS;
-  FJ[2][2] = mu * thetay / dij * dS;
-  FJ[3][1] = pix * mu / dij * dS;
-  FJ[3][2] = piy * mu / dij * dS;
-  FJ[3][3] = ktr * theta / dij * dS;
+    for (int c = 0; c < NF; ++c) FJ[r][c] = FI[r][c] = 0.0;
+  double UN[NDIM], th[NDIM][NDIM], pi[NDIM];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int d = 0; d < NDIM; ++d) UN[d] = sm[L::UN + d];
+  // theta_x = theta + n_x^2/3 on the diagonal, eta = n_a n_b / 3 off it (:1265-1275 / :1300-1320)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) FI[r][c] = -FJ[r][c];
+  for (int a = 0; a < NDIM; ++a)
+#pragma unroll
+    for (int c = 0; c < NDIM; ++c) th[a][c] = (a == c) ? theta + UN[a] * UN[a] / 3.0 : UN[a] * UN[c] / 3.0;
+#pragma unroll
+  for (int c = 0; c < NDIM; ++c) {
+    double p = sm[L::VM] * th[0][c];
+#pragma unroll
+    for (int a = 1; a < NDIM; ++a) p += sm[L::VM + a] * th[a][c];
+    pi[c] = p;
+  }
+#pragma unroll
+  for (int a = 0; a < NDIM; ++a)
+#pragma unroll
+    for (int c = 0; c < NDIM; ++c) FJ[1 + a][1 + c] = mu * th[a][c] / dij * dS;
+#pragma unroll
+  for (int c = 0; c < NDIM; ++c) FJ[RHOE_S][1 + c] = pi[c] * mu / dij * dS;
+  FJ[RHOE_S][RHOE_S] = ktr * theta / dij * dS;
+#pragma unroll
+  for (int r = 0; r < NF; ++r)
+#pragma unroll
+    for (int c = 0; c < NF; ++c) FI[r][c] = -FJ[r][c];
 #pragma unroll
   for (int q = 0; q < NS; ++q) {
-    FI[3][3] += -0.5 * Jd[q] * Cps[q];
-    FJ[3][3] += -0.5 * Jd[q] * Cps[q];
+    FI[RHOE_S][RHOE_S] += -0.5 * Jd[q] * Cps[q];
+    FJ[RHOE_S][RHOE_S] += -0.5 * Jd[q] * Cps[q];
   }
-  // species column of rows 0 (rho) and 3 (rho E), accumulated over the species rows in order
+  // species column of rows 0 (rho) and RHOE (rho E), accumulated over the species rows in order
   double FJ0k = 0.0, FI0k = 0.0, FJ3k = 0.0, FI3k = 0.0;
   if (k >= 0) {
 #pragma unroll
@@ -722,62 +736,70 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
       FI3k += -coli[a] * hs[a] * dS;
     }
   }
+  double dsj = 0.0, dsi = 0.0;  // 3-D species-species diagonal closure term of this lane's column (:1053-1060)
   if (P.rans) {
-    FJ[1][1] += mut * thetax / sq * Area;
-    FJ[1][2] += mut * etaz / sq * Area;
-    FI[1][1] -= mut * thetax / sq * Area;
-    FI[1][2] -= mut * etaz / sq * Area;
-    FJ[2][1] += mut * etaz / sq * Area;
-    FJ[2][2] += mut * thetay / sq * Area;
-    FI[2][1] -= mut * etaz / sq * Area;
-    FI[2][2] -= mut * thetay / sq * Area;
-    FJ[3][1] += pix * mut / sq * Area;
-    FJ[3][2] += piy * mut / sq * Area;
-    FI[3][1] -= pix * mut / sq * Area;
-    FI[3][2] -= piy * mut / sq * Area;
+#pragma unroll
+    for (int a = 0; a < NDIM; ++a)
+#pragma unroll
+      for (int c = 0; c < NDIM; ++c) {
+        FJ[1 + a][1 + c] += mut * th[a][c] / sq * Area;
+        FI[1 + a][1 + c] -= mut * th[a][c] / sq * Area;
+      }
+#pragma unroll
+    for (int c = 0; c < NDIM; ++c) {
+      FJ[RHOE_S][1 + c] += pi[c] * mut / sq * Area;
+      FI[RHOE_S][1 + c] -= pi[c] * mut / sq * Area;
+    }
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      FJ[3][3] += mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
-      FI[3][3] -= mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
+      FJ[RHOE_S][RHOE_S] += mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
+      FI[RHOE_S][RHOE_S] -= mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
     }
     if (k >= 0) {
-      FJ3k += mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_j * theta / sq * Area;
-      FI3k -= mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_i * theta / sq * Area;
+      if constexpr (NDIM == 2) {
+        FJ3k += mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_j * theta / sq * Area;
+        FI3k -= mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_i * theta / sq * Area;
+      } else {
+        dsj = mut * Ys[kk] / (PrT * LeT) / rho_j * theta / sq * Area;
+        dsi = mut * Ys[kk] / (PrT * LeT) / rho_i * theta / sq * Area;
+        FJ3k += mut / (PrT * LeT) * hs[kk] / rho_j * theta / sq * Area;
+        FI3k -= mut / (PrT * LeT) * hs[kk] / rho_i * theta / sq * Area;
+      }
     }
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      FJ[3][3] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
-      FI[3][3] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
+      FJ[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
+      FI[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
     }
   }
-  FI[3][1] += 0.5 * sm[VS_PF];
-  FJ[3][1] += 0.5 * sm[VS_PF];
-  FI[3][2] += 0.5 * sm[VS_PF + 1];
-  FJ[3][2] += 0.5 * sm[VS_PF + 1];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    FI[RHOE_S][1 + d] += 0.5 * sm[L::PF + d];
+    FJ[RHOE_S][1 + d] += 0.5 * sm[L::PF + d];
+  }
   // ---- J[a][b] = sum_k F[a][k] dV/dU[k][b]
-  const double ui = sm[VS_VI], vvi = sm[VS_VI + 1], uj = sm[VS_VJ], vvj = sm[VS_VJ + 1];
-  double ci1, ci2, cj1, cj2;  // dV/dU velocity rows, column b
-  if (b == 0) {
-    ci1 = -ui / rho_i;
-    ci2 = -vvi / rho_i;
-    cj1 = -uj / rho_j;
-    cj2 = -vvj / rho_j;
-  } else {
-    ci1 = (b == 1) ? 1.0 / rho_i : 0.0;
-    ci2 = (b == 2) ? 1.0 / rho_i : 0.0;
-    cj1 = (b == 1) ? 1.0 / rho_j : 0.0;
-    cj2 = (b == 2) ? 1.0 / rho_j : 0.0;
+  double ci[NDIM], cj[NDIM];  // dV/dU velocity rows, column b
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    if (b == 0) {
+      ci[d] = -sm[L::VI + d] / rho_i;
+      cj[d] = -sm[L::VJ + d] / rho_j;
+    } else {
+      ci[d] = (b == 1 + d) ? 1.0 / rho_i : 0.0;
+      cj[d] = (b == 1 + d) ? 1.0 / rho_j : 0.0;
+    }
   }
   const double d0 = (b == 0) ? 1.0 : 0.0;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < NF; ++r) {
     double si = 0.0, sj = 0.0;
     si += FI[r][0] * d0;
     sj += FJ[r][0] * d0;
-    si += FI[r][1] * ci1;
-    sj += FJ[r][1] * cj1;
-    si += FI[r][2] * ci2;
-    sj += FJ[r][2] * cj2;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+      si += FI[r][1 + d] * ci[d];
+      sj += FJ[r][1 + d] * cj[d];
+    }
     si += FI[r][RHOE_S] * Sib;
     sj += FJ[r][RHOE_S] * Sjb;
     if (k >= 0) {
@@ -798,6 +820,10 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
     if (k >= 0) {
       si = -coli[a] * dS;
       sj = -colj[a] * dS;
+      if (NDIM == 3 && a == k) {
+        si -= dsi;
+        sj += dsj;
+      }
     }
     Ji[(RHOS_S + a) * nVar + b] = si;
     Jj[(RHOS_S + a) * nVar + b] = sj;

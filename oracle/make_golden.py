@@ -349,6 +349,37 @@ def case_it3d():
     return a
 
 
+def case_muscl3d():
+    """a2 MUSCL branch + a13 Venkatakrishnan limiter in 3-D: the mini3d state with 2ND_ORDER_LIMITER (the
+    jet9w dumps on the extruded jet: whole-loop residual, a sample of Jacobian rows, limiter, records)."""
+    pts, hexes, U, writer = mini3d_inputs()
+    wd = make_workdir("muscl3d", writer, cfl=0.1, order="2ND_ORDER_LIMITER", extra=SYM3D)
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False)
+    out = {k: a[k] for k in ("coord", "volume", "U", "V", "dPdU", "dTdU", "grad_prim", "limiter_out", "edges",
+                             "edge_normal", "nbr_ptr", "nbr", "dims", "mach_inf", "limiter_params", "muscl_params",
+                             "muscl_loop_res", "bvertex", "bvertex_normal", "wall_distance", "visc_params",
+                             "src_params", "mu", "kappa", "Dij", "turb_k", "turb_omega", "mu_t",
+                             "sigma_k", "grad_k", "eddy_visc_flow")}
+    rng = np.random.default_rng(12345)
+    N = len(a["coord"])
+    rs = np.sort(rng.choice(N, size=48, replace=False))
+    rp, cl, blk = a["muscl_bsr_row_ptr"], a["muscl_bsr_col"], a["muscl_bsr"]
+    deg = max(int(rp[r + 1] - rp[r]) for r in rs)
+    nv = blk.shape[1]
+    mc = -np.ones((len(rs), deg), dtype=np.int64)
+    mb = np.zeros((len(rs), deg, nv, nv))
+    for q, r in enumerate(rs):
+        cols = cl[rp[r]:rp[r + 1]]
+        mc[q, :len(cols)] = cols
+        mb[q, :len(cols)] = blk[rp[r]:rp[r + 1]]
+    out["muscl_jac_rows"] = rs
+    out["muscl_jac_cols"] = mc
+    out["muscl_jac"] = mb
+    out.update(mech_arrays())
+    return out
+
+
 def case_jet9w():
     def writer(wd):
         os.symlink(os.path.join(CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
@@ -434,7 +465,7 @@ def main():
     for case in args.cases.split(","):
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
-             "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d}[case]()
+             "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

@@ -51,17 +51,20 @@ def rows(g, A, nb):
 
 
 def bc_case(name):
+    if name == "bc3d":
+        return golden(name)
     g = golden("bc9")
     if name != "bc9":
         g.update(golden(name))
     return g
 
 
-@pytest.mark.parametrize("case", ["bc9", "bc9t", "bc9m"])
+@pytest.mark.parametrize("case", ["bc9", "bc9t", "bc9m", "bc3d"])
 @pytest.mark.parametrize("implicit", [1, 0])
 def test_flow_bc_vs_reference(implicit, case):
     g = bc_case(case)
-    nVar = int(g["dims"][1])
+    nDim, nVar = int(g["dims"][0]), int(g["dims"][1])
+    F = nDim + 2
     N = len(g["V"])
     s, t = solvers(g, implicit)
     s.set_state(g)
@@ -72,8 +75,8 @@ def test_flow_bc_vs_reference(implicit, case):
     s.BC()
     s.sync()
     R = s.download("RES").reshape(N, nVar)
-    per_column_close(R[:, :4], g["bc_res"][:, :4], what="residual after BCs, flow rows")
-    assert_close(R[:, 4:], g["bc_res"][:, 4:], floor=1.0, what="residual after BCs, species rows")
+    per_column_close(R[:, :F], g["bc_res"][:, :F], what="residual after BCs, flow rows")
+    assert_close(R[:, F:], g["bc_res"][:, F:], floor=1.0, what="residual after BCs, species rows")
     if implicit:
         J = rows(g, s.download("JAC"), nVar)
         assert_close(J, g["bc_bsr"], rtol=1e-10, floor=1e-9, what="boundary Jacobian rows")
@@ -83,7 +86,7 @@ def test_flow_bc_vs_reference(implicit, case):
         iso = np.nonzero(g["bc_marker"][:, 0] == g["bc_params"][13])[0]
         for i in np.unique(g["bvertex"][np.isin(g["bvertex"][:, 0], iso), 1]):
             for k in range(rp[i], rp[i + 1]):
-                for r in (1, 2):
+                for r in range(1, nDim + 1):
                     want = np.zeros(nVar)
                     if g["bsr_col"][k] == i:
                         want[r] = 1.0
@@ -91,7 +94,7 @@ def test_flow_bc_vs_reference(implicit, case):
     s.close()
 
 
-@pytest.mark.parametrize("case", ["bc9", "bc9t", "bc9m"])
+@pytest.mark.parametrize("case", ["bc9", "bc9t", "bc9m", "bc3d"])
 def test_sst_bc_vs_reference(case):
     g = bc_case(case)
     N = len(g["V"])
@@ -136,23 +139,38 @@ def load_iteration_state(g, s, t, k):
     t.set_state(T, g["wall_distance"], f1, f2, cd)
 
 
+def iter_floor(g):
+    """Elementwise relative error with a floor of 1e-3 x the column max in 2-D. In 3-D the spanwise / wall-normal
+    momentum columns hold entries 1e4 below their column max, into which FGMRES mixes the rounding of the large
+    columns (the CPU oracle itself is 8e-10 elementwise off the reference there, 4e-12 column-relative), so 3-D
+    iterations are compared relative to each column's max."""
+    return 1e-3 if int(g["dims"][0]) == 2 else 1.0
+
+
 def check_iteration(g, s, t, k, rms, rms_t, tol):
     N = len(g["it_U0"])
     p = f"it{k}_"
-    per_column_close(s.download("U").reshape(N, -1), g[p + "U"], rtol=tol, floor=1e-3, what=f"{p}U")
-    per_column_close(s.download("V").reshape(N, -1), g[p + "V"], rtol=tol, floor=1e-3, what=f"{p}V")
-    per_column_close(t.download("U").reshape(N, 2), g[p + "sst"], rtol=tol, floor=1e-3, what=f"{p}(k, omega)")
-    assert_close(t.download("MUT"), g[p + "mut"], rtol=tol, floor=1e-3, what=f"{p}mu_t")
+    fl = iter_floor(g)
+    per_column_close(s.download("U").reshape(N, -1), g[p + "U"], rtol=tol, floor=fl, what=f"{p}U")
+    per_column_close(s.download("V").reshape(N, -1), g[p + "V"], rtol=tol, floor=fl, what=f"{p}V")
+    per_column_close(t.download("U").reshape(N, 2), g[p + "sst"], rtol=tol, floor=fl, what=f"{p}(k, omega)")
+    assert_close(t.download("MUT"), g[p + "mut"], rtol=tol, floor=fl, what=f"{p}mu_t")
     assert_close(rms, g[p + "rms"], rtol=tol, what=f"{p}RMS flow")
     assert_close(rms_t, g[p + "sst_rms"], rtol=tol, what=f"{p}RMS SST")
 
 
-def test_outer_iterations_vs_reference():
-    """Each of three whole reference iterations (flow + SST, boundary conditions included) on the device, started
-    from the reference's own state before it: U, V, (k, omega), mu_t, RMS within 1e-10 relative per column."""
-    g = golden("it9")
+def n_iters(g):
+    return sum(1 for k in g if k.startswith("it") and k.endswith("_U") and k[2:-2].isdigit())
+
+
+@pytest.mark.parametrize("case", ["it9", "it3d"])
+def test_outer_iterations_vs_reference(case):
+    """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d: 2) on the device,
+    started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within 1e-10 relative per
+    column."""
+    g = golden(case)
     s, t = solvers(g, 1)
-    for k in range(3):
+    for k in range(n_iters(g)):
         load_iteration_state(g, s, t, k)
         rms, rms_t, _ = rx.Iterate(s, t, ext_iter=k)
         s.sync()
@@ -160,25 +178,27 @@ def test_outer_iterations_vs_reference():
     s.close()
 
 
-def test_free_running_iterations_vs_reference():
+@pytest.mark.parametrize("case", ["it9", "it3d"])
+def test_free_running_iterations_vs_reference(case):
     """Two iterations chained on the device. The reference's viscous Jacobian is discontinuous at the last bit where
     a mass fraction tends to 1 (Ds = (1 - X_s) / sum_b X_b / D_bs, numerics_direct_reactive.cpp:1578-1588: a pure-O2
     wall point flips between Ds = 0 and Ds ~ 1e21 with the last bit of X_O2), so chained trajectories are compared
-    over the iterations before such a flip."""
-    g = golden("it9")
+    over the iterations before such a flip (it3d: the first)."""
+    g = golden(case)
     s, t = solvers(g, 1)
     load_iteration_state(g, s, t, 0)
-    for k in range(2):
+    for k in range(2 if case == "it9" else 1):
         rms, rms_t, _ = rx.Iterate(s, t, ext_iter=k)
         s.sync()
         check_iteration(g, s, t, k + 1, rms, rms_t, 1e-10)
     s.close()
 
 
-def test_outer_iteration_vs_oracle_device_order():
+@pytest.mark.parametrize("case", ["it9", "it3d"])
+def test_outer_iteration_vs_oracle_device_order(case):
     """One iteration against the oracle run with the device's inner-product order: the residual side and the
     Krylov recurrence then agree to the Stefan-Maxwell rounding only (amplified by FGMRES: the same 1e-10 bar)."""
-    g = golden("it9")
+    g = golden(case)
     N = len(g["it_U0"])
     s, t = solvers(g, 1)
     load_iteration_state(g, s, t, 0)
@@ -187,7 +207,7 @@ def test_outer_iteration_vs_oracle_device_order():
     from tests.test_oracle_bc import iteration_cfg
     cfg, bc, st = iteration_cfg(g)
     with O.dot_order("device"):
-        o = O.outer_iteration(O.Mechanism(g), 2, g, st, bc, cfg, 0, (g["bsr_row_ptr"], g["bsr_col"]))
-    per_column_close(s.download("U").reshape(N, -1), o["U"], rtol=1e-10, floor=1e-3, what="U vs oracle")
-    per_column_close(t.download("U").reshape(N, 2), o["T"], rtol=1e-10, floor=1e-3, what="(k, omega) vs oracle")
+        o = O.outer_iteration(O.Mechanism(g), int(g["dims"][0]), g, st, bc, cfg, 0, (g["bsr_row_ptr"], g["bsr_col"]))
+    per_column_close(s.download("U").reshape(N, -1), o["U"], rtol=1e-10, floor=iter_floor(g), what="U vs oracle")
+    per_column_close(t.download("U").reshape(N, 2), o["T"], rtol=1e-10, floor=iter_floor(g), what="(k, omega) vs oracle")
     s.close()

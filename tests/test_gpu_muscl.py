@@ -12,9 +12,10 @@ from tests.test_oracle_muscl import muscl_loop
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("case", ["jet9w", "muscl3d"])
 @pytest.mark.parametrize("implicit", [1, 0])
-def test_muscl_loop_vs_reference(implicit):
-    g = golden("jet9w")
+def test_muscl_loop_vs_reference(implicit, case):
+    g = golden(case)
     s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=implicit, spatial_order=2)
     s.upload("GRAD", g["grad_prim"])
     s.upload("LIMITER", g["limiter_out"])
@@ -22,7 +23,7 @@ def test_muscl_loop_vs_reference(implicit):
     s.Upwind_Residual()
     s.sync()
     R = s.download("RES").reshape(-1, nVar)
-    ii = np.nonzero(g["interior"])[0]
+    ii = np.nonzero(g["interior"])[0] if "interior" in g else np.arange(len(g["V"]))
     assert np.array_equal(R[ii], g["muscl_loop_res"][ii])
     if implicit:
         rp, col = s.bsr_pattern()

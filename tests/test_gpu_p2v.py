@@ -4,7 +4,8 @@ residual) against the oracle. Requires an MI355X.
 
 Bars: the primitive record, dP/dU, dT/dU, mu, kappa, eddy viscosity and the clamped U bitwise (same IEEE
 operations; the mechanism's pow/sqrt/cbrt constants are evaluated on the host with the reference's libm);
-Dij within 1e-14 (device pow(T, 1.75))."""
+Dij within 1e-14 and bitwise at >= 99 % of the points (the device's correctly rounded T^1.75 against the host
+libm's pow, itself misrounded at ~0.07 % of temperatures)."""
 import numpy as np
 import pytest
 
@@ -16,7 +17,7 @@ from tests.test_gpu_parity import golden, make_solver
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("case", ["mini9", "jet9w"])
+@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d"])
 def test_set_primitive_vs_reference(case):
     g = golden(case)
     s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=True)
@@ -31,7 +32,9 @@ def test_set_primitive_vs_reference(case):
                         ("MU", "p2v_mu", (N,)), ("KAPPA", "p2v_kappa", (N,)), ("EDDY", "p2v_eddy", (N,)),
                         ("U", "p2v_U_after", (N, nVar))):
         assert np.array_equal(s.download(f).reshape(shape), g[k]), f
-    assert_close(s.download("DIJ").reshape(N, ns, ns), g["p2v_Dij"], rtol=1e-14, what="Dij")
+    D = s.download("DIJ").reshape(N, ns, ns)
+    assert_close(D, g["p2v_Dij"], rtol=1e-14, what="Dij")
+    assert np.mean(np.all(D == g["p2v_Dij"], axis=(1, 2))) >= 0.99, "Dij bitwise"
     s.close()
 
 

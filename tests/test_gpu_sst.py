@@ -20,8 +20,8 @@ MESH_KEYS = ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr", "bvert
              "wall_distance")
 
 
-def golden_solvers(prec):
-    g = dict(np.load(os.path.join(GOLD, "mini9.npz")))
+def golden_solvers(prec, case="mini9"):
+    g = dict(np.load(os.path.join(GOLD, case + ".npz")))
     mesh = {k: g[k] for k in MESH_KEYS}
     kw = dict(mach_inf=float(g["mach_inf"][0]), prandtl_turb=float(g["visc_params"][1]),
               lewis_turb=float(g["visc_params"][2]), c_mu=float(g["src_params"][0]), pasr_lb=float(g["src_params"][1]))
@@ -34,16 +34,18 @@ def golden_solvers(prec):
     return g, s, t
 
 
+@pytest.mark.parametrize("case", ["mini9", "mini3d"])
 @pytest.mark.parametrize("prec", ["lusgs", "ilu"])
-def test_sst_iteration_vs_reference(prec):
-    g, s, t = golden_solvers(prec)
+def test_sst_iteration_vs_reference(prec, case):
+    g, s, t = golden_solvers(prec, case)
     N = len(g["V"])
+    nDim = int(g["dims"][0])
     s.SetStrainMag()
     s.sync()
     assert_close(s.download("STRAIN"), g["strain_mag"], rtol=1e-14, what="StrainMag")
     t.Preprocessing()
     t.sync()
-    assert np.array_equal(t.download("GRAD").reshape(N, 2, 2), g["sst_grad_ls"]), "LS gradient of (k, omega)"
+    assert np.array_equal(t.download("GRAD").reshape(N, 2, nDim), g["sst_grad_ls"]), "LS gradient of (k, omega)"
     t.Upwind_Residual()
     t.sync()
     assert np.array_equal(t.download("RES").reshape(N, 2), g["sst_loop_upw_res"]), "upwind loop"
@@ -75,7 +77,7 @@ def test_sst_iteration_vs_reference(prec):
     assert np.array_equal(s.download("TKE"), T[:, 0]) and np.array_equal(s.download("OMEGA"), T[:, 1])
     assert np.array_equal(s.download("MUT"), t.download("MUT"))
     assert np.array_equal(s.download("EDDY"), t.download("MUT"))
-    assert np.array_equal(s.download("GRADK").reshape(N, 2), t.download("GRAD").reshape(N, 2, 2)[:, 0])
+    assert np.array_equal(s.download("GRADK").reshape(N, nDim), t.download("GRAD").reshape(N, 2, nDim)[:, 0])
     s.close()
 
 
