@@ -51,6 +51,10 @@ WORKLOADS = {
     "c1": dict(nx=100, ny=90, ns=4, desc="configs[0]: 2-D jet 100x90, 4 species"),
     "c2": dict(nx=500, ny=200, ns=7, desc="configs[1]: 2-D reactive jet 500x200 (100k cells), implicit FGMRES+ILU0"),
     "c3": dict(nx=2000, ny=500, ns=7, desc="configs[2]: 2-D reactive jet 2000x500 (1M cells), 7 species PaSR+SST"),
+    # configs[4] (3-D extruded jet 1000x400x20 = 8M cells over 8 GPUs): one GPU's share, 1000x50x20 = 1M cells;
+    # --gpus N runs the N-times-taller slab (N = 8: the whole C5 mesh)
+    "c5": dict(nx=1000, ny=50, nz=20, ns=7,
+               desc="configs[4]: 3-D extruded jet, 7 species, implicit; 1000x50x20 per GPU (8 GPUs: 1000x400x20)"),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFS = 78.6       # MI355X FP64 vector spec
@@ -62,7 +66,7 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
     nVar, nPV, nG = ns + nDim + 2, ns + nDim + 5, ns + nDim + 2
     d = 8
     blk = nVar * nVar * d
-    summ = (24 + 9 * ns) * d
+    summ = (14 + 5 * nDim + 9 * ns) * d  # visc_summary_size<NS, NDIM>
     hbm = lambda b, name: dict(bound="hbm", work=float(b), unit="GB/s", peak=HBM_PEAK_GBS, kernel=name)
     return {
         # k_ausm_edge: V (nPV) and dPdU (nVar) per node once; edge (2 int32 + normal); flux + 2 Jacobians
@@ -97,9 +101,9 @@ def pmc_traffic(kernel, workload_key):
     return None if k is None else k.get("hbm_bytes")
 
 
-def build_workload(nx, ny, ns, n_part=1):
+def build_workload(nx, ny, ns, n_part=1, nz=0):
     from tests.rxpkg import synth
-    mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=ns, n_part=n_part)
+    mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=ns, n_part=n_part, nz=nz)
     return mesh, st, mech, kw
 
 
@@ -114,28 +118,19 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
              pasr_lb=cfg.pasr_lb, lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter, relaxation=cfg.relaxation)
     N = len(st["V"])
     pattern = O.bsr_pattern(N, mesh["edges"])
+    nDim = int(np.shape(mesh["coord"])[1])
     if bc is not None:
-        from tests.rxpkg import synth
-        bp = np.asarray(dict(np.load(os.path.join(ROOT, "tests", "golden", "bc9.npz")))["bc_params"])
-        md = np.array(bc["data"], dtype=np.float64)
-        md[:, 0] = [{1: bp[11], 2: bp[12], 3: bp[13]}.get(int(k), -1.0) for k in bc["kind"]]
-        mesh_o = dict(mesh, bvertex=np.c_[np.asarray(mesh["bvertex"])[:, :2], np.zeros(len(mesh["bvertex"]))])
-        bco = dict(marker=md, prm=O.bc_prm(bp, cfg.mach_inf, cfg.prandtl_turb, cfg.lewis_turb))
-        c.update(p2v=[cfg.t_min, cfg.t_max, cfg.T_ref, cfg.E_ref, cfg.R_ref, cfg.p_ref, cfg.visc_ref, cfg.cond_ref,
-                      cfg.vel_ref, cfg.len_ref, 0.0, float(cfg.clip_temp)])
-        T = np.ascontiguousarray(st["sst_sol"])
-        state = dict(U=st["U"], V=st["V"], Uold=st["U"], T=T, TG=O.sol_grad_ls(2, mesh["coord"], T, mesh["nbr_ptr"],
-                                                                             mesh["nbr"]),
-                     F1=st["sst_F1"], F2=st["sst_F2"], CDkw=st["sst_CDkw"], mut=st["mu_t"])
+        from tests.oracle_inputs import outer_iteration_inputs
+        mesh_o, state, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
         t0 = time.perf_counter()
-        O.outer_iteration(om, 2, mesh_o, state, bco, c, 0, pattern, part_ptr=mesh.get("part_ptr"))
+        O.outer_iteration(om, nDim, mesh_o, state, bco, c, 0, pattern, part_ptr=mesh.get("part_ptr"))
         what = "1 reference outer iteration (flow + SST, jet boundary conditions)"
     else:
         t0 = time.perf_counter()
-        _, info = O.implicit_step(om, 2, ns, mesh, st, c, pattern=pattern, part_ptr=mesh.get("part_ptr"))
+        _, info = O.implicit_step(om, nDim, ns, mesh, st, c, pattern=pattern, part_ptr=mesh.get("part_ptr"))
         flow = dict(V=st["V"], grad=info["grad"], mu=st["mu"], eddy=st["eddy_visc_flow"],
-                    strain=O.strain_mag(2, info["grad"]))
-        O.sst_step(2, mesh, flow, st["sst_sol"], None, st["sst_F1"], st["sst_F2"], st["sst_CDkw"], info["dt"],
+                    strain=O.strain_mag(nDim, info["grad"]))
+        O.sst_step(nDim, mesh, flow, st["sst_sol"], None, st["sst_F1"], st["sst_F2"], st["sst_CDkw"], info["dt"],
                    dict(lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter), pattern=pattern, part_ptr=mesh.get("part_ptr"))
         what = "1 outer iteration (flow implicit step + SST step, no boundary conditions)"
     dt = time.perf_counter() - t0
@@ -143,10 +138,10 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
                 sample=f"{what} of the same {N}-cell mesh on 1 host core ({dt:.2f} s)")
 
 
-def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist):
+def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist, nz=0):
     """Build the rank's shard of the N-times-taller jet and attach the RCCL communicator."""
     from tests.rxpkg import meshgen, synth
-    mesh, st, mech_arrays, kw = build_workload(nx, ny * world, ns, args.parts * world)
+    mesh, st, mech_arrays, kw = build_workload(nx, ny * world, ns, args.parts * world, nz)
     sh = meshgen.shard(mesh, world, rank)
     st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
     if args.cfl:
@@ -175,6 +170,7 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--nx", type=int, default=0)
     ap.add_argument("--ny", type=int, default=0)
+    ap.add_argument("--nz", type=int, default=0, help="z planes of the 3-D extrusion (c5)")
     ap.add_argument("--species", type=int, default=0)
     ap.add_argument("--parts", type=int, default=256,
                     help="partitions (= the reference's MPI ranks) of the ILU(0)/LU-SGS preconditioner")
@@ -201,6 +197,8 @@ def main():
 
     wl = dict(WORKLOADS[args.workload])
     nx, ny, ns = args.nx or wl["nx"], args.ny or wl["ny"], args.species or wl["ns"]
+    nz = args.nz or wl.get("nz", 0)
+    nDim = 3 if nz > 1 else 2
     s = None
     parallelism = "1 GPU"
     n_owned = 0
@@ -208,7 +206,7 @@ def main():
         err = ""
         try:
             s, t, mesh, st, mech_arrays, kw, cfg, n_owned = setup_sharded(rx, args, nx, ny, ns, world, rank, local,
-                                                                          dist)
+                                                                          dist, nz)
             set_states(s, t, mesh, st)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             err = repr(e)[:200]
@@ -223,7 +221,7 @@ def main():
         else:
             parallelism = f"sharded x{world} (RCCL halo exchange + all-reduce)"
     if s is None:
-        mesh, st, mech_arrays, kw = build_workload(nx, ny, ns, args.parts)
+        mesh, st, mech_arrays, kw = build_workload(nx, ny, ns, args.parts, nz)
         if args.cfl:
             kw["cfl"] = args.cfl
         cfg = rx.default_cfg(implicit=1, rans=1, lin_prec=1, lin_iter=5, **kw)
@@ -308,9 +306,10 @@ def main():
     s.profile(False)
     t.profile(False)
 
-    models = kernel_models(N, E, nnzb, ns, 2, 5)
+    models = kernel_models(N, E, nnzb, ns, nDim, 5)
     phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0}
-    wkey = f"{args.workload} {nx}x{ny} ns{ns} parts{args.parts}"
+    dims = f"{nx}x{ny}" + (f"x{nz}" if nz > 1 else "")
+    wkey = f"{args.workload} {dims} ns{ns} parts{args.parts}"
 
     def roof(k):
         ms, n = prof[k]
@@ -354,13 +353,14 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference jet geometry; node records resampled from the reference PaSR jet state)",
-        "config": {"workload": f"{args.workload}: 2-D reactive jet {nx}x{ny}" + (
-                       f" per GPU (global {nx}x{ny * world})" if parallelism.startswith("sharded") else ""),
+        "config": {"workload": f"{args.workload}: {nDim}-D reactive jet {dims}" + (
+                       f" per GPU (global {nx}x{ny * world}" + (f"x{nz})" if nz > 1 else ")")
+                       if parallelism.startswith("sharded") else ""),
                    "cells_per_gpu": n_owned, "halo_points": N - n_owned, "edges": E,
-                   "species": ns, "nVar": ns + 4, "nnz_blocks": nnzb,
+                   "species": ns, "nVar": ns + nDim + 2, "nnz_blocks": nnzb,
                    "time": "EULER_IMPLICIT flow + SST (one reference outer iteration per step" +
                            (", no boundary conditions)" if args.no_bc else ", jet boundary conditions)"),
-                   "linear_solver": "FGMRES(5)+ILU0 (flow 11x11 and SST 2x2 systems)",
+                   "linear_solver": f"FGMRES(5)+ILU0 (flow {ns + nDim + 2}x{ns + nDim + 2} and SST 2x2 systems)",
                    "partitions": args.parts,
                    "parallelism": parallelism, "solve_graph": graph, "cells_total": cells,
                    "lin_iters_mean": float(np.mean([a for a, _ in lin_its[-args.steps:]])),

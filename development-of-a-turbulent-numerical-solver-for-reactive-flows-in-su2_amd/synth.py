@@ -69,18 +69,33 @@ def species_subset(g, keep, nDim=2):
     return out
 
 
-def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1):
-    """Mesh (RCM-ordered median dual) + node records for an nx x ny jet with 9 (reference-native), 7
-    or 4 species."""
+def lift_records_3d(g):
+    """2-D node records as 3-D records of a spanwise-uniform flow: w = 0 inserted after v in V, U, dP/dU and dT/dU
+    (dP/d(rho w) = -(gamma - 1) w = 0 and dT/d(rho w) = -w / (rho c_v) = 0 at w = 0), a zero third component of the
+    TKE gradient; every other record (rho E included, the kinetic energy being unchanged) stays the reference's."""
+    out = dict(g)
+    for k in ("V", "U", "dPdU", "dTdU"):
+        a = np.asarray(g[k])
+        out[k] = np.concatenate([a[:, :3], np.zeros((len(a), 1)), a[:, 3:]], axis=1)
+    gk = np.asarray(g["grad_k"])
+    out["grad_k"] = np.concatenate([gk, np.zeros((len(gk), 1))], axis=1)
+    return out
+
+
+def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1, nz=0):
+    """Mesh (RCM-ordered median dual) + node records for an nx x ny jet (nz > 1: the 3-D extrusion over nz planes)
+    with 9 (reference-native), 7 or 4 species."""
     mg = _meshgen()
-    mesh = mg.build_jet(nx, ny, n_part=n_part)
+    mesh = mg.build_jet(nx, ny, n_part=n_part, nz=nz)
     g = load_records(records)
     if n_species != int(g["mech_n_species"]):
         g = species_subset(g, np.arange(n_species))
+    if nz > 1:
+        g = lift_records_3d(g)
     src = g["coord"]
     lo, hi = src.min(axis=0), src.max(axis=0)
     sn = (src - lo) / np.where(hi > lo, hi - lo, 1.0)
-    dst = mesh["coord"]
+    dst = mesh["coord"][:, :2]  # records sampled by (x, y); spanwise-uniform in 3-D
     dlo, dhi = dst.min(axis=0), dst.max(axis=0)
     dn = (dst - dlo) / np.where(dhi > dlo, dhi - dlo, 1.0)
     rng = np.random.default_rng(seed)
@@ -89,7 +104,7 @@ def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1):
     _, idx = cKDTree(sn).query(dn)
     state = {k: np.ascontiguousarray(g[k][idx]) for k in NODE_KEYS if k in g}
     state["sst_sol"] = np.ascontiguousarray(np.stack([state["turb_k"], state["turb_omega"]], axis=1))
-    mesh["n_dim"] = 2
+    mesh["n_dim"] = 3 if nz > 1 else 2
     mech = {k: g[k] for k in g if k.startswith("mech_")}
     return mesh, state, mech, {"mach_inf": float(g["mach_inf"][0]), "prandtl_turb": float(g["visc_params"][1]),
                                "lewis_turb": float(g["visc_params"][2]), "c_mu": float(g["src_params"][0]),
@@ -117,10 +132,11 @@ def jet_bc(mesh, n_species):
     mg = _meshgen()
     g = dict(np.load(os.path.join(GOLDEN, "bc9.npz")))
     bp = g["bc_params"]
-    kinds = {"inlet": 1, "outlet": 2, "isothermal": 3}
+    kinds = {"inlet": 1, "outlet": 2, "isothermal": 3, "symmetry": 0}  # MARKER_SYM: no action (BC_Sym_Plane)
     rows, kk = [], []
-    for name in mg.MARKERS:
-        kind, a, b, d, sp = JET_MARKERS[name]
+    names = mg.MARKERS3 if np.shape(mesh["coord"])[1] == 3 else mg.MARKERS
+    for name in names:
+        kind, a, b, d, sp = JET_MARKERS.get(name, ("symmetry", 0.0, 0.0, (0.0, 0.0, 0.0), None))
         y = np.zeros(n_species)
         if sp is not None:
             y[SPECIES_ORDER.index(sp)] = 1.0

@@ -211,3 +211,38 @@ def test_outer_iteration_vs_oracle_device_order(case):
     per_column_close(s.download("U").reshape(N, -1), o["U"], rtol=1e-10, floor=iter_floor(g), what="U vs oracle")
     per_column_close(t.download("U").reshape(N, 2), o["T"], rtol=1e-10, floor=iter_floor(g), what="(k, omega) vs oracle")
     s.close()
+
+
+@pytest.mark.parametrize("nz", [0, 4])
+def test_synthetic_jet_iteration_vs_oracle(nz):
+    """rx.Iterate with the jet's boundary conditions on a partitioned synthetic jet with the C2/C5 mechanism
+    (7 species; nz = 4: the 3-D extrusion with symmetry planes) against O.outer_iteration in the device's
+    inner-product order: U and (k, omega) within 1e-10 of each column's max (FGMRES-amplified rounding of the
+    Stefan-Maxwell solve, as in test_outer_iteration_vs_oracle_device_order)."""
+    from tests.oracle_inputs import outer_iteration_inputs
+    from tests.rxpkg import synth
+    mesh, st, mech, kw = synth.jet_case(24, 10, n_species=7, n_part=4, nz=nz)
+    cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
+    bc = synth.jet_bc(mesh, 7)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
+    s.set_bc(bc)
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+    s.set_state(st)
+    t.set_state(st["sst_sol"], mesh["wall_distance"], st["sst_F1"], st["sst_F2"], st["sst_CDkw"])
+    N = len(st["V"])
+    mesh_o, state, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
+    # the reference state at an iteration start: grad k = the LS gradient of the turbulent solution, sigma_k =
+    # CTurbSSTVariable::Get_Sigmak (constants[0])
+    s.upload("GRADK", np.ascontiguousarray(state["TG"][:, 0, :]))
+    s.upload("SIGMAK", np.full(N, 0.85))
+    rms, rms_t, its = rx.Iterate(s, t, ext_iter=0)
+    s.sync()
+    pat = O.bsr_pattern(N, mesh["edges"])
+    with O.dot_order("device"):
+        o = O.outer_iteration(O.Mechanism(mech), 3 if nz else 2, mesh_o, state, bco, c, 0, pat,
+                              part_ptr=mesh["part_ptr"])
+    assert its[0] == o["lin_iters"]
+    per_column_close(s.download("U").reshape(N, -1), o["U"], rtol=1e-10, floor=1.0, what="U vs oracle")
+    per_column_close(t.download("U").reshape(N, 2), o["T"], rtol=1e-10, floor=1.0, what="(k, omega) vs oracle")
+    assert_close(rms, o["rms"], rtol=1e-10, what="RMS")
+    s.close()
