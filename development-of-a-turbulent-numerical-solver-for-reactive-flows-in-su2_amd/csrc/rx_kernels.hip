@@ -702,9 +702,12 @@ __global__ __launch_bounds__(128) void k_source(int N, const double* __restrict_
 //   R  = 0 + conv(edge order) - visc(edge order) + source
 //   Aii = 0 + conv(edge order) + visc(edge order) + source     (AddVal2Diag comes later)
 //   A(n0,n1) = (0 + Jc_j) - Jv_j ;  A(n1,n0) = (0 - Jc_i) + Jv_i
+// Team = one or two whole wavefronts up to nVar = 11; above, exactly nVar^2 lanes (no intra-team synchronisation:
+// teams may straddle wavefronts), so nVar = 12 / 13 / 14 do not idle 112 / 87 / 60 of 256 lanes (C5 assembly
+// 10.0 -> 7.9 ms).
 template <int NVAR>
 constexpr int asm_team() {
-  return NVAR * NVAR <= 64 ? 64 : (NVAR * NVAR <= 128 ? 128 : 256);
+  return NVAR * NVAR <= 64 ? 64 : (NVAR * NVAR <= 128 ? 128 : NVAR * NVAR);
 }
 template <int NVAR>
 __global__ __launch_bounds__(kBlock) void k_assemble(int N, const int32_t* __restrict__ adj_ptr,
