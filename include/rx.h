@@ -69,7 +69,8 @@ typedef struct {
 } rx_mech_desc;
 
 /* Dual grid (CGeometry edges / dual volumes / boundary vertices). Edge order is the reference's
- * (i < j), normals oriented i -> j. nbr = point neighbour lists in the reference's order. */
+ * (i < j), normals oriented i -> j. nbr = point neighbour lists in the reference's order.
+ * n_dim 2 or 3 (3-D flow contexts: 7 or 9 species; node records then carry w / rho w after v / rho v). */
 typedef struct {
   int32_t n_dim;
   int64_t n_point, n_edge, n_bvert;
@@ -245,7 +246,9 @@ int rx_sst_postprocessing(rx_ctx *turb);
  * (numerics_direct_reactive.cpp:478-648, a8) and CUpwSca_TurbSST + CAvgGrad_TurbSST. Marker m of a mesh bvert is
  * rx_mesh_desc.bvert[2b]. data rows [n_marker][6 + Ns]: inlet (Ttotal | density | T, Ptotal | velocity, flow
  * direction[3], mass fractions[Ns]) as MARKER_INLET / INLET_MASS_FRAC, outlet (back pressure), isothermal (wall
- * temperature). */
+ * temperature). RX_BC_NONE: a marker with no action — MARKER_SYM, which the reactive and turbulent solvers leave to
+ * the empty CSolver::BC_Sym_Plane (solver_structure.inl:731-732) / CTurbSolver::BC_Sym_Plane
+ * (solver_direct_turbulent.cpp:602-606); its vertices still enter SetTime_Step through rx_mesh_desc. */
 typedef enum { RX_BC_NONE = 0, RX_BC_INLET = 1, RX_BC_OUTLET = 2, RX_BC_ISOTHERMAL = 3 } rx_bc_kind;
 typedef enum { RX_INLET_TOTAL_CONDITIONS = 0, RX_INLET_MASS_FLOW = 1, RX_INLET_TEMPERATURE_IMPOSE = 2 } rx_inlet_kind;
 typedef struct {
