@@ -99,7 +99,8 @@ WRT_CON_FREQ= 1
 """
 
 
-def read_plot(path):
+def read_plot(path, ncons=15):
+    """(coords, conservatives + k + omega) per node of a Tecplot POINT file (ncons columns after x, y)."""
     rows = []
     with open(path) as f:
         for line in f:
@@ -110,10 +111,10 @@ def read_plot(path):
                 vals = [float(x) for x in t]
             except ValueError:
                 continue
-            if len(vals) >= 17:
+            if len(vals) >= 2 + ncons:
                 rows.append(vals)
     a = np.array(rows)
-    return a[:, :2], a[:, 2:17]  # coords, 13 flow conservatives + k + omega
+    return a[:, :2], a[:, 2:2 + ncons]
 
 
 # INLET_TYPE variants: (a, b) of MARKER_INLET per inlet — TEMPERATURE_IMPOSE (T, |u|) as the shipped jet cfgs,
@@ -161,9 +162,9 @@ def run_harness(wd, bsr, extra=None):
     return arrays
 
 
-def mech_arrays():
+def mech_arrays(case_dir=None, list_file="test_chem_second.txt"):
     mech = _load("rx_oracle_mech", os.path.join(HERE, "mech.py"))
-    m = mech.load_mechanism(CASE_DIR, "test_chem_second.txt")
+    m = mech.load_mechanism(case_dir or CASE_DIR, list_file)
     return {"mech_" + k: v for k, v in m.items()}
 
 
@@ -394,7 +395,91 @@ def case_jet9w():
     T = a["V"][:, 0]
     c = coord[np.argmax(T)]
     box = (np.abs(coord[:, 0] - c[0]) < 0.008) & (np.abs(coord[:, 1] - c[1]) < 0.0025)
-    keep = np.nonzero(box)[0]
+    out = window_case(a, np.nonzero(box)[0])
+    out.update(mech_arrays())
+    return out
+
+
+FP_DIR = os.path.join(REF, "Test_Cases/TURBOLENT/TURBOLENT_FLAT_PLATE")
+FP_CFG = """\
+% golden-vector cfg written by oracle/make_golden.py: the reference's turbulent flat plate (air, 3 species, no
+% reactions; values of Test_Cases/TURBOLENT/TURBOLENT_FLAT_PLATE/my_turbulent_flatplate_air.cfg)
+CONFIG_LIB_FILE = test_air.txt
+FREESTREAM_MASS_FRAC = (0.2197, 0.0302, 0.7501)
+SPECIES_ORDER = (O2, CO2, N2)
+PHYSICAL_PROBLEM= REACTIVE_NAVIER_STOKES
+KIND_TURB_MODEL= SST
+MATH_PROBLEM= DIRECT
+RESTART_SOL= NO
+MACH_NUMBER= 0.2
+FREESTREAM_TEMPERATURE= 297.62
+FREESTREAM_VELOCITY= (69.1687, 0.0, 0.0)
+FREESTREAM_PRESSURE= 113303.0
+REYNOLDS_LENGTH= 1.000
+REYNOLDS_NUMBER= 500000
+REF_DIMENSIONALIZATION= DIMENSIONAL
+REF_LENGTH= 1.0
+REF_AREA= 2.00
+MARKER_HEATFLUX = (wall, 0.0)
+MARKER_EULER= ( symmetry )
+MARKER_INLET= ( inlet, 300.0, 100000.0, 1.0, 0.0, 0.0 )
+INLET_MASS_FRAC = (inlet, 0.2197, 0.0302, 0.7501)
+MARKER_OUTLET= ( outlet, 97250.0, farfield, 97250.0 )
+NUM_METHOD_GRAD= WEIGHTED_LEAST_SQUARES
+CFL_NUMBER= 9
+CFL_ADAPT= NO
+EXT_ITER= 1
+LINEAR_SOLVER= FGMRES
+LINEAR_SOLVER_PREC= LU_SGS
+LINEAR_SOLVER_ERROR= 1E-6
+LINEAR_SOLVER_ITER= 5
+MGLEVEL= 0
+CONV_NUM_METHOD_FLOW= AUSM
+SPATIAL_ORDER_FLOW= 2ND_ORDER
+SLOPE_LIMITER_FLOW= VENKATAKRISHNAN
+TIME_DISCRE_FLOW= EULER_IMPLICIT
+CONV_NUM_METHOD_TURB= SCALAR_UPWIND
+SLOPE_LIMITER_TURB= VENKATAKRISHNAN
+TIME_DISCRE_TURB= EULER_IMPLICIT
+CONV_CRITERIA= RESIDUAL
+RESIDUAL_REDUCTION= 6
+RESIDUAL_MINVAL= -7
+MESH_FILENAME= mesh.su2
+MESH_FORMAT= SU2
+OUTPUT_FORMAT= TECPLOT
+CONV_FILENAME= history
+WRT_SOL_FREQ= 100000
+WRT_CON_FREQ= 1
+"""
+
+
+def case_fp3():
+    """The reference's own second test case: the 137x97 turbulent flat plate (air: O2, CO2, N2, no reactions) with
+    its converged state (PLOT/flow.dat), cfg SPATIAL_ORDER_FLOW = 2ND_ORDER (the unlimited MUSCL branch); a window
+    of the boundary layer at the leading edge is kept, as for jet9w."""
+    wd = "/tmp/rx_golden/fp3"
+    shutil.rmtree(wd, ignore_errors=True)
+    os.makedirs(os.path.join(wd, "out"))
+    for d in ("Mixture", "Thermo", "Transp"):
+        os.symlink(os.path.join(FP_DIR, d), os.path.join(wd, d))
+    os.symlink(os.path.join(FP_DIR, "test_air.txt"), os.path.join(wd, "test_air.txt"))
+    os.symlink(os.path.join(FP_DIR, "mesh_flatplate_turb_137x97.su2"), os.path.join(wd, "mesh.su2"))
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(FP_CFG)
+    xy, cons = read_plot(os.path.join(FP_DIR, "PLOT/flow.dat"), ncons=9)
+    write_state(wd, cons)
+    a = run_harness(wd, bsr=False)
+    coord = a["coord"]
+    box = (coord[:, 0] > -0.02) & (coord[:, 0] < 0.06) & (coord[:, 1] < 0.004)
+    out = window_case(a, np.nonzero(box)[0])
+    out.update(mech_arrays(FP_DIR, "test_air.txt"))
+    return out
+
+
+def window_case(a, keep):
+    """Restrict a whole-mesh harness dump to the points `keep` (and the edges between them); interior = points
+    whose whole neighbourhood is kept (where loop results are complete)."""
+    coord = a["coord"]
     loc = -np.ones(len(coord), dtype=np.int64)
     loc[keep] = np.arange(len(keep))
     e = a["edges"]
@@ -449,8 +534,6 @@ def case_jet9w():
     out["muscl_jac_rows"] = rs
     out["muscl_jac_cols"] = mc
     out["muscl_jac"] = mb
-    # limiter_out at window points needs neighbours' V/grad too: keep only interior as checked
-    out.update(mech_arrays())
     return out
 
 
@@ -465,7 +548,8 @@ def main():
     for case in args.cases.split(","):
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
-             "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d}[case]()
+             "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
+             "fp3": case_fp3}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

@@ -180,6 +180,11 @@ def load_mechanism(base_dir, list_file):
                     Ab[rr] *= 10.0 ** (6.0 * (1.0 - ep[rr].sum()))
         out.update(stoich_reac=sr, stoich_prod=sp, exp_reac=er, exp_prod=ep, A=A, beta=beta, Ta=Ta,
                    A_back=Ab, beta_back=betab, Ta_back=Tab, reversible=rev, has_backward=hasb)
+    else:  # no chemistry file (the flat plate's air): zero reactions
+        z = np.zeros(0)
+        out.update(stoich_reac=np.zeros((ns, 0)), stoich_prod=np.zeros((ns, 0)), exp_reac=np.zeros((0, ns)),
+                   exp_prod=np.zeros((0, ns)), A=z, beta=z, Ta=z, A_back=z, beta_back=z, Ta_back=z,
+                   reversible=np.zeros(0, dtype=np.int64), has_backward=np.zeros(0, dtype=np.int64))
     # --- per-species tables (transport file then thermo file for each species)
     off = 0 if has_chem else 1
     tabs = {}

@@ -12,13 +12,16 @@ from tests.test_oracle_muscl import muscl_loop
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("case", ["jet9w", "muscl3d"])
+@pytest.mark.parametrize("case", ["jet9w", "muscl3d", "fp3"])
 @pytest.mark.parametrize("implicit", [1, 0])
 def test_muscl_loop_vs_reference(implicit, case):
+    """jet9w / muscl3d: SECOND_ORDER_LIMITER; fp3 (the flat plate): SECOND_ORDER, no limiter."""
     g = golden(case)
-    s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=implicit, spatial_order=2)
+    order = int(g["muscl_params"][0])
+    s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=implicit, spatial_order=order)
     s.upload("GRAD", g["grad_prim"])
-    s.upload("LIMITER", g["limiter_out"])
+    if order == 2:
+        s.upload("LIMITER", g["limiter_out"])
     s.Preprocessing_zero()
     s.Upwind_Residual()
     s.sync()

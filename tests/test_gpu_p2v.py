@@ -17,7 +17,7 @@ from tests.test_gpu_parity import golden, make_solver
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d"])
+@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d", "fp3"])
 def test_set_primitive_vs_reference(case):
     g = golden(case)
     s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=True)

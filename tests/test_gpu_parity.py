@@ -45,7 +45,7 @@ def make_solver(g, implicit, lin_prec=1, cfl=None, spatial_order=0):
     return s, (nDim, nVar, nPV, nG, ns)
 
 
-@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d", "muscl3d"])
+@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d", "muscl3d", "fp3"])
 def test_gradient_and_limiter(case):
     g = golden(case)
     s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=False)
@@ -96,10 +96,11 @@ def test_explicit_residual_loops_and_time_step(case):
     s.close()
 
 
-def test_jet_window_edge_fluxes_vs_reference():
-    """Per-edge AUSM / viscous fluxes of the reference jet window, gathered per node by the HIP path,
-    against the same gather of the reference's own per-edge fluxes."""
-    g = golden("jet9w")
+@pytest.mark.parametrize("case", ["jet9w", "fp3"])
+def test_jet_window_edge_fluxes_vs_reference(case):
+    """Per-edge AUSM / viscous fluxes of the reference jet window (and of the flat-plate boundary-layer window),
+    gathered per node by the HIP path, against the same gather of the reference's own per-edge fluxes."""
+    g = golden(case)
     s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=False)
     N = len(g["V"])
     ref_c = np.zeros((N, nVar))

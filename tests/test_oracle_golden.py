@@ -5,6 +5,8 @@ Fixtures:
   mini9.npz  21x11 synthetic jet, 9 species, SST, implicit: every operator + whole loops + BSR.
   jet9w.npz  window of the reference's own 9000-point jet mesh around the flame, PaSR state.
   mini3d.npz the 3-D extruded jet (13x7x4 points, symmetry planes in z, spanwise velocity), mini9's dumps.
+  fp3.npz    window of the reference's second test case, the turbulent flat plate (air: 3 species, no
+             reactions), with its converged state; 2ND_ORDER (unlimited MUSCL).
 """
 import os
 
@@ -15,7 +17,7 @@ from oracle import oracle as O
 from tests.parity import assert_close
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-CASES = ["mini9", "jet9w", "mini3d"]
+CASES = ["mini9", "jet9w", "mini3d", "fp3"]
 
 
 def load(case):
@@ -32,6 +34,9 @@ def case(request):
 
 def test_mechanism_tables(case):
     name, g, dims, mech = case
+    if name == "fp3":  # air: O2, CO2, N2, no chemistry file
+        assert mech.ns == 3 and mech.nr == 0
+        return
     assert mech.ns == 9 and mech.nr == 2
     # CGS -> SI conversion of the first reaction (reacting_model_library.cpp:1123-1132)
     assert np.isclose(g["mech_A"][0], 8.80e11 * 1e-6)

@@ -35,15 +35,16 @@ def muscl_loop(g, edge_res, Ji, Jj):
     return R, J
 
 
-@pytest.mark.parametrize("case", ["jet9w", "muscl3d"])
+@pytest.mark.parametrize("case", ["jet9w", "muscl3d", "fp3"])
 def test_muscl_upwind_loop_bitwise(case):
-    """jet9w: the reference's 2-D jet window; muscl3d: the 3-D extruded jet, every point."""
+    """jet9w: the reference's 2-D jet window (2ND_ORDER_LIMITER); muscl3d: the 3-D extruded jet, every point;
+    fp3: the flat-plate window, 2ND_ORDER (no limiter)."""
     g = dict(np.load(os.path.join(GOLD, case + ".npz")))
     nDim, ns = int(g["dims"][0]), int(g["dims"][4])
-    assert int(g["muscl_params"][0]) == 2  # SECOND_ORDER_LIMITER
+    limited = int(g["muscl_params"][0]) == 2  # SECOND_ORDER_LIMITER (1: SECOND_ORDER)
     m = O.Mechanism(g)
     r, Ji, Jj = O.muscl_edges(m, nDim, g["edges"], g["edge_normal"], g["coord"], g["V"], g["dPdU"], g["grad_prim"],
-                              g["limiter_out"], g["muscl_params"][1:], g["mach_inf"][0], True)
+                              g["limiter_out"] if limited else None, g["muscl_params"][1:], g["mach_inf"][0], True)
     R, J = muscl_loop(g, r, Ji, Jj)
     ii = np.nonzero(g["interior"])[0] if "interior" in g else np.arange(len(g["V"]))
     assert np.array_equal(R[ii], g["muscl_loop_res"][ii])

@@ -13,7 +13,7 @@ KEYS = (("V", "p2v_V"), ("dPdU", "p2v_dPdU"), ("dTdU", "p2v_dTdU"), ("mu", "p2v_
         ("Dij", "p2v_Dij"), ("eddy", "p2v_eddy"), ("cp", "p2v_cp"), ("U", "p2v_U_after"))
 
 
-@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d"])
+@pytest.mark.parametrize("case", ["mini9", "jet9w", "mini3d", "fp3"])
 def test_set_primitive_bitwise(case):
     g = dict(np.load(os.path.join(GOLD, case + ".npz")))
     m = O.Mechanism(g)

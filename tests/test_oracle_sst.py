@@ -17,7 +17,7 @@ def load(case):
     return g, [int(x) for x in g["dims"]]
 
 
-@pytest.fixture(scope="module", params=["mini9", "jet9w", "mini3d"])
+@pytest.fixture(scope="module", params=["mini9", "jet9w", "mini3d", "fp3"])
 def case(request):
     g, dims = load(request.param)
     return request.param, g, dims
