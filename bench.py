@@ -12,7 +12,9 @@ them):
         Postprocessing (gradient, F1/F2/CDkw, mu_t, coupling fields the flow reads next step).
 
 Default workload (N=1): BASELINE configs[1] — synthetic 2-D reactive jet, 500x200 = 100k points,
-7 species PaSR + SST, implicit FGMRES+ILU0. `--workload c3` runs configs[2] (2000x500, 1M points).
+7 species PaSR + SST, implicit FGMRES+ILU0. `--workload c3` runs configs[2] (2000x500, 1M points);
+`--workload c5` one GPU's share of configs[4], the 3-D extruded jet (1000x50x20 = 1M points per GPU; with --gpus 8
+the slab is the whole 1000x400x20 mesh).
 Inputs are resident in HBM before the timed region. Data are synthetic: the mesh replicates the
 reference jet geometry, node records are resampled from the reference's converged PaSR jet state
 (tests/golden/jet9w.npz, see synth.py).
