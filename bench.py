@@ -11,13 +11,14 @@ them):
         ImplicitEuler_Iteration (system, ILU(0), FGMRES(5), conservative clipped update, RMS) ->
         Postprocessing (gradient, F1/F2/CDkw, mu_t, coupling fields the flow reads next step).
 
-Default workload (N=1): BASELINE configs[1] — synthetic 2-D reactive jet, 500x200 = 100k points,
-7 species PaSR + SST, implicit FGMRES+ILU0. `--workload c3` runs configs[2] (2000x500, 1M points);
-`--workload c5` one GPU's share of configs[4], the 3-D extruded jet (1000x50x20 = 1M points per GPU; with --gpus 8
-the slab is the whole 1000x400x20 mesh).
+Default workload (N=1): BASELINE configs[2], the north-star roofline run — synthetic 2-D reactive jet,
+2000x500 = 1M points, 7 species PaSR + SST, implicit FGMRES+ILU0. `--workload c2` runs configs[1]
+(500x200, 100k points); `--workload c5` one GPU's share of configs[4], the 3-D extruded jet (1000x50x20 = 1M
+points per GPU; with --gpus 8 the slab is the whole 1000x400x20 mesh).
 Inputs are resident in HBM before the timed region. Data are synthetic: the mesh replicates the
-reference jet geometry, node records are resampled from the reference's converged PaSR jet state
-(tests/golden/jet9w.npz, see synth.py).
+reference jet geometry (same domain and markers, nx x ny points); the initial field is the reference's
+converged PaSR jet (its own 9 000-point mesh, tests/golden/jet9k.npz) linearly interpolated onto it, and
+the node records are completed by the reference's start-up preprocessing on the device (see synth.py).
 
 The preconditioner is partitioned like the reference run on `--parts` MPI ranks (RCB partition,
 local RCM per part, ILU(0) per rank; default 256 = one rank per CU); `--parts 1` is the serial
@@ -104,15 +105,20 @@ def pmc_traffic(kernel, workload_key):
 
 
 def build_workload(nx, ny, ns, n_part=1, nz=0):
+    """Mesh + initial field: the reference's converged PaSR jet interpolated onto the synthetic mesh
+    (synth.jet_field_case); the node records are completed on the device by synth.device_preprocess."""
     from tests.rxpkg import synth
-    mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=ns, n_part=n_part, nz=nz)
+    mesh, st, mech, kw = synth.jet_field_case(nx, ny, n_species=ns, n_part=n_part, nz=nz)
     return mesh, st, mech, kw
 
 
 def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
-    """One reference outer iteration of the CPU restatement (oracle/, one core) on the same mesh and state:
-    O.outer_iteration (flow Preprocessing, time step, loops + boundary conditions, FGMRES(5)+ILU0 update,
-    Preprocessing(Output), SST iteration) — or, with bc None (--no-bc), the legacy flow + SST step."""
+    """One reference outer iteration of the CPU restatement (oracle/, OpenMP over the host cores it is given:
+    OMP_NUM_THREADS, 16 on the GPU box) on the same mesh and state: O.outer_iteration (flow Preprocessing, time
+    step, loops + boundary conditions, FGMRES(5)+ILU0 update, Preprocessing(Output), SST iteration) — or, with bc
+    None (--no-bc), the legacy flow + SST step. The per-edge / per-point / per-rank loops run in parallel with the
+    reference's per-item arithmetic (results are thread-count independent); the scatters of the time step and
+    the SST system, the inner products and the host orchestration stay serial."""
     from oracle import oracle as O
     om = O.Mechanism(mech_arrays)
     c = dict(cfl=cfg.cfl, max_delta_time=cfg.max_delta_time, prandtl_lam=cfg.prandtl_lam,
@@ -125,7 +131,7 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
         from tests.oracle_inputs import outer_iteration_inputs
         mesh_o, state, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
         t0 = time.perf_counter()
-        O.outer_iteration(om, nDim, mesh_o, state, bco, c, 0, pattern, part_ptr=mesh.get("part_ptr"))
+        O.outer_iteration(om, nDim, mesh_o, state, bco, c, 0, pattern, part_ptr=mesh.get("part_ptr"), keep=False)
         what = "1 reference outer iteration (flow + SST, jet boundary conditions)"
     else:
         t0 = time.perf_counter()
@@ -136,8 +142,9 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
                    dict(lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter), pattern=pattern, part_ptr=mesh.get("part_ptr"))
         what = "1 outer iteration (flow implicit step + SST step, no boundary conditions)"
     dt = time.perf_counter() - t0
-    return dict(value=N / dt / 1e6, unit="Mcells*iters/s", cores=1, kind="port",
-                sample=f"{what} of the same {N}-cell mesh on 1 host core ({dt:.2f} s)")
+    cores = int(O.lib().orc_num_threads())
+    return dict(value=N / dt / 1e6, unit="Mcells*iters/s", cores=cores, kind="port",
+                sample=f"{what} of the same {N}-cell mesh, {cores} host threads ({dt:.2f} s)")
 
 
 def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist, nz=0):
@@ -156,6 +163,7 @@ def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist, nz=0):
     if not args.no_bc:
         s.set_bc(synth.jet_bc(sh, ns))
     t = rx.TurbSSTSolver(sh, s, rx.sst_cfg())
+    st_l = synth.device_preprocess(s, t, sh, st_l)
     return s, t, sh, st_l, mech_arrays, kw, cfg, int(sh["n_domain"])
 
 
@@ -169,7 +177,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--nx", type=int, default=0)
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--nz", type=int, default=0, help="z planes of the 3-D extrusion (c5)")
@@ -209,7 +217,6 @@ def main():
         try:
             s, t, mesh, st, mech_arrays, kw, cfg, n_owned = setup_sharded(rx, args, nx, ny, ns, world, rank, local,
                                                                           dist, nz)
-            set_states(s, t, mesh, st)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             err = repr(e)[:200]
         flags = [None] * world
@@ -233,6 +240,8 @@ def main():
             synth_bc = synth.jet_bc(mesh, ns)
             s.set_bc(synth_bc)
         t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+        from tests.rxpkg import synth
+        st = synth.device_preprocess(s, t, mesh, st)
         set_states(s, t, mesh, st)
         n_owned = s.N
     N, E = s.N, s.E

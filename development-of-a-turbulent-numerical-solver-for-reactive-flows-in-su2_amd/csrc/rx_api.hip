@@ -393,7 +393,9 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       si[q] = (int32_t)mesh->send_idx[q];
     }
     CK(dupload(ctx, &ctx->send_idx, si.data(), si.size()));
-    CK(dalloc(ctx, &ctx->sendbuf, (size_t)std::max<int64_t>(1, ctx->n_send) * kHaloMaxStride));
+    // the widest exchangeable node record: D_ij (Ns^2), the primitive gradient (nG x nDim) or V (nPV)
+    ctx->halo_stride = std::max({kHaloMaxStride, ctx->ns * ctx->ns, ctx->nG * ctx->nDim, ctx->nPV});
+    CK(dalloc(ctx, &ctx->sendbuf, (size_t)std::max<int64_t>(1, ctx->n_send) * ctx->halo_stride));
   }
   CK(dalloc(ctx, &ctx->rms_sum, 32));
   // LSQ neighbour lists (reference order) and boundary vertices per node
@@ -818,6 +820,16 @@ bool graphs_enabled(const rx_ctx* ctx) {
   return !(e && e[0] == '1') && !ctx->has_hcomm;
 }
 
+}  // namespace
+
+void rx_graph_reset(rx_ctx* ctx) {
+  if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
+  if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
+  ctx->solve_exec = nullptr;
+  ctx->solve_graph = nullptr;
+}
+
+namespace {
 // Shared by the flow and the SST context: system build, preconditioner build (CSysSolve::Solve
 // :601-653), then FGMRES + RMS + update replayed as one hipGraph.
 int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
@@ -839,7 +851,10 @@ int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   {
     RxPhase ph(ctx, sst ? RX_K_SST_SOLVE : RX_K_SOLVE);
     if (graphs_enabled(ctx)) {
+      const uint64_t epoch = (sst && ctx->flow ? ctx->flow : ctx)->bc_epoch;
+      if (ctx->solve_exec && ctx->graph_epoch != epoch) rx_graph_reset(ctx);
       if (!ctx->solve_exec) {
+        ctx->graph_epoch = epoch;
         RX_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
         ctx->capturing = true;
         rc = enqueue_solve(ctx);

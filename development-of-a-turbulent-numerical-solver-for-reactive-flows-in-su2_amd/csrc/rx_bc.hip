@@ -812,6 +812,8 @@ int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
       }
   }
   rx_bc_free(ctx);
+  rx_graph_reset(ctx);  // the captured solve's update reads bc_wall
+  ++ctx->bc_epoch;      // and the SST context's graph the flow's markers
   ctx->bc_nmark = nM;
   ctx->bc_W = W;
   ctx->bc_inlet_kind = bc->inlet_kind;

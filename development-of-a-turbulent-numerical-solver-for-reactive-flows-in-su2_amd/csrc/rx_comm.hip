@@ -28,7 +28,7 @@ int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? RX_OK : RX_ERR_COMM; }
 
 int stage_alloc(rx_ctx* ctx) {
   if (ctx->h_stage) return RX_OK;
-  const size_t n = (size_t)(ctx->n_send + (ctx->N - ctx->Nd)) * kHaloMaxStride + 64;
+  const size_t n = (size_t)(ctx->n_send + (ctx->N - ctx->Nd)) * ctx->halo_stride + 64;
   RX_HIP(hipHostMalloc(&ctx->h_stage, n * sizeof(double)));
   return RX_OK;
 }
@@ -37,7 +37,7 @@ int stage_alloc(rx_ctx* ctx) {
 
 int rx_la_exchange(rx_ctx* ctx, double* f, int stride) {
   if (!ctx->distributed() || ctx->n_neigh == 0) return RX_OK;
-  if (stride > kHaloMaxStride) return RX_ERR_ARG;
+  if (stride > ctx->halo_stride) return RX_ERR_ARG;
   if (ctx->n_send > 0) {
     const int64_t n = ctx->n_send * stride;
     k_pack<<<(int)((n + 255) / 256), 256, 0, ctx->stream>>>(ctx->n_send, stride, ctx->send_idx, f, ctx->sendbuf);
@@ -77,7 +77,7 @@ int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count) {
   if (!ctx->distributed()) return RX_OK;
   if (ctx->has_hcomm) {
     if (count > 64) return RX_ERR_ARG;
-    double* h = ctx->h_stage + (ctx->n_send + (ctx->N - ctx->Nd)) * kHaloMaxStride;
+    double* h = ctx->h_stage + (ctx->n_send + (ctx->N - ctx->Nd)) * ctx->halo_stride;
     RX_HIP(hipMemcpyAsync(h, in, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
     RX_HIP(hipStreamSynchronize(ctx->stream));
     if (ctx->hcomm.allreduce(ctx->hcomm.user, h, h, count) != 0) return RX_ERR_COMM;
@@ -105,14 +105,7 @@ int comm_attached(rx_ctx* ctx) {
     rc = RX_ERR_HIP;
   if (!rc) ctx->n_global = (int64_t)h;
   (void)hipFree(d);
-  if (ctx->solve_exec) {
-    (void)hipGraphExecDestroy(ctx->solve_exec);
-    ctx->solve_exec = nullptr;
-  }
-  if (ctx->solve_graph) {
-    (void)hipGraphDestroy(ctx->solve_graph);
-    ctx->solve_graph = nullptr;
-  }
+  rx_graph_reset(ctx);
   return rc;
 }
 

@@ -32,12 +32,13 @@ struct rx_ctx {
   std::vector<int64_t> h_send_ptr, h_recv_ptr;
   int32_t* send_idx = nullptr;  // [n_send] owned points to send, grouped per neighbour
   int64_t n_send = 0;
-  double* sendbuf = nullptr;    // [n_send * kHaloMaxStride]
+  double* sendbuf = nullptr;    // [n_send * halo_stride]
+  int halo_stride = 64;         // doubles per point of the widest exchangeable node field (>= kHaloMaxStride)
   void* comm = nullptr;         // ncclComm_t
   bool comm_owned = true;       // SST contexts borrow the flow context's communicator
   bool has_hcomm = false;       // host-staged transport (rx_comm_init_host)
   rx_host_comm hcomm{};
-  double* h_stage = nullptr;    // pinned [(n_send + N - Nd) * kHaloMaxStride + 64]
+  double* h_stage = nullptr;    // pinned [(n_send + N - Nd) * halo_stride + 64]
   int nranks = 1, rank = 0;
   bool distributed() const { return comm != nullptr || has_hcomm; }
   int64_t n_global = 0;         // owned points over all ranks
@@ -122,6 +123,10 @@ struct rx_ctx {
   void* h_kstate = nullptr;  // pinned host mirror
   // captured implicit solve (system build + preconditioner build + FGMRES + update)
   hipGraphExec_t solve_exec = nullptr;
+  // buffers a captured solve graph bakes in: bumped by rx_bc_set (bc arrays reallocated); a graph captured under
+  // another epoch of its own (flow) or its flow context's (SST) markers is re-captured
+  uint64_t bc_epoch = 0;
+  uint64_t graph_epoch = 0;
   hipGraph_t solve_graph = nullptr;
   bool capturing = false;
 
@@ -169,7 +174,7 @@ struct rx_ctx {
 };
 
 int rx_fail_hip(rx_ctx* ctx, hipError_t e);
-constexpr int kHaloMaxStride = 64;  // doubles per point of the largest exchanged field (gradient)
+constexpr int kHaloMaxStride = 64;  // minimum doubles per point of the exchange buffers (ctx->halo_stride)
 // halo exchange of a device array with `stride` doubles per point (no-op without communicator)
 int rx_la_exchange(rx_ctx* ctx, double* f, int stride);
 // out[i] = sum over ranks of in[i] (in == out allowed), ordered on the context stream; no-op
@@ -221,6 +226,8 @@ int rx_la_prepare(rx_ctx* ctx);
 int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv);
 double* rx_invd_buf(rx_ctx* ctx);
 int rx_la_krylov_alloc(rx_ctx* ctx, int m);
+// Drop the captured solve graph (its kernel arguments point at buffers about to be replaced).
+void rx_graph_reset(rx_ctx* ctx);
 int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m);
 int rx_la_fgmres_result(rx_ctx* ctx, int* iters, double* resid);
 int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid);

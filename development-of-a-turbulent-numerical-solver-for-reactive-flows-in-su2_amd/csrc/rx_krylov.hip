@@ -374,6 +374,7 @@ int rx_la_krylov_alloc(rx_ctx* ctx, int m) {
   const int64_t n = ctx->N * ctx->nVar;
   if (m < 1 || m > kMaxM) return RX_ERR_ARG;
   if (ctx->krylov_m < m) {
+    rx_graph_reset(ctx);  // a captured solve reads kw / kz
     if (ctx->kw) (void)hipFree(ctx->kw);
     if (ctx->kz) (void)hipFree(ctx->kz);
     ctx->kw = ctx->kz = nullptr;

@@ -1202,7 +1202,8 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
   const int nv = ctx->nVar;
   const size_t shm = sizeof(double) * ((size_t)ctx->maxpart * nv + (size_t)(256 / nv) * nv + 1) +
                      sizeof(int32_t) * (8 * (size_t)ctx->maxpart + (size_t)ctx->maxpart_nnzb);
-  if (shm <= (size_t)ctx->lds_max) {
+  static const bool no_lds = getenv("RX_NO_LDS_APPLY") != nullptr;  // diagnosis: force the global sweeps
+  if (shm <= (size_t)ctx->lds_max && !no_lds) {
     RX_NV_SWITCH(nv, (k_ilu_apply_lds<NV_><<<ctx->npart, 256, shm, ctx->stream>>>(
                          ctx->part_ptr, ctx->rp, ctx->fs.part_lvl, ctx->fs.lvl_ptr,
                          reinterpret_cast<const int4*>(ctx->fs.slot), ctx->bs.part_lvl, ctx->bs.lvl_ptr,

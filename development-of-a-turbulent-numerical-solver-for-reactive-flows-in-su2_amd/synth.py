@@ -52,8 +52,10 @@ def species_subset(g, keep, nDim=2):
     pv = nDim + 5  # [T, u, v, P, rho, h, a] then Y_s in V
     out["V"] = np.concatenate([g["V"][:, :pv], g["V"][:, pv + keep]], axis=1)
     for k in ("U", "dPdU", "dTdU"):
-        out[k] = np.concatenate([g[k][:, :fl], g[k][:, fl + keep]], axis=1)
-    out["Dij"] = g["Dij"][:, keep][:, :, keep]
+        if k in g:
+            out[k] = np.concatenate([g[k][:, :fl], g[k][:, fl + keep]], axis=1)
+    if "Dij" in g:
+        out["Dij"] = g["Dij"][:, keep][:, :, keep]
     for k in ("mmass", "diff_vol", "form_enthalpy", "species"):
         out["mech_" + k] = g["mech_" + k][keep]
     for k in ("tab_x", "tab_y", "tab_y2"):
@@ -109,6 +111,122 @@ def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1, nz=0):
     return mesh, state, mech, {"mach_inf": float(g["mach_inf"][0]), "prandtl_turb": float(g["visc_params"][1]),
                                "lewis_turb": float(g["visc_params"][2]), "c_mu": float(g["src_params"][0]),
                                "pasr_lb": float(g["src_params"][1])}
+
+
+JET_LENGTH, JET_HEIGHT = 0.125, 0.006  # mesh_stretched.su2's domain (meshgen.jet_points)
+
+
+def field_subset(g, n_species):
+    """Restrict the reference's 9-species field (and mechanism) to its first n_species species: the dropped
+    partial densities are folded into the kept ones in proportion (rho and rho E unchanged), so the state stays
+    a valid conservative state of the smaller mixture; T is re-derived by Cons2PrimVar on the device."""
+    ns0 = int(g["mech_n_species"])
+    if n_species == ns0:
+        return g
+    out = species_subset(g, np.arange(n_species))
+    nDim = int(np.shape(g["coord"])[1])
+    fl = nDim + 2
+    U = np.asarray(g["U"], dtype=np.float64)
+    rs = U[:, fl:fl + ns0]
+    kept = rs[:, :n_species]
+    tot = rs.sum(axis=1, keepdims=True)
+    ks = kept.sum(axis=1, keepdims=True)
+    out["U"] = np.concatenate([U[:, :fl], kept * (tot / np.where(ks > 0, ks, 1.0))], axis=1)
+    return out
+
+
+def jet_field_case(nx, ny, n_species=7, n_part=1, nz=0, field="jet9k"):
+    """Mesh (RCM-ordered median dual, partitioned) + a smooth, physically consistent initial state for an nx x ny
+    (x nz) jet: the reference's converged PaSR field on its own 9 000-point mesh (tests/golden/jet9k.npz, after the
+    reference's preprocessing) linearly interpolated onto the synthetic mesh, which covers the same physical domain
+    (SURVEY.md §8(d) 'bilinearly interpolate flow_second_chem.dat onto the finer mesh'). Interpolated quantities are
+    the conservatives U, (k, omega), mu_t and T (the secant's starting temperature); a convex combination of
+    valid conservative states is a valid conservative state. The other node records (V, dP/dU, dT/dU, mu, kappa,
+    D_ij, SST fields) are produced on the device by the reference's preprocessing sequence (device_preprocess).
+    3-D: spanwise-uniform (rho w = 0)."""
+    mg = _meshgen()
+    mesh = mg.build_jet(nx, ny, n_part=n_part, nz=nz)
+    g = field_subset(load_records(field), n_species)
+    src = np.asarray(g["coord"]) / np.array([JET_LENGTH, JET_HEIGHT])
+    dst = np.asarray(mesh["coord"])[:, :2] / np.array([JET_LENGTH, JET_HEIGHT])
+    vals = np.concatenate([g["U"], np.stack([g["turb_k"], g["turb_omega"], g["mu_t"], g["V"][:, 0]], axis=1)],
+                          axis=1)
+    from scipy.interpolate import LinearNDInterpolator
+    from scipy.spatial import cKDTree
+    out = LinearNDInterpolator(src, vals)(dst)
+    bad = np.isnan(out[:, 0])
+    if bad.any():  # outside the reference points' convex hull (curved-boundary slivers): nearest point
+        _, idx = cKDTree(src).query(dst[bad])
+        out[bad] = vals[idx]
+    nU = g["U"].shape[1]
+    U = out[:, :nU]
+    # trace species. The viscous Jacobian's Ds = (1 - X_s) / sum_b X_b / D_sb (numerics_direct_reactive.cpp:1578-1588)
+    # is 0/0 -> 0 (the reference's NaN guard) at a pure-species point, but once an update leaves 1e-30-level
+    # partial densities there (negative ones are clamped to 1e-30, reacting_model_library.cpp:65-79) it is
+    # rounding / 1e-30 ~ 1e280, and the ILU(0) factor overflows (DESIGN.md §2, the Ds discontinuity). The
+    # reference's oxidiser stream is pure O2, so every species is floored at a mass fraction of 1e-10 and the
+    # partial densities rescaled to the interpolated density (the mixture and its energy change by ~1e-10).
+    rho = U[:, 0]
+    rs = U[:, 4:]
+    np.maximum(rs, 1e-10 * rho[:, None], out=rs)
+    rs *= (rho / rs.sum(axis=1))[:, None]
+    k, om, mut, T = (out[:, nU + q] for q in range(4))
+    nDim = 3 if nz > 1 else 2
+    if nDim == 3:
+        U = np.concatenate([U[:, :3], np.zeros((len(U), 1)), U[:, 3:]], axis=1)
+    ns = n_species
+    V = np.zeros((len(U), ns + nDim + 5))
+    V[:, 0] = T
+    state = dict(U=np.ascontiguousarray(U), V=V, turb_k=np.ascontiguousarray(k), turb_omega=np.ascontiguousarray(om),
+                 mu_t=np.ascontiguousarray(mut), eddy_visc_flow=np.ascontiguousarray(mut))
+    state["sst_sol"] = np.ascontiguousarray(np.stack([k, om], axis=1))
+    mesh["n_dim"] = nDim
+    mech = {q: g[q] for q in g if q.startswith("mech_")}
+    return mesh, state, mech, {"mach_inf": float(g["mach_inf"][0]), "prandtl_turb": float(g["visc_params"][1]),
+                               "lewis_turb": float(g["visc_params"][2]), "c_mu": float(g["src_params"][0]),
+                               "pasr_lb": float(g["src_params"][1])}
+
+
+def device_preprocess(flow, turb, mesh, state):
+    """The reference's start-up preprocessing on the device (the sequence its driver runs before the first
+    iteration, as oracle/ref_harness reproduces it: flow Preprocessing, turbulence Postprocessing, flow
+    Preprocessing, turbulence Preprocessing + Postprocessing), from U, the starting T, (k, omega) and mu_t. Returns
+    the completed node records (host copies, NODE_KEYS + sst_sol) for the CPU baseline and the parity tests."""
+    flow.upload("U", state["U"])
+    flow.upload("V", state["V"])
+    flow.upload("TKE", state["turb_k"])
+    flow.upload("OMEGA", state["turb_omega"])
+    flow.upload("MUT", state["mu_t"])
+    flow.upload("EDDY", state["eddy_visc_flow"])
+    turb.set_state(state["sst_sol"], mesh["wall_distance"])
+
+    def flow_pre():
+        flow.SetPrimitive_Variables(0)
+        flow.SetPrimitive_Gradient_LS()
+        flow.SetStrainMag()
+
+    flow_pre()
+    turb.Preprocessing()
+    turb.Postprocessing()
+    flow_pre()
+    turb.Preprocessing()
+    turb.Postprocessing()
+    flow.sync()
+    N, nDim = flow.N, flow.nDim
+    out = {}
+    for key, fld in (("V", "V"), ("U", "U"), ("dPdU", "DPDU"), ("dTdU", "DTDU"), ("mu", "MU"), ("kappa", "KAPPA"),
+                     ("Dij", "DIJ"), ("turb_k", "TKE"), ("turb_omega", "OMEGA"), ("mu_t", "MUT"),
+                     ("sigma_k", "SIGMAK"), ("grad_k", "GRADK"), ("eddy_visc_flow", "EDDY"), ("grad_prim", "GRAD")):
+        out[key] = flow.download(fld).reshape(N, -1)
+    for key in ("mu", "kappa", "turb_k", "turb_omega", "mu_t", "sigma_k", "eddy_visc_flow"):
+        out[key] = out[key].ravel()
+    ns = flow.mech.ns
+    out["Dij"] = out["Dij"].reshape(N, ns, ns)
+    out["grad_prim"] = out["grad_prim"].reshape(N, -1, nDim)
+    for key, fld in (("sst_F1", "F1"), ("sst_F2", "F2"), ("sst_CDkw", "CDKW")):
+        out[key] = turb.download(fld)
+    out["sst_sol"] = turb.download("U").reshape(N, 2)
+    return out
 
 
 # MARKER_* of the reference's jet cfg (Test_Cases/TURBOLENT/TURBOLENT_COMBUSTION/*.cfg, oracle/make_golden.py):

@@ -187,7 +187,10 @@ typedef struct {
 } rx_host_comm;
 int rx_comm_init_host(rx_ctx *ctx, int nranks, int rank, const rx_host_comm *ops);
 
-int rx_halo_exchange(rx_ctx *ctx, rx_field f); /* owned -> halo copies of a node field */
+/* owned -> halo copies of a node field (every per-point field: U, V, D_ij, GRAD, ...; the exchange buffers are
+ * sized for the widest, max(Ns^2, nPrimVarGrad*nDim, nPrimVar, 64) doubles per point). JAC / ILU (per block, not
+ * per point) return RX_ERR_ARG. */
+int rx_halo_exchange(rx_ctx *ctx, rx_field f);
 
 /* CReactiveEulerSolver::SetPrimitive_Variables (solver_direct_reactive.cpp:985-1040) on every point:
  * CReactiveNSVariable::SetPrimVar(eddy = MUT, k = TKE) (variable_direct_reactive.cpp:1188-1228) — Cons2PrimVar

@@ -400,6 +400,25 @@ def case_jet9w():
     return out
 
 
+def case_jet9k():
+    """The reference's whole 9 000-point jet (mesh_stretched.su2) with its converged PaSR state after the
+    reference's own preprocessing: the node field the synthetic bench meshes interpolate (synth.jet_field_case),
+    plus the dual-grid summary of the reference mesh. Only node records are kept (coords, U, V, k, omega, mu_t)."""
+    def writer(wd):
+        os.symlink(os.path.join(CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
+        return "mesh.su2"
+
+    xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    wd = make_workdir("jet9k", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    write_state(wd, cons)
+    a = run_harness(wd, bsr=False)
+    out = {k: a[k] for k in ("coord", "volume", "global_index", "U", "V", "turb_k", "turb_omega", "mu_t",
+                             "dims", "mach_inf", "visc_params", "src_params")}
+    out["n_edge"] = np.array(len(a["edges"]))
+    out.update(mech_arrays())
+    return out
+
+
 FP_DIR = os.path.join(REF, "Test_Cases/TURBOLENT/TURBOLENT_FLAT_PLATE")
 FP_CFG = """\
 % golden-vector cfg written by oracle/make_golden.py: the reference's turbulent flat plate (air, 3 species, no
@@ -549,7 +568,7 @@ def main():
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
-             "fp3": case_fp3}[case]()
+             "fp3": case_fp3, "jet9k": case_jet9k}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

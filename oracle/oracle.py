@@ -229,7 +229,7 @@ def lusgs(rp, col, A, b, part_ptr=None):
 @_keepalive
 def ilu_build(rp, col, A, part_ptr=None):
     N, nb = len(rp) - 1, A.shape[1]
-    F = np.zeros_like(np.ascontiguousarray(A))
+    F = np.empty_like(np.ascontiguousarray(A))  # orc_ilu_build_p copies A first
     lib().orc_ilu_build_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
                           F.ctypes.data_as(C.c_void_p), *_parts(N, part_ptr))
     return F
@@ -527,7 +527,7 @@ def bc_sst(nDim, mesh, bc_marker, prm, V, mu, eddy, charac, TG, F1, rp, col, T, 
                      _f(R), _f(A) if A is not None else None)
 
 
-def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=None):
+def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=None, keep=True):
     """One reference outer iteration for REACTIVE_RANS, restated on the CPU in the reference's order
     (CMeanFlowIteration::Iterate iteration_structure.cpp:486-560 -> CMultiGridIntegration::MultiGrid_Iteration
     integration_time.cpp:40-140 with MGLEVEL = 0, then CSingleGridIntegration::SingleGrid_Iteration :770-810):
@@ -536,7 +536,8 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
             Preprocessing(Output = true) on the updated solution;
       SST   Preprocessing (gradient), Space_Integration (loops + BCs), ImplicitEuler_Iteration, Postprocessing.
     s: state dict (U, V, Uold, T = (k, omega), TG, F1, F2, CDkw, mut) — returned updated with the iteration's
-    RMS (rms, sst_rms) and linear-solver counts. bc: dict(marker, prm) of the golden's bc_marker / oracle bc_prm."""
+    RMS (rms, sst_rms) and linear-solver counts. bc: dict(marker, prm) of the golden's bc_marker / oracle bc_prm.
+    keep=False drops the copies of the loop-only system kept for the tests (bench.py's CPU baseline)."""
     ns = mech.ns
     nb = ns + nDim + 2
     N = len(s["U"])
@@ -572,17 +573,15 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     A = np.ascontiguousarray(A)
     st = dict(U=U, V=o["V"], dPdU=o["dPdU"], dTdU=o["dTdU"], grad_prim=G, mu=o["mu"], kappa=o["kappa"], Dij=o["Dij"],
               turb_k=T[:, 0].copy(), mu_t=mut, sigma_k=sig, grad_k=gk, eddy_visc_flow=o["eddy"])
-    A_loops, R_loops = A.copy(), R.copy()
+    A_loops, R_loops = (A.copy(), R.copy()) if keep else (None, None)
     charac = bc_flow(mech, nDim, mesh, bc["marker"], bc["prm"], st, rp, col, R, A, Uold, True, True)
-    diag = np.array([rp[i] + np.searchsorted(col[rp[i]:rp[i + 1]], i) for i in range(N)])
+    diag = np.nonzero(np.asarray(col) == np.repeat(np.arange(N), np.diff(rp)))[0]  # the diagonal block of each row
     ok = dt > 1e-16
     D = A[diag]
     idx = np.arange(nb)
-    for i in np.nonzero(ok)[0]:
-        D[i][idx, idx] += vol[i] / dt[i]
-    for i in np.nonzero(~ok)[0]:
-        D[i] = np.eye(nb)
-        R[i] = 0.0
+    D[:, idx, idx] += np.where(ok, vol / np.where(ok, dt, 1.0), 0.0)[:, None]
+    D[~ok] = np.eye(nb)
+    R[~ok] = 0.0
     A[diag] = D
     rhs = -(R + 0.0)
     F = ilu_build(rp, col, A, part_ptr)
@@ -608,10 +607,9 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     bc_sst(nDim, mesh, bc["marker"], bc["prm"], V2, o2["mu"], o2["eddy"], charac, TG0, s["F1"], rp, col, T, R2, A2,
            True)
     D2 = A2[diag]
-    for i in range(N):
-        delta = vol[i] / (cfg.get("cfl_red_turb", 1.0) * dt[i])
-        D2[i][0, 0] += delta
-        D2[i][1, 1] += delta
+    delta = vol / (cfg.get("cfl_red_turb", 1.0) * dt)
+    D2[:, 0, 0] += delta
+    D2[:, 1, 1] += delta
     A2[diag] = D2
     rhs2 = -R2
     F2 = ilu_build(rp, col, A2, part_ptr)

@@ -21,6 +21,8 @@
 #include <stdexcept>
 #include <vector>
 
+#include <omp.h>
+
 namespace {
 
 constexpr double EPS = 1.0e-16;                         // Common/include/option_structure.hpp:134
@@ -1230,6 +1232,10 @@ std::vector<Mech*> g_mechs;
 // =================================================================================================
 extern "C" {
 
+// Threads the OpenMP loops of this file use (OMP_NUM_THREADS); 1 = the serial restatement. Every parallel loop
+// writes disjoint outputs and keeps the reference's per-item operation order, so results do not depend on it.
+int orc_num_threads() { return omp_get_max_threads(); }
+
 void* orc_mech_create(int ns, int nr, int ntab, const double* mm, const double* dv, const double* sr,
                       const double* sp, const double* er, const double* ep, const double* A, const double* beta,
                       const double* Ta, const double* Ab, const double* betab, const double* Tab,
@@ -1278,6 +1284,7 @@ double orc_spline(void* h, int prop, int s, double T) { return spline(*static_ca
 void orc_ausm_edges(int nDim, int ns, int64_t E, const int64_t* edges, const double* normal, const double* V,
                     const double* dPdU, double mach_inf, int implicit, double* res, double* Ji, double* Jj) {
   const int nVar = ns + nDim + 2, nPV = ns + nDim + 5;
+#pragma omp parallel for schedule(static)
   for (int64_t e = 0; e < E; ++e) {
     const int64_t i = edges[2 * e], j = edges[2 * e + 1];
     ausm(nDim, ns, V + i * nPV, V + j * nPV, normal + e * nDim, implicit ? dPdU + i * nVar : nullptr,
@@ -1293,8 +1300,10 @@ int orc_muscl_edges(void* h, int nDim, int64_t E, const int64_t* edges, const do
                     const double* refs, double mach_inf, int implicit, double* res, double* Ji, double* Jj) {
   const Mech& m = *static_cast<Mech*>(h);
   const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5, nG = ns + nDim + 2, nL = nDim + 2;
-  try {
-    for (int64_t e = 0; e < E; ++e) {
+  int err = 0;
+#pragma omp parallel for schedule(static) reduction(| : err)
+  for (int64_t e = 0; e < E; ++e) {
+    try {
       const int64_t i = edges[2 * e], j = edges[2 * e + 1];
       const double* Vi = V + i * nPV;
       const double* Vj = V + j * nPV;
@@ -1336,11 +1345,11 @@ int orc_muscl_edges(void* h, int nDim, int64_t E, const int64_t* edges, const do
       ausm(nDim, ns, Pi, Pj, normal + e * nDim, implicit ? Si : nullptr, implicit ? Sj : nullptr, mach_inf,
            implicit != 0, res + e * nVar, implicit ? Ji + e * nVar * nVar : nullptr,
            implicit ? Jj + e * nVar * nVar : nullptr);
+    } catch (const std::out_of_range&) {
+      err = 1;
     }
-  } catch (const std::out_of_range&) {
-    return 1;
   }
-  return 0;
+  return err;
 }
 
 // a9 over N cells. params = {C_mu, PaSR_lb, rho_ref, t_ref, T_ref}
@@ -1348,15 +1357,18 @@ int orc_source_cells(void* h, int nDim, int64_t N, const double* V, const double
                      const double* omega_turb, int rans, int implicit, const double* params, double* res, double* J) {
   const Mech& m = *static_cast<Mech*>(h);
   const int nVar = m.ns + nDim + 2, nPV = m.ns + nDim + 5;
-  try {
-    for (int64_t i = 0; i < N; ++i)
+  int err = 0;
+#pragma omp parallel for schedule(static) reduction(| : err)
+  for (int64_t i = 0; i < N; ++i) {
+    try {
       source(m, nDim, V + i * nPV, implicit ? dTdU + i * nVar : nullptr, vol[i], rans ? omega_turb[i] : 0.0,
              rans != 0, implicit != 0, params[0], params[1], params[2], params[3], params[4], res + i * nVar,
              implicit ? J + i * nVar * nVar : nullptr);
-  } catch (const std::exception&) {
-    return 1;
+    } catch (const std::exception&) {
+      err = 1;
+    }
   }
-  return 0;
+  return err;
 }
 
 // a3-a6 over E edges. vparams = {T_ref, E_ref, R_ref, Prandtl_Turb, Lewis_Turb}
@@ -1368,8 +1380,10 @@ int orc_visc_edges(void* h, int nDim, int64_t E, const int64_t* edges, const dou
   const Mech& m = *static_cast<Mech*>(h);
   const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5, nG = ns + nDim + 2;
   ViscParams P{vparams[0], vparams[1], vparams[2], vparams[3], vparams[4], rans, implicit};
-  try {
-    for (int64_t e = 0; e < E; ++e) {
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(| : err)
+  for (int64_t e = 0; e < E; ++e) {
+    try {
       const int64_t i = edges[2 * e], j = edges[2 * e + 1];
       visc_flux(m, nDim, P, V + i * nPV, V + j * nPV, grad + i * nG * nDim, grad + j * nG * nDim, mu[i], mu[j],
                 kappa[i], kappa[j], Dij + i * ns * ns, Dij + j * ns * ns, coord + i * nDim, coord + j * nDim,
@@ -1377,11 +1391,11 @@ int orc_visc_edges(void* h, int nDim, int64_t E, const int64_t* edges, const dou
                 rans ? tke[i] : 0.0, rans ? tke[j] : 0.0, rans ? mut[i] : 0.0, rans ? mut[j] : 0.0,
                 rans ? sigma_k[i] : 1.0, rans ? gradk + i * nDim : nullptr, rans ? gradk + j * nDim : nullptr,
                 res + e * nVar, implicit ? Ji + e * nVar * nVar : nullptr, implicit ? Jj + e * nVar * nVar : nullptr);
+    } catch (const std::exception&) {
+      err = 1;
     }
-  } catch (const std::exception&) {
-    return 1;
   }
-  return 0;
+  return err;
 }
 
 // a12 for the listed points (pts), all others untouched.
@@ -1389,6 +1403,7 @@ void orc_grad_lsq(void* h, int nDim, int64_t npts, const int64_t* pts, const dou
                   const int64_t* nptr, const int64_t* nbr, double* grad) {
   const Mech& m = *static_cast<Mech*>(h);
   const int nG = m.ns + nDim + 2;
+#pragma omp parallel for schedule(static)
   for (int64_t k = 0; k < npts; ++k) {
     const int64_t i = pts[k];
     grad_lsq_node(m, nDim, (int)i, coord, V, nptr, nbr, grad + i * nG * nDim);
@@ -1519,14 +1534,16 @@ void orc_time_step(int nDim, int ns, int64_t N, int64_t E, const int64_t* edges,
 // MatrixVectorProduct (:997-1030)
 void orc_bsr_spmv(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* x,
                   double* y) {
-  for (int64_t q = 0; q < N * nb; ++q) y[q] = 0.0;
-  for (int64_t i = 0; i < N; ++i)
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < N; ++i) {
+    for (int a = 0; a < nb; ++a) y[i * nb + a] = 0.0;
     for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
       const double* b = A + k * nb * nb;
       const double* xv = x + col[k] * nb;
       for (int a = 0; a < nb; ++a)
         for (int c = 0; c < nb; ++c) y[i * nb + a] += b[a * nb + c] * xv[c];
     }
+  }
 }
 
 static void gauss_elim(int nb, const double* Block, double* rhs) {  // Gauss_Elimination (:594-643)
@@ -1566,59 +1583,64 @@ static int64_t find_diag(const int64_t* rp, const int64_t* col, int64_t i) {
 //   exchanged after the forward sweep (SendReceive_Solution :1687). The halo columns of a row come
 //   after its domain columns, in increasing global index.
 // np = 1, part_ptr = {0, N} is the serial reference.
-struct Parts {
-  std::vector<int64_t> lo, hi;
-  Parts(int64_t N, int64_t np, const int64_t* pp) : lo(N), hi(N) {
-    if (!pp || np <= 1) {
-      std::fill(lo.begin(), lo.end(), 0);
-      std::fill(hi.begin(), hi.end(), N);
-      return;
-    }
-    for (int64_t p = 0; p < np; ++p)
-      for (int64_t i = pp[p]; i < pp[p + 1]; ++i) {
-        lo[i] = pp[p];
-        hi[i] = pp[p + 1];
-      }
-  }
-};
+
+// Row ranges [b[p], b[p+1]) of the ranks; {0, N} is the serial reference. The ranks are independent in every
+// preconditioner sweep below (the halo couplings are block-Jacobi or read the exchanged copy), so they run on
+// separate threads with the reference's per-rank arithmetic unchanged.
+static std::vector<int64_t> part_bounds(int64_t N, int64_t np, const int64_t* pp) {
+  if (!pp || np <= 1) return {0, N};
+  return std::vector<int64_t>(pp, pp + np + 1);
+}
 
 // ComputeLU_SGSPreconditioner (:1673-1709)
 void orc_lusgs_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* b,
                  double* x, int64_t np, const int64_t* part_ptr) {
-  Parts P(N, np, part_ptr);
-  std::vector<double> aux(nb), prv(nb), xs(N * nb);
-  auto blockprod = [&](int64_t k, const double* xv) {
-    const double* blk = A + k * nb * nb;
-    for (int a = 0; a < nb; ++a) {
-      double pb = 0.0;
-      for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * xv[c];
-      prv[a] += pb;
+  const std::vector<int64_t> B = part_bounds(N, np, part_ptr);
+  const int64_t nparts = (int64_t)B.size() - 1;
+  std::vector<double> xs(N * nb);
+#pragma omp parallel
+  {
+    std::vector<double> aux(nb), prv(nb);
+    auto blockprod = [&](int64_t k, const double* xv) {
+      const double* blk = A + k * nb * nb;
+      for (int a = 0; a < nb; ++a) {
+        double pb = 0.0;
+        for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * xv[c];
+        prv[a] += pb;
+      }
+    };
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t p = 0; p < nparts; ++p)
+      for (int64_t i = B[p]; i < B[p + 1]; ++i) {  // (D+L) x* = b, per rank
+        for (int a = 0; a < nb; ++a) prv[a] = 0.0;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+          if (col[k] < i && col[k] >= B[p]) blockprod(k, x + col[k] * nb);
+        for (int a = 0; a < nb; ++a) aux[a] = b[i * nb + a] - prv[a];
+        gauss_elim(nb, A + find_diag(rp, col, i) * nb * nb, aux.data());
+        for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+      }
+#pragma omp for schedule(static)
+    for (int64_t q = 0; q < N * nb; ++q) xs[q] = x[q];  // halo copies of x*
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t p = 0; p < nparts; ++p) {
+      const int64_t lo = B[p], hi = B[p + 1];
+      for (int64_t i = hi - 1; i >= lo; --i) {  // (D+U) x = D x*
+        const double* dblk = A + find_diag(rp, col, i) * nb * nb;
+        for (int a = 0; a < nb; ++a) {
+          double pb = 0.0;
+          for (int c = 0; c < nb; ++c) pb += dblk[a * nb + c] * x[i * nb + c];
+          aux[a] = pb;  // DiagonalProduct: prod_row_vector = 0 + block*x
+        }
+        for (int a = 0; a < nb; ++a) prv[a] = 0.0;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+          if (col[k] > i && col[k] < hi) blockprod(k, x + col[k] * nb);
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+          if (col[k] < lo || col[k] >= hi) blockprod(k, xs.data() + col[k] * nb);
+        for (int a = 0; a < nb; ++a) aux[a] -= prv[a];
+        gauss_elim(nb, dblk, aux.data());
+        for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+      }
     }
-  };
-  for (int64_t i = 0; i < N; ++i) {  // (D+L) x* = b, per rank
-    for (int a = 0; a < nb; ++a) prv[a] = 0.0;
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
-      if (col[k] < i && col[k] >= P.lo[i]) blockprod(k, x + col[k] * nb);
-    for (int a = 0; a < nb; ++a) aux[a] = b[i * nb + a] - prv[a];
-    gauss_elim(nb, A + find_diag(rp, col, i) * nb * nb, aux.data());
-    for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
-  }
-  std::memcpy(xs.data(), x, sizeof(double) * N * nb);  // halo copies of x*
-  for (int64_t i = N - 1; i >= 0; --i) {  // (D+U) x = D x*
-    const double* dblk = A + find_diag(rp, col, i) * nb * nb;
-    for (int a = 0; a < nb; ++a) {
-      double pb = 0.0;
-      for (int c = 0; c < nb; ++c) pb += dblk[a * nb + c] * x[i * nb + c];
-      aux[a] = pb;  // DiagonalProduct: prod_row_vector = 0 + block*x
-    }
-    for (int a = 0; a < nb; ++a) prv[a] = 0.0;
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
-      if (col[k] > i && col[k] < P.hi[i]) blockprod(k, x + col[k] * nb);
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
-      if (col[k] < P.lo[i] || col[k] >= P.hi[i]) blockprod(k, xs.data() + col[k] * nb);
-    for (int a = 0; a < nb; ++a) aux[a] -= prv[a];
-    gauss_elim(nb, dblk, aux.data());
-    for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
   }
 }
 
@@ -1655,34 +1677,42 @@ static void mat_vec(int nb, const double* a, const double* x, double* y) {
 // BuildILUPreconditioner (:1368-1451), including the left-multiply quirk at :1432-1436; per rank.
 void orc_ilu_build_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, double* F,
                      int64_t np, const int64_t* part_ptr) {
-  Parts P(N, np, part_ptr);
+  const std::vector<int64_t> B = part_bounds(N, np, part_ptr);
+  const int64_t nparts = (int64_t)B.size() - 1;
   const int64_t nnzb = rp[N];
-  std::memcpy(F, A, sizeof(double) * nnzb * nb * nb);
-  std::vector<double> inv(nb * nb), w(nb * nb), blk(nb * nb);
+#pragma omp parallel for schedule(static)
+  for (int64_t q = 0; q < nnzb * nb * nb; ++q) F[q] = A[q];
   auto findb = [&](int64_t i, int64_t j) -> double* {
     for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
       if (col[k] == j) return F + k * nb * nb;
     return nullptr;
   };
-  for (int64_t i = 0; i < N; ++i) {
-    if (i == P.lo[i]) continue;  // the loop of each rank starts at its second row
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-      const int64_t j = col[k];
-      if (j < i && j >= P.lo[i]) {
-        double* Bij = F + k * nb * nb;
-        inverse_diag(nb, findb(j, j), inv.data());
-        mat_mat(nb, Bij, inv.data(), w.data());
-        for (int64_t kk = rp[j]; kk < rp[j + 1]; ++kk) {
-          const int64_t kp = col[kk];
-          if (kp >= j && kp < P.hi[i]) {
-            const double* Bjk = F + kk * nb * nb;
-            mat_mat(nb, Bjk, w.data(), blk.data());
-            double* Bik = findb(i, kp);
-            if (Bik)  // SubtractBlock_ILUMatrix on a missing block is a no-op of the pattern
-              for (int q = 0; q < nb * nb; ++q) Bik[q] -= blk[q];
+#pragma omp parallel
+  {
+    std::vector<double> inv(nb * nb), w(nb * nb), blk(nb * nb);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t p = 0; p < nparts; ++p) {
+      const int64_t lo = B[p], hi = B[p + 1];
+      for (int64_t i = lo + 1; i < hi; ++i) {  // the loop of each rank starts at its second row
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+          const int64_t j = col[k];
+          if (j < i && j >= lo) {
+            double* Bij = F + k * nb * nb;
+            inverse_diag(nb, findb(j, j), inv.data());
+            mat_mat(nb, Bij, inv.data(), w.data());
+            for (int64_t kk = rp[j]; kk < rp[j + 1]; ++kk) {
+              const int64_t kp = col[kk];
+              if (kp >= j && kp < hi) {
+                const double* Bjk = F + kk * nb * nb;
+                mat_mat(nb, Bjk, w.data(), blk.data());
+                double* Bik = findb(i, kp);
+                if (Bik)  // SubtractBlock_ILUMatrix on a missing block is a no-op of the pattern
+                  for (int q = 0; q < nb * nb; ++q) Bik[q] -= blk[q];
+              }
+            }
+            std::memcpy(Bij, w.data(), sizeof(double) * nb * nb);
           }
         }
-        std::memcpy(Bij, w.data(), sizeof(double) * nb * nb);
       }
     }
   }
@@ -1695,39 +1725,45 @@ void orc_ilu_build(int64_t N, int nb, const int64_t* rp, const int64_t* col, con
 // ComputeILUPreconditioner (:1453-1515), per rank.
 void orc_ilu_apply_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* F, const double* b,
                      double* x, int64_t np, const int64_t* part_ptr) {
-  Parts P(N, np, part_ptr);
-  std::vector<double> aux(nb), sum(nb), inv(nb * nb);
-  for (int64_t q = 0; q < N * nb; ++q) x[q] = b[q];
-  for (int64_t i = 0; i < N; ++i) {
-    if (i == P.lo[i]) continue;
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-      const int64_t j = col[k];
-      if (j < i && j >= P.lo[i]) {
-        mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
-        for (int a = 0; a < nb; ++a) x[i * nb + a] -= aux[a];
-      }
-    }
-  }
+  const std::vector<int64_t> B = part_bounds(N, np, part_ptr);
+  const int64_t nparts = (int64_t)B.size() - 1;
   auto diag = [&](int64_t i) { return F + find_diag(rp, col, i) * nb * nb; };
-  for (int64_t i = N - 1; i >= 0; --i) {
-    if (i == P.hi[i] - 1) {  // last row of the rank
-      inverse_diag(nb, diag(i), inv.data());
-      mat_vec(nb, inv.data(), x + i * nb, aux.data());
-      for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
-      continue;
-    }
-    for (int a = 0; a < nb; ++a) sum[a] = 0.0;
-    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-      const int64_t j = col[k];
-      if (j >= i + 1 && j < P.hi[i]) {
-        mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
-        for (int a = 0; a < nb; ++a) sum[a] += aux[a];
+#pragma omp parallel
+  {
+    std::vector<double> aux(nb), sum(nb), inv(nb * nb);
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t p = 0; p < nparts; ++p) {
+      const int64_t lo = B[p], hi = B[p + 1];
+      for (int64_t q = lo * nb; q < hi * nb; ++q) x[q] = b[q];
+      for (int64_t i = lo + 1; i < hi; ++i)
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+          const int64_t j = col[k];
+          if (j < i && j >= lo) {
+            mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
+            for (int a = 0; a < nb; ++a) x[i * nb + a] -= aux[a];
+          }
+        }
+      for (int64_t i = hi - 1; i >= lo; --i) {
+        if (i == hi - 1) {  // last row of the rank
+          inverse_diag(nb, diag(i), inv.data());
+          mat_vec(nb, inv.data(), x + i * nb, aux.data());
+          for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+          continue;
+        }
+        for (int a = 0; a < nb; ++a) sum[a] = 0.0;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+          const int64_t j = col[k];
+          if (j >= i + 1 && j < hi) {
+            mat_vec(nb, F + k * nb * nb, x + j * nb, aux.data());
+            for (int a = 0; a < nb; ++a) sum[a] += aux[a];
+          }
+        }
+        for (int a = 0; a < nb; ++a) x[i * nb + a] = x[i * nb + a] - sum[a];
+        inverse_diag(nb, diag(i), inv.data());
+        mat_vec(nb, inv.data(), x + i * nb, aux.data());
+        for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
       }
     }
-    for (int a = 0; a < nb; ++a) x[i * nb + a] = x[i * nb + a] - sum[a];
-    inverse_diag(nb, diag(i), inv.data());
-    mat_vec(nb, inv.data(), x + i * nb, aux.data());
-    for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
   }
 }
 
@@ -1753,6 +1789,7 @@ double orc_dot(int64_t n, const double* a, const double* c) {
   }
   const int NB = 512, BS = 256;
   std::vector<double> part(NB), sh(BS);
+#pragma omp parallel for schedule(static) firstprivate(sh)
   for (int b = 0; b < NB; ++b) {
     for (int t = 0; t < BS; ++t) {
       double s = 0.0;
@@ -1780,6 +1817,7 @@ int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
   std::vector<std::vector<double>> H(m + 1, std::vector<double>(m, 0.0));
   double norm0 = norm(b);
   orc_bsr_spmv(N, nb, rp, col, A, x, w[0].data());
+#pragma omp parallel for schedule(static)
   for (int64_t q = 0; q < n; ++q) w[0][q] -= b[q];
   double beta = norm(w[0].data());
   const double epsm = std::numeric_limits<double>::epsilon();
@@ -1787,6 +1825,7 @@ int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
     *resid = beta;
     return 0;
   }
+#pragma omp parallel for schedule(static)
   for (int64_t q = 0; q < n; ++q) w[0][q] /= -beta;
   g[0] = beta;
   norm0 = beta;
@@ -1804,10 +1843,12 @@ int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
     for (int k = 0; k < i + 1; ++k) {
       double prod = dotp(w[i + 1].data(), w[k].data());
       H[k][i] = prod;
+#pragma omp parallel for schedule(static)
       for (int64_t q = 0; q < n; ++q) w[i + 1][q] += -prod * w[k][q];
       if (prod * prod > thr) {
         prod = dotp(w[i + 1].data(), w[k].data());
         H[k][i] += prod;
+#pragma omp parallel for schedule(static)
         for (int64_t q = 0; q < n; ++q) w[i + 1][q] += -prod * w[k][q];
       }
       nrm -= H[k][i] * H[k][i];
@@ -1816,6 +1857,7 @@ int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
     }
     nrm = norm(w[i + 1].data());
     H[i + 1][i] = nrm;
+#pragma omp parallel for schedule(static)
     for (int64_t q = 0; q < n; ++q) w[i + 1][q] /= nrm;
     auto applyG = [](double s, double c, double& h1, double& h2) {
       const double t = c * h1 + s * h2;
@@ -1861,6 +1903,7 @@ int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
     for (int j = k - 1; j >= 0; --j) y[j] -= H[j][k] * y[k];
   }
   for (int k = 0; k < i; ++k)
+#pragma omp parallel for schedule(static)
     for (int64_t q = 0; q < n; ++q) x[q] += y[k] * z[k][q];
   *resid = beta;
   return i;
@@ -1887,9 +1930,23 @@ void orc_assemble(int64_t N, int64_t E, int nb, const int64_t* edges, const int6
                   const double* Fc, const double* Jci, const double* Jcj, const double* Fv, const double* Jvi,
                   const double* Jvj, const double* Rs, const double* Js, const double* vol, const double* dt,
                   double* R, double* A, double* rhs) {
+  // The reference scatters edge by edge; every row's residual and blocks receive their contributions in edge
+  // order, pass by pass. Gathering per row over its incident edges in increasing edge id (convective pass, then
+  // viscous) reproduces each sum's order exactly, so the rows are assembled in parallel.
   const int nb2 = nb * nb;
-  std::fill(R, R + N * nb, 0.0);
-  if (A) std::fill(A, A + rp[N] * nb2, 0.0);
+  std::vector<int64_t> ip(N + 1, 0), ie(2 * E);
+  for (int64_t e = 0; e < E; ++e) {
+    ++ip[edges[2 * e] + 1];
+    ++ip[edges[2 * e + 1] + 1];
+  }
+  for (int64_t i = 0; i < N; ++i) ip[i + 1] += ip[i];
+  {
+    std::vector<int64_t> fill(ip.begin(), ip.end() - 1);
+    for (int64_t e = 0; e < E; ++e) {
+      ie[fill[edges[2 * e]]++] = e;
+      ie[fill[edges[2 * e + 1]]++] = e;
+    }
+  }
   auto add = [&](int64_t b, const double* J, double sgn) {
     double* d = A + b * nb2;
     if (sgn > 0)
@@ -1897,48 +1954,56 @@ void orc_assemble(int64_t N, int64_t E, int nb, const int64_t* edges, const int6
     else
       for (int q = 0; q < nb2; ++q) d[q] -= J[q];
   };
-  for (int pass = 0; pass < 2; ++pass) {
-    const double* F = pass ? Fv : Fc;
-    const double* Ji = pass ? Jvi : Jci;
-    const double* Jj = pass ? Jvj : Jcj;
-    if (!F) continue;
-    const double s = pass ? -1.0 : 1.0;
-    for (int64_t e = 0; e < E; ++e) {
-      const int64_t i = edges[2 * e], j = edges[2 * e + 1];
-      for (int v = 0; v < nb; ++v) {
-        if (s > 0) {
-          R[i * nb + v] += F[e * nb + v];
-          R[j * nb + v] -= F[e * nb + v];
+#pragma omp parallel for schedule(dynamic, 1024)
+  for (int64_t r = 0; r < N; ++r) {
+    for (int v = 0; v < nb; ++v) R[r * nb + v] = 0.0;
+    if (A)
+      for (int64_t q = rp[r] * nb2; q < rp[r + 1] * nb2; ++q) A[q] = 0.0;
+    for (int pass = 0; pass < 2; ++pass) {
+      const double* F = pass ? Fv : Fc;
+      const double* Ji = pass ? Jvi : Jci;
+      const double* Jj = pass ? Jvj : Jcj;
+      if (!F) continue;
+      const double s = pass ? -1.0 : 1.0;
+      for (int64_t q = ip[r]; q < ip[r + 1]; ++q) {
+        const int64_t e = ie[q];
+        const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+        if (r == i) {
+          for (int v = 0; v < nb; ++v) {
+            if (s > 0) R[i * nb + v] += F[e * nb + v];
+            else R[i * nb + v] -= F[e * nb + v];
+          }
+          if (A && Ji) {
+            add(blk_of(rp, col, i, i), Ji + e * nb2, s);
+            add(blk_of(rp, col, i, j), Jj + e * nb2, s);
+          }
         } else {
-          R[i * nb + v] -= F[e * nb + v];
-          R[j * nb + v] += F[e * nb + v];
+          for (int v = 0; v < nb; ++v) {
+            if (s > 0) R[j * nb + v] -= F[e * nb + v];
+            else R[j * nb + v] += F[e * nb + v];
+          }
+          if (A && Ji) {
+            add(blk_of(rp, col, j, i), Ji + e * nb2, -s);
+            add(blk_of(rp, col, j, j), Jj + e * nb2, -s);
+          }
         }
       }
-      if (A && Ji) {
-        add(blk_of(rp, col, i, i), Ji + e * nb2, s);
-        add(blk_of(rp, col, i, j), Jj + e * nb2, s);
-        add(blk_of(rp, col, j, i), Ji + e * nb2, -s);
-        add(blk_of(rp, col, j, j), Jj + e * nb2, -s);
-      }
     }
-  }
-  if (Rs)
-    for (int64_t i = 0; i < N; ++i) {
-      for (int v = 0; v < nb; ++v) R[i * nb + v] += Rs[i * nb + v];
-      if (A && Js) add(blk_of(rp, col, i, i), Js + i * nb2, 1.0);
+    if (Rs) {
+      for (int v = 0; v < nb; ++v) R[r * nb + v] += Rs[r * nb + v];
+      if (A && Js) add(blk_of(rp, col, r, r), Js + r * nb2, 1.0);
     }
-  if (!A) return;
-  for (int64_t i = 0; i < N; ++i) {
-    double* D = A + blk_of(rp, col, i, i) * nb2;
-    if (dt[i] > EPS) {
-      const double delta = vol[i] / dt[i];
+    if (!A) continue;
+    double* D = A + blk_of(rp, col, r, r) * nb2;
+    if (dt[r] > EPS) {
+      const double delta = vol[r] / dt[r];
       for (int a = 0; a < nb; ++a) D[a * nb + a] += delta;
     } else {
       for (int a = 0; a < nb; ++a)
         for (int c = 0; c < nb; ++c) D[a * nb + c] = (a == c) ? 1.0 : 0.0;
-      for (int a = 0; a < nb; ++a) R[i * nb + a] = 0.0;
+      for (int a = 0; a < nb; ++a) R[r * nb + a] = 0.0;
     }
-    for (int a = 0; a < nb; ++a) rhs[i * nb + a] = -(R[i * nb + a] + 0.0);
+    for (int a = 0; a < nb; ++a) rhs[r * nb + a] = -(R[r * nb + a] + 0.0);
   }
 }
 
@@ -1947,6 +2012,7 @@ void orc_assemble(int64_t N, int64_t E, int nb, const int64_t* edges, const int6
 // -Res * dt / Vol). Lower bound 0 for density/species/… and -1/EPS for momentum/energy, upper 1/EPS.
 void orc_update(int64_t N, int nb, int nDim, int mode, const double* d, double relax, const double* vol,
                 const double* dt, double* U) {
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < N; ++i)
     for (int v = 0; v < nb; ++v) {
       double delta;
@@ -1967,6 +2033,7 @@ void orc_update(int64_t N, int nb, int nDim, int mode, const double* d, double r
 // U = clip(U_old + (-(Res + 0) * dt / Vol) * alpha) via AddClippedSolution (variable_structure.cpp:207-211).
 void orc_update_rk(int64_t N, int nb, int nDim, const double* Res, double alpha, const double* vol, const double* dt,
                    const double* Uold, double* U) {
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < N; ++i) {
     double Delta = 0.0;
     if (vol[i] > EPS) Delta = dt[i] / vol[i];
@@ -2134,8 +2201,10 @@ int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const 
   const double T_ref = prm[2], E_ref = prm[3], R_ref = prm[4], P_ref = prm[5], Visc_ref = prm[6],
                Cond_ref = prm[7], Vel_ref = prm[8], Len_ref = prm[9];
   int64_t count = 0;
-  try {
-    for (int64_t i = 0; i < N; ++i) {
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 512) reduction(+ : count) reduction(| : err)
+  for (int64_t i = 0; i < N; ++i) {
+    try {
       double* u = U + i * nVar;
       double* v = V + i * nPV;
       const double ke = tke ? tke[i] : 0.0;
@@ -2145,7 +2214,7 @@ int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const 
         for (int q = 0; q < nVar; ++q) u[q] = Uold[i * nVar + q];
         (void)vT0;
         const bool np_old = cons2prim(m, nDim, u, v, ke, prm);
-        if (np_old) return -1;
+        if (np_old) err = 1;
       }
       // Cp = ComputeCP_FromSoundSpeed(T, a, Ys) / R_ref (:304-311)
       const double dim_temp = v[T_] * T_ref, dim_a = v[A_] * Vel_ref;
@@ -2223,11 +2292,11 @@ int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const 
         }
       }
       if (nonPhys) ++count;
+    } catch (const std::exception&) {
+      err = 1;
     }
-  } catch (const std::exception&) {
-    return -1;
   }
-  return (int)count;
+  return err ? -1 : (int)count;
 }
 
 // =================================================================================================
@@ -2262,6 +2331,7 @@ static inline double smax(double a, double b) { return (a < b) ? b : a; }  // st
 void orc_sol_grad_ls(int nDim, int nVar, int64_t N, const double* coord, const double* sol, const int64_t* nptr,
                      const int64_t* nbr, double* grad) {
   double Cv[8][3];
+#pragma omp parallel for schedule(static) private(Cv)
   for (int64_t i = 0; i < N; ++i) {
     bool singular = false;
     const double* ci = coord + i * nDim;
@@ -2357,6 +2427,7 @@ void orc_strain_mag(int nDim, int nG, int64_t N, const double* G, double* out) {
 void orc_sst_blending(int nDim, int64_t N, const double* T, const double* TG, const double* rho, const double* mu,
                       const double* dist, const double* strain, double* F1, double* F2, double* CDkw, double* muT) {
   const SSTConst c = sst_const();
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < N; ++i) {
     const double* t = T + 2 * i;
     const double* g = TG + i * 2 * nDim;
@@ -2380,6 +2451,7 @@ void orc_sst_blending(int nDim, int64_t N, const double* T, const double* TG, co
 // CUpwSca_TurbSST::ComputeResidual (numerics_direct_turbulent.cpp:865-922), 1st order, fixed grid.
 void orc_sst_upwind(int nDim, int nPV, int64_t E, const int64_t* edges, const double* normal, const double* V,
                     const double* T, double* res, double* Ji, double* Jj) {
+#pragma omp parallel for schedule(static)
   for (int64_t e = 0; e < E; ++e) {
     const int64_t i = edges[2 * e], j = edges[2 * e + 1];
     const double* vi = V + i * nPV;
@@ -2407,6 +2479,7 @@ void orc_sst_visc(int nDim, int nPV, int64_t E, const int64_t* edges, const doub
                   const double* V, const double* T, const double* TG, const double* F1, const double* mu,
                   const double* eddy, double* res, double* Ji, double* Jj) {
   const SSTConst c = sst_const();
+#pragma omp parallel for schedule(static)
   for (int64_t e = 0; e < E; ++e) {
     const int64_t i = edges[2 * e], j = edges[2 * e + 1];
     const double* n = normal + e * nDim;
@@ -2454,6 +2527,7 @@ void orc_sst_source(int nDim, int nPV, int nG, int64_t N, const double* V, const
                     const double* vol, const double* dist, const double* F1, const double* F2, const double* CDkw,
                     const double* strain, const double* eddy, double* res, double* J) {
   const SSTConst c = sst_const();
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < N; ++i) {
     double* r = res + 2 * i;
     double* A = J ? J + 4 * i : nullptr;

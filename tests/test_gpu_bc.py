@@ -246,3 +246,36 @@ def test_synthetic_jet_iteration_vs_oracle(nz):
     per_column_close(t.download("U").reshape(N, 2), o["T"], rtol=1e-10, floor=1.0, what="(k, omega) vs oracle")
     assert_close(rms, o["rms"], rtol=1e-10, what="RMS")
     s.close()
+
+
+@pytest.mark.parametrize("mutation", ["set_bc", "fgmres_m"])
+def test_solve_graph_invalidated_by_buffer_changes(mutation):
+    """The captured solve graph bakes in buffer addresses: re-setting the markers (rx_bc_set reallocates the wall
+    list the update reads) or a public rx_fgmres with a longer restart (reallocates the Krylov basis) between two
+    implicit iterations must re-capture it. The sequence is compared bitwise with the same sequence run eagerly
+    (RX_NO_GRAPH=1)."""
+    g = golden("it9")
+    bc = rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"])
+
+    def run(no_graph):
+        if no_graph:
+            os.environ["RX_NO_GRAPH"] = "1"
+        try:
+            s, t = solvers(g, 1)
+            load_iteration_state(g, s, t, 0)
+            rx.Iterate(s, t, ext_iter=0)
+            if mutation == "set_bc":
+                s.set_bc(bc)
+            else:
+                s.fgmres(m=int(g["bc_params"][20]) + 1)
+            load_iteration_state(g, s, t, 1)
+            rms, rms_t, _ = rx.Iterate(s, t, ext_iter=1)
+            s.sync()
+            out = (s.download("U"), t.download("U"), rms, rms_t)
+            s.close()
+            return out
+        finally:
+            os.environ.pop("RX_NO_GRAPH", None)
+
+    for a, b in zip(run(False), run(True)):
+        assert np.array_equal(a, b)
