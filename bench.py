@@ -87,21 +87,22 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
     }
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc.json")
-
-
 def pmc_traffic(kernel, workload_key):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (tools/pmc_summary.py),
-    when they were taken on this workload; else None."""
-    try:
-        with open(PMC_FILE) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if d.get("workload") != workload_key:
-        return None
-    k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k.get("hbm_bytes")
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/r*_pmc*.json, written by
+    tools/pmc_summary.py; the newest file taken on this workload wins); else None."""
+    import glob
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")), reverse=True):
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != workload_key:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k is not None:
+            return k.get("hbm_bytes")
+    return None
 
 
 def build_workload(nx, ny, ns, n_part=1, nz=0):

@@ -822,12 +822,16 @@ bool graphs_enabled(const rx_ctx* ctx) {
 
 }  // namespace
 
+}  // extern "C"
+
 void rx_graph_reset(rx_ctx* ctx) {
   if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
   if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
   ctx->solve_exec = nullptr;
   ctx->solve_graph = nullptr;
 }
+
+extern "C" {
 
 namespace {
 // Shared by the flow and the SST context: system build, preconditioner build (CSysSolve::Solve

@@ -17,6 +17,7 @@
 #include "../../SU2_CFD/include/solver_reactive.hpp"
 #include "../../SU2_CFD/include/numerics_reactive.hpp"
 
+#include <chrono>
 #include <cstdio>
 #include <cstdint>
 #include <fstream>
@@ -462,8 +463,11 @@ int main(int argc, char** argv) {
       }
       for (int k = 0; k < n_iters; ++k) {
         cfg->SetExtIter(k);
+        const auto t0 = std::chrono::steady_clock::now();
         drv.iterate();
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         const std::string p = "it" + std::to_string(k + 1) + "_";
+        dumpd(p + "wall", std::vector<double>{wall}, {1});  // the reference's own time for this iteration
         dump_sol(flow, nVar, false, p + "U");
         std::vector<double> V(nPoint * nPrimVar), rms(nVar);
         for (unsigned long i = 0; i < nPoint; ++i)

@@ -1235,6 +1235,7 @@ extern "C" {
 // Threads the OpenMP loops of this file use (OMP_NUM_THREADS); 1 = the serial restatement. Every parallel loop
 // writes disjoint outputs and keeps the reference's per-item operation order, so results do not depend on it.
 int orc_num_threads() { return omp_get_max_threads(); }
+void orc_set_num_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
 void* orc_mech_create(int ns, int nr, int ntab, const double* mm, const double* dv, const double* sr,
                       const double* sp, const double* er, const double* ep, const double* A, const double* beta,

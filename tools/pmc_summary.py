@@ -2,11 +2,15 @@
 MI355X_MICROARCH.md §rocprofv3 PMC slots requires) -> profiles/<name>.json used by bench.py.
 
 FETCH_SIZE and WRITE_SIZE are in KB per dispatch. On gfx950 FETCH_SIZE under-reads wide streaming
-loads (cdna_hip_programming.md §7), so the read side is calibrated on a kernel with a known byte count
-in the same access pattern: k_dot (FGMRES's |b|^2, one coalesced 8-B-per-lane stream of N*nVar
-doubles). hbm_bytes = FETCH_SIZE*1024*factor + WRITE_SIZE*1024.
+loads (MI355X_MICROARCH.md §HBM: exactly 1/2 for 16-B-per-lane streams), so the read side is calibrated on
+a kernel with a known byte count in a coalesced streaming pattern: k_fg_spmv<nVar>, whose HBM reads are the
+BSR matrix stream (nnzb * nVar^2 * 8 bytes, read once, coalesced 8 B per lane; its column indices and x / y
+vectors are < 5 % and L2/Infinity-Cache resident at these sizes), so factor = matrix bytes / FETCH bytes (≈ 2,
+the guide's gfx950 correction).
+hbm_bytes = FETCH_SIZE*1024*factor + WRITE_SIZE*1024. Kernels are keyed by name with template arguments
+(k_fg_spmv<11>, k_fg_spmv<2>, ...), non-template kernels by name.
 
-python tools/pmc_summary.py <fetch_dir> <write_dir> <workload_key> <n_rhs_doubles> > profiles/r01_pmc.json
+python tools/pmc_summary.py <fetch_dir> <write_dir> <workload_key> <nVar> <nnzb> > profiles/r02_pmc_<wl>.json
 """
 import csv
 import glob
@@ -17,29 +21,33 @@ import sys
 from collections import defaultdict
 
 
-def read_counters(d):
+def read_counters(d, peak=False):
+    """Mean (or, peak=True, max) counter value per dispatch of each kernel."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     acc = defaultdict(lambda: [0.0, 0])
+    mx = defaultdict(float)
     for fn in files:
         with open(fn) as f:
             for r in csv.DictReader(f):
                 name = r.get("Kernel_Name", "")
-                m = re.search(r"::(k_\w+)", name) or re.search(r"(k_\w+)", name)
+                m = re.search(r"(k_\w+(?:<[^>]*>)?)", name)
                 key = m.group(1) if m else name
                 acc[(key, r["Counter_Name"])][0] += float(r["Counter_Value"])
                 acc[(key, r["Counter_Name"])][1] += 1
-    return {k: v[0] / v[1] for k, v in acc.items()}
+                mx[(key, r["Counter_Name"])] = max(mx[(key, r["Counter_Name"])], float(r["Counter_Value"]))
+    return dict(mx) if peak else {k: v[0] / v[1] for k, v in acc.items()}
 
 
 def main():
-    fetch_dir, write_dir, wkey, n_rhs = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    fetch_dir, write_dir, wkey, nv, nnzb = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
     fe = read_counters(fetch_dir)
     wr = read_counters(write_dir)
-    known = 8.0 * n_rhs
-    cal_kb = fe.get(("k_dot", "FETCH_SIZE"))
+    known = 8.0 * nnzb * nv * nv
+    cal = [f"k_fg_spmv<{nv}>"]
+    cal_kb = fe.get((cal[0], "FETCH_SIZE"))
     factor = known / (cal_kb * 1024.0) if cal_kb else 1.0
     out = {"workload": wkey,
-           "calibration": {"kernel": "k_dot", "known_bytes": known, "fetch_kb": cal_kb, "factor": factor},
+           "calibration": {"kernel": cal[0] if cal else None, "known_bytes": known, "fetch_kb": cal_kb, "factor": factor},
            "kernels": {}}
     names = sorted({k for (k, c) in fe} | {k for (k, c) in wr})
     for k in names:
