@@ -71,19 +71,25 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
     blk = nVar * nVar * d
     summ = (14 + 5 * nDim + 9 * ns) * d  # visc_summary_size<NS, NDIM>
     hbm = lambda b, name: dict(bound="hbm", work=float(b), unit="GB/s", peak=HBM_PEAK_GBS, kernel=name)
+    te, tv = f"<{ns}, {nDim}>", f"<{nVar}>"  # template arguments of the flow kernels (rocprof / PMC names)
     return {
         # k_ausm_edge: V (nPV) and dPdU (nVar) per node once; edge (2 int32 + normal); flux + 2 Jacobians
-        "CONV": hbm(N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk), "k_ausm_edge"),
+        "CONV": hbm(N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk), "k_ausm_edge" + te),
         # k_visc_edge: FP64-compute bound, SURVEY §8(d): ~8-10 kflop per edge for flux + closures
-        "VISC": dict(bound="fp64", work=9000.0 * E, unit="TFLOP/s", peak=FP64_PEAK_TFS, kernel="k_visc_edge"),
+        "VISC": dict(bound="fp64", work=9000.0 * E, unit="TFLOP/s", peak=FP64_PEAK_TFS, kernel="k_visc_edge" + te),
         # k_visc_jac: per-edge summary + dT/dU in, two Jacobian blocks out
-        "VISC_JAC": hbm(E * summ + N * nVar * d + E * 2 * blk, "k_visc_jac"),
+        "VISC_JAC": hbm(E * summ + N * nVar * d + E * 2 * blk, "k_visc_jac" + te),
         # k_assemble: 4 scratch blocks per edge + source block per node in; BSR + residual out
-        "ASSEMBLE": hbm((4 * E + N + nnzb) * blk + (2 * E + 2 * N) * nVar * d, "k_assemble"),
-        "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq"),
-        "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar * d + blk), "k_source"),
+        "ASSEMBLE": hbm((4 * E + N + nnzb) * blk + (2 * E + 2 * N) * nVar * d, "k_assemble" + tv),
+        "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq" + te),
+        "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar * d + blk), "k_source" + te),
         # k_ilu_build_part: A in, factor + inv(D) out
-        "ILU_BUILD": hbm((2 * nnzb + N) * blk, "k_ilu_build_part"),
+        "ILU_BUILD": hbm((2 * nnzb + N) * blk, "k_ilu_build_part" + tv),
+        # SOLVE phase (inside the FGMRES graph; timed one launch at a time after the timed region):
+        # y = A x: every block + its column index once, x gathered, y written
+        "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d, "k_spmv" + tv),
+        # ILU(0) apply: L and U blocks + inv(D_i) (= nnzb blocks) + column indices, b in, x out
+        "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, f"k_ilu_fwd_part{tv}+k_ilu_bwd_part{tv}"),
     }
 
 
@@ -99,9 +105,9 @@ def pmc_traffic(kernel, workload_key):
             continue
         if d.get("workload") != workload_key:
             continue
-        k = d.get("kernels", {}).get(kernel)
-        if k is not None:
-            return k.get("hbm_bytes")
+        ks = [d.get("kernels", {}).get(p) for p in kernel.split("+")]  # "a+b": both launches of one phase
+        if all(k is not None for k in ks):
+            return sum(k["hbm_bytes"] for k in ks)
     return None
 
 
@@ -315,11 +321,22 @@ def main():
     prof = {k: s.profile_read(k) for k in rx.K}
     tprof = {k: t.profile_read(k) for k in rx.K}
     prof = {k: (prof[k][0] + tprof[k][0], prof[k][1] + tprof[k][1]) for k in rx.K}
+    # the SOLVE phase's two HBM kernels one launch at a time (in the step they run inside the FGMRES graph): the
+    # flow system and ILU(0) factor of the last step, public rx_bsr_spmv / rx_ilu0_apply (plain SpMV; the graph's
+    # k_fg_spmv adds the MGS inner products)
+    s.profile(True)
+    for _ in range(5):
+        s.spmv("RHS", "SOL")
+    for _ in range(5):
+        s.ilu0_apply("RHS", "SOL")
+    s.sync()
+    for k in ("SPMV", "ILU_APPLY"):
+        prof[k] = s.profile_read(k)
     s.profile(False)
     t.profile(False)
 
     models = kernel_models(N, E, nnzb, ns, nDim, 5)
-    phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0}
+    phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0 and k not in ("SPMV", "ILU_APPLY")}
     dims = f"{nx}x{ny}" + (f"x{nz}" if nz > 1 else "")
     wkey = f"{args.workload} {dims} ns{ns} parts{args.parts}"
 
@@ -343,8 +360,9 @@ def main():
 
     timed = [k for k in models if prof[k][1] > 0]
     kernels = {k: roof(k) for k in timed}
-    # dominant kernel: the longest average launch among the single-launch phases
-    dom = max(timed, key=lambda k: prof[k][0] / prof[k][1])
+    # dominant kernel: the longest average launch among the per-step phases (SPMV / ILU_APPLY are timed outside
+    # the step, above)
+    dom = max((k for k in timed if k not in ("SPMV", "ILU_APPLY")), key=lambda k: prof[k][0] / prof[k][1])
 
     if world > 1:
         tot = [None] * world

@@ -534,13 +534,20 @@ class TurbSSTSolver:
         self._call("rx_bc_sst")
 
 
-def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=False):
+def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=None, rk_alpha=None):
     """One reference outer iteration for REACTIVE_RANS on the device, in the reference's order
     (CMeanFlowIteration::Iterate iteration_structure.cpp:486-560; CMultiGridIntegration::MultiGrid_Iteration
-    integration_time.cpp:40-140 with MGLEVEL = 0; CSingleGridIntegration::SingleGrid_Iteration :770-810):
-    flow Preprocessing, SetTime_Step, Space_Integration (loops + BCs), ImplicitEuler_Iteration, the flow
-    Preprocessing(Output = true) on the updated solution; then the SST iteration. Nothing leaves the device
-    except the two RMS vectors and the linear-solver counts. Returns (rms_flow, rms_turb, lin_iters)."""
+    integration_time.cpp:40-140 with MGLEVEL = 0, whose MultiGrid_Cycle pre-smoothing sweep runs iRKLimit stages
+    :144-183; CSingleGridIntegration::SingleGrid_Iteration :770-810). Each flow stage: Preprocessing
+    (SetPrimitive_Variables, gradient, StrainMag, the limiter for 2ND_ORDER_LIMITER), Set_OldSolution + SetTime_Step
+    at stage 0, Space_Integration (loops + BCs), Time_Integration (integration_structure.cpp:325-335):
+    ImplicitEuler_Iteration when the flow cfg is implicit, else ExplicitEuler_Iteration (EULER_EXPLICIT, rk_alpha
+    None) or one ExplicitRK_Iteration per RK_ALPHA_COEFF entry (RUNGE-KUTTA_EXPLICIT). Then the flow
+    Preprocessing(Output = true) on the updated solution and the SST iteration. limiter None: from
+    cfg.spatial_order == 2 (SECOND_ORDER_LIMITER, solver_direct_reactive.cpp:4739-4742). Nothing leaves the device
+    except the RMS vectors and the linear-solver counts. Returns (rms_flow of the last stage, rms_turb, lin_iters)."""
+    if limiter is None:
+        limiter = flow.cfg.spatial_order == 2
 
     def preprocess(output):
         flow.SetPrimitive_Variables(ext_iter)
@@ -549,14 +556,24 @@ def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=Fal
         if limiter and not output:
             flow.SetPrimitive_Limiter()
 
-    preprocess(False)
-    flow.SetTime_Step()
-    flow.Preprocessing_zero()
-    flow.Upwind_Residual()
-    flow.Viscous_Residual()
-    flow.Source_Residual()
-    flow.BC()
-    rms, it = flow.ImplicitEuler_Iteration()
+    implicit = bool(flow.cfg.implicit)
+    stages = [None] if implicit or not rk_alpha else list(rk_alpha)
+    it = 0
+    for k, alpha in enumerate(stages):
+        preprocess(False)
+        if k == 0:
+            flow.SetTime_Step()
+        flow.Preprocessing_zero()
+        flow.Upwind_Residual()
+        flow.Viscous_Residual()
+        flow.Source_Residual()
+        flow.BC()
+        if implicit:
+            rms, it = flow.ImplicitEuler_Iteration()
+        elif alpha is None:
+            rms = flow.ExplicitEuler_Iteration()
+        else:
+            rms = flow.ExplicitRK_Iteration(k, alpha)
     preprocess(True)
     turb.Preprocessing()
     turb.Upwind_Residual()

@@ -116,39 +116,50 @@ def jet_case(nx, ny, records="jet9w", seed=12345, n_species=9, n_part=1, nz=0):
 JET_LENGTH, JET_HEIGHT = 0.125, 0.006  # mesh_stretched.su2's domain (meshgen.jet_points)
 
 
+def fold_matrix(n_species, ns0=9):
+    """[ns0][n_species] map of the 9 jet species' partial densities onto the first n_species (SPECIES_ORDER C4H6,
+    H2O, O2, CO, CO2, H2, O, OH, H): the dropped radicals / H2 go to O2; for 4 species CO2 goes to H2O and CO in the
+    mass ratio 0.53 : 0.47, which keeps the mixture's formation enthalpy per unit mass (CO2 -8.94 kJ/g = 0.53 x
+    H2O -13.42 + 0.47 x CO -3.95), so rho, rho E and T stay close to the reference's state."""
+    M = np.zeros((ns0, n_species))
+    for s in range(min(ns0, n_species)):
+        M[s, s] = 1.0
+    for s in range(n_species, ns0):
+        if s == 4:  # CO2
+            M[s, 1], M[s, 3] = 0.53, 0.47
+        else:
+            M[s, 2] = 1.0
+    return M
+
+
+def fold_species(U, n_species, fl=4, ns0=9):
+    """Conservative state of the first n_species species from a 9-species one (fold_matrix); columns after the
+    species (k, omega) are kept."""
+    U = np.asarray(U, dtype=np.float64)
+    return np.concatenate([U[:, :fl], U[:, fl:fl + ns0] @ fold_matrix(n_species, ns0), U[:, fl + ns0:]], axis=1)
+
+
 def field_subset(g, n_species):
-    """Restrict the reference's 9-species field (and mechanism) to its first n_species species: the dropped
-    partial densities are folded into the kept ones in proportion (rho and rho E unchanged), so the state stays
-    a valid conservative state of the smaller mixture; T is re-derived by Cons2PrimVar on the device."""
+    """Restrict the reference's 9-species field (and mechanism) to its first n_species species, the dropped
+    partial densities folded into the kept ones (fold_species: rho unchanged, formation enthalpy kept); T is
+    re-derived by Cons2PrimVar on the device."""
     ns0 = int(g["mech_n_species"])
     if n_species == ns0:
         return g
     out = species_subset(g, np.arange(n_species))
     nDim = int(np.shape(g["coord"])[1])
-    fl = nDim + 2
-    U = np.asarray(g["U"], dtype=np.float64)
-    rs = U[:, fl:fl + ns0]
-    kept = rs[:, :n_species]
-    tot = rs.sum(axis=1, keepdims=True)
-    ks = kept.sum(axis=1, keepdims=True)
-    out["U"] = np.concatenate([U[:, :fl], kept * (tot / np.where(ks > 0, ks, 1.0))], axis=1)
+    out["U"] = fold_species(g["U"], n_species, fl=nDim + 2, ns0=ns0)
     return out
 
 
-def jet_field_case(nx, ny, n_species=7, n_part=1, nz=0, field="jet9k"):
-    """Mesh (RCM-ordered median dual, partitioned) + a smooth, physically consistent initial state for an nx x ny
-    (x nz) jet: the reference's converged PaSR field on its own 9 000-point mesh (tests/golden/jet9k.npz, after the
-    reference's preprocessing) linearly interpolated onto the synthetic mesh, which covers the same physical domain
-    (SURVEY.md §8(d) 'bilinearly interpolate flow_second_chem.dat onto the finer mesh'). Interpolated quantities are
-    the conservatives U, (k, omega), mu_t and T (the secant's starting temperature); a convex combination of
-    valid conservative states is a valid conservative state. The other node records (V, dP/dU, dT/dU, mu, kappa,
-    D_ij, SST fields) are produced on the device by the reference's preprocessing sequence (device_preprocess).
-    3-D: spanwise-uniform (rho w = 0)."""
-    mg = _meshgen()
-    mesh = mg.build_jet(nx, ny, n_part=n_part, nz=nz)
+def field_at(xy, n_species=7, field="jet9k"):
+    """The reference's converged PaSR jet (tests/golden/jet9k.npz: its own 9 000-point mesh after its start-up
+    preprocessing) linearly interpolated at the physical points xy [n][2] of the jet domain: (g, U, k, omega,
+    mu_t, T) with g the (species-restricted) field dict. Species are floored at a mass fraction of 1e-10 (see
+    below)."""
     g = field_subset(load_records(field), n_species)
     src = np.asarray(g["coord"]) / np.array([JET_LENGTH, JET_HEIGHT])
-    dst = np.asarray(mesh["coord"])[:, :2] / np.array([JET_LENGTH, JET_HEIGHT])
+    dst = np.asarray(xy)[:, :2] / np.array([JET_LENGTH, JET_HEIGHT])
     vals = np.concatenate([g["U"], np.stack([g["turb_k"], g["turb_omega"], g["mu_t"], g["V"][:, 0]], axis=1)],
                           axis=1)
     from scipy.interpolate import LinearNDInterpolator
@@ -170,7 +181,21 @@ def jet_field_case(nx, ny, n_species=7, n_part=1, nz=0, field="jet9k"):
     rs = U[:, 4:]
     np.maximum(rs, 1e-10 * rho[:, None], out=rs)
     rs *= (rho / rs.sum(axis=1))[:, None]
-    k, om, mut, T = (out[:, nU + q] for q in range(4))
+    return g, U, out[:, nU], out[:, nU + 1], out[:, nU + 2], out[:, nU + 3]
+
+
+def jet_field_case(nx, ny, n_species=7, n_part=1, nz=0, field="jet9k"):
+    """Mesh (RCM-ordered median dual, partitioned) + a smooth, physically consistent initial state for an nx x ny
+    (x nz) jet: the reference's converged PaSR field on its own 9 000-point mesh (tests/golden/jet9k.npz, after the
+    reference's preprocessing) linearly interpolated onto the synthetic mesh, which covers the same physical domain
+    (SURVEY.md §8(d) 'bilinearly interpolate flow_second_chem.dat onto the finer mesh'; field_at). Interpolated
+    quantities are the conservatives U, (k, omega), mu_t and T (the secant's starting temperature); a convex
+    combination of valid conservative states is a valid conservative state. The other node records (V, dP/dU,
+    dT/dU, mu, kappa, D_ij, SST fields) are produced on the device by the reference's preprocessing sequence
+    (device_preprocess). 3-D: spanwise-uniform (rho w = 0)."""
+    mg = _meshgen()
+    mesh = mg.build_jet(nx, ny, n_part=n_part, nz=nz)
+    g, U, k, om, mut, T = field_at(mesh["coord"], n_species, field)
     nDim = 3 if nz > 1 else 2
     if nDim == 3:
         U = np.concatenate([U[:, :3], np.zeros((len(U), 1)), U[:, 3:]], axis=1)

@@ -56,6 +56,7 @@ class ReactiveNSSolver {
 
   rx_ctx* context() const { return ctx_; }
   int nVar() const { return nvar_; }
+  const rx_cfg& config() const { return cfg_; }
 
   // ---- node state (Preprocessing output of the reference: primitives, transport, SST fields)
   void Upload(rx_field f, const std::vector<double>& host) {
@@ -179,23 +180,40 @@ class TurbSSTSolver {
 };
 
 // One outer iteration in the reference's order (CMultiGridIntegration::MultiGrid_Iteration with MGLEVEL = 0,
-// integration_time.cpp:40-140, then CSingleGridIntegration::SingleGrid_Iteration :770-810 for the SST solver).
-// Returns the flow RMS; turb_rms gets the SST one.
+// integration_time.cpp:40-140: MultiGrid_Cycle's pre-smoothing sweep of iRKLimit stages :144-183, each with its own
+// Preprocessing and Space_Integration, Set_OldSolution + SetTime_Step at stage 0, then Time_Integration
+// (integration_structure.cpp:325-335), and the Preprocessing(Output = true) of the updated solution; then
+// CSingleGridIntegration::SingleGrid_Iteration :770-810 for the SST solver). TIME_DISCRE_FLOW follows the flow
+// context's cfg: implicit -> ImplicitEuler_Iteration; explicit with rk_alpha empty -> ExplicitEuler_Iteration
+// (EULER_EXPLICIT); explicit with rk_alpha = RK_ALPHA_COEFF -> one ExplicitRK_Iteration per stage
+// (RUNGE-KUTTA_EXPLICIT). SPATIAL_ORDER_FLOW = 2ND_ORDER_LIMITER (cfg.spatial_order == 2) adds
+// SetPrimitive_Limiter to the non-Output Preprocessing (solver_direct_reactive.cpp:4739-4742).
+// Returns the flow RMS (of the last stage); turb_rms gets the SST one.
 inline std::vector<double> Iterate(ReactiveNSSolver& flow, TurbSSTSolver& turb, int ext_iter,
-                                   std::vector<double>* turb_rms = nullptr) {
-  flow.SetPrimitive_Variables(ext_iter);
-  flow.SetPrimitive_Gradient_LS();
-  flow.SetStrainMag();
-  flow.SetTime_Step();
-  flow.Preprocessing();
-  flow.Upwind_Residual();
-  flow.Viscous_Residual();
-  flow.Source_Residual();
-  flow.BC_Apply();
-  std::vector<double> rms = flow.ImplicitEuler_Iteration();
-  flow.SetPrimitive_Variables(ext_iter);  // Preprocessing(Output = true) on the updated solution
-  flow.SetPrimitive_Gradient_LS();
-  flow.SetStrainMag();
+                                   std::vector<double>* turb_rms = nullptr,
+                                   const std::vector<double>& rk_alpha = std::vector<double>()) {
+  const rx_cfg& cfg = flow.config();
+  auto preprocess = [&](bool output) {
+    flow.SetPrimitive_Variables(ext_iter);
+    flow.SetPrimitive_Gradient_LS();
+    flow.SetStrainMag();
+    if (cfg.spatial_order == 2 && !output) flow.SetPrimitive_Limiter();
+  };
+  const size_t stages = (!cfg.implicit && !rk_alpha.empty()) ? rk_alpha.size() : 1;
+  std::vector<double> rms;
+  for (size_t k = 0; k < stages; ++k) {
+    preprocess(false);
+    if (k == 0) flow.SetTime_Step();
+    flow.Preprocessing();
+    flow.Upwind_Residual();
+    flow.Viscous_Residual();
+    flow.Source_Residual();
+    flow.BC_Apply();
+    if (cfg.implicit) rms = flow.ImplicitEuler_Iteration();
+    else if (rk_alpha.empty()) rms = flow.ExplicitEuler_Iteration();
+    else rms = flow.ExplicitRK_Iteration((int)k, rk_alpha[k]);
+  }
+  preprocess(true);  // Preprocessing(Output = true) on the updated solution
   turb.Preprocessing();
   turb.Upwind_Residual();
   turb.Viscous_Residual();

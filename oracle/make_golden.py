@@ -82,7 +82,7 @@ MGLEVEL= 0
 CONV_NUM_METHOD_FLOW= AUSM
 SPATIAL_ORDER_FLOW= {order}
 SLOPE_LIMITER_FLOW= VENKATAKRISHNAN
-TIME_DISCRE_FLOW= EULER_IMPLICIT
+TIME_DISCRE_FLOW= {time_flow}
 CONV_NUM_METHOD_TURB= SCALAR_UPWIND
 SLOPE_LIMITER_TURB= VENKATAKRISHNAN
 TIME_DISCRE_TURB= EULER_IMPLICIT
@@ -126,18 +126,68 @@ INLETS = {
 }
 
 
-def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATURE_IMPOSE", extra=""):
+SPECIES9 = ("C4H6", "H2O", "O2", "CO", "CO2", "H2", "O", "OH", "H")
+
+
+def write_subset_library(wd, ns):
+    """Library input files of the first `ns` species of the jet mixture (7 species = both shipped
+    reactions; 4 species = reaction 1 only), written into the work dir in the reference's own formats
+    (Mixture / Chemistry / list file); the per-species Thermo / Transp tables are the reference's, read in place."""
+    os.makedirs(os.path.join(wd, "Mixture"))
+    os.makedirs(os.path.join(wd, "Chemistry"))
+    for d in ("Thermo", "Transp"):
+        os.symlink(os.path.join(CASE_DIR, d), os.path.join(wd, d))
+    mix = open(os.path.join(CASE_DIR, "Mixture/Test_Mixture.txt")).read().splitlines()
+    rows = [ln for ln in mix if ln.split() and ln.split()[0] in SPECIES9[:ns]]
+    with open(os.path.join(wd, "Mixture/Test_Mixture.txt"), "w") as f:
+        f.write("//Number of species\n%d\n%s\n" % (ns, mix[2]) + "\n".join(rows) + "\n\nSTOP\n")
+    chem = open(os.path.join(CASE_DIR, "Chemistry/Test_Reactions_second.txt")).read()
+    if ns < 5:  # reaction 2 (CO + 0.5 O2 <=> CO2) needs CO2: reaction 1 only
+        head, rest = chem.split("//Reactions", 1)
+        r1 = rest.strip().split("\n\n")[0]
+        chem = head.replace("2\n", "1\n", 1) + "//Reactions\n" + r1 + "\n\nSTOP\n"
+    with open(os.path.join(wd, "Chemistry/Test_Reactions_second.txt"), "w") as f:
+        f.write(chem)
+    with open(os.path.join(wd, "test_chem_second.txt"), "w") as f:
+        f.write("Mixture/Test_Mixture.txt\nChemistry/Test_Reactions_second.txt\n")
+        for sp in SPECIES9[:ns]:
+            f.write(f"Transp/{sp}_transp.txt\nThermo/{sp}_thermo.txt\n")
+
+
+def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATURE_IMPOSE", extra="",
+                 time_flow="EULER_IMPLICIT", ns=9):
     wd = os.path.join("/tmp/rx_golden", case)
     shutil.rmtree(wd, ignore_errors=True)
     os.makedirs(os.path.join(wd, "out"))
-    for d in ("Mixture", "Chemistry", "Thermo", "Transp"):
-        os.symlink(os.path.join(CASE_DIR, d), os.path.join(wd, d))
-    os.symlink(os.path.join(CASE_DIR, "test_chem_second.txt"), os.path.join(wd, "test_chem_second.txt"))
+    if ns == 9:
+        for d in ("Mixture", "Chemistry", "Thermo", "Transp"):
+            os.symlink(os.path.join(CASE_DIR, d), os.path.join(wd, d))
+        os.symlink(os.path.join(CASE_DIR, "test_chem_second.txt"), os.path.join(wd, "test_chem_second.txt"))
+    else:
+        write_subset_library(wd, ns)
     mesh_name = mesh_writer(wd)
+    cfg = CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec, inlet_type=inlet,
+                              inlet_ox=INLETS[inlet][0], inlet_fuel=INLETS[inlet][1], extra=extra, time_flow=time_flow)
+    if ns != 9:  # the mixture's species lists
+        y = lambda k: ", ".join("1.0" if q == k else "0.0" for q in range(ns))
+        cfg = cfg.replace("FREESTREAM_MASS_FRAC = (0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)",
+                          f"FREESTREAM_MASS_FRAC = ({y(2)})")
+        cfg = cfg.replace("SPECIES_ORDER = (C4H6, H2O, O2, CO, CO2, H2, O, OH, H)",
+                          "SPECIES_ORDER = (" + ", ".join(SPECIES9[:ns]) + ")")
+        cfg = cfg.replace("INLET_MASS_FRAC = (Oxidizer_Inlet, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0; Fuel_Inlet, "
+                          "1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)",
+                          f"INLET_MASS_FRAC = (Oxidizer_Inlet, {y(2)}; Fuel_Inlet, {y(0)})")
     with open(os.path.join(wd, "case.cfg"), "w") as f:
-        f.write(CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec, inlet_type=inlet,
-                                    inlet_ox=INLETS[inlet][0], inlet_fuel=INLETS[inlet][1], extra=extra))
+        f.write(cfg)
     return wd
+
+
+synth = _load("rx_synth", os.path.join(PKG, "synth.py"))
+
+
+def fold_species(U, ns):
+    """Conservative state of the first ns species (synth.fold_species, the bench's own fold)."""
+    return synth.fold_species(U, ns)
 
 
 def write_state(wd, U):
@@ -419,6 +469,58 @@ def case_jet9k():
     return out
 
 
+# keys an iteration golden keeps (the rest of the harness dump is the per-operator data the other cases hold)
+ITER_KEEP = ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr", "bvertex", "bvertex_normal", "wall_distance",
+             "bvertex_pn", "bc_marker", "bc_params", "dims", "mach_inf", "visc_params", "src_params", "dt_params",
+             "p2v_params", "bsr_row_ptr", "bsr_col", "global_index")
+
+
+def iteration_case(name, writer, U, ns, n_iters, cfl, prec, time_flow, extra=""):
+    wd = make_workdir(name, writer, cfl=cfl, order="1ST_ORDER", prec=prec, time_flow=time_flow, ns=ns, extra=extra)
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--iters", str(n_iters)])
+    out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it")}
+    big = len(a["coord"]) > 5000  # whole-mesh cases: one iteration, no later Solution_Old needed
+    out = {k: v for k, v in out.items()
+           if not k.endswith("_wall") and not (big and k.endswith("_Uold") and k != "it_Uold0")}
+    out.update(mech_arrays(wd) if ns != 9 else mech_arrays())
+    out["time_flow"] = np.array(time_flow)
+    out["lin_prec"] = np.array(prec)
+    if "RK_ALPHA_COEFF" in extra:
+        out["rk_alpha"] = np.array([float(x) for x in extra.split("(")[1].split(")")[0].split(",")])
+    return out
+
+
+def full_jet_writer(wd):
+    os.symlink(os.path.join(CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
+    return "mesh.su2"
+
+
+def case_itx9():
+    """The reference's shipped jet setup (my_combustion_second_chem_PaSR.cfg: TIME_DISCRE_FLOW = EULER_EXPLICIT,
+    CFL 0.1, implicit SST with LU_SGS) on its whole 9 000-point mesh_stretched.su2 from its converged PaSR state,
+    9 species: one whole reference outer iteration (the fixture holds the whole mesh; a second iteration would
+    double it)."""
+    _, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    return iteration_case("itx9", full_jet_writer, cons, 9, 1, 0.1, "LU_SGS", "EULER_EXPLICIT")
+
+
+def case_itx4():
+    """BASELINE configs[0] (C1): the 9 000-point jet, 4 species (reaction 1 only; library files of the mixture's
+    first four species), explicit Runge-Kutta (RK_ALPHA_COEFF 0.66667 / 0.66667 / 1), SST with LU_SGS, from the
+    converged state with the dropped species folded in: one reference outer iteration (three RK stages)."""
+    _, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    return iteration_case("itx4", full_jet_writer, fold_species(cons, 4), 4, 1, 0.1, "LU_SGS", "RUNGE-KUTTA_EXPLICIT",
+                          extra="RK_ALPHA_COEFF= ( 0.66667, 0.66667, 1.000000 )\n")
+
+
+def case_it7():
+    """The bench mechanism (7 species, both reactions) through the reference: the mini9 jet, implicit ILU0, two
+    reference outer iterations."""
+    pts, quads, U, writer = mini9_inputs()
+    return iteration_case("it7", writer, fold_species(U, 7), 7, 2, 5.0, "ILU0", "EULER_IMPLICIT")
+
+
 FP_DIR = os.path.join(REF, "Test_Cases/TURBOLENT/TURBOLENT_FLAT_PLATE")
 FP_CFG = """\
 % golden-vector cfg written by oracle/make_golden.py: the reference's turbulent flat plate (air, 3 species, no
@@ -568,7 +670,7 @@ def main():
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
-             "fp3": case_fp3, "jet9k": case_jet9k}[case]()
+             "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "it7": case_it7}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

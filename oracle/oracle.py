@@ -532,9 +532,12 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     (CMeanFlowIteration::Iterate iteration_structure.cpp:486-560 -> CMultiGridIntegration::MultiGrid_Iteration
     integration_time.cpp:40-140 with MGLEVEL = 0, then CSingleGridIntegration::SingleGrid_Iteration :770-810):
       flow  Preprocessing (SetPrimitive_Variables, LSQ gradient, StrainMag), Set_OldSolution, SetTime_Step,
-            Space_Integration (upwind, viscous, source, weak then strong BCs), ImplicitEuler_Iteration (ILU0 FGMRES),
-            Preprocessing(Output = true) on the updated solution;
-      SST   Preprocessing (gradient), Space_Integration (loops + BCs), ImplicitEuler_Iteration, Postprocessing.
+            Space_Integration (upwind, viscous, source, weak then strong BCs), ImplicitEuler_Iteration (ILU0 FGMRES)
+            — or, cfg["time"] = "euler_explicit" / "rk", ExplicitEuler_Iteration / the RK_ALPHA_COEFF stages of
+            ExplicitRK_Iteration, each stage with its own Preprocessing and Space_Integration (MultiGrid_Cycle
+            integration_time.cpp:144-183) —, then Preprocessing(Output = true) on the updated solution;
+      SST   Preprocessing (gradient), Space_Integration (loops + BCs), ImplicitEuler_Iteration (cfg["sst_prec"] ILU0 or
+            LU-SGS), Postprocessing.
     s: state dict (U, V, Uold, T = (k, omega), TG, F1, F2, CDkw, mut) — returned updated with the iteration's
     RMS (rms, sst_rms) and linear-solver counts. bc: dict(marker, prm) of the golden's bc_marker / oracle bc_prm.
     keep=False drops the copies of the loop-only system kept for the tests (bench.py's CPU baseline)."""
@@ -555,39 +558,54 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         return o, G, strain_mag(nDim, G)
 
     T, TG, mut = s["T"], s["TG"], s["mut"]
-    o, G, strain = preprocess(s["U"], s["V"], s["Uold"], T, mut)
-    U = o["U"]
-    Uold = U.copy()  # Set_OldSolution (integration_time.cpp:162)
-    dt, _, _ = time_step(nDim, ns, mesh["edges"], mesh["edge_normal"], mesh["bvertex"], mesh["bvertex_normal"], o["V"],
-                         o["dPdU"], o["mu"], o["eddy"], vol, mesh["nbr_ptr"],
-                         [cfg["cfl"], cfg["max_delta_time"], cfg["prandtl_lam"], cfg["prandtl_turb"]])
+    scheme = cfg.get("time", "implicit")  # TIME_DISCRE_FLOW: implicit | euler_explicit | rk (RK_ALPHA_COEFF)
+    alphas = list(cfg.get("rk_alpha", [1.0])) if scheme == "rk" else [None]
     gk = np.ascontiguousarray(TG[:, 0, :])
-    rc, Jci, Jcj = ausm_edges(nDim, ns, mesh["edges"], mesh["edge_normal"], o["V"], o["dPdU"], cfg["mach_inf"], True)
-    rv, Jvi, Jvj = visc_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], o["V"], G, o["mu"],
-                              o["kappa"], o["Dij"], o["dTdU"], T[:, 0].copy(), mut, sig, gk, True, True,
-                              [1, 1, 1, cfg["prandtl_turb"], cfg["lewis_turb"]])
-    rs, Js = source_cells(mech, nDim, o["V"], o["dTdU"], vol, T[:, 1].copy(), True, True,
-                          [cfg["c_mu"], cfg["pasr_lb"], 1, 1, 1])
-    R, A, _ = assemble(rp, col, mesh["edges"], rc, Jci, Jcj, rv, Jvi, Jvj, rs, Js, vol, np.full(N, np.inf), nb)
-    R = np.ascontiguousarray(R)
-    A = np.ascontiguousarray(A)
-    st = dict(U=U, V=o["V"], dPdU=o["dPdU"], dTdU=o["dTdU"], grad_prim=G, mu=o["mu"], kappa=o["kappa"], Dij=o["Dij"],
-              turb_k=T[:, 0].copy(), mu_t=mut, sigma_k=sig, grad_k=gk, eddy_visc_flow=o["eddy"])
-    A_loops, R_loops = (A.copy(), R.copy()) if keep else (None, None)
-    charac = bc_flow(mech, nDim, mesh, bc["marker"], bc["prm"], st, rp, col, R, A, Uold, True, True)
+    U, Vg, Uold = s["U"], s["V"], s["Uold"]
+    # MultiGrid_Cycle (integration_time.cpp:144-183), MGLEVEL = 0: one pre-smoothing sweep of iRKLimit stages
+    for k, alpha in enumerate(alphas):
+        o, G, strain = preprocess(U, Vg, Uold, T, mut)
+        U = o["U"]
+        if k == 0:
+            Uold = U.copy()  # Set_OldSolution (integration_time.cpp:162)
+            dt, _, _ = time_step(nDim, ns, mesh["edges"], mesh["edge_normal"], mesh["bvertex"], mesh["bvertex_normal"],
+                                 o["V"], o["dPdU"], o["mu"], o["eddy"], vol, mesh["nbr_ptr"],
+                                 [cfg["cfl"], cfg["max_delta_time"], cfg["prandtl_lam"], cfg["prandtl_turb"]])
+        imp = scheme == "implicit"
+        rc, Jci, Jcj = ausm_edges(nDim, ns, mesh["edges"], mesh["edge_normal"], o["V"], o["dPdU"], cfg["mach_inf"], imp)
+        rv, Jvi, Jvj = visc_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], o["V"], G, o["mu"],
+                                  o["kappa"], o["Dij"], o["dTdU"], T[:, 0].copy(), mut, sig, gk, True, imp,
+                                  [1, 1, 1, cfg["prandtl_turb"], cfg["lewis_turb"]])
+        rs, Js = source_cells(mech, nDim, o["V"], o["dTdU"], vol, T[:, 1].copy(), True, imp,
+                              [cfg["c_mu"], cfg["pasr_lb"], 1, 1, 1])
+        R, A, _ = assemble(rp, col, mesh["edges"], rc, Jci if imp else None, Jcj, rv, Jvi, Jvj, rs, Js if imp else None,
+                           vol, np.full(N, np.inf), nb)
+        R = np.ascontiguousarray(R)
+        A = np.ascontiguousarray(A) if imp else None
+        st = dict(U=U, V=o["V"], dPdU=o["dPdU"], dTdU=o["dTdU"], grad_prim=G, mu=o["mu"], kappa=o["kappa"],
+                  Dij=o["Dij"], turb_k=T[:, 0].copy(), mu_t=mut, sigma_k=sig, grad_k=gk, eddy_visc_flow=o["eddy"])
+        A_loops, R_loops = (A.copy() if imp else None, R.copy()) if keep else (None, None)
+        charac = bc_flow(mech, nDim, mesh, bc["marker"], bc["prm"], st, rp, col, R, A, Uold, imp, True)
+        if not imp:  # ExplicitEuler_Iteration (solver_direct_reactive.cpp:2414-2449) / ExplicitRK_Iteration (:2456-2493)
+            Un = update(Uold, R, nDim, 1, 1.0, vol, dt) if alpha is None else update_rk(Uold, R, nDim, alpha, vol, dt)
+            rms = np.maximum(1e-32, np.sqrt(np.sum(R * R, axis=0) / N))
+            it, rhs, x = 0, None, None
+            U, Vg = Un, o["V"]
     diag = np.nonzero(np.asarray(col) == np.repeat(np.arange(N), np.diff(rp)))[0]  # the diagonal block of each row
-    ok = dt > 1e-16
-    D = A[diag]
-    idx = np.arange(nb)
-    D[:, idx, idx] += np.where(ok, vol / np.where(ok, dt, 1.0), 0.0)[:, None]
-    D[~ok] = np.eye(nb)
-    R[~ok] = 0.0
-    A[diag] = D
-    rhs = -(R + 0.0)
-    F = ilu_build(rp, col, A, part_ptr)
-    x, it, _ = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"], part_ptr=part_ptr)
-    Un = update(Uold, x, nDim, 0, cfg["relaxation"], vol, dt)
-    rms = np.maximum(1e-32, np.sqrt(np.sum(rhs * rhs, axis=0) / N))
+    if imp:
+        ok = dt > 1e-16
+        D = A[diag]
+        idx = np.arange(nb)
+        D[:, idx, idx] += np.where(ok, vol / np.where(ok, dt, 1.0), 0.0)[:, None]
+        D[~ok] = np.eye(nb)
+        R[~ok] = 0.0
+        A[diag] = D
+        rhs = -(R + 0.0)
+        F = ilu_build(rp, col, A, part_ptr)
+        x, it, _ = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                          part_ptr=part_ptr)
+        Un = update(Uold, x, nDim, 0, cfg["relaxation"], vol, dt)
+        rms = np.maximum(1e-32, np.sqrt(np.sum(rhs * rhs, axis=0) / N))
     # MultiGrid_Iteration's Preprocessing(Output = true) on the updated solution (integration_time.cpp:127-129)
     o2, G2, strain2 = preprocess(Un, o["V"], Uold, T, mut)
     Un = o2["U"]
@@ -612,9 +630,13 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     D2[:, 1, 1] += delta
     A2[diag] = D2
     rhs2 = -R2
-    F2 = ilu_build(rp, col, A2, part_ptr)
-    x2, it2, _ = fgmres(rp, col, A2, rhs2.ravel(), "ilu", F=F2, tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                        part_ptr=part_ptr)
+    if cfg.get("sst_prec", "ilu") == "ilu":
+        F2 = ilu_build(rp, col, A2, part_ptr)
+        x2, it2, _ = fgmres(rp, col, A2, rhs2.ravel(), "ilu", F=F2, tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                            part_ptr=part_ptr)
+    else:  # LINEAR_SOLVER_PREC = LU_SGS (the shipped jet cfg)
+        x2, it2, _ = fgmres(rp, col, A2, rhs2.ravel(), "lusgs", tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                            part_ptr=part_ptr)
     Tn = sst_update(T, x2.ravel(), cfg.get("relaxation_turb", 1.0), rho, np.ascontiguousarray(Uold[:, 0]))
     sst_rms = np.maximum(1e-32, np.sqrt(np.sum(rhs2 * rhs2, axis=0) / N))
     TG1 = sol_grad_ls(nDim, mesh["coord"], Tn, mesh["nbr_ptr"], mesh["nbr"])

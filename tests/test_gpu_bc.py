@@ -35,12 +35,22 @@ def cfg_kw(g):
                 relaxation=float(bp[22]), t_min=float(p2v[1]), t_max=float(p2v[2]))
 
 
+def scheme(g):
+    """(flow implicit?, RK_ALPHA_COEFF or None, SST lin_prec) of a golden's cfg (it9 / it3d: implicit, ILU0)."""
+    tf = str(g["time_flow"]) if "time_flow" in g else "EULER_IMPLICIT"
+    rk = [float(x) for x in g["rk_alpha"]] if "rk_alpha" in g else None
+    prec = 0 if ("lin_prec" in g and str(g["lin_prec"]) == "LU_SGS") else 1
+    return tf == "EULER_IMPLICIT", rk, prec
+
+
 def solvers(g, implicit=1):
     mesh = {k: g[k] for k in MESH_KEYS}
-    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(g), rx.default_cfg(implicit=implicit, lin_prec=1, **cfg_kw(g)))
+    flow_imp, _, prec = scheme(g)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(g), rx.default_cfg(implicit=implicit if flow_imp else 0, lin_prec=1,
+                                                                  **cfg_kw(g)))
     s.set_bc(rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"]))
     bp = g["bc_params"]
-    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(implicit=implicit, lin_prec=1, lin_tol=float(bp[19]),
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(implicit=implicit, lin_prec=prec, lin_tol=float(bp[19]),
                                              lin_iter=int(bp[20]), relaxation_turb=float(bp[23]),
                                              cfl_red_turb=float(bp[24])))
     return s, t
@@ -163,16 +173,19 @@ def n_iters(g):
     return sum(1 for k in g if k.startswith("it") and k.endswith("_U") and k[2:-2].isdigit())
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4"])
 def test_outer_iterations_vs_reference(case):
-    """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d: 2) on the device,
-    started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within 1e-10 relative per
-    column."""
+    """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d / it7: 2, itx9 /
+    itx4: 1) on the device, started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within
+    1e-10 relative per column. it7: the bench's 7-species mechanism, implicit; itx9: the reference's shipped cfg
+    (EULER_EXPLICIT flow, CFL 0.1, LU-SGS SST) on its whole 9 000-point mesh; itx4: configs[0] (C1), 4 species,
+    3-stage Runge-Kutta, on the same mesh."""
     g = golden(case)
     s, t = solvers(g, 1)
+    rk = scheme(g)[1]
     for k in range(n_iters(g)):
         load_iteration_state(g, s, t, k)
-        rms, rms_t, _ = rx.Iterate(s, t, ext_iter=k)
+        rms, rms_t, _ = rx.Iterate(s, t, ext_iter=k, rk_alpha=rk)
         s.sync()
         check_iteration(g, s, t, k + 1, rms, rms_t, 1e-10)
     s.close()
@@ -194,7 +207,7 @@ def test_free_running_iterations_vs_reference(case):
     s.close()
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4"])
 def test_outer_iteration_vs_oracle_device_order(case):
     """One iteration against the oracle run with the device's inner-product order: the residual side and the
     Krylov recurrence then agree to the Stefan-Maxwell rounding only (amplified by FGMRES: the same 1e-10 bar)."""
@@ -202,7 +215,7 @@ def test_outer_iteration_vs_oracle_device_order(case):
     N = len(g["it_U0"])
     s, t = solvers(g, 1)
     load_iteration_state(g, s, t, 0)
-    rx.Iterate(s, t, ext_iter=0)
+    rx.Iterate(s, t, ext_iter=0, rk_alpha=scheme(g)[1])
     s.sync()
     from tests.test_oracle_bc import iteration_cfg
     cfg, bc, st = iteration_cfg(g)

@@ -1,0 +1,63 @@
+"""Size-true parity: one whole reference outer iteration (rx.Iterate: flow SetPrimitive_Variables, gradient, time
+step, loops + jet boundary conditions, FGMRES(5)+ILU0 implicit update, Preprocessing(Output), SST iteration) on the
+device at the full single-GPU sizes of BASELINE.json's configs, from the bench's own initial state (synth.jet_field_case
++ the device's start-up preprocessing), against the CPU oracle's O.outer_iteration (oracle/rx_oracle.cpp, OpenMP,
+thread-count independent) run in the device's inner-product order on the same records:
+
+  c2  configs[1]: 2-D jet 500 x 200 = 100 000 points, 7 species, 256 partitions
+  c3  configs[2]: 2-D jet 2000 x 500 = 1 000 000 points, 7 species, 256 partitions (the north-star roofline run)
+  c5  configs[4], one GPU's share: 3-D jet 1000 x 50 x 20 = 1 000 000 points, 7 species, nVar 12, 256 partitions
+
+Bar: U, (k, omega) within 1e-10 of each column's max (the FGMRES-amplified rounding of the Stefan-Maxwell solve, as in
+test_gpu_bc.test_synthetic_jet_iteration_vs_oracle), both RMS vectors within 1e-10 relative, identical linear-solver
+iteration counts. c5's state is spanwise-uniform (rho w = 0), so after one iteration its rho w column holds only
+rounding-level values: that column is compared relative to the in-plane momentum's max. Requires an MI355X."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.oracle_inputs import outer_iteration_inputs
+from tests.parity import assert_close, per_column_close
+from tests.rxpkg import rx, synth
+
+pytestmark = pytest.mark.gpu
+
+CASES = {"c2": (500, 200, 0), "c3": (2000, 500, 0), "c5": (1000, 50, 20)}
+
+
+@pytest.mark.parametrize("case", ["c2", "c3", "c5"])
+def test_full_size_iteration_vs_oracle(case):
+    nx, ny, nz = CASES[case]
+    ns, parts = 7, 256
+    mesh, st0, mech, kw = synth.jet_field_case(nx, ny, n_species=ns, n_part=parts, nz=nz)
+    cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
+    bc = synth.jet_bc(mesh, ns)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
+    s.set_bc(bc)
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+    st = synth.device_preprocess(s, t, mesh, st0)
+    N = len(st["V"])
+    mesh_o, state, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
+    # the reference's iteration-start state: grad k = the LS gradient of the turbulent solution, sigma_k =
+    # CTurbSSTVariable::Get_Sigmak (constants[0])
+    s.upload("GRADK", np.ascontiguousarray(state["TG"][:, 0, :]))
+    s.upload("SIGMAK", np.full(N, 0.85))
+    rms, rms_t, its = rx.Iterate(s, t, ext_iter=0)
+    s.sync()
+    U, T = s.download("U").reshape(N, -1), t.download("U").reshape(N, 2)
+    s.close()
+    pat = O.bsr_pattern(N, mesh["edges"])
+    with O.dot_order("device"):
+        o = O.outer_iteration(O.Mechanism(mech), 3 if nz else 2, mesh_o, state, bco, c, 0, pat,
+                              part_ptr=mesh["part_ptr"], keep=False)
+    assert its == (o["lin_iters"], o["sst_lin_iters"])
+    if nz:
+        cols = [v for v in range(U.shape[1]) if v != 3]
+        per_column_close(U[:, cols], o["U"][:, cols], rtol=1e-10, floor=1.0, what=f"{case} U vs oracle")
+        assert_close(U[:, 3], o["U"][:, 3], rtol=1e-10, floor=1.0, scale=np.abs(o["U"][:, 1:3]).max(),
+                     what=f"{case} rho w vs oracle (in-plane momentum scale)")
+    else:
+        per_column_close(U, o["U"], rtol=1e-10, floor=1.0, what=f"{case} U vs oracle")
+    per_column_close(T, o["T"], rtol=1e-10, floor=1.0, what=f"{case} (k, omega) vs oracle")
+    assert_close(rms, o["rms"], rtol=1e-10, what=f"{case} RMS flow")
+    assert_close(rms_t, o["sst_rms"], rtol=1e-10, what=f"{case} RMS SST")

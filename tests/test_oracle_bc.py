@@ -39,7 +39,7 @@ def bc9(request):
     return bc_case(request.param)
 
 
-@pytest.fixture(scope="module", params=["it9", "it3d"])
+@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4"])
 def it9(request):
     return golden(request.param)
 
@@ -99,6 +99,12 @@ def iteration_cfg(g):
                prandtl_lam=g["dt_params"][2], prandtl_turb=g["dt_params"][3], lewis_turb=g["visc_params"][2],
                mach_inf=g["mach_inf"][0], c_mu=g["src_params"][0], pasr_lb=g["src_params"][1], lin_tol=bp[19],
                lin_iter=int(bp[20]), relaxation=bp[22], relaxation_turb=bp[23], cfl_red_turb=bp[24])
+    # TIME_DISCRE_FLOW / RK_ALPHA_COEFF / LINEAR_SOLVER_PREC of the golden's cfg (it9 / it3d: implicit, ILU0)
+    tf = str(g["time_flow"]) if "time_flow" in g else "EULER_IMPLICIT"
+    cfg["time"] = {"EULER_IMPLICIT": "implicit", "EULER_EXPLICIT": "euler_explicit", "RUNGE-KUTTA_EXPLICIT": "rk"}[tf]
+    if "rk_alpha" in g:
+        cfg["rk_alpha"] = [float(x) for x in g["rk_alpha"]]
+    cfg["sst_prec"] = "lusgs" if ("lin_prec" in g and str(g["lin_prec"]) == "LU_SGS") else "ilu"
     bc = dict(marker=g["bc_marker"], prm=O.bc_prm(bp, g["mach_inf"][0], g["visc_params"][1], g["visc_params"][2]))
     state = dict(U=g["it_U0"], V=g["it_V0"], Uold=g["it_Uold0"], T=g["it_sst0"], TG=g["it_sstgrad0"],
                  F1=g["it_F1_0"], F2=g["it_F2_0"], CDkw=g["it_CDkw0"], mut=g["it_mut0"])
