@@ -23,10 +23,13 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
-                os.path.join(HERE, "rx_oracle.cpp")):
-            build()
-        _lib = C.CDLL(LIB_PATH)
+        path = os.environ.get("RX_ORACLE_LIB")  # e.g. the sanitizer build of oracle/sanitize.sh
+        if not path:
+            path = LIB_PATH
+            if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
+                    os.path.join(HERE, "rx_oracle.cpp")):
+                build()
+        _lib = C.CDLL(path)
         _lib.orc_mech_create.restype = C.c_void_p
         _lib.orc_spline.restype = C.c_double
         _lib.orc_spline.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double]
