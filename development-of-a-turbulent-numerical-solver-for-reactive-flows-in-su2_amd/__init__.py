@@ -154,6 +154,31 @@ def lib():
         _lib.rx_bc_set.argtypes = [C.c_void_p, C.POINTER(BcDesc)]
         _lib.rx_bc_flow.argtypes = [C.c_void_p]
         _lib.rx_bc_sst.argtypes = [C.c_void_p]
+        # rx_io.h (host-side setup and file formats)
+        _lib.rx_mesh_read_su2.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
+        _lib.rx_mesh_destroy.argtypes = [C.c_void_p]
+        _lib.rx_mesh_destroy.restype = None
+        _lib.rx_mesh_info.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+        _lib.rx_mesh_marker_tag.argtypes = [C.c_void_p, C.c_int32]
+        _lib.rx_mesh_marker_tag.restype = C.c_char_p
+        _lib.rx_mesh_describe.argtypes = [C.c_void_p, C.POINTER(MeshDesc)]
+        for name in ("rx_mesh_global_index", "rx_mesh_normal_neighbor"):
+            getattr(_lib, name).argtypes = [C.c_void_p]
+            getattr(_lib, name).restype = C.POINTER(C.c_int64)
+        _lib.rx_mesh_wall_distance.argtypes = [C.c_void_p, C.c_void_p]
+        _lib.rx_mesh_wall_distance.restype = C.POINTER(C.c_double)
+        _lib.rx_mech_read.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]
+        _lib.rx_mech_destroy.argtypes = [C.c_void_p]
+        _lib.rx_mech_destroy.restype = None
+        _lib.rx_mech_describe.argtypes = [C.c_void_p, C.POINTER(MechDesc)]
+        _lib.rx_mech_species.argtypes = [C.c_void_p, C.c_int32]
+        _lib.rx_mech_species.restype = C.c_char_p
+        _lib.rx_mech_formation_enthalpy.argtypes = [C.c_void_p, C.c_int32]
+        _lib.rx_mech_formation_enthalpy.restype = C.c_double
+        _lib.rx_restart_write.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_int64]
+        _lib.rx_restart_read.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     return _lib
 
 
@@ -209,10 +234,14 @@ class TorchHostTransport:
 
 
 def header_symbols():
-    """Function names declared in include/rx.h (the ABI contract)."""
+    """Function names declared in include/rx.h and include/rx_io.h (the ABI contract)."""
     import re
-    txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(rx_[a-z0-9_]+)\s*\(", txt, re.M)))
+    out = set()
+    for h in (HEADER, os.path.join(os.path.dirname(HEADER), "rx_io.h")):
+        txt = open(h).read()
+        out |= set(re.findall(r"^\s*(?:int|int64_t|void|double|const char \*|const int64_t \*|const double \*)\s*"
+                              r"(rx_[a-z0-9_]+)\s*\(", txt, re.M))
+    return sorted(out)
 
 
 def _chk(rc, what, ctx=None):
@@ -532,6 +561,98 @@ class TurbSSTSolver:
     def BC(self):
         """The SST boundary-condition loops (after the flow's BC of the same iteration)."""
         self._call("rx_bc_sst")
+
+
+class SU2Mesh:
+    """A mesh read by the reference's SU2 reader and dual-grid preprocessing, restated natively (rx_io.h
+    rx_mesh_read_su2: connectivity, RCM ordering, edges, median dual, boundary vertices, normal neighbours).
+    mesh() gives the dict ReactiveNSSolver / TurbSSTSolver take; is_wall marks the HEAT_FLUX / ISOTHERMAL markers
+    for the wall distance."""
+
+    def __init__(self, path, walls=()):
+        h = C.c_void_p()
+        _chk(lib().rx_mesh_read_su2(os.fsencode(path), C.byref(h)), f"rx_mesh_read_su2({path})")
+        self.h = h
+        nd, n, e, nb, nm = C.c_int32(), C.c_int64(), C.c_int64(), C.c_int64(), C.c_int32()
+        lib().rx_mesh_info(h, C.byref(nd), C.byref(n), C.byref(e), C.byref(nb), C.byref(nm))
+        self.n_dim, self.N, self.E, self.NB = nd.value, n.value, e.value, nb.value
+        self.tags = [lib().rx_mesh_marker_tag(h, k).decode() for k in range(nm.value)]
+        md = MeshDesc()
+        _chk(lib().rx_mesh_describe(h, C.byref(md)), "rx_mesh_describe")
+        self.desc = md
+        arr = lambda p, shape, t=np.float64: np.ctypeslib.as_array(C.cast(p, C.POINTER(
+            C.c_double if t == np.float64 else C.c_int64)), shape=shape).copy()
+        nnb = int(arr(md.nbr_ptr, (self.N + 1,), np.int64)[-1])
+        self._mesh = dict(edges=arr(md.edges, (self.E, 2), np.int64), edge_normal=arr(md.edge_normal, (self.E, nd.value)),
+                          coord=arr(md.coord, (self.N, nd.value)), volume=arr(md.volume, (self.N,)),
+                          nbr_ptr=arr(md.nbr_ptr, (self.N + 1,), np.int64), nbr=arr(md.nbr, (nnb,), np.int64),
+                          bvertex=arr(md.bvert, (self.NB, 2), np.int64),
+                          bvertex_normal=arr(md.bvert_normal, (self.NB, nd.value)), n_dim=nd.value)
+        self.global_index = np.ctypeslib.as_array(lib().rx_mesh_global_index(h), shape=(self.N,)).copy()
+        self._mesh["bvertex_pn"] = np.ctypeslib.as_array(lib().rx_mesh_normal_neighbor(h), shape=(self.NB,)).copy()
+        self.wall_distance(walls)
+
+    def wall_distance(self, walls):
+        flags = np.array([1 if t in walls else 0 for t in self.tags], dtype=np.int32)
+        p = lib().rx_mesh_wall_distance(self.h, flags.ctypes.data)
+        self._mesh["wall_distance"] = np.ctypeslib.as_array(p, shape=(self.N,)).copy()
+        return self._mesh["wall_distance"]
+
+    def mesh(self):
+        return dict(self._mesh)
+
+    def write_restart(self, path, U, T, extra=None, ext_iter=0):
+        """COutput::SetRestart format (%.15e, global-index order) from U [N][nVar], T [N][2], extra [N][5] (P, T,
+        Mach, mu, mu_t) or None."""
+        U = np.ascontiguousarray(U, dtype=np.float64)
+        T = np.ascontiguousarray(T, dtype=np.float64)
+        ex = None if extra is None else np.ascontiguousarray(extra, dtype=np.float64)
+        _chk(lib().rx_restart_write(os.fsencode(path), self.h, U.shape[1], U.ctypes.data, T.ctypes.data,
+                                    None if ex is None else ex.ctypes.data, int(ext_iter)), "rx_restart_write")
+
+    def read_restart(self, path, n_var):
+        U = np.zeros((self.N, n_var))
+        T = np.zeros((self.N, 2))
+        _chk(lib().rx_restart_read(os.fsencode(path), self.h, n_var, U.ctypes.data, T.ctypes.data), "rx_restart_read")
+        return U, T
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rx_mesh_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def read_mechanism(base_dir, list_file):
+    """ReactingModelLibrary::Setup restated (rx_io.h rx_mech_read): the mechanism arrays (mech_* keys, as the golden
+    files and Mechanism take them) of the library files listed in base_dir/list_file."""
+    h = C.c_void_p()
+    _chk(lib().rx_mech_read(os.fsencode(base_dir), os.fsencode(list_file), C.byref(h)), f"rx_mech_read({list_file})")
+    try:
+        d = MechDesc()
+        _chk(lib().rx_mech_describe(h, C.byref(d)), "rx_mech_describe")
+        ns, nr, nt = d.n_species, d.n_reactions, d.n_tab
+        f8 = lambda p, shape: (np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_double)), shape=shape).copy()
+                               if int(np.prod(shape)) else np.zeros(shape))
+        i4 = lambda p, n: (np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), shape=(n,)).astype(np.int64)
+                           if n else np.zeros(0, dtype=np.int64))
+        out = dict(n_species=np.array(ns), n_reactions=np.array(nr), mmass=f8(d.mmass, (ns,)),
+                   diff_vol=f8(d.diff_vol, (ns,)), stoich_reac=f8(d.stoich_reac, (ns, nr)),
+                   stoich_prod=f8(d.stoich_prod, (ns, nr)), exp_reac=f8(d.exp_reac, (nr, ns)),
+                   exp_prod=f8(d.exp_prod, (nr, ns)), A=f8(d.A, (nr,)), beta=f8(d.beta, (nr,)), Ta=f8(d.Ta, (nr,)),
+                   A_back=f8(d.A_back, (nr,)), beta_back=f8(d.beta_back, (nr,)), Ta_back=f8(d.Ta_back, (nr,)),
+                   reversible=i4(d.reversible, nr), has_backward=i4(d.has_backward, nr),
+                   tab_x=f8(d.tab_x, (5, ns, nt)), tab_y=f8(d.tab_y, (5, ns, nt)), tab_y2=f8(d.tab_y2, (5, ns, nt)),
+                   form_enthalpy=np.array([lib().rx_mech_formation_enthalpy(h, s) for s in range(ns)]),
+                   species=np.array([lib().rx_mech_species(h, s).decode() for s in range(ns)]))
+        return {"mech_" + k: v for k, v in out.items()}
+    finally:
+        lib().rx_mech_destroy(h)
 
 
 def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=None, rk_alpha=None):

@@ -152,7 +152,7 @@ def field_subset(g, n_species):
     return out
 
 
-def field_at(xy, n_species=7, field="jet9k"):
+def field_at(xy, n_species=7, field="jet9k", y_floor=1e-6):
     """The reference's converged PaSR jet (tests/golden/jet9k.npz: its own 9 000-point mesh after its start-up
     preprocessing) linearly interpolated at the physical points xy [n][2] of the jet domain: (g, U, k, omega,
     mu_t, T) with g the (species-restricted) field dict. Species are floored at a mass fraction of 1e-10 (see
@@ -174,17 +174,20 @@ def field_at(xy, n_species=7, field="jet9k"):
     # trace species. The viscous Jacobian's Ds = (1 - X_s) / sum_b X_b / D_sb (numerics_direct_reactive.cpp:1578-1588)
     # is 0/0 -> 0 (the reference's NaN guard) at a pure-species point, but once an update leaves 1e-30-level
     # partial densities there (negative ones are clamped to 1e-30, reacting_model_library.cpp:65-79) it is
-    # rounding / 1e-30 ~ 1e280, and the ILU(0) factor overflows (the Ds discontinuity). The
-    # reference's oxidiser stream is pure O2, so every species is floored at a mass fraction of 1e-10 and the
-    # partial densities rescaled to the interpolated density (the mixture and its energy change by ~1e-10).
+    # rounding / 1e-30 ~ 1e280 and the ILU(0) factor overflows (the Ds discontinuity). The
+    # reference's oxidiser stream is pure O2, so every species is floored at a mass fraction y_floor and the
+    # partial densities rescaled to the interpolated density. 1e-6 rather than just above the 1e-30 clamp: with
+    # 1e-10 trace species the Ds cancellation (1 - X_s carries 1e-16 / 1e-10 relative rounding) and the PaSR
+    # rates' C^(nu-1) derivatives make the FGMRES(5) update amplify last-bit residual differences ~1e6-fold
+    # (tools/size_diag.py: device vs oracle U 3e-7 column-relative at C3 with 1e-10, 1e-12 with 1e-6).
     rho = U[:, 0]
     rs = U[:, 4:]
-    np.maximum(rs, 1e-10 * rho[:, None], out=rs)
+    np.maximum(rs, y_floor * rho[:, None], out=rs)
     rs *= (rho / rs.sum(axis=1))[:, None]
     return g, U, out[:, nU], out[:, nU + 1], out[:, nU + 2], out[:, nU + 3]
 
 
-def jet_field_case(nx, ny, n_species=7, n_part=1, nz=0, field="jet9k"):
+def jet_field_case(nx, ny, n_species=7, n_part=1, nz=0, field="jet9k", y_floor=1e-6):
     """Mesh (RCM-ordered median dual, partitioned) + a smooth, physically consistent initial state for an nx x ny
     (x nz) jet: the reference's converged PaSR field on its own 9 000-point mesh (tests/golden/jet9k.npz, after the
     reference's preprocessing) linearly interpolated onto the synthetic mesh, which covers the same physical domain
@@ -195,7 +198,7 @@ def jet_field_case(nx, ny, n_species=7, n_part=1, nz=0, field="jet9k"):
     (device_preprocess). 3-D: spanwise-uniform (rho w = 0)."""
     mg = _meshgen()
     mesh = mg.build_jet(nx, ny, n_part=n_part, nz=nz)
-    g, U, k, om, mut, T = field_at(mesh["coord"], n_species, field)
+    g, U, k, om, mut, T = field_at(mesh["coord"], n_species, field, y_floor)
     nDim = 3 if nz > 1 else 2
     if nDim == 3:
         U = np.concatenate([U[:, :3], np.zeros((len(U), 1)), U[:, 3:]], axis=1)

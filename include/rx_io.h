@@ -1,0 +1,74 @@
+/* rx_io.h — host-side setup and on-disk formats of the reactive-RANS path, C ABI.
+ *
+ * What the reference's driver does before the first iteration, restated natively (C++ in librx.so, no GPU):
+ *   rx_mesh_read_su2   CPhysicalGeometry's SU2 ASCII reader (Common/src/geometry_structure.cpp:4819), then
+ *                      CGeometry preprocessing in CDriver::Geometrical_Preprocessing's order
+ *                      (SU2_CFD/src/driver_structure.cpp:552-585): SetPoint_Connectivity (:9145-9198),
+ *                      SetRCM_Ordering (:9200-9340), SetPoint_Connectivity again, SetEdges (:223-252),
+ *                      SetVertex, SetCoord_CG (:9518-9590), SetControlVolume (:10457-10560, median dual, edge
+ *                      normals and dual volumes in the reference's element / face accumulation order),
+ *                      SetBoundControlVolume (:9595-9660), FindNormal_Neighbor (:12610-12652); and
+ *                      ComputeWall_Distance (nearest vertex of the HEAT_FLUX / ISOTHERMAL markers).
+ *                      Serial reader (one rank); elements: triangle, quadrilateral (2-D), tetrahedron,
+ *                      hexahedron (3-D); boundary: line (2-D), triangle, quadrilateral (3-D). Elements must be
+ *                      consistently oriented (the reference's Check_*_Orientation flips are not restated).
+ *   rx_mech_read       ReactingModelLibrary::Setup (Common/src/Framework/reacting_model_library.cpp:925-1506):
+ *                      file list, mixture, chemistry (Parse_Terms Common/src/Tools/utility.cpp:12-86, CGS->SI
+ *                      :1122-1132, Ta/R_cal :1209-1210, reversible product exponents :1113-1120, backward-rate
+ *                      line :1218-1260), thermo / transport tables with spline second derivatives
+ *                      (Common/src/Tools/spline.cpp:10-58, clamped zero-slope ends).
+ *   rx_restart_write   COutput::SetRestart (SU2_CFD/src/output_structure.cpp:3858-4060) for REACTIVE_RANS:
+ *                      header, one line per point in global-index order (index, coordinates, flow
+ *                      conservatives, k, omega[, Pressure, Temperature, Mach, Laminar_Viscosity, mu_t]) at
+ *                      precision(15) scientific, tab-separated, then the AOA / SIDESLIP / BCTHRUST / DCD_DCL /
+ *                      EXT_ITER trailer.
+ *   rx_restart_read    CReactiveEulerSolver::Load_Restart (solver_direct_reactive.cpp:566-686) + the SST
+ *                      solver's restart columns (solver_direct_turbulent.cpp:2838-2850).
+ * Errors: RX_ERR_ARG (bad argument / unsupported element), RX_ERR_STATE (unreadable or malformed file; the
+ * reference exits). Points of an rx_mesh are in the reference's RCM order; global_index maps them to the file.
+ */
+#ifndef RX_IO_H
+#define RX_IO_H
+
+#include <stdint.h>
+
+#include "rx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rx_mesh rx_mesh;
+int rx_mesh_read_su2(const char *path, rx_mesh **out);
+void rx_mesh_destroy(rx_mesh *mesh);
+/* sizes: n_dim, points, edges, boundary vertices, markers */
+int rx_mesh_info(const rx_mesh *mesh, int32_t *n_dim, int64_t *n_point, int64_t *n_edge, int64_t *n_bvert,
+                 int32_t *n_marker);
+/* MARKER_TAG of marker m (file order) or NULL */
+const char *rx_mesh_marker_tag(const rx_mesh *mesh, int32_t m);
+/* rx_mesh_desc over the mesh's arrays (one partition, single rank); valid until rx_mesh_destroy */
+int rx_mesh_describe(const rx_mesh *mesh, rx_mesh_desc *out);
+/* global (file) index of every point [N]; normal neighbour of every boundary vertex [n_bvert] */
+const int64_t *rx_mesh_global_index(const rx_mesh *mesh);
+const int64_t *rx_mesh_normal_neighbor(const rx_mesh *mesh);
+/* ComputeWall_Distance: is_wall[n_marker] != 0 for the HEAT_FLUX / ISOTHERMAL markers of the cfg; distance of every
+ * point to the nearest vertex of those markers (0 everywhere when there is none). Returns a pointer to [N]. */
+const double *rx_mesh_wall_distance(rx_mesh *mesh, const int32_t *is_wall);
+
+typedef struct rx_mech rx_mech;
+int rx_mech_read(const char *base_dir, const char *list_file, rx_mech **out);
+void rx_mech_destroy(rx_mech *mech);
+int rx_mech_describe(const rx_mech *mech, rx_mech_desc *out); /* valid until rx_mech_destroy */
+const char *rx_mech_species(const rx_mech *mech, int32_t s);  /* SPECIES name of species s */
+double rx_mech_formation_enthalpy(const rx_mech *mech, int32_t s);
+
+/* U [N][n_var] flow conservatives and T [N][2] (k, omega) in the mesh's point order; extra [N][5] (Pressure,
+ * Temperature, Mach, Laminar_Viscosity, Eddy_Viscosity) or NULL (the reference's low-memory output). */
+int rx_restart_write(const char *path, const rx_mesh *mesh, int32_t n_var, const double *U, const double *T,
+                     const double *extra, int64_t ext_iter);
+int rx_restart_read(const char *path, const rx_mesh *mesh, int32_t n_var, double *U, double *T);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RX_IO_H */

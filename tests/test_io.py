@@ -1,0 +1,138 @@
+"""next-4: the native SU2 mesh reader + the reference's dual-grid preprocessing, the reacting-library
+readers and the restart format (librx.so, include/rx_io.h; host code, no GPU), against the reference's own
+geometry and tables in the golden files (oracle/ref_harness dumps: global_index, edges, normals, volumes,
+neighbour lists, boundary vertices, normal neighbours, wall distances; oracle/mech.py tables pinned by the
+reference's spline values).
+
+Meshes: mini9 / mini3d were meshed by the reference from meshgen's SU2 files, which these tests rewrite with the same
+writer; with /root/reference present (this container) also the reference's own mesh_stretched.su2 (the whole
+9 000-point jet, golden itx9) and its library files."""
+import os
+
+import numpy as np
+import pytest
+
+from tests.rxpkg import meshgen, rx
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+REF_CASE = "/root/reference/Test_Cases/TURBOLENT/TURBOLENT_COMBUSTION"
+WALLS = ("upper_wall", "lower_wall_pre", "lower_wall_post")
+
+
+def golden(name):
+    return dict(np.load(os.path.join(GOLD, name + ".npz")))
+
+
+def check_geometry(m, g, volume_bitwise=True):
+    d = m.mesh()
+    assert np.array_equal(m.global_index, g["global_index"]), "RCM point order"
+    assert np.array_equal(d["coord"], g["coord"])
+    assert np.array_equal(d["edges"], g["edges"]), "edge order"
+    assert np.array_equal(d["edge_normal"], g["edge_normal"]), "edge normals"
+    if volume_bitwise:
+        assert np.array_equal(d["volume"], g["volume"]), "dual volumes"
+    else:
+        assert np.max(np.abs(d["volume"] - g["volume"])) <= 1e-15 * np.abs(g["volume"]).max()
+    assert np.array_equal(d["nbr_ptr"], g["nbr_ptr"]) and np.array_equal(d["nbr"], g["nbr"]), "neighbour lists"
+    assert np.array_equal(d["bvertex"], g["bvertex"][:, :2]), "boundary vertices"
+    assert np.array_equal(d["bvertex_normal"], g["bvertex_normal"]), "boundary normals"
+    assert np.array_equal(d["wall_distance"], g["wall_distance"]), "wall distance"
+    if "bvertex_pn" in g:
+        assert np.array_equal(d["bvertex_pn"], g["bvertex_pn"]), "normal neighbours"
+
+
+@pytest.mark.parametrize("case", ["mini9", "mini3d"])
+def test_su2_reader_reproduces_reference_geometry(case, tmp_path):
+    pts, el, bnd = meshgen.jet_mesh(21, 11) if case == "mini9" else meshgen.jet_mesh3d(13, 7, 4)
+    path = str(tmp_path / "mesh.su2")
+    meshgen.write_su2(path, pts, el, bnd)
+    m = rx.SU2Mesh(path, walls=WALLS)
+    assert m.tags[:len(meshgen.MARKERS)] == list(meshgen.MARKERS)
+    g = golden(case)
+    g["bvertex_pn"] = golden("bc9" if case == "mini9" else "bc3d")["bvertex_pn"]
+    check_geometry(m, g)
+    m.close()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CASE), reason="reference test case files absent")
+def test_su2_reader_on_the_reference_jet_mesh():
+    """The reference's own mesh_stretched.su2 (9 000 points): every geometric array of the reference's
+    preprocessing, bitwise (golden itx9, the reference run on this mesh)."""
+    m = rx.SU2Mesh(os.path.join(REF_CASE, "mesh_stretched.su2"), walls=WALLS)
+    check_geometry(m, golden("itx9"))
+    m.close()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CASE), reason="reference test case files absent")
+def test_library_reader_on_the_reference_files():
+    """ReactingModelLibrary::Setup restated natively equals the tables and rate constants the oracle and the device
+    were pinned with (9 species, two reactions, CGS units, a reversible reaction with an explicit backward rate)."""
+    got = rx.read_mechanism(REF_CASE, "test_chem_second.txt")
+    g = golden("mini9")
+    for k, v in got.items():
+        if k in g:
+            want = g[k]
+            if want.dtype.kind in "iu":
+                assert np.array_equal(v.astype(np.int64), want.astype(np.int64)), k
+            elif want.dtype.kind in "fc":
+                assert np.array_equal(v, want), k
+            else:
+                assert [str(x) for x in v] == [str(x) for x in want], k
+
+
+def test_library_reader_tables_roundtrip(tmp_path):
+    """Library files in the reference's formats (mixture, per-species transport / thermo tables, no chemistry file:
+    the flat plate's layout) written from a golden mechanism and read back: the spline second derivatives
+    (spline.cpp:10-58, clamped ends) equal the golden's bitwise."""
+    g = golden("fp3")
+    r = lambda x: repr(float(x))  # shortest round-trip decimal
+    ns = int(g["mech_n_species"])
+    names = [str(x) for x in g["mech_species"]]
+    with open(tmp_path / "mix.txt", "w") as f:
+        f.write(f"//Number of species\n{ns}\n//Species Molar masses Formation enthalpies Diffusion volume\n")
+        for s in range(ns):
+            f.write(f"{names[s]} {r(g['mech_mmass'][s])} {r(g['mech_form_enthalpy'][s])} {r(g['mech_diff_vol'][s])}\n")
+        f.write("\nSTOP\n")
+    tx, ty = g["mech_tab_x"], g["mech_tab_y"]
+    lst = ["mix.txt"]
+    for s in range(ns):
+        with open(tmp_path / f"{names[s]}_transp.txt", "w") as f:
+            f.write(f"{names[s]}\n" + "".join(f"{r(tx[3, s, k])} {r(ty[3, s, k])} {r(ty[4, s, k])}\n"
+                                              for k in range(tx.shape[2])))
+        with open(tmp_path / f"{names[s]}_thermo.txt", "w") as f:
+            f.write(f"{names[s]}\n" + "".join(f"{r(tx[0, s, k])} {r(ty[0, s, k])} {r(ty[1, s, k])} {r(ty[2, s, k])}\n"
+                                              for k in range(tx.shape[2])))
+        lst += [f"{names[s]}_transp.txt", f"{names[s]}_thermo.txt"]
+    with open(tmp_path / "list.txt", "w") as f:
+        f.write("\n".join(lst) + "\n")
+    got = rx.read_mechanism(str(tmp_path), "list.txt")
+    assert int(got["mech_n_reactions"]) == 0
+    for k in ("mech_mmass", "mech_diff_vol", "mech_tab_x", "mech_tab_y", "mech_tab_y2"):
+        assert np.array_equal(got[k], g[k]), k
+
+
+def test_restart_roundtrip(tmp_path):
+    """COutput::SetRestart's layout: header, points in global-index order with their file coordinates, %.15e
+    values, trailer; Load_Restart reads back the flow and SST columns (at the format's 16 significant digits)."""
+    pts, el, bnd = meshgen.jet_mesh(21, 11)
+    path = str(tmp_path / "mesh.su2")
+    meshgen.write_su2(path, pts, el, bnd)
+    m = rx.SU2Mesh(path, walls=WALLS)
+    rng = np.random.default_rng(3)
+    nv = 13
+    U = rng.normal(size=(m.N, nv)) * 10.0 ** rng.integers(-8, 6, size=(m.N, nv))
+    T = rng.random((m.N, 2))
+    rst = str(tmp_path / "restart_flow.dat")
+    m.write_restart(rst, U, T, extra=rng.random((m.N, 5)), ext_iter=41)
+    lines = open(rst).read().splitlines()
+    assert lines[0].startswith('"PointID"\t"x"\t"y"\t"Conservative_1"')
+    assert lines[0].count("Conservative_") == nv + 2 and lines[0].endswith('"<greek>m</greek><sub>t</sub>"')
+    assert lines[-1] == "EXT_ITER= 42" and lines[-5].startswith("AOA=")
+    row = lines[1 + 17].split("\t")
+    i = int(np.nonzero(m.global_index == 17)[0][0])
+    assert int(row[0]) == 17 and float(row[1]) == float(f"{pts[17, 0]:.15e}") and row[1] == f"{pts[17, 0]:.15e}"
+    U2, T2 = m.read_restart(rst, nv)
+    q = np.vectorize(lambda x: float(f"{x:.15e}"))
+    assert np.array_equal(U2, q(U)) and np.array_equal(T2, q(T))
+    assert np.array_equal(U2[i], q(U[i]))
+    m.close()

@@ -19,7 +19,8 @@ from tests.rxpkg import rx, synth  # noqa: E402
 case = sys.argv[1] if len(sys.argv) > 1 else "c3"
 nx, ny, nz = {"c2": (500, 200, 0), "c3": (2000, 500, 0), "c5": (1000, 50, 20)}[case]
 ns = 7
-mesh, st0, mech, kw = synth.jet_field_case(nx, ny, n_species=ns, n_part=256, nz=nz)
+y_floor = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-10
+mesh, st0, mech, kw = synth.jet_field_case(nx, ny, n_species=ns, n_part=256, nz=nz, y_floor=y_floor)
 cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
 bc = synth.jet_bc(mesh, ns)
 s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
@@ -31,10 +32,19 @@ nDim = 3 if nz else 2
 mesh_o, state, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
 s.upload("GRADK", np.ascontiguousarray(state["TG"][:, 0, :]))
 s.upload("SIGMAK", np.full(N, 0.85))
-rms, rms_t, its = rx.Iterate(s, t, ext_iter=0)
-s.sync()
 nv = s.nVar
-dev = {k: s.download(k) for k in ("U", "JAC", "RHS", "SOL", "DT")}
+runs = []
+for rep in range(2):  # determinism: the same iteration twice from the same records
+    synth.device_preprocess(s, t, mesh, st0)
+    s.upload("GRADK", np.ascontiguousarray(state["TG"][:, 0, :]))
+    s.upload("SIGMAK", np.full(N, 0.85))
+    rms, rms_t, its = rx.Iterate(s, t, ext_iter=0)
+    s.sync()
+    runs.append({k: s.download(k) for k in ("U", "JAC", "RHS", "SOL", "DT")})
+dev = runs[0]
+for k in dev:
+    print(f"repeat {k}: bitwise {np.array_equal(runs[0][k], runs[1][k])} max abs diff "
+          f"{np.nanmax(np.abs(runs[0][k] - runs[1][k])):.3e}")
 pat = O.bsr_pattern(N, mesh["edges"])
 with O.dot_order("device"):
     o = O.outer_iteration(O.Mechanism(mech), nDim, mesh_o, state, bco, c, 0, pat, part_ptr=mesh["part_ptr"], keep=True)
@@ -48,14 +58,21 @@ def worst(name, a, b, per_row, k=5):
     rel = np.abs(a - b) / scale
     r = rel.max(axis=1)
     idx = np.argsort(r)[-k:][::-1]
-    print(f"{name}: max col-rel {r.max():.3e}; worst rows {idx.tolist()} {np.array2string(r[idx], precision=2)}")
+    print(f"{name}: max col-rel {r.max():.3e}; per column {np.array2string(rel.max(axis=0), precision=1)}; worst rows "
+          f"{idx.tolist()} {np.array2string(r[idx], precision=2)}")
     return idx
 
 
 print(f"{case}: lin iters device {its} oracle {(o['lin_iters'], o['sst_lin_iters'])}; rms rel "
       f"{np.max(np.abs(rms - o['rms']) / np.abs(o['rms'])):.3e}")
 worst("dt", dev["DT"], o["dt"], np.zeros((N, 1)))
-worst("rhs", dev["RHS"], o["rhs"], np.zeros((N, nv)))
+ir = worst("rhs", dev["RHS"], o["rhs"], np.zeros((N, nv)))
+Rd, Ro = dev["RHS"].reshape(N, nv), o["rhs"].reshape(N, nv)
+for r in ir[:3]:
+    v = int(np.argmax(np.abs(Rd[r] - Ro[r]) / np.maximum(np.abs(Ro).max(axis=0), 1e-300)))
+    print(f"  rhs row {r} var {v}: device {Rd[r, v]:.17e} oracle {Ro[r, v]:.17e} (col max {np.abs(Ro[:, v]).max():.3e}) "
+          f"coord {mesh['coord'][r]} boundary {r in set(np.asarray(mesh['bvertex'])[:, 1].tolist())}")
+    print(f"    V {np.array2string(st['V'][r], precision=5)}")
 J = dev["JAC"].reshape(-1, nv * nv)
 Jo = o["sys"].reshape(-1, nv * nv)
 blk_scale = np.maximum(np.abs(Jo).max(axis=1), 1e-300)
