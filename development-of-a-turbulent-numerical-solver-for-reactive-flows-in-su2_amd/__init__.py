@@ -655,6 +655,146 @@ def read_mechanism(base_dir, list_file):
         lib().rx_mech_destroy(h)
 
 
+R_UNGAS = 6.02214129e23 * 1.3806488e-23 * 1.0e3  # J/(kmol K) (physical_chemical_library.hpp:571-579)
+
+
+def read_cfg(path):
+    """The reference's cfg grammar for the keys this path uses (CConfig::SetConfig_Parsing: `KEY= value` lines,
+    `%` comments; values kept as strings). Returns {KEY: value}."""
+    out = {}
+    with open(path) as f:
+        for raw in f:
+            line = raw.split("%", 1)[0].strip()
+            if "=" not in line:
+                continue
+            k, v = line.split("=", 1)
+            out[k.strip().upper()] = v.strip()
+    return out
+
+
+def _cfg_list(v):
+    return [t.strip() for t in v.strip().strip("()").replace(";", ",").split(",") if t.strip()]
+
+
+def _spline(mech, prop, s, T):
+    """MathTools::GetSpline (spline.cpp:62-77) on the library tables (host; free-stream values only)."""
+    x, y, y2 = (mech["mech_tab_" + k][prop, s] for k in ("x", "y", "y2"))
+    h = x[1] - x[0]
+    klo = int((T - x[0]) / h + 1)
+    a = (x[klo] - T) / h
+    b = (T - x[klo - 1]) / h
+    return a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0
+
+
+def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
+    """The inputs of a reference REACTIVE_RANS case from its cfg (the keys of the shipped jet cfgs): the mesh
+    (SU2Mesh: MESH_FILENAME), the library (read_mechanism: CONFIG_LIB_FILE), the flow and SST rx_cfg keyword sets,
+    the boundary markers in the mesh's marker order (MARKER_INLET / INLET_TYPE / INLET_MASS_FRAC, MARKER_OUTLET,
+    MARKER_ISOTHERMAL, MARKER_SYM), the free-stream turbulence values of CReactiveEulerSolver::
+    SetNondimensionalization (solver_direct_reactive.cpp:4534-4590: k = 3/2 (|V| I)^2, omega = rho k / (mu
+    TURB2LAMVISC), rho = ComputeDensity, mu = ComputeEta) and TIME_DISCRE_FLOW / RK_ALPHA_COEFF. DIMENSIONAL cases
+    (reference values 1). Returns a dict: mesh (SU2Mesh), mech (mech_* arrays), flow_cfg / sst_cfg (keyword dicts
+    for default_cfg / sst_cfg), bc (rx_bc_desc inputs), rk_alpha (None unless RUNGE-KUTTA_EXPLICIT)."""
+    c = read_cfg(cfg_path)
+    base = os.path.dirname(os.path.abspath(cfg_path))
+    if c.get("REF_DIMENSIONALIZATION", "DIMENSIONAL") != "DIMENSIONAL":
+        raise RxError("case_from_cfg: only REF_DIMENSIONALIZATION= DIMENSIONAL")
+    walls = _cfg_list(c.get("MARKER_ISOTHERMAL", ""))[0::2]
+    mesh = SU2Mesh(mesh_path or os.path.join(base, c["MESH_FILENAME"]), walls=walls)
+    mech = read_mechanism(lib_dir or base, c["CONFIG_LIB_FILE"])
+    names = [str(x) for x in mech["mech_species"]]
+    order = _cfg_list(c.get("SPECIES_ORDER", ""))
+    if order and order != names:
+        raise RxError(f"SPECIES_ORDER {order} does not match the library's {names}")
+    ns = len(names)
+    f = lambda k, d: float(c.get(k, d))
+    tf = c.get("TIME_DISCRE_FLOW", "RUNGE-KUTTA_EXPLICIT")
+    prec = {"ILU": 1, "ILU0": 1, "LU_SGS": 0}[c.get("LINEAR_SOLVER_PREC", "ILU")]
+    order_map = {"1ST_ORDER": 0, "2ND_ORDER": 1, "2ND_ORDER_LIMITER": 2}
+    flow_cfg = dict(mach_inf=f("MACH_NUMBER", 0.0), cfl=f("CFL_NUMBER", 1.25), max_delta_time=f("MAX_DELTA_TIME", 1e6),
+                    prandtl_lam=f("PRANDTL_LAM", 0.72), prandtl_turb=f("PRANDTL_TURB", 0.9),
+                    lewis_turb=f("LEWIS_TURB", 1.2), c_mu=f("C_MU", 0.09), pasr_lb=f("PASR_LB", 1.0),
+                    lin_tol=f("LINEAR_SOLVER_ERROR", 1e-5), lin_iter=int(f("LINEAR_SOLVER_ITER", 10)),
+                    lin_prec=prec, relaxation=f("RELAXATION_FACTOR_FLOW", 1.0),
+                    implicit=int(tf == "EULER_IMPLICIT"), rans=int(c.get("KIND_TURB_MODEL", "NONE") == "SST"),
+                    spatial_order=order_map[c.get("SPATIAL_ORDER_FLOW", "2ND_ORDER")],
+                    ref_elem_length=f("REF_ELEM_LENGTH", 0.1), limiter_coeff=f("LIMITER_COEFF", 0.5),
+                    t_min=f("TEMPERATURE_MIN", 200.0), t_max=f("TEMPERATURE_MAX", 6000.0),
+                    clip_temp=int(c.get("CLIPPING_TEMPRATURE", "NO") == "YES"))
+    sst_cfg_kw = dict(implicit=int(c.get("TIME_DISCRE_TURB", "EULER_IMPLICIT") == "EULER_IMPLICIT"),
+                      lin_tol=flow_cfg["lin_tol"], lin_iter=flow_cfg["lin_iter"], lin_prec=prec,
+                      relaxation_turb=f("RELAXATION_FACTOR_TURB", 1.0), cfl_red_turb=f("CFL_REDUCTION_TURB", 1.0))
+    rk = [float(x) for x in _cfg_list(c.get("RK_ALPHA_COEFF", "(0.66667, 0.66667, 1.0)"))] \
+        if tf == "RUNGE-KUTTA_EXPLICIT" else None
+    # boundary markers, mesh marker order
+    inlets = _cfg_list(c.get("MARKER_INLET", ""))
+    inlet = {inlets[k]: [float(x) for x in inlets[k + 1:k + 6]] for k in range(0, len(inlets), 6)}
+    fr = [t for t in c.get("INLET_MASS_FRAC", "").strip().strip("()").split(";") if t.strip()]
+    inlet_y = {}
+    for t in fr:
+        p = _cfg_list(t)
+        inlet_y[p[0]] = [float(x) for x in p[1:1 + ns]]
+    outs = _cfg_list(c.get("MARKER_OUTLET", ""))
+    outlet = {outs[k]: float(outs[k + 1]) for k in range(0, len(outs), 2)}
+    isos = _cfg_list(c.get("MARKER_ISOTHERMAL", ""))
+    iso = {isos[k]: float(isos[k + 1]) for k in range(0, len(isos), 2)}
+    sym = set(_cfg_list(c.get("MARKER_SYM", "")))
+    kinds, rows = [], []
+    for tag in mesh.tags:
+        r = np.zeros(6 + ns)
+        if tag in inlet:
+            kinds.append(BC_INLET)
+            r[1:3] = inlet[tag][:2]
+            r[3:6] = inlet[tag][2:5]
+            r[6:] = inlet_y.get(tag, np.zeros(ns))
+        elif tag in outlet:
+            kinds.append(BC_OUTLET)
+            r[1] = outlet[tag]
+        elif tag in iso:
+            kinds.append(BC_ISOTHERMAL)
+            r[1] = iso[tag]
+        elif tag in sym:
+            kinds.append(BC_NONE)
+        else:
+            raise RxError(f"marker {tag}: boundary kind not supported on this path")
+        rows.append(r)
+    # free stream (SetNondimensionalization, DIMENSIONAL)
+    T_inf, P_inf = f("FREESTREAM_TEMPERATURE", 288.15), f("FREESTREAM_PRESSURE", 101325.0)
+    Y = np.array([float(x) for x in _cfg_list(c["FREESTREAM_MASS_FRAC"])])
+    mm = mech["mech_mmass"]
+    rgas = 0.0
+    for q in range(ns):  # ComputeRgas: inner_product(Ys, Ri), Ri = R_ungas / M_s
+        rgas += Y[q] * (R_UNGAS / mm[q])
+    rho_inf = P_inf / (rgas * T_inf)
+    cp = 0.0
+    for q in range(ns):  # ComputeCP
+        cp += Y[q] * (_spline(mech, 0, q, T_inf) / mm[q])
+    gamma = cp / (cp - rgas)  # ComputeFrozenGamma
+    mod_v0 = float(np.sqrt(sum(v * v for v in [float(x) for x in _cfg_list(c.get("FREESTREAM_VELOCITY",
+                                                                                "(1.0, 0.0, 0.0)"))][:mesh.n_dim])))
+    flow_cfg["mach_inf"] = mod_v0 / np.sqrt(gamma * rgas * T_inf)  # CConfig::SetMach (:973), frozen sound speed
+    visc = np.array([_spline(mech, 3, s, T_inf) for s in range(ns)])
+    yom = np.where(Y < 0.0, 1.0e-30, Y) / mm
+    eta = 0.0
+    for a in range(ns):  # ComputeEta (Wilke), the same expression as SetPrimVar's
+        phi = 0.0
+        for b in range(ns):
+            t = (1.0 + np.sqrt(visc[a] / visc[b]) * (mm[b] / mm[a]) ** 0.25)
+            phi += yom[b] / np.sqrt(8.0 * (1.0 + mm[a] / mm[b])) * t * t
+        eta += visc[a] * yom[a] / phi
+    vel = [float(x) for x in _cfg_list(c.get("FREESTREAM_VELOCITY", "(1.0, 0.0, 0.0)"))]
+    mod_v = float(np.sqrt(sum(v * v for v in vel[:mesh.n_dim])))
+    inten = f("FREESTREAM_TURBULENCEINTENSITY", 0.05)
+    tke = 3.0 / 2.0 * (mod_v * mod_v * inten * inten)
+    omega = rho_inf * tke / (eta * f("FREESTREAM_TURB2LAMVISCRATIO", 10.0))
+    bc = dict(kind=np.array(kinds, dtype=np.int32), data=np.array(rows), normal_neighbor=mesh.mesh()["bvertex_pn"],
+              inlet_kind={"TOTAL_CONDITIONS": INLET_TOTAL_CONDITIONS, "MASS_FLOW": INLET_MASS_FLOW,
+                          "TEMPERATURE_IMPOSE": INLET_TEMPERATURE_IMPOSE}[c.get("INLET_TYPE", "TOTAL_CONDITIONS")],
+              tke_inf=tke, kine_inf=tke, omega_inf=omega)
+    return dict(mesh=mesh, mech=mech, flow_cfg=flow_cfg, sst_cfg=sst_cfg_kw, bc=bc, rk_alpha=rk,
+                free_stream=dict(rho=rho_inf, mu=eta, T=T_inf, P=P_inf, Y=Y))
+
+
 def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=None, rk_alpha=None):
     """One reference outer iteration for REACTIVE_RANS on the device, in the reference's order
     (CMeanFlowIteration::Iterate iteration_structure.cpp:486-560; CMultiGridIntegration::MultiGrid_Iteration

@@ -136,3 +136,28 @@ def test_restart_roundtrip(tmp_path):
     assert np.array_equal(U2, q(U)) and np.array_equal(T2, q(T))
     assert np.array_equal(U2[i], q(U[i]))
     m.close()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CASE), reason="reference test case files absent")
+def test_case_from_cfg_matches_the_reference_setup(tmp_path):
+    """A cfg in the reference's grammar (the golden cases' cfg, oracle/make_golden.py CFG_TEMPLATE, with the
+    reference's mesh and library files): markers, inlet kind, free-stream turbulence values and the solver knobs
+    equal what the reference derived from the same cfg (golden bc9 / itx9 bc_params, dt_params)."""
+    from oracle import make_golden as MG
+    wd = MG.make_workdir("cfgcase", MG.full_jet_writer, cfl=0.1, order="1ST_ORDER", prec="LU_SGS",
+                         time_flow="EULER_EXPLICIT")
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    g = golden("itx9")
+    want = rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"])
+    bc = case["bc"]
+    assert np.array_equal(bc["kind"], want["kind"]) and bc["inlet_kind"] == want["inlet_kind"]
+    k = want["kind"] != 0
+    assert np.array_equal(bc["data"][k][:, 1:], want["data"][k][:, 1:])
+    assert np.array_equal(bc["normal_neighbor"], want["normal_neighbor"])
+    for key in ("tke_inf", "kine_inf", "omega_inf"):
+        assert abs(bc[key] - want[key]) <= 1e-14 * abs(want[key]), key
+    fc = case["flow_cfg"]
+    assert fc["cfl"] == g["dt_params"][0] and fc["implicit"] == 0 and fc["lin_prec"] == 0
+    assert fc["mach_inf"] == g["mach_inf"][0] and case["rk_alpha"] is None
+    check_geometry(case["mesh"], g)
+    case["mesh"].close()
