@@ -181,7 +181,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   ctx->nnzb = ctx->h_rp[N];
   ctx->h_col.resize(ctx->nnzb);
   std::vector<int32_t> rp32(N + 1), col32(ctx->nnzb);
-  std::vector<int64_t> diag(N), adj_blk(2 * E);
+  std::vector<int64_t> diag(N), adj_blk(2 * E), edge_blk(2 * E);
   for (int64_t i = 0; i < N; ++i) {
     rp32[i] = (int32_t)ctx->h_rp[i];
     for (size_t q = 0; q < rows[i].size(); ++q) {
@@ -194,6 +194,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       const int32_t o = e32[2 * e + (side ^ 1)];
       const auto it = std::lower_bound(rows[i].begin(), rows[i].end(), o);
       adj_blk[k] = ctx->h_rp[i] + (it - rows[i].begin());
+      edge_blk[2 * e + side] = adj_blk[k];
     }
   }
   rp32[N] = (int32_t)ctx->nnzb;
@@ -423,6 +424,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   CK(dupload(ctx, &ctx->adj_ptr, adj_ptr.data(), N + 1));
   CK(dupload(ctx, &ctx->adj, adj.data(), 2 * E));
   CK(dupload(ctx, &ctx->adj_blk, adj_blk.data(), 2 * E));
+  CK(dupload(ctx, &ctx->edge_blk, edge_blk.data(), 2 * E));
   CK(dupload(ctx, &ctx->nbr_ptr, nptr.data(), N + 1));
   CK(dupload(ctx, &ctx->nbr, nbr.data(), nbr.size()));
   CK(dupload(ctx, &ctx->bv_ptr, bvp.data(), N + 1));
@@ -538,7 +540,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->vsumm, E * (int64_t)(14 + 5 * ctx->nDim + 9 * ns)));  // visc_summary_size<NS, NDIM>
-    CK(dalloc(ctx, &ctx->jsrc, N * (int64_t)nv * nv));
+    CK(dalloc(ctx, &ctx->jsrc, (N + kSrcTile - 1) / kSrcTile * kSrcTile * (int64_t)ctx->ns * nv));
     CK(dalloc(ctx, &ctx->rsrc, N * nv));
   }
   if (ctx->cfg.implicit) {
@@ -581,7 +583,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   if (!ctx) return RX_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->nbr_ptr,
+  void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->sendbuf, ctx->rms_sum,
@@ -648,7 +650,7 @@ int64_t rx_last_error_index(const rx_ctx* ctx) { return ctx ? ctx->last_err_inde
 int rx_residual_zero(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
-  ctx->phase_conv = ctx->phase_visc = ctx->phase_src = 0;
+  ctx->phase_conv = ctx->phase_visc = ctx->phase_src = ctx->offdiag_done = 0;
   ctx->assembled = ctx->cfg.implicit ? 0 : 1;
   if (ctx->bc_on && ctx->bc_stream && !ctx->capturing) {
     // the boundary fluxes of the current node records, overlapped with the interior sweeps (rx_bc.hip)
@@ -670,6 +672,7 @@ int rx_edge_flux_conv(rx_ctx* ctx) {
   rc = ctx->cfg.implicit ? rx_launch_ausm_edge(ctx) : rx_launch_ausm_node(ctx);
   if (rc) return rc;
   ctx->phase_conv = 1;
+  ctx->offdiag_done = 0;  // new convective blocks: off-diagonals are (re)assembled from them
   ctx->assembled = ctx->cfg.implicit ? 0 : 1;
   return RX_OK;
 }

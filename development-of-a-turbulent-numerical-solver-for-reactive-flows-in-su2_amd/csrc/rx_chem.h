@@ -35,11 +35,12 @@ __device__ inline double delta_gibbs(const DevMech& m, int r, double T, double* 
   return dG;
 }
 
-// Residual (species rows) and, if implicit, the species rows of the cell Jacobian ([nVar][nVar],
-// other rows zero). V: primitives, S: dT/dU. Returns an error code.
+// Residual (species rows) and, if implicit, the species rows of the cell Jacobian (the other rows are zero and
+// not stored): entry (species row s, column j) goes to J[(s * nVar + j) * jstride]. V: primitives, S: dT/dU.
+// Returns an error code.
 template <int NS, int NDIM>
 __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const double* V, const double* S,
-                                  double vol, double omega_turb, double* res, double* J) {
+                                  double vol, double omega_turb, double* res, double* J, int jstride) {
   constexpr int nVar = NS + NDIM + 2, RHOS_P = NDIM + 5, RHO_P = NDIM + 2, RHOS_S = NDIM + 2;
   const int nr = m.nr;
   int err = ERR_NONE;
@@ -160,7 +161,6 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
       bc[r] = !m.hasb[r] ? k.B[r] * (tmp - Kcd / k.Kc[r]) : k.B[r] * (m.betab[r] + m.Tab[r] / T) / T;
     }
   }
-  for (int q = 0; q < nVar * nVar; ++q) J[q] = 0.0;
   for (int s = 0; s < NS; ++s) {
     // column 0 (temperature) of the [Ns][Ns+1] source Jacobian, reaction-ordered accumulation
     double sj0 = 0.0;
@@ -170,11 +170,11 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
       sj0 += P.rans ? fixed * (fc[r] - bc[r]) * k.k[r] : fixed * (fc[r] - bc[r]);
     }
     const double fx = sj0 * P.t_ref * P.T_ref / P.rho_ref;
-    double* row = J + (RHOS_S + s) * nVar;
+    double* row = J + (size_t)s * nVar * jstride;
     row[0] = -fx * S[0] * vol;
 #pragma unroll
-    for (int d = 0; d < NDIM; ++d) row[1 + d] = -fx * S[1 + d] * vol;
-    row[NDIM + 1] = -fx * S[NDIM + 1] * vol;
+    for (int d = 0; d < NDIM; ++d) row[(1 + d) * jstride] = -fx * S[1 + d] * vol;
+    row[(NDIM + 1) * jstride] = -fx * S[NDIM + 1] * vol;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       double sjj = 0.0;
@@ -187,7 +187,7 @@ __device__ inline int source_cell(const DevMech& m, const SourceParams& P, const
           else sjj += fixed * num / (drho * k.Ys[j]);
         }
       }
-      row[RHOS_S + j] = -fx * S[RHOS_S + j] * vol - sjj * P.t_ref * vol;
+      row[(RHOS_S + j) * jstride] = -fx * S[RHOS_S + j] * vol - sjj * P.t_ref * vol;
     }
   }
   return err;

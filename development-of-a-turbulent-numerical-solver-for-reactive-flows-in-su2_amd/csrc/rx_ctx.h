@@ -17,6 +17,8 @@
 
 enum rx_kind { RX_KIND_FLOW = 0, RX_KIND_SST = 1 };
 
+constexpr int kSrcTile = 64;  // cells per tile of the source-Jacobian scratch (one wavefront, cell index fastest)
+
 struct rx_ctx {
   int device = 0;
   int kind = RX_KIND_FLOW;
@@ -53,6 +55,7 @@ struct rx_ctx {
   int32_t* adj_ptr = nullptr;   // [N+1] incident edges per node, increasing edge id
   int32_t* adj = nullptr;       // [2E] (edge << 1) | (node is the edge's second node)
   int64_t* adj_blk = nullptr;   // [2E] BSR block index of (node, other)
+  int64_t* edge_blk = nullptr;  // [E][2] BSR block index of (n0, n1) and (n1, n0)
   int32_t* nbr_ptr = nullptr;   // [N+1] LSQ neighbours in the reference order
   int32_t* nbr = nullptr;
   int32_t* bv_ptr = nullptr;    // [N+1] boundary vertices per node in (marker, vertex) order
@@ -104,11 +107,12 @@ struct rx_ctx {
   double* jconv = nullptr;   // [E][2][nVar*nVar]
   double* jvisc = nullptr;   // [E][2][nVar*nVar]
   double* vsumm = nullptr;   // [E][visc_summary_size] per-edge viscous summary (implicit)
-  double* jsrc = nullptr;    // [N][nVar*nVar]
+  double* jsrc = nullptr;    // [ceil(N/kSrcTile)][ns*nVar][kSrcTile] species rows of the source Jacobians
   double* rsrc = nullptr;    // [N][nVar] source residual (implicit path)
   double* uold = nullptr;    // [N][nVar] Solution_Old of the RK stages
   double* recon = nullptr;   // [E][2][nPV] reconstructed edge states + [E][2][nVar] their dP/dU (2nd order)
   int phase_conv = 0, phase_visc = 0, phase_src = 0, assembled = 1;
+  int offdiag_done = 0;      // k_visc_jac wrote the off-diagonal blocks of this residual (fused assembly)
   double* lim_mn = nullptr;  // [N][nL]
   double* lim_mx = nullptr;
   double* red = nullptr;     // reduction scratch

@@ -6,6 +6,8 @@
 // 5374-5381). No atomics: results are bitwise reproducible run to run.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "rx_chem.h"
 #include "rx_ctx.h"
 #include "rx_visc.h"
@@ -636,10 +638,15 @@ __global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restri
 
 // a6: viscous Jacobians from the per-edge summary; a team of 16 lanes per edge, lane b = column b,
 // so every row of Ji / Jj is stored as one contiguous segment per team.
+// Fused assembly (Jc != nullptr): the same lanes also write the edge's two off-diagonal BSR blocks from its own
+// convective scratch, so k_assemble only builds the diagonal blocks and the residual (each Jc / Jv block is read
+// by the edge that made it and by its own node's diagonal, instead of by both nodes' teams).
 template <int NS, int NDIM>
-__global__ __launch_bounds__(kBlock) void k_visc_jac(int E, const int32_t* __restrict__ edges,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_visc_jac(int E, const int32_t* __restrict__ edges,
                                                      const double* __restrict__ dTdU, const double* __restrict__ Summ,
-                                                     DevMech m, ViscParams P, double* __restrict__ Jac) {
+                                                     DevMech m, ViscParams P, double* __restrict__ Jac,
+                                                     const double* __restrict__ Jc,
+                                                     const int64_t* __restrict__ edge_blk, double* __restrict__ A) {
   constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / 16, b = gt % 16;
@@ -648,7 +655,21 @@ __global__ __launch_bounds__(kBlock) void k_visc_jac(int E, const int32_t* __res
   const int bc = b < nVar ? b : 0;
   const double sib = dTdU[(size_t)n0 * nVar + bc], sjb = dTdU[(size_t)n1 * nVar + bc];
   double* Ji = Jac + (size_t)e * 2 * nVar2;
-  visc_jac_column<NS, NDIM>(m, P, Summ + (size_t)e * visc_summary_size<NS, NDIM>(), sib, sjb, b, b, Ji, Ji + nVar2);
+  const double* sm = Summ + (size_t)e * visc_summary_size<NS, NDIM>();
+  if (Jc) {
+    // this lane's column of both convective blocks, loaded before the Jacobian arithmetic hides their latency
+    const double* Jci = Jc + (size_t)e * 2 * nVar2;
+    double jci[nVar], jcj[nVar];
+#pragma unroll
+    for (int r = 0; r < nVar; ++r) {
+      jci[r] = Jci[r * nVar + bc];
+      jcj[r] = Jci[nVar2 + r * nVar + bc];
+    }
+    visc_jac_column<NS, NDIM>(m, P, sm, sib, sjb, b, b, Ji, Ji + nVar2, jci, jcj, A + edge_blk[2 * e] * nVar2,
+                              A + edge_blk[2 * e + 1] * nVar2);
+  } else {
+    visc_jac_column<NS, NDIM>(m, P, sm, sib, sjb, b, b, Ji, Ji + nVar2);
+  }
 }
 
 // Generic node gather of an edge flux array: node0 += sign*F, node1 -= sign*F (edge order).
@@ -669,7 +690,10 @@ __global__ __launch_bounds__(kBlock) void k_gather_flux(int N, int nVar, const i
   R[t] = acc;
 }
 
-// a9: PaSR source per cell: R[i] += S; implicit: cell Jacobian into scratch.
+// a9: PaSR source per cell: R[i] += S; implicit: the species rows of the cell Jacobian into scratch, in
+// 64-cell tiles with the cell index fastest ([N/64][NS*nVar][64], kSrcTile): every store of a wavefront is one
+// contiguous 512-B segment (the [N][nVar^2] thread-per-cell layout wrote 64 lines per store and amplified the
+// kernel's HBM writes 2.8x, profiles/r02_pmc_c3.json).
 template <int NS, int NDIM>
 __global__ __launch_bounds__(128) void k_source(int N, const double* __restrict__ V, const double* __restrict__ dTdU,
                                                 const double* __restrict__ vol, const double* __restrict__ omega,
@@ -682,9 +706,9 @@ __global__ __launch_bounds__(128) void k_source(int N, const double* __restrict_
 #pragma unroll
   for (int v = 0; v < nPV; ++v) Vl[v] = V[(size_t)i * nPV + v];
   double res[nVar];
-  const int rc = source_cell<NS, NDIM>(m, P, Vl, P.implicit ? dTdU + (size_t)i * nVar : nullptr, vol[i],
-                                       P.rans ? omega[i] : 0.0, res,
-                                       P.implicit ? Js + (size_t)i * nVar * nVar : nullptr);
+  const int rc = source_cell<NS, NDIM>(
+      m, P, Vl, P.implicit ? dTdU + (size_t)i * nVar : nullptr, vol[i], P.rans ? omega[i] : 0.0, res,
+      P.implicit ? Js + (size_t)(i / kSrcTile) * NS * nVar * kSrcTile + (i % kSrcTile) : nullptr, kSrcTile);
   bool bad = false;
 #pragma unroll
   for (int v = 0; v < nVar; ++v) {
@@ -705,60 +729,122 @@ __global__ __launch_bounds__(128) void k_source(int N, const double* __restrict_
 // Team = one or two whole wavefronts up to nVar = 11; above, exactly nVar^2 lanes (no intra-team synchronisation:
 // teams may straddle wavefronts), so nVar = 12 / 13 / 14 do not idle 112 / 87 / 60 of 256 lanes (C5 assembly
 // 10.0 -> 7.9 ms).
+constexpr int kAsmDeg = 8;  // incident edges of a node assembled from registers (larger degrees: the loop)
 template <int NVAR>
 constexpr int asm_team() {
   return NVAR * NVAR <= 64 ? 64 : (NVAR * NVAR <= 128 ? 128 : NVAR * NVAR);
 }
+// XCD-aware block order: the hardware deals consecutive workgroups round-robin to the 8 XCDs; this remaps them
+// so that XCD x assembles one contiguous range of nodes, and the 64 teams reading one source tile (and the
+// neighbouring nodes sharing edge blocks) run under the same L2.
+__device__ inline int xcd_block(int b, int nb) {
+  constexpr int kXcd = 8;
+  const int x = b % kXcd, idx = b / kXcd, q = nb / kXcd, r = nb % kXcd;
+  return x < r ? x * (q + 1) + idx : r * (q + 1) + (x - r) * q + idx;
+}
+
 template <int NVAR>
-__global__ __launch_bounds__(kBlock) void k_assemble(int N, const int32_t* __restrict__ adj_ptr,
+__global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int32_t* __restrict__ adj_ptr,
                                                      const int32_t* __restrict__ adj,
                                                      const int64_t* __restrict__ adj_blk,
                                                      const int64_t* __restrict__ diag, const double* __restrict__ Fc,
                                                      const double* __restrict__ Fv, const double* __restrict__ Jc,
                                                      const double* __restrict__ Jv, const double* __restrict__ Js,
                                                      const double* __restrict__ Rsrc, double* __restrict__ R,
-                                                     double* __restrict__ A, int visc, int src) {
+                                                     double* __restrict__ A, int visc, int src, int write_off) {
   constexpr int nVar2 = NVAR * NVAR, kTeam = asm_team<NVAR>();
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int gt = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int i = gt / kTeam, t = gt % kTeam;
   if (i >= N || t >= nVar2) return;
   const bool res = t < NVAR;
   double r = 0.0, D = 0.0;
   const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
-  // convective pass: residual and diagonal (own-side blocks)
-  for (int k = k0; k < k1; ++k) {
-    const int ad = adj[k];
-    const size_t e = (size_t)(ad >> 1);
-    const int side = ad & 1;
-    if (res) {
-      const double f = Fc[e * NVAR + t];
-      r = side ? r - f : r + f;
-    }
-    const double jd = Jc[(e * 2 + side) * nVar2 + t];  // own side: Ji for n0, Jj for n1
-    D = side ? D - jd : D + jd;
+  double rs = 0.0, js = 0.0;  // source residual / Jacobian entry, loaded up front
+  if (src) {
+    if (res) rs = Rsrc[(size_t)i * NVAR + t];
+    // species rows from the tiled scratch of k_source; the other rows of the reference's block are zeros
+    const int a = t / NVAR;
+    const int nsv = (NVAR - rhos) * NVAR;
+    js = a >= rhos ? Js[(size_t)(i / kSrcTile) * nsv * kSrcTile + (size_t)((a - rhos) * NVAR + t % NVAR) * kSrcTile +
+                        i % kSrcTile]
+                   : 0.0;
   }
-  // viscous pass: residual, diagonal, and each off-diagonal block written once as (0 +- Jc) -+ Jv
-  for (int k = k0; k < k1; ++k) {
-    const int ad = adj[k];
-    const size_t e = (size_t)(ad >> 1);
-    const int side = ad & 1;
-    const double joc = Jc[(e * 2 + (side ^ 1)) * nVar2 + t];  // other side
-    double off = side ? 0.0 - joc : 0.0 + joc;
-    if (visc) {
-      if (res) {
-        const double f = Fv[e * NVAR + t];
-        r = side ? r + f : r - f;
+  if (!write_off && k1 - k0 <= kAsmDeg) {
+    // fused path (k_visc_jac wrote the off-diagonals), degree <= kAsmDeg: every load of the node is issued
+    // before the first sum, so a team waits for one round trip instead of one per incident edge and pass;
+    // the sums then run in the reference's order (conv over edges, then visc over edges)
+    int ad[kAsmDeg];
+    double jc[kAsmDeg], jv[kAsmDeg], fc[kAsmDeg], fv[kAsmDeg];
+#pragma unroll
+    for (int q = 0; q < kAsmDeg; ++q) ad[q] = k0 + q < k1 ? adj[k0 + q] : 0;
+#pragma unroll
+    for (int q = 0; q < kAsmDeg; ++q) {
+      if (k0 + q < k1) {
+        const size_t e = (size_t)(ad[q] >> 1);
+        const int side = ad[q] & 1;
+        jc[q] = Jc[(e * 2 + side) * nVar2 + t];
+        jv[q] = visc ? Jv[(e * 2 + side) * nVar2 + t] : 0.0;
+        fc[q] = res ? Fc[e * NVAR + t] : 0.0;
+        fv[q] = res && visc ? Fv[e * NVAR + t] : 0.0;
       }
-      const double jd = Jv[(e * 2 + side) * nVar2 + t];
-      const double jov = Jv[(e * 2 + (side ^ 1)) * nVar2 + t];
-      D = side ? D + jd : D - jd;
-      off = side ? off + jov : off - jov;
     }
-    A[adj_blk[k] * nVar2 + t] = off;
+#pragma unroll
+    for (int q = 0; q < kAsmDeg; ++q)
+      if (k0 + q < k1) {
+        const int side = ad[q] & 1;
+        r = side ? r - fc[q] : r + fc[q];
+        D = side ? D - jc[q] : D + jc[q];
+      }
+    if (visc) {
+#pragma unroll
+      for (int q = 0; q < kAsmDeg; ++q)
+        if (k0 + q < k1) {
+          const int side = ad[q] & 1;
+          r = side ? r + fv[q] : r - fv[q];
+          D = side ? D + jv[q] : D - jv[q];
+        }
+    }
+  } else {
+    // convective pass: residual and diagonal (own-side blocks)
+    for (int k = k0; k < k1; ++k) {
+      const int ad = adj[k];
+      const size_t e = (size_t)(ad >> 1);
+      const int side = ad & 1;
+      if (res) {
+        const double f = Fc[e * NVAR + t];
+        r = side ? r - f : r + f;
+      }
+      const double jd = Jc[(e * 2 + side) * nVar2 + t];  // own side: Ji for n0, Jj for n1
+      D = side ? D - jd : D + jd;
+    }
+    // viscous pass: residual, diagonal, and (unless k_visc_jac wrote them) each off-diagonal block written once
+    // as (0 +- Jc) -+ Jv
+    for (int k = k0; k < k1; ++k) {
+      const int ad = adj[k];
+      const size_t e = (size_t)(ad >> 1);
+      const int side = ad & 1;
+      if (visc) {
+        if (res) {
+          const double f = Fv[e * NVAR + t];
+          r = side ? r + f : r - f;
+        }
+        const double jd = Jv[(e * 2 + side) * nVar2 + t];
+        D = side ? D + jd : D - jd;
+      }
+      if (write_off) {
+        const double joc = Jc[(e * 2 + (side ^ 1)) * nVar2 + t];  // other side
+        double off = side ? 0.0 - joc : 0.0 + joc;
+        if (visc) {
+          const double jov = Jv[(e * 2 + (side ^ 1)) * nVar2 + t];
+          off = side ? off + jov : off - jov;
+        }
+        A[adj_blk[k] * nVar2 + t] = off;
+      }
+    }
   }
   if (src) {
-    if (res) r += Rsrc[(size_t)i * NVAR + t];
-    D += Js[(size_t)i * nVar2 + t];
+    if (res) r += rs;
+    D += js;
   }
   if (res) R[(size_t)i * NVAR + t] = r;
   A[diag[i] * nVar2 + t] = D;
@@ -1131,9 +1217,14 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
   }
   if (ctx->cfg.implicit) {
     RxPhase ph(ctx, RX_K_VISC_JAC);
+    // fused off-diagonal assembly needs this residual's convective blocks (rx_edge_flux_conv ran first)
+    static const bool no_fuse = getenv("RX_NO_FUSED_ASM") != nullptr;  // diagnostic: the unfused assembly
+    const int fuse = ctx->phase_conv && !no_fuse ? 1 : 0;
     RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_visc_jac<NS_, ND_><<<blocks(ctx->E * 16), kBlock, 0, ctx->stream>>>(
-                              (int)ctx->E, ctx->edges, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->mech, P, ctx->jvisc)));
+                              (int)ctx->E, ctx->edges, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->mech, P, ctx->jvisc,
+                              fuse ? ctx->jconv : nullptr, ctx->edge_blk, ctx->f[RX_F_JAC])));
     RX_HIP(hipGetLastError());
+    ctx->offdiag_done = fuse;
   }
   return RX_OK;
 }
@@ -1163,10 +1254,10 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   switch (nv) {
 #define RX_ASM(NV)                                                                                          \
   case NV:                                                                                                  \
-    k_assemble<NV><<<blocks(ctx->N * asm_team<NV>()), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk,        \
+    k_assemble<NV><<<blocks(ctx->N * asm_team<NV>()), kBlock, 0, ctx->stream>>>((int)ctx->N, NV - ctx->ns, ctx->adj_ptr, ctx->adj, ctx->adj_blk, \
                                                    ctx->diag, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, \
                                                    ctx->jsrc, ctx->rsrc, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], \
-                                                   with_visc, with_src);                                      \
+                                                   with_visc, with_src, with_visc && ctx->offdiag_done ? 0 : 1); \
     break;
     RX_ASM(7)
     RX_ASM(8)

@@ -616,7 +616,9 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
 template <int NS, int NDIM>
 __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, const double* __restrict__ sm,
                                        double Sib, double Sjb, int b, int tl, double* __restrict__ Ji,
-                                       double* __restrict__ Jj) {
+                                       double* __restrict__ Jj, const double* jci = nullptr,
+                                       const double* jcj = nullptr, double* __restrict__ Aij = nullptr,
+                                       double* __restrict__ Aji = nullptr) {
   using L = VSL<NDIM>;
   constexpr int nVar = NS + NDIM + 2, NF = NDIM + 2;
   constexpr int RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
@@ -777,7 +779,19 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
     FI[RHOE_S][1 + d] += 0.5 * sm[L::PF + d];
     FJ[RHOE_S][1 + d] += 0.5 * sm[L::PF + d];
   }
-  // ---- J[a][b] = sum_k F[a][k] dV/dU[k][b]
+  // ---- J[a][b] = sum_k F[a][k] dV/dU[k][b]; with Aij/Aji the fused assembly also writes the edge's two
+  // off-diagonal blocks in the reference order A(i,j) = (0 + Jc_j) - Jv_j, A(j,i) = (0 - Jc_i) + Jv_i
+  // (AddBlock / SubtractBlock of Upwind_Residual then Viscous_Residual, solver_direct_reactive.cpp:2240-2246,
+  // :5365-5371); jci / jcj: column b of the convective blocks, row r at [r] (registers, loaded up front)
+  auto put = [&](int r, double si, double sj) {
+    const int idx = r * nVar + b;
+    Ji[idx] = si;
+    Jj[idx] = sj;
+    if (Aij) {
+      Aij[idx] = (0.0 + jcj[r]) - sj;
+      Aji[idx] = (0.0 - jci[r]) + si;
+    }
+  };
   double ci[NDIM], cj[NDIM];  // dV/dU velocity rows, column b
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) {
@@ -811,8 +825,7 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
         sj += FJ3k;
       }
     }
-    Ji[r * nVar + b] = si;
-    Jj[r * nVar + b] = sj;
+    put(r, si, sj);
   }
 #pragma unroll
   for (int a = 0; a < NS; ++a) {
@@ -825,8 +838,7 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
         sj += dsj;
       }
     }
-    Ji[(RHOS_S + a) * nVar + b] = si;
-    Jj[(RHOS_S + a) * nVar + b] = sj;
+    put(RHOS_S + a, si, sj);
   }
 }
 
