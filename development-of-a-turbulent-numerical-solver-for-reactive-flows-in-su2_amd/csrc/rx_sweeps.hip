@@ -18,6 +18,9 @@
 // scalar reference's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "rx_ctx.h"
 
 namespace {
@@ -847,6 +850,101 @@ __global__ __launch_bounds__(256) void k_ilu_bwd_part(const int32_t* __restrict_
   }
 }
 
+// Wide variants of the two sweeps for partitions whose vector does not fit in LDS: TB threads per
+// workgroup (TB / NV rows in flight, so a level of the C3 jet's 62-row-wide partitions is one pass instead
+// of three), row metadata from the schedule's slot records {i, klo, diag, khi} (one load instead of
+// rows -> klo / diag), and the first pass's slot of level l+1 loaded while level l runs. Same arithmetic,
+// operation for operation, as k_ilu_fwd_part / k_ilu_bwd_part.
+template <int NV, int TB>
+__global__ __launch_bounds__(TB) void k_ilu_fwd_wide(const int32_t* __restrict__ part_lvl,
+                                                     const int32_t* __restrict__ lvl_ptr,
+                                                     const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                                     const double* __restrict__ F, const double* __restrict__ b,
+                                                     double* __restrict__ x, int* __restrict__ done,
+                                                     const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  constexpr int NV2 = NV * NV, RPB = TB / NV;
+  const int p = blockIdx.x;
+  const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
+  const bool lane = rl < RPB;
+  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  int4 nxt = make_int4(-1, 0, 0, 0);
+  if (lane && l0 < l1 && lvl_ptr[l0] + rl < lvl_ptr[l0 + 1]) nxt = slot[lvl_ptr[l0] + rl];
+  for (int l = l0; l < l1; ++l) {
+    const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
+    const int4 cur = nxt;
+    nxt = make_int4(-1, 0, 0, 0);
+    if (lane && l + 1 < l1 && r1 + rl < lvl_ptr[l + 2]) nxt = slot[r1 + rl];
+    for (int r = r0 + rl; lane && r < r1; r += RPB) {
+      const int4 sl = (r == r0 + rl) ? cur : slot[r];
+      const int i = sl.x;
+      double xi = b[(size_t)i * NV + a];
+      for (int k = sl.y; k < sl.z; ++k) {
+        const double* blk = F + (size_t)k * NV2 + a * NV;
+        const double* xj = x + (size_t)col[k] * NV;
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
+        xi -= s;
+      }
+      x[(size_t)i * NV + a] = xi;
+    }
+    __syncthreads();
+  }
+}
+
+template <int NV, int TB>
+__global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__ part_lvl,
+                                                     const int32_t* __restrict__ lvl_ptr,
+                                                     const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                                     const double* __restrict__ F, const double* __restrict__ invD,
+                                                     double* __restrict__ x, int* __restrict__ done,
+                                                     const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  constexpr int NV2 = NV * NV, RPB = TB / NV;
+  __shared__ double v[RPB * NV];
+  const int p = blockIdx.x;
+  const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
+  const bool lane = rl < RPB;
+  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  int4 nxt = make_int4(-1, 0, 0, 0);
+  if (lane && l0 < l1 && lvl_ptr[l0] + rl < lvl_ptr[l0 + 1]) nxt = slot[lvl_ptr[l0] + rl];
+  for (int l = l0; l < l1; ++l) {
+    const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
+    const int4 cur = nxt;
+    nxt = make_int4(-1, 0, 0, 0);
+    if (lane && l + 1 < l1 && r1 + rl < lvl_ptr[l + 2]) nxt = slot[r1 + rl];
+    for (int base = r0; base < r1; base += RPB) {
+      const int r = base + rl;
+      const bool act = lane && r < r1;
+      int i = 0;
+      if (act) {
+        const int4 sl = (base == r0) ? cur : slot[r];
+        i = sl.x;
+        double sum = 0.0;
+        for (int k = sl.z + 1; k < sl.w; ++k) {
+          const double* blk = F + (size_t)k * NV2 + a * NV;
+          const double* xj = x + (size_t)col[k] * NV;
+          double s = 0.0;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
+          sum += s;
+        }
+        v[rl * NV + a] = x[(size_t)i * NV + a] - sum;
+      }
+      __syncthreads();
+      if (act) {
+        const double* inv = invD + (size_t)i * NV2 + a * NV;
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
+        x[(size_t)i * NV + a] = s;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ILU(0) application with the partition's vector resident in LDS: b is loaded once, the forward
 // and backward substitutions run level by level on the LDS copy, and x is stored once. The row
 // metadata of both schedules and the partition's column indices (local) are staged in LDS too, so the
@@ -1211,6 +1309,19 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                          b, x, done, conv)));
     RX_HIP(hipGetLastError());
     return rx_la_exchange(ctx, x, nv);  // ComputeILUPreconditioner's closing SendReceive_Solution (:1513)
+  }
+  static const bool narrow = getenv("RX_NARROW_APPLY") != nullptr;  // diagnosis: the 256-thread sweeps
+  const int width = std::max(ctx->fs.maxwidth, ctx->bs.maxwidth);
+  if (!narrow && width * nv > 256) {
+    const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
+    const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
+    RX_NV_SWITCH(nv, (k_ilu_fwd_wide<NV_, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
+                         ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->col, ctx->f[RX_F_ILU], b, x, done, conv)));
+    RX_NV_SWITCH(nv, (k_ilu_bwd_wide<NV_, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
+                         ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx), x,
+                         done, conv)));
+    RX_HIP(hipGetLastError());
+    return rx_la_exchange(ctx, x, nv);
   }
   RX_NV_SWITCH(ctx->nVar, (k_ilu_fwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->diag,
