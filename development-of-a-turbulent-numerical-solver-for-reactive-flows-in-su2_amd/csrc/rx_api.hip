@@ -394,6 +394,18 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       si[q] = (int32_t)mesh->send_idx[q];
     }
     CK(dupload(ctx, &ctx->send_idx, si.data(), si.size()));
+    {  // gradient order of the overlapped exchange: points some neighbour receives, then the others
+      std::vector<char> sent(ctx->Nd, 0);
+      for (int32_t q : si) sent[q] = 1;
+      std::vector<int32_t> gl;
+      gl.reserve(ctx->Nd);
+      for (int64_t i = 0; i < ctx->Nd; ++i)
+        if (sent[i]) gl.push_back((int32_t)i);
+      ctx->n_grad_bnd = (int64_t)gl.size();
+      for (int64_t i = 0; i < ctx->Nd; ++i)
+        if (!sent[i]) gl.push_back((int32_t)i);
+      CK(dupload(ctx, &ctx->grad_list, gl.data(), gl.size()));
+    }
     // the widest exchangeable node record: D_ij (Ns^2), the primitive gradient (nG x nDim) or V (nPV)
     ctx->halo_stride = std::max({kHaloMaxStride, ctx->ns * ctx->ns, ctx->nG * ctx->nDim, ctx->nPV});
     CK(dalloc(ctx, &ctx->sendbuf, (size_t)std::max<int64_t>(1, ctx->n_send) * ctx->halo_stride));
@@ -586,7 +598,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
-                  ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->sendbuf, ctx->rms_sum,
+                  ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->grad_list, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   rx_comm_free(ctx);
@@ -703,10 +715,30 @@ int rx_cell_source_pasr(rx_ctx* ctx) {
 int rx_grad_lsq(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_GRAD);
-  const int rc = rx_launch_grad(ctx);
+  const int stride = (int)(ctx->fcount[RX_F_GRAD] / ctx->N);
+  if (!ctx->distributed() || !ctx->grad_list) {
+    const int rc = rx_launch_grad(ctx, nullptr, ctx->N);
+    if (rc) return rc;
+    // Set_MPI_Primitive_Gradient (solver_direct_reactive.cpp:5049)
+    return rx_la_exchange(ctx, ctx->f[RX_F_GRAD], stride);
+  }
+  // Distributed: the owned points the neighbours receive first, then their exchange (on comm_stream with
+  // RCCL) runs while the remaining owned points are computed; halo rows come only from their owners, as
+  // Set_MPI_Primitive_Gradient leaves them. Every point's arithmetic is unchanged (bitwise the same).
+  int rc = rx_launch_grad(ctx, ctx->grad_list, ctx->n_grad_bnd);
   if (rc) return rc;
-  // Set_MPI_Primitive_Gradient (solver_direct_reactive.cpp:5049)
-  return rx_la_exchange(ctx, ctx->f[RX_F_GRAD], (int)(ctx->fcount[RX_F_GRAD] / ctx->N));
+  const bool overlap = ctx->comm_stream != nullptr && !ctx->capturing;
+  if (overlap) {
+    RX_HIP(hipEventRecord(ctx->comm_fork, ctx->stream));
+    RX_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->comm_fork, 0));
+    if ((rc = rx_la_exchange_on(ctx, ctx->f[RX_F_GRAD], stride, ctx->comm_stream))) return rc;
+    RX_HIP(hipEventRecord(ctx->comm_join, ctx->comm_stream));
+  } else if ((rc = rx_la_exchange(ctx, ctx->f[RX_F_GRAD], stride))) {
+    return rc;
+  }
+  if ((rc = rx_launch_grad(ctx, ctx->grad_list + ctx->n_grad_bnd, ctx->Nd - ctx->n_grad_bnd))) return rc;
+  if (overlap) RX_HIP(hipStreamWaitEvent(ctx->stream, ctx->comm_join, 0));
+  return RX_OK;
 }
 
 int rx_limiter_venkat(rx_ctx* ctx) {

@@ -1,5 +1,6 @@
 // rx_comm.hip — multi-GPU plumbing: halo exchange and all-reduce on the context stream, over RCCL
-// (graph-capturable: the FGMRES graph contains them) or over a caller-provided host transport.
+// (graph-capturable: the FGMRES graph contains them) or over a caller-provided host transport. The
+// primitive-gradient exchange overlaps the interior gradients on a side stream (rx_grad_lsq).
 //
 // Halo exchange = the reference's SendReceive_Solution / Set_MPI_Solution / Set_MPI_Primitive_*
 // (Common/src/matrix_structure.cpp:794-880; SU2_CFD/src/solver_direct_reactive.cpp:1530-1640,
@@ -35,12 +36,17 @@ int stage_alloc(rx_ctx* ctx) {
 
 }  // namespace
 
-int rx_la_exchange(rx_ctx* ctx, double* f, int stride) {
+int rx_la_exchange(rx_ctx* ctx, double* f, int stride) { return rx_la_exchange_on(ctx, f, stride, ctx->stream); }
+
+// The exchange on stream st (the context stream, or comm_stream for the overlapped gradient exchange; the host
+// transport always runs on the context stream).
+int rx_la_exchange_on(rx_ctx* ctx, double* f, int stride, hipStream_t st) {
   if (!ctx->distributed() || ctx->n_neigh == 0) return RX_OK;
   if (stride > ctx->halo_stride) return RX_ERR_ARG;
+  if (ctx->has_hcomm) st = ctx->stream;
   if (ctx->n_send > 0) {
     const int64_t n = ctx->n_send * stride;
-    k_pack<<<(int)((n + 255) / 256), 256, 0, ctx->stream>>>(ctx->n_send, stride, ctx->send_idx, f, ctx->sendbuf);
+    k_pack<<<(int)((n + 255) / 256), 256, 0, st>>>(ctx->n_send, stride, ctx->send_idx, f, ctx->sendbuf);
     RX_HIP(hipGetLastError());
   }
   double* halo = f + ctx->Nd * stride;
@@ -64,10 +70,9 @@ int rx_la_exchange(rx_ctx* ctx, double* f, int stride) {
     const int64_t r0 = ctx->h_recv_ptr[k], r1 = ctx->h_recv_ptr[k + 1];
     if (s1 > s0)
       rc = nccl_rc(ncclSend(ctx->sendbuf + s0 * stride, (size_t)((s1 - s0) * stride), ncclDouble, ctx->h_neigh[k],
-                            comm, ctx->stream));
+                            comm, st));
     if (!rc && r1 > r0)
-      rc = nccl_rc(ncclRecv(halo + r0 * stride, (size_t)((r1 - r0) * stride), ncclDouble, ctx->h_neigh[k], comm,
-                            ctx->stream));
+      rc = nccl_rc(ncclRecv(halo + r0 * stride, (size_t)((r1 - r0) * stride), ncclDouble, ctx->h_neigh[k], comm, st));
   }
   const int rc2 = nccl_rc(ncclGroupEnd());
   return rc ? rc : rc2;
@@ -131,6 +136,10 @@ int rx_comm_init(rx_ctx* ctx, int nranks, int rank, const void* id128) {
   ctx->comm = comm;
   ctx->nranks = nranks;
   ctx->rank = rank;
+  // side stream of the overlapped gradient exchange (rx_grad_lsq)
+  RX_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+  RX_HIP(hipEventCreateWithFlags(&ctx->comm_fork, hipEventDisableTiming));
+  RX_HIP(hipEventCreateWithFlags(&ctx->comm_join, hipEventDisableTiming));
   return comm_attached(ctx);
 }
 
@@ -175,6 +184,13 @@ int rx_comm_borrow(rx_ctx* ctx, const rx_ctx* from) {
 }
 
 void rx_comm_free(rx_ctx* ctx) {
+  if (ctx->comm_stream) {
+    (void)hipStreamSynchronize(ctx->comm_stream);
+    (void)hipStreamDestroy(ctx->comm_stream);
+    (void)hipEventDestroy(ctx->comm_fork);
+    (void)hipEventDestroy(ctx->comm_join);
+    ctx->comm_stream = nullptr;
+  }
   if (ctx->comm && ctx->comm_owned) (void)ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
   ctx->comm = nullptr;
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);

@@ -43,6 +43,12 @@ struct rx_ctx {
   double* h_stage = nullptr;    // pinned [(n_send + N - Nd) * halo_stride + 64]
   int nranks = 1, rank = 0;
   bool distributed() const { return comm != nullptr || has_hcomm; }
+  // compute / communication overlap of the primitive-gradient exchange (rx_grad_lsq): the owned points
+  // the neighbours need first (n_grad_bnd of them), then the rest while the exchange runs on comm_stream
+  int32_t* grad_list = nullptr; // [Nd]
+  int64_t n_grad_bnd = 0;
+  hipStream_t comm_stream = nullptr;  // RCCL transport only
+  hipEvent_t comm_fork = nullptr, comm_join = nullptr;
   int64_t n_global = 0;         // owned points over all ranks
   double* rms_sum = nullptr;    // [32] per-variable sums of squares (device)
   rx_cfg cfg{};
@@ -181,6 +187,7 @@ int rx_fail_hip(rx_ctx* ctx, hipError_t e);
 constexpr int kHaloMaxStride = 64;  // minimum doubles per point of the exchange buffers (ctx->halo_stride)
 // halo exchange of a device array with `stride` doubles per point (no-op without communicator)
 int rx_la_exchange(rx_ctx* ctx, double* f, int stride);
+int rx_la_exchange_on(rx_ctx* ctx, double* f, int stride, hipStream_t st);
 // out[i] = sum over ranks of in[i] (in == out allowed), ordered on the context stream; no-op
 // without communicator
 int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count);
@@ -217,7 +224,7 @@ int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);
 int rx_launch_source(rx_ctx* ctx);
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src);
-int rx_launch_grad(rx_ctx* ctx);
+int rx_launch_grad(rx_ctx* ctx, const int32_t* list, int64_t n);  // list null: points 0..n-1
 int rx_launch_limiter(rx_ctx* ctx);
 int rx_launch_time_step(rx_ctx* ctx);
 int rx_check_error(rx_ctx* ctx);

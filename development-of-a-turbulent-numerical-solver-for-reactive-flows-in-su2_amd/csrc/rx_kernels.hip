@@ -854,11 +854,13 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int3
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) void k_grad_lsq(int N, const int32_t* __restrict__ nptr,
                                                      const int32_t* __restrict__ nbr, const double* __restrict__ coord,
-                                                     const double* __restrict__ V, DevMech m, double* __restrict__ Gout) {
+                                                     const double* __restrict__ V, DevMech m, double* __restrict__ Gout,
+                                                     const int32_t* __restrict__ list) {
   constexpr int nPV = NS + NDIM + 5, nG = NS + NDIM + 2, P_P = NDIM + 1, RHOS_P = NDIM + 5, P_G = NDIM + 1,
                 RHOS_G = NDIM + 2;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const int i = list ? list[t] : t;  // list: the points of one half of the distributed split (rx_grad_lsq)
   double pi[nG], pj[nG], C[nG][NDIM];
   {
     const double* v = V + (size_t)i * nPV;
@@ -1273,10 +1275,11 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   return RX_OK;
 }
 
-int rx_launch_grad(rx_ctx* ctx) {
-  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_grad_lsq<NS_, ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
-                            (int)ctx->N, ctx->nbr_ptr, ctx->nbr, ctx->coord, ctx->f[RX_F_V], ctx->mech,
-                            ctx->f[RX_F_GRAD])));
+int rx_launch_grad(rx_ctx* ctx, const int32_t* list, int64_t n) {
+  if (n <= 0) return RX_OK;
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_grad_lsq<NS_, ND_><<<blocks(n), kBlock, 0, ctx->stream>>>(
+                            (int)n, ctx->nbr_ptr, ctx->nbr, ctx->coord, ctx->f[RX_F_V], ctx->mech,
+                            ctx->f[RX_F_GRAD], list)));
   RX_HIP(hipGetLastError());
   return RX_OK;
 }

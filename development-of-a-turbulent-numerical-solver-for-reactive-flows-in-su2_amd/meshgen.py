@@ -233,27 +233,55 @@ def renumber(pts, quads, bnd, perm):
     return pts[perm], old2new[quads], {k: old2new[v] for k, v in bnd.items()}, old2new
 
 
-def partition_rcb(coord, n_part: int):
+def partition_rcb(coord, n_part: int, edges=None):
     """Recursive coordinate bisection into n_part balanced parts (stand-in for the reference's METIS
     k-way call, geometry_structure.cpp:11465-11530: any partition is valid input, the solver records
-    it). Returns the part id of every point."""
-    part = np.zeros(len(coord), dtype=np.int64)
+    it). Returns the part id of every point.
 
-    def split(idx, p0, np_):
+    edges None: each cut is across the longer extent normalised by the domain's. With the mesh edges, the
+    extent is measured in mesh spacings (extent / median length of the part's edges running along that axis),
+    i.e. in cells, so parts come out square in the graph and the edge cut approaches the grid's
+    isoperimetric bound (tools/edge_cut.py, profiles/r02_edge_cut.json) on stretched meshes too."""
+    part = np.zeros(len(coord), dtype=np.int64)
+    nd = coord.shape[1]
+    if edges is not None:
+        edges = np.asarray(edges)
+        d = np.abs(coord[edges[:, 1]] - coord[edges[:, 0]])
+        along = np.argmax(d, axis=1)
+        inside = np.zeros(len(coord), dtype=bool)
+
+    def axis_of(idx, eidx):
+        ext = coord[idx].max(axis=0) - coord[idx].min(axis=0)
+        if edges is None:
+            return int(np.argmax(ext / np.maximum(dom, 1e-300)))
+        cells = np.zeros(nd)
+        for a in range(nd):
+            da = d[eidx[along[eidx] == a], a]
+            h = np.median(da) if len(da) else ext[a] / max(1.0, len(idx) ** (1.0 / nd))
+            cells[a] = ext[a] / max(h, 1e-300)
+        return int(np.argmax(cells))
+
+    def split(idx, eidx, p0, np_):
         if np_ == 1:
             part[idx] = p0
             return
         left = np_ // 2
-        ext = coord[idx].max(axis=0) - coord[idx].min(axis=0)
-        # split along the longer extent, normalised by the domain aspect so slabs stay square-ish
-        ax = int(np.argmax(ext / np.maximum(dom, 1e-300)))
+        ax = axis_of(idx, eidx)
         o = idx[np.argsort(coord[idx, ax], kind="stable")]
         cut = int(round(len(o) * left / np_))
-        split(o[:cut], p0, left)
-        split(o[cut:], p0 + left, np_ - left)
+        lo, hi = o[:cut], o[cut:]
+        el = eh = None
+        if edges is not None:
+            inside[lo] = True
+            inside[hi] = False
+            a, b = inside[edges[eidx, 0]], inside[edges[eidx, 1]]
+            el = eidx[a & b]
+            eh = eidx[~a & ~b]
+        split(lo, el, p0, left)
+        split(hi, eh, p0 + left, np_ - left)
 
     dom = coord.max(axis=0) - coord.min(axis=0)
-    split(np.arange(len(coord)), 0, int(n_part))
+    split(np.arange(len(coord)), None if edges is None else np.arange(len(edges)), 0, int(n_part))
     return part
 
 
@@ -275,17 +303,19 @@ def partition_order(n, edges, part):
     return np.concatenate(perm), np.asarray(ptr, dtype=np.int64)
 
 
-def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, nz: int = 0, **kw):
+def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, nz: int = 0, partitioner: str = "coord", **kw):
     """Synthetic jet mesh ready for the solver: RCM-ordered points + median dual (nz > 1: the 3-D extrusion).
 
     n_part > 1: points are split into n_part RCB parts (the reference's MPI ranks), numbered part by
-    part with a local RCM; `part_ptr` gives the row range of every part."""
+    part with a local RCM; `part_ptr` gives the row range of every part. partitioner "coord" (default: the
+    partitions every golden, size test and bench line was measured on) or "spacing" (cuts in mesh spacings:
+    within 2 % of the grid's edge-cut bound, profiles/r02_edge_cut.json)."""
     pts, quads, bnd = jet_mesh3d(nx, ny, nz, **kw) if nz > 1 else jet_mesh(nx, ny, **kw)
     median_dual = median_dual3d if nz > 1 else median_dual2d
     part_ptr = np.array([0, len(pts)], dtype=np.int64)
     if n_part > 1:
         d0 = median_dual(pts, quads, bnd)
-        perm, part_ptr = partition_order(len(pts), d0["edges"], partition_rcb(pts, n_part))
+        perm, part_ptr = partition_order(len(pts), d0["edges"], partition_rcb(pts, n_part, edges=d0["edges"] if partitioner == "spacing" else None))
         pts, quads, bnd, _ = renumber(pts, quads, bnd, perm)
     elif rcm:
         d0 = median_dual(pts, quads, bnd)

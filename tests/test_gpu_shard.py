@@ -3,6 +3,8 @@
 
 - World size 1 with an RCCL communicator: the all-reduce path of FGMRES (rank-local sums -> landing
   slots) and the RCCL calls inside the captured solve graph give bitwise the single-context result.
+- World size 2, EULER_EXPLICIT flow: the same against one context at 1e-10 (no linear solver to amplify the
+  ranks' edge-order rounding).
 - World size 2 on the one GPU of the test box (RCCL refuses two ranks on one device, so the ranks use
   the host-staged transport over gloo, the reference's own MPI pattern): gradients are bitwise the
   global ones on every local row (owned rows recomputed in the same neighbour order, halo rows
@@ -25,9 +27,10 @@ pytestmark = pytest.mark.gpu
 NX, NY, NPART, NS = 48, 20, 8, 7
 
 
-def _case():
+def _case(implicit=1):
     mesh, st, mech_arrays, kw = synth.jet_case(NX, NY, n_species=NS, n_part=NPART)
-    cfg = rx.default_cfg(implicit=1, lin_prec=1, cfl=5.0, max_delta_time=1e6, prandtl_lam=0.72,
+    cfg = rx.default_cfg(implicit=implicit, lin_prec=1, cfl=5.0 if implicit else 0.5, max_delta_time=1e6,
+                         prandtl_lam=0.72,
                          prandtl_turb=kw["prandtl_turb"], lewis_turb=kw["lewis_turb"], mach_inf=kw["mach_inf"],
                          c_mu=kw["c_mu"], pasr_lb=kw["pasr_lb"], lin_tol=1e-6, lin_iter=5, relaxation=1.0)
     return mesh, st, mech_arrays, cfg
@@ -53,18 +56,33 @@ def _step(s, t):
     return grad, np.r_[rms, trms], (it, tit)
 
 
+def _step_explicit(s):
+    """One EULER_EXPLICIT flow iteration (ExplicitEuler_Iteration, solver_direct_reactive.cpp:2412-2454): no
+    linear solver, so the ranks' results differ from one context by the edge-order rounding only."""
+    s.SetPrimitive_Gradient_LS()
+    grad = s.download("GRAD")
+    s.SetStrainMag()
+    s.SetTime_Step()
+    s.Preprocessing_zero()
+    s.Upwind_Residual()
+    s.Viscous_Residual()
+    s.Source_Residual()
+    rms = s.ExplicitEuler_Iteration()
+    return grad, rms, 0
+
+
 def _set(s, t, mesh, st):
     s.set_state(st)
     t.set_state(st["sst_sol"], mesh["wall_distance"], st["sst_F1"], st["sst_F2"], st["sst_CDkw"])
 
 
-def _global_run():
-    mesh, st, mech_arrays, cfg = _case()
+def _global_run(implicit=1):
+    mesh, st, mech_arrays, cfg = _case(implicit)
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), cfg)
     t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
     _set(s, t, mesh, st)
     U0 = s.download("U")
-    grad, rms, it = _step(s, t)
+    grad, rms, it = _step(s, t) if implicit else _step_explicit(s)
     U = s.download("U")
     T = t.download("U")
     s.close()
@@ -89,20 +107,20 @@ def test_rccl_world1_matches_single_context():
     s.close()
 
 
-def _rank_worker(rank, world, port, q):
+def _rank_worker(rank, world, port, q, implicit=1):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        mesh, st, mech_arrays, cfg = _case()
+        mesh, st, mech_arrays, cfg = _case(implicit)
         sh = meshgen.shard(mesh, world, rank)
         st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
         s = rx.ReactiveNSSolver(sh, rx.Mechanism(mech_arrays), cfg)
         s.comm_init_host(world, rank, rx.TorchHostTransport())
         t = rx.TurbSSTSolver(sh, s, rx.sst_cfg())
         _set(s, t, sh, st_l)
-        grad, rms, it = _step(s, t)
+        grad, rms, it = _step(s, t) if implicit else _step_explicit(s)
         U = s.download("U")
         T = t.download("U")
         s.close()
@@ -113,15 +131,13 @@ def _rank_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_ranks_host_transport_match_single_context():
-    g0, rms0, it0, U_init, U0, T0 = _global_run()
-    nvar = NS + 4
+def _run_ranks(world, implicit):
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_rank_worker, args=(r, world, port, q, implicit)) for r in range(world)]
     for p in ps:
         p.start()
     try:
@@ -129,8 +145,40 @@ def test_two_ranks_host_transport_match_single_context():
     finally:
         for p in ps:
             p.join(timeout=120)
-    for r in range(2):
+    for r in range(world):
         assert isinstance(res[r], dict), res[r]
+    return res
+
+
+def test_two_ranks_explicit_match_single_context_1e10():
+    """EULER_EXPLICIT flow on two ranks (host transport; the gradient split around its exchange on every rank)
+    against one context: gradients bitwise on every local row, the all-reduced RMS and the update to 1e-10."""
+    g0, rms0, _, U_init, U0, _ = _global_run(implicit=0)
+    nvar = NS + 4
+    res = _run_ranks(2, implicit=0)
+    g0 = g0.reshape(len(U0) // nvar, -1)
+    U0 = U0.reshape(-1, nvar)
+    U_init = U_init.reshape(-1, nvar)
+    U_sh = np.zeros_like(U0)
+    for r in range(2):
+        d = res[r]
+        l2g, nd = d["l2g"], d["nd"]
+        assert np.array_equal(d["grad"].reshape(len(l2g), -1), g0[l2g])
+        assert np.array_equal(d["rms"], res[0]["rms"])
+        U_l = d["U"].reshape(len(l2g), nvar)
+        U_sh[l2g[:nd]] = U_l[:nd]
+    for r in range(2):
+        d = res[r]
+        l2g, nd = d["l2g"], d["nd"]
+        assert np.array_equal(d["U"].reshape(len(l2g), nvar)[nd:], U_sh[l2g[nd:]]), "halo rows = owners' rows"
+    assert_close(res[0]["rms"], rms0, rtol=1e-10, what="RMS (two ranks vs one context, explicit)")
+    per_column_close(U_sh - U_init, U0 - U_init, rtol=1e-10, floor=1e-14, what="dU (two ranks vs one context, explicit)")
+
+
+def test_two_ranks_host_transport_match_single_context():
+    g0, rms0, it0, U_init, U0, T0 = _global_run()
+    nvar = NS + 4
+    res = _run_ranks(2, implicit=1)
     g0 = g0.reshape(len(U0) // nvar, -1)
     U0 = U0.reshape(-1, nvar)
     U_init = U_init.reshape(-1, nvar)
@@ -161,7 +209,8 @@ def test_two_ranks_host_transport_match_single_context():
     assert_close(res[0]["rms"], rms0, rtol=1e-10, what="RMS (two ranks vs one context)")
     # Each rank orders its local edges by local ids (halo points last), as the reference's partitioned
     # CGeometry does, so residual/Jacobian sums round differently from the one-context run (RMS above
-    # agrees to 1e-10); FGMRES(5)+ILU(0) amplifies that to ~1e-8 in the update (measured 1.1e-8).
+    # agrees to 1e-10); FGMRES(5)+ILU(0) amplifies that to ~1e-8 in the update (measured 1.1e-8; 8.7e-8 on the
+    # spacing-aware partitions; the explicit test above holds 1e-10 without a solver).
     per_column_close(U_sh - U_init, U0 - U_init, rtol=5e-8, floor=1e-14, what="dU (two ranks vs one context)")
     # the SST step on the same shards (RMS all-reduced, (k, omega) halos exchanged after the update)
     per_column_close(T_sh, T0, rtol=5e-8, floor=1e-14, what="(k, omega) (two ranks vs one context)")
