@@ -551,7 +551,9 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     CK(dalloc(ctx, &ctx->fconv, E * nv));
     CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
-    CK(dalloc(ctx, &ctx->vsumm, E * (int64_t)(14 + 5 * ctx->nDim + 9 * ns)));  // visc_summary_size<NS, NDIM>
+    // visc_summary_size<NS, NDIM> per edge, in tiles of rx::kSummTile edges
+    CK(dalloc(ctx, &ctx->vsumm, (E + rx::kSummTile - 1) / rx::kSummTile * rx::kSummTile *
+                                    (int64_t)(14 + 5 * ctx->nDim + 9 * ns)));
     CK(dalloc(ctx, &ctx->jsrc, (N + kSrcTile - 1) / kSrcTile * kSrcTile * (int64_t)ctx->ns * nv));
     CK(dalloc(ctx, &ctx->rsrc, N * nv));
   }

@@ -396,7 +396,8 @@ __global__ __launch_bounds__(64) void k_bc_weak(int NW, const int32_t* __restric
   }
   double res[nVar];
   double* sm = B.implicit ? summ + (size_t)b * visc_summary_size<NS, NDIM>() : nullptr;
-  const int rc = visc_edge<NS, NDIM>(m, B.vp, a, g, sk, Normal, res, sm, scr_all + threadIdx.x * NS * NS, false);
+  const int rc = visc_edge<NS, NDIM>(m, B.vp, a, g, sk, Normal, res, SummRef{sm, 1}, scr_all + threadIdx.x * NS * NS,
+                                     false);
   bad = false;
 #pragma unroll
   for (int v = 0; v < nVar; ++v) {
@@ -422,7 +423,8 @@ __global__ __launch_bounds__(kBlock) void k_bc_visc_jac(int NW, const int32_t* _
   const int cc = c < nVar ? c : 0;
   const double sib = dTdU[(size_t)i * nVar + cc], sjb = sv[(size_t)b * nVar + cc];
   double* Ji = jacv + (size_t)b * 2 * nVar2;
-  visc_jac_column<NS, NDIM>(m, P, summ + (size_t)b * visc_summary_size<NS, NDIM>(), sib, sjb, c, c, Ji, Ji + nVar2);
+  visc_jac_column<NS, NDIM>(m, P, SummCRef{summ + (size_t)b * visc_summary_size<NS, NDIM>(), 1}, sib, sjb, c, c, Ji,
+                            Ji + nVar2);
 }
 
 // CSysMatrix::DeleteValsRowi (Common/src/matrix_structure.cpp:483-495) for scalar row r of block row i.

@@ -112,7 +112,7 @@ struct rx_ctx {
   double* fvisc = nullptr;   // [E][nVar]   viscous edge fluxes
   double* jconv = nullptr;   // [E][2][nVar*nVar]
   double* jvisc = nullptr;   // [E][2][nVar*nVar]
-  double* vsumm = nullptr;   // [E][visc_summary_size] per-edge viscous summary (implicit)
+  double* vsumm = nullptr;   // [E/kSummTile][visc_summary_size][kSummTile] per-edge viscous summary (implicit)
   double* jsrc = nullptr;    // [ceil(N/kSrcTile)][ns*nVar][kSrcTile] species rows of the source Jacobians
   double* rsrc = nullptr;    // [N][nVar] source residual (implicit path)
   double* uold = nullptr;    // [N][nVar] Solution_Old of the RK stages

@@ -11,6 +11,7 @@
 
 namespace rx {
 
+constexpr int kSummTile = 64;  // edges per tile of the viscous summary scratch (rx_visc.h SummRef)
 constexpr double kEPS = 1.0e-16;  // Common/include/option_structure.hpp:134
 constexpr double kNA = 6.02214129 * 1.0e23;
 constexpr double kKB = 1.3806488 * 1.0e-23;

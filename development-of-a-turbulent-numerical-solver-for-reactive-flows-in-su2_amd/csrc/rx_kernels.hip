@@ -588,52 +588,58 @@ __global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restri
                                                   DevMech m, ViscParams P, double* __restrict__ F,
                                                   double* __restrict__ Summ, int* err) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nG = NS + NDIM + 2;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
-  ViscNode<NS, NDIM> a, b;
-  a.V = V + (size_t)n0 * nPV;
-  b.V = V + (size_t)n1 * nPV;
-  a.G = G + (size_t)n0 * nG * NDIM;
-  b.G = G + (size_t)n1 * nG * NDIM;
-  a.Dij = Dij + (size_t)n0 * NS * NS;
-  b.Dij = Dij + (size_t)n1 * NS * NS;
-  a.S = P.implicit ? dTdU + (size_t)n0 * nVar : nullptr;
-  b.S = P.implicit ? dTdU + (size_t)n1 * nVar : nullptr;
-  a.coord = coord + (size_t)n0 * NDIM;
-  b.coord = coord + (size_t)n1 * NDIM;
-  a.mu = mu[n0];
-  b.mu = mu[n1];
-  a.kappa = kappa[n0];
-  b.kappa = kappa[n1];
-  double sk = 1.0;
-  if (P.rans) {
-    a.tke = tke[n0];
-    b.tke = tke[n1];
-    a.mut = mut[n0];
-    b.mut = mut[n1];
-    a.gk = gk + (size_t)n0 * NDIM;
-    b.gk = gk + (size_t)n1 * NDIM;
-    sk = sigk[n0];  // Set_Sigmak(node i), solver_direct_reactive.cpp:5345
-  } else {
-    a.tke = b.tke = a.mut = b.mut = 0.0;
-    a.gk = b.gk = nullptr;
-  }
-  double nrm[NDIM];
-#pragma unroll
-  for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
-  double res[nVar];
-  double* summ = P.implicit ? Summ + (size_t)e * visc_summary_size<NS, NDIM>() : nullptr;
+  constexpr int SS = visc_summary_size<NS, NDIM>();
   __shared__ double scr_all[64 * NS * NS];  // dense Stefan-Maxwell / QR matrices, one slice per lane
-  const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ, scr_all + threadIdx.x * NS * NS);
-  bool bad = false;
-#pragma unroll
-  for (int v = 0; v < nVar; ++v) {
-    bad |= isnan(res[v]);
-    F[(size_t)e * nVar + v] = res[v];
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < E) {
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    ViscNode<NS, NDIM> a, b;
+    a.V = V + (size_t)n0 * nPV;
+    b.V = V + (size_t)n1 * nPV;
+    a.G = G + (size_t)n0 * nG * NDIM;
+    b.G = G + (size_t)n1 * nG * NDIM;
+    a.Dij = Dij + (size_t)n0 * NS * NS;
+    b.Dij = Dij + (size_t)n1 * NS * NS;
+    a.S = P.implicit ? dTdU + (size_t)n0 * nVar : nullptr;
+    b.S = P.implicit ? dTdU + (size_t)n1 * nVar : nullptr;
+    a.coord = coord + (size_t)n0 * NDIM;
+    b.coord = coord + (size_t)n1 * NDIM;
+    a.mu = mu[n0];
+    b.mu = mu[n1];
+    a.kappa = kappa[n0];
+    b.kappa = kappa[n1];
+    double sk = 1.0;
+    if (P.rans) {
+      a.tke = tke[n0];
+      b.tke = tke[n1];
+      a.mut = mut[n0];
+      b.mut = mut[n1];
+      a.gk = gk + (size_t)n0 * NDIM;
+      b.gk = gk + (size_t)n1 * NDIM;
+      sk = sigk[n0];  // Set_Sigmak(node i), solver_direct_reactive.cpp:5345
+    } else {
+      a.tke = b.tke = a.mut = b.mut = 0.0;
+      a.gk = b.gk = nullptr;
+    }
+    double nrm[NDIM];
+  #pragma unroll
+    for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
+    double res[nVar];
+    // the summary in 64-edge tiles, edge index fastest ([E/64][SS][64]): each store of the wavefront is one
+    // contiguous 512-B run (per-edge [SS] rows touched 64 lines per store and amplified the kernel's HBM writes
+    // 1.25x, profiles/r02_pmc_c3.json); k_visc_jac stages its 16 edges' records from the tile through LDS
+    const SummRef summ{P.implicit ? Summ + (size_t)(e / kSummTile) * SS * kSummTile + e % kSummTile : nullptr,
+                       kSummTile};
+    const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ, scr_all + threadIdx.x * NS * NS);
+    bool bad = false;
+  #pragma unroll
+    for (int v = 0; v < nVar; ++v) {
+      bad |= isnan(res[v]);
+      F[(size_t)e * nVar + v] = res[v];
+    }
+    if (rc != ERR_NONE) set_err(err, rc == ERR_RANGE ? ERR_RANGE : ERR_NAN, e);
+    else if (bad) set_err(err, ERR_NAN, e);
   }
-  if (rc != ERR_NONE) set_err(err, rc == ERR_RANGE ? ERR_RANGE : ERR_NAN, e);
-  else if (bad) set_err(err, ERR_NAN, e);
 }
 
 // a6: viscous Jacobians from the per-edge summary; a team of 16 lanes per edge, lane b = column b,
@@ -647,7 +653,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
                                                      DevMech m, ViscParams P, double* __restrict__ Jac,
                                                      const double* __restrict__ Jc,
                                                      const int64_t* __restrict__ edge_blk, double* __restrict__ A) {
-  constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar;
+  constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>(), kEB = kBlock / 16;
+  static_assert(kSummTile % kEB == 0, "a workgroup's edges lie in one summary tile");
+  // the workgroup's kEB consecutive edge records, staged from their tile: each load is kEB consecutive doubles
+  __shared__ double ssm[SS * kEB];
+  const int eb = blockIdx.x * kEB;
+  {
+    const double* tile = Summ + (size_t)(eb / kSummTile) * SS * kSummTile + eb % kSummTile;
+    for (int q = threadIdx.x; q < SS * kEB; q += kBlock) {
+      const int k = q / kEB, el = q - k * kEB;
+      if (eb + el < E) ssm[q] = tile[(size_t)k * kSummTile + el];
+    }
+  }
+  __syncthreads();
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / 16, b = gt % 16;
   if (e >= E) return;  // whole teams exit together (E * 16 threads)
@@ -655,7 +673,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   const int bc = b < nVar ? b : 0;
   const double sib = dTdU[(size_t)n0 * nVar + bc], sjb = dTdU[(size_t)n1 * nVar + bc];
   double* Ji = Jac + (size_t)e * 2 * nVar2;
-  const double* sm = Summ + (size_t)e * visc_summary_size<NS, NDIM>();
+  const SummCRef sm{ssm + (e - eb), kEB};
   if (Jc) {
     // this lane's column of both convective blocks, loaded before the Jacobian arithmetic hides their latency
     const double* Jci = Jc + (size_t)e * 2 * nVar2;

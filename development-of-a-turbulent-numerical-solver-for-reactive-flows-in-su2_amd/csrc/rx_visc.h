@@ -280,6 +280,22 @@ struct VSL {
 template <int NS, int NDIM>
 constexpr int visc_summary_size() { return VSL<NDIM>::ARR + 9 * NS; }
 
+// A summary record seen through its layout: entry q at p[q * s]. Interior edges: kSummTile-edge tiles with the
+// edge index fastest ([E/kSummTile][size][kSummTile], s = kSummTile, written by k_visc_edge) and the LDS copy
+// of a k_visc_jac workgroup's edges (s = edges per workgroup); boundary vertices: [size] rows (s = 1).
+struct SummRef {
+  double* p;
+  int s;
+  __device__ double& operator[](int q) const { return p[(size_t)q * s]; }
+  __device__ SummRef operator+(int q) const { return SummRef{p + (size_t)q * s, s}; }
+};
+struct SummCRef {
+  const double* p;
+  int s;
+  __device__ double operator[](int q) const { return p[(size_t)q * s]; }
+  __device__ SummCRef operator+(int q) const { return SummCRef{p + (size_t)q * s, s}; }
+};
+
 // Per-edge inputs gathered from the two node records.
 template <int NS, int NDIM>
 struct ViscNode {
@@ -291,7 +307,7 @@ struct ViscNode {
 template <int NS, int NDIM>
 __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const ViscNode<NS, NDIM>& ni,
                                 const ViscNode<NS, NDIM>& nj, double sigma_k, const double* Normal, double* res,
-                                double* summ, double* scr, bool corrected = true) {
+                                SummRef summ, double* scr, bool corrected = true) {
   // corrected = false: CAvgGradReactive_Boundary::ComputeResidual (numerics_direct_reactive.cpp:478-648, a8):
   // the plain mean gradient — no edge correction, no coincident-point check.
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
@@ -567,7 +583,7 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     qaux[s] = aux;
   }
   using L = VSL<NDIM>;
-  double* o = summ;
+  const SummRef o = summ;
   o[L::MU] = Mean_mu;
   o[L::K] = Mean_k;
   o[L::MUT] = Mean_mut;
@@ -614,7 +630,7 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
 // change the sign of an exact zero). base_i/base_j: the column-independent part of row a of dJ/drho
 // (this lane's a = lane index in the team), shared through shuffles.
 template <int NS, int NDIM>
-__device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, const double* __restrict__ sm,
+__device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, const SummCRef sm,
                                        double Sib, double Sjb, int b, int tl, double* __restrict__ Ji,
                                        double* __restrict__ Jj, const double* jci = nullptr,
                                        const double* jcj = nullptr, double* __restrict__ Aij = nullptr,
@@ -627,15 +643,15 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
   const double theta = sm[L::THETA], dij = sm[L::DIJ], dS = sm[L::DS], sq = sm[L::DIJ], Area = sm[L::DS];
   const double totMass = sm[L::TM], totMass_i = sm[L::TMI], totMass_j = sm[L::TMJ];
   const double sigma_i = sm[L::SGI], sigma_j = sm[L::SGJ];
-  const double* Xs_i = sm + L::ARR;
-  const double* Xs_j = Xs_i + NS;
-  const double* Ys = Xs_j + NS;
-  const double* hs = Ys + NS;
-  const double* Cps = hs + NS;
-  const double* Jd = Cps + NS;
-  const double* Gxn = Jd + NS;
-  const double* Ds = Gxn + NS;
-  const double* qaux = Ds + NS;
+  const SummCRef Xs_i = sm + L::ARR;
+  const SummCRef Xs_j = Xs_i + NS;
+  const SummCRef Ys = Xs_j + NS;
+  const SummCRef hs = Ys + NS;
+  const SummCRef Cps = hs + NS;
+  const SummCRef Jd = Cps + NS;
+  const SummCRef Gxn = Jd + NS;
+  const SummCRef Ds = Gxn + NS;
+  const SummCRef qaux = Ds + NS;
   const double PrT = P.Pr_t, LeT = P.Le_t;
   // ---- column-independent part of dJ/drho rows (lane tl < NS owns row a = tl)
   double bj = 0.0, bi = 0.0;
