@@ -10,8 +10,9 @@
  *                      SetBoundControlVolume (:9595-9660), FindNormal_Neighbor (:12610-12652); and
  *                      ComputeWall_Distance (nearest vertex of the HEAT_FLUX / ISOTHERMAL markers).
  *                      Serial reader (one rank); elements: triangle, quadrilateral (2-D), tetrahedron,
- *                      hexahedron (3-D); boundary: line (2-D), triangle, quadrilateral (3-D). Elements must be
- *                      consistently oriented (the reference's Check_*_Orientation flips are not restated).
+ *                      hexahedron (3-D); boundary: line (2-D), triangle, quadrilateral (3-D). Inverted elements
+ *                      are flipped as Check_IntElem_Orientation / Check_BoundElem_Orientation do
+ *                      (geometry_structure.cpp:8640-8960), after the connectivity, as the reference orders it.
  *   rx_mech_read       ReactingModelLibrary::Setup (Common/src/Framework/reacting_model_library.cpp:925-1506):
  *                      file list, mixture, chemistry (Parse_Terms Common/src/Tools/utility.cpp:12-86, CGS->SI
  *                      :1122-1132, Ta/R_cal :1209-1210, reversible product exponents :1113-1120, backward-rate
