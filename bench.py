@@ -63,7 +63,32 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFS = 78.6       # MI355X FP64 vector spec
 
 
-def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
+def pmc_fp64_flop(kernel, workload_key):
+    """FP64 FLOP per launch of `kernel` counted by rocprofv3 (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64,
+    tools/pmc_fp64.py -> profiles/r*_fp64*.json; the newest file on this workload wins); else None."""
+    import glob
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fp64*.json")), reverse=True):
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload_key and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["fp64_flop"]
+    return None
+
+
+def ilu_apply_kernels(N, nnzb, nVar, parts):
+    """The ILU(0) apply kernels rx_la_ilu_apply launches for this partitioning (rx_sweeps.hip): the LDS-resident
+    sweep when a partition's vector, metadata and columns fit the 160 KiB LDS, else the wide global sweeps."""
+    rows = -(-N // parts)
+    shm = 8 * (rows * nVar + (256 // nVar) * nVar + 1) + 4 * (8 * rows + rows * nnzb // max(N, 1))
+    if shm <= 160 * 1024:
+        return f"k_ilu_apply_lds<{nVar}>"
+    return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
+
+
+def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None):
     """Algorithmic bytes (or flops) per launch of the single-launch kernels timed per phase
     (each unique datum once per sweep)."""
     nVar, nPV, nG = ns + nDim + 2, ns + nDim + 5, ns + nDim + 2
@@ -72,24 +97,31 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter):
     summ = (14 + 5 * nDim + 9 * ns) * d  # visc_summary_size<NS, NDIM>
     hbm = lambda b, name: dict(bound="hbm", work=float(b), unit="GB/s", peak=HBM_PEAK_GBS, kernel=name)
     te, tv = f"<{ns}, {nDim}>", f"<{nVar}>"  # template arguments of the flow kernels (rocprof / PMC names)
+    # k_visc_edge's FP64 work: counted by PMC on this workload when a count is committed, else SURVEY §8(d)'s
+    # ~9 kflop per edge (the C3 count is 13.9 kflop per edge, profiles/r02_c3_v2_fp64.json)
+    visc_flop = pmc_fp64_flop("k_visc_edge" + te, workload_key) or 9000.0 * E
     return {
         # k_ausm_edge: V (nPV) and dPdU (nVar) per node once; edge (2 int32 + normal); flux + 2 Jacobians
         "CONV": hbm(N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk), "k_ausm_edge" + te),
-        # k_visc_edge: FP64-compute bound, SURVEY §8(d): ~8-10 kflop per edge for flux + closures
-        "VISC": dict(bound="fp64", work=9000.0 * E, unit="TFLOP/s", peak=FP64_PEAK_TFS, kernel="k_visc_edge" + te),
-        # k_visc_jac: per-edge summary + dT/dU in, two Jacobian blocks out
-        "VISC_JAC": hbm(E * summ + N * nVar * d + E * 2 * blk, "k_visc_jac" + te),
-        # k_assemble: 4 scratch blocks per edge + source block per node in; BSR + residual out
-        "ASSEMBLE": hbm((4 * E + N + nnzb) * blk + (2 * E + 2 * N) * nVar * d, "k_assemble" + tv),
+        "VISC": dict(bound="fp64", work=float(visc_flop), unit="TFLOP/s", peak=FP64_PEAK_TFS,
+                     kernel="k_visc_edge" + te),
+        # k_visc_jac (fused assembly): per-edge summary + dT/dU + the edge's two convective blocks in; two viscous
+        # blocks (for the diagonals) and the two off-diagonal BSR blocks out
+        "VISC_JAC": hbm(E * summ + N * nVar * d + E * 16 + E * 6 * blk, "k_visc_jac" + te),
+        # k_assemble: each node's own-side conv + visc blocks (2 per edge each), the edge fluxes, the source
+        # Jacobian's species rows and residual in; diagonal blocks + residual out
+        "ASSEMBLE": hbm(4 * E * blk + 2 * E * nVar * d + N * (ns * nVar + nVar) * d + N * (blk + nVar * d),
+                        "k_assemble" + tv),
         "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq" + te),
-        "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar * d + blk), "k_source" + te),
+        # k_source: V, dT/dU, volume, omega in; residual + the Jacobian's species rows out
+        "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar + ns * nVar) * d, "k_source" + te),
         # k_ilu_build_part: A in, factor + inv(D) out
         "ILU_BUILD": hbm((2 * nnzb + N) * blk, "k_ilu_build_part" + tv),
         # SOLVE phase (inside the FGMRES graph; timed one launch at a time after the timed region):
         # y = A x: every block + its column index once, x gathered, y written
         "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d, "k_spmv" + tv),
         # ILU(0) apply: L and U blocks + inv(D_i) (= nnzb blocks) + column indices, b in, x out
-        "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, f"k_ilu_fwd_part{tv}+k_ilu_bwd_part{tv}"),
+        "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, ilu_apply_kernels(N, nnzb, nVar, parts)),
     }
 
 
@@ -335,10 +367,10 @@ def main():
     s.profile(False)
     t.profile(False)
 
-    models = kernel_models(N, E, nnzb, ns, nDim, 5)
-    phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0 and k not in ("SPMV", "ILU_APPLY")}
     dims = f"{nx}x{ny}" + (f"x{nz}" if nz > 1 else "")
     wkey = f"{args.workload} {dims} ns{ns} parts{args.parts}"
+    models = kernel_models(N, E, nnzb, ns, nDim, 5, parts=args.parts, workload_key=wkey)
+    phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0 and k not in ("SPMV", "ILU_APPLY")}
 
     def roof(k):
         ms, n = prof[k]

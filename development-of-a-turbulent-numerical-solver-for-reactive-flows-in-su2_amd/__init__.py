@@ -117,9 +117,11 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RxError(f"librx.so not built ({LIB_PATH}); run __graft_entry__.build()")
-        _lib = C.CDLL(LIB_PATH)
+        # RX_LIB: an in-tree build variant of librx.so for same-box A/B measurements (tools/gpu_ab.sh)
+        path = os.environ.get("RX_LIB", LIB_PATH)
+        if not os.path.exists(path):
+            raise RxError(f"librx.so not built ({path}); run __graft_entry__.build()")
+        _lib = C.CDLL(path)
         _lib.rx_status_string.restype = C.c_char_p
         _lib.rx_last_error_index.restype = C.c_int64
         _lib.rx_ctx_create.argtypes = [C.POINTER(MeshDesc), C.POINTER(MechDesc), C.POINTER(Cfg), C.c_int,

@@ -4,7 +4,7 @@ per dispatch counted as 64 lanes x (ADD + MUL + 2 FMA + TRANS) (an upper bound: 
 waves count too). Durations are the dispatches' own start/end stamps in the same pass. Peak: 78.6 TFLOP/s FP64
 vector (MI355X spec).
 
-usage: python tools/pmc_fp64.py <pmc_dir> > profiles/<name>.json
+usage: python tools/pmc_fp64.py <pmc_dir> "<bench workload key>" > profiles/<name>_fp64.json
 """
 import csv
 import glob
@@ -19,6 +19,7 @@ PEAK = 78.6e12
 
 def main():
     d = sys.argv[1]
+    workload = sys.argv[2] if len(sys.argv) > 2 else None
     acc = defaultdict(lambda: defaultdict(float))
     cnt = defaultdict(lambda: defaultdict(int))
     dur = defaultdict(dict)
@@ -32,7 +33,7 @@ def main():
                 acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 cnt[k][r["Counter_Name"]] += 1
                 dur[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    out = {"peak_fp64_tflops": PEAK / 1e12, "kernels": {}}
+    out = {"workload": workload, "peak_fp64_tflops": PEAK / 1e12, "kernels": {}}
     for k in acc:
         c = {q: acc[k][q] / max(1, cnt[k][q]) for q in acc[k]}
         add, mul, fma, trans = (c.get("SQ_INSTS_VALU_%s_F64" % x, 0.0) for x in ("ADD", "MUL", "FMA", "TRANS"))
