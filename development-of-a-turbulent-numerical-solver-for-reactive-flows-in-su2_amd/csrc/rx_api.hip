@@ -374,9 +374,10 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       CK(dupload(ctx, &ctx->ilu_plan, plan.data(), plan.size()));
     }
 
-    const size_t per_wave = sizeof(double) * ((size_t)(rowmax + 7) * nv * nv + 16);
+    const size_t per_wave = sizeof(double) * ((size_t)(rowmax + 1 + rx_ilu_stage()) * nv * nv + 16);
     if (per_wave > (size_t)ctx->lds_max) CK(RX_ERR_ARG);  // a row with more blocks than one wave's LDS slice
-    ctx->ilu_waves = (int)std::max<size_t>(1, std::min<size_t>({12, (size_t)std::max(1, ctx->fs.maxwidth),
+    ctx->ilu_waves = (int)std::max<size_t>(1, std::min<size_t>({(size_t)rx_ilu_max_waves(),
+                                                                (size_t)std::max(1, ctx->fs.maxwidth),
                                                                 (size_t)ctx->lds_max / per_wave}));
   }
   // halo exchange plan (distributed mesh)

@@ -236,6 +236,8 @@ int rx_la_ilu_build(rx_ctx* ctx);
 int rx_la_prepare(rx_ctx* ctx);
 int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv);
 double* rx_invd_buf(rx_ctx* ctx);
+int rx_ilu_stage();      // staged blocks per wave of the ILU(0) build (rx_sweeps.hip kStage)
+int rx_ilu_max_waves();  // wavefronts per workgroup cap of the ILU(0) build
 int rx_la_krylov_alloc(rx_ctx* ctx, int m);
 // Drop the captured solve graph (its kernel arguments point at buffers about to be replaced).
 void rx_graph_reset(rx_ctx* ctx);

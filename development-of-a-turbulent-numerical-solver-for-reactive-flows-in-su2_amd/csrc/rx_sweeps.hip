@@ -189,7 +189,10 @@ __global__ __launch_bounds__(256) void k_diag_factor(int N, const int64_t* __res
 // inv(A_jj) and every A_jk it reads from finished rows; the products run from LDS; inv(D_i) is the
 // right-looking Gauss elimination with pivot rows broadcast through LDS.
 // LDS per wave: row blocks [rowmax][NV2] + W + staging [kStage][NV2] + plan[32].
-constexpr int kStage = 6;
+#ifndef RX_ILU_STAGE
+#define RX_ILU_STAGE 6
+#endif
+constexpr int kStage = RX_ILU_STAGE;
 constexpr int kPlan = 32;
 constexpr int kPrefA = 10;  // doubles per lane of the next row's A blocks held in registers
 
@@ -245,8 +248,11 @@ __device__ __forceinline__ void wave_inverse_lds(const double* D, double* L, dou
   wave_sync();
 }
 
+#ifndef RX_ILU_LB
+#define RX_ILU_LB 768  // 12 wavefronts (rx_ilu_max_waves)
+#endif
 template <int NV>
-__global__ __launch_bounds__(768) void k_ilu_build_part(const int32_t* __restrict__ part_lvl,
+__global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __restrict__ part_lvl,
                                                          const int32_t* __restrict__ lvl_ptr,
                                                          const int32_t* __restrict__ plan,
                                                          const int32_t* __restrict__ col,
@@ -1244,6 +1250,11 @@ __global__ __launch_bounds__(256) void k_lusgs_bwd_part(const int32_t* __restric
 }  // namespace
 
 double* rx_invd_buf(rx_ctx* ctx) { return ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)ctx->nVar * ctx->nVar; }
+#ifndef RX_ILU_MAX_WAVES
+#define RX_ILU_MAX_WAVES 12
+#endif
+int rx_ilu_stage() { return kStage; }
+int rx_ilu_max_waves() { return RX_ILU_MAX_WAVES; }
 
 // Raise the dynamic-LDS limit of the LDS-resident kernels to what the device allows (once).
 int rx_la_prepare(rx_ctx* ctx) {
@@ -1318,6 +1329,18 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
     RX_NV_SWITCH(nv, (k_ilu_fwd_wide<NV_, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
                          ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->col, ctx->f[RX_F_ILU], b, x, done, conv)));
     RX_NV_SWITCH(nv, (k_ilu_bwd_wide<NV_, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
+                         ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx), x,
+                         done, conv)));
+    RX_HIP(hipGetLastError());
+    return rx_la_exchange(ctx, x, nv);
+  }
+  static const bool narrow_small = getenv("RX_NARROW_SMALL") != nullptr;  // diagnosis: the part sweeps below
+  if (!narrow && !narrow_small) {  // levels narrower than 256 / NV rows: the same wide sweeps on 256 threads
+    const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
+    const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
+    RX_NV_SWITCH(nv, (k_ilu_fwd_wide<NV_, 256><<<ctx->npart, 256, 0, ctx->stream>>>(
+                         ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->col, ctx->f[RX_F_ILU], b, x, done, conv)));
+    RX_NV_SWITCH(nv, (k_ilu_bwd_wide<NV_, 256><<<ctx->npart, 256, 0, ctx->stream>>>(
                          ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx), x,
                          done, conv)));
     RX_HIP(hipGetLastError());
