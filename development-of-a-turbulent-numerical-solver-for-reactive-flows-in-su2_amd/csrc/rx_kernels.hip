@@ -577,8 +577,13 @@ __global__ __launch_bounds__(kAusmBlock) void k_ausm_edge(int E, const int32_t* 
 }
 
 // a3-a6: viscous flux (+ Jacobians) per edge into scratch.
+#ifdef RX_VISC_WPE  // build knob (tools/build_variant.sh): waves per SIMD the viscous edge kernel is compiled for
+#define RX_VISC_ATTR __attribute__((amdgpu_waves_per_eu(RX_VISC_WPE)))
+#else
+#define RX_VISC_ATTR
+#endif
 template <int NS, int NDIM>
-__global__ __launch_bounds__(64) void k_visc_edge(int E, const int32_t* __restrict__ edges,
+__global__ __launch_bounds__(64) RX_VISC_ATTR void k_visc_edge(int E, const int32_t* __restrict__ edges,
                                                   const double* __restrict__ normal, const double* __restrict__ coord,
                                                   const double* __restrict__ V, const double* __restrict__ G,
                                                   const double* __restrict__ mu, const double* __restrict__ kappa,

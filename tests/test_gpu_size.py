@@ -7,6 +7,8 @@ thread-count independent) run in the device's inner-product order on the same re
   c2  configs[1]: 2-D jet 500 x 200 = 100 000 points, 7 species, 256 partitions
   c3  configs[2]: 2-D jet 2000 x 500 = 1 000 000 points, 7 species, 256 partitions (the north-star roofline run)
   c5  configs[4], one GPU's share: 3-D jet 1000 x 50 x 20 = 1 000 000 points, 7 species, nVar 12, 256 partitions
+  c3p1024  c3 on 1024 partitions (~980 rows each): the LDS-resident ILU(0) apply (k_ilu_apply_lds) and its ILU build
+           at the size where round 1's partition sweep diverged on the old bench state
 
 Bar: U, (k, omega) within 1e-10 of each column's max (the FGMRES-amplified rounding of the Stefan-Maxwell solve, as in
 test_gpu_bc.test_synthetic_jet_iteration_vs_oracle), both RMS vectors within 1e-10 relative, identical linear-solver
@@ -23,13 +25,13 @@ from tests.rxpkg import rx, synth
 
 pytestmark = pytest.mark.gpu
 
-CASES = {"c2": (500, 200, 0), "c3": (2000, 500, 0), "c5": (1000, 50, 20)}
+CASES = {"c2": (500, 200, 0, 256), "c3": (2000, 500, 0, 256), "c5": (1000, 50, 20, 256), "c3p1024": (2000, 500, 0, 1024)}
 
 
-@pytest.mark.parametrize("case", ["c2", "c3", "c5"])
+@pytest.mark.parametrize("case", ["c2", "c3", "c5", "c3p1024"])
 def test_full_size_iteration_vs_oracle(case):
-    nx, ny, nz = CASES[case]
-    ns, parts = 7, 256
+    nx, ny, nz, parts = CASES[case]
+    ns = 7
     mesh, st0, mech, kw = synth.jet_field_case(nx, ny, n_species=ns, n_part=parts, nz=nz)
     cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
     bc = synth.jet_bc(mesh, ns)
