@@ -124,7 +124,11 @@ int main(int argc, char** argv) {
       cfg.relaxation = ci[10];
       cfg.t_min = ci[11];
       cfg.t_max = ci[12];
-      cfg.implicit = 1;
+      // cfg_scheme (optional): [flow implicit, SST lin_prec]; cfg_rk (optional): RK_ALPHA_COEFF
+      std::vector<double> scheme{1.0, 1.0}, rk;
+      if (std::ifstream(d + "/cfg_scheme.f64").good()) scheme = f64(d, "cfg_scheme");
+      if (std::ifstream(d + "/cfg_rk.f64").good()) rk = f64(d, "cfg_rk");
+      cfg.implicit = (int32_t)scheme[0];
       rx::ReactiveNSSolver flow(mesh, mech, cfg, 0);
       auto pn = i64(d, "bvertex_pn");
       auto kind = i32(d, "bc_kind");
@@ -140,6 +144,8 @@ int main(int argc, char** argv) {
       bc.omega_inf = bsc[3];
       flow.SetBoundaryConditions(bc);
       rx_cfg tcfg = cfg;
+      tcfg.implicit = 1;
+      tcfg.lin_prec = (int32_t)scheme[1];
       tcfg.relaxation = ci[13];
       tcfg.cfl = ci[14];
       rx::TurbSSTSolver turb(mesh, flow, tcfg);
@@ -165,7 +171,7 @@ int main(int argc, char** argv) {
       turb.Upload(RX_F_F2, f64(d, "it_F2_0"));
       turb.Upload(RX_F_CDKW, f64(d, "it_CDkw0"));
       std::vector<double> trms;
-      auto rms = rx::Iterate(flow, turb, 0, &trms);
+      auto rms = rx::Iterate(flow, turb, 0, &trms, rk);
       flow.Synchronize();
       save(d, "out_u", flow.Download(RX_F_U));
       save(d, "out_sst_u", turb.Download(RX_F_U));

@@ -81,10 +81,12 @@ def test_cpp_driver_matches_reference(tmp_path, implicit):
 
 
 @pytest.mark.gpu
-def test_cpp_driver_reference_iteration(tmp_path):
+@pytest.mark.parametrize("case", ["it9", "itx9", "itx4"])
+def test_cpp_driver_reference_iteration(tmp_path, case):
     """rx::Iterate (the reference's outer iteration with the jet's boundary conditions) from the C++ mirror, against
-    the reference's own iteration (golden it9)."""
-    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "it9.npz")))
+    the reference's own iteration: it9 (implicit, ILU0), itx9 (the shipped cfg: EULER_EXPLICIT flow, LU_SGS SST, the
+    whole reference mesh), itx4 (C1: 4 species, RUNGE-KUTTA_EXPLICIT, 3 stages)."""
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", case + ".npz")))
     d = str(tmp_path)
 
     def w(name, arr, dt):
@@ -106,6 +108,10 @@ def test_cpp_driver_reference_iteration(tmp_path):
     w("cfg_it", [g["mach_inf"][0], g["visc_params"][0], g["visc_params"][1], g["visc_params"][2], g["src_params"][0],
                  g["src_params"][1], g["dt_params"][0], g["dt_params"][1], bp[19], bp[20], bp[22], p2v[1], p2v[2],
                  bp[23], bp[24]], np.float64)
+    flow_imp = str(g.get("time_flow", "EULER_IMPLICIT")) == "EULER_IMPLICIT"
+    w("cfg_scheme", [1.0 if flow_imp else 0.0, 0.0 if str(g.get("lin_prec", "ILU")) == "LU_SGS" else 1.0], np.float64)
+    if "rk_alpha" in g:
+        w("cfg_rk", g["rk_alpha"], np.float64)
     bc = rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"])
     w("bc_kind", bc["kind"], np.int32)
     w("bc_data", bc["data"], np.float64)

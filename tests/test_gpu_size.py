@@ -9,6 +9,8 @@ thread-count independent) run in the device's inner-product order on the same re
   c5  configs[4], one GPU's share: 3-D jet 1000 x 50 x 20 = 1 000 000 points, 7 species, nVar 12, 256 partitions
   c3p1024  c3 on 1024 partitions (~980 rows each): the LDS-resident ILU(0) apply (k_ilu_apply_lds) and its ILU build
            at the size where round 1's partition sweep diverged on the old bench state
+  c3rk     c3 with C1's time integration (golden itx4): RUNGE-KUTTA_EXPLICIT flow (3 stages, RK_ALPHA_COEFF
+           0.66667 0.66667 1.0, CFL 0.5) and the LU_SGS SST solve of the shipped cfgs
 
 Bar: U, (k, omega) within 1e-10 of each column's max (the FGMRES-amplified rounding of the Stefan-Maxwell solve, as in
 test_gpu_bc.test_synthetic_jet_iteration_vs_oracle), both RMS vectors within 1e-10 relative, identical linear-solver
@@ -25,19 +27,23 @@ from tests.rxpkg import rx, synth
 
 pytestmark = pytest.mark.gpu
 
-CASES = {"c2": (500, 200, 0, 256), "c3": (2000, 500, 0, 256), "c5": (1000, 50, 20, 256), "c3p1024": (2000, 500, 0, 1024)}
+RK3 = [0.66667, 0.66667, 1.0]
+CASES = {"c2": (500, 200, 0, 256, None), "c3": (2000, 500, 0, 256, None), "c5": (1000, 50, 20, 256, None),
+         "c3p1024": (2000, 500, 0, 1024, None), "c3rk": (2000, 500, 0, 256, RK3)}
 
 
-@pytest.mark.parametrize("case", ["c2", "c3", "c5", "c3p1024"])
+@pytest.mark.parametrize("case", ["c2", "c3", "c5", "c3p1024", "c3rk"])
 def test_full_size_iteration_vs_oracle(case):
-    nx, ny, nz, parts = CASES[case]
+    nx, ny, nz, parts, rk = CASES[case]
     ns = 7
     mesh, st0, mech, kw = synth.jet_field_case(nx, ny, n_species=ns, n_part=parts, nz=nz)
-    cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
+    if rk:
+        kw = dict(kw, cfl=0.5)
+    cfg = rx.default_cfg(implicit=0 if rk else 1, lin_prec=1, **kw)
     bc = synth.jet_bc(mesh, ns)
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
     s.set_bc(bc)
-    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(lin_prec=0 if rk else 1))
     st = synth.device_preprocess(s, t, mesh, st0)
     N = len(st["V"])
     mesh_o, state, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
@@ -45,15 +51,17 @@ def test_full_size_iteration_vs_oracle(case):
     # CTurbSSTVariable::Get_Sigmak (constants[0])
     s.upload("GRADK", np.ascontiguousarray(state["TG"][:, 0, :]))
     s.upload("SIGMAK", np.full(N, 0.85))
-    rms, rms_t, its = rx.Iterate(s, t, ext_iter=0)
+    rms, rms_t, its = rx.Iterate(s, t, ext_iter=0, rk_alpha=rk)
     s.sync()
     U, T = s.download("U").reshape(N, -1), t.download("U").reshape(N, 2)
     s.close()
+    if rk:
+        c.update(time="rk", rk_alpha=rk, sst_prec="lusgs")
     pat = O.bsr_pattern(N, mesh["edges"])
     with O.dot_order("device"):
         o = O.outer_iteration(O.Mechanism(mech), 3 if nz else 2, mesh_o, state, bco, c, 0, pat,
                               part_ptr=mesh["part_ptr"], keep=False)
-    assert its == (o["lin_iters"], o["sst_lin_iters"])
+    assert its[1] == o["sst_lin_iters"] and (rk or its[0] == o["lin_iters"])
     nd = 3 if nz else 2
     cols = [v for v in range(U.shape[1]) if not 1 <= v <= nd]
     per_column_close(U[:, cols], o["U"][:, cols], rtol=1e-10, floor=1.0, what=f"{case} U vs oracle")
