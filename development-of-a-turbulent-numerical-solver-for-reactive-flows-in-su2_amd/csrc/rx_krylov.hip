@@ -113,16 +113,42 @@ __device__ inline void grid_reduce(const double (&v)[NR], double* __restrict__ p
 
 // Row-block product of y = A x for element q = (row i, component a): the reference's
 // MatrixVectorProduct order (blocks of the row in column order, columns c ascending).
+// Small blocks (the SST's 2x2) are taken kSpmvChunk at a time: the chunk's column indices, then all of its
+// matrix-row and x loads, are issued before the first product (loads from clamped, always valid addresses; the
+// sums of the blocks past the row's end are skipped). Measured on one box at C3: the SST solve 2.14 -> 2.05 ms;
+// for the 11x11 flow blocks chunks of 3 / 5 made the solve slower (15.40 -> 16.14 / 15.70 ms), so those keep
+// one block at a time.
+template <int NV>
+constexpr int rx_spmv_chunk() {
+  return NV <= 4 ? 5 : 1;
+}
 template <int NV>
 __device__ inline double spmv_elem(int64_t q, const int32_t* __restrict__ rp, const int32_t* __restrict__ col,
                                    const double* __restrict__ A, const double* __restrict__ x) {
+  constexpr int kSpmvChunk = rx_spmv_chunk<NV>();
   const int i = (int)(q / NV), a = (int)(q - (int64_t)i * NV);
+  const int k0 = rp[i], k1 = rp[i + 1];
   double acc = 0.0;
-  for (int k = rp[i]; k < rp[i + 1]; ++k) {
-    const double* blk = A + (size_t)k * NV * NV + a * NV;
-    const double* xv = x + (size_t)col[k] * NV;
+  for (int k = k0; k < k1; k += kSpmvChunk) {
+    int cc[kSpmvChunk];
 #pragma unroll
-    for (int c = 0; c < NV; ++c) acc += blk[c] * xv[c];
+    for (int t = 0; t < kSpmvChunk; ++t) cc[t] = col[k + t < k1 ? k + t : k];
+    double av[kSpmvChunk][NV], xv[kSpmvChunk][NV];
+#pragma unroll
+    for (int t = 0; t < kSpmvChunk; ++t) {
+      const double* blk = A + (size_t)(k + t < k1 ? k + t : k) * NV * NV + a * NV;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        av[t][c] = blk[c];
+        xv[t][c] = x[(size_t)cc[t] * NV + c];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < kSpmvChunk; ++t)
+      if (k + t < k1) {
+#pragma unroll
+        for (int c = 0; c < NV; ++c) acc += av[t][c] * xv[t][c];
+      }
   }
   return acc;
 }
