@@ -856,6 +856,38 @@ __global__ __launch_bounds__(256) void k_ilu_bwd_part(const int32_t* __restrict_
   }
 }
 
+// Row a of the blocks k0..k1-1 of one row times their x segments: f(s_k) with s_k = sum_c F_k[a][c] x_col(k)[c]
+// (from 0.0, c ascending), k ascending. Small blocks (NV <= 4, the SST's 2x2) are taken four at a time with every
+// load of the chunk issued before the first product (clamped, always valid addresses; the blocks past the row's
+// end are skipped), as in the SpMV.
+template <int NV, typename Fn>
+__device__ __forceinline__ void row_blocks(const double* __restrict__ F, const int32_t* __restrict__ col,
+                                           const double* x, int k0, int k1, int a, Fn f) {
+  constexpr int NV2 = NV * NV, CH = NV <= 4 ? 4 : 1;
+  for (int k = k0; k < k1; k += CH) {
+    double av[CH][NV], xv[CH][NV];
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      const int kk = k + t < k1 ? k + t : k;
+      const double* blk = F + (size_t)kk * NV2 + a * NV;
+      const double* xj = x + (size_t)col[kk] * NV;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        av[t][c] = blk[c];
+        xv[t][c] = xj[c];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < CH; ++t)
+      if (k + t < k1) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) s += av[t][c] * xv[t][c];
+        f(s);
+      }
+  }
+}
+
 // Wide variants of the two sweeps for partitions whose vector does not fit in LDS: TB threads per
 // workgroup (TB / NV rows in flight, so a level of the C3 jet's 62-row-wide partitions is one pass instead
 // of three), row metadata from the schedule's slot records {i, klo, diag, khi} (one load instead of
@@ -885,14 +917,7 @@ __global__ __launch_bounds__(TB) void k_ilu_fwd_wide(const int32_t* __restrict__
       const int4 sl = (r == r0 + rl) ? cur : slot[r];
       const int i = sl.x;
       double xi = b[(size_t)i * NV + a];
-      for (int k = sl.y; k < sl.z; ++k) {
-        const double* blk = F + (size_t)k * NV2 + a * NV;
-        const double* xj = x + (size_t)col[k] * NV;
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
-        xi -= s;
-      }
+      row_blocks<NV>(F, col, x, sl.y, sl.z, a, [&](double s) { xi -= s; });
       x[(size_t)i * NV + a] = xi;
     }
     __syncthreads();
@@ -928,14 +953,7 @@ __global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__
         const int4 sl = (base == r0) ? cur : slot[r];
         i = sl.x;
         double sum = 0.0;
-        for (int k = sl.z + 1; k < sl.w; ++k) {
-          const double* blk = F + (size_t)k * NV2 + a * NV;
-          const double* xj = x + (size_t)col[k] * NV;
-          double s = 0.0;
-#pragma unroll
-          for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
-          sum += s;
-        }
+        row_blocks<NV>(F, col, x, sl.z + 1, sl.w, a, [&](double s) { sum += s; });
         v[rl * NV + a] = x[(size_t)i * NV + a] - sum;
       }
       __syncthreads();
