@@ -863,7 +863,10 @@ __global__ __launch_bounds__(256) void k_ilu_bwd_part(const int32_t* __restrict_
 template <int NV, typename Fn>
 __device__ __forceinline__ void row_blocks(const double* __restrict__ F, const int32_t* __restrict__ col,
                                            const double* x, int k0, int k1, int a, Fn f) {
-  constexpr int NV2 = NV * NV, CH = NV <= 4 ? 4 : 1;
+#ifndef RX_ROWCH_BIG
+#define RX_ROWCH_BIG 1
+#endif
+  constexpr int NV2 = NV * NV, CH = NV <= 4 ? 4 : RX_ROWCH_BIG;
   for (int k = k0; k < k1; k += CH) {
     double av[CH][NV], xv[CH][NV];
 #pragma unroll
