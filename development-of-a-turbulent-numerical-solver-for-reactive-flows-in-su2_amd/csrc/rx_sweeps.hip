@@ -153,6 +153,25 @@ __device__ __forceinline__ void wave_solve_rows(const double (&row)[NV], double 
   }
 }
 
+// The same solve with the factorisation in LDS (row-major LU[r][k], written by the lanes of wave_factor_rows):
+// every lane reads the entries at one address (LDS broadcast), and those reads do not depend on the solve, so
+// they are issued ahead instead of two readlanes per entry.
+template <int NV>
+__device__ __forceinline__ void wave_solve_lds(const double* LU, double (&rhs)[NV]) {
+#pragma unroll
+  for (int ii = 1; ii < NV; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < ii; ++jj) rhs[ii] -= LU[ii * NV + jj] * rhs[jj];
+  rhs[NV - 1] = rhs[NV - 1] / LU[NV * NV - 1];
+#pragma unroll
+  for (int ii = NV - 2; ii >= 0; --ii) {
+    double aux = 0.0;
+#pragma unroll
+    for (int jj = ii + 1; jj < NV; ++jj) aux += LU[ii * NV + jj] * rhs[jj];
+    rhs[ii] = (rhs[ii] - aux) / LU[ii * NV + ii];
+  }
+}
+
 // Factorise every diagonal block once (LU-SGS uses Gauss_Elimination on the same, unchanged diagonal
 // block for every row and every call, so one factorisation per matrix is bitwise equivalent).
 // One wavefront per row.
@@ -421,10 +440,21 @@ __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __r
 #pragma unroll
         for (int kk = 0; kk < NV; ++kk) row[kk] = lane < NV ? D[lane * NV + kk] : 1.0;
         wave_factor_rows<NV>(row, lane);
+#ifndef RX_ILU_SOLVE_READLANE
+        if (lane < NV) {  // the factorisation to LDS (W is free here) for the broadcast solve
+#pragma unroll
+          for (int kk = 0; kk < NV; ++kk) Wb[lane * NV + kk] = row[kk];
+        }
+        wave_sync();
+#endif
         double rhs[NV];
 #pragma unroll
         for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == lane) ? 1.0 : 0.0;
+#ifndef RX_ILU_SOLVE_READLANE
+        wave_solve_lds<NV>(Wb, rhs);
+#else
         wave_solve_rows<NV>(row, rhs);
+#endif
         if (lane < NV) {
 #pragma unroll
           for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + lane] = rhs[rr];
