@@ -270,6 +270,25 @@ __device__ __forceinline__ void wave_inverse_lds(const double* D, double* L, dou
 #ifndef RX_ILU_LB
 #define RX_ILU_LB 768  // 12 wavefronts (rx_ilu_max_waves)
 #endif
+// Staging loads of one row of the ILU(0) build (plan record in prec, lane q of record slot q): inv(A_jj) of its
+// nlow lower blocks, then the A_jk blocks of its npair updates, one NV^2 block per stg slot.
+template <int NV>
+__device__ __forceinline__ void stage_loads(double (&stg)[kStage][(NV * NV + 63) / 64], int prec, int nlow, int npair,
+                                            const double* invD, const double* F, int lane) {
+  constexpr int NV2 = NV * NV, PER = (NV2 + 63) / 64;
+#pragma unroll
+  for (int t = 0; t < kStage; ++t) {
+    const double* src = nullptr;
+    if (t < nlow) src = invD + (size_t)__builtin_amdgcn_readlane(prec, 8 + (t < 3 ? t : 0)) * NV2;
+    else if (t < nlow + npair) src = F + (size_t)__builtin_amdgcn_readlane(prec, 14 + 2 * (t - nlow)) * NV2;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int q = lane + 64 * u;
+      if (src && q < NV2) stg[t][u] = src[q];
+    }
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __restrict__ part_lvl,
                                                          const int32_t* __restrict__ lvl_ptr,
@@ -320,6 +339,9 @@ __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __r
       if (q < (k1 - k0) * NV2) pa[t] = A[(size_t)k0 * NV2 + q];
     }
   }
+  constexpr int PER = (NV2 + 63) / 64;
+  double stg[kStage][PER];  // staged inv(A_jj) / A_jk of the row (loaded ahead for a same-level next row)
+  bool stg_ready = false;
   for (int l = l0; l < l1; ++l) {
     for (int r = lvl_ptr[l] + wave; r < lvl_ptr[l + 1]; r += nwave) {
       RX_STAMP(0);
@@ -341,19 +363,7 @@ __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __r
       for (int q = lane; q < (rb - k1) * NV2; q += 64) F[(size_t)k1 * NV2 + q] = A[(size_t)k1 * NV2 + q];
       const bool fast = nlow >= 0 && nlow + npair <= kStage;
       if (fast) {  // one round trip: inv(A_jj) of every lower block, then the plan's A_jk blocks
-        constexpr int PER = (NV2 + 63) / 64;
-        double stg[kStage][PER];
-#pragma unroll
-        for (int t = 0; t < kStage; ++t) {
-          const double* src = nullptr;
-          if (t < nlow) src = invD + (size_t)__builtin_amdgcn_readlane(prec, 8 + (t < 3 ? t : 0)) * NV2;
-          else if (t < nlow + npair) src = F + (size_t)__builtin_amdgcn_readlane(prec, 14 + 2 * (t - nlow)) * NV2;
-#pragma unroll
-          for (int u = 0; u < PER; ++u) {
-            const int q = lane + 64 * u;
-            if (src && q < NV2) stg[t][u] = src[q];
-          }
-        }
+        if (!stg_ready) stage_loads<NV>(stg, prec, nlow, npair, invD, F, lane);
 #pragma unroll
         for (int t = 0; t < kStage; ++t)
           if (t < nlow + npair) {
@@ -364,6 +374,7 @@ __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __r
             }
           }
       }
+      stg_ready = false;
       // prefetch the next row's plan and A blocks (inputs only)
       const int nr = next_slot(r, l);
       if (nr >= 0) {
@@ -434,6 +445,15 @@ __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __r
         wave_sync();
       }
       RX_STAMP(2);
+      // a next row of the same level depends only on finished levels: its staging loads are issued now and land
+      // while this row's inverse runs
+      if (nr >= 0 && nr < lvl_ptr[l + 1]) {
+        const int nl = __builtin_amdgcn_readlane(prec, 6), np = __builtin_amdgcn_readlane(prec, 7);
+        if (nl >= 0 && nl + np <= kStage) {
+          stage_loads<NV>(stg, prec, nl, np, invD, F, lane);
+          stg_ready = true;
+        }
+      }
       {  // inv(D_i): right-looking elimination with register broadcasts, then one unit column per lane
         const double* D = rowbuf + (size_t)(kd - k0) * NV2;
         double row[NV];
