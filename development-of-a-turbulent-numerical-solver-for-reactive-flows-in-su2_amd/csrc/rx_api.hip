@@ -438,6 +438,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   CK(dupload(ctx, &ctx->adj, adj.data(), 2 * E));
   CK(dupload(ctx, &ctx->adj_blk, adj_blk.data(), 2 * E));
   CK(dupload(ctx, &ctx->edge_blk, edge_blk.data(), 2 * E));
+  for (int64_t i = 0; i < N; ++i) ctx->max_degree = std::max(ctx->max_degree, (int)(adj_ptr[i + 1] - adj_ptr[i]));
   CK(dupload(ctx, &ctx->nbr_ptr, nptr.data(), N + 1));
   CK(dupload(ctx, &ctx->nbr, nbr.data(), nbr.size()));
   CK(dupload(ctx, &ctx->bv_ptr, bvp.data(), N + 1));

@@ -62,6 +62,7 @@ struct rx_ctx {
   int32_t* adj = nullptr;       // [2E] (edge << 1) | (node is the edge's second node)
   int64_t* adj_blk = nullptr;   // [2E] BSR block index of (node, other)
   int64_t* edge_blk = nullptr;  // [E][2] BSR block index of (n0, n1) and (n1, n0)
+  int max_degree = 0;           // incident edges of the busiest node
   int32_t* nbr_ptr = nullptr;   // [N+1] LSQ neighbours in the reference order
   int32_t* nbr = nullptr;
   int32_t* bv_ptr = nullptr;    // [N+1] boundary vertices per node in (marker, vertex) order

@@ -752,7 +752,6 @@ __global__ __launch_bounds__(128) void k_source(int N, const double* __restrict_
 // Team = one or two whole wavefronts up to nVar = 11; above, exactly nVar^2 lanes (no intra-team synchronisation:
 // teams may straddle wavefronts), so nVar = 12 / 13 / 14 do not idle 112 / 87 / 60 of 256 lanes (C5 assembly
 // 10.0 -> 7.9 ms).
-constexpr int kAsmDeg = 8;  // incident edges of a node assembled from registers (larger degrees: the loop)
 template <int NVAR>
 constexpr int asm_team() {
   return NVAR * NVAR <= 64 ? 64 : (NVAR * NVAR <= 128 ? 128 : NVAR * NVAR);
@@ -766,7 +765,9 @@ __device__ inline int xcd_block(int b, int nb) {
   return x < r ? x * (q + 1) + idx : r * (q + 1) + (x - r) * q + idx;
 }
 
-template <int NVAR>
+// DEG: incident edges of a node assembled from registers (larger degrees take the loop); the launcher picks the
+// smallest of 4 / 8 that covers the mesh's maximum degree (2-D quads: 4, so fewer registers and more waves)
+template <int NVAR, int kAsmDeg>
 __global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int32_t* __restrict__ adj_ptr,
                                                      const int32_t* __restrict__ adj,
                                                      const int64_t* __restrict__ adj_blk,
@@ -1277,12 +1278,17 @@ int rx_launch_source(rx_ctx* ctx) {
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   const int nv = ctx->nVar;
   switch (nv) {
-#define RX_ASM(NV)                                                                                          \
-  case NV:                                                                                                  \
-    k_assemble<NV><<<blocks(ctx->N * asm_team<NV>()), kBlock, 0, ctx->stream>>>((int)ctx->N, NV - ctx->ns, ctx->adj_ptr, ctx->adj, ctx->adj_blk, \
-                                                   ctx->diag, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, \
-                                                   ctx->jsrc, ctx->rsrc, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], \
-                                                   with_visc, with_src, with_visc && ctx->offdiag_done ? 0 : 1); \
+#define RX_ASM_DEG(NV, DEG)                                                                                       \
+  k_assemble<NV, DEG><<<blocks(ctx->N * asm_team<NV>()), kBlock, 0, ctx->stream>>>(                              \
+      (int)ctx->N, NV - ctx->ns, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->diag, ctx->fconv, ctx->fvisc, ctx->jconv, \
+      ctx->jvisc, ctx->jsrc, ctx->rsrc, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_visc, with_src,                   \
+      with_visc && ctx->offdiag_done ? 0 : 1)
+#define RX_ASM(NV)                      \
+  case NV:                              \
+    if (ctx->max_degree <= 4)           \
+      RX_ASM_DEG(NV, 4);                \
+    else                                \
+      RX_ASM_DEG(NV, 8);                \
     break;
     RX_ASM(7)
     RX_ASM(8)
@@ -1291,6 +1297,7 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
     RX_ASM(13)
     RX_ASM(14)
 #undef RX_ASM
+#undef RX_ASM_DEG
     default:
       return RX_ERR_ARG;
   }
