@@ -17,6 +17,19 @@ using namespace rx;
 namespace {
 
 constexpr int kBlock = 256;
+// waves-per-SIMD targets of register-heavy kernels (build knobs; empty = the compiler's choice). Measured on one
+// box at C3: 3 waves per SIMD take SetPrimitive_Variables 1.32 -> 1.22 ms per step (175 -> 157 VGPRs) and the
+// source 0.57 -> 0.46 ms (180 -> 168 VGPRs, 12 B spilled); the AUSM edge kernel at 3 spills and slows 1.30 -> 2.06 ms.
+#define RX_WPE(n) __attribute__((amdgpu_waves_per_eu(n)))
+#ifndef RX_WPE_PRIM
+#define RX_WPE_PRIM RX_WPE(3)
+#endif
+#ifndef RX_WPE_AUSM
+#define RX_WPE_AUSM
+#endif
+#ifndef RX_WPE_SRC
+#define RX_WPE_SRC RX_WPE(3)
+#endif
 
 __device__ inline void set_err(int* err, int code, int64_t idx) {
   if (atomicCAS(err, 0, code) == 0) err[1] = (int)idx;
@@ -237,7 +250,7 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
 }
 
 template <int NS, int NDIM>
-__global__ __launch_bounds__(kBlock) void k_set_primitive(int N, DevMech m, PrimParams P, double* __restrict__ Ug,
+__global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, DevMech m, PrimParams P, double* __restrict__ Ug,
                                                           double* __restrict__ Vg, const double* __restrict__ Uold,
                                                           const double* __restrict__ tke,
                                                           const double* __restrict__ mut, double* __restrict__ dPdU,
@@ -486,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void k_muscl_edge(int E, const int32_t* __r
 constexpr int kAusmTeam = 4;
 constexpr int kAusmBlock = 128;
 template <int NS, int NDIM>
-__global__ __launch_bounds__(kAusmBlock) void k_ausm_edge(int E, const int32_t* __restrict__ edges,
+__global__ __launch_bounds__(kAusmBlock) RX_WPE_AUSM void k_ausm_edge(int E, const int32_t* __restrict__ edges,
                                                           const double* __restrict__ normal,
                                                           const double* __restrict__ V,
                                                           const double* __restrict__ dPdU,
@@ -718,7 +731,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_flux(int N, int nVar, const i
 // contiguous 512-B segment (the [N][nVar^2] thread-per-cell layout wrote 64 lines per store and amplified the
 // kernel's HBM writes 2.8x, profiles/r02_pmc_c3.json).
 template <int NS, int NDIM>
-__global__ __launch_bounds__(128) void k_source(int N, const double* __restrict__ V, const double* __restrict__ dTdU,
+__global__ __launch_bounds__(128) RX_WPE_SRC void k_source(int N, const double* __restrict__ V, const double* __restrict__ dTdU,
                                                 const double* __restrict__ vol, const double* __restrict__ omega,
                                                 DevMech m, SourceParams P, double* __restrict__ R, int add,
                                                 double* __restrict__ Js, int* err) {
