@@ -88,7 +88,7 @@ def ilu_apply_kernels(N, nnzb, nVar, parts):
     return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
 
 
-def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None):
+def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, max_degree=4):
     """Algorithmic bytes (or flops) per launch of the single-launch kernels timed per phase
     (each unique datum once per sweep)."""
     nVar, nPV, nG = ns + nDim + 2, ns + nDim + 5, ns + nDim + 2
@@ -111,7 +111,7 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None):
         # k_assemble: each node's own-side conv + visc blocks (2 per edge each), the edge fluxes, the source
         # Jacobian's species rows and residual in; diagonal blocks + residual out
         "ASSEMBLE": hbm(4 * E * blk + 2 * E * nVar * d + N * (ns * nVar + nVar) * d + N * (blk + nVar * d),
-                        "k_assemble" + tv),
+                        f"k_assemble<{nVar}, {4 if max_degree <= 4 else 8}>"),  # register path by max degree
         "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq" + te),
         # k_source: V, dT/dU, volume, omega in; residual + the Jacobian's species rows out
         "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar + ns * nVar) * d, "k_source" + te),
@@ -369,7 +369,8 @@ def main():
 
     dims = f"{nx}x{ny}" + (f"x{nz}" if nz > 1 else "")
     wkey = f"{args.workload} {dims} ns{ns} parts{args.parts}"
-    models = kernel_models(N, E, nnzb, ns, nDim, 5, parts=args.parts, workload_key=wkey)
+    max_degree = int(np.bincount(np.asarray(mesh["edges"]).ravel()).max())
+    models = kernel_models(N, E, nnzb, ns, nDim, 5, parts=args.parts, workload_key=wkey, max_degree=max_degree)
     phase_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1] > 0 and k not in ("SPMV", "ILU_APPLY")}
 
     def roof(k):
