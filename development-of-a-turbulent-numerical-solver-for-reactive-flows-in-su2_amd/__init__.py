@@ -78,7 +78,8 @@ class Cfg(C.Structure):
                 ("relaxation", C.c_double), ("implicit", C.c_int32), ("rans", C.c_int32), ("lin_iter", C.c_int32),
                 ("lin_prec", C.c_int32), ("spatial_order", C.c_int32), ("clip_temp", C.c_int32),
                 ("t_min", C.c_double), ("t_max", C.c_double), ("p_ref", C.c_double), ("visc_ref", C.c_double),
-                ("cond_ref", C.c_double), ("vel_ref", C.c_double), ("len_ref", C.c_double)]
+                ("cond_ref", C.c_double), ("vel_ref", C.c_double), ("len_ref", C.c_double),
+                ("slope_limiter", C.c_int32)]
 
 
 class BcDesc(C.Structure):
@@ -280,7 +281,7 @@ def default_cfg(**kw):
              prandtl_turb=0.9, lewis_turb=1.2, c_mu=0.09, pasr_lb=0.2, cfl=5.0, max_delta_time=1e6,
              ref_elem_length=0.1, limiter_coeff=0.5, lin_tol=1e-6, relaxation=1.0, implicit=1, rans=1, lin_iter=5,
              lin_prec=1, spatial_order=0, clip_temp=0, t_min=200.0, t_max=6000.0, p_ref=1.0, visc_ref=1.0,
-             cond_ref=1.0, vel_ref=1.0, len_ref=1.0)
+             cond_ref=1.0, vel_ref=1.0, len_ref=1.0, slope_limiter=0)
     c.update(kw)
     cfg = Cfg()
     for k, v in c.items():
@@ -721,6 +722,8 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
                     implicit=int(tf == "EULER_IMPLICIT"), rans=int(c.get("KIND_TURB_MODEL", "NONE") == "SST"),
                     spatial_order=order_map[c.get("SPATIAL_ORDER_FLOW", "2ND_ORDER")],
                     ref_elem_length=f("REF_ELEM_LENGTH", 0.1), limiter_coeff=f("LIMITER_COEFF", 0.5),
+                    slope_limiter={"VENKATAKRISHNAN": 0, "BARTH_JESPERSEN": 1}[c.get("SLOPE_LIMITER_FLOW",
+                                                                                     "VENKATAKRISHNAN")],
                     t_min=f("TEMPERATURE_MIN", 200.0), t_max=f("TEMPERATURE_MAX", 6000.0),
                     clip_temp=int(c.get("CLIPPING_TEMPRATURE", "NO") == "YES"))
     sst_cfg_kw = dict(implicit=int(c.get("TIME_DISCRE_TURB", "EULER_IMPLICIT") == "EULER_IMPLICIT"),

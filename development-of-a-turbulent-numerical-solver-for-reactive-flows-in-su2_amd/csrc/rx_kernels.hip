@@ -1072,6 +1072,52 @@ __global__ __launch_bounds__(kBlock) void k_limiter_venkat(int N, int nG, const 
   for (int v = 0; v < nL; ++v) lim[(size_t)i * nL + v] = l[v];
 }
 
+// a13: Barth-Jespersen branch (solver_direct_reactive.cpp:1383-1440), node-centric. Unlike Venkatakrishnan's min,
+// the j side's update (:1426-1427: `if (limiter < L_j) L_j = value`, the bool member, 1 whenever the limiter runs)
+// is an overwrite, so the order matters: a node walks its incident edges in ascending edge index (adj is built
+// edge-ordered), i.e. the reference's edge loop restricted to that node. dm < EPS gives 2.0; dp is the max for
+// dm > EPS, the min for dm == EPS. Then y -> (y^2 + 2y) / (y^2 + y + 2) (:1433-1439).
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_limiter_barth(int N, int nG, const int32_t* __restrict__ adj_ptr,
+                                                          const int32_t* __restrict__ adj,
+                                                          const int32_t* __restrict__ edges,
+                                                          const double* __restrict__ coord,
+                                                          const double* __restrict__ G, const double* __restrict__ mn,
+                                                          const double* __restrict__ mx, double* __restrict__ lim) {
+  constexpr int nL = NDIM + 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double l[nL], lo[nL], hi[nL];
+#pragma unroll
+  for (int v = 0; v < nL; ++v) {
+    l[v] = 2.0;
+    lo[v] = mn[(size_t)i * nL + v];
+    hi[v] = mx[(size_t)i * nL + v];
+  }
+  double ci[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) ci[d] = coord[(size_t)i * NDIM + d];
+  const double* Gi = G + (size_t)i * nG * NDIM;
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k];
+    const int e = a >> 1, side = a & 1;
+    const int other = edges[2 * e + (side ^ 1)];
+#pragma unroll
+    for (int v = 0; v < nL; ++v) {
+      double dm = 0.0;
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) dm += 0.5 * (coord[(size_t)other * NDIM + d] - ci[d]) * Gi[v * NDIM + d];
+      const double lv = dm < kEPS ? 2.0 : (dm > kEPS ? hi[v] : lo[v]) / dm;
+      if (side ? 1.0 < l[v] : lv < l[v]) l[v] = lv;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < nL; ++v) {
+    const double y = l[v];
+    lim[(size_t)i * nL + v] = (y * y + 2.0 * y) / (y * y + y + 2.0);
+  }
+}
+
 // a18: SetTime_Step (RANS branch), node-centric over incident edges then boundary vertices.
 template <int NDIM>
 __global__ __launch_bounds__(kBlock) void k_time_step(int N, int nPV, int nVar, const int32_t* __restrict__ adj_ptr,
@@ -1332,6 +1378,14 @@ int rx_launch_limiter(rx_ctx* ctx) {
                                                                   ctx->edges, ctx->f[RX_F_V], ctx->lim_mn,
                                                                   ctx->lim_mx)));
   RX_HIP(hipGetLastError());
+  if (ctx->cfg.slope_limiter == RX_LIMITER_BARTH_JESPERSEN) {
+    RX_ND_SWITCH(ctx->nDim, (k_limiter_barth<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->adj_ptr,
+                                                                   ctx->adj, ctx->edges, ctx->coord,
+                                                                   ctx->f[RX_F_GRAD], ctx->lim_mn, ctx->lim_mx,
+                                                                   ctx->f[RX_F_LIMITER])));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
   const double eps1 = ctx->cfg.limiter_coeff * ctx->cfg.ref_elem_length;
   const double eps2 = eps1 * eps1 * eps1;
   RX_ND_SWITCH(ctx->nDim, (k_limiter_venkat<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nG, ctx->adj_ptr, ctx->adj,

@@ -13,6 +13,7 @@
  *                        CSourceReactive::ComputeChemistry numerics_direct_reactive.cpp:1728-1879
  *   rx_grad_lsq          CReactiveNSSolver::SetPrimitive_Gradient_LS solver_direct_reactive.cpp:4887-5050
  *   rx_limiter_venkat    CReactiveEulerSolver::SetPrimitive_Limiter solver_direct_reactive.cpp:1328-1523
+ *                        (Venkatakrishnan or Barth-Jespersen by rx_cfg.slope_limiter)
  *   rx_time_step         CReactiveNSSolver::SetTime_Step solver_direct_reactive.cpp:5057-5298
  *   rx_bsr_spmv          CSysMatrix::MatrixVectorProduct Common/src/matrix_structure.cpp:997-1030
  *   rx_ilu0_build        CSysMatrix::BuildILUPreconditioner matrix_structure.cpp:1368-1451
@@ -116,7 +117,10 @@ typedef struct {
   int32_t clip_temp;      /* CLIPPING_TEMPRATURE (Cons2PrimVar :711-712) */
   double t_min, t_max;    /* TEMPERATURE_MIN / TEMPERATURE_MAX (Cons2PrimVar secant / bisection bounds) */
   double p_ref, visc_ref, cond_ref, vel_ref, len_ref;  /* Pressure/Viscosity/Conductivity/Velocity/Length_Ref */
+  int32_t slope_limiter;  /* SLOPE_LIMITER_FLOW: rx_slope_limiter (SetPrimitive_Limiter :1383 / :1443) */
 } rx_cfg;
+
+typedef enum { RX_LIMITER_VENKATAKRISHNAN = 0, RX_LIMITER_BARTH_JESPERSEN = 1 } rx_slope_limiter;
 
 typedef enum {
   RX_F_U = 0, RX_F_V, RX_F_DPDU, RX_F_DTDU, RX_F_MU, RX_F_KAPPA, RX_F_DIJ, RX_F_GRAD, RX_F_LIMITER,

@@ -155,7 +155,7 @@ def write_subset_library(wd, ns):
 
 
 def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATURE_IMPOSE", extra="",
-                 time_flow="EULER_IMPLICIT", ns=9):
+                 time_flow="EULER_IMPLICIT", ns=9, slope_limiter="VENKATAKRISHNAN"):
     wd = os.path.join("/tmp/rx_golden", case)
     shutil.rmtree(wd, ignore_errors=True)
     os.makedirs(os.path.join(wd, "out"))
@@ -168,6 +168,7 @@ def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATUR
     mesh_name = mesh_writer(wd)
     cfg = CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec, inlet_type=inlet,
                               inlet_ox=INLETS[inlet][0], inlet_fuel=INLETS[inlet][1], extra=extra, time_flow=time_flow)
+    cfg = cfg.replace("SLOPE_LIMITER_FLOW= VENKATAKRISHNAN", "SLOPE_LIMITER_FLOW= " + slope_limiter)
     if ns != 9:  # the mixture's species lists
         y = lambda k: ", ".join("1.0" if q == k else "0.0" for q in range(ns))
         cfg = cfg.replace("FREESTREAM_MASS_FRAC = (0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)",
@@ -431,6 +432,34 @@ def case_muscl3d():
     return out
 
 
+BJ_KEYS = ("coord", "volume", "U", "V", "dPdU", "dTdU", "grad_prim", "limiter_out", "edges", "edge_normal",
+           "nbr_ptr", "nbr", "dims", "mach_inf", "limiter_params", "muscl_params", "muscl_loop_res", "bvertex",
+           "bvertex_normal", "wall_distance", "visc_params", "src_params", "mu", "kappa", "Dij", "turb_k",
+           "turb_omega", "mu_t", "sigma_k", "grad_k", "eddy_visc_flow")
+
+
+def case_bj9():
+    """a13 Barth-Jespersen branch (solver_direct_reactive.cpp:1383-1440) in 2-D: the mini9 mesh and state with
+    2ND_ORDER_LIMITER + SLOPE_LIMITER_FLOW= BARTH_JESPERSEN (limiter after the reference's own Preprocessing,
+    and the MUSCL loop residual that reads it)."""
+    pts, quads, bnd = meshgen.jet_mesh(21, 11)
+    xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    from scipy.spatial import cKDTree
+    scale = np.array([1.0 / 0.125, 1.0 / 0.006])
+    _, idx = cKDTree(xy * scale).query(pts * scale)
+
+    def writer(wd):
+        meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, quads, bnd)
+        return "mesh.su2"
+
+    wd = make_workdir("bj9", writer, cfl=0.1, order="2ND_ORDER_LIMITER", slope_limiter="BARTH_JESPERSEN")
+    write_state(wd, cons[idx])
+    a = run_harness(wd, bsr=False)
+    out = {k: a[k] for k in BJ_KEYS}
+    out.update(mech_arrays())
+    return out
+
+
 def case_jet9w():
     def writer(wd):
         os.symlink(os.path.join(CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
@@ -670,7 +699,8 @@ def main():
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
-             "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "it7": case_it7}[case]()
+             "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "it7": case_it7,
+             "bj9": case_bj9}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

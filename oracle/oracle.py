@@ -188,6 +188,17 @@ def limiter_venkat(nDim, ns, edges, coord, V, grad, ref_len, coeff):
 
 
 @_keepalive
+def limiter_barth(nDim, ns, edges, coord, V, grad):
+    """a13 Barth-Jespersen branch (solver_direct_reactive.cpp:1383-1440), reference quirks kept."""
+    N = len(coord)
+    lim = np.zeros((N, nDim + 2))
+    edges = np.ascontiguousarray(edges, dtype=np.int64)
+    lib().orc_limiter_barth(C.c_int(nDim), C.c_int(ns), C.c_int64(N), C.c_int64(len(edges)), _p(edges, np.int64),
+                            _p(coord), _p(V), _p(grad), lim.ctypes.data_as(C.c_void_p))
+    return lim
+
+
+@_keepalive
 def bsr_spmv(rp, col, A, x):
     N, nb = len(rp) - 1, A.shape[1]
     y = np.zeros(N * nb)

@@ -1457,6 +1457,65 @@ void orc_limiter_venkat(int nDim, int ns, int64_t N, int64_t E, const int64_t* e
   }
 }
 
+// a13: Barth-Jespersen branch (solver_direct_reactive.cpp:1383-1440), edge-loop form after the same min/max pass
+// (:1346-1379). Reproduced as written: dm < EPS gives 2.0, dp = max only for dm > EPS (min at dm == EPS), and the
+// j side tests the bool member `limiter` (true whenever SetPrimitive_Limiter runs, :4739-4742), so node j takes
+// the edge's value whenever its current limiter exceeds 1 (:1426-1427). Then y -> (y^2 + 2y) / (y^2 + y + 2).
+void orc_limiter_barth(int nDim, int ns, int64_t N, int64_t E, const int64_t* edges, const double* coord,
+                       const double* V, const double* grad, double* lim) {
+  const int nL = nDim + 2, nPV = ns + nDim + 5, nG = ns + nDim + 2;
+  std::vector<double> mx(N * nL, -EPS), mn(N * nL, EPS);
+  for (int64_t q = 0; q < N * nL; ++q) lim[q] = 2.0;
+  auto pl = [&](int64_t p, int v) {
+    const double* pv = V + p * nPV;
+    if (v == 0) return pv[0];
+    if (v == nL - 1) return pv[nDim + 1];
+    return pv[v];
+  };
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    for (int v = 0; v < nL; ++v) {
+      const double du = pl(j, v) - pl(i, v);
+      mn[i * nL + v] = std::min(mn[i * nL + v], du);
+      mx[i * nL + v] = std::max(mx[i * nL + v], du);
+      mn[j * nL + v] = std::min(mn[j * nL + v], -du);
+      mx[j * nL + v] = std::max(mx[j * nL + v], -du);
+    }
+  }
+  const double flag = 1.0;  // (double)limiter
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    const double* Gi = grad + i * nG * nDim;
+    const double* Gj = grad + j * nG * nDim;
+    const double* ci = coord + i * nDim;
+    const double* cj = coord + j * nDim;
+    for (int v = 0; v < nL; ++v) {
+      double dm = 0.0, lv;
+      for (int d = 0; d < nDim; ++d) dm += 0.5 * (cj[d] - ci[d]) * Gi[v * nDim + d];
+      if (dm < EPS) {
+        lv = 2.0;
+      } else {
+        const double dp = dm > EPS ? mx[i * nL + v] : mn[i * nL + v];
+        lv = dp / dm;
+      }
+      if (lv < lim[i * nL + v]) lim[i * nL + v] = lv;
+      dm = 0.0;
+      for (int d = 0; d < nDim; ++d) dm += 0.5 * (ci[d] - cj[d]) * Gj[v * nDim + d];
+      if (dm < EPS) {
+        lv = 2.0;
+      } else {
+        const double dp = dm > EPS ? mx[j * nL + v] : mn[j * nL + v];
+        lv = dp / dm;
+      }
+      if (flag < lim[j * nL + v]) lim[j * nL + v] = lv;
+    }
+  }
+  for (int64_t q = 0; q < N * nL; ++q) {
+    const double y = lim[q];
+    lim[q] = (y * y + 2.0 * y) / (y * y + y + 2.0);
+  }
+}
+
 // a18: CReactiveNSSolver::SetTime_Step, RANS branch (solver_direct_reactive.cpp:5057-5298).
 // bverts[nb][2] = (marker, node) in marker/vertex order, bnormal[nb][nDim]. params = {CFL, Max_DeltaTime,
 // Prandtl_Lam, Prandtl_Turb}. Outputs dt, lambda_inv, lambda_visc per node.

@@ -23,7 +23,7 @@ def golden(case):
     return g
 
 
-def make_solver(g, implicit, lin_prec=1, cfl=None, spatial_order=0):
+def make_solver(g, implicit, lin_prec=1, cfl=None, spatial_order=0, slope_limiter=0):
     nDim, nVar, nPV, nG, ns, imp, rans = [int(x) for x in g["dims"]]
     mesh = {k: g[k] for k in ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr")}
     mesh["bvertex"] = g.get("bvertex", np.zeros((0, 3), dtype=np.int64))
@@ -32,7 +32,7 @@ def make_solver(g, implicit, lin_prec=1, cfl=None, spatial_order=0):
     kw = dict(mach_inf=float(g["mach_inf"][0]), prandtl_turb=float(g["visc_params"][1]),
               lewis_turb=float(g["visc_params"][2]), c_mu=float(g["src_params"][0]),
               pasr_lb=float(g["src_params"][1]), implicit=int(implicit), lin_prec=lin_prec,
-              spatial_order=spatial_order)
+              spatial_order=spatial_order, slope_limiter=slope_limiter)
     if "limiter_params" in g:
         kw.update(ref_elem_length=float(g["limiter_params"][0]), limiter_coeff=float(g["limiter_params"][1]))
     if "dt_params" in g:
@@ -64,6 +64,27 @@ def test_gradient_and_limiter(case):
         L = s.download("LIMITER").reshape(-1, nDim + 2)
         it = g["interior"] if "interior" in g else slice(None)
         assert_close(L[it], g["limiter_out"][it], what="Venkatakrishnan limiter (HIP vs reference)")
+    s.close()
+
+
+@pytest.mark.parametrize("case", ["bj9", "muscl3d", "jet9w"])
+def test_limiter_barth(case):
+    """a13 Barth-Jespersen branch on the device: bitwise against the reference's own limiter (bj9, 2-D,
+    SLOPE_LIMITER_FLOW= BARTH_JESPERSEN) and against the oracle's restatement on the 3-D / jet-window records."""
+    g = golden(case)
+    s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=False, spatial_order=2, slope_limiter=1)
+    s.upload("GRAD", g["grad_prim"])
+    s.SetPrimitive_Limiter()
+    s.sync()
+    L = s.download("LIMITER").reshape(-1, nDim + 2)
+    ref = g["limiter_out"] if case == "bj9" else O.limiter_barth(nDim, ns, g["edges"], g["coord"], g["V"],
+                                                                 g["grad_prim"])
+    assert np.array_equal(L, ref)
+    if case == "bj9":  # the MUSCL loop on the device limiter against the reference's residual
+        s.Preprocessing_zero()
+        s.Upwind_Residual()
+        s.sync()
+        assert np.array_equal(s.download("RES").reshape(-1, nVar), g["muscl_loop_res"])
     s.close()
 
 

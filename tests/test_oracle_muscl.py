@@ -52,3 +52,19 @@ def test_muscl_upwind_loop_bitwise(case):
     # the reconstruction changes the flux (the check is not vacuous)
     r1, _, _ = O.ausm_edges(nDim, ns, g["edges"], g["edge_normal"], g["V"], g["dPdU"], g["mach_inf"][0], False)
     assert np.abs(r1 - r).max() > 1e-6 * np.abs(r).max()
+
+
+def test_muscl_upwind_loop_barth_bitwise():
+    """bj9: the 2-D mini jet with 2ND_ORDER_LIMITER + BARTH_JESPERSEN; the reconstruction reads the oracle's own
+    Barth-Jespersen limiter, so this pins limiter and loop together against the reference's residual."""
+    g = dict(np.load(os.path.join(GOLD, "bj9.npz")))
+    nDim, ns = int(g["dims"][0]), int(g["dims"][4])
+    m = O.Mechanism(g)
+    L = O.limiter_barth(nDim, ns, g["edges"], g["coord"], g["V"], g["grad_prim"])
+    r, _, _ = O.muscl_edges(m, nDim, g["edges"], g["edge_normal"], g["coord"], g["V"], g["dPdU"], g["grad_prim"], L,
+                            g["muscl_params"][1:], g["mach_inf"][0], True)
+    R = np.zeros_like(g["muscl_loop_res"])
+    for e, (i, j) in enumerate(g["edges"]):
+        R[i] += r[e]
+        R[j] -= r[e]
+    assert np.array_equal(R, g["muscl_loop_res"])
