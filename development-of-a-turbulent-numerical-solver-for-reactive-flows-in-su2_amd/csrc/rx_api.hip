@@ -86,7 +86,6 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   const bool sst = flow != nullptr;
   const int ns = sst ? 0 : mech->n_species;
   if (!sst && !(ns == 3 || ns == 4 || ns == 7 || ns == 9)) return RX_ERR_ARG;
-  if (!sst && mesh->n_dim == 3 && !(ns == 7 || ns == 9)) return RX_ERR_ARG;  // 3-D instantiations (rx_kernels.hip)
   if (!sst && mech->n_reactions > rx::kMaxNR) return RX_ERR_ARG;
   if (mesh->n_point >= (1LL << 31) || 2 * mesh->n_edge >= (1LL << 31)) return RX_ERR_ARG;
   if (sst && (mesh->n_point != flow->N || mesh->n_edge != flow->E)) return RX_ERR_ARG;

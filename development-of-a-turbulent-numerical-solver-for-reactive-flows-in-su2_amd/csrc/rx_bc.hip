@@ -671,8 +671,10 @@ __global__ __launch_bounds__(kBlock) void k_sst_bc(int nbn, const int32_t* __res
       case 9: { constexpr int NS_ = 9, ND_ = 2; CALL; } break;             \
       default: return RX_ERR_ARG;                                          \
     }                                                                      \
-  } else if ((nd) == 3) { /* 3-D: the 7-species C5 mechanism, 9 (golden) */ \
+  } else if ((nd) == 3) {                                                 \
     switch (ns) {                                                          \
+      case 3: { constexpr int NS_ = 3, ND_ = 3; CALL; } break;             \
+      case 4: { constexpr int NS_ = 4, ND_ = 3; CALL; } break;             \
       case 7: { constexpr int NS_ = 7, ND_ = 3; CALL; } break;             \
       case 9: { constexpr int NS_ = 9, ND_ = 3; CALL; } break;             \
       default: return RX_ERR_ARG;                                          \

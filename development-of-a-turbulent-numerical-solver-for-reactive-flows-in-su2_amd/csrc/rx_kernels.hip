@@ -1204,8 +1204,10 @@ inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
       case 9: { constexpr int NS_ = 9, ND_ = 2; CALL; } break;             \
       default: return RX_ERR_ARG;                                          \
     }                                                                      \
-  } else if ((nd) == 3) { /* 3-D: the 7-species C5 mechanism, 9 (golden) */ \
+  } else if ((nd) == 3) {                                                 \
     switch (ns) {                                                          \
+      case 3: { constexpr int NS_ = 3, ND_ = 3; CALL; } break;             \
+      case 4: { constexpr int NS_ = 4, ND_ = 3; CALL; } break;             \
       case 7: { constexpr int NS_ = 7, ND_ = 3; CALL; } break;             \
       case 9: { constexpr int NS_ = 9, ND_ = 3; CALL; } break;             \
       default: return RX_ERR_ARG;                                          \
@@ -1351,6 +1353,7 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
     break;
     RX_ASM(7)
     RX_ASM(8)
+    RX_ASM(9)
     RX_ASM(11)
     RX_ASM(12)
     RX_ASM(13)

@@ -1311,6 +1311,7 @@ __global__ __launch_bounds__(256) void k_lusgs_bwd_part(const int32_t* __restric
     case 2: { constexpr int NV_ = 2; CALL; } break;   \
     case 7: { constexpr int NV_ = 7; CALL; } break;   \
     case 8: { constexpr int NV_ = 8; CALL; } break;   \
+    case 9: { constexpr int NV_ = 9; CALL; } break;   \
     case 11: { constexpr int NV_ = 11; CALL; } break; \
     case 12: { constexpr int NV_ = 12; CALL; } break; \
     case 13: { constexpr int NV_ = 13; CALL; } break; \

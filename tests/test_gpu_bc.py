@@ -226,17 +226,20 @@ def test_outer_iteration_vs_oracle_device_order(case):
     s.close()
 
 
-@pytest.mark.parametrize("nz", [0, 4])
-def test_synthetic_jet_iteration_vs_oracle(nz):
+@pytest.mark.parametrize("ns,nz", [(7, 0), (7, 4), (4, 4)])
+def test_synthetic_jet_iteration_vs_oracle(ns, nz):
     """rx.Iterate with the jet's boundary conditions on a partitioned synthetic jet with the C2/C5 mechanism
-    (7 species; nz = 4: the 3-D extrusion with symmetry planes) against O.outer_iteration in the device's
+    (7 species; nz = 4: the 3-D extrusion with symmetry planes; 4 species: the C1 mechanism in 3-D, nVar 9)
+    against O.outer_iteration in the device's
     inner-product order: U and (k, omega) within 1e-10 of each column's max (FGMRES-amplified rounding of the
     Stefan-Maxwell solve, as in test_outer_iteration_vs_oracle_device_order)."""
     from tests.oracle_inputs import outer_iteration_inputs
     from tests.rxpkg import synth
-    mesh, st, mech, kw = synth.jet_case(24, 10, n_species=7, n_part=4, nz=nz)
+    mesh, st, mech, kw = synth.jet_case(24, 10, n_species=ns, n_part=4, nz=nz)
+    if ns == 4:  # at the default CFL 5 this state leaves the tables in the oracle too (bisection failure)
+        kw["cfl"] = 1.0
     cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
-    bc = synth.jet_bc(mesh, 7)
+    bc = synth.jet_bc(mesh, ns)
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
     s.set_bc(bc)
     t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
