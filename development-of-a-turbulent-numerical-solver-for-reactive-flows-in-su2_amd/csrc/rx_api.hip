@@ -846,7 +846,8 @@ namespace {
 // before it as single kernels (timed per phase).
 int enqueue_solve(rx_ctx* ctx) {
   int rc;
-  if ((rc = rx_la_fgmres_enqueue(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter))) return rc;
+  static const bool x_product = getenv("RX_FG_X_PRODUCT") != nullptr;  // diagnosis: the A x product at x = 0
+  if ((rc = rx_la_fgmres_enqueue(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter, !x_product))) return rc;
   if ((rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RHS]))) return rc;
   return ctx->kind == RX_KIND_SST ? rx_sst_update(ctx) : rx_la_implicit_update(ctx);
 }

@@ -242,7 +242,7 @@ int rx_ilu_max_waves();  // wavefronts per workgroup cap of the ILU(0) build
 int rx_la_krylov_alloc(rx_ctx* ctx, int m);
 // Drop the captured solve graph (its kernel arguments point at buffers about to be replaced).
 void rx_graph_reset(rx_ctx* ctx);
-int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m);
+int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero);  // x_zero: SOL is all +0.0
 int rx_la_fgmres_result(rx_ctx* ctx, int* iters, double* resid);
 int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid);
 void rx_la_krylov_free(rx_ctx* ctx);

@@ -174,6 +174,24 @@ __global__ __launch_bounds__(kBlock) void k_fg_residual(int Nd, const int32_t* _
   grid_reduce<2>(v, part, s, sl, dist);
 }
 
+// k_fg_residual for x = 0 (ImplicitEuler_Iteration zeroes LinSysSol before the solve, solver_direct_reactive.cpp:2373 / :2384): A x is then
+// +0.0 in every element (spmv_elem sums from +0.0, so +0 + (+-0) = +0 for any finite A), and w0 = +0.0 - b is the
+// same double as the product path gives, with the same grid loop and reduction, without streaming the matrix.
+__global__ __launch_bounds__(kBlock) void k_fg_residual0(int64_t n, const double* __restrict__ b,
+                                                         double* __restrict__ w, double* __restrict__ part,
+                                                         KState* __restrict__ s, bool dist) {
+  double v[2] = {0.0, 0.0};
+  GRID_LOOP(q, n) {
+    const double bq = b[q];
+    v[0] += bq * bq;
+    const double y = 0.0 - bq;
+    w[q] = y;
+    v[1] += y * y;
+  }
+  const int sl[2] = {kNorm0In, kDot};
+  grid_reduce<2>(v, part, s, sl, dist);
+}
+
 // w_{i+1} = A z_i with |w_{i+1}|^2 -> dotn and <w_{i+1}, w_0> -> dot
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_fg_spmv(int Nd, const int32_t* __restrict__ rp,
@@ -418,7 +436,7 @@ int rx_la_krylov_alloc(rx_ctx* ctx, int m) {
 }
 
 // Enqueue FGMRES(m) on JAC * SOL = RHS (SOL = initial guess) without any host synchronisation.
-int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m) {
+int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
   int rc = rx_la_krylov_alloc(ctx, m);
   if (rc) return rc;
   const int64_t ld = ctx->N * ctx->nVar;  // vector length (owned + halo)
@@ -435,8 +453,12 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m) {
   auto Z = [&](int k) { return ctx->kz + (int64_t)k * ld; };
   auto reduce = [&]() { return dist ? rx_la_allreduce(ctx, s->loc, land_host(s), 4) : RX_OK; };
   k_fg_reset<<<1, 64, 0, st>>>(s, tol);
-  RX_NV_SWITCH(ctx->nVar, (k_fg_residual<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, x,
-                                                                             b, W(0), part, s, dist)));
+  if (x_zero) {
+    k_fg_residual0<<<kRedBlocks, kBlock, 0, st>>>(n, b, W(0), part, s, dist);
+  } else {
+    RX_NV_SWITCH(ctx->nVar, (k_fg_residual<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, x,
+                                                                               b, W(0), part, s, dist)));
+  }
   if ((rc = reduce())) return rc;
   k_fg_start_div<<<nb, kBlock, 0, st>>>(n, s, W(0));
   for (int i = 0; i < m; ++i) {
@@ -473,7 +495,7 @@ int rx_la_fgmres_result(rx_ctx* ctx, int* iters, double* resid) {
 }
 
 int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
-  int rc = rx_la_fgmres_enqueue(ctx, tol, m);
+  int rc = rx_la_fgmres_enqueue(ctx, tol, m, false);
   if (rc) return rc;
   return rx_la_fgmres_result(ctx, iters, resid);
 }

@@ -76,6 +76,34 @@ __global__ __launch_bounds__(kBlock) void k_build_system(int Nd, int N, const in
   }
 }
 
+// The same system build with one thread per (node, variable): coalesced R / rhs / x rows and NV times the
+// threads in flight for the scattered diagonal read-modify-writes. Identical operations per element.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_build_system_elem(int Nd, int N, const int64_t* __restrict__ diag,
+                                                              const double* __restrict__ vol,
+                                                              const double* __restrict__ dt, double* __restrict__ A,
+                                                              double* __restrict__ R, double* __restrict__ rhs,
+                                                              double* __restrict__ x) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)N * NV) return;
+  const int i = (int)(q / NV), a = (int)(q - (int64_t)i * NV);
+  x[q] = 0.0;
+  if (i >= Nd) {
+    rhs[q] = 0.0;
+    return;
+  }
+  double* D = A + diag[i] * NV * NV + a * NV;
+  if (dt[i] > rx::kEPS) {
+    D[a] += vol[i] / dt[i];
+    rhs[q] = -(R[q] + 0.0);
+  } else {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) D[c] = (a == c) ? 1.0 : 0.0;
+    R[q] = 0.0;
+    rhs[q] = -(0.0 + 0.0);
+  }
+}
+
 // AddClippedSolution: U = clip(U_old + delta) (variable_structure.cpp:207-211) with
 //   mode 0 implicit  delta = relax * LinSysSol                          (:2390-2400)
 //   mode 1 explicit  delta = -(Res + 0) * dt / Vol                       (:2430-2440)
@@ -166,9 +194,16 @@ int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y, const i
 }
 
 int rx_la_build_system(rx_ctx* ctx) {
-  RX_NV_SWITCH(ctx->nVar, (k_build_system<NV_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
-                              (int)ctx->Nd, (int)ctx->N, ctx->diag, ctx->vol, ctx->f[RX_F_DT], ctx->f[RX_F_JAC], ctx->f[RX_F_RES],
-                              ctx->f[RX_F_RHS], ctx->f[RX_F_SOL])));
+  static const bool per_node = getenv("RX_BUILD_PER_NODE") != nullptr;  // A/B: the thread-per-node build
+  if (per_node) {
+    RX_NV_SWITCH(ctx->nVar, (k_build_system<NV_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
+                                (int)ctx->Nd, (int)ctx->N, ctx->diag, ctx->vol, ctx->f[RX_F_DT], ctx->f[RX_F_JAC],
+                                ctx->f[RX_F_RES], ctx->f[RX_F_RHS], ctx->f[RX_F_SOL])));
+  } else {
+    RX_NV_SWITCH(ctx->nVar, (k_build_system_elem<NV_><<<blocks(ctx->N * NV_), kBlock, 0, ctx->stream>>>(
+                                (int)ctx->Nd, (int)ctx->N, ctx->diag, ctx->vol, ctx->f[RX_F_DT], ctx->f[RX_F_JAC],
+                                ctx->f[RX_F_RES], ctx->f[RX_F_RHS], ctx->f[RX_F_SOL])));
+  }
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
