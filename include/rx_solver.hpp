@@ -5,7 +5,7 @@
  * (SU2_CFD/include/solver_reactive.hpp:141-363, 476-554):
  *   Preprocessing residual reset  -> rx_residual_zero            (LinSysRes.SetValZero, Jacobian.SetValZero)
  *   SetPrimitive_Gradient_LS      -> rx_grad_lsq                 (solver_direct_reactive.cpp:4887-5050)
- *   SetPrimitive_Limiter          -> rx_limiter_venkat           (:1328-1523)
+ *   SetPrimitive_Limiter          -> rx_limiter_venkat           (:1328-1523; Venkatakrishnan or Barth-Jespersen by rx_cfg.slope_limiter)
  *   SetTime_Step                  -> rx_time_step                (:5057-5298)
  *   Upwind_Residual               -> rx_edge_flux_conv           (:2535-2785)  throws "NaN found in the upwind residual"
  *   Viscous_Residual              -> rx_edge_flux_visc           (:5305-5386)  throws "NaN found in the viscous residual"
