@@ -588,7 +588,8 @@ __global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__
                                                      const int32_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                      const int32_t* __restrict__ upd_ptr,
                                                      const int2* __restrict__ upd, const double* __restrict__ A,
-                                                     double* __restrict__ F, double* __restrict__ invD) {
+                                                     double* __restrict__ F, double* __restrict__ invD,
+                                                     bool diag_regs) {
   constexpr int NV = 2, NV2 = 4;
   const int p = blockIdx.x;
   for (int l = part_lvl[p]; l < part_lvl[p + 1]; ++l) {
@@ -605,6 +606,8 @@ __global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__
       }
       const int i = rec[0], k0 = rec[1], kd = rec[2], k1 = rec[3], ra = rec[4], rb = rec[5];
       const int nlow = rec[6], npair = rec[7], nbk = k1 - k0;
+      double L[NV2];
+      bool have_d = false;  // the factored D_i still in registers (register path): no reload of what was just stored
       for (int q = ra * NV2; q < k0 * NV2; ++q) F[q] = A[q];
       for (int q = k1 * NV2; q < rb * NV2; ++q) F[q] = A[q];
       if (nlow < 0 || nbk > kSmallMaxB) {  // general per-block path
@@ -703,14 +706,21 @@ __global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__
         }
 #pragma unroll
         for (int b = 0; b < kSmallMaxB; ++b)
-          if (b < nbk)
+          if (b < nbk) {
 #pragma unroll
             for (int q = 0; q < NV2; ++q) F[(size_t)(k0 + b) * NV2 + q] = B[b][q];
+            if (diag_regs && b == kd - k0) {
+#pragma unroll
+              for (int q = 0; q < NV2; ++q) L[q] = B[b][q];
+              have_d = true;
+            }
+          }
       }
       // inv(D_i) (Gauss elimination per unit column, factor once)
-      double L[NV2];
+      if (!have_d) {
 #pragma unroll
-      for (int q = 0; q < NV2; ++q) L[q] = F[(size_t)kd * NV2 + q];
+        for (int q = 0; q < NV2; ++q) L[q] = F[(size_t)kd * NV2 + q];
+      }
       {
         const double w = L[2] / L[0];
         L[3] -= w * L[1];
@@ -1357,7 +1367,8 @@ int rx_la_ilu_build(rx_ctx* ctx) {
     k_ilu_build_2<<<ctx->npart, 256, 0, ctx->stream>>>(ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_plan,
                                                        reinterpret_cast<const int4*>(ctx->fs.slot), ctx->rp, ctx->col,
                                                        ctx->upd_ptr, reinterpret_cast<const int2*>(ctx->upd),
-                                                       ctx->f[RX_F_JAC], ctx->f[RX_F_ILU], rx_invd_buf(ctx));
+                                                       ctx->f[RX_F_JAC], ctx->f[RX_F_ILU], rx_invd_buf(ctx),
+                                                       getenv("RX_ILU2_RELOAD") == nullptr);
     RX_HIP(hipGetLastError());
     return RX_OK;
   }
