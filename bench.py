@@ -125,9 +125,11 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
     }
 
 
-def pmc_traffic(kernel, workload_key):
+def pmc_traffic(kernel, workload_key, field="hbm_bytes"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/r*_pmc*.json, written by
-    tools/pmc_summary.py; the newest file taken on this workload wins); else None."""
+    tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the guide's gfx950 correction; field "hbm_bytes_calibrated"
+    for the SpMV-calibrated figure). The file's workload key must equal bench.py's (`c3 2000x500 ns7 parts256`);
+    the newest file on this workload wins; else None."""
     import glob
     for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")), reverse=True):
         try:
@@ -139,7 +141,7 @@ def pmc_traffic(kernel, workload_key):
             continue
         ks = [d.get("kernels", {}).get(p) for p in kernel.split("+")]  # "a+b": both launches of one phase
         if all(k is not None for k in ks):
-            return sum(k["hbm_bytes"] for k in ks)
+            return sum(k.get(field, k["hbm_bytes"]) for k in ks)
     return None
 
 
@@ -384,8 +386,10 @@ def main():
                    launches=int(n))
         if m["unit"] == "GB/s":
             t = pmc_traffic(m["kernel"], wkey)
+            tc = pmc_traffic(m["kernel"], wkey, "hbm_bytes_calibrated")
             out["algorithmic_bytes"] = int(m["work"])
             out["traffic"] = None if t is None else int(t)
+            out["traffic_spmv_calibrated"] = None if tc is None else int(tc)
         else:
             out["algorithmic_flops"] = int(m["work"])
             out["traffic"] = None

@@ -711,8 +711,19 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
         raise RxError(f"SPECIES_ORDER {order} does not match the library's {names}")
     ns = len(names)
     f = lambda k, d: float(c.get(k, d))
-    tf = c.get("TIME_DISCRE_FLOW", "RUNGE-KUTTA_EXPLICIT")
-    prec = {"ILU": 1, "ILU0": 1, "LU_SGS": 0}[c.get("LINEAR_SOLVER_PREC", "ILU")]
+    # keys this path does not implement are rejected, not ignored (CConfig defaults: CFL_ADAPT NO, MGLEVEL 0,
+    # config_structure.cpp:985, 1128)
+    if c.get("CFL_ADAPT", "NO").upper() != "NO":
+        raise RxError("case_from_cfg: CFL_ADAPT= YES is not supported on this path")
+    if int(c.get("MGLEVEL", "0")) != 0:
+        raise RxError("case_from_cfg: MGLEVEL > 0 is not supported on this path (the jet cfgs run MGLEVEL= 0)")
+    # CConfig defaults (config_structure.cpp): TIME_DISCRE_FLOW EULER_IMPLICIT (:1026), LINEAR_SOLVER_PREC LU_SGS
+    # (:1050), RK_ALPHA_COEFF one stage of 1.0 (:3038-3041)
+    tf = c.get("TIME_DISCRE_FLOW", "EULER_IMPLICIT")
+    prec_kw = c.get("LINEAR_SOLVER_PREC", "LU_SGS")
+    if prec_kw not in ("ILU", "ILU0", "LU_SGS"):
+        raise RxError(f"case_from_cfg: LINEAR_SOLVER_PREC= {prec_kw} is not supported on this path")
+    prec = {"ILU": 1, "ILU0": 1, "LU_SGS": 0}[prec_kw]
     order_map = {"1ST_ORDER": 0, "2ND_ORDER": 1, "2ND_ORDER_LIMITER": 2}
     flow_cfg = dict(mach_inf=f("MACH_NUMBER", 0.0), cfl=f("CFL_NUMBER", 1.25), max_delta_time=f("MAX_DELTA_TIME", 1e6),
                     prandtl_lam=f("PRANDTL_LAM", 0.72), prandtl_turb=f("PRANDTL_TURB", 0.9),
@@ -729,7 +740,9 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
     sst_cfg_kw = dict(implicit=int(c.get("TIME_DISCRE_TURB", "EULER_IMPLICIT") == "EULER_IMPLICIT"),
                       lin_tol=flow_cfg["lin_tol"], lin_iter=flow_cfg["lin_iter"], lin_prec=prec,
                       relaxation_turb=f("RELAXATION_FACTOR_TURB", 1.0), cfl_red_turb=f("CFL_REDUCTION_TURB", 1.0))
-    rk = [float(x) for x in _cfg_list(c.get("RK_ALPHA_COEFF", "(0.66667, 0.66667, 1.0)"))] \
+    if tf not in ("EULER_IMPLICIT", "EULER_EXPLICIT", "RUNGE-KUTTA_EXPLICIT"):
+        raise RxError(f"case_from_cfg: TIME_DISCRE_FLOW= {tf} is not supported on this path")
+    rk = ([float(x) for x in _cfg_list(c["RK_ALPHA_COEFF"])] if "RK_ALPHA_COEFF" in c else [1.0]) \
         if tf == "RUNGE-KUTTA_EXPLICIT" else None
     # boundary markers, mesh marker order
     inlets = _cfg_list(c.get("MARKER_INLET", ""))

@@ -551,15 +551,30 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   if (ctx->cfg.implicit && !sst) {
     CK(dalloc(ctx, &ctx->fconv, E * nv));
     CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
-    CK(dalloc(ctx, &ctx->jvisc, E * 2 * (int64_t)nv * nv));
-    // visc_summary_size<NS, NDIM> per edge, in tiles of rx::kSummTile edges
-    CK(dalloc(ctx, &ctx->vsumm, (E + rx::kSummTile - 1) / rx::kSummTile * rx::kSummTile *
-                                    (int64_t)(14 + 5 * ctx->nDim + 9 * ns)));
+    // The per-edge viscous Jacobians and the viscous summary live only between the viscous sweep and the assembly
+    // (k_visc_edge -> k_visc_jac -> k_assemble); the ILU(0) factor is written only later, by the ILU build of the
+    // implicit step. So both share the ILU buffer when it is large enough (on the jet meshes it is: (2N + 2E) nVar^2
+    // doubles against 2E nVar^2 + E (14 + 5 nDim + 9 Ns)): at C5 (8M points, nVar 12) this saves 71.6 GB, which is
+    // what lets the whole 1000x400x20 mesh fit one 288 GB MI355X. Otherwise they get their own buffers.
+    const int64_t jv_n = E * 2 * (int64_t)nv * nv;
+    const int64_t vs_n = (E + rx::kSummTile - 1) / rx::kSummTile * rx::kSummTile *
+                         (int64_t)(14 + 5 * ctx->nDim + 9 * ns);  // visc_summary_size<NS, NDIM> per edge, tiled
+    const int64_t vs_off = (jv_n + 255) / 256 * 256;             // 2 KiB-aligned summary tiles
+    if (vs_off + vs_n <= sizes[RX_F_ILU]) {
+      ctx->jvisc = ctx->f[RX_F_ILU];
+      ctx->vsumm = ctx->f[RX_F_ILU] + vs_off;
+      ctx->scratch_in_ilu = 1;
+    } else {
+      CK(dalloc(ctx, &ctx->jvisc, jv_n));
+      CK(dalloc(ctx, &ctx->vsumm, vs_n));
+    }
     CK(dalloc(ctx, &ctx->jsrc, (N + kSrcTile - 1) / kSrcTile * kSrcTile * (int64_t)ctx->ns * nv));
     CK(dalloc(ctx, &ctx->rsrc, N * nv));
   }
   if (ctx->cfg.implicit) {
-    CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
+    // LU-SGS's factorised diagonal blocks: only with the LU_SGS preconditioner (rx_lusgs_apply allocates them on
+    // first use otherwise)
+    if (ctx->cfg.lin_prec == 0) CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->xstar, N * nv));
   }
   if (!sst && ctx->cfg.spatial_order) CK(dalloc(ctx, &ctx->recon, E * 2 * (int64_t)(ctx->nPV + nv)));
@@ -602,7 +617,8 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->grad_list, ctx->sendbuf, ctx->rms_sum,
-                  ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->jvisc, ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
+                  ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,
+                  ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   rx_comm_free(ctx);
   if (ctx->kind == RX_KIND_FLOW) rx_bc_free(ctx);
@@ -785,6 +801,7 @@ int rx_lusgs_apply(rx_ctx* ctx, rx_field b, rx_field x) {
   if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
+  if (!ctx->dlu) RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->dlu), sizeof(double) * ctx->N * ctx->nVar * ctx->nVar));
   RxPhase ph(ctx, RX_K_LUSGS);
   if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
   return rx_la_lusgs(ctx, ctx->f[RX_F_JAC], ctx->f[b], ctx->f[x], nullptr, nullptr);

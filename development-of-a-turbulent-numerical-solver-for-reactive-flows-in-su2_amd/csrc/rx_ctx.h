@@ -114,6 +114,7 @@ struct rx_ctx {
   double* jconv = nullptr;   // [E][2][nVar*nVar]
   double* jvisc = nullptr;   // [E][2][nVar*nVar]
   double* vsumm = nullptr;   // [E/kSummTile][visc_summary_size][kSummTile] per-edge viscous summary (implicit)
+  int scratch_in_ilu = 0;    // jvisc / vsumm alias the ILU buffer (dead before the ILU build writes it)
   double* jsrc = nullptr;    // [ceil(N/kSrcTile)][ns*nVar][kSrcTile] species rows of the source Jacobians
   double* rsrc = nullptr;    // [N][nVar] source residual (implicit path)
   double* uold = nullptr;    // [N][nVar] Solution_Old of the RK stages

@@ -1440,6 +1440,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
 }
 
 int rx_la_diag_factor(rx_ctx* ctx, const double* A) {
+  if (!ctx->dlu) return RX_ERR_STATE;  // LU-SGS factor storage (allocated with the LU_SGS preconditioner)
   RX_NV_SWITCH(ctx->nVar, (k_diag_factor<NV_><<<(int)((ctx->Nd + 3) / 4), 256, 0, ctx->stream>>>(
                               (int)ctx->Nd, ctx->diag, A, ctx->dlu)));
   RX_HIP(hipGetLastError());
@@ -1447,6 +1448,7 @@ int rx_la_diag_factor(rx_ctx* ctx, const double* A) {
 }
 
 int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, int* done, const int* conv) {
+  if (!ctx->dlu) return RX_ERR_STATE;
   RX_NV_SWITCH(ctx->nVar, (k_lusgs_fwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->diag, A,
                               ctx->dlu, b, ctx->xstar, done, conv)));

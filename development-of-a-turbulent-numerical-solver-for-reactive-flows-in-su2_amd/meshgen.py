@@ -90,27 +90,44 @@ def median_dual3d(pts, hexes, bnd):
     (:9595-9660, 3-D branch) with CVertex::SetNodes_Coord (dual_grid_structure.cpp:589-616). Sums are taken in
     numpy order (the reference's element order gives the same values up to rounding)."""
     n = len(pts)
-    ecg = pts[hexes].mean(axis=1)                                     # (nE, 3)
-    fnodes = hexes[:, HEX_FACES]                                      # (nE, 6, 4)
-    fcg = pts[fnodes].mean(axis=2)                                    # (nE, 6, 3)
-    fi = fnodes.reshape(-1, 4)
-    fj = np.roll(fnodes, -1, axis=2).reshape(-1, 4)
-    fi, fj = fi.ravel(), fj.ravel()                                   # (nE*24,)
-    F = np.repeat(fcg.reshape(-1, 3), 4, axis=0)
-    E = np.repeat(ecg, 24, axis=0)
-    lo, hi = np.minimum(fi, fj), np.maximum(fi, fj)
-    ukey, inv = np.unique(lo * n + hi, return_inverse=True)
-    edges = np.stack([ukey // n, ukey % n], axis=1).astype(np.int64)
+    hexes = np.asarray(hexes, dtype=np.int64)
+    edges = element_edges(n, hexes)  # the face edges' set
+    ukey = edges[:, 0] * n + edges[:, 1]
     emid = 0.5 * (pts[edges[:, 0]] + pts[edges[:, 1]])
-    e = emid[inv]
-    contrib = 0.5 * np.cross(E - e, F - e)
-    contrib[fi > fj] *= -1.0
     normal = np.zeros((len(edges), 3))
-    np.add.at(normal, inv, contrib)
     vol = np.zeros(n)
-    for P_ in (fi, fj):
-        P = pts[P_]
-        np.add.at(vol, P_, np.abs(np.einsum("ij,ij->i", E - P, np.cross(e - P, F - P))) / 6.0)
+    # elements in chunks of `blk` (bounded host memory at C5's 7.6 M hexahedra); np.add.at accumulates in element
+    # order either way, and the volume pass keeps its two sweeps (all i ends, then all j ends)
+    blk = 1 << 19
+
+    def faces(c0, c1):
+        h = hexes[c0:c1]
+        ecg = pts[h].mean(axis=1)                                     # (nE, 3)
+        fnodes = h[:, HEX_FACES]                                      # (nE, 6, 4)
+        fcg = pts[fnodes].mean(axis=2)                                # (nE, 6, 3)
+        fi = fnodes.reshape(-1, 4).ravel()
+        fj = np.roll(fnodes, -1, axis=2).reshape(-1, 4).ravel()      # (nE*24,)
+        F = np.repeat(fcg.reshape(-1, 3), 4, axis=0)
+        E = np.repeat(ecg, 24, axis=0)
+        inv = np.searchsorted(ukey, np.minimum(fi, fj) * n + np.maximum(fi, fj))
+        return fi, fj, F, E, inv
+
+    vj = []  # the j ends' volume terms, added after every i end's
+    for c0 in range(0, len(hexes), blk):
+        fi, fj, F, E, inv = faces(c0, c0 + blk)
+        e = emid[inv]
+        contrib = 0.5 * np.cross(E - e, F - e)
+        contrib[fi > fj] *= -1.0
+        np.add.at(normal, inv, contrib)
+        for end, P_ in enumerate((fi, fj)):
+            P = pts[P_]
+            t = np.abs(np.einsum("ij,ij->i", E - P, np.cross(e - P, F - P))) / 6.0
+            if end == 0:
+                np.add.at(vol, P_, t)
+            else:
+                vj.append((P_, t))
+    for P_, t in vj:
+        np.add.at(vol, P_, t)
     nb_i = np.r_[edges[:, 0], edges[:, 1]]
     nb_j = np.r_[edges[:, 1], edges[:, 0]]
     order = np.lexsort((nb_j, nb_i))
@@ -154,6 +171,21 @@ def write_su2(path: str, pts, quads, bnd):
             f.write(f"MARKER_TAG= {name}\nMARKER_ELEMS= {len(lines)}\n")
             for l in lines:
                 f.write(f"{bnd_t} " + " ".join(str(int(v)) for v in l) + "\n")
+
+
+def element_edges(n, elems):
+    """The edge set (i < j, lexicographic) of a quad or hexahedral mesh: the edges median_dual2d / median_dual3d
+    produce, without their geometry (the partitioner and the RCM ordering need only the graph)."""
+    elems = np.asarray(elems, dtype=np.int64)
+    if elems.shape[1] == 4:
+        a, b = elems, np.roll(elems, -1, axis=1)
+    else:  # hexahedron: the 4 edges of the bottom face, of the top face, and the 4 vertical edges
+        a = np.concatenate([elems[:, :4], elems[:, 4:], elems[:, :4]], axis=1)
+        b = np.concatenate([np.roll(elems[:, :4], -1, axis=1), np.roll(elems[:, 4:], -1, axis=1), elems[:, 4:]],
+                           axis=1)
+    lo, hi = np.minimum(a, b).ravel(), np.maximum(a, b).ravel()
+    ukey = np.unique(lo * n + hi)
+    return np.stack([ukey // n, ukey % n], axis=1).astype(np.int64)
 
 
 def rcm_order(n, edges):
@@ -314,12 +346,12 @@ def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, nz: int = 0, 
     median_dual = median_dual3d if nz > 1 else median_dual2d
     part_ptr = np.array([0, len(pts)], dtype=np.int64)
     if n_part > 1:
-        d0 = median_dual(pts, quads, bnd)
-        perm, part_ptr = partition_order(len(pts), d0["edges"], partition_rcb(pts, n_part, edges=d0["edges"] if partitioner == "spacing" else None))
+        e0 = element_edges(len(pts), quads)
+        perm, part_ptr = partition_order(len(pts), e0, partition_rcb(pts, n_part,
+                                                                     edges=e0 if partitioner == "spacing" else None))
         pts, quads, bnd, _ = renumber(pts, quads, bnd, perm)
     elif rcm:
-        d0 = median_dual(pts, quads, bnd)
-        perm = rcm_order(len(pts), d0["edges"])
+        perm = rcm_order(len(pts), element_edges(len(pts), quads))
         pts, quads, bnd, _ = renumber(pts, quads, bnd, perm)
     dual = median_dual(pts, quads, bnd)
     dual["coord"] = pts
@@ -333,26 +365,33 @@ def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, nz: int = 0, 
 def normal_neighbor(coord, nbr_ptr, nbr, bvertex, bvertex_normal):
     """CPhysicalGeometry::FindNormal_Neighbor (Common/src/geometry_structure.cpp:12610-12652): for every boundary
     vertex the neighbour whose edge makes the largest cosine with the vertex normal (the last one on ties, the
-    reference's `>=`), with the reference's arithmetic."""
+    reference's `>=`), with the reference's arithmetic (per-component sums in dimension order, then
+    sp / (sqrt(nv) sqrt(nn)); evaluated for all (vertex, neighbour) pairs at once)."""
     coord = np.asarray(coord, dtype=np.float64)
     bv = np.asarray(bvertex)
-    out = np.zeros(len(bv), dtype=np.int64)
-    for b in range(len(bv)):
-        i = int(bv[b, 1])
-        n = np.asarray(bvertex_normal[b], dtype=np.float64)
-        best, cmax = 0, -1.0
-        for j in nbr[nbr_ptr[i]:nbr_ptr[i + 1]]:
-            sp = nv = nn = 0.0
-            for d in range(coord.shape[1]):
-                dc = coord[j, d] - coord[i, d]
-                sp += dc * n[d]
-                nv += dc * dc
-                nn += n[d] * n[d]
-            c = sp / (np.sqrt(nv) * np.sqrt(nn))
-            if c >= cmax:
-                best, cmax = int(j), c
-        out[b] = best
-    return out
+    nbr_ptr, nbr = np.asarray(nbr_ptr), np.asarray(nbr)
+    if len(bv) == 0:
+        return np.zeros(0, dtype=np.int64)
+    i = bv[:, 1].astype(np.int64)
+    cnt = nbr_ptr[i + 1] - nbr_ptr[i]
+    seg = np.repeat(np.arange(len(bv)), cnt)
+    start = np.cumsum(cnt) - cnt
+    j = nbr[np.repeat(nbr_ptr[i], cnt) + (np.arange(cnt.sum()) - np.repeat(start, cnt))]
+    n = np.asarray(bvertex_normal, dtype=np.float64)[seg]
+    sp = np.zeros(len(j))
+    nv = np.zeros(len(j))
+    nn = np.zeros(len(j))
+    for d in range(coord.shape[1]):
+        dc = coord[j, d] - coord[i[seg], d]
+        sp += dc * n[:, d]
+        nv += dc * dc
+        nn += n[:, d] * n[:, d]
+    c = sp / (np.sqrt(nv) * np.sqrt(nn))
+    cmax = np.maximum.reduceat(c, start)
+    # the last neighbour reaching the maximum (the loop's `c >= cmax` keeps moving to later ties)
+    pos = np.where(c == cmax[seg], np.arange(len(c)), -1)
+    last = np.maximum.reduceat(pos, start)
+    return j[last].astype(np.int64)
 
 
 WALLS = ("upper_wall", "lower_wall_pre", "lower_wall_post")  # the cfg's MARKER_ISOTHERMAL
@@ -363,7 +402,7 @@ def wall_distance(pts, bnd):
     viscous-wall markers; wall points get 0)."""
     from scipy.spatial import cKDTree
     wp = np.unique(np.concatenate([np.asarray(bnd[m]).ravel() for m in WALLS]))
-    d, _ = cKDTree(pts[wp]).query(pts)
+    d, _ = cKDTree(pts[wp]).query(pts, workers=-1)
     return np.ascontiguousarray(d, dtype=np.float64)
 
 

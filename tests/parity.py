@@ -36,3 +36,21 @@ def per_column_close(a, b, rtol=RTOL, floor=1e-6, what=""):
     for v in range(b.shape[1]):
         worst = max(worst, assert_close(a[:, v], b[:, v], rtol, floor, what=f"{what}[var {v}]"))
     return worst
+
+
+def species_close(U, Uo, nDim, rtol=RTOL, rho_floor=1e-8, what=""):
+    """Species partial densities compared elementwise: |a - b| <= rtol * max(|b|, rho_floor * rho_i) at every point
+    i, with rho_i the point's density (column 0 of U). A minor species at 1e-6 of its column's max is held to rtol
+    of its own value, not of the column max (per_column_close). Returns the worst relative error."""
+    U, Uo = np.asarray(U, dtype=np.float64), np.asarray(Uo, dtype=np.float64)
+    rho = np.abs(Uo[:, 0])
+    b = Uo[:, nDim + 2:]
+    den = np.maximum(np.abs(b), rho_floor * rho[:, None])
+    den = np.where(den == 0.0, 1.0, den)
+    e = np.abs(U[:, nDim + 2:] - b) / den
+    worst = float(e.max()) if e.size else 0.0
+    if worst > rtol:
+        i, s = np.unravel_index(int(np.argmax(e)), e.shape)
+        raise AssertionError(f"{what}: species {s} at point {i}: rel err {worst:.3e} > {rtol:.1e} "
+                             f"({U[i, nDim + 2 + s]!r} vs {b[i, s]!r}, rho {rho[i]!r})")
+    return worst

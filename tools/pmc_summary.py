@@ -1,16 +1,15 @@
 """Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs as
 MI355X_MICROARCH.md §rocprofv3 PMC slots requires) -> profiles/<name>.json used by bench.py.
 
-FETCH_SIZE and WRITE_SIZE are in KB per dispatch. On gfx950 FETCH_SIZE under-reads wide streaming
-loads (MI355X_MICROARCH.md §HBM: exactly 1/2 for 16-B-per-lane streams), so the read side is calibrated on
-a kernel with a known byte count in a coalesced streaming pattern: k_fg_spmv<nVar>, whose HBM reads are the
-BSR matrix stream (nnzb * nVar^2 * 8 bytes, read once, coalesced 8 B per lane; its column indices and x / y
-vectors are < 5 % and L2/Infinity-Cache resident at these sizes), so factor = matrix bytes / FETCH bytes (≈ 2,
-the guide's gfx950 correction).
-hbm_bytes = FETCH_SIZE*1024*factor + WRITE_SIZE*1024. Kernels are keyed by name with template arguments
-(k_fg_spmv<11>, k_fg_spmv<2>, ...), non-template kernels by name.
+FETCH_SIZE and WRITE_SIZE are in KB per dispatch. On gfx950 FETCH_SIZE reports exactly 1/2 of the bytes of a wide
+coalesced streaming read (MI355X_MICROARCH.md §HBM), so the guide's correction is applied:
+    hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+For comparison the file also carries a self-calibrated figure (hbm_bytes_calibrated): FETCH scaled so that
+k_fg_spmv<nVar> reads exactly its BSR matrix stream (nnzb * nVar^2 * 8 bytes); that calibration is circular for that
+kernel and is not what bench.py reports. Kernels are keyed by name with template arguments (k_fg_spmv<11>, ...),
+non-template kernels by name. The workload key must be bench.py's (`<workload> <dims> ns<Ns> parts<P>`).
 
-python tools/pmc_summary.py <fetch_dir> <write_dir> <workload_key> <nVar> <nnzb> > profiles/r02_pmc_<wl>.json
+python tools/pmc_summary.py <fetch_dir> <write_dir> "<workload key>" <nVar> <nnzb> > profiles/r03_pmc_<wl>.json
 """
 import csv
 import glob
@@ -46,7 +45,7 @@ def main():
     cal = [f"k_fg_spmv<{nv}>"]
     cal_kb = fe.get((cal[0], "FETCH_SIZE"))
     factor = known / (cal_kb * 1024.0) if cal_kb else 1.0
-    out = {"workload": wkey,
+    out = {"workload": wkey, "fetch_factor": 2.0,
            "calibration": {"kernel": cal[0] if cal else None, "known_bytes": known, "fetch_kb": cal_kb, "factor": factor},
            "kernels": {}}
     names = sorted({k for (k, c) in fe} | {k for (k, c) in wr})
@@ -55,7 +54,8 @@ def main():
         w = wr.get((k, "WRITE_SIZE"))
         if f is None or w is None:
             continue
-        out["kernels"][k] = {"fetch_kb": f, "write_kb": w, "hbm_bytes": f * 1024.0 * factor + w * 1024.0}
+        out["kernels"][k] = {"fetch_kb": f, "write_kb": w, "hbm_bytes": 2.0 * f * 1024.0 + w * 1024.0,
+                             "hbm_bytes_calibrated": f * 1024.0 * factor + w * 1024.0}
     json.dump(out, sys.stdout, indent=1)
     print()
 
