@@ -79,7 +79,8 @@ class Cfg(C.Structure):
                 ("lin_prec", C.c_int32), ("spatial_order", C.c_int32), ("clip_temp", C.c_int32),
                 ("t_min", C.c_double), ("t_max", C.c_double), ("p_ref", C.c_double), ("visc_ref", C.c_double),
                 ("cond_ref", C.c_double), ("vel_ref", C.c_double), ("len_ref", C.c_double),
-                ("slope_limiter", C.c_int32)]
+                ("slope_limiter", C.c_int32), ("ignition", C.c_int32), ("fuel_index", C.c_int32),
+                ("oxidizer_index", C.c_int32), ("ignition_iter", C.c_int64), ("ignition_temp", C.c_double)]
 
 
 class BcDesc(C.Structure):
@@ -281,7 +282,9 @@ def default_cfg(**kw):
              prandtl_turb=0.9, lewis_turb=1.2, c_mu=0.09, pasr_lb=0.2, cfl=5.0, max_delta_time=1e6,
              ref_elem_length=0.1, limiter_coeff=0.5, lin_tol=1e-6, relaxation=1.0, implicit=1, rans=1, lin_iter=5,
              lin_prec=1, spatial_order=0, clip_temp=0, t_min=200.0, t_max=6000.0, p_ref=1.0, visc_ref=1.0,
-             cond_ref=1.0, vel_ref=1.0, len_ref=1.0, slope_limiter=0)
+             cond_ref=1.0, vel_ref=1.0, len_ref=1.0, slope_limiter=0,
+             # CConfig defaults (config_structure.cpp:591-603)
+             ignition=0, fuel_index=0, oxidizer_index=2, ignition_iter=999999, ignition_temp=1700.0)
     c.update(kw)
     cfg = Cfg()
     for k, v in c.items():
@@ -736,7 +739,10 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
                     slope_limiter={"VENKATAKRISHNAN": 0, "BARTH_JESPERSEN": 1}[c.get("SLOPE_LIMITER_FLOW",
                                                                                      "VENKATAKRISHNAN")],
                     t_min=f("TEMPERATURE_MIN", 200.0), t_max=f("TEMPERATURE_MAX", 6000.0),
-                    clip_temp=int(c.get("CLIPPING_TEMPRATURE", "NO") == "YES"))
+                    clip_temp=int(c.get("CLIPPING_TEMPRATURE", "NO") == "YES"),
+                    ignition=int(c.get("IGNITION", "NO").upper() == "YES"), fuel_index=int(f("FUEL_INDEX", 0)),
+                    oxidizer_index=int(f("OXIDIZER_INDEX", 2)), ignition_iter=int(f("IGNITION_ITER", 999999)),
+                    ignition_temp=f("IGNITION_TEMPERATURE", 1700.0))
     sst_cfg_kw = dict(implicit=int(c.get("TIME_DISCRE_TURB", "EULER_IMPLICIT") == "EULER_IMPLICIT"),
                       lin_tol=flow_cfg["lin_tol"], lin_iter=flow_cfg["lin_iter"], lin_prec=prec,
                       relaxation_turb=f("RELAXATION_FACTOR_TURB", 1.0), cfl_red_turb=f("CFL_REDUCTION_TURB", 1.0))

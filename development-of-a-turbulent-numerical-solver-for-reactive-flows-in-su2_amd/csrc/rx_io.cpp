@@ -1009,11 +1009,12 @@ int rx_restart_write(const char* path, const rx_mesh* m, int32_t n_var, const do
       for (int v = 0; v < 5; ++v) f << std::scientific << extra[i * 5 + v] << "\t";
     f << "\n";
   }
-  f.unsetf(std::ios::floatfield);
-  f << "AOA= " << 0 << "\n";
-  f << "SIDESLIP_ANGLE= " << 0 << "\n";
-  f << "INITIAL_BCTHRUST= " << 4000 << "\n";
-  f << "DCD_DCL_VALUE= " << 0 << "\n";
+  // trailer (output_structure.cpp:4056-4065): the doubles AoA - offset, AoS - offset, INITIAL_BCTHRUST (CConfig
+  // default 4000) and dCD/dCL, still in scientific at precision 15; then the integer EXT_ITER (+ 1)
+  f << "AOA= " << 0.0 << "\n";
+  f << "SIDESLIP_ANGLE= " << 0.0 << "\n";
+  f << "INITIAL_BCTHRUST= " << 4000.0 << "\n";
+  f << "DCD_DCL_VALUE= " << 0.0 << "\n";
   f << "EXT_ITER= " << ext_iter + 1 << "\n";
   return f ? RX_OK : RX_ERR_STATE;
 }

@@ -102,6 +102,8 @@ __global__ __launch_bounds__(kBlock) void k_ausm_node(int N, const int32_t* __re
 struct PrimParams {
   double Tmin, Tmax, T_ref, E_ref, R_ref, P_ref, Visc_ref, Cond_ref, Vel_ref, Len_ref;
   int ext_iter, clip_temp, rans;
+  int ignite, fuel, oxidizer;  // ignition branch active at this ext_iter (IGNITION and ext_iter < IGNITION_ITER)
+  double T_ign;
 };
 
 template <int NS>
@@ -374,6 +376,11 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, Dev
   if (e4 != ERR_NONE) {
     if (atomicCAS(err, 0, ERR_RANGE) == 0) err[1] = i;
   }
+  // ignition (SetPrimitive_Variables solver_direct_reactive.cpp:1013-1024): after SetPrimVar only the record's
+  // temperature is overwritten (CReactiveEulerVariable::SetTemperature, variable_reactive.hpp:602-607); the
+  // derivatives and transport above keep the secant's temperature, as in the reference
+  if (P.ignite && V[RHOS + P.fuel] > 0.4 && V[RHOS + P.oxidizer] > 0.2 && V[0] < P.T_ign)
+    Vg[(size_t)i * nPV] = P.T_ign;
 }
 
 // a2 second order: MUSCL reconstruction of (T, u, v, P) per edge side with the optional limiter, and the
@@ -1249,8 +1256,11 @@ int rx_check_error(rx_ctx* ctx) {
 
 int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter) {
   const rx_cfg& c = ctx->cfg;
+  const int ignite = c.ignition && (int64_t)ext_iter < c.ignition_iter ? 1 : 0;
+  if (ignite && (c.fuel_index < 0 || c.fuel_index >= ctx->ns || c.oxidizer_index < 0 || c.oxidizer_index >= ctx->ns))
+    return RX_ERR_ARG;
   PrimParams P{c.t_min, c.t_max, c.T_ref, c.E_ref, c.R_ref, c.p_ref, c.visc_ref, c.cond_ref, c.vel_ref, c.len_ref,
-               ext_iter, c.clip_temp, c.rans};
+               ext_iter, c.clip_temp, c.rans, ignite, c.fuel_index, c.oxidizer_index, c.ignition_temp};
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_set_primitive<NS_, ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->mech, P, ctx->f[RX_F_U], ctx->f[RX_F_V], ext_iter > 0 ? ctx->uold : nullptr,
                             ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_DPDU], ctx->f[RX_F_DTDU], ctx->f[RX_F_MU],

@@ -118,6 +118,14 @@ typedef struct {
   double t_min, t_max;    /* TEMPERATURE_MIN / TEMPERATURE_MAX (Cons2PrimVar secant / bisection bounds) */
   double p_ref, visc_ref, cond_ref, vel_ref, len_ref;  /* Pressure/Viscosity/Conductivity/Velocity/Length_Ref */
   int32_t slope_limiter;  /* SLOPE_LIMITER_FLOW: rx_slope_limiter (SetPrimitive_Limiter :1383 / :1443) */
+  /* IGNITION / IGNITION_ITER / IGNITION_TEMPERATURE / FUEL_INDEX / OXIDIZER_INDEX (config_structure.cpp:591-603;
+   * defaults 0, 999999, 1700, 0, 2): SetPrimitive_Variables (solver_direct_reactive.cpp:1013-1024) sets the record's
+   * temperature to ignition_temp at points with Y_fuel > 0.4, Y_oxidizer > 0.2 and T < ignition_temp while the
+   * outer iteration (rx_set_primitive's ext_iter) is below ignition_iter; the rest of the record keeps the
+   * secant's temperature. */
+  int32_t ignition, fuel_index, oxidizer_index;
+  int64_t ignition_iter;
+  double ignition_temp;
 } rx_cfg;
 
 typedef enum { RX_LIMITER_VENKATAKRISHNAN = 0, RX_LIMITER_BARTH_JESPERSEN = 1 } rx_slope_limiter;

