@@ -455,6 +455,8 @@ __global__ __launch_bounds__(kApplyBlock) void k_bc_apply(const int32_t* __restr
                                                           const double* __restrict__ kappa,
                                                           const double* __restrict__ dTdU,
                                                           const double* __restrict__ eddy,
+                                                          const double* __restrict__ dPdU,
+                                                          const double* __restrict__ tke,
                                                           const int32_t* __restrict__ rp,
                                                           const int32_t* __restrict__ col,
                                                           const int64_t* __restrict__ diag,
@@ -473,10 +475,34 @@ __global__ __launch_bounds__(kApplyBlock) void k_bc_apply(const int32_t* __restr
   double* D = A ? A + diag[i] * nVar2 : nullptr;
   double r = (q < nVar) ? Ri[q] : 0.0;
   double dq = (D && ent) ? D[q] : 0.0;
-  // weak markers (inlet, outlet) in marker / vertex order
+  // weak markers (inlet, outlet, Euler wall) in marker / vertex order
   for (int k = bn_ptr[t]; k < bn_ptr[t + 1]; ++k) {
     const int b = bn_vtx[k];
     const int kind = mkind[bmark[b]];
+    if (kind == RX_BC_EULER) {
+      // BC_Euler_Wall (:2881-2966): Residual[RHOVX + d] = P n_d A + 2/3 rho k n_d A with n = -Normal / Area,
+      // LinSysRes.AddBlock (every entry, zeros included); Jacobian_i momentum rows dPdU[c] n_d A, AddBlock
+      double Area = 0.0;
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) Area += bnrm[(size_t)b * NDIM + d] * bnrm[(size_t)b * NDIM + d];
+      Area = sqrt(Area);
+      const double Pi = V[(size_t)i * nPV + NDIM + 1], rho = V[(size_t)i * nPV + NDIM + 2];
+      const double ke = B.rans ? tke[i] : 0.0;
+      if (q < nVar) {
+        double res = 0.0;
+        if (q >= 1 && q <= NDIM) {
+          const double un = -bnrm[(size_t)b * NDIM + q - 1] / Area;
+          res = Pi * un * Area + 2.0 / 3.0 * rho * ke * un * Area;
+        }
+        r += res;
+      }
+      if (D && ent) {
+        double J = 0.0;
+        if (a >= 1 && a <= NDIM) J = dPdU[(size_t)i * nVar + c] * (-bnrm[(size_t)b * NDIM + a - 1] / Area) * Area;
+        dq += J;
+      }
+      continue;
+    }
     if (kind != RX_BC_INLET && kind != RX_BC_OUTLET) continue;
     if (q < nVar) {
       r += resc[(size_t)b * nVar + q];
@@ -487,11 +513,28 @@ __global__ __launch_bounds__(kApplyBlock) void k_bc_apply(const int32_t* __restr
       dq -= jacv[(size_t)b * 2 * nVar2 + q];
     }
   }
-  // strong markers: BC_Isothermal_Wall (:5441-5710)
+  // strong markers: BC_Isothermal_Wall (:5441-5710), BC_HeatFlux_Wall (:5717-5911)
   bool walled = false;
   for (int k = bn_ptr[t]; k < bn_ptr[t + 1]; ++k) {
     const int b = bn_vtx[k];
     const int mk = bmark[b];
+    if (mkind[mk] == RX_BC_HEATFLUX) {
+      // SetVelocity_Old(0) (in the update, bc_wall), momentum rows of the residual zeroed, Res_Conv = 0 added,
+      // Res_Visc[RHOE] = q A subtracted, then DeleteValsRowi on the momentum rows (no Jacobian_i without grid motion)
+      walled = true;
+      double Area = 0.0;
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) Area += bnrm[(size_t)b * NDIM + d] * bnrm[(size_t)b * NDIM + d];
+      Area = sqrt(Area);
+      const double resE = mdata[(size_t)mk * B.W + 1] * Area;
+      if (q < nVar) {
+        if (q >= 1 && q <= NDIM) r = 0.0;
+        r += 0.0;
+        r -= (q == E_) ? resE : 0.0;
+      }
+      if (D && ent && a >= 1 && a <= NDIM) dq = (a == c) ? 1.0 : 0.0;
+      continue;
+    }
     if (mkind[mk] != RX_BC_ISOTHERMAL) continue;
     walled = true;
     const double* md = mdata + (size_t)mk * B.W;
@@ -641,7 +684,8 @@ __global__ __launch_bounds__(kBlock) void k_sst_bc(int nbn, const int32_t* __res
   }
   for (int k = bn_ptr[t]; k < bn_ptr[t + 1]; ++k) {
     const int b = bn_vtx[k];
-    if (mkind[bmark[b]] != RX_BC_ISOTHERMAL) continue;
+    // BC_Isothermal_Wall (:3142-3196) and BC_HeatFlux_Wall (:3087-3140) set the same wall values
+    if (mkind[bmark[b]] != RX_BC_ISOTHERMAL && mkind[bmark[b]] != RX_BC_HEATFLUX) continue;
     const int j = bpn[b];
     double distance = 0.0;
 #pragma unroll
@@ -786,7 +830,7 @@ int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
   if (bc->inlet_kind < RX_INLET_TOTAL_CONDITIONS || bc->inlet_kind > RX_INLET_TEMPERATURE_IMPOSE) return RX_ERR_ARG;
   const int nM = bc->n_marker, W = 6 + ctx->ns, nd = ctx->nDim;
   for (int k = 0; k < nM; ++k)
-    if (bc->kind[k] < RX_BC_NONE || bc->kind[k] > RX_BC_ISOTHERMAL) return RX_ERR_ARG;
+    if (bc->kind[k] < RX_BC_NONE || bc->kind[k] > RX_BC_EULER) return RX_ERR_ARG;
   std::vector<int32_t> node(NB), pn(NB), mark(NB), weak;
   std::vector<uint8_t> wall(ctx->N, 0);
   for (int64_t b = 0; b < NB; ++b) {
@@ -797,7 +841,7 @@ int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
     mark[b] = (int32_t)mk;
     const int kd = bc->kind[mk];
     if ((kd == RX_BC_INLET || kd == RX_BC_OUTLET) && p < ctx->Nd) weak.push_back((int32_t)b);
-    if (kd == RX_BC_ISOTHERMAL && p < ctx->Nd) wall[p] = 1;
+    if ((kd == RX_BC_ISOTHERMAL || kd == RX_BC_HEATFLUX) && p < ctx->Nd) wall[p] = 1;
   }
   // owned boundary points and their vertices in (marker, vertex) = input order
   std::vector<int32_t> cnt(ctx->N + 1, 0);
@@ -878,7 +922,8 @@ int rx_bc_flow(rx_ctx* ctx) {
     RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_bc_apply<NS_, ND_><<<ctx->bc_nbn, kApplyBlock, 0, ctx->stream>>>(
                               ctx->bc_bn, ctx->bc_bn_ptr, ctx->bc_bn_vtx, ctx->bc_mark, ctx->bc_pn,
                               ctx->bc_nrm, ctx->bc_mkind, ctx->bc_mdata, B, ctx->mech, ctx->coord, ctx->f[RX_F_U],
-                              ctx->f[RX_F_V], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DTDU], ctx->f[RX_F_EDDY], ctx->rp,
+                              ctx->f[RX_F_V], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DTDU], ctx->f[RX_F_EDDY],
+                              ctx->f[RX_F_DPDU], ctx->f[RX_F_TKE], ctx->rp,
                               ctx->col, ctx->diag, ctx->bc_resc, ctx->bc_resv, ctx->bc_jacc, ctx->bc_jacv,
                               ctx->f[RX_F_RES], A, ctx->err)));
     RX_HIP(hipGetLastError());

@@ -264,7 +264,16 @@ int rx_sst_postprocessing(rx_ctx *turb);
  * temperature). RX_BC_NONE: a marker with no action — MARKER_SYM, which the reactive and turbulent solvers leave to
  * the empty CSolver::BC_Sym_Plane (solver_structure.inl:731-732) / CTurbSolver::BC_Sym_Plane
  * (solver_direct_turbulent.cpp:602-606); its vertices still enter SetTime_Step through rx_mesh_desc. */
-typedef enum { RX_BC_NONE = 0, RX_BC_INLET = 1, RX_BC_OUTLET = 2, RX_BC_ISOTHERMAL = 3 } rx_bc_kind;
+/* and, for the reference's turbulent flat plate (Test_Cases/TURBOLENT/TURBOLENT_FLAT_PLATE: MARKER_HEATFLUX,
+ * MARKER_EULER):
+ *   RX_BC_HEATFLUX    CReactiveNSSolver::BC_HeatFlux_Wall :5717-5911 (strong no-slip, rho E residual -= q A, data
+ *                     row a = the wall heat flux) / CTurbSSTSolver::BC_HeatFlux_Wall solver_direct_turbulent.cpp:
+ *                     3087-3140 (the isothermal wall's k = 0, omega = 60 mu / (rho beta_1 d^2))
+ *   RX_BC_EULER       CReactiveEulerSolver::BC_Euler_Wall :2881-2966 (weak: momentum += (p + 2/3 rho k) n A, the
+ *                     Jacobian's momentum rows += dP/dU n A) / CTurbSolver::BC_Euler_Wall (no action, :608-613) */
+typedef enum {
+  RX_BC_NONE = 0, RX_BC_INLET = 1, RX_BC_OUTLET = 2, RX_BC_ISOTHERMAL = 3, RX_BC_HEATFLUX = 4, RX_BC_EULER = 5
+} rx_bc_kind;
 typedef enum { RX_INLET_TOTAL_CONDITIONS = 0, RX_INLET_MASS_FLOW = 1, RX_INLET_TEMPERATURE_IMPOSE = 2 } rx_inlet_kind;
 typedef struct {
   int32_t n_marker;

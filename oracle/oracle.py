@@ -505,12 +505,18 @@ def sst_step(nDim, mesh, flow, T, TG, F1, F2, CDkw, dt, cfg, pattern=None, part_
                     F1=F1n, F2=F2n, CDkw=CDn, mut=mut)
 
 
+EULER_WALL = 1.0  # the reference's BC_TYPE enum value (Common/include/option_structure.hpp:750)
+
+
 def bc_prm(bc_params, mach_inf, prandtl_turb, lewis_turb):
     """Oracle BC parameter vector: the harness's bc_params[:18] (inlet kind, Tke_Inf, kine_Inf, omega_Inf, beta_1,
-    reference values, the reference's marker / inlet enum values) + (Mach_inf, Pr_t, Le_t)."""
-    p = np.zeros(21)
-    p[:18] = np.asarray(bc_params, dtype=np.float64)[:18]
-    p[18:] = (mach_inf, prandtl_turb, lewis_turb)
+    reference values, the reference's marker / inlet enum values) + (Mach_inf, Pr_t, Le_t) + the EULER_WALL enum
+    value (bc_params[27] of the newer harness dumps)."""
+    bp = np.asarray(bc_params, dtype=np.float64)
+    p = np.zeros(22)
+    p[:18] = bp[:18]
+    p[18:21] = (mach_inf, prandtl_turb, lewis_turb)
+    p[21] = bp[27] if len(bp) > 27 else EULER_WALL
     return p
 
 

@@ -322,7 +322,7 @@ int main(int argc, char** argv) {
                               cfg->GetCFL(MESH_0), cfg->GetLinear_Solver_Error(), (double)cfg->GetLinear_Solver_Iter(),
                               (double)cfg->GetKind_Linear_Solver_Prec(), cfg->GetRelaxation_Factor_Flow(),
                               cfg->GetRelaxation_Factor_Turb(), cfg->GetCFLRedCoeff_Turb(), cfg->GetMax_DeltaTime(),
-                              (double)SYMMETRY_PLANE};
+                              (double)SYMMETRY_PLANE, (double)EULER_WALL};
     dumpd("bc_params", bp, {(long)bp.size()});
     // the cfg values the other modes dump with their operators, same layouts
     dumpd("mach_inf", std::vector<double>{cfg->GetMach()}, {1});

@@ -2717,6 +2717,7 @@ struct BCPrm {
   double P_ref, vel_ref, T_ref, E_ref, R_ref, rho_ref;
   int k_inlet, k_outlet, k_iso, k_hf, k_total, k_massflow, k_timpose;  // the reference's enum values
   double mach_inf, Pr_t, Le_t;
+  int k_euler;                // EULER_WALL (option_structure.hpp:750)
   int implicit, rans;
 };
 
@@ -3030,6 +3031,53 @@ void flow_wall_vertex(const Mech& m, int nDim, const BCPrm& P, const double* md,
     for (int d = 0; d < nDim; ++d) delete_row(i, 1 + d, nVar, f.rp, f.col, f.A);
 }
 
+// CReactiveEulerSolver::BC_Euler_Wall (:2881-2966), no grid motion: momentum residual (p + 2/3 rho k) n A, n = -Normal / A,
+// added as a whole block; Jacobian_i's momentum rows dPdU n A, added as a whole block.
+void flow_euler_vertex(const Mech& m, int nDim, const BCPrm& P, int64_t i, const double* bn, BCField& f) {
+  const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5;
+  double Area = 0.0;
+  for (int d = 0; d < nDim; ++d) Area += bn[d] * bn[d];
+  Area = std::sqrt(Area);
+  double UnitNormal[3];
+  for (int d = 0; d < nDim; ++d) UnitNormal[d] = -bn[d] / Area;
+  const double Pressure = f.V[i * nPV + nDim + 1], Density = f.V[i * nPV + nDim + 2];
+  const double turb_ke = P.rans ? f.tke[i] : 0.0;
+  double Residual[32];
+  for (int v = 0; v < nVar; ++v) Residual[v] = 0.0;
+  for (int d = 0; d < nDim; ++d)
+    Residual[1 + d] = Pressure * UnitNormal[d] * Area + 2.0 / 3.0 * Density * turb_ke * UnitNormal[d] * Area;
+  double* Ri = f.R + i * nVar;
+  for (int v = 0; v < nVar; ++v) Ri[v] += Residual[v];
+  if (P.implicit) {
+    double J[32 * 32];
+    for (int q = 0; q < nVar * nVar; ++q) J[q] = 0.0;
+    const double* dPdU = f.dPdU + i * nVar;
+    for (int d = 0; d < nDim; ++d)
+      for (int v = 0; v < nVar; ++v) J[(1 + d) * nVar + v] = dPdU[v] * UnitNormal[d] * Area;
+    double* D = f.A + find_diag(f.rp, f.col, i) * nVar * nVar;
+    for (int q = 0; q < nVar * nVar; ++q) D[q] += J[q];
+  }
+}
+
+// CReactiveNSSolver::BC_HeatFlux_Wall (:5717-5911), no grid motion.
+void flow_heatflux_vertex(const Mech& m, int nDim, const BCPrm& P, const double* md, int64_t i, const double* bn,
+                          BCField& f) {
+  const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5;
+  double Area = 0.0;
+  for (int d = 0; d < nDim; ++d) Area += bn[d] * bn[d];
+  Area = std::sqrt(Area);
+  for (int d = 0; d < nDim; ++d) f.Uold[i * nVar + 1 + d] = 0.0 * f.V[i * nPV + nDim + 2];  // SetVelocity_Old
+  double* Ri = f.R + i * nVar;
+  for (int d = 0; d < nDim; ++d) Ri[1 + d] = 0.0;  // LinSysRes.SetBlock_Zero(iPoint, RHOVX + iDim)
+  double Res_Conv[32], Res_Visc[32];
+  for (int v = 0; v < nVar; ++v) Res_Conv[v] = Res_Visc[v] = 0.0;
+  Res_Visc[nDim + 1] = md[1] * Area;  // Wall_HeatFlux * Area
+  for (int v = 0; v < nVar; ++v) Ri[v] += Res_Conv[v];
+  for (int v = 0; v < nVar; ++v) Ri[v] -= Res_Visc[v];
+  if (P.implicit)
+    for (int d = 0; d < nDim; ++d) delete_row(i, 1 + d, nVar, f.rp, f.col, f.A);
+}
+
 BCPrm bc_params(const double* p, int implicit, int rans) {
   BCPrm P;
   P.kind_inlet = (int)p[0];
@@ -3053,6 +3101,7 @@ BCPrm bc_params(const double* p, int implicit, int rans) {
   P.mach_inf = p[18];
   P.Pr_t = p[19];
   P.Le_t = p[20];
+  P.k_euler = (int)p[21];
   P.implicit = implicit;
   P.rans = rans;
   return P;
@@ -3081,13 +3130,17 @@ int orc_bc_flow(void* h, int nDim, int64_t NB, const int64_t* bvert, const doubl
       for (int mk = 0; mk < nMarker; ++mk) {
         const double* md = mdata + (size_t)mk * W;
         const int kind = (int)md[0];
-        const bool weak = kind == P.k_inlet || kind == P.k_outlet;
-        const bool strong = kind == P.k_iso;
+        const bool weak = kind == P.k_inlet || kind == P.k_outlet || kind == P.k_euler;
+        const bool strong = kind == P.k_iso || kind == P.k_hf;
         if ((pass == 0 && !weak) || (pass == 1 && !strong)) continue;
         for (int64_t b = 0; b < NB; ++b) {
           if (bvert[3 * b] != mk) continue;
           const int64_t i = bvert[3 * b + 1];
-          if (pass == 0)
+          if (kind == P.k_euler)
+            flow_euler_vertex(m, nDim, P, i, bnormal + b * nDim, f);
+          else if (kind == P.k_hf)
+            flow_heatflux_vertex(m, nDim, P, md, i, bnormal + b * nDim, f);
+          else if (pass == 0)
             flow_weak_vertex(m, nDim, P, kind, md, i, pn[b], bnormal + b * nDim, f, charac + b * nPV);
           else
             flow_wall_vertex(m, nDim, P, md, i, pn[b], bnormal + b * nDim, f);
@@ -3111,8 +3164,8 @@ void orc_bc_sst(int nDim, int nPV, int64_t NB, const int64_t* bvert, const doubl
   for (int pass = 0; pass < 2; ++pass)
     for (int mk = 0; mk < nMarker; ++mk) {
       const int kind = (int)mdata[(size_t)mk * W];
-      const bool weak = kind == P.k_inlet || kind == P.k_outlet;
-      const bool strong = kind == P.k_iso;
+      const bool weak = kind == P.k_inlet || kind == P.k_outlet;  // CTurbSolver::BC_Euler_Wall: no action
+      const bool strong = kind == P.k_iso || kind == P.k_hf;      // BC_HeatFlux_Wall :3087-3140 = the isothermal wall
       if ((pass == 0 && !weak) || (pass == 1 && !strong)) continue;
       for (int64_t b = 0; b < NB; ++b) {
         if (bvert[3 * b] != mk) continue;

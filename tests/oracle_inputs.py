@@ -17,7 +17,7 @@ def outer_iteration_inputs(mesh, st, cfg, bc):
     nDim = int(np.shape(mesh["coord"])[1])
     bp = np.asarray(dict(np.load(os.path.join(GOLD, "bc9.npz")))["bc_params"])
     md = np.array(bc["data"], dtype=np.float64)
-    md[:, 0] = [{1: bp[11], 2: bp[12], 3: bp[13]}.get(int(k), -1.0) for k in bc["kind"]]
+    md[:, 0] = [{1: bp[11], 2: bp[12], 3: bp[13], 4: bp[14], 5: O.EULER_WALL}.get(int(k), -1.0) for k in bc["kind"]]
     bco = dict(marker=md, prm=O.bc_prm(bp, cfg.mach_inf, cfg.prandtl_turb, cfg.lewis_turb))
     c = dict(cfl=cfg.cfl, max_delta_time=cfg.max_delta_time, prandtl_lam=cfg.prandtl_lam,
              prandtl_turb=cfg.prandtl_turb, lewis_turb=cfg.lewis_turb, mach_inf=cfg.mach_inf, c_mu=cfg.c_mu,
