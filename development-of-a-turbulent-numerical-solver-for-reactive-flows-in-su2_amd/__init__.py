@@ -699,7 +699,7 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
     """The inputs of a reference REACTIVE_RANS case from its cfg (the keys of the shipped jet cfgs): the mesh
     (SU2Mesh: MESH_FILENAME), the library (read_mechanism: CONFIG_LIB_FILE), the flow and SST rx_cfg keyword sets,
     the boundary markers in the mesh's marker order (MARKER_INLET / INLET_TYPE / INLET_MASS_FRAC, MARKER_OUTLET,
-    MARKER_ISOTHERMAL, MARKER_SYM), the free-stream turbulence values of CReactiveEulerSolver::
+    MARKER_ISOTHERMAL, MARKER_HEATFLUX, MARKER_EULER, MARKER_SYM), the free-stream turbulence values of CReactiveEulerSolver::
     SetNondimensionalization (solver_direct_reactive.cpp:4534-4590: k = 3/2 (|V| I)^2, omega = rho k / (mu
     TURB2LAMVISC), rho = ComputeDensity, mu = ComputeEta) and TIME_DISCRE_FLOW / RK_ALPHA_COEFF. DIMENSIONAL cases
     (reference values 1). Returns a dict: mesh (SU2Mesh), mech (mech_* arrays), flow_cfg / sst_cfg (keyword dicts
@@ -708,7 +708,8 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
     base = os.path.dirname(os.path.abspath(cfg_path))
     if c.get("REF_DIMENSIONALIZATION", "DIMENSIONAL") != "DIMENSIONAL":
         raise RxError("case_from_cfg: only REF_DIMENSIONALIZATION= DIMENSIONAL")
-    walls = _cfg_list(c.get("MARKER_ISOTHERMAL", ""))[0::2]
+    # viscous walls for the wall distance (CGeometry::ComputeWall_Distance: HEAT_FLUX and ISOTHERMAL markers)
+    walls = _cfg_list(c.get("MARKER_ISOTHERMAL", ""))[0::2] + _cfg_list(c.get("MARKER_HEATFLUX", ""))[0::2]
     mesh = SU2Mesh(mesh_path or os.path.join(base, c["MESH_FILENAME"]), walls=walls)
     mech = read_mechanism(lib_dir or base, c["CONFIG_LIB_FILE"])
     names = [str(x) for x in mech["mech_species"]]
@@ -765,6 +766,9 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
     outlet = {outs[k]: float(outs[k + 1]) for k in range(0, len(outs), 2)}
     isos = _cfg_list(c.get("MARKER_ISOTHERMAL", ""))
     iso = {isos[k]: float(isos[k + 1]) for k in range(0, len(isos), 2)}
+    hfs = _cfg_list(c.get("MARKER_HEATFLUX", ""))
+    hf = {hfs[k]: float(hfs[k + 1]) for k in range(0, len(hfs), 2)}
+    euler = set(_cfg_list(c.get("MARKER_EULER", "")))
     sym = set(_cfg_list(c.get("MARKER_SYM", "")))
     kinds, rows = [], []
     for tag in mesh.tags:
@@ -780,6 +784,11 @@ def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
         elif tag in iso:
             kinds.append(BC_ISOTHERMAL)
             r[1] = iso[tag]
+        elif tag in hf:
+            kinds.append(BC_HEATFLUX)
+            r[1] = hf[tag]
+        elif tag in euler:
+            kinds.append(BC_EULER)
         elif tag in sym:
             kinds.append(BC_NONE)
         else:

@@ -155,17 +155,21 @@ def write_subset_library(wd, ns):
 
 
 def make_workdir(case, mesh_writer, cfl, order, prec="LU_SGS", inlet="TEMPERATURE_IMPOSE", extra="",
-                 time_flow="EULER_IMPLICIT", ns=9, slope_limiter="VENKATAKRISHNAN"):
-    wd = os.path.join("/tmp/rx_golden", case)
+                 time_flow="EULER_IMPLICIT", ns=9, slope_limiter="VENKATAKRISHNAN", case_dir=None, root="/tmp/rx_golden"):
+    """A work dir holding a cfg of CFG_TEMPLATE, the mesh (mesh_writer) and the library files of case_dir (default:
+    the reference's TURBOLENT_COMBUSTION; the tests pass the unpacked tests/golden/case_files.npz)."""
+    case_dir = case_dir or CASE_DIR
+    wd = os.path.join(root, case)
     shutil.rmtree(wd, ignore_errors=True)
     os.makedirs(os.path.join(wd, "out"))
     if ns == 9:
         for d in ("Mixture", "Chemistry", "Thermo", "Transp"):
-            os.symlink(os.path.join(CASE_DIR, d), os.path.join(wd, d))
-        os.symlink(os.path.join(CASE_DIR, "test_chem_second.txt"), os.path.join(wd, "test_chem_second.txt"))
+            os.symlink(os.path.join(case_dir, d), os.path.join(wd, d))
+        for lst in ("test_chem_second.txt", "test_chem_first.txt"):
+            os.symlink(os.path.join(case_dir, lst), os.path.join(wd, lst))
     else:
         write_subset_library(wd, ns)
-    mesh_name = mesh_writer(wd)
+    mesh_name = mesh_writer(wd) if case_dir == CASE_DIR else mesh_writer(wd, case_dir)
     cfg = CFG_TEMPLATE.format(cfl=cfl, order=order, mesh=mesh_name, prec=prec, inlet_type=inlet,
                               inlet_ox=INLETS[inlet][0], inlet_fuel=INLETS[inlet][1], extra=extra, time_flow=time_flow)
     cfg = cfg.replace("SLOPE_LIMITER_FLOW= VENKATAKRISHNAN", "SLOPE_LIMITER_FLOW= " + slope_limiter)
@@ -535,8 +539,8 @@ def iteration_case(name, writer, U, ns, n_iters, cfl, prec, time_flow, extra="")
     return out
 
 
-def full_jet_writer(wd):
-    os.symlink(os.path.join(CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
+def full_jet_writer(wd, case_dir=None):
+    os.symlink(os.path.join(case_dir or CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
     return "mesh.su2"
 
 
@@ -549,6 +553,33 @@ def case_itx9():
     return iteration_case("itx9", full_jet_writer, cons, 9, 1, 0.1, "LU_SGS", "EULER_EXPLICIT")
 
 
+def ig9_workdir(case_dir=None, root="/tmp/rx_golden"):
+    """Work dir of stage 1 (my_combustion_first_chem_PaSR.cfg's keys on CFG_TEMPLATE)."""
+    wd = make_workdir("ig9", full_jet_writer, cfl=0.1, order="1ST_ORDER", prec="LU_SGS", time_flow="EULER_EXPLICIT",
+                      case_dir=case_dir, root=root)
+    cfg = open(os.path.join(wd, "case.cfg")).read()
+    cfg = cfg.replace("CONFIG_LIB_FILE = test_chem_second.txt", "CONFIG_LIB_FILE = test_chem_first.txt")
+    cfg = cfg.replace("IGNITION = NO", "IGNITION = YES\nIGNITION_ITER = 8000\nFUEL_INDEX = 0\nOXIDIZER_INDEX = 2")
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(cfg)
+    return wd
+
+
+def fp_workdir(case_dir=None, root="/tmp/rx_golden", name="fpit"):
+    """Work dir of the flat plate (FP_CFG) over the plate's files (default: the reference's TURBOLENT_FLAT_PLATE)."""
+    case_dir = case_dir or FP_DIR
+    wd = os.path.join(root, name)
+    shutil.rmtree(wd, ignore_errors=True)
+    os.makedirs(os.path.join(wd, "out"))
+    for d in ("Mixture", "Thermo", "Transp"):
+        os.symlink(os.path.join(case_dir, d), os.path.join(wd, d))
+    os.symlink(os.path.join(case_dir, "test_air.txt"), os.path.join(wd, "test_air.txt"))
+    os.symlink(os.path.join(case_dir, "mesh_flatplate_turb_137x97.su2"), os.path.join(wd, "mesh.su2"))
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(FP_CFG)
+    return wd
+
+
 def case_ig9():
     """Stage 1 of the reference's own procedure (my_combustion_first_chem_PaSR.cfg: the first chemistry,
     test_chem_first.txt, IGNITION = YES with IGNITION_ITER 8000, FUEL_INDEX 0, OXIDIZER_INDEX 2, EULER_EXPLICIT at
@@ -557,13 +588,7 @@ def case_ig9():
     raises T to 1700 K at the 1 283 mixing points, in the start-up preprocessing and in the iteration. One reference
     outer iteration."""
     _, cons = read_plot(os.path.join(CASE_DIR, "PLOT/no_chem.dat"))
-    wd = make_workdir("ig9", full_jet_writer, cfl=0.1, order="1ST_ORDER", prec="LU_SGS", time_flow="EULER_EXPLICIT")
-    os.symlink(os.path.join(CASE_DIR, "test_chem_first.txt"), os.path.join(wd, "test_chem_first.txt"))
-    cfg = open(os.path.join(wd, "case.cfg")).read()
-    cfg = cfg.replace("CONFIG_LIB_FILE = test_chem_second.txt", "CONFIG_LIB_FILE = test_chem_first.txt")
-    cfg = cfg.replace("IGNITION = NO", "IGNITION = YES\nIGNITION_ITER = 8000\nFUEL_INDEX = 0\nOXIDIZER_INDEX = 2")
-    with open(os.path.join(wd, "case.cfg"), "w") as f:
-        f.write(cfg)
+    wd = ig9_workdir()
     write_state(wd, cons)
     a = run_harness(wd, bsr=False, extra=["--iters", "1"])
     out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it")}
@@ -667,6 +692,25 @@ def case_fp3():
     return out
 
 
+def case_fpit():
+    """The reference's second shipped case end to end: one whole reference outer iteration of the turbulent flat plate
+    (Test_Cases/TURBOLENT/TURBOLENT_FLAT_PLATE, the whole 137x97 mesh = 13 289 points, air O2 / CO2 / N2 without
+    reactions, nVar 7) from its converged state (PLOT/flow.dat), with its cfg's markers: MARKER_HEATFLUX (wall, 0),
+    MARKER_EULER (symmetry), a TOTAL_CONDITIONS inlet and two outlets; 2ND_ORDER (unlimited MUSCL), EULER_IMPLICIT
+    with FGMRES(5) + LU_SGS at CFL 9."""
+    wd = fp_workdir()
+    _, cons = read_plot(os.path.join(FP_DIR, "PLOT/flow.dat"), ncons=9)
+    write_state(wd, cons)
+    a = run_harness(wd, bsr=False, extra=["--iters", "1"])
+    out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it")}
+    out = {k: v for k, v in out.items() if not k.endswith("_wall") and not (k.endswith("_Uold") and k != "it_Uold0")}
+    out.update(mech_arrays(FP_DIR, "test_air.txt"))
+    out["time_flow"] = np.array("EULER_IMPLICIT")
+    out["lin_prec"] = np.array("LU_SGS")
+    out["spatial_order"] = np.array(1)  # 2ND_ORDER: MUSCL without limiter
+    return out
+
+
 def window_case(a, keep):
     """Restrict a whole-mesh harness dump to the points `keep` (and the edges between them); interior = points
     whose whole neighbourhood is kept (where loop results are complete)."""
@@ -740,7 +784,7 @@ def main():
         a = {"mini9": case_mini9, "jet9w": case_jet9w, "bc9": case_bc9, "it9": case_it9,
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
-             "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "it7": case_it7,
+             "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
              "bj9": case_bj9}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)

@@ -562,7 +562,9 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     integration_time.cpp:40-140 with MGLEVEL = 0, then CSingleGridIntegration::SingleGrid_Iteration :770-810):
       flow  Preprocessing (SetPrimitive_Variables, LSQ gradient, StrainMag), Set_OldSolution, SetTime_Step,
             Space_Integration (upwind, viscous, source, weak then strong BCs), ImplicitEuler_Iteration (ILU0 FGMRES)
-            — or, cfg["time"] = "euler_explicit" / "rk", ExplicitEuler_Iteration / the RK_ALPHA_COEFF stages of
+            (cfg["spatial_order"] 1 / 2: the MUSCL branch, 2 with cfg["slope_limiter"]'s limiter; cfg["flow_prec"]
+            "ilu" / "lusgs") — or, cfg["time"] = "euler_explicit" / "rk", ExplicitEuler_Iteration / the RK_ALPHA_COEFF
+            stages of
             ExplicitRK_Iteration, each stage with its own Preprocessing and Space_Integration (MultiGrid_Cycle
             integration_time.cpp:144-183) —, then Preprocessing(Output = true) on the updated solution;
       SST   Preprocessing (gradient), Space_Integration (loops + BCs), ImplicitEuler_Iteration (cfg["sst_prec"] ILU0 or
@@ -601,7 +603,19 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
                                  o["V"], o["dPdU"], o["mu"], o["eddy"], vol, mesh["nbr_ptr"],
                                  [cfg["cfl"], cfg["max_delta_time"], cfg["prandtl_lam"], cfg["prandtl_turb"]])
         imp = scheme == "implicit"
-        rc, Jci, Jcj = ausm_edges(nDim, ns, mesh["edges"], mesh["edge_normal"], o["V"], o["dPdU"], cfg["mach_inf"], imp)
+        order = int(cfg.get("spatial_order", 0))  # SPATIAL_ORDER_FLOW: 0 1ST_ORDER, 1 2ND_ORDER, 2 2ND_ORDER_LIMITER
+        if order == 0:
+            rc, Jci, Jcj = ausm_edges(nDim, ns, mesh["edges"], mesh["edge_normal"], o["V"], o["dPdU"], cfg["mach_inf"],
+                                      imp)
+        else:  # Upwind_Residual's MUSCL branch (solver_direct_reactive.cpp:2554-2729), limiter from Preprocessing
+            L = None
+            if order == 2:
+                L = (limiter_barth(nDim, ns, mesh["edges"], mesh["coord"], o["V"], G)
+                     if int(cfg.get("slope_limiter", 0)) == 1 else
+                     limiter_venkat(nDim, ns, mesh["edges"], mesh["coord"], o["V"], G, cfg["ref_elem_length"],
+                                    cfg["limiter_coeff"]))
+            rc, Jci, Jcj = muscl_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], o["V"], o["dPdU"],
+                                       G, L, [1.0, 1.0, 1.0], cfg["mach_inf"], imp)
         rv, Jvi, Jvj = visc_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], o["V"], G, o["mu"],
                                   o["kappa"], o["Dij"], o["dTdU"], T[:, 0].copy(), mut, sig, gk, True, imp,
                                   [1, 1, 1, cfg["prandtl_turb"], cfg["lewis_turb"]])
@@ -630,9 +644,13 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         R[~ok] = 0.0
         A[diag] = D
         rhs = -(R + 0.0)
-        F = ilu_build(rp, col, A, part_ptr)
-        x, it, _ = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                          part_ptr=part_ptr)
+        if cfg.get("flow_prec", "ilu") == "ilu":
+            F = ilu_build(rp, col, A, part_ptr)
+            x, it, _ = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                              part_ptr=part_ptr)
+        else:  # LINEAR_SOLVER_PREC = LU_SGS
+            x, it, _ = fgmres(rp, col, A, rhs.ravel(), "lusgs", tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                              part_ptr=part_ptr)
         Un = update(Uold, x, nDim, 0, cfg["relaxation"], vol, dt)
         rms = np.maximum(1e-32, np.sqrt(np.sum(rhs * rhs, axis=0) / N))
     # MultiGrid_Iteration's Preprocessing(Output = true) on the updated solution (integration_time.cpp:127-129)

@@ -55,8 +55,9 @@ def ignition_kw(g):
 def solvers(g, implicit=1):
     mesh = {k: g[k] for k in MESH_KEYS}
     flow_imp, _, prec = scheme(g)
-    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(g), rx.default_cfg(implicit=implicit if flow_imp else 0, lin_prec=1,
-                                                                  **cfg_kw(g), **ignition_kw(g)))
+    order = int(g["spatial_order"]) if "spatial_order" in g else 0  # SPATIAL_ORDER_FLOW (fpit: 2ND_ORDER)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(g), rx.default_cfg(implicit=implicit if flow_imp else 0, lin_prec=prec,
+                                                                  spatial_order=order, **cfg_kw(g), **ignition_kw(g)))
     s.set_bc(rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"]))
     bp = g["bc_params"]
     t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(implicit=implicit, lin_prec=prec, lin_tol=float(bp[19]),
@@ -182,14 +183,16 @@ def n_iters(g):
     return sum(1 for k in g if k.startswith("it") and k.endswith("_U") and k[2:-2].isdigit())
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit"])
 def test_outer_iterations_vs_reference(case):
     """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d / it7: 2, itx9 /
     itx4: 1) on the device, started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within
     1e-10 relative per column. it7: the bench's 7-species mechanism, implicit; itx9: the reference's shipped cfg
     (EULER_EXPLICIT flow, CFL 0.1, LU-SGS SST) on its whole 9 000-point mesh; itx4: configs[0] (C1), 4 species,
     3-stage Runge-Kutta, on the same mesh; ig9: stage 1 of the reference's procedure (first chemistry, IGNITION =
-    YES: the 1 283 mixing points' record temperature raised to 1700 K) from its non-reacting start."""
+    YES: the 1 283 mixing points' record temperature raised to 1700 K) from its non-reacting start; fpit: the
+    reference's second shipped case, the whole turbulent flat plate (13 289 points, 3 species, nVar 7, heat-flux wall,
+    Euler wall, total-conditions inlet, outlets, 2ND_ORDER MUSCL, implicit FGMRES(5) + LU_SGS)."""
     g = golden(case)
     s, t = solvers(g, 1)
     rk = scheme(g)[1]
@@ -217,7 +220,7 @@ def test_free_running_iterations_vs_reference(case):
     s.close()
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit"])
 def test_outer_iteration_vs_oracle_device_order(case):
     """One iteration against the oracle run with the device's inner-product order: the residual side and the
     Krylov recurrence then agree to the Stefan-Maxwell rounding only (amplified by FGMRES: the same 1e-10 bar)."""

@@ -5,13 +5,15 @@ neighbour lists, boundary vertices, normal neighbours, wall distances; oracle/me
 reference's spline values).
 
 Meshes: mini9 / mini3d were meshed by the reference from meshgen's SU2 files, which these tests rewrite with the same
-writer; with /root/reference present (this container) also the reference's own mesh_stretched.su2 (the whole
-9 000-point jet, golden itx9) and its library files."""
+writer; the reference's own mesh_stretched.su2 (the whole 9 000-point jet, golden itx9) and
+mesh_flatplate_turb_137x97.su2 (the whole plate, golden fpit) with their library files come from
+tests/golden/case_files.npz (oracle/pack_case_files.py), so these tests run without /root/reference."""
 import os
 
 import numpy as np
 import pytest
 
+from tests.casefiles import unpack
 from tests.rxpkg import meshgen, rx
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -54,20 +56,28 @@ def test_su2_reader_reproduces_reference_geometry(case, tmp_path):
     m.close()
 
 
-@pytest.mark.skipif(not os.path.isdir(REF_CASE), reason="reference test case files absent")
-def test_su2_reader_on_the_reference_jet_mesh():
+def test_su2_reader_on_the_reference_jet_mesh(tmp_path):
     """The reference's own mesh_stretched.su2 (9 000 points): every geometric array of the reference's
     preprocessing, bitwise (golden itx9, the reference run on this mesh)."""
-    m = rx.SU2Mesh(os.path.join(REF_CASE, "mesh_stretched.su2"), walls=WALLS)
+    d = unpack(tmp_path, "jet")
+    m = rx.SU2Mesh(os.path.join(d, "mesh_stretched.su2"), walls=WALLS)
     check_geometry(m, golden("itx9"))
     m.close()
 
 
-@pytest.mark.skipif(not os.path.isdir(REF_CASE), reason="reference test case files absent")
-def test_library_reader_on_the_reference_files():
+def test_su2_reader_on_the_reference_flat_plate_mesh(tmp_path):
+    """The reference's mesh_flatplate_turb_137x97.su2 (13 289 points; markers inlet, outlet, farfield, symmetry, wall;
+    the HEAT_FLUX wall for the wall distance): every geometric array bitwise (golden fpit)."""
+    d = unpack(tmp_path, "plate")
+    m = rx.SU2Mesh(os.path.join(d, "mesh_flatplate_turb_137x97.su2"), walls=("wall",))
+    check_geometry(m, golden("fpit"))
+    m.close()
+
+
+def test_library_reader_on_the_reference_files(tmp_path):
     """ReactingModelLibrary::Setup restated natively equals the tables and rate constants the oracle and the device
     were pinned with (9 species, two reactions, CGS units, a reversible reaction with an explicit backward rate)."""
-    got = rx.read_mechanism(REF_CASE, "test_chem_second.txt")
+    got = rx.read_mechanism(unpack(tmp_path, "jet"), "test_chem_second.txt")
     g = golden("mini9")
     for k, v in got.items():
         if k in g:
@@ -174,14 +184,81 @@ def test_restart_matches_the_reference_writer(tmp_path):
     m.close()
 
 
-@pytest.mark.skipif(not os.path.isdir(REF_CASE), reason="reference test case files absent")
+def check_case_setup(case, g):
+    """case_from_cfg's markers, inlet kind, free-stream turbulence values and geometry against the reference's own
+    setup of the same cfg (a golden's bc_marker / bc_params / geometry)."""
+    want = rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"])
+    bc = case["bc"]
+    assert np.array_equal(bc["kind"], want["kind"]) and bc["inlet_kind"] == want["inlet_kind"]
+    k = want["kind"] != 0
+    assert np.array_equal(bc["data"][k][:, 1:], want["data"][k][:, 1:])
+    assert np.array_equal(bc["normal_neighbor"], want["normal_neighbor"])
+    for key in ("tke_inf", "kine_inf", "omega_inf"):
+        assert abs(bc[key] - want[key]) <= 1e-14 * abs(want[key]), key
+    check_geometry(case["mesh"], g)
+
+
+def test_case_from_cfg_flat_plate(tmp_path):
+    """The reference's flat-plate setup (oracle/make_golden.py FP_CFG: MARKER_HEATFLUX wall, MARKER_EULER symmetry,
+    TOTAL_CONDITIONS inlet, two outlets, 2ND_ORDER, EULER_IMPLICIT with LU_SGS) read by case_from_cfg from the
+    plate's own mesh and air library equals the reference's (golden fpit)."""
+    from oracle import make_golden as MG
+    wd = MG.fp_workdir(case_dir=unpack(tmp_path / "files", "plate"), root=str(tmp_path))
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    g = golden("fpit")
+    check_case_setup(case, g)
+    assert list(case["bc"]["kind"]) == [rx.BC_OUTLET, rx.BC_INLET, rx.BC_OUTLET, rx.BC_EULER, rx.BC_HEATFLUX]
+    fc = case["flow_cfg"]
+    assert fc["cfl"] == g["dt_params"][0] and fc["implicit"] == 1 and fc["lin_prec"] == 0 and fc["spatial_order"] == 1
+    assert abs(fc["mach_inf"] - g["mach_inf"][0]) <= 1e-15 * g["mach_inf"][0]
+    case["mesh"].close()
+
+
+def test_case_from_cfg_ignition_keys(tmp_path):
+    """Stage 1 of the reference's procedure (IGNITION = YES, IGNITION_ITER 8000, FUEL_INDEX 0, OXIDIZER_INDEX 2 on the
+    first chemistry): the keys reach rx_cfg (defaults of CConfig otherwise, config_structure.cpp:591-603)."""
+    from oracle import make_golden as MG
+    wd = MG.ig9_workdir(case_dir=unpack(tmp_path / "files", "jet"), root=str(tmp_path))
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    fc = case["flow_cfg"]
+    assert (fc["ignition"], fc["ignition_iter"], fc["ignition_temp"], fc["fuel_index"], fc["oxidizer_index"]) == \
+        (1, 8000, 1700.0, 0, 2)
+    assert int(case["mech"]["mech_n_reactions"]) == 2
+    case["mesh"].close()
+
+
+def test_case_from_cfg_defaults_and_rejections(tmp_path):
+    """Keys left out take CConfig's defaults (TIME_DISCRE_FLOW EULER_IMPLICIT :1026, LINEAR_SOLVER_PREC LU_SGS :1050,
+    RK_ALPHA_COEFF one stage of 1.0 :3038-3041); keys this path does not implement are rejected, not ignored."""
+    from oracle import make_golden as MG
+    files = unpack(tmp_path / "files", "jet")
+    wd = MG.make_workdir("dflt", MG.full_jet_writer, cfl=0.1, order="1ST_ORDER", case_dir=files, root=str(tmp_path))
+    base = open(os.path.join(wd, "case.cfg")).read()
+    drop = ("TIME_DISCRE_FLOW", "LINEAR_SOLVER_PREC", "RK_ALPHA_COEFF")
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write("\n".join(ln for ln in base.splitlines() if not ln.split("=")[0].strip() in drop) + "\n")
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    assert case["flow_cfg"]["implicit"] == 1 and case["flow_cfg"]["lin_prec"] == 0 and case["rk_alpha"] is None
+    case["mesh"].close()
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(base.replace("TIME_DISCRE_FLOW= EULER_IMPLICIT", "TIME_DISCRE_FLOW= RUNGE-KUTTA_EXPLICIT"))
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    assert case["rk_alpha"] == [1.0]
+    case["mesh"].close()
+    for key, val in (("CFL_ADAPT", "YES"), ("MGLEVEL", "2"), ("LINEAR_SOLVER_PREC", "JACOBI")):
+        with open(os.path.join(wd, "case.cfg"), "w") as f:
+            f.write(base + f"{key}= {val}\n")
+        with pytest.raises(rx.RxError):
+            rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+
+
 def test_case_from_cfg_matches_the_reference_setup(tmp_path):
     """A cfg in the reference's grammar (the golden cases' cfg, oracle/make_golden.py CFG_TEMPLATE, with the
     reference's mesh and library files): markers, inlet kind, free-stream turbulence values and the solver knobs
     equal what the reference derived from the same cfg (golden bc9 / itx9 bc_params, dt_params)."""
     from oracle import make_golden as MG
     wd = MG.make_workdir("cfgcase", MG.full_jet_writer, cfl=0.1, order="1ST_ORDER", prec="LU_SGS",
-                         time_flow="EULER_EXPLICIT")
+                         time_flow="EULER_EXPLICIT", case_dir=unpack(tmp_path / "files", "jet"), root=str(tmp_path))
     case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
     g = golden("itx9")
     want = rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"])
