@@ -22,7 +22,8 @@ LIB_PATH = os.path.join(HERE, "librx.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rx.h")
 
 # rx_status
-RX_OK, RX_ERR_ARG, RX_ERR_HIP, RX_ERR_NAN, RX_ERR_RANGE, RX_ERR_NONPHYS, RX_ERR_DIVERGED, RX_ERR_STATE = range(8)
+(RX_OK, RX_ERR_ARG, RX_ERR_HIP, RX_ERR_NAN, RX_ERR_RANGE, RX_ERR_NONPHYS, RX_ERR_DIVERGED, RX_ERR_STATE, RX_ERR_COMM,
+ RX_ERR_UNSUPPORTED) = range(10)
 # rx_field
 FIELDS = ["U", "V", "DPDU", "DTDU", "MU", "KAPPA", "DIJ", "GRAD", "LIMITER", "TKE", "OMEGA", "MUT", "SIGMAK", "GRADK",
           "EDDY", "RES", "DT", "LAMBDA_INV", "LAMBDA_VISC", "JAC", "ILU", "SOL", "RHS", "STRAIN", "F1", "F2", "CDKW",
@@ -688,6 +689,8 @@ def _cfg_list(v):
 def _spline(mech, prop, s, T):
     """MathTools::GetSpline (spline.cpp:62-77) on the library tables (host; free-stream values only)."""
     x, y, y2 = (mech["mech_tab_" + k][prop, s] for k in ("x", "y", "y2"))
+    if T < x[0] or T > x[-1]:  # GetSpline's std::out_of_range (spline.cpp:63-64)
+        raise RxError(f"The required temperature ({T} K) is out of data range")
     h = x[1] - x[0]
     klo = int((T - x[0]) / h + 1)
     a = (x[klo] - T) / h

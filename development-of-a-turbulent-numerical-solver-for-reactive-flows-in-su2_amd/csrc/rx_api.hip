@@ -67,6 +67,7 @@ const char* rx_status_string(int s) {
     case RX_ERR_DIVERGED: return "linear solver diverged";
     case RX_ERR_STATE: return "call sequence error";
     case RX_ERR_COMM: return "RCCL communication error";
+    case RX_ERR_UNSUPPORTED: return "input not supported on this path";
     default: return "unknown";
   }
 }

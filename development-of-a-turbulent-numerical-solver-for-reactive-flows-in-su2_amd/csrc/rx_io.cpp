@@ -537,6 +537,11 @@ int rx_mesh_read_su2(const char* path, rx_mesh** out) {
       for (int64_t e = 0; e < nelem; ++e) {
         if (!std::getline(f, line)) return fail(RX_ERR_STATE);
         std::istringstream is(line);
+        {
+          std::istringstream peek(line);
+          int vt = 0;
+          if ((peek >> vt) && (vt == 13 || vt == 14)) return fail(RX_ERR_UNSUPPORTED);  // prism / pyramid
+        }
         if (!read_elem(is, &m->elems[e])) return fail(RX_ERR_ARG);
         const int vtk = m->elems[e].t->vtk;
         if ((m->nDim == 2) != (vtk == 5 || vtk == 9)) return fail(RX_ERR_ARG);
@@ -727,6 +732,19 @@ std::vector<std::string> lib_lines(const std::string& path, bool* ok) {
     if (!line.empty() && !std::ispunct((unsigned char)line[0])) out.push_back(line);
   }
   return out;
+}
+
+// MathTools::SetSpline's table checks (Common/src/Tools/spline.cpp:12-25): at least 2 points, x sorted and unique,
+// and equispaced (GetSpline finds the interval by integer division) — the reference's loop compares the steps
+// x[i] - x[i-1] for 2 <= i < n - 1 with the first one exactly (the last step is not compared).
+bool spline_table_ok(const double* x, int n) {
+  if (n < 2) return false;
+  for (int i = 1; i < n; ++i)
+    if (!(x[i - 1] < x[i])) return false;  // sorted and unique
+  const double step = x[1] - x[0];
+  for (int i = 2; i < n - 1; ++i)
+    if (x[i] - x[i - 1] != step) return false;
+  return true;
 }
 
 // MathTools::SetSpline (spline.cpp:10-58), called with zero end slopes
@@ -941,6 +959,7 @@ int rx_mech_read(const char* base_dir, const char* list_file, rx_mech** out) {
         x[k] = t[2 * k];
         y[k] = t[2 * k + 1];
       }
+      if (!spline_table_ok(x, nt)) return fail(RX_ERR_STATE);
       set_spline(x, y, nt, &m->ty2[((size_t)p * ns + s) * nt]);
     }
   *out = m;

@@ -175,8 +175,11 @@ __global__ __launch_bounds__(kBlock) void k_fg_residual(int Nd, const int32_t* _
 }
 
 // k_fg_residual for x = 0 (ImplicitEuler_Iteration zeroes LinSysSol before the solve, solver_direct_reactive.cpp:2373 / :2384): A x is then
-// +0.0 in every element (spmv_elem sums from +0.0, so +0 + (+-0) = +0 for any finite A), and w0 = +0.0 - b is the
+// +0.0 in every element for a FINITE A (spmv_elem sums from +0.0, so +0 + (+-0) = +0), and w0 = +0.0 - b is the
 // same double as the product path gives, with the same grid loop and reduction, without streaming the matrix.
+// For a non-finite A (Inf / NaN entries) the reference's A * 0 makes w0 NaN at the first residual; here w0 stays
+// -b and the NaN enters at the first SpMV, one Krylov step later. Either way the update is non-finite and the
+// following SetPrimitive_Variables / rx_sync report it; RX_FG_X_PRODUCT=1 restores the product path.
 __global__ __launch_bounds__(kBlock) void k_fg_residual0(int64_t n, const double* __restrict__ b,
                                                          double* __restrict__ w, double* __restrict__ part,
                                                          KState* __restrict__ s, bool dist) {

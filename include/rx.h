@@ -52,7 +52,8 @@ typedef enum {
   RX_ERR_NONPHYS = 5,
   RX_ERR_DIVERGED = 6,
   RX_ERR_STATE = 7,
-  RX_ERR_COMM = 8     /* RCCL error */
+  RX_ERR_COMM = 8,    /* RCCL error */
+  RX_ERR_UNSUPPORTED = 9  /* input the path does not implement (rx_mesh_read_su2: prism / pyramid elements) */
 } rx_status;
 
 typedef struct rx_ctx rx_ctx;

@@ -274,3 +274,30 @@ def test_case_from_cfg_matches_the_reference_setup(tmp_path):
     assert fc["mach_inf"] == g["mach_inf"][0] and case["rk_alpha"] is None
     check_geometry(case["mesh"], g)
     case["mesh"].close()
+
+
+def test_reader_rejections(tmp_path):
+    """Inputs the native readers refuse as the reference does (or, for element types this path does not build,
+    with RX_ERR_UNSUPPORTED): a prism in an SU2 file; a property table that is not equispaced (SetSpline's
+    assertion, spline.cpp:12-25)."""
+    pts, el, bnd = meshgen.jet_mesh3d(4, 3, 2)
+    path = str(tmp_path / "prism.su2")
+    meshgen.write_su2(path, pts, el, bnd)
+    txt = open(path).read().splitlines()
+    k = txt.index(next(ln for ln in txt if ln.startswith("NELEM="))) + 1
+    txt[k] = "13 0 1 2 3 4 5 0"  # a prism in place of the first hexahedron
+    with open(path, "w") as f:
+        f.write("\n".join(txt) + "\n")
+    with pytest.raises(rx.RxError, match="status 9"):
+        rx.SU2Mesh(path, walls=WALLS)
+    d = unpack(tmp_path / "files", "jet")
+    fn = os.path.join(d, "Thermo", "O2_thermo.txt")
+    lines = open(fn).read().splitlines()
+    row = next(q for q, ln in enumerate(lines) if ln.split() and ln.split()[0][0].isdigit())
+    t = lines[row + 5].split()
+    t[0] = repr(float(t[0]) + 0.5)  # one temperature off the uniform grid
+    lines[row + 5] = " ".join(t)
+    with open(fn, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    with pytest.raises(rx.RxError, match="status 7"):
+        rx.read_mechanism(d, "test_chem_second.txt")
