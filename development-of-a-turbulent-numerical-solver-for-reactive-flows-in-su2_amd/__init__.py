@@ -187,6 +187,19 @@ def lib():
         _lib.rx_restart_write.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_int64]
         _lib.rx_restart_read.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        _lib.rx_cfg_default.argtypes = [C.POINTER(Cfg)]
+        _lib.rx_cfg_default.restype = None
+        _lib.rx_case_read.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
+        _lib.rx_case_destroy.argtypes = [C.c_void_p]
+        _lib.rx_case_destroy.restype = None
+        _lib.rx_case_error.restype = C.c_char_p
+        for name in ("rx_case_mesh", "rx_case_mech"):
+            getattr(_lib, name).argtypes = [C.c_void_p]
+            getattr(_lib, name).restype = C.c_void_p
+        _lib.rx_case_cfg.argtypes = [C.c_void_p, C.POINTER(Cfg), C.POINTER(Cfg)]
+        _lib.rx_case_bc.argtypes = [C.c_void_p, C.POINTER(BcDesc)]
+        _lib.rx_case_rk.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.POINTER(C.c_double))]
+        _lib.rx_case_free_stream.argtypes = [C.c_void_p] + [C.POINTER(C.c_double)] * 4
     return _lib
 
 
@@ -579,9 +592,16 @@ class SU2Mesh:
     mesh() gives the dict ReactiveNSSolver / TurbSSTSolver take; is_wall marks the HEAT_FLUX / ISOTHERMAL markers
     for the wall distance."""
 
-    def __init__(self, path, walls=()):
-        h = C.c_void_p()
-        _chk(lib().rx_mesh_read_su2(os.fsencode(path), C.byref(h)), f"rx_mesh_read_su2({path})")
+    def __init__(self, path=None, walls=(), handle=None, owner=None):
+        """path: read the file; handle: an rx_mesh owned by `owner` (an rx_case), borrowed, never destroyed here."""
+        self._owner = owner
+        if handle is not None:
+            h = C.c_void_p(handle)
+            self._borrowed = True
+        else:
+            h = C.c_void_p()
+            _chk(lib().rx_mesh_read_su2(os.fsencode(path), C.byref(h)), f"rx_mesh_read_su2({path})")
+            self._borrowed = False
         self.h = h
         nd, n, e, nb, nm = C.c_int32(), C.c_int64(), C.c_int64(), C.c_int64(), C.c_int32()
         lib().rx_mesh_info(h, C.byref(nd), C.byref(n), C.byref(e), C.byref(nb), C.byref(nm))
@@ -628,8 +648,10 @@ class SU2Mesh:
 
     def close(self):
         if getattr(self, "h", None):
-            lib().rx_mesh_destroy(self.h)
+            if not self._borrowed:
+                lib().rx_mesh_destroy(self.h)
             self.h = None
+            self._owner = None
 
     def __del__(self):
         try:
@@ -644,6 +666,14 @@ def read_mechanism(base_dir, list_file):
     h = C.c_void_p()
     _chk(lib().rx_mech_read(os.fsencode(base_dir), os.fsencode(list_file), C.byref(h)), f"rx_mech_read({list_file})")
     try:
+        return _mech_arrays(h)
+    finally:
+        lib().rx_mech_destroy(h)
+
+
+def _mech_arrays(h):
+    """mech_* arrays of an rx_mech handle (copies)."""
+    if True:
         d = MechDesc()
         _chk(lib().rx_mech_describe(h, C.byref(d)), "rx_mech_describe")
         ns, nr, nt = d.n_species, d.n_reactions, d.n_tab
@@ -661,8 +691,6 @@ def read_mechanism(base_dir, list_file):
                    form_enthalpy=np.array([lib().rx_mech_formation_enthalpy(h, s) for s in range(ns)]),
                    species=np.array([lib().rx_mech_species(h, s).decode() for s in range(ns)]))
         return {"mech_" + k: v for k, v in out.items()}
-    finally:
-        lib().rx_mech_destroy(h)
 
 
 R_UNGAS = 6.02214129e23 * 1.3806488e-23 * 1.0e3  # J/(kmol K) (physical_chemical_library.hpp:571-579)
@@ -698,140 +726,64 @@ def _spline(mech, prop, s, T):
     return a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0
 
 
-def case_from_cfg(cfg_path, mesh_path=None, lib_dir=None):
-    """The inputs of a reference REACTIVE_RANS case from its cfg (the keys of the shipped jet cfgs): the mesh
-    (SU2Mesh: MESH_FILENAME), the library (read_mechanism: CONFIG_LIB_FILE), the flow and SST rx_cfg keyword sets,
-    the boundary markers in the mesh's marker order (MARKER_INLET / INLET_TYPE / INLET_MASS_FRAC, MARKER_OUTLET,
-    MARKER_ISOTHERMAL, MARKER_HEATFLUX, MARKER_EULER, MARKER_SYM), the free-stream turbulence values of CReactiveEulerSolver::
-    SetNondimensionalization (solver_direct_reactive.cpp:4534-4590: k = 3/2 (|V| I)^2, omega = rho k / (mu
-    TURB2LAMVISC), rho = ComputeDensity, mu = ComputeEta) and TIME_DISCRE_FLOW / RK_ALPHA_COEFF. DIMENSIONAL cases
-    (reference values 1). Returns a dict: mesh (SU2Mesh), mech (mech_* arrays), flow_cfg / sst_cfg (keyword dicts
-    for default_cfg / sst_cfg), bc (rx_bc_desc inputs), rk_alpha (None unless RUNGE-KUTTA_EXPLICIT)."""
-    c = read_cfg(cfg_path)
-    base = os.path.dirname(os.path.abspath(cfg_path))
-    if c.get("REF_DIMENSIONALIZATION", "DIMENSIONAL") != "DIMENSIONAL":
-        raise RxError("case_from_cfg: only REF_DIMENSIONALIZATION= DIMENSIONAL")
-    # viscous walls for the wall distance (CGeometry::ComputeWall_Distance: HEAT_FLUX and ISOTHERMAL markers)
-    walls = _cfg_list(c.get("MARKER_ISOTHERMAL", ""))[0::2] + _cfg_list(c.get("MARKER_HEATFLUX", ""))[0::2]
-    mesh = SU2Mesh(mesh_path or os.path.join(base, c["MESH_FILENAME"]), walls=walls)
-    mech = read_mechanism(lib_dir or base, c["CONFIG_LIB_FILE"])
-    names = [str(x) for x in mech["mech_species"]]
-    order = _cfg_list(c.get("SPECIES_ORDER", ""))
-    if order and order != names:
-        raise RxError(f"SPECIES_ORDER {order} does not match the library's {names}")
-    ns = len(names)
-    f = lambda k, d: float(c.get(k, d))
-    # keys this path does not implement are rejected, not ignored (CConfig defaults: CFL_ADAPT NO, MGLEVEL 0,
-    # config_structure.cpp:985, 1128)
-    if c.get("CFL_ADAPT", "NO").upper() != "NO":
-        raise RxError("case_from_cfg: CFL_ADAPT= YES is not supported on this path")
-    if int(c.get("MGLEVEL", "0")) != 0:
-        raise RxError("case_from_cfg: MGLEVEL > 0 is not supported on this path (the jet cfgs run MGLEVEL= 0)")
-    # CConfig defaults (config_structure.cpp): TIME_DISCRE_FLOW EULER_IMPLICIT (:1026), LINEAR_SOLVER_PREC LU_SGS
-    # (:1050), RK_ALPHA_COEFF one stage of 1.0 (:3038-3041)
-    tf = c.get("TIME_DISCRE_FLOW", "EULER_IMPLICIT")
-    prec_kw = c.get("LINEAR_SOLVER_PREC", "LU_SGS")
-    if prec_kw not in ("ILU", "ILU0", "LU_SGS"):
-        raise RxError(f"case_from_cfg: LINEAR_SOLVER_PREC= {prec_kw} is not supported on this path")
-    prec = {"ILU": 1, "ILU0": 1, "LU_SGS": 0}[prec_kw]
-    order_map = {"1ST_ORDER": 0, "2ND_ORDER": 1, "2ND_ORDER_LIMITER": 2}
-    flow_cfg = dict(mach_inf=f("MACH_NUMBER", 0.0), cfl=f("CFL_NUMBER", 1.25), max_delta_time=f("MAX_DELTA_TIME", 1e6),
-                    prandtl_lam=f("PRANDTL_LAM", 0.72), prandtl_turb=f("PRANDTL_TURB", 0.9),
-                    lewis_turb=f("LEWIS_TURB", 1.2), c_mu=f("C_MU", 0.09), pasr_lb=f("PASR_LB", 1.0),
-                    lin_tol=f("LINEAR_SOLVER_ERROR", 1e-5), lin_iter=int(f("LINEAR_SOLVER_ITER", 10)),
-                    lin_prec=prec, relaxation=f("RELAXATION_FACTOR_FLOW", 1.0),
-                    implicit=int(tf == "EULER_IMPLICIT"), rans=int(c.get("KIND_TURB_MODEL", "NONE") == "SST"),
-                    spatial_order=order_map[c.get("SPATIAL_ORDER_FLOW", "2ND_ORDER")],
-                    ref_elem_length=f("REF_ELEM_LENGTH", 0.1), limiter_coeff=f("LIMITER_COEFF", 0.5),
-                    slope_limiter={"VENKATAKRISHNAN": 0, "BARTH_JESPERSEN": 1}[c.get("SLOPE_LIMITER_FLOW",
-                                                                                     "VENKATAKRISHNAN")],
-                    t_min=f("TEMPERATURE_MIN", 200.0), t_max=f("TEMPERATURE_MAX", 6000.0),
-                    clip_temp=int(c.get("CLIPPING_TEMPRATURE", "NO") == "YES"),
-                    ignition=int(c.get("IGNITION", "NO").upper() == "YES"), fuel_index=int(f("FUEL_INDEX", 0)),
-                    oxidizer_index=int(f("OXIDIZER_INDEX", 2)), ignition_iter=int(f("IGNITION_ITER", 999999)),
-                    ignition_temp=f("IGNITION_TEMPERATURE", 1700.0))
-    sst_cfg_kw = dict(implicit=int(c.get("TIME_DISCRE_TURB", "EULER_IMPLICIT") == "EULER_IMPLICIT"),
-                      lin_tol=flow_cfg["lin_tol"], lin_iter=flow_cfg["lin_iter"], lin_prec=prec,
-                      relaxation_turb=f("RELAXATION_FACTOR_TURB", 1.0), cfl_red_turb=f("CFL_REDUCTION_TURB", 1.0))
-    if tf not in ("EULER_IMPLICIT", "EULER_EXPLICIT", "RUNGE-KUTTA_EXPLICIT"):
-        raise RxError(f"case_from_cfg: TIME_DISCRE_FLOW= {tf} is not supported on this path")
-    rk = ([float(x) for x in _cfg_list(c["RK_ALPHA_COEFF"])] if "RK_ALPHA_COEFF" in c else [1.0]) \
-        if tf == "RUNGE-KUTTA_EXPLICIT" else None
-    # boundary markers, mesh marker order
-    inlets = _cfg_list(c.get("MARKER_INLET", ""))
-    inlet = {inlets[k]: [float(x) for x in inlets[k + 1:k + 6]] for k in range(0, len(inlets), 6)}
-    fr = [t for t in c.get("INLET_MASS_FRAC", "").strip().strip("()").split(";") if t.strip()]
-    inlet_y = {}
-    for t in fr:
-        p = _cfg_list(t)
-        inlet_y[p[0]] = [float(x) for x in p[1:1 + ns]]
-    outs = _cfg_list(c.get("MARKER_OUTLET", ""))
-    outlet = {outs[k]: float(outs[k + 1]) for k in range(0, len(outs), 2)}
-    isos = _cfg_list(c.get("MARKER_ISOTHERMAL", ""))
-    iso = {isos[k]: float(isos[k + 1]) for k in range(0, len(isos), 2)}
-    hfs = _cfg_list(c.get("MARKER_HEATFLUX", ""))
-    hf = {hfs[k]: float(hfs[k + 1]) for k in range(0, len(hfs), 2)}
-    euler = set(_cfg_list(c.get("MARKER_EULER", "")))
-    sym = set(_cfg_list(c.get("MARKER_SYM", "")))
-    kinds, rows = [], []
-    for tag in mesh.tags:
-        r = np.zeros(6 + ns)
-        if tag in inlet:
-            kinds.append(BC_INLET)
-            r[1:3] = inlet[tag][:2]
-            r[3:6] = inlet[tag][2:5]
-            r[6:] = inlet_y.get(tag, np.zeros(ns))
-        elif tag in outlet:
-            kinds.append(BC_OUTLET)
-            r[1] = outlet[tag]
-        elif tag in iso:
-            kinds.append(BC_ISOTHERMAL)
-            r[1] = iso[tag]
-        elif tag in hf:
-            kinds.append(BC_HEATFLUX)
-            r[1] = hf[tag]
-        elif tag in euler:
-            kinds.append(BC_EULER)
-        elif tag in sym:
-            kinds.append(BC_NONE)
-        else:
-            raise RxError(f"marker {tag}: boundary kind not supported on this path")
-        rows.append(r)
-    # free stream (SetNondimensionalization, DIMENSIONAL)
-    T_inf, P_inf = f("FREESTREAM_TEMPERATURE", 288.15), f("FREESTREAM_PRESSURE", 101325.0)
-    Y = np.array([float(x) for x in _cfg_list(c["FREESTREAM_MASS_FRAC"])])
-    mm = mech["mech_mmass"]
-    rgas = 0.0
-    for q in range(ns):  # ComputeRgas: inner_product(Ys, Ri), Ri = R_ungas / M_s
-        rgas += Y[q] * (R_UNGAS / mm[q])
-    rho_inf = P_inf / (rgas * T_inf)
-    cp = 0.0
-    for q in range(ns):  # ComputeCP
-        cp += Y[q] * (_spline(mech, 0, q, T_inf) / mm[q])
-    gamma = cp / (cp - rgas)  # ComputeFrozenGamma
-    mod_v0 = float(np.sqrt(sum(v * v for v in [float(x) for x in _cfg_list(c.get("FREESTREAM_VELOCITY",
-                                                                                "(1.0, 0.0, 0.0)"))][:mesh.n_dim])))
-    flow_cfg["mach_inf"] = mod_v0 / np.sqrt(gamma * rgas * T_inf)  # CConfig::SetMach (:973), frozen sound speed
-    visc = np.array([_spline(mech, 3, s, T_inf) for s in range(ns)])
-    yom = np.where(Y < 0.0, 1.0e-30, Y) / mm
-    eta = 0.0
-    for a in range(ns):  # ComputeEta (Wilke), the same expression as SetPrimVar's
-        phi = 0.0
-        for b in range(ns):
-            t = (1.0 + np.sqrt(visc[a] / visc[b]) * (mm[b] / mm[a]) ** 0.25)
-            phi += yom[b] / np.sqrt(8.0 * (1.0 + mm[a] / mm[b])) * t * t
-        eta += visc[a] * yom[a] / phi
-    vel = [float(x) for x in _cfg_list(c.get("FREESTREAM_VELOCITY", "(1.0, 0.0, 0.0)"))]
-    mod_v = float(np.sqrt(sum(v * v for v in vel[:mesh.n_dim])))
-    inten = f("FREESTREAM_TURBULENCEINTENSITY", 0.05)
-    tke = 3.0 / 2.0 * (mod_v * mod_v * inten * inten)
-    omega = rho_inf * tke / (eta * f("FREESTREAM_TURB2LAMVISCRATIO", 10.0))
-    bc = dict(kind=np.array(kinds, dtype=np.int32), data=np.array(rows), normal_neighbor=mesh.mesh()["bvertex_pn"],
-              inlet_kind={"TOTAL_CONDITIONS": INLET_TOTAL_CONDITIONS, "MASS_FLOW": INLET_MASS_FLOW,
-                          "TEMPERATURE_IMPOSE": INLET_TEMPERATURE_IMPOSE}[c.get("INLET_TYPE", "TOTAL_CONDITIONS")],
-              tke_inf=tke, kine_inf=tke, omega_inf=omega)
-    return dict(mesh=mesh, mech=mech, flow_cfg=flow_cfg, sst_cfg=sst_cfg_kw, bc=bc, rk_alpha=rk,
-                free_stream=dict(rho=rho_inf, mu=eta, T=T_inf, P=P_inf, Y=Y))
+class _Case:
+    """Owner of an rx_case handle (the mesh of case_from_cfg borrows from it)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().rx_case_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def _cfg_dict(c: Cfg):
+    return {name: getattr(c, name) for name, _ in Cfg._fields_}
+
+
+def case_from_cfg(cfg_path):
+    """The inputs of a reference REACTIVE_RANS case from its cfg, read natively (include/rx_io.h rx_case_read,
+    csrc/rx_case.cpp): the mesh (MESH_FILENAME: SU2 reader + dual-grid preprocessing + wall distance to the
+    ISOTHERMAL / HEAT_FLUX markers), the library (CONFIG_LIB_FILE), the flow and SST rx_cfg, the boundary markers in
+    the mesh's marker order and the free-stream values of SetNondimensionalization. Returns a dict: mesh (SU2Mesh,
+    borrowed from the case), mech (mech_* arrays), flow_cfg (keyword dict for default_cfg), sst_cfg (keyword dict for
+    default_cfg: the SST context's rx_cfg), bc (rx_bc_desc inputs), rk_alpha (None unless RUNGE-KUTTA_EXPLICIT),
+    free_stream."""
+    h = C.c_void_p()
+    rc = lib().rx_case_read(os.fsencode(cfg_path), C.byref(h))
+    if rc != RX_OK:
+        raise RxError(f"case_from_cfg({cfg_path}): {lib().rx_case_error().decode()} "
+                      f"({lib().rx_status_string(rc).decode()}, status {rc})")
+    case = _Case(h)
+    mesh = SU2Mesh(handle=lib().rx_case_mesh(h), owner=case)
+    mech = _mech_arrays(C.c_void_p(lib().rx_case_mech(h)))
+    fc, sc = Cfg(), Cfg()
+    _chk(lib().rx_case_cfg(h, C.byref(fc), C.byref(sc)), "rx_case_cfg")
+    bd = BcDesc()
+    _chk(lib().rx_case_bc(h, C.byref(bd)), "rx_case_bc")
+    nm, nb = bd.n_marker, mesh.NB
+    kinds = np.ctypeslib.as_array(C.cast(bd.kind, C.POINTER(C.c_int32)), shape=(nm,)).copy()
+    ns = int(mech["mech_n_species"])
+    data = np.ctypeslib.as_array(C.cast(bd.data, C.POINTER(C.c_double)), shape=(nm, 6 + ns)).copy()
+    nn = (np.ctypeslib.as_array(C.cast(bd.normal_neighbor, C.POINTER(C.c_int64)), shape=(nb,)).copy() if nb
+          else np.zeros(0, dtype=np.int64))
+    bc = dict(kind=kinds, data=data, normal_neighbor=nn, inlet_kind=int(bd.inlet_kind), tke_inf=bd.tke_inf,
+              kine_inf=bd.kine_inf, omega_inf=bd.omega_inf)
+    n = C.c_int32()
+    ap = C.POINTER(C.c_double)()
+    _chk(lib().rx_case_rk(h, C.byref(n), C.byref(ap)), "rx_case_rk")
+    rk = [ap[k] for k in range(n.value)] if n.value else None
+    fs = [C.c_double() for _ in range(4)]
+    _chk(lib().rx_case_free_stream(h, *[C.byref(x) for x in fs]), "rx_case_free_stream")
+    mesh._mesh["wall_distance"] = np.ctypeslib.as_array(
+        lib().rx_mesh_wall_distance(mesh.h, np.array([1 if k in (BC_ISOTHERMAL, BC_HEATFLUX) else 0 for k in kinds],
+                                                     dtype=np.int32).ctypes.data), shape=(mesh.N,)).copy()
+    return dict(mesh=mesh, mech=mech, flow_cfg=_cfg_dict(fc), sst_cfg=_cfg_dict(sc), bc=bc, rk_alpha=rk,
+                free_stream=dict(rho=fs[0].value, mu=fs[1].value, T=fs[2].value, P=fs[3].value), case=case)
 
 
 def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=None, rk_alpha=None):

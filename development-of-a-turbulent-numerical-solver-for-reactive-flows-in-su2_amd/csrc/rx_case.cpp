@@ -1,0 +1,418 @@
+// rx_case.cpp — a reference case from its cfg file (host C++, no GPU): the cfg grammar of
+// CConfig::SetConfig_Parsing (Common/src/config_structure.cpp: "KEY= value" lines, '%' comments, lists in
+// parentheses separated by ',' / ';') for the keys of this path, the mesh (rx_mesh_read_su2, MESH_FILENAME), the
+// library (rx_mech_read, CONFIG_LIB_FILE), the flow and SST rx_cfg, the boundary markers in the mesh's marker
+// order, and the free-stream turbulence values CReactiveEulerSolver::SetNondimensionalization derives
+// (SU2_CFD/src/solver_direct_reactive.cpp:4534-4590) for DIMENSIONAL cases.
+//
+// Defaults are CConfig's (config_structure.cpp): TIME_DISCRE_FLOW EULER_IMPLICIT (:1026), LINEAR_SOLVER_PREC LU_SGS
+// (:1050), LINEAR_SOLVER_ERROR 1e-5 (:1052), LINEAR_SOLVER_ITER 10 (:1054), CFL_NUMBER 1.25 (:981), PASR_LB 1.0
+// (:609), SPATIAL_ORDER_FLOW 2ND_ORDER (:1163), INLET_TYPE TOTAL_CONDITIONS (:884), RK_ALPHA_COEFF one stage of
+// 1.0 (:3038-3041), IGNITION NO / 999999 / 1700 K / fuel 0 / oxidizer 2 (:591-603). Keys the path does not
+// implement are rejected with RX_ERR_UNSUPPORTED (CFL_ADAPT YES, MGLEVEL > 0, other preconditioners / time schemes
+// / marker kinds, non-DIMENSIONAL cases), never silently ignored.
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/rx_io.h"
+
+struct rx_case {
+  rx_mesh* mesh = nullptr;
+  rx_mech* mech = nullptr;
+  rx_cfg flow{}, sst{};
+  std::vector<int32_t> kind;
+  std::vector<double> data;
+  std::vector<int64_t> pn;
+  int32_t inlet_kind = RX_INLET_TOTAL_CONDITIONS;
+  double tke_inf = 0.0, omega_inf = 0.0;
+  std::vector<double> rk;  // RK_ALPHA_COEFF (RUNGE-KUTTA_EXPLICIT), else empty
+  double rho_inf = 0.0, mu_inf = 0.0, T_inf = 0.0, P_inf = 0.0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+constexpr double kRUngas = 6.02214129e23 * 1.3806488e-23 * 1.0e3;  // J/(kmol K) (physical_chemical_library.hpp:571-579)
+
+std::string trim(const std::string& s) {
+  const size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
+  return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+}
+
+std::string upper(std::string s) {
+  for (char& ch : s) ch = (char)std::toupper((unsigned char)ch);
+  return s;
+}
+
+// list tokens: strip, strip '(' / ')' at both ends, ';' as ','
+std::vector<std::string> list(const std::string& v) {
+  std::string t = trim(v);
+  const size_t a = t.find_first_not_of("()"), b = t.find_last_not_of("()");
+  t = a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+  std::replace(t.begin(), t.end(), ';', ',');
+  std::vector<std::string> out;
+  size_t p = 0;
+  while (p <= t.size()) {
+    const size_t q = t.find(',', p);
+    const std::string tok = trim(t.substr(p, q == std::string::npos ? std::string::npos : q - p));
+    if (!tok.empty()) out.push_back(tok);
+    if (q == std::string::npos) break;
+    p = q + 1;
+  }
+  return out;
+}
+
+struct Cfg {
+  std::map<std::string, std::string> kv;
+  bool has(const char* k) const { return kv.count(k) != 0; }
+  std::string str(const char* k, const char* d) const {
+    auto it = kv.find(k);
+    return it == kv.end() ? std::string(d) : it->second;
+  }
+  double num(const char* k, double d) const {
+    auto it = kv.find(k);
+    return it == kv.end() ? d : std::strtod(it->second.c_str(), nullptr);
+  }
+};
+
+bool read_cfg(const char* path, Cfg* c) {
+  std::ifstream f(path);
+  if (!f) return false;
+  std::string line;
+  while (std::getline(f, line)) {
+    const size_t pc = line.find('%');
+    if (pc != std::string::npos) line = line.substr(0, pc);
+    line = trim(line);
+    const size_t eq = line.find('=');
+    if (eq == std::string::npos) continue;
+    c->kv[upper(trim(line.substr(0, eq)))] = trim(line.substr(eq + 1));
+  }
+  return true;
+}
+
+// MathTools::GetSpline (spline.cpp:62-77) on the library tables, with its range check (:63-64)
+bool spline(const rx_mech_desc& d, int prop, int s, double T, double* out) {
+  const int nt = d.n_tab;
+  const size_t o = ((size_t)prop * d.n_species + s) * nt;
+  const double *x = d.tab_x + o, *y = d.tab_y + o, *y2 = d.tab_y2 + o;
+  if (T < x[0] || T > x[nt - 1]) return false;
+  const double h = x[1] - x[0];
+  const unsigned long klo = (unsigned long)((T - x[0]) / h + 1);
+  const double a = (x[klo] - T) / h, b = (T - x[klo - 1]) / h;
+  *out = a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0;
+  return true;
+}
+
+std::string dir_of(const std::string& p) {
+  const size_t k = p.find_last_of('/');
+  return k == std::string::npos ? std::string(".") : p.substr(0, k);
+}
+
+int fail(rx_case* c, int rc, const std::string& msg) {
+  g_err = msg;
+  rx_case_destroy(c);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+void rx_cfg_default(rx_cfg* c) {
+  if (!c) return;
+  *c = rx_cfg{};
+  c->mach_inf = 0.01819;
+  c->T_ref = c->E_ref = c->R_ref = c->rho_ref = c->t_ref = 1.0;
+  c->prandtl_lam = 0.72;
+  c->prandtl_turb = 0.9;
+  c->lewis_turb = 1.2;
+  c->c_mu = 0.09;
+  c->pasr_lb = 0.2;
+  c->cfl = 5.0;
+  c->max_delta_time = 1e6;
+  c->ref_elem_length = 0.1;
+  c->limiter_coeff = 0.5;
+  c->lin_tol = 1e-6;
+  c->relaxation = 1.0;
+  c->implicit = 1;
+  c->rans = 1;
+  c->lin_iter = 5;
+  c->lin_prec = 1;
+  c->spatial_order = 0;
+  c->clip_temp = 0;
+  c->t_min = 200.0;
+  c->t_max = 6000.0;
+  c->p_ref = c->visc_ref = c->cond_ref = c->vel_ref = c->len_ref = 1.0;
+  c->slope_limiter = RX_LIMITER_VENKATAKRISHNAN;
+  c->ignition = 0;
+  c->fuel_index = 0;
+  c->oxidizer_index = 2;
+  c->ignition_iter = 999999;
+  c->ignition_temp = 1700.0;
+}
+
+const char* rx_case_error(void) { return g_err.c_str(); }
+
+int rx_case_read(const char* cfg_path, rx_case** out) {
+  if (!cfg_path || !out) return RX_ERR_ARG;
+  *out = nullptr;
+  Cfg c;
+  rx_case* k = new rx_case();
+  if (!read_cfg(cfg_path, &c)) return fail(k, RX_ERR_STATE, std::string("cannot read ") + cfg_path);
+  const std::string base = dir_of(cfg_path);
+  if (upper(c.str("REF_DIMENSIONALIZATION", "DIMENSIONAL")) != "DIMENSIONAL")
+    return fail(k, RX_ERR_UNSUPPORTED, "only REF_DIMENSIONALIZATION= DIMENSIONAL");
+  if (upper(c.str("CFL_ADAPT", "NO")) != "NO") return fail(k, RX_ERR_UNSUPPORTED, "CFL_ADAPT= YES");
+  if (std::atoi(c.str("MGLEVEL", "0").c_str()) != 0) return fail(k, RX_ERR_UNSUPPORTED, "MGLEVEL > 0");
+  if (!c.has("MESH_FILENAME") || !c.has("CONFIG_LIB_FILE"))
+    return fail(k, RX_ERR_STATE, "MESH_FILENAME / CONFIG_LIB_FILE missing");
+  // mesh + library
+  int rc = rx_mesh_read_su2((base + "/" + c.str("MESH_FILENAME", "")).c_str(), &k->mesh);
+  if (rc) return fail(k, rc, "mesh " + c.str("MESH_FILENAME", ""));
+  rc = rx_mech_read(base.c_str(), c.str("CONFIG_LIB_FILE", "").c_str(), &k->mech);
+  if (rc) return fail(k, rc, "library " + c.str("CONFIG_LIB_FILE", ""));
+  rx_mech_desc md{};
+  rx_mech_describe(k->mech, &md);
+  const int ns = md.n_species;
+  int32_t nd = 0, nmark = 0;
+  int64_t npt = 0, ned = 0, nbv = 0;
+  rx_mesh_info(k->mesh, &nd, &npt, &ned, &nbv, &nmark);
+  {
+    const auto order = list(c.str("SPECIES_ORDER", ""));
+    if (!order.empty()) {
+      if ((int)order.size() != ns) return fail(k, RX_ERR_STATE, "SPECIES_ORDER does not match the library");
+      for (int s = 0; s < ns; ++s)
+        if (order[s] != rx_mech_species(k->mech, s))
+          return fail(k, RX_ERR_STATE, "SPECIES_ORDER does not match the library");
+    }
+  }
+  // solver knobs
+  const std::string tf = upper(c.str("TIME_DISCRE_FLOW", "EULER_IMPLICIT"));
+  if (tf != "EULER_IMPLICIT" && tf != "EULER_EXPLICIT" && tf != "RUNGE-KUTTA_EXPLICIT")
+    return fail(k, RX_ERR_UNSUPPORTED, "TIME_DISCRE_FLOW= " + tf);
+  const std::string pk = upper(c.str("LINEAR_SOLVER_PREC", "LU_SGS"));
+  if (pk != "ILU" && pk != "ILU0" && pk != "LU_SGS") return fail(k, RX_ERR_UNSUPPORTED, "LINEAR_SOLVER_PREC= " + pk);
+  const int prec = pk == "LU_SGS" ? 0 : 1;
+  const std::string so = upper(c.str("SPATIAL_ORDER_FLOW", "2ND_ORDER"));
+  const std::string sl = upper(c.str("SLOPE_LIMITER_FLOW", "VENKATAKRISHNAN"));
+  if ((so != "1ST_ORDER" && so != "2ND_ORDER" && so != "2ND_ORDER_LIMITER") ||
+      (sl != "VENKATAKRISHNAN" && sl != "BARTH_JESPERSEN"))
+    return fail(k, RX_ERR_UNSUPPORTED, "SPATIAL_ORDER_FLOW / SLOPE_LIMITER_FLOW");
+  rx_cfg& F = k->flow;
+  rx_cfg_default(&F);
+  F.cfl = c.num("CFL_NUMBER", 1.25);
+  F.max_delta_time = c.num("MAX_DELTA_TIME", 1e6);
+  F.prandtl_lam = c.num("PRANDTL_LAM", 0.72);
+  F.prandtl_turb = c.num("PRANDTL_TURB", 0.9);
+  F.lewis_turb = c.num("LEWIS_TURB", 1.2);
+  F.c_mu = c.num("C_MU", 0.09);
+  F.pasr_lb = c.num("PASR_LB", 1.0);
+  F.lin_tol = c.num("LINEAR_SOLVER_ERROR", 1e-5);
+  F.lin_iter = (int32_t)c.num("LINEAR_SOLVER_ITER", 10);
+  F.lin_prec = prec;
+  F.relaxation = c.num("RELAXATION_FACTOR_FLOW", 1.0);
+  F.implicit = tf == "EULER_IMPLICIT";
+  F.rans = upper(c.str("KIND_TURB_MODEL", "NONE")) == "SST";
+  F.spatial_order = so == "1ST_ORDER" ? 0 : (so == "2ND_ORDER" ? 1 : 2);
+  F.ref_elem_length = c.num("REF_ELEM_LENGTH", 0.1);
+  F.limiter_coeff = c.num("LIMITER_COEFF", 0.5);
+  F.slope_limiter = sl == "BARTH_JESPERSEN" ? RX_LIMITER_BARTH_JESPERSEN : RX_LIMITER_VENKATAKRISHNAN;
+  F.t_min = c.num("TEMPERATURE_MIN", 200.0);
+  F.t_max = c.num("TEMPERATURE_MAX", 6000.0);
+  F.clip_temp = upper(c.str("CLIPPING_TEMPRATURE", "NO")) == "YES";
+  F.ignition = upper(c.str("IGNITION", "NO")) == "YES";
+  F.fuel_index = (int32_t)c.num("FUEL_INDEX", 0);
+  F.oxidizer_index = (int32_t)c.num("OXIDIZER_INDEX", 2);
+  F.ignition_iter = (int64_t)c.num("IGNITION_ITER", 999999);
+  F.ignition_temp = c.num("IGNITION_TEMPERATURE", 1700.0);
+  if (F.ignition && (F.fuel_index < 0 || F.fuel_index >= ns || F.oxidizer_index < 0 || F.oxidizer_index >= ns))
+    return fail(k, RX_ERR_STATE, "FUEL_INDEX / OXIDIZER_INDEX out of the mixture");
+  rx_cfg& S = k->sst;  // SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl
+  rx_cfg_default(&S);
+  S.implicit = upper(c.str("TIME_DISCRE_TURB", "EULER_IMPLICIT")) == "EULER_IMPLICIT";
+  S.lin_tol = F.lin_tol;
+  S.lin_iter = F.lin_iter;
+  S.lin_prec = prec;
+  S.relaxation = c.num("RELAXATION_FACTOR_TURB", 1.0);
+  S.cfl = c.num("CFL_REDUCTION_TURB", 1.0);
+  if (tf == "RUNGE-KUTTA_EXPLICIT") {
+    if (c.has("RK_ALPHA_COEFF"))
+      for (const auto& t : list(c.str("RK_ALPHA_COEFF", ""))) k->rk.push_back(std::strtod(t.c_str(), nullptr));
+    if (k->rk.empty()) k->rk.push_back(1.0);
+  }
+  // boundary markers (mesh marker order)
+  std::map<std::string, std::vector<double>> inlet, inlet_y;
+  std::map<std::string, double> outlet, iso, hf;
+  std::map<std::string, int> euler, sym;
+  {
+    const auto t = list(c.str("MARKER_INLET", ""));
+    for (size_t q = 0; q + 5 < t.size(); q += 6) {
+      std::vector<double> v;
+      for (size_t r = 1; r < 6; ++r) v.push_back(std::strtod(t[q + r].c_str(), nullptr));
+      inlet[t[q]] = v;
+    }
+    std::string fr = trim(c.str("INLET_MASS_FRAC", ""));
+    const size_t a = fr.find_first_not_of("()"), b = fr.find_last_not_of("()");
+    fr = a == std::string::npos ? std::string() : fr.substr(a, b - a + 1);
+    size_t p = 0;
+    while (p < fr.size()) {
+      const size_t q = fr.find(';', p);
+      const auto seg = list(fr.substr(p, q == std::string::npos ? std::string::npos : q - p));
+      if (!seg.empty()) {
+        std::vector<double> y;
+        for (size_t r = 1; r < seg.size() && (int)y.size() < ns; ++r) y.push_back(std::strtod(seg[r].c_str(), nullptr));
+        inlet_y[seg[0]] = y;
+      }
+      if (q == std::string::npos) break;
+      p = q + 1;
+    }
+    auto pairs = [&](const char* key, std::map<std::string, double>& m) {
+      const auto u = list(c.str(key, ""));
+      for (size_t q = 0; q + 1 < u.size(); q += 2) m[u[q]] = std::strtod(u[q + 1].c_str(), nullptr);
+    };
+    pairs("MARKER_OUTLET", outlet);
+    pairs("MARKER_ISOTHERMAL", iso);
+    pairs("MARKER_HEATFLUX", hf);
+    for (const auto& u : list(c.str("MARKER_EULER", ""))) euler[u] = 1;
+    for (const auto& u : list(c.str("MARKER_SYM", ""))) sym[u] = 1;
+  }
+  const int W = 6 + ns;
+  std::vector<int32_t> is_wall(nmark, 0);
+  k->data.assign((size_t)nmark * W, 0.0);
+  for (int m = 0; m < nmark; ++m) {
+    const std::string tag = rx_mesh_marker_tag(k->mesh, m);
+    double* r = k->data.data() + (size_t)m * W;
+    if (inlet.count(tag)) {
+      k->kind.push_back(RX_BC_INLET);
+      const auto& v = inlet[tag];
+      for (int q = 0; q < 5; ++q) r[1 + q] = v[q];
+      if (inlet_y.count(tag))
+        for (size_t s = 0; s < inlet_y[tag].size(); ++s) r[6 + s] = inlet_y[tag][s];
+    } else if (outlet.count(tag)) {
+      k->kind.push_back(RX_BC_OUTLET);
+      r[1] = outlet[tag];
+    } else if (iso.count(tag)) {
+      k->kind.push_back(RX_BC_ISOTHERMAL);
+      r[1] = iso[tag];
+      is_wall[m] = 1;
+    } else if (hf.count(tag)) {
+      k->kind.push_back(RX_BC_HEATFLUX);
+      r[1] = hf[tag];
+      is_wall[m] = 1;
+    } else if (euler.count(tag)) {
+      k->kind.push_back(RX_BC_EULER);
+    } else if (sym.count(tag)) {
+      k->kind.push_back(RX_BC_NONE);
+    } else {
+      return fail(k, RX_ERR_UNSUPPORTED, "marker " + tag + ": boundary kind not supported on this path");
+    }
+  }
+  const std::string it = upper(c.str("INLET_TYPE", "TOTAL_CONDITIONS"));
+  if (it == "TOTAL_CONDITIONS") k->inlet_kind = RX_INLET_TOTAL_CONDITIONS;
+  else if (it == "MASS_FLOW") k->inlet_kind = RX_INLET_MASS_FLOW;
+  else if (it == "TEMPERATURE_IMPOSE") k->inlet_kind = RX_INLET_TEMPERATURE_IMPOSE;
+  else return fail(k, RX_ERR_UNSUPPORTED, "INLET_TYPE= " + it);
+  rx_mesh_wall_distance(k->mesh, is_wall.data());  // ComputeWall_Distance over the HEAT_FLUX / ISOTHERMAL markers
+  const int64_t* nn = rx_mesh_normal_neighbor(k->mesh);
+  k->pn.assign(nn, nn + nbv);
+  // free stream (SetNondimensionalization, DIMENSIONAL)
+  const double T_inf = c.num("FREESTREAM_TEMPERATURE", 288.15), P_inf = c.num("FREESTREAM_PRESSURE", 101325.0);
+  std::vector<double> Y;
+  for (const auto& t : list(c.str("FREESTREAM_MASS_FRAC", ""))) Y.push_back(std::strtod(t.c_str(), nullptr));
+  if ((int)Y.size() != ns) return fail(k, RX_ERR_STATE, "FREESTREAM_MASS_FRAC needs one value per species");
+  double rgas = 0.0;
+  for (int q = 0; q < ns; ++q) rgas += Y[q] * (kRUngas / md.mmass[q]);  // ComputeRgas
+  const double rho_inf = P_inf / (rgas * T_inf);
+  double cp = 0.0;
+  for (int q = 0; q < ns; ++q) {  // ComputeCP
+    double v;
+    if (!spline(md, 0, q, T_inf, &v)) return fail(k, RX_ERR_RANGE, "FREESTREAM_TEMPERATURE out of the tables");
+    cp += Y[q] * (v / md.mmass[q]);
+  }
+  const double gamma = cp / (cp - rgas);  // ComputeFrozenGamma
+  std::vector<double> vel;
+  for (const auto& t : list(c.str("FREESTREAM_VELOCITY", "(1.0, 0.0, 0.0)"))) vel.push_back(std::strtod(t.c_str(), nullptr));
+  double mv2 = 0.0;
+  for (int d = 0; d < nd && d < (int)vel.size(); ++d) mv2 += vel[d] * vel[d];
+  const double mod_v = std::sqrt(mv2);
+  F.mach_inf = mod_v / std::sqrt(gamma * rgas * T_inf);  // CConfig::SetMach (:973), frozen sound speed
+  std::vector<double> visc(ns), yom(ns);
+  for (int s = 0; s < ns; ++s) {
+    if (!spline(md, 3, s, T_inf, &visc[s])) return fail(k, RX_ERR_RANGE, "FREESTREAM_TEMPERATURE out of the tables");
+    yom[s] = (Y[s] < 0.0 ? 1.0e-30 : Y[s]) / md.mmass[s];
+  }
+  double eta = 0.0;
+  for (int a = 0; a < ns; ++a) {  // ComputeEta (Wilke), SetPrimVar's expression
+    double phi = 0.0;
+    for (int b = 0; b < ns; ++b) {
+      const double t = 1.0 + std::sqrt(visc[a] / visc[b]) * std::pow(md.mmass[b] / md.mmass[a], 0.25);
+      phi += yom[b] / std::sqrt(8.0 * (1.0 + md.mmass[a] / md.mmass[b])) * t * t;
+    }
+    eta += visc[a] * yom[a] / phi;
+  }
+  const double inten = c.num("FREESTREAM_TURBULENCEINTENSITY", 0.05);
+  k->tke_inf = 3.0 / 2.0 * (mod_v * mod_v * inten * inten);
+  k->omega_inf = rho_inf * k->tke_inf / (eta * c.num("FREESTREAM_TURB2LAMVISCRATIO", 10.0));
+  k->rho_inf = rho_inf;
+  k->mu_inf = eta;
+  k->T_inf = T_inf;
+  k->P_inf = P_inf;
+  *out = k;
+  return RX_OK;
+}
+
+void rx_case_destroy(rx_case* c) {
+  if (!c) return;
+  if (c->mesh) rx_mesh_destroy(c->mesh);
+  if (c->mech) rx_mech_destroy(c->mech);
+  delete c;
+}
+
+rx_mesh* rx_case_mesh(rx_case* c) { return c ? c->mesh : nullptr; }
+rx_mech* rx_case_mech(rx_case* c) { return c ? c->mech : nullptr; }
+
+int rx_case_cfg(const rx_case* c, rx_cfg* flow, rx_cfg* sst) {
+  if (!c) return RX_ERR_ARG;
+  if (flow) *flow = c->flow;
+  if (sst) *sst = c->sst;
+  return RX_OK;
+}
+
+int rx_case_bc(const rx_case* c, rx_bc_desc* bc) {
+  if (!c || !bc) return RX_ERR_ARG;
+  bc->n_marker = (int32_t)c->kind.size();
+  bc->kind = c->kind.data();
+  bc->data = c->data.data();
+  bc->normal_neighbor = c->pn.data();
+  bc->inlet_kind = c->inlet_kind;
+  bc->tke_inf = c->tke_inf;
+  bc->kine_inf = c->tke_inf;
+  bc->omega_inf = c->omega_inf;
+  return RX_OK;
+}
+
+int rx_case_rk(const rx_case* c, int32_t* n_stage, const double** alpha) {
+  if (!c || !n_stage) return RX_ERR_ARG;
+  *n_stage = (int32_t)c->rk.size();
+  if (alpha) *alpha = c->rk.empty() ? nullptr : c->rk.data();
+  return RX_OK;
+}
+
+int rx_case_free_stream(const rx_case* c, double* rho, double* mu, double* T, double* P) {
+  if (!c) return RX_ERR_ARG;
+  if (rho) *rho = c->rho_inf;
+  if (mu) *mu = c->mu_inf;
+  if (T) *T = c->T_inf;
+  if (P) *P = c->P_inf;
+  return RX_OK;
+}
+
+}  // extern "C"

@@ -631,7 +631,8 @@ const int64_t* rx_mesh_global_index(const rx_mesh* m) { return m ? m->gidx.data(
 const int64_t* rx_mesh_normal_neighbor(const rx_mesh* m) { return m ? m->pn.data() : nullptr; }
 
 const double* rx_mesh_wall_distance(rx_mesh* m, const int32_t* is_wall) {
-  if (!m || !is_wall) return nullptr;
+  if (!m) return nullptr;
+  if (!is_wall) return m->wall.empty() ? nullptr : m->wall.data();  // the last computed distances
   const int nd = m->nDim;
   std::vector<int64_t> wp;  // wall vertices in marker / vertex order
   for (size_t b = 0; b < m->bvert.size() / 2; ++b)

@@ -58,7 +58,8 @@ int rx_mesh_describe(const rx_mesh *mesh, rx_mesh_desc *out);
 const int64_t *rx_mesh_global_index(const rx_mesh *mesh);
 const int64_t *rx_mesh_normal_neighbor(const rx_mesh *mesh);
 /* ComputeWall_Distance: is_wall[n_marker] != 0 for the HEAT_FLUX / ISOTHERMAL markers of the cfg; distance of every
- * point to the nearest vertex of those markers (0 everywhere when there is none). Returns a pointer to [N]. */
+ * point to the nearest vertex of those markers (0 everywhere when there is none). Returns a pointer to [N].
+ * is_wall NULL: the distances of the last call (rx_case_read computes them from the cfg's wall markers). */
 const double *rx_mesh_wall_distance(rx_mesh *mesh, const int32_t *is_wall);
 
 typedef struct rx_mech rx_mech;
@@ -67,6 +68,28 @@ void rx_mech_destroy(rx_mech *mech);
 int rx_mech_describe(const rx_mech *mech, rx_mech_desc *out); /* valid until rx_mech_destroy */
 const char *rx_mech_species(const rx_mech *mech, int32_t s);  /* SPECIES name of species s */
 double rx_mech_formation_enthalpy(const rx_mech *mech, int32_t s);
+
+/* A reference case from its cfg (rx_case.cpp): CConfig::SetConfig_Parsing's grammar for the keys of this path, the
+ * mesh (MESH_FILENAME, rx_mesh_read_su2) and library (CONFIG_LIB_FILE, rx_mech_read) relative to the cfg's directory,
+ * the flow and SST rx_cfg (CConfig defaults for keys left out; SST: RELAXATION_FACTOR_TURB -> relaxation,
+ * CFL_REDUCTION_TURB -> cfl), the markers in the mesh's marker order (MARKER_INLET / INLET_TYPE / INLET_MASS_FRAC,
+ * MARKER_OUTLET, MARKER_ISOTHERMAL, MARKER_HEATFLUX, MARKER_EULER, MARKER_SYM), the wall distance to the
+ * ISOTHERMAL / HEAT_FLUX markers, Mach_inf (CConfig::SetMach with the frozen sound speed) and the free-stream
+ * turbulence of SetNondimensionalization (solver_direct_reactive.cpp:4534-4590). DIMENSIONAL cases only. Keys the
+ * path does not implement give RX_ERR_UNSUPPORTED (message: rx_case_error). The mesh / mech / bc arrays belong to
+ * the case until rx_case_destroy. */
+typedef struct rx_case rx_case;
+void rx_cfg_default(rx_cfg *cfg); /* the defaults of every rx_cfg field (jet values; refs 1; no ignition) */
+int rx_case_read(const char *cfg_path, rx_case **out);
+void rx_case_destroy(rx_case *c);
+const char *rx_case_error(void);  /* message of the last failed rx_case_read (this thread) */
+rx_mesh *rx_case_mesh(rx_case *c);
+rx_mech *rx_case_mech(rx_case *c);
+int rx_case_cfg(const rx_case *c, rx_cfg *flow, rx_cfg *sst);
+int rx_case_bc(const rx_case *c, rx_bc_desc *bc);
+/* RK_ALPHA_COEFF of a RUNGE-KUTTA_EXPLICIT case (n_stage 0 otherwise: EULER_EXPLICIT / EULER_IMPLICIT) */
+int rx_case_rk(const rx_case *c, int32_t *n_stage, const double **alpha);
+int rx_case_free_stream(const rx_case *c, double *rho, double *mu, double *T, double *P);
 
 /* U [N][n_var] flow conservatives and T [N][2] (k, omega) in the mesh's point order; extra [N][5] (Pressure,
  * Temperature, Mach, Laminar_Viscosity, Eddy_Viscosity) or NULL (the reference's low-memory output). */

@@ -5,6 +5,9 @@
 // rx::Iterate), writes the results back as <name>.f64.
 //
 //   rx_driver <case_dir> <mode 0|1|2>
+//   rx_driver <cfg_path> 3 <state_dir>: the case read natively from its cfg (include/rx_io.h rx_case_read: mesh,
+//                                      library, rx_cfg, markers), the reference's iteration-start records from
+//                                      <state_dir>, then one rx::Iterate; results written to <state_dir>.
 #include <cstdint>
 #include <cstdio>
 #include <fstream>
@@ -12,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "rx_io.h"
 #include "rx_solver.hpp"
 
 template <typename T>
@@ -39,6 +43,72 @@ int main(int argc, char** argv) {
   }
   const std::string d = argv[1];
   const int implicit = std::atoi(argv[2]);
+  if (implicit == 3) {
+    if (argc < 4) {
+      std::cerr << "usage: rx_driver <cfg_path> 3 <state_dir>\n";
+      return 2;
+    }
+    const std::string sd = argv[3];
+    rx_case* cs = nullptr;
+    if (int rc = rx_case_read(d.c_str(), &cs)) {
+      std::printf("rx_case_read: %s (status %d)\n", rx_case_error(), rc);
+      return 1;
+    }
+    try {
+      rx_mesh_desc mesh{};
+      rx_mech_desc mech{};
+      rx_cfg fcfg{}, tcfg{};
+      rx_bc_desc bc{};
+      rx_mesh_describe(rx_case_mesh(cs), &mesh);
+      rx_mech_describe(rx_case_mech(cs), &mech);
+      rx_case_cfg(cs, &fcfg, &tcfg);
+      rx_case_bc(cs, &bc);
+      int32_t nrk = 0;
+      const double* ark = nullptr;
+      rx_case_rk(cs, &nrk, &ark);
+      const std::vector<double> rk(ark, ark + nrk);
+      const int nd = mesh.n_dim;
+      const int64_t N = mesh.n_point;
+      rx::ReactiveNSSolver flow(mesh, mech, fcfg, 0);
+      flow.SetBoundaryConditions(bc);
+      rx::TurbSSTSolver turb(mesh, flow, tcfg);
+      const double* wd = rx_mesh_wall_distance(rx_case_mesh(cs), nullptr);
+      auto T = f64(sd, "it_sst0");
+      auto tg = f64(sd, "it_sstgrad0");
+      std::vector<double> k(N), w(N), gk((size_t)N * nd);
+      for (int64_t i = 0; i < N; ++i) {
+        k[i] = T[2 * i];
+        w[i] = T[2 * i + 1];
+        for (int q = 0; q < nd; ++q) gk[(size_t)i * nd + q] = tg[(size_t)i * 2 * nd + q];  // grad k
+      }
+      flow.Upload(RX_F_V, f64(sd, "it_V0"));
+      flow.Upload(RX_F_U, f64(sd, "it_U0"));
+      flow.Upload(RX_F_TKE, k);
+      flow.Upload(RX_F_OMEGA, w);
+      flow.Upload(RX_F_MUT, f64(sd, "it_mut0"));
+      flow.Upload(RX_F_SIGMAK, std::vector<double>(N, 0.85));
+      flow.Upload(RX_F_GRADK, gk);
+      turb.Upload(RX_F_U, T);
+      turb.Upload(RX_F_WALLDIST, std::vector<double>(wd, wd + N));
+      turb.Upload(RX_F_F1, f64(sd, "it_F1_0"));
+      turb.Upload(RX_F_F2, f64(sd, "it_F2_0"));
+      turb.Upload(RX_F_CDKW, f64(sd, "it_CDkw0"));
+      std::vector<double> trms;
+      auto rms = rx::Iterate(flow, turb, 0, &trms, rk);
+      flow.Synchronize();
+      save(sd, "out_u", flow.Download(RX_F_U));
+      save(sd, "out_sst_u", turb.Download(RX_F_U));
+      save(sd, "out_rms", rms);
+      save(sd, "out_sst_rms", trms);
+      std::printf("ok case iterate (%lld points)\n", (long long)N);
+    } catch (const std::exception& e) {
+      std::printf("exception: %s\n", e.what());
+      rx_case_destroy(cs);
+      return 1;
+    }
+    rx_case_destroy(cs);
+    return 0;
+  }
   try {
     // mesh
     auto edges = i64(d, "edges"), nbr_ptr = i64(d, "nbr_ptr"), nbr = i64(d, "nbr"), bvert = i64(d, "bvertex");

@@ -38,7 +38,7 @@ def test_case_from_files_runs_the_reference_iteration(case, tmp_path):
     mesh = c["mesh"].mesh()
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(c["mech"]), rx.default_cfg(**c["flow_cfg"]))
     s.set_bc(c["bc"])
-    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(**c["sst_cfg"]))
+    t = rx.TurbSSTSolver(mesh, s, rx.default_cfg(**c["sst_cfg"]))
     g = golden(case)
     load_iteration_state(g, s, t, 0)
     rms, rms_t, _ = rx.Iterate(s, t, ext_iter=0, rk_alpha=c["rk_alpha"])

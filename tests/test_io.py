@@ -301,3 +301,13 @@ def test_reader_rejections(tmp_path):
         f.write("\n".join(lines) + "\n")
     with pytest.raises(rx.RxError, match="status 7"):
         rx.read_mechanism(d, "test_chem_second.txt")
+
+
+def test_native_cfg_defaults_match_the_python_mirror():
+    """rx_cfg_default (the C++ host's defaults, rx_case.cpp) and rx.default_cfg give the same rx_cfg."""
+    import ctypes as C
+    c = rx.Cfg()
+    rx.lib().rx_cfg_default(C.byref(c))
+    d = rx.default_cfg()
+    for name, _ in rx.Cfg._fields_:
+        assert getattr(c, name) == getattr(d, name), name
