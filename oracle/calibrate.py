@@ -12,6 +12,10 @@ boundary conditions, then the SST step) on identical meshes and states here:
   c2  a 500 x 200 = 100 000-point synthetic jet (meshgen, read by the reference's SU2 reader, its dual grid), the
       bench's initial field on it (synth.field_at: the converged jet interpolated, species floored at 1e-10),
       9 species
+  c2b the same mesh with the bench's own state: 7 species (the subset library files), every species floored at
+      1e-6 of rho (synth.field_at's default, the state bench.py runs), serial ILU(0) (the reference's one rank)
+  c2e the c2b mesh and state under the shipped cfgs' scheme: EULER_EXPLICIT flow at CFL 0.5 (no flow linear
+      solve), SST with FGMRES(5) + LU_SGS
 
 Outputs (profiles/r02_calibration.json): the reference's wall time per iteration (1 core; the serial reference
 build has no MPI), the restatement's wall time on 1 thread and on all threads, their ratio (the factor that turns
@@ -51,21 +55,31 @@ def run_case(name):
             return "mesh.su2"
         _, U = MG.read_plot(os.path.join(MG.CASE_DIR, "PLOT/flow_second_chem.dat"))
     else:
-        nx, ny = {"c2": (500, 200)}[name]
+        nx, ny = {"c2": (500, 200), "c2b": (500, 200), "c2e": (500, 200)}[name]
+        ns = 7 if name in ("c2b", "c2e") else 9
         pts, quads, bnd = MG.meshgen.jet_mesh(nx, ny)
         from tests.rxpkg import synth
-        _, Uc, k, om, _, _ = synth.field_at(pts, 9)
+        # c2b: the bench's own state (7 species, every species floored at 1e-6 of rho: synth.field_at's default)
+        _, Uc, k, om, _, _ = synth.field_at(pts, ns, y_floor=1e-6 if name in ("c2b", "c2e") else 1e-10)
         U = np.concatenate([Uc, k[:, None], om[:, None]], axis=1)
 
         def writer(wd):
             MG.meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, quads, bnd)
             return "mesh.su2"
-    wd = MG.make_workdir("calib_" + name, writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    ns = 7 if name in ("c2b", "c2e") else 9
+    if name == "c2e":  # the shipped cfgs' scheme: EULER_EXPLICIT flow (no flow linear solve), LU_SGS SST
+        wd = MG.make_workdir("calib_" + name, writer, cfl=0.5, order="1ST_ORDER", prec="LU_SGS", ns=ns,
+                             time_flow="EULER_EXPLICIT")
+    else:
+        wd = MG.make_workdir("calib_" + name, writer, cfl=5.0, order="1ST_ORDER", prec="ILU0", ns=ns)
     MG.write_state(wd, U)
     t0 = time.perf_counter()
     g = MG.run_harness(wd, bsr=False, extra=["--iters", "1"])
     harness_s = time.perf_counter() - t0
-    g.update(MG.mech_arrays())
+    g.update(MG.mech_arrays(wd, "test_chem_second.txt") if ns != 9 else MG.mech_arrays())
+    # the cfg's scheme for iteration_cfg (as make_golden.iteration_case records it)
+    g["time_flow"] = np.array("EULER_EXPLICIT" if name == "c2e" else "EULER_IMPLICIT")
+    g["lin_prec"] = np.array("LU_SGS" if name == "c2e" else "ILU0")
     return g, harness_s
 
 
