@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "rx_ctx.h"
 
@@ -195,7 +196,36 @@ __global__ __launch_bounds__(kBlock) void k_fg_residual0(int64_t n, const double
   grid_reduce<2>(v, part, s, sl, dist);
 }
 
-// w_{i+1} = A z_i with |w_{i+1}|^2 -> dotn and <w_{i+1}, w_0> -> dot
+// w_{i+1} = A z_i on a full grid (one thread per element, every CU filled like k_spmv); the inner products follow
+// in k_fg_spmv_dots.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_fg_spmv_full(int Nd, const int32_t* __restrict__ rp,
+                                                         const int32_t* __restrict__ col, const double* __restrict__ A,
+                                                         const double* __restrict__ z, double* __restrict__ w,
+                                                         const KState* __restrict__ s) {
+  if (s->done) return;
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q < (int64_t)Nd * NV) w[q] = spmv_elem<NV>(q, rp, col, A, z);
+}
+
+// |w_{i+1}|^2 -> dotn and <w_{i+1}, w_0> -> dot over the stored product, in k_fg_spmv's grid-stride order (each
+// thread sums the same elements in the same order, then the same fixed trees): bitwise k_fg_spmv's sums.
+__global__ __launch_bounds__(kBlock) void k_fg_spmv_dots(int64_t n, const double* __restrict__ w0,
+                                                         const double* __restrict__ w, double* __restrict__ part,
+                                                         KState* __restrict__ s, bool dist) {
+  if (s->done) return;
+  double v[2] = {0.0, 0.0};
+  GRID_LOOP(q, n) {
+    const double y = w[q];
+    v[0] += y * y;
+    v[1] += y * w0[q];
+  }
+  const int sl[2] = {kDotN, kDot};
+  grid_reduce<2>(v, part, s, sl, dist);
+}
+
+// w_{i+1} = A z_i with |w_{i+1}|^2 -> dotn and <w_{i+1}, w_0> -> dot (one launch on the 512-block reduction grid;
+// RX_FG_FUSED_SPMV=1 selects it instead of k_fg_spmv_full + k_fg_spmv_dots)
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_fg_spmv(int Nd, const int32_t* __restrict__ rp,
                                                     const int32_t* __restrict__ col, const double* __restrict__ A,
@@ -470,8 +500,17 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
     } else {
       if ((rc = rx_la_lusgs(ctx, A, W(i), Z(i), &s->done, &s->conv))) return rc;
     }
-    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, Z(i),
-                                                                           W(0), W(i + 1), part, s, dist)));
+    // the product on a full grid (the 512-block reduction grid left 2 waves per SIMD, 91 % parked),
+    // then the two inner products in the reduction's own order
+    static const bool fused_spmv = getenv("RX_FG_FUSED_SPMV") != nullptr;
+    if (fused_spmv) {
+      RX_NV_SWITCH(ctx->nVar, (k_fg_spmv<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, Z(i),
+                                                                             W(0), W(i + 1), part, s, dist)));
+    } else {
+      RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_full<NV_><<<blocks(n), kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A,
+                                                                                 Z(i), W(i + 1), s)));
+      k_fg_spmv_dots<<<kRedBlocks, kBlock, 0, st>>>(n, W(0), W(i + 1), part, s, dist);
+    }
     if ((rc = reduce())) return rc;
     for (int k = 0; k <= i; ++k) {
       k_fg_proj<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, k, i, ctx->kw, part, dist);

@@ -1478,3 +1478,90 @@ extern "C" int rx_debug_ilu_trace(rx_ctx* ctx, long long* host, int64_t n) {
   ctx->ilu_trace = nullptr;
   return RX_OK;
 }
+
+#ifdef RX_PROBE
+// Probe build only (tools/sweep_probe.py, librx_probe.so): timing variants of the wide forward sweep that break
+// its semantics on purpose, to locate where a level's time goes. MODE bits: 1 = x read from b (no dependence on
+// the level's results), 2 = no workgroup barrier between levels, 4 = factor blocks not loaded (a constant).
+namespace {
+template <int NV, int TB, int MODE>
+__global__ __launch_bounds__(TB) void k_probe_fwd(const int32_t* __restrict__ part_lvl, const int32_t* __restrict__ lvl_ptr,
+                                                  const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                                  const double* __restrict__ F, const double* __restrict__ b,
+                                                  double* __restrict__ x) {
+  constexpr int NV2 = NV * NV, RPB = TB / NV;
+  const int p = blockIdx.x;
+  const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
+  const bool lane = rl < RPB;
+  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  const double* xs = (MODE & 1) ? b : x;
+  for (int l = l0; l < l1; ++l) {
+    const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
+    for (int r = r0 + rl; lane && r < r1; r += RPB) {
+      const int4 sl = slot[r];
+      const int i = sl.x;
+      double xi = b[(size_t)i * NV + a];
+      for (int k = sl.y; k < sl.z; ++k) {
+        const double* blk = F + (size_t)k * NV2 + a * NV;
+        const double* xj = xs + (size_t)col[k] * NV;
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) s += ((MODE & 4) ? 1e-3 : blk[c]) * xj[c];
+        xi -= s;
+      }
+      x[(size_t)i * NV + a] = xi;
+    }
+    if (!(MODE & 2)) __syncthreads();
+  }
+}
+}  // namespace
+
+extern "C" int rx_debug_sweep_probe(rx_ctx* ctx, int mode, int reps, double* ms) {
+  if (!ctx || !ctx->cfg.implicit || ctx->nVar != 11) return RX_ERR_ARG;
+  const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
+  double* b = ctx->f[RX_F_RHS];
+  double* x = ctx->f[RX_F_SOL];
+  hipEvent_t e0, e1;
+  RX_HIP(hipEventCreate(&e0));
+  RX_HIP(hipEventCreate(&e1));
+  RX_HIP(hipEventRecord(e0, ctx->stream));
+  for (int q = 0; q < reps; ++q) {
+#define RX_PROBE_CASE(M)                                                                                          \
+  case M:                                                                                                         \
+    k_probe_fwd<11, 1024, M><<<ctx->npart, 1024, 0, ctx->stream>>>(ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->col, \
+                                                                  ctx->f[RX_F_ILU], b, x);                        \
+    break;
+    switch (mode) {
+      RX_PROBE_CASE(0)
+      RX_PROBE_CASE(1)
+      RX_PROBE_CASE(2)
+      RX_PROBE_CASE(3)
+      RX_PROBE_CASE(4)
+      RX_PROBE_CASE(5)
+      RX_PROBE_CASE(6)
+      RX_PROBE_CASE(7)
+      case 8:  // the production forward sweep
+        k_ilu_fwd_wide<11, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl,
+                                                                        ctx->col, ctx->f[RX_F_ILU], b, x, nullptr,
+                                                                        nullptr);
+        break;
+      case 9:  // the production backward sweep
+        k_ilu_bwd_wide<11, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
+            ctx->bs.part_lvl, ctx->bs.lvl_ptr, reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col,
+            ctx->f[RX_F_ILU], rx_invd_buf(ctx), x, nullptr, nullptr);
+        break;
+      default:
+        return RX_ERR_ARG;
+    }
+#undef RX_PROBE_CASE
+  }
+  RX_HIP(hipEventRecord(e1, ctx->stream));
+  RX_HIP(hipEventSynchronize(e1));
+  float t = 0.0f;
+  RX_HIP(hipEventElapsedTime(&t, e0, e1));
+  *ms = t / reps;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return RX_OK;
+}
+#endif
