@@ -6,6 +6,8 @@
 // 5374-5381). No atomics: results are bitwise reproducible run to run.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include <cstdlib>
 
 #include "rx_chem.h"
@@ -1238,7 +1240,7 @@ inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 
 int rx_fail_hip(rx_ctx* ctx, hipError_t e) {
   (void)ctx;
-  (void)e;
+  fprintf(stderr, "rx: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
   return RX_ERR_HIP;
 }
 

@@ -486,9 +486,10 @@ __global__ __launch_bounds__(kBlock) void k_sst_post(int N, SSTC c, const double
 bool is_sst(const rx_ctx* ctx) { return ctx && ctx->kind == RX_KIND_SST && ctx->flow; }
 
 int sst_gradient(rx_ctx* ctx) {
-  if (ctx->Nd > 0)
+  if (ctx->Nd > 0) {
     RX_ND_SWITCH(ctx->nDim, (k_sol_grad_ls<ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->coord, ctx->nbr_ptr, ctx->nbr,
                                                                    ctx->f[RX_F_U], ctx->f[RX_F_GRAD])));
+  }
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, ctx->f[RX_F_GRAD], 2 * ctx->nDim);  // Set_MPI_Solution_Gradient
 }
@@ -562,11 +563,12 @@ int rx_sst_source(rx_ctx* ctx) {
   if (!is_sst(ctx)) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_SST_SOURCE);
   const rx_ctx* fl = ctx->flow;
-  if (ctx->Nd > 0)
+  if (ctx->Nd > 0) {
     RX_ND_SWITCH(ctx->nDim, (k_sst_source<ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
         (int)ctx->Nd, sst_constants(), ctx->diag, fl->f[RX_F_V], fl->nPV, fl->f[RX_F_GRAD], fl->nG, fl->f[RX_F_EDDY],
         fl->f[RX_F_STRAIN], ctx->f[RX_F_U], ctx->vol, ctx->f[RX_F_WALLDIST], ctx->f[RX_F_F1], ctx->f[RX_F_F2],
         ctx->f[RX_F_CDKW], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr)));
+  }
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
