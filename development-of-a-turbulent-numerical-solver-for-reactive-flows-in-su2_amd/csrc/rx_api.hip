@@ -267,28 +267,10 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         slot[4 * r + 2] = (int32_t)diag[i];
         slot[4 * r + 3] = khi[i];
       }
-      // staged-sweep row spans (rx_sweeps.hip, k_ilu_sweep_ws): LDS double offset of each row's blocks in its level
-      const int32_t nv2 = (int32_t)(ctx->nVar * ctx->nVar);
-      auto pad2 = [](int32_t n) { return (n + 1) & ~1; };
-      std::vector<int32_t> sslot(4 * order.size());
-      for (int32_t l = 0; l < S.nlevels; ++l) {
-        int32_t off = 0;
-        for (int32_t r = lvl_ptr[l]; r < lvl_ptr[l + 1]; ++r) {
-          const int32_t i = order[r];
-          const int32_t k0 = fwd ? klo[i] : (int32_t)diag[i] + 1, k1 = fwd ? (int32_t)diag[i] : khi[i];
-          sslot[4 * r] = i;
-          sslot[4 * r + 1] = k0;
-          sslot[4 * r + 2] = k1;
-          sslot[4 * r + 3] = off;
-          off += pad2(std::max(0, k1 - k0) * nv2) + (fwd ? 0 : pad2(nv2));
-        }
-        S.maxlvld = std::max(S.maxlvld, off);
-      }
       int rc2 = dupload(ctx, &S.part_lvl, part_lvl.data(), part_lvl.size());
       if (!rc2) rc2 = dupload(ctx, &S.lvl_ptr, lvl_ptr.data(), lvl_ptr.size());
       if (!rc2) rc2 = dupload(ctx, &S.rows, order.data(), order.size());
       if (!rc2) rc2 = dupload(ctx, &S.slot, slot.data(), slot.size());
-      if (!rc2) rc2 = dupload(ctx, &S.sslot, sslot.data(), sslot.size());
       return rc2;
     };
     {
@@ -545,7 +527,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         N * nv,                 // res
         N, N, N,                // dt, lambda_inv, lambda_visc
         imp * nb2,                       // jac
-        imp * (nb2 + N * (int64_t)nv * nv + 2), // ilu (+ inverse diagonals; +2: the staged sweeps' 16-byte copies)
+        imp * (nb2 + N * (int64_t)nv * nv), // ilu (+ inverse diagonals)
         N * nv, N * nv,         // sol, rhs
         N,                      // strain
         0, 0, 0, 0              // SST-only
@@ -635,7 +617,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
-                  ctx->fs.slot, ctx->bs.slot, ctx->fs.sslot, ctx->bs.sslot, ctx->send_idx, ctx->grad_list, ctx->sendbuf, ctx->rms_sum,
+                  ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->grad_list, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,
                   ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};

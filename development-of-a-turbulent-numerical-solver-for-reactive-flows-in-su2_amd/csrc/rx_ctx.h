@@ -94,11 +94,7 @@ struct rx_ctx {
     int32_t* lvl_ptr = nullptr;
     int32_t* rows = nullptr;
     int32_t* slot = nullptr;      // [rows][4] {row, klo, diag, khi} in schedule order
-    // staged sweeps (rx_sweeps.hip, k_ilu_sweep_ws): per slot {row, k0, k1, LDS double offset of the row's span
-    // in its level}, [k0, k1) the factor blocks the sweep reads (fwd: lower; bwd: upper, then inv(D_row));
-    // maxlvld = the largest level's total span (doubles)
-    int32_t* sslot = nullptr;
-    int nlevels = 0, maxwidth = 0, maxlvld = 0;
+    int nlevels = 0, maxwidth = 0;
   } fs, bs;
   double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)
   double* xstar = nullptr;      // [N][nVar] LU-SGS forward-sweep result (halo values)

@@ -1032,267 +1032,6 @@ __global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__
   }
 }
 
-// Staged sweeps, for partitions whose vector does not fit in LDS (the C3 jet's 3900-row partitions). The
-// wide sweeps above spend most of a level loading factor rows (88-byte rows per lane, 11 strided loads per
-// block; sweep probe: 589 -> 250 us without them), and those loads sit on the level's critical path. Here
-// the workgroup is split by wavefront: kWsProd producer waves copy the factor blocks (and column indices) of
-// level l+1 into LDS with direct global -> LDS loads (16 bytes per lane over each row's contiguous blocks)
-// while the consumer waves compute level l from the other LDS buffer; a level's consumers wait only on
-// their x segments. Wait counters are per wave, so the consumers never wait on the copies; the two roles
-// meet at the level barrier. Rows whose staged span does not fit the buffer (very wide levels) read their
-// blocks from global memory. The backward sweep stages inv(D_i) after row i's upper blocks.
-// Same arithmetic, operation for operation, as k_ilu_fwd_part / k_ilu_bwd_part.
-// Row layout (host-built, Sched::sslot): {row, k0, k1, LDS double offset of the row's span in its level}, span
-// = pad2(nb NV^2) (+ pad2(NV^2) backward), pad2 = round up to even (16-byte copies).
-// LDS: two buffers of capd doubles, column indices [2][RPB][maxb], and (backward) v[RPB][NV].
-constexpr int kWsTB = 1024, kWsProd = 4;  // threads per workgroup, producer waves (the last ones)
-__device__ __forceinline__ int pad2(int n) { return (n + 1) & ~1; }
-template <int NV, bool BWD>
-__device__ __forceinline__ int ws_span(int nb) {
-  return pad2(nb * NV * NV) + (BWD ? pad2(NV * NV) : 0);
-}
-// Direct global -> LDS loads (global_load_lds_dword / _dwordx4): lane L's BYTES bytes land at wave_dst + BYTES L;
-// wave_dst is made wave-uniform here (it goes to M0).
-typedef __attribute__((address_space(3))) char lds_char;
-__device__ __forceinline__ lds_char* wave_lds(void* p) {
-  return (lds_char*)(size_t)__builtin_amdgcn_readfirstlane((int)(size_t)(lds_char*)p);
-}
-__device__ __forceinline__ void g2lds4(const void* src, void* wave_dst) {
-  __builtin_amdgcn_global_load_lds(src, wave_lds(wave_dst), 4, 0, 0);
-}
-__device__ __forceinline__ void g2lds16(const void* src, void* wave_dst) {
-  __builtin_amdgcn_global_load_lds(src, wave_lds(wave_dst), 16, 0, 0);
-}
-
-// PF > 0: no LDS staging (capd = 0); the producer waves instead load the blocks of level l+PF while level l runs
-// (global -> LDS loads into a per-wave scratch slice that nothing reads), so that they stream from HBM into the
-// caches ahead of the consumers' own loads. The producers never wait on these loads (their barriers do not fence).
-// PROBE (timing builds only): 1 = no copies, 2 = no consumer work.
-template <int NV, bool BWD, int PROBE = 0, int PF = 0>
-__global__ __launch_bounds__(kWsTB) void k_ilu_sweep_ws(
-    const int32_t* __restrict__ part_lvl, const int32_t* __restrict__ lvl_ptr, const int4* __restrict__ sslot,
-    const int32_t* __restrict__ col, const double* __restrict__ F, const double* __restrict__ b,
-    double* __restrict__ x, int capd, int maxb, int nnzb, int* __restrict__ done, const int* __restrict__ conv) {
-  if (skip_sweep(done, conv)) return;
-  constexpr int NV2 = NV * NV, CT = kWsTB - 64 * kWsProd, RPB = CT / NV, CH = 2;
-  extern __shared__ double lds[];
-  int* const cbuf = reinterpret_cast<int*>(lds + 2 * (size_t)capd);               // [2][RPB][maxb]
-  double* const v = lds + 2 * (size_t)capd + ((2 * RPB * maxb + 1) >> 1);          // BWD: [RPB][NV]
-  const int t = threadIdx.x, wave = t >> 6;
-  const int p = blockIdx.x;
-  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
-  auto fits = [&](int so, int nb) { return so + ws_span<NV, BWD>(nb) <= capd; };
-
-  if (PF > 0 && wave >= CT / 64) {  // ---- prefetching producer waves
-    const int pw = wave - CT / 64, lane = t & 63;
-    double* scratch = lds + 2 * (size_t)capd + ((2 * RPB * maxb + 1) >> 1) + (BWD ? RPB * NV : 0) + pw * 128;
-    auto warm = [&](int L) {
-      if (L >= l1 || (PROBE & 1)) return;
-      const int R0 = lvl_ptr[L], R1 = lvl_ptr[L + 1];
-      for (int r = R0 + pw; r < R1; r += kWsProd) {
-        const int4 sl = sslot[__builtin_amdgcn_readfirstlane(r)];  // uniform: a scalar load
-        const int nb = sl.y < sl.z ? sl.z - sl.y : 0;
-        const double* src = F + (size_t)sl.y * NV2;
-        const int ch = (nb * NV2 + 1) >> 1;
-        for (int c0 = 0; c0 < ch; c0 += 64)
-          if (c0 + lane < ch) g2lds16(src + 2 * (c0 + lane), scratch);
-        if (BWD) {
-          const double* s2 = F + (size_t)(nnzb + sl.x) * NV2;
-          constexpr int ch2 = (NV2 + 1) >> 1;
-          for (int c0 = 0; c0 < ch2; c0 += 64)
-            if (c0 + lane < ch2) g2lds16(s2 + 2 * (c0 + lane), scratch);
-        }
-      }
-    };
-    for (int L = l0; L < l0 + PF; ++L) warm(L);
-    __builtin_amdgcn_s_barrier();
-    for (int l = l0; l < l1; ++l) {
-      warm(l + PF);
-      if (BWD) {
-        for (int base = lvl_ptr[l]; base < lvl_ptr[l + 1]; base += RPB) {
-          __builtin_amdgcn_s_barrier();
-          __builtin_amdgcn_s_barrier();
-        }
-      }
-      __builtin_amdgcn_s_barrier();
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    return;
-  }
-  if (wave >= CT / 64) {  // ---- producer waves
-    const int pw = wave - CT / 64, lane = t & 63;
-    // the wave's rows of level L are r = R0 + pw + kWsProd j: lane j holds slot j (loaded one level ahead, so a
-    // level's copies start right after the barrier), rows are broadcast one by one (a load per row would wait, in
-    // order, on the previous row's copies)
-    auto load_slots = [&](int L, int j0) {
-      int4 my = make_int4(0, 0, 0, 0);
-      if (L < l1) {
-        const int rj = lvl_ptr[L] + pw + kWsProd * (j0 + lane);
-        if (rj < lvl_ptr[L + 1]) my = sslot[rj];
-      }
-      return my;
-    };
-    auto produce = [&](int L, int4 my) {  // level L into buffer (L - l0) & 1
-      if (L >= l1 || (PROBE & 1)) return;
-      const int bf = (L - l0) & 1, R0 = lvl_ptr[L], R1 = lvl_ptr[L + 1];
-      for (int j0 = 0; R0 + pw + kWsProd * j0 < R1; j0 += 64) {
-        if (j0) my = load_slots(L, j0);  // levels wider than 64 kWsProd rows
-        const int nj = min(64, (R1 - (R0 + pw + kWsProd * j0) + kWsProd - 1) / kWsProd);
-        for (int j = 0; j < nj; ++j) {
-          const int r = R0 + pw + kWsProd * (j0 + j);
-          const int4 sl = make_int4(__builtin_amdgcn_readlane(my.x, j), __builtin_amdgcn_readlane(my.y, j),
-                                    __builtin_amdgcn_readlane(my.z, j), __builtin_amdgcn_readlane(my.w, j));
-          const int nb = sl.y < sl.z ? sl.z - sl.y : 0;
-          if (!fits(sl.w, nb)) break;  // spans are laid out in slot order: the rest of the level does not fit either
-          double* dst = lds + (size_t)bf * capd + sl.w;
-          const double* src = F + (size_t)sl.y * NV2;
-          const int ch = (nb * NV2 + 1) >> 1;
-          for (int c0 = 0; c0 < ch; c0 += 64)
-            if (c0 + lane < ch) g2lds16(src + 2 * (c0 + lane), dst + 2 * c0);
-          if (BWD) {
-            const double* s2 = F + (size_t)(nnzb + sl.x) * NV2;
-            double* d2 = dst + pad2(nb * NV2);
-            constexpr int ch2 = (NV2 + 1) >> 1;
-            for (int c0 = 0; c0 < ch2; c0 += 64)
-              if (c0 + lane < ch2) g2lds16(s2 + 2 * (c0 + lane), d2 + 2 * c0);
-          }
-          const int rr = r - R0;
-          if (rr < RPB && lane < nb) g2lds4(col + sl.y + lane, cbuf + (bf * RPB + rr) * maxb);
-        }
-      }
-    };
-    int4 my = load_slots(l0, 0);
-    produce(l0, my);
-    my = load_slots(l0 + 1, 0);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    for (int l = l0; l < l1; ++l) {
-      produce(l + 1, my);
-      my = load_slots(l + 2, 0);
-      if (BWD) {  // the consumers' two barriers per pass
-        for (int base = lvl_ptr[l]; base < lvl_ptr[l + 1]; base += RPB) {
-          __builtin_amdgcn_s_barrier();
-          __builtin_amdgcn_s_barrier();
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0);  // level l+1's copies have landed
-      __syncthreads();
-    }
-    return;
-  }
-
-  // ---- consumer waves: thread (rl, a) = component a of the level's rl-th row
-  const int rl = t / NV, a = t - rl * NV;
-  const bool lane = rl < RPB;
-  int4 nxt = make_int4(-1, 0, 0, 0);
-  if (lane && l0 < l1 && lvl_ptr[l0] + rl < lvl_ptr[l0 + 1]) nxt = sslot[lvl_ptr[l0] + rl];
-  __syncthreads();
-  for (int l = l0; l < l1; ++l) {
-    const int bf = (l - l0) & 1;
-    const double* fb = lds + (size_t)bf * capd;
-    const int* cb = cbuf + (bf * RPB + rl) * maxb;
-    const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
-    const int4 cur = nxt;
-    nxt = make_int4(-1, 0, 0, 0);
-    if (lane && l + 1 < l1 && r1 + rl < lvl_ptr[l + 2]) nxt = sslot[r1 + rl];
-
-    // one row: fwd x_i = b_i - sum_k F_k x_col(k); bwd v = x_i - sum_k F_k x_col(k), then x_i = inv(D_i) v.
-    // pre: its b / x value and the x segments of its first CH blocks (loads only); fin: the arithmetic
-    double acc = 0.0, xa[CH][NV];
-    auto pre = [&](const int4 sl, bool first) {
-      const int i = sl.x, k0 = sl.y, nb = sl.z > sl.y ? sl.z - sl.y : 0;
-      const bool stc = fits(sl.w, nb) && first && !(PROBE & 1);  // column indices staged too (first pass rows)
-      acc = BWD ? x[(size_t)i * NV + a] : b[(size_t)i * NV + a];
-#pragma unroll
-      for (int u = 0; u < CH; ++u)
-        if (u < nb) {
-          const int cj = stc ? cb[u] : col[k0 + u];
-#pragma unroll
-          for (int c = 0; c < NV; ++c) xa[u][c] = x[(size_t)cj * NV + c];
-        }
-    };
-    auto fin = [&](const int4 sl, bool first) -> double {
-      const int k0 = sl.y, nb = sl.z > sl.y ? sl.z - sl.y : 0;
-      const bool st = fits(sl.w, nb);
-      const bool stc = st && first && !(PROBE & 1);
-      double sum = 0.0, ac = acc;
-      for (int u = 0; u < nb; ++u) {
-        double xj[NV], fr[NV];
-        if (u < CH) {
-#pragma unroll
-          for (int c = 0; c < NV; ++c) xj[c] = (CH > 1 && u == 1) ? xa[CH - 1][c] : xa[0][c];
-        } else {
-          const int cj = stc ? cb[u] : col[k0 + u];
-#pragma unroll
-          for (int c = 0; c < NV; ++c) xj[c] = x[(size_t)cj * NV + c];
-        }
-        if (st) {
-#pragma unroll
-          for (int c = 0; c < NV; ++c) fr[c] = fb[sl.w + u * NV2 + a * NV + c];
-        } else {
-#pragma unroll
-          for (int c = 0; c < NV; ++c) fr[c] = F[(size_t)(k0 + u) * NV2 + a * NV + c];
-        }
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < NV; ++c) s += fr[c] * xj[c];
-        if (BWD)
-          sum += s;
-        else
-          ac -= s;
-      }
-      return BWD ? ac - sum : ac;
-    };
-    const bool act = lane && cur.x >= 0;
-    if (act && !(PROBE & 2)) pre(cur, true);
-    if (PROBE & 2) {
-      for (int base = r0; BWD && base < r1; base += RPB) {
-        __syncthreads();
-        __syncthreads();
-      }
-    } else if (!BWD) {
-      if (act) x[(size_t)cur.x * NV + a] = fin(cur, true);
-      for (int r = r0 + rl + RPB; lane && r < r1; r += RPB) {
-        const int4 sl = sslot[r];
-        pre(sl, false);
-        x[(size_t)sl.x * NV + a] = fin(sl, false);
-      }
-    } else {
-      for (int base = r0; base < r1; base += RPB) {
-        const int r = base + rl;
-        const bool on = lane && r < r1;
-        const bool first = base == r0;
-        int4 sl = cur;
-        if (on) {
-          if (!first) {
-            sl = sslot[r];
-            pre(sl, false);
-          }
-          v[rl * NV + a] = fin(sl, first);
-        }
-        __syncthreads();
-        if (on) {
-          const int nb = sl.z > sl.y ? sl.z - sl.y : 0;
-          double inv[NV];
-          if (fits(sl.w, nb)) {
-#pragma unroll
-            for (int c = 0; c < NV; ++c) inv[c] = fb[sl.w + pad2(nb * NV2) + a * NV + c];
-          } else {
-#pragma unroll
-            for (int c = 0; c < NV; ++c) inv[c] = F[(size_t)(nnzb + sl.x) * NV2 + a * NV + c];
-          }
-          double s = 0.0;
-#pragma unroll
-          for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
-          x[(size_t)sl.x * NV + a] = s;
-        }
-        __syncthreads();
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // ILU(0) application with the partition's vector resident in LDS: b is loaded once, the forward
 // and backward substitutions run level by level on the LDS copy, and x is stored once. The row
 // metadata of both schedules and the partition's column indices (local) are staged in LDS too, so the
@@ -1609,10 +1348,6 @@ int rx_la_prepare(rx_ctx* ctx) {
     if (NV_ <= 4)
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_lds<NV_>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
-    RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_sweep_ws<NV_, false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
-    RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_sweep_ws<NV_, true>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
   });
   return RX_OK;
 }
@@ -1655,75 +1390,6 @@ int rx_la_ilu_build(rx_ctx* ctx) {
   return RX_OK;
 }
 
-// Staged sweeps (k_ilu_sweep_ws): which = 1 forward, 2 backward, 3 both.
-static int ilu_staged(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv, int which,
-                      int probe = 0) {
-  const int nv = ctx->nVar;
-  const int rpb = (kWsTB - 64 * kWsProd) / nv;
-  const int maxb = std::max(1, ctx->rowmax);
-  // LDS bytes besides the two span buffers: column indices (+ v backward)
-  const size_t fix = sizeof(double) * ((2 * (size_t)rpb * maxb + 1) / 2);
-  const size_t vbytes = sizeof(double) * (size_t)rpb * nv;
-  auto capd_of = [&](const rx_ctx::Sched& S, size_t extra) {
-    const long fit = ((long)ctx->lds_max - (long)(fix + extra)) / (2 * (long)sizeof(double));
-    return (int)std::max(0L, std::min((long)S.maxlvld, fit)) & ~1;
-  };
-  const int fcap = capd_of(ctx->fs, 0), bcap = capd_of(ctx->bs, vbytes);
-  const size_t fshm = 2 * sizeof(double) * (size_t)fcap + fix;
-  const size_t bshm = 2 * sizeof(double) * (size_t)bcap + fix + vbytes;
-  const int nnzb = (int)ctx->nnzb;
-#ifdef RX_PROBE
-  if (probe >= 16 && nv == 11) {  // cache-prefetch variants: probe 16 + 2 (d - 1) + bwd, distance d = 1..3
-    const bool bwd = probe & 1;
-    const int d = 1 + (probe - 16) / 2;
-    const auto& S = bwd ? ctx->bs : ctx->fs;
-    const int4* sl = reinterpret_cast<const int4*>(S.sslot);
-    const void* kf[3] = {reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, false, 0, 1>),
-                         reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, false, 0, 2>),
-                         reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, false, 0, 3>)};
-    const void* kb[3] = {reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, true, 0, 1>),
-                         reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, true, 0, 2>),
-                         reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, true, 0, 3>)};
-    const void* kern = bwd ? kb[d - 1] : kf[d - 1];
-    const size_t shm = fix + (bwd ? vbytes : 0) + sizeof(double) * 128 * kWsProd;
-    RX_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
-    const double* F = ctx->f[RX_F_ILU];
-    int cap = 0;
-    void* args[] = {(void*)&S.part_lvl, (void*)&S.lvl_ptr, (void*)&sl, (void*)&ctx->col, (void*)&F, (void*)&b,
-                    (void*)&x, (void*)&cap, (void*)&maxb, (void*)&nnzb, (void*)&done, (void*)&conv};
-    RX_HIP(hipLaunchKernel(kern, dim3(ctx->npart), dim3(kWsTB), args, shm, ctx->stream));
-    return RX_OK;
-  }
-  if (probe && nv == 11) {
-    const bool bwd = which != 1;
-    const auto& S = bwd ? ctx->bs : ctx->fs;
-    const int4* sl = reinterpret_cast<const int4*>(S.sslot);
-    const void* kern = bwd ? (probe == 1 ? reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, true, 1>)
-                                         : reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, true, 2>))
-                           : (probe == 1 ? reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, false, 1>)
-                                         : reinterpret_cast<const void*>(&k_ilu_sweep_ws<11, false, 2>));
-    RX_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
-    const double* F = ctx->f[RX_F_ILU];
-    int cap = bwd ? bcap : fcap;
-    void* args[] = {(void*)&S.part_lvl, (void*)&S.lvl_ptr, (void*)&sl, (void*)&ctx->col, (void*)&F, (void*)&b,
-                    (void*)&x, (void*)&cap, (void*)&maxb, (void*)&nnzb, (void*)&done, (void*)&conv};
-    RX_HIP(hipLaunchKernel(kern, dim3(ctx->npart), dim3(kWsTB), args, bwd ? bshm : fshm, ctx->stream));
-    return RX_OK;
-  }
-#endif
-  (void)probe;
-  if (which & 1)
-    RX_NV_SWITCH(nv, (k_ilu_sweep_ws<NV_, false><<<ctx->npart, kWsTB, fshm, ctx->stream>>>(
-                     ctx->fs.part_lvl, ctx->fs.lvl_ptr, reinterpret_cast<const int4*>(ctx->fs.sslot), ctx->col,
-                     ctx->f[RX_F_ILU], b, x, fcap, maxb, nnzb, done, conv)));
-  if (which & 2)
-    RX_NV_SWITCH(nv, (k_ilu_sweep_ws<NV_, true><<<ctx->npart, kWsTB, bshm, ctx->stream>>>(
-                     ctx->bs.part_lvl, ctx->bs.lvl_ptr, reinterpret_cast<const int4*>(ctx->bs.sslot), ctx->col,
-                     ctx->f[RX_F_ILU], x, x, bcap, maxb, nnzb, done, conv)));
-  RX_HIP(hipGetLastError());
-  return RX_OK;
-}
-
 int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv) {
   const int nv = ctx->nVar;
   const size_t shm = sizeof(double) * ((size_t)ctx->maxpart * nv + (size_t)(256 / nv) * nv + 1) +
@@ -1739,15 +1405,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
     return rx_la_exchange(ctx, x, nv);  // ComputeILUPreconditioner's closing SendReceive_Solution (:1513)
   }
   static const bool narrow = getenv("RX_NARROW_APPLY") != nullptr;  // diagnosis: the 256-thread sweeps
-  // the staged sweeps (k_ilu_sweep_ws) are opt-in: bitwise equal to the wide ones, not yet faster at C3
-  // (fwd 628 vs 607 us, bwd 814 vs 827 us; profiles/r03_stage_probe.log)
-  static const bool no_stage = getenv("RX_STAGE") == nullptr;
   const int width = std::max(ctx->fs.maxwidth, ctx->bs.maxwidth);
-  if (!narrow && !no_stage && nv > 4 && ctx->rowmax <= 64 && width * nv > 256) {
-    const int rc = ilu_staged(ctx, b, x, done, conv, 3);
-    if (rc) return rc;
-    return rx_la_exchange(ctx, x, nv);
-  }
   if (!narrow && width * nv > 256) {
     const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
     const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
@@ -1892,31 +1550,6 @@ extern "C" int rx_debug_sweep_probe(rx_ctx* ctx, int mode, int reps, double* ms)
             ctx->bs.part_lvl, ctx->bs.lvl_ptr, reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col,
             ctx->f[RX_F_ILU], rx_invd_buf(ctx), x, nullptr, nullptr);
         break;
-      case 12:
-      case 13:
-      case 14:
-      case 15: {  // staged sweep timing variants: 12/13 fwd/bwd without copies, 14/15 fwd/bwd copies only
-        const int which = (mode & 1) ? 2 : 1, pr = mode < 14 ? 1 : 2;
-        const int rc = ilu_staged(ctx, b, x, nullptr, nullptr, which, pr);
-        if (rc) return rc;
-        break;
-      }
-      case 16:
-      case 17:
-      case 18:
-      case 19:
-      case 20:
-      case 21: {  // cache-prefetch producers, distance 1..3, fwd / bwd
-        const int rc = ilu_staged(ctx, b, x, nullptr, nullptr, (mode & 1) ? 2 : 1, mode);
-        if (rc) return rc;
-        break;
-      }
-      case 10:  // the staged forward sweep
-      case 11: {  // the staged backward sweep
-        const int rc = ilu_staged(ctx, b, x, nullptr, nullptr, mode == 10 ? 1 : 2);
-        if (rc) return rc;
-        break;
-      }
       default:
         return RX_ERR_ARG;
     }
