@@ -257,6 +257,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         }
         order.insert(order.end(), loc.begin(), loc.end());
         part_lvl[p + 1] = part_lvl[p] + maxl + 1;
+        S.maxlev = std::max(S.maxlev, maxl + 1);
       }
       S.nlevels = part_lvl[np];
       std::vector<int32_t> slot(4 * order.size());
@@ -342,6 +343,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         }
       }
       std::vector<int32_t> plan((size_t)Nd * 32, 0);
+      bool grp_ok = true;
       for (int64_t r = 0; r < Nd; ++r) {
         const int32_t i = fo[r];
         int32_t* rec = plan.data() + r * 32;
@@ -370,7 +372,10 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         }
         rec[6] = ok ? nlow : -1;
         rec[7] = ok ? npair : 0;
+        for (int32_t h = 0; h < npair && ok; ++h) ok = rec[15 + 2 * h] == rec[2];
+        grp_ok = grp_ok && ok;
       }
+      ctx->ilu_grp_ok = grp_ok;
       CK(dupload(ctx, &ctx->ilu_plan, plan.data(), plan.size()));
     }
 
@@ -658,6 +663,10 @@ int rx_download(rx_ctx* ctx, rx_field f, double* host, int64_t count) {
   if (f == RX_F_RES || f == RX_F_JAC) {
     int rc = ensure_assembled(ctx);
     if (rc && rc != RX_ERR_STATE) return rc;
+  }
+  if (f == RX_F_ILU && ctx->assembled) {  // the factor with the blocks ILU(0) leaves unchanged (rx_sweeps.hip);
+    int rc = rx_la_ilu_materialize(ctx);  // while a residual is being assembled the field holds its scratch
+    if (rc) return rc;
   }
   RX_HIP(hipMemcpyAsync(host, ctx->f[f], count * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   RX_HIP(hipStreamSynchronize(ctx->stream));

@@ -87,6 +87,7 @@ struct rx_ctx {
   int32_t* upd = nullptr;       // [2 * n_upd] (kk, pos) pairs
   int32_t* ilu_plan = nullptr;  // [N][32] per forward-schedule slot row plan (rx_sweeps.hip)
   int ilu_waves = 1;            // wavefronts per workgroup of the ILU factorisation
+  bool ilu_grp_ok = false;      // every row's plan is compact and updates only its diagonal (k_ilu_build_grp)
   // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
   // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])
   struct Sched {
@@ -94,7 +95,7 @@ struct rx_ctx {
     int32_t* lvl_ptr = nullptr;
     int32_t* rows = nullptr;
     int32_t* slot = nullptr;      // [rows][4] {row, klo, diag, khi} in schedule order
-    int nlevels = 0, maxwidth = 0;
+    int nlevels = 0, maxwidth = 0, maxlev = 0;  // maxlev: most levels of one partition
   } fs, bs;
   double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)
   double* xstar = nullptr;      // [N][nVar] LU-SGS forward-sweep result (halo values)
@@ -238,6 +239,8 @@ int rx_la_ilu_build(rx_ctx* ctx);
 int rx_la_prepare(rx_ctx* ctx);
 int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv);
 double* rx_invd_buf(rx_ctx* ctx);
+const double* rx_ilu_upper(rx_ctx* ctx);  // the factor's upper blocks as the sweeps read them
+int rx_la_ilu_materialize(rx_ctx* ctx);   // complete ILU field for rx_download
 int rx_ilu_stage();      // staged blocks per wave of the ILU(0) build (rx_sweeps.hip kStage)
 int rx_ilu_max_waves();  // wavefronts per workgroup cap of the ILU(0) build
 int rx_la_krylov_alloc(rx_ctx* ctx, int m);

@@ -492,6 +492,285 @@ __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __r
 #undef RX_STAMP
 }
 
+// ---------------------------------------------------------------------------------------------
+// ILU(0) factorisation with four rows per wavefront (round 3; the flow systems, 5 <= NV <= 16).
+// A 16-lane group (one DPP row) owns one row of a dependency level; lane c of the group holds COLUMN c of the
+// blocks it works on, so every global access of a block is a run of consecutive doubles across the lanes:
+//   W = A_ij inv(A_jj):   lane c: W[a][c] = sum_q A_ij[a][q] inv(A_jj)[q][c] with column c of inv(A_jj) in
+//                         registers and A_ij in the group's LDS slot (group-uniform, i.e. broadcast, reads);
+//   A_ii -= A_ji W:       lane c: column c of W in registers, A_ji in the LDS slot;
+//   inv(D_i):             D_i transposed through the slot, wave_factor_rows within the group (pivot row
+//                         broadcast by DPP row_newbcast), the factorisation back through the slot, lane c
+//                         solving unit column c.
+// Every sum is the reference's (from 0.0, q ascending; the elimination of Gauss_Elimination :594-643), so the
+// factor is bitwise k_ilu_build_part's. The kernel takes meshes whose row plans are compact and update only the
+// diagonal (ctx->ilu_grp_ok: 5-point quad / 7-point hex stencils, i.e. the jet meshes, where no two neighbours of
+// a point are neighbours of each other); others keep k_ilu_build_part. There ILU(0) changes no upper block and
+// no block outside the partition, so those are not copied: the triangular sweeps read the upper blocks from the
+// matrix itself (rx_ilu_upper), and rx_download("ILU") materialises the copies (k_ilu_materialize). One level
+// is one round of all groups (48 per workgroup), so the rows of a level run concurrently instead of in rounds
+// of one row per wavefront.
+template <int L>
+__device__ __forceinline__ double grp_bcast(double v) {  // lane L of the lane's 16-lane row
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u, 0x150 + L, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x150 + L, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// wave_factor_rows within a 16-lane group: lane a holds row a. The broadcasts run on every lane (DPP reads a
+// source lane that must be active), the update only on the rows below the pivot.
+template <int NV, int JJ = 0>
+__device__ __forceinline__ void grp_factor_rows(double (&d)[NV], int a) {
+  if constexpr (JJ < NV - 1) {
+    double pr[NV];
+#pragma unroll
+    for (int kk = JJ; kk < NV; ++kk) pr[kk] = grp_bcast<JJ>(d[kk]);
+    const double w = d[JJ] / pr[JJ];
+    if (a > JJ) {
+#pragma unroll
+      for (int kk = JJ + 1; kk < NV; ++kk) d[kk] -= w * pr[kk];
+      d[JJ] = w;
+    }
+    grp_factor_rows<NV, JJ + 1>(d, a);
+  }
+}
+
+// Row offset of an LDS operand, tied to a value computed two rows earlier: the reads of row ii cannot be issued
+// before `dep` exists, so an unrolled product / solve keeps about two rows of operands in flight instead of
+// issuing all NV^2 reads up front (which spills).
+__device__ __forceinline__ int lds_row(int off, double dep) {
+  asm volatile("" : "+v"(off) : "v"(dep));
+  return off;
+}
+// The same tied to every accumulator of a block product: row q's operand reads wait for row q-1's updates of all
+// NV accumulators (tied to one of them, the compiler finishes that one chain first and defers the others).
+template <int NV>
+__device__ __forceinline__ int lds_row_tied(int off, const double (&v)[NV]) {
+#pragma unroll
+  for (int c = 0; c < NV; ++c) asm volatile("" : "+v"(off) : "v"(v[c]));
+  return off;
+}
+
+// wave_solve_lds with the factorisation stored at row stride NP.
+template <int NV, int NP>
+__device__ __forceinline__ void grp_solve_lds(const double* LU, double (&rhs)[NV]) {
+#pragma unroll
+  for (int ii = 1; ii < NV; ++ii) {
+    const int o = lds_row(ii * NP, rhs[ii >= 2 ? ii - 2 : 0]);
+#pragma unroll
+    for (int jj = 0; jj < ii; ++jj) rhs[ii] -= LU[o + jj] * rhs[jj];
+  }
+  rhs[NV - 1] = rhs[NV - 1] / LU[(NV - 1) * NP + NV - 1];
+#pragma unroll
+  for (int ii = NV - 2; ii >= 0; --ii) {
+    const int o = lds_row(ii * NP, rhs[ii + 2 < NV ? ii + 2 : NV - 1]);
+    double aux = 0.0;
+#pragma unroll
+    for (int jj = ii + 1; jj < NV; ++jj) aux += LU[o + jj] * rhs[jj];
+    rhs[ii] = (rhs[ii] - aux) / LU[o + ii];
+  }
+}
+
+#ifndef RX_GRP_WAVES
+#define RX_GRP_WAVES 12
+#endif
+constexpr int kGrpMaxWaves = RX_GRP_WAVES;
+constexpr int kGrpTraceRows = 64, kGrpTraceGroups = 64, kGrpTraceLevels = 512;  // >= 4 * kGrpMaxWaves groups
+template <int NV>
+constexpr int grp_np() { return (NV + 1) & ~1; }
+template <int NV>
+constexpr int grp_slot_doubles() { return NV * grp_np<NV>() + kPlan / 2; }
+
+template <int NV>
+__global__ __launch_bounds__(64 * kGrpMaxWaves) void k_ilu_build_grp(const int32_t* __restrict__ part_lvl,
+                                                                    const int32_t* __restrict__ lvl_ptr,
+                                                                    const int32_t* __restrict__ plan,
+                                                                    const double* __restrict__ A,
+                                                                    double* __restrict__ F, double* __restrict__ invD,
+                                                                    long long* __restrict__ trace) {
+  constexpr int NV2 = NV * NV, NP = grp_np<NV>();
+  extern __shared__ double lds[];
+  const int a = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = blockDim.x >> 4;
+  double* S = lds + (size_t)grp * grp_slot_doubles<NV>();  // inv(A_jj), then W, then the LU of D_i
+  int* rec = reinterpret_cast<int*>(S + NV * NP);          // the row's plan record
+  const int p = blockIdx.x, l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  // the partition's level pointers in LDS (behind the group slots): the loop bounds and the next-row search read
+  // them every row
+  int* lp = reinterpret_cast<int*>(lds + (size_t)ngrp * grp_slot_doubles<NV>()) - l0;
+  for (int l = l0 + (int)threadIdx.x; l <= l1; l += blockDim.x) lp[l] = lvl_ptr[l];
+  __syncthreads();
+  auto next_slot = [&](int r, int l) -> int {  // the group's next row after slot r of level l, -1 if none
+    if (r + ngrp < lp[l + 1]) return r + ngrp;
+    for (int ll = l + 1; ll < l1; ++ll)
+      if (lp[ll] + grp < lp[ll + 1]) return lp[ll] + grp;
+    return -1;
+  };
+  int2 prec = make_int2(0, 0);
+  {
+    int pr = -1;
+    for (int ll = l0; ll < l1 && pr < 0; ++ll)
+      if (lp[ll] + grp < lp[ll + 1]) pr = lp[ll] + grp;
+    if (pr >= 0) prec = reinterpret_cast<const int2*>(plan + (size_t)pr * kPlan)[a];
+  }
+  // optional phase trace of block 0 (tools/ilu_trace.py --grp): per group, per row 4 stamps; then one per level
+  long long* tr = (trace && blockIdx.x == 0 && a == 0) ? trace + 1 + (size_t)grp * kGrpTraceRows * 8 : nullptr;
+  int trow = 0;
+#define RX_GSTAMP(ph)                                                                             \
+  do {                                                                                            \
+    if (tr && trow < kGrpTraceRows) tr[trow * 8 + (ph)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+  constexpr int PB = (NV2 + 15) / 16;  // doubles per lane of a block loaded lane-contiguously
+  for (int l = l0; l < l1; ++l) {
+    for (int r = lp[l] + grp; r < lp[l + 1]; r += ngrp) {
+      RX_GSTAMP(0);
+      // the lane's column, laundered per row so that nothing derived from it is hoisted out of the row loop
+      // (the hoisted unit vectors / addresses otherwise spill)
+      int al = a;
+      asm volatile("" : "+v"(al));
+      const bool act = al < NV;
+      const int ac = act ? al : 0;  // lanes NV..15 of a group load column 0 and store nothing
+      reinterpret_cast<int2*>(rec)[al] = prec;
+      {
+        const int nr = next_slot(r, l);  // the next row's plan is an input: fetched now, used next row
+        if (nr >= 0) prec = reinterpret_cast<const int2*>(plan + (size_t)nr * kPlan)[al];
+      }
+      wave_sync();
+      const int i = rec[0], k0 = rec[1], kd = rec[2];
+      // every load of the diagonal and the first lower block issued together: A blocks (inputs), inv(A_jj) (a
+      // finished row), A_jk (an upper block of row j, i.e. unchanged A)
+      double d[NV], s[NV], bl[PB], jl[PB];
+#pragma unroll
+      for (int q = 0; q < NV; ++q) d[q] = A[(size_t)kd * NV2 + q * NV + ac];
+      if (kd > k0) {
+        const int j0 = rec[8], kk0 = rec[14];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)j0 * NV2 + q * NV + ac];
+#pragma unroll
+        for (int u = 0; u < PB; ++u)
+          if (16 * u + al < NV2) bl[u] = A[(size_t)k0 * NV2 + 16 * u + al];
+        if (rec[11] > 0) {
+#pragma unroll
+          for (int u = 0; u < PB; ++u)
+            if (16 * u + al < NV2) jl[u] = A[(size_t)kk0 * NV2 + 16 * u + al];
+        }
+      }
+      int pcur = 0;
+      for (int k = k0; k < kd; ++k) {
+        const int t = k - k0, nu = rec[11 + t];
+        wave_sync();
+#pragma unroll
+        for (int u = 0; u < PB; ++u)
+          if (16 * u + al < NV2) S[16 * u + al] = bl[u];  // A_ij, row-major (stride NV)
+        wave_sync();
+        if (t < 2) RX_GSTAMP(4 + 2 * t);
+        // W = A_ij * inv(A_jj)  (MatrixMatrixProduct, sum from 0.0 over q ascending): column c of W
+        double w[NV];
+#pragma unroll
+        for (int e = 0; e < NV; ++e) w[e] = 0.0;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+          const int o = lds_row_tied<NV>(q, w);
+#pragma unroll
+          for (int e = 0; e < NV; ++e) w[e] += S[o + e * NV] * s[q];
+        }
+        if (t < 2) RX_GSTAMP(5 + 2 * t);
+        wave_sync();
+        if (nu > 0) {
+#pragma unroll
+          for (int u = 0; u < PB; ++u)
+            if (16 * u + al < NV2) S[16 * u + al] = jl[u];  // A_ji
+        }
+        wave_sync();
+        if (k + 1 < kd) {  // the next lower block's loads, into the registers just freed (before W's store, so
+                           // that waiting for them does not wait for the store)
+          const int jn = rec[9 + t];
+#pragma unroll
+          for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)jn * NV2 + q * NV + ac];
+#pragma unroll
+          for (int u = 0; u < PB; ++u)
+            if (16 * u + al < NV2) bl[u] = A[(size_t)(k + 1) * NV2 + 16 * u + al];
+          if (rec[12 + t] > 0) {
+            const int kk = rec[14 + 2 * (pcur + nu)];
+#pragma unroll
+            for (int u = 0; u < PB; ++u)
+              if (16 * u + al < NV2) jl[u] = A[(size_t)kk * NV2 + 16 * u + al];
+          }
+        }
+        if (act) {
+#pragma unroll
+          for (int e = 0; e < NV; ++e) F[(size_t)k * NV2 + e * NV + al] = w[e];
+        }
+        // D_i -= A_ji * W (left-multiply quirk; the plan's updates of this row all hit the diagonal)
+        for (int h = 0; h < nu; ++h, ++pcur) {
+          if (h > 0) {  // further A_jk of the same lower block (not on quad / hex meshes)
+            const int kk = rec[14 + 2 * pcur];
+            double xl[PB];
+#pragma unroll
+            for (int u = 0; u < PB; ++u)
+              if (16 * u + al < NV2) xl[u] = A[(size_t)kk * NV2 + 16 * u + al];
+            wave_sync();
+#pragma unroll
+            for (int u = 0; u < PB; ++u)
+              if (16 * u + al < NV2) S[16 * u + al] = xl[u];
+            wave_sync();
+          }
+          double x[NV];
+#pragma unroll
+          for (int e = 0; e < NV; ++e) x[e] = 0.0;
+#pragma unroll
+          for (int q = 0; q < NV; ++q) {
+            const int o = lds_row_tied<NV>(q, x);
+#pragma unroll
+            for (int e = 0; e < NV; ++e) x[e] += S[o + e * NV] * w[q];
+          }
+#pragma unroll
+          for (int e = 0; e < NV; ++e) d[e] -= x[e];
+        }
+      }
+      if (act) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) F[(size_t)kd * NV2 + e * NV + al] = d[e];
+      }
+      RX_GSTAMP(1);
+      // inv(D_i): D_i transposed through the slot (lane a then holds row a), the right-looking elimination in the
+      // group, the factorisation back to the slot, one unit column per lane
+      wave_sync();
+      if (act) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) S[e * NP + al] = d[e];
+      }
+      wave_sync();
+      double rw[NV];
+#pragma unroll
+      for (int e = 0; e < NV; ++e) rw[e] = S[ac * NP + e];
+      grp_factor_rows<NV>(rw, al);
+      RX_GSTAMP(2);
+      wave_sync();
+      if (act) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) S[al * NP + e] = rw[e];
+      }
+      wave_sync();
+      double rhs[NV];
+#pragma unroll
+      for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == al) ? 1.0 : 0.0;
+      grp_solve_lds<NV, NP>(S, rhs);
+      if (act) {
+#pragma unroll
+        for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + al] = rhs[rr];
+      }
+      RX_GSTAMP(3);
+      ++trow;
+    }
+    __syncthreads();
+    if (trace && blockIdx.x == 0 && threadIdx.x == 0 && l - l0 < kGrpTraceLevels)
+      trace[1 + kGrpTraceGroups * kGrpTraceRows * 8 + (l - l0)] = (long long)__builtin_amdgcn_s_memtime();
+  }
+  if (trace && blockIdx.x == 0 && threadIdx.x == 0) trace[0] = (long long)__builtin_amdgcn_s_memtime();
+#undef RX_GSTAMP
+}
+
 // ILU(0) factorisation for small blocks (NV <= 4, the SST system's 2x2): one thread per row, rows of a
 // dependency level spread over the workgroup. Same arithmetic as k_ilu_build_part: W = A_ij inv(A_jj)
 // (sums from 0.0, q ascending), A_ik -= A_jk W over the update plan in the reference's order, then
@@ -1065,6 +1344,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
                                                        const int32_t* __restrict__ b_lvl_ptr,
                                                        const int4* __restrict__ b_slot,
                                                        const int32_t* __restrict__ col, const double* __restrict__ F,
+                                                       const double* __restrict__ Fu,
                                                        const double* __restrict__ invD, const double* __restrict__ b,
                                                        double* __restrict__ x, int* __restrict__ done,
                                                        const int* __restrict__ conv) {
@@ -1135,7 +1415,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
   double icur[NV], inxt[NV];
   if (lane_ok && br0 + rl < b_lvl_ptr[bl0 + 1]) {
     const int4 sl = bsl[rl];
-    pf_load<NV>(ucur, F, sl.z + 1, sl.w, a);
+    pf_load<NV>(ucur, Fu, sl.z + 1, sl.w, a);
 #pragma unroll
     for (int c = 0; c < NV; ++c) icur[c] = invD[(size_t)sl.x * NV2 + a * NV + c];
   }
@@ -1143,7 +1423,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
     const int r0 = b_lvl_ptr[l], r1 = b_lvl_ptr[l + 1];
     if (lane_ok && l + 1 < bl1 && r1 + rl < b_lvl_ptr[l + 2]) {
       const int4 sl = bsl[r1 + rl - br0];
-      pf_load<NV>(unxt, F, sl.z + 1, sl.w, a);
+      pf_load<NV>(unxt, Fu, sl.z + 1, sl.w, a);
 #pragma unroll
       for (int c = 0; c < NV; ++c) inxt[c] = invD[(size_t)sl.x * NV2 + a * NV + c];
     }
@@ -1169,7 +1449,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
                 for (int c = 0; c < NV; ++c) s += ucur.f[tt][c] * xj[c];
               }
           } else {
-            const double* blk = F + (size_t)k * NV2 + a * NV;
+            const double* blk = Fu + (size_t)k * NV2 + a * NV;
 #pragma unroll
             for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
           }
@@ -1329,9 +1609,55 @@ __global__ __launch_bounds__(256) void k_lusgs_bwd_part(const int32_t* __restric
     default: return RX_ERR_ARG;                      \
   }
 
+template <int NV>
+void launch_ilu_build_grp(rx_ctx* ctx, int gwaves) {
+  if constexpr (NV >= 5) {
+    const size_t shm = sizeof(double) * (size_t)(4 * gwaves) * grp_slot_doubles<NV>() +
+                       sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1);
+    k_ilu_build_grp<NV><<<ctx->npart, 64 * gwaves, shm, ctx->stream>>>(
+        ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_plan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
+        ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)NV * NV, ctx->ilu_trace);
+  }
+}
+
 }  // namespace
 
 double* rx_invd_buf(rx_ctx* ctx) { return ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)ctx->nVar * ctx->nVar; }
+
+// The factorisation runs k_ilu_build_grp (the factor's upper blocks and the blocks outside the partition are
+// then the matrix's own, and are not copied).
+static bool ilu_grouped(const rx_ctx* ctx) {
+  static const bool rowwave = getenv("RX_ILU_ROWWAVE") != nullptr;  // A/B: one row per wavefront
+  return ctx->nVar >= 5 && ctx->ilu_grp_ok && !rowwave;
+}
+// Where the triangular sweeps read the factor's upper blocks.
+const double* rx_ilu_upper(rx_ctx* ctx) { return ilu_grouped(ctx) ? ctx->f[RX_F_JAC] : ctx->f[RX_F_ILU]; }
+
+namespace {
+// ILU_matrix as the reference holds it (rx_download of the ILU field after k_ilu_build_grp): the blocks ILU(0)
+// leaves unchanged (outside [klo, diag]) copied from the matrix. One wavefront per row.
+template <int NV>
+__global__ __launch_bounds__(256) void k_ilu_materialize(int N, const int32_t* __restrict__ rp,
+                                                         const int32_t* __restrict__ klo,
+                                                         const int64_t* __restrict__ diag,
+                                                         const double* __restrict__ A, double* __restrict__ F) {
+  constexpr int NV2 = NV * NV;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= N) return;
+  const int kd = (int)diag[i];
+  for (int k = rp[i]; k < rp[i + 1]; ++k)
+    if (k < klo[i] || k > kd)
+      for (int q = lane; q < NV2; q += 64) F[(size_t)k * NV2 + q] = A[(size_t)k * NV2 + q];
+}
+}  // namespace
+
+int rx_la_ilu_materialize(rx_ctx* ctx) {
+  if (!ilu_grouped(ctx) || !ctx->f[RX_F_ILU]) return RX_OK;
+  RX_NV_SWITCH(ctx->nVar, (k_ilu_materialize<NV_><<<(int)((ctx->Nd + 3) / 4), 256, 0, ctx->stream>>>(
+                              (int)ctx->Nd, ctx->rp, ctx->klo, ctx->diag, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU])));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
 #ifndef RX_ILU_MAX_WAVES
 #define RX_ILU_MAX_WAVES 12
 #endif
@@ -1345,6 +1671,9 @@ int rx_la_prepare(rx_ctx* ctx) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_part<NV_>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    if constexpr (NV_ >= 5)
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_grp<NV_>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     if (NV_ <= 4)
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_lds<NV_>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
@@ -1380,6 +1709,12 @@ int rx_la_ilu_build(rx_ctx* ctx) {
     RX_HIP(hipGetLastError());
     return RX_OK;
   }
+  if (ilu_grouped(ctx)) {
+    const int gwaves = std::max(1, std::min(kGrpMaxWaves, (ctx->fs.maxwidth + 3) / 4));
+    RX_NV_SWITCH(nv, (launch_ilu_build_grp<NV_>(ctx, gwaves)));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
   const int waves = ctx->ilu_waves;
   const size_t shm = sizeof(double) * (size_t)waves * ((ctx->rowmax + 1 + kStage) * nv * nv + kPlan / 2);
   RX_NV_SWITCH(nv, (k_ilu_build_part<NV_><<<ctx->npart, 64 * waves, shm, ctx->stream>>>(
@@ -1399,8 +1734,8 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
     RX_NV_SWITCH(nv, (k_ilu_apply_lds<NV_><<<ctx->npart, 256, shm, ctx->stream>>>(
                          ctx->part_ptr, ctx->rp, ctx->fs.part_lvl, ctx->fs.lvl_ptr,
                          reinterpret_cast<const int4*>(ctx->fs.slot), ctx->bs.part_lvl, ctx->bs.lvl_ptr,
-                         reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx),
-                         b, x, done, conv)));
+                         reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_ilu_upper(ctx),
+                         rx_invd_buf(ctx), b, x, done, conv)));
     RX_HIP(hipGetLastError());
     return rx_la_exchange(ctx, x, nv);  // ComputeILUPreconditioner's closing SendReceive_Solution (:1513)
   }
@@ -1412,7 +1747,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
     RX_NV_SWITCH(nv, (k_ilu_fwd_wide<NV_, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
                          ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->col, ctx->f[RX_F_ILU], b, x, done, conv)));
     RX_NV_SWITCH(nv, (k_ilu_bwd_wide<NV_, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
-                         ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx), x,
+                         ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, rx_ilu_upper(ctx), rx_invd_buf(ctx), x,
                          done, conv)));
     RX_HIP(hipGetLastError());
     return rx_la_exchange(ctx, x, nv);
@@ -1424,7 +1759,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
     RX_NV_SWITCH(nv, (k_ilu_fwd_wide<NV_, 256><<<ctx->npart, 256, 0, ctx->stream>>>(
                          ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->col, ctx->f[RX_F_ILU], b, x, done, conv)));
     RX_NV_SWITCH(nv, (k_ilu_bwd_wide<NV_, 256><<<ctx->npart, 256, 0, ctx->stream>>>(
-                         ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, ctx->f[RX_F_ILU], rx_invd_buf(ctx), x,
+                         ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, rx_ilu_upper(ctx), rx_invd_buf(ctx), x,
                          done, conv)));
     RX_HIP(hipGetLastError());
     return rx_la_exchange(ctx, x, nv);
@@ -1434,7 +1769,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                               ctx->f[RX_F_ILU], b, x, done, conv)));
   RX_NV_SWITCH(ctx->nVar, (k_ilu_bwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows, ctx->col, ctx->khi, ctx->diag,
-                              ctx->f[RX_F_ILU], rx_invd_buf(ctx), x, done, conv)));
+                              rx_ilu_upper(ctx), rx_invd_buf(ctx), x, done, conv)));
   RX_HIP(hipGetLastError());
   return rx_la_exchange(ctx, x, nv);
 }
@@ -1464,7 +1799,7 @@ int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, int* d
 
 // Debug: trace the phases of the ILU(0) factorisation of partition 0 (see tools/ilu_trace.py).
 extern "C" int rx_debug_ilu_trace(rx_ctx* ctx, long long* host, int64_t n) {
-  const int64_t need = 1 + 16 * 5 * 64;
+  const int64_t need = std::max<int64_t>(1 + 16 * 5 * 64, 1 + kGrpTraceGroups * kGrpTraceRows * 8 + kGrpTraceLevels);
   if (!ctx || n < need) return RX_ERR_ARG;
   if (!ctx->ilu_trace) {
     RX_HIP(hipMalloc(&ctx->ilu_trace, sizeof(long long) * need));
