@@ -88,7 +88,8 @@ def ilu_apply_kernels(N, nnzb, nVar, parts):
     return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
 
 
-def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, max_degree=4):
+def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, max_degree=4,
+                  ilu_grouped=os.environ.get("RX_ILU_ROWWAVE") is None):
     """Algorithmic bytes (or flops) per launch of the single-launch kernels timed per phase
     (each unique datum once per sweep)."""
     nVar, nPV, nG = ns + nDim + 2, ns + nDim + 5, ns + nDim + 2
@@ -115,8 +116,12 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq" + te),
         # k_source: V, dT/dU, volume, omega in; residual + the Jacobian's species rows out
         "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar + ns * nVar) * d, "k_source" + te),
-        # k_ilu_build_part: A in, factor + inv(D) out
-        "ILU_BUILD": hbm((2 * nnzb + N) * blk, "k_ilu_build_part" + tv),
+        # k_ilu_build_grp (the jet meshes: ILU(0) changes only the lower blocks and the diagonal): every
+        # block of A in once (the lower blocks and the diagonal of row i, the upper blocks as the A_ji of the rows
+        # below), the lower factor blocks W, the factored diagonal and inv(D_i) out. k_ilu_build_part (other meshes,
+        # RX_ILU_ROWWAVE=1): A in, the whole factor + inv(D) out
+        "ILU_BUILD": (hbm((nnzb + (nnzb - N) // 2 + 2 * N) * blk, "k_ilu_build_grp" + tv) if ilu_grouped else
+                      hbm((2 * nnzb + N) * blk, "k_ilu_build_part" + tv)),
         # SOLVE phase (inside the FGMRES graph; timed one launch at a time after the timed region):
         # y = A x: every block + its column index once, x gathered, y written
         "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d, "k_spmv" + tv),

@@ -37,7 +37,13 @@ K = {name: k for k, name in enumerate(KERNELS)}
 
 
 class RxError(RuntimeError):
-    pass
+    """A failed rx_* call: status = the rx_status code, index = rx_last_error_index (the first offending point /
+    edge a kernel flagged, -1 if none)."""
+
+    def __init__(self, msg, status=None, index=-1):
+        super().__init__(msg)
+        self.status = status
+        self.index = index
 
 
 class MechDesc(C.Structure):
@@ -269,7 +275,7 @@ def _chk(rc, what, ctx=None):
     if rc != RX_OK:
         msg = lib().rx_status_string(rc).decode()
         idx = lib().rx_last_error_index(ctx) if ctx is not None else -1
-        raise RxError(f"{what}: {msg} (status {rc}, index {idx})")
+        raise RxError(f"{what}: {msg} (status {rc}, index {idx})", status=rc, index=idx)
 
 
 class Mechanism:

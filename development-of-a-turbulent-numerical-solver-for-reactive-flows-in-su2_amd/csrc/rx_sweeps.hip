@@ -1849,13 +1849,120 @@ __global__ __launch_bounds__(TB) void k_probe_fwd(const int32_t* __restrict__ pa
     if (!(MODE & 2)) __syncthreads();
   }
 }
+// Compact sweep layouts (modes 10 / 11): the blocks a sweep reads, copied in schedule order, so that a level's
+// blocks are one contiguous run. Forward: the lower blocks [klo, diag) of slot r at Lc[off[r]..]; backward: the upper
+// blocks (diag, khi) and then inv(D_i) of slot r at Uc[off[r]..].
+template <int NV>
+__global__ __launch_bounds__(256) void k_probe_gather(int n, const int4* __restrict__ slot, const int64_t* __restrict__ off,
+                                                      int bwd, const double* __restrict__ A,
+                                                      const double* __restrict__ invD, double* __restrict__ dst) {
+  constexpr int NV2 = NV * NV;
+  const int r = blockIdx.x;
+  if (r >= n) return;
+  const int4 sl = slot[r];
+  const int k0 = bwd ? sl.z + 1 : sl.y, k1 = bwd ? sl.w : sl.z;
+  double* o = dst + (size_t)off[r] * NV2;
+  for (int q = threadIdx.x; q < (k1 - k0) * NV2; q += 256) o[q] = A[(size_t)k0 * NV2 + q];
+  if (bwd)
+    for (int q = threadIdx.x; q < NV2; q += 256) o[(size_t)(k1 - k0) * NV2 + q] = invD[(size_t)sl.x * NV2 + q];
+}
+
+template <int NV, int TB>
+__global__ __launch_bounds__(TB) void k_probe_fwd_c(const int32_t* __restrict__ part_lvl,
+                                                    const int32_t* __restrict__ lvl_ptr, const int4* __restrict__ slot,
+                                                    const int32_t* __restrict__ col, const double* __restrict__ Lc,
+                                                    const int64_t* __restrict__ off, const double* __restrict__ b,
+                                                    double* __restrict__ x) {
+  constexpr int NV2 = NV * NV, RPB = TB / NV;
+  const int p = blockIdx.x;
+  const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
+  const bool lane = rl < RPB;
+  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  for (int l = l0; l < l1; ++l) {
+    const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
+    for (int r = r0 + rl; lane && r < r1; r += RPB) {
+      const int4 sl = slot[r];
+      const int i = sl.x;
+      double xi = b[(size_t)i * NV + a];
+      row_blocks<NV>(Lc + ((int64_t)off[r] - sl.y) * NV2, col, x, sl.y, sl.z, a, [&](double s) { xi -= s; });
+      x[(size_t)i * NV + a] = xi;
+    }
+    __syncthreads();
+  }
+}
+
+template <int NV, int TB>
+__global__ __launch_bounds__(TB) void k_probe_bwd_c(const int32_t* __restrict__ part_lvl,
+                                                    const int32_t* __restrict__ lvl_ptr, const int4* __restrict__ slot,
+                                                    const int32_t* __restrict__ col, const double* __restrict__ Uc,
+                                                    const int64_t* __restrict__ off, double* __restrict__ x) {
+  constexpr int NV2 = NV * NV, RPB = TB / NV;
+  __shared__ double v[RPB * NV];
+  const int p = blockIdx.x;
+  const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
+  const bool lane = rl < RPB;
+  const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
+  for (int l = l0; l < l1; ++l) {
+    const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
+    for (int base = r0; base < r1; base += RPB) {
+      const int r = base + rl;
+      const bool act = lane && r < r1;
+      int i = 0;
+      const double* inv = nullptr;
+      if (act) {
+        const int4 sl = slot[r];
+        i = sl.x;
+        double sum = 0.0;
+        row_blocks<NV>(Uc + ((int64_t)off[r] - (sl.z + 1)) * NV2, col, x, sl.z + 1, sl.w, a, [&](double s) { sum += s; });
+        v[rl * NV + a] = x[(size_t)i * NV + a] - sum;
+        inv = Uc + ((size_t)off[r] + (sl.w - sl.z - 1)) * NV2 + a * NV;
+      }
+      __syncthreads();
+      if (act) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
+        x[(size_t)i * NV + a] = s;
+      }
+      __syncthreads();
+    }
+  }
+}
 }  // namespace
+
+// builds the compact copies once per context (probe only; leaked)
+static int probe_compact(rx_ctx* ctx, int bwd, double** buf, int64_t** off) {
+  const int n = (int)ctx->Nd, nv = ctx->nVar;
+  const rx_ctx::Sched& S = bwd ? ctx->bs : ctx->fs;
+  std::vector<int> h((size_t)4 * n);
+  RX_HIP(hipMemcpy(h.data(), S.slot, sizeof(int) * 4 * (size_t)n, hipMemcpyDeviceToHost));
+  std::vector<int64_t> o((size_t)n + 1, 0);
+  for (int r = 0; r < n; ++r) {
+    const int* sl = &h[(size_t)4 * r];
+    o[r + 1] = o[r] + (bwd ? (sl[3] - sl[2] - 1 + 1) : (sl[2] - sl[1]));
+  }
+  RX_HIP(hipMalloc(off, sizeof(int64_t) * (n + 1)));
+  RX_HIP(hipMemcpy(*off, o.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+  RX_HIP(hipMalloc(buf, sizeof(double) * (size_t)o[n] * nv * nv + 64));
+  RX_NV_SWITCH(nv, (k_probe_gather<NV_><<<n, 256, 0, ctx->stream>>>(
+                       n, reinterpret_cast<const int4*>(S.slot), *off, bwd, bwd ? rx_ilu_upper(ctx) : ctx->f[RX_F_ILU],
+                       rx_invd_buf(ctx), *buf)));
+  RX_HIP(hipStreamSynchronize(ctx->stream));
+  return RX_OK;
+}
 
 extern "C" int rx_debug_sweep_probe(rx_ctx* ctx, int mode, int reps, double* ms) {
   if (!ctx || !ctx->cfg.implicit || ctx->nVar != 11) return RX_ERR_ARG;
   const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
   double* b = ctx->f[RX_F_RHS];
   double* x = ctx->f[RX_F_SOL];
+  static double *Lc = nullptr, *Uc = nullptr;
+  static int64_t *loff = nullptr, *uoff = nullptr;
+  if (mode >= 10 && !Lc) {
+    int rc = probe_compact(ctx, 0, &Lc, &loff);
+    if (!rc) rc = probe_compact(ctx, 1, &Uc, &uoff);
+    if (rc) return rc;
+  }
   hipEvent_t e0, e1;
   RX_HIP(hipEventCreate(&e0));
   RX_HIP(hipEventCreate(&e1));
@@ -1883,7 +1990,15 @@ extern "C" int rx_debug_sweep_probe(rx_ctx* ctx, int mode, int reps, double* ms)
       case 9:  // the production backward sweep
         k_ilu_bwd_wide<11, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
             ctx->bs.part_lvl, ctx->bs.lvl_ptr, reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col,
-            ctx->f[RX_F_ILU], rx_invd_buf(ctx), x, nullptr, nullptr);
+            rx_ilu_upper(ctx), rx_invd_buf(ctx), x, nullptr, nullptr);
+        break;
+      case 10:  // forward sweep on the compact lower blocks
+        k_probe_fwd_c<11, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->col,
+                                                                       Lc, loff, b, x);
+        break;
+      case 11:  // backward sweep on the compact upper blocks + inv(D)
+        k_probe_bwd_c<11, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
+            ctx->bs.part_lvl, ctx->bs.lvl_ptr, reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, Uc, uoff, x);
         break;
       default:
         return RX_ERR_ARG;

@@ -318,6 +318,15 @@ def update_rk(Uold, R, nDim, alpha, vol, dt):
     return U
 
 
+class PrimitiveFailure(RuntimeError):
+    """SetPrimitive_Variables threw (the bisection's std::runtime_error, or SetPrimVar's SU2_Assert that the old
+    solution is feasible, variable_direct_reactive.cpp:297-301): points = the indices of every failing point."""
+
+    def __init__(self, points):
+        super().__init__(f"SetPrimitive_Variables: bisection failed at {len(points)} point(s), first {points[:8]}")
+        self.points = points
+
+
 IGNITION_OFF = [0.0, 999999.0, 1700.0, 0.0, 2.0]  # IGNITION NO and the CConfig defaults (config_structure.cpp:591-603)
 
 
@@ -336,13 +345,13 @@ def set_primitive(mech, nDim, U, V_before, tke, mut, prm, Uold=None):
     N, nVar = U.shape
     ns = mech.ns
     out = dict(dPdU=np.zeros((N, nVar)), dTdU=np.zeros((N, nVar)), mu=np.zeros(N), kappa=np.zeros(N),
-               Dij=np.zeros((N, ns, ns)), eddy=np.zeros(N), cp=np.zeros(N))
+               Dij=np.zeros((N, ns, ns)), eddy=np.zeros(N), cp=np.zeros(N), fail=np.zeros(N, dtype=np.int8))
     n = lib().orc_set_primitive(mech.h, C.c_int(nDim), C.c_int64(N), U.ctypes.data_as(C.c_void_p),
                                 V.ctypes.data_as(C.c_void_p), _p(Uold) if Uold is not None else None,
                                 _p(tke) if tke is not None else None, _p(mut) if mut is not None else None,
                                 _p(ignition_params(prm)),
                                 *[out[k].ctypes.data_as(C.c_void_p) for k in ("dPdU", "dTdU", "mu", "kappa", "Dij",
-                                                                              "eddy", "cp")])
+                                                                              "eddy", "cp", "fail")])
     out.update(U=U, V=V, nonphys=n)
     return out
 
@@ -584,7 +593,7 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         prm[10] = float(ext_iter)
         o = set_primitive(mech, nDim, U, V, T[:, 0].copy(), mut, prm, Uold=Uold)
         if o["nonphys"] < 0:
-            raise RuntimeError("SetPrimitive_Variables: bisection failed")
+            raise PrimitiveFailure(np.flatnonzero(o["fail"]))
         G = grad_lsq(mech, nDim, np.arange(N), mesh["coord"], o["V"], mesh["nbr_ptr"], mesh["nbr"])
         return o, G, strain_mag(nDim, G)
 

@@ -2255,7 +2255,7 @@ bool cons2prim(const Mech& m, int nDim, double* U, double* V, double val_ke, con
 // prm: [0..9] TEMPERATURE_MIN / MAX and the reference values, [10] ExtIter, [11] CLIPPING_TEMPRATURE, [12..16] ignition
 int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const double* Uold, const double* tke,
                       const double* mut, const double* prm, double* dPdU, double* dTdU, double* mu, double* kappa,
-                      double* Dij, double* eddy, double* cp_out) {
+                      double* Dij, double* eddy, double* cp_out, int8_t* fail) {
   const Mech& m = *static_cast<Mech*>(h);
   const int ns = m.ns, nVar = ns + nDim + 2, nPV = ns + nDim + 5;
   const int T_ = 0, VX = 1, P_ = nDim + 1, RHO = nDim + 2, A_ = nDim + 4, RHOS = nDim + 5;
@@ -2275,7 +2275,10 @@ int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const 
         for (int q = 0; q < nVar; ++q) u[q] = Uold[i * nVar + q];
         (void)vT0;
         const bool np_old = cons2prim(m, nDim, u, v, ke, prm);
-        if (np_old) err = 1;
+        if (np_old) {
+          err = 1;
+          if (fail) fail[i] = 1;
+        }
       }
       // Cp = ComputeCP_FromSoundSpeed(T, a, Ys) / R_ref (:304-311)
       const double dim_temp = v[T_] * T_ref, dim_a = v[A_] * Vel_ref;
@@ -2361,6 +2364,7 @@ int orc_set_primitive(void* h, int nDim, int64_t N, double* U, double* V, const 
       if (nonPhys) ++count;
     } catch (const std::exception&) {
       err = 1;
+      if (fail) fail[i] = 1;  // the points whose SetPrimVar throws (error-path parity with the device's index)
     }
   }
   return err ? -1 : (int)count;

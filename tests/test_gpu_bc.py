@@ -249,8 +249,8 @@ def test_synthetic_jet_iteration_vs_oracle(ns, nz):
     from tests.oracle_inputs import outer_iteration_inputs
     from tests.rxpkg import synth
     mesh, st, mech, kw = synth.jet_case(24, 10, n_species=ns, n_part=4, nz=nz)
-    if ns == 4:  # at the default CFL 5 this state leaves the tables in the oracle too (bisection failure)
-        kw["cfl"] = 1.0
+    if ns == 4:  # at the default CFL 5 this state leaves the tables, on the device and in the oracle at the same
+        kw["cfl"] = 1.0  # point (test_synthetic_jet_failure_matches_oracle)
     cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
     bc = synth.jet_bc(mesh, ns)
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
@@ -274,6 +274,37 @@ def test_synthetic_jet_iteration_vs_oracle(ns, nz):
     per_column_close(s.download("U").reshape(N, -1), o["U"], rtol=1e-10, floor=1.0, what="U vs oracle")
     per_column_close(t.download("U").reshape(N, 2), o["T"], rtol=1e-10, floor=1.0, what="(k, omega) vs oracle")
     assert_close(rms, o["rms"], rtol=1e-10, what="RMS")
+    s.close()
+
+
+def test_synthetic_jet_failure_matches_oracle():
+    """Error-path parity: the 3-D 4-species synthetic jet at the cfg's CFL 5 leaves the property tables in the
+    second Preprocessing (the updated solution's SetPrimitive_Variables). The device reports RX_ERR_NONPHYS (the
+    reference's bisection std::runtime_error / SetPrimVar's SU2_Assert, variable_direct_reactive.cpp:297-301) at a
+    point the oracle's SetPrimVar also throws at, from the same iteration."""
+    from tests.oracle_inputs import outer_iteration_inputs
+    from tests.rxpkg import synth
+    mesh, st, mech, kw = synth.jet_case(24, 10, n_species=4, n_part=4, nz=4)
+    cfg = rx.default_cfg(implicit=1, lin_prec=1, **kw)
+    bc = synth.jet_bc(mesh, 4)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
+    s.set_bc(bc)
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+    s.set_state(st)
+    t.set_state(st["sst_sol"], mesh["wall_distance"], st["sst_F1"], st["sst_F2"], st["sst_CDkw"])
+    N = len(st["V"])
+    mesh_o, state, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
+    s.upload("GRADK", np.ascontiguousarray(state["TG"][:, 0, :]))
+    s.upload("SIGMAK", np.full(N, 0.85))
+    with pytest.raises(rx.RxError) as dev:
+        rx.Iterate(s, t, ext_iter=0)
+        s.sync()
+    pat = O.bsr_pattern(N, mesh["edges"])
+    with pytest.raises(O.PrimitiveFailure) as ora:
+        with O.dot_order("device"):
+            O.outer_iteration(O.Mechanism(mech), 3, mesh_o, state, bco, c, 0, pat, part_ptr=mesh["part_ptr"])
+    assert dev.value.status == rx.RX_ERR_NONPHYS
+    assert dev.value.index in set(ora.value.points.tolist()), (dev.value.index, ora.value.points)
     s.close()
 
 

@@ -20,9 +20,28 @@ rx.Iterate(s, t, ext_iter=0)
 s.sync()
 names = {0: "fwd as production (probe kernel)", 1: "no x dependence", 2: "no level barrier", 3: "no x dep + no barrier",
          4: "no factor loads", 5: "no factor loads + no x dep", 6: "no factor loads + no barrier", 7: "x from b, no F, no barrier",
-         8: "production k_ilu_fwd_wide", 9: "production k_ilu_bwd_wide"}
-for mode in (8, 9, 0, 1, 2, 3, 4, 5, 6, 7, 8):
+         8: "production k_ilu_fwd_wide", 9: "production k_ilu_bwd_wide", 10: "fwd, compact lower blocks",
+         11: "bwd, compact upper blocks + inv(D)"}
+import numpy as np  # noqa: E402
+
+
+def run(mode, reps):
     ms = C.c_double()
-    rc = rx.lib().rx_debug_sweep_probe(s.h, C.c_int(mode), C.c_int(20), C.byref(ms))
+    rc = rx.lib().rx_debug_sweep_probe(s.h, C.c_int(mode), C.c_int(reps), C.byref(ms))
     assert rc == 0, rc
-    print(f"mode {mode}: {ms.value * 1e3:8.1f} us  {names[mode]}", flush=True)
+    return ms.value
+
+
+# the compact layouts against the production sweeps, bitwise (forward: x from b; backward: from the same x)
+run(8, 1)
+xf = s.download("SOL").copy()
+run(10, 1)
+print("fwd compact bitwise:", np.array_equal(s.download("SOL"), xf), flush=True)
+run(9, 1)
+xb = s.download("SOL").copy()
+s.upload("SOL", xf)
+run(11, 1)
+print("bwd compact bitwise:", np.array_equal(s.download("SOL"), xb), flush=True)
+modes = [int(m) for m in sys.argv[1:]] or [8, 9, 10, 11, 8, 9, 10, 11, 0, 1, 2, 3, 4, 5, 6, 7]
+for mode in modes:
+    print(f"mode {mode}: {run(mode, 20) * 1e3:8.1f} us  {names[mode]}", flush=True)
