@@ -112,6 +112,14 @@ __device__ inline void grid_reduce(const double (&v)[NR], double* __restrict__ p
 #define GRID_LOOP(q, n) \
   for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < (n); q += (int64_t)kRedBlocks * kBlock)
 
+// The same grid-stride walk, kU elements per round: every load of the round is issued before the first element's
+// arithmetic, then the elements are processed in the walk's order (q, q + S, ..., S = the reduction grid's thread
+// count), so each thread's partial sums and stores are GRID_LOOP's, operation for operation. The 512-block reduction
+// grid runs 2 wavefronts per SIMD; with one element per round each thread had a single load chain in flight.
+constexpr int kU = 4;
+constexpr int64_t kGridS = (int64_t)kRedBlocks * kBlock;
+#define GRID_LOOP_U(q0, n) for (int64_t q0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; q0 < (n); q0 += kU * kGridS)
+
 // Row-block product of y = A x for element q = (row i, component a): the reference's
 // MatrixVectorProduct order (blocks of the row in column order, columns c ascending).
 // Small blocks (the SST's 2x2) are taken kSpmvChunk at a time: the chunk's column indices, then all of its
@@ -185,12 +193,20 @@ __global__ __launch_bounds__(kBlock) void k_fg_residual0(int64_t n, const double
                                                          double* __restrict__ w, double* __restrict__ part,
                                                          KState* __restrict__ s, bool dist) {
   double v[2] = {0.0, 0.0};
-  GRID_LOOP(q, n) {
-    const double bq = b[q];
-    v[0] += bq * bq;
-    const double y = 0.0 - bq;
-    w[q] = y;
-    v[1] += y * y;
+  GRID_LOOP_U(q0, n) {
+    double bb[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) bb[u] = b[q0 + u * kGridS];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) {
+        const double bq = bb[u];
+        v[0] += bq * bq;
+        const double y = 0.0 - bq;
+        w[q0 + u * kGridS] = y;
+        v[1] += y * y;
+      }
   }
   const int sl[2] = {kNorm0In, kDot};
   grid_reduce<2>(v, part, s, sl, dist);
@@ -215,10 +231,22 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv_dots(int64_t n, const double
                                                          KState* __restrict__ s, bool dist) {
   if (s->done) return;
   double v[2] = {0.0, 0.0};
-  GRID_LOOP(q, n) {
-    const double y = w[q];
-    v[0] += y * y;
-    v[1] += y * w0[q];
+  GRID_LOOP_U(q0, n) {
+    double y[kU], z[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t q = q0 + u * kGridS;
+      if (q < n) {
+        y[u] = w[q];
+        z[u] = w0[q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) {
+        v[0] += y[u] * y[u];
+        v[1] += y[u] * z[u];
+      }
   }
   const int sl[2] = {kDotN, kDot};
   grid_reduce<2>(v, part, s, sl, dist);
@@ -269,6 +297,32 @@ __global__ __launch_bounds__(kBlock) void k_fg_start_div(int64_t n, KState* __re
   if (q < n) w0[q] /= -beta;
 }
 
+// w -= prod * wk over this thread's walk, with the partial sum of y * wn (wn null: y * y) in walk order.
+__device__ __forceinline__ void proj_walk(int64_t n, double prod, const double* wk, double* w, const double* wn,
+                                          double& acc) {
+  GRID_LOOP_U(q0, n) {
+    double a[kU], b[kU], c[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t q = q0 + u * kGridS;
+      if (q < n) {
+        a[u] = w[q];
+        b[u] = wk[q];
+        if (wn) c[u] = wn[q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t q = q0 + u * kGridS;
+      if (q < n) {
+        const double y = a[u] + (-1.0 * prod) * b[u];
+        w[q] = y;
+        acc += y * (wn ? c[u] : y);
+      }
+    }
+  }
+}
+
 // ModGramSchmidt (:87-186) projection k of iteration i: H[k][i] = prod = <w, w_k> (in s->dot),
 // w -= prod w_k, the re-orthogonalisation test prod^2 > thr, and the inner product the recurrence
 // needs next: <w, w_k> (re-orthogonalise), else <w, w_{k+1}> (k < i) or |w|^2 (k == i).
@@ -294,11 +348,7 @@ __global__ __launch_bounds__(kBlock) void k_fg_proj(int64_t n, int64_t ld, KStat
   double* w = W + (int64_t)(i + 1) * ld;
   const double* wn = reo ? wk : (k < i ? W + (int64_t)(k + 1) * ld : nullptr);
   double v[1] = {0.0};
-  GRID_LOOP(q, n) {
-    const double y = w[q] + (-1.0 * prod) * wk[q];
-    w[q] = y;
-    v[0] += y * (wn ? wn[q] : y);
-  }
+  proj_walk(n, prod, wk, w, wn, v[0]);
   if (lead()) {
     if (k == 0) s->nrm = nrm0;
     Hk(s, k, i) = prod;
@@ -324,11 +374,7 @@ __global__ __launch_bounds__(kBlock) void k_fg_reo(int64_t n, int64_t ld, KState
   double* w = W + (int64_t)(i + 1) * ld;
   const double* wn = k < i ? W + (int64_t)(k + 1) * ld : nullptr;
   double v[1] = {0.0};
-  GRID_LOOP(q, n) {
-    const double y = w[q] + (-1.0 * prod) * wk[q];
-    w[q] = y;
-    v[0] += y * (wn ? wn[q] : y);
-  }
+  proj_walk(n, prod, wk, w, wn, v[0]);
   if (lead()) {
     Hk(s, k, i) += prod;
     s->nrm -= Hk(s, k, i) * Hk(s, k, i);
@@ -385,7 +431,15 @@ __global__ __launch_bounds__(kBlock) void k_fg_close_div(int64_t n, KState* __re
                                                          double* __restrict__ w) {
   if (s->done) return;
   const double nrm = sqrt(s->dotn);
-  GRID_LOOP(q, n) w[q] /= nrm;
+  GRID_LOOP_U(q0, n) {
+    double a[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) a[u] = w[q0 + u * kGridS];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) w[q0 + u * kGridS] = a[u] / nrm;
+  }
   if (lead()) fg_close(s, i);
 }
 
@@ -423,10 +477,22 @@ __global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, int64_t ld, KSt
     for (int k = 0; k < it; ++k) s->y[k] = y[k];
   }
   if (it == 0) return;
-  GRID_LOOP(q, n) {
-    double v = x[q];
-    for (int k = 0; k < it; ++k) v += y[k] * Z[(int64_t)k * ld + q];
-    x[q] = v;
+  GRID_LOOP_U(q0, n) {
+    double v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) v[u] = x[q0 + u * kGridS];
+    for (int k = 0; k < it; ++k) {
+      double zz[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (q0 + u * kGridS < n) zz[u] = Z[(int64_t)k * ld + q0 + u * kGridS];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) v[u] += y[k] * zz[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) x[q0 + u * kGridS] = v[u];
   }
 }
 

@@ -142,21 +142,33 @@ __global__ __launch_bounds__(kBlock) void k_update(int N, int nVar, int nDim, co
 __global__ __launch_bounds__(kBlock) void k_sumsq_cols(int N, int nVar, const double* __restrict__ r,
                                                        double* __restrict__ part) {
   // part[blockIdx.x * nVar + v] = sum over this block's rows of r^2 (fixed order)
+  // one pass over the rows with every column's partial in registers (each column's sum in the same row order as a
+  // pass per column; nVar <= kMaxCols)
   __shared__ double sh[kBlock];
-  for (int v = 0; v < nVar; ++v) {
-    double s = 0.0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < N; i += gridDim.x * kBlock) {
-      const double x = r[(size_t)i * nVar + v];
-      s += x * x;
-    }
-    sh[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = kBlock / 2; w > 0; w >>= 1) {
-      if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+  constexpr int kMaxCols = 16;
+  double acc[kMaxCols];
+#pragma unroll
+  for (int v = 0; v < kMaxCols; ++v) acc[v] = 0.0;
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < N; i += gridDim.x * kBlock) {
+#pragma unroll
+    for (int v = 0; v < kMaxCols; ++v)
+      if (v < nVar) {
+        const double x = r[(size_t)i * nVar + v];
+        acc[v] += x * x;
+      }
+  }
+#pragma unroll
+  for (int v = 0; v < kMaxCols; ++v) {
+    if (v < nVar) {  // block-uniform
+      sh[threadIdx.x] = acc[v];
+      __syncthreads();
+      for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) part[blockIdx.x * nVar + v] = sh[0];
       __syncthreads();
     }
-    if (threadIdx.x == 0) part[blockIdx.x * nVar + v] = sh[0];
-    __syncthreads();
   }
 }
 

@@ -572,18 +572,26 @@ __device__ __forceinline__ void grp_solve_lds(const double* LU, double (&rhs)[NV
   }
 }
 
+// Wavefronts per workgroup: 12 (3 per SIMD, 168 VGPRs) for blocks up to 9x9; 8 (256 VGPRs) for larger blocks, whose
+// prefetched next-row blocks spill at 168 (C3, 11x11: 3.59 ms with 12 waves before the prefetch, 4.34 ms with it
+// and 31 spills, 3.21 ms with 8 waves).
 #ifndef RX_GRP_WAVES
 #define RX_GRP_WAVES 12
 #endif
-constexpr int kGrpMaxWaves = RX_GRP_WAVES;
+#ifndef RX_GRP_WAVES_BIG
+#define RX_GRP_WAVES_BIG 8
+#endif
+constexpr int kGrpMaxWaves = RX_GRP_WAVES > RX_GRP_WAVES_BIG ? RX_GRP_WAVES : RX_GRP_WAVES_BIG;
+template <int NV>
+constexpr int grp_waves() { return NV >= 10 ? RX_GRP_WAVES_BIG : RX_GRP_WAVES; }
 constexpr int kGrpTraceRows = 64, kGrpTraceGroups = 64, kGrpTraceLevels = 512;  // >= 4 * kGrpMaxWaves groups
 template <int NV>
 constexpr int grp_np() { return (NV + 1) & ~1; }
 template <int NV>
-constexpr int grp_slot_doubles() { return NV * grp_np<NV>() + kPlan / 2; }
+constexpr int grp_slot_doubles() { return NV * grp_np<NV>() + kPlan; }  // + two plan records (this row, the next)
 
 template <int NV>
-__global__ __launch_bounds__(64 * kGrpMaxWaves) void k_ilu_build_grp(const int32_t* __restrict__ part_lvl,
+__global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const int32_t* __restrict__ part_lvl,
                                                                     const int32_t* __restrict__ lvl_ptr,
                                                                     const int32_t* __restrict__ plan,
                                                                     const double* __restrict__ A,
@@ -593,25 +601,78 @@ __global__ __launch_bounds__(64 * kGrpMaxWaves) void k_ilu_build_grp(const int32
   extern __shared__ double lds[];
   const int a = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = blockDim.x >> 4;
   double* S = lds + (size_t)grp * grp_slot_doubles<NV>();  // inv(A_jj), then W, then the LU of D_i
-  int* rec = reinterpret_cast<int*>(S + NV * NP);          // the row's plan record
+  int* const recb = reinterpret_cast<int*>(S + NV * NP);   // plan records: this row's and the next row's
   const int p = blockIdx.x, l0 = part_lvl[p], l1 = part_lvl[p + 1];
   // the partition's level pointers in LDS (behind the group slots): the loop bounds and the next-row search read
   // them every row
   int* lp = reinterpret_cast<int*>(lds + (size_t)ngrp * grp_slot_doubles<NV>()) - l0;
   for (int l = l0 + (int)threadIdx.x; l <= l1; l += blockDim.x) lp[l] = lvl_ptr[l];
   __syncthreads();
-  auto next_slot = [&](int r, int l) -> int {  // the group's next row after slot r of level l, -1 if none
-    if (r + ngrp < lp[l + 1]) return r + ngrp;
+  auto next_slot = [&](int r, int l, int& ln) -> int {  // the group's next row after slot r of level l (its level
+    if (r + ngrp < lp[l + 1]) {                         // in ln), -1 if none
+      ln = l;
+      return r + ngrp;
+    }
     for (int ll = l + 1; ll < l1; ++ll)
-      if (lp[ll] + grp < lp[ll + 1]) return lp[ll] + grp;
+      if (lp[ll] + grp < lp[ll + 1]) {
+        ln = ll;
+        return lp[ll] + grp;
+      }
     return -1;
   };
-  int2 prec = make_int2(0, 0);
+  constexpr int PB = (NV2 + 15) / 16;  // doubles per lane of a block loaded lane-contiguously
+  // The A blocks a row reads first — its diagonal (column per lane), its first lower block A_ij and that block's
+  // A_ji — are inputs, so they are loaded for the group's NEXT row while this row factors its diagonal: plain loads
+  // stay in flight across the level barrier. Only inv(A_jj) (a row of an earlier level) waits for the barrier.
+  auto prefetch = [&](const int* rc, int lane, double (&pd)[NV], double (&pbl)[PB], double (&pjl)[PB]) {
+    const int pc = lane < NV ? lane : 0;
+    const int pk0 = rc[1], pkd = rc[2];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) pd[q] = A[(size_t)pkd * NV2 + q * NV + pc];
+    if (pkd > pk0) {
+#pragma unroll
+      for (int u = 0; u < PB; ++u)
+        if (16 * u + lane < NV2) pbl[u] = A[(size_t)pk0 * NV2 + 16 * u + lane];
+      if (rc[11] > 0) {
+#pragma unroll
+        for (int u = 0; u < PB; ++u)
+          if (16 * u + lane < NV2) pjl[u] = A[(size_t)rc[14] * NV2 + 16 * u + lane];
+      }
+    }
+  };
+  // the second lower block and its A_ji (issued at the row start with both inv(A_jj))
+  auto load_second = [&](const int* rc, int lane, double (&pbl2)[PB], double (&pjl2)[PB]) {
+    const int pk0 = rc[1], pkd = rc[2];
+    if (pkd > pk0 + 1) {
+#pragma unroll
+      for (int u = 0; u < PB; ++u)
+        if (16 * u + lane < NV2) pbl2[u] = A[(size_t)(pk0 + 1) * NV2 + 16 * u + lane];
+      if (rc[12] > 0) {
+        const int kk = rc[14 + 2 * rc[11]];
+#pragma unroll
+        for (int u = 0; u < PB; ++u)
+          if (16 * u + lane < NV2) pjl2[u] = A[(size_t)kk * NV2 + 16 * u + lane];
+      }
+    }
+  };
+  double d[NV], bl[PB], jl[PB];  // the current row's prefetched blocks
+  int2 prec = make_int2(0, 0);   // the plan of the group's row after the current one
+  int cur = 0;                   // recb slot of the current row's plan
   {
-    int pr = -1;
+    int pr = -1, pl = 0;
     for (int ll = l0; ll < l1 && pr < 0; ++ll)
-      if (lp[ll] + grp < lp[ll + 1]) pr = lp[ll] + grp;
-    if (pr >= 0) prec = reinterpret_cast<const int2*>(plan + (size_t)pr * kPlan)[a];
+      if (lp[ll] + grp < lp[ll + 1]) {
+        pr = lp[ll] + grp;
+        pl = ll;
+      }
+    if (pr >= 0) {
+      reinterpret_cast<int2*>(recb)[a] = reinterpret_cast<const int2*>(plan + (size_t)pr * kPlan)[a];
+      wave_sync();
+      prefetch(recb, a, d, bl, jl);
+      int ln;
+      const int nr = next_slot(pr, pl, ln);
+      if (nr >= 0) prec = reinterpret_cast<const int2*>(plan + (size_t)nr * kPlan)[a];
+    }
   }
   // optional phase trace of block 0 (tools/ilu_trace.py --grp): per group, per row 4 stamps; then one per level
   long long* tr = (trace && blockIdx.x == 0 && a == 0) ? trace + 1 + (size_t)grp * kGrpTraceRows * 8 : nullptr;
@@ -620,7 +681,6 @@ __global__ __launch_bounds__(64 * kGrpMaxWaves) void k_ilu_build_grp(const int32
   do {                                                                                            \
     if (tr && trow < kGrpTraceRows) tr[trow * 8 + (ph)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
-  constexpr int PB = (NV2 + 15) / 16;  // doubles per lane of a block loaded lane-contiguously
   for (int l = l0; l < l1; ++l) {
     for (int r = lp[l] + grp; r < lp[l + 1]; r += ngrp) {
       RX_GSTAMP(0);
@@ -630,31 +690,28 @@ __global__ __launch_bounds__(64 * kGrpMaxWaves) void k_ilu_build_grp(const int32
       asm volatile("" : "+v"(al));
       const bool act = al < NV;
       const int ac = act ? al : 0;  // lanes NV..15 of a group load column 0 and store nothing
-      reinterpret_cast<int2*>(rec)[al] = prec;
-      {
-        const int nr = next_slot(r, l);  // the next row's plan is an input: fetched now, used next row
-        if (nr >= 0) prec = reinterpret_cast<const int2*>(plan + (size_t)nr * kPlan)[al];
-      }
-      wave_sync();
+      const int* rec = recb + cur * kPlan;
+      int nl = l;
+      const int nr = next_slot(r, l, nl);  // the group's next row (its plan is in prec)
       const int i = rec[0], k0 = rec[1], kd = rec[2];
-      // every load of the diagonal and the first lower block issued together: A blocks (inputs), inv(A_jj) (a
-      // finished row), A_jk (an upper block of row j, i.e. unchanged A)
-      double d[NV], s[NV], bl[PB], jl[PB];
-#pragma unroll
-      for (int q = 0; q < NV; ++q) d[q] = A[(size_t)kd * NV2 + q * NV + ac];
+      // the first two lower blocks' inv(A_jj) (finished rows) and the second block's A_ij / A_ji; d and the first
+      // block's A_ij / A_ji were prefetched
+      double s[NV], s2[NV], bl2[PB], jl2[PB];
+#ifdef RX_GRP_EARLY2
+      load_second(rec, al, bl2, jl2);
+#endif
       if (kd > k0) {
-        const int j0 = rec[8], kk0 = rec[14];
+        const int j0 = rec[8];
 #pragma unroll
         for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)j0 * NV2 + q * NV + ac];
-#pragma unroll
-        for (int u = 0; u < PB; ++u)
-          if (16 * u + al < NV2) bl[u] = A[(size_t)k0 * NV2 + 16 * u + al];
-        if (rec[11] > 0) {
-#pragma unroll
-          for (int u = 0; u < PB; ++u)
-            if (16 * u + al < NV2) jl[u] = A[(size_t)kk0 * NV2 + 16 * u + al];
-        }
       }
+#ifdef RX_GRP_EARLY2
+      if (kd > k0 + 1) {
+        const int j1 = rec[9];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) s2[q] = invD[(size_t)j1 * NV2 + q * NV + ac];
+      }
+#endif
       int pcur = 0;
       for (int k = k0; k < kd; ++k) {
         const int t = k - k0, nu = rec[11 + t];
@@ -682,8 +739,20 @@ __global__ __launch_bounds__(64 * kGrpMaxWaves) void k_ilu_build_grp(const int32
             if (16 * u + al < NV2) S[16 * u + al] = jl[u];  // A_ji
         }
         wave_sync();
-        if (k + 1 < kd) {  // the next lower block's loads, into the registers just freed (before W's store, so
-                           // that waiting for them does not wait for the store)
+#ifndef RX_GRP_EARLY2
+        if (false) {
+#else
+        if (t == 0 && k + 1 < kd) {  // the second block: loaded at the row start
+#endif
+#pragma unroll
+          for (int q = 0; q < NV; ++q) s[q] = s2[q];
+#pragma unroll
+          for (int u = 0; u < PB; ++u) {
+            bl[u] = bl2[u];
+            jl[u] = jl2[u];
+          }
+        } else if (k + 1 < kd) {  // further lower blocks' loads (not on quad / hex meshes), into the registers
+                                  // just freed (before W's store, so that waiting for them does not wait for it)
           const int jn = rec[9 + t];
 #pragma unroll
           for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)jn * NV2 + q * NV + ac];
@@ -740,7 +809,18 @@ __global__ __launch_bounds__(64 * kGrpMaxWaves) void k_ilu_build_grp(const int32
 #pragma unroll
         for (int e = 0; e < NV; ++e) S[e * NP + al] = d[e];
       }
+      // the next row's plan into the other record, its input blocks into d / bl / jl (dead from here on), and the
+      // plan of the row after it
+      int* nrec = recb + (cur ^ 1) * kPlan;
+      reinterpret_cast<int2*>(nrec)[al] = prec;
       wave_sync();
+      if (nr >= 0) {
+        prefetch(nrec, al, d, bl, jl);
+        int nnl;
+        const int nnr = next_slot(nr, nl, nnl);
+        if (nnr >= 0) prec = reinterpret_cast<const int2*>(plan + (size_t)nnr * kPlan)[al];
+      }
+      cur ^= 1;
       double rw[NV];
 #pragma unroll
       for (int e = 0; e < NV; ++e) rw[e] = S[ac * NP + e];
@@ -1710,8 +1790,7 @@ int rx_la_ilu_build(rx_ctx* ctx) {
     return RX_OK;
   }
   if (ilu_grouped(ctx)) {
-    const int gwaves = std::max(1, std::min(kGrpMaxWaves, (ctx->fs.maxwidth + 3) / 4));
-    RX_NV_SWITCH(nv, (launch_ilu_build_grp<NV_>(ctx, gwaves)));
+    RX_NV_SWITCH(nv, (launch_ilu_build_grp<NV_>(ctx, std::max(1, std::min(grp_waves<NV_>(), (ctx->fs.maxwidth + 3) / 4)))));
     RX_HIP(hipGetLastError());
     return RX_OK;
   }
