@@ -253,6 +253,9 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
   return nonPhys;
 }
 
+#ifndef RX_PRIM_UNROLL
+#define RX_PRIM_UNROLL 16  // >= NS: the species-pair loops fully unrolled (rolled: primitives 1.22 -> 1.43 ms at C3)
+#endif
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, DevMech m, PrimParams P, double* __restrict__ Ug,
                                                           double* __restrict__ Vg, const double* __restrict__ Uold,
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, Dev
     yom[s] = Yc[s] / m.mm[s];
   }
   double eta = 0.0;
-#pragma unroll
+#pragma unroll RX_PRIM_UNROLL
   for (int a = 0; a < NS; ++a) {
     double phi = 0.0;
 #pragma unroll
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, Dev
 #pragma unroll
   for (int s = 0; s < NS; ++s) yom[s] = Ys[s] / m.mm[s];  // ComputeLambda: the unclamped argument
   double lam = 0.0;
-#pragma unroll
+#pragma unroll RX_PRIM_UNROLL
   for (int a = 0; a < NS; ++a) {
     double phi = 0.0;
 #pragma unroll
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, Dev
   const double pT = 1.0e-3 * pow175_cr(dim_temp);
   const double scale = P.Vel_ref * P.Len_ref * 1.0e4;
   double* D = Dij + (size_t)i * NS * NS;
-#pragma unroll
+#pragma unroll RX_PRIM_UNROLL
   for (int a = 0; a < NS; ++a)
 #pragma unroll
     for (int b = a; b < NS; ++b) {
@@ -381,8 +384,15 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, Dev
   // ignition (SetPrimitive_Variables solver_direct_reactive.cpp:1013-1024): after SetPrimVar only the record's
   // temperature is overwritten (CReactiveEulerVariable::SetTemperature, variable_reactive.hpp:602-607); the
   // derivatives and transport above keep the secant's temperature, as in the reference
-  if (P.ignite && V[RHOS + P.fuel] > 0.4 && V[RHOS + P.oxidizer] > 0.2 && V[0] < P.T_ign)
-    Vg[(size_t)i * nPV] = P.T_ign;
+  if (P.ignite) {
+    double yf = 0.0, yo = 0.0;  // selected by an unrolled compare: a run-time index would put V in scratch
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s == P.fuel) yf = V[RHOS + s];
+      if (s == P.oxidizer) yo = V[RHOS + s];
+    }
+    if (yf > 0.4 && yo > 0.2 && V[0] < P.T_ign) Vg[(size_t)i * nPV] = P.T_ign;
+  }
 }
 
 // a2 second order: MUSCL reconstruction of (T, u, v, P) per edge side with the optional limiter, and the

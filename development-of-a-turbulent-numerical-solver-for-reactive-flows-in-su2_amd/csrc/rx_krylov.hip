@@ -116,7 +116,10 @@ __device__ inline void grid_reduce(const double (&v)[NR], double* __restrict__ p
 // arithmetic, then the elements are processed in the walk's order (q, q + S, ..., S = the reduction grid's thread
 // count), so each thread's partial sums and stores are GRID_LOOP's, operation for operation. The 512-block reduction
 // grid runs 2 wavefronts per SIMD; with one element per round each thread had a single load chain in flight.
-constexpr int kU = 4;
+#ifndef RX_FG_U
+#define RX_FG_U 4
+#endif
+constexpr int kU = RX_FG_U;
 constexpr int64_t kGridS = (int64_t)kRedBlocks * kBlock;
 #define GRID_LOOP_U(q0, n) for (int64_t q0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; q0 < (n); q0 += kU * kGridS)
 

@@ -1,9 +1,9 @@
 """FGMRES on a non-finite system: the matrix-free initial residual (k_fg_residual0, the default: LinSysSol is zeroed
 before the solve, solver_direct_reactive.cpp:2373, so A x = +0 for a finite A) against the A x product path
-(RX_FG_X_PRODUCT=1, read once per process, hence one child process per path). A NaN local time step at one point
-puts NaN on that point's diagonal block (Vol / dt, :2380-2387). The reference's A * 0 then makes w0 NaN at the first
-residual; the matrix-free path meets the NaN one Krylov step later, in the preconditioned vector. Both must report the
-same outcome: rx_implicit_euler returns RX_ERR_DIVERGED (the breakdown test of ModGramSchmidt,
+(RX_FG_X_PRODUCT=1, read once per process, hence one child process per path). A NaN in one point's dP/dU puts NaN
+in the convective Jacobian blocks of its edges while the residual stays finite. The reference's A * 0 then makes w0
+NaN at the first residual; the matrix-free path meets the NaN one Krylov step later, in the preconditioned vector.
+Both must report the same outcome: rx_implicit_euler returns RX_ERR_DIVERGED (the breakdown test of ModGramSchmidt,
 linear_solvers_structure.cpp:97-100, on a NaN norm) and no finite update is claimed."""
 import json
 import os
@@ -26,14 +26,17 @@ s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), rx.default_cfg(implicit=1, lin
 s.set_state(st)
 s.SetPrimitive_Gradient_LS()
 s.SetTime_Step()
+# dP/dU enters only the convective Jacobian (the AUSM residual and the time step read V): A gets NaN blocks, b stays
+# finite
+dpdu = s.download("DPDU")
+dpdu[17 * s.nVar + 2] = np.nan
+s.upload("DPDU", dpdu)
 s.Preprocessing_zero()
 s.Upwind_Residual()
 s.Viscous_Residual()
 s.Source_Residual()
-dt = s.download("DT")
-dt[17] = np.nan
-s.upload("DT", dt)
-out = {"status": 0}
+out = {"rhs_finite": bool(np.isfinite(s.download("RES")).all())}
+out["status"] = 0
 try:
     rms, it = s.ImplicitEuler_Iteration()
     out["iters"] = it
@@ -58,9 +61,10 @@ def run_child(product, prec):
 
 
 @pytest.mark.parametrize("prec", [1, 0])  # ILU0, LU_SGS
-def test_nan_diagonal_same_status_on_both_residual_paths(prec):
+def test_nan_jacobian_same_status_on_both_residual_paths(prec):
     import tests.rxpkg as rxpkg
     a = run_child(False, prec)
     b = run_child(True, prec)
     assert a == b, (a, b)
+    assert a["rhs_finite"], a
     assert a["status"] == rxpkg.rx.RX_ERR_DIVERGED, a
