@@ -343,7 +343,30 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         }
       }
       std::vector<int32_t> plan((size_t)Nd * 32, 0);
+      // k_ilu_build_grp's plans (rx_sweeps.hip): rows with at most six lower blocks, each of whose single update
+      // (if any) is the diagonal (triangle-free stencils: quads, hexahedra) — [0..5] as plan, [8 + t] the column j
+      // of lower block t, [14 + t] the position of A_ji in row j (-1: the block updates nothing)
+      std::vector<int32_t> gplan((size_t)Nd * 32, 0);
       bool grp_ok = true;
+      for (int64_t r = 0; r < Nd && grp_ok; ++r) {
+        const int32_t i = fo[r];
+        int32_t* g = gplan.data() + r * 32;
+        g[0] = i;
+        g[1] = klo[i];
+        g[2] = (int32_t)diag[i];
+        g[3] = khi[i];
+        g[4] = (int32_t)ctx->h_rp[i];
+        g[5] = (int32_t)ctx->h_rp[i + 1];
+        const int32_t nlow = (int32_t)diag[i] - klo[i];
+        grp_ok = nlow <= 6;
+        for (int32_t t = 0; t < nlow && grp_ok; ++t) {
+          const int32_t k = klo[i] + t;
+          const int32_t nu = uptr[k + 1] - uptr[k];
+          grp_ok = nu == 0 || (nu == 1 && upd[2 * uptr[k] + 1] == (int32_t)diag[i]);
+          g[8 + t] = col32[k];
+          g[14 + t] = nu == 1 ? upd[2 * uptr[k]] : -1;  // -1: no update
+        }
+      }
       for (int64_t r = 0; r < Nd; ++r) {
         const int32_t i = fo[r];
         int32_t* rec = plan.data() + r * 32;
@@ -372,11 +395,10 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         }
         rec[6] = ok ? nlow : -1;
         rec[7] = ok ? npair : 0;
-        for (int32_t h = 0; h < npair && ok; ++h) ok = rec[15 + 2 * h] == rec[2];
-        grp_ok = grp_ok && ok;
       }
       ctx->ilu_grp_ok = grp_ok;
       CK(dupload(ctx, &ctx->ilu_plan, plan.data(), plan.size()));
+      if (grp_ok) CK(dupload(ctx, &ctx->ilu_gplan, gplan.data(), gplan.size()));
     }
 
     const size_t per_wave = sizeof(double) * ((size_t)(rowmax + 1 + rx_ilu_stage()) * nv * nv + 16);
@@ -620,7 +642,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->nbr_ptr,
-                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan,
+                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->grad_list, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,

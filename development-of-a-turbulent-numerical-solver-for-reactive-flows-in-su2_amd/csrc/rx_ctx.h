@@ -88,6 +88,7 @@ struct rx_ctx {
   int32_t* ilu_plan = nullptr;  // [N][32] per forward-schedule slot row plan (rx_sweeps.hip)
   int ilu_waves = 1;            // wavefronts per workgroup of the ILU factorisation
   bool ilu_grp_ok = false;      // every row's plan is compact and updates only its diagonal (k_ilu_build_grp)
+  int32_t* ilu_gplan = nullptr; // [N][32] k_ilu_build_grp's row plans (up to 6 lower blocks, one update each)
   // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
   // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])
   struct Sched {

@@ -503,9 +503,10 @@ __global__ __launch_bounds__(RX_ILU_LB) void k_ilu_build_part(const int32_t* __r
 //                         broadcast by DPP row_newbcast), the factorisation back through the slot, lane c
 //                         solving unit column c.
 // Every sum is the reference's (from 0.0, q ascending; the elimination of Gauss_Elimination :594-643), so the
-// factor is bitwise k_ilu_build_part's. The kernel takes meshes whose row plans are compact and update only the
-// diagonal (ctx->ilu_grp_ok: 5-point quad / 7-point hex stencils, i.e. the jet meshes, where no two neighbours of
-// a point are neighbours of each other); others keep k_ilu_build_part. There ILU(0) changes no upper block and
+// factor is bitwise k_ilu_build_part's. The kernel takes meshes whose lower blocks (at most six per row) each update
+// only the diagonal (ctx->ilu_grp_ok: 5-point quad / 7-point hex stencils, i.e. the jet meshes, where no two
+// neighbours of a point are neighbours of each other; its row plans ctx->ilu_gplan: [8 + t] the column of lower
+// block t, [14 + t] the position of its A_ji); others keep k_ilu_build_part. There ILU(0) changes no upper block and
 // no block outside the partition, so those are not copied: the triangular sweeps read the upper blocks from the
 // matrix itself (rx_ilu_upper), and rx_download("ILU") materialises the copies (k_ilu_materialize). One level
 // is one round of all groups (48 per workgroup), so the rows of a level run concurrently instead of in rounds
@@ -633,7 +634,7 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #pragma unroll
       for (int u = 0; u < PB; ++u)
         if (16 * u + lane < NV2) pbl[u] = A[(size_t)pk0 * NV2 + 16 * u + lane];
-      if (rc[11] > 0) {
+      if (rc[14] >= 0) {
 #pragma unroll
         for (int u = 0; u < PB; ++u)
           if (16 * u + lane < NV2) pjl[u] = A[(size_t)rc[14] * NV2 + 16 * u + lane];
@@ -647,8 +648,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #pragma unroll
       for (int u = 0; u < PB; ++u)
         if (16 * u + lane < NV2) pbl2[u] = A[(size_t)(pk0 + 1) * NV2 + 16 * u + lane];
-      if (rc[12] > 0) {
-        const int kk = rc[14 + 2 * rc[11]];
+      if (rc[15] >= 0) {
+        const int kk = rc[15];
 #pragma unroll
         for (int u = 0; u < PB; ++u)
           if (16 * u + lane < NV2) pjl2[u] = A[(size_t)kk * NV2 + 16 * u + lane];
@@ -712,9 +713,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
         for (int q = 0; q < NV; ++q) s2[q] = invD[(size_t)j1 * NV2 + q * NV + ac];
       }
 #endif
-      int pcur = 0;
       for (int k = k0; k < kd; ++k) {
-        const int t = k - k0, nu = rec[11 + t];
+        const int t = k - k0, nu = rec[14 + t] >= 0 ? 1 : 0;
         wave_sync();
 #pragma unroll
         for (int u = 0; u < PB; ++u)
@@ -759,8 +759,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #pragma unroll
           for (int u = 0; u < PB; ++u)
             if (16 * u + al < NV2) bl[u] = A[(size_t)(k + 1) * NV2 + 16 * u + al];
-          if (rec[12 + t] > 0) {
-            const int kk = rec[14 + 2 * (pcur + nu)];
+          if (rec[15 + t] >= 0) {
+            const int kk = rec[15 + t];
 #pragma unroll
             for (int u = 0; u < PB; ++u)
               if (16 * u + al < NV2) jl[u] = A[(size_t)kk * NV2 + 16 * u + al];
@@ -770,20 +770,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #pragma unroll
           for (int e = 0; e < NV; ++e) F[(size_t)k * NV2 + e * NV + al] = w[e];
         }
-        // D_i -= A_ji * W (left-multiply quirk; the plan's updates of this row all hit the diagonal)
-        for (int h = 0; h < nu; ++h, ++pcur) {
-          if (h > 0) {  // further A_jk of the same lower block (not on quad / hex meshes)
-            const int kk = rec[14 + 2 * pcur];
-            double xl[PB];
-#pragma unroll
-            for (int u = 0; u < PB; ++u)
-              if (16 * u + al < NV2) xl[u] = A[(size_t)kk * NV2 + 16 * u + al];
-            wave_sync();
-#pragma unroll
-            for (int u = 0; u < PB; ++u)
-              if (16 * u + al < NV2) S[16 * u + al] = xl[u];
-            wave_sync();
-          }
+        // D_i -= A_ji * W (left-multiply quirk; the block's one update hits the diagonal)
+        if (nu > 0) {
           double x[NV];
 #pragma unroll
           for (int e = 0; e < NV; ++e) x[e] = 0.0;
@@ -1695,7 +1683,7 @@ void launch_ilu_build_grp(rx_ctx* ctx, int gwaves) {
     const size_t shm = sizeof(double) * (size_t)(4 * gwaves) * grp_slot_doubles<NV>() +
                        sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1);
     k_ilu_build_grp<NV><<<ctx->npart, 64 * gwaves, shm, ctx->stream>>>(
-        ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_plan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
+        ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_gplan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
         ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)NV * NV, ctx->ilu_trace);
   }
 }

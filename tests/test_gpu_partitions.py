@@ -131,3 +131,38 @@ def test_implicit_step_vs_oracle(n_part):
     assert np.array_equal(rms2, rms)
     assert np.array_equal(s.download("SOL"), sol.ravel())
     s.close()
+
+
+@pytest.mark.parametrize("nx,ny,nz,n_part", [(20, 8, 6, 1), (20, 8, 6, 4), (50, 10, 10, 32)])
+def test_ilu_factor_3d_vs_oracle(nx, ny, nz, n_part):
+    """The grouped ILU(0) build on 3-D hexahedral jets (7-point stencil: up to six lower blocks per row under the
+    partitions' RCM orderings; 50x10x10 in 32 partitions has 72 rows with four, like 22 272 rows of C5), on a
+    diagonally dominant random matrix of the mesh's pattern: factor and apply bitwise equal to the oracle
+    (BuildILUPreconditioner / ComputeILUPreconditioner, matrix_structure.cpp:1368-1515)."""
+    mesh, st, mech_arrays, kw = synth.jet_case(nx, ny, n_species=7, n_part=n_part, nz=nz)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), rx.default_cfg(implicit=1, lin_prec=1, **kw))
+    s.set_state(st)
+    rp, col = s.bsr_pattern()
+    N, nv = len(rp) - 1, s.nVar
+    rng = np.random.default_rng(nz * 100 + n_part)
+    A = rng.standard_normal((len(col), nv, nv))
+    for i in range(N):
+        k = rp[i] + np.searchsorted(col[rp[i]:rp[i + 1]], i)
+        A[k] += 8.0 * nv * np.eye(nv)
+    b = rng.standard_normal(N * nv)
+    s.Preprocessing_zero()
+    s.Upwind_Residual()
+    s.sync()
+    s.download("RES")
+    s.upload("JAC", A.ravel())
+    s.upload("RHS", b)
+    s.ilu0_build()
+    s.sync()
+    pp = mesh["part_ptr"]
+    F = O.ilu_build(rp, col, A, part_ptr=pp)
+    assert_close(s.download("ILU").reshape(F.shape), F, rtol=0.0, what=f"3-D ILU(0) factor nz={nz} P={n_part}")
+    s.ilu0_apply("RHS", "SOL")
+    s.sync()
+    assert_close(s.download("SOL"), O.ilu_apply(rp, col, F, b, part_ptr=pp).ravel(), rtol=0.0,
+                 what=f"3-D ILU(0) apply nz={nz} P={n_part}")
+    s.close()

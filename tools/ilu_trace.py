@@ -1,6 +1,6 @@
 """Debug: phase timing of the ILU(0) factorisation kernel (partition 0) on the GPU.
 
-python tools/ilu_trace.py [nx ny parts]  — prints median shader-clock cycles per row phase:
+python tools/ilu_trace.py [nx ny parts [nz]]  — prints median shader-clock cycles per row phase:
   0-1 row/staging loads, 1-2 lower-block products and updates, 2-3 inverse of D_i, 3-4 write-back.
 With the grouped kernel (k_ilu_build_grp, the default on the jet meshes) the phases are
   0-1 loads + lower-block products + diagonal updates, 1-2 factor of D_i, 2-3 solve + stores,
@@ -15,7 +15,8 @@ sys.path.insert(0, ".")
 from tests.rxpkg import rx, synth  # noqa: E402
 
 nx, ny, P = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (500, 200, 256)))
-mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=7, n_part=P)
+nz = int(sys.argv[4]) if len(sys.argv) > 4 else 0  # 3-D extrusion (C5: 1000 50 256 20)
+mesh, st, mech, kw = synth.jet_case(nx, ny, n_species=7, n_part=P, nz=nz)
 s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), rx.default_cfg(implicit=1, lin_prec=1, **kw))
 s.set_state(st)
 s.SetPrimitive_Gradient_LS()
