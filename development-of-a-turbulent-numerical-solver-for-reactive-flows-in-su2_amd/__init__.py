@@ -558,6 +558,8 @@ class TurbSSTSolver:
     sync = ReactiveNSSolver.sync
     profile = ReactiveNSSolver.profile
     profile_read = ReactiveNSSolver.profile_read
+    ilu0_build = ReactiveNSSolver.ilu0_build
+    ilu0_apply = ReactiveNSSolver.ilu0_apply
 
     def set_state(self, T, wall_distance, F1=None, F2=None, CDkw=None):
         self.upload("U", T)

@@ -936,7 +936,7 @@ __global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__
                                                      const int32_t* __restrict__ upd_ptr,
                                                      const int2* __restrict__ upd, const double* __restrict__ A,
                                                      double* __restrict__ F, double* __restrict__ invD,
-                                                     bool diag_regs) {
+                                                     bool diag_regs, const int32_t* __restrict__ gplan) {
   constexpr int NV = 2, NV2 = 4;
   const int p = blockIdx.x;
   for (int l = part_lvl[p]; l < part_lvl[p + 1]; ++l) {
@@ -957,7 +957,53 @@ __global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__
       bool have_d = false;  // the factored D_i still in registers (register path): no reload of what was just stored
       for (int q = ra * NV2; q < k0 * NV2; ++q) F[q] = A[q];
       for (int q = k1 * NV2; q < rb * NV2; ++q) F[q] = A[q];
-      if (nlow < 0 || nbk > kSmallMaxB) {  // general per-block path
+      if (nlow < 0 && gplan) {
+        // more lower blocks than the compact plan holds (3-D: four at C5), on a mesh whose lower blocks each update
+        // only the diagonal (k_ilu_build_grp's plan): the general path's arithmetic, block by block
+        const int32_t* g = gplan + (size_t)r * 32;
+        for (int q = (kd + 1) * NV2; q < k1 * NV2; ++q) F[q] = A[q];
+        double D[NV2];
+#pragma unroll
+        for (int q = 0; q < NV2; ++q) D[q] = A[(size_t)kd * NV2 + q];
+        for (int k = k0; k < kd; ++k) {
+          const int t = k - k0, kk = g[14 + t];
+          double Sinv[NV2], Bij[NV2], W[NV2];
+#pragma unroll
+          for (int q = 0; q < NV2; ++q) {
+            Sinv[q] = invD[(size_t)g[8 + t] * NV2 + q];
+            Bij[q] = A[(size_t)k * NV2 + q];
+          }
+#pragma unroll
+          for (int a = 0; a < NV; ++a)
+#pragma unroll
+            for (int c = 0; c < NV; ++c) {
+              double sm = 0.0;
+#pragma unroll
+              for (int q = 0; q < NV; ++q) sm += Bij[a * NV + q] * Sinv[q * NV + c];
+              W[a * NV + c] = sm;
+            }
+          if (kk >= 0) {
+            const double* Bjk = F + (size_t)kk * NV2;
+#pragma unroll
+            for (int a = 0; a < NV; ++a)
+#pragma unroll
+              for (int c = 0; c < NV; ++c) {
+                double sm = 0.0;
+#pragma unroll
+                for (int q = 0; q < NV; ++q) sm += Bjk[a * NV + q] * W[q * NV + c];
+                D[a * NV + c] -= sm;
+              }
+          }
+#pragma unroll
+          for (int q = 0; q < NV2; ++q) F[(size_t)k * NV2 + q] = W[q];
+        }
+#pragma unroll
+        for (int q = 0; q < NV2; ++q) {
+          F[(size_t)kd * NV2 + q] = D[q];
+          L[q] = D[q];
+        }
+        have_d = true;
+      } else if (nlow < 0 || nbk > kSmallMaxB) {  // general per-block path
         for (int q = k0 * NV2; q < k1 * NV2; ++q) F[q] = A[q];
         for (int k = k0; k < kd; ++k) {
           const int j = col[k];
@@ -1765,7 +1811,8 @@ int rx_la_ilu_build(rx_ctx* ctx) {
                                                        reinterpret_cast<const int4*>(ctx->fs.slot), ctx->rp, ctx->col,
                                                        ctx->upd_ptr, reinterpret_cast<const int2*>(ctx->upd),
                                                        ctx->f[RX_F_JAC], ctx->f[RX_F_ILU], rx_invd_buf(ctx),
-                                                       getenv("RX_ILU2_RELOAD") == nullptr);
+                                                       getenv("RX_ILU2_RELOAD") == nullptr,
+                                                       ctx->ilu_grp_ok ? ctx->ilu_gplan : nullptr);
     RX_HIP(hipGetLastError());
     return RX_OK;
   }

@@ -165,4 +165,20 @@ def test_ilu_factor_3d_vs_oracle(nx, ny, nz, n_part):
     s.sync()
     assert_close(s.download("SOL"), O.ilu_apply(rp, col, F, b, part_ptr=pp).ravel(), rtol=0.0,
                  what=f"3-D ILU(0) apply nz={nz} P={n_part}")
+    # the SST context's 2x2 factor (k_ilu_build_2; rows with more than three lower blocks take the grouped plan)
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg())
+    A2 = rng.standard_normal((len(col), 2, 2))
+    for i in range(N):
+        A2[rp[i] + np.searchsorted(col[rp[i]:rp[i + 1]], i)] += 16.0 * np.eye(2)
+    b2 = rng.standard_normal(N * 2)
+    t.upload("JAC", A2.ravel())
+    t.upload("RHS", b2)
+    t.ilu0_build()
+    t.sync()
+    F2 = O.ilu_build(rp, col, A2, part_ptr=pp)
+    assert_close(t.download("ILU")[:F2.size].reshape(F2.shape), F2, rtol=0.0, what=f"3-D SST ILU(0) nz={nz} P={n_part}")
+    t.ilu0_apply("RHS", "SOL")
+    t.sync()
+    assert_close(t.download("SOL"), O.ilu_apply(rp, col, F2, b2, part_ptr=pp).ravel(), rtol=0.0,
+                 what=f"3-D SST ILU(0) apply nz={nz} P={n_part}")
     s.close()
