@@ -843,15 +843,14 @@ int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
     if ((kd == RX_BC_INLET || kd == RX_BC_OUTLET) && p < ctx->Nd) weak.push_back((int32_t)b);
     if ((kd == RX_BC_ISOTHERMAL || kd == RX_BC_HEATFLUX) && p < ctx->Nd) wall[p] = 1;
   }
-  // owned boundary points and their vertices in (marker, vertex) = input order
-  std::vector<int32_t> cnt(ctx->N + 1, 0);
-  for (int64_t b = 0; b < NB; ++b)
-    if (node[b] < ctx->Nd) cnt[node[b] + 1]++;
+  // owned boundary points and their vertices in (marker, vertex) = input order; vertices of RX_BC_NONE markers
+  // (symmetry planes: the reactive and SST solvers act on them in neither k_bc_apply nor k_sst_bc) are left out,
+  // so a point on none but such markers gets no workgroup (C5: the two symmetry planes, 100k points)
   std::vector<int32_t> bn, bn_ptr(1, 0), bn_vtx;
   {
     std::vector<std::vector<int32_t>> per(ctx->N);
     for (int64_t b = 0; b < NB; ++b)
-      if (node[b] < ctx->Nd) per[node[b]].push_back((int32_t)b);
+      if (node[b] < ctx->Nd && bc->kind[mark[b]] != RX_BC_NONE) per[node[b]].push_back((int32_t)b);
     for (int64_t p = 0; p < ctx->Nd; ++p)
       if (!per[p].empty()) {
         bn.push_back((int32_t)p);
