@@ -1448,7 +1448,7 @@ __device__ __forceinline__ void pf_load(RowPF<NV>& d, const double* __restrict__
     }
 }
 
-template <int NV>
+template <int NV, bool GMETA>
 __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict__ part_ptr,
                                                        const int32_t* __restrict__ rp,
                                                        const int32_t* __restrict__ f_part_lvl,
@@ -1470,40 +1470,48 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
   const int kb = rp[lo], ke = rp[hi];
   double* xs = lds;
   double* v = xs + (size_t)nr * NV;
-  int4* fsl = reinterpret_cast<int4*>(lds + (((size_t)nr * NV + RPB * NV + 1) & ~(size_t)1));  // 16-B aligned
-  int4* bsl = fsl + nr;
-  int* colL = reinterpret_cast<int*>(bsl + nr);
   // rows of partition p occupy slots [f_lvl_ptr[f_part_lvl[p]], +nr) in both schedules
   const int fl0 = f_part_lvl[p], fl1 = f_part_lvl[p + 1], bl0 = b_part_lvl[p], bl1 = b_part_lvl[p + 1];
   const int fr0 = f_lvl_ptr[fl0], br0 = b_lvl_ptr[bl0];
+  // GMETA: only the vector lives in LDS; the slot records and column indices are read from the global tables
+  // (L2-resident, a few tens of KB per partition) — the partitions whose metadata does not fit beside the vector
+  int4* fsl_l = reinterpret_cast<int4*>(lds + (((size_t)nr * NV + RPB * NV + 1) & ~(size_t)1));  // 16-B aligned
+  int4* bsl_l = fsl_l + nr;
+  int* colL_l = reinterpret_cast<int*>(bsl_l + nr);
+  const int4* fsl = GMETA ? f_slot + fr0 : fsl_l;
+  const int4* bsl = GMETA ? b_slot + br0 : bsl_l;
+  auto colx = [&](int k) { return GMETA ? col[k] - lo : colL_l[k - kb]; };
   const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
   const bool lane_ok = rl < RPB;
   RowPF<NV> cur, nxt;
+  int4 csl = make_int4(0, 0, 0, 0), nsl = csl;  // the first-pass slot records of this level and the next (GMETA)
   // first forward level's factor rows straight from the global slot table
   if (lane_ok && fr0 + rl < f_lvl_ptr[fl0 + 1]) {
-    const int4 sl = f_slot[fr0 + rl];
-    pf_load<NV>(cur, F, sl.y, sl.z, a);
+    csl = f_slot[fr0 + rl];
+    pf_load<NV>(cur, F, csl.y, csl.z, a);
   }
   for (int q = threadIdx.x; q < nr * NV; q += blockDim.x) xs[q] = b[(size_t)lo * NV + q];
-  for (int q = threadIdx.x; q < nr; q += blockDim.x) {
-    fsl[q] = f_slot[fr0 + q];
-    bsl[q] = b_slot[br0 + q];
+  if (!GMETA) {
+    for (int q = threadIdx.x; q < nr; q += blockDim.x) {
+      fsl_l[q] = f_slot[fr0 + q];
+      bsl_l[q] = b_slot[br0 + q];
+    }
+    for (int q = threadIdx.x; q < ke - kb; q += blockDim.x) colL_l[q] = col[kb + q] - lo;
   }
-  for (int q = threadIdx.x; q < ke - kb; q += blockDim.x) colL[q] = col[kb + q] - lo;
   lds_barrier();
   for (int l = fl0; l < fl1; ++l) {
     const int r0 = f_lvl_ptr[l], r1 = f_lvl_ptr[l + 1];
     if (lane_ok && l + 1 < fl1 && r1 + rl < f_lvl_ptr[l + 2]) {
-      const int4 sl = fsl[r1 + rl - fr0];
-      pf_load<NV>(nxt, F, sl.y, sl.z, a);
+      nsl = fsl[r1 + rl - fr0];
+      pf_load<NV>(nxt, F, nsl.y, nsl.z, a);
     }
     for (int r = r0 + rl; r < r1 && lane_ok; r += RPB) {
-      const int4 sl = fsl[r - fr0];
+      const int4 sl = (GMETA && r == r0 + rl) ? csl : fsl[r - fr0];
       const int li = sl.x - lo;
       double xi = xs[li * NV + a];
       for (int k = sl.y; k < sl.z; ++k) {
         const int t = k - sl.y;
-        const double* xj = xs + colL[k - kb] * NV;
+        const double* xj = xs + colx(k) * NV;
         double s = 0.0;
         if (r == r0 + rl && t < kPF) {
 #pragma unroll
@@ -1523,23 +1531,25 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
     }
     lds_barrier();
     cur = nxt;
+    csl = nsl;
   }
   // backward: upper blocks + the row of inv(D_i)
   RowPF<NV> ucur, unxt;
   double icur[NV], inxt[NV];
+  int4 bcsl = make_int4(0, 0, 0, 0), bnsl = bcsl;
   if (lane_ok && br0 + rl < b_lvl_ptr[bl0 + 1]) {
-    const int4 sl = bsl[rl];
-    pf_load<NV>(ucur, Fu, sl.z + 1, sl.w, a);
+    bcsl = bsl[rl];
+    pf_load<NV>(ucur, Fu, bcsl.z + 1, bcsl.w, a);
 #pragma unroll
-    for (int c = 0; c < NV; ++c) icur[c] = invD[(size_t)sl.x * NV2 + a * NV + c];
+    for (int c = 0; c < NV; ++c) icur[c] = invD[(size_t)bcsl.x * NV2 + a * NV + c];
   }
   for (int l = bl0; l < bl1; ++l) {
     const int r0 = b_lvl_ptr[l], r1 = b_lvl_ptr[l + 1];
     if (lane_ok && l + 1 < bl1 && r1 + rl < b_lvl_ptr[l + 2]) {
-      const int4 sl = bsl[r1 + rl - br0];
-      pf_load<NV>(unxt, Fu, sl.z + 1, sl.w, a);
+      bnsl = bsl[r1 + rl - br0];
+      pf_load<NV>(unxt, Fu, bnsl.z + 1, bnsl.w, a);
 #pragma unroll
-      for (int c = 0; c < NV; ++c) inxt[c] = invD[(size_t)sl.x * NV2 + a * NV + c];
+      for (int c = 0; c < NV; ++c) inxt[c] = invD[(size_t)bnsl.x * NV2 + a * NV + c];
     }
     for (int base = r0; base < r1; base += RPB) {
       const int r = base + rl;
@@ -1547,13 +1557,13 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
       const bool first = base == r0;
       int i = 0, li = 0;
       if (act) {
-        const int4 sl = bsl[r - br0];
+        const int4 sl = (GMETA && first) ? bcsl : bsl[r - br0];
         i = sl.x;
         li = i - lo;
         double sum = 0.0;
         for (int k = sl.z + 1; k < sl.w; ++k) {
           const int t = k - sl.z - 1;
-          const double* xj = xs + colL[k - kb] * NV;
+          const double* xj = xs + colx(k) * NV;
           double s = 0.0;
           if (first && t < kPF) {
 #pragma unroll
@@ -1587,6 +1597,7 @@ __global__ __launch_bounds__(256) void k_ilu_apply_lds(const int32_t* __restrict
       lds_barrier();
     }
     ucur = unxt;
+    bcsl = bnsl;
 #pragma unroll
     for (int c = 0; c < NV; ++c) icur[c] = inxt[c];
   }
@@ -1781,7 +1792,9 @@ int rx_ilu_max_waves() { return RX_ILU_MAX_WAVES; }
 // Raise the dynamic-LDS limit of the LDS-resident kernels to what the device allows (once).
 int rx_la_prepare(rx_ctx* ctx) {
   RX_NV_SWITCH(ctx->nVar, {
-    RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_lds<NV_>),
+    RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_lds<NV_, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_lds<NV_, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_part<NV_>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
@@ -1845,13 +1858,28 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                      sizeof(int32_t) * (8 * (size_t)ctx->maxpart + (size_t)ctx->maxpart_nnzb);
   static const bool no_lds = getenv("RX_NO_LDS_APPLY") != nullptr;  // diagnosis: force the global sweeps
   if (shm <= (size_t)ctx->lds_max && !no_lds) {
-    RX_NV_SWITCH(nv, (k_ilu_apply_lds<NV_><<<ctx->npart, 256, shm, ctx->stream>>>(
+    RX_NV_SWITCH(nv, (k_ilu_apply_lds<NV_, false><<<ctx->npart, 256, shm, ctx->stream>>>(
                          ctx->part_ptr, ctx->rp, ctx->fs.part_lvl, ctx->fs.lvl_ptr,
                          reinterpret_cast<const int4*>(ctx->fs.slot), ctx->bs.part_lvl, ctx->bs.lvl_ptr,
                          reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_ilu_upper(ctx),
                          rx_invd_buf(ctx), b, x, done, conv)));
     RX_HIP(hipGetLastError());
     return rx_la_exchange(ctx, x, nv);  // ComputeILUPreconditioner's closing SendReceive_Solution (:1513)
+  }
+  // RX_LDS_GMETA=1 (measured, not the default): when the vector alone fits (the SST's 2x2 system at C3 / C5, 62 KB
+  // per partition), the LDS-resident apply with slot records and columns read from the global tables. Bitwise the
+  // same, but slower than the wide sweeps below: SST_SOLVE 1.78 -> 1.90 ms at C3, 2.79 -> 3.41 ms at C5 (the
+  // global metadata loads become the level's dependent chain at one wavefront per SIMD)
+  const size_t shm_v = sizeof(double) * ((size_t)ctx->maxpart * nv + (size_t)(256 / nv) * nv + 1);
+  static const bool gmeta = getenv("RX_LDS_GMETA") != nullptr;
+  if (shm_v <= (size_t)ctx->lds_max && !no_lds && gmeta) {
+    RX_NV_SWITCH(nv, (k_ilu_apply_lds<NV_, true><<<ctx->npart, 256, shm_v, ctx->stream>>>(
+                         ctx->part_ptr, ctx->rp, ctx->fs.part_lvl, ctx->fs.lvl_ptr,
+                         reinterpret_cast<const int4*>(ctx->fs.slot), ctx->bs.part_lvl, ctx->bs.lvl_ptr,
+                         reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_ilu_upper(ctx),
+                         rx_invd_buf(ctx), b, x, done, conv)));
+    RX_HIP(hipGetLastError());
+    return rx_la_exchange(ctx, x, nv);
   }
   static const bool narrow = getenv("RX_NARROW_APPLY") != nullptr;  // diagnosis: the 256-thread sweeps
   const int width = std::max(ctx->fs.maxwidth, ctx->bs.maxwidth);
