@@ -695,6 +695,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
   // the workgroup's kEB consecutive edge records, staged from their tile: each load is kEB consecutive doubles
   __shared__ double ssm[SS * kEB];
   const int eb = blockIdx.x * kEB;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = gt / 16, b = gt % 16;
+  const bool live = e < E;
+  const int bc = b < nVar ? b : 0;
+  // the team's own inputs (edge, dT/dU of both nodes and, in 2-D, this lane's column of both convective blocks) are
+  // loaded before the summary staging and its barrier, so that both sets of loads are in flight together (plain
+  // loads stay in flight across __syncthreads): C3 VISC_JAC 3.86 -> 3.73 ms. In 3-D the 12-row columns held across
+  // the staging spilled (46 VGPRs) and the kernel was slower (C5 7.03 -> 7.29 ms): there they are loaded after it.
+  constexpr bool kEarlyJc = NDIM == 2;
+  int n0 = 0, n1 = 0;
+  double sib = 0.0, sjb = 0.0, jci[nVar], jcj[nVar];
+  auto load_jc = [&]() {
+    const double* Jci = Jc + (size_t)e * 2 * nVar2;
+#pragma unroll
+    for (int r = 0; r < nVar; ++r) {
+      jci[r] = Jci[r * nVar + bc];
+      jcj[r] = Jci[nVar2 + r * nVar + bc];
+    }
+  };
+  if (live) {
+    n0 = edges[2 * e];
+    n1 = edges[2 * e + 1];
+    sib = dTdU[(size_t)n0 * nVar + bc];
+    sjb = dTdU[(size_t)n1 * nVar + bc];
+    if (kEarlyJc && Jc) load_jc();
+  }
   {
     const double* tile = Summ + (size_t)(eb / kSummTile) * SS * kSummTile + eb % kSummTile;
     for (int q = threadIdx.x; q < SS * kEB; q += kBlock) {
@@ -703,23 +729,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
     }
   }
   __syncthreads();
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-  const int e = gt / 16, b = gt % 16;
-  if (e >= E) return;  // whole teams exit together (E * 16 threads)
-  const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
-  const int bc = b < nVar ? b : 0;
-  const double sib = dTdU[(size_t)n0 * nVar + bc], sjb = dTdU[(size_t)n1 * nVar + bc];
+  if (!live) return;  // whole teams exit together (E * 16 threads)
   double* Ji = Jac + (size_t)e * 2 * nVar2;
   const SummCRef sm{ssm + (e - eb), kEB};
   if (Jc) {
-    // this lane's column of both convective blocks, loaded before the Jacobian arithmetic hides their latency
-    const double* Jci = Jc + (size_t)e * 2 * nVar2;
-    double jci[nVar], jcj[nVar];
-#pragma unroll
-    for (int r = 0; r < nVar; ++r) {
-      jci[r] = Jci[r * nVar + bc];
-      jcj[r] = Jci[nVar2 + r * nVar + bc];
-    }
+    if (!kEarlyJc) load_jc();
     visc_jac_column<NS, NDIM>(m, P, sm, sib, sjb, b, b, Ji, Ji + nVar2, jci, jcj, A + edge_blk[2 * e] * nVar2,
                               A + edge_blk[2 * e + 1] * nVar2);
   } else {
