@@ -1405,16 +1405,25 @@ __global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__
       const int r = base + rl;
       const bool act = lane && r < r1;
       int i = 0;
+      double inv[NV];  // row a of inv(D_i): an input, loaded with the row's blocks (it stays in flight across the
+                       // barrier) instead of after it, one global round trip less per level
       if (act) {
         const int4 sl = (base == r0) ? cur : slot[r];
         i = sl.x;
+#ifndef RX_BWD_LATE_INV
+#pragma unroll
+        for (int c = 0; c < NV; ++c) inv[c] = invD[(size_t)i * NV2 + a * NV + c];
+#endif
         double sum = 0.0;
         row_blocks<NV>(F, col, x, sl.z + 1, sl.w, a, [&](double s) { sum += s; });
         v[rl * NV + a] = x[(size_t)i * NV + a] - sum;
       }
       __syncthreads();
       if (act) {
-        const double* inv = invD + (size_t)i * NV2 + a * NV;
+#ifdef RX_BWD_LATE_INV
+#pragma unroll
+        for (int c = 0; c < NV; ++c) inv[c] = invD[(size_t)i * NV2 + a * NV + c];
+#endif
         double s = 0.0;
 #pragma unroll
         for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
