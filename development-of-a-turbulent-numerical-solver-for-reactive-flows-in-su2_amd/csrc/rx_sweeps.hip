@@ -1388,11 +1388,21 @@ __global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__
                                                      double* __restrict__ x, int* __restrict__ done,
                                                      const int* __restrict__ conv) {
   if (skip_sweep(done, conv)) return;
-  constexpr int NV2 = NV * NV, RPB = TB / NV;
+  // Rows are laid out wavefront by wavefront (64 / NV rows per wavefront, the last 64 mod NV lanes idle), so that a
+  // row's lanes never straddle two wavefronts: the exchange of v between the two halves of a level is then
+  // wavefront-local (wave_sync) instead of a workgroup barrier. RX_BWD_BLOCK_ROWS restores the dense layout.
+#ifdef RX_BWD_BLOCK_ROWS
+  constexpr bool kWaveRows = false;
+#else
+  constexpr bool kWaveRows = true;
+#endif
+  constexpr int NV2 = NV * NV, RW = 64 / NV, RPB = kWaveRows ? (TB / 64) * RW : TB / NV;
   __shared__ double v[RPB * NV];
   const int p = blockIdx.x;
-  const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
-  const bool lane = rl < RPB;
+  const int wl = threadIdx.x & 63;
+  const int rl = kWaveRows ? (int)(threadIdx.x >> 6) * RW + wl / NV : (int)threadIdx.x / NV;
+  const int a = kWaveRows ? wl - (wl / NV) * NV : (int)threadIdx.x - rl * NV;
+  const bool lane = kWaveRows ? wl < RW * NV : rl < RPB;
   const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
   int4 nxt = make_int4(-1, 0, 0, 0);
   if (lane && l0 < l1 && lvl_ptr[l0] + rl < lvl_ptr[l0 + 1]) nxt = slot[lvl_ptr[l0] + rl];
@@ -1418,7 +1428,8 @@ __global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__
         row_blocks<NV>(F, col, x, sl.z + 1, sl.w, a, [&](double s) { sum += s; });
         v[rl * NV + a] = x[(size_t)i * NV + a] - sum;
       }
-      __syncthreads();
+      if (kWaveRows) wave_sync();
+      else __syncthreads();
       if (act) {
 #ifdef RX_BWD_LATE_INV
 #pragma unroll
