@@ -684,8 +684,13 @@ __global__ __launch_bounds__(64) RX_VISC_ATTR void k_visc_edge(int E, const int3
 // Fused assembly (Jc != nullptr): the same lanes also write the edge's two off-diagonal BSR blocks from its own
 // convective scratch, so k_assemble only builds the diagonal blocks and the residual (each Jc / Jv block is read
 // by the edge that made it and by its own node's diagonal, instead of by both nodes' teams).
+// waves per SIMD: 3 in 2-D (at 2: VISC_JAC 3.86 -> 4.27 ms at C3), 2 in 3-D (at 3 the 12-row columns spill 28
+// VGPRs: C5 VISC_JAC 7.54 -> 7.16 ms at 2)
+#ifndef RX_WPE_VJAC
+#define RX_WPE_VJAC RX_WPE(NDIM == 2 ? 3 : 2)
+#endif
 template <int NS, int NDIM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_visc_jac(int E, const int32_t* __restrict__ edges,
+__global__ __launch_bounds__(kBlock) RX_WPE_VJAC void k_visc_jac(int E, const int32_t* __restrict__ edges,
                                                      const double* __restrict__ dTdU, const double* __restrict__ Summ,
                                                      DevMech m, ViscParams P, double* __restrict__ Jac,
                                                      const double* __restrict__ Jc,
