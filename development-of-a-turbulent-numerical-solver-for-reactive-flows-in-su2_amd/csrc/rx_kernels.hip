@@ -708,7 +708,11 @@ __global__ __launch_bounds__(kBlock) RX_WPE_VJAC void k_visc_jac(int E, const in
   // loaded before the summary staging and its barrier, so that both sets of loads are in flight together (plain
   // loads stay in flight across __syncthreads): C3 VISC_JAC 3.86 -> 3.73 ms. In 3-D the 12-row columns held across
   // the staging spilled (46 VGPRs) and the kernel was slower (C5 7.03 -> 7.29 ms): there they are loaded after it.
+#ifdef RX_VJ_EARLY3
+  constexpr bool kEarlyJc = true;
+#else
   constexpr bool kEarlyJc = NDIM == 2;
+#endif
   int n0 = 0, n1 = 0;
   double sib = 0.0, sjb = 0.0, jci[nVar], jcj[nVar];
   auto load_jc = [&]() {
