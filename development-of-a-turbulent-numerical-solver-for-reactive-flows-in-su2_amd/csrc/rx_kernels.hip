@@ -704,14 +704,14 @@ __global__ __launch_bounds__(kBlock) RX_WPE_VJAC void k_visc_jac(int E, const in
   const int e = gt / 16, b = gt % 16;
   const bool live = e < E;
   const int bc = b < nVar ? b : 0;
-  // the team's own inputs (edge, dT/dU of both nodes and, in 2-D, this lane's column of both convective blocks) are
-  // loaded before the summary staging and its barrier, so that both sets of loads are in flight together (plain
-  // loads stay in flight across __syncthreads): C3 VISC_JAC 3.86 -> 3.73 ms. In 3-D the 12-row columns held across
-  // the staging spilled (46 VGPRs) and the kernel was slower (C5 7.03 -> 7.29 ms): there they are loaded after it.
-#ifdef RX_VJ_EARLY3
-  constexpr bool kEarlyJc = true;
-#else
+  // the team's own inputs (edge, dT/dU of both nodes, this lane's column of both convective blocks) are loaded
+  // before the summary staging and its barrier, so that both sets of loads are in flight together (plain loads stay
+  // in flight across __syncthreads): C3 VISC_JAC 3.86 -> 3.73 ms; in 3-D, with 2 waves per SIMD (no spills), C5
+  // 7.16 -> 6.68 ms (at 3 waves the 12-row columns spilled and it lost 0.27 ms). RX_VJ_LATE3 keeps 3-D's late loads.
+#ifdef RX_VJ_LATE3
   constexpr bool kEarlyJc = NDIM == 2;
+#else
+  constexpr bool kEarlyJc = true;
 #endif
   int n0 = 0, n1 = 0;
   double sib = 0.0, sjb = 0.0, jci[nVar], jcj[nVar];
