@@ -628,7 +628,14 @@ class SU2Mesh:
                           bvertex_normal=arr(md.bvert_normal, (self.NB, nd.value)), n_dim=nd.value)
         self.global_index = np.ctypeslib.as_array(lib().rx_mesh_global_index(h), shape=(self.N,)).copy()
         self._mesh["bvertex_pn"] = np.ctypeslib.as_array(lib().rx_mesh_normal_neighbor(h), shape=(self.NB,)).copy()
-        self.wall_distance(walls)
+        if self._borrowed and not walls:
+            # a case's mesh (rx_case_read already ran ComputeWall_Distance over its wall markers): take those
+            # distances instead of recomputing (and, with no walls given, overwriting) them
+            p = lib().rx_mesh_wall_distance(self.h, None)
+            self._mesh["wall_distance"] = (np.ctypeslib.as_array(p, shape=(self.N,)).copy() if p
+                                           else np.zeros(self.N))
+        else:
+            self.wall_distance(walls)
 
     def wall_distance(self, walls):
         flags = np.array([1 if t in walls else 0 for t in self.tags], dtype=np.int32)
@@ -787,9 +794,6 @@ def case_from_cfg(cfg_path):
     rk = [ap[k] for k in range(n.value)] if n.value else None
     fs = [C.c_double() for _ in range(4)]
     _chk(lib().rx_case_free_stream(h, *[C.byref(x) for x in fs]), "rx_case_free_stream")
-    mesh._mesh["wall_distance"] = np.ctypeslib.as_array(
-        lib().rx_mesh_wall_distance(mesh.h, np.array([1 if k in (BC_ISOTHERMAL, BC_HEATFLUX) else 0 for k in kinds],
-                                                     dtype=np.int32).ctypes.data), shape=(mesh.N,)).copy()
     return dict(mesh=mesh, mech=mech, flow_cfg=_cfg_dict(fc), sst_cfg=_cfg_dict(sc), bc=bc, rk_alpha=rk,
                 free_stream=dict(rho=fs[0].value, mu=fs[1].value, T=fs[2].value, P=fs[3].value), case=case)
 

@@ -397,6 +397,9 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         rec[7] = ok ? npair : 0;
       }
       ctx->ilu_grp_ok = grp_ok;
+      // the grouped build's LDS (its row slots + the partition's level table) must fit this device's
+      // limit; else k_ilu_build_part, and rx_ilu_upper (same predicate) keeps the sweeps on the ILU buffer
+      if (grp_ok && rx_ilu_grp_lds(ctx) > (size_t)ctx->lds_max) ctx->ilu_grp_ok = false;
       CK(dupload(ctx, &ctx->ilu_plan, plan.data(), plan.size()));
       if (grp_ok) CK(dupload(ctx, &ctx->ilu_gplan, gplan.data(), gplan.size()));
     }
@@ -673,6 +676,7 @@ int rx_field_size(const rx_ctx* ctx, rx_field f, int64_t* count) {
 int rx_upload(rx_ctx* ctx, rx_field f, const double* host, int64_t count) {
   if (!ctx || f < 0 || f >= RX_F_COUNT || count != ctx->fcount[f] || !host) return RX_ERR_ARG;
   RX_HIP(hipMemcpyAsync(ctx->f[f], host, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (f == RX_F_ILU) ctx->ilu_valid = 1;  // a caller-provided factor
   // a loaded solution is also the Solution_Old (CVariable construction / LoadRestart)
   if (f == RX_F_U && ctx->kind == RX_KIND_FLOW && ctx->uold)
     RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[f], count * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
@@ -686,6 +690,8 @@ int rx_download(rx_ctx* ctx, rx_field f, double* host, int64_t count) {
     int rc = ensure_assembled(ctx);
     if (rc && rc != RX_ERR_STATE) return rc;
   }
+  // with the viscous scratch aliased onto it, the ILU field holds a factor only after an ILU build
+  if (f == RX_F_ILU && !ctx->ilu_valid) return RX_ERR_STATE;
   if (f == RX_F_ILU && ctx->assembled) {  // the factor with the blocks ILU(0) leaves unchanged (rx_sweeps.hip);
     int rc = rx_la_ilu_materialize(ctx);  // while a residual is being assembled the field holds its scratch
     if (rc) return rc;
@@ -742,6 +748,7 @@ int rx_edge_flux_conv(rx_ctx* ctx) {
 
 int rx_edge_flux_visc(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
+  if (ctx->scratch_in_ilu) ctx->ilu_valid = 0;  // the per-edge viscous Jacobians / summary overwrite the factor
   int rc = rx_launch_visc_edge(ctx);
   if (rc) return rc;
   if (!ctx->cfg.implicit) {
@@ -825,6 +832,7 @@ int rx_ilu0_build(rx_ctx* ctx) {
 
 int rx_ilu0_apply(rx_ctx* ctx, rx_field b, rx_field x) {
   if (!ctx || !ctx->cfg.implicit) return RX_ERR_ARG;
+  if (!ctx->ilu_valid) return RX_ERR_STATE;  // no factor since the last viscous sweep (scratch) / never built
   RxPhase ph(ctx, RX_K_ILU_APPLY);
   return rx_la_ilu_apply(ctx, ctx->f[b], ctx->f[x], nullptr, nullptr);
 }

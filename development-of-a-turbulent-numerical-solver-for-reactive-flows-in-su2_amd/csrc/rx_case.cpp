@@ -105,7 +105,9 @@ bool spline(const rx_mech_desc& d, int prop, int s, double T, double* out) {
   const double *x = d.tab_x + o, *y = d.tab_y + o, *y2 = d.tab_y2 + o;
   if (T < x[0] || T > x[nt - 1]) return false;
   const double h = x[1] - x[0];
-  const unsigned long klo = (unsigned long)((T - x[0]) / h + 1);
+  // the reference's klo is nt at T == x[nt - 1] and reads one past the table (spline.cpp:66-70, undefined
+  // behaviour); clamped to the last interval, whose b = 1 gives y[nt - 1], the spline's value there
+  const unsigned long klo = std::min((unsigned long)((T - x[0]) / h + 1), (unsigned long)(nt - 1));
   const double a = (x[klo] - T) / h, b = (T - x[klo - 1]) / h;
   *out = a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0;
   return true;
@@ -172,6 +174,48 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
     return fail(k, RX_ERR_UNSUPPORTED, "only REF_DIMENSIONALIZATION= DIMENSIONAL");
   if (upper(c.str("CFL_ADAPT", "NO")) != "NO") return fail(k, RX_ERR_UNSUPPORTED, "CFL_ADAPT= YES");
   if (std::atoi(c.str("MGLEVEL", "0").c_str()) != 0) return fail(k, RX_ERR_UNSUPPORTED, "MGLEVEL > 0");
+  {
+    // the solver and numerics this path builds (VERDICT r03 missing #3): anything else is refused by name
+    struct Need {
+      const char* key;
+      const char* dflt;  // CConfig's default ("" = NO_SOLVER / NO_CONVECTIVE: the reference refuses to run)
+      const char* want;
+      const char* why;
+    };
+    static const Need need[] = {
+        // Kind_Solver (config_structure.cpp:622, default NO_SOLVER); REACTIVE_NAVIER_STOKES + a turbulence model
+        // becomes REACTIVE_RANS (:2872-2874), the solver pair driver_structure.cpp:795-822 builds
+        {"PHYSICAL_PROBLEM", "", "REACTIVE_NAVIER_STOKES", "the outer iteration on this path is REACTIVE_RANS"},
+        // :626 (default NONE): SA would build CTurbSASolver (driver_structure.cpp:806-814), NONE a laminar
+        // CReactiveNSSolver without TURB_SOL; rx::Iterate / rx.Iterate always run the SST SingleGrid_Iteration
+        {"KIND_TURB_MODEL", "NONE", "SST", "only the Menter SST turbulence solver is built"},
+        // :1147 (default WEIGHTED_LEAST_SQUARES): GREEN_GAUSS branches to SetPrimitive_Gradient_GG
+        // (solver_direct_reactive.cpp:1055, 4717, 4784-4880)
+        {"NUM_METHOD_GRAD", "WEIGHTED_LEAST_SQUARES", "WEIGHTED_LEAST_SQUARES", "only the weighted LSQ gradient"},
+        // :1047 (default FGMRES): CSysSolve::Solve's other Krylov methods (linear_solvers_structure.cpp:601-724)
+        {"LINEAR_SOLVER", "FGMRES", "FGMRES", "only FGMRES"},
+        // :1160 (default NO_CONVECTIVE): the reactive driver exits for any upwind scheme but AUSM
+        // (driver_structure.cpp:1517-1529)
+        {"CONV_NUM_METHOD_FLOW", "", "AUSM", "the reactive solvers implement AUSM only"},
+        // :1195: the SST convective term is CUpwSca_TurbSST
+        {"CONV_NUM_METHOD_TURB", "SCALAR_UPWIND", "SCALAR_UPWIND", "the SST convection is the scalar upwind"},
+        // :1189 (default FIRST_ORDER): the turbulent MUSCL branch is not built
+        {"SPATIAL_ORDER_TURB", "1ST_ORDER", "1ST_ORDER", "the SST upwind is first order"},
+        // :1030: the SST SingleGrid_Iteration calls ImplicitEuler_Iteration
+        {"TIME_DISCRE_TURB", "EULER_IMPLICIT", "EULER_IMPLICIT", "the SST update is the implicit Euler step"},
+        // :979 (default STEADY): dual time stepping is not built
+        {"UNSTEADY_SIMULATION", "NO", "NO", "steady (local time stepping) only"},
+        {"MATH_PROBLEM", "DIRECT", "DIRECT", "the direct problem only"},
+    };
+    for (const Need& n : need) {
+      std::string v = upper(c.str(n.key, n.dflt));
+      if (std::string(n.key) == "UNSTEADY_SIMULATION" && v == "STEADY") v = "NO";
+      if (std::string(n.key) == "PHYSICAL_PROBLEM" && v == "REACTIVE_RANS") v = "REACTIVE_NAVIER_STOKES";
+      if (v != n.want)
+        return fail(k, RX_ERR_UNSUPPORTED,
+                    std::string(n.key) + "= " + (v.empty() ? std::string("(unset)") : v) + ": " + n.why);
+    }
+  }
   if (!c.has("MESH_FILENAME") || !c.has("CONFIG_LIB_FILE"))
     return fail(k, RX_ERR_STATE, "MESH_FILENAME / CONFIG_LIB_FILE missing");
   // mesh + library
@@ -343,7 +387,15 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
   double mv2 = 0.0;
   for (int d = 0; d < nd && d < (int)vel.size(); ++d) mv2 += vel[d] * vel[d];
   const double mod_v = std::sqrt(mv2);
-  F.mach_inf = mod_v / std::sqrt(gamma * rgas * T_inf);  // CConfig::SetMach (:973), frozen sound speed
+  // mInfty of the AUSM numerics is config->GetMach() (numerics_direct_reactive.cpp:19). The reactive solver
+  // overwrites MACH_NUMBER with the frozen-sound-speed Mach (CConfig::SetMach, solver_direct_reactive.cpp:973) only
+  // inside its CONSOLE_OUTPUT_VERBOSITY == VERB_HIGH (the default, config_structure.cpp:1384) && rank == MASTER_NODE
+  // block; otherwise MACH_NUMBER (default 0.0, :725) stands. In an MPI run of the reference the other ranks keep
+  // MACH_NUMBER even with VERB_HIGH; this path gives every rank the master's value.
+  if (upper(c.str("CONSOLE_OUTPUT_VERBOSITY", "HIGH")) == "HIGH")
+    F.mach_inf = mod_v / std::sqrt(gamma * rgas * T_inf);
+  else
+    F.mach_inf = c.num("MACH_NUMBER", 0.0);
   std::vector<double> visc(ns), yom(ns);
   for (int s = 0; s < ns; ++s) {
     if (!spline(md, 3, s, T_inf, &visc[s])) return fail(k, RX_ERR_RANGE, "FREESTREAM_TEMPERATURE out of the tables");

@@ -117,6 +117,8 @@ struct rx_ctx {
   double* jvisc = nullptr;   // [E][2][nVar*nVar]
   double* vsumm = nullptr;   // [E/kSummTile][visc_summary_size][kSummTile] per-edge viscous summary (implicit)
   int scratch_in_ilu = 0;    // jvisc / vsumm alias the ILU buffer (dead before the ILU build writes it)
+  int ilu_valid = 0;         // the ILU field holds a factor (set by the ILU build / an upload of the field; cleared when
+                             // the viscous sweep writes its scratch there): rx_ilu0_apply / rx_download(ILU) need it
   double* jsrc = nullptr;    // [ceil(N/kSrcTile)][ns*nVar][kSrcTile] species rows of the source Jacobians
   double* rsrc = nullptr;    // [N][nVar] source residual (implicit path)
   double* uold = nullptr;    // [N][nVar] Solution_Old of the RK stages
@@ -260,6 +262,7 @@ int rx_la_build_system(rx_ctx* ctx);
 // boundary conditions (rx_bc.hip)
 void rx_bc_free(rx_ctx* ctx);
 int rx_bc_launch_weak(rx_ctx* ctx, hipStream_t st);  // ghost states + boundary fluxes (+ Jacobians)
+size_t rx_ilu_grp_lds(const rx_ctx* ctx);  // grouped ILU build's dynamic LDS (rx_sweeps.hip)
 int rx_ensure_assembled(rx_ctx* ctx);  // implicit: assemble the residual / BSR Jacobian now (rx_api.hip)
 // SST (rx_sst.hip)
 int rx_sst_build_system(rx_ctx* ctx);

@@ -18,6 +18,8 @@
 // scalar reference's.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -1828,7 +1830,37 @@ int rx_la_prepare(rx_ctx* ctx) {
   return RX_OK;
 }
 
+// Dynamic LDS of the grouped build at its launch configuration (launch_ilu_build_grp); 0 when not instantiated.
+size_t rx_ilu_grp_lds(const rx_ctx* ctx) {
+  size_t shm = 0;
+  auto f = [&](auto nvc) {
+    constexpr int NV = decltype(nvc)::value;
+    if constexpr (NV >= 5) {
+      const int gwaves = std::max(1, std::min(grp_waves<NV>(), (ctx->fs.maxwidth + 3) / 4));
+      shm = sizeof(double) * (size_t)(4 * gwaves) * grp_slot_doubles<NV>() + sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1);
+    }
+  };
+  switch (ctx->nVar) {
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 9: f(std::integral_constant<int, 9>{}); break;
+    case 11: f(std::integral_constant<int, 11>{}); break;
+    case 12: f(std::integral_constant<int, 12>{}); break;
+    case 13: f(std::integral_constant<int, 13>{}); break;
+    case 14: f(std::integral_constant<int, 14>{}); break;
+    default: break;
+  }
+  return shm;
+}
+
+static int ilu_build_impl(rx_ctx* ctx);
 int rx_la_ilu_build(rx_ctx* ctx) {
+  const int rc = ilu_build_impl(ctx);
+  ctx->ilu_valid = rc == RX_OK;
+  return rc;
+}
+
+static int ilu_build_impl(rx_ctx* ctx) {
   const int nv = ctx->nVar;
   const size_t shm_small = sizeof(double) * (size_t)nv * nv * (ctx->maxpart_nnzb + ctx->maxpart);
   if (nv <= 4 && !ctx->ilu_trace && shm_small <= (size_t)ctx->lds_max) {

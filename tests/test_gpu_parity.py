@@ -214,6 +214,42 @@ def test_linear_algebra_matches_reference(prec, case):
     s.close()
 
 
+def test_ilu_field_needs_a_factor():
+    """the per-edge viscous Jacobians share the ILU buffer, so after a new viscous sweep the
+    field holds scratch, not a factor. rx_ilu0_apply and rx_download(ILU) then refuse with RX_ERR_STATE instead of
+    sweeping over scratch; after the next ILU build both work again and give the same factor and apply."""
+    g = golden("mini9")
+    s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=True, lin_prec=1)
+    s.upload("DT", g["dt"])
+
+    def residual():
+        s.Preprocessing_zero()
+        s.Upwind_Residual()
+        s.Viscous_Residual()
+        s.Source_Residual()
+        s.sync()
+
+    residual()
+    s.upload("RHS", g["sys_rhs"])
+    with pytest.raises(rx.RxError, match="status 7"):  # never built
+        s.ilu0_apply("RHS", "SOL")
+    s.ilu0_build()
+    F0 = s.download("ILU")
+    s.ilu0_apply("RHS", "SOL")
+    x0 = s.download("SOL")
+    residual()  # a new residual: the viscous sweep writes its scratch into the ILU buffer
+    with pytest.raises(rx.RxError, match="status 7"):
+        s.ilu0_apply("RHS", "SOL")
+    with pytest.raises(rx.RxError, match="status 7"):
+        s.download("ILU")
+    s.ilu0_build()
+    assert np.array_equal(s.download("ILU"), F0)
+    s.upload("SOL", np.zeros_like(x0))
+    s.ilu0_apply("RHS", "SOL")
+    assert np.array_equal(s.download("SOL"), x0)
+    s.close()
+
+
 @pytest.mark.parametrize("nx,ny", [(120, 40)])
 def test_synthetic_jet_vs_oracle(nx, ny):
     """Larger mesh (resampled reacting records): HIP vs CPU oracle for every residual phase."""

@@ -252,6 +252,101 @@ def test_case_from_cfg_defaults_and_rejections(tmp_path):
             rx.case_from_cfg(os.path.join(wd, "case.cfg"))
 
 
+REJECTED = [  # (key, value): physics / numerics this path does not build (VERDICT r03 missing #3), None = key removed
+    ("PHYSICAL_PROBLEM", "REACTIVE_EULER"), ("PHYSICAL_PROBLEM", None), ("PHYSICAL_PROBLEM", "NAVIER_STOKES"),
+    ("KIND_TURB_MODEL", "SA"), ("KIND_TURB_MODEL", "NONE"), ("KIND_TURB_MODEL", None),
+    ("NUM_METHOD_GRAD", "GREEN_GAUSS"), ("LINEAR_SOLVER", "BCGSTAB"), ("LINEAR_SOLVER", "RESTARTED_FGMRES"),
+    ("CONV_NUM_METHOD_FLOW", "ROE"), ("CONV_NUM_METHOD_FLOW", None), ("CONV_NUM_METHOD_TURB", "JST"),
+    ("SPATIAL_ORDER_TURB", "2ND_ORDER"), ("TIME_DISCRE_TURB", "EULER_EXPLICIT"),
+    ("UNSTEADY_SIMULATION", "DUAL_TIME_STEPPING-2ND_ORDER"), ("MATH_PROBLEM", "CONTINUOUS_ADJOINT")]
+
+
+def _jet_cfg(tmp_path):
+    from oracle import make_golden as MG
+    wd = MG.make_workdir("rej", MG.full_jet_writer, cfl=0.1, order="1ST_ORDER", case_dir=unpack(tmp_path / "files", "jet"),
+                         root=str(tmp_path))
+    return wd, open(os.path.join(wd, "case.cfg")).read()
+
+
+def _with_key(base, key, val):
+    lines = [ln for ln in base.splitlines() if ln.split("=")[0].strip() != key]
+    if val is not None:
+        lines.append(f"{key}= {val}")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("key,val", REJECTED)
+def test_case_from_cfg_rejects_unbuilt_physics(tmp_path, key, val):
+    """Each key selects a solver or numerics the reference has and this path does not build: rx_case_read refuses it
+    with RX_ERR_UNSUPPORTED (status 9) naming the key, instead of running something else (config_structure.cpp:622,
+    626, 979, 1030, 1047, 1147, 1160, 1189, 1195; driver_structure.cpp:795-822, 1517-1529)."""
+    wd, base = _jet_cfg(tmp_path)
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(_with_key(base, key, val))
+    with pytest.raises(rx.RxError, match=f"{key}.*status 9"):
+        rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+
+
+def test_case_from_cfg_keys_at_their_defaults_pass(tmp_path):
+    """Keys whose CConfig default is the built path may be left out (NUM_METHOD_GRAD, LINEAR_SOLVER,
+    CONV_NUM_METHOD_TURB, SPATIAL_ORDER_TURB, TIME_DISCRE_TURB, UNSTEADY_SIMULATION, MATH_PROBLEM), and
+    PHYSICAL_PROBLEM= REACTIVE_RANS names the same solver pair."""
+    wd, base = _jet_cfg(tmp_path)
+    txt = base
+    for key in ("NUM_METHOD_GRAD", "LINEAR_SOLVER", "CONV_NUM_METHOD_TURB", "SPATIAL_ORDER_TURB", "TIME_DISCRE_TURB",
+                "UNSTEADY_SIMULATION", "MATH_PROBLEM"):
+        txt = _with_key(txt, key, None)
+    txt = _with_key(txt, "PHYSICAL_PROBLEM", "REACTIVE_RANS")
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(txt)
+    rx.case_from_cfg(os.path.join(wd, "case.cfg"))["mesh"].close()
+
+
+def test_case_from_cfg_mach_follows_console_verbosity(tmp_path):
+    """mInfty (numerics_direct_reactive.cpp:19) is MACH_NUMBER unless the reactive solver's VERB_HIGH block runs
+    CConfig::SetMach (solver_direct_reactive.cpp:973; CONSOLE_OUTPUT_VERBOSITY default HIGH, config_structure.cpp:1384)."""
+    wd, base = _jet_cfg(tmp_path)
+    high = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    m_high = high["flow_cfg"]["mach_inf"]
+    high["mesh"].close()
+    for verb, mach, want in (("MEDIUM", "0.25", 0.25), ("NONE", None, 0.0)):
+        txt = _with_key(_with_key(base, "CONSOLE_OUTPUT_VERBOSITY", verb), "MACH_NUMBER", mach)
+        with open(os.path.join(wd, "case.cfg"), "w") as f:
+            f.write(txt)
+        case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+        assert case["flow_cfg"]["mach_inf"] == want and m_high not in (0.25, 0.0)
+        case["mesh"].close()
+
+
+def test_case_from_cfg_spline_at_the_table_end(tmp_path):
+    """FREESTREAM_TEMPERATURE equal to the tables' last temperature: the spline lookup of the free-stream c_p and
+    viscosities stays inside the table (the reference's GetSpline reads one past it there, spline.cpp:66-70) and
+    gives the tabulated end values."""
+    wd, base = _jet_cfg(tmp_path)
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    tmax = float(case["mech"]["mech_tab_x"][0, 0, -1])
+    case["mesh"].close()
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(_with_key(base, "FREESTREAM_TEMPERATURE", repr(tmax)))
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    m = case["mech"]
+    kv = rx.read_cfg(os.path.join(wd, "case.cfg"))
+    Y = [float(v) for v in kv["FREESTREAM_MASS_FRAC"].strip("()").split(",")]
+    vel = [float(v) for v in kv["FREESTREAM_VELOCITY"].strip("()").split(",")][:2]
+    M = m["mech_mmass"]
+    rgas = cp = mv2 = 0.0
+    for s in range(len(Y)):  # ComputeRgas / ComputeCP in species order, c_p at the table's last entry
+        rgas += Y[s] * (rx.R_UNGAS / M[s])
+    for s in range(len(Y)):
+        cp += Y[s] * (m["mech_tab_y"][0, s, -1] / M[s])
+    for v in vel:
+        mv2 += v * v
+    assert case["free_stream"]["T"] == tmax
+    assert case["flow_cfg"]["mach_inf"] == np.sqrt(mv2) / np.sqrt(cp / (cp - rgas) * rgas * tmax)
+    assert np.isfinite(case["bc"]["omega_inf"])
+    case["mesh"].close()
+
+
 def test_case_from_cfg_matches_the_reference_setup(tmp_path):
     """A cfg in the reference's grammar (the golden cases' cfg, oracle/make_golden.py CFG_TEMPLATE, with the
     reference's mesh and library files): markers, inlet kind, free-stream turbulence values and the solver knobs
