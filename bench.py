@@ -24,11 +24,14 @@ The preconditioner is partitioned like the reference run on `--parts` MPI ranks 
 local RCM per part, ILU(0) per rank; default 256 = one rank per CU); `--parts 1` is the serial
 reference.
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`, one rank per GPU): weak scaling by domain
-decomposition like the reference's MPI run. The global jet is N times taller (nx x ny*N points,
-parts*N partitions); every rank owns a contiguous block of `parts` partitions plus one halo layer
-(meshgen.shard) and exchanges halos over RCCL where the reference calls SendReceive / Set_MPI_*,
-with every FGMRES inner product and the RMS all-reduced (rx_comm_init). The first warm-up step runs
+Multi-GPU (`torch.distributed.run --nproc-per-node N`, one rank per GPU): domain decomposition like the reference's
+MPI run. `--scaling strong` (the default for c2 / c3: BASELINE configs[3], C4 = the 1M-point C3 jet split over the
+GPUs) keeps the global nx x ny mesh and splits it into parts*N partitions (parts per GPU, the N = 1 line's own
+partitioning at N = 1); `--scaling weak` (the default for c5, whose per-GPU slab stacks to the whole 1000x400x20 C5
+mesh at N = 8) makes the jet N times taller (nx x ny*N points, parts*N partitions). Every rank owns a contiguous
+block of `parts` partitions plus one halo layer (meshgen.shard) and exchanges halos over RCCL where the reference
+calls SendReceive / Set_MPI_*, with every FGMRES inner product and the RMS all-reduced (rx_comm_init; all-gather +
+rank-ordered sum). The first warm-up step runs
 eagerly and must give bitwise the RMS of the next (graph-replayed) one, else the graph is disabled.
 If the communicator cannot be set up, every rank falls back to an independent replica of the
 single-GPU workload and `config.parallelism` says so. Timing = max over ranks; value = all ranks'
@@ -122,9 +125,9 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         # RX_ILU_ROWWAVE=1): A in, the whole factor + inv(D) out
         "ILU_BUILD": (hbm((nnzb + (nnzb - N) // 2 + 2 * N) * blk, "k_ilu_build_grp" + tv) if ilu_grouped else
                       hbm((2 * nnzb + N) * blk, "k_ilu_build_part" + tv)),
-        # SOLVE phase (inside the FGMRES graph; timed one launch at a time after the timed region):
-        # y = A x: every block + its column index once, x gathered, y written
-        "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d, "k_spmv" + tv),
+        # SOLVE phase (inside the FGMRES graph; timed by an eager replay of one step after the timed region):
+        # FGMRES's w = A z (k_fg_spmv_full): every block + its column index once, z gathered, w written
+        "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d, "k_fg_spmv_full" + tv),
         # ILU(0) apply: L and U blocks + inv(D_i) (= nnzb blocks) + column indices, b in, x out
         "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, ilu_apply_kernels(N, nnzb, nVar, parts)),
     }
@@ -194,9 +197,11 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
 
 
 def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist, nz=0):
-    """Build the rank's shard of the N-times-taller jet and attach the RCCL communicator."""
+    """Build the rank's shard (strong: of the fixed nx x ny jet; weak: of the N-times-taller one) and attach the RCCL
+    communicator."""
     from tests.rxpkg import meshgen, synth
-    mesh, st, mech_arrays, kw = build_workload(nx, ny * world, ns, args.parts * world, nz)
+    gy = ny if args.scaling == "strong" else ny * world
+    mesh, st, mech_arrays, kw = build_workload(nx, gy, ns, args.parts * world, nz)
     sh = meshgen.shard(mesh, world, rank)
     st_l = {k: np.asarray(v)[sh["l2g"]] for k, v in st.items()}
     if args.cfl:
@@ -235,7 +240,12 @@ def main():
                     help="legacy step without boundary conditions and without the post-update Preprocessing")
     ap.add_argument("--cfl", type=float, default=0.0, help="CFL_NUMBER (default: the case's)")
     ap.add_argument("--breakdown", action="store_true", help="print per-phase times to stderr")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default=None,
+                    help="N > 1: strong = split the fixed mesh (default for c2 / c3: C4), weak = N-times-taller mesh "
+                         "(default for c5)")
     args = ap.parse_args()
+    if args.scaling is None:
+        args.scaling = "weak" if args.workload == "c5" else "strong"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -352,6 +362,7 @@ def main():
     s.sync()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    timed_its = list(lin_its[-args.steps:])
     if dist:
         dist.barrier()
         tel = torch.tensor([el], dtype=torch.float64)
@@ -360,19 +371,20 @@ def main():
     prof = {k: s.profile_read(k) for k in rx.K}
     tprof = {k: t.profile_read(k) for k in rx.K}
     prof = {k: (prof[k][0] + tprof[k][0], prof[k][1] + tprof[k][1]) for k in rx.K}
-    # the SOLVE phase's two HBM kernels one launch at a time (in the step they run inside the FGMRES graph): the
-    # flow system and ILU(0) factor of the last step, public rx_bsr_spmv / rx_ilu0_apply (plain SpMV; the graph's
-    # k_fg_spmv adds the MGS inner products)
+    s.profile(False)
+    t.profile(False)
+    # The SOLVE phase's kernels (inside the FGMRES graph in the timed steps, where no event can bracket them): one
+    # more step with the solve launched eagerly (RX_NO_GRAPH=1: the same kernels on the same stream, each in-solve
+    # ILU apply and k_fg_spmv_full bracketed by events, rx_krylov.hip), flow context only.
+    os.environ["RX_NO_GRAPH"] = "1"
     s.profile(True)
-    for _ in range(5):
-        s.spmv("RHS", "SOL")
-    for _ in range(5):
-        s.ilu0_apply("RHS", "SOL")
+    step()
     s.sync()
     for k in ("SPMV", "ILU_APPLY"):
         prof[k] = s.profile_read(k)
     s.profile(False)
-    t.profile(False)
+    if graph:
+        os.environ.pop("RX_NO_GRAPH", None)
 
     dims = f"{nx}x{ny}" + (f"x{nz}" if nz > 1 else "")
     wkey = f"{args.workload} {dims} ns{ns} parts{args.parts}"
@@ -402,9 +414,16 @@ def main():
 
     timed = [k for k in models if prof[k][1] > 0]
     kernels = {k: roof(k) for k in timed}
-    # dominant kernel: the longest average launch among the per-step phases (SPMV / ILU_APPLY are timed outside
-    # the step, above)
-    dom = max((k for k in timed if k not in ("SPMV", "ILU_APPLY")), key=lambda k: prof[k][0] / prof[k][1])
+    # GPU time per step of each single-kernel phase (SPMV / ILU_APPLY: average launch of the eager pass x launches per
+    # step, i.e. per linear iteration of the flow solve; ILU_APPLY is two kernels, the forward and backward sweeps)
+    its_mean = float(np.mean([a for a, _ in timed_its]))
+    for k in timed:
+        per = its_mean if k in ("SPMV", "ILU_APPLY") else prof[k][1] / args.steps
+        kernels[k]["ms_per_step"] = round(prof[k][0] / prof[k][1] * per, 4)
+    single = [k for k in timed if k != "ILU_APPLY"]
+    # dominant kernel: the most GPU time per step; the longest single launch beside it
+    dom = max(single, key=lambda k: kernels[k]["ms_per_step"])
+    longest = max((k for k in single if k != "SPMV"), key=lambda k: prof[k][0] / prof[k][1])
 
     if world > 1:
         tot = [None] * world
@@ -421,12 +440,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling if world == 1 or parallelism.startswith("sharded") else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference jet geometry; node records resampled from the reference PaSR jet state)",
         "config": {"workload": f"{args.workload}: {nDim}-D reactive jet {dims}" + (
-                       f" per GPU (global {nx}x{ny * world}" + (f"x{nz})" if nz > 1 else ")")
+                       (f" split over {world} GPUs (configs[3], C4)" if args.scaling == "strong" else
+                        f" per GPU (global {nx}x{ny * world}" + (f"x{nz})" if nz > 1 else ")"))
                        if parallelism.startswith("sharded") else ""),
                    "cells_per_gpu": n_owned, "halo_points": N - n_owned, "edges": E,
                    "species": ns, "nVar": ns + nDim + 2, "nnz_blocks": nnzb,
@@ -435,9 +455,10 @@ def main():
                    "linear_solver": f"FGMRES(5)+ILU0 (flow {ns + nDim + 2}x{ns + nDim + 2} and SST 2x2 systems)",
                    "partitions": args.parts,
                    "parallelism": parallelism, "solve_graph": graph, "cells_total": cells,
-                   "lin_iters_mean": float(np.mean([a for a, _ in lin_its[-args.steps:]])),
-                   "sst_lin_iters_mean": float(np.mean([b for _, b in lin_its[-args.steps:]]))},
+                   "lin_iters_mean": float(np.mean([a for a, _ in timed_its])),
+                   "sst_lin_iters_mean": float(np.mean([b for _, b in timed_its]))},
         "roofline": kernels[dom],
+        "roofline_longest_launch": kernels[longest],
         "roofline_edge_flux": kernels.get("CONV"),
         "roofline_kernels": kernels,
         "phase_ms_per_step": {k: round(v, 4) for k, v in phase_ms.items()},

@@ -63,7 +63,7 @@ class MeshDesc(C.Structure):
                 ("nbr_ptr", C.c_void_p), ("nbr", C.c_void_p), ("bvert", C.c_void_p), ("bvert_normal", C.c_void_p),
                 ("n_part", C.c_int64), ("part_ptr", C.c_void_p),
                 ("n_domain", C.c_int64), ("n_neigh", C.c_int32), ("neigh", C.c_void_p), ("send_ptr", C.c_void_p),
-                ("send_idx", C.c_void_p), ("recv_ptr", C.c_void_p)]
+                ("send_idx", C.c_void_p), ("recv_ptr", C.c_void_p), ("global_id", C.c_void_p)]
 
 
 SENDRECV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
@@ -217,9 +217,9 @@ def comm_unique_id() -> bytes:
 
 
 class TorchHostTransport:
-    """rx_host_comm over torch.distributed point-to-point and all_reduce (gloo on CPU tensors): the
-    reference's MPI_Isend/Irecv halo exchange and MPI_Allreduce, for ranks that cannot share RCCL
-    (several ranks on one GPU, CPU-side validation)."""
+    """rx_host_comm over torch.distributed point-to-point and all_gather (gloo on CPU tensors): the
+    reference's MPI_Isend/Irecv halo exchange and MPI_Allreduce (as a rank-ordered sum), for ranks that cannot
+    share RCCL (several ranks on one GPU, CPU-side validation)."""
 
     def __init__(self, group=None):
         import torch
@@ -247,10 +247,15 @@ class TorchHostTransport:
                 return 1
 
         def allreduce(user, inp, out, count):
+            # rx_host_comm's contract: the rank-ordered sum (all-gather, then ((in_0 + in_1) + in_2) + ...)
             try:
                 t = torch.from_numpy(np.ctypeslib.as_array(inp, shape=(count,)).copy())
-                dist.all_reduce(t, group=self.group)
-                np.ctypeslib.as_array(out, shape=(count,))[:] = t.numpy()
+                parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group=self.group))]
+                dist.all_gather(parts, t, group=self.group)
+                acc = parts[0].numpy().copy()
+                for p in parts[1:]:
+                    acc += p.numpy()
+                np.ctypeslib.as_array(out, shape=(count,))[:] = acc
                 return 0
             except Exception as e:
                 self.error = e
@@ -336,6 +341,8 @@ def mesh_desc(mesh):
         keep["neigh"] = np.ascontiguousarray(mesh["neigh"], dtype=np.int32)
         for k in ("send_ptr", "send_idx", "recv_ptr"):
             keep[k] = np.ascontiguousarray(mesh[k], dtype=np.int64)
+        if "l2g" in mesh:  # meshgen.shard: BSR rows in global column order (rx_mesh_desc.global_id)
+            keep["global_id"] = np.ascontiguousarray(mesh["l2g"], dtype=np.int64)
     md = MeshDesc()
     md.n_dim, md.n_point, md.n_edge = nDim, N, len(keep["edges"])
     md.n_bvert = len(keep["bvert"])

@@ -165,19 +165,32 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       adj[fill[e32[2 * e + 1]]++] = (int32_t)((e << 1) | 1);
     }
   }
-  // BSR: neighbours + diagonal, sorted (matrix_structure.cpp:113-201)
+  // BSR: neighbours + diagonal, sorted (matrix_structure.cpp:113-201) by local number, or by global number when the
+  // mesh carries it (a shard of a distributed mesh: the rows then sum in the undivided mesh's order). Either way a
+  // partition's columns form one run, in increasing local number (owned points keep the global order).
   ctx->h_rp.assign(N + 1, 0);
   std::vector<std::vector<int32_t>> rows(N);
+  const int64_t* gid = mesh->global_id;
+  auto key = [&](int32_t c) { return gid ? gid[c] : (int64_t)c; };
   for (int64_t i = 0; i < N; ++i) {
     rows[i].push_back((int32_t)i);
     for (int32_t k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
       const int e = adj[k] >> 1, side = adj[k] & 1;
       rows[i].push_back(e32[2 * e + (side ^ 1)]);
     }
-    std::sort(rows[i].begin(), rows[i].end());
+    std::sort(rows[i].begin(), rows[i].end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
     rows[i].erase(std::unique(rows[i].begin(), rows[i].end()), rows[i].end());
     ctx->h_rp[i + 1] = ctx->h_rp[i] + (int64_t)rows[i].size();
   }
+  if (gid) {  // owned points must be in increasing global order (partition runs stay contiguous and ascending)
+    for (int64_t i = 1; i < ctx->Nd; ++i)
+      if (gid[i] <= gid[i - 1]) CK(RX_ERR_ARG);
+  }
+  auto pos_in = [](const std::vector<int32_t>& r, int32_t c) -> int64_t {
+    for (size_t q = 0; q < r.size(); ++q)
+      if (r[q] == c) return (int64_t)q;
+    return -1;
+  };
   ctx->nnzb = ctx->h_rp[N];
   ctx->h_col.resize(ctx->nnzb);
   std::vector<int32_t> rp32(N + 1), col32(ctx->nnzb);
@@ -192,8 +205,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     for (int32_t k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
       const int e = adj[k] >> 1, side = adj[k] & 1;
       const int32_t o = e32[2 * e + (side ^ 1)];
-      const auto it = std::lower_bound(rows[i].begin(), rows[i].end(), o);
-      adj_blk[k] = ctx->h_rp[i] + (it - rows[i].begin());
+      adj_blk[k] = ctx->h_rp[i] + pos_in(rows[i], o);
       edge_blk[2 * e + side] = adj_blk[k];
     }
   }
@@ -217,9 +229,13 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     for (int64_t p = 0; p < np; ++p) {
       const int64_t lo = ctx->h_part_ptr[p], hi = ctx->h_part_ptr[p + 1];
       for (int64_t i = lo; i < hi; ++i) {
+        // the row's columns inside the partition: one run (see the BSR ordering above)
         const auto& r = rows[i];
-        klo[i] = (int32_t)(ctx->h_rp[i] + (std::lower_bound(r.begin(), r.end(), (int32_t)lo) - r.begin()));
-        khi[i] = (int32_t)(ctx->h_rp[i] + (std::lower_bound(r.begin(), r.end(), (int32_t)hi) - r.begin()));
+        size_t a = 0, b = r.size();
+        while (a < r.size() && !(r[a] >= lo && r[a] < hi)) ++a;
+        while (b > a && !(r[b - 1] >= lo && r[b - 1] < hi)) --b;
+        klo[i] = (int32_t)(ctx->h_rp[i] + (int64_t)a);
+        khi[i] = (int32_t)(ctx->h_rp[i] + (int64_t)b);
         rowmax = std::max(rowmax, khi[i] - klo[i]);
       }
     }
@@ -305,10 +321,9 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
             const int32_t j = col32[k];
             for (int32_t kk = (int32_t)diag[j] + 1; kk < khi[j]; ++kk) {
               const int32_t kp = col32[kk];
-              const auto& r = rows[i];
-              const auto it = std::lower_bound(r.begin(), r.end(), kp);
-              if (it != r.end() && *it == kp) {
-                const int32_t pos = (int32_t)(ctx->h_rp[i] + (it - r.begin()));
+              const int64_t q = pos_in(rows[i], kp);
+              if (q >= 0) {
+                const int32_t pos = (int32_t)(ctx->h_rp[i] + q);
                 if (pos >= klo[i] && pos < khi[i]) {
                   upd.push_back(kk);
                   upd.push_back(pos);

@@ -16,6 +16,8 @@
 
 namespace {
 
+constexpr int kGatherStride = 64;  // the widest all-reduce (the RMS columns): ctx->gather holds [nranks][<= 64]
+
 __global__ void k_pack(int64_t n, int stride, const int32_t* __restrict__ idx, const double* __restrict__ f,
                        double* __restrict__ out) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -25,7 +27,24 @@ __global__ void k_pack(int64_t n, int stride, const int32_t* __restrict__ idx, c
   out[t] = f[(int64_t)idx[k] * stride + c];
 }
 
+// out[c] = sum over ranks r = 0, 1, ... of g[r][c], added in rank order from rank 0's value: the all-reduce's
+// result is then a fixed function of the rank sums (the oracle's rank-split inner products restate it,
+// oracle/rx_oracle.cpp orc_dot), identical on every rank, independent of the collective's algorithm.
+__global__ void k_sum_ranks(int nranks, int count, const double* __restrict__ g, double* __restrict__ out) {
+  const int c = threadIdx.x;
+  if (c >= count) return;
+  double s = g[c];
+  for (int r = 1; r < nranks; ++r) s += g[(size_t)r * count + c];  // ncclAllGather: rank r's block at r * count
+  out[c] = s;
+}
+
 int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? RX_OK : RX_ERR_COMM; }
+
+int gather_alloc(rx_ctx* ctx) {
+  if (ctx->gather) return RX_OK;
+  RX_HIP(hipMalloc(&ctx->gather, sizeof(double) * (size_t)ctx->nranks * kGatherStride));
+  return RX_OK;
+}
 
 int stage_alloc(rx_ctx* ctx) {
   if (ctx->h_stage) return RX_OK;
@@ -78,10 +97,13 @@ int rx_la_exchange_on(rx_ctx* ctx, double* f, int stride, hipStream_t st) {
   return rc ? rc : rc2;
 }
 
+// dotProd's / SetResidual_RMS's MPI_Allreduce (vector_structure.cpp:397-419), as a rank-ordered sum: RCCL all-gather
+// of every rank's `count` sums, then k_sum_ranks; the host transport's allreduce callback has the same contract
+// (rx_host_comm, include/rx.h).
 int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count) {
   if (!ctx->distributed()) return RX_OK;
+  if (count > kGatherStride) return RX_ERR_ARG;
   if (ctx->has_hcomm) {
-    if (count > 64) return RX_ERR_ARG;
     double* h = ctx->h_stage + (ctx->n_send + (ctx->N - ctx->Nd)) * ctx->halo_stride;
     RX_HIP(hipMemcpyAsync(h, in, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
     RX_HIP(hipStreamSynchronize(ctx->stream));
@@ -89,8 +111,14 @@ int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count) {
     RX_HIP(hipMemcpyAsync(out, h, sizeof(double) * count, hipMemcpyHostToDevice, ctx->stream));
     return RX_OK;
   }
-  return nccl_rc(ncclAllReduce(in, out, (size_t)count, ncclDouble, ncclSum, static_cast<ncclComm_t>(ctx->comm),
-                               ctx->stream));
+  int rc = gather_alloc(ctx);
+  if (rc) return rc;
+  rc = nccl_rc(ncclAllGather(in, ctx->gather, (size_t)count, ncclDouble, static_cast<ncclComm_t>(ctx->comm),
+                             ctx->stream));
+  if (rc) return rc;
+  k_sum_ranks<<<1, 64, 0, ctx->stream>>>(ctx->nranks, count, ctx->gather, out);
+  RX_HIP(hipGetLastError());
+  return RX_OK;
 }
 
 namespace {
@@ -136,6 +164,7 @@ int rx_comm_init(rx_ctx* ctx, int nranks, int rank, const void* id128) {
   ctx->comm = comm;
   ctx->nranks = nranks;
   ctx->rank = rank;
+  if (int rc = gather_alloc(ctx)) return rc;  // before any graph capture
   // side stream of the overlapped gradient exchange (rx_grad_lsq)
   RX_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
   RX_HIP(hipEventCreateWithFlags(&ctx->comm_fork, hipEventDisableTiming));
@@ -180,6 +209,7 @@ int rx_comm_borrow(rx_ctx* ctx, const rx_ctx* from) {
     ctx->has_hcomm = true;
   }
   ctx->n_global = from->n_global;
+  if (!ctx->has_hcomm && ctx->comm) return gather_alloc(ctx);  // the SST solve graph all-reduces through it
   return RX_OK;
 }
 
@@ -191,6 +221,8 @@ void rx_comm_free(rx_ctx* ctx) {
     (void)hipEventDestroy(ctx->comm_join);
     ctx->comm_stream = nullptr;
   }
+  if (ctx->gather) (void)hipFree(ctx->gather);
+  ctx->gather = nullptr;
   if (ctx->comm && ctx->comm_owned) (void)ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
   ctx->comm = nullptr;
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);

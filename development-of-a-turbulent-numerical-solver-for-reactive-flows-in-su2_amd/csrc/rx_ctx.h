@@ -42,6 +42,7 @@ struct rx_ctx {
   rx_host_comm hcomm{};
   double* h_stage = nullptr;    // pinned [(n_send + N - Nd) * halo_stride + 64]
   int nranks = 1, rank = 0;
+  double* gather = nullptr;     // RCCL all-reduce: [nranks][64] all-gathered rank sums, added in rank order
   bool distributed() const { return comm != nullptr || has_hcomm; }
   // compute / communication overlap of the primitive-gradient exchange (rx_grad_lsq): the owned points
   // the neighbours need first (n_grad_bnd of them), then the rest while the exchange runs on comm_stream

@@ -564,7 +564,10 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
   if ((rc = reduce())) return rc;
   k_fg_start_div<<<nb, kBlock, 0, st>>>(n, s, W(0));
   for (int i = 0; i < m; ++i) {
+    // RxPhase records only outside a graph capture: an eager solve (RX_NO_GRAPH=1, bench.py's kernel-timing pass)
+    // times the in-solve ILU applies and SpMVs themselves
     if (ctx->cfg.lin_prec == 1) {
+      RxPhase ph(ctx, RX_K_ILU_APPLY);
       if ((rc = rx_la_ilu_apply(ctx, W(i), Z(i), &s->done, &s->conv))) return rc;
     } else {
       if ((rc = rx_la_lusgs(ctx, A, W(i), Z(i), &s->done, &s->conv))) return rc;
@@ -576,6 +579,7 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
       RX_NV_SWITCH(ctx->nVar, (k_fg_spmv<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, Z(i),
                                                                              W(0), W(i + 1), part, s, dist)));
     } else {
+      RxPhase ph(ctx, RX_K_SPMV);
       RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_full<NV_><<<blocks(n), kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A,
                                                                                  Z(i), W(i + 1), s)));
       k_fg_spmv_dots<<<kRedBlocks, kBlock, 0, st>>>(n, W(0), W(i + 1), part, s, dist);

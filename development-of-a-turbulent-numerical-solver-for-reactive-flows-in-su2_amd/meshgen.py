@@ -412,10 +412,17 @@ def shard(mesh, n_ranks: int, rank: int):
     partitioned CGeometry (geometry_structure.cpp:11465-11530: domain points, then halo points).
 
     Local numbering: own points in global order, then halo points in global order (so the halo is
-    contiguous per owning rank). Local edges: every global edge with an own endpoint, oriented low ->
-    high local id (normal negated when the orientation flips), sorted by (i, j). LSQ neighbour lists of
-    own points keep the global order; halo points keep only their local neighbours (their gradients
-    are overwritten by the halo exchange). Returns the local mesh dict plus the exchange plan
+    contiguous per owning rank). Local edges: every global edge with an own endpoint, in the global edge
+    order and orientation (an edge whose halo end has the lower local id keeps its global direction).
+    LSQ neighbour lists of own points keep the global order; halo points keep only their local neighbours
+    (their gradients are overwritten by the halo exchange). `l2g` (the global point numbers) also orders
+    each BSR row by global column (rx_mesh_desc.global_id). So every owned point gathers the same
+    contributions in the same order as the undivided mesh: the rank's residual, Jacobian rows, gradient,
+    limiter, time step and SpMV rows are bitwise the single-context ones, and only the inner products
+    (rank-local partial sums, then the rank-ordered sum) differ.
+    The reference's own MPI ranks renumber edges and matrix columns locally (SetEdges / CSysMatrix on the
+    rank's CGeometry), which changes rounding but no formula; keeping the global order makes the sharded
+    iteration checkable against the undivided oracle. Returns the local mesh dict plus the exchange plan
     (`neigh`, `send_ptr`, `send_idx`, `recv_ptr`, `n_domain`) and `l2g`.
     """
     pp = np.asarray(mesh["part_ptr"], dtype=np.int64)
@@ -434,12 +441,7 @@ def shard(mesh, n_ranks: int, rank: int):
     g2l = np.full(int(pp[-1]), -1, dtype=np.int64)
     g2l[l2g] = np.arange(len(l2g))
     le = g2l[e[own_e]]
-    ln = np.asarray(mesh["edge_normal"])[own_e].copy()
-    flip = le[:, 0] > le[:, 1]
-    le[flip] = le[flip][:, ::-1]
-    ln[flip] *= -1.0
-    o = np.lexsort((le[:, 1], le[:, 0]))
-    le, ln = le[o], ln[o]
+    ln = np.ascontiguousarray(np.asarray(mesh["edge_normal"])[own_e])
     # LSQ neighbours
     nptr_g, nbr_g = np.asarray(mesh["nbr_ptr"]), np.asarray(mesh["nbr"])
     cnt = nptr_g[l2g + 1] - nptr_g[l2g]

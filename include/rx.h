@@ -32,7 +32,8 @@
  *   V   [N][nPrimVar]  T, u, v, P, rho, h, a, Y_1..Y_Ns   (nPrimVar = Ns + nDim + 5)
  *   U   [N][nVar]      rho, rho u, rho v, rho E, rho Y_s   (nVar = Ns + nDim + 2)
  *   grad[N][nPrimVarGrad][nDim]  T, u, v, P, X_1..X_Ns    (nPrimVarGrad = Ns + nDim + 2)
- *   Dij [N][Ns][Ns], BSR blocks [nnzb][nVar][nVar] row-major, columns sorted per row, diagonal included.
+ *   Dij [N][Ns][Ns], BSR blocks [nnzb][nVar][nVar] row-major, columns sorted per row (local number, or global
+ *   number with rx_mesh_desc.global_id), diagonal included.
  */
 #ifndef RX_H
 #define RX_H
@@ -102,6 +103,12 @@ typedef struct {
   const int64_t *send_ptr;   /* [n_neigh+1] */
   const int64_t *send_idx;   /* [send_ptr[n_neigh]] local owned point ids */
   const int64_t *recv_ptr;   /* [n_neigh+1] offsets into the halo block */
+  /* Distributed mesh, optional: the global number of every local point [n_point] (owned points in increasing
+   * global order). When given, each BSR row holds its blocks in increasing global column (rx_bsr_pattern then
+   * returns that order) and the caller's local edges keep the global edge order and orientation, so an owned
+   * row's residual, Jacobian and SpMV sums run in the undivided mesh's order (meshgen.shard). NULL: columns in
+   * increasing local number, as a reference rank's own CSysMatrix (matrix_structure.cpp:113-201). */
+  const int64_t *global_id;
 } rx_mesh_desc;
 
 typedef struct {
@@ -190,7 +197,9 @@ int rx_comm_init(rx_ctx *ctx, int nranks, int rank, const void *id128);
  *   sendrecv: for every neighbour k, send points [send_ptr[k], send_ptr[k+1]) of `send` (stride
  *             doubles each) to rank neigh[k] and receive points [recv_ptr[k], recv_ptr[k+1]) of
  *             `recv` from it.
- *   allreduce: out[i] = sum over ranks of in[i], i < count (in == out allowed).
+ *   allreduce: out[i] = sum over ranks of in[i], i < count (in == out allowed), added in rank order starting from
+ *             rank 0's value (((in_0 + in_1) + in_2) + ...), as the RCCL path does (all-gather, then the ordered
+ *             sum): every rank gets the same doubles, and the result is a fixed function of the rank sums.
  * Both return 0 on success. */
 typedef struct {
   void *user;

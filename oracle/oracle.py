@@ -209,17 +209,23 @@ def bsr_spmv(rp, col, A, x):
 
 class dot_order:
     """Context manager: FGMRES inner products in the device's reduction order (mode "device") instead
-    of the reference's sequential sum (mode "reference", the default)."""
+    of the reference's sequential sum (mode "reference", the default). ranks (device mode): the row pointer
+    [R+1] of a distributed run's ranks (meshgen.shard rank_ptr): each rank's partial over its own rows in the
+    device order, then the rank-ordered sum of the all-reduce (rx_comm.hip k_sum_ranks)."""
 
-    def __init__(self, mode="device"):
+    def __init__(self, mode="device", ranks=None):
         self.mode = 1 if mode == "device" else 0
+        self.ranks = None if ranks is None else np.ascontiguousarray(ranks, dtype=np.int64)
 
     def __enter__(self):
         lib().orc_set_dot_mode(C.c_int(self.mode))
+        if self.ranks is not None:
+            lib().orc_set_dot_ranks(C.c_int64(len(self.ranks) - 1), self.ranks.ctypes.data_as(C.c_void_p))
         return self
 
     def __exit__(self, *a):
         lib().orc_set_dot_mode(C.c_int(0))
+        lib().orc_set_dot_ranks(C.c_int64(0), None)
 
 
 def _parts(N, part_ptr):

@@ -1839,14 +1839,35 @@ void orc_ilu_apply(int64_t N, int nb, const int64_t* rp, const int64_t* col, con
 // a sequential sum. Mode 1: the summation order of the device kernels (rx_krylov.hip k_dot_part /
 // k_dot_fin: 512 x 256 grid-stride partial sums, pairwise tree in each block, then a pairwise tree
 // over the 512 partials) — lets tests separate algorithmic parity (bitwise) from reduction order.
+// Mode 1 with rank splits (orc_set_dot_ranks): the distributed device solve (rx_comm.hip), one context per rank
+// owning the rows [rank_ptr[r], rank_ptr[r+1]): each rank's partial in the device order over its own rows, then
+// the rank-ordered sum of the all-reduce (k_sum_ranks / rx_host_comm: ((p_0 + p_1) + p_2) + ...).
 static int g_dot_mode = 0;
+static std::vector<int64_t> g_dot_ranks;
 void orc_set_dot_mode(int mode) { g_dot_mode = mode; }
+void orc_set_dot_ranks(int64_t nr, const int64_t* row_ptr) {
+  g_dot_ranks.assign(row_ptr ? row_ptr : nullptr, row_ptr ? row_ptr + nr + 1 : nullptr);
+}
+static double dot_device(int64_t n, const double* a, const double* c);
 double orc_dot(int64_t n, const double* a, const double* c) {
   if (g_dot_mode == 0) {
     double s = 0.0;
     for (int64_t q = 0; q < n; ++q) s += a[q] * c[q];
     return s;
   }
+  if (g_dot_ranks.size() >= 2 && g_dot_ranks.back() > 0 && n % g_dot_ranks.back() == 0) {
+    const int64_t nb = n / g_dot_ranks.back();
+    double s = 0.0;
+    for (size_t r = 0; r + 1 < g_dot_ranks.size(); ++r) {
+      const int64_t q0 = g_dot_ranks[r] * nb, q1 = g_dot_ranks[r + 1] * nb;
+      const double p = dot_device(q1 - q0, a + q0, c + q0);
+      s = r == 0 ? p : s + p;
+    }
+    return s;
+  }
+  return dot_device(n, a, c);
+}
+static double dot_device(int64_t n, const double* a, const double* c) {
   const int NB = 512, BS = 256;
   std::vector<double> part(NB), sh(BS);
 #pragma omp parallel for schedule(static) firstprivate(sh)

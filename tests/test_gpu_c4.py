@@ -1,0 +1,64 @@
+"""BASELINE configs[3] (C4): the 1M-point C3 jet (2000 x 500, 7 species, PaSR + SST, 256 partitions) decomposed over 8
+ranks, as `bench.py --gpus 8` runs it (strong scaling: 125 000 owned points per rank, 32 partitions each, one halo
+layer; meshgen.shard). The 8 ranks share the test box's one MI355X through the host-staged transport over gloo
+(tests/shard_run.py; RCCL refuses two ranks on one device and runs the same exchange plan and rank-ordered
+all-reduce). Reference: CMeanFlowIteration::Iterate (iteration_structure.cpp:486-560) on 8 MPI ranks of a
+partitioned CGeometry (geometry_structure.cpp:11465-11530).
+
+- EULER_EXPLICIT (CFL 0.5, LU_SGS SST): one outer iteration on 8 ranks against one context on the undivided mesh:
+  U and both RMS vectors within 1e-10 (the flow update has no inner product: bitwise expected), (k, omega) within
+  1e-10 (its FGMRES sums inner products in the ranks' order).
+- EULER_IMPLICIT (the bench step, FGMRES(5) + ILU0, CFL 5): one outer iteration on 8 ranks against the CPU oracle's
+  O.outer_iteration on the same global mesh and partitions, inner products in the ranks' order, at 1e-10 (U per
+  column, species elementwise, momentum, (k, omega), both RMS vectors, identical linear-iteration counts).
+- Every rank's start-up records bitwise equal to one context's; halo rows equal their owners' rows."""
+import numpy as np
+import pytest
+
+from tests.oracle_inputs import outer_iteration_inputs
+from tests.parity import assert_close, per_column_close
+from tests.rxpkg import rx, synth
+from tests.shard_run import NS, gather, run_ranks, write_shards
+from tests.test_gpu_shard_iterate import check_preprocessing, check_vs_oracle, single_context
+
+pytestmark = pytest.mark.gpu
+
+NX, NY, PARTS, WORLD = 2000, 500, 256, 8
+
+
+@pytest.mark.timeout(1200)
+def test_c4_explicit_vs_one_context(tmp_path):
+    mesh, st0, mech, kw = synth.jet_field_case(NX, NY, n_species=NS, n_part=PARTS)
+    s, t, st, cfg, bc = single_context(mesh, st0, mech, kw, 0, 0.5)
+    U_init = s.download("U").reshape(s.N, -1)
+    rms, rms_t, its0 = rx.Iterate(s, t, ext_iter=0)
+    s.sync()
+    U0, T0 = s.download("U").reshape(s.N, -1), t.download("U").reshape(s.N, 2)
+    s.close()
+    write_shards(tmp_path, mesh, st0, mech, kw, WORLD)
+    res = run_ranks(tmp_path, WORLD, 0, 1, 0.5)
+    U, T, pre = gather(res, len(U0), U0.shape[1])
+    check_preprocessing(pre, st, "C4 explicit")
+    for r, d in res.items():
+        assert np.array_equal(d["hist"][0][0], res[0]["hist"][0][0]), f"rank {r}: RMS differs across ranks"
+        assert tuple(d["hist"][0][1]) == tuple(its0)
+    assert_close(res[0]["hist"][0][0], np.r_[rms, rms_t], rtol=1e-10, what="C4 explicit: RMS vs one context")
+    eU = per_column_close(U - U_init, U0 - U_init, rtol=1e-10, floor=1e-14, what="C4 explicit: dU vs one context")
+    eT = per_column_close(T, T0, rtol=1e-10, floor=1e-14, what="C4 explicit: (k, omega) vs one context")
+    print(f"C4 explicit x{WORLD}: dU {eU:.2e} (bitwise {np.array_equal(U, U0)}), (k, omega) {eT:.2e}")
+
+
+@pytest.mark.timeout(1200)
+def test_c4_implicit_vs_oracle(tmp_path):
+    mesh, st0, mech, kw = synth.jet_field_case(NX, NY, n_species=NS, n_part=PARTS)
+    s, t, st, cfg, bc = single_context(mesh, st0, mech, kw, 1, 5.0)
+    s.close()
+    _, state, _, _ = outer_iteration_inputs(mesh, st, cfg, bc)
+    shards = write_shards(tmp_path, mesh, st0, mech, kw, WORLD, tg=state["TG"])
+    assert [sh["n_domain"] for sh in shards] == [NX * NY // WORLD] * WORLD
+    res = run_ranks(tmp_path, WORLD, 1, 1, 5.0)
+    U, T, pre = gather(res, len(st["V"]), st["U"].shape[1])
+    check_preprocessing(pre, st, "C4 implicit")
+    for r, d in res.items():
+        assert np.array_equal(d["hist"][0][0], res[0]["hist"][0][0]), f"rank {r}: RMS differs across ranks"
+    check_vs_oracle(mesh, mech, st, cfg, bc, shards[0]["rank_ptr"], U, T, res[0]["hist"], 2, f"C4 implicit x{WORLD}")

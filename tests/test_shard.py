@@ -59,8 +59,10 @@ def test_owned_residual_matches_global(R):
         np.add.at(R_loc, s["edges"][:, 0], rcl)
         np.add.at(R_loc, s["edges"][:, 1], -rcl)
         ref = R_glob[s["l2g"][:nd]]
-        # flipped edges and a different gather order: agreement to rounding
-        assert np.max(np.abs(R_loc[:nd] - ref)) <= 1e-12 * np.abs(ref).max()
+        # local edges keep the global order and orientation: every owned point adds the same fluxes in the same
+        # order, bitwise
+        assert np.array_equal(R_loc[:nd], ref)
+        assert np.array_equal(s["l2g"][s["edges"]], mesh["edges"][np.isin(mesh["edges"], s["l2g"][:nd]).any(axis=1)])
 
 
 def _exchange_worker(rank, world, port, R_nx, q):
@@ -108,3 +110,69 @@ def test_halo_exchange_gloo_world2():
     for p in ps:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _allreduce_worker(rank, world, port, q):
+    import ctypes as C
+
+    import torch.distributed as dist
+
+    from tests.rxpkg import rx
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = rx.TorchHostTransport()
+        # rank sums whose total depends on the addition order: ((1e16 + 1) + -1e16) + 1 = 1 in rank order,
+        # 2 in exact arithmetic, 0 or 1 in other orders
+        vals = {0: [1e16, 3.0], 1: [1.0, 0.5], 2: [-1e16, 0.25], 3: [1.0, 0.125]}[rank]
+        a = np.array(vals)
+        out = np.zeros(2)
+        rc = t._cb[1](None, a.ctypes.data_as(C.POINTER(C.c_double)), out.ctypes.data_as(C.POINTER(C.c_double)), 2)
+        q.put((rank, (rc, out.tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_transport_allreduce_is_rank_ordered():
+    """rx_host_comm's all-reduce contract (include/rx.h): the rank-ordered sum ((in_0 + in_1) + in_2) + ..., the same
+    doubles on every rank, as the RCCL path's all-gather + k_sum_ranks; the oracle's rank-split inner products
+    (O.dot_order("device", ranks=...)) restate it."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_allreduce_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    want = [((1e16 + 1.0) + -1e16) + 1.0, ((3.0 + 0.5) + 0.25) + 0.125]
+    for r in range(4):
+        assert res[r] == (0, want), res[r]
+
+
+def test_oracle_rank_split_dot():
+    """O.dot_order("device", ranks=rank_ptr): each rank's rows in the device's reduction order, then the rank-ordered
+    sum; a single rank is the plain device order."""
+    rng = np.random.default_rng(3)
+    nb, rp = 3, np.array([0, 700, 1500, 2300], dtype=np.int64)
+    a, c = rng.normal(size=rp[-1] * nb), rng.normal(size=rp[-1] * nb)
+    L = O.lib()
+    with O.dot_order("device"):
+        dev = [L.orc_dot(C_i64(q1 - q0), O._p(a[q0:q1]), O._p(c[q0:q1])) for q0, q1 in zip(rp[:-1] * nb, rp[1:] * nb)]
+        whole = L.orc_dot(C_i64(len(a)), O._p(a), O._p(c))
+    with O.dot_order("device", ranks=rp):
+        split = L.orc_dot(C_i64(len(a)), O._p(a), O._p(c))
+    with O.dot_order("device", ranks=np.array([0, rp[-1]])):
+        one = L.orc_dot(C_i64(len(a)), O._p(a), O._p(c))
+    assert split == (dev[0] + dev[1]) + dev[2] and one == whole
+
+
+def C_i64(v):
+    import ctypes as C
+    return C.c_int64(int(v))
