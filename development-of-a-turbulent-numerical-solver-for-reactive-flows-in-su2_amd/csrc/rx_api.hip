@@ -284,7 +284,17 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         slot[4 * r + 2] = (int32_t)diag[i];
         slot[4 * r + 3] = khi[i];
       }
-      int rc2 = dupload(ctx, &S.part_lvl, part_lvl.data(), part_lvl.size());
+      // passes of <= 64 rows within one level (the one-wavefront 2x2 kernels, rx_sweeps.hip)
+      std::vector<int32_t> pass_lo, part_pass(np + 1, 0);
+      for (int64_t p = 0; p < np; ++p) {
+        for (int32_t l = part_lvl[p]; l < part_lvl[p + 1]; ++l)
+          for (int32_t b = lvl_ptr[l]; b < lvl_ptr[l + 1]; b += 64) pass_lo.push_back(b);
+        part_pass[p + 1] = (int32_t)pass_lo.size();
+      }
+      pass_lo.push_back((int32_t)order.size());
+      int rc2 = dupload(ctx, &S.pass_lo, pass_lo.data(), pass_lo.size());
+      if (!rc2) rc2 = dupload(ctx, &S.part_pass, part_pass.data(), part_pass.size());
+      if (!rc2) rc2 = dupload(ctx, &S.part_lvl, part_lvl.data(), part_lvl.size());
       if (!rc2) rc2 = dupload(ctx, &S.lvl_ptr, lvl_ptr.data(), lvl_ptr.size());
       if (!rc2) rc2 = dupload(ctx, &S.rows, order.data(), order.size());
       if (!rc2) rc2 = dupload(ctx, &S.slot, slot.data(), slot.size());
@@ -451,6 +461,20 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       for (int64_t i = 0; i < ctx->Nd; ++i)
         if (!sent[i]) gl.push_back((int32_t)i);
       CK(dupload(ctx, &ctx->grad_list, gl.data(), gl.size()));
+    }
+    {  // SpMV rows: interior (no halo column) first, then the rows on the rank boundary
+      std::vector<int32_t> rl;
+      rl.reserve(ctx->Nd);
+      std::vector<char> bnd(ctx->Nd, 0);
+      for (int64_t i = 0; i < ctx->Nd; ++i)
+        for (int64_t k = ctx->h_rp[i]; k < ctx->h_rp[i + 1]; ++k)
+          if (ctx->h_col[k] >= ctx->Nd) bnd[i] = 1;
+      for (int64_t i = 0; i < ctx->Nd; ++i)
+        if (!bnd[i]) rl.push_back((int32_t)i);
+      ctx->n_spmv_int = (int64_t)rl.size();
+      for (int64_t i = 0; i < ctx->Nd; ++i)
+        if (bnd[i]) rl.push_back((int32_t)i);
+      CK(dupload(ctx, &ctx->spmv_rows, rl.data(), rl.size()));
     }
     // the widest exchangeable node record: D_ij (Ns^2), the primitive gradient (nG x nDim) or V (nPV)
     ctx->halo_stride = std::max({kHaloMaxStride, ctx->ns * ctx->ns, ctx->nG * ctx->nDim, ctx->nPV});
@@ -662,7 +686,8 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
-                  ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->grad_list, ctx->sendbuf, ctx->rms_sum,
+                  ctx->fs.pass_lo, ctx->fs.part_pass, ctx->bs.pass_lo, ctx->bs.part_pass,
+                  ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->grad_list, ctx->spmv_rows, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,
                   ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};

@@ -48,6 +48,11 @@ struct rx_ctx {
   // the neighbours need first (n_grad_bnd of them), then the rest while the exchange runs on comm_stream
   int32_t* grad_list = nullptr; // [Nd]
   int64_t n_grad_bnd = 0;
+  // SpMV rows of a distributed context: owned rows with only owned columns first (n_spmv_int of them), then the rows
+  // that read halo columns; FGMRES computes the first set while the preconditioned vector's halo is exchanged
+  int32_t* spmv_rows = nullptr; // [Nd]
+  int64_t n_spmv_int = 0;
+  bool defer_exchange = false;  // the preconditioner apply leaves its closing halo exchange to the caller
   hipStream_t comm_stream = nullptr;  // RCCL transport only
   hipEvent_t comm_fork = nullptr, comm_join = nullptr;
   int64_t n_global = 0;         // owned points over all ranks
@@ -97,6 +102,8 @@ struct rx_ctx {
     int32_t* lvl_ptr = nullptr;
     int32_t* rows = nullptr;
     int32_t* slot = nullptr;      // [rows][4] {row, klo, diag, khi} in schedule order
+    int32_t* pass_lo = nullptr;   // [npass + 1] schedule positions of the passes: <= 64 rows of one level each
+    int32_t* part_pass = nullptr; // [npart + 1] each partition's passes
     int nlevels = 0, maxwidth = 0, maxlev = 0;  // maxlev: most levels of one partition
   } fs, bs;
   double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)

@@ -515,6 +515,14 @@ __global__ __launch_bounds__(kBlock) void k_muscl_edge(int E, const int32_t* __r
 // reference's operation order per entry. The 16 edges of a wavefront own one contiguous scratch range
 // ([e][Ji|Jj], edge-major), so Ji and then Jj of the 16 edges are staged in LDS and stored as whole
 // 512-byte rows (full cache lines).
+// RX_AUSM_STAGE (build knob): 2 = both Jacobians staged through LDS (Jj held in registers while
+// Ji is stored: 201 VGPRs, 2 waves per SIMD); 1 = Ji staged, Jj stored straight from the lane (no register copy);
+// 0 = both stored straight from the lanes (no LDS). A team's four lanes write four consecutive doubles of a block row,
+// so a direct store instruction writes sixteen 32-byte runs, and every byte of the edge's two blocks is written by
+// the same wavefront within a few hundred cycles (the L2 merges the partial lines).
+#ifndef RX_AUSM_STAGE
+#define RX_AUSM_STAGE 2
+#endif
 constexpr int kAusmTeam = 4;
 constexpr int kAusmBlock = 128;
 template <int NS, int NDIM>
@@ -529,7 +537,8 @@ __global__ __launch_bounds__(kAusmBlock) RX_WPE_AUSM void k_ausm_edge(int E, con
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5, nVar2 = nVar * nVar;
   constexpr int CPL = (nVar + kAusmTeam - 1) / kAusmTeam;
   constexpr int EW = 64 / kAusmTeam;
-  __shared__ double stage[kAusmBlock / 64][EW * nVar2];
+  constexpr int kStage = RX_AUSM_STAGE;
+  __shared__ double stage[kAusmBlock / 64][kStage ? EW * nVar2 : 1];
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63, k = lane / kAusmTeam, t = lane % kAusmTeam;
   const int e0 = (gt >> 6) * EW;  // first edge of this wavefront
@@ -556,7 +565,8 @@ __global__ __launch_bounds__(kAusmBlock) RX_WPE_AUSM void k_ausm_edge(int E, con
   AusmEdge s;
   ausm_scalars<NDIM>(Vi, Vj, nrm, mInfty, s);
   bool bad = false;
-  double jjr[CPL][nVar];
+  double jjr[kStage == 2 ? CPL : 1][nVar];
+  double* Jd = Jac + (size_t)ee * 2 * nVar2;  // this lane's edge (direct stores)
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int b = t + kAusmTeam * c;
@@ -578,22 +588,28 @@ __global__ __launch_bounds__(kAusmBlock) RX_WPE_AUSM void k_ausm_edge(int E, con
         ausm_jac_entry<NDIM>(s, col, ausm_phi<NDIM>(Vi, Vi[NDIM + 3], a), ausm_phi<NDIM>(Vj, Vj[NDIM + 3], a), sib,
                              sjb, a, b, &ji, &jj);
         bad |= isnan(ji) || isnan(jj);
-        sj[k * nVar2 + a * nVar + b] = ji;
-        jjr[c][a] = jj;
+        if (kStage) sj[k * nVar2 + a * nVar + b] = ji;
+        else if (live) Jd[a * nVar + b] = ji;
+        if (kStage == 2) jjr[c][a] = jj;
+        else if (live) Jd[nVar2 + a * nVar + b] = jj;
       }
     }
+  }
+  if (kStage == 0) {
+    if (live && bad) set_err(err, ERR_NAN, e);
+    return;
   }
   const int ne = min(EW, E - e0);
   double* Jo = Jac + (size_t)e0 * 2 * nVar2;
 #pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    if (side) {
+  for (int side = 0; side < (kStage == 2 ? 2 : 1); ++side) {
+    if (side && kStage == 2) {
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         const int b = t + kAusmTeam * c;
         if (b < nVar)
 #pragma unroll
-          for (int a = 0; a < nVar; ++a) sj[k * nVar2 + a * nVar + b] = jjr[c][a];
+          for (int a = 0; a < nVar; ++a) sj[k * nVar2 + a * nVar + b] = jjr[kStage == 2 ? c : 0][a];
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -227,6 +227,21 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv_full(int Nd, const int32_t* 
   if (q < (int64_t)Nd * NV) w[q] = spmv_elem<NV>(q, rp, col, A, z);
 }
 
+// k_fg_spmv_full over a row list (rows[0..n)): the same element arithmetic at the same positions. A distributed
+// solve computes the rows without halo columns while the preconditioned vector's halo is in flight, then the rest.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_fg_spmv_rows(int n, const int32_t* __restrict__ rows,
+                                                         const int32_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                         const double* __restrict__ A, const double* __restrict__ z,
+                                                         double* __restrict__ w, const KState* __restrict__ s) {
+  if (s->done) return;
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (int64_t)n * NV) return;
+  const int r = (int)(t / NV), a = (int)(t - (int64_t)r * NV);
+  const int64_t q = (int64_t)rows[r] * NV + a;
+  w[q] = spmv_elem<NV>(q, rp, col, A, z);
+}
+
 // |w_{i+1}|^2 -> dotn and <w_{i+1}, w_0> -> dot over the stored product, in k_fg_spmv's grid-stride order (each
 // thread sums the same elements in the same order, then the same fixed trees): bitwise k_fg_spmv's sums.
 __global__ __launch_bounds__(kBlock) void k_fg_spmv_dots(int64_t n, const double* __restrict__ w0,
@@ -566,11 +581,49 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
   for (int i = 0; i < m; ++i) {
     // RxPhase records only outside a graph capture: an eager solve (RX_NO_GRAPH=1, bench.py's kernel-timing pass)
     // times the in-solve ILU applies and SpMVs themselves
+    // distributed: the preconditioner's closing halo exchange of z_i (SendReceive_Solution, matrix_structure.cpp:
+    // 1513 / :1707) overlaps the SpMV rows that read no halo column (on comm_stream with RCCL)
+    const bool split = dist && ctx->spmv_rows && !getenv("RX_NO_SPMV_SPLIT");
+    ctx->defer_exchange = split;
     if (ctx->cfg.lin_prec == 1) {
       RxPhase ph(ctx, RX_K_ILU_APPLY);
-      if ((rc = rx_la_ilu_apply(ctx, W(i), Z(i), &s->done, &s->conv))) return rc;
+      rc = rx_la_ilu_apply(ctx, W(i), Z(i), &s->done, &s->conv);
     } else {
-      if ((rc = rx_la_lusgs(ctx, A, W(i), Z(i), &s->done, &s->conv))) return rc;
+      rc = rx_la_lusgs(ctx, A, W(i), Z(i), &s->done, &s->conv);
+    }
+    ctx->defer_exchange = false;
+    if (rc) return rc;
+    if (split) {
+      const bool overlap = ctx->comm_stream != nullptr && !ctx->has_hcomm;
+      if (overlap) {
+        RX_HIP(hipEventRecord(ctx->comm_fork, st));
+        RX_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->comm_fork, 0));
+        if ((rc = rx_la_exchange_on(ctx, Z(i), ctx->nVar, ctx->comm_stream))) return rc;
+        RX_HIP(hipEventRecord(ctx->comm_join, ctx->comm_stream));
+      } else if ((rc = rx_la_exchange(ctx, Z(i), ctx->nVar))) {
+        return rc;
+      }
+      const int ni = (int)ctx->n_spmv_int, nb_rows = (int)(ctx->Nd - ctx->n_spmv_int);
+      {
+        RxPhase ph(ctx, RX_K_SPMV);
+        if (ni > 0)
+          RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)ni * NV_), kBlock, 0, st>>>(
+                                      ni, ctx->spmv_rows, ctx->rp, ctx->col, A, Z(i), W(i + 1), s)));
+        if (overlap) RX_HIP(hipStreamWaitEvent(st, ctx->comm_join, 0));
+        if (nb_rows > 0)
+          RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)nb_rows * NV_), kBlock, 0, st>>>(
+                                      nb_rows, ctx->spmv_rows + ni, ctx->rp, ctx->col, A, Z(i), W(i + 1), s)));
+      }
+      k_fg_spmv_dots<<<kRedBlocks, kBlock, 0, st>>>(n, W(0), W(i + 1), part, s, dist);
+      if ((rc = reduce())) return rc;
+      for (int k = 0; k <= i; ++k) {
+        k_fg_proj<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, k, i, ctx->kw, part, dist);
+        if ((rc = reduce())) return rc;
+        k_fg_reo<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, k, i, ctx->kw, part, dist);
+        if ((rc = reduce())) return rc;
+      }
+      k_fg_close_div<<<kRedBlocks, kBlock, 0, st>>>(n, s, i, W(i + 1));
+      continue;
     }
     // the product on a full grid (the 512-block reduction grid left 2 waves per SIMD, 91 % parked),
     // then the two inner products in the reduction's own order

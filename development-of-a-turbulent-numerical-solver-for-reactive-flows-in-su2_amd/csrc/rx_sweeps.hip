@@ -1133,6 +1133,296 @@ __global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__
   }
 }
 
+// The SST's 2x2 ILU(0) on triangle-free meshes (ctx->ilu_grp_ok: every lower block A_ij updates only the diagonal,
+// D_i = A_ii - sum_t A_ji (A_ij inv(D_j)), k_ilu_build_2's gplan branch), one wavefront per partition (VERDICT r03
+// #7). k_ilu_build_2 ran one thread per row on 256-thread workgroups: a level's ~27 rows are one wavefront, whose
+// per-row instruction stream (compact plans with runtime block positions resolved by selects) and the global
+// round trips of inv(D_j) set the time (0.87 ms at C3 for ~146 levels). Here:
+//   * the pass's rows (<= 64 rows of one level, the schedule's pass table) are the wavefront's lanes, so no
+//     barrier is needed: a later pass of the same wavefront sees this pass's LDS stores;
+//   * inv(D_j) of the partition's rows stays in LDS (partition-local index, 32 B per row), written by the pass that
+//     factors row j and read by the passes of its lower neighbours' rows;
+//   * every load a pass needs is an input (its plan, A_ii, A_ij, A_ji), so the plan of pass q + 2 and the blocks of
+//     pass q + 1 are issued before pass q is computed (all loads unconditional, from clamped valid addresses, so
+//     the wait counts stay static);
+//   * the upper blocks and the blocks outside the partition are the matrix's own and are neither copied nor
+//     rewritten (rx_ilu_upper: the sweeps read them from the Jacobian; rx_la_ilu_materialize for a download).
+// Rows with more than kB2 lower blocks (3-D: up to six) take the extra blocks with direct loads. Arithmetic as
+// k_ilu_build_2's gplan branch, operation for operation.
+constexpr int kB2 = 3;
+struct Plan2 {
+  int4 h;        // i, klo, kd, khi
+  int j[kB2];    // columns of the first lower blocks
+  int kk[kB2];   // A_ji positions (-1: no update)
+};
+struct Blk2 {
+  double d[4], a[kB2][4], u[kB2][4];  // A_ii, A_ij, A_ji
+};
+__device__ __forceinline__ Plan2 plan2_load(const int32_t* __restrict__ gplan, int r) {
+  const int4* g = reinterpret_cast<const int4*>(gplan + (size_t)r * 32);
+  Plan2 P;
+  P.h = g[0];
+  const int4 c = g[2], k3 = g[3], k4 = g[4];  // [8..11] columns, [14..16] A_ji positions
+  P.j[0] = c.x;
+  P.j[1] = c.y;
+  P.j[2] = c.z;
+  P.kk[0] = k3.z;
+  P.kk[1] = k3.w;
+  P.kk[2] = k4.x;
+  return P;
+}
+__device__ __forceinline__ void blk2_load(const double* __restrict__ A, const Plan2& P, Blk2& B) {
+  const int kd = P.h.z, nlow = P.h.z - P.h.y;
+  const double2* a2 = reinterpret_cast<const double2*>(A);
+  double2 x0 = a2[(size_t)kd * 2], x1 = a2[(size_t)kd * 2 + 1];
+  B.d[0] = x0.x, B.d[1] = x0.y, B.d[2] = x1.x, B.d[3] = x1.y;
+#pragma unroll
+  for (int t = 0; t < kB2; ++t) {
+    const int k = t < nlow ? P.h.y + t : kd;
+    const int u = (t < nlow && P.kk[t] >= 0) ? P.kk[t] : kd;
+    double2 y0 = a2[(size_t)k * 2], y1 = a2[(size_t)k * 2 + 1], z0 = a2[(size_t)u * 2], z1 = a2[(size_t)u * 2 + 1];
+    B.a[t][0] = y0.x, B.a[t][1] = y0.y, B.a[t][2] = y1.x, B.a[t][3] = y1.y;
+    B.u[t][0] = z0.x, B.u[t][1] = z0.y, B.u[t][2] = z1.x, B.u[t][3] = z1.y;
+  }
+}
+// W = Bij inv(D_j), D -= Bji W (each product summed from 0.0, q ascending)
+__device__ __forceinline__ void ilu2_lower(const double (&Bij)[4], const double* Sinv, const double (&Bji)[4],
+                                          bool upd, double (&D)[4], double (&W)[4]) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      double sm = 0.0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) sm += Bij[a * 2 + q] * Sinv[q * 2 + c];
+      W[a * 2 + c] = sm;
+    }
+  if (upd) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        double sm = 0.0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) sm += Bji[a * 2 + q] * W[q * 2 + c];
+        D[a * 2 + c] -= sm;
+      }
+  }
+}
+__global__ __launch_bounds__(64) void k_ilu_build_2w(const int32_t* __restrict__ part_ptr,
+                                                     const int32_t* __restrict__ part_pass,
+                                                     const int32_t* __restrict__ pass_lo,
+                                                     const int32_t* __restrict__ gplan, const double* __restrict__ A,
+                                                     double* __restrict__ F, double* __restrict__ invD) {
+  extern __shared__ double sinv[];  // [partition rows][4]
+  const int p = blockIdx.x, lane = threadIdx.x;
+  const int p0 = part_ptr[p];
+  const int q0 = part_pass[p], q1 = part_pass[p + 1];
+  if (q0 >= q1) return;
+  const int rlast = pass_lo[q1] - 1;  // clamp target: a valid slot of this partition
+  auto slot_of = [&](int q) {
+    const int qq = q < q1 ? q : q1 - 1;
+    const int r = pass_lo[qq] + lane;
+    return r < pass_lo[qq + 1] ? r : rlast;
+  };
+  // pipeline: the plans of passes q .. q + kPB2 - 1 (a register ring shifted every pass) and the blocks of passes
+  // q .. q + kBB2 - 1 are in flight while pass q is computed; a pass's blocks are loaded from a plan that arrived
+  // passes earlier, so no load waits on another one
+  constexpr int kPB2 = 6, kBB2 = 2;
+  Plan2 Pr[kPB2];
+#pragma unroll
+  for (int d = 0; d < kPB2; ++d) Pr[d] = plan2_load(gplan, slot_of(q0 + d));
+  Blk2 Br[kBB2];
+#pragma unroll
+  for (int d = 0; d < kBB2; ++d) blk2_load(A, Pr[d], Br[d]);
+  for (int q = q0; q < q1; ++q) {
+    const bool act = pass_lo[q] + lane < pass_lo[q + 1];
+    const Plan2 P = Pr[0];
+    const Blk2 B = Br[0];
+#pragma unroll
+    for (int d = 0; d + 1 < kPB2; ++d) Pr[d] = Pr[d + 1];
+    Pr[kPB2 - 1] = plan2_load(gplan, slot_of(q + kPB2));
+#pragma unroll
+    for (int d = 0; d + 1 < kBB2; ++d) Br[d] = Br[d + 1];
+    blk2_load(A, Pr[kBB2 - 1], Br[kBB2 - 1]);
+    if (act) {
+      const int i = P.h.x, klo = P.h.y, kd = P.h.z, nlow = kd - klo;
+      double D[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) D[e] = B.d[e];
+#pragma unroll
+      for (int t = 0; t < kB2; ++t) {
+        if (t < nlow) {
+          double W[4];
+          ilu2_lower(B.a[t], sinv + (size_t)(P.j[t] - p0) * 4, B.u[t], P.kk[t] >= 0, D, W);
+          double2* f2 = reinterpret_cast<double2*>(F + (size_t)(klo + t) * 4);
+          f2[0] = make_double2(W[0], W[1]);
+          f2[1] = make_double2(W[2], W[3]);
+        }
+      }
+      for (int t = kB2; t < nlow; ++t) {  // rows past the plan's register blocks (3-D)
+        const int32_t* g = gplan + (size_t)(pass_lo[q] + lane) * 32;
+        const int kk = g[14 + t];
+        double Bij[4], Bji[4], W[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          Bij[e] = A[(size_t)(klo + t) * 4 + e];
+          Bji[e] = kk >= 0 ? A[(size_t)kk * 4 + e] : 0.0;
+        }
+        ilu2_lower(Bij, sinv + (size_t)(g[8 + t] - p0) * 4, Bji, kk >= 0, D, W);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) F[(size_t)(klo + t) * 4 + e] = W[e];
+      }
+      double2* fd = reinterpret_cast<double2*>(F + (size_t)kd * 4);
+      fd[0] = make_double2(D[0], D[1]);
+      fd[1] = make_double2(D[2], D[3]);
+      // inv(D_i): Gauss elimination of D_i, then one unit column at a time (k_ilu_build_2)
+      {
+        const double w = D[2] / D[0];
+        D[3] -= w * D[1];
+        D[2] = w;
+      }
+      double inv[4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        double rhs[2] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0};
+        lu_solve<2>(D, rhs);
+        inv[c] = rhs[0];
+        inv[2 + c] = rhs[1];
+      }
+      double2* iv = reinterpret_cast<double2*>(invD + (size_t)i * 4);
+      iv[0] = make_double2(inv[0], inv[1]);
+      iv[1] = make_double2(inv[2], inv[3]);
+      double2* sv = reinterpret_cast<double2*>(sinv + (size_t)(i - p0) * 4);
+      sv[0] = make_double2(inv[0], inv[1]);
+      sv[1] = make_double2(inv[2], inv[3]);
+    }
+  }
+}
+
+// The SST's 2x2 ILU(0) apply, forward and backward sweeps in one launch, one wavefront per partition (VERDICT r03
+// #7): the partition's vector lives in LDS from b to x (loaded and stored once, coalesced), the sweeps run pass by
+// pass (<= 64 rows of one level, one row per lane, no barrier). A pass's slot record is loaded kS2 passes ahead
+// (a register ring shifted every pass) and its blocks, column indices and inv(D_i) kD2 passes ahead, from that
+// slot, so no load of the pass being computed waits on another load; every load is unconditional (clamped valid
+// addresses) so the wait counts stay static. Rows with more than kB2 blocks on a side take the rest with direct
+// loads. Arithmetic as k_ilu_fwd_wide / k_ilu_bwd_wide, operation for operation.
+constexpr int kS2 = 8, kD2 = 3;
+struct Row2 {
+  int c[kB2];        // block columns
+  double f[kB2][4];  // blocks
+  double inv[4];     // inv(D_i) (backward)
+};
+template <bool BWD>
+__device__ __forceinline__ void row2_load(const int4& s, const int32_t* __restrict__ col,
+                                          const double* __restrict__ F, const double* __restrict__ invD, Row2& R) {
+  const int k0 = BWD ? s.z + 1 : s.y, k1 = BWD ? s.w : s.z;
+  const double2* f2 = reinterpret_cast<const double2*>(F);
+#pragma unroll
+  for (int t = 0; t < kB2; ++t) {
+    const int k = k0 + t < k1 ? k0 + t : s.z;  // clamped to the diagonal block (always present)
+    R.c[t] = col[k];
+    const double2 a = f2[(size_t)k * 2], b = f2[(size_t)k * 2 + 1];
+    R.f[t][0] = a.x, R.f[t][1] = a.y, R.f[t][2] = b.x, R.f[t][3] = b.y;
+  }
+  if (BWD) {
+    const double2* i2 = reinterpret_cast<const double2*>(invD);
+    const double2 a = i2[(size_t)s.x * 2], b = i2[(size_t)s.x * 2 + 1];
+    R.inv[0] = a.x, R.inv[1] = a.y, R.inv[2] = b.x, R.inv[3] = b.y;
+  }
+}
+template <bool BWD>
+__device__ __forceinline__ void sweep2(const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                       const double* __restrict__ F, const double* __restrict__ invD,
+                                       const int32_t* __restrict__ pass_lo, int q0, int q1, int p0, double* xs) {
+  const int lane = threadIdx.x;
+  const int rlast = pass_lo[q1] - 1;
+  auto slot_of = [&](int q) {
+    const int qq = q < q1 ? q : q1 - 1;
+    const int r = pass_lo[qq] + lane;
+    return slot[r < pass_lo[qq + 1] ? r : rlast];
+  };
+  int4 S[kS2];  // slots of passes q .. q + kS2 - 1
+#pragma unroll
+  for (int d = 0; d < kS2; ++d) S[d] = slot_of(q0 + d);
+  Row2 R[kD2];  // blocks of passes q .. q + kD2 - 1
+#pragma unroll
+  for (int d = 0; d < kD2; ++d) row2_load<BWD>(S[d], col, F, invD, R[d]);
+  for (int q = q0; q < q1; ++q) {
+    const bool act = pass_lo[q] + lane < pass_lo[q + 1];
+    const int4 sc = S[0];
+    const Row2 Rc = R[0];
+#pragma unroll
+    for (int d = 0; d + 1 < kS2; ++d) S[d] = S[d + 1];
+    S[kS2 - 1] = slot_of(q + kS2);
+#pragma unroll
+    for (int d = 0; d + 1 < kD2; ++d) R[d] = R[d + 1];
+    row2_load<BWD>(S[kD2 - 1], col, F, invD, R[kD2 - 1]);
+    if (!act) continue;
+    const int i = sc.x;
+    const int k0 = BWD ? sc.z + 1 : sc.y, k1 = BWD ? sc.w : sc.z;
+    double* xi = xs + (size_t)(i - p0) * 2;
+    double acc[2];
+    if (BWD) {
+      acc[0] = 0.0;
+      acc[1] = 0.0;
+    } else {
+      acc[0] = xi[0];
+      acc[1] = xi[1];
+    }
+    auto take = [&](const double* blk, int j) {
+      const double* xj = xs + (size_t)(j - p0) * 2;
+      const double x0 = xj[0], x1 = xj[1];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        double sm = 0.0;
+        sm += blk[a * 2] * x0;
+        sm += blk[a * 2 + 1] * x1;
+        if (BWD) acc[a] += sm;
+        else acc[a] -= sm;
+      }
+    };
+#pragma unroll
+    for (int t = 0; t < kB2; ++t)
+      if (k0 + t < k1) take(Rc.f[t], Rc.c[t]);
+    for (int k = k0 + kB2; k < k1; ++k) {  // more blocks than the registers hold
+      double blk[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) blk[e] = F[(size_t)k * 4 + e];
+      take(blk, col[k]);
+    }
+    if (BWD) {
+      const double v0 = xi[0] - acc[0], v1 = xi[1] - acc[1];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        double sm = 0.0;
+        sm += Rc.inv[a * 2] * v0;
+        sm += Rc.inv[a * 2 + 1] * v1;
+        acc[a] = sm;
+      }
+    }
+    xi[0] = acc[0];
+    xi[1] = acc[1];
+  }
+}
+__global__ __launch_bounds__(64) void k_ilu_apply_2w(const int32_t* __restrict__ part_ptr,
+                                                     const int32_t* __restrict__ fpart, const int32_t* __restrict__ fpass,
+                                                     const int4* __restrict__ fslot, const int32_t* __restrict__ bpart,
+                                                     const int32_t* __restrict__ bpass, const int4* __restrict__ bslot,
+                                                     const int32_t* __restrict__ col, const double* __restrict__ L,
+                                                     const double* __restrict__ U, const double* __restrict__ invD,
+                                                     const double* __restrict__ b, double* __restrict__ x,
+                                                     int* __restrict__ done, const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  extern __shared__ double xs[];  // [partition rows][2]
+  const int p = blockIdx.x;
+  const int p0 = part_ptr[p], n = (part_ptr[p + 1] - p0) * 2;
+  for (int q = threadIdx.x; q < n; q += 64) xs[q] = b[(size_t)p0 * 2 + q];
+  if (fpart[p] < fpart[p + 1]) sweep2<false>(fslot, col, L, invD, fpass, fpart[p], fpart[p + 1], p0, xs);
+  if (bpart[p] < bpart[p + 1]) sweep2<true>(bslot, col, U, invD, bpass, bpart[p], bpart[p + 1], p0, xs);
+  for (int q = threadIdx.x; q < n; q += 64) x[(size_t)p0 * 2 + q] = xs[q];
+}
+
 // Small-block ILU(0) with the whole partition resident in LDS (the SST system's 2x2 blocks: a 390-row
 // partition is ~2 000 blocks = 64 KB). The workgroup loads the partition rows' A blocks once, every
 // dependency level then reads finished rows' blocks and inverses from LDS (no global round trip between
@@ -1352,13 +1642,10 @@ __device__ __forceinline__ void row_blocks(const double* __restrict__ F, const i
 // rows -> klo / diag), and the first pass's slot of level l+1 loaded while level l runs. Same arithmetic,
 // operation for operation, as k_ilu_fwd_part / k_ilu_bwd_part.
 template <int NV, int TB>
-__global__ __launch_bounds__(TB) void k_ilu_fwd_wide(const int32_t* __restrict__ part_lvl,
-                                                     const int32_t* __restrict__ lvl_ptr,
-                                                     const int4* __restrict__ slot, const int32_t* __restrict__ col,
-                                                     const double* __restrict__ F, const double* __restrict__ b,
-                                                     double* __restrict__ x, int* __restrict__ done,
-                                                     const int* __restrict__ conv) {
-  if (skip_sweep(done, conv)) return;
+__device__ __forceinline__ void fwd_wide_body(const int32_t* __restrict__ part_lvl, const int32_t* __restrict__ lvl_ptr,
+                                              const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                              const double* __restrict__ F, const double* __restrict__ b,
+                                              double* __restrict__ x) {
   constexpr int NV2 = NV * NV, RPB = TB / NV;
   const int p = blockIdx.x;
   const int rl = threadIdx.x / NV, a = threadIdx.x - rl * NV;
@@ -1383,13 +1670,10 @@ __global__ __launch_bounds__(TB) void k_ilu_fwd_wide(const int32_t* __restrict__
 }
 
 template <int NV, int TB>
-__global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__ part_lvl,
-                                                     const int32_t* __restrict__ lvl_ptr,
-                                                     const int4* __restrict__ slot, const int32_t* __restrict__ col,
-                                                     const double* __restrict__ F, const double* __restrict__ invD,
-                                                     double* __restrict__ x, int* __restrict__ done,
-                                                     const int* __restrict__ conv) {
-  if (skip_sweep(done, conv)) return;
+__device__ __forceinline__ void bwd_wide_body(const int32_t* __restrict__ part_lvl, const int32_t* __restrict__ lvl_ptr,
+                                              const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                              const double* __restrict__ F, const double* __restrict__ invD,
+                                              double* __restrict__ x) {
   // Rows are laid out wavefront by wavefront (64 / NV rows per wavefront, the last 64 mod NV lanes idle), so that a
   // row's lanes never straddle two wavefronts: the exchange of v between the two halves of a level is then
   // wavefront-local (wave_sync) instead of a workgroup barrier. RX_BWD_BLOCK_ROWS restores the dense layout.
@@ -1445,6 +1729,48 @@ __global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__
       __syncthreads();
     }
   }
+}
+
+template <int NV, int TB>
+__global__ __launch_bounds__(TB) void k_ilu_fwd_wide(const int32_t* __restrict__ part_lvl,
+                                                     const int32_t* __restrict__ lvl_ptr,
+                                                     const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                                     const double* __restrict__ F, const double* __restrict__ b,
+                                                     double* __restrict__ x, int* __restrict__ done,
+                                                     const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  fwd_wide_body<NV, TB>(part_lvl, lvl_ptr, slot, col, F, b, x);
+}
+template <int NV, int TB>
+__global__ __launch_bounds__(TB) void k_ilu_bwd_wide(const int32_t* __restrict__ part_lvl,
+                                                     const int32_t* __restrict__ lvl_ptr,
+                                                     const int4* __restrict__ slot, const int32_t* __restrict__ col,
+                                                     const double* __restrict__ F, const double* __restrict__ invD,
+                                                     double* __restrict__ x, int* __restrict__ done,
+                                                     const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  bwd_wide_body<NV, TB>(part_lvl, lvl_ptr, slot, col, F, invD, x);
+}
+// Both sweeps of a partition in one launch: the block-Jacobi partitions are independent, so the
+// backward sweep of partition p needs only p's forward sweep, and a barrier (which makes the forward sweep's x
+// stores visible to the workgroup, as between the levels) replaces the grid-wide boundary between two launches;
+// the partition's x is then read back from the L2 it was just written to, and the kernel's time is the slowest
+// partition's forward + backward instead of the slowest forward + the slowest backward. Same arithmetic.
+template <int NV, int TB>
+__global__ __launch_bounds__(TB) void k_ilu_apply_wide(const int32_t* __restrict__ fpart_lvl,
+                                                       const int32_t* __restrict__ flvl_ptr,
+                                                       const int4* __restrict__ fslot,
+                                                       const int32_t* __restrict__ bpart_lvl,
+                                                       const int32_t* __restrict__ blvl_ptr,
+                                                       const int4* __restrict__ bslot, const int32_t* __restrict__ col,
+                                                       const double* __restrict__ L, const double* __restrict__ U,
+                                                       const double* __restrict__ invD, const double* __restrict__ b,
+                                                       double* __restrict__ x, int* __restrict__ done,
+                                                       const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  fwd_wide_body<NV, TB>(fpart_lvl, flvl_ptr, fslot, col, L, b, x);
+  __syncthreads();
+  bwd_wide_body<NV, TB>(bpart_lvl, blvl_ptr, bslot, col, U, invD, x);
 }
 
 // ILU(0) application with the partition's vector resident in LDS: b is loaded once, the forward
@@ -1777,8 +2103,15 @@ static bool ilu_grouped(const rx_ctx* ctx) {
   static const bool rowwave = getenv("RX_ILU_ROWWAVE") != nullptr;  // A/B: one row per wavefront
   return ctx->nVar >= 5 && ctx->ilu_grp_ok && !rowwave;
 }
+// The one-wavefront 2x2 build (k_ilu_build_2w): triangle-free meshes whose partitions' inv(D) fit LDS.
+static bool ilu2_wave(const rx_ctx* ctx) {
+  static const bool old = getenv("RX_ILU2_OLD") != nullptr;  // A/B: k_ilu_build_lds / k_ilu_build_2
+  return ctx->nVar == 2 && ctx->ilu_grp_ok && !old && (size_t)ctx->maxpart * 4 * sizeof(double) <= (size_t)ctx->lds_max;
+}
 // Where the triangular sweeps read the factor's upper blocks.
-const double* rx_ilu_upper(rx_ctx* ctx) { return ilu_grouped(ctx) ? ctx->f[RX_F_JAC] : ctx->f[RX_F_ILU]; }
+const double* rx_ilu_upper(rx_ctx* ctx) {
+  return (ilu_grouped(ctx) || ilu2_wave(ctx)) ? ctx->f[RX_F_JAC] : ctx->f[RX_F_ILU];
+}
 
 namespace {
 // ILU_matrix as the reference holds it (rx_download of the ILU field after k_ilu_build_grp): the blocks ILU(0)
@@ -1799,7 +2132,7 @@ __global__ __launch_bounds__(256) void k_ilu_materialize(int N, const int32_t* _
 }  // namespace
 
 int rx_la_ilu_materialize(rx_ctx* ctx) {
-  if (!ilu_grouped(ctx) || !ctx->f[RX_F_ILU]) return RX_OK;
+  if ((!ilu_grouped(ctx) && !ilu2_wave(ctx)) || !ctx->f[RX_F_ILU]) return RX_OK;
   RX_NV_SWITCH(ctx->nVar, (k_ilu_materialize<NV_><<<(int)((ctx->Nd + 3) / 4), 256, 0, ctx->stream>>>(
                               (int)ctx->Nd, ctx->rp, ctx->klo, ctx->diag, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU])));
   RX_HIP(hipGetLastError());
@@ -1826,6 +2159,12 @@ int rx_la_prepare(rx_ctx* ctx) {
     if (NV_ <= 4)
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_lds<NV_>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    if (NV_ == 2) {
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_2w),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_2w),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    }
   });
   return RX_OK;
 }
@@ -1862,6 +2201,13 @@ int rx_la_ilu_build(rx_ctx* ctx) {
 
 static int ilu_build_impl(rx_ctx* ctx) {
   const int nv = ctx->nVar;
+  if (ilu2_wave(ctx) && !ctx->ilu_trace) {
+    k_ilu_build_2w<<<ctx->npart, 64, (size_t)ctx->maxpart * 4 * sizeof(double), ctx->stream>>>(
+        ctx->part_ptr, ctx->fs.part_pass, ctx->fs.pass_lo, ctx->ilu_gplan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
+        rx_invd_buf(ctx));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
   const size_t shm_small = sizeof(double) * (size_t)nv * nv * (ctx->maxpart_nnzb + ctx->maxpart);
   if (nv <= 4 && !ctx->ilu_trace && shm_small <= (size_t)ctx->lds_max) {
     RX_NV_SWITCH(nv, (k_ilu_build_lds<NV_><<<ctx->npart, 256, shm_small, ctx->stream>>>(
@@ -1904,8 +2250,22 @@ static int ilu_build_impl(rx_ctx* ctx) {
   return RX_OK;
 }
 
+// The one-wavefront 2x2 apply (k_ilu_apply_2w): partitions whose vector fits LDS.
+static bool ilu2_apply_wave(const rx_ctx* ctx) {
+  static const bool old = getenv("RX_ILU2_APPLY_OLD") != nullptr;  // A/B: the LDS-resident / wide sweeps
+  return ctx->nVar == 2 && !old && (size_t)ctx->maxpart * 2 * sizeof(double) <= (size_t)ctx->lds_max;
+}
+
 int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv) {
   const int nv = ctx->nVar;
+  if (ilu2_apply_wave(ctx)) {
+    k_ilu_apply_2w<<<ctx->npart, 64, (size_t)ctx->maxpart * 2 * sizeof(double), ctx->stream>>>(
+        ctx->part_ptr, ctx->fs.part_pass, ctx->fs.pass_lo, reinterpret_cast<const int4*>(ctx->fs.slot),
+        ctx->bs.part_pass, ctx->bs.pass_lo, reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU],
+        rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv);
+    RX_HIP(hipGetLastError());
+    return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
+  }
   const size_t shm = sizeof(double) * ((size_t)ctx->maxpart * nv + (size_t)(256 / nv) * nv + 1) +
                      sizeof(int32_t) * (8 * (size_t)ctx->maxpart + (size_t)ctx->maxpart_nnzb);
   static const bool no_lds = getenv("RX_NO_LDS_APPLY") != nullptr;  // diagnosis: force the global sweeps
@@ -1916,7 +2276,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                          reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_ilu_upper(ctx),
                          rx_invd_buf(ctx), b, x, done, conv)));
     RX_HIP(hipGetLastError());
-    return rx_la_exchange(ctx, x, nv);  // ComputeILUPreconditioner's closing SendReceive_Solution (:1513)
+    return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);  // ComputeILUPreconditioner's closing SendReceive_Solution (:1513)
   }
   // RX_LDS_GMETA=1 (measured, not the default): when the vector alone fits (the SST's 2x2 system at C3 / C5, 62 KB
   // per partition), the LDS-resident apply with slot records and columns read from the global tables. Bitwise the
@@ -1931,10 +2291,20 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                          reinterpret_cast<const int4*>(ctx->bs.slot), ctx->col, ctx->f[RX_F_ILU], rx_ilu_upper(ctx),
                          rx_invd_buf(ctx), b, x, done, conv)));
     RX_HIP(hipGetLastError());
-    return rx_la_exchange(ctx, x, nv);
+    return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
   }
   static const bool narrow = getenv("RX_NARROW_APPLY") != nullptr;  // diagnosis: the 256-thread sweeps
   const int width = std::max(ctx->fs.maxwidth, ctx->bs.maxwidth);
+  static const bool split = getenv("RX_ILU_SPLIT") != nullptr;  // A/B: the two sweeps as separate launches
+  if (!narrow && width * nv > 256 && !split) {
+    const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
+    const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
+    RX_NV_SWITCH(nv, (k_ilu_apply_wide<NV_, 1024><<<ctx->npart, 1024, 0, ctx->stream>>>(
+                         ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col,
+                         ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv)));
+    RX_HIP(hipGetLastError());
+    return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
+  }
   if (!narrow && width * nv > 256) {
     const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
     const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
@@ -1944,7 +2314,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                          ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, rx_ilu_upper(ctx), rx_invd_buf(ctx), x,
                          done, conv)));
     RX_HIP(hipGetLastError());
-    return rx_la_exchange(ctx, x, nv);
+    return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
   }
   static const bool narrow_small = getenv("RX_NARROW_SMALL") != nullptr;  // diagnosis: the part sweeps below
   if (!narrow && !narrow_small) {  // levels narrower than 256 / NV rows: the same wide sweeps on 256 threads
@@ -1956,7 +2326,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                          ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, ctx->col, rx_ilu_upper(ctx), rx_invd_buf(ctx), x,
                          done, conv)));
     RX_HIP(hipGetLastError());
-    return rx_la_exchange(ctx, x, nv);
+    return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
   }
   RX_NV_SWITCH(ctx->nVar, (k_ilu_fwd_part<NV_><<<ctx->npart, 256, 0, ctx->stream>>>(
                               ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->col, ctx->klo, ctx->diag,
@@ -1965,7 +2335,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
                               ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows, ctx->col, ctx->khi, ctx->diag,
                               rx_ilu_upper(ctx), rx_invd_buf(ctx), x, done, conv)));
   RX_HIP(hipGetLastError());
-  return rx_la_exchange(ctx, x, nv);
+  return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
 }
 
 int rx_la_diag_factor(rx_ctx* ctx, const double* A) {
@@ -1988,7 +2358,7 @@ int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, int* d
                               ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows, ctx->rp, ctx->col, ctx->klo, ctx->khi,
                               ctx->diag, A, ctx->dlu, ctx->xstar, x, done, conv)));
   RX_HIP(hipGetLastError());
-  return rx_la_exchange(ctx, x, ctx->nVar);  // :1707
+  return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, ctx->nVar);  // :1707
 }
 
 // Debug: trace the phases of the ILU(0) factorisation of partition 0 (see tools/ilu_trace.py).
