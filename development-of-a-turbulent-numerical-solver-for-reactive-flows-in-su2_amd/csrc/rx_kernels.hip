@@ -976,8 +976,7 @@ __global__ __launch_bounds__(kBlock) void k_grad_lsq(int N, const int32_t* __res
   double ci[NDIM];
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) ci[d] = coord[(size_t)i * NDIM + d];
-  for (int k = nptr[i]; k < nptr[i + 1]; ++k) {
-    const int j = nbr[k];
+  auto neighbour = [&](int j) {
     const double* v = V + (size_t)j * nPV;
     pj[0] = v[0];
     pj[P_G] = v[P_P];
@@ -1008,6 +1007,19 @@ __global__ __launch_bounds__(kBlock) void k_grad_lsq(int N, const int32_t* __res
 #pragma unroll
         for (int d = 0; d < NDIM; ++d) C[g][d] += cij[d] * (pj[g] - pi[g]) / w;
     }
+  };
+  // neighbours in the reference's order; the first 2 NDIM indices are loaded together first, so the neighbours'
+  // record loads do not each wait on their index load
+  {
+    const int k0 = nptr[i], k1 = nptr[i + 1];
+    constexpr int PF = 2 * NDIM;
+    int jp[PF];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) jp[t] = nbr[k0 + t < k1 ? k0 + t : k0];
+#pragma unroll
+    for (int t = 0; t < PF; ++t)
+      if (k0 + t < k1) neighbour(jp[t]);
+    for (int k = k0 + PF; k < k1; ++k) neighbour(nbr[k]);
   }
   r11 = (r11 > kEPS) ? sqrt(r11) : 0.0;
   r12 = (fabs(r11) > kEPS) ? r12 / r11 : 0.0;
@@ -1200,9 +1212,7 @@ __global__ __launch_bounds__(kBlock) void k_time_step(int N, int nPV, int nVar, 
     for (int d = 0; d < NDIM; ++d) s += V[(size_t)p * nPV + 1 + d] * n[d];
     return s;
   };
-  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
-    const int e = adj[k] >> 1;
-    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+  auto edge = [&](int e, int n0, int n1) {
     double n[NDIM];
 #pragma unroll
     for (int d = 0; d < NDIM; ++d) n[d] = normal[(size_t)e * NDIM + d];
@@ -1220,6 +1230,25 @@ __global__ __launch_bounds__(kBlock) void k_time_step(int N, int nPV, int nVar, 
     const double l1 = 4.0 / 3.0 * (m + mt);
     const double l2 = (1.0 + (Pr_l / Pr_t) * (mt / m)) * (gam * m / Pr_l);
     lv += (l1 + l2) * Area * Area / rho;
+  };
+  // incident edges in edge order; the index chains of the first 2 NDIM edges are loaded together first, so the
+  // edges' data loads do not wait on one another (DT 0.18 ms at C3 with the serial adj -> edges -> data chain)
+  const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  constexpr int PF = 2 * NDIM;
+  int ep[PF], e0p[PF], e1p[PF];
+#pragma unroll
+  for (int t = 0; t < PF; ++t) ep[t] = adj[k0 + t < k1 ? k0 + t : k0] >> 1;
+#pragma unroll
+  for (int t = 0; t < PF; ++t) {
+    e0p[t] = edges[2 * ep[t]];
+    e1p[t] = edges[2 * ep[t] + 1];
+  }
+#pragma unroll
+  for (int t = 0; t < PF; ++t)
+    if (k0 + t < k1) edge(ep[t], e0p[t], e1p[t]);
+  for (int k = k0 + PF; k < k1; ++k) {
+    const int e = adj[k] >> 1;
+    edge(e, edges[2 * e], edges[2 * e + 1]);
   }
   for (int b = bv_ptr[i]; b < bv_ptr[i + 1]; ++b) {
     double n[NDIM];
