@@ -317,7 +317,7 @@ def main():
             ext_iter[0] += 1
         else:
             s.SetPrimitive_Variables()  # Cons2Prim + transport from the U of the previous update (next-1)
-            s.SetPrimitive_Gradient_LS()
+            s.SetPrimitive_Gradient()
             s.SetStrainMag()
             s.SetTime_Step()
             s.Preprocessing_zero()

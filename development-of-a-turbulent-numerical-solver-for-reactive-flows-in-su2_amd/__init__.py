@@ -87,7 +87,8 @@ class Cfg(C.Structure):
                 ("t_min", C.c_double), ("t_max", C.c_double), ("p_ref", C.c_double), ("visc_ref", C.c_double),
                 ("cond_ref", C.c_double), ("vel_ref", C.c_double), ("len_ref", C.c_double),
                 ("slope_limiter", C.c_int32), ("ignition", C.c_int32), ("fuel_index", C.c_int32),
-                ("oxidizer_index", C.c_int32), ("ignition_iter", C.c_int64), ("ignition_temp", C.c_double)]
+                ("oxidizer_index", C.c_int32), ("ignition_iter", C.c_int64), ("ignition_temp", C.c_double),
+                ("grad_method", C.c_int32)]
 
 
 class BcDesc(C.Structure):
@@ -139,7 +140,7 @@ def lib():
         _lib.rx_ctx_create.argtypes = [C.POINTER(MeshDesc), C.POINTER(MechDesc), C.POINTER(Cfg), C.c_int,
                                        C.POINTER(C.c_void_p)]
         for name in ("rx_ctx_destroy", "rx_sync", "rx_residual_zero", "rx_edge_flux_conv", "rx_edge_flux_visc",
-                     "rx_cell_source_pasr", "rx_grad_lsq", "rx_limiter_venkat", "rx_time_step", "rx_ilu0_build"):
+                     "rx_cell_source_pasr", "rx_grad_lsq", "rx_grad_gg", "rx_limiter_venkat", "rx_time_step", "rx_ilu0_build"):
             getattr(_lib, name).argtypes = [C.c_void_p]
         _lib.rx_upload.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
         _lib.rx_download.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
@@ -312,7 +313,8 @@ def default_cfg(**kw):
              lin_prec=1, spatial_order=0, clip_temp=0, t_min=200.0, t_max=6000.0, p_ref=1.0, visc_ref=1.0,
              cond_ref=1.0, vel_ref=1.0, len_ref=1.0, slope_limiter=0,
              # CConfig defaults (config_structure.cpp:591-603)
-             ignition=0, fuel_index=0, oxidizer_index=2, ignition_iter=999999, ignition_temp=1700.0)
+             ignition=0, fuel_index=0, oxidizer_index=2, ignition_iter=999999, ignition_temp=1700.0,
+             grad_method=0)  # NUM_METHOD_GRAD: 0 WEIGHTED_LEAST_SQUARES, 1 GREEN_GAUSS
     c.update(kw)
     cfg = Cfg()
     for k, v in c.items():
@@ -452,6 +454,18 @@ class ReactiveNSSolver:
     def SetPrimitive_Gradient_LS(self):
         self._call("rx_grad_lsq")
 
+    def SetPrimitive_Gradient_GG(self):
+        """CReactiveNSSolver::SetPrimitive_Gradient_GG (solver_direct_reactive.cpp:4784-4880)."""
+        self._call("rx_grad_gg")
+
+    def SetPrimitive_Gradient(self):
+        """The primitive gradient of NUM_METHOD_GRAD (CReactiveNSSolver::Preprocessing, solver_direct_reactive.cpp:
+        4714-4718)."""
+        if self.cfg.grad_method == 1:
+            self.SetPrimitive_Gradient_GG()
+        else:
+            self.SetPrimitive_Gradient_LS()
+
     def SetPrimitive_Limiter(self):
         self._call("rx_limiter_venkat")
 
@@ -531,10 +545,11 @@ class ReactiveNSSolver:
         return ms.value, n.value
 
 
-def sst_cfg(implicit=1, lin_tol=1e-6, lin_iter=5, lin_prec=1, relaxation_turb=1.0, cfl_red_turb=1.0):
-    """rx_cfg for the SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl."""
+def sst_cfg(implicit=1, lin_tol=1e-6, lin_iter=5, lin_prec=1, relaxation_turb=1.0, cfl_red_turb=1.0, grad_method=0):
+    """rx_cfg for the SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl, NUM_METHOD_GRAD
+    -> grad_method."""
     return default_cfg(implicit=implicit, lin_tol=lin_tol, lin_iter=lin_iter, lin_prec=lin_prec,
-                       relaxation=relaxation_turb, cfl=cfl_red_turb)
+                       relaxation=relaxation_turb, cfl=cfl_red_turb, grad_method=grad_method)
 
 
 class TurbSSTSolver:
@@ -822,7 +837,7 @@ def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=Non
 
     def preprocess(output):
         flow.SetPrimitive_Variables(ext_iter)
-        flow.SetPrimitive_Gradient_LS()
+        flow.SetPrimitive_Gradient()
         flow.SetStrainMag()
         if limiter and not output:
             flow.SetPrimitive_Limiter()

@@ -839,6 +839,15 @@ int rx_grad_lsq(rx_ctx* ctx) {
   return RX_OK;
 }
 
+int rx_grad_gg(rx_ctx* ctx) {
+  if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
+  RxPhase ph(ctx, RX_K_GRAD);
+  const int rc = rx_launch_grad_gg(ctx);
+  if (rc) return rc;
+  // Set_MPI_Primitive_Gradient (solver_direct_reactive.cpp:4878)
+  return rx_la_exchange(ctx, ctx->f[RX_F_GRAD], (int)(ctx->fcount[RX_F_GRAD] / ctx->N));
+}
+
 int rx_limiter_venkat(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_LIMITER);

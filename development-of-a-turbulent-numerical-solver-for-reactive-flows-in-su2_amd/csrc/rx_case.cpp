@@ -189,9 +189,10 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
         // :626 (default NONE): SA would build CTurbSASolver (driver_structure.cpp:806-814), NONE a laminar
         // CReactiveNSSolver without TURB_SOL; rx::Iterate / rx.Iterate always run the SST SingleGrid_Iteration
         {"KIND_TURB_MODEL", "NONE", "SST", "only the Menter SST turbulence solver is built"},
-        // :1147 (default WEIGHTED_LEAST_SQUARES): GREEN_GAUSS branches to SetPrimitive_Gradient_GG
-        // (solver_direct_reactive.cpp:1055, 4717, 4784-4880)
-        {"NUM_METHOD_GRAD", "WEIGHTED_LEAST_SQUARES", "WEIGHTED_LEAST_SQUARES", "only the weighted LSQ gradient"},
+        // :1147 (default WEIGHTED_LEAST_SQUARES): both methods of Gradient_Map (option_structure.hpp:723-725) are
+        // built: rx_grad_lsq / rx_grad_gg (SetPrimitive_Gradient_LS / _GG, solver_direct_reactive.cpp:4717) and the
+        // SST's SetSolution_Gradient_LS / _GG (solver_direct_turbulent.cpp:2944, 2963)
+        {"NUM_METHOD_GRAD", "WEIGHTED_LEAST_SQUARES", "", "WEIGHTED_LEAST_SQUARES or GREEN_GAUSS"},
         // :1047 (default FGMRES): CSysSolve::Solve's other Krylov methods (linear_solvers_structure.cpp:601-724)
         {"LINEAR_SOLVER", "FGMRES", "FGMRES", "only FGMRES"},
         // :1160 (default NO_CONVECTIVE): the reactive driver exits for any upwind scheme but AUSM
@@ -209,6 +210,10 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
     };
     for (const Need& n : need) {
       std::string v = upper(c.str(n.key, n.dflt));
+      if (std::string(n.key) == "NUM_METHOD_GRAD") {
+        if (v == "WEIGHTED_LEAST_SQUARES" || v == "GREEN_GAUSS") continue;
+        return fail(k, RX_ERR_UNSUPPORTED, "NUM_METHOD_GRAD= " + v + ": " + n.why);
+      }
       if (std::string(n.key) == "UNSTEADY_SIMULATION" && v == "STEADY") v = "NO";
       if (std::string(n.key) == "PHYSICAL_PROBLEM" && v == "REACTIVE_RANS") v = "REACTIVE_NAVIER_STOKES";
       if (v != n.want)
@@ -277,6 +282,8 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
   F.oxidizer_index = (int32_t)c.num("OXIDIZER_INDEX", 2);
   F.ignition_iter = (int64_t)c.num("IGNITION_ITER", 999999);
   F.ignition_temp = c.num("IGNITION_TEMPERATURE", 1700.0);
+  F.grad_method = upper(c.str("NUM_METHOD_GRAD", "WEIGHTED_LEAST_SQUARES")) == "GREEN_GAUSS" ? RX_GRAD_GREEN_GAUSS
+                                                                                         : RX_GRAD_WEIGHTED_LEAST_SQUARES;
   if (F.ignition && (F.fuel_index < 0 || F.fuel_index >= ns || F.oxidizer_index < 0 || F.oxidizer_index >= ns))
     return fail(k, RX_ERR_STATE, "FUEL_INDEX / OXIDIZER_INDEX out of the mixture");
   rx_cfg& S = k->sst;  // SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl
@@ -287,6 +294,7 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
   S.lin_prec = prec;
   S.relaxation = c.num("RELAXATION_FACTOR_TURB", 1.0);
   S.cfl = c.num("CFL_REDUCTION_TURB", 1.0);
+  S.grad_method = F.grad_method;
   if (tf == "RUNGE-KUTTA_EXPLICIT") {
     if (c.has("RK_ALPHA_COEFF"))
       for (const auto& t : list(c.str("RK_ALPHA_COEFF", ""))) k->rk.push_back(std::strtod(t.c_str(), nullptr));

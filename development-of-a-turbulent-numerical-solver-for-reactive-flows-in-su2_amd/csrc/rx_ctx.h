@@ -238,7 +238,8 @@ int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);
 int rx_launch_source(rx_ctx* ctx);
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src);
-int rx_launch_grad(rx_ctx* ctx, const int32_t* list, int64_t n);  // list null: points 0..n-1
+int rx_launch_grad(rx_ctx* ctx, const int32_t* list, int64_t n);
+int rx_launch_grad_gg(rx_ctx* ctx);  // list null: points 0..n-1
 int rx_launch_limiter(rx_ctx* ctx);
 int rx_launch_time_step(rx_ctx* ctx);
 int rx_check_error(rx_ctx* ctx);

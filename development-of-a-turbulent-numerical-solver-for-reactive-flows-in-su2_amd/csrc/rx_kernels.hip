@@ -1457,6 +1457,86 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   return RX_OK;
 }
 
+namespace {
+// NUM_METHOD_GRAD = GREEN_GAUSS: CReactiveNSSolver::SetPrimitive_Gradient_GG (solver_direct_reactive.cpp:4784-4880),
+// one thread per owned point gathering its incident edges in edge order (the reference's edge loop restricted to the
+// point: + at node 0, - at node 1), then its boundary vertices in (marker, vertex) order, then / Volume. Edge face
+// value 0.5 (P_i + P_j) of (T, u, v(, w), P, X_s), with the reference's quirk (:4812-4813): both sides' species are
+// node 0's, so X_j = X_i. Boundary vertex value: the point's own record.
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) void k_grad_gg(int Nd, const int32_t* __restrict__ adj_ptr,
+                                                    const int32_t* __restrict__ adj, const int32_t* __restrict__ edges,
+                                                    const double* __restrict__ normal, const int32_t* __restrict__ bv_ptr,
+                                                    const double* __restrict__ bv_normal,
+                                                    const double* __restrict__ vol, const double* __restrict__ V,
+                                                    DevMech m, double* __restrict__ Gout) {
+  constexpr int nPV = NS + NDIM + 5, nG = NS + NDIM + 2, P_P = NDIM + 1, RHOS_P = NDIM + 5, P_G = NDIM + 1,
+                RHOS_G = NDIM + 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Nd) return;
+  // (T, u, v(, w), P) of point p into out[0 .. P_G]; X_s of point q into out[RHOS_G ..]
+  auto prim = [&](int p, int q, double* out) {
+    const double* v = V + (size_t)p * nPV;
+    out[0] = v[0];
+    out[P_G] = v[P_P];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) out[1 + d] = v[1 + d];
+    const double* w = V + (size_t)q * nPV;
+    double ys[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ys[s] = w[RHOS_P + s];
+    molar_from_mass<NS>(m, ys, out + RHOS_G);
+  };
+  double g[nG][NDIM];
+#pragma unroll
+  for (int v = 0; v < nG; ++v)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) g[v][d] = 0.0;
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k], e = a >> 1, side = a & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    double pi[nG], pj[nG], nrm[NDIM];
+    prim(n0, n0, pi);
+    prim(n1, n0, pj);  // :4812-4813: node 0's species on both sides
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) nrm[d] = normal[(size_t)e * NDIM + d];
+#pragma unroll
+    for (int v = 0; v < nG; ++v) {
+      const double avg = 0.5 * (pi[v] + pj[v]);
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) {
+        const double pr = avg * nrm[d];
+        if (side == 0) g[v][d] += pr;
+        else g[v][d] -= pr;
+      }
+    }
+  }
+  if (bv_ptr[i] < bv_ptr[i + 1]) {
+    double pv[nG];
+    prim(i, i, pv);
+    for (int b = bv_ptr[i]; b < bv_ptr[i + 1]; ++b)
+#pragma unroll
+      for (int v = 0; v < nG; ++v)
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) g[v][d] -= pv[v] * bv_normal[(size_t)b * NDIM + d];
+  }
+  const double V_i = vol[i];
+#pragma unroll
+  for (int v = 0; v < nG; ++v)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) Gout[((size_t)i * nG + v) * NDIM + d] = g[v][d] / V_i;
+}
+}  // namespace
+
+int rx_launch_grad_gg(rx_ctx* ctx) {
+  if (ctx->Nd <= 0) return RX_OK;
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_grad_gg<NS_, ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
+                            (int)ctx->Nd, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->bv_ptr, ctx->bv_normal,
+                            ctx->vol, ctx->f[RX_F_V], ctx->mech, ctx->f[RX_F_GRAD])));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
 int rx_launch_grad(rx_ctx* ctx, const int32_t* list, int64_t n) {
   if (n <= 0) return RX_OK;
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_grad_lsq<NS_, ND_><<<blocks(n), kBlock, 0, ctx->stream>>>(

@@ -156,6 +156,52 @@ __global__ __launch_bounds__(kBlock) void k_sol_grad_ls(int Nd, const double* __
     }
 }
 
+// NUM_METHOD_GRAD = GREEN_GAUSS: CSolver::SetSolution_Gradient_GG (SU2_CFD/src/solver_structure.cpp:519-578) of the
+// turbulent solution, called from CTurbSSTSolver::Preprocessing / Postprocessing (solver_direct_turbulent.cpp:2944,
+// 2963): edges in edge order (+ at node 0, - at node 1, face value 0.5 (S_i + S_j)), then the point's boundary
+// vertices (every marker: no INTERNAL_BOUNDARY here), then / (Volume + EPS).
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_sol_grad_gg(int Nd, const int32_t* __restrict__ adj_ptr,
+                                                        const int32_t* __restrict__ adj,
+                                                        const int32_t* __restrict__ edges,
+                                                        const double* __restrict__ normal,
+                                                        const int32_t* __restrict__ bv_ptr,
+                                                        const double* __restrict__ bv_normal,
+                                                        const double* __restrict__ vol, const double* __restrict__ U,
+                                                        double* __restrict__ grad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Nd) return;
+  double g[2][NDIM];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) g[v][d] = 0.0;
+  for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+    const int a = adj[k], e = a >> 1, side = a & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const double avg = 0.5 * (U[2 * (size_t)n0 + v] + U[2 * (size_t)n1 + v]);
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) {
+        const double pr = avg * normal[(size_t)e * NDIM + d];
+        if (side == 0) g[v][d] += pr;
+        else g[v][d] -= pr;
+      }
+    }
+  }
+  for (int b = bv_ptr[i]; b < bv_ptr[i + 1]; ++b)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) g[v][d] -= U[2 * (size_t)i + v] * bv_normal[(size_t)b * NDIM + d];
+  const double da = vol[i] + rx::kEPS;
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) grad[((size_t)i * 2 + v) * NDIM + d] = g[v][d] / da;
+}
+
 // SetStrainMag from the flow primitive gradient (rows 1..NDIM = velocity); pow(x, 2.0) -> x * x.
 template <int NDIM>
 __global__ __launch_bounds__(kBlock) void k_strain(int N, int nG, const double* __restrict__ G,
@@ -519,7 +565,11 @@ __global__ __launch_bounds__(kBlock) void k_sst_post(int N, SSTC c, const double
 bool is_sst(const rx_ctx* ctx) { return ctx && ctx->kind == RX_KIND_SST && ctx->flow; }
 
 int sst_gradient(rx_ctx* ctx) {
-  if (ctx->Nd > 0) {
+  if (ctx->Nd > 0 && ctx->cfg.grad_method == RX_GRAD_GREEN_GAUSS) {
+    RX_ND_SWITCH(ctx->nDim, (k_sol_grad_gg<ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
+                                 (int)ctx->Nd, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->bv_ptr,
+                                 ctx->bv_normal, ctx->vol, ctx->f[RX_F_U], ctx->f[RX_F_GRAD])));
+  } else if (ctx->Nd > 0) {
     RX_ND_SWITCH(ctx->nDim, (k_sol_grad_ls<ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>((int)ctx->Nd, ctx->coord, ctx->nbr_ptr, ctx->nbr,
                                                                    ctx->f[RX_F_U], ctx->f[RX_F_GRAD])));
   }

@@ -230,7 +230,7 @@ def device_preprocess(flow, turb, mesh, state):
 
     def flow_pre():
         flow.SetPrimitive_Variables(0)
-        flow.SetPrimitive_Gradient_LS()
+        flow.SetPrimitive_Gradient()
         flow.SetStrainMag()
 
     flow_pre()

@@ -12,6 +12,7 @@
  *   rx_cell_source_pasr  CReactiveEulerSolver::Source_Residual solver_direct_reactive.cpp:2792-2874 with
  *                        CSourceReactive::ComputeChemistry numerics_direct_reactive.cpp:1728-1879
  *   rx_grad_lsq          CReactiveNSSolver::SetPrimitive_Gradient_LS solver_direct_reactive.cpp:4887-5050
+ *   rx_grad_gg           CReactiveNSSolver::SetPrimitive_Gradient_GG solver_direct_reactive.cpp:4784-4880
  *   rx_limiter_venkat    CReactiveEulerSolver::SetPrimitive_Limiter solver_direct_reactive.cpp:1328-1523
  *                        (Venkatakrishnan or Barth-Jespersen by rx_cfg.slope_limiter)
  *   rx_time_step         CReactiveNSSolver::SetTime_Step solver_direct_reactive.cpp:5057-5298
@@ -134,7 +135,13 @@ typedef struct {
   int32_t ignition, fuel_index, oxidizer_index;
   int64_t ignition_iter;
   double ignition_temp;
+  /* NUM_METHOD_GRAD (config_structure.cpp:1147): rx_grad_method. The flow's Preprocessing calls rx_grad_lsq or
+   * rx_grad_gg by it (solver_direct_reactive.cpp:4717); the SST context's Preprocessing / Postprocessing gradient of
+   * (k, omega) follows its own rx_cfg (solver_direct_turbulent.cpp:2944, 2963). */
+  int32_t grad_method;
 } rx_cfg;
+
+typedef enum { RX_GRAD_WEIGHTED_LEAST_SQUARES = 0, RX_GRAD_GREEN_GAUSS = 1 } rx_grad_method;
 
 typedef enum { RX_LIMITER_VENKATAKRISHNAN = 0, RX_LIMITER_BARTH_JESPERSEN = 1 } rx_slope_limiter;
 
@@ -171,7 +178,10 @@ int rx_residual_zero(rx_ctx *ctx);      /* LinSysRes = 0, Jacobian = 0 (Preproce
 int rx_edge_flux_conv(rx_ctx *ctx);     /* R[i] += F, R[j] -= F (+ Jacobian blocks) */
 int rx_edge_flux_visc(rx_ctx *ctx);     /* R[i] -= Fv, R[j] += Fv (+ Jacobian blocks) */
 int rx_cell_source_pasr(rx_ctx *ctx);   /* R[i] += S (+ diagonal block) */
-int rx_grad_lsq(rx_ctx *ctx);           /* grad from V */
+int rx_grad_lsq(rx_ctx *ctx);           /* grad from V (weighted least squares) */
+/* CReactiveNSSolver::SetPrimitive_Gradient_GG (solver_direct_reactive.cpp:4784-4880): Green-Gauss grad from V, with
+ * the reference's node-0 species on both sides of an edge (:4812-4813) */
+int rx_grad_gg(rx_ctx *ctx);
 int rx_limiter_venkat(rx_ctx *ctx);     /* limiter from V, grad */
 int rx_time_step(rx_ctx *ctx);          /* dt, lambda_inv, lambda_visc */
 

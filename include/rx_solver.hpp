@@ -5,6 +5,7 @@
  * (SU2_CFD/include/solver_reactive.hpp:141-363, 476-554):
  *   Preprocessing residual reset  -> rx_residual_zero            (LinSysRes.SetValZero, Jacobian.SetValZero)
  *   SetPrimitive_Gradient_LS      -> rx_grad_lsq                 (solver_direct_reactive.cpp:4887-5050)
+ *   SetPrimitive_Gradient_GG      -> rx_grad_gg                  (solver_direct_reactive.cpp:4784-4880)
  *   SetPrimitive_Limiter          -> rx_limiter_venkat           (:1328-1523; Venkatakrishnan or Barth-Jespersen by rx_cfg.slope_limiter)
  *   SetTime_Step                  -> rx_time_step                (:5057-5298)
  *   Upwind_Residual               -> rx_edge_flux_conv           (:2535-2785)  throws "NaN found in the upwind residual"
@@ -73,6 +74,12 @@ class ReactiveNSSolver {
   // ---- phases, reference names
   void Preprocessing() { check(rx_residual_zero(ctx_), "Preprocessing"); }
   void SetPrimitive_Gradient_LS() { check(rx_grad_lsq(ctx_), "SetPrimitive_Gradient_LS"); }
+  void SetPrimitive_Gradient_GG() { check(rx_grad_gg(ctx_), "SetPrimitive_Gradient_GG"); }
+  // CReactiveNSSolver::Preprocessing's choice by NUM_METHOD_GRAD (solver_direct_reactive.cpp:4714-4718)
+  void SetPrimitive_Gradient() {
+    if (cfg_.grad_method == RX_GRAD_GREEN_GAUSS) SetPrimitive_Gradient_GG();
+    else SetPrimitive_Gradient_LS();
+  }
   void SetPrimitive_Limiter() { check(rx_limiter_venkat(ctx_), "SetPrimitive_Limiter"); }
   void SetTime_Step() { check(rx_time_step(ctx_), "SetTime_Step"); }
   void SetStrainMag() { check(rx_strain_mag(ctx_), "SetStrainMag"); }
@@ -195,7 +202,7 @@ inline std::vector<double> Iterate(ReactiveNSSolver& flow, TurbSSTSolver& turb, 
   const rx_cfg& cfg = flow.config();
   auto preprocess = [&](bool output) {
     flow.SetPrimitive_Variables(ext_iter);
-    flow.SetPrimitive_Gradient_LS();
+    flow.SetPrimitive_Gradient();
     flow.SetStrainMag();
     if (cfg.spatial_order == 2 && !output) flow.SetPrimitive_Limiter();
   };

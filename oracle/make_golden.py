@@ -319,6 +319,18 @@ def case_it9():
     return a
 
 
+def case_gg9():
+    """case_it9 with NUM_METHOD_GRAD= GREEN_GAUSS (CReactiveEulerSolver::SetPrimitive_Gradient_GG and
+    CTurbSolver::SetSolution_Gradient_GG in place of the least-squares gradients): 2 outer iterations, ILU0."""
+    pts, quads, U, writer = mini9_inputs()
+    wd = make_workdir("gg9", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0", extra="NUM_METHOD_GRAD= GREEN_GAUSS\n%")
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--iters", "2"])
+    a.update(mech_arrays())
+    a["grad_method"] = np.array("GREEN_GAUSS")
+    return a
+
+
 def case_rst9():
     """The reference's own restart file (next-4): one reference outer iteration on the mini9 jet, then COutput's
     MergeCoordinates / MergeSolution / SetRestart (output_structure.cpp:3858-4060, the CDriver output step), as
@@ -785,7 +797,7 @@ def main():
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
              "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
-             "bj9": case_bj9}[case]()
+             "bj9": case_bj9, "gg9": case_gg9}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

@@ -177,6 +177,33 @@ def grad_lsq(mech, nDim, pts, coord, V, nbr_ptr, nbr, out=None):
 
 
 @_keepalive
+def grad_gg(mech, nDim, mesh, V):
+    """CReactiveNSSolver::SetPrimitive_Gradient_GG (solver_direct_reactive.cpp:4784-4880) over all points."""
+    N = len(mesh["coord"])
+    nG = mech.ns + nDim + 2
+    g = np.zeros((N, nG, nDim))
+    bv = np.asarray(mesh["bvertex"])
+    lib().orc_grad_gg(mech.h, C.c_int(nDim), C.c_int64(N), C.c_int64(len(mesh["edges"])), _p(mesh["edges"], np.int64),
+                      _p(mesh["edge_normal"]), C.c_int64(len(bv)), _p(np.ascontiguousarray(bv[:, 1]), np.int64),
+                      _p(mesh["bvertex_normal"]), _p(mesh["volume"]), _p(V), g.ctypes.data_as(C.c_void_p))
+    return g
+
+
+@_keepalive
+def sol_grad_gg(nDim, mesh, sol):
+    """CSolver::SetSolution_Gradient_GG (solver_structure.cpp:519-578) of an [N][nVar] solution."""
+    sol = np.ascontiguousarray(sol, dtype=np.float64)
+    N, nv = sol.shape
+    g = np.zeros((N, nv, nDim))
+    bv = np.asarray(mesh["bvertex"])
+    lib().orc_sol_grad_gg(C.c_int(nDim), C.c_int(nv), C.c_int64(N), C.c_int64(len(mesh["edges"])),
+                          _p(mesh["edges"], np.int64), _p(mesh["edge_normal"]), C.c_int64(len(bv)),
+                          _p(np.ascontiguousarray(bv[:, 1]), np.int64), _p(mesh["bvertex_normal"]), _p(mesh["volume"]),
+                          _p(sol), _f(g))
+    return g
+
+
+@_keepalive
 def limiter_venkat(nDim, ns, edges, coord, V, grad, ref_len, coeff):
     N = len(coord)
     lim = np.zeros((N, nDim + 2))
@@ -584,6 +611,7 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
             integration_time.cpp:144-183) —, then Preprocessing(Output = true) on the updated solution;
       SST   Preprocessing (gradient), Space_Integration (loops + BCs), ImplicitEuler_Iteration (cfg["sst_prec"] ILU0 or
             LU-SGS), Postprocessing.
+    cfg["grad"] "lsq" (default) / "gg": NUM_METHOD_GRAD's weighted least squares or Green-Gauss, flow and SST.
     s: state dict (U, V, Uold, T = (k, omega), TG, F1, F2, CDkw, mut) — returned updated with the iteration's
     RMS (rms, sst_rms) and linear-solver counts. bc: dict(marker, prm) of the golden's bc_marker / oracle bc_prm.
     keep=False drops the copies of the loop-only system kept for the tests (bench.py's CPU baseline)."""
@@ -593,6 +621,10 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     rp, col = pattern
     vol = mesh["volume"]
     sig = np.full(N, 0.85)  # CTurbSSTVariable::Get_Sigmak = constants[0]
+    gg = cfg.get("grad", "lsq") == "gg"  # NUM_METHOD_GRAD (flow Preprocessing, SST Preprocessing / Postprocessing)
+
+    def sol_grad(T_):
+        return sol_grad_gg(nDim, mesh, T_) if gg else sol_grad_ls(nDim, mesh["coord"], T_, mesh["nbr_ptr"], mesh["nbr"])
 
     def preprocess(U, V, Uold, T, mut):
         prm = list(cfg["p2v"])
@@ -600,7 +632,10 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         o = set_primitive(mech, nDim, U, V, T[:, 0].copy(), mut, prm, Uold=Uold)
         if o["nonphys"] < 0:
             raise PrimitiveFailure(np.flatnonzero(o["fail"]))
-        G = grad_lsq(mech, nDim, np.arange(N), mesh["coord"], o["V"], mesh["nbr_ptr"], mesh["nbr"])
+        if gg:  # NUM_METHOD_GRAD = GREEN_GAUSS (solver_direct_reactive.cpp:4717)
+            G = grad_gg(mech, nDim, mesh, o["V"])
+        else:
+            G = grad_lsq(mech, nDim, np.arange(N), mesh["coord"], o["V"], mesh["nbr_ptr"], mesh["nbr"])
         return o, G, strain_mag(nDim, G)
 
     T, TG, mut = s["T"], s["TG"], s["mut"]
@@ -674,7 +709,7 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     V2 = o2["V"]
     rho = np.ascontiguousarray(V2[:, nDim + 2])
     # SST SingleGrid_Iteration
-    TG0 = sol_grad_ls(nDim, mesh["coord"], T, mesh["nbr_ptr"], mesh["nbr"])
+    TG0 = sol_grad(T)
     ru, Jui, Juj = sst_upwind(nDim, mesh["edges"], mesh["edge_normal"], V2, T)
     rv2, Jvi2, Jvj2 = sst_visc(nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], V2, T, TG0, s["F1"], o2["mu"],
                                o2["eddy"])
@@ -701,7 +736,7 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
                             part_ptr=part_ptr)
     Tn = sst_update(T, x2.ravel(), cfg.get("relaxation_turb", 1.0), rho, np.ascontiguousarray(Uold[:, 0]))
     sst_rms = np.maximum(1e-32, np.sqrt(np.sum(rhs2 * rhs2, axis=0) / N))
-    TG1 = sol_grad_ls(nDim, mesh["coord"], Tn, mesh["nbr_ptr"], mesh["nbr"])
+    TG1 = sol_grad(Tn)
     F1n, F2n, CDn, mutn = sst_blending(nDim, Tn, TG1, rho, o2["mu"], mesh["wall_distance"], strain2)
     return dict(U=Un, V=V2, Uold=Uold, T=Tn, TG=TG1, F1=F1n, F2=F2n, CDkw=CDn, mut=mutn, rms=rms, sst_rms=sst_rms,
                 lin_iters=it, sst_lin_iters=it2, dt=dt, pre=o, pre_grad=G, jac_loops=A_loops, res_loops=R_loops, sys=A, rhs=rhs, sol=x, sst_sys=A2, sst_rhs=rhs2, sst_sol=x2)

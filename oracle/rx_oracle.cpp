@@ -1411,6 +1411,75 @@ void orc_grad_lsq(void* h, int nDim, int64_t npts, const int64_t* pts, const dou
   }
 }
 
+// a12, NUM_METHOD_GRAD = GREEN_GAUSS: CReactiveNSSolver::SetPrimitive_Gradient_GG (solver_direct_reactive.cpp:
+// 4784-4880) in the reference's loop form: the edge loop (face value 0.5 (P_i + P_j) of (T, u, v(, w), P, X_s) with
+// both sides' species taken from node 0, :4812-4813; + to node 0, - to node 1), the boundary vertices in (marker,
+// vertex) order (- P_i n), then / Volume. Points [0, Nd) are updated (nPointDomain).
+void orc_grad_gg(void* h, int nDim, int64_t Nd, int64_t E, const int64_t* edges, const double* normal, int64_t NB,
+                 const int64_t* bpoint, const double* bnormal, const double* vol, const double* V, double* grad) {
+  const Mech& m = *static_cast<Mech*>(h);
+  const int ns = m.ns, nG = ns + nDim + 2, nPV = ns + nDim + 5, P_P = nDim + 1, RHOS_P = nDim + 5, P_G = nDim + 1,
+            RHOS_G = nDim + 2;
+  std::vector<double> pi(nG), pj(nG), yc(ns);
+  auto prim = [&](int64_t p, int64_t q, double* out) {
+    const double* v = V + p * nPV;
+    out[0] = v[0];
+    out[P_G] = v[P_P];
+    for (int d = 0; d < nDim; ++d) out[1 + d] = v[1 + d];
+    molar_from_mass(m, V + q * nPV + RHOS_P, yc.data(), out + RHOS_G);
+  };
+  for (int64_t q = 0; q < Nd * nG * nDim; ++q) grad[q] = 0.0;
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    prim(i, i, pi.data());
+    prim(j, i, pj.data());
+    for (int v = 0; v < nG; ++v) {
+      const double avg = 0.5 * (pi[v] + pj[v]);
+      for (int d = 0; d < nDim; ++d) {
+        const double pr = avg * normal[e * nDim + d];
+        if (i < Nd) grad[(i * nG + v) * nDim + d] += pr;
+        if (j < Nd) grad[(j * nG + v) * nDim + d] -= pr;
+      }
+    }
+  }
+  for (int64_t b = 0; b < NB; ++b) {
+    const int64_t i = bpoint[b];
+    if (i >= Nd) continue;
+    prim(i, i, pi.data());
+    for (int v = 0; v < nG; ++v)
+      for (int d = 0; d < nDim; ++d) grad[(i * nG + v) * nDim + d] -= pi[v] * bnormal[b * nDim + d];
+  }
+  for (int64_t i = 0; i < Nd; ++i)
+    for (int q = 0; q < nG * nDim; ++q) grad[i * nG * nDim + q] = grad[i * nG * nDim + q] / vol[i];
+}
+
+// CSolver::SetSolution_Gradient_GG (solver_structure.cpp:519-578) of an [N][nVar] solution (the SST's (k, omega)):
+// edge loop, boundary vertices of every marker, / (Volume + EPS).
+void orc_sol_grad_gg(int nDim, int nVar, int64_t Nd, int64_t E, const int64_t* edges, const double* normal,
+                     int64_t NB, const int64_t* bpoint, const double* bnormal, const double* vol, const double* sol,
+                     double* grad) {
+  for (int64_t q = 0; q < Nd * nVar * nDim; ++q) grad[q] = 0.0;
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    for (int v = 0; v < nVar; ++v) {
+      const double avg = 0.5 * (sol[i * nVar + v] + sol[j * nVar + v]);
+      for (int d = 0; d < nDim; ++d) {
+        const double pr = avg * normal[e * nDim + d];
+        if (i < Nd) grad[(i * nVar + v) * nDim + d] += pr;
+        if (j < Nd) grad[(j * nVar + v) * nDim + d] -= pr;
+      }
+    }
+  }
+  for (int64_t b = 0; b < NB; ++b) {
+    const int64_t i = bpoint[b];
+    if (i >= Nd) continue;
+    for (int v = 0; v < nVar; ++v)
+      for (int d = 0; d < nDim; ++d) grad[(i * nVar + v) * nDim + d] -= sol[i * nVar + v] * bnormal[b * nDim + d];
+  }
+  for (int64_t i = 0; i < Nd; ++i)
+    for (int q = 0; q < nVar * nDim; ++q) grad[i * nVar * nDim + q] = grad[i * nVar * nDim + q] / (vol[i] + EPS);
+}
+
 // a13: Venkatakrishnan limiter (solver_direct_reactive.cpp:1328-1523), edge-loop form.
 void orc_limiter_venkat(int nDim, int ns, int64_t N, int64_t E, const int64_t* edges, const double* coord,
                         const double* V, const double* grad, double ref_len, double lim_coeff, double* lim) {

@@ -67,6 +67,23 @@ def test_gradient_and_limiter(case):
     s.close()
 
 
+@pytest.mark.parametrize("case", ["mini9", "mini3d"])
+def test_gradient_green_gauss(case):
+    """NUM_METHOD_GRAD= GREEN_GAUSS: CReactiveNSSolver::SetPrimitive_Gradient_GG (solver_direct_reactive.cpp:
+    4784-4880, node 0's species on both sides of an edge, / Volume) against the oracle's edge-loop restatement
+    (the device accumulates each point's edges in edge order, then its boundary vertices in marker order), and
+    the SST's SetSolution_Gradient_GG (solver_structure.cpp:519-578, / (Volume + EPS)) of (k, omega)."""
+    g = golden(case)
+    s, (nDim, nVar, nPV, nG, ns) = make_solver(g, implicit=False)
+    N = len(g["V"])
+    s.SetPrimitive_Gradient_GG()
+    s.sync()
+    G = s.download("GRAD").reshape(N, nG, nDim)
+    ref = O.grad_gg(O.Mechanism(g), nDim, g, g["V"])
+    per_column_close(G.reshape(N, -1), ref.reshape(N, -1), rtol=1e-13, what="Green-Gauss gradient (HIP vs oracle)")
+    s.close()
+
+
 @pytest.mark.parametrize("case", ["bj9", "muscl3d", "jet9w"])
 def test_limiter_barth(case):
     """a13 Barth-Jespersen branch on the device: bitwise against the reference's own limiter (bj9, 2-D,

@@ -255,7 +255,7 @@ def test_case_from_cfg_defaults_and_rejections(tmp_path):
 REJECTED = [  # (key, value): physics / numerics this path does not build (VERDICT r03 missing #3), None = key removed
     ("PHYSICAL_PROBLEM", "REACTIVE_EULER"), ("PHYSICAL_PROBLEM", None), ("PHYSICAL_PROBLEM", "NAVIER_STOKES"),
     ("KIND_TURB_MODEL", "SA"), ("KIND_TURB_MODEL", "NONE"), ("KIND_TURB_MODEL", None),
-    ("NUM_METHOD_GRAD", "GREEN_GAUSS"), ("LINEAR_SOLVER", "BCGSTAB"), ("LINEAR_SOLVER", "RESTARTED_FGMRES"),
+    ("NUM_METHOD_GRAD", "LEAST_SQUARES"), ("LINEAR_SOLVER", "BCGSTAB"), ("LINEAR_SOLVER", "RESTARTED_FGMRES"),
     ("CONV_NUM_METHOD_FLOW", "ROE"), ("CONV_NUM_METHOD_FLOW", None), ("CONV_NUM_METHOD_TURB", "JST"),
     ("SPATIAL_ORDER_TURB", "2ND_ORDER"), ("TIME_DISCRE_TURB", "EULER_EXPLICIT"),
     ("UNSTEADY_SIMULATION", "DUAL_TIME_STEPPING-2ND_ORDER"), ("MATH_PROBLEM", "CONTINUOUS_ADJOINT")]
@@ -300,6 +300,18 @@ def test_case_from_cfg_keys_at_their_defaults_pass(tmp_path):
     with open(os.path.join(wd, "case.cfg"), "w") as f:
         f.write(txt)
     rx.case_from_cfg(os.path.join(wd, "case.cfg"))["mesh"].close()
+
+
+def test_case_from_cfg_gradient_method(tmp_path):
+    """NUM_METHOD_GRAD selects the flow's SetPrimitive_Gradient_GG / _LS (solver_direct_reactive.cpp:4717) and the
+    SST's SetSolution_Gradient_GG / _LS (solver_direct_turbulent.cpp:2944-2945, 2963-2970) alike."""
+    wd, base = _jet_cfg(tmp_path)
+    for val, want in (("WEIGHTED_LEAST_SQUARES", 0), ("GREEN_GAUSS", 1), (None, 0)):
+        with open(os.path.join(wd, "case.cfg"), "w") as f:
+            f.write(_with_key(base, "NUM_METHOD_GRAD", val))
+        case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+        assert case["flow_cfg"]["grad_method"] == want and case["sst_cfg"]["grad_method"] == want, val
+        case["mesh"].close()
 
 
 def test_case_from_cfg_mach_follows_console_verbosity(tmp_path):

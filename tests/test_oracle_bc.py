@@ -39,7 +39,7 @@ def bc9(request):
     return bc_case(request.param)
 
 
-@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit"])
+@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9"])
 def it9(request):
     return golden(request.param)
 
@@ -107,6 +107,8 @@ def iteration_cfg(g):
     cfg["sst_prec"] = "lusgs" if ("lin_prec" in g and str(g["lin_prec"]) == "LU_SGS") else "ilu"
     cfg["flow_prec"] = cfg["sst_prec"]  # LINEAR_SOLVER_PREC serves both solvers
     cfg["spatial_order"] = int(g["spatial_order"]) if "spatial_order" in g else 0
+    if "grad_method" in g and str(g["grad_method"]) == "GREEN_GAUSS":  # NUM_METHOD_GRAD (gg9)
+        cfg["grad"] = "gg"
     if "ignition" in g:  # IGNITION, IGNITION_ITER, IGNITION_TEMPERATURE, FUEL_INDEX, OXIDIZER_INDEX (ig9)
         cfg["p2v"] = list(cfg["p2v"]) + [float(x) for x in g["ignition"]]
     bc = dict(marker=g["bc_marker"], prm=O.bc_prm(bp, g["mach_inf"][0], g["visc_params"][1], g["visc_params"][2]))
