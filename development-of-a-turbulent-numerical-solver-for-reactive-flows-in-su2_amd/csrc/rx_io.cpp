@@ -25,7 +25,7 @@ struct ElemType {
   int faces[6][4];
   int nnodes_face[6];
   int nneigh[8];
-  int neigh[8][3];
+  int neigh[8][4];
 };
 const ElemType kLine = {3, 2, 1, {{0, 1}}, {2}, {1, 1}, {{1}, {0}}};
 const ElemType kTri = {5, 3, 3, {{0, 1}, {1, 2}, {2, 0}}, {2, 2, 2}, {2, 2, 2}, {{1, 2}, {2, 0}, {0, 1}}};
@@ -37,6 +37,14 @@ const ElemType kHex = {12, 8, 6,
                        {{0, 1, 5, 4}, {1, 2, 6, 5}, {2, 3, 7, 6}, {3, 0, 4, 7}, {0, 3, 2, 1}, {4, 5, 6, 7}},
                        {4, 4, 4, 4, 4, 4}, {3, 3, 3, 3, 3, 3, 3, 3},
                        {{1, 3, 4}, {0, 2, 5}, {1, 3, 6}, {0, 2, 7}, {0, 5, 7}, {4, 6, 1}, {2, 5, 7}, {4, 3, 6}}};
+// CPrism / CPyramid (primal_grid_structure.cpp:478-494, 566-582): the triangular faces of a prism and the
+// triangular faces of a pyramid carry a repeated fourth entry the face loops never reach (nNodesFace = 3)
+const ElemType kPrism = {13, 6, 5, {{3, 4, 1, 0}, {5, 2, 1, 4}, {2, 5, 3, 0}, {0, 1, 2, 2}, {5, 4, 3, 3}},
+                         {4, 4, 4, 3, 3}, {3, 3, 3, 3, 3, 3},
+                         {{1, 2, 3}, {0, 2, 4}, {1, 0, 5}, {0, 4, 5}, {3, 5, 1}, {4, 3, 2}}};
+const ElemType kPyramid = {14, 5, 5, {{0, 3, 2, 1}, {4, 3, 0, 0}, {4, 0, 1, 1}, {2, 4, 1, 1}, {3, 4, 2, 2}},
+                           {4, 3, 3, 3, 3}, {3, 3, 3, 3, 4},
+                           {{1, 3, 4, 4}, {0, 2, 4, 4}, {1, 3, 4, 4}, {2, 0, 4, 4}, {0, 1, 2, 3}}};
 // boundary triangles / quadrilaterals of a 3-D mesh use the 2-D element tables (CTriangle / CQuadrilateral)
 
 const ElemType* elem_type(int vtk) {
@@ -46,6 +54,8 @@ const ElemType* elem_type(int vtk) {
     case 9: return &kQuad;
     case 10: return &kTet;
     case 12: return &kHex;
+    case 13: return &kPrism;
+    case 14: return &kPyramid;
     default: return nullptr;
   }
 }
@@ -392,6 +402,22 @@ double orient3(const double* c1, const double* c2, const double* c3, const doubl
   return n[0] * c[0] + n[1] * c[1] + n[2] * c[2];
 }
 
+// The prism test of Check_IntElem_Orientation (geometry_structure.cpp:8641-8684): a = (B - A)/2, b = (C - A)/2,
+// c = (D0 - E0) + (D1 - E1) + (D2 - E2) (the three edges joining the triangles), test (a x b) . c.
+double orient_prism(const double* A, const double* B, const double* Cc, const double* const D[3],
+                    const double* const Ee[3]) {
+  double a[3], b[3], c[3], n[3];
+  for (int d = 0; d < 3; ++d) {
+    a[d] = 0.5 * (B[d] - A[d]);
+    b[d] = 0.5 * (Cc[d] - A[d]);
+    c[d] = (D[0][d] - Ee[0][d]) + (D[1][d] - Ee[1][d]) + (D[2][d] - Ee[2][d]);
+  }
+  n[0] = a[1] * b[2] - b[1] * a[2];
+  n[1] = -(a[0] * b[2] - b[0] * a[2]);
+  n[2] = a[0] * b[1] - b[0] * a[1];
+  return n[0] * c[0] + n[1] * c[1] + n[2] * c[2];
+}
+
 // Change_Orientation of each element kind (primal_grid_structure.cpp)
 void change_orientation(Elem& e) {
   switch (e.t->vtk) {
@@ -405,6 +431,11 @@ void change_orientation(Elem& e) {
       for (int k = 0; k < 8; ++k) e.n[k] = o[map[k]];
       break;
     }
+    case 13:  // CPrism (primal_grid_structure.cpp:548-560)
+      std::swap(e.n[0], e.n[1]);
+      std::swap(e.n[3], e.n[4]);
+      break;
+    case 14: break;  // CPyramid::Change_Orientation only prints "Not defined orientation change" (:622)
   }
 }
 
@@ -426,6 +457,12 @@ void check_orientation(rx_mesh& m) {
     } else if (e.t->vtk == 12) {
       flip = orient3(X(n[0]), X(n[1]), X(n[2]), X(n[5])) < 0.0 || orient3(X(n[2]), X(n[3]), X(n[0]), X(n[7])) < 0.0 ||
              orient3(X(n[1]), X(n[2]), X(n[3]), X(n[6])) < 0.0 || orient3(X(n[3]), X(n[0]), X(n[1]), X(n[4])) < 0.0;
+    } else if (e.t->vtk == 13) {
+      const double* lo[3] = {X(n[0]), X(n[1]), X(n[2])};
+      const double* up[3] = {X(n[3]), X(n[4]), X(n[5])};
+      flip = orient_prism(lo[0], lo[2], lo[1], up, lo) < 0.0 || orient_prism(up[0], up[1], up[2], lo, up) < 0.0;
+    } else if (e.t->vtk == 14) {
+      flip = orient3(X(n[0]), X(n[1]), X(n[2]), X(n[4])) < 0.0 || orient3(X(n[2]), X(n[3]), X(n[0]), X(n[4])) < 0.0;
     }
     if (flip) change_orientation(e);
   }
@@ -537,14 +574,9 @@ int rx_mesh_read_su2(const char* path, rx_mesh** out) {
       for (int64_t e = 0; e < nelem; ++e) {
         if (!std::getline(f, line)) return fail(RX_ERR_STATE);
         std::istringstream is(line);
-        {
-          std::istringstream peek(line);
-          int vt = 0;
-          if ((peek >> vt) && (vt == 13 || vt == 14)) return fail(RX_ERR_UNSUPPORTED);  // prism / pyramid
-        }
         if (!read_elem(is, &m->elems[e])) return fail(RX_ERR_ARG);
         const int vtk = m->elems[e].t->vtk;
-        if ((m->nDim == 2) != (vtk == 5 || vtk == 9)) return fail(RX_ERR_ARG);
+        if ((m->nDim == 2) != (vtk == 5 || vtk == 9) || vtk == 3) return fail(RX_ERR_ARG);
       }
     } else if (keyword(line, "NPOIN=", &v)) {
       npoin = std::atoll(v.c_str());  // "NPOIN= n [n_domain]": a serial mesh has every point in its domain
@@ -574,7 +606,7 @@ int rx_mesh_read_su2(const char* path, rx_mesh** out) {
           std::istringstream is(line);
           if (!read_elem(is, &m->bound.back()[e])) return fail(RX_ERR_ARG);
           const int vtk = m->bound.back()[e].t->vtk;
-          if ((m->nDim == 2) != (vtk == 3)) return fail(RX_ERR_ARG);
+          if (m->nDim == 2 ? vtk != 3 : (vtk != 5 && vtk != 9)) return fail(RX_ERR_ARG);
         }
       }
     }
@@ -587,6 +619,17 @@ int rx_mesh_read_su2(const char* path, rx_mesh** out) {
     for (const Elem& e : bm)
       for (int a = 0; a < e.t->nnodes; ++a)
         if (e.n[a] < 0 || e.n[a] >= m->N) return fail(RX_ERR_STATE);
+  // CPhysicalGeometry(geometry, config), the partitioned copy the driver solves on (geometry_structure.cpp:2960-3080,
+  // 4128-4150), stores the elements grouped by kind — triangles, quadrilaterals, tetrahedra, hexahedra, prisms,
+  // pyramids — and each marker's boundary elements as lines, triangles, quadrilaterals, file order within a kind;
+  // the point connectivity (and so the RCM order and the edge numbering) follows that order
+  auto rank = [](int vtk) {
+    const int order[] = {3, 5, 9, 10, 12, 13, 14};
+    return (int)(std::find(order, order + 7, vtk) - order);
+  };
+  auto by_kind = [&](const Elem& a, const Elem& b) { return rank(a.t->vtk) < rank(b.t->vtk); };
+  std::stable_sort(m->elems.begin(), m->elems.end(), by_kind);
+  for (auto& bm : m->bound) std::stable_sort(bm.begin(), bm.end(), by_kind);
   preprocess(*m);
   *out = m;
   return RX_OK;

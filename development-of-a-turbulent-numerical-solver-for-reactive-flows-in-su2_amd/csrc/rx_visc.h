@@ -12,6 +12,10 @@
 
 #include "rx_device.h"
 
+#ifndef RX_VISC_PROBE
+#define RX_VISC_PROBE 0
+#endif
+
 namespace rx {
 
 struct ViscParams {
@@ -436,7 +440,12 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     double nG[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) nG[s] = -Gxn[s];
+#if RX_VISC_PROBE & 1  // timing probe (build variant only): no Stefan-Maxwell solve
+#pragma unroll
+    for (int s = 0; s < NS; ++s) Jd[s] = nG[s] * Gt[s * NS + s];
+#else
     bicgstab<NS>(Gt, nG, Jd, 1.0e-11);
+#endif
   }
   {
     double ones[NS];
@@ -485,7 +494,14 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
       for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int d = 0; d < NDIM; ++d) rhs[s][d] = G[RHOS_A + s][d];
+#if RX_VISC_PROBE & 2  // timing probe (build variant only): no closure QR solve
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) MG[s][d] = rhs[s][d] * Mt[s * NS + s];
+#else
       colpiv_qr_solve<NS, NDIM>(Mt, rhs, MG);
+#endif
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s)

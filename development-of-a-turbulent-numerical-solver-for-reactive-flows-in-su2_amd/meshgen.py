@@ -81,6 +81,76 @@ def jet_mesh3d(nx: int, ny: int, nz: int, depth=0.003, **kw):
     return pts, hexes, bnd
 
 
+def _orient3(c1, c2, c3, c4):
+    """The tetrahedral orientation test of Check_IntElem_Orientation (geometry_structure.cpp:8542-8794)."""
+    a, b, c = 0.5 * (c2 - c1), 0.5 * (c3 - c1), c4 - c1
+    n = np.array([a[1] * b[2] - b[1] * a[2], -(a[0] * b[2] - b[0] * a[2]), a[0] * b[1] - b[0] * a[1]])
+    return float(n @ c)
+
+
+def mixed_mesh3d(nx: int, ny: int, nz: int, **kw):
+    """jet_mesh3d with every element kind of the 3-D SU2 reader: the columns of 2-D cells q with q % 3 == 1 are
+    split along the bottom-face diagonal (node 0 - node 2) into two prisms (VTK 13) per layer, whose z-plane faces
+    become boundary triangles (VTK 5); in the other columns, the cells with (q + k) % 4 == 2 become six pyramids
+    (VTK 14) on the hexahedron's faces around an added centroid point, each base ordered so that the reference's
+    pyramid test passes (CPyramid::Change_Orientation does nothing); the rest stay hexahedra. Returns pts,
+    elems = [(vtk, nodes)], bnd = {marker: [(vtk, nodes)]}."""
+    pts, hexes, bnd = jet_mesh3d(nx, ny, nz, **kw)
+    nq = len(hexes) // (nz - 1)
+    extra, elems = [], []
+    n0 = len(pts)
+    for c, h in enumerate(hexes):
+        k, q = divmod(c, nq)
+        if q % 3 == 1:
+            elems.append((13, [h[0], h[1], h[2], h[4], h[5], h[6]]))
+            elems.append((13, [h[0], h[2], h[3], h[4], h[6], h[7]]))
+        elif (q + k) % 4 == 2:
+            apex = n0 + len(extra)
+            extra.append(pts[h].mean(axis=0))
+            X = lambda p: pts[p] if p < n0 else extra[p - n0]  # noqa: E731
+            for f in HEX_FACES:
+                b = [int(h[v]) for v in f]
+                if _orient3(X(b[0]), X(b[1]), X(b[2]), X(apex)) < 0 or _orient3(X(b[2]), X(b[3]), X(b[0]), X(apex)) < 0:
+                    b = [b[0], b[3], b[2], b[1]]
+                assert _orient3(X(b[0]), X(b[1]), X(b[2]), X(apex)) >= 0 and _orient3(X(b[2]), X(b[3]), X(b[0]), X(apex)) >= 0
+                elems.append((14, b + [apex]))
+        else:
+            elems.append((12, [int(v) for v in h]))
+    pts = np.concatenate([pts, np.asarray(extra).reshape(-1, 3)])
+    out = {}
+    for name, quads in bnd.items():
+        lst = []
+        for qi, qd in enumerate(quads):
+            qd = [int(v) for v in qd]
+            if name in ("sym_back", "sym_front") and qi % 3 == 1:
+                if name == "sym_back":  # (q0, q1, q2, q3): diagonal q0 - q2
+                    lst += [(5, [qd[0], qd[1], qd[2]]), (5, [qd[0], qd[2], qd[3]])]
+                else:  # reversed (q3, q2, q1, q0) + offset: the same diagonal
+                    lst += [(5, [qd[1], qd[2], qd[3]]), (5, [qd[3], qd[0], qd[1]])]
+            else:
+                lst.append((9, qd))
+        out[name] = lst
+    return pts, elems, out
+
+
+def write_su2_mixed(path: str, pts, elems, bnd):
+    """SU2 native mesh file of a mesh with element kinds given per element: elems = [(vtk, nodes)], bnd = {marker:
+    [(vtk, nodes)]} in marker order."""
+    with open(path, "w") as f:
+        f.write(f"NDIME= {pts.shape[1]}\n")
+        f.write(f"NELEM= {len(elems)}\n")
+        for k, (t, nodes) in enumerate(elems):
+            f.write(f"{t} " + " ".join(str(int(v)) for v in nodes) + f" {k}\n")
+        f.write(f"NPOIN= {len(pts)}\n")
+        for k, p in enumerate(pts):
+            f.write(" ".join(f"{c:.17g}" for c in p) + f" {k}\n")
+        f.write(f"NMARK= {len(bnd)}\n")
+        for name, lst in bnd.items():
+            f.write(f"MARKER_TAG= {name}\nMARKER_ELEMS= {len(lst)}\n")
+            for t, nodes in lst:
+                f.write(f"{t} " + " ".join(str(int(v)) for v in nodes) + "\n")
+
+
 def median_dual3d(pts, hexes, bnd):
     """3-D median dual of a hexahedral mesh, vectorised restatement of CPhysicalGeometry::SetControlVolume
     (geometry_structure.cpp:10457-10560, 3-D branch): for every face edge (i, j) of every element the triangle

@@ -25,13 +25,14 @@
  *                      EXT_ITER trailer.
  *   rx_restart_read    CReactiveEulerSolver::Load_Restart (solver_direct_reactive.cpp:566-686) + the SST
  *                      solver's restart columns (solver_direct_turbulent.cpp:2838-2850).
- *                      Prisms (VTK 13) and pyramids (VTK 14), which the reference reads, are not supported here:
- *                      rx_mesh_read_su2 returns RX_ERR_UNSUPPORTED for them.
+ *                      Elements: triangles / quadrilaterals (2-D), tetrahedra, hexahedra, prisms (VTK 13) and
+ *                      pyramids (VTK 14) with the reference's tables (primal_grid_structure.cpp:478-622) and its
+ *                      orientation tests (geometry_structure.cpp:8641-8794; a pyramid is never re-oriented:
+ *                      CPyramid::Change_Orientation only prints); boundary lines (2-D), triangles / quads (3-D).
  *                      rx_mech_read rejects (RX_ERR_STATE) a property table that is not sorted, unique and
  *                      equispaced, as SetSpline's assertions do (spline.cpp:12-25): GetSpline locates the interval
  *                      by integer division.
- * Errors: RX_ERR_ARG (bad argument / malformed element line), RX_ERR_UNSUPPORTED (an element type listed above as
- * unsupported), RX_ERR_STATE (unreadable or malformed file; the reference exits). Points of an rx_mesh are in the reference's RCM order; global_index maps them to the file.
+ * Errors: RX_ERR_ARG (bad argument / malformed or unknown element line), RX_ERR_STATE (unreadable or malformed file; the reference exits). Points of an rx_mesh are in the reference's RCM order; global_index maps them to the file.
  */
 #ifndef RX_IO_H
 #define RX_IO_H

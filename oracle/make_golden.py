@@ -432,6 +432,42 @@ def case_it3d():
     return a
 
 
+def mix3d_inputs():
+    """mini3d's extruded jet and state recipe on meshgen.mixed_mesh3d: prisms, pyramids (around added centroid points)
+    and hexahedra, boundary triangles and quadrilaterals."""
+    nx, ny, nz = MINI3D
+    pts, elems, bnd = meshgen.mixed_mesh3d(nx, ny, nz)
+    xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
+    from scipy.spatial import cKDTree
+    scale = np.array([1.0 / 0.125, 1.0 / 0.006])
+    _, idx = cKDTree(xy * scale).query(pts[:, :2] * scale)
+    c2 = cons[idx]
+    depth = pts[:, 2].max()
+    w = 0.8 * np.sin(np.pi * pts[:, 2] / depth) * np.sin(np.pi * pts[:, 0] / 0.125)
+    rho = c2[:, 0]
+    U = np.c_[c2[:, :3], rho * w, c2[:, 3] + 0.5 * rho * w * w, c2[:, 4:]]
+
+    def writer(wd):
+        meshgen.write_su2_mixed(os.path.join(wd, "mesh.su2"), pts, elems, bnd)
+        return "mesh.su2"
+
+    return pts, elems, U, writer
+
+
+def case_mix3d():
+    """The SU2 reader's prism / pyramid branches (geometry_structure.cpp:8641-8794 orientation, the CPrism / CPyramid
+    tables of primal_grid_structure.cpp:478-622 in the connectivity and the median dual) on a mixed-element mesh, and
+    two whole reference outer iterations on it (ILU0). CFL 1: at mini3d's CFL 5 this start's FGMRES(5)+ILU0 solve
+    on the mixed mesh is chaotic (reordering the inner products alone moves U by 16 %, the c2b mechanism of
+    DESIGN.md §2), at CFL 1 the same perturbation moves it by 4e-15."""
+    pts, elems, U, writer = mix3d_inputs()
+    wd = make_workdir("mix3d", writer, cfl=1.0, order="1ST_ORDER", prec="ILU0", extra=SYM3D)
+    write_state(wd, U)
+    a = run_harness(wd, bsr=False, extra=["--iters", "2"])
+    a.update(mech_arrays())
+    return a
+
+
 def case_muscl3d():
     """a2 MUSCL branch + a13 Venkatakrishnan limiter in 3-D: the mini3d state with 2ND_ORDER_LIMITER (the
     jet9w dumps on the extruded jet: whole-loop residual, a sample of Jacobian rows, limiter, records)."""
@@ -797,7 +833,7 @@ def main():
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
              "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
-             "bj9": case_bj9, "gg9": case_gg9}[case]()
+             "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

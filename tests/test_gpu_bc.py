@@ -185,7 +185,7 @@ def n_iters(g):
     return sum(1 for k in g if k.startswith("it") and k.endswith("_U") and k[2:-2].isdigit())
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d"])
 def test_outer_iterations_vs_reference(case):
     """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d / it7: 2, itx9 /
     itx4: 1) on the device, started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within
@@ -223,7 +223,7 @@ def test_free_running_iterations_vs_reference(case):
     s.close()
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d"])
 def test_outer_iteration_vs_oracle_device_order(case):
     """One iteration against the oracle run with the device's inner-product order: the residual side and the
     Krylov recurrence then agree to the Stefan-Maxwell rounding only (amplified by FGMRES: the same 1e-10 bar)."""

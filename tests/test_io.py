@@ -383,20 +383,37 @@ def test_case_from_cfg_matches_the_reference_setup(tmp_path):
     case["mesh"].close()
 
 
+def test_su2_reader_prisms_and_pyramids(tmp_path):
+    """Every 3-D element kind of the reference's reader: meshgen.mixed_mesh3d (prism columns with boundary
+    triangles, pyramids around added centroids, hexahedra) read by the reference itself (golden mix3d) and by
+    rx_mesh_read_su2 — RCM order, edges, dual normals and volumes, boundary vertices, wall distance — bitwise."""
+    nx, ny, nz = 13, 7, 4
+    pts, el, bnd = meshgen.mixed_mesh3d(nx, ny, nz)
+    kinds = {t for t, _ in el}
+    assert kinds == {12, 13, 14} and {t for lst in bnd.values() for t, _ in lst} == {5, 9}
+    path = str(tmp_path / "mix.su2")
+    meshgen.write_su2_mixed(path, pts, el, bnd)
+    m = rx.SU2Mesh(path, walls=WALLS)
+    check_geometry(m, golden("mix3d"))
+    m.close()
+
+
 def test_reader_rejections(tmp_path):
-    """Inputs the native readers refuse as the reference does (or, for element types this path does not build,
-    with RX_ERR_UNSUPPORTED): a prism in an SU2 file; a property table that is not equispaced (SetSpline's
+    """Inputs the native readers refuse as the reference does: an element line of an unknown VTK type, a boundary
+    element that is not a face of the mesh's dimension; a property table that is not equispaced (SetSpline's
     assertion, spline.cpp:12-25)."""
     pts, el, bnd = meshgen.jet_mesh3d(4, 3, 2)
-    path = str(tmp_path / "prism.su2")
+    path = str(tmp_path / "bad.su2")
     meshgen.write_su2(path, pts, el, bnd)
     txt = open(path).read().splitlines()
     k = txt.index(next(ln for ln in txt if ln.startswith("NELEM="))) + 1
-    txt[k] = "13 0 1 2 3 4 5 0"  # a prism in place of the first hexahedron
-    with open(path, "w") as f:
-        f.write("\n".join(txt) + "\n")
-    with pytest.raises(rx.RxError, match="status 9"):
-        rx.SU2Mesh(path, walls=WALLS)
+    for bad in ("7 0 1 2 3 4 5 0", "9 0 1 2 3 0"):  # polygon; a quadrilateral inside a 3-D mesh
+        t2 = list(txt)
+        t2[k] = bad
+        with open(path, "w") as f:
+            f.write("\n".join(t2) + "\n")
+        with pytest.raises(rx.RxError, match="status"):
+            rx.SU2Mesh(path, walls=WALLS)
     d = unpack(tmp_path / "files", "jet")
     fn = os.path.join(d, "Thermo", "O2_thermo.txt")
     lines = open(fn).read().splitlines()

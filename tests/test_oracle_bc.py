@@ -39,7 +39,7 @@ def bc9(request):
     return bc_case(request.param)
 
 
-@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9"])
+@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d"])
 def it9(request):
     return golden(request.param)
 
