@@ -396,7 +396,7 @@ __global__ __launch_bounds__(64) void k_bc_weak(int NW, const int32_t* __restric
   }
   double res[nVar];
   double* sm = B.implicit ? summ + (size_t)b * visc_summary_size<NS, NDIM>() : nullptr;
-  const int rc = visc_edge<NS, NDIM>(m, B.vp, a, g, sk, Normal, res, SummRef{sm, 1}, scr_all + threadIdx.x * NS * NS,
+  const int rc = visc_edge<NS, NDIM>(m, B.vp, a, g, sk, Normal, res, SummRef{sm, 1}, Scr{scr_all + threadIdx.x},
                                      false);
   bad = false;
 #pragma unroll

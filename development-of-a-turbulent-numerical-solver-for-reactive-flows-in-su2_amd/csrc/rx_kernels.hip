@@ -683,7 +683,7 @@ __global__ __launch_bounds__(64) RX_VISC_ATTR void k_visc_edge(int E, const int3
     // 1.25x, profiles/r02_pmc_c3.json); k_visc_jac stages its 16 edges' records from the tile through LDS
     const SummRef summ{P.implicit ? Summ + (size_t)(e / kSummTile) * SS * kSummTile + e % kSummTile : nullptr,
                        kSummTile};
-    const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ, scr_all + threadIdx.x * NS * NS);
+    const int rc = visc_edge<NS, NDIM>(m, P, a, b, sk, nrm, res, summ, Scr{scr_all + threadIdx.x});
     bool bad = false;
   #pragma unroll
     for (int v = 0; v < nVar; ++v) {

@@ -1641,21 +1641,6 @@ __device__ __forceinline__ void row_blocks(const double* __restrict__ F, const i
 // of three), row metadata from the schedule's slot records {i, klo, diag, khi} (one load instead of
 // rows -> klo / diag), and the first pass's slot of level l+1 loaded while level l runs. Same arithmetic,
 // operation for operation, as k_ilu_fwd_part / k_ilu_bwd_part.
-// RX_SWEEP_TOUCH (build knob): after issuing a level's rows, the lanes of each row touch one double per 128-byte
-// line of the blocks their next-level row will read (its slot record is already in registers), so those lines are
-// in the L2 when the next level starts; the touched values are folded into a dummy that is never stored (the compiler
-// waits for them at the next level's top, one level after issue). The sweeps are level-latency bound with about one
-// level's factor rows in flight per CU (DESIGN §5, r03 probes).
-#ifndef RX_SWEEP_TOUCH
-#define RX_SWEEP_TOUCH 0
-#endif
-__device__ __forceinline__ double touch_lines(const double* base, int nbytes, int a, int stride) {
-  double t = 0.0;
-  const char* p = reinterpret_cast<const char*>(base);
-  for (int q = a * 128; q < nbytes; q += stride * 128) t += *reinterpret_cast<const double*>(p + q);
-  return t;
-}
-
 template <int NV, int TB>
 __device__ __forceinline__ void fwd_wide_body(const int32_t* __restrict__ part_lvl, const int32_t* __restrict__ lvl_ptr,
                                               const int4* __restrict__ slot, const int32_t* __restrict__ col,
@@ -1668,7 +1653,6 @@ __device__ __forceinline__ void fwd_wide_body(const int32_t* __restrict__ part_l
   const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
   int4 nxt = make_int4(-1, 0, 0, 0);
   if (lane && l0 < l1 && lvl_ptr[l0] + rl < lvl_ptr[l0 + 1]) nxt = slot[lvl_ptr[l0] + rl];
-  double dummy = 0.0, touched = 0.0;
   for (int l = l0; l < l1; ++l) {
     const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
     const int4 cur = nxt;
@@ -1681,14 +1665,8 @@ __device__ __forceinline__ void fwd_wide_body(const int32_t* __restrict__ part_l
       row_blocks<NV>(F, col, x, sl.y, sl.z, a, [&](double s) { xi -= s; });
       x[(size_t)i * NV + a] = xi;
     }
-    if (RX_SWEEP_TOUCH) {
-      dummy += touched;
-      touched = 0.0;
-      if (lane && nxt.x >= 0) touched = touch_lines(F + (size_t)nxt.y * NV2, (nxt.z - nxt.y) * NV2 * 8, a, NV);
-    }
     __syncthreads();
   }
-  if (RX_SWEEP_TOUCH && dummy != dummy && l1 < 0) x[0] = dummy + touched;  // never: keeps the touches alive
 }
 
 template <int NV, int TB>
@@ -1714,16 +1692,11 @@ __device__ __forceinline__ void bwd_wide_body(const int32_t* __restrict__ part_l
   const int l0 = part_lvl[p], l1 = part_lvl[p + 1];
   int4 nxt = make_int4(-1, 0, 0, 0);
   if (lane && l0 < l1 && lvl_ptr[l0] + rl < lvl_ptr[l0 + 1]) nxt = slot[lvl_ptr[l0] + rl];
-  double dummy = 0.0, touched = 0.0;
   for (int l = l0; l < l1; ++l) {
     const int r0 = lvl_ptr[l], r1 = lvl_ptr[l + 1];
     const int4 cur = nxt;
     nxt = make_int4(-1, 0, 0, 0);
     if (lane && l + 1 < l1 && r1 + rl < lvl_ptr[l + 2]) nxt = slot[r1 + rl];
-    if (RX_SWEEP_TOUCH) {
-      dummy += touched;
-      touched = 0.0;
-    }
     for (int base = r0; base < r1; base += RPB) {
       const int r = base + rl;
       const bool act = lane && r < r1;
@@ -1753,13 +1726,9 @@ __device__ __forceinline__ void bwd_wide_body(const int32_t* __restrict__ part_l
         for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
         x[(size_t)i * NV + a] = s;
       }
-      if (RX_SWEEP_TOUCH && base + RPB >= r1 && lane && nxt.x >= 0)
-        touched = touch_lines(F + (size_t)(nxt.z + 1) * NV2, (nxt.w - nxt.z - 1) * NV2 * 8, a, NV) +
-                  touch_lines(invD + (size_t)nxt.x * NV2, NV2 * 8, a, NV);
       __syncthreads();
     }
   }
-  if (RX_SWEEP_TOUCH && dummy != dummy && l1 < 0) x[0] = dummy + touched;  // never: keeps the touches alive
 }
 
 template <int NV, int TB>

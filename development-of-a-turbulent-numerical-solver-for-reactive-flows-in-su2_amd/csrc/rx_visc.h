@@ -18,6 +18,16 @@
 
 namespace rx {
 
+// The lane's dense NS x NS matrix (Gamma, then the closure matrix) in its workgroup's LDS scratch, entry q at
+// p[q * kScrLanes]: the 64 lanes' matrices interleaved, so that a wavefront's access to one entry touches 64
+// consecutive 8-byte words (no bank conflicts; a lane-contiguous [NS*NS] slice per lane put lanes 16 apart on the
+// same bank).
+constexpr int kScrLanes = 64;
+struct Scr {
+  double* p;
+  __device__ double& operator[](int q) const { return p[q * kScrLanes]; }
+};
+
 struct ViscParams {
   double T_ref, E_ref, R_ref, Pr_t, Le_t;
   int rans, implicit;
@@ -60,7 +70,7 @@ __device__ inline double eig_dot(const double* a, const double* b) {
 
 // Eigen col-major GEMV order (4 columns at once, packet rows, odd tail row sequential), A row-major.
 template <int N>
-__device__ inline void eig_gemv(const double* A, const double* x, double* y) {
+__device__ inline void eig_gemv(const Scr A, const double* x, double* y) {
   constexpr int aligned = N & ~1, bound = (N / 4) * 4;
 #pragma unroll
   for (int i = 0; i < N; ++i) y[i] = 0.0;
@@ -88,7 +98,7 @@ __device__ inline void eig_gemv(const double* A, const double* x, double* y) {
 }
 
 template <int N>
-__device__ inline void bicgstab(const double* A, const double* rhs, double* x, double tol) {
+__device__ inline void bicgstab(const Scr A, const double* rhs, double* x, double tol) {
   const int maxIters = 2 * N;
   double invdiag[N];
 #pragma unroll
@@ -149,9 +159,11 @@ __device__ inline void bicgstab(const double* A, const double* rhs, double* x, d
   }
 }
 
-// ColPivHouseholderQR: factor M (row-major NxN, overwritten) and solve for NDIM right-hand sides.
+// ColPivHouseholderQR: factor M (row-major NxN, overwritten) and solve for NDIM right-hand sides. Every loop has a
+// compile-time trip count (fully unrolled: static LDS offsets, register arrays); the data-dependent parts — the pivot
+// column, the rank `nonzero`, the permutation — are predicated, in Eigen's order.
 template <int N, int NDIM>
-__device__ inline void colpiv_qr_solve(double* Q, const double (*rhs)[NDIM], double (*sol)[NDIM]) {
+__device__ inline void colpiv_qr_solve(const Scr Q, const double (*rhs)[NDIM], double (*sol)[NDIM]) {
   double hc[N], normsU[N], normsD[N];
   int trans[N];
 #pragma unroll
@@ -169,49 +181,70 @@ __device__ inline void colpiv_qr_solve(double* Q, const double (*rhs)[NDIM], dou
   const double threshold_helper = (mx * epsm) * (mx * epsm) / double(N);
   const double ndt = sqrt(epsm);
   int nonzero = N;
+#pragma unroll
   for (int k = 0; k < N; ++k) {
     int big = k;
+    double bigU = normsU[k];
+#pragma unroll
     for (int j = k + 1; j < N; ++j)
-      if (normsU[j] > normsU[big]) big = j;
-    const double big_sq = normsU[big] * normsU[big];
+      if (normsU[j] > bigU) {
+        big = j;
+        bigU = normsU[j];
+      }
+    const double big_sq = bigU * bigU;
     if (nonzero == N && big_sq < threshold_helper * double(N - k)) nonzero = k;
     trans[k] = big;
     if (k != big) {
+#pragma unroll
       for (int i = 0; i < N; ++i) {
         const double t = Q[i * N + k];
         Q[i * N + k] = Q[i * N + big];
         Q[i * N + big] = t;
       }
-      double t = normsU[k]; normsU[k] = normsU[big]; normsU[big] = t;
-      t = normsD[k]; normsD[k] = normsD[big]; normsD[big] = t;
+#pragma unroll
+      for (int j = k + 1; j < N; ++j)
+        if (j == big) {
+          double t = normsU[k]; normsU[k] = normsU[j]; normsU[j] = t;
+          t = normsD[k]; normsD[k] = normsD[j]; normsD[j] = t;
+        }
     }
     double tailSq = 0.0;
+#pragma unroll
     for (int i = k + 1; i < N; ++i) tailSq += Q[i * N + k] * Q[i * N + k];
     const double c0 = Q[k * N + k];
     double tau, beta;
     if (tailSq <= 2.2250738585072014e-308) {
       tau = 0.0;
       beta = c0;
+#pragma unroll
       for (int i = k + 1; i < N; ++i) Q[i * N + k] = 0.0;
     } else {
       beta = sqrt(c0 * c0 + tailSq);
       if (c0 >= 0.0) beta = -beta;
+#pragma unroll
       for (int i = k + 1; i < N; ++i) Q[i * N + k] = Q[i * N + k] / (c0 - beta);
       tau = (beta - c0) / beta;
     }
     hc[k] = tau;
     Q[k * N + k] = beta;
     if (N - k == 1) {
-      for (int j = k + 1; j < N; ++j) Q[k * N + j] *= (1.0 - tau);
+      // (no trailing columns: Eigen's `*= (1 - tau)` loop over j > k is empty)
     } else if (tau != 0.0) {
+      double v[N];  // the Householder vector below the diagonal, read once
+#pragma unroll
+      for (int i = k + 1; i < N; ++i) v[i] = Q[i * N + k];
+#pragma unroll
       for (int j = k + 1; j < N; ++j) {
         double tmp = 0.0;
-        for (int i = k + 1; i < N; ++i) tmp += Q[i * N + k] * Q[i * N + j];
+#pragma unroll
+        for (int i = k + 1; i < N; ++i) tmp += v[i] * Q[i * N + j];
         tmp += Q[k * N + j];
         Q[k * N + j] -= tau * tmp;
-        for (int i = k + 1; i < N; ++i) Q[i * N + j] -= tau * Q[i * N + k] * tmp;
+#pragma unroll
+        for (int i = k + 1; i < N; ++i) Q[i * N + j] -= tau * v[i] * tmp;
       }
     }
+#pragma unroll
     for (int j = k + 1; j < N; ++j) {
       if (normsU[j] != 0.0) {
         double temp = fabs(Q[k * N + j]) / normsU[j];
@@ -221,6 +254,7 @@ __device__ inline void colpiv_qr_solve(double* Q, const double (*rhs)[NDIM], dou
         const double temp2 = temp * (rr * rr);
         if (temp2 <= ndt) {
           double s = 0.0;
+#pragma unroll
           for (int i = k + 1; i < N; ++i) s += Q[i * N + j] * Q[i * N + j];
           normsD[j] = sqrt(s);
           normsU[j] = normsD[j];
@@ -233,42 +267,57 @@ __device__ inline void colpiv_qr_solve(double* Q, const double (*rhs)[NDIM], dou
   int perm[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) perm[k] = k;
+#pragma unroll
   for (int k = 0; k < N; ++k) {
-    const int t = perm[k];
-    perm[k] = perm[trans[k]];
-    perm[trans[k]] = t;
+    // swap perm[k] and perm[trans[k]] (trans[k] >= k)
+    int pt = perm[k];
+#pragma unroll
+    for (int j = k + 1; j < N; ++j)
+      if (trans[k] == j) pt = perm[j];
+    const int pk = perm[k];
+#pragma unroll
+    for (int j = k + 1; j < N; ++j)
+      if (trans[k] == j) perm[j] = pk;
+    perm[k] = pt;
   }
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) {
     double c[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) c[i] = rhs[i][d];
-    if (nonzero == 0) {
 #pragma unroll
-      for (int i = 0; i < N; ++i) sol[i][d] = 0.0;
-      continue;
-    }
-    for (int k = 0; k < nonzero; ++k) {
-      const double tau = hc[k];
-      if (N - k == 1) {
-        c[k] *= (1.0 - tau);
-      } else if (tau != 0.0) {
-        double tmp = 0.0;
-        for (int i = k + 1; i < N; ++i) tmp += Q[i * N + k] * c[i];
-        tmp += c[k];
-        c[k] -= tau * tmp;
-        for (int i = k + 1; i < N; ++i) c[i] -= tau * Q[i * N + k] * tmp;
+    for (int k = 0; k < N; ++k) {
+      if (k < nonzero) {
+        const double tau = hc[k];
+        if (N - k == 1) {
+          c[k] *= (1.0 - tau);
+        } else if (tau != 0.0) {
+          double tmp = 0.0;
+#pragma unroll
+          for (int i = k + 1; i < N; ++i) tmp += Q[i * N + k] * c[i];
+          tmp += c[k];
+          c[k] -= tau * tmp;
+#pragma unroll
+          for (int i = k + 1; i < N; ++i) c[i] -= tau * Q[i * N + k] * tmp;
+        }
       }
     }
-    for (int i = nonzero - 1; i >= 0; --i) {
-      c[i] /= Q[i * N + i];
-      for (int j = 0; j < i; ++j) c[j] -= c[i] * Q[j * N + i];
-    }
-    double out[N];
-    for (int i = 0; i < N; ++i) out[i] = 0.0;
-    for (int i = 0; i < nonzero; ++i) out[perm[i]] = c[i];
 #pragma unroll
-    for (int i = 0; i < N; ++i) sol[i][d] = out[i];
+    for (int i = N - 1; i >= 0; --i) {
+      if (i < nonzero) {
+        c[i] /= Q[i * N + i];
+#pragma unroll
+        for (int j = 0; j < i; ++j) c[j] -= c[i] * Q[j * N + i];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < N; ++p) {
+      double o = 0.0;
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (i < nonzero && perm[i] == p) o = c[i];
+      sol[p][d] = o;
+    }
   }
 }
 
@@ -311,7 +360,7 @@ struct ViscNode {
 template <int NS, int NDIM>
 __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const ViscNode<NS, NDIM>& ni,
                                 const ViscNode<NS, NDIM>& nj, double sigma_k, const double* Normal, double* res,
-                                SummRef summ, double* scr, bool corrected = true) {
+                                SummRef summ, Scr scr, bool corrected = true) {
   // corrected = false: CAvgGradReactive_Boundary::ComputeResidual (numerics_direct_reactive.cpp:478-648, a8):
   // the plain mean gradient — no edge correction, no coincident-point check.
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
@@ -324,17 +373,11 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   const double* Vj = nj.V;
   const double Mean_mu = 2.0 / (1.0 / ni.mu + 1.0 / nj.mu);
   const double Mean_k = 2.0 / (1.0 / ni.kappa + 1.0 / nj.kappa);
-  // harmonic means of the binary diffusion coefficients (recomputed where used: same arithmetic)
+  // harmonic means of the binary diffusion coefficients
   auto Dm = [&](int q) { return 2.0 / (1.0 / ni.Dij[q] + 1.0 / nj.Dij[q]); };
-  double Dmax = -INFINITY;
-#pragma unroll
-  for (int q = 0; q < NS * NS; ++q) Dmax = fmax(Dmax, Dm(q));
   double Vm[nPV];
 #pragma unroll
   for (int v = 0; v < nPV; ++v) Vm[v] = 0.5 * (Vi[v] + Vj[v]);
-  double Xs_i[NS], Xs_j[NS];
-  molar_from_mass<NS>(m, Vi + RHOS_P, Xs_i);
-  molar_from_mass<NS>(m, Vj + RHOS_P, Xs_j);
   double Edge[NDIM];
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) Edge[d] = nj.coord[d] - ni.coord[d];
@@ -353,6 +396,9 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   for (int d = 0; d < NDIM; ++d) dist2 += Edge[d] * Edge[d];
   if (corrected && !(dist2 > kEPS)) return ERR_GEOM;
   if (corrected) {
+    double Xs_i[NS], Xs_j[NS];  // recomputed for the summary below: not live across the two solves
+    molar_from_mass<NS>(m, Vi + RHOS_P, Xs_i);
+    molar_from_mass<NS>(m, Vj + RHOS_P, Xs_j);
     double Diff[nAvg], Proj[nAvg];
 #pragma unroll
     for (int r = 0; r < nAvg; ++r) {
@@ -371,50 +417,38 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
 #pragma unroll
       for (int d = 0; d < NDIM; ++d) G[r][d] -= (Proj[r] - Diff[r]) * Edge[d] / dist2;
   }
-  // ---- SetLaminarTensorFlux
-  double Flux[nVar][NDIM], PF[nVar];
-#pragma unroll
-  for (int v = 0; v < nVar; ++v) {
-    PF[v] = 0.0;
-#pragma unroll
-    for (int d = 0; d < NDIM; ++d) Flux[v][d] = 0.0;
-  }
+  // ---- SetLaminarTensorFlux, in an order that keeps few values live across the two dense solves: the
+  // Stefan-Maxwell solve first, then the SST closure solve, then the tensors and the flux rows. Every
+  // accumulator keeps the reference's operation order (each Flux / PF entry sums its terms in the same sequence).
   const double rho = Vm[RHO_P];
   const double dim_temp = Vm[T_P] * P.T_ref;
-  double hs[NS], Ys[NS], Xs[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) hs[s] = spline(m, P_H, s, dim_temp, &err) / m.mm[s] / P.E_ref;
+  double Ys[NS], Xs[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) Ys[s] = Vm[RHOS_P + s];
   molar_from_mass<NS>(m, Ys, Xs);
-  double div_vel = 0.0;
-#pragma unroll
-  for (int d = 0; d < NDIM; ++d) div_vel += G[VX_A + d][d];
-  double tau[NDIM][NDIM];
-#pragma unroll
-  for (int a = 0; a < NDIM; ++a) {
-#pragma unroll
-    for (int b = 0; b < NDIM; ++b) tau[a][b] = 0.0 + Mean_mu * (G[VX_A + b][a] + G[VX_A + a][b]);
-    tau[a][a] -= kTWO3 * (Mean_mu * div_vel);
-  }
-  const double alpha = 1.0 / (rho * Dmax);
   double Gxn[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) Gxn[s] = 0.0;
 #pragma unroll
-  for (int a = 0; a < NDIM; ++a) {
-#pragma unroll
-    for (int b = 0; b < NDIM; ++b) {
-      Flux[RHOVX_S + b][a] = tau[a][b];
-      Flux[RHOE_S][a] += tau[a][b] * Vm[VX_P + b];
-    }
-    Flux[RHOE_S][a] += Mean_k * G[T_A][a];
+  for (int a = 0; a < NDIM; ++a)
 #pragma unroll
     for (int s = 0; s < NS; ++s) Gxn[s] += G[RHOS_A + s][a] * Normal[a];
-  }
   double Jd[NS];
   {
-    double* Gt = scr;  // LDS scratch of this lane (NS*NS)
+    // The harmonic means go to the lane's LDS scratch as they are made, transposed (row a = Dm(. * NS + a), what
+    // row a of Gamma reads), and Gamma is built over them in place row by row: the 2 NS^2 Dij loads are consumed
+    // at once instead of being held in registers from the top of the kernel. Dmax is an exact max (order-free).
+    const Scr Gt = scr;  // LDS scratch of this lane (NS*NS)
+    double Dmax = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < NS; ++b)
+#pragma unroll
+      for (int a = 0; a < NS; ++a) {
+        const double dm = Dm(b * NS + a);
+        Dmax = fmax(Dmax, dm);
+        Gt[a * NS + b] = dm;
+      }
+    const double alpha = 1.0 / (rho * Dmax);
     double sigma = 0.0, massTot = 0.0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) sigma += Ys[s];
@@ -422,21 +456,25 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     for (int s = 0; s < NS; ++s) massTot += Ys[s] / m.mm[s];
     massTot = 1.0 / massTot;
 #pragma unroll
-    for (int a = 0; a < NS; ++a)
+    for (int a = 0; a < NS; ++a) {
+      double dr[NS];  // Dm(b * NS + a), b = 0 .. NS-1
+#pragma unroll
+      for (int b = 0; b < NS; ++b) dr[b] = Gt[a * NS + b];
 #pragma unroll
       for (int b = 0; b < NS; ++b) {
         double g;
         if (a != b) {
-          g = -sigma * massTot * Xs[a] / (rho * m.mm[b] * Dm(b * NS + a));
+          g = -sigma * massTot * Xs[a] / (rho * m.mm[b] * dr[b]);
         } else {
           double tmp = 0.0;
 #pragma unroll
           for (int c = 0; c < NS; ++c)
-            if (c != a) tmp += Xs[c] / Dm(c * NS + a);
+            if (c != a) tmp += Xs[c] / dr[c];
           g = sigma * massTot * tmp / (rho * m.mm[a]);
         }
         Gt[a * NS + b] = g + alpha * Ys[a];
       }
+    }
     double nG[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) nG[s] = -Gxn[s];
@@ -447,6 +485,12 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     bicgstab<NS>(Gt, nG, Jd, 1.0e-11);
 #endif
   }
+  double hs[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) hs[s] = spline(m, P_H, s, dim_temp, &err) / m.mm[s] / P.E_ref;
+  double PF[nVar];
+#pragma unroll
+  for (int v = 0; v < nVar; ++v) PF[v] = 0.0;
   {
     double ones[NS];
 #pragma unroll
@@ -463,23 +507,10 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   if (P.rans) {
     Mean_mut = 2.0 / (1.0 / ni.mut + 1.0 / nj.mut);
     Mean_tke = 0.5 * (ni.tke + nj.tke);
-    double gk[NDIM];
-#pragma unroll
-    for (int d = 0; d < NDIM; ++d) gk[d] = 0.5 * (ni.gk[d] + nj.gk[d]);
 #pragma unroll
     for (int s = 0; s < NS; ++s) Cps[s] = spline(m, P_CP, s, dim_temp, &err) / m.mm[s] / P.R_ref;
-    double dv = 0.0;
-#pragma unroll
-    for (int d = 0; d < NDIM; ++d) dv += G[VX_A + d][d];
-    double tt[NDIM][NDIM];
-#pragma unroll
-    for (int a = 0; a < NDIM; ++a) {
-#pragma unroll
-      for (int b = 0; b < NDIM; ++b) tt[a][b] = 0.0 + Mean_mut * (G[VX_A + b][a] + G[VX_A + a][b]);
-      tt[a][a] -= kTWO3 * (Mean_mut * dv + Mean_tke * rho);
-    }
     {
-      double* Mt = scr;  // LDS scratch of this lane (NS*NS), Gt is dead here
+      const Scr Mt = scr;  // LDS scratch of this lane (NS*NS), Gt is dead here
       double sig = 0.0;
 #pragma unroll
       for (int s = 0; s < NS; ++s) sig += Xs[s];
@@ -508,6 +539,47 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
 #pragma unroll
       for (int d = 0; d < NDIM; ++d)
         if (fabs(G[RHOS_A + s][d]) < 1e-8) MG[s][d] = 0.0;
+  }
+  double Flux[nVar][NDIM];
+#pragma unroll
+  for (int v = 0; v < nVar; ++v)
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) Flux[v][d] = 0.0;
+  {
+    double div_vel = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) div_vel += G[VX_A + d][d];
+    double tau[NDIM][NDIM];
+#pragma unroll
+    for (int a = 0; a < NDIM; ++a) {
+#pragma unroll
+      for (int b = 0; b < NDIM; ++b) tau[a][b] = 0.0 + Mean_mu * (G[VX_A + b][a] + G[VX_A + a][b]);
+      tau[a][a] -= kTWO3 * (Mean_mu * div_vel);
+    }
+#pragma unroll
+    for (int a = 0; a < NDIM; ++a) {
+#pragma unroll
+      for (int b = 0; b < NDIM; ++b) {
+        Flux[RHOVX_S + b][a] = tau[a][b];
+        Flux[RHOE_S][a] += tau[a][b] * Vm[VX_P + b];
+      }
+      Flux[RHOE_S][a] += Mean_k * G[T_A][a];
+    }
+  }
+  if (P.rans) {
+    double gk[NDIM];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) gk[d] = 0.5 * (ni.gk[d] + nj.gk[d]);
+    double dv = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) dv += G[VX_A + d][d];
+    double tt[NDIM][NDIM];
+#pragma unroll
+    for (int a = 0; a < NDIM; ++a) {
+#pragma unroll
+      for (int b = 0; b < NDIM; ++b) tt[a][b] = 0.0 + Mean_mut * (G[VX_A + b][a] + G[VX_A + a][b]);
+      tt[a][a] -= kTWO3 * (Mean_mut * dv + Mean_tke * rho);
+    }
 #pragma unroll
     for (int a = 0; a < NDIM; ++a) {
 #pragma unroll
@@ -534,6 +606,9 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   for (int v = 0; v < nVar; ++v) res[v] = PF[v];
   if (!P.implicit) return err;
 
+  double Xs_i[NS], Xs_j[NS];
+  molar_from_mass<NS>(m, Vi + RHOS_P, Xs_i);
+  molar_from_mass<NS>(m, Vj + RHOS_P, Xs_j);
   // ---- implicit part: the per-edge summary the Jacobian kernel (visc_jac_column) needs
   double Ds[NS];
   {
