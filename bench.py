@@ -88,7 +88,9 @@ def ilu_apply_kernels(N, nnzb, nVar, parts):
     shm = 8 * (rows * nVar + (256 // nVar) * nVar + 1) + 4 * (8 * rows + rows * nnzb // max(N, 1))
     if shm <= 160 * 1024:
         return f"k_ilu_apply_lds<{nVar}>"
-    return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
+    if os.environ.get("RX_ILU_SPLIT"):
+        return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
+    return f"k_ilu_apply_wide<{nVar}, 1024>"  # both sweeps of a partition in one launch (round 4)
 
 
 def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, max_degree=4,
@@ -415,12 +417,12 @@ def main():
     timed = [k for k in models if prof[k][1] > 0]
     kernels = {k: roof(k) for k in timed}
     # GPU time per step of each single-kernel phase (SPMV / ILU_APPLY: average launch of the eager pass x launches per
-    # step, i.e. per linear iteration of the flow solve; ILU_APPLY is two kernels, the forward and backward sweeps)
+    # step, i.e. per linear iteration of the flow solve; ILU_APPLY is one kernel, both sweeps, unless RX_ILU_SPLIT)
     its_mean = float(np.mean([a for a, _ in timed_its]))
     for k in timed:
         per = its_mean if k in ("SPMV", "ILU_APPLY") else prof[k][1] / args.steps
         kernels[k]["ms_per_step"] = round(prof[k][0] / prof[k][1] * per, 4)
-    single = [k for k in timed if k != "ILU_APPLY"]
+    single = [k for k in timed if "+" not in kernels[k]["kernel"]]
     # dominant kernel: the most GPU time per step; the longest single launch beside it
     dom = max(single, key=lambda k: kernels[k]["ms_per_step"])
     longest = max((k for k in single if k != "SPMV"), key=lambda k: prof[k][0] / prof[k][1])
