@@ -1,0 +1,24 @@
+"""bench.py's kernel bookkeeping (CPU): the ILU(0) apply kernel the bench line names must be the one rx_la_ilu_apply
+launches for the workload (rx_sweeps.hip), so that `roofline.kernel` matches the rocprof summary."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def test_ilu_apply_kernel_names(monkeypatch):
+    monkeypatch.delenv("RX_ILU_SPLIT", raising=False)
+    # C3: 1M points, 256 partitions of 3 906 rows -> the vector does not fit LDS: the fused wide sweeps (one kernel)
+    assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_wide<11, 1024>"
+    # C4's share per GPU at 2048 partitions: 488-row partitions fit LDS
+    assert bench.ilu_apply_kernels(125_000, 624_000, 11, 256) == "k_ilu_apply_lds<11>"
+    monkeypatch.setenv("RX_ILU_SPLIT", "1")
+    assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_fwd_wide<11, 1024>+k_ilu_bwd_wide<11, 1024>"
+
+
+def test_kernel_models_cover_the_timed_phases():
+    m = bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)
+    for k in ("CONV", "VISC", "VISC_JAC", "ASSEMBLE", "GRAD", "SOURCE", "ILU_BUILD", "SPMV", "ILU_APPLY"):
+        assert k in m and m[k]["kernel"] and m[k]["peak"] > 0, k
+    assert m["SPMV"]["unit"] == "GB/s" and m["ILU_APPLY"]["kernel"].startswith("k_ilu_apply_")
