@@ -198,6 +198,48 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
                 sample=f"{what} of the same {N}-cell mesh, {cores} host threads ({dt:.2f} s)")
 
 
+def cpu_baseline_reference(ns, cfl, nx=300, ny=75):
+    """One outer iteration of the reference itself (SU2's CMeanFlowIteration::Iterate through oracle/ref_harness,
+    compiled from /root/reference's sources by oracle/ref_build.mk into oracle/_ref, serial: one MPI rank, one core)
+    on a bounded sample of the bench workload: the same synthetic jet geometry and interpolated PaSR state
+    (synth.field_at) at nx x ny points, the bench's mechanism (`ns` species), EULER_IMPLICIT with ILU0 FGMRES(5)
+    and the jet's boundary conditions. The time is the harness's own clock around Iterate (it1_wall). None when the
+    harness is not built."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "harness")
+    if not os.path.exists(harness):
+        return None
+    import shutil
+    import tempfile
+    from tests.casefiles import unpack
+    from tests.rxpkg import meshgen, synth
+    root = tempfile.mkdtemp(prefix="rx_refbase_")
+    try:
+        cd = os.path.join(root, "ref", "Test_Cases", "TURBOLENT", "TURBOLENT_COMBUSTION")
+        unpack(cd, "jet")
+        os.environ["RX_REFERENCE"] = os.path.join(root, "ref")
+        from oracle import make_golden as MG
+        MG.CASE_DIR = cd
+        pts, quads, bnd = meshgen.jet_mesh(nx, ny)
+        _, U, k, om, _, _ = synth.field_at(pts, ns)
+        state = np.c_[U, k, om]
+
+        def writer(wd):
+            meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, quads, bnd)
+            return "mesh.su2"
+
+        wd = MG.make_workdir("refbase", writer, cfl=cfl, order="1ST_ORDER", prec="ILU0", ns=ns, root=root)
+        MG.write_state(wd, state)
+        a = MG.run_harness(wd, bsr=False, extra=["--iters", "1"])
+        wall = float(np.ravel(a["it1_wall"])[0])
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    n = len(pts)
+    return dict(value=round(n / wall / 1e6, 6), unit="Mcells*iters/s", cores=1, kind="reference",
+                sample=f"1 outer iteration of the reference itself (oracle/_ref harness, serial, one core) on the "
+                       f"{nx}x{ny} synthetic jet ({n} points, {ns} species, EULER_IMPLICIT ILU0 FGMRES(5), jet BCs): "
+                       f"{wall:.2f} s")
+
+
 def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist, nz=0):
     """Build the rank's shard (strong: of the fixed nx x ny jet; weak: of the N-times-taller one) and attach the RCCL
     communicator."""
@@ -466,8 +508,17 @@ def main():
         "phase_ms_per_step": {k: round(v, 4) for k, v in phase_ms.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg,
-                                           None if args.no_bc else synth_bc)
+        # the reference itself on a bounded sample when its harness is built (kind "reference"), beside the
+        # restatement on the whole mesh on all host cores (kind "port")
+        port = cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, None if args.no_bc else synth_bc)
+        ref = None
+        if nz <= 1 and not args.no_bc:
+            try:
+                ref = cpu_baseline_reference(ns, cfg.cfl)
+            except (SystemExit, Exception) as e:  # noqa: BLE001 - the port line stands
+                port["reference_error"] = repr(e)[:200]
+        out["cpu_baseline"] = ref if ref is not None else port
+        out["cpu_baseline_port"] = port
     else:
         out["cpu_baseline"] = None
     s.close()

@@ -22,3 +22,13 @@ def test_kernel_models_cover_the_timed_phases():
     for k in ("CONV", "VISC", "VISC_JAC", "ASSEMBLE", "GRAD", "SOURCE", "ILU_BUILD", "SPMV", "ILU_APPLY"):
         assert k in m and m[k]["kernel"] and m[k]["peak"] > 0, k
     assert m["SPMV"]["unit"] == "GB/s" and m["ILU_APPLY"]["kernel"].startswith("k_ilu_apply_")
+
+
+def test_cpu_baseline_reference_runs_the_compiled_reference():
+    """The bench line's cpu_baseline (kind "reference"): the reference's own Iterate on a bounded sample of the
+    bench's jet, through the harness compiled from the reference sources (skipped where it is not built)."""
+    import pytest
+    if not os.path.exists(os.path.join(bench.ROOT, "oracle", "_ref", "harness")):
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    r = bench.cpu_baseline_reference(7, 5.0, nx=40, ny=12)
+    assert r["kind"] == "reference" and r["cores"] == 1 and r["value"] > 0 and "480 points" in r["sample"]
