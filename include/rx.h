@@ -55,7 +55,7 @@ typedef enum {
   RX_ERR_DIVERGED = 6,
   RX_ERR_STATE = 7,
   RX_ERR_COMM = 8,    /* RCCL error */
-  RX_ERR_UNSUPPORTED = 9  /* input the path does not implement (rx_mesh_read_su2: prism / pyramid elements) */
+  RX_ERR_UNSUPPORTED = 9  /* input the path does not implement (rx_case_read: physics / numerics keys of other solvers) */
 } rx_status;
 
 typedef struct rx_ctx rx_ctx;
