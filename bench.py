@@ -116,8 +116,14 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         "VISC_JAC": hbm(E * summ + N * nVar * d + E * 16 + E * 6 * blk, "k_visc_jac" + te),
         # k_assemble: each node's own-side conv + visc blocks (2 per edge each), the edge fluxes, the source
         # Jacobian's species rows and residual in; diagonal blocks + residual out
-        "ASSEMBLE": hbm(4 * E * blk + 2 * E * nVar * d + N * (ns * nVar + nVar) * d + N * (blk + nVar * d),
-                        f"k_assemble<{nVar}, {4 if max_degree <= 4 else 8}>"),  # register path by max degree
+        "ASSEMBLE": (hbm(4 * E * blk + 2 * E * nVar * d + N * (ns * nVar + nVar) * d + N * (blk + nVar * d),
+                         f"k_assemble<{nVar}, {4 if max_degree <= 4 else 8}>")  # register path by max degree
+                     if os.environ.get("RX_NO_ASM_VISC") else
+                     # k_asm_visc (round 4: viscous Jacobians made by the node-centric assembly, VISC_JAC not
+                     # launched): each edge's two convective blocks, summary record, fluxes and ends' dT/dU in once,
+                     # the source rows; the two off-diagonal blocks, the diagonal blocks and the residual out
+                     hbm(2 * E * blk + 2 * E * nVar * d + E * summ + N * nVar * d + 24 * E
+                         + N * (ns * nVar + nVar) * d + 2 * E * blk + N * (blk + nVar * d), "k_asm_visc" + te)),
         "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq" + te),
         # k_source: V, dT/dU, volume, omega in; residual + the Jacobian's species rows out
         "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar + ns * nVar) * d, "k_source" + te),

@@ -945,6 +945,104 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int3
   A[diag[i] * nVar2 + t] = D;
 }
 
+// Node-centric viscous Jacobians + assembly (round 4): one 16-lane team per node, lane b =
+// column b. The team walks the node's edges in adjacency (= edge) order twice, as k_assemble does: the convective
+// pass adds its own-side convective blocks to the diagonal and the convective fluxes to the residual; the viscous pass
+// stages each edge's summary record in the team's LDS slot, evaluates the edge's viscous Jacobian columns
+// (visc_jac_column_f, the same arithmetic as k_visc_jac), folds its own side into the diagonal and writes the
+// edge's off-diagonal block of the neighbour's row from its own side, A(n1,n0) = (0 - Jc_i) + Jv_i or
+// A(n0,n1) = (0 + Jc_j) - Jv_j. Every diagonal entry, residual component and off-diagonal entry is the same sum in
+// the same order as k_visc_jac + k_assemble make it, so the system is bitwise theirs; the per-edge viscous blocks
+// (2 x 968 B per edge, written once and read once) and the second read of the convective blocks are gone, at the
+// price of evaluating each edge's columns at both ends.
+#ifndef RX_WPE_ASMV
+#define RX_WPE_ASMV RX_WPE(2)
+#endif
+template <int NS, int NDIM>
+__global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
+    int N, const int32_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj, const int32_t* __restrict__ edges,
+    const int64_t* __restrict__ edge_blk, const int64_t* __restrict__ diag, const double* __restrict__ Fc,
+    const double* __restrict__ Fv, const double* __restrict__ Jc, const double* __restrict__ dTdU,
+    const double* __restrict__ Summ, const double* __restrict__ Js, const double* __restrict__ Rsrc, DevMech m,
+    ViscParams P, double* __restrict__ R, double* __restrict__ A, int src) {
+  constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>(), kTeams = kBlock / 16;
+  constexpr int rhos = NDIM + 2, nsv = NS * nVar;
+  __shared__ double ssm[kTeams * SS];
+  const int gt = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const int i = gt / 16, b = gt % 16, team = threadIdx.x / 16;
+  if (i >= N) return;  // whole teams (N * 16 threads)
+  const bool col = b < nVar;
+  const int bc = col ? b : 0;
+  double* slot = ssm + team * SS;
+  const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  double r = 0.0, D[nVar];
+#pragma unroll
+  for (int a = 0; a < nVar; ++a) D[a] = 0.0;
+  // convective pass
+  for (int k = k0; k < k1; ++k) {
+    const int ad = adj[k];
+    const size_t e = (size_t)(ad >> 1);
+    const int side = ad & 1;
+    if (col) {
+      const double f = Fc[e * nVar + b];
+      r = side ? r - f : r + f;
+    }
+    const double* J = Jc + (e * 2 + side) * nVar2 + bc;
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) {
+      const double jd = J[a * nVar];
+      D[a] = side ? D[a] - jd : D[a] + jd;
+    }
+  }
+  // viscous pass
+  for (int k = k0; k < k1; ++k) {
+    const int ad = adj[k];
+    const int e = ad >> 1;
+    const int side = ad & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    {
+      const double* tile = Summ + (size_t)(e / kSummTile) * SS * kSummTile + e % kSummTile;
+      for (int q = b; q < SS; q += 16) slot[q] = tile[(size_t)q * kSummTile];
+    }
+    const double sib = dTdU[(size_t)n0 * nVar + bc], sjb = dTdU[(size_t)n1 * nVar + bc];
+    double jco[nVar];  // this lane's column of the own-side convective block (for the off-diagonal)
+    {
+      const double* J = Jc + ((size_t)e * 2 + side) * nVar2 + bc;
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) jco[a] = J[a * nVar];
+    }
+    if (col) {
+      const double f = Fv[(size_t)e * nVar + b];
+      r = side ? r + f : r - f;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
+    visc_jac_column_f<NS, NDIM>(m, P, SummCRef{slot, 1}, sib, sjb, b, b, [&](int rr, double si, double sj) {
+      const double jv = side ? sj : si;
+      D[rr] = side ? D[rr] + jv : D[rr] - jv;
+      Ao[rr * nVar + b] = side ? (0.0 + jco[rr]) - sj : (0.0 - jco[rr]) + si;
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!col) return;
+  if (src) {
+    r += Rsrc[(size_t)i * nVar + b];
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) {
+      const double js = a >= rhos ? Js[(size_t)(i / kSrcTile) * nsv * kSrcTile +
+                                       (size_t)((a - rhos) * nVar + b) * kSrcTile + i % kSrcTile]
+                                  : 0.0;
+      D[a] += js;
+    }
+  }
+  R[(size_t)i * nVar + b] = r;
+  double* Ad = A + diag[i] * nVar2 + b;
+#pragma unroll
+  for (int a = 0; a < nVar; ++a) Ad[a * nVar] = D[a];
+}
+
 // a12: weighted least-squares gradient of (T, u, v, P, X_s) per node.
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) void k_grad_lsq(int N, const int32_t* __restrict__ nptr,
@@ -1392,6 +1490,11 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
                               ctx->mech, P, ctx->fvisc, ctx->vsumm, ctx->err)));
     RX_HIP(hipGetLastError());
   }
+  // the node-centric viscous Jacobians + assembly (k_asm_visc, launched by rx_launch_assemble) replace k_visc_jac
+  // and k_assemble's viscous pass; RX_NO_ASM_VISC=1 restores the edge kernel + node assembly (A/B, diagnosis)
+  static const bool no_asm_visc = getenv("RX_NO_ASM_VISC") != nullptr;
+  ctx->asm_visc = ctx->cfg.implicit && !no_asm_visc ? 1 : 0;
+  if (ctx->cfg.implicit && ctx->asm_visc) return RX_OK;
   if (ctx->cfg.implicit) {
     RxPhase ph(ctx, RX_K_VISC_JAC);
     // fused off-diagonal assembly needs this residual's convective blocks (rx_edge_flux_conv ran first)
@@ -1428,6 +1531,16 @@ int rx_launch_source(rx_ctx* ctx) {
 
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   const int nv = ctx->nVar;
+  if (with_visc && ctx->asm_visc) {  // k_visc_jac was skipped: the node-centric viscous Jacobians + assembly
+    ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
+                 ctx->cfg.rans, ctx->cfg.implicit};
+    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<blocks(ctx->N * 16), kBlock, 0, ctx->stream>>>(
+                              (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
+                              ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech,
+                              P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src)));
+    RX_HIP(hipGetLastError());
+    return RX_OK;
+  }
   switch (nv) {
 #define RX_ASM_DEG(NV, DEG)                                                                                       \
   k_assemble<NV, DEG><<<blocks(ctx->N * asm_team<NV>()), kBlock, 0, ctx->stream>>>(                              \

@@ -725,7 +725,14 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
                                        double Sib, double Sjb, int b, int tl, double* __restrict__ Ji,
                                        double* __restrict__ Jj, const double* jci = nullptr,
                                        const double* jcj = nullptr, double* __restrict__ Aij = nullptr,
-                                       double* __restrict__ Aji = nullptr) {
+                                       double* __restrict__ Aji = nullptr);
+
+// The column computation with the entries handed to put(r, Ji[r][b], Jj[r][b]) row by row (r = 0 .. nVar-1, in
+// order) instead of stored: visc_jac_column is this with put = the stores; the node-centric assembly
+// (k_asm_visc) folds them into the node's diagonal and off-diagonal blocks.
+template <int NS, int NDIM, typename Put>
+__device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, const SummCRef sm, double Sib,
+                                         double Sjb, int b, int tl, Put put) {
   using L = VSL<NDIM>;
   constexpr int nVar = NS + NDIM + 2, NF = NDIM + 2;
   constexpr int RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
@@ -890,15 +897,6 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
   // off-diagonal blocks in the reference order A(i,j) = (0 + Jc_j) - Jv_j, A(j,i) = (0 - Jc_i) + Jv_i
   // (AddBlock / SubtractBlock of Upwind_Residual then Viscous_Residual, solver_direct_reactive.cpp:2240-2246,
   // :5365-5371); jci / jcj: column b of the convective blocks, row r at [r] (registers, loaded up front)
-  auto put = [&](int r, double si, double sj) {
-    const int idx = r * nVar + b;
-    Ji[idx] = si;
-    Jj[idx] = sj;
-    if (Aij) {
-      Aij[idx] = (0.0 + jcj[r]) - sj;
-      Aji[idx] = (0.0 - jci[r]) + si;
-    }
-  };
   double ci[NDIM], cj[NDIM];  // dV/dU velocity rows, column b
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) {
@@ -947,6 +945,23 @@ __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, co
     }
     put(RHOS_S + a, si, sj);
   }
+}
+
+template <int NS, int NDIM>
+__device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, const SummCRef sm,
+                                       double Sib, double Sjb, int b, int tl, double* __restrict__ Ji,
+                                       double* __restrict__ Jj, const double* jci, const double* jcj,
+                                       double* __restrict__ Aij, double* __restrict__ Aji) {
+  constexpr int nVar = NS + NDIM + 2;
+  visc_jac_column_f<NS, NDIM>(m, P, sm, Sib, Sjb, b, tl, [&](int r, double si, double sj) {
+    const int idx = r * nVar + b;
+    Ji[idx] = si;
+    Jj[idx] = sj;
+    if (Aij) {
+      Aij[idx] = (0.0 + jcj[r]) - sj;
+      Aji[idx] = (0.0 - jci[r]) + si;
+    }
+  });
 }
 
 }  // namespace rx
