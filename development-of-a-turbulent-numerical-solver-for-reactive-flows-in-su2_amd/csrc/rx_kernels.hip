@@ -951,12 +951,12 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int3
 // stages each edge's summary record in the team's LDS slot, evaluates the edge's viscous Jacobian columns
 // (visc_jac_column_f, the same arithmetic as k_visc_jac), folds its own side into the diagonal and writes the
 // edge's off-diagonal block of the neighbour's row from its own side, A(n1,n0) = (0 - Jc_i) + Jv_i or
-// A(n0,n1) = (0 + Jc_j) - Jv_j. Every diagonal entry, residual component and off-diagonal entry is the same sum in
-// the same order as k_visc_jac + k_assemble make it, so the system is bitwise theirs; the per-edge viscous blocks
-// (2 x 968 B per edge, written once and read once) and the second read of the convective blocks are gone, at the
-// price of evaluating each edge's columns at both ends.
+// A(n0,n1) = (0 + Jc_j) - Jv_j. Only the own side's columns are evaluated (visc_jac_column_own), so each side of
+// each edge is still evaluated once. Every diagonal entry, residual component and off-diagonal entry is the same
+// sum in the same order as k_visc_jac + k_assemble make it, so the system is bitwise theirs; the per-edge viscous
+// blocks (2 x 968 B per edge, written once and read once) and the second read of the convective blocks are gone.
 #ifndef RX_WPE_ASMV
-#define RX_WPE_ASMV RX_WPE(2)
+#define RX_WPE_ASMV RX_WPE(NDIM == 2 ? 3 : 2)
 #endif
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
       const double* tile = Summ + (size_t)(e / kSummTile) * SS * kSummTile + e % kSummTile;
       for (int q = b; q < SS; q += 16) slot[q] = tile[(size_t)q * kSummTile];
     }
-    const double sib = dTdU[(size_t)n0 * nVar + bc], sjb = dTdU[(size_t)n1 * nVar + bc];
+    const double sob = dTdU[(size_t)(side ? n1 : n0) * nVar + bc];  // the own node's dT/dU
     double jco[nVar];  // this lane's column of the own-side convective block (for the off-diagonal)
     {
       const double* J = Jc + ((size_t)e * 2 + side) * nVar2 + bc;
@@ -1018,10 +1018,9 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
-    visc_jac_column_f<NS, NDIM>(m, P, SummCRef{slot, 1}, sib, sjb, b, b, [&](int rr, double si, double sj) {
-      const double jv = side ? sj : si;
+    visc_jac_column_own<NS, NDIM>(m, P, SummCRef{slot, 1}, sob, side, b, b, [&](int rr, double jv) {
       D[rr] = side ? D[rr] + jv : D[rr] - jv;
-      Ao[rr * nVar + b] = side ? (0.0 + jco[rr]) - sj : (0.0 - jco[rr]) + si;
+      Ao[rr * nVar + b] = side ? (0.0 + jco[rr]) - jv : (0.0 - jco[rr]) + jv;
     });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();

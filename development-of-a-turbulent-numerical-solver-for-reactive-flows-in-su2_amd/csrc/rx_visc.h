@@ -947,6 +947,165 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
   }
 }
 
+// One side's column only (side 0: Jac_i, side 1: Jac_j), for the node-centric assembly, which needs at each end of
+// an edge only that end's block. The two sides' expressions differ only in the node data they read (rho, X_s,
+// sigma, sum M_s X_s, dT/dU, velocity) and in signs: every j-side quantity is the i-side expression evaluated on the
+// j data with the sign flipped at the same points (-(a - t) = (-a) + t exactly in round-to-nearest), so each entry
+// here is, bitwise, the one visc_jac_column_f hands to put for that side. Sob: dT/dU[b] of the own node.
+template <int NS, int NDIM, typename Put>
+__device__ inline void visc_jac_column_own(const DevMech& m, const ViscParams& P, const SummCRef sm, double Sob,
+                                           int side, int b, int tl, Put put) {
+  using L = VSL<NDIM>;
+  constexpr int nVar = NS + NDIM + 2, NF = NDIM + 2;
+  constexpr int RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
+  const bool J = side != 0;
+  const double mu = sm[L::MU], ktr = sm[L::K], mut = sm[L::MUT], rho = sm[L::RHO];
+  const double rho_o = J ? sm[L::RHOJ] : sm[L::RHOI];
+  const double theta = sm[L::THETA], dij = sm[L::DIJ], dS = sm[L::DS], sq = sm[L::DIJ], Area = sm[L::DS];
+  const double totMass = sm[L::TM], totMass_o = J ? sm[L::TMJ] : sm[L::TMI];
+  const double sigma_o = J ? sm[L::SGJ] : sm[L::SGI];
+  const SummCRef Xs_o = sm + L::ARR + (J ? NS : 0);
+  const SummCRef Ys = sm + L::ARR + 2 * NS;
+  const SummCRef hs = Ys + NS;
+  const SummCRef Cps = hs + NS;
+  const SummCRef Jd = Cps + NS;
+  const SummCRef Gxn = Jd + NS;
+  const SummCRef Ds = Gxn + NS;
+  const SummCRef qaux = Ds + NS;
+  const double PrT = P.Pr_t, LeT = P.Le_t;
+  // column-independent part of dJ/drho row a = tl, i-side form on the own data (the j side is its negative)
+  double bo = 0.0;
+  if (tl < NS) {
+    const int a = tl;
+    double v = rho * m.mm[a] * Ds[a] * Xs_o[a] / (totMass * dij * sigma_o * rho_o);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) v -= rho * Ys[a] * m.mm[q] * Ds[q] * Xs_o[q] / (totMass * dij * sigma_o * rho_o);
+    bo = v;
+  }
+  double col[NS];  // dJ/drho column k = b - RHOS_S, own side (signed)
+  const int k = b - RHOS_S;
+  const int kk = (k >= 0 && k < NS) ? k : 0;
+  const double dko = rho * Ds[kk] * totMass_o * sigma_o / (dij * totMass * rho_o);
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    double v = __shfl(bo, a, 16);
+    if (k >= 0) {
+      v -= rho * Ys[a] * Ds[kk] * totMass_o * sigma_o / (dij * totMass * rho_o);
+      if (a == k) v += dko;
+    }
+    col[a] = J ? -v : v;
+  }
+  if (b >= nVar) return;
+  if (k >= 0) {
+    double to[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) to[q] = 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_o);
+#pragma unroll
+    for (int a = 0; a < NS; ++a)
+      if (a == k) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) col[a] += to[q];
+      }
+  }
+  // dF/dV flow block of the own side: F_j = the i-side base, F_i = its negative (zeros included: -0.0)
+  double F[NF][NF];
+#pragma unroll
+  for (int r = 0; r < NF; ++r)
+#pragma unroll
+    for (int c = 0; c < NF; ++c) F[r][c] = 0.0;
+  double UN[NDIM], th[NDIM][NDIM], pi[NDIM];
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) UN[d] = sm[L::UN + d];
+#pragma unroll
+  for (int a = 0; a < NDIM; ++a)
+#pragma unroll
+    for (int c = 0; c < NDIM; ++c) th[a][c] = (a == c) ? theta + UN[a] * UN[a] / 3.0 : UN[a] * UN[c] / 3.0;
+#pragma unroll
+  for (int c = 0; c < NDIM; ++c) {
+    double p = sm[L::VM] * th[0][c];
+#pragma unroll
+    for (int a = 1; a < NDIM; ++a) p += sm[L::VM + a] * th[a][c];
+    pi[c] = p;
+  }
+#pragma unroll
+  for (int a = 0; a < NDIM; ++a)
+#pragma unroll
+    for (int c = 0; c < NDIM; ++c) F[1 + a][1 + c] = mu * th[a][c] / dij * dS;
+#pragma unroll
+  for (int c = 0; c < NDIM; ++c) F[RHOE_S][1 + c] = pi[c] * mu / dij * dS;
+  F[RHOE_S][RHOE_S] = ktr * theta / dij * dS;
+  if (!J) {
+#pragma unroll
+    for (int r = 0; r < NF; ++r)
+#pragma unroll
+      for (int c = 0; c < NF; ++c) F[r][c] = -F[r][c];
+  }
+#pragma unroll
+  for (int q = 0; q < NS; ++q) F[RHOE_S][RHOE_S] += -0.5 * Jd[q] * Cps[q];
+  double F0k = 0.0, F3k = 0.0;
+  if (k >= 0) {
+#pragma unroll
+    for (int a = 0; a < NS; ++a) {
+      F0k += -col[a] * dS;
+      F3k += -col[a] * hs[a] * dS;
+    }
+  }
+  double dso = 0.0;  // 3-D species-species diagonal closure term (own side)
+  auto pm = [&](double f, double x) { return J ? f + x : f - x; };  // FJ += x / FI -= x
+  if (P.rans) {
+#pragma unroll
+    for (int a = 0; a < NDIM; ++a)
+#pragma unroll
+      for (int c = 0; c < NDIM; ++c) F[1 + a][1 + c] = pm(F[1 + a][1 + c], mut * th[a][c] / sq * Area);
+#pragma unroll
+    for (int c = 0; c < NDIM; ++c) F[RHOE_S][1 + c] = pm(F[RHOE_S][1 + c], pi[c] * mut / sq * Area);
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+      F[RHOE_S][RHOE_S] = pm(F[RHOE_S][RHOE_S], mut / PrT * Cps[q] * Ys[q] * theta / sq * Area);
+    if (k >= 0) {
+      if constexpr (NDIM == 2) {
+        F3k = pm(F3k, mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_o * theta / sq * Area);
+      } else {
+        dso = mut * Ys[kk] / (PrT * LeT) / rho_o * theta / sq * Area;
+        F3k = pm(F3k, mut / (PrT * LeT) * hs[kk] / rho_o * theta / sq * Area);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NS; ++q) F[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
+  }
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) F[RHOE_S][1 + d] += 0.5 * sm[L::PF + d];
+  double co[NDIM];  // dV/dU velocity rows, column b, own node
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) {
+    if (b == 0) co[d] = -sm[(J ? L::VJ : L::VI) + d] / rho_o;
+    else co[d] = (b == 1 + d) ? 1.0 / rho_o : 0.0;
+  }
+  const double d0 = (b == 0) ? 1.0 : 0.0;
+#pragma unroll
+  for (int r = 0; r < NF; ++r) {
+    double so = 0.0;
+    so += F[r][0] * d0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) so += F[r][1 + d] * co[d];
+    so += F[r][RHOE_S] * Sob;
+    if (k >= 0) {
+      if (r == 0) so += F0k;
+      else if (r == RHOE_S) so += F3k;
+    }
+    put(r, so);
+  }
+#pragma unroll
+  for (int a = 0; a < NS; ++a) {
+    double so = 0.0;
+    if (k >= 0) {
+      so = -col[a] * dS;
+      if (NDIM == 3 && a == k) so = pm(so, dso);
+    }
+    put(RHOS_S + a, so);
+  }
+}
+
 template <int NS, int NDIM>
 __device__ inline void visc_jac_column(const DevMech& m, const ViscParams& P, const SummCRef sm,
                                        double Sib, double Sjb, int b, int tl, double* __restrict__ Ji,
