@@ -1490,9 +1490,13 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
     RX_HIP(hipGetLastError());
   }
   // the node-centric viscous Jacobians + assembly (k_asm_visc, launched by rx_launch_assemble) replace k_visc_jac
-  // and k_assemble's viscous pass; RX_NO_ASM_VISC=1 restores the edge kernel + node assembly (A/B, diagnosis)
-  static const bool no_asm_visc = getenv("RX_NO_ASM_VISC") != nullptr;
-  ctx->asm_visc = ctx->cfg.implicit && !no_asm_visc ? 1 : 0;
+  // and k_assemble's viscous pass when RX_ASM_VISC=1 (default off until measured on the GPU; RX_ASM_VISC=0 / unset:
+  // the edge kernel + node assembly)
+  static const bool asm_visc = [] {
+    const char* v = getenv("RX_ASM_VISC");
+    return v && v[0] == '1';
+  }();
+  ctx->asm_visc = ctx->cfg.implicit && asm_visc ? 1 : 0;
   if (ctx->cfg.implicit && ctx->asm_visc) return RX_OK;
   if (ctx->cfg.implicit) {
     RxPhase ph(ctx, RX_K_VISC_JAC);
