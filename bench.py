@@ -118,7 +118,7 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         # Jacobian's species rows and residual in; diagonal blocks + residual out
         "ASSEMBLE": (hbm(4 * E * blk + 2 * E * nVar * d + N * (ns * nVar + nVar) * d + N * (blk + nVar * d),
                          f"k_assemble<{nVar}, {4 if max_degree <= 4 else 8}>")  # register path by max degree
-                     if os.environ.get("RX_ASM_VISC", "0") != "1" else
+                     if os.environ.get("RX_ASM_VISC", "1") == "0" else
                      # k_asm_visc (round 4: viscous Jacobians made by the node-centric assembly, VISC_JAC not
                      # launched): each edge's two convective blocks, summary record, fluxes and ends' dT/dU in once,
                      # the source rows; the two off-diagonal blocks, the diagonal blocks and the residual out

@@ -1490,11 +1490,11 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
     RX_HIP(hipGetLastError());
   }
   // the node-centric viscous Jacobians + assembly (k_asm_visc, launched by rx_launch_assemble) replace k_visc_jac
-  // and k_assemble's viscous pass when RX_ASM_VISC=1 (default off until measured on the GPU; RX_ASM_VISC=0 / unset:
-  // the edge kernel + node assembly)
+  // and k_assemble's viscous pass (C3: 3.57 + 2.17 -> 5.13 ms, 128/128 GPU tests bitwise); RX_ASM_VISC=0 restores
+  // the edge kernel + node assembly (A/B, diagnosis)
   static const bool asm_visc = [] {
     const char* v = getenv("RX_ASM_VISC");
-    return v && v[0] == '1';
+    return !(v && v[0] == '0');
   }();
   ctx->asm_visc = ctx->cfg.implicit && asm_visc ? 1 : 0;
   if (ctx->cfg.implicit && ctx->asm_visc) return RX_OK;
