@@ -11,7 +11,10 @@
 
 namespace rx {
 
-constexpr int kSummTile = 64;  // edges per tile of the viscous summary scratch (rx_visc.h SummRef)
+#ifndef RX_SUMM_TILE
+#define RX_SUMM_TILE 64  // build knob: edges per tile of the viscous summary scratch (1: edge-major records)
+#endif
+constexpr int kSummTile = RX_SUMM_TILE;  // edges per tile of the viscous summary scratch (rx_visc.h SummRef)
 constexpr double kEPS = 1.0e-16;  // Common/include/option_structure.hpp:134
 constexpr double kNA = 6.02214129 * 1.0e23;
 constexpr double kKB = 1.3806488 * 1.0e-23;

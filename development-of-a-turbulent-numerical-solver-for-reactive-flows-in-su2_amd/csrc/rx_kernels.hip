@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_VJAC void k_visc_jac(int E, const in
                                                      const double* __restrict__ Jc,
                                                      const int64_t* __restrict__ edge_blk, double* __restrict__ A) {
   constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>(), kEB = kBlock / 16;
-  static_assert(kSummTile % kEB == 0, "a workgroup's edges lie in one summary tile");
+
   // the workgroup's kEB consecutive edge records, staged from their tile: each load is kEB consecutive doubles
   __shared__ double ssm[SS * kEB];
   const int eb = blockIdx.x * kEB;
@@ -746,12 +746,9 @@ __global__ __launch_bounds__(kBlock) RX_WPE_VJAC void k_visc_jac(int E, const in
     sjb = dTdU[(size_t)n1 * nVar + bc];
     if (kEarlyJc && Jc) load_jc();
   }
-  {
-    const double* tile = Summ + (size_t)(eb / kSummTile) * SS * kSummTile + eb % kSummTile;
-    for (int q = threadIdx.x; q < SS * kEB; q += kBlock) {
-      const int k = q / kEB, el = q - k * kEB;
-      if (eb + el < E) ssm[q] = tile[(size_t)k * kSummTile + el];
-    }
+  for (int q = threadIdx.x; q < SS * kEB; q += kBlock) {
+    const int k = q / kEB, el = q - k * kEB, ee = eb + el;
+    if (ee < E) ssm[q] = Summ[(size_t)(ee / kSummTile) * SS * kSummTile + (size_t)k * kSummTile + ee % kSummTile];
   }
   __syncthreads();
   if (!live) return;  // whole teams exit together (E * 16 threads)
@@ -955,6 +952,9 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int3
 // each edge is still evaluated once. Every diagonal entry, residual component and off-diagonal entry is the same
 // sum in the same order as k_visc_jac + k_assemble make it, so the system is bitwise theirs; the per-edge viscous
 // blocks (2 x 968 B per edge, written once and read once) and the second read of the convective blocks are gone.
+#ifndef RX_ASMV_CDEG
+#define RX_ASMV_CDEG 0  // build knob: node degree up to which k_asm_visc's convective pass loads everything first
+#endif
 #ifndef RX_WPE_ASMV
 #define RX_WPE_ASMV RX_WPE(NDIM == 2 ? 3 : 2)
 #endif
@@ -978,20 +978,45 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   double r = 0.0, D[nVar];
 #pragma unroll
   for (int a = 0; a < nVar; ++a) D[a] = 0.0;
-  // convective pass
-  for (int k = k0; k < k1; ++k) {
-    const int ad = adj[k];
-    const size_t e = (size_t)(ad >> 1);
-    const int side = ad & 1;
-    if (col) {
-      const double f = Fc[e * nVar + b];
-      r = side ? r - f : r + f;
-    }
-    const double* J = Jc + (e * 2 + side) * nVar2 + bc;
+  // convective pass; for degrees up to RX_ASMV_CDEG every load of the pass is issued before the first sum (one round
+  // trip instead of one per edge), then the sums run in edge order
+  if (RX_ASMV_CDEG > 0 && k1 - k0 <= RX_ASMV_CDEG) {
+    constexpr int CD = RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1;
+    int sd[CD];
+    double fc[CD], jc[CD][nVar];
 #pragma unroll
-    for (int a = 0; a < nVar; ++a) {
-      const double jd = J[a * nVar];
-      D[a] = side ? D[a] - jd : D[a] + jd;
+    for (int q = 0; q < CD; ++q) {
+      const int k = k0 + q < k1 ? k0 + q : k0;  // clamped: always a valid address
+      const int ad = adj[k];
+      const size_t e = (size_t)(ad >> 1);
+      sd[q] = ad & 1;
+      fc[q] = Fc[e * nVar + bc];
+      const double* J = Jc + (e * 2 + sd[q]) * nVar2 + bc;
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) jc[q][a] = J[a * nVar];
+    }
+#pragma unroll
+    for (int q = 0; q < CD; ++q)
+      if (k0 + q < k1) {
+        if (col) r = sd[q] ? r - fc[q] : r + fc[q];
+#pragma unroll
+        for (int a = 0; a < nVar; ++a) D[a] = sd[q] ? D[a] - jc[q][a] : D[a] + jc[q][a];
+      }
+  } else {
+    for (int k = k0; k < k1; ++k) {
+      const int ad = adj[k];
+      const size_t e = (size_t)(ad >> 1);
+      const int side = ad & 1;
+      if (col) {
+        const double f = Fc[e * nVar + b];
+        r = side ? r - f : r + f;
+      }
+      const double* J = Jc + (e * 2 + side) * nVar2 + bc;
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) {
+        const double jd = J[a * nVar];
+        D[a] = side ? D[a] - jd : D[a] + jd;
+      }
     }
   }
   // viscous pass
