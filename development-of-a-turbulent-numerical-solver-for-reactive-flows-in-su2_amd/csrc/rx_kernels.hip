@@ -953,8 +953,8 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int3
 // sum in the same order as k_visc_jac + k_assemble make it, so the system is bitwise theirs; the per-edge viscous
 // blocks (2 x 968 B per edge, written once and read once) and the second read of the convective blocks are gone.
 #ifndef RX_ASMV_CDEG
-#define RX_ASMV_CDEG 0  // build knob: node degree up to which k_asm_visc's convective pass loads everything first
-#endif
+#define RX_ASMV_CDEG -1  // build knob: node degree up to which k_asm_visc's convective pass loads everything first
+#endif                   // (-1: the quad / hex stencils' 4 in 2-D, 6 in 3-D; 0: never)
 #ifndef RX_WPE_ASMV
 #define RX_WPE_ASMV RX_WPE(NDIM == 2 ? 3 : 2)
 #endif
@@ -980,8 +980,8 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   for (int a = 0; a < nVar; ++a) D[a] = 0.0;
   // convective pass; for degrees up to RX_ASMV_CDEG every load of the pass is issued before the first sum (one round
   // trip instead of one per edge), then the sums run in edge order
-  if (RX_ASMV_CDEG > 0 && k1 - k0 <= RX_ASMV_CDEG) {
-    constexpr int CD = RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1;
+  constexpr int CD = RX_ASMV_CDEG < 0 ? (NDIM == 2 ? 4 : 6) : (RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1);
+  if (RX_ASMV_CDEG != 0 && k1 - k0 <= CD) {
     int sd[CD];
     double fc[CD], jc[CD][nVar];
 #pragma unroll
