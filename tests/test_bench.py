@@ -22,6 +22,8 @@ def test_kernel_models_cover_the_timed_phases():
     for k in ("CONV", "VISC", "VISC_JAC", "ASSEMBLE", "GRAD", "SOURCE", "ILU_BUILD", "SPMV", "ILU_APPLY"):
         assert k in m and m[k]["kernel"] and m[k]["peak"] > 0, k
     assert m["SPMV"]["unit"] == "GB/s" and m["ILU_APPLY"]["kernel"].startswith("k_ilu_apply_")
+    # the node-centric viscous assembly (default) replaces k_visc_jac + k_assemble's viscous pass
+    assert os.environ.get("RX_ASM_VISC", "1") == "0" or m["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>"
 
 
 def test_cpu_baseline_reference_runs_the_compiled_reference():
