@@ -106,7 +106,8 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
     # k_visc_edge's FP64 work: counted by PMC on this workload when a count is committed, else SURVEY §8(d)'s
     # ~9 kflop per edge (the C3 count is 13.9 kflop per edge, profiles/r02_c3_v2_fp64.json)
     visc_flop = pmc_fp64_flop("k_visc_edge" + te, workload_key) or 9000.0 * E
-    return {
+    fused = conv_fused(nDim)
+    models = {
         # k_ausm_edge: V (nPV) and dPdU (nVar) per node once; edge (2 int32 + normal); flux + 2 Jacobians
         "CONV": hbm(N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk), "k_ausm_edge" + te),
         "VISC": dict(bound="fp64", work=float(visc_flop), unit="TFLOP/s", peak=FP64_PEAK_TFS,
@@ -123,6 +124,12 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
                      # launched): each edge's two convective blocks, summary record, fluxes and ends' dT/dU in once,
                      # the source rows; the two off-diagonal blocks, the diagonal blocks and the residual out
                      hbm(2 * E * blk + 2 * E * nVar * d + E * summ + N * nVar * d + 24 * E
+                         + N * (ns * nVar + nVar) * d + 2 * E * blk + N * (blk + nVar * d), "k_asm_visc" + te)
+                     if not fused else
+                     # k_asm_visc with the fused AUSM pass (round 4, k_ausm_edge not launched): V and dP/dU per
+                     # node and each edge's normal once, the viscous fluxes, summary records, dT/dU and index
+                     # arrays, the source rows; the two off-diagonal blocks, the diagonal blocks and the residual out
+                     hbm(N * (nPV + nVar) * d + E * nDim * d + E * nVar * d + E * summ + N * nVar * d + 24 * E
                          + N * (ns * nVar + nVar) * d + 2 * E * blk + N * (blk + nVar * d), "k_asm_visc" + te)),
         "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq" + te),
         # k_source: V, dT/dU, volume, omega in; residual + the Jacobian's species rows out
@@ -139,6 +146,18 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         # ILU(0) apply: L and U blocks + inv(D_i) (= nnzb blocks) + column indices, b in, x out
         "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, ilu_apply_kernels(N, nnzb, nVar, parts)),
     }
+    if fused:
+        del models["CONV"]  # the CONV phase launches no flux kernel (only MUSCL's reconstruction at 2nd order)
+    return models
+
+
+def conv_fused(nDim):
+    """Whether the implicit AUSM fluxes and Jacobians are made inside k_asm_visc (rx_fuse_conv, rx_kernels.hip):
+    in 2-D by default, RX_ASM_CONV=1 / 0 in both / neither, never with RX_ASM_VISC=0."""
+    if os.environ.get("RX_ASM_VISC", "1") == "0":
+        return False
+    v = os.environ.get("RX_ASM_CONV")
+    return v == "1" if v is not None else nDim == 2
 
 
 def pmc_traffic(kernel, workload_key, field="hbm_bytes"):
@@ -509,7 +528,8 @@ def main():
                    "sst_lin_iters_mean": float(np.mean([b for _, b in timed_its]))},
         "roofline": kernels[dom],
         "roofline_longest_launch": kernels[longest],
-        "roofline_edge_flux": kernels.get("CONV"),
+        # the edge flux: k_ausm_edge, or (fused, the default) the assembly kernel that now evaluates it
+        "roofline_edge_flux": kernels.get("CONV") or dict(kernels.get("ASSEMBLE") or {}, fused_into_assembly=True),
         "roofline_kernels": kernels,
         "phase_ms_per_step": {k: round(v, 4) for k, v in phase_ms.items()},
     }

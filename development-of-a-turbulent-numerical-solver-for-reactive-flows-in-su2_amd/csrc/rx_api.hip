@@ -759,7 +759,7 @@ int64_t rx_last_error_index(const rx_ctx* ctx) { return ctx ? ctx->last_err_inde
 int rx_residual_zero(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
   RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
-  ctx->phase_conv = ctx->phase_visc = ctx->phase_src = ctx->offdiag_done = 0;
+  ctx->phase_conv = ctx->phase_visc = ctx->phase_src = ctx->offdiag_done = ctx->conv_deferred = 0;
   ctx->assembled = ctx->cfg.implicit ? 0 : 1;
   if (ctx->bc_on && ctx->bc_stream && !ctx->capturing) {
     // the boundary fluxes of the current node records, overlapped with the interior sweeps (rx_bc.hip)
@@ -778,7 +778,8 @@ int rx_edge_flux_conv(rx_ctx* ctx) {
   RxPhase ph(ctx, RX_K_CONV);
   int rc = RX_OK;
   if (ctx->cfg.spatial_order && (rc = rx_launch_muscl(ctx))) return rc;
-  rc = ctx->cfg.implicit ? rx_launch_ausm_edge(ctx) : rx_launch_ausm_node(ctx);
+  ctx->conv_deferred = ctx->cfg.implicit && rx_fuse_conv(ctx->nDim) ? 1 : 0;
+  if (!ctx->conv_deferred) rc = ctx->cfg.implicit ? rx_launch_ausm_edge(ctx) : rx_launch_ausm_node(ctx);
   if (rc) return rc;
   ctx->phase_conv = 1;
   ctx->offdiag_done = 0;  // new convective blocks: off-diagonals are (re)assembled from them

@@ -133,6 +133,7 @@ struct rx_ctx {
   double* recon = nullptr;   // [E][2][nPV] reconstructed edge states + [E][2][nVar] their dP/dU (2nd order)
   int phase_conv = 0, phase_visc = 0, phase_src = 0, assembled = 1;
   int offdiag_done = 0;      // k_visc_jac wrote the off-diagonal blocks of this residual (fused assembly)
+  int conv_deferred = 0;     // implicit AUSM left to the assembly (rx_fuse_conv): k_asm_visc or, without it, k_ausm_edge
   int asm_visc = 0;          // this residual's viscous Jacobians are made by the assembly (k_asm_visc), not k_visc_jac
   double* lim_mn = nullptr;  // [N][nL]
   double* lim_mx = nullptr;
@@ -235,6 +236,7 @@ int rx_launch_ausm_node(rx_ctx* ctx);
 int rx_launch_muscl(rx_ctx* ctx);
 int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter);
 int rx_launch_ausm_edge(rx_ctx* ctx);
+bool rx_fuse_conv(int nDim);
 int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);
 int rx_launch_source(rx_ctx* ctx);

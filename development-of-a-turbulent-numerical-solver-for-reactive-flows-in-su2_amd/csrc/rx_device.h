@@ -97,7 +97,13 @@ template <int N>
 __device__ __host__ inline double pick(const double* a, int idx) {
   double v = a[0];
 #pragma unroll
-  for (int q = 1; q < N; ++q) v = (idx == q) ? a[q] : v;
+  for (int q = 1; q < N; ++q) {
+    double aq = a[q];
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(aq));  // a value, not a load: the selects cannot fold back into an indexed load
+#endif
+    v = (idx == q) ? aq : v;
+  }
   return v;
 }
 

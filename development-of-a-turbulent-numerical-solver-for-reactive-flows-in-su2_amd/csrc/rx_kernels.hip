@@ -952,6 +952,15 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int N, int rhos, const int3
 // each edge is still evaluated once. Every diagonal entry, residual component and off-diagonal entry is the same
 // sum in the same order as k_visc_jac + k_assemble make it, so the system is bitwise theirs; the per-edge viscous
 // blocks (2 x 968 B per edge, written once and read once) and the second read of the convective blocks are gone.
+// inputs of k_asm_visc's fused AUSM pass (V == nullptr: the convective blocks and fluxes come from k_ausm_edge)
+struct AusmIn {
+  const double *V, *dPdU, *VR, *SR, *normal;
+  double mInfty;
+  int* err;
+};
+#ifndef RX_ASMV_FUSE
+#define RX_ASMV_FUSE 1  // build knob: 0 compiles k_asm_visc without its fused AUSM pass
+#endif
 #ifndef RX_ASMV_CDEG
 #define RX_ASMV_CDEG -1  // build knob: node degree up to which k_asm_visc's convective pass loads everything first
 #endif                   // (-1: the quad / hex stencils' 4 in 2-D, 6 in 3-D; 0: never)
@@ -964,8 +973,9 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     const int64_t* __restrict__ edge_blk, const int64_t* __restrict__ diag, const double* __restrict__ Fc,
     const double* __restrict__ Fv, const double* __restrict__ Jc, const double* __restrict__ dTdU,
     const double* __restrict__ Summ, const double* __restrict__ Js, const double* __restrict__ Rsrc, DevMech m,
-    ViscParams P, double* __restrict__ R, double* __restrict__ A, int src) {
+    ViscParams P, double* __restrict__ R, double* __restrict__ A, int src, AusmIn cv) {
   constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>(), kTeams = kBlock / 16;
+  constexpr int nPV = NS + NDIM + 5;
   constexpr int rhos = NDIM + 2, nsv = NS * nVar;
   __shared__ double ssm[kTeams * SS];
   const int gt = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
@@ -981,7 +991,57 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   // convective pass; for degrees up to RX_ASMV_CDEG every load of the pass is issued before the first sum (one round
   // trip instead of one per edge), then the sums run in edge order
   constexpr int CD = RX_ASMV_CDEG < 0 ? (NDIM == 2 ? 4 : 6) : (RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1);
-  if (RX_ASMV_CDEG != 0 && k1 - k0 <= CD) {
+  if (RX_ASMV_FUSE && cv.V) {
+    // fused AUSM (cv.V set, k_ausm_edge skipped): the edge's flux and its own-side Jacobian column are evaluated here
+    // with k_ausm_edge's arithmetic (the other side's column by the neighbour's team), folded into the residual and
+    // diagonal in edge order, and parked in the neighbour row's off-diagonal block as 0 -+ J for the viscous pass
+    auto fused_edge = [&](int ad, int n0, int n1) {
+      const size_t e = (size_t)(ad >> 1);
+      const int side = ad & 1;
+      const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
+      const double* Vsj = cv.VR ? cv.VR + (2 * e + 1) * nPV : cv.V + (size_t)n1 * nPV;
+      const double* Ssi = cv.VR ? cv.SR + 2 * e * nVar : cv.dPdU + (size_t)n0 * nVar;
+      const double* Ssj = cv.VR ? cv.SR + (2 * e + 1) * nVar : cv.dPdU + (size_t)n1 * nVar;
+      double Vi[nPV], Vj[nPV], nrm[NDIM];  // the entries ausm_scalars reads (the convected states are re-read below)
+#pragma unroll
+      for (int v = 0; v < nPV; ++v) {
+        Vi[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsi[v] : 0.0;
+        Vj[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsj[v] : 0.0;
+      }
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[e * NDIM + d];
+      const double sib = Ssi[bc], sjb = Ssj[bc];
+      double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
+      AusmEdge s;
+      ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+      bool bad = false;
+      if (col) {
+        const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
+        const double pi = b == 0 ? 1.0 : Vsi[pidx];
+        const double pj = b == 0 ? 1.0 : Vsj[pidx];
+        double f = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
+        if (b >= 1 && b <= NDIM) f += s.pLF * pick<NDIM>(s.UN, b - 1) * s.Area;
+        bad |= isnan(f);
+        r = side ? r - f : r + f;
+      }
+      const AusmCol cc = ausm_col_b<NDIM>(s, sib, sjb, bc);
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) {
+        double ji, jj;
+        ausm_jac_entry<NDIM>(s, cc, ausm_phi<NDIM>(Vsi, Vsi[NDIM + 3], a), ausm_phi<NDIM>(Vsj, Vsj[NDIM + 3], a), sib,
+                             sjb, a, bc, &ji, &jj);
+        bad |= isnan(ji) || isnan(jj);
+        const double jd = side ? jj : ji;
+        D[a] = side ? D[a] - jd : D[a] + jd;
+        if (col) Ao[a * nVar + b] = side ? 0.0 + jd : 0.0 - jd;
+      }
+      if (col && bad) set_err(cv.err, ERR_NAN, (int64_t)e);
+    };
+    for (int k = k0; k < k1; ++k) {
+      const int ad = adj[k];
+      fused_edge(ad, edges[2 * (ad >> 1)], edges[2 * (ad >> 1) + 1]);
+    }
+  } else if (RX_ASMV_CDEG != 0 && k1 - k0 <= CD) {
     int sd[CD];
     double fc[CD], jc[CD][nVar];
 #pragma unroll
@@ -1030,11 +1090,15 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
       for (int q = b; q < SS; q += 16) slot[q] = tile[(size_t)q * kSummTile];
     }
     const double sob = dTdU[(size_t)(side ? n1 : n0) * nVar + bc];  // the own node's dT/dU
-    double jco[nVar];  // this lane's column of the own-side convective block (for the off-diagonal)
-    {
+    double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
+    double jco[nVar];  // this lane's column of the own-side convective block, or (fused AUSM) 0 -+ that column
+    if (RX_ASMV_FUSE && cv.V) {
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) jco[a] = col ? Ao[a * nVar + b] : 0.0;
+    } else {
       const double* J = Jc + ((size_t)e * 2 + side) * nVar2 + bc;
 #pragma unroll
-      for (int a = 0; a < nVar; ++a) jco[a] = J[a * nVar];
+      for (int a = 0; a < nVar; ++a) jco[a] = side ? 0.0 + J[a * nVar] : 0.0 - J[a * nVar];
     }
     if (col) {
       const double f = Fv[(size_t)e * nVar + b];
@@ -1042,10 +1106,9 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
     visc_jac_column_own<NS, NDIM>(m, P, SummCRef{slot, 1}, sob, side, b, b, [&](int rr, double jv) {
       D[rr] = side ? D[rr] + jv : D[rr] - jv;
-      Ao[rr * nVar + b] = side ? (0.0 + jco[rr]) - jv : (0.0 - jco[rr]) + jv;
+      Ao[rr * nVar + b] = side ? jco[rr] - jv : jco[rr] + jv;
     });
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -1492,6 +1555,20 @@ int rx_launch_ausm_node(rx_ctx* ctx) {
   return RX_OK;
 }
 
+// the implicit convective fluxes and Jacobians are made by the node-centric assembly (k_asm_visc's fused AUSM pass)
+// instead of k_ausm_edge when the assembly also makes the viscous Jacobians, in 2-D by default: C3 (same box) CONV
+// 1.31 + ASSEMBLE 4.89 -> ASSEMBLE 6.79 ms; in 3-D each node's 6 edges and the 2-wave occupancy lose, C5 CONV 2.29 +
+// ASSEMBLE 8.71 -> 12.10 ms. RX_ASM_CONV=1 fuses in both, =0 in neither (A/B); RX_ASM_VISC=0 never fuses
+bool rx_fuse_conv(int nDim) {
+  static const int mode = [] {
+    const char* v = getenv("RX_ASM_CONV");
+    const char* w = getenv("RX_ASM_VISC");
+    if (w && w[0] == '0') return 0;
+    return v ? (v[0] == '1' ? 1 : 0) : 2;
+  }();
+  return mode == 1 || (mode == 2 && nDim == 2);
+}
+
 int rx_launch_ausm_edge(rx_ctx* ctx) {
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_ausm_edge<NS_, ND_><<<blocks(ctx->E * kAusmTeam, kAusmBlock), kAusmBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
@@ -1559,13 +1636,27 @@ int rx_launch_source(rx_ctx* ctx) {
 
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   const int nv = ctx->nVar;
+  const bool fused_conv = ctx->conv_deferred && with_visc && ctx->asm_visc;
+  if (ctx->conv_deferred && !fused_conv) {  // deferred, but no viscous pass to fuse it into: the edge kernel now
+    const int rc = rx_launch_ausm_edge(ctx);
+    if (rc) return rc;
+  }
+  ctx->conv_deferred = 0;
   if (with_visc && ctx->asm_visc) {  // k_visc_jac was skipped: the node-centric viscous Jacobians + assembly
     ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
                  ctx->cfg.rans, ctx->cfg.implicit};
+    AusmIn cv{nullptr, nullptr, nullptr, nullptr, nullptr, ctx->cfg.mach_inf, ctx->err};
+    if (fused_conv) {
+      cv.V = ctx->f[RX_F_V];
+      cv.dPdU = ctx->f[RX_F_DPDU];
+      cv.VR = ctx->cfg.spatial_order ? ctx->recon : nullptr;
+      cv.SR = ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
+      cv.normal = ctx->normal;
+    }
     RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<blocks(ctx->N * 16), kBlock, 0, ctx->stream>>>(
                               (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
                               ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech,
-                              P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src)));
+                              P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv)));
     RX_HIP(hipGetLastError());
     return RX_OK;
   }

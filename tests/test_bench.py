@@ -17,13 +17,24 @@ def test_ilu_apply_kernel_names(monkeypatch):
     assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_fwd_wide<11, 1024>+k_ilu_bwd_wide<11, 1024>"
 
 
-def test_kernel_models_cover_the_timed_phases():
+def test_kernel_models_cover_the_timed_phases(monkeypatch):
+    monkeypatch.delenv("RX_ASM_CONV", raising=False)
+    monkeypatch.delenv("RX_ASM_VISC", raising=False)
     m = bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)
-    for k in ("CONV", "VISC", "VISC_JAC", "ASSEMBLE", "GRAD", "SOURCE", "ILU_BUILD", "SPMV", "ILU_APPLY"):
+    for k in ("VISC", "VISC_JAC", "ASSEMBLE", "GRAD", "SOURCE", "ILU_BUILD", "SPMV", "ILU_APPLY"):
         assert k in m and m[k]["kernel"] and m[k]["peak"] > 0, k
     assert m["SPMV"]["unit"] == "GB/s" and m["ILU_APPLY"]["kernel"].startswith("k_ilu_apply_")
-    # the node-centric viscous assembly (default) replaces k_visc_jac + k_assemble's viscous pass
-    assert os.environ.get("RX_ASM_VISC", "1") == "0" or m["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>"
+    # the node-centric assembly (default) makes the viscous Jacobians and the AUSM fluxes / Jacobians itself:
+    # no k_ausm_edge launch in the CONV phase, and no per-edge convective blocks in the assembly's bytes
+    assert m["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>" and "CONV" not in m
+    m3 = bench.kernel_models(8_000_000, 23_580_000, 62_000_000, 7, 3, 5)  # 3-D: the edge kernel by default
+    assert m3["CONV"]["kernel"] == "k_ausm_edge<7, 3>"
+    monkeypatch.setenv("RX_ASM_CONV", "0")
+    u = bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)
+    assert u["CONV"]["kernel"] == "k_ausm_edge<7, 2>" and u["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>"
+    assert u["ASSEMBLE"]["work"] > m["ASSEMBLE"]["work"]
+    monkeypatch.setenv("RX_ASM_VISC", "0")
+    assert bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)["ASSEMBLE"]["kernel"] == "k_assemble<11, 4>"
 
 
 def test_cpu_baseline_reference_runs_the_compiled_reference():
