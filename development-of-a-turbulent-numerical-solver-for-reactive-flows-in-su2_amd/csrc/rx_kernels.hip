@@ -958,6 +958,9 @@ struct AusmIn {
   double mInfty;
   int* err;
 };
+#ifndef RX_ASMV_SHS
+#define RX_ASMV_SHS 1  // build knob: the fused AUSM pass makes each edge's scalars once per team (LDS-shared)
+#endif
 #ifndef RX_ASMV_FUSE
 #define RX_ASMV_FUSE 1  // build knob: 0 compiles k_asm_visc without its fused AUSM pass
 #endif
@@ -977,25 +980,27 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>(), kTeams = kBlock / 16;
   constexpr int nPV = NS + NDIM + 5;
   constexpr int rhos = NDIM + 2, nsv = NS * nVar;
-  __shared__ double ssm[kTeams * SS];
+  constexpr int CD = RX_ASMV_CDEG < 0 ? (NDIM == 2 ? 4 : 6) : (RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1);
+  constexpr int kES = sizeof(AusmEdge) / sizeof(double);  // one edge's AUSM scalars
+  constexpr int TS = RX_ASMV_SHS && CD * kES > SS ? CD * kES : SS;  // a team's LDS slot
+  __shared__ double ssm[kTeams * TS];
   const int gt = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int i = gt / 16, b = gt % 16, team = threadIdx.x / 16;
   if (i >= N) return;  // whole teams (N * 16 threads)
   const bool col = b < nVar;
   const int bc = col ? b : 0;
-  double* slot = ssm + team * SS;
+  double* slot = ssm + team * TS;
   const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
   double r = 0.0, D[nVar];
 #pragma unroll
   for (int a = 0; a < nVar; ++a) D[a] = 0.0;
   // convective pass; for degrees up to RX_ASMV_CDEG every load of the pass is issued before the first sum (one round
   // trip instead of one per edge), then the sums run in edge order
-  constexpr int CD = RX_ASMV_CDEG < 0 ? (NDIM == 2 ? 4 : 6) : (RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1);
   if (RX_ASMV_FUSE && cv.V) {
     // fused AUSM (cv.V set, k_ausm_edge skipped): the edge's flux and its own-side Jacobian column are evaluated here
     // with k_ausm_edge's arithmetic (the other side's column by the neighbour's team), folded into the residual and
     // diagonal in edge order, and parked in the neighbour row's off-diagonal block as 0 -+ J for the viscous pass
-    auto fused_edge = [&](int ad, int n0, int n1) {
+    auto fused_edge = [&](int ad, int n0, int n1, const double* shared_s) {
       const size_t e = (size_t)(ad >> 1);
       const int side = ad & 1;
       const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
@@ -1013,7 +1018,13 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
       const double sib = Ssi[bc], sjb = Ssj[bc];
       double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
       AusmEdge s;
-      ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+      if (RX_ASMV_SHS && shared_s) {
+        double* sp = reinterpret_cast<double*>(&s);
+#pragma unroll
+        for (int f = 0; f < kES; ++f) sp[f] = shared_s[f];
+      } else {
+        ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+      }
       bool bad = false;
       if (col) {
         const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
@@ -1037,9 +1048,45 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
       }
       if (col && bad) set_err(cv.err, ERR_NAN, (int64_t)e);
     };
-    for (int k = k0; k < k1; ++k) {
+    int kq = k0;
+    if (RX_ASMV_SHS && k1 > k0) {
+      // the edge scalars of the node's first CD edges are made once, lane q of the team making edge k0 + q's (the
+      // same function on the same inputs, so the same values), and read back from the team's LDS slot
+      const int nq = k1 - k0 < CD ? k1 - k0 : CD;
+      {
+        const int ad = adj[k0 + (b < nq ? b : 0)];
+        const size_t e = (size_t)(ad >> 1);
+        const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+        const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
+        const double* Vsj = cv.VR ? cv.VR + (2 * e + 1) * nPV : cv.V + (size_t)n1 * nPV;
+        double Vi[nPV], Vj[nPV], nrm[NDIM];
+#pragma unroll
+        for (int v = 0; v < nPV; ++v) {
+          Vi[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsi[v] : 0.0;
+          Vj[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsj[v] : 0.0;
+        }
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[e * NDIM + d];
+        AusmEdge s;
+        ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+        const double* sp = reinterpret_cast<const double*>(&s);
+        if (b < nq)
+#pragma unroll
+          for (int f = 0; f < kES; ++f) slot[b * kES + f] = sp[f];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      for (int q = 0; q < nq; ++q) {
+        const int ad = adj[k0 + q];
+        fused_edge(ad, edges[2 * (ad >> 1)], edges[2 * (ad >> 1) + 1], slot + q * kES);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();  // the viscous pass reuses the slot
+      kq = k0 + nq;
+    }
+    for (int k = kq; k < k1; ++k) {
       const int ad = adj[k];
-      fused_edge(ad, edges[2 * (ad >> 1)], edges[2 * (ad >> 1) + 1]);
+      fused_edge(ad, edges[2 * (ad >> 1)], edges[2 * (ad >> 1) + 1], nullptr);
     }
   } else if (RX_ASMV_CDEG != 0 && k1 - k0 <= CD) {
     int sd[CD];
