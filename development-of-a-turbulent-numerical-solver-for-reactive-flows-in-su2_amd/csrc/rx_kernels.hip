@@ -1605,7 +1605,7 @@ int rx_launch_ausm_node(rx_ctx* ctx) {
 // the implicit convective fluxes and Jacobians are made by the node-centric assembly (k_asm_visc's fused AUSM pass)
 // instead of k_ausm_edge when the assembly also makes the viscous Jacobians, in 2-D by default: C3 (same box) CONV
 // 1.31 + ASSEMBLE 4.89 -> ASSEMBLE 6.79 ms; in 3-D each node's 6 edges and the 2-wave occupancy lose, C5 CONV 2.29 +
-// ASSEMBLE 8.71 -> 12.10 ms. RX_ASM_CONV=1 fuses in both, =0 in neither (A/B); RX_ASM_VISC=0 never fuses
+// ASSEMBLE 8.71 -> 12.10 ms (11.76 with the LDS-shared edge scalars). RX_ASM_CONV=1 fuses in both, =0 in neither (A/B); RX_ASM_VISC=0 never fuses
 bool rx_fuse_conv(int nDim) {
   static const int mode = [] {
     const char* v = getenv("RX_ASM_CONV");
