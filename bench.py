@@ -519,7 +519,8 @@ def main():
                        if parallelism.startswith("sharded") else ""),
                    "cells_per_gpu": n_owned, "halo_points": N - n_owned, "edges": E,
                    "species": ns, "nVar": ns + nDim + 2, "nnz_blocks": nnzb,
-                   "time": "EULER_IMPLICIT flow + SST (one reference outer iteration per step" +
+                   "time": f"EULER_IMPLICIT flow at CFL {cfg.cfl:g} (rx.BENCH_CFL: reference-pinned, "
+                           "profiles/r05_calibration_c2.json) + SST (one reference outer iteration per step" +
                            (", no boundary conditions)" if args.no_bc else ", jet boundary conditions)"),
                    "linear_solver": f"FGMRES(5)+ILU0 (flow {ns + nDim + 2}x{ns + nDim + 2} and SST 2x2 systems)",
                    "partitions": args.parts,

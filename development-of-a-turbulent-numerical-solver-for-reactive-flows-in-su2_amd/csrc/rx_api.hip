@@ -619,8 +619,8 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   }
   ctx->fcount[RX_F_ILU] = imp * nb2;
   if (ctx->cfg.implicit && !sst) {
-    CK(dalloc(ctx, &ctx->fconv, E * nv));
-    CK(dalloc(ctx, &ctx->jconv, E * 2 * (int64_t)nv * nv));
+    // fconv / jconv (the per-edge convective fluxes and blocks, 2 E nVar^2 doubles: 3.9 GB at C3) are allocated by
+    // the first k_ausm_edge launch (rx_launch_ausm_edge); the 2-D fused assembly never needs them
     // The per-edge viscous Jacobians and the viscous summary live only between the viscous sweep and the assembly
     // (k_visc_edge -> k_visc_jac -> k_assemble); the ILU(0) factor is written only later, by the ILU build of the
     // implicit step. So both share the ILU buffer when it is large enough (on the jet meshes it is: (2N + 2E) nVar^2
@@ -755,6 +755,8 @@ int rx_sync(rx_ctx* ctx) {
 }
 
 int64_t rx_last_error_index(const rx_ctx* ctx) { return ctx ? ctx->last_err_index : -1; }
+
+int rx_last_error_phase(const rx_ctx* ctx) { return ctx ? ctx->last_err_phase : RX_ERR_PHASE_CALL; }
 
 int rx_residual_zero(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;

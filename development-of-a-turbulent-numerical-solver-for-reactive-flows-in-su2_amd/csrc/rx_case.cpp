@@ -138,7 +138,7 @@ void rx_cfg_default(rx_cfg* c) {
   c->lewis_turb = 1.2;
   c->c_mu = 0.09;
   c->pasr_lb = 0.2;
-  c->cfl = 5.0;
+  c->cfl = 1.0;  // the bench CFL pinned against the reference (rx.BENCH_CFL, profiles/r05_calibration_c2.json)
   c->max_delta_time = 1e6;
   c->ref_elem_length = 0.1;
   c->limiter_coeff = 0.5;

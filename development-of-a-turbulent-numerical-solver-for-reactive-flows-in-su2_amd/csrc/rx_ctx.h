@@ -133,6 +133,7 @@ struct rx_ctx {
   double* recon = nullptr;   // [E][2][nPV] reconstructed edge states + [E][2][nVar] their dP/dU (2nd order)
   int phase_conv = 0, phase_visc = 0, phase_src = 0, assembled = 1;
   int offdiag_done = 0;      // k_visc_jac wrote the off-diagonal blocks of this residual (fused assembly)
+  int last_err_phase = 0;    // rx_err_phase of the last RX_ERR_NAN (rx_check_error)
   int conv_deferred = 0;     // implicit AUSM left to the assembly (rx_fuse_conv): k_asm_visc or, without it, k_ausm_edge
   int asm_visc = 0;          // this residual's viscous Jacobians are made by the assembly (k_asm_visc), not k_visc_jac
   double* lim_mn = nullptr;  // [N][nL]

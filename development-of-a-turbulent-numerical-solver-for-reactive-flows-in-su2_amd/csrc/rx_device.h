@@ -22,7 +22,7 @@ constexpr double kR = kNA * kKB * 1.0e3;           // physical_chemical_library.
 constexpr double kRatm = 1.0e-3 * 0.082057338;     // :579
 constexpr double kTWO3 = 2.0 / 3.0;
 enum { P_CP = 0, P_H = 1, P_S = 2, P_MU = 3, P_KAPPA = 4 };
-enum { ERR_NONE = 0, ERR_RANGE = 1, ERR_NAN = 2, ERR_GEOM = 3, ERR_CONV = 4 };
+enum { ERR_NONE = 0, ERR_RANGE = 1, ERR_NAN = 2, ERR_GEOM = 3, ERR_CONV = 4, ERR_NAN_UPWIND = 5 };  // 5: fused AUSM pass
 
 constexpr int kMaxNS = 12;
 constexpr int kMaxNR = 8;

@@ -983,6 +983,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   constexpr int CD = RX_ASMV_CDEG < 0 ? (NDIM == 2 ? 4 : 6) : (RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1);
   constexpr int kES = sizeof(AusmEdge) / sizeof(double);  // one edge's AUSM scalars
   constexpr int TS = RX_ASMV_SHS && CD * kES > SS ? CD * kES : SS;  // a team's LDS slot
+  static_assert(CD <= 16, "the shared edge scalars of the first CD edges are made by team lanes 0..CD-1 (16 lanes)");
   __shared__ double ssm[kTeams * TS];
   const int gt = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int i = gt / 16, b = gt % 16, team = threadIdx.x / 16;
@@ -1046,7 +1047,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
         D[a] = side ? D[a] - jd : D[a] + jd;
         if (col) Ao[a * nVar + b] = side ? 0.0 + jd : 0.0 - jd;
       }
-      if (col && bad) set_err(cv.err, ERR_NAN, (int64_t)e);
+      if (col && bad) set_err(cv.err, ERR_NAN_UPWIND, (int64_t)e);
     };
     int kq = k0;
     if (RX_ASMV_SHS && k1 > k0) {
@@ -1560,6 +1561,7 @@ int rx_check_error(rx_ctx* ctx) {
   RX_HIP(hipStreamSynchronize(ctx->stream));
   if (h[0] != 0) {
     ctx->last_err_index = h[1];
+    ctx->last_err_phase = h[0] == ERR_NAN_UPWIND ? 1 : 0;
     RX_HIP(hipMemsetAsync(ctx->err, 0, 2 * sizeof(int), ctx->stream));
     return h[0] == ERR_RANGE ? RX_ERR_RANGE : (h[0] == ERR_CONV ? RX_ERR_NONPHYS : RX_ERR_NAN);
   }
@@ -1617,6 +1619,11 @@ bool rx_fuse_conv(int nDim) {
 }
 
 int rx_launch_ausm_edge(rx_ctx* ctx) {
+  if (!ctx->jconv) {  // allocated at first use: the 2-D fused assembly never needs the per-edge blocks
+    if (ctx->capturing) return RX_ERR_STATE;
+    RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->fconv), sizeof(double) * ctx->E * ctx->nVar));
+    RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->jconv), sizeof(double) * ctx->E * 2 * ctx->nVar * ctx->nVar));
+  }
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_ausm_edge<NS_, ND_><<<blocks(ctx->E * kAusmTeam, kAusmBlock), kAusmBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
                             ctx->cfg.spatial_order ? ctx->recon : nullptr,
@@ -1687,8 +1694,11 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   if (ctx->conv_deferred && !fused_conv) {  // deferred, but no viscous pass to fuse it into: the edge kernel now
     const int rc = rx_launch_ausm_edge(ctx);
     if (rc) return rc;
+    ctx->conv_deferred = 0;  // this residual's per-edge convective blocks now exist; later assemblies read them
   }
-  ctx->conv_deferred = 0;
+  // fused: conv_deferred stays set (only rx_residual_zero / rx_edge_flux_conv change it), so a re-assembly of the
+  // same residual (e.g. a RES download after the viscous loop, then Source_Residual) fuses the AUSM pass again: it
+  // rewrites the residual, the diagonal and the off-diagonal blocks, and no per-edge convective block ever exists
   if (with_visc && ctx->asm_visc) {  // k_visc_jac was skipped: the node-centric viscous Jacobians + assembly
     ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
                  ctx->cfg.rans, ctx->cfg.implicit};

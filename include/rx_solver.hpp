@@ -128,7 +128,9 @@ class ReactiveNSSolver {
  private:
   void phase(int rc, const char* nan_msg) {
     if (rc == RX_OK) rc = rx_sync(ctx_);
-    if (rc == RX_ERR_NAN) throw std::runtime_error(nan_msg);
+    if (rc == RX_ERR_NAN)  // a NaN of the fused AUSM pass is the upwind loop's, whichever call assembled it
+      throw std::runtime_error(rx_last_error_phase(ctx_) == RX_ERR_PHASE_UPWIND ? "NaN found in the upwind residual"
+                                                                                 : nan_msg);
     check(rc, nan_msg);
   }
   void check(int rc, const char* what) const {

@@ -48,30 +48,32 @@ def colrel(a, ref):
     return float((np.abs(a - ref).max(axis=0) / np.maximum(np.abs(ref).max(axis=0), 1e-300)).max())
 
 
-def run_case(name):
+def run_case(name, cfl=None):
+    """cfl: the flow CFL of c2b (default 5.0, the round-2..4 bench value); c2e keeps 0.5."""
     if name == "c1":
         def writer(wd):
             os.symlink(os.path.join(MG.CASE_DIR, "mesh_stretched.su2"), os.path.join(wd, "mesh.su2"))
             return "mesh.su2"
         _, U = MG.read_plot(os.path.join(MG.CASE_DIR, "PLOT/flow_second_chem.dat"))
     else:
-        nx, ny = {"c2": (500, 200), "c2b": (500, 200), "c2e": (500, 200)}[name]
-        ns = 7 if name in ("c2b", "c2e") else 9
+        nx, ny = {"c2": (500, 200), "c2b": (500, 200), "c2e": (500, 200), "c3b": (2000, 500)}[name]
+        ns = 7 if name in ("c2b", "c2e", "c3b") else 9
         pts, quads, bnd = MG.meshgen.jet_mesh(nx, ny)
         from tests.rxpkg import synth
         # c2b: the bench's own state (7 species, every species floored at 1e-6 of rho: synth.field_at's default)
-        _, Uc, k, om, _, _ = synth.field_at(pts, ns, y_floor=1e-6 if name in ("c2b", "c2e") else 1e-10)
+        _, Uc, k, om, _, _ = synth.field_at(pts, ns, y_floor=1e-6 if name in ("c2b", "c2e", "c3b") else 1e-10)
         U = np.concatenate([Uc, k[:, None], om[:, None]], axis=1)
 
         def writer(wd):
             MG.meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, quads, bnd)
             return "mesh.su2"
-    ns = 7 if name in ("c2b", "c2e") else 9
+    ns = 7 if name in ("c2b", "c2e", "c3b") else 9
     if name == "c2e":  # the shipped cfgs' scheme: EULER_EXPLICIT flow (no flow linear solve), LU_SGS SST
         wd = MG.make_workdir("calib_" + name, writer, cfl=0.5, order="1ST_ORDER", prec="LU_SGS", ns=ns,
                              time_flow="EULER_EXPLICIT")
     else:
-        wd = MG.make_workdir("calib_" + name, writer, cfl=5.0, order="1ST_ORDER", prec="ILU0", ns=ns)
+        wd = MG.make_workdir("calib_" + name + ("" if cfl is None else f"_cfl{cfl:g}"), writer,
+                             cfl=5.0 if cfl is None else cfl, order="1ST_ORDER", prec="ILU0", ns=ns)
     MG.write_state(wd, U)
     t0 = time.perf_counter()
     g = MG.run_harness(wd, bsr=False, extra=["--iters", "1"])

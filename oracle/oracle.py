@@ -682,7 +682,7 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         if not imp:  # ExplicitEuler_Iteration (solver_direct_reactive.cpp:2414-2449) / ExplicitRK_Iteration (:2456-2493)
             Un = update(Uold, R, nDim, 1, 1.0, vol, dt) if alpha is None else update_rk(Uold, R, nDim, alpha, vol, dt)
             rms = np.maximum(1e-32, np.sqrt(np.sum(R * R, axis=0) / N))
-            it, rhs, x = 0, None, None
+            it, rhs, x, lres = 0, None, None, None
             U, Vg = Un, o["V"]
     diag = np.nonzero(np.asarray(col) == np.repeat(np.arange(N), np.diff(rp)))[0]  # the diagonal block of each row
     if imp:
@@ -696,11 +696,11 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         rhs = -(R + 0.0)
         if cfg.get("flow_prec", "ilu") == "ilu":
             F = ilu_build(rp, col, A, part_ptr)
-            x, it, _ = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                              part_ptr=part_ptr)
+            x, it, lres = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                                 part_ptr=part_ptr)
         else:  # LINEAR_SOLVER_PREC = LU_SGS
-            x, it, _ = fgmres(rp, col, A, rhs.ravel(), "lusgs", tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                              part_ptr=part_ptr)
+            x, it, lres = fgmres(rp, col, A, rhs.ravel(), "lusgs", tol=cfg["lin_tol"], m=cfg["lin_iter"],
+                                 part_ptr=part_ptr)
         Un = update(Uold, x, nDim, 0, cfg["relaxation"], vol, dt)
         rms = np.maximum(1e-32, np.sqrt(np.sum(rhs * rhs, axis=0) / N))
     # MultiGrid_Iteration's Preprocessing(Output = true) on the updated solution (integration_time.cpp:127-129)
@@ -739,4 +739,4 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     TG1 = sol_grad(Tn)
     F1n, F2n, CDn, mutn = sst_blending(nDim, Tn, TG1, rho, o2["mu"], mesh["wall_distance"], strain2)
     return dict(U=Un, V=V2, Uold=Uold, T=Tn, TG=TG1, F1=F1n, F2=F2n, CDkw=CDn, mut=mutn, rms=rms, sst_rms=sst_rms,
-                lin_iters=it, sst_lin_iters=it2, dt=dt, pre=o, pre_grad=G, jac_loops=A_loops, res_loops=R_loops, sys=A, rhs=rhs, sol=x, sst_sys=A2, sst_rhs=rhs2, sst_sol=x2)
+                lin_iters=it, lin_resid=lres, sst_lin_iters=it2, dt=dt, pre=o, pre_grad=G, jac_loops=A_loops, res_loops=R_loops, sys=A, rhs=rhs, sol=x, sst_sys=A2, sst_rhs=rhs2, sst_sol=x2)

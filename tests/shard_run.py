@@ -36,7 +36,8 @@ def write_shards(tmpdir, mesh, st0, mech, kw, world, tg=None):
             arr["tg"] = np.ascontiguousarray(np.asarray(tg)[sh["l2g"]])
         arr["kw"] = np.array(json.dumps(kw))
         np.savez(os.path.join(tmpdir, f"rank{r}.npz"), **arr)
-        out.append(dict(l2g=sh["l2g"], n_domain=int(sh["n_domain"]), rank_ptr=sh["rank_ptr"]))
+        out.append(dict(l2g=sh["l2g"], n_domain=int(sh["n_domain"]), rank_ptr=sh["rank_ptr"],
+                        n_point=len(sh["coord"]), n_edge=len(sh["edges"]), n_part=len(sh["part_ptr"]) - 1))
     return out
 
 

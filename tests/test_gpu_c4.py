@@ -1,6 +1,6 @@
-"""BASELINE configs[3] (C4): the 1M-point C3 jet (2000 x 500, 7 species, PaSR + SST, 256 partitions) decomposed over 8
-ranks, as `bench.py --gpus 8` runs it (strong scaling: 125 000 owned points per rank, 32 partitions each, one halo
-layer; meshgen.shard). The 8 ranks share the test box's one MI355X through the host-staged transport over gloo
+"""BASELINE configs[3] (C4): the 1M-point C3 jet (2000 x 500, 7 species, PaSR + SST) decomposed over 8 ranks exactly
+as `bench.py --gpus 8` builds it (strong scaling: 256 partitions per rank = 2048 in all, ~490 rows each, so the ILU(0)
+apply is the LDS-resident k_ilu_apply_lds; 125 000 owned points per rank, one halo layer; meshgen.shard). The 8 ranks share the test box's one MI355X through the host-staged transport over gloo
 (tests/shard_run.py; RCCL refuses two ranks on one device and runs the same exchange plan and rank-ordered
 all-reduce). Reference: CMeanFlowIteration::Iterate (iteration_structure.cpp:486-560) on 8 MPI ranks of a
 partitioned CGeometry (geometry_structure.cpp:11465-11530).
@@ -8,7 +8,7 @@ partitioned CGeometry (geometry_structure.cpp:11465-11530).
 - EULER_EXPLICIT (CFL 0.5, LU_SGS SST): one outer iteration on 8 ranks against one context on the undivided mesh:
   U and both RMS vectors within 1e-10 (the flow update has no inner product: bitwise expected), (k, omega) within
   1e-10 (its FGMRES sums inner products in the ranks' order).
-- EULER_IMPLICIT (the bench step, FGMRES(5) + ILU0, CFL 5): one outer iteration on 8 ranks against the CPU oracle's
+- EULER_IMPLICIT (the bench step, FGMRES(5) + ILU0, the bench's CFL rx.BENCH_CFL): one outer iteration on 8 ranks against the CPU oracle's
   O.outer_iteration on the same global mesh and partitions, inner products in the ranks' order, at 1e-10 (U per
   column, species elementwise, momentum, (k, omega), both RMS vectors, identical linear-iteration counts).
 - Every rank's start-up records bitwise equal to one context's; halo rows equal their owners' rows."""
@@ -23,7 +23,8 @@ from tests.test_gpu_shard_iterate import check_preprocessing, check_vs_oracle, s
 
 pytestmark = pytest.mark.gpu
 
-NX, NY, PARTS, WORLD = 2000, 500, 256, 8
+NX, NY, WORLD = 2000, 500, 8
+PARTS = 256 * WORLD  # bench.py --gpus 8 --scaling strong: args.parts * world
 
 
 @pytest.mark.timeout(1200)
@@ -51,12 +52,17 @@ def test_c4_explicit_vs_one_context(tmp_path):
 @pytest.mark.timeout(1200)
 def test_c4_implicit_vs_oracle(tmp_path):
     mesh, st0, mech, kw = synth.jet_field_case(NX, NY, n_species=NS, n_part=PARTS)
-    s, t, st, cfg, bc = single_context(mesh, st0, mech, kw, 1, 5.0)
+    s, t, st, cfg, bc = single_context(mesh, st0, mech, kw, 1, rx.BENCH_CFL)
     s.close()
     _, state, _, _ = outer_iteration_inputs(mesh, st, cfg, bc)
     shards = write_shards(tmp_path, mesh, st0, mech, kw, WORLD, tg=state["TG"])
     assert [sh["n_domain"] for sh in shards] == [NX * NY // WORLD] * WORLD
-    res = run_ranks(tmp_path, WORLD, 1, 1, 5.0)
+    import bench  # the ILU(0) apply the 8-GPU bench line times at this decomposition: the LDS-resident sweep
+    for sh in shards:
+        assert sh["n_part"] == PARTS // WORLD
+        assert bench.ilu_apply_kernels(sh["n_point"], sh["n_point"] + 2 * sh["n_edge"], NS + 4,
+                                       sh["n_part"]).startswith("k_ilu_apply_lds")
+    res = run_ranks(tmp_path, WORLD, 1, 1, rx.BENCH_CFL)
     U, T, pre = gather(res, len(st["V"]), st["U"].shape[1])
     check_preprocessing(pre, st, "C4 implicit")
     for r, d in res.items():

@@ -28,7 +28,7 @@ NX, NY, NPART, NS = 48, 20, 8, 7
 
 def _case(implicit=1):
     mesh, st, mech_arrays, kw = synth.jet_case(NX, NY, n_species=NS, n_part=NPART)
-    cfg = rx.default_cfg(implicit=implicit, lin_prec=1, cfl=5.0 if implicit else 0.5, max_delta_time=1e6,
+    cfg = rx.default_cfg(implicit=implicit, lin_prec=1, cfl=rx.BENCH_CFL if implicit else 0.5, max_delta_time=1e6,
                          prandtl_lam=0.72,
                          prandtl_turb=kw["prandtl_turb"], lewis_turb=kw["lewis_turb"], mach_inf=kw["mach_inf"],
                          c_mu=kw["c_mu"], pasr_lb=kw["pasr_lb"], lin_tol=1e-6, lin_iter=5, relaxation=1.0)

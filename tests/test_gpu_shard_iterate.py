@@ -105,11 +105,11 @@ def test_sharded_explicit_matches_single_context(world, geom, tmp_path):
 def test_sharded_implicit_matches_oracle_on_the_ranks(world, geom, tmp_path):
     nx, ny, nz, parts = GEOM[geom]
     mesh, st0, mech, kw = synth.jet_field_case(nx, ny, n_species=NS, n_part=parts, nz=nz)
-    s, t, st, cfg, bc = single_context(mesh, st0, mech, kw, 1, 5.0)
+    s, t, st, cfg, bc = single_context(mesh, st0, mech, kw, 1, rx.BENCH_CFL)
     s.close()
     _, state, _, _ = outer_iteration_inputs(mesh, st, cfg, bc)
     shards = write_shards(tmp_path, mesh, st0, mech, kw, world, tg=state["TG"])
-    res = run_ranks(tmp_path, world, 1, 1, 5.0)
+    res = run_ranks(tmp_path, world, 1, 1, rx.BENCH_CFL)
     N, nv = len(st["V"]), st["U"].shape[1]
     U, T, pre = gather(res, N, nv)
     tag = f"{geom} x{world} implicit"
