@@ -223,13 +223,15 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
                 sample=f"{what} of the same {N}-cell mesh, {cores} host threads ({dt:.2f} s)")
 
 
-def cpu_baseline_reference(ns, cfl, nx=300, ny=75):
+def cpu_baseline_reference(ns, cfl, nx=500, ny=200):
     """One outer iteration of the reference itself (SU2's CMeanFlowIteration::Iterate through oracle/ref_harness,
     compiled from /root/reference's sources by oracle/ref_build.mk into oracle/_ref, serial: one MPI rank, one core)
     on a bounded sample of the bench workload: the same synthetic jet geometry and interpolated PaSR state
-    (synth.field_at) at nx x ny points, the bench's mechanism (`ns` species), EULER_IMPLICIT with ILU0 FGMRES(5)
-    and the jet's boundary conditions. The time is the harness's own clock around Iterate (it1_wall). None when the
-    harness is not built."""
+    (synth.field_at) at nx x ny points — by default configs[1]'s 500 x 200 = 100 000-point mesh (~30 s of CPU; the
+    reference's per-cell cost grows with the mesh: 0.0105 Mcells*iters/s at 300 x 75 (round 4), 0.0033 at 500 x 200, 0.0032 at
+    the C3 mesh itself, profiles/r05_calibration_c{2,3}.json) —, the bench's mechanism (`ns` species), EULER_IMPLICIT
+    with ILU0 FGMRES(5) at the bench's CFL and the jet's boundary conditions. The time is the harness's own clock
+    around Iterate (it1_wall). None when the harness is not built."""
     harness = os.path.join(ROOT, "oracle", "_ref", "harness")
     if not os.path.exists(harness):
         return None

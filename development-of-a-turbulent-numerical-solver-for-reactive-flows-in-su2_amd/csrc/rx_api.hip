@@ -240,8 +240,9 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       }
     }
     ctx->rowmax = rowmax;
+    std::vector<int32_t> ring_xoff(ctx->nnzb, 0);
     auto schedule = [&](bool fwd, rx_ctx::Sched& S) -> int {
-      std::vector<int32_t> lv(N, 0), part_lvl(np + 1, 0), lvl_ptr(1, 0), order;
+      std::vector<int32_t> lv(N, 0), pos(N, 0), part_lvl(np + 1, 0), lvl_ptr(1, 0), order;
       order.reserve(N);
       for (int64_t p = 0; p < np; ++p) {
         const int64_t lo = ctx->h_part_ptr[p], hi = ctx->h_part_ptr[p + 1];
@@ -265,7 +266,10 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         for (int64_t i = lo; i < hi; ++i) cnt[lv[i] + 1]++;
         for (int32_t l = 0; l <= maxl; ++l) cnt[l + 1] += cnt[l];
         std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1), loc(hi - lo);
-        for (int64_t i = lo; i < hi; ++i) loc[fill[lv[i]]++] = (int32_t)i;
+        for (int64_t i = lo; i < hi; ++i) {
+          pos[i] = fill[lv[i]] - cnt[lv[i]];  // position within its level
+          loc[fill[lv[i]]++] = (int32_t)i;
+        }
         const int32_t base = (int32_t)order.size();
         for (int32_t l = 0; l <= maxl; ++l) {
           lvl_ptr.push_back(base + cnt[l + 1]);
@@ -292,6 +296,39 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         part_pass[p + 1] = (int32_t)pass_lo.size();
       }
       pass_lo.push_back((int32_t)order.size());
+      // k_ilu_apply_ring's LDS plan: row j's result goes to ring row (level(j) mod R) W + position(j) (W = the widest
+      // level); a block (i, j) of a dependency less than R levels back reads it there, a farther one from j's far row
+      // R W + (its index among the partition's far sources), written by j as well
+      {
+        const int R = kIluRing, W = std::max(1, S.maxwidth);
+        std::vector<int32_t> farid(N, -1);
+        int32_t nfar_max = 0;
+        for (int64_t p = 0; p < np; ++p) {
+          int32_t nfar = 0;
+          for (int64_t i = ctx->h_part_ptr[p]; i < ctx->h_part_ptr[p + 1]; ++i) {
+            const int32_t k0 = fwd ? klo[i] : (int32_t)diag[i] + 1, k1 = fwd ? (int32_t)diag[i] : khi[i];
+            for (int32_t k = k0; k < k1; ++k) {
+              const int32_t j = col32[k];
+              if (lv[i] - lv[j] < R) {
+                ring_xoff[k] = (lv[j] % R) * W + pos[j];
+              } else {
+                if (farid[j] < 0) farid[j] = nfar++;
+                ring_xoff[k] = R * W + farid[j];
+              }
+            }
+          }
+          nfar_max = std::max(nfar_max, nfar);
+        }
+        std::vector<int32_t> ring(2 * order.size());
+        for (size_t r = 0; r < order.size(); ++r) {
+          const int32_t i = order[r];
+          ring[2 * r] = (lv[i] % R) * W + pos[i];
+          ring[2 * r + 1] = farid[i] >= 0 ? R * W + farid[i] : -1;
+        }
+        S.ring_rows = R * W + nfar_max;
+        const int rc3 = dupload(ctx, &S.ring, ring.data(), ring.size());
+        if (rc3) return rc3;
+      }
       int rc2 = dupload(ctx, &S.pass_lo, pass_lo.data(), pass_lo.size());
       if (!rc2) rc2 = dupload(ctx, &S.part_pass, part_pass.data(), part_pass.size());
       if (!rc2) rc2 = dupload(ctx, &S.part_lvl, part_lvl.data(), part_lvl.size());
@@ -319,6 +356,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     }
     CK(schedule(true, ctx->fs));
     CK(schedule(false, ctx->bs));
+    CK(dupload(ctx, &ctx->ring_xoff, ring_xoff.data(), ring_xoff.size()));
     CK(dupload(ctx, &ctx->klo, klo.data(), N));
     CK(dupload(ctx, &ctx->khi, khi.data(), N));
     // ILU(0) update plan: for each intra lower block k = (i, j): upper blocks kk = (j, kp), kp > j
@@ -687,7 +725,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.pass_lo, ctx->fs.part_pass, ctx->bs.pass_lo, ctx->bs.part_pass,
-                  ctx->fs.slot, ctx->bs.slot, ctx->send_idx, ctx->grad_list, ctx->spmv_rows, ctx->sendbuf, ctx->rms_sum,
+                  ctx->fs.slot, ctx->bs.slot, ctx->fs.ring, ctx->bs.ring, ctx->ring_xoff, ctx->send_idx, ctx->grad_list, ctx->spmv_rows, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,
                   ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};

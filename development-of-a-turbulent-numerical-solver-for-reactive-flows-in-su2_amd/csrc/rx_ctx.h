@@ -105,7 +105,12 @@ struct rx_ctx {
     int32_t* pass_lo = nullptr;   // [npass + 1] schedule positions of the passes: <= 64 rows of one level each
     int32_t* part_pass = nullptr; // [npart + 1] each partition's passes
     int nlevels = 0, maxwidth = 0, maxlev = 0;  // maxlev: most levels of one partition
+    // k_ilu_apply_ring (rx_sweeps.hip): per schedule slot {ring row, far row or -1}, the LDS rows the slot's result
+    // is written to; ring_rows = kIluRing * maxwidth + the most far rows of one partition
+    int32_t* ring = nullptr;
+    int ring_rows = 0;
   } fs, bs;
+  int32_t* ring_xoff = nullptr;  // [nnzb] LDS row of x_col(k) for the blocks the sweeps read (L: fs ring, U: bs ring)
   double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)
   double* xstar = nullptr;      // [N][nVar] LU-SGS forward-sweep result (halo values)
   long long* ilu_trace = nullptr;  // debug phase trace of the ILU factorisation (rx_debug_ilu_trace)
@@ -238,6 +243,10 @@ int rx_launch_muscl(rx_ctx* ctx);
 int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter);
 int rx_launch_ausm_edge(rx_ctx* ctx);
 bool rx_fuse_conv(int nDim);
+// levels of the ILU(0) sweeps' LDS ring (k_ilu_apply_ring): a row's result is read from the ring slot of its level
+// by the rows up to kIluRing - 1 levels later, from a per-partition "far" slot by later ones
+constexpr int kIluRing = 4;
+int rx_ilu_ring_rpb(int nv);  // rows per pass of k_ilu_apply_ring (1024 threads)
 int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);
 int rx_launch_source(rx_ctx* ctx);

@@ -964,6 +964,9 @@ struct AusmIn {
 #ifndef RX_ASMV_FUSE
 #define RX_ASMV_FUSE 1  // build knob: 0 compiles k_asm_visc without its fused AUSM pass
 #endif
+#ifndef RX_ASMV_PARK
+#define RX_ASMV_PARK 0  // build knob: 1 = round 4's fused pass, which parked 0 -+ Jc in the off-diagonal block for the
+#endif                  // viscous pass to finish (each off-diagonal block written twice and read back once)
 #ifndef RX_ASMV_CDEG
 #define RX_ASMV_CDEG -1  // build knob: node degree up to which k_asm_visc's convective pass loads everything first
 #endif                   // (-1: the quad / hex stencils' 4 in 2-D, 6 in 3-D; 0: never)
@@ -982,7 +985,11 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   constexpr int rhos = NDIM + 2, nsv = NS * nVar;
   constexpr int CD = RX_ASMV_CDEG < 0 ? (NDIM == 2 ? 4 : 6) : (RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1);
   constexpr int kES = sizeof(AusmEdge) / sizeof(double);  // one edge's AUSM scalars
-  constexpr int TS = RX_ASMV_SHS && CD * kES > SS ? CD * kES : SS;  // a team's LDS slot
+  // a team's LDS slot: the viscous summary record of the edge being folded at [0, SS); the shared edge scalars of
+  // the node's first CD edges at [SCO, SCO + CD kES) — after the summary, so that the viscous pass still reads them
+  // (RX_ASMV_PARK: at 0, reused by the summary)
+  constexpr int SCO = RX_ASMV_PARK ? 0 : SS;
+  constexpr int TS = !RX_ASMV_SHS ? SS : (RX_ASMV_PARK ? (CD * kES > SS ? CD * kES : SS) : SS + CD * kES);
   static_assert(CD <= 16, "the shared edge scalars of the first CD edges are made by team lanes 0..CD-1 (16 lanes)");
   __shared__ double ssm[kTeams * TS];
   const int gt = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
@@ -995,39 +1002,61 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   double r = 0.0, D[nVar];
 #pragma unroll
   for (int a = 0; a < nVar; ++a) D[a] = 0.0;
+  const bool fused = RX_ASMV_FUSE && cv.V != nullptr;
+  // fused AUSM (cv.V set, k_ausm_edge skipped): the edge scalars (from the team's LDS slot for the node's first CD
+  // edges, else made here) and this lane's column of the own side's convective Jacobian, with k_ausm_edge's
+  // arithmetic (the other side's column is the neighbour team's own side): jd[a] = J_own[a][bc]
+  auto edge_scalars = [&](size_t e, int n0, int n1, AusmEdge& s) {
+    const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
+    const double* Vsj = cv.VR ? cv.VR + (2 * e + 1) * nPV : cv.V + (size_t)n1 * nPV;
+    double Vi[nPV], Vj[nPV], nrm[NDIM];  // the entries ausm_scalars reads
+#pragma unroll
+    for (int v = 0; v < nPV; ++v) {
+      Vi[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsi[v] : 0.0;
+      Vj[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsj[v] : 0.0;
+    }
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[e * NDIM + d];
+    ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+  };
+  auto own_column = [&](size_t e, int side, int n0, int n1, const AusmEdge& s, double* jd) {
+    const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
+    const double* Vsj = cv.VR ? cv.VR + (2 * e + 1) * nPV : cv.V + (size_t)n1 * nPV;
+    const double* Ssi = cv.VR ? cv.SR + 2 * e * nVar : cv.dPdU + (size_t)n0 * nVar;
+    const double* Ssj = cv.VR ? cv.SR + (2 * e + 1) * nVar : cv.dPdU + (size_t)n1 * nVar;
+    const double sib = Ssi[bc], sjb = Ssj[bc];
+    const AusmCol cc = ausm_col_b<NDIM>(s, sib, sjb, bc);
+    bool bad = false;
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) {
+      double ji, jj;
+      ausm_jac_entry<NDIM>(s, cc, ausm_phi<NDIM>(Vsi, Vsi[NDIM + 3], a), ausm_phi<NDIM>(Vsj, Vsj[NDIM + 3], a), sib,
+                           sjb, a, bc, &ji, &jj);
+      bad |= isnan(ji) || isnan(jj);
+      jd[a] = side ? jj : ji;
+    }
+    return bad;
+  };
+  auto load_scalars = [&](const double* from, AusmEdge& s) {
+    double* sp = reinterpret_cast<double*>(&s);
+#pragma unroll
+    for (int f = 0; f < kES; ++f) sp[f] = from[f];
+  };
+  int nq = 0;  // the node's first nq edges have their scalars in the team's slot
   // convective pass; for degrees up to RX_ASMV_CDEG every load of the pass is issued before the first sum (one round
   // trip instead of one per edge), then the sums run in edge order
-  if (RX_ASMV_FUSE && cv.V) {
-    // fused AUSM (cv.V set, k_ausm_edge skipped): the edge's flux and its own-side Jacobian column are evaluated here
-    // with k_ausm_edge's arithmetic (the other side's column by the neighbour's team), folded into the residual and
-    // diagonal in edge order, and parked in the neighbour row's off-diagonal block as 0 -+ J for the viscous pass
+  if (fused) {
+    // the edge's flux and its own-side Jacobian column, folded into the residual and diagonal in edge order
     auto fused_edge = [&](int ad, int n0, int n1, const double* shared_s) {
       const size_t e = (size_t)(ad >> 1);
       const int side = ad & 1;
-      const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
-      const double* Vsj = cv.VR ? cv.VR + (2 * e + 1) * nPV : cv.V + (size_t)n1 * nPV;
-      const double* Ssi = cv.VR ? cv.SR + 2 * e * nVar : cv.dPdU + (size_t)n0 * nVar;
-      const double* Ssj = cv.VR ? cv.SR + (2 * e + 1) * nVar : cv.dPdU + (size_t)n1 * nVar;
-      double Vi[nPV], Vj[nPV], nrm[NDIM];  // the entries ausm_scalars reads (the convected states are re-read below)
-#pragma unroll
-      for (int v = 0; v < nPV; ++v) {
-        Vi[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsi[v] : 0.0;
-        Vj[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsj[v] : 0.0;
-      }
-#pragma unroll
-      for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[e * NDIM + d];
-      const double sib = Ssi[bc], sjb = Ssj[bc];
-      double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
       AusmEdge s;
-      if (RX_ASMV_SHS && shared_s) {
-        double* sp = reinterpret_cast<double*>(&s);
-#pragma unroll
-        for (int f = 0; f < kES; ++f) sp[f] = shared_s[f];
-      } else {
-        ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
-      }
+      if (RX_ASMV_SHS && shared_s) load_scalars(shared_s, s);
+      else edge_scalars(e, n0, n1, s);
       bool bad = false;
       if (col) {
+        const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
+        const double* Vsj = cv.VR ? cv.VR + (2 * e + 1) * nPV : cv.V + (size_t)n1 * nPV;
         const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
         const double pi = b == 0 ? 1.0 : Vsi[pidx];
         const double pj = b == 0 ? 1.0 : Vsj[pidx];
@@ -1036,16 +1065,13 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
         bad |= isnan(f);
         r = side ? r - f : r + f;
       }
-      const AusmCol cc = ausm_col_b<NDIM>(s, sib, sjb, bc);
+      double jd[nVar];
+      bad |= own_column(e, side, n0, n1, s, jd);
+      double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
 #pragma unroll
       for (int a = 0; a < nVar; ++a) {
-        double ji, jj;
-        ausm_jac_entry<NDIM>(s, cc, ausm_phi<NDIM>(Vsi, Vsi[NDIM + 3], a), ausm_phi<NDIM>(Vsj, Vsj[NDIM + 3], a), sib,
-                             sjb, a, bc, &ji, &jj);
-        bad |= isnan(ji) || isnan(jj);
-        const double jd = side ? jj : ji;
-        D[a] = side ? D[a] - jd : D[a] + jd;
-        if (col) Ao[a * nVar + b] = side ? 0.0 + jd : 0.0 - jd;
+        D[a] = side ? D[a] - jd[a] : D[a] + jd[a];
+        if (RX_ASMV_PARK && col) Ao[a * nVar + b] = side ? 0.0 + jd[a] : 0.0 - jd[a];
       }
       if (col && bad) set_err(cv.err, ERR_NAN_UPWIND, (int64_t)e);
     };
@@ -1053,37 +1079,27 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     if (RX_ASMV_SHS && k1 > k0) {
       // the edge scalars of the node's first CD edges are made once, lane q of the team making edge k0 + q's (the
       // same function on the same inputs, so the same values), and read back from the team's LDS slot
-      const int nq = k1 - k0 < CD ? k1 - k0 : CD;
+      nq = k1 - k0 < CD ? k1 - k0 : CD;
       {
         const int ad = adj[k0 + (b < nq ? b : 0)];
         const size_t e = (size_t)(ad >> 1);
-        const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
-        const double* Vsi = cv.VR ? cv.VR + 2 * e * nPV : cv.V + (size_t)n0 * nPV;
-        const double* Vsj = cv.VR ? cv.VR + (2 * e + 1) * nPV : cv.V + (size_t)n1 * nPV;
-        double Vi[nPV], Vj[nPV], nrm[NDIM];
-#pragma unroll
-        for (int v = 0; v < nPV; ++v) {
-          Vi[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsi[v] : 0.0;
-          Vj[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsj[v] : 0.0;
-        }
-#pragma unroll
-        for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[e * NDIM + d];
         AusmEdge s;
-        ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+        edge_scalars(e, edges[2 * e], edges[2 * e + 1], s);
         const double* sp = reinterpret_cast<const double*>(&s);
         if (b < nq)
 #pragma unroll
-          for (int f = 0; f < kES; ++f) slot[b * kES + f] = sp[f];
+          for (int f = 0; f < kES; ++f) slot[SCO + b * kES + f] = sp[f];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       for (int q = 0; q < nq; ++q) {
         const int ad = adj[k0 + q];
-        fused_edge(ad, edges[2 * (ad >> 1)], edges[2 * (ad >> 1) + 1], slot + q * kES);
+        fused_edge(ad, edges[2 * (ad >> 1)], edges[2 * (ad >> 1) + 1], slot + SCO + q * kES);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();  // the viscous pass reuses the slot
+      __builtin_amdgcn_wave_barrier();  // (RX_ASMV_PARK) the viscous pass reuses the slot
       kq = k0 + nq;
+      if (RX_ASMV_PARK) nq = 0;
     }
     for (int k = kq; k < k1; ++k) {
       const int ad = adj[k];
@@ -1127,7 +1143,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
       }
     }
   }
-  // viscous pass
+  // viscous pass: each edge's off-diagonal block of the neighbour's row is written once, (0 -+ Jc) +- Jv
   for (int k = k0; k < k1; ++k) {
     const int ad = adj[k];
     const int e = ad >> 1;
@@ -1139,8 +1155,18 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     }
     const double sob = dTdU[(size_t)(side ? n1 : n0) * nVar + bc];  // the own node's dT/dU
     double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
-    double jco[nVar];  // this lane's column of the own-side convective block, or (fused AUSM) 0 -+ that column
-    if (RX_ASMV_FUSE && cv.V) {
+    double jco[nVar];  // 0 -+ this lane's column of the own-side convective block
+    if (fused && !RX_ASMV_PARK) {
+      // the column the convective pass folded into the diagonal, evaluated again (same function, same inputs: the
+      // same doubles) instead of parked in the off-diagonal block and read back
+      AusmEdge s;
+      if (RX_ASMV_SHS && k - k0 < nq) load_scalars(slot + SCO + (k - k0) * kES, s);
+      else edge_scalars((size_t)e, n0, n1, s);
+      double jd[nVar];
+      (void)own_column((size_t)e, side, n0, n1, s, jd);
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) jco[a] = side ? 0.0 + jd[a] : 0.0 - jd[a];
+    } else if (fused) {
 #pragma unroll
       for (int a = 0; a < nVar; ++a) jco[a] = col ? Ao[a * nVar + b] : 0.0;
     } else {

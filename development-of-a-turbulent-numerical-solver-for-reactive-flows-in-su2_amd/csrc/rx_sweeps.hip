@@ -1773,6 +1773,178 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_wide(const int32_t* __restrict
   bwd_wide_body<NV, TB>(bpart_lvl, blvl_ptr, bslot, col, U, invD, x);
 }
 
+// Both sweeps of a partition with the sweep's recent results in an LDS ring (round 5). In the wide sweeps each level
+// reads its x segments from global memory after the previous level's stores, so a level's time is the chain
+// column index -> x -> product -> store -> barrier (which waits for the stores, and with them for every load issued
+// before it). Here every result is also written to LDS: into the ring row (level mod kIluRing, position in the level),
+// and, when some row more than kIluRing - 1 levels later reads it, into the partition's far row (the host's plan,
+// rx_api.hip: ring_xoff per block, {ring, far} per schedule slot). The sweeps then read x only from LDS, the global
+// stores of x are never waited for inside a sweep, and the level barrier is an LDS barrier (lgkmcnt). So the next
+// level's factor rows, column offsets and b / inv(D) / forward result are loaded during this level and stay in flight
+// across the barrier. One row per lane group and level (the widest level fits the workgroup's rows); MB blocks of a
+// row come from registers, further ones are loaded when used. Same arithmetic, operation for operation, as the wide
+// sweeps (row_blocks: each block's sum from 0.0, c ascending; blocks ascending).
+template <int NV, int TB>
+constexpr int ring_rpb() {
+  return (TB / 64) * (64 / NV);  // rows per pass: whole rows per wavefront (the backward's v exchange is wave-local)
+}
+template <int NV, int TB, int MB>
+__global__ __launch_bounds__(TB) void k_ilu_apply_ring(
+    const int32_t* __restrict__ fpart_lvl, const int32_t* __restrict__ flvl_ptr, const int4* __restrict__ fslot,
+    const int2* __restrict__ fring, const int32_t* __restrict__ bpart_lvl, const int32_t* __restrict__ blvl_ptr,
+    const int4* __restrict__ bslot, const int2* __restrict__ bring, const int32_t* __restrict__ xoff,
+    const double* __restrict__ L, const double* __restrict__ U, const double* __restrict__ invD,
+    const double* __restrict__ b, double* __restrict__ x, int* __restrict__ done, const int* __restrict__ conv,
+    int ring_rows) {
+  if (skip_sweep(done, conv)) return;
+  constexpr int NV2 = NV * NV, RW = 64 / NV, RPB = ring_rpb<NV, TB>();
+  extern __shared__ double lds[];
+  double* xs = lds;                                               // [ring_rows][NV]
+  double* v = lds + (size_t)ring_rows * NV;                       // [RPB][NV] backward: x_i - sum, per row
+  int32_t* lp = reinterpret_cast<int32_t*>(v + (size_t)RPB * NV);  // the sweep's level table for this partition
+  const int p = blockIdx.x;
+  const int wl = threadIdx.x & 63;
+  const int rl = (int)(threadIdx.x >> 6) * RW + wl / NV;
+  const int a = wl - (wl / NV) * NV;
+  const bool lane = wl < RW * NV;
+  // ---- forward: x_i = b_i - sum_k L_ik x_col(k)
+  {
+    const int l0 = fpart_lvl[p], nl = fpart_lvl[p + 1] - l0;
+    for (int q = threadIdx.x; q <= nl; q += TB) lp[q] = flvl_ptr[l0 + q];
+    __syncthreads();
+    auto slot_at = [&](int l, int4& sl, int2& w) {
+      if (!lane || l >= nl) return false;
+      const int r = lp[l] + rl;
+      if (r >= lp[l + 1]) return false;
+      sl = fslot[r];
+      w = fring[r];
+      return true;
+    };
+    int4 sl = make_int4(0, 0, 0, 0), sln = sl;
+    int2 w = make_int2(0, -1), wn = w;
+    double F[MB][NV], bi = 0.0;
+    int xo[MB];
+    auto issue = [&]() {  // this lane's loads of row sl (its level is the next one computed)
+      bi = b[(size_t)sl.x * NV + a];
+#pragma unroll
+      for (int t = 0; t < MB; ++t)
+        if (sl.y + t < sl.z) {
+          xo[t] = xoff[sl.y + t];
+          const double* blk = L + (size_t)(sl.y + t) * NV2 + a * NV;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) F[t][c] = blk[c];
+        }
+    };
+    bool act = slot_at(0, sl, w);
+    if (act) issue();
+    bool actn = slot_at(1, sln, wn);
+    for (int l = 0; l < nl; ++l) {
+      if (act) {
+        double xi = bi;
+#pragma unroll
+        for (int t = 0; t < MB; ++t)
+          if (sl.y + t < sl.z) {
+            const double* xj = xs + xo[t] * NV;
+            double s = 0.0;
+#pragma unroll
+            for (int c = 0; c < NV; ++c) s += F[t][c] * xj[c];
+            xi -= s;
+          }
+        for (int k = sl.y + MB; k < sl.z; ++k) {  // rows with more than MB lower blocks
+          const double* blk = L + (size_t)k * NV2 + a * NV;
+          const double* xj = xs + xoff[k] * NV;
+          double s = 0.0;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
+          xi -= s;
+        }
+        xs[w.x * NV + a] = xi;
+        if (w.y >= 0) xs[w.y * NV + a] = xi;
+        x[(size_t)sl.x * NV + a] = xi;
+      }
+      act = actn;
+      sl = sln;
+      w = wn;
+      if (act) issue();
+      actn = slot_at(l + 2, sln, wn);
+      lds_barrier();
+    }
+  }
+  __syncthreads();  // the forward's global x stores (the backward reads x_i) and its level-table reads are done
+  // ---- backward: x_i = inv(D_i) (x_i - sum_k U_ik x_col(k))
+  {
+    const int l0 = bpart_lvl[p], nl = bpart_lvl[p + 1] - l0;
+    for (int q = threadIdx.x; q <= nl; q += TB) lp[q] = blvl_ptr[l0 + q];
+    __syncthreads();
+    auto slot_at = [&](int l, int4& sl, int2& w) {
+      if (!lane || l >= nl) return false;
+      const int r = lp[l] + rl;
+      if (r >= lp[l + 1]) return false;
+      sl = bslot[r];
+      w = bring[r];
+      return true;
+    };
+    int4 sl = make_int4(0, 0, 0, 0), sln = sl;
+    int2 w = make_int2(0, -1), wn = w;
+    double F[MB][NV], inv[NV], xf = 0.0;
+    int xo[MB];
+    auto issue = [&]() {
+      xf = x[(size_t)sl.x * NV + a];
+#pragma unroll
+      for (int c = 0; c < NV; ++c) inv[c] = invD[(size_t)sl.x * NV2 + a * NV + c];
+#pragma unroll
+      for (int t = 0; t < MB; ++t)
+        if (sl.z + 1 + t < sl.w) {
+          xo[t] = xoff[sl.z + 1 + t];
+          const double* blk = U + (size_t)(sl.z + 1 + t) * NV2 + a * NV;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) F[t][c] = blk[c];
+        }
+    };
+    bool act = slot_at(0, sl, w);
+    if (act) issue();
+    bool actn = slot_at(1, sln, wn);
+    for (int l = 0; l < nl; ++l) {
+      if (act) {
+        double sum = 0.0;
+#pragma unroll
+        for (int t = 0; t < MB; ++t)
+          if (sl.z + 1 + t < sl.w) {
+            const double* xj = xs + xo[t] * NV;
+            double s = 0.0;
+#pragma unroll
+            for (int c = 0; c < NV; ++c) s += F[t][c] * xj[c];
+            sum += s;
+          }
+        for (int k = sl.z + 1 + MB; k < sl.w; ++k) {
+          const double* blk = U + (size_t)k * NV2 + a * NV;
+          const double* xj = xs + xoff[k] * NV;
+          double s = 0.0;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
+          sum += s;
+        }
+        v[rl * NV + a] = xf - sum;
+      }
+      wave_sync();
+      if (act) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
+        xs[w.x * NV + a] = s;
+        if (w.y >= 0) xs[w.y * NV + a] = s;
+        x[(size_t)sl.x * NV + a] = s;
+      }
+      act = actn;
+      sl = sln;
+      w = wn;
+      if (act) issue();
+      actn = slot_at(l + 2, sln, wn);
+      lds_barrier();
+    }
+  }
+}
+
 // ILU(0) application with the partition's vector resident in LDS: b is loaded once, the forward
 // and backward substitutions run level by level on the LDS copy, and x is stored once. The row
 // metadata of both schedules and the partition's column indices (local) are staged in LDS too, so the
@@ -2142,6 +2314,7 @@ int rx_la_ilu_materialize(rx_ctx* ctx) {
 #define RX_ILU_MAX_WAVES 12
 #endif
 int rx_ilu_stage() { return kStage; }
+int rx_ilu_ring_rpb(int nv) { return (1024 / 64) * (64 / nv); }  // ring_rpb<nv, 1024>()
 int rx_ilu_max_waves() { return RX_ILU_MAX_WAVES; }
 
 // Raise the dynamic-LDS limit of the LDS-resident kernels to what the device allows (once).
@@ -2153,6 +2326,9 @@ int rx_la_prepare(rx_ctx* ctx) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_part<NV_>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    if constexpr (NV_ >= 5)
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     if constexpr (NV_ >= 5)
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_grp<NV_>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
@@ -2295,6 +2471,24 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
   }
   static const bool narrow = getenv("RX_NARROW_APPLY") != nullptr;  // diagnosis: the 256-thread sweeps
   const int width = std::max(ctx->fs.maxwidth, ctx->bs.maxwidth);
+  // the LDS-ring sweeps (round 5) when the widest level fits one pass and the ring fits the LDS; RX_ILU_NO_RING=1
+  // restores the wide sweeps below (A/B)
+  static const bool no_ring = getenv("RX_ILU_NO_RING") != nullptr;
+  const size_t ring_shm = sizeof(double) * ((size_t)std::max(ctx->fs.ring_rows, ctx->bs.ring_rows) * nv +
+                                            (size_t)rx_ilu_ring_rpb(nv) * nv) +
+                          sizeof(int32_t) * (size_t)(std::max(ctx->fs.maxlev, ctx->bs.maxlev) + 1);
+  if (!no_ring && !narrow && nv >= 5 && width * nv > 256 && width <= rx_ilu_ring_rpb(nv) && ring_shm <= (size_t)ctx->lds_max) {
+    const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
+    const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
+    const int2* fr = reinterpret_cast<const int2*>(ctx->fs.ring);
+    const int2* br = reinterpret_cast<const int2*>(ctx->bs.ring);
+    const int rr = std::max(ctx->fs.ring_rows, ctx->bs.ring_rows);
+    RX_NV_SWITCH(nv, (k_ilu_apply_ring<NV_, 1024, 2><<<ctx->npart, 1024, ring_shm, ctx->stream>>>(
+                         ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, fr, ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, br,
+                         ctx->ring_xoff, ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv, rr)));
+    RX_HIP(hipGetLastError());
+    return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
+  }
   static const bool split = getenv("RX_ILU_SPLIT") != nullptr;  // A/B: the two sweeps as separate launches
   if (!narrow && width * nv > 256 && !split) {
     const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);

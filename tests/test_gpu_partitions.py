@@ -133,12 +133,16 @@ def test_implicit_step_vs_oracle(n_part):
     s.close()
 
 
-@pytest.mark.parametrize("nx,ny,nz,n_part", [(20, 8, 6, 1), (20, 8, 6, 4), (50, 10, 10, 32)])
+@pytest.mark.parametrize("nx,ny,nz,n_part", [(20, 8, 6, 1), (20, 8, 6, 4), (50, 10, 10, 32), (40, 10, 8, 1),
+                                             (40, 10, 8, 2)])
 def test_ilu_factor_3d_vs_oracle(nx, ny, nz, n_part):
     """The grouped ILU(0) build on 3-D hexahedral jets (7-point stencil: up to six lower blocks per row under the
     partitions' RCM orderings; 50x10x10 in 32 partitions has 72 rows with four, like 22 272 rows of C5), on a
     diagonally dominant random matrix of the mesh's pattern: factor and apply bitwise equal to the oracle
-    (BuildILUPreconditioner / ComputeILUPreconditioner, matrix_structure.cpp:1368-1515)."""
+    (BuildILUPreconditioner / ComputeILUPreconditioner, matrix_structure.cpp:1368-1515). 40x10x8 in 1 / 2 partitions
+    (3 200 / 1 600 rows, levels up to 80 rows wide): partitions too large for the LDS-resident apply, so the apply is
+    the LDS-ring sweep (k_ilu_apply_ring); 2-D ring cases with far rows (dependencies more than kIluRing - 1 levels
+    back): test_partitioned_preconditioners_vs_oracle's 100x40 in 3 partitions."""
     mesh, st, mech_arrays, kw = synth.jet_case(nx, ny, n_species=7, n_part=n_part, nz=nz)
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), rx.default_cfg(implicit=1, lin_prec=1, **kw))
     s.set_state(st)
