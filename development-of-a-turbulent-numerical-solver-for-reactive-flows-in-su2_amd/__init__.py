@@ -99,6 +99,7 @@ class BcDesc(C.Structure):
 
 
 ERR_PHASE_CALL, ERR_PHASE_UPWIND = 0, 1  # rx_err_phase (rx_last_error_phase)
+LIMITER_VENKATAKRISHNAN, LIMITER_BARTH_JESPERSEN = 0, 1  # rx_slope_limiter
 
 BC_NONE, BC_INLET, BC_OUTLET, BC_ISOTHERMAL, BC_HEATFLUX, BC_EULER = 0, 1, 2, 3, 4, 5
 EULER_WALL_ENUM = 1  # the reference's BC_TYPE value of EULER_WALL (Common/include/option_structure.hpp:750)
@@ -562,11 +563,15 @@ class ReactiveNSSolver:
         return ms.value, n.value
 
 
-def sst_cfg(implicit=1, lin_tol=1e-6, lin_iter=5, lin_prec=1, relaxation_turb=1.0, cfl_red_turb=1.0, grad_method=0):
+def sst_cfg(implicit=1, lin_tol=1e-6, lin_iter=5, lin_prec=1, relaxation_turb=1.0, cfl_red_turb=1.0, grad_method=0,
+            spatial_order=0, slope_limiter=0, ref_elem_length=0.1, limiter_coeff=0.5):
     """rx_cfg for the SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl, NUM_METHOD_GRAD
-    -> grad_method."""
+    -> grad_method, SPATIAL_ORDER_TURB -> spatial_order (0 1ST_ORDER, 1 2ND_ORDER, 2 2ND_ORDER_LIMITER),
+    SLOPE_LIMITER_TURB -> slope_limiter, REF_ELEM_LENGTH / LIMITER_COEFF (the flow's)."""
     return default_cfg(implicit=implicit, lin_tol=lin_tol, lin_iter=lin_iter, lin_prec=lin_prec,
-                       relaxation=relaxation_turb, cfl=cfl_red_turb, grad_method=grad_method)
+                       relaxation=relaxation_turb, cfl=cfl_red_turb, grad_method=grad_method,
+                       spatial_order=spatial_order, slope_limiter=slope_limiter, ref_elem_length=ref_elem_length,
+                       limiter_coeff=limiter_coeff)
 
 
 class TurbSSTSolver:

@@ -643,6 +643,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   } else {
     sizes[RX_F_U] = N * 2;
     sizes[RX_F_GRAD] = N * 2 * nd;
+    sizes[RX_F_LIMITER] = N * 2;  // SetSolution_Limiter of (k, omega) (SPATIAL_ORDER_TURB = 2ND_ORDER_LIMITER)
     sizes[RX_F_MUT] = N;
     sizes[RX_F_RES] = N * 2;
     sizes[RX_F_JAC] = imp * nb2;

@@ -200,8 +200,6 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
         {"CONV_NUM_METHOD_FLOW", "", "AUSM", "the reactive solvers implement AUSM only"},
         // :1195: the SST convective term is CUpwSca_TurbSST
         {"CONV_NUM_METHOD_TURB", "SCALAR_UPWIND", "SCALAR_UPWIND", "the SST convection is the scalar upwind"},
-        // :1189 (default FIRST_ORDER): the turbulent MUSCL branch is not built
-        {"SPATIAL_ORDER_TURB", "1ST_ORDER", "1ST_ORDER", "the SST upwind is first order"},
         // :1030: the SST SingleGrid_Iteration calls ImplicitEuler_Iteration
         {"TIME_DISCRE_TURB", "EULER_IMPLICIT", "EULER_IMPLICIT", "the SST update is the implicit Euler step"},
         // :979 (default STEADY): dual time stepping is not built
@@ -286,8 +284,21 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
                                                                                          : RX_GRAD_WEIGHTED_LEAST_SQUARES;
   if (F.ignition && (F.fuel_index < 0 || F.fuel_index >= ns || F.oxidizer_index < 0 || F.oxidizer_index >= ns))
     return fail(k, RX_ERR_STATE, "FUEL_INDEX / OXIDIZER_INDEX out of the mixture");
+  // :1189 (default FIRST_ORDER), :1192 (default VENKATAKRISHNAN): the SST upwind's MUSCL branch
+  // (solver_direct_turbulent.cpp:464-510) and CSolver::SetSolution_Limiter's branches (solver_structure.cpp:951-1204:
+  // VENKATAKRISHNAN; BARTH_JESPERSEN has no branch there, the limiter stays 2.0; SHARP_EDGES and SOLID_WALL_DISTANCE
+  // need geometry the path does not build)
+  const std::string sot = upper(c.str("SPATIAL_ORDER_TURB", "1ST_ORDER"));
+  const std::string slt = upper(c.str("SLOPE_LIMITER_TURB", "VENKATAKRISHNAN"));
+  if ((sot != "1ST_ORDER" && sot != "2ND_ORDER" && sot != "2ND_ORDER_LIMITER") ||
+      (slt != "VENKATAKRISHNAN" && slt != "BARTH_JESPERSEN"))
+    return fail(k, RX_ERR_UNSUPPORTED, "SPATIAL_ORDER_TURB / SLOPE_LIMITER_TURB");
   rx_cfg& S = k->sst;  // SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl
   rx_cfg_default(&S);
+  S.spatial_order = sot == "1ST_ORDER" ? 0 : (sot == "2ND_ORDER" ? 1 : 2);
+  S.slope_limiter = slt == "BARTH_JESPERSEN" ? RX_LIMITER_BARTH_JESPERSEN : RX_LIMITER_VENKATAKRISHNAN;
+  S.ref_elem_length = F.ref_elem_length;
+  S.limiter_coeff = F.limiter_coeff;
   S.implicit = upper(c.str("TIME_DISCRE_TURB", "EULER_IMPLICIT")) == "EULER_IMPLICIT";
   S.lin_tol = F.lin_tol;
   S.lin_iter = F.lin_iter;

@@ -273,7 +273,19 @@ __device__ __forceinline__ void sst_edges(int i, const int32_t* __restrict__ adj
 // zeros included (CSysMatrix::AddBlock / SubtractBlock, matrix_structure.cpp:327-357).
 // CTurbSolver::Upwind_Residual (solver_direct_turbulent.cpp:429-543) + CUpwSca_TurbSST (:865-922):
 // R_i += F, R_j -= F; A_ii += Ji, A_ij += Jj, A_ji -= Ji, A_jj -= Jj.
-template <int NDIM>
+// Second-order inputs of the SST upwind (SPATIAL_ORDER_TURB, CTurbSolver::Upwind_Residual :464-510): the coordinates,
+// the flow's primitive gradient (rows T, u, v(, w), P, X_s) and limiter (T, u, v(, w), P), the SST gradient and
+// limiter of (k, omega).
+struct SstRecon {
+  const double *coord, *G, *Lf, *TG, *TL;
+  int nG;
+};
+// ORDER 0: first order; 1: 2ND_ORDER, 2: 2ND_ORDER_LIMITER. The flow record entry iVar is reconstructed with the
+// gradient ROW iVar (:481-493): the velocity entries with their own rows, the density entry V[nDim+2] with the row of
+// X_0 (reproduced); with the limiter the flow's Limiter_Primitive is read at iVar = nDim+2, one past its nDim+2
+// entries — undefined in the reference — restated as 0.0 (the oracle's orc_sst_upwind2, pinned by the goldens fpit2 /
+// fpit2l / it4t).
+template <int NDIM, int ORDER>
 __global__ __launch_bounds__(kBlock) void k_sst_upwind(int N, const int32_t* __restrict__ adj_ptr,
                                                        const int32_t* __restrict__ adj,
                                                        const int64_t* __restrict__ adj_blk,
@@ -282,10 +294,10 @@ __global__ __launch_bounds__(kBlock) void k_sst_upwind(int N, const int32_t* __r
                                                        const double* __restrict__ normal,
                                                        const double* __restrict__ V, int nPV,
                                                        const double* __restrict__ T, double* __restrict__ R,
-                                                       double* __restrict__ A) {
+                                                       double* __restrict__ A, SstRecon rc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
-  constexpr int RHO = NDIM + 2;
+  constexpr int RHO = NDIM + 2, nL = NDIM + 2;
   double r0 = R[2 * (size_t)i], r1 = R[2 * (size_t)i + 1];
   double* Dp = A ? A + diag[i] * 4 : nullptr;
   double D[4] = {0, 0, 0, 0};
@@ -295,13 +307,61 @@ __global__ __launch_bounds__(kBlock) void k_sst_upwind(int N, const int32_t* __r
   auto edge = [&](int e, int side, int n0, int n1, int64_t ob) {
     const double* v0 = V + (size_t)n0 * nPV;
     const double* v1 = V + (size_t)n1 * nPV;
+    double u0[NDIM], u1[NDIM], rho0, rho1, k0, w0, k1, w1;
+    if (ORDER == 0) {
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) {
+        u0[d] = v0[d + 1];
+        u1[d] = v1[d + 1];
+      }
+      rho0 = v0[RHO];
+      rho1 = v1[RHO];
+      k0 = T[2 * (size_t)n0];
+      w0 = T[2 * (size_t)n0 + 1];
+      k1 = T[2 * (size_t)n1];
+      w1 = T[2 * (size_t)n1 + 1];
+    } else {
+      double vec0[NDIM], vec1[NDIM];
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) {
+        const double c0 = rc.coord[(size_t)n0 * NDIM + d], c1 = rc.coord[(size_t)n1 * NDIM + d];
+        vec0[d] = 0.5 * (c1 - c0);
+        vec1[d] = 0.5 * (c0 - c1);
+      }
+      auto flow = [&](int p, const double* vp, const double* vec, int v) {
+        const double* g = rc.G + ((size_t)p * rc.nG + v) * NDIM;
+        double pg = 0.0;
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) pg += vec[d] * g[d];
+        if (ORDER == 1) return vp[v] + pg;
+        const double l = v < nL ? rc.Lf[(size_t)p * nL + v] : 0.0;
+        return vp[v] + l * pg;
+      };
+      auto turb = [&](int p, const double* vec, int v) {
+        const double* g = rc.TG + ((size_t)p * 2 + v) * NDIM;
+        double pg = 0.0;
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) pg += vec[d] * g[d];
+        return ORDER == 2 ? T[2 * (size_t)p + v] + rc.TL[2 * (size_t)p + v] * pg : T[2 * (size_t)p + v] + pg;
+      };
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) {
+        u0[d] = flow(n0, v0, vec0, d + 1);
+        u1[d] = flow(n1, v1, vec1, d + 1);
+      }
+      rho0 = flow(n0, v0, vec0, RHO);
+      rho1 = flow(n1, v1, vec1, RHO);
+      k0 = turb(n0, vec0, 0);
+      w0 = turb(n0, vec0, 1);
+      k1 = turb(n1, vec1, 0);
+      w1 = turb(n1, vec1, 1);
+    }
     double q = 0.0;
 #pragma unroll
-    for (int d = 0; d < NDIM; ++d) q += 0.5 * (v0[d + 1] + v1[d + 1]) * normal[(size_t)e * NDIM + d];
+    for (int d = 0; d < NDIM; ++d) q += 0.5 * (u0[d] + u1[d]) * normal[(size_t)e * NDIM + d];
     const double a0 = 0.5 * (q + fabs(q)), a1 = 0.5 * (q - fabs(q));
-    const double rho0 = v0[RHO], rho1 = v1[RHO];
-    const double f0 = a0 * rho0 * T[2 * (size_t)n0] + a1 * rho1 * T[2 * (size_t)n1];
-    const double f1 = a0 * rho0 * T[2 * (size_t)n0 + 1] + a1 * rho1 * T[2 * (size_t)n1 + 1];
+    const double f0 = a0 * rho0 * k0 + a1 * rho1 * k1;
+    const double f1 = a0 * rho0 * w0 + a1 * rho1 * w1;
     // Ji = diag(a0), Jj = diag(a1) with explicit zeros
     const double Ji[4] = {a0, 0.0, 0.0, a0}, Jj[4] = {a1, 0.0, 0.0, a1};
     if (side == 0) {
@@ -334,6 +394,58 @@ __global__ __launch_bounds__(kBlock) void k_sst_upwind(int N, const int32_t* __r
   if (Dp)
 #pragma unroll
     for (int q = 0; q < 4; ++q) Dp[q] = D[q];
+}
+
+// CSolver::SetSolution_Limiter (solver_structure.cpp:951-1204) on (k, omega), SLOPE_LIMITER_TURB = VENKATAKRISHNAN
+// (venkat = 1) or BARTH_JESPERSEN (0: the function has no branch for it, the limiter stays 2.0), node-centric: a
+// domain point's Solution_Min / _Max over its incident edges (du = U_j - U_i at node i of the edge, -du at node j;
+// order-free), then the edge minimum of the Venkatakrishnan function with its own dm. Halo rows: the exchange.
+template <int NDIM>
+__global__ __launch_bounds__(kBlock) void k_sst_limiter(int Nd, const int32_t* __restrict__ adj_ptr,
+                                                        const int32_t* __restrict__ adj,
+                                                        const int32_t* __restrict__ edges,
+                                                        const double* __restrict__ coord, const double* __restrict__ T,
+                                                        const double* __restrict__ TG, double eps2, int venkat,
+                                                        double* __restrict__ L) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Nd) return;
+  double lo[2] = {rx::kEPS, rx::kEPS}, hi[2] = {-rx::kEPS, -rx::kEPS};
+  const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  for (int k = k0; k < k1; ++k) {
+    const int a = adj[k];
+    const int e = a >> 1, side = a & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const double du = T[2 * (size_t)n1 + v] - T[2 * (size_t)n0 + v];
+      const double d = side ? -du : du;
+      lo[v] = fmin(lo[v], d);
+      hi[v] = fmax(hi[v], d);
+    }
+  }
+  double l[2] = {2.0, 2.0};
+  if (venkat) {
+    double ci[NDIM];
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) ci[d] = coord[(size_t)i * NDIM + d];
+    const double* Gi = TG + (size_t)i * 2 * NDIM;
+    for (int k = k0; k < k1; ++k) {
+      const int a = adj[k];
+      const int e = a >> 1, side = a & 1;
+      const int other = edges[2 * e + (side ^ 1)];
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        double dm = 0.0;
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) dm += 0.5 * (coord[(size_t)other * NDIM + d] - ci[d]) * Gi[v * NDIM + d];
+        const double dp = (dm > 0.0) ? hi[v] : lo[v];
+        const double lv = (dp * dp + 2.0 * dp * dm + eps2) / (dp * dp + dp * dm + 2.0 * dm * dm + eps2);
+        if (lv < l[v]) l[v] = lv;
+      }
+    }
+  }
+  L[2 * (size_t)i] = l[0];
+  L[2 * (size_t)i + 1] = l[1];
 }
 
 // CTurbSolver::Viscous_Residual (:545-600) + CAvgGradCorrected_TurbSST (:1080-1163):
@@ -609,23 +721,54 @@ int rx_strain_mag(rx_ctx* ctx) {
   return RX_OK;
 }
 
+// CTurbSSTSolver::Preprocessing (solver_direct_turbulent.cpp:2923-2951): residual and Jacobian zero, the gradient of
+// (k, omega), SetSolution_Limiter when SPATIAL_ORDER_TURB = 2ND_ORDER_LIMITER (this context's cfg.spatial_order = 2),
+// and the flow's SetPrimitive_Limiter again when SPATIAL_ORDER_FLOW = 2ND_ORDER_LIMITER (ExtIter <= LIMITER_ITER, whose
+// default 999999 is taken): the flow limiter the SST upwind then reads is that of the post-update records.
 int rx_sst_preprocessing(rx_ctx* ctx) {
   if (!is_sst(ctx)) return RX_ERR_ARG;
-  RxPhase ph(ctx, RX_K_SST_GRAD);
-  RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
-  if (ctx->cfg.implicit)
-    RX_HIP(hipMemsetAsync(ctx->f[RX_F_JAC], 0, sizeof(double) * ctx->fcount[RX_F_JAC], ctx->stream));
-  ctx->assembled = 1;
-  return sst_gradient(ctx);
+  {
+    RxPhase ph(ctx, RX_K_SST_GRAD);
+    RX_HIP(hipMemsetAsync(ctx->f[RX_F_RES], 0, sizeof(double) * ctx->fcount[RX_F_RES], ctx->stream));
+    if (ctx->cfg.implicit)
+      RX_HIP(hipMemsetAsync(ctx->f[RX_F_JAC], 0, sizeof(double) * ctx->fcount[RX_F_JAC], ctx->stream));
+    ctx->assembled = 1;
+    const int rc = sst_gradient(ctx);
+    if (rc) return rc;
+    if (ctx->cfg.spatial_order == 2 && ctx->Nd > 0) {
+      const double eps1 = ctx->cfg.limiter_coeff * ctx->cfg.ref_elem_length;
+      const double eps2 = eps1 * eps1 * eps1;
+      RX_ND_SWITCH(ctx->nDim, (k_sst_limiter<ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
+                                   (int)ctx->Nd, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->coord, ctx->f[RX_F_U],
+                                   ctx->f[RX_F_GRAD], eps2,
+                                   ctx->cfg.slope_limiter == RX_LIMITER_VENKATAKRISHNAN ? 1 : 0,
+                                   ctx->f[RX_F_LIMITER])));
+      RX_HIP(hipGetLastError());
+      const int rc2 = rx_la_exchange(ctx, ctx->f[RX_F_LIMITER], 2);  // Set_MPI_Solution_Limiter (:1202)
+      if (rc2) return rc2;
+    }
+  }
+  if (ctx->flow->cfg.spatial_order == 2) return rx_limiter_venkat(ctx->flow);
+  return RX_OK;
 }
 
 int rx_sst_upwind(rx_ctx* ctx) {
   if (!is_sst(ctx)) return RX_ERR_ARG;
   RxPhase ph(ctx, RX_K_SST_UPW);
   const rx_ctx* fl = ctx->flow;
-  RX_ND_SWITCH(ctx->nDim, (k_sst_upwind<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
-      (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->diag, ctx->edges, ctx->normal, fl->f[RX_F_V], fl->nPV,
-      ctx->f[RX_F_U], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr)));
+  // SPATIAL_ORDER_TURB: 0 1ST_ORDER, 1 2ND_ORDER, 2 2ND_ORDER_LIMITER (the SST context's cfg.spatial_order)
+  const SstRecon rc{ctx->coord, fl->f[RX_F_GRAD], fl->f[RX_F_LIMITER], ctx->f[RX_F_GRAD], ctx->f[RX_F_LIMITER], fl->nG};
+  switch (ctx->cfg.spatial_order) {
+#define RX_SST_UPW(ORD)                                                                                           \
+  RX_ND_SWITCH(ctx->nDim, (k_sst_upwind<ND_, ORD><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(                      \
+      (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->diag, ctx->edges, ctx->normal, fl->f[RX_F_V], fl->nPV, \
+      ctx->f[RX_F_U], ctx->f[RX_F_RES], ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr, rc)))
+    case 0: RX_SST_UPW(0); break;
+    case 1: RX_SST_UPW(1); break;
+    case 2: RX_SST_UPW(2); break;
+    default: return RX_ERR_ARG;
+#undef RX_SST_UPW
+  }
   RX_HIP(hipGetLastError());
   return RX_OK;
 }

@@ -571,11 +571,11 @@ ITER_KEEP = ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr", "bvert
              "p2v_params", "bsr_row_ptr", "bsr_col", "global_index")
 
 
-def iteration_case(name, writer, U, ns, n_iters, cfl, prec, time_flow, extra=""):
-    wd = make_workdir(name, writer, cfl=cfl, order="1ST_ORDER", prec=prec, time_flow=time_flow, ns=ns, extra=extra)
+def iteration_case(name, writer, U, ns, n_iters, cfl, prec, time_flow, extra="", order="1ST_ORDER"):
+    wd = make_workdir(name, writer, cfl=cfl, order=order, prec=prec, time_flow=time_flow, ns=ns, extra=extra)
     write_state(wd, U)
     a = run_harness(wd, bsr=False, extra=["--iters", str(n_iters)])
-    out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it")}
+    out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it") or k == "limiter_params"}
     big = len(a["coord"]) > 5000  # whole-mesh cases: one iteration, no later Solution_Old needed
     out = {k: v for k, v in out.items()
            if not k.endswith("_wall") and not (big and k.endswith("_Uold") and k != "it_Uold0")}
@@ -613,8 +613,9 @@ def ig9_workdir(case_dir=None, root="/tmp/rx_golden"):
     return wd
 
 
-def fp_workdir(case_dir=None, root="/tmp/rx_golden", name="fpit"):
-    """Work dir of the flat plate (FP_CFG) over the plate's files (default: the reference's TURBOLENT_FLAT_PLATE)."""
+def fp_workdir(case_dir=None, root="/tmp/rx_golden", name="fpit", cfg_edit=None):
+    """Work dir of the flat plate (FP_CFG) over the plate's files (default: the reference's TURBOLENT_FLAT_PLATE);
+    cfg_edit(text) -> text changes the cfg."""
     case_dir = case_dir or FP_DIR
     wd = os.path.join(root, name)
     shutil.rmtree(wd, ignore_errors=True)
@@ -624,7 +625,7 @@ def fp_workdir(case_dir=None, root="/tmp/rx_golden", name="fpit"):
     os.symlink(os.path.join(case_dir, "test_air.txt"), os.path.join(wd, "test_air.txt"))
     os.symlink(os.path.join(case_dir, "mesh_flatplate_turb_137x97.su2"), os.path.join(wd, "mesh.su2"))
     with open(os.path.join(wd, "case.cfg"), "w") as f:
-        f.write(FP_CFG)
+        f.write(cfg_edit(FP_CFG) if cfg_edit else FP_CFG)
     return wd
 
 
@@ -662,6 +663,24 @@ def case_it7():
     reference outer iterations."""
     pts, quads, U, writer = mini9_inputs()
     return iteration_case("it7", writer, fold_species(U, 7), 7, 2, 5.0, "ILU0", "EULER_IMPLICIT")
+
+
+def case_it4t(limiter=False):
+    """The SST's second-order upwind on a reacting state (the flat plate's composition is uniform, so there its
+    density reconstruction along the gradient of X_0 — CTurbSolver::Upwind_Residual reconstructs the flow record
+    entry iVar with gradient row iVar, solver_direct_turbulent.cpp:481-493 — and the flow limiter entry it reads past
+    the end are invisible): the mini9 jet with the 4-species mechanism (nPrimVarGrad = 8 fits the reference's
+    FlowPrimVar of nDim + 7 = 9 entries; with more species the reference writes past it), implicit ILU0 at CFL 1,
+    SPATIAL_ORDER_TURB= 2ND_ORDER (it4t) or 2ND_ORDER_LIMITER with the flow at 2ND_ORDER_LIMITER (it4tl), two
+    reference outer iterations."""
+    pts, quads, U, writer = mini9_inputs()
+    ord_t = "2ND_ORDER_LIMITER" if limiter else "2ND_ORDER"
+    out = iteration_case("it4tl" if limiter else "it4t", writer, fold_species(U, 4), 4, 2, 1.0, "ILU0",
+                         "EULER_IMPLICIT", extra=f"SPATIAL_ORDER_TURB= {ord_t}\n",
+                         order="2ND_ORDER_LIMITER" if limiter else "1ST_ORDER")
+    out["spatial_order"] = np.array(2 if limiter else 0)
+    out["sst_spatial_order"] = np.array(2 if limiter else 1)
+    return out
 
 
 FP_DIR = os.path.join(REF, "Test_Cases/TURBOLENT/TURBOLENT_FLAT_PLATE")
@@ -759,6 +778,33 @@ def case_fpit():
     return out
 
 
+def case_fpit2(limiter=False):
+    """The whole flat plate (fpit) with the SST's second-order upwind: SPATIAL_ORDER_TURB= 2ND_ORDER (fpit2), or
+    2ND_ORDER_LIMITER with SLOPE_LIMITER_TURB= VENKATAKRISHNAN and the flow's SPATIAL_ORDER_FLOW= 2ND_ORDER_LIMITER
+    (fpit2l: CTurbSolver::Upwind_Residual's MUSCL branch, solver_direct_turbulent.cpp:464-510, on the limiters of
+    CSolver::SetSolution_Limiter, solver_structure.cpp:951-1204, and of the flow's SetPrimitive_Limiter that
+    CTurbSSTSolver::Preprocessing repeats, :2945-2949). One reference outer iteration from the converged state."""
+    def edit(t):
+        t = t.replace("SLOPE_LIMITER_TURB= VENKATAKRISHNAN",
+                      "SLOPE_LIMITER_TURB= VENKATAKRISHNAN\nSPATIAL_ORDER_TURB= " +
+                      ("2ND_ORDER_LIMITER" if limiter else "2ND_ORDER"))
+        if limiter:
+            t = t.replace("SPATIAL_ORDER_FLOW= 2ND_ORDER", "SPATIAL_ORDER_FLOW= 2ND_ORDER_LIMITER")
+        return t
+    wd = fp_workdir(name="fpit2l" if limiter else "fpit2", cfg_edit=edit)
+    _, cons = read_plot(os.path.join(FP_DIR, "PLOT/flow.dat"), ncons=9)
+    write_state(wd, cons)
+    a = run_harness(wd, bsr=False, extra=["--iters", "1"])
+    out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it") or k == "limiter_params"}
+    out = {k: v for k, v in out.items() if not k.endswith("_wall") and not (k.endswith("_Uold") and k != "it_Uold0")}
+    out.update(mech_arrays(FP_DIR, "test_air.txt"))
+    out["time_flow"] = np.array("EULER_IMPLICIT")
+    out["lin_prec"] = np.array("LU_SGS")
+    out["spatial_order"] = np.array(2 if limiter else 1)
+    out["sst_spatial_order"] = np.array(2 if limiter else 1)
+    return out
+
+
 def window_case(a, keep):
     """Restrict a whole-mesh harness dump to the points `keep` (and the edges between them); interior = points
     whose whole neighbourhood is kept (where loop results are complete)."""
@@ -833,7 +879,9 @@ def main():
              "bc9t": lambda: case_bc9("TOTAL_CONDITIONS"), "bc9m": lambda: case_bc9("MASS_FLOW"),
              "mini3d": case_mini3d, "bc3d": case_bc3d, "it3d": case_it3d, "muscl3d": case_muscl3d,
              "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
-             "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d}[case]()
+             "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d, "fpit2": case_fpit2,
+             "fpit2l": lambda: case_fpit2(limiter=True), "it4t": case_it4t,
+             "it4tl": lambda: case_it4t(limiter=True)}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

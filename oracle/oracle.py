@@ -478,6 +478,30 @@ def sst_upwind(nDim, edges, normal, V, T):
 
 
 @_keepalive
+def sst_limiter(nDim, edges, coord, T, TG, ref_len, coeff, kind=0):
+    """CSolver::SetSolution_Limiter on (k, omega) (orc_sst_limiter): kind 0 VENKATAKRISHNAN, 1 BARTH_JESPERSEN (2.0)."""
+    N = len(T)
+    L = np.zeros((N, 2))
+    lib().orc_sst_limiter(C.c_int(nDim), C.c_int64(N), C.c_int64(len(edges)), _p(edges, np.int64), _p(coord), _p(T),
+                          _p(TG), C.c_double(ref_len), C.c_double(coeff), C.c_int(kind), _f(L))
+    return L
+
+
+@_keepalive
+def sst_upwind2(nDim, edges, normal, coord, V, G, Lf, T, TG, TL, order):
+    """CTurbSolver::Upwind_Residual's second-order branch + CUpwSca_TurbSST (orc_sst_upwind2): order 1 2ND_ORDER,
+    2 2ND_ORDER_LIMITER (Lf: the flow's limiter [N][nDim + 2], TL: the SST limiter [N][2])."""
+    E = len(edges)
+    res, Ji, Jj = np.zeros((E, 2)), np.zeros((E, 2, 2)), np.zeros((E, 2, 2))
+    G = np.ascontiguousarray(G, dtype=np.float64)
+    lib().orc_sst_upwind2(C.c_int(nDim), C.c_int(V.shape[1]), C.c_int(G.reshape(len(V), -1).shape[1] // nDim),
+                          C.c_int64(E), _p(edges, np.int64), _p(normal), _p(coord), _p(V), _p(G),
+                          _p(Lf) if Lf is not None else None, _p(T), _p(TG), _p(TL) if TL is not None else None,
+                          C.c_int(order), _f(res), _f(Ji), _f(Jj))
+    return res, Ji, Jj
+
+
+@_keepalive
 def sst_visc(nDim, edges, normal, coord, V, T, TG, F1, mu, eddy):
     E = len(edges)
     res, Ji, Jj = np.zeros((E, 2)), np.zeros((E, 2, 2)), np.zeros((E, 2, 2))
@@ -708,9 +732,27 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     Un = o2["U"]
     V2 = o2["V"]
     rho = np.ascontiguousarray(V2[:, nDim + 2])
-    # SST SingleGrid_Iteration
+    # SST SingleGrid_Iteration: CTurbSSTSolver::Preprocessing (solver_direct_turbulent.cpp:2923-2951): the gradient,
+    # SetSolution_Limiter when SPATIAL_ORDER_TURB = 2ND_ORDER_LIMITER, and the flow's SetPrimitive_Limiter again when
+    # SPATIAL_ORDER_FLOW = 2ND_ORDER_LIMITER (ExtIter <= LIMITER_ITER, default 999999) on the post-update records
     TG0 = sol_grad(T)
-    ru, Jui, Juj = sst_upwind(nDim, mesh["edges"], mesh["edge_normal"], V2, T)
+    sst_order = int(cfg.get("sst_order", 0))  # SPATIAL_ORDER_TURB: 0 1ST_ORDER, 1 2ND_ORDER, 2 2ND_ORDER_LIMITER
+    if sst_order == 0:
+        ru, Jui, Juj = sst_upwind(nDim, mesh["edges"], mesh["edge_normal"], V2, T)
+    else:
+        TL = (sst_limiter(nDim, mesh["edges"], mesh["coord"], T, TG0, cfg["ref_elem_length"], cfg["limiter_coeff"],
+                          int(cfg.get("sst_slope_limiter", 0))) if sst_order == 2 else None)
+        Lf = None
+        if sst_order == 2:  # the flow's Limiter_Primitive at this point
+            if int(cfg.get("spatial_order", 0)) == 2:
+                Lf = (limiter_barth(nDim, ns, mesh["edges"], mesh["coord"], V2, G2)
+                      if int(cfg.get("slope_limiter", 0)) == 1 else
+                      limiter_venkat(nDim, ns, mesh["edges"], mesh["coord"], V2, G2, cfg["ref_elem_length"],
+                                     cfg["limiter_coeff"]))
+            else:  # never computed: CReactiveEulerVariable's Limiter_Primitive.resize(nPrimVarLim, 0.0)
+                Lf = np.zeros((N, nDim + 2))
+        ru, Jui, Juj = sst_upwind2(nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], V2, G2, Lf, T, TG0, TL,
+                                   sst_order)
     rv2, Jvi2, Jvj2 = sst_visc(nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], V2, T, TG0, s["F1"], o2["mu"],
                                o2["eddy"])
     rs2, Js2 = sst_source(nDim, V2, G2, T, vol, mesh["wall_distance"], s["F1"], s["F2"], s["CDkw"], strain2, o2["eddy"])

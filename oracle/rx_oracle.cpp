@@ -2633,6 +2633,101 @@ void orc_sst_upwind(int nDim, int nPV, int64_t E, const int64_t* edges, const do
   }
 }
 
+// CSolver::SetSolution_Limiter (solver_structure.cpp:951-1204) on the SST solution (k, omega), called by
+// CTurbSSTSolver::Preprocessing when SPATIAL_ORDER_TURB = 2ND_ORDER_LIMITER (solver_direct_turbulent.cpp:2945-2947):
+// Solution_Max / _Min from -EPS / EPS over the edges (du = U_j - U_i at i, -du at j), the limiter 2.0 at every
+// domain point, then SLOPE_LIMITER_TURB = VENKATAKRISHNAN (kind 0) takes the edge minimum of
+// (dp^2 + 2 dp dm + eps2) / (dp^2 + dp dm + 2 dm^2 + eps2), eps2 = (LIMITER_COEFF * REF_ELEM_LENGTH)^3; the function has
+// no branch for BARTH_JESPERSEN (kind 1), which leaves 2.0.
+void orc_sst_limiter(int nDim, int64_t N, int64_t E, const int64_t* edges, const double* coord, const double* T,
+                     const double* TG, double ref_len, double lim_coeff, int kind, double* lim) {
+  std::vector<double> mx(N * 2, -EPS), mn(N * 2, EPS);
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    for (int v = 0; v < 2; ++v) {
+      const double du = T[2 * j + v] - T[2 * i + v];
+      mn[2 * i + v] = std::min(mn[2 * i + v], du);
+      mx[2 * i + v] = std::max(mx[2 * i + v], du);
+      mn[2 * j + v] = std::min(mn[2 * j + v], -du);
+      mx[2 * j + v] = std::max(mx[2 * j + v], -du);
+    }
+  }
+  for (int64_t q = 0; q < N * 2; ++q) lim[q] = 2.0;
+  if (kind != 0) return;
+  const double eps1 = lim_coeff * ref_len;
+  const double eps2 = eps1 * eps1 * eps1;
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    const double* Gi = TG + i * 2 * nDim;
+    const double* Gj = TG + j * 2 * nDim;
+    const double* ci = coord + i * nDim;
+    const double* cj = coord + j * nDim;
+    for (int v = 0; v < 2; ++v) {
+      double dm = 0.0;
+      for (int d = 0; d < nDim; ++d) dm += 0.5 * (cj[d] - ci[d]) * Gi[v * nDim + d];
+      double dp = (dm > 0.0) ? mx[2 * i + v] : mn[2 * i + v];
+      double lv = (dp * dp + 2.0 * dp * dm + eps2) / (dp * dp + dp * dm + 2.0 * dm * dm + eps2);
+      if (lv < lim[2 * i + v]) lim[2 * i + v] = lv;
+      dm = 0.0;
+      for (int d = 0; d < nDim; ++d) dm += 0.5 * (ci[d] - cj[d]) * Gj[v * nDim + d];
+      dp = (dm > 0.0) ? mx[2 * j + v] : mn[2 * j + v];
+      lv = (dp * dp + 2.0 * dp * dm + eps2) / (dp * dp + dp * dm + 2.0 * dm * dm + eps2);
+      if (lv < lim[2 * j + v]) lim[2 * j + v] = lv;
+    }
+  }
+}
+
+// CTurbSolver::Upwind_Residual's second-order branch (solver_direct_turbulent.cpp:464-510) + CUpwSca_TurbSST, fixed
+// grid. order 1 = SPATIAL_ORDER_TURB 2ND_ORDER, 2 = 2ND_ORDER_LIMITER. Vector_i = (x_j - x_i) / 2, Vector_j = (x_i -
+// x_j) / 2 (computed as 0.5 * difference). The flow record is reconstructed entry by entry for iVar <
+// nPrimVarGrad as FlowPrimVar[iVar] = V[iVar] (+ Limiter_Primitive[iVar] *) sum_d Vector[d] Gradient_Primitive[iVar][d],
+// i.e. with the gradient ROW iVar of (T, u, v(, w), P, X_s) against the primitive ENTRY iVar of (T, u, v(, w), P, rho,
+// h, a, Y_s): the velocity entries the scalar upwind reads match their rows, its density entry V[nDim+2] is moved
+// along the gradient of X_0 (reproduced). With the limiter the flow's Limiter_Primitive (nDim+2 entries: T, u, v(, w),
+// P) is read at iVar = nDim+2, one past its end — undefined in the reference; restated as 0.0 (the density is not
+// moved), which the flat-plate golden fpit2l pins (tests/test_oracle_bc.py). Lf: the flow limiter [N][nDim+2] or null
+// (order 1). The turbulent solution: T (+ TL *) sum_d Vector[d] TG[v][d].
+void orc_sst_upwind2(int nDim, int nPV, int nG, int64_t E, const int64_t* edges, const double* normal,
+                     const double* coord, const double* V, const double* G, const double* Lf, const double* T,
+                     const double* TG, const double* TL, int order, double* res, double* Ji, double* Jj) {
+  const bool lim = order == 2;
+  const int nL = nDim + 2;
+#pragma omp parallel for schedule(static)
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t i = edges[2 * e], j = edges[2 * e + 1];
+    double vec_i[3], vec_j[3];
+    for (int d = 0; d < nDim; ++d) {
+      vec_i[d] = 0.5 * (coord[j * nDim + d] - coord[i * nDim + d]);
+      vec_j[d] = 0.5 * (coord[i * nDim + d] - coord[j * nDim + d]);
+    }
+    auto flow = [&](int64_t p, const double* vec, int v) {  // FlowPrimVar entry v (v = 1..nDim, nDim + 2)
+      double pg = 0.0;
+      for (int d = 0; d < nDim; ++d) pg += vec[d] * G[(p * nG + v) * nDim + d];
+      if (!lim) return V[p * nPV + v] + pg;
+      const double l = v < nL ? Lf[p * nL + v] : 0.0;  // v = nDim + 2: past the limiter's end (see above)
+      return V[p * nPV + v] + l * pg;
+    };
+    auto turb = [&](int64_t p, const double* vec, int v) {
+      double pg = 0.0;
+      for (int d = 0; d < nDim; ++d) pg += vec[d] * TG[(p * 2 + v) * nDim + d];
+      return lim ? T[2 * p + v] + TL[2 * p + v] * pg : T[2 * p + v] + pg;
+    };
+    const double* n = normal + e * nDim;
+    double q = 0.0;
+    for (int d = 0; d < nDim; ++d) q += 0.5 * (flow(i, vec_i, d + 1) + flow(j, vec_j, d + 1)) * n[d];
+    const double a0 = 0.5 * (q + std::fabs(q)), a1 = 0.5 * (q - std::fabs(q));
+    const double ri = flow(i, vec_i, nDim + 2), rj = flow(j, vec_j, nDim + 2);
+    res[2 * e] = a0 * ri * turb(i, vec_i, 0) + a1 * rj * turb(j, vec_j, 0);
+    res[2 * e + 1] = a0 * ri * turb(i, vec_i, 1) + a1 * rj * turb(j, vec_j, 1);
+    if (Ji) {
+      double* A = Ji + 4 * e;
+      double* B = Jj + 4 * e;
+      A[0] = a0; A[1] = 0.0; A[2] = 0.0; A[3] = a0;
+      B[0] = a1; B[1] = 0.0; B[2] = 0.0; B[3] = a1;
+    }
+  }
+}
+
 // CAvgGradCorrected_TurbSST::ComputeResidual (numerics_direct_turbulent.cpp:1080-1163) with the
 // setters of CTurbSolver::Viscous_Residual (solver_direct_turbulent.cpp:545-600): laminar and
 // eddy viscosity of the flow nodes, F1 of the turbulent nodes.

@@ -57,14 +57,17 @@ def solvers(g, implicit=1):
     flow_imp, _, prec = scheme(g)
     order = int(g["spatial_order"]) if "spatial_order" in g else 0  # SPATIAL_ORDER_FLOW (fpit: 2ND_ORDER)
     gm = int("grad_method" in g and str(g["grad_method"]) == "GREEN_GAUSS")  # NUM_METHOD_GRAD (gg9)
+    lim = (dict(ref_elem_length=float(g["limiter_params"][0]), limiter_coeff=float(g["limiter_params"][1]))
+           if "limiter_params" in g else {})  # REF_ELEM_LENGTH, LIMITER_COEFF
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(g), rx.default_cfg(implicit=implicit if flow_imp else 0, lin_prec=prec,
                                                                   spatial_order=order, grad_method=gm, **cfg_kw(g),
-                                                                  **ignition_kw(g)))
+                                                                  **ignition_kw(g), **lim))
     s.set_bc(rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"]))
     bp = g["bc_params"]
+    so_t = int(g["sst_spatial_order"]) if "sst_spatial_order" in g else 0  # SPATIAL_ORDER_TURB (fpit2 / fpit2l / it4t)
     t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(implicit=implicit, lin_prec=prec, lin_tol=float(bp[19]),
                                              lin_iter=int(bp[20]), relaxation_turb=float(bp[23]),
-                                             cfl_red_turb=float(bp[24]), grad_method=gm))
+                                             cfl_red_turb=float(bp[24]), grad_method=gm, spatial_order=so_t, **lim))
     return s, t
 
 
@@ -185,7 +188,8 @@ def n_iters(g):
     return sum(1 for k in g if k.startswith("it") and k.endswith("_U") and k[2:-2].isdigit())
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
+                                  "fpit2l", "it4t"])
 def test_outer_iterations_vs_reference(case):
     """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d / it7: 2, itx9 /
     itx4: 1) on the device, started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within
@@ -223,7 +227,8 @@ def test_free_running_iterations_vs_reference(case):
     s.close()
 
 
-@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d"])
+@pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
+                                  "fpit2l", "it4t"])
 def test_outer_iteration_vs_oracle_device_order(case):
     """One iteration against the oracle run with the device's inner-product order: the residual side and the
     Krylov recurrence then agree to the Stefan-Maxwell rounding only (amplified by FGMRES: the same 1e-10 bar)."""

@@ -257,7 +257,7 @@ REJECTED = [  # (key, value): physics / numerics this path does not build (VERDI
     ("KIND_TURB_MODEL", "SA"), ("KIND_TURB_MODEL", "NONE"), ("KIND_TURB_MODEL", None),
     ("NUM_METHOD_GRAD", "LEAST_SQUARES"), ("LINEAR_SOLVER", "BCGSTAB"), ("LINEAR_SOLVER", "RESTARTED_FGMRES"),
     ("CONV_NUM_METHOD_FLOW", "ROE"), ("CONV_NUM_METHOD_FLOW", None), ("CONV_NUM_METHOD_TURB", "JST"),
-    ("SPATIAL_ORDER_TURB", "2ND_ORDER"), ("TIME_DISCRE_TURB", "EULER_EXPLICIT"),
+    ("SLOPE_LIMITER_TURB", "SHARP_EDGES"), ("TIME_DISCRE_TURB", "EULER_EXPLICIT"),
     ("UNSTEADY_SIMULATION", "DUAL_TIME_STEPPING-2ND_ORDER"), ("MATH_PROBLEM", "CONTINUOUS_ADJOINT")]
 
 
@@ -435,3 +435,19 @@ def test_native_cfg_defaults_match_the_python_mirror():
     d = rx.default_cfg()
     for name, _ in rx.Cfg._fields_:
         assert getattr(c, name) == getattr(d, name), name
+
+
+@pytest.mark.parametrize("order,want", [("1ST_ORDER", 0), ("2ND_ORDER", 1), ("2ND_ORDER_LIMITER", 2)])
+def test_case_from_cfg_sst_spatial_order(tmp_path, order, want):
+    """SPATIAL_ORDER_TURB (config_structure.cpp:1189) selects the SST upwind's MUSCL branch (round 5: built, goldens
+    fpit2 / fpit2l / it4t): it is the SST context's spatial_order, with the flow's REF_ELEM_LENGTH / LIMITER_COEFF and
+    SLOPE_LIMITER_TURB for SetSolution_Limiter."""
+    wd, base = _jet_cfg(tmp_path)
+    txt = _with_key(_with_key(base, "SPATIAL_ORDER_TURB", order), "SLOPE_LIMITER_TURB", "BARTH_JESPERSEN")
+    with open(os.path.join(wd, "case.cfg"), "w") as f:
+        f.write(_with_key(_with_key(txt, "REF_ELEM_LENGTH", "0.002"), "LIMITER_COEFF", "0.3"))
+    case = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
+    sc = case["sst_cfg"]
+    assert sc["spatial_order"] == want and sc["slope_limiter"] == rx.LIMITER_BARTH_JESPERSEN
+    assert sc["ref_elem_length"] == 0.002 and sc["limiter_coeff"] == 0.3
+    case["mesh"].close()

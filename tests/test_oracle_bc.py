@@ -39,7 +39,8 @@ def bc9(request):
     return bc_case(request.param)
 
 
-@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d"])
+@pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
+                                        "fpit2l", "it4t"])
 def it9(request):
     return golden(request.param)
 
@@ -107,6 +108,10 @@ def iteration_cfg(g):
     cfg["sst_prec"] = "lusgs" if ("lin_prec" in g and str(g["lin_prec"]) == "LU_SGS") else "ilu"
     cfg["flow_prec"] = cfg["sst_prec"]  # LINEAR_SOLVER_PREC serves both solvers
     cfg["spatial_order"] = int(g["spatial_order"]) if "spatial_order" in g else 0
+    if "limiter_params" in g:  # REF_ELEM_LENGTH, LIMITER_COEFF
+        cfg.update(ref_elem_length=float(g["limiter_params"][0]), limiter_coeff=float(g["limiter_params"][1]))
+    if "sst_spatial_order" in g:  # SPATIAL_ORDER_TURB (fpit2 / fpit2l), SLOPE_LIMITER_TURB VENKATAKRISHNAN
+        cfg["sst_order"] = int(g["sst_spatial_order"])
     if "grad_method" in g and str(g["grad_method"]) == "GREEN_GAUSS":  # NUM_METHOD_GRAD (gg9)
         cfg["grad"] = "gg"
     if "ignition" in g:  # IGNITION, IGNITION_ITER, IGNITION_TEMPERATURE, FUEL_INDEX, OXIDIZER_INDEX (ig9)
