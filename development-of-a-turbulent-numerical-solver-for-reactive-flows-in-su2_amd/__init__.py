@@ -88,7 +88,11 @@ class Cfg(C.Structure):
                 ("cond_ref", C.c_double), ("vel_ref", C.c_double), ("len_ref", C.c_double),
                 ("slope_limiter", C.c_int32), ("ignition", C.c_int32), ("fuel_index", C.c_int32),
                 ("oxidizer_index", C.c_int32), ("ignition_iter", C.c_int64), ("ignition_temp", C.c_double),
-                ("grad_method", C.c_int32)]
+                ("grad_method", C.c_int32), ("lin_solver", C.c_int32), ("lin_restart", C.c_int32)]
+
+# rx_lin_prec / rx_lin_solver (include/rx.h): LINEAR_SOLVER_PREC and LINEAR_SOLVER
+PREC_LU_SGS, PREC_ILU, PREC_JACOBI = 0, 1, 2
+LIN_FGMRES, LIN_BCGSTAB, LIN_RESTARTED_FGMRES, LIN_SMOOTHER_LUSGS, LIN_SMOOTHER_JACOBI, LIN_SMOOTHER_ILU = range(6)
 
 
 class BcDesc(C.Structure):
@@ -153,6 +157,7 @@ def lib():
         _lib.rx_ilu0_apply.argtypes = [C.c_void_p, C.c_int, C.c_int]
         _lib.rx_lusgs_apply.argtypes = [C.c_void_p, C.c_int, C.c_int]
         _lib.rx_fgmres.argtypes = [C.c_void_p, C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        _lib.rx_linear_solve.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         _lib.rx_explicit_euler.argtypes = [C.c_void_p, C.c_void_p]
         _lib.rx_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         _lib.rx_explicit_rk.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p]
@@ -332,7 +337,8 @@ def default_cfg(**kw):
              cond_ref=1.0, vel_ref=1.0, len_ref=1.0, slope_limiter=0,
              # CConfig defaults (config_structure.cpp:591-603)
              ignition=0, fuel_index=0, oxidizer_index=2, ignition_iter=999999, ignition_temp=1700.0,
-             grad_method=0)  # NUM_METHOD_GRAD: 0 WEIGHTED_LEAST_SQUARES, 1 GREEN_GAUSS
+             grad_method=0,  # NUM_METHOD_GRAD: 0 WEIGHTED_LEAST_SQUARES, 1 GREEN_GAUSS
+             lin_solver=0, lin_restart=10)  # LINEAR_SOLVER (LIN_*), LINEAR_SOLVER_RESTART_FREQUENCY
     c.update(kw)
     cfg = Cfg()
     for k, v in c.items():
@@ -537,6 +543,14 @@ class ReactiveNSSolver:
         _chk(lib().rx_fgmres(self.h, tol, m, C.byref(it), C.byref(res)), "rx_fgmres", self.h)
         return it.value, res.value
 
+    def linear_solve(self):
+        """CSysSolve::Solve on JAC * SOL = RHS with the cfg's LINEAR_SOLVER / _PREC / _ERROR / _ITER /
+        _RESTART_FREQUENCY (rx_linear_solve) -> (iterations, residual norm)."""
+        it = C.c_int()
+        res = C.c_double()
+        _chk(lib().rx_linear_solve(self.h, C.byref(it), C.byref(res)), "rx_linear_solve", self.h)
+        return it.value, res.value
+
     def ExplicitEuler_Iteration(self):
         rms = np.zeros(self.nVar)
         _chk(lib().rx_explicit_euler(self.h, rms.ctypes.data), "rx_explicit_euler", self.h)
@@ -564,14 +578,15 @@ class ReactiveNSSolver:
 
 
 def sst_cfg(implicit=1, lin_tol=1e-6, lin_iter=5, lin_prec=1, relaxation_turb=1.0, cfl_red_turb=1.0, grad_method=0,
-            spatial_order=0, slope_limiter=0, ref_elem_length=0.1, limiter_coeff=0.5):
+            spatial_order=0, slope_limiter=0, ref_elem_length=0.1, limiter_coeff=0.5, lin_solver=0, lin_restart=10):
     """rx_cfg for the SST context: RELAXATION_FACTOR_TURB -> relaxation, CFL_REDUCTION_TURB -> cfl, NUM_METHOD_GRAD
     -> grad_method, SPATIAL_ORDER_TURB -> spatial_order (0 1ST_ORDER, 1 2ND_ORDER, 2 2ND_ORDER_LIMITER),
-    SLOPE_LIMITER_TURB -> slope_limiter, REF_ELEM_LENGTH / LIMITER_COEFF (the flow's)."""
+    SLOPE_LIMITER_TURB -> slope_limiter, REF_ELEM_LENGTH / LIMITER_COEFF (the flow's); LINEAR_SOLVER /
+    LINEAR_SOLVER_RESTART_FREQUENCY are the flow's (one System.Solve config)."""
     return default_cfg(implicit=implicit, lin_tol=lin_tol, lin_iter=lin_iter, lin_prec=lin_prec,
                        relaxation=relaxation_turb, cfl=cfl_red_turb, grad_method=grad_method,
                        spatial_order=spatial_order, slope_limiter=slope_limiter, ref_elem_length=ref_elem_length,
-                       limiter_coeff=limiter_coeff)
+                       limiter_coeff=limiter_coeff, lin_solver=lin_solver, lin_restart=lin_restart)
 
 
 class TurbSSTSolver:

@@ -82,6 +82,10 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
                 rx_ctx** out) {
   if (!mesh || !cfg || !out || (!mech && !flow)) return RX_ERR_ARG;
   if (cfg->spatial_order < 0 || cfg->spatial_order > 2) return RX_ERR_ARG;
+  if (cfg->implicit && (cfg->lin_solver < RX_LIN_FGMRES || cfg->lin_solver > RX_LIN_SMOOTHER_ILU ||
+                        cfg->lin_prec < RX_PREC_LU_SGS || cfg->lin_prec > RX_PREC_JACOBI || cfg->lin_restart < 0 ||
+                        cfg->lin_iter < 1))
+    return RX_ERR_ARG;
   *out = nullptr;
   if (mesh->n_dim != 2 && mesh->n_dim != 3) return RX_ERR_ARG;
   const bool sst = flow != nullptr;
@@ -683,7 +687,8 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   if (ctx->cfg.implicit) {
     // LU-SGS's factorised diagonal blocks: only with the LU_SGS preconditioner (rx_lusgs_apply allocates them on
     // first use otherwise)
-    if (ctx->cfg.lin_prec == 0) CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
+    if (rx_la_eff_prec(ctx) == RX_PREC_LU_SGS) CK(dalloc(ctx, &ctx->dlu, N * (int64_t)nv * nv));
+    if (rx_la_eff_prec(ctx) == RX_PREC_JACOBI) CK(dalloc(ctx, &ctx->jinv, ctx->Nd * (int64_t)nv * nv));
     CK(dalloc(ctx, &ctx->xstar, N * nv));
   }
   if (!sst && ctx->cfg.spatial_order) CK(dalloc(ctx, &ctx->recon, E * 2 * (int64_t)(ctx->nPV + nv)));
@@ -728,7 +733,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->fs.pass_lo, ctx->fs.part_pass, ctx->bs.pass_lo, ctx->bs.part_pass,
                   ctx->fs.slot, ctx->bs.slot, ctx->fs.ring, ctx->bs.ring, ctx->ring_xoff, ctx->send_idx, ctx->grad_list, ctx->spmv_rows, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,
-                  ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar,
+                  ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar, ctx->jinv,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   rx_comm_free(ctx);
   if (ctx->kind == RX_KIND_FLOW) rx_bc_free(ctx);
@@ -943,8 +948,29 @@ int rx_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
   RxPhase ph(ctx, RX_K_KRYLOV);
-  if (ctx->cfg.lin_prec == 0 && (rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
+  if (rx_la_eff_prec(ctx) != RX_PREC_ILU && (rc = rx_la_prec_build(ctx))) return rc;  // ILU: rx_ilu0_build's factor
   return rx_la_fgmres(ctx, tol, m, iters, resid);
+}
+
+// CSysSolve::Solve (linear_solvers_structure.cpp:601-708) on the assembled system: the preconditioner build of the
+// configured branch, then cfg.lin_solver with cfg.lin_tol / lin_iter on JAC * SOL = RHS from SOL's current values
+// (their halo is the caller's). Synchronous: returns the iteration count and the final residual norm.
+int rx_linear_solve(rx_ctx* ctx, int* iters, double* resid) {
+  if (!ctx || !ctx->cfg.implicit || !iters || !resid) return RX_ERR_ARG;
+  int rc = ensure_assembled(ctx);
+  if (rc) return rc;
+  const int ls = ctx->cfg.lin_solver;
+  if ((rc = rx_la_krylov_alloc(ctx, (ls == RX_LIN_FGMRES || ls == RX_LIN_RESTARTED_FGMRES) ? ctx->cfg.lin_iter : 3)))
+    return rc;
+  RxPhase ph(ctx, RX_K_KRYLOV);
+  if ((rc = rx_la_prec_build(ctx))) return rc;
+  if ((rc = rx_la_solve_enqueue(ctx, false))) return rc;
+  int it = 0;
+  double r = 0.0;
+  if ((rc = rx_la_fgmres_result(ctx, &it, &r))) return rc;
+  *iters = ctx->solve_iters >= 0 ? ctx->solve_iters : it;
+  *resid = r;
+  return RX_OK;
 }
 
 int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
@@ -989,13 +1015,13 @@ int rx_explicit_rk(rx_ctx* ctx, int rk_step, double alpha, double* res_rms) {
 }
 
 namespace {
-// FGMRES, RMS partials and the clipped update: a fixed kernel sequence with no host decision
-// (rx_krylov.hip), recorded once as a hipGraph. System and preconditioner builds are launched
+// The linear solve (FGMRES by default), RMS partials and the clipped update: a fixed kernel sequence with no host
+// decision (rx_krylov.hip), recorded once as a hipGraph (RESTARTED_FGMRES runs eagerly: its cycles are host decisions). System and preconditioner builds are launched
 // before it as single kernels (timed per phase).
 int enqueue_solve(rx_ctx* ctx) {
   int rc;
   static const bool x_product = getenv("RX_FG_X_PRODUCT") != nullptr;  // diagnosis: the A x product at x = 0
-  if ((rc = rx_la_fgmres_enqueue(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter, !x_product))) return rc;
+  if ((rc = rx_la_solve_enqueue(ctx, !x_product))) return rc;
   if ((rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RHS]))) return rc;
   return ctx->kind == RX_KIND_SST ? rx_sst_update(ctx) : rx_la_implicit_update(ctx);
 }
@@ -1027,21 +1053,20 @@ int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   const bool sst = ctx->kind == RX_KIND_SST;
   int rc = ensure_assembled(ctx);
   if (rc) return rc;
-  if ((rc = rx_la_krylov_alloc(ctx, ctx->cfg.lin_iter))) return rc;
+  const int ls = ctx->cfg.lin_solver;
+  if ((rc = rx_la_krylov_alloc(ctx, (ls == RX_LIN_FGMRES || ls == RX_LIN_RESTARTED_FGMRES) ? ctx->cfg.lin_iter : 3)))
+    return rc;
   {
     RxPhase ph(ctx, sst ? RX_K_SST_SYSTEM : RX_K_UPDATE);
     if ((rc = sst ? rx_sst_build_system(ctx) : rx_la_build_system(ctx))) return rc;
   }
-  if (ctx->cfg.lin_prec == 1) {
-    RxPhase ph(ctx, sst ? RX_K_SST_SYSTEM : RX_K_ILU_BUILD);
-    if ((rc = rx_la_ilu_build(ctx))) return rc;
-  } else {
-    RxPhase ph(ctx, sst ? RX_K_SST_SYSTEM : RX_K_LUSGS);
-    if ((rc = rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]))) return rc;
+  {
+    RxPhase ph(ctx, sst ? RX_K_SST_SYSTEM : (rx_la_eff_prec(ctx) == RX_PREC_ILU ? RX_K_ILU_BUILD : RX_K_LUSGS));
+    if ((rc = rx_la_prec_build(ctx))) return rc;
   }
   {
     RxPhase ph(ctx, sst ? RX_K_SST_SOLVE : RX_K_SOLVE);
-    if (graphs_enabled(ctx)) {
+    if (graphs_enabled(ctx) && rx_la_solve_capturable(ctx)) {
       const uint64_t epoch = (sst && ctx->flow ? ctx->flow : ctx)->bc_epoch;
       if (ctx->solve_exec && ctx->graph_epoch != epoch) rx_graph_reset(ctx);
       if (!ctx->solve_exec) {
@@ -1069,7 +1094,7 @@ int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   int it = 0;
   double resid = 0.0;
   if ((rc = rx_la_fgmres_result(ctx, &it, &resid))) return rc;
-  if (lin_iters) *lin_iters = it;
+  if (lin_iters) *lin_iters = ctx->solve_iters >= 0 ? ctx->solve_iters : it;
   return RX_OK;
 }
 }  // namespace

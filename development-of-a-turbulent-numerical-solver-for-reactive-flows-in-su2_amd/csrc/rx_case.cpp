@@ -159,6 +159,8 @@ void rx_cfg_default(rx_cfg* c) {
   c->oxidizer_index = 2;
   c->ignition_iter = 999999;
   c->ignition_temp = 1700.0;
+  c->lin_solver = RX_LIN_FGMRES;
+  c->lin_restart = 10;
 }
 
 const char* rx_case_error(void) { return g_err.c_str(); }
@@ -193,8 +195,6 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
         // built: rx_grad_lsq / rx_grad_gg (SetPrimitive_Gradient_LS / _GG, solver_direct_reactive.cpp:4717) and the
         // SST's SetSolution_Gradient_LS / _GG (solver_direct_turbulent.cpp:2944, 2963)
         {"NUM_METHOD_GRAD", "WEIGHTED_LEAST_SQUARES", "", "WEIGHTED_LEAST_SQUARES or GREEN_GAUSS"},
-        // :1047 (default FGMRES): CSysSolve::Solve's other Krylov methods (linear_solvers_structure.cpp:601-724)
-        {"LINEAR_SOLVER", "FGMRES", "FGMRES", "only FGMRES"},
         // :1160 (default NO_CONVECTIVE): the reactive driver exits for any upwind scheme but AUSM
         // (driver_structure.cpp:1517-1529)
         {"CONV_NUM_METHOD_FLOW", "", "AUSM", "the reactive solvers implement AUSM only"},
@@ -245,9 +245,25 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
   const std::string tf = upper(c.str("TIME_DISCRE_FLOW", "EULER_IMPLICIT"));
   if (tf != "EULER_IMPLICIT" && tf != "EULER_EXPLICIT" && tf != "RUNGE-KUTTA_EXPLICIT")
     return fail(k, RX_ERR_UNSUPPORTED, "TIME_DISCRE_FLOW= " + tf);
+  // :1050 (default LU_SGS), Linear_Solver_Prec_Map (option_structure.hpp:1312-1316); LINELET needs the line
+  // construction of BuildLineletPreconditioner (matrix_structure.cpp:1837), which is not built
   const std::string pk = upper(c.str("LINEAR_SOLVER_PREC", "LU_SGS"));
-  if (pk != "ILU" && pk != "ILU0" && pk != "LU_SGS") return fail(k, RX_ERR_UNSUPPORTED, "LINEAR_SOLVER_PREC= " + pk);
-  const int prec = pk == "LU_SGS" ? 0 : 1;
+  if (pk != "ILU" && pk != "ILU0" && pk != "LU_SGS" && pk != "JACOBI")
+    return fail(k, RX_ERR_UNSUPPORTED, "LINEAR_SOLVER_PREC= " + pk);
+  const int prec = pk == "LU_SGS" ? RX_PREC_LU_SGS : (pk == "JACOBI" ? RX_PREC_JACOBI : RX_PREC_ILU);
+  // :1047 (default FGMRES), Linear_Solver_Map (option_structure.hpp:1249-1260): the branches of CSysSolve::Solve
+  // (linear_solvers_structure.cpp:626-708); SMOOTHER_LINELET needs the linelets (see above), CONJUGATE_GRADIENT and
+  // the point-inversion methods are not solver kinds of Solve (it does nothing for them)
+  const std::string lk = upper(c.str("LINEAR_SOLVER", "FGMRES"));
+  static const std::pair<const char*, int> lin_map[] = {
+      {"FGMRES", RX_LIN_FGMRES}, {"BCGSTAB", RX_LIN_BCGSTAB}, {"RESTARTED_FGMRES", RX_LIN_RESTARTED_FGMRES},
+      {"SMOOTHER_LUSGS", RX_LIN_SMOOTHER_LUSGS}, {"SMOOTHER_JACOBI", RX_LIN_SMOOTHER_JACOBI},
+      {"SMOOTHER_ILU0", RX_LIN_SMOOTHER_ILU}};
+  int lin_solver = -1;
+  for (const auto& e : lin_map)
+    if (lk == e.first) lin_solver = e.second;
+  if (lin_solver < 0) return fail(k, RX_ERR_UNSUPPORTED, "LINEAR_SOLVER= " + lk);
+  const int32_t lin_restart = (int32_t)c.num("LINEAR_SOLVER_RESTART_FREQUENCY", 10);
   const std::string so = upper(c.str("SPATIAL_ORDER_FLOW", "2ND_ORDER"));
   const std::string sl = upper(c.str("SLOPE_LIMITER_FLOW", "VENKATAKRISHNAN"));
   if ((so != "1ST_ORDER" && so != "2ND_ORDER" && so != "2ND_ORDER_LIMITER") ||
@@ -265,6 +281,8 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
   F.lin_tol = c.num("LINEAR_SOLVER_ERROR", 1e-5);
   F.lin_iter = (int32_t)c.num("LINEAR_SOLVER_ITER", 10);
   F.lin_prec = prec;
+  F.lin_solver = lin_solver;
+  F.lin_restart = lin_restart;
   F.relaxation = c.num("RELAXATION_FACTOR_FLOW", 1.0);
   F.implicit = tf == "EULER_IMPLICIT";
   F.rans = upper(c.str("KIND_TURB_MODEL", "NONE")) == "SST";
@@ -303,6 +321,8 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
   S.lin_tol = F.lin_tol;
   S.lin_iter = F.lin_iter;
   S.lin_prec = prec;
+  S.lin_solver = lin_solver;  // the SST's ImplicitEuler_Iteration calls the same System.Solve with the same config
+  S.lin_restart = lin_restart;
   S.relaxation = c.num("RELAXATION_FACTOR_TURB", 1.0);
   S.cfl = c.num("CFL_REDUCTION_TURB", 1.0);
   S.grad_method = F.grad_method;

@@ -113,6 +113,7 @@ struct rx_ctx {
   int32_t* ring_xoff = nullptr;  // [nnzb] LDS row of x_col(k) for the blocks the sweeps read (L: fs ring, U: bs ring)
   double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)
   double* xstar = nullptr;      // [N][nVar] LU-SGS forward-sweep result (halo values)
+  double* jinv = nullptr;       // [Nd][nVar^2] invM of the JACOBI preconditioner / SMOOTHER_JACOBI
   long long* ilu_trace = nullptr;  // debug phase trace of the ILU factorisation (rx_debug_ilu_trace)
 
   // ---- mechanism
@@ -153,6 +154,7 @@ struct rx_ctx {
   double* kz = nullptr;      // [(m+1)][N*nVar]
   void* kstate = nullptr;    // device KState
   void* h_kstate = nullptr;  // pinned host mirror
+  int solve_iters = -1;      // iterations of the last host-driven solve (RESTARTED_FGMRES: the cycles' sum), else -1
   // captured implicit solve (system build + preconditioner build + FGMRES + update)
   hipGraphExec_t solve_exec = nullptr;
   // buffers a captured solve graph bakes in: bumped by rx_bc_set (bc arrays reallocated); a graph captured under
@@ -274,6 +276,20 @@ void rx_graph_reset(rx_ctx* ctx);
 int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero);  // x_zero: SOL is all +0.0
 int rx_la_fgmres_result(rx_ctx* ctx, int* iters, double* resid);
 int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid);
+// the other Krylov / smoother branches of CSysSolve::Solve (rx_krylov.hip); results via rx_la_fgmres_result
+int rx_la_bcgstab_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero);
+int rx_la_smoother_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero);
+int rx_la_restarted_fgmres(rx_ctx* ctx, double tol, int iter, int restart, bool x_zero, int* iters, double* resid);
+int rx_la_solve_enqueue(rx_ctx* ctx, bool x_zero);  // cfg.lin_solver's branch (host-synchronous for RESTARTED)
+bool rx_la_solve_capturable(const rx_ctx* ctx);     // the branch is a fixed kernel sequence (graph-capturable)
+// JACOBI preconditioner (rx_sweeps.hip): invM build, apply (+ halo exchange unless defer_exchange), smoother update
+int rx_la_jacobi_build(rx_ctx* ctx, const double* A);
+int rx_la_jacobi_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv);
+int rx_la_jacobi_smooth(rx_ctx* ctx, const double* r, double* x, const int* done);
+int rx_la_prec_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv);  // by rx_la_eff_prec
+// the preconditioner the solve applies: cfg.lin_prec for the Krylov solvers, the smoother's own for SMOOTHER_*
+int rx_la_eff_prec(const rx_ctx* ctx);
+int rx_la_prec_build(rx_ctx* ctx);  // the preconditioner build CSysSolve::Solve does before the solve
 void rx_la_krylov_free(rx_ctx* ctx);
 int rx_la_rms_enqueue(rx_ctx* ctx, const double* r);
 int rx_la_rms_read(rx_ctx* ctx, double* rms);

@@ -28,6 +28,7 @@
 // SendReceive_Solution :794).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -46,6 +47,8 @@ struct KState {
   double loc[4];                     // rank-local sums in landing-slot order
   int done, noreo, iters, diverged, conv;
   unsigned int ticket;          // arrival counter of the in-launch reductions
+  double bnorm;                 // |b| of the solve (RESTARTED_FGMRES's tolerance update reads it)
+  double bc_alpha, bc_omega, bc_rho[2];  // BCGSTAB scalars; rho of iteration i in bc_rho[i & 1]
   double H[(kMaxM + 1) * kMaxM];  // H[k][i] at k * kMaxM + i
   double g[kMaxM + 1], cs[kMaxM + 1], sn[kMaxM + 1], y[kMaxM];
 };
@@ -303,10 +306,12 @@ __global__ __launch_bounds__(kBlock) void k_fg_start_div(int64_t n, KState* __re
       s->resid = beta;
       s->beta = beta;
       s->norm0 = norm0;
+      s->bnorm = norm0;
     }
     return;
   }
   if (lead()) {
+    s->bnorm = norm0;
     s->g[0] = beta;
     s->norm0 = beta;
     s->beta = beta;
@@ -473,6 +478,8 @@ __global__ void k_fg_reset(KState* s, double tol) {
   s->iters = 0;
   s->diverged = 0;
   s->resid = 0.0;
+  s->bc_alpha = s->bc_omega = 1.0;  // BCGSTAB_LinSolver :509
+  s->bc_rho[0] = s->bc_rho[1] = 1.0;
 }
 
 // SolveReduced (:73-85) and x += sum_k y_k z_k (k ascending, element by element as the reference's
@@ -514,6 +521,147 @@ __global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, int64_t ld, KSt
   }
 }
 
+// ---- BCGSTAB_LinSolver (linear_solvers_structure.cpp:465-599) and the smoothers of Solve's non-Krylov branch
+// (:683-708; LU_SGS_Smoother / Jacobi_Smoother / ILU0_Smoother, matrix_structure.cpp:1711 / :1268 / :1517).
+// The same device-resident scheme as FGMRES: scalars in KState, updated by lead lanes in the reference's operation
+// order, every lane evaluating the decisions from the same inputs, inner products reduced inside the launch.
+
+// r = b - A x (x_zero: b - 0.0, the +0.0 product of A * 0 for a finite A; see k_fg_residual0) with |b|^2 ->
+// norm0_in and |r|^2 -> dot; BCGSTAB also copies r_0 = r and starts p = v = b (its CSysVector p(b), v(b), :486-499).
+template <int NV, bool XZ>
+__global__ __launch_bounds__(kBlock) void k_lin_resid(int Nd, const int32_t* __restrict__ rp,
+                                                      const int32_t* __restrict__ col, const double* __restrict__ A,
+                                                      const double* __restrict__ x, const double* __restrict__ b,
+                                                      double* __restrict__ r, double* __restrict__ r0,
+                                                      double* __restrict__ p, double* __restrict__ v,
+                                                      double* __restrict__ part, KState* __restrict__ s, bool dist) {
+  if (s->done) return;
+  const int64_t n = (int64_t)Nd * NV;
+  double acc[2] = {0.0, 0.0};
+  GRID_LOOP(q, n) {
+    const double bq = b[q];
+    acc[0] += bq * bq;
+    double ax = 0.0;
+    if constexpr (!XZ) ax = spmv_elem<NV>(q, rp, col, A, x);
+    const double y = bq - ax;
+    r[q] = y;
+    if (r0) r0[q] = y;
+    if (p) p[q] = bq;
+    if (v) v[q] = bq;
+    acc[1] += y * y;
+  }
+  const int sl[2] = {kNorm0In, kDot};
+  grid_reduce<2>(acc, part, s, sl, dist);
+}
+
+// the start test (:500-505 / :1302-1307): norm_r = |r|, norm0 = |b|; solved by the initial guess -> done, 0
+// iterations; else norm0 = norm_r (:513)
+__global__ void k_lin_start(KState* s) {
+  const double norm_r = sqrt(s->dot), norm0 = sqrt(s->norm0_in);
+  const double epsm = 2.220446049250313e-16;  // numeric_limits<su2double>::epsilon() (matrix_structure.hpp:49)
+  s->bnorm = norm0;
+  s->resid = norm_r;
+  s->iters = 0;
+  if ((norm_r < s->tol * norm0) || (norm_r < epsm)) {
+    s->done = 1;
+    return;
+  }
+  s->norm0 = norm_r;
+}
+
+// the convergence test closing iteration i (:575-576 / :1352-1353): break with i iterations, else i + 1
+__global__ void k_lin_check(KState* s, int i, int slot) {
+  if (s->done) return;
+  const double norm_r = sqrt(land(s)[slot]);
+  s->resid = norm_r;
+  if (norm_r < s->tol * s->norm0) {
+    s->done = 1;
+    s->iters = i;
+  } else {
+    s->iters = i + 1;
+  }
+}
+
+// rho_i = <r, r_0> -> dot (:533)
+__global__ __launch_bounds__(kBlock) void k_bc_rho(int64_t n, const double* __restrict__ r,
+                                                   const double* __restrict__ r0, double* __restrict__ part,
+                                                   KState* __restrict__ s, bool dist) {
+  if (s->done) return;
+  double acc[1] = {0.0};
+  GRID_LOOP_U(q0, n) {
+    double a[kU], c[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) {
+        a[u] = r[q0 + u * kGridS];
+        c[u] = r0[q0 + u * kGridS];
+      }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (q0 + u * kGridS < n) acc[0] += a[u] * c[u];
+  }
+  const int sl[1] = {kDot};
+  grid_reduce<1>(acc, part, s, sl, dist);
+}
+
+// beta = (rho_i / rho_{i-1}) (alpha / omega), p = beta p + (-beta omega) v, p += 1.0 r (:529-543)
+__global__ __launch_bounds__(kBlock) void k_bc_p(int64_t n, KState* __restrict__ s, int i,
+                                                 const double* __restrict__ r, const double* __restrict__ v,
+                                                 double* __restrict__ p) {
+  if (s->done) return;
+  const double rho = s->dot, rho_prime = s->bc_rho[(i + 1) & 1];
+  const double beta = (rho / rho_prime) * (s->bc_alpha / s->bc_omega);
+  const double beta_omega = -beta * s->bc_omega;
+  if (lead()) s->bc_rho[i & 1] = rho;
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q < n) {
+    const double t = beta * p[q] + beta_omega * v[q];
+    p[q] = t + 1.0 * r[q];
+  }
+}
+
+// alpha = rho_i / <r_0, v> (:552-553), s = 1.0 r + (-alpha) v (:557)
+__global__ __launch_bounds__(kBlock) void k_bc_s(int64_t n, KState* __restrict__ s, int i,
+                                                 const double* __restrict__ r, const double* __restrict__ v,
+                                                 double* __restrict__ sv) {
+  if (s->done) return;
+  const double alpha = s->bc_rho[i & 1] / s->dot;
+  if (lead()) s->bc_alpha = alpha;
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q < n) sv[q] = 1.0 * r[q] + (-alpha) * v[q];
+}
+
+// omega = <t, s> / <t, t> (:566), x += alpha phat, x += omega shat (:570), r = 1.0 s + (-omega) t (:571) and
+// |r|^2 -> dot2 (:575)
+__global__ __launch_bounds__(kBlock) void k_bc_x(int64_t n, KState* __restrict__ s, double* __restrict__ x,
+                                                 const double* __restrict__ ph, const double* __restrict__ sh,
+                                                 const double* __restrict__ sv, const double* __restrict__ t,
+                                                 double* __restrict__ r, double* __restrict__ part, bool dist) {
+  if (s->done) return;
+  const double omega = s->dot / s->dotn, alpha = s->bc_alpha;
+  double acc[1] = {0.0};
+  GRID_LOOP(q, n) {
+    double xq = x[q];
+    xq += alpha * ph[q];
+    xq += omega * sh[q];
+    x[q] = xq;
+    const double y = 1.0 * sv[q] + (-omega) * t[q];
+    r[q] = y;
+    acc[0] += y * y;
+  }
+  if (lead()) s->bc_omega = omega;
+  const int sl[1] = {kDot2};
+  grid_reduce<1>(acc, part, s, sl, dist);
+}
+
+// the LU_SGS / ILU0 smoothers' update x.Plus_AX(omega = 1.0, M^-1 r) (matrix_structure.cpp:1805 / :1642)
+__global__ __launch_bounds__(kBlock) void k_sm_add(int64_t n, const KState* __restrict__ s,
+                                                   const double* __restrict__ z, double* __restrict__ x) {
+  if (s->done) return;
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q < n) x[q] += 1.0 * z[q];
+}
+
 #define RX_NV_SWITCH(nv, CALL)                       \
   switch (nv) {                                      \
     case 2: { constexpr int NV_ = 2; CALL; } break;   \
@@ -529,6 +677,51 @@ __global__ __launch_bounds__(kBlock) void k_fg_finish(int64_t n, int64_t ld, KSt
 
 // device address of the landing slots (host-side pointer arithmetic on the device KState)
 double* land_host(KState* s) { return &s->norm0_in; }
+
+// distributed: the preconditioner's closing halo exchange (SendReceive_Solution, matrix_structure.cpp:1513 / :1707 /
+// :1264) is deferred and overlaps the SpMV rows that read no halo column (on comm_stream with RCCL)
+bool spmv_split(const rx_ctx* ctx) {
+  static const bool off = getenv("RX_NO_SPMV_SPLIT") != nullptr;
+  return ctx->distributed() && ctx->spmv_rows && !off;
+}
+
+// CSysSolve's `precond(in, z)` + `mat_vec(z, w)` pair: z = M^-1 in (halo exchanged), w = A z over the owned rows
+// (MatrixVectorProduct :997-1029). RxPhase records only outside a graph capture: an eager solve (RX_NO_GRAPH=1,
+// bench.py's kernel-timing pass) times the in-solve preconditioner applies and SpMVs themselves.
+int prec_spmv(rx_ctx* ctx, const double* in, double* z, double* w, KState* s) {
+  hipStream_t st = ctx->stream;
+  const double* A = ctx->f[RX_F_JAC];
+  const bool split = spmv_split(ctx);
+  ctx->defer_exchange = split;
+  int rc = rx_la_prec_apply(ctx, in, z, &s->done, &s->conv);
+  ctx->defer_exchange = false;
+  if (rc) return rc;
+  if (!split) {
+    RxPhase ph(ctx, RX_K_SPMV);
+    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_full<NV_><<<blocks(ctx->Nd * NV_), kBlock, 0, st>>>((int)ctx->Nd, ctx->rp,
+                                                                                          ctx->col, A, z, w, s)));
+    return RX_OK;
+  }
+  const bool overlap = ctx->comm_stream != nullptr && !ctx->has_hcomm;
+  if (overlap) {
+    RX_HIP(hipEventRecord(ctx->comm_fork, st));
+    RX_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->comm_fork, 0));
+    if ((rc = rx_la_exchange_on(ctx, z, ctx->nVar, ctx->comm_stream))) return rc;
+    RX_HIP(hipEventRecord(ctx->comm_join, ctx->comm_stream));
+  } else if ((rc = rx_la_exchange(ctx, z, ctx->nVar))) {
+    return rc;
+  }
+  const int ni = (int)ctx->n_spmv_int, nb_rows = (int)(ctx->Nd - ctx->n_spmv_int);
+  RxPhase ph(ctx, RX_K_SPMV);
+  if (ni > 0)
+    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)ni * NV_), kBlock, 0, st>>>(
+                                ni, ctx->spmv_rows, ctx->rp, ctx->col, A, z, w, s)));
+  if (overlap) RX_HIP(hipStreamWaitEvent(st, ctx->comm_join, 0));
+  if (nb_rows > 0)
+    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)nb_rows * NV_), kBlock, 0, st>>>(
+                                nb_rows, ctx->spmv_rows + ni, ctx->rp, ctx->col, A, z, w, s)));
+  return RX_OK;
+}
 
 }  // namespace
 
@@ -578,63 +771,16 @@ int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
   }
   if ((rc = reduce())) return rc;
   k_fg_start_div<<<nb, kBlock, 0, st>>>(n, s, W(0));
+  // the product on a full grid (the 512-block reduction grid left 2 waves per SIMD, 91 % parked),
+  // then the two inner products in the reduction's own order; RX_FG_FUSED_SPMV=1: one launch on the reduction grid
+  static const bool fused_spmv = getenv("RX_FG_FUSED_SPMV") != nullptr;
   for (int i = 0; i < m; ++i) {
-    // RxPhase records only outside a graph capture: an eager solve (RX_NO_GRAPH=1, bench.py's kernel-timing pass)
-    // times the in-solve ILU applies and SpMVs themselves
-    // distributed: the preconditioner's closing halo exchange of z_i (SendReceive_Solution, matrix_structure.cpp:
-    // 1513 / :1707) overlaps the SpMV rows that read no halo column (on comm_stream with RCCL)
-    const bool split = dist && ctx->spmv_rows && !getenv("RX_NO_SPMV_SPLIT");
-    ctx->defer_exchange = split;
-    if (ctx->cfg.lin_prec == 1) {
-      RxPhase ph(ctx, RX_K_ILU_APPLY);
-      rc = rx_la_ilu_apply(ctx, W(i), Z(i), &s->done, &s->conv);
-    } else {
-      rc = rx_la_lusgs(ctx, A, W(i), Z(i), &s->done, &s->conv);
-    }
-    ctx->defer_exchange = false;
-    if (rc) return rc;
-    if (split) {
-      const bool overlap = ctx->comm_stream != nullptr && !ctx->has_hcomm;
-      if (overlap) {
-        RX_HIP(hipEventRecord(ctx->comm_fork, st));
-        RX_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->comm_fork, 0));
-        if ((rc = rx_la_exchange_on(ctx, Z(i), ctx->nVar, ctx->comm_stream))) return rc;
-        RX_HIP(hipEventRecord(ctx->comm_join, ctx->comm_stream));
-      } else if ((rc = rx_la_exchange(ctx, Z(i), ctx->nVar))) {
-        return rc;
-      }
-      const int ni = (int)ctx->n_spmv_int, nb_rows = (int)(ctx->Nd - ctx->n_spmv_int);
-      {
-        RxPhase ph(ctx, RX_K_SPMV);
-        if (ni > 0)
-          RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)ni * NV_), kBlock, 0, st>>>(
-                                      ni, ctx->spmv_rows, ctx->rp, ctx->col, A, Z(i), W(i + 1), s)));
-        if (overlap) RX_HIP(hipStreamWaitEvent(st, ctx->comm_join, 0));
-        if (nb_rows > 0)
-          RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)nb_rows * NV_), kBlock, 0, st>>>(
-                                      nb_rows, ctx->spmv_rows + ni, ctx->rp, ctx->col, A, Z(i), W(i + 1), s)));
-      }
-      k_fg_spmv_dots<<<kRedBlocks, kBlock, 0, st>>>(n, W(0), W(i + 1), part, s, dist);
-      if ((rc = reduce())) return rc;
-      for (int k = 0; k <= i; ++k) {
-        k_fg_proj<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, k, i, ctx->kw, part, dist);
-        if ((rc = reduce())) return rc;
-        k_fg_reo<<<kRedBlocks, kBlock, 0, st>>>(n, ld, s, k, i, ctx->kw, part, dist);
-        if ((rc = reduce())) return rc;
-      }
-      k_fg_close_div<<<kRedBlocks, kBlock, 0, st>>>(n, s, i, W(i + 1));
-      continue;
-    }
-    // the product on a full grid (the 512-block reduction grid left 2 waves per SIMD, 91 % parked),
-    // then the two inner products in the reduction's own order
-    static const bool fused_spmv = getenv("RX_FG_FUSED_SPMV") != nullptr;
-    if (fused_spmv) {
+    if (fused_spmv && !spmv_split(ctx)) {
+      if ((rc = rx_la_prec_apply(ctx, W(i), Z(i), &s->done, &s->conv))) return rc;
       RX_NV_SWITCH(ctx->nVar, (k_fg_spmv<NV_><<<kRedBlocks, kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A, Z(i),
                                                                              W(0), W(i + 1), part, s, dist)));
     } else {
-      RxPhase ph(ctx, RX_K_SPMV);
-      RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_full<NV_><<<blocks(n), kBlock, 0, st>>>((int)ctx->Nd, ctx->rp, ctx->col, A,
-                                                                                 Z(i), W(i + 1), s)));
+      if ((rc = prec_spmv(ctx, W(i), Z(i), W(i + 1), s))) return rc;
       k_fg_spmv_dots<<<kRedBlocks, kBlock, 0, st>>>(n, W(0), W(i + 1), part, s, dist);
     }
     if ((rc = reduce())) return rc;
@@ -666,6 +812,160 @@ int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid) {
   int rc = rx_la_fgmres_enqueue(ctx, tol, m, false);
   if (rc) return rc;
   return rx_la_fgmres_result(ctx, iters, resid);
+}
+
+namespace {
+// r = b - A x (+ the BCGSTAB copies) and the start test; x's halo is the caller's (x_zero: not read)
+int lin_start(rx_ctx* ctx, double tol, bool x_zero, double* r, double* r0, double* p, double* v) {
+  KState* s = static_cast<KState*>(ctx->kstate);
+  hipStream_t st = ctx->stream;
+  const bool dist = ctx->distributed();
+  const double* A = ctx->f[RX_F_JAC];
+  k_fg_reset<<<1, 64, 0, st>>>(s, tol);
+  if (x_zero) {
+    RX_NV_SWITCH(ctx->nVar, (k_lin_resid<NV_, true><<<kRedBlocks, kBlock, 0, st>>>(
+                                (int)ctx->Nd, ctx->rp, ctx->col, A, ctx->f[RX_F_SOL], ctx->f[RX_F_RHS], r, r0, p, v,
+                                ctx->red, s, dist)));
+  } else {
+    RX_NV_SWITCH(ctx->nVar, (k_lin_resid<NV_, false><<<kRedBlocks, kBlock, 0, st>>>(
+                                (int)ctx->Nd, ctx->rp, ctx->col, A, ctx->f[RX_F_SOL], ctx->f[RX_F_RHS], r, r0, p, v,
+                                ctx->red, s, dist)));
+  }
+  int rc = dist ? rx_la_allreduce(ctx, s->loc, land_host(s), 4) : RX_OK;
+  if (rc) return rc;
+  k_lin_start<<<1, 1, 0, st>>>(s);
+  return RX_OK;
+}
+}  // namespace
+
+// BCGSTAB_LinSolver (linear_solvers_structure.cpp:465-599) on JAC * SOL = RHS with the configured preconditioner,
+// m iterations at most, no host synchronisation. Vectors: r, r_0, v, t in kw[0..3], p, s, phat, shat in kz[0..3].
+int rx_la_bcgstab_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
+  if (m < 1) return RX_ERR_ARG;  // :475-484
+  int rc = rx_la_krylov_alloc(ctx, std::max(3, std::min(ctx->krylov_m, kMaxM)));
+  if (rc) return rc;
+  const int64_t ld = ctx->N * ctx->nVar, n = ctx->Nd * ctx->nVar;
+  const int nb = blocks(n);
+  const bool dist = ctx->distributed();
+  hipStream_t st = ctx->stream;
+  KState* s = static_cast<KState*>(ctx->kstate);
+  double* part = ctx->red;
+  double *r = ctx->kw, *r0 = ctx->kw + ld, *v = ctx->kw + 2 * ld, *t = ctx->kw + 3 * ld;
+  double *p = ctx->kz, *sv = ctx->kz + ld, *ph = ctx->kz + 2 * ld, *sh = ctx->kz + 3 * ld;
+  double* x = ctx->f[RX_F_SOL];
+  auto reduce = [&]() { return dist ? rx_la_allreduce(ctx, s->loc, land_host(s), 4) : RX_OK; };
+  if ((rc = lin_start(ctx, tol, x_zero, r, r0, p, v))) return rc;
+  for (int i = 0; i < m; ++i) {
+    k_bc_rho<<<kRedBlocks, kBlock, 0, st>>>(n, r, r0, part, s, dist);
+    if ((rc = reduce())) return rc;
+    k_bc_p<<<nb, kBlock, 0, st>>>(n, s, i, r, v, p);
+    if ((rc = prec_spmv(ctx, p, ph, v, s))) return rc;  // precond(p, phat); mat_vec(phat, v) (:547-548)
+    k_fg_spmv_dots<<<kRedBlocks, kBlock, 0, st>>>(n, r0, v, part, s, dist);  // <r_0, v> -> dot
+    if ((rc = reduce())) return rc;
+    k_bc_s<<<nb, kBlock, 0, st>>>(n, s, i, r, v, sv);
+    if ((rc = prec_spmv(ctx, sv, sh, t, s))) return rc;  // precond(s, shat); mat_vec(shat, t) (:561-562)
+    k_fg_spmv_dots<<<kRedBlocks, kBlock, 0, st>>>(n, sv, t, part, s, dist);  // <t, t> -> dotn, <t, s> -> dot
+    if ((rc = reduce())) return rc;
+    k_bc_x<<<kRedBlocks, kBlock, 0, st>>>(n, s, x, ph, sh, sv, t, r, part, dist);
+    if ((rc = reduce())) return rc;
+    k_lin_check<<<1, 1, 0, st>>>(s, i, kDot2);
+  }
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+// The smoothers of Solve's non-Krylov branch (:683-701), m smoothing iterations at most: x += M^-1 r (LU_SGS /
+// ILU0: the preconditioner sweeps of ComputeLU_SGSPreconditioner / ComputeILUPreconditioner, whose arithmetic the
+// smoothers repeat; JACOBI: accumulated into x itself, k_jacobi_smooth), x's halo exchanged (:1809 / :1646 / :1341),
+// r = b - A x, |r| against tol * |r_0|. r in kw[0], M^-1 r in kz[0].
+int rx_la_smoother_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
+  if (m < 1) return RX_ERR_ARG;  // :1279 / :1531 / :1723
+  int rc = rx_la_krylov_alloc(ctx, std::max(1, std::min(ctx->krylov_m, kMaxM)));
+  if (rc) return rc;
+  const int64_t n = ctx->Nd * ctx->nVar;
+  const int nb = blocks(n);
+  const bool dist = ctx->distributed();
+  hipStream_t st = ctx->stream;
+  KState* s = static_cast<KState*>(ctx->kstate);
+  double *r = ctx->kw, *z = ctx->kz;
+  double* x = ctx->f[RX_F_SOL];
+  const double* A = ctx->f[RX_F_JAC];
+  const bool jacobi = rx_la_eff_prec(ctx) == RX_PREC_JACOBI;
+  if ((rc = lin_start(ctx, tol, x_zero, r, nullptr, nullptr, nullptr))) return rc;
+  for (int i = 0; i < m; ++i) {
+    if (jacobi) {
+      if ((rc = rx_la_jacobi_smooth(ctx, r, x, &s->done))) return rc;
+    } else {
+      ctx->defer_exchange = true;  // M^-1 r's halo is never read: x's is exchanged below
+      rc = rx_la_prec_apply(ctx, r, z, &s->done, nullptr);
+      ctx->defer_exchange = false;
+      if (rc) return rc;
+      k_sm_add<<<nb, kBlock, 0, st>>>(n, s, z, x);
+    }
+    if ((rc = rx_la_exchange(ctx, x, ctx->nVar))) return rc;
+    RX_NV_SWITCH(ctx->nVar, (k_lin_resid<NV_, false><<<kRedBlocks, kBlock, 0, st>>>(
+                                (int)ctx->Nd, ctx->rp, ctx->col, A, x, ctx->f[RX_F_RHS], r, nullptr, nullptr, nullptr,
+                                ctx->red, s, dist)));
+    if (dist && (rc = rx_la_allreduce(ctx, s->loc, land_host(s), 4))) return rc;
+    k_lin_check<<<1, 1, 0, st>>>(s, i, kDot);
+  }
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+// RESTARTED_FGMRES (Solve :662-671): FGMRES cycles of `iter` iterations (the remainder once fewer than `restart`
+// are left) from the previous cycle's x, the tolerance scaled by 1 / |b| after each cycle, until `iter` iterations
+// are spent or |b| < tol. Each cycle's iteration count decides the next, so the cycles synchronise with the host.
+// The reference's loop does not end if a cycle keeps returning 0 iterations with |b| >= tol (its start test meets
+// |r| < eps); this one stops after kMaxCycles and reports RX_ERR_DIVERGED.
+int rx_la_restarted_fgmres(rx_ctx* ctx, double tol, int iter, int restart, bool x_zero, int* iters, double* resid) {
+  constexpr int kMaxCycles = 4096;
+  if (iter < 1 || iter > kMaxM) return RX_ERR_ARG;
+  int total = 0, max_iter = iter, rc;
+  double stol = tol, res = 0.0;
+  for (int cycle = 0; total < iter; ++cycle) {
+    if (cycle == kMaxCycles) return RX_ERR_DIVERGED;
+    if ((int64_t)total + restart > iter) max_iter = iter - total;
+    if ((rc = rx_la_fgmres_enqueue(ctx, stol, max_iter, x_zero && cycle == 0))) return rc;
+    int it = 0;
+    if ((rc = rx_la_fgmres_result(ctx, &it, &res))) return rc;
+    total += it;
+    // FGMRES updates x over every element, its halo from the exchanged z (:455-457): the next cycle's A x reads it
+    if (ctx->distributed() && (rc = rx_la_exchange(ctx, ctx->f[RX_F_SOL], ctx->nVar))) return rc;
+    const double bn = static_cast<KState*>(ctx->h_kstate)->bnorm;
+    if (bn < stol) break;
+    stol = stol * (1.0 / bn);
+  }
+  if (iters) *iters = total;
+  if (resid) *resid = res;
+  return RX_OK;
+}
+
+bool rx_la_solve_capturable(const rx_ctx* ctx) { return ctx->cfg.lin_solver != RX_LIN_RESTARTED_FGMRES; }
+
+// CSysSolve::Solve's branch for cfg.lin_solver (the preconditioner is built before, rx_la_prec_build)
+int rx_la_solve_enqueue(rx_ctx* ctx, bool x_zero) {
+  const rx_cfg& c = ctx->cfg;
+  ctx->solve_iters = -1;
+  switch (c.lin_solver) {
+    case RX_LIN_FGMRES:
+      return rx_la_fgmres_enqueue(ctx, c.lin_tol, c.lin_iter, x_zero);
+    case RX_LIN_BCGSTAB:
+      return rx_la_bcgstab_enqueue(ctx, c.lin_tol, c.lin_iter, x_zero);
+    case RX_LIN_RESTARTED_FGMRES: {
+      int it = 0;
+      double res = 0.0;
+      const int rc = rx_la_restarted_fgmres(ctx, c.lin_tol, c.lin_iter, c.lin_restart, x_zero, &it, &res);
+      ctx->solve_iters = it;
+      return rc;
+    }
+    case RX_LIN_SMOOTHER_LUSGS:
+    case RX_LIN_SMOOTHER_JACOBI:
+    case RX_LIN_SMOOTHER_ILU:
+      return rx_la_smoother_enqueue(ctx, c.lin_tol, c.lin_iter, x_zero);
+    default:
+      return RX_ERR_ARG;
+  }
 }
 
 void rx_la_krylov_free(rx_ctx* ctx) {

@@ -2555,6 +2555,129 @@ int rx_la_lusgs(rx_ctx* ctx, const double* A, const double* b, double* x, int* d
   return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, ctx->nVar);  // :1707
 }
 
+namespace {
+// BuildJacobiPreconditioner (matrix_structure.cpp:1230-1246): invM_i = InverseDiagonalBlock (:1129-1143), column c
+// the Gauss_Elimination (:594-643) of the unit vector e_c. One wavefront per row: the block is factorised with
+// lane r holding row r (wave_factor_rows, the reference's elimination order), then lane c < NV solves e_c with the
+// stored multipliers and U (wave_solve_rows, the reference's rhs order) and writes column c of the inverse.
+template <int NV>
+__global__ __launch_bounds__(256) void k_jacobi_build(int N, const int64_t* __restrict__ diag,
+                                                      const double* __restrict__ A, double* __restrict__ inv) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= N) return;
+  const double* D = A + diag[i] * (NV * NV);
+  double row[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) row[k] = lane < NV ? D[lane * NV + k] : 1.0;
+  wave_factor_rows<NV>(row, lane);
+  double rhs[NV];
+#pragma unroll
+  for (int r = 0; r < NV; ++r) rhs[r] = (r == lane) ? 1.0 : 0.0;
+  wave_solve_rows<NV>(row, rhs);
+  if (lane < NV) {
+#pragma unroll
+    for (int r = 0; r < NV; ++r) inv[(size_t)i * NV * NV + r * NV + lane] = rhs[r];
+  }
+}
+
+// ComputeJacobiPreconditioner (:1249-1266): prod_ia = 0.0 + sum_c invM_i[a][c] vec_ic (c ascending), owned rows.
+// One thread per element; the rows of invM are read whole (NV consecutive doubles).
+template <int NV>
+__global__ __launch_bounds__(256) void k_jacobi_apply(int N, const double* __restrict__ inv,
+                                                      const double* __restrict__ b, double* __restrict__ x,
+                                                      int* __restrict__ done, const int* __restrict__ conv) {
+  if (skip_sweep(done, conv)) return;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (int64_t)N * NV) return;
+  const int64_t i = q / NV;
+  const double* m = inv + (size_t)q * NV;  // row a of block i: (i * NV + a) * NV
+  const double* v = b + i * NV;
+  double acc = 0.0;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) acc += m[c] * v[c];
+  x[q] = acc;
+}
+
+// Jacobi_Smoother's update (:1331-1337): x_ia += invM_i[a][c] r_ic, accumulated into x itself (c ascending).
+template <int NV>
+__global__ __launch_bounds__(256) void k_jacobi_smooth(int N, const double* __restrict__ inv,
+                                                       const double* __restrict__ r, double* __restrict__ x,
+                                                       const int* __restrict__ done) {
+  if (*done) return;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (int64_t)N * NV) return;
+  const int64_t i = q / NV;
+  const double* m = inv + (size_t)q * NV;
+  const double* v = r + i * NV;
+  double acc = x[q];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) acc += m[c] * v[c];
+  x[q] = acc;
+}
+}  // namespace
+
+int rx_la_jacobi_build(rx_ctx* ctx, const double* A) {
+  if (!ctx->jinv) return RX_ERR_STATE;  // allocated with the JACOBI preconditioner / SMOOTHER_JACOBI
+  RX_NV_SWITCH(ctx->nVar, (k_jacobi_build<NV_><<<(int)((ctx->Nd + 3) / 4), 256, 0, ctx->stream>>>(
+                              (int)ctx->Nd, ctx->diag, A, ctx->jinv)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+int rx_la_jacobi_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv) {
+  if (!ctx->jinv) return RX_ERR_STATE;
+  const int64_t n = ctx->Nd * ctx->nVar;
+  RX_NV_SWITCH(ctx->nVar, (k_jacobi_apply<NV_><<<(int)((n + 255) / 256), 256, 0, ctx->stream>>>(
+                              (int)ctx->Nd, ctx->jinv, b, x, done, conv)));
+  RX_HIP(hipGetLastError());
+  return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, ctx->nVar);  // :1264
+}
+
+int rx_la_jacobi_smooth(rx_ctx* ctx, const double* r, double* x, const int* done) {
+  if (!ctx->jinv) return RX_ERR_STATE;
+  const int64_t n = ctx->Nd * ctx->nVar;
+  RX_NV_SWITCH(ctx->nVar, (k_jacobi_smooth<NV_><<<(int)((n + 255) / 256), 256, 0, ctx->stream>>>(
+                              (int)ctx->Nd, ctx->jinv, r, x, done)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+
+// The preconditioner of CSysSolve::Solve (linear_solvers_structure.cpp:633-653) applied to b -> x, with x's halo
+// exchanged unless ctx->defer_exchange.
+int rx_la_eff_prec(const rx_ctx* ctx) {
+  switch (ctx->cfg.lin_solver) {
+    case RX_LIN_SMOOTHER_LUSGS: return RX_PREC_LU_SGS;
+    case RX_LIN_SMOOTHER_JACOBI: return RX_PREC_JACOBI;
+    case RX_LIN_SMOOTHER_ILU: return RX_PREC_ILU;
+    default: return ctx->cfg.lin_prec;
+  }
+}
+
+int rx_la_prec_build(rx_ctx* ctx) {
+  switch (rx_la_eff_prec(ctx)) {
+    case RX_PREC_ILU: return rx_la_ilu_build(ctx);  // BuildILUPreconditioner (:1368)
+    case RX_PREC_LU_SGS: return rx_la_diag_factor(ctx, ctx->f[RX_F_JAC]);  // Gauss_Elimination's factor, once
+    case RX_PREC_JACOBI: return rx_la_jacobi_build(ctx, ctx->f[RX_F_JAC]);  // BuildJacobiPreconditioner (:1230)
+    default: return RX_ERR_ARG;
+  }
+}
+
+int rx_la_prec_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv) {
+  switch (rx_la_eff_prec(ctx)) {
+    case RX_PREC_ILU: {
+      RxPhase ph(ctx, RX_K_ILU_APPLY);
+      return rx_la_ilu_apply(ctx, b, x, done, conv);
+    }
+    case RX_PREC_LU_SGS:
+      return rx_la_lusgs(ctx, ctx->f[RX_F_JAC], b, x, done, conv);
+    case RX_PREC_JACOBI:
+      return rx_la_jacobi_apply(ctx, b, x, done, conv);
+    default:
+      return RX_ERR_ARG;
+  }
+}
+
 // Debug: trace the phases of the ILU(0) factorisation of partition 0 (see tools/ilu_trace.py).
 extern "C" int rx_debug_ilu_trace(rx_ctx* ctx, long long* host, int64_t n) {
   const int64_t need = std::max<int64_t>(1 + 16 * 5 * 64, 1 + kGrpTraceGroups * kGrpTraceRows * 8 + kGrpTraceLevels);

@@ -21,6 +21,9 @@
  *   rx_ilu0_apply        CSysMatrix::ComputeILUPreconditioner matrix_structure.cpp:1453-1515
  *   rx_lusgs_apply       CSysMatrix::ComputeLU_SGSPreconditioner matrix_structure.cpp:1673-1709
  *   rx_fgmres            CSysSolve::FGMRES_LinSolver Common/src/linear_solvers_structure.cpp:309-463
+ *   rx_linear_solve      CSysSolve::Solve linear_solvers_structure.cpp:601-708 (FGMRES, BCGSTAB :465-599,
+ *                        RESTARTED_FGMRES; JACOBI / ILU0 / LU_SGS preconditioners; the LU_SGS / Jacobi / ILU0
+ *                        smoothers matrix_structure.cpp:1268-1835)
  *   rx_implicit_euler    CReactiveEulerSolver::ImplicitEuler_Iteration solver_direct_reactive.cpp:2336-2407
  *   rx_explicit_euler    CReactiveEulerSolver::ExplicitEuler_Iteration solver_direct_reactive.cpp:2414-2449
  *   rx_explicit_rk       CReactiveEulerSolver::ExplicitRK_Iteration solver_direct_reactive.cpp:2456-2493
@@ -120,7 +123,7 @@ typedef struct {
   double cfl, max_delta_time;                    /* SetTime_Step */
   double ref_elem_length, limiter_coeff;         /* Venkatakrishnan */
   double lin_tol, relaxation;                    /* LINEAR_SOLVER_ERROR, RELAXATION_FACTOR_FLOW */
-  int32_t implicit, rans, lin_iter, lin_prec;    /* lin_prec: 0 = LU_SGS, 1 = ILU0 */
+  int32_t implicit, rans, lin_iter, lin_prec;    /* lin_prec: rx_lin_prec (0 = LU_SGS, 1 = ILU0, 2 = JACOBI) */
   int32_t spatial_order;  /* SPATIAL_ORDER_FLOW: 0 = 1ST_ORDER, 1 = 2ND_ORDER (MUSCL), 2 = 2ND_ORDER_LIMITER
                              (MUSCL with RX_F_LIMITER), Upwind_Residual :2554-2729 */
   int32_t clip_temp;      /* CLIPPING_TEMPRATURE (Cons2PrimVar :711-712) */
@@ -139,9 +142,23 @@ typedef struct {
    * rx_grad_gg by it (solver_direct_reactive.cpp:4717); the SST context's Preprocessing / Postprocessing gradient of
    * (k, omega) follows its own rx_cfg (solver_direct_turbulent.cpp:2944, 2963). */
   int32_t grad_method;
+  /* LINEAR_SOLVER (config_structure.cpp:1047, default FGMRES): rx_lin_solver, the Krylov branch of CSysSolve::Solve
+   * (linear_solvers_structure.cpp:655-672). LINEAR_SOLVER_RESTART_FREQUENCY (:1056, default 10): RESTARTED_FGMRES's
+   * lin_restart. The subspace size / iteration cap is lin_iter (LINEAR_SOLVER_ITER) for every solver. rx_cfg_default:
+   * FGMRES, 10. */
+  int32_t lin_solver, lin_restart;
 } rx_cfg;
 
 typedef enum { RX_GRAD_WEIGHTED_LEAST_SQUARES = 0, RX_GRAD_GREEN_GAUSS = 1 } rx_grad_method;
+
+typedef enum { RX_PREC_LU_SGS = 0, RX_PREC_ILU = 1, RX_PREC_JACOBI = 2 } rx_lin_prec;
+
+/* the SMOOTHER_* kinds are Solve's non-Krylov branch (:683-708): LU_SGS_Smoother / Jacobi_Smoother / ILU0_Smoother
+ * (matrix_structure.cpp:1711 / :1268 / :1517) with lin_iter smoothing iterations; lin_prec is not read for them */
+typedef enum {
+  RX_LIN_FGMRES = 0, RX_LIN_BCGSTAB = 1, RX_LIN_RESTARTED_FGMRES = 2,
+  RX_LIN_SMOOTHER_LUSGS = 3, RX_LIN_SMOOTHER_JACOBI = 4, RX_LIN_SMOOTHER_ILU = 5
+} rx_lin_solver;
 
 typedef enum { RX_LIMITER_VENKATAKRISHNAN = 0, RX_LIMITER_BARTH_JESPERSEN = 1 } rx_slope_limiter;
 
@@ -198,6 +215,9 @@ int rx_ilu0_build(rx_ctx *ctx);
 int rx_ilu0_apply(rx_ctx *ctx, rx_field b, rx_field x);
 int rx_lusgs_apply(rx_ctx *ctx, rx_field b, rx_field x);
 int rx_fgmres(rx_ctx *ctx, double tol, int m, int *iters, double *resid); /* solves JAC * SOL = RHS */
+/* CSysSolve::Solve (linear_solvers_structure.cpp:601-708): the configured preconditioner build and linear solver
+ * (rx_cfg lin_solver / lin_prec / lin_tol / lin_iter / lin_restart) on JAC * SOL = RHS from SOL's current values */
+int rx_linear_solve(rx_ctx *ctx, int *iters, double *resid);
 
 /* Multi-GPU (RCCL over xGMI). rx_comm_unique_id on one rank, broadcast the 128 bytes, then
  * rx_comm_init on every rank. With a communicator the context exchanges halo values where the

@@ -571,8 +571,13 @@ ITER_KEEP = ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr", "bvert
              "p2v_params", "bsr_row_ptr", "bsr_col", "global_index")
 
 
-def iteration_case(name, writer, U, ns, n_iters, cfl, prec, time_flow, extra="", order="1ST_ORDER"):
+def iteration_case(name, writer, U, ns, n_iters, cfl, prec, time_flow, extra="", order="1ST_ORDER", cfg_edit=None):
     wd = make_workdir(name, writer, cfl=cfl, order=order, prec=prec, time_flow=time_flow, ns=ns, extra=extra)
+    if cfg_edit:
+        path = os.path.join(wd, "case.cfg")
+        text = open(path).read()
+        with open(path, "w") as f:
+            f.write(cfg_edit(text))
     write_state(wd, U)
     a = run_harness(wd, bsr=False, extra=["--iters", str(n_iters)])
     out = {k: a[k] for k in a if k in ITER_KEEP or k.startswith("it") or k == "limiter_params"}
@@ -680,6 +685,34 @@ def case_it4t(limiter=False):
                          order="2ND_ORDER_LIMITER" if limiter else "1ST_ORDER")
     out["spatial_order"] = np.array(2 if limiter else 0)
     out["sst_spatial_order"] = np.array(2 if limiter else 1)
+    return out
+
+
+# CSysSolve::Solve's branches (linear_solvers_structure.cpp:626-708) beside the default FGMRES: (LINEAR_SOLVER,
+# LINEAR_SOLVER_PREC, LINEAR_SOLVER_RESTART_FREQUENCY) of each golden
+LIN_CASES = {"lsbc": ("BCGSTAB", "ILU0", 10), "lsbj": ("BCGSTAB", "JACOBI", 10), "lsfj": ("FGMRES", "JACOBI", 10),
+             "lsrs": ("RESTARTED_FGMRES", "LU_SGS", 2), "lssl": ("SMOOTHER_LUSGS", "LU_SGS", 10),
+             "lssj": ("SMOOTHER_JACOBI", "LU_SGS", 10), "lssi": ("SMOOTHER_ILU0", "LU_SGS", 10)}
+
+
+def lin_edit(t, solver):
+    t = t.replace("LINEAR_SOLVER= FGMRES", "LINEAR_SOLVER= " + solver)
+    if solver == "RESTARTED_FGMRES":  # cycles that stop early (tolerance met), so the restart loop runs several
+        t = t.replace("LINEAR_SOLVER_ERROR= 1E-6", "LINEAR_SOLVER_ERROR= 0.05")
+    return t
+
+
+def case_lin(name):
+    """The mini9 jet with the 4-species mechanism (as it4t) through one of CSysSolve::Solve's other branches
+    (LIN_CASES: BCGSTAB_LinSolver, the JACOBI preconditioner, RESTARTED_FGMRES, the LU_SGS / Jacobi / ILU0 smoothers)
+    for the flow and the SST solve: implicit at CFL 1, LINEAR_SOLVER_ITER 5, two reference outer iterations."""
+    solver, prec, restart = LIN_CASES[name]
+    pts, quads, U, writer = mini9_inputs()
+    out = iteration_case(name, writer, fold_species(U, 4), 4, 2, 1.0, prec, "EULER_IMPLICIT",
+                         extra=f"LINEAR_SOLVER_RESTART_FREQUENCY= {restart}\n",
+                         cfg_edit=lambda t: lin_edit(t, solver))
+    out["lin_solver"] = np.array(solver)
+    out["lin_restart"] = np.array(restart)
     return out
 
 
@@ -881,7 +914,8 @@ def main():
              "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
              "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d, "fpit2": case_fpit2,
              "fpit2l": lambda: case_fpit2(limiter=True), "it4t": case_it4t,
-             "it4tl": lambda: case_it4t(limiter=True)}[case]()
+             "it4tl": lambda: case_it4t(limiter=True),
+             **{k: (lambda k=k: case_lin(k)) for k in LIN_CASES}}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

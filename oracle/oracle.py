@@ -37,6 +37,9 @@ def lib():
         _lib.orc_visc_edges.restype = C.c_int
         _lib.orc_fgmres.restype = C.c_int
         _lib.orc_fgmres_p.restype = C.c_int
+        _lib.orc_bcgstab_p.restype = C.c_int
+        _lib.orc_restarted_fgmres_p.restype = C.c_int
+        _lib.orc_smoother_p.restype = C.c_int
         _lib.orc_dot.restype = C.c_double
         _lib.orc_muscl_edges.restype = C.c_int
         _lib.orc_set_primitive.restype = C.c_int
@@ -291,16 +294,84 @@ def ilu_apply(rp, col, F, b, part_ptr=None):
     return x.reshape(N, nb)
 
 
+PREC = {"lusgs": 0, "ilu": 1, "jacobi": 2}  # LINEAR_SOLVER_PREC LU_SGS / ILU0 / JACOBI
+
+
 @_keepalive
 def fgmres(rp, col, A, b, prec="lusgs", F=None, tol=1e-6, m=5, x0=None, part_ptr=None):
     N, nb = len(rp) - 1, A.shape[1]
     x = np.zeros(N * nb) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).ravel().copy()
     resid = C.c_double(0.0)
     it = lib().orc_fgmres_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
-                            _p(F) if F is not None else None, C.c_int(0 if prec == "lusgs" else 1), _p(b),
+                            _p(F) if F is not None else None, C.c_int(PREC[prec]), _p(b),
                             x.ctypes.data_as(C.c_void_p), C.c_double(tol), C.c_int(m), C.byref(resid),
                             *_parts(N, part_ptr))
     return x.reshape(N, nb), it, resid.value
+
+
+@_keepalive
+def bcgstab(rp, col, A, b, prec="lusgs", F=None, tol=1e-6, m=5, x0=None, part_ptr=None):
+    """BCGSTAB_LinSolver (linear_solvers_structure.cpp:465-599) -> (x, iterations, |r|)."""
+    N, nb = len(rp) - 1, A.shape[1]
+    x = np.zeros(N * nb) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).ravel().copy()
+    resid = C.c_double(0.0)
+    it = lib().orc_bcgstab_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
+                             _p(F) if F is not None else None, C.c_int(PREC[prec]), _p(b),
+                             x.ctypes.data_as(C.c_void_p), C.c_double(tol), C.c_int(m), C.byref(resid),
+                             *_parts(N, part_ptr))
+    return x.reshape(N, nb), it, resid.value
+
+
+@_keepalive
+def restarted_fgmres(rp, col, A, b, prec="lusgs", F=None, tol=1e-6, iters=10, restart=10, x0=None, part_ptr=None):
+    """RESTARTED_FGMRES (CSysSolve::Solve :662-671) -> (x, summed iterations, last cycle's residual)."""
+    N, nb = len(rp) - 1, A.shape[1]
+    x = np.zeros(N * nb) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).ravel().copy()
+    resid = C.c_double(0.0)
+    it = lib().orc_restarted_fgmres_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
+                                      _p(F) if F is not None else None, C.c_int(PREC[prec]), _p(b),
+                                      x.ctypes.data_as(C.c_void_p), C.c_double(tol), C.c_int(iters),
+                                      C.c_int(restart), C.byref(resid), *_parts(N, part_ptr))
+    return x.reshape(N, nb), it, resid.value
+
+
+SMOOTHER = {"SMOOTHER_LUSGS": 0, "SMOOTHER_ILU0": 1, "SMOOTHER_JACOBI": 2}
+
+
+@_keepalive
+def smoother(rp, col, A, b, kind="SMOOTHER_LUSGS", F=None, tol=1e-6, m=5, x0=None, part_ptr=None):
+    """LU_SGS_Smoother / ILU0_Smoother / Jacobi_Smoother (matrix_structure.cpp:1711 / :1517 / :1268) -> (x, iterations,
+    |r|); SMOOTHER_ILU0 needs the ILU(0) factor F."""
+    N, nb = len(rp) - 1, A.shape[1]
+    x = np.zeros(N * nb) if x0 is None else np.ascontiguousarray(x0, dtype=np.float64).ravel().copy()
+    resid = C.c_double(0.0)
+    it = lib().orc_smoother_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A),
+                              _p(F) if F is not None else None, C.c_int(SMOOTHER[kind]), _p(b),
+                              x.ctypes.data_as(C.c_void_p), C.c_double(tol), C.c_int(m), C.byref(resid),
+                              *_parts(N, part_ptr))
+    return x.reshape(N, nb), it, resid.value
+
+
+LIN_SOLVERS = ("FGMRES", "BCGSTAB", "RESTARTED_FGMRES", "SMOOTHER_LUSGS", "SMOOTHER_JACOBI", "SMOOTHER_ILU0")
+
+
+def lin_solve(rp, col, A, b, solver="FGMRES", prec="ilu", tol=1e-6, m=5, restart=10, part_ptr=None):
+    """CSysSolve::Solve (linear_solvers_structure.cpp:601-708) for LINEAR_SOLVER `solver` and LINEAR_SOLVER_PREC
+    `prec` ("ilu" / "lusgs" / "jacobi"), x0 = 0 (ImplicitEuler_Iteration's LinSysSol): the preconditioner build of
+    the branch (BuildILUPreconditioner for ILU0 / SMOOTHER_ILU0; JACOBI's invM inside the solver), then the solver.
+    Returns (x, iterations, residual)."""
+    solver = solver.upper()
+    needs_f = (solver == "SMOOTHER_ILU0") or (solver in ("FGMRES", "BCGSTAB", "RESTARTED_FGMRES") and prec == "ilu")
+    F = ilu_build(rp, col, A, part_ptr) if needs_f else None
+    if solver == "FGMRES":
+        return fgmres(rp, col, A, b, prec, F=F, tol=tol, m=m, part_ptr=part_ptr)
+    if solver == "BCGSTAB":
+        return bcgstab(rp, col, A, b, prec, F=F, tol=tol, m=m, part_ptr=part_ptr)
+    if solver == "RESTARTED_FGMRES":
+        return restarted_fgmres(rp, col, A, b, prec, F=F, tol=tol, iters=m, restart=restart, part_ptr=part_ptr)
+    if solver in SMOOTHER:
+        return smoother(rp, col, A, b, solver, F=F, tol=tol, m=m, part_ptr=part_ptr)
+    raise ValueError(f"LINEAR_SOLVER {solver}")
 
 
 @_keepalive
@@ -718,13 +789,10 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         R[~ok] = 0.0
         A[diag] = D
         rhs = -(R + 0.0)
-        if cfg.get("flow_prec", "ilu") == "ilu":
-            F = ilu_build(rp, col, A, part_ptr)
-            x, it, lres = fgmres(rp, col, A, rhs.ravel(), "ilu", F=F, tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                                 part_ptr=part_ptr)
-        else:  # LINEAR_SOLVER_PREC = LU_SGS
-            x, it, lres = fgmres(rp, col, A, rhs.ravel(), "lusgs", tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                                 part_ptr=part_ptr)
+        # LINEAR_SOLVER (cfg["lin_solver"], default FGMRES) with LINEAR_SOLVER_PREC (cfg["flow_prec"], default ILU0)
+        x, it, lres = lin_solve(rp, col, A, rhs.ravel(), cfg.get("lin_solver", "FGMRES"), cfg.get("flow_prec", "ilu"),
+                                tol=cfg["lin_tol"], m=cfg["lin_iter"], restart=cfg.get("lin_restart", 10),
+                                part_ptr=part_ptr)
         Un = update(Uold, x, nDim, 0, cfg["relaxation"], vol, dt)
         rms = np.maximum(1e-32, np.sqrt(np.sum(rhs * rhs, axis=0) / N))
     # MultiGrid_Iteration's Preprocessing(Output = true) on the updated solution (integration_time.cpp:127-129)
@@ -769,13 +837,9 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     D2[:, 1, 1] += delta
     A2[diag] = D2
     rhs2 = -R2
-    if cfg.get("sst_prec", "ilu") == "ilu":
-        F2 = ilu_build(rp, col, A2, part_ptr)
-        x2, it2, _ = fgmres(rp, col, A2, rhs2.ravel(), "ilu", F=F2, tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                            part_ptr=part_ptr)
-    else:  # LINEAR_SOLVER_PREC = LU_SGS (the shipped jet cfg)
-        x2, it2, _ = fgmres(rp, col, A2, rhs2.ravel(), "lusgs", tol=cfg["lin_tol"], m=cfg["lin_iter"],
-                            part_ptr=part_ptr)
+    # the same System.Solve config (cfg["sst_prec"]: LU_SGS in the shipped jet cfg)
+    x2, it2, _ = lin_solve(rp, col, A2, rhs2.ravel(), cfg.get("lin_solver", "FGMRES"), cfg.get("sst_prec", "ilu"),
+                           tol=cfg["lin_tol"], m=cfg["lin_iter"], restart=cfg.get("lin_restart", 10), part_ptr=part_ptr)
     Tn = sst_update(T, x2.ravel(), cfg.get("relaxation_turb", 1.0), rho, np.ascontiguousarray(Uold[:, 0]))
     sst_rms = np.maximum(1e-32, np.sqrt(np.sum(rhs2 * rhs2, axis=0) / N))
     TG1 = sol_grad(Tn)

@@ -1956,12 +1956,40 @@ static double dot_device(int64_t n, const double* a, const double* c) {
   return sh[0];
 }
 
+// BuildJacobiPreconditioner (matrix_structure.cpp:1230-1246): invM_i = InverseDiagonalBlock of the diagonal block
+// (:1129-1143, the Gauss_Elimination of each unit column)
+static std::vector<double> jacobi_build(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A) {
+  std::vector<double> inv((size_t)N * nb * nb);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < N; ++i) inverse_diag(nb, A + find_diag(rp, col, i) * nb * nb, inv.data() + i * nb * nb);
+  return inv;
+}
+
+// The preconditioner of CSysSolve::Solve (linear_solvers_structure.cpp:633-653) applied to in -> out.
+// prec: 0 LU_SGS (ComputeLU_SGSPreconditioner), 1 ILU0 with factor F (ComputeILUPreconditioner), 2 JACOBI with invM
+// (ComputeJacobiPreconditioner :1249-1266: prod = 0.0 + invM_i vec_i, c ascending — mat_vec's order).
+static void prec_apply(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F,
+                       const std::vector<double>& invM, int prec, const double* in, double* out, int64_t np,
+                       const int64_t* part_ptr) {
+  if (prec == 0) {
+    orc_lusgs_p(N, nb, rp, col, A, in, out, np, part_ptr);
+  } else if (prec == 1) {
+    orc_ilu_apply_p(N, nb, rp, col, F, in, out, np, part_ptr);
+  } else {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < N; ++i) mat_vec(nb, invM.data() + i * nb * nb, in + i * nb, out + i * nb);
+  }
+}
+
 int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F,
                  int prec, const double* b, double* x, double tol, int m, double* resid, int64_t np,
                  const int64_t* part_ptr) {
   const int64_t n = N * nb;
   auto dotp = [&](const double* a, const double* c) { return orc_dot(n, a, c); };
   auto norm = [&](const double* a) { return std::sqrt(dotp(a, a)); };
+  std::vector<double> invM;
+  if (prec == 2) invM = jacobi_build(N, nb, rp, col, A);
+  auto precond = [&](const double* in, double* out) { prec_apply(N, nb, rp, col, A, F, invM, prec, in, out, np, part_ptr); };
   std::vector<std::vector<double>> w(m + 1, std::vector<double>(n)), z(m + 1, std::vector<double>(n));
   std::vector<double> g(m + 1, 0.0), sn(m + 1, 0.0), cs(m + 1, 0.0), y(m, 0.0);
   std::vector<std::vector<double>> H(m + 1, std::vector<double>(m, 0.0));
@@ -1982,8 +2010,7 @@ int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
   int i = 0;
   for (i = 0; i < m; ++i) {
     if (beta < tol * norm0) break;
-    if (prec == 0) orc_lusgs_p(N, nb, rp, col, A, w[i].data(), z[i].data(), np, part_ptr);
-    else orc_ilu_apply_p(N, nb, rp, col, F, w[i].data(), z[i].data(), np, part_ptr);
+    precond(w[i].data(), z[i].data());
     orc_bsr_spmv(N, nb, rp, col, A, z[i].data(), w[i + 1].data());
     // ModGramSchmidt
     const double reorth = 0.98;
@@ -2062,6 +2089,117 @@ int orc_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
 int orc_fgmres(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F, int prec,
                const double* b, double* x, double tol, int m, double* resid) {
   return orc_fgmres_p(N, nb, rp, col, A, F, prec, b, x, tol, m, resid, 1, nullptr);
+}
+
+// BCGSTAB_LinSolver (linear_solvers_structure.cpp:465-599). prec as orc_fgmres_p. Returns the iteration index of
+// the break (or m); *resid = the last |r| (on the initial-guess exit the reference leaves *residual unset).
+int orc_bcgstab_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F,
+                  int prec, const double* b, double* x, double tol, int m, double* resid, int64_t np,
+                  const int64_t* part_ptr) {
+  const int64_t n = N * nb;
+  auto dotp = [&](const double* a, const double* c) { return orc_dot(n, a, c); };
+  std::vector<double> invM;
+  if (prec == 2) invM = jacobi_build(N, nb, rp, col, A);
+  auto precond = [&](const double* in, double* out) { prec_apply(N, nb, rp, col, A, F, invM, prec, in, out, np, part_ptr); };
+  std::vector<double> r(b, b + n), r0(b, b + n), p(b, b + n), v(b, b + n), sv(b, b + n), t(b, b + n),
+      ph(b, b + n), sh(b, b + n), Ax(n);
+  orc_bsr_spmv(N, nb, rp, col, A, x, Ax.data());  // mat_vec(x, A_x)
+  for (int64_t q = 0; q < n; ++q) r[q] -= Ax[q];  // r -= A_x
+  r0 = r;
+  double norm_r = std::sqrt(dotp(r.data(), r.data()));
+  double norm0 = std::sqrt(dotp(b, b));
+  const double epsm = std::numeric_limits<double>::epsilon();
+  *resid = norm_r;
+  if ((norm_r < tol * norm0) || (norm_r < epsm)) return 0;
+  double alpha = 1.0, beta = 1.0, omega = 1.0, rho = 1.0, rho_prime = 1.0;
+  norm0 = norm_r;
+  int i = 0;
+  for (i = 0; i < m; ++i) {
+    rho_prime = rho;
+    rho = dotp(r.data(), r0.data());
+    beta = (rho / rho_prime) * (alpha / omega);
+    const double beta_omega = -beta * omega;
+    for (int64_t q = 0; q < n; ++q) p[q] = beta * p[q] + beta_omega * v[q];  // Equals_AX_Plus_BY
+    for (int64_t q = 0; q < n; ++q) p[q] += 1.0 * r[q];                       // Plus_AX
+    precond(p.data(), ph.data());
+    orc_bsr_spmv(N, nb, rp, col, A, ph.data(), v.data());
+    const double r_0_v = dotp(r0.data(), v.data());
+    alpha = rho / r_0_v;
+    for (int64_t q = 0; q < n; ++q) sv[q] = 1.0 * r[q] + (-alpha) * v[q];
+    precond(sv.data(), sh.data());
+    orc_bsr_spmv(N, nb, rp, col, A, sh.data(), t.data());
+    omega = dotp(t.data(), sv.data()) / dotp(t.data(), t.data());
+    for (int64_t q = 0; q < n; ++q) x[q] += alpha * ph[q];
+    for (int64_t q = 0; q < n; ++q) x[q] += omega * sh[q];
+    for (int64_t q = 0; q < n; ++q) r[q] = 1.0 * sv[q] + (-omega) * t[q];
+    norm_r = std::sqrt(dotp(r.data(), r.data()));
+    *resid = norm_r;
+    if (norm_r < tol * norm0) break;
+  }
+  return i;
+}
+
+// RESTARTED_FGMRES (CSysSolve::Solve :662-671): FGMRES cycles from the previous cycle's x, MaxIter = iter (the
+// remainder once total + restart > iter), the tolerance multiplied by 1 / |b| after each cycle, until iter iterations
+// are spent or |b| < tol. Returns the summed iterations (-1 on an FGMRES breakdown); stops after 4096 cycles (the
+// reference's loop would not end, see rx_la_restarted_fgmres).
+int orc_restarted_fgmres_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A,
+                           const double* F, int prec, const double* b, double* x, double tol, int iter, int restart,
+                           double* resid, int64_t np, const int64_t* part_ptr) {
+  int total = 0, max_iter = iter;
+  double stol = tol;
+  for (int cycle = 0; total < iter; ++cycle) {
+    if (cycle == 4096) return -2;
+    if ((int64_t)total + restart > iter) max_iter = iter - total;
+    const int it = orc_fgmres_p(N, nb, rp, col, A, F, prec, b, x, stol, max_iter, resid, np, part_ptr);
+    if (it < 0) return it;
+    total += it;
+    const double bn = std::sqrt(orc_dot(N * nb, b, b));  // LinSysRes.norm()
+    if (bn < stol) break;
+    stol = stol * (1.0 / bn);
+  }
+  return total;
+}
+
+// The smoothers of Solve's non-Krylov branch (:683-701): kind 0 LU_SGS_Smoother (matrix_structure.cpp:1711-1835),
+// 1 ILU0_Smoother (:1517-1671, factor F), 2 Jacobi_Smoother (:1268-1366). x += M^-1 r (LU_SGS / ILU0: the
+// preconditioner sweeps, whose arithmetic the smoothers repeat, then Plus_AX(omega = 1.0); JACOBI: invM r added into x
+// term by term), r = b - A x, |r| < tol |r_0| ends the loop. Returns the iteration index of the break (or m).
+int orc_smoother_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* F,
+                   int kind, const double* b, double* x, double tol, int m, double* resid, int64_t np,
+                   const int64_t* part_ptr) {
+  const int64_t n = N * nb;
+  auto dotp = [&](const double* a, const double* c) { return orc_dot(n, a, c); };
+  std::vector<double> invM;
+  if (kind == 2) invM = jacobi_build(N, nb, rp, col, A);
+  std::vector<double> r(b, b + n), Ax(n), z(n);
+  orc_bsr_spmv(N, nb, rp, col, A, x, Ax.data());
+  for (int64_t q = 0; q < n; ++q) r[q] -= Ax[q];
+  double norm_r = std::sqrt(dotp(r.data(), r.data()));
+  double norm0 = std::sqrt(dotp(b, b));
+  const double epsm = std::numeric_limits<double>::epsilon();
+  *resid = norm_r;
+  if ((norm_r < tol * norm0) || (norm_r < epsm)) return 0;
+  norm0 = norm_r;
+  int i = 0;
+  for (i = 0; i < m; ++i) {
+    if (kind == 2) {
+#pragma omp parallel for schedule(static)
+      for (int64_t pt = 0; pt < N; ++pt)
+        for (int a = 0; a < nb; ++a)
+          for (int c = 0; c < nb; ++c) x[pt * nb + a] += invM[(pt * nb + a) * nb + c] * r[pt * nb + c];
+    } else {
+      if (kind == 0) orc_lusgs_p(N, nb, rp, col, A, r.data(), z.data(), np, part_ptr);
+      else orc_ilu_apply_p(N, nb, rp, col, F, r.data(), z.data(), np, part_ptr);
+      for (int64_t q = 0; q < n; ++q) x[q] += 1.0 * z[q];
+    }
+    orc_bsr_spmv(N, nb, rp, col, A, x, Ax.data());
+    for (int64_t q = 0; q < n; ++q) r[q] = b[q] - Ax[q];  // r = b; r -= A_x
+    norm_r = std::sqrt(dotp(r.data(), r.data()));
+    *resid = norm_r;
+    if (norm_r < tol * norm0) break;
+  }
+  return i;
 }
 
 static int64_t blk_of(const int64_t* rp, const int64_t* col, int64_t i, int64_t j) {

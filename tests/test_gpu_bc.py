@@ -22,6 +22,11 @@ MESH_KEYS = ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr", "bvert
              "wall_distance")
 
 
+# CSysSolve::Solve's other branches (oracle/make_golden.py LIN_CASES): BCGSTAB with ILU0 / JACOBI, FGMRES with JACOBI,
+# RESTARTED_FGMRES, the LU_SGS / Jacobi / ILU0 smoothers (4-species mini9 jet, CFL 1, two iterations)
+LIN_GOLDENS = ["lsbc", "lsbj", "lsfj", "lsrs", "lssl", "lssj", "lssi"]
+
+
 def golden(case):
     return dict(np.load(os.path.join(GOLD, case + ".npz")))
 
@@ -39,8 +44,21 @@ def scheme(g):
     """(flow implicit?, RK_ALPHA_COEFF or None, SST lin_prec) of a golden's cfg (it9 / it3d: implicit, ILU0)."""
     tf = str(g["time_flow"]) if "time_flow" in g else "EULER_IMPLICIT"
     rk = [float(x) for x in g["rk_alpha"]] if "rk_alpha" in g else None
-    prec = 0 if ("lin_prec" in g and str(g["lin_prec"]) == "LU_SGS") else 1
+    prec = {"LU_SGS": rx.PREC_LU_SGS, "JACOBI": rx.PREC_JACOBI}.get(str(g["lin_prec"]), rx.PREC_ILU) \
+        if "lin_prec" in g else rx.PREC_ILU
     return tf == "EULER_IMPLICIT", rk, prec
+
+
+LIN_SOLVER = {"FGMRES": rx.LIN_FGMRES, "BCGSTAB": rx.LIN_BCGSTAB, "RESTARTED_FGMRES": rx.LIN_RESTARTED_FGMRES,
+              "SMOOTHER_LUSGS": rx.LIN_SMOOTHER_LUSGS, "SMOOTHER_JACOBI": rx.LIN_SMOOTHER_JACOBI,
+              "SMOOTHER_ILU0": rx.LIN_SMOOTHER_ILU}
+
+
+def lin_kw(g):
+    """LINEAR_SOLVER / LINEAR_SOLVER_RESTART_FREQUENCY of a golden's cfg (ls*), for the flow and the SST solve."""
+    if "lin_solver" not in g:
+        return {}
+    return dict(lin_solver=LIN_SOLVER[str(g["lin_solver"])], lin_restart=int(g["lin_restart"]))
 
 
 def ignition_kw(g):
@@ -61,13 +79,14 @@ def solvers(g, implicit=1):
            if "limiter_params" in g else {})  # REF_ELEM_LENGTH, LIMITER_COEFF
     s = rx.ReactiveNSSolver(mesh, rx.Mechanism(g), rx.default_cfg(implicit=implicit if flow_imp else 0, lin_prec=prec,
                                                                   spatial_order=order, grad_method=gm, **cfg_kw(g),
-                                                                  **ignition_kw(g), **lim))
+                                                                  **ignition_kw(g), **lim, **lin_kw(g)))
     s.set_bc(rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"]))
     bp = g["bc_params"]
     so_t = int(g["sst_spatial_order"]) if "sst_spatial_order" in g else 0  # SPATIAL_ORDER_TURB (fpit2 / fpit2l / it4t)
     t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(implicit=implicit, lin_prec=prec, lin_tol=float(bp[19]),
                                              lin_iter=int(bp[20]), relaxation_turb=float(bp[23]),
-                                             cfl_red_turb=float(bp[24]), grad_method=gm, spatial_order=so_t, **lim))
+                                             cfl_red_turb=float(bp[24]), grad_method=gm, spatial_order=so_t, **lim,
+                                             **lin_kw(g)))
     return s, t
 
 
@@ -189,7 +208,7 @@ def n_iters(g):
 
 
 @pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
-                                  "fpit2l", "it4t"])
+                                  "fpit2l", "it4t"] + LIN_GOLDENS)
 def test_outer_iterations_vs_reference(case):
     """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d / it7: 2, itx9 /
     itx4: 1) on the device, started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within
@@ -228,7 +247,7 @@ def test_free_running_iterations_vs_reference(case):
 
 
 @pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
-                                  "fpit2l", "it4t"])
+                                  "fpit2l", "it4t"] + LIN_GOLDENS)
 def test_outer_iteration_vs_oracle_device_order(case):
     """One iteration against the oracle run with the device's inner-product order: the residual side and the
     Krylov recurrence then agree to the Stefan-Maxwell rounding only (amplified by FGMRES: the same 1e-10 bar)."""

@@ -39,8 +39,13 @@ def bc9(request):
     return bc_case(request.param)
 
 
+# ls*: CSysSolve::Solve's other branches (oracle/make_golden.py LIN_CASES): BCGSTAB with ILU0 / JACOBI, FGMRES with
+# JACOBI, RESTARTED_FGMRES, the LU_SGS / Jacobi / ILU0 smoothers
+LIN_GOLDENS = ["lsbc", "lsbj", "lsfj", "lsrs", "lssl", "lssj", "lssi"]
+
+
 @pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
-                                        "fpit2l", "it4t"])
+                                        "fpit2l", "it4t"] + LIN_GOLDENS)
 def it9(request):
     return golden(request.param)
 
@@ -105,8 +110,10 @@ def iteration_cfg(g):
     cfg["time"] = {"EULER_IMPLICIT": "implicit", "EULER_EXPLICIT": "euler_explicit", "RUNGE-KUTTA_EXPLICIT": "rk"}[tf]
     if "rk_alpha" in g:
         cfg["rk_alpha"] = [float(x) for x in g["rk_alpha"]]
-    cfg["sst_prec"] = "lusgs" if ("lin_prec" in g and str(g["lin_prec"]) == "LU_SGS") else "ilu"
+    cfg["sst_prec"] = {"LU_SGS": "lusgs", "JACOBI": "jacobi"}.get(str(g["lin_prec"]), "ilu") if "lin_prec" in g else "ilu"
     cfg["flow_prec"] = cfg["sst_prec"]  # LINEAR_SOLVER_PREC serves both solvers
+    if "lin_solver" in g:  # LINEAR_SOLVER, LINEAR_SOLVER_RESTART_FREQUENCY (ls*)
+        cfg.update(lin_solver=str(g["lin_solver"]), lin_restart=int(g["lin_restart"]))
     cfg["spatial_order"] = int(g["spatial_order"]) if "spatial_order" in g else 0
     if "limiter_params" in g:  # REF_ELEM_LENGTH, LIMITER_COEFF
         cfg.update(ref_elem_length=float(g["limiter_params"][0]), limiter_coeff=float(g["limiter_params"][1]))
