@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "rx_ctx.h"
+#include "rx_species.h"
 
 namespace {
 
@@ -90,7 +91,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   if (mesh->n_dim != 2 && mesh->n_dim != 3) return RX_ERR_ARG;
   const bool sst = flow != nullptr;
   const int ns = sst ? 0 : mech->n_species;
-  if (!sst && !(ns == 3 || ns == 4 || ns == 7 || ns == 9)) return RX_ERR_ARG;
+  if (!sst && (ns < kMinSpecies || ns > kMaxSpecies)) return RX_ERR_ARG;  // the instantiated counts (rx_species.h)
   if (!sst && mech->n_reactions > rx::kMaxNR) return RX_ERR_ARG;
   if (mesh->n_point >= (1LL << 31) || 2 * mesh->n_edge >= (1LL << 31)) return RX_ERR_ARG;
   if (sst && (mesh->n_point != flow->N || mesh->n_edge != flow->E)) return RX_ERR_ARG;

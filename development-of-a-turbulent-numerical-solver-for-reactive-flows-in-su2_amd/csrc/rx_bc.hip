@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "rx_ctx.h"
+#include "rx_species.h"
 #include "rx_visc.h"
 
 using namespace rx;
@@ -706,27 +707,6 @@ __global__ __launch_bounds__(kBlock) void k_sst_bc(int nbn, const int32_t* __res
   }
 }
 
-#define RX_DNS_SWITCH(nd, ns, CALL)                                        \
-  if ((nd) == 2) {                                                         \
-    switch (ns) {                                                          \
-      case 3: { constexpr int NS_ = 3, ND_ = 2; CALL; } break;             \
-      case 4: { constexpr int NS_ = 4, ND_ = 2; CALL; } break;             \
-      case 7: { constexpr int NS_ = 7, ND_ = 2; CALL; } break;             \
-      case 9: { constexpr int NS_ = 9, ND_ = 2; CALL; } break;             \
-      default: return RX_ERR_ARG;                                          \
-    }                                                                      \
-  } else if ((nd) == 3) {                                                 \
-    switch (ns) {                                                          \
-      case 3: { constexpr int NS_ = 3, ND_ = 3; CALL; } break;             \
-      case 4: { constexpr int NS_ = 4, ND_ = 3; CALL; } break;             \
-      case 7: { constexpr int NS_ = 7, ND_ = 3; CALL; } break;             \
-      case 9: { constexpr int NS_ = 9, ND_ = 3; CALL; } break;             \
-      default: return RX_ERR_ARG;                                          \
-    }                                                                      \
-  } else {                                                                 \
-    return RX_ERR_ARG;                                                     \
-  }
-
 #define RX_ND_SWITCH(nd, CALL)                   \
   if ((nd) == 2) {                               \
     constexpr int ND_ = 2;                       \
@@ -778,7 +758,8 @@ BCDev bc_dev(const rx_ctx* fl) {
 
 }  // namespace
 
-int rx_bc_launch_weak(rx_ctx* ctx, hipStream_t st) {
+#if RX_NS
+int RX_NSFN(rx_bc_launch_weak)(rx_ctx* ctx, hipStream_t st) {
   if (ctx->bc_nweak <= 0) return RX_OK;
   const BCDev B = bc_dev(ctx);
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_bc_weak<NS_, ND_><<<blocks(ctx->bc_nweak, 64), 64, 0, st>>>(
@@ -797,6 +778,24 @@ int rx_bc_launch_weak(rx_ctx* ctx, hipStream_t st) {
   }
   return RX_OK;
 }
+
+// the strong conditions and the weak markers' fluxes applied per owned boundary point (k_bc_apply)
+int RX_NSFN(rx_bc_apply)(rx_ctx* ctx) {
+  const BCDev B = bc_dev(ctx);
+  double* A = ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr;
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_bc_apply<NS_, ND_><<<ctx->bc_nbn, kApplyBlock, 0, ctx->stream>>>(
+                            ctx->bc_bn, ctx->bc_bn_ptr, ctx->bc_bn_vtx, ctx->bc_mark, ctx->bc_pn,
+                            ctx->bc_nrm, ctx->bc_mkind, ctx->bc_mdata, B, ctx->mech, ctx->coord, ctx->f[RX_F_U],
+                            ctx->f[RX_F_V], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DTDU], ctx->f[RX_F_EDDY],
+                            ctx->f[RX_F_DPDU], ctx->f[RX_F_TKE], ctx->rp,
+                            ctx->col, ctx->diag, ctx->bc_resc, ctx->bc_resv, ctx->bc_jacc, ctx->bc_jacv,
+                            ctx->f[RX_F_RES], A, ctx->err)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+#else
+RX_NS_DISPATCH(rx_bc_launch_weak, (rx_ctx * ctx, hipStream_t st), (ctx, st))
+RX_NS_DISPATCH(rx_bc_apply, (rx_ctx * ctx), (ctx))
 
 void rx_bc_free(rx_ctx* ctx) {
   void* ps[] = {ctx->bc_mkind, ctx->bc_mdata, ctx->bc_node,  ctx->bc_pn,      ctx->bc_mark,  ctx->bc_nrm,
@@ -909,24 +908,13 @@ int rx_bc_flow(rx_ctx* ctx) {
   int rc = ctx->cfg.implicit ? rx_ensure_assembled(ctx) : RX_OK;
   if (rc) return rc;
   RxPhase ph(ctx, RX_K_BC);
-  const BCDev B = bc_dev(ctx);
-  double* A = ctx->cfg.implicit ? ctx->f[RX_F_JAC] : nullptr;
   if (ctx->bc_pending) {  // boundary fluxes launched by rx_residual_zero on the side stream
     RX_HIP(hipStreamWaitEvent(ctx->stream, ctx->bc_join, 0));
     ctx->bc_pending = false;
   } else if ((rc = rx_bc_launch_weak(ctx, ctx->stream))) {
     return rc;
   }
-  if (ctx->bc_nbn > 0) {
-    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_bc_apply<NS_, ND_><<<ctx->bc_nbn, kApplyBlock, 0, ctx->stream>>>(
-                              ctx->bc_bn, ctx->bc_bn_ptr, ctx->bc_bn_vtx, ctx->bc_mark, ctx->bc_pn,
-                              ctx->bc_nrm, ctx->bc_mkind, ctx->bc_mdata, B, ctx->mech, ctx->coord, ctx->f[RX_F_U],
-                              ctx->f[RX_F_V], ctx->f[RX_F_KAPPA], ctx->f[RX_F_DTDU], ctx->f[RX_F_EDDY],
-                              ctx->f[RX_F_DPDU], ctx->f[RX_F_TKE], ctx->rp,
-                              ctx->col, ctx->diag, ctx->bc_resc, ctx->bc_resv, ctx->bc_jacc, ctx->bc_jacv,
-                              ctx->f[RX_F_RES], A, ctx->err)));
-    RX_HIP(hipGetLastError());
-  }
+  if (ctx->bc_nbn > 0) return rx_bc_apply(ctx);
   return RX_OK;
 }
 
@@ -948,3 +936,4 @@ int rx_bc_sst(rx_ctx* ctx) {
 }
 
 }  // extern "C"
+#endif  // RX_NS

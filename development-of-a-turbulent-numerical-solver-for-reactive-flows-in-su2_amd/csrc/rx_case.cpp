@@ -245,14 +245,17 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
   const std::string tf = upper(c.str("TIME_DISCRE_FLOW", "EULER_IMPLICIT"));
   if (tf != "EULER_IMPLICIT" && tf != "EULER_EXPLICIT" && tf != "RUNGE-KUTTA_EXPLICIT")
     return fail(k, RX_ERR_UNSUPPORTED, "TIME_DISCRE_FLOW= " + tf);
-  // :1050 (default LU_SGS), Linear_Solver_Prec_Map (option_structure.hpp:1312-1316); LINELET needs the line
-  // construction of BuildLineletPreconditioner (matrix_structure.cpp:1837), which is not built
+  // :1050 (default LU_SGS), Linear_Solver_Prec_Map (option_structure.hpp:1312-1316). LINELET / SMOOTHER_LINELET: the
+  // reactive flow solver never builds the linelets (BuildLineletPreconditioner, matrix_structure.cpp:1837, is called
+  // by the SST / SA / compressible solvers' constructors, e.g. solver_direct_turbulent.cpp:2691-2694, not by
+  // CReactiveEulerSolver / CReactiveNSSolver), so its Solve reads a null LineletBool (ComputeLineletPreconditioner
+  // :2049): the reference cannot run the flow solve with them, and they are refused here
   const std::string pk = upper(c.str("LINEAR_SOLVER_PREC", "LU_SGS"));
   if (pk != "ILU" && pk != "ILU0" && pk != "LU_SGS" && pk != "JACOBI")
     return fail(k, RX_ERR_UNSUPPORTED, "LINEAR_SOLVER_PREC= " + pk);
   const int prec = pk == "LU_SGS" ? RX_PREC_LU_SGS : (pk == "JACOBI" ? RX_PREC_JACOBI : RX_PREC_ILU);
   // :1047 (default FGMRES), Linear_Solver_Map (option_structure.hpp:1249-1260): the branches of CSysSolve::Solve
-  // (linear_solvers_structure.cpp:626-708); SMOOTHER_LINELET needs the linelets (see above), CONJUGATE_GRADIENT and
+  // (linear_solvers_structure.cpp:626-708); SMOOTHER_LINELET is refused (see above), CONJUGATE_GRADIENT and
   // the point-inversion methods are not solver kinds of Solve (it does nothing for them)
   const std::string lk = upper(c.str("LINEAR_SOLVER", "FGMRES"));
   static const std::pair<const char*, int> lin_map[] = {

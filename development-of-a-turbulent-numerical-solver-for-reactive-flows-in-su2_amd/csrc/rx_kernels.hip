@@ -12,6 +12,7 @@
 
 #include "rx_chem.h"
 #include "rx_ctx.h"
+#include "rx_species.h"
 #include "rx_visc.h"
 
 using namespace rx;
@@ -1541,27 +1542,6 @@ __global__ __launch_bounds__(kBlock) void k_time_step(int N, int nPV, int nVar, 
 
 inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 
-#define RX_DNS_SWITCH(nd, ns, CALL)                                        \
-  if ((nd) == 2) {                                                         \
-    switch (ns) {                                                          \
-      case 3: { constexpr int NS_ = 3, ND_ = 2; CALL; } break;             \
-      case 4: { constexpr int NS_ = 4, ND_ = 2; CALL; } break;             \
-      case 7: { constexpr int NS_ = 7, ND_ = 2; CALL; } break;             \
-      case 9: { constexpr int NS_ = 9, ND_ = 2; CALL; } break;             \
-      default: return RX_ERR_ARG;                                          \
-    }                                                                      \
-  } else if ((nd) == 3) {                                                 \
-    switch (ns) {                                                          \
-      case 3: { constexpr int NS_ = 3, ND_ = 3; CALL; } break;             \
-      case 4: { constexpr int NS_ = 4, ND_ = 3; CALL; } break;             \
-      case 7: { constexpr int NS_ = 7, ND_ = 3; CALL; } break;             \
-      case 9: { constexpr int NS_ = 9, ND_ = 3; CALL; } break;             \
-      default: return RX_ERR_ARG;                                          \
-    }                                                                      \
-  } else {                                                                 \
-    return RX_ERR_ARG;                                                     \
-  }
-
 #define RX_ND_SWITCH(nd, CALL)                   \
   if ((nd) == 2) {                               \
     constexpr int ND_ = 2;                       \
@@ -1575,6 +1555,7 @@ inline int blocks(int64_t n, int b = kBlock) { return (int)((n + b - 1) / b); }
 
 }  // namespace
 
+#if !RX_NS
 int rx_fail_hip(rx_ctx* ctx, hipError_t e) {
   (void)ctx;
   fprintf(stderr, "rx: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
@@ -1594,7 +1575,10 @@ int rx_check_error(rx_ctx* ctx) {
   return RX_OK;
 }
 
-int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter) {
+#endif  // !RX_NS
+
+#if RX_NS
+int RX_NSFN(rx_launch_set_primitive)(rx_ctx* ctx, int ext_iter) {
   const rx_cfg& c = ctx->cfg;
   const int ignite = c.ignition && (int64_t)ext_iter < c.ignition_iter ? 1 : 0;
   if (ignite && (c.fuel_index < 0 || c.fuel_index >= ctx->ns || c.oxidizer_index < 0 || c.oxidizer_index >= ctx->ns))
@@ -1609,7 +1593,7 @@ int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter) {
   return RX_OK;
 }
 
-int rx_launch_muscl(rx_ctx* ctx) {
+int RX_NSFN(rx_launch_muscl)(rx_ctx* ctx) {
   if (!ctx->recon) return RX_ERR_ARG;
   const double* lim = ctx->cfg.spatial_order == 2 ? ctx->f[RX_F_LIMITER] : nullptr;
   double* SR = ctx->cfg.implicit ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
@@ -1621,7 +1605,7 @@ int rx_launch_muscl(rx_ctx* ctx) {
   return RX_OK;
 }
 
-int rx_launch_ausm_node(rx_ctx* ctx) {
+int RX_NSFN(rx_launch_ausm_node)(rx_ctx* ctx) {
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_ausm_node<NS_, ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->f[RX_F_V],
                             ctx->cfg.spatial_order ? ctx->recon : nullptr, ctx->cfg.mach_inf, ctx->f[RX_F_RES],
@@ -1630,6 +1614,9 @@ int rx_launch_ausm_node(rx_ctx* ctx) {
   return RX_OK;
 }
 
+#endif  // RX_NS
+
+#if !RX_NS
 // the implicit convective fluxes and Jacobians are made by the node-centric assembly (k_asm_visc's fused AUSM pass)
 // instead of k_ausm_edge when the assembly also makes the viscous Jacobians, in 2-D by default: C3 (same box) CONV
 // 1.31 + ASSEMBLE 4.89 -> ASSEMBLE 6.79 ms; in 3-D each node's 6 edges and the 2-wave occupancy lose, C5 CONV 2.29 +
@@ -1643,8 +1630,10 @@ bool rx_fuse_conv(int nDim) {
   }();
   return mode == 1 || (mode == 2 && nDim == 2);
 }
+#endif  // !RX_NS
 
-int rx_launch_ausm_edge(rx_ctx* ctx) {
+#if RX_NS
+int RX_NSFN(rx_launch_ausm_edge)(rx_ctx* ctx) {
   if (!ctx->jconv) {  // allocated at first use: the 2-D fused assembly never needs the per-edge blocks
     if (ctx->capturing) return RX_ERR_STATE;
     RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->fconv), sizeof(double) * ctx->E * ctx->nVar));
@@ -1659,7 +1648,7 @@ int rx_launch_ausm_edge(rx_ctx* ctx) {
   return RX_OK;
 }
 
-int rx_launch_visc_edge(rx_ctx* ctx) {
+int RX_NSFN(rx_launch_visc_edge)(rx_ctx* ctx) {
   ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
                ctx->cfg.rans, ctx->cfg.implicit};
   {
@@ -1694,6 +1683,9 @@ int rx_launch_visc_edge(rx_ctx* ctx) {
   return RX_OK;
 }
 
+#endif  // RX_NS
+
+#if !RX_NS
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first) {
   k_gather_flux<<<blocks(ctx->N * ctx->nVar), kBlock, 0, ctx->stream>>>(
       (int)ctx->N, ctx->nVar, ctx->adj_ptr, ctx->adj, flux, sign_first, ctx->f[RX_F_RES]);
@@ -1701,7 +1693,10 @@ int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_firs
   return RX_OK;
 }
 
-int rx_launch_source(rx_ctx* ctx) {
+#endif  // !RX_NS
+
+#if RX_NS
+int RX_NSFN(rx_launch_source)(rx_ctx* ctx) {
   SourceParams P{ctx->cfg.c_mu, ctx->cfg.pasr_lb, ctx->cfg.rho_ref, ctx->cfg.t_ref, ctx->cfg.T_ref, ctx->cfg.rans,
                  ctx->cfg.implicit};
   // explicit: R += S directly; implicit: S and its Jacobian go to scratch, folded in by k_assemble
@@ -1714,6 +1709,38 @@ int rx_launch_source(rx_ctx* ctx) {
   return RX_OK;
 }
 
+// the node-centric viscous Jacobians + assembly (k_asm_visc), with the AUSM pass fused when fused_conv
+int RX_NSFN(rx_launch_asm_visc)(rx_ctx* ctx, int with_src, int fused_conv) {
+  ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
+               ctx->cfg.rans, ctx->cfg.implicit};
+  AusmIn cv{nullptr, nullptr, nullptr, nullptr, nullptr, ctx->cfg.mach_inf, ctx->err};
+  if (fused_conv) {
+    cv.V = ctx->f[RX_F_V];
+    cv.dPdU = ctx->f[RX_F_DPDU];
+    cv.VR = ctx->cfg.spatial_order ? ctx->recon : nullptr;
+    cv.SR = ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
+    cv.normal = ctx->normal;
+  }
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<blocks(ctx->N * 16), kBlock, 0, ctx->stream>>>(
+                            (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
+                            ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech,
+                            P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv)));
+  RX_HIP(hipGetLastError());
+  return RX_OK;
+}
+#endif  // RX_NS
+
+#if !RX_NS
+RX_NS_DISPATCH(rx_launch_set_primitive, (rx_ctx * ctx, int ext_iter), (ctx, ext_iter))
+RX_NS_DISPATCH(rx_launch_muscl, (rx_ctx * ctx), (ctx))
+RX_NS_DISPATCH(rx_launch_ausm_node, (rx_ctx * ctx), (ctx))
+RX_NS_DISPATCH(rx_launch_ausm_edge, (rx_ctx * ctx), (ctx))
+RX_NS_DISPATCH(rx_launch_visc_edge, (rx_ctx * ctx), (ctx))
+RX_NS_DISPATCH(rx_launch_source, (rx_ctx * ctx), (ctx))
+RX_NS_DISPATCH(rx_launch_asm_visc, (rx_ctx * ctx, int with_src, int fused_conv), (ctx, with_src, fused_conv))
+RX_NS_DISPATCH(rx_launch_grad_gg, (rx_ctx * ctx), (ctx))
+RX_NS_DISPATCH(rx_launch_grad, (rx_ctx * ctx, const int32_t* list, int64_t n), (ctx, list, n))
+
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   const int nv = ctx->nVar;
   const bool fused_conv = ctx->conv_deferred && with_visc && ctx->asm_visc;
@@ -1725,24 +1752,8 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   // fused: conv_deferred stays set (only rx_residual_zero / rx_edge_flux_conv change it), so a re-assembly of the
   // same residual (e.g. a RES download after the viscous loop, then Source_Residual) fuses the AUSM pass again: it
   // rewrites the residual, the diagonal and the off-diagonal blocks, and no per-edge convective block ever exists
-  if (with_visc && ctx->asm_visc) {  // k_visc_jac was skipped: the node-centric viscous Jacobians + assembly
-    ViscParams P{ctx->cfg.T_ref, ctx->cfg.E_ref, ctx->cfg.R_ref, ctx->cfg.prandtl_turb, ctx->cfg.lewis_turb,
-                 ctx->cfg.rans, ctx->cfg.implicit};
-    AusmIn cv{nullptr, nullptr, nullptr, nullptr, nullptr, ctx->cfg.mach_inf, ctx->err};
-    if (fused_conv) {
-      cv.V = ctx->f[RX_F_V];
-      cv.dPdU = ctx->f[RX_F_DPDU];
-      cv.VR = ctx->cfg.spatial_order ? ctx->recon : nullptr;
-      cv.SR = ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
-      cv.normal = ctx->normal;
-    }
-    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<blocks(ctx->N * 16), kBlock, 0, ctx->stream>>>(
-                              (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
-                              ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech,
-                              P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv)));
-    RX_HIP(hipGetLastError());
-    return RX_OK;
-  }
+  if (with_visc && ctx->asm_visc)  // k_visc_jac was skipped: the node-centric viscous Jacobians + assembly
+    return rx_launch_asm_visc(ctx, with_src, fused_conv ? 1 : 0);
   switch (nv) {
 #define RX_ASM_DEG(NV, DEG)                                                                                       \
   k_assemble<NV, DEG><<<blocks(ctx->N * asm_team<NV>()), kBlock, 0, ctx->stream>>>(                              \
@@ -1759,6 +1770,7 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
     RX_ASM(7)
     RX_ASM(8)
     RX_ASM(9)
+    RX_ASM(10)
     RX_ASM(11)
     RX_ASM(12)
     RX_ASM(13)
@@ -1771,6 +1783,7 @@ int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
+#endif  // !RX_NS
 
 namespace {
 // NUM_METHOD_GRAD = GREEN_GAUSS: CReactiveNSSolver::SetPrimitive_Gradient_GG (solver_direct_reactive.cpp:4784-4880),
@@ -1843,7 +1856,8 @@ __global__ __launch_bounds__(kBlock) void k_grad_gg(int Nd, const int32_t* __res
 }
 }  // namespace
 
-int rx_launch_grad_gg(rx_ctx* ctx) {
+#if RX_NS
+int RX_NSFN(rx_launch_grad_gg)(rx_ctx* ctx) {
   if (ctx->Nd <= 0) return RX_OK;
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_grad_gg<NS_, ND_><<<blocks(ctx->Nd), kBlock, 0, ctx->stream>>>(
                             (int)ctx->Nd, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->normal, ctx->bv_ptr, ctx->bv_normal,
@@ -1852,7 +1866,7 @@ int rx_launch_grad_gg(rx_ctx* ctx) {
   return RX_OK;
 }
 
-int rx_launch_grad(rx_ctx* ctx, const int32_t* list, int64_t n) {
+int RX_NSFN(rx_launch_grad)(rx_ctx* ctx, const int32_t* list, int64_t n) {
   if (n <= 0) return RX_OK;
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_grad_lsq<NS_, ND_><<<blocks(n), kBlock, 0, ctx->stream>>>(
                             (int)n, ctx->nbr_ptr, ctx->nbr, ctx->coord, ctx->f[RX_F_V], ctx->mech,
@@ -1861,6 +1875,9 @@ int rx_launch_grad(rx_ctx* ctx, const int32_t* list, int64_t n) {
   return RX_OK;
 }
 
+#endif  // RX_NS
+
+#if !RX_NS
 int rx_launch_limiter(rx_ctx* ctx) {
   RX_ND_SWITCH(ctx->nDim, (k_limiter_minmax<ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>((int)ctx->N, ctx->nPV, ctx->adj_ptr, ctx->adj,
                                                                   ctx->edges, ctx->f[RX_F_V], ctx->lim_mn,
@@ -1893,3 +1910,4 @@ int rx_launch_time_step(rx_ctx* ctx) {
   RX_HIP(hipGetLastError());
   return RX_OK;
 }
+#endif  // !RX_NS

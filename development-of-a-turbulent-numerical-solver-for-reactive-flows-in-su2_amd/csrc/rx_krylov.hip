@@ -668,6 +668,7 @@ __global__ __launch_bounds__(kBlock) void k_sm_add(int64_t n, const KState* __re
     case 7: { constexpr int NV_ = 7; CALL; } break;   \
     case 8: { constexpr int NV_ = 8; CALL; } break;   \
     case 9: { constexpr int NV_ = 9; CALL; } break;   \
+    case 10: { constexpr int NV_ = 10; CALL; } break; \
     case 11: { constexpr int NV_ = 11; CALL; } break; \
     case 12: { constexpr int NV_ = 12; CALL; } break; \
     case 13: { constexpr int NV_ = 13; CALL; } break; \

@@ -187,6 +187,7 @@ __global__ void k_sumsq_total(int nVar, int nblk, const double* __restrict__ par
     case 7: { constexpr int NV_ = 7; CALL; } break;   \
     case 8: { constexpr int NV_ = 8; CALL; } break;   \
     case 9: { constexpr int NV_ = 9; CALL; } break;   \
+    case 10: { constexpr int NV_ = 10; CALL; } break; \
     case 11: { constexpr int NV_ = 11; CALL; } break; \
     case 12: { constexpr int NV_ = 12; CALL; } break; \
     case 13: { constexpr int NV_ = 13; CALL; } break; \

@@ -2247,6 +2247,7 @@ __global__ __launch_bounds__(256) void k_lusgs_bwd_part(const int32_t* __restric
     case 7: { constexpr int NV_ = 7; CALL; } break;   \
     case 8: { constexpr int NV_ = 8; CALL; } break;   \
     case 9: { constexpr int NV_ = 9; CALL; } break;   \
+    case 10: { constexpr int NV_ = 10; CALL; } break; \
     case 11: { constexpr int NV_ = 11; CALL; } break; \
     case 12: { constexpr int NV_ = 12; CALL; } break; \
     case 13: { constexpr int NV_ = 13; CALL; } break; \
@@ -2359,6 +2360,7 @@ size_t rx_ilu_grp_lds(const rx_ctx* ctx) {
     case 7: f(std::integral_constant<int, 7>{}); break;
     case 8: f(std::integral_constant<int, 8>{}); break;
     case 9: f(std::integral_constant<int, 9>{}); break;
+    case 10: f(std::integral_constant<int, 10>{}); break;
     case 11: f(std::integral_constant<int, 11>{}); break;
     case 12: f(std::integral_constant<int, 12>{}); break;
     case 13: f(std::integral_constant<int, 13>{}); break;

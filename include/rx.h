@@ -77,7 +77,8 @@ typedef struct {
 
 /* Dual grid (CGeometry edges / dual volumes / boundary vertices). Edge order is the reference's
  * (i < j), normals oriented i -> j. nbr = point neighbour lists in the reference's order.
- * n_dim 2 or 3 (flow contexts: 3, 4, 7 or 9 species in either; 3-D node records carry w / rho w after v / rho v). */
+ * n_dim 2 or 3 (flow contexts: 3 to 9 species in either, csrc/rx_species.h; 3-D node records carry w / rho w after
+ * v / rho v). */
 typedef struct {
   int32_t n_dim;
   int64_t n_point, n_edge, n_bvert;

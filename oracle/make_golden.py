@@ -688,6 +688,14 @@ def case_it4t(limiter=False):
     return out
 
 
+def case_itns(ns):
+    """The mini9 jet with the first ns species of the jet mixture (subset library; ns 5, 6, 8: the species counts the
+    device instantiates besides the shipped 3 / 9 and the bench's 4 / 7, csrc/rx_species.h), implicit ILU0 at CFL 1,
+    two reference outer iterations."""
+    pts, quads, U, writer = mini9_inputs()
+    return iteration_case(f"it{ns}s", writer, fold_species(U, ns), ns, 2, 1.0, "ILU0", "EULER_IMPLICIT")
+
+
 # CSysSolve::Solve's branches (linear_solvers_structure.cpp:626-708) beside the default FGMRES: (LINEAR_SOLVER,
 # LINEAR_SOLVER_PREC, LINEAR_SOLVER_RESTART_FREQUENCY) of each golden
 LIN_CASES = {"lsbc": ("BCGSTAB", "ILU0", 10), "lsbj": ("BCGSTAB", "JACOBI", 10), "lsfj": ("FGMRES", "JACOBI", 10),
@@ -915,7 +923,8 @@ def main():
              "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d, "fpit2": case_fpit2,
              "fpit2l": lambda: case_fpit2(limiter=True), "it4t": case_it4t,
              "it4tl": lambda: case_it4t(limiter=True),
-             **{k: (lambda k=k: case_lin(k)) for k in LIN_CASES}}[case]()
+             **{k: (lambda k=k: case_lin(k)) for k in LIN_CASES},
+             **{f"it{n}s": (lambda n=n: case_itns(n)) for n in (5, 6, 8)}}[case]()
         path = os.path.join(gold, case + ".npz")
         np.savez_compressed(path, **a)
         print(f"{case}: {len(a)} arrays -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")

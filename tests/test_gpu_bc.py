@@ -25,6 +25,8 @@ MESH_KEYS = ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr", "bvert
 # CSysSolve::Solve's other branches (oracle/make_golden.py LIN_CASES): BCGSTAB with ILU0 / JACOBI, FGMRES with JACOBI,
 # RESTARTED_FGMRES, the LU_SGS / Jacobi / ILU0 smoothers (4-species mini9 jet, CFL 1, two iterations)
 LIN_GOLDENS = ["lsbc", "lsbj", "lsfj", "lsrs", "lssl", "lssj", "lssi"]
+# it5s / it6s / it8s: the species counts the device instantiates beside 3 / 4 / 7 / 9 (csrc/rx_species.h)
+NS_GOLDENS = ["it5s", "it6s", "it8s"]
 
 
 def golden(case):
@@ -208,7 +210,7 @@ def n_iters(g):
 
 
 @pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
-                                  "fpit2l", "it4t"] + LIN_GOLDENS)
+                                  "fpit2l", "it4t"] + LIN_GOLDENS + NS_GOLDENS)
 def test_outer_iterations_vs_reference(case):
     """Each whole reference iteration (flow + SST, boundary conditions included; it9: 3, it3d / it7: 2, itx9 /
     itx4: 1) on the device, started from the reference's own state before it: U, V, (k, omega), mu_t, RMS within
@@ -247,7 +249,7 @@ def test_free_running_iterations_vs_reference(case):
 
 
 @pytest.mark.parametrize("case", ["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
-                                  "fpit2l", "it4t"] + LIN_GOLDENS)
+                                  "fpit2l", "it4t"] + LIN_GOLDENS + NS_GOLDENS)
 def test_outer_iteration_vs_oracle_device_order(case):
     """One iteration against the oracle run with the device's inner-product order: the residual side and the
     Krylov recurrence then agree to the Stefan-Maxwell rounding only (amplified by FGMRES: the same 1e-10 bar)."""

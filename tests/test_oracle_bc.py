@@ -42,10 +42,12 @@ def bc9(request):
 # ls*: CSysSolve::Solve's other branches (oracle/make_golden.py LIN_CASES): BCGSTAB with ILU0 / JACOBI, FGMRES with
 # JACOBI, RESTARTED_FGMRES, the LU_SGS / Jacobi / ILU0 smoothers
 LIN_GOLDENS = ["lsbc", "lsbj", "lsfj", "lsrs", "lssl", "lssj", "lssi"]
+# it5s / it6s / it8s: the species counts the device instantiates beside 3 / 4 / 7 / 9 (csrc/rx_species.h)
+NS_GOLDENS = ["it5s", "it6s", "it8s"]
 
 
 @pytest.fixture(scope="module", params=["it9", "it3d", "it7", "itx9", "itx4", "ig9", "fpit", "gg9", "mix3d", "fpit2",
-                                        "fpit2l", "it4t"] + LIN_GOLDENS)
+                                        "fpit2l", "it4t"] + LIN_GOLDENS + NS_GOLDENS)
 def it9(request):
     return golden(request.param)
 
