@@ -157,7 +157,8 @@ def lib():
         _lib.rx_ilu0_apply.argtypes = [C.c_void_p, C.c_int, C.c_int]
         _lib.rx_lusgs_apply.argtypes = [C.c_void_p, C.c_int, C.c_int]
         _lib.rx_fgmres.argtypes = [C.c_void_p, C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
-        _lib.rx_linear_solve.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        if hasattr(_lib, "rx_linear_solve"):  # an RX_LIB A/B variant built before it may lack it
+            _lib.rx_linear_solve.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         _lib.rx_explicit_euler.argtypes = [C.c_void_p, C.c_void_p]
         _lib.rx_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         _lib.rx_explicit_rk.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p]
@@ -165,7 +166,8 @@ def lib():
         _lib.rx_profile_enable.argtypes = [C.c_void_p, C.c_int]
         _lib.rx_profile_read.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         _lib.rx_last_error_index.argtypes = [C.c_void_p]
-        _lib.rx_last_error_phase.argtypes = [C.c_void_p]
+        if hasattr(_lib, "rx_last_error_phase"):
+            _lib.rx_last_error_phase.argtypes = [C.c_void_p]
         _lib.rx_comm_unique_id.argtypes = [C.c_void_p]
         _lib.rx_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         _lib.rx_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(HostComm)]
