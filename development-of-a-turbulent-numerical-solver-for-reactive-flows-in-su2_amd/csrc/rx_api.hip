@@ -104,6 +104,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   if (sst) {
     ctx->kind = RX_KIND_SST;
     ctx->flow = flow;
+    ++flow->n_children;
     ctx->stream = flow->stream;
     ctx->own_stream = false;
   } else if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -726,8 +727,16 @@ int rx_sst_create(const rx_mesh_desc* mesh, rx_ctx* flow, const rx_cfg* cfg, rx_
 
 int rx_ctx_destroy(rx_ctx* ctx) {
   if (!ctx) return RX_OK;
+  if (ctx->n_children > 0) return RX_ERR_STATE;  // an SST context still runs on this stream / communicator
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  // the captured solve first: a graph holding RCCL work keeps the communicator's persistent resources, and
+  // ncclCommDestroy waits for them (the self-halo RCCL test hung here with the graph destroyed after the comm)
+  if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
+  if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
+  ctx->solve_exec = nullptr;
+  ctx->solve_graph = nullptr;
+  if (ctx->kind == RX_KIND_SST && ctx->flow) --ctx->flow->n_children;
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
@@ -738,8 +747,6 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
   rx_comm_free(ctx);
   if (ctx->kind == RX_KIND_FLOW) rx_bc_free(ctx);
-  if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
-  if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
   rx_la_krylov_free(ctx);
   for (void* p : ptrs) dfree(p);
   for (void* p : ctx->mech_bufs) dfree(p);

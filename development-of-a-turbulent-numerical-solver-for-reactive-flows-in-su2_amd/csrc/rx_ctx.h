@@ -38,6 +38,7 @@ struct rx_ctx {
   int halo_stride = 64;         // doubles per point of the widest exchangeable node field (>= kHaloMaxStride)
   void* comm = nullptr;         // ncclComm_t
   bool comm_owned = true;       // SST contexts borrow the flow context's communicator
+  int n_children = 0;           // live SST contexts on this flow context's stream / communicator
   bool has_hcomm = false;       // host-staged transport (rx_comm_init_host)
   rx_host_comm hcomm{};
   double* h_stage = nullptr;    // pinned [(n_send + N - Nd) * halo_stride + 64]

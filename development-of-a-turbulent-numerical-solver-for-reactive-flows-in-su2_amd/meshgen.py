@@ -387,6 +387,34 @@ def partition_rcb(coord, n_part: int, edges=None):
     return part
 
 
+def graph_csr(n, edges):
+    """CSR adjacency (xadj [n+1], adj) of the undirected edge list, both directions, neighbours in increasing order."""
+    e = np.asarray(edges, dtype=np.int64)
+    a, b = np.r_[e[:, 0], e[:, 1]], np.r_[e[:, 1], e[:, 0]]
+    o = np.lexsort((b, a))
+    a, b = a[o], b[o]
+    xadj = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(xadj, a + 1, 1)
+    return np.cumsum(xadj), np.ascontiguousarray(b, dtype=np.int64)
+
+
+def partition_graph(n, edges, n_part: int, imbalance: float = 0.03):
+    """Multilevel graph partition of the points (rx_partition_graph, csrc/rx_part.cpp: recursive bisection with
+    heavy-edge coarsening and FM refinement, then a k-way boundary pass) — the graph-based stand-in for the reference's
+    METIS call (geometry_structure.cpp:11360-11450), within a few percent of METIS's edge cut on the jet grids
+    (tools/edge_cut.py -> profiles/r05_edge_cut.json). Returns the part id of every point."""
+    import ctypes as C
+    import os
+    lib = C.CDLL(os.environ.get("RX_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "librx.so")))
+    xadj, adj = graph_csr(n, edges)
+    part = np.zeros(n, dtype=np.int32)
+    rc = lib.rx_partition_graph(C.c_int64(n), xadj.ctypes.data_as(C.c_void_p), adj.ctypes.data_as(C.c_void_p),
+                                C.c_int32(n_part), C.c_double(imbalance), part.ctypes.data_as(C.c_void_p), None)
+    if rc != 0:
+        raise ValueError(f"rx_partition_graph failed (status {rc})")
+    return part.astype(np.int64)
+
+
 def partition_order(n, edges, part):
     """New->old permutation: partitions in order, each one RCM-ordered on its own subgraph (the
     reference renumbers every rank's domain points with RCM, CPhysicalGeometry::SetRCM_Ordering)."""
@@ -410,15 +438,17 @@ def build_jet(nx: int, ny: int, rcm: bool = True, n_part: int = 1, nz: int = 0, 
 
     n_part > 1: points are split into n_part RCB parts (the reference's MPI ranks), numbered part by
     part with a local RCM; `part_ptr` gives the row range of every part. partitioner "coord" (default: the
-    partitions every golden, size test and bench line was measured on) or "spacing" (cuts in mesh spacings:
-    within 2 % of the grid's edge-cut bound, profiles/r02_edge_cut.json)."""
+    partitions every golden, size test and bench line was measured on), "spacing" (cuts in mesh spacings:
+    within 2 % of the grid's edge-cut bound, profiles/r02_edge_cut.json) or "graph" (partition_graph, the multilevel
+    graph partitioner, for meshes whose coordinates say little about their connectivity)."""
     pts, quads, bnd = jet_mesh3d(nx, ny, nz, **kw) if nz > 1 else jet_mesh(nx, ny, **kw)
     median_dual = median_dual3d if nz > 1 else median_dual2d
     part_ptr = np.array([0, len(pts)], dtype=np.int64)
     if n_part > 1:
         e0 = element_edges(len(pts), quads)
-        perm, part_ptr = partition_order(len(pts), e0, partition_rcb(pts, n_part,
-                                                                     edges=e0 if partitioner == "spacing" else None))
+        part = (partition_graph(len(pts), e0, n_part) if partitioner == "graph" else
+                partition_rcb(pts, n_part, edges=e0 if partitioner == "spacing" else None))
+        perm, part_ptr = partition_order(len(pts), e0, part)
         pts, quads, bnd, _ = renumber(pts, quads, bnd, perm)
     elif rcm:
         perm = rcm_order(len(pts), element_edges(len(pts), quads))

@@ -182,7 +182,8 @@ typedef enum {
 } rx_field;
 
 int rx_ctx_create(const rx_mesh_desc *mesh, const rx_mech_desc *mech, const rx_cfg *cfg, int device, rx_ctx **out);
-int rx_ctx_destroy(rx_ctx *ctx);
+int rx_ctx_destroy(rx_ctx *ctx); /* RX_ERR_STATE for a flow context whose SST context (rx_sst_create) is alive:
+                                    destroy the SST context first (it runs on the flow's stream / communicator) */
 int rx_field_size(const rx_ctx *ctx, rx_field f, int64_t *count);
 int rx_upload(rx_ctx *ctx, rx_field f, const double *host, int64_t count);
 int rx_download(rx_ctx *ctx, rx_field f, double *host, int64_t count);

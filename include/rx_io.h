@@ -98,6 +98,14 @@ int rx_restart_write(const char *path, const rx_mesh *mesh, int32_t n_var, const
                      const double *extra, int64_t ext_iter);
 int rx_restart_read(const char *path, const rx_mesh *mesh, int32_t n_var, double *U, double *T);
 
+/* Multilevel recursive-bisection partition of a graph (CSR xadj[n+1] / adj, both directions of every edge, no self
+ * loops, unit weights) into nparts parts of n / nparts vertices within a relative `imbalance` (e.g. 0.03): part[n]
+ * receives each vertex's part, edge_cut (may be NULL) the number of cut edges. Deterministic. The stand-in for the
+ * reference's METIS call (CPhysicalGeometry::SetColorGrid, Common/src/geometry_structure.cpp:11360-11450; csrc/
+ * rx_part.cpp); meshgen.partition_graph orders the parts into rx_mesh_desc.part_ptr. */
+int rx_partition_graph(int64_t n, const int64_t *xadj, const int64_t *adj, int32_t nparts, double imbalance,
+                       int32_t *part, int64_t *edge_cut);
+
 #ifdef __cplusplus
 }
 #endif

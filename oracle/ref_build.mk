@@ -35,3 +35,22 @@ $(OUT)/harness: $(dir $(lastword $(MAKEFILE_LIST)))ref_harness/harness.cpp $(OUT
 
 harness: $(OUT)/harness
 .PHONY: harness
+
+# The reference's vendored METIS 5 (externals/metis, with the CPPFLAGS of its m4/metis.m4): the partitioner that
+# CPhysicalGeometry::SetColorGrid calls (Common/src/geometry_structure.cpp:11446). tools/edge_cut.py and
+# tests/test_partition.py compare rx_partition_graph's edge cut with it; nothing in the product links it.
+METIS_DIR := $(REF)/externals/metis
+METIS_SRC := $(wildcard $(METIS_DIR)/GKlib/*.c) $(wildcard $(METIS_DIR)/libmetis/*.c)
+METIS_OBJ := $(patsubst $(METIS_DIR)/%.c,$(OUT)/obj/metis/%.o,$(METIS_SRC))
+METIS_FLAGS := -O2 -fPIC -std=gnu99 -w -D_FILE_OFFSET_BITS=64 -DNDEBUG -DNDEBUG2 -DHAVE_EXECINFO_H -DHAVE_GETLINE \
+               -I$(METIS_DIR)/include -I$(METIS_DIR)/GKlib -I$(METIS_DIR)/libmetis
+
+$(OUT)/obj/metis/%.o: $(METIS_DIR)/%.c
+	@mkdir -p $(dir $@)
+	gcc $(METIS_FLAGS) -c $< -o $@
+
+$(OUT)/libmetis.so: $(METIS_OBJ)
+	gcc -shared $^ -o $@ -lm
+
+metis: $(OUT)/libmetis.so
+.PHONY: metis

@@ -24,6 +24,7 @@ def case(nx, ny, n_part, ns=7):
     cfg = dict(cfl=5.0, max_delta_time=1e6, prandtl_lam=0.72, prandtl_turb=kw["prandtl_turb"],
                lewis_turb=kw["lewis_turb"], mach_inf=kw["mach_inf"], c_mu=kw["c_mu"], pasr_lb=kw["pasr_lb"],
                lin_tol=1e-6, lin_iter=5, relaxation=1.0)
+    kw["cfl"] = cfg["cfl"]  # the device cfg's CFL is the oracle's (default_cfg's is the bench's, rx.BENCH_CFL)
     return mesh, st, mech_arrays, kw, cfg
 
 
