@@ -32,7 +32,7 @@ struct Graph {
 
 // Heavy-edge matching: vertices in a random order match their unmatched neighbour of largest edge weight (lightest
 // vertex on ties); cmap[v] = coarse vertex. Returns the coarse graph.
-Graph coarsen(const Graph& g, std::vector<int>& cmap, std::mt19937& rng) {
+Graph coarsen(const Graph& g, std::vector<int>& cmap, std::mt19937& rng, const int32_t* label = nullptr) {
   std::vector<int> perm(g.n), match(g.n, -1);
   for (int v = 0; v < g.n; ++v) perm[v] = v;
   std::shuffle(perm.begin(), perm.end(), rng);
@@ -41,7 +41,7 @@ Graph coarsen(const Graph& g, std::vector<int>& cmap, std::mt19937& rng) {
     int best = -1, bw = -1;
     for (int k = g.xadj[v]; k < g.xadj[v + 1]; ++k) {
       const int u = g.adj[k];
-      if (match[u] >= 0 || u == v) continue;
+      if (match[u] >= 0 || u == v || (label && label[u] != label[v])) continue;
       if (g.ew[k] > bw || (g.ew[k] == bw && g.vw[u] < g.vw[best])) {
         best = u;
         bw = g.ew[k];
@@ -131,7 +131,7 @@ void fm_refine(const Graph& g, std::vector<int>& where, const int64_t (&maxw)[2]
     int64_t best_cut = cut, best_over = over(pw);
     size_t best_len = 0;
     // moves without improvement before the pass ends
-    const size_t limit = std::min<size_t>(2000, std::max<size_t>(50, (size_t)g.n / 100));
+    const size_t limit = std::min<size_t>(5000, std::max<size_t>(200, (size_t)g.n / 20));
     while (moves.size() < (size_t)g.n) {
       // the side to move from: the overweight one, else the one whose best move is better (and allowed)
       int from = -1;
@@ -301,40 +301,66 @@ void recurse(const Graph& g, const std::vector<int>& verts, int nparts, int p0, 
   recurse(g, b, nparts - left, p0 + left, eps, rng, local, part);
 }
 
-// Greedy k-way boundary refinement after the recursive bisection (the bisections never see two sibling subtrees'
-// shared boundary): a boundary vertex moves to the neighbouring part it has the most edges into when that strictly
-// lowers the cut and both parts stay within [minw, maxw]; vertices in increasing id, a few passes.
-void kway_refine(const Graph& g, int32_t* part, int nparts, int64_t minw, int64_t maxw, int passes) {
-  std::vector<int64_t> pw(nparts, 0);
-  for (int v = 0; v < g.n; ++v) pw[part[v]] += g.vw[v];
-  std::vector<int> conn(nparts, 0), touched;
-  for (int pass = 0; pass < passes; ++pass) {
-    int64_t moved = 0;
-    for (int v = 0; v < g.n; ++v) {
-      const int p = part[v];
-      touched.clear();
-      for (int k = g.xadj[v]; k < g.xadj[v + 1]; ++k) {
-        const int q = part[g.adj[k]];
-        if (conn[q] == 0) touched.push_back(q);
-        conn[q] += g.ew[k];
-      }
-      int best = p, bg = 0;
-      for (int q : touched)
-        if (q != p && conn[q] - conn[p] > bg && pw[q] + g.vw[v] <= maxw && pw[p] - g.vw[v] >= minw) {
-          bg = conn[q] - conn[p];
+// Greedy k-way boundary refinement of one level (vertex weights) in place; returns the number of moves.
+int64_t kway_greedy(const Graph& g, int32_t* part, std::vector<int64_t>& pw, int64_t minw, int64_t maxw,
+                    std::vector<int>& conn, std::vector<int>& touched) {
+  int64_t moved = 0;
+  for (int v = 0; v < g.n; ++v) {
+    const int p = part[v];
+    touched.clear();
+    for (int k = g.xadj[v]; k < g.xadj[v + 1]; ++k) {
+      const int q = part[g.adj[k]];
+      if (conn[q] == 0) touched.push_back(q);
+      conn[q] += g.ew[k];
+    }
+    int best = p, bg = 0;
+    for (int q : touched)
+      if (q != p && pw[q] + g.vw[v] <= maxw && pw[p] - g.vw[v] >= minw) {
+        const int gq = conn[q] - conn[p];
+        // a strictly better cut, or an equal one that moves weight to a lighter part
+        if (gq > bg || (gq == bg && gq == 0 && best == p && pw[q] + g.vw[v] < pw[p])) {
+          bg = gq;
           best = q;
         }
-      for (int q : touched) conn[q] = 0;
-      conn[p] = 0;
-      if (best != p) {
-        pw[p] -= g.vw[v];
-        pw[best] += g.vw[v];
-        part[v] = best;
-        ++moved;
       }
+    for (int q : touched) conn[q] = 0;
+    conn[p] = 0;
+    if (best != p) {
+      pw[p] -= g.vw[v];
+      pw[best] += g.vw[v];
+      part[v] = best;
+      ++moved;
     }
-    if (!moved) break;
   }
+  return moved;
+}
+
+// k-way refinement over a hierarchy: the graph coarsened with matches inside a part only (so the partition carries
+// to every level), then greedy boundary passes from the coarsest level down — coarse moves shift whole clusters.
+void kway_vcycle(const Graph& g, int32_t* part, int nparts, int64_t minw, int64_t maxw, std::mt19937& rng) {
+  std::vector<Graph> levels{g};
+  std::vector<std::vector<int>> maps;
+  std::vector<std::vector<int32_t>> parts{std::vector<int32_t>(part, part + g.n)};
+  while (levels.back().n > 40 * nparts) {
+    std::vector<int> cmap;
+    Graph c = coarsen(levels.back(), cmap, rng, parts.back().data());
+    if (c.n > 0.9 * levels.back().n) break;
+    std::vector<int32_t> cp(c.n);
+    for (int v = 0; v < levels.back().n; ++v) cp[cmap[v]] = parts.back()[v];
+    maps.push_back(std::move(cmap));
+    levels.push_back(std::move(c));
+    parts.push_back(std::move(cp));
+  }
+  std::vector<int> conn(nparts, 0), touched;
+  for (int l = (int)levels.size() - 1; l >= 0; --l) {
+    if (l + 1 < (int)levels.size())  // project the coarser level's refined partition
+      for (int v = 0; v < levels[l].n; ++v) parts[l][v] = parts[l + 1][maps[l][v]];
+    std::vector<int64_t> pw(nparts, 0);
+    for (int v = 0; v < levels[l].n; ++v) pw[parts[l][v]] += levels[l].vw[v];
+    for (int pass = 0; pass < 6; ++pass)
+      if (!kway_greedy(levels[l], parts[l].data(), pw, minw, maxw, conn, touched)) break;
+  }
+  std::copy(parts[0].begin(), parts[0].end(), part);
 }
 
 }  // namespace
@@ -365,8 +391,8 @@ extern "C" int rx_partition_graph(int64_t n, const int64_t* xadj, const int64_t*
   recurse(g, verts, nparts, 0, eps, rng, local, part);
   if (nparts > 2) {
     const double mean = (double)n / nparts;
-    kway_refine(g, part, nparts, (int64_t)std::floor(mean * (1.0 - imbalance)), (int64_t)std::ceil(mean * (1.0 + imbalance)),
-                8);
+    kway_vcycle(g, part, nparts, (int64_t)std::floor(mean * (1.0 - imbalance)),
+                (int64_t)std::ceil(mean * (1.0 + imbalance)), rng);
   }
   if (edge_cut) {
     std::vector<int> w(part, part + n);

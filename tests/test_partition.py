@@ -1,0 +1,85 @@
+"""The multilevel graph partitioner (rx_partition_graph, csrc/rx_part.cpp; meshgen.partition_graph): the stand-in for
+the reference's METIS call (CPhysicalGeometry::SetColorGrid, Common/src/geometry_structure.cpp:11360-11450).
+
+Checks: a valid, balanced, deterministic partition, and an edge cut within 8 % of METIS 5's k-way cut on the same
+graph — METIS compiled from the reference's own vendored sources (oracle/ref_build.mk `metis`, oracle/_ref/
+libmetis.so, test infrastructure only); without that library the bar is the coordinate bisection's cut. CPU only."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from tests.rxpkg import meshgen
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+METIS = os.path.join(ROOT, "oracle", "_ref", "libmetis.so")
+
+
+def jet_graph(nx, ny):
+    pts, el, _ = meshgen.jet_mesh(nx, ny)
+    e = np.concatenate([el[:, [0, 1]], el[:, [1, 2]], el[:, [2, 3]], el[:, [3, 0]]])
+    return pts, np.unique(np.sort(e, axis=1), axis=0)
+
+
+def cut(edges, part):
+    return int(np.sum(part[edges[:, 0]] != part[edges[:, 1]]))
+
+
+def metis_kway_cut(n, edges, P):
+    lib = C.CDLL(METIS)
+    xadj, adj = meshgen.graph_csr(n, edges)
+    x32, a32 = xadj.astype(np.int32), adj.astype(np.int32)
+    part = np.zeros(n, dtype=np.int32)
+    nv, ncon, np_, obj = C.c_int32(n), C.c_int32(1), C.c_int32(P), C.c_int32()
+    rc = lib.METIS_PartGraphKway(C.byref(nv), C.byref(ncon), x32.ctypes.data_as(C.c_void_p),
+                                 a32.ctypes.data_as(C.c_void_p), None, None, None, C.byref(np_), None, None, None,
+                                 C.byref(obj), part.ctypes.data_as(C.c_void_p))
+    assert rc == 1  # METIS_OK
+    return cut(edges, part)
+
+
+@pytest.mark.parametrize("nx,ny,P", [(100, 40, 1), (100, 40, 4), (100, 40, 16), (100, 40, 37), (300, 120, 64)])
+def test_partition_graph_valid_balanced_deterministic(nx, ny, P):
+    pts, e = jet_graph(nx, ny)
+    n = len(pts)
+    part = meshgen.partition_graph(n, e, P)
+    assert part.shape == (n,) and part.min() == 0 and part.max() == P - 1
+    sizes = np.bincount(part, minlength=P)
+    assert sizes.min() >= np.floor(n / P * 0.97) and sizes.max() <= np.ceil(n / P * 1.03), (sizes.min(), sizes.max())
+    assert np.array_equal(part, meshgen.partition_graph(n, e, P))  # deterministic
+    if P == 1:
+        return
+    c = cut(e, part)
+    if os.path.exists(METIS):
+        ref = metis_kway_cut(n, e, P)
+        assert c <= 1.08 * ref, (c, ref)
+    else:
+        assert c <= 1.15 * cut(e, meshgen.partition_rcb(pts, P)), c
+
+
+def test_partition_graph_on_a_disconnected_graph():
+    """Two separate grids: every vertex still gets a part and the parts stay balanced."""
+    pts, e = jet_graph(40, 20)
+    n = len(pts)
+    e2 = np.concatenate([e, e + n])
+    part = meshgen.partition_graph(2 * n, e2, 6)
+    sizes = np.bincount(part, minlength=6)
+    assert sizes.min() > 0 and sizes.max() <= np.ceil(2 * n / 6 * 1.03)
+
+
+def test_partition_graph_rejects_bad_input():
+    pts, e = jet_graph(10, 5)
+    with pytest.raises(ValueError):
+        meshgen.partition_graph(len(pts), e, len(pts) + 1)
+    with pytest.raises(ValueError):
+        meshgen.partition_graph(len(pts), e, 0)
+
+
+def test_build_jet_with_the_graph_partitioner():
+    """build_jet(partitioner="graph"): partitions numbered part by part (part_ptr), each a connected RCM block."""
+    mesh = meshgen.build_jet(60, 24, n_part=8, partitioner="graph")
+    pp = mesh["part_ptr"]
+    assert len(pp) == 9 and pp[0] == 0 and pp[-1] == len(mesh["coord"])
+    sizes = np.diff(pp)
+    assert sizes.min() >= np.floor(len(mesh["coord"]) / 8 * 0.97)

@@ -6,7 +6,11 @@ cut edge shared by two parts), which METIS approaches on such grids). "coord": b
 extent in coordinates normalised by the domain's (round 1); "spacing": across the longer extent in mesh
 spacings (meshgen.partition_rcb with edges, what build_jet uses).
 
-usage: python tools/edge_cut.py [c3|c4|c2] > profiles/r02_edge_cut.json
+Round 5: "graph" (meshgen.partition_graph, the multilevel graph partitioner rx_partition_graph) and "metis" (METIS 5's
+k-way partitioner compiled from the reference's own vendored sources, oracle/_ref/libmetis.so, on the same graph;
+omitted when that library is not built).
+
+usage: python tools/edge_cut.py [c3|c4|c2] > profiles/r05_edge_cut.json
 """
 import json
 import os
@@ -34,6 +38,22 @@ def cut_stats(edges, part):
     return int(cut.sum()), int(halo.max()), float(halo.mean())
 
 
+METIS = os.path.join(ROOT, "oracle", "_ref", "libmetis.so")
+
+
+def metis_kway(n, edges, P):
+    import ctypes as C
+    lib = C.CDLL(METIS)
+    xadj, adj = meshgen.graph_csr(n, edges)
+    x32, a32 = xadj.astype(np.int32), adj.astype(np.int32)
+    part = np.zeros(n, dtype=np.int32)
+    nv, ncon, np_, obj = C.c_int32(n), C.c_int32(1), C.c_int32(P), C.c_int32()
+    lib.METIS_PartGraphKway(C.byref(nv), C.byref(ncon), x32.ctypes.data_as(C.c_void_p), a32.ctypes.data_as(C.c_void_p),
+                            None, None, None, C.byref(np_), None, None, None, C.byref(obj),
+                            part.ctypes.data_as(C.c_void_p))
+    return part.astype(np.int64)
+
+
 def main():
     case = sys.argv[1] if len(sys.argv) > 1 else "c3"
     nx, ny = CASES[case]
@@ -46,8 +66,14 @@ def main():
         A = len(pts) / P
         bound = max(P * 2.0 * np.sqrt(A) - (nx + ny), 1.0)
         row = {"lower_bound_cut": round(bound)}
-        for mode in ("coord", "spacing"):
-            part = meshgen.partition_rcb(pts, P, edges=e if mode == "spacing" else None)
+        modes = ["coord", "spacing", "graph"] + (["metis"] if os.path.exists(METIS) else [])
+        for mode in modes:
+            if mode == "graph":
+                part = meshgen.partition_graph(len(pts), e, P)
+            elif mode == "metis":
+                part = metis_kway(len(pts), e, P)
+            else:
+                part = meshgen.partition_rcb(pts, P, edges=e if mode == "spacing" else None)
             c, hmax, hmean = cut_stats(e, part)
             row[mode] = {"edge_cut": c, "cut_over_bound": round(c / bound, 3), "halo_max": hmax,
                          "halo_mean": round(hmean, 1)}
