@@ -966,8 +966,13 @@ struct AusmIn {
 #define RX_ASMV_FUSE 1  // build knob: 0 compiles k_asm_visc without its fused AUSM pass
 #endif
 #ifndef RX_ASMV_PARK
-#define RX_ASMV_PARK 0  // build knob: 1 = round 4's fused pass, which parked 0 -+ Jc in the off-diagonal block for the
-#endif                  // viscous pass to finish (each off-diagonal block written twice and read back once)
+// build knob: 1 (default) = the fused pass parks 0 -+ Jc in the off-diagonal block for the viscous pass to finish (each
+// off-diagonal block written twice, read back once); 0 = written once, the column re-evaluated in the viscous pass
+// (VERDICT r04 #3). Same-box A/B at C3 (gpurun_out r05c, two runs each): ASSEMBLE 6.16 / 6.15 ms parked against
+// 6.92 / 6.93 single-write — re-evaluating the AUSM column costs more than the second write of the block; C5 8.81 vs
+// 9.06 ms
+#define RX_ASMV_PARK 1
+#endif
 #ifndef RX_ASMV_CDEG
 #define RX_ASMV_CDEG -1  // build knob: node degree up to which k_asm_visc's convective pass loads everything first
 #endif                   // (-1: the quad / hex stencils' 4 in 2-D, 6 in 3-D; 0: never)
