@@ -90,6 +90,10 @@ def ilu_apply_kernels(N, nnzb, nVar, parts):
         return f"k_ilu_apply_lds<{nVar}>"
     if os.environ.get("RX_ILU_SPLIT"):
         return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
+    if nVar >= 5 and not (os.environ.get("RX_ILU_NO_RING") or os.environ.get("RX_NARROW_APPLY")):
+        # round 5: both sweeps with the x rows in an LDS ring (when every level has at most 16 * (64 // nVar) rows,
+        # as on the C3 / C5 partitions: rocprof shows it there, profiles/r05_c3_kernel_stats.md)
+        return f"k_ilu_apply_ring<{nVar}, 1024, 2>"
     return f"k_ilu_apply_wide<{nVar}, 1024>"  # both sweeps of a partition in one launch (round 4)
 
 
@@ -478,6 +482,10 @@ def main():
             out["algorithmic_bytes"] = int(m["work"])
             out["traffic"] = None if t is None else int(t)
             out["traffic_spmv_calibrated"] = None if tc is None else int(tc)
+            f64 = pmc_fp64_flop(m["kernel"], wkey)
+            if f64 is not None:  # the FP64 view beside the HBM one (PMC-counted flops / this run's launch time)
+                out["fp64_tflops"] = round(f64 / avg_s / 1e12, 3)
+                out["fp64_frac"] = round(f64 / avg_s / 1e12 / FP64_PEAK_TFS, 4)
         else:
             out["algorithmic_flops"] = int(m["work"])
             out["traffic"] = None

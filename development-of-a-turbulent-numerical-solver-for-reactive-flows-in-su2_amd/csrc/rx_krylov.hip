@@ -133,9 +133,12 @@ constexpr int64_t kGridS = (int64_t)kRedBlocks * kBlock;
 // sums of the blocks past the row's end are skipped). Measured on one box at C3: the SST solve 2.14 -> 2.05 ms;
 // for the 11x11 flow blocks chunks of 3 / 5 made the solve slower (15.40 -> 16.14 / 15.70 ms), so those keep
 // one block at a time.
+#ifndef RX_SPMV_CHUNK_BIG
+#define RX_SPMV_CHUNK_BIG 1  // build knob: blocks per chunk for NV > 4
+#endif
 template <int NV>
 constexpr int rx_spmv_chunk() {
-  return NV <= 4 ? 5 : 1;
+  return NV <= 4 ? 5 : RX_SPMV_CHUNK_BIG;
 }
 template <int NV>
 __device__ inline double spmv_elem(int64_t q, const int32_t* __restrict__ rp, const int32_t* __restrict__ col,

@@ -8,8 +8,11 @@ import bench  # noqa: E402
 
 
 def test_ilu_apply_kernel_names(monkeypatch):
-    monkeypatch.delenv("RX_ILU_SPLIT", raising=False)
-    # C3: 1M points, 256 partitions of 3 906 rows -> the vector does not fit LDS: the fused wide sweeps (one kernel)
+    for v in ("RX_ILU_SPLIT", "RX_ILU_NO_RING", "RX_NARROW_APPLY"):
+        monkeypatch.delenv(v, raising=False)
+    # C3: 1M points, 256 partitions of 3 906 rows -> the vector does not fit LDS: the LDS-ring sweeps (round 5)
+    assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_ring<11, 1024, 2>"
+    monkeypatch.setenv("RX_ILU_NO_RING", "1")  # the fused wide sweeps (round 4)
     assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_wide<11, 1024>"
     # C4's share per GPU at 2048 partitions: 488-row partitions fit LDS
     assert bench.ilu_apply_kernels(125_000, 624_000, 11, 256) == "k_ilu_apply_lds<11>"
