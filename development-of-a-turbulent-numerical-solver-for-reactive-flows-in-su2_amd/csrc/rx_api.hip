@@ -15,6 +15,12 @@
 
 namespace {
 
+// y[i] = rx_recip(x[i]).y: divisors' reciprocals made by the device's own instructions (rx_fdiv.h)
+__global__ void k_recip_table(const double* __restrict__ x, double* __restrict__ y, int n) {
+  const int i = threadIdx.x;
+  if (i < n) y[i] = rx::rx_recip(x[i]).y;
+}
+
 template <typename T>
 int dalloc(rx_ctx* ctx, T** p, size_t n) {
   *p = nullptr;
@@ -302,11 +308,39 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         part_pass[p + 1] = (int32_t)pass_lo.size();
       }
       pass_lo.push_back((int32_t)order.size());
-      // k_ilu_apply_ring's LDS plan: row j's result goes to ring row (level(j) mod R) W + position(j) (W = the widest
-      // level); a block (i, j) of a dependency less than R levels back reads it there, a farther one from j's far row
-      // R W + (its index among the partition's far sources), written by j as well
+      // k_ilu_apply_ring's plan. Its wavefronts take turns by level in G groups (rx_ilu_ring_groups), so a level has
+      // at most cap = rows per pass / G rows: a wider level is split into ceil(width / cap) consecutive sub-levels of
+      // nearly equal width (the rows of a level are independent, so any split keeps every row's arithmetic; the rows
+      // keep their schedule order). Row j's result goes to ring row (sub-level(j) mod R) W + position(j) (W = the
+      // widest sub-level); a block (i, j) of a dependency less than R sub-levels back reads it there, a farther one
+      // from j's far row R W + (its index among the partition's far sources), written by j as well
       {
-        const int R = kIluRing, W = std::max(1, S.maxwidth);
+        const int cap = std::max(1, rx_ilu_ring_rpb(ctx->nVar) / rx_ilu_ring_groups());
+        std::vector<int32_t> slv(N, 0), spos(N, 0), rpart_lvl(np + 1, 0), rlvl_ptr(1, 0);
+        int W = 1;
+        S.rmaxlev = 0;
+        for (int64_t p = 0; p < np; ++p) {
+          int32_t nsub_p = 0;
+          for (int32_t l = part_lvl[p]; l < part_lvl[p + 1]; ++l) {
+            const int32_t c = lvl_ptr[l + 1] - lvl_ptr[l];
+            const int32_t nsub = (c + cap - 1) / cap, chunk = (c + nsub - 1) / nsub;
+            for (int32_t q = 0; q < c; ++q) {
+              const int32_t i = order[lvl_ptr[l] + q];
+              slv[i] = nsub_p + q / chunk;
+              spos[i] = q % chunk;
+            }
+            for (int32_t s = 0; s < nsub; ++s) {
+              const int32_t e = std::min(c, (s + 1) * chunk);
+              rlvl_ptr.push_back(lvl_ptr[l] + e);
+              W = std::max(W, e - s * chunk);
+            }
+            nsub_p += nsub;
+          }
+          rpart_lvl[p + 1] = rpart_lvl[p] + nsub_p;
+          S.rmaxlev = std::max(S.rmaxlev, nsub_p);
+        }
+        S.rmaxwidth = W;
+        const int R = kIluRing;
         std::vector<int32_t> farid(N, -1);
         int32_t nfar_max = 0;
         for (int64_t p = 0; p < np; ++p) {
@@ -315,8 +349,8 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
             const int32_t k0 = fwd ? klo[i] : (int32_t)diag[i] + 1, k1 = fwd ? (int32_t)diag[i] : khi[i];
             for (int32_t k = k0; k < k1; ++k) {
               const int32_t j = col32[k];
-              if (lv[i] - lv[j] < R) {
-                ring_xoff[k] = (lv[j] % R) * W + pos[j];
+              if (slv[i] - slv[j] < R) {
+                ring_xoff[k] = (slv[j] % R) * W + spos[j];
               } else {
                 if (farid[j] < 0) farid[j] = nfar++;
                 ring_xoff[k] = R * W + farid[j];
@@ -328,11 +362,13 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         std::vector<int32_t> ring(2 * order.size());
         for (size_t r = 0; r < order.size(); ++r) {
           const int32_t i = order[r];
-          ring[2 * r] = (lv[i] % R) * W + pos[i];
+          ring[2 * r] = (slv[i] % R) * W + spos[i];
           ring[2 * r + 1] = farid[i] >= 0 ? R * W + farid[i] : -1;
         }
         S.ring_rows = R * W + nfar_max;
-        const int rc3 = dupload(ctx, &S.ring, ring.data(), ring.size());
+        int rc3 = dupload(ctx, &S.ring, ring.data(), ring.size());
+        if (!rc3) rc3 = dupload(ctx, &S.rpart_lvl, rpart_lvl.data(), rpart_lvl.size());
+        if (!rc3) rc3 = dupload(ctx, &S.rlvl_ptr, rlvl_ptr.data(), rlvl_ptr.size());
         if (rc3) return rc3;
       }
       int rc2 = dupload(ctx, &S.pass_lo, pass_lo.data(), pass_lo.size());
@@ -595,6 +631,14 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     m.tx = up(mech->tab_x, (size_t)5 * ns * nt);
     m.ty = up(mech->tab_y, (size_t)5 * ns * nt);
     m.ty2 = up(mech->tab_y2, (size_t)5 * ns * nt);
+    {  // the molar masses' reciprocals as the device's division makes them (rx_fdiv.h)
+      double* d = nullptr;
+      RX_HIP(hipMalloc(&d, sizeof(double) * ns));
+      ctx->mech_bufs.push_back(d);
+      k_recip_table<<<1, 64, 0, ctx->stream>>>(m.mm, d, ns);
+      RX_HIP(hipGetLastError());
+      m.rmm = d;
+    }
     m.mtot = 0.0;
     for (int s = 0; s < ns; ++s) m.mtot += mech->mmass[s];
     {
@@ -729,6 +773,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   if (!ctx) return RX_OK;
   if (ctx->n_children > 0) return RX_ERR_STATE;  // an SST context still runs on this stream / communicator
   (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)rx_settle_u(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   // the captured solve first: a graph holding RCCL work keeps the communicator's persistent resources, and
   // ncclCommDestroy waits for them (the self-halo RCCL test hung here with the graph destroyed after the comm)
@@ -741,7 +786,8 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.pass_lo, ctx->fs.part_pass, ctx->bs.pass_lo, ctx->bs.part_pass,
-                  ctx->fs.slot, ctx->bs.slot, ctx->fs.ring, ctx->bs.ring, ctx->ring_xoff, ctx->send_idx, ctx->grad_list, ctx->spmv_rows, ctx->sendbuf, ctx->rms_sum,
+                  ctx->fs.slot, ctx->bs.slot, ctx->fs.ring, ctx->bs.ring, ctx->fs.rpart_lvl, ctx->fs.rlvl_ptr,
+                  ctx->bs.rpart_lvl, ctx->bs.rlvl_ptr, ctx->ring_xoff, ctx->send_idx, ctx->grad_list, ctx->spmv_rows, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,
                   ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar, ctx->jinv,
                   ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
@@ -767,6 +813,7 @@ int rx_field_size(const rx_ctx* ctx, rx_field f, int64_t* count) {
 
 int rx_upload(rx_ctx* ctx, rx_field f, const double* host, int64_t count) {
   if (!ctx || f < 0 || f >= RX_F_COUNT || count != ctx->fcount[f] || !host) return RX_ERR_ARG;
+  if (int rc = rx_settle_u(ctx)) return rc;
   RX_HIP(hipMemcpyAsync(ctx->f[f], host, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   if (f == RX_F_ILU) ctx->ilu_valid = 1;  // a caller-provided factor
   // a loaded solution is also the Solution_Old (CVariable construction / LoadRestart)
@@ -778,6 +825,7 @@ int rx_upload(rx_ctx* ctx, rx_field f, const double* host, int64_t count) {
 
 int rx_download(rx_ctx* ctx, rx_field f, double* host, int64_t count) {
   if (!ctx || f < 0 || f >= RX_F_COUNT || count != ctx->fcount[f] || !host) return RX_ERR_ARG;
+  if (int rc = rx_settle_u(ctx)) return rc;
   if (f == RX_F_RES || f == RX_F_JAC) {
     int rc = ensure_assembled(ctx);
     if (rc && rc != RX_ERR_STATE) return rc;
@@ -802,6 +850,7 @@ int rx_bsr_pattern(const rx_ctx* ctx, int64_t* row_ptr, int64_t* col) {
 
 int rx_sync(rx_ctx* ctx) {
   if (!ctx) return RX_ERR_ARG;
+  if (int rc = rx_settle_u(ctx)) return rc;
   RX_HIP(hipStreamSynchronize(ctx->stream));
   return rx_check_error(ctx);
 }
@@ -983,7 +1032,8 @@ int rx_linear_solve(rx_ctx* ctx, int* iters, double* resid) {
 
 int rx_explicit_euler(rx_ctx* ctx, double* res_rms) {
   if (!ctx || ctx->kind != RX_KIND_FLOW) return RX_ERR_ARG;
-  int rc;
+  int rc = rx_settle_u(ctx);
+  if (rc) return rc;
   {
     RxPhase ph(ctx, RX_K_UPDATE);
     if (res_rms && (rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RES]))) return rc;
@@ -999,7 +1049,10 @@ int rx_set_primitive(rx_ctx* ctx, int ext_iter, int64_t* n_nonphys) {
   {
     RxPhase ph(ctx, RX_K_PRIMITIVE);
     RX_HIP(hipMemsetAsync(ctx->err + 2, 0, sizeof(int), ctx->stream));
-    const int rc = rx_launch_set_primitive(ctx, ext_iter);
+    // with the post-update exchange still running on comm_stream (rx_la_u_exchange_begin), the owned points first
+    // (they read no halo value), then the halo points once it has arrived; each point's arithmetic is unchanged
+    int rc = rx_launch_set_primitive(ctx, ext_iter, 0, ctx->u_pending ? ctx->Nd : ctx->N);
+    if (!rc && ctx->u_pending && !(rc = rx_settle_u(ctx))) rc = rx_launch_set_primitive(ctx, ext_iter, ctx->Nd, ctx->N);
     if (rc) return rc;
   }
   if (!n_nonphys) return RX_OK;
@@ -1013,7 +1066,8 @@ int rx_set_primitive(rx_ctx* ctx, int ext_iter, int64_t* n_nonphys) {
 // ExplicitRK_Iteration (solver_direct_reactive.cpp:2456-2493): stage iRKStep with RK_ALPHA_COEFF[iRKStep].
 int rx_explicit_rk(rx_ctx* ctx, int rk_step, double alpha, double* res_rms) {
   if (!ctx || ctx->kind != RX_KIND_FLOW || rk_step < 0) return RX_ERR_ARG;
-  int rc;
+  int rc = rx_settle_u(ctx);
+  if (rc) return rc;
   {
     RxPhase ph(ctx, RX_K_UPDATE);
     if (res_rms && (rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RES]))) return rc;
@@ -1059,7 +1113,8 @@ namespace {
 // :601-653), then FGMRES + RMS + update replayed as one hipGraph.
 int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   const bool sst = ctx->kind == RX_KIND_SST;
-  int rc = ensure_assembled(ctx);
+  int rc = rx_settle_u(ctx);  // (nothing waits on an event recorded outside the capture below)
+  if (!rc) rc = ensure_assembled(ctx);
   if (rc) return rc;
   const int ls = ctx->cfg.lin_solver;
   if ((rc = rx_la_krylov_alloc(ctx, (ls == RX_LIN_FGMRES || ls == RX_LIN_RESTARTED_FGMRES) ? ctx->cfg.lin_iter : 3)))
@@ -1097,6 +1152,9 @@ int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
     } else {
       if ((rc = enqueue_solve(ctx))) return rc;
     }
+    // the flow's Set_MPI_Solution after the update, on comm_stream (rx_u_exchange_deferred), overlapping the owned
+    // points of the next SetPrimitive_Variables
+    if (rx_u_exchange_deferred(ctx) && (rc = rx_la_u_exchange_begin(ctx))) return rc;
   }
   if (res_rms && (rc = rx_la_rms_read(ctx, res_rms))) return rc;
   int it = 0;

@@ -905,7 +905,8 @@ int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
 
 int rx_bc_flow(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_FLOW || !ctx->bc_on) return RX_ERR_ARG;
-  int rc = ctx->cfg.implicit ? rx_ensure_assembled(ctx) : RX_OK;
+  int rc = rx_settle_u(ctx);  // the walls write U
+  if (!rc && ctx->cfg.implicit) rc = rx_ensure_assembled(ctx);
   if (rc) return rc;
   RxPhase ph(ctx, RX_K_BC);
   if (ctx->bc_pending) {  // boundary fluxes launched by rx_residual_zero on the side stream
@@ -920,6 +921,7 @@ int rx_bc_flow(rx_ctx* ctx) {
 
 int rx_bc_sst(rx_ctx* ctx) {
   if (!ctx || ctx->kind != RX_KIND_SST || !ctx->flow || !ctx->flow->bc_on) return RX_ERR_ARG;
+  if (int rc0 = rx_settle_u(ctx)) return rc0;
   const rx_ctx* fl = ctx->flow;
   RxPhase ph(ctx, RX_K_SST_BC);
   if (fl->bc_pending) RX_HIP(hipStreamWaitEvent(ctx->stream, fl->bc_join, 0));  // ghost states of this iteration

@@ -57,12 +57,42 @@ int stage_alloc(rx_ctx* ctx) {
 
 int rx_la_exchange(rx_ctx* ctx, double* f, int stride) { return rx_la_exchange_on(ctx, f, stride, ctx->stream); }
 
+// The flow's post-update Set_MPI_Solution (solver_direct_reactive.cpp:2403) with RCCL: k_update's owned rows are
+// final when the solve graph ends, and SetPrimitive_Variables' owned points do not read the halo, so the exchange
+// runs on comm_stream while they are computed (rx_set_primitive), and the halo points wait for it.
+bool rx_u_exchange_deferred(const rx_ctx* ctx) {
+  return ctx->kind == RX_KIND_FLOW && ctx->comm_stream && ctx->u_join && !ctx->has_hcomm && ctx->n_neigh > 0 &&
+         getenv("RX_NO_U_OVERLAP") == nullptr;
+}
+
+int rx_la_u_exchange_begin(rx_ctx* ctx) {
+  RX_HIP(hipEventRecord(ctx->comm_fork, ctx->stream));
+  RX_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->comm_fork, 0));
+  const int rc = rx_la_exchange_on(ctx, ctx->f[RX_F_U], ctx->nVar, ctx->comm_stream);
+  if (rc) return rc;
+  RX_HIP(hipEventRecord(ctx->u_join, ctx->comm_stream));
+  ctx->u_pending = true;
+  return RX_OK;
+}
+
+int rx_settle_u(rx_ctx* ctx) {
+  rx_ctx* f = ctx->kind == RX_KIND_SST && ctx->flow ? ctx->flow : ctx;
+  if (!f->u_pending) return RX_OK;
+  RX_HIP(hipStreamWaitEvent(ctx->stream, f->u_join, 0));  // an SST context shares its flow's stream
+  f->u_pending = false;
+  return RX_OK;
+}
+
 // The exchange on stream st (the context stream, or comm_stream for the overlapped gradient exchange; the host
 // transport always runs on the context stream).
 int rx_la_exchange_on(rx_ctx* ctx, double* f, int stride, hipStream_t st) {
   if (!ctx->distributed() || ctx->n_neigh == 0) return RX_OK;
   if (stride > ctx->halo_stride) return RX_ERR_ARG;
   if (ctx->has_hcomm) st = ctx->stream;
+  if (st == ctx->stream) {  // the send buffer and the communicator are free once a pending U exchange is waited for
+    const int rc0 = rx_settle_u(ctx);
+    if (rc0) return rc0;
+  }
   if (ctx->n_send > 0) {
     const int64_t n = ctx->n_send * stride;
     k_pack<<<(int)((n + 255) / 256), 256, 0, st>>>(ctx->n_send, stride, ctx->send_idx, f, ctx->sendbuf);
@@ -103,6 +133,7 @@ int rx_la_exchange_on(rx_ctx* ctx, double* f, int stride, hipStream_t st) {
 int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count) {
   if (!ctx->distributed()) return RX_OK;
   if (count > kGatherStride) return RX_ERR_ARG;
+  if (int rc0 = rx_settle_u(ctx)) return rc0;  // one RCCL operation of the communicator at a time
   if (ctx->has_hcomm) {
     double* h = ctx->h_stage + (ctx->n_send + (ctx->N - ctx->Nd)) * ctx->halo_stride;
     RX_HIP(hipMemcpyAsync(h, in, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
@@ -169,6 +200,7 @@ int rx_comm_init(rx_ctx* ctx, int nranks, int rank, const void* id128) {
   RX_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
   RX_HIP(hipEventCreateWithFlags(&ctx->comm_fork, hipEventDisableTiming));
   RX_HIP(hipEventCreateWithFlags(&ctx->comm_join, hipEventDisableTiming));
+  RX_HIP(hipEventCreateWithFlags(&ctx->u_join, hipEventDisableTiming));
   return comm_attached(ctx);
 }
 
@@ -188,7 +220,8 @@ int rx_comm_init_host(rx_ctx* ctx, int nranks, int rank, const rx_host_comm* ops
 int rx_halo_exchange(rx_ctx* ctx, rx_field f) {
   if (!ctx || f < 0 || f >= RX_F_COUNT || ctx->fcount[f] % ctx->N != 0) return RX_ERR_ARG;
   if (f == RX_F_JAC || f == RX_F_ILU) return RX_ERR_ARG;
-  const int rc = rx_la_exchange(ctx, ctx->f[f], (int)(ctx->fcount[f] / ctx->N));
+  int rc = rx_settle_u(ctx);
+  if (!rc) rc = rx_la_exchange(ctx, ctx->f[f], (int)(ctx->fcount[f] / ctx->N));
   if (rc) return rc;
   RX_HIP(hipStreamSynchronize(ctx->stream));
   return RX_OK;
@@ -219,6 +252,9 @@ void rx_comm_free(rx_ctx* ctx) {
     (void)hipStreamDestroy(ctx->comm_stream);
     (void)hipEventDestroy(ctx->comm_fork);
     (void)hipEventDestroy(ctx->comm_join);
+    if (ctx->u_join) (void)hipEventDestroy(ctx->u_join);
+    ctx->u_join = nullptr;
+    ctx->u_pending = false;
     ctx->comm_stream = nullptr;
   }
   if (ctx->gather) (void)hipFree(ctx->gather);

@@ -56,6 +56,12 @@ struct rx_ctx {
   bool defer_exchange = false;  // the preconditioner apply leaves its closing halo exchange to the caller
   hipStream_t comm_stream = nullptr;  // RCCL transport only
   hipEvent_t comm_fork = nullptr, comm_join = nullptr;
+  // the flow's post-update Set_MPI_Solution runs on comm_stream after the solve (rx_la_u_exchange_begin) while
+  // SetPrimitive_Variables computes the owned points; u_pending until the context stream has waited for u_join
+  // (rx_settle_u: at rx_set_primitive's halo points, and before anything else that reads / writes U, exchanges or
+  // all-reduces)
+  hipEvent_t u_join = nullptr;
+  bool u_pending = false;
   int64_t n_global = 0;         // owned points over all ranks
   double* rms_sum = nullptr;    // [32] per-variable sums of squares (device)
   rx_cfg cfg{};
@@ -107,9 +113,12 @@ struct rx_ctx {
     int32_t* part_pass = nullptr; // [npart + 1] each partition's passes
     int nlevels = 0, maxwidth = 0, maxlev = 0;  // maxlev: most levels of one partition
     // k_ilu_apply_ring (rx_sweeps.hip): per schedule slot {ring row, far row or -1}, the LDS rows the slot's result
-    // is written to; ring_rows = kIluRing * maxwidth + the most far rows of one partition
+    // is written to; its sub-level tables (levels wider than rows per pass / groups split, rx_api.hip) like part_lvl /
+    // lvl_ptr; ring_rows = kIluRing * rmaxwidth + the most far rows of one partition
     int32_t* ring = nullptr;
-    int ring_rows = 0;
+    int32_t* rpart_lvl = nullptr;
+    int32_t* rlvl_ptr = nullptr;
+    int ring_rows = 0, rmaxlev = 0, rmaxwidth = 0;
   } fs, bs;
   int32_t* ring_xoff = nullptr;  // [nnzb] LDS row of x_col(k) for the blocks the sweeps read (L: fs ring, U: bs ring)
   double* dlu = nullptr;        // [N][nVar^2] factorised diagonal blocks (LU-SGS)
@@ -213,6 +222,9 @@ constexpr int kHaloMaxStride = 64;  // minimum doubles per point of the exchange
 // halo exchange of a device array with `stride` doubles per point (no-op without communicator)
 int rx_la_exchange(rx_ctx* ctx, double* f, int stride);
 int rx_la_exchange_on(rx_ctx* ctx, double* f, int stride, hipStream_t st);
+bool rx_u_exchange_deferred(const rx_ctx* ctx);  // the flow's post-update exchange overlaps SetPrimitive_Variables
+int rx_la_u_exchange_begin(rx_ctx* ctx);          // that exchange, on comm_stream
+int rx_settle_u(rx_ctx* ctx);                     // the context stream waits for it (an SST context: its flow's)
 // out[i] = sum over ranks of in[i] (in == out allowed), ordered on the context stream; no-op
 // without communicator
 int rx_la_allreduce(rx_ctx* ctx, const double* in, double* out, int count);
@@ -243,13 +255,14 @@ struct RxPhase {
 // kernel launchers (rx_kernels.hip)
 int rx_launch_ausm_node(rx_ctx* ctx);
 int rx_launch_muscl(rx_ctx* ctx);
-int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter);
+int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter, int64_t lo, int64_t hi);  // points [lo, hi)
 int rx_launch_ausm_edge(rx_ctx* ctx);
 bool rx_fuse_conv(int nDim);
 // levels of the ILU(0) sweeps' LDS ring (k_ilu_apply_ring): a row's result is read from the ring slot of its level
 // by the rows up to kIluRing - 1 levels later, from a per-partition "far" slot by later ones
 constexpr int kIluRing = 4;
 int rx_ilu_ring_rpb(int nv);  // rows per pass of k_ilu_apply_ring (1024 threads)
+int rx_ilu_ring_groups();     // wavefront groups of k_ilu_apply_ring taking turns by level (RX_ILU_RING_G, default 2)
 int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);
 int rx_launch_source(rx_ctx* ctx);

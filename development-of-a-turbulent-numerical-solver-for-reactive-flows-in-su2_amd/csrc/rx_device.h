@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rx_fdiv.h"
+
 namespace rx {
 
 #ifndef RX_SUMM_TILE
@@ -43,8 +45,18 @@ struct DevMech {
   const double *pw25;           // [ns][ns] pow(M_b / M_a, 0.25)
   const double *mij;            // [ns][ns] sqrt(M_a M_b / (M_a + M_b))
   const double *dvs;            // [ns][ns] cbrt(V_a) + cbrt(V_b)
+  const double *rmm;            // [ns] rx_recip(mm[s]).y, made on the device (k_recip_table): quotients by M_s
   uint32_t neg_reac[kMaxNR], neg_prod[kMaxNR];  // species masks with negative rate exponents
 };
+
+// the divisor M_s with its reciprocal (rx_fdiv.h); host passes divide directly
+__device__ __host__ inline Recip mm_recip(const DevMech& m, int s) {
+#if RX_FDIV_DEV
+  return Recip{m.mm[s], m.rmm[s]};
+#else
+  return Recip{m.mm[s], 0.0};
+#endif
+}
 
 // MathTools::GetSpline (Common/src/Tools/spline.cpp:62-77). Out of range sets *err (the reference
 // throws std::out_of_range).
@@ -59,10 +71,11 @@ __device__ __host__ inline double spline(const DevMech& m, int prop, int s, doub
     return 0.0;
   }
   const double h = x[1] - x0;
-  unsigned long klo = (unsigned long)((T - x0) / h + 1);
+  const Recip rh = rx_recip(h);  // three quotients by h (rx_fdiv.h: the same doubles as `/`)
+  unsigned long klo = (unsigned long)(rx_div(T - x0, rh) + 1);
   if (klo > (unsigned long)(m.ntab - 1)) klo = m.ntab - 1;  // T == Tmax reads x[n] in the reference
-  const double a = (x[klo] - T) / h;
-  const double b = (T - x[klo - 1]) / h;
+  const double a = rx_div(x[klo] - T, rh);
+  const double b = rx_div(T - x[klo - 1], rh);
   return a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0;
 }
 
@@ -76,7 +89,7 @@ __device__ __host__ inline void molar_from_mass(const DevMech& m, const double* 
     double y = ys[s];
     if (y < 0.0) y = 1.0e-30;
     yc[s] = y;
-    xs[s] = y / m.mm[s];
+    xs[s] = rx_div(y, mm_recip(m, s));
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) sy += yc[s];
@@ -123,8 +136,11 @@ __device__ __host__ inline void ausm_scalars(const double* Vi, const double* Vj,
   for (int d = 0; d < NDIM; ++d) Area += Normal[d] * Normal[d];
   Area = sqrt(Area);
   s.Area = Area;
+  {
+    const Recip rA = rx_recip(Area);  // (rx_fdiv.h: the same doubles as `/`)
 #pragma unroll
-  for (int d = 0; d < NDIM; ++d) s.UN[d] = Normal[d] / Area;
+    for (int d = 0; d < NDIM; ++d) s.UN[d] = rx_div(Normal[d], rA);
+  }
   s.rho_i = Vi[RHO];
   s.rho_j = Vj[RHO];
   s.p_i = Vi[P_];
@@ -139,7 +155,8 @@ __device__ __host__ inline void ausm_scalars(const double* Vi, const double* Vj,
   s.pv_j = pvj;
   const double mss = 0.5 * (Vi[A_] + Vj[A_]);
   s.mss = mss;
-  const double mL = pvi / mss, mR = pvj / mss;
+  const Recip rmss = rx_recip(mss);
+  const double mL = rx_div(pvi, rmss), mR = rx_div(pvj, rmss);
   s.mL = mL;
   s.mR = mR;
   const double mF2 = 0.5 * (mL * mL + mR * mR);
@@ -159,20 +176,21 @@ __device__ __host__ inline void ausm_scalars(const double* Vi, const double* Vj,
     pLP = 0.25 * (mL + 1.0) * (mL + 1.0) * (2.0 - mL) + alpha * mL * (mL * mL - 1.0) * (mL * mL - 1.0);
   } else {
     mLP = 0.5 * (mL + fabs(mL));
-    pLP = 0.5 * (1.0 + fabs(mL) / mL);
+    pLP = 0.5 * (1.0 + rx_div(fabs(mL), rx_recip(mL)));
   }
   if (fabs(mR) < 1.0) {
     mRM = -0.25 * (mR - 1.0) * (mR - 1.0) - beta * (mR * mR - 1.0) * (mR * mR - 1.0);
     pRM = 0.25 * (mR - 1.0) * (mR - 1.0) * (2.0 + mR) - alpha * mR * (mR * mR - 1.0) * (mR * mR - 1.0);
   } else {
     mRM = 0.5 * (mR - fabs(mR));
-    pRM = 0.5 * (1.0 - fabs(mR) / mR);
+    pRM = 0.5 * (1.0 - rx_div(fabs(mR), rx_recip(mR)));
   }
   s.pLP = pLP;
   s.pRM = pRM;
   const double kP = 0.25, sigma = 1.0;
   double m12 = mLP + mRM;
-  m12 -= kP / fa * fmax(1.0 - sigma * mF2, 0.0) * (s.p_j - s.p_i) / (0.5 * (s.rho_i + s.rho_j) * mss * mss);
+  m12 -= rx_div(rx_div(kP, rx_recip(fa)) * fmax(1.0 - sigma * mF2, 0.0) * (s.p_j - s.p_i),
+                rx_recip(0.5 * (s.rho_i + s.rho_j) * mss * mss));
   s.m12 = m12;
   s.mLF = 0.5 * (m12 + fabs(m12));
   s.mRF = 0.5 * (m12 - fabs(m12));
@@ -183,7 +201,7 @@ __device__ __host__ inline void ausm_scalars(const double* Vi, const double* Vj,
   s.pLF = pLF;
   s.factor = fmax(1.0 - sigma * mF2, 0.0);
   s.fpos = (s.factor > 0.0) ? 1.0 : 0.0;
-  s.sign_m12 = (m12 != 0.0) ? fabs(m12) / m12 : 0.0;
+  s.sign_m12 = (m12 != 0.0) ? rx_div(fabs(m12), rx_recip(m12)) : 0.0;
 }
 
 // Phi (the convected state) for index v of the conservative vector.
@@ -216,35 +234,40 @@ __device__ __host__ inline AusmCol ausm_col_impl(const AusmEdge& s, double Sib, 
   const double kP = 0.25, sigma = 1.0, beta = 0.125, Ku = 0.75;
   const double mL = s.mL, mR = s.mR, mss = s.mss, fa = s.fa, alpha = s.alpha;
   const double rho_i = s.rho_i, rho_j = s.rho_j;
+  // divisors shared by several quotients, each with its reciprocal (rx_fdiv.h: the same doubles as `/`)
+  const Recip rri = rx_recip(rho_i), rrj = rx_recip(rho_j);
   double MLD = 0.0, MRD = 0.0;
   if (b == 0) {
-    MLD = -mL / rho_i;
-    MRD = -mR / rho_j;
+    MLD = rx_div(-mL, rri);
+    MRD = rx_div(-mR, rrj);
   } else if (b <= NDIM) {
     const double unb = pick<NDIM>(s.UN, b - 1);
-    MLD = unb / (rho_i * mss);
-    MRD = unb / (rho_j * mss);
+    MLD = rx_div(unb, rx_recip(rho_i * mss));
+    MRD = rx_div(unb, rx_recip(rho_j * mss));
   }
   double MPL, MPR;
   if (fabs(mL) < 1.0) MPL = MLD * (0.5 * (mL + 1.0) + 4.0 * beta * mL * (mL * mL - 1.0));
-  else MPL = MLD * (0.5 * (1.0 + fabs(mL) / mL));
+  else MPL = MLD * (0.5 * (1.0 + rx_div(fabs(mL), rx_recip(mL))));
   if (fabs(mR) < 1.0) MPR = MRD * (0.5 * (1.0 - mR) + 4.0 * beta * mR * (1.0 - mR * mR));
-  else MPR = MRD * (0.5 * (1.0 - fabs(mR) / mR));
+  else MPR = MRD * (0.5 * (1.0 - rx_div(fabs(mR), rx_recip(mR))));
   double SL = 0.0, SR = 0.0;
   if (s.mF2 == s.mRef2) {
-    SL = MLD * mL * (1.0 - s.mF) / s.mF;
-    SR = MRD * mR * (1.0 - s.mF) / s.mF;
+    const Recip rmF = rx_recip(s.mF);
+    SL = rx_div(MLD * mL * (1.0 - s.mF), rmF);
+    SR = rx_div(MRD * mR * (1.0 - s.mF), rmF);
   }
   const double MD = 0.5 * (rho_i + rho_j);
   const double dp = s.p_j - s.p_i;
-  double MEL = -kP / (mss * mss * fa * fa * MD * MD) *
+  const Recip rme = rx_recip(mss * mss * fa * fa * MD * MD);
+  double MEL = rx_div(-kP, rme) *
                ((s.fpos * sigma * mL * MLD * dp * fa * MD) + (s.factor * Sib * fa * MD) + (s.factor * dp * MD * SL));
-  double MER = kP / (mss * mss * fa * fa * MD * MD) *
+  double MER = rx_div(kP, rme) *
                ((s.fpos * sigma * mR * MRD * (s.p_i - s.p_j) * fa * MD) + (s.factor * Sjb * fa * MD) -
                 (s.factor * dp * MD * SR));
   if (b == 0) {
-    MEL -= kP / (mss * mss * fa * MD * MD) * 0.5 * s.factor * dp;
-    MER -= kP / (mss * mss * fa * MD * MD) * 0.5 * s.factor * dp;
+    const double kq = rx_div(kP, rx_recip(mss * mss * fa * MD * MD));  // kP / (mss^2 fa MD^2), both rows
+    MEL -= kq * 0.5 * s.factor * dp;
+    MER -= kq * 0.5 * s.factor * dp;
   }
   AusmCol c;
   c.PlL = 0.5 * (MPL - MEL) * (1.0 + s.sign_m12);
@@ -262,12 +285,12 @@ __device__ __host__ inline AusmCol ausm_col_impl(const AusmEdge& s, double Sib, 
   double PEL = Ku * s.pRM * mss * ((PPL * (rho_i + rho_j) * fa * dvn) + (s.pLP * (rho_i + rho_j) * dvn * SL));
   double PER = Ku * s.pLP * mss * ((PPR * (rho_i + rho_j) * fa * dvn) + (s.pRM * (rho_i + rho_j) * dvn * SR));
   if (b == 0) {
-    PEL += Ku * s.pRM * mss * s.pLP * fa * (dvn + (rho_i + rho_j) * s.pv_i / rho_i);
-    PER += Ku * s.pLP * mss * s.pRM * fa * (dvn - (rho_i + rho_j) * s.pv_j / rho_j);
+    PEL += Ku * s.pRM * mss * s.pLP * fa * (dvn + rx_div((rho_i + rho_j) * s.pv_i, rri));
+    PER += Ku * s.pLP * mss * s.pRM * fa * (dvn - rx_div((rho_i + rho_j) * s.pv_j, rrj));
   } else if (b <= NDIM) {
     const double unb = pick<NDIM>(s.UN, b - 1);
-    PEL -= Ku * s.pRM * mss * s.pLP * fa * (rho_i + rho_j) * unb / rho_i;
-    PER += Ku * s.pLP * mss * s.pRM * fa * (rho_i + rho_j) * unb / rho_j;
+    PEL -= rx_div(Ku * s.pRM * mss * s.pLP * fa * (rho_i + rho_j) * unb, rri);
+    PER += rx_div(Ku * s.pLP * mss * s.pRM * fa * (rho_i + rho_j) * unb, rrj);
   }
   c.PDL = s.pLP * Sib + s.p_i * PPL - PEL;
   c.PDR = s.pRM * Sjb + s.p_j * PPR - PER;

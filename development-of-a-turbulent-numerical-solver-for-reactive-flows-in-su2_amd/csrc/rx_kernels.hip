@@ -258,7 +258,7 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
 #define RX_PRIM_UNROLL 16  // >= NS: the species-pair loops fully unrolled (rolled: primitives 1.22 -> 1.43 ms at C3)
 #endif
 template <int NS, int NDIM>
-__global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, DevMech m, PrimParams P, double* __restrict__ Ug,
+__global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int lo, int N, DevMech m, PrimParams P, double* __restrict__ Ug,
                                                           double* __restrict__ Vg, const double* __restrict__ Uold,
                                                           const double* __restrict__ tke,
                                                           const double* __restrict__ mut, double* __restrict__ dPdU,
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int N, Dev
                                                           double* __restrict__ eddy, int* __restrict__ err) {
   constexpr int nVar = NS + NDIM + 2, nPV = NS + NDIM + 5;
   constexpr int VX = 1, P_ = NDIM + 1, RHO = NDIM + 2, A_ = NDIM + 4, RHOS = NDIM + 5;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = lo + (int)(blockIdx.x * blockDim.x + threadIdx.x);  // points [lo, N)
   if (i >= N) return;
   double U[nVar], V[nPV];
 #pragma unroll
@@ -1583,15 +1583,16 @@ int rx_check_error(rx_ctx* ctx) {
 #endif  // !RX_NS
 
 #if RX_NS
-int RX_NSFN(rx_launch_set_primitive)(rx_ctx* ctx, int ext_iter) {
+int RX_NSFN(rx_launch_set_primitive)(rx_ctx* ctx, int ext_iter, int64_t lo, int64_t hi) {  // points [lo, hi)
+  if (hi <= lo) return RX_OK;
   const rx_cfg& c = ctx->cfg;
   const int ignite = c.ignition && (int64_t)ext_iter < c.ignition_iter ? 1 : 0;
   if (ignite && (c.fuel_index < 0 || c.fuel_index >= ctx->ns || c.oxidizer_index < 0 || c.oxidizer_index >= ctx->ns))
     return RX_ERR_ARG;
   PrimParams P{c.t_min, c.t_max, c.T_ref, c.E_ref, c.R_ref, c.p_ref, c.visc_ref, c.cond_ref, c.vel_ref, c.len_ref,
                ext_iter, c.clip_temp, c.rans, ignite, c.fuel_index, c.oxidizer_index, c.ignition_temp};
-  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_set_primitive<NS_, ND_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
-                            (int)ctx->N, ctx->mech, P, ctx->f[RX_F_U], ctx->f[RX_F_V], ext_iter > 0 ? ctx->uold : nullptr,
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_set_primitive<NS_, ND_><<<blocks(hi - lo), kBlock, 0, ctx->stream>>>(
+                            (int)lo, (int)hi, ctx->mech, P, ctx->f[RX_F_U], ctx->f[RX_F_V], ext_iter > 0 ? ctx->uold : nullptr,
                             ctx->f[RX_F_TKE], ctx->f[RX_F_MUT], ctx->f[RX_F_DPDU], ctx->f[RX_F_DTDU], ctx->f[RX_F_MU],
                             ctx->f[RX_F_KAPPA], ctx->f[RX_F_DIJ], ctx->f[RX_F_EDDY], ctx->err)));
   RX_HIP(hipGetLastError());
@@ -1736,7 +1737,7 @@ int RX_NSFN(rx_launch_asm_visc)(rx_ctx* ctx, int with_src, int fused_conv) {
 #endif  // RX_NS
 
 #if !RX_NS
-RX_NS_DISPATCH(rx_launch_set_primitive, (rx_ctx * ctx, int ext_iter), (ctx, ext_iter))
+RX_NS_DISPATCH(rx_launch_set_primitive, (rx_ctx * ctx, int ext_iter, int64_t lo, int64_t hi), (ctx, ext_iter, lo, hi))
 RX_NS_DISPATCH(rx_launch_muscl, (rx_ctx * ctx), (ctx))
 RX_NS_DISPATCH(rx_launch_ausm_node, (rx_ctx * ctx), (ctx))
 RX_NS_DISPATCH(rx_launch_ausm_edge, (rx_ctx * ctx), (ctx))

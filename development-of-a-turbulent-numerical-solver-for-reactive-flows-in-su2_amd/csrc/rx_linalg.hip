@@ -254,7 +254,8 @@ int rx_la_implicit_update(rx_ctx* ctx) {
                                                   ctx->cfg.relaxation, ctx->vol, ctx->f[RX_F_DT], 0, nullptr,
                                                   ctx->f[RX_F_U], ctx->bc_wall, ctx->uold);
   RX_HIP(hipGetLastError());
-  return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
+  // with RCCL, implicit_solve starts the exchange on comm_stream after the solve (rx_la_u_exchange_begin)
+  return rx_u_exchange_deferred(ctx) ? RX_OK : rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }
 
 int rx_la_explicit_update(rx_ctx* ctx) {
@@ -265,7 +266,7 @@ int rx_la_explicit_update(rx_ctx* ctx) {
                                                   ctx->vol, ctx->f[RX_F_DT], 1, nullptr, ctx->f[RX_F_U], ctx->bc_wall,
                                                   ctx->uold);
   RX_HIP(hipGetLastError());
-  return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
+  return rx_u_exchange_deferred(ctx) ? rx_la_u_exchange_begin(ctx) : rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }
 
 // ExplicitRK_Iteration stage: Set_OldSolution at stage 0 (integration_time.cpp:162), then
@@ -279,5 +280,5 @@ int rx_la_rk_update(rx_ctx* ctx, int stage, double alpha) {
                                                   ctx->vol, ctx->f[RX_F_DT], 2, ctx->uold, ctx->f[RX_F_U], ctx->bc_wall,
                                                   ctx->uold);
   RX_HIP(hipGetLastError());
-  return rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
+  return rx_u_exchange_deferred(ctx) ? rx_la_u_exchange_begin(ctx) : rx_la_exchange(ctx, ctx->f[RX_F_U], ctx->nVar);
 }

@@ -1788,7 +1788,11 @@ template <int NV, int TB>
 constexpr int ring_rpb() {
   return (TB / 64) * (64 / NV);  // rows per pass: whole rows per wavefront (the backward's v exchange is wave-local)
 }
-template <int NV, int TB, int MB>
+// G > 1 (round 5): the workgroup's wavefronts form G groups that take turns by level (group l mod G computes level l),
+// so a wavefront's loads for its next level are issued G levels ahead: G - 1 other levels run while they are in flight,
+// with the same registers per wavefront. A group holds rows per pass / G rows; the host splits wider levels into
+// sub-levels (rx_api.hip), which the level tables passed here describe.
+template <int NV, int TB, int MB, int G>
 __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
     const int32_t* __restrict__ fpart_lvl, const int32_t* __restrict__ flvl_ptr, const int4* __restrict__ fslot,
     const int2* __restrict__ fring, const int32_t* __restrict__ bpart_lvl, const int32_t* __restrict__ blvl_ptr,
@@ -1802,9 +1806,13 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
   double* xs = lds;                                               // [ring_rows][NV]
   double* v = lds + (size_t)ring_rows * NV;                       // [RPB][NV] backward: x_i - sum, per row
   int32_t* lp = reinterpret_cast<int32_t*>(v + (size_t)RPB * NV);  // the sweep's level table for this partition
+  constexpr int WPG = (TB / 64) / G;  // wavefronts per group
+  static_assert(G >= 1 && (TB / 64) % G == 0, "whole wavefronts per group");
   const int p = blockIdx.x;
-  const int wl = threadIdx.x & 63;
-  const int rl = (int)(threadIdx.x >> 6) * RW + wl / NV;
+  const int wl = threadIdx.x & 63, wave = (int)(threadIdx.x >> 6);
+  const int g = wave / WPG;                       // this wavefront's group: it computes the levels l = g mod G
+  const int rl = (wave % WPG) * RW + wl / NV;      // row of the level within the group
+  const int vr = wave * RW + wl / NV;              // the backward's v row (exchanged inside the wavefront)
   const int a = wl - (wl / NV) * NV;
   const bool lane = wl < RW * NV;
   // ---- forward: x_i = b_i - sum_k L_ik x_col(k)
@@ -1812,13 +1820,18 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
     const int l0 = fpart_lvl[p], nl = fpart_lvl[p + 1] - l0;
     for (int q = threadIdx.x; q <= nl; q += TB) lp[q] = flvl_ptr[l0 + q];
     __syncthreads();
+    // the slot loads — the last memory operations of a level — are issued by every lane on every path (a clamped,
+    // valid address when out of range): the loads a level issues before them are then always followed by exactly
+    // these two, so the compiler's vmcnt waits count them exactly and the next level's loads stay in flight (a slot
+    // load on some paths only made it wait for all of them, vmcnt(0), right after they were issued). The row loads
+    // themselves stay predicated (idle rows and missing blocks issue nothing).
     auto slot_at = [&](int l, int4& sl, int2& w) {
-      if (!lane || l >= nl) return false;
-      const int r = lp[l] + rl;
-      if (r >= lp[l + 1]) return false;
-      sl = fslot[r];
-      w = fring[r];
-      return true;
+      const int lc = l < nl ? l : nl - 1;
+      const int r = lp[lc] + rl;
+      const bool ok = lane && l < nl && r < lp[lc + 1];
+      sl = fslot[ok ? r : 0];
+      w = fring[ok ? r : 0];
+      return ok;
     };
     int4 sl = make_int4(0, 0, 0, 0), sln = sl;
     int2 w = make_int2(0, -1), wn = w;
@@ -1835,10 +1848,14 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
           for (int c = 0; c < NV; ++c) F[t][c] = blk[c];
         }
     };
-    bool act = slot_at(0, sl, w);
+    bool act = slot_at(g, sl, w);
     if (act) issue();
-    bool actn = slot_at(1, sln, wn);
+    bool actn = slot_at(g + G, sln, wn);
     for (int l = 0; l < nl; ++l) {
+      if (G > 1 && l % G != g) {  // another group's level (wavefront-uniform)
+        lds_barrier();
+        continue;
+      }
       if (act) {
         double xi = bi;
 #pragma unroll
@@ -1866,7 +1883,7 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
       sl = sln;
       w = wn;
       if (act) issue();
-      actn = slot_at(l + 2, sln, wn);
+      actn = slot_at(l + 2 * G, sln, wn);
       lds_barrier();
     }
   }
@@ -1876,13 +1893,13 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
     const int l0 = bpart_lvl[p], nl = bpart_lvl[p + 1] - l0;
     for (int q = threadIdx.x; q <= nl; q += TB) lp[q] = blvl_ptr[l0 + q];
     __syncthreads();
-    auto slot_at = [&](int l, int4& sl, int2& w) {
-      if (!lane || l >= nl) return false;
-      const int r = lp[l] + rl;
-      if (r >= lp[l + 1]) return false;
-      sl = bslot[r];
-      w = bring[r];
-      return true;
+    auto slot_at = [&](int l, int4& sl, int2& w) {  // unconditional loads, as in the forward sweep
+      const int lc = l < nl ? l : nl - 1;
+      const int r = lp[lc] + rl;
+      const bool ok = lane && l < nl && r < lp[lc + 1];
+      sl = bslot[ok ? r : 0];
+      w = bring[ok ? r : 0];
+      return ok;
     };
     int4 sl = make_int4(0, 0, 0, 0), sln = sl;
     int2 w = make_int2(0, -1), wn = w;
@@ -1901,10 +1918,14 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
           for (int c = 0; c < NV; ++c) F[t][c] = blk[c];
         }
     };
-    bool act = slot_at(0, sl, w);
+    bool act = slot_at(g, sl, w);
     if (act) issue();
-    bool actn = slot_at(1, sln, wn);
+    bool actn = slot_at(g + G, sln, wn);
     for (int l = 0; l < nl; ++l) {
+      if (G > 1 && l % G != g) {
+        lds_barrier();
+        continue;
+      }
       if (act) {
         double sum = 0.0;
 #pragma unroll
@@ -1924,13 +1945,13 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
           for (int c = 0; c < NV; ++c) s += blk[c] * xj[c];
           sum += s;
         }
-        v[rl * NV + a] = xf - sum;
+        v[vr * NV + a] = xf - sum;
       }
       wave_sync();
       if (act) {
         double s = 0.0;
 #pragma unroll
-        for (int c = 0; c < NV; ++c) s += inv[c] * v[rl * NV + c];
+        for (int c = 0; c < NV; ++c) s += inv[c] * v[vr * NV + c];
         xs[w.x * NV + a] = s;
         if (w.y >= 0) xs[w.y * NV + a] = s;
         x[(size_t)sl.x * NV + a] = s;
@@ -1939,7 +1960,7 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
       sl = sln;
       w = wn;
       if (act) issue();
-      actn = slot_at(l + 2, sln, wn);
+      actn = slot_at(l + 2 * G, sln, wn);
       lds_barrier();
     }
   }
@@ -2316,6 +2337,10 @@ int rx_la_ilu_materialize(rx_ctx* ctx) {
 #endif
 int rx_ilu_stage() { return kStage; }
 int rx_ilu_ring_rpb(int nv) { return (1024 / 64) * (64 / nv); }  // ring_rpb<nv, 1024>()
+int rx_ilu_ring_groups() {  // RX_ILU_RING_G=1: every wavefront at every level (the first ring kernel, A/B)
+  static const int g = getenv("RX_ILU_RING_G") && atoi(getenv("RX_ILU_RING_G")) == 1 ? 1 : 2;
+  return g;
+}
 int rx_ilu_max_waves() { return RX_ILU_MAX_WAVES; }
 
 // Raise the dynamic-LDS limit of the LDS-resident kernels to what the device allows (once).
@@ -2327,9 +2352,12 @@ int rx_la_prepare(rx_ctx* ctx) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_part<NV_>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
-    if constexpr (NV_ >= 5)
-      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2>),
+    if constexpr (NV_ >= 5) {
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2, 1>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2, 2>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    }
     if constexpr (NV_ >= 5)
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_grp<NV_>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
@@ -2476,18 +2504,26 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
   // the LDS-ring sweeps (round 5) when the widest level fits one pass and the ring fits the LDS; RX_ILU_NO_RING=1
   // restores the wide sweeps below (A/B)
   static const bool no_ring = getenv("RX_ILU_NO_RING") != nullptr;
+  // (its sub-level plan splits the levels wider than one group's rows)
   const size_t ring_shm = sizeof(double) * ((size_t)std::max(ctx->fs.ring_rows, ctx->bs.ring_rows) * nv +
                                             (size_t)rx_ilu_ring_rpb(nv) * nv) +
-                          sizeof(int32_t) * (size_t)(std::max(ctx->fs.maxlev, ctx->bs.maxlev) + 1);
-  if (!no_ring && !narrow && nv >= 5 && width * nv > 256 && width <= rx_ilu_ring_rpb(nv) && ring_shm <= (size_t)ctx->lds_max) {
+                          sizeof(int32_t) * (size_t)(std::max(ctx->fs.rmaxlev, ctx->bs.rmaxlev) + 1);
+  if (!no_ring && !narrow && nv >= 5 && width * nv > 256 && width <= rx_ilu_ring_rpb(nv) &&
+      ring_shm <= (size_t)ctx->lds_max) {
     const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
     const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
     const int2* fr = reinterpret_cast<const int2*>(ctx->fs.ring);
     const int2* br = reinterpret_cast<const int2*>(ctx->bs.ring);
     const int rr = std::max(ctx->fs.ring_rows, ctx->bs.ring_rows);
-    RX_NV_SWITCH(nv, (k_ilu_apply_ring<NV_, 1024, 2><<<ctx->npart, 1024, ring_shm, ctx->stream>>>(
-                         ctx->fs.part_lvl, ctx->fs.lvl_ptr, fsl, fr, ctx->bs.part_lvl, ctx->bs.lvl_ptr, bsl, br,
-                         ctx->ring_xoff, ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv, rr)));
+    if (rx_ilu_ring_groups() == 1) {
+      RX_NV_SWITCH(nv, (k_ilu_apply_ring<NV_, 1024, 2, 1><<<ctx->npart, 1024, ring_shm, ctx->stream>>>(
+                           ctx->fs.rpart_lvl, ctx->fs.rlvl_ptr, fsl, fr, ctx->bs.rpart_lvl, ctx->bs.rlvl_ptr, bsl, br,
+                           ctx->ring_xoff, ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv, rr)));
+    } else {
+      RX_NV_SWITCH(nv, (k_ilu_apply_ring<NV_, 1024, 2, 2><<<ctx->npart, 1024, ring_shm, ctx->stream>>>(
+                           ctx->fs.rpart_lvl, ctx->fs.rlvl_ptr, fsl, fr, ctx->bs.rpart_lvl, ctx->bs.rlvl_ptr, bsl, br,
+                           ctx->ring_xoff, ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv, rr)));
+    }
     RX_HIP(hipGetLastError());
     return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
   }

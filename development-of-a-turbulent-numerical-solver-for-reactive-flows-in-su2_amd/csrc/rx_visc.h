@@ -18,6 +18,11 @@
 
 namespace rx {
 
+// 2 / (1 / a + 1 / b) with the device's division sequence (rx_fdiv.h): the same double
+__device__ __forceinline__ double hmean2(double a, double b) {
+  return rx_div(2.0, rx_recip(rx_div(1.0, rx_recip(a)) + rx_div(1.0, rx_recip(b))));
+}
+
 // The lane's dense NS x NS matrix (Gamma, then the closure matrix) in its workgroup's LDS scratch, entry q at
 // p[q * kScrLanes]: the 64 lanes' matrices interleaved, so that a wavefront's access to one entry touches 64
 // consecutive 8-byte words (no bank conflicts; a lane-contiguous [NS*NS] slice per lane put lanes 16 apart on the
@@ -102,7 +107,7 @@ __device__ inline void bicgstab(const Scr A, const double* rhs, double* x, doubl
   const int maxIters = 2 * N;
   double invdiag[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j) invdiag[j] = (A[j * N + j] != 0.0) ? 1.0 / A[j * N + j] : 1.0;
+  for (int j = 0; j < N; ++j) invdiag[j] = (A[j * N + j] != 0.0) ? rx_div(1.0, rx_recip(A[j * N + j])) : 1.0;
   double r[N], r0[N], tmp[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) x[i] = 0.0;
@@ -137,20 +142,20 @@ __device__ inline void bicgstab(const Scr A, const double* rhs, double* x, doubl
       rho = r0_sqnorm = eig_dot<N>(r, r);
       if (restarts++ == 0) i = 0;
     }
-    const double beta = (rho / rho_old) * (alpha / w);
+    const double beta = rx_div(rho, rx_recip(rho_old)) * rx_div(alpha, rx_recip(w));
 #pragma unroll
     for (int q = 0; q < N; ++q) p[q] = r[q] + beta * (p[q] - w * v[q]);
 #pragma unroll
     for (int q = 0; q < N; ++q) y[q] = invdiag[q] * p[q];
     eig_gemv<N>(A, y, v);
-    alpha = rho / eig_dot<N>(r0, v);
+    alpha = rx_div(rho, rx_recip(eig_dot<N>(r0, v)));
 #pragma unroll
     for (int q = 0; q < N; ++q) s[q] = r[q] - alpha * v[q];
 #pragma unroll
     for (int q = 0; q < N; ++q) z[q] = invdiag[q] * s[q];
     eig_gemv<N>(A, z, t);
     const double tt = eig_dot<N>(t, t);
-    w = (tt > 0.0) ? eig_dot<N>(t, s) / tt : 0.0;
+    w = (tt > 0.0) ? rx_div(eig_dot<N>(t, s), rx_recip(tt)) : 0.0;
 #pragma unroll
     for (int q = 0; q < N; ++q) x[q] += alpha * y[q] + w * z[q];
 #pragma unroll
@@ -221,9 +226,10 @@ __device__ inline void colpiv_qr_solve(const Scr Q, const double (*rhs)[NDIM], d
     } else {
       beta = sqrt(c0 * c0 + tailSq);
       if (c0 >= 0.0) beta = -beta;
+      const Recip rcb = rx_recip(c0 - beta);  // one divisor for the column (rx_fdiv.h)
 #pragma unroll
-      for (int i = k + 1; i < N; ++i) Q[i * N + k] = Q[i * N + k] / (c0 - beta);
-      tau = (beta - c0) / beta;
+      for (int i = k + 1; i < N; ++i) Q[i * N + k] = rx_div(Q[i * N + k], rcb);
+      tau = rx_div(beta - c0, rx_recip(beta));
     }
     hc[k] = tau;
     Q[k * N + k] = beta;
@@ -247,10 +253,10 @@ __device__ inline void colpiv_qr_solve(const Scr Q, const double (*rhs)[NDIM], d
 #pragma unroll
     for (int j = k + 1; j < N; ++j) {
       if (normsU[j] != 0.0) {
-        double temp = fabs(Q[k * N + j]) / normsU[j];
+        double temp = rx_div(fabs(Q[k * N + j]), rx_recip(normsU[j]));
         temp = (1.0 + temp) * (1.0 - temp);
         temp = temp < 0.0 ? 0.0 : temp;
-        const double rr = normsU[j] / normsD[j];
+        const double rr = rx_div(normsU[j], rx_recip(normsD[j]));
         const double temp2 = temp * (rr * rr);
         if (temp2 <= ndt) {
           double s = 0.0;
@@ -305,7 +311,7 @@ __device__ inline void colpiv_qr_solve(const Scr Q, const double (*rhs)[NDIM], d
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
       if (i < nonzero) {
-        c[i] /= Q[i * N + i];
+        c[i] = rx_div(c[i], rx_recip(Q[i * N + i]));
 #pragma unroll
         for (int j = 0; j < i; ++j) c[j] -= c[i] * Q[j * N + i];
       }
@@ -371,10 +377,10 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   int err = ERR_NONE;
   const double* Vi = ni.V;
   const double* Vj = nj.V;
-  const double Mean_mu = 2.0 / (1.0 / ni.mu + 1.0 / nj.mu);
-  const double Mean_k = 2.0 / (1.0 / ni.kappa + 1.0 / nj.kappa);
+  const double Mean_mu = hmean2(ni.mu, nj.mu);
+  const double Mean_k = hmean2(ni.kappa, nj.kappa);
   // harmonic means of the binary diffusion coefficients
-  auto Dm = [&](int q) { return 2.0 / (1.0 / ni.Dij[q] + 1.0 / nj.Dij[q]); };
+  auto Dm = [&](int q) { return hmean2(ni.Dij[q], nj.Dij[q]); };
   double Vm[nPV];
 #pragma unroll
   for (int v = 0; v < nPV; ++v) Vm[v] = 0.5 * (Vi[v] + Vj[v]);
@@ -396,6 +402,7 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   for (int d = 0; d < NDIM; ++d) dist2 += Edge[d] * Edge[d];
   if (corrected && !(dist2 > kEPS)) return ERR_GEOM;
   if (corrected) {
+    const Recip rd2 = rx_recip(dist2);
     double Xs_i[NS], Xs_j[NS];  // recomputed for the summary below: not live across the two solves
     molar_from_mass<NS>(m, Vi + RHOS_P, Xs_i);
     molar_from_mass<NS>(m, Vj + RHOS_P, Xs_j);
@@ -415,7 +422,7 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
 #pragma unroll
     for (int r = 0; r < nAvg; ++r)
 #pragma unroll
-      for (int d = 0; d < NDIM; ++d) G[r][d] -= (Proj[r] - Diff[r]) * Edge[d] / dist2;
+      for (int d = 0; d < NDIM; ++d) G[r][d] -= rx_div((Proj[r] - Diff[r]) * Edge[d], rd2);
   }
   // ---- SetLaminarTensorFlux, in an order that keeps few values live across the two dense solves: the
   // Stefan-Maxwell solve first, then the SST closure solve, then the tensors and the flux rows. Every
@@ -448,13 +455,13 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
         Dmax = fmax(Dmax, dm);
         Gt[a * NS + b] = dm;
       }
-    const double alpha = 1.0 / (rho * Dmax);
+    const double alpha = rx_div(1.0, rx_recip(rho * Dmax));
     double sigma = 0.0, massTot = 0.0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) sigma += Ys[s];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) massTot += Ys[s] / m.mm[s];
-    massTot = 1.0 / massTot;
+    for (int s = 0; s < NS; ++s) massTot += rx_div(Ys[s], mm_recip(m, s));
+    massTot = rx_div(1.0, rx_recip(massTot));
 #pragma unroll
     for (int a = 0; a < NS; ++a) {
       double dr[NS];  // Dm(b * NS + a), b = 0 .. NS-1
@@ -464,13 +471,13 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
       for (int b = 0; b < NS; ++b) {
         double g;
         if (a != b) {
-          g = -sigma * massTot * Xs[a] / (rho * m.mm[b] * dr[b]);
+          g = rx_div(-sigma * massTot * Xs[a], rx_recip(rho * m.mm[b] * dr[b]));
         } else {
           double tmp = 0.0;
 #pragma unroll
           for (int c = 0; c < NS; ++c)
-            if (c != a) tmp += Xs[c] / dr[c];
-          g = sigma * massTot * tmp / (rho * m.mm[a]);
+            if (c != a) tmp += rx_div(Xs[c], rx_recip(dr[c]));
+          g = rx_div(sigma * massTot * tmp, rx_recip(rho * m.mm[a]));
         }
         Gt[a * NS + b] = g + alpha * Ys[a];
       }
@@ -486,8 +493,11 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
 #endif
   }
   double hs[NS];
+  {
+    const Recip rE = rx_recip(P.E_ref);
 #pragma unroll
-  for (int s = 0; s < NS; ++s) hs[s] = spline(m, P_H, s, dim_temp, &err) / m.mm[s] / P.E_ref;
+    for (int s = 0; s < NS; ++s) hs[s] = rx_div(rx_div(spline(m, P_H, s, dim_temp, &err), mm_recip(m, s)), rE);
+  }
   double PF[nVar];
 #pragma unroll
   for (int v = 0; v < nVar; ++v) PF[v] = 0.0;
@@ -505,10 +515,13 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   double Mean_mut = 0.0, Mean_tke = 0.0, Cps[NS];
   double MG[NS][NDIM];
   if (P.rans) {
-    Mean_mut = 2.0 / (1.0 / ni.mut + 1.0 / nj.mut);
+    Mean_mut = hmean2(ni.mut, nj.mut);
     Mean_tke = 0.5 * (ni.tke + nj.tke);
+    {
+      const Recip rR = rx_recip(P.R_ref);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) Cps[s] = spline(m, P_CP, s, dim_temp, &err) / m.mm[s] / P.R_ref;
+      for (int s = 0; s < NS; ++s) Cps[s] = rx_div(rx_div(spline(m, P_CP, s, dim_temp, &err), mm_recip(m, s)), rR);
+    }
     {
       const Scr Mt = scr;  // LDS scratch of this lane (NS*NS), Gt is dead here
       double sig = 0.0;
@@ -518,8 +531,8 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
       for (int a = 0; a < NS; ++a)
 #pragma unroll
         for (int b = 0; b < NS; ++b)
-          Mt[a * NS + b] = m.mtot / m.mm[a] * (Ys[a] - Xs[a] + sig) * (double)(a == b) +
-                           m.mtot * (Ys[a] / m.mm[a] - Xs[a] / m.mm[b]) * (double)(a != b);
+          Mt[a * NS + b] = rx_div(m.mtot, mm_recip(m, a)) * (Ys[a] - Xs[a] + sig) * (double)(a == b) +
+                           m.mtot * (rx_div(Ys[a], mm_recip(m, a)) - rx_div(Xs[a], mm_recip(m, b))) * (double)(a != b);
       double rhs[NS][NDIM];
 #pragma unroll
       for (int s = 0; s < NS; ++s)
@@ -573,6 +586,10 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     double dv = 0.0;
 #pragma unroll
     for (int d = 0; d < NDIM; ++d) dv += G[VX_A + d][d];
+    // Mean_mut / (Pr_t Le_t), Mean_mut / Pr_t, Mean_mut / sigma_k: the same quotients in every term that uses them
+    const double mut_prle = rx_div(Mean_mut, rx_recip(P.Pr_t * P.Le_t));
+    const double mut_pr = rx_div(Mean_mut, rx_recip(P.Pr_t));
+    const double mut_sk = rx_div(Mean_mut, rx_recip(sigma_k));
     double tt[NDIM][NDIM];
 #pragma unroll
     for (int a = 0; a < NDIM; ++a) {
@@ -588,12 +605,12 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
         Flux[RHOE_S][a] += tt[a][b] * Vm[VX_P + b];
       }
 #pragma unroll
-      for (int s = 0; s < NS; ++s) PF[RHOS_S + s] += Mean_mut / (P.Pr_t * P.Le_t) * MG[s][a] * Normal[a];
+      for (int s = 0; s < NS; ++s) PF[RHOS_S + s] += mut_prle * MG[s][a] * Normal[a];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) Flux[RHOE_S][a] += Mean_mut / (P.Pr_t * P.Le_t) * hs[s] * Ys[s] * MG[s][a];
+      for (int s = 0; s < NS; ++s) Flux[RHOE_S][a] += mut_prle * hs[s] * Ys[s] * MG[s][a];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) Flux[RHOE_S][a] += Mean_mut / P.Pr_t * Cps[s] * Ys[s] * G[T_A][a];
-      Flux[RHOE_S][a] += (Mean_mu + Mean_mut / sigma_k) * gk[a];
+      for (int s = 0; s < NS; ++s) Flux[RHOE_S][a] += mut_pr * Cps[s] * Ys[s] * G[T_A][a];
+      Flux[RHOE_S][a] += (Mean_mu + mut_sk) * gk[a];
     }
   }
 #pragma unroll
@@ -619,11 +636,11 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
 #pragma unroll
       for (int b = 0; b < NS; ++b)
         if (b != a) {
-          di += Xs_i[b] / ni.Dij[b * NS + a];
-          dj += Xs_j[b] / nj.Dij[b * NS + a];
+          di += rx_div(Xs_i[b], rx_recip(ni.Dij[b * NS + a]));
+          dj += rx_div(Xs_j[b], rx_recip(nj.Dij[b * NS + a]));
         }
-      Ds_i[a] = (1.0 - Xs_i[a]) / di;
-      Ds_j[a] = (1.0 - Xs_j[a]) / dj;
+      Ds_i[a] = rx_div(1.0 - Xs_i[a], rx_recip(di));
+      Ds_j[a] = rx_div(1.0 - Xs_j[a], rx_recip(dj));
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -637,16 +654,18 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   for (int d = 0; d < NDIM; ++d) Area += Normal[d] * Normal[d];
   Area = sqrt(Area);
   double UN[NDIM];
+  const Recip rA = rx_recip(Area);
 #pragma unroll
-  for (int d = 0; d < NDIM; ++d) UN[d] = Normal[d] / Area;
+  for (int d = 0; d < NDIM; ++d) UN[d] = rx_div(Normal[d], rA);
 #pragma unroll
-  for (int s = 0; s < NS; ++s) Gxn[s] /= Area;
+  for (int s = 0; s < NS; ++s) Gxn[s] = rx_div(Gxn[s], rA);
   double theta = 0.0;
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) theta += UN[d] * UN[d];
   if (!P.rans) {
+    const Recip rR = rx_recip(P.R_ref);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) Cps[s] = spline(m, P_CP, s, dim_temp, &err) / m.mm[s] / P.R_ref;
+    for (int s = 0; s < NS; ++s) Cps[s] = rx_div(rx_div(spline(m, P_CP, s, dim_temp, &err), mm_recip(m, s)), rR);
   }
   double totMass = 0.0, totMass_i = 0.0, totMass_j = 0.0, sigma_i = 0.0, sigma_j = 0.0;
 #pragma unroll
@@ -751,16 +770,19 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
   const SummCRef Ds = Gxn + NS;
   const SummCRef qaux = Ds + NS;
   const double PrT = P.Pr_t, LeT = P.Le_t;
+  // the divisors shared by many quotients below, each with its reciprocal (rx_fdiv.h: the same doubles as `/`)
+  const Recip rdij = rx_recip(dij), rri = rx_recip(rho_i), rrj = rx_recip(rho_j);
   // ---- column-independent part of dJ/drho rows (lane tl < NS owns row a = tl)
   double bj = 0.0, bi = 0.0;
   if (tl < NS) {
     const int a = tl;
-    double vj = -rho * m.mm[a] * Ds[a] * Xs_j[a] / (totMass * dij * sigma_j * rho_j);
-    double vi = rho * m.mm[a] * Ds[a] * Xs_i[a] / (totMass * dij * sigma_i * rho_i);
+    const Recip r1j = rx_recip(totMass * dij * sigma_j * rho_j), r1i = rx_recip(totMass * dij * sigma_i * rho_i);
+    double vj = rx_div(-rho * m.mm[a] * Ds[a] * Xs_j[a], r1j);
+    double vi = rx_div(rho * m.mm[a] * Ds[a] * Xs_i[a], r1i);
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      vj += rho * Ys[a] * m.mm[q] * Ds[q] * Xs_j[q] / (totMass * dij * sigma_j * rho_j);
-      vi -= rho * Ys[a] * m.mm[q] * Ds[q] * Xs_i[q] / (totMass * dij * sigma_i * rho_i);
+      vj += rx_div(rho * Ys[a] * m.mm[q] * Ds[q] * Xs_j[q], r1j);
+      vi -= rx_div(rho * Ys[a] * m.mm[q] * Ds[q] * Xs_i[q], r1i);
     }
     bj = vj;
     bi = vi;
@@ -769,15 +791,16 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
   const int k = b - RHOS_S;
   const int kk = (k >= 0 && k < NS) ? k : 0;
   // the a == k term of :1352-1357, evaluated once for this lane's column (no divergent divisions)
-  const double dkj = rho * Ds[kk] * totMass_j * sigma_j / (dij * totMass * rho_j);
-  const double dki = rho * Ds[kk] * totMass_i * sigma_i / (dij * totMass * rho_i);
+  const Recip r2j = rx_recip(dij * totMass * rho_j), r2i = rx_recip(dij * totMass * rho_i);
+  const double dkj = rx_div(rho * Ds[kk] * totMass_j * sigma_j, r2j);
+  const double dki = rx_div(rho * Ds[kk] * totMass_i * sigma_i, r2i);
 #pragma unroll
   for (int a = 0; a < NS; ++a) {
     const double baj = __shfl(bj, a, 16), bai = __shfl(bi, a, 16);
     double vj = baj, vi = bai;
     if (k >= 0) {
-      vj += rho * Ys[a] * Ds[kk] * totMass_j * sigma_j / (dij * totMass * rho_j);
-      vi -= rho * Ys[a] * Ds[kk] * totMass_i * sigma_i / (dij * totMass * rho_i);
+      vj += rx_div(rho * Ys[a] * Ds[kk] * totMass_j * sigma_j, r2j);
+      vi -= rx_div(rho * Ys[a] * Ds[kk] * totMass_i * sigma_i, r2i);
       if (a == k) {
         vj -= dkj;
         vi += dki;
@@ -788,11 +811,12 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
   }
   if (b >= nVar) return;
   if (k >= 0) {  // diagonal increments of dJ/drho (:1369-1374): the same sequence for every diagonal entry
+    const Recip r3j = rx_recip(totMass * rho_j), r3i = rx_recip(totMass * rho_i);
     double tj[NS], ti[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      tj[q] = 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_j);
-      ti[q] = 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_i);
+      tj[q] = rx_div(0.5 * rho * m.mm[q] * Ds[q] * Gxn[q], r3j);
+      ti[q] = rx_div(0.5 * rho * m.mm[q] * Ds[q] * Gxn[q], r3i);
     }
 #pragma unroll
     for (int a = 0; a < NS; ++a)
@@ -828,10 +852,10 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
 #pragma unroll
   for (int a = 0; a < NDIM; ++a)
 #pragma unroll
-    for (int c = 0; c < NDIM; ++c) FJ[1 + a][1 + c] = mu * th[a][c] / dij * dS;
+    for (int c = 0; c < NDIM; ++c) FJ[1 + a][1 + c] = rx_div(mu * th[a][c], rdij) * dS;
 #pragma unroll
-  for (int c = 0; c < NDIM; ++c) FJ[RHOE_S][1 + c] = pi[c] * mu / dij * dS;
-  FJ[RHOE_S][RHOE_S] = ktr * theta / dij * dS;
+  for (int c = 0; c < NDIM; ++c) FJ[RHOE_S][1 + c] = rx_div(pi[c] * mu, rdij) * dS;
+  FJ[RHOE_S][RHOE_S] = rx_div(ktr * theta, rdij) * dS;
 #pragma unroll
   for (int r = 0; r < NF; ++r)
 #pragma unroll
@@ -854,38 +878,40 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
   }
   double dsj = 0.0, dsi = 0.0;  // 3-D species-species diagonal closure term of this lane's column (:1053-1060)
   if (P.rans) {
+    const Recip rprle = rx_recip(PrT * LeT);
+    const double mut_pr = rx_div(mut, rx_recip(PrT)), mut_prle = rx_div(mut, rprle);  // mut / PrT, mut / (PrT LeT)
 #pragma unroll
     for (int a = 0; a < NDIM; ++a)
 #pragma unroll
       for (int c = 0; c < NDIM; ++c) {
-        FJ[1 + a][1 + c] += mut * th[a][c] / sq * Area;
-        FI[1 + a][1 + c] -= mut * th[a][c] / sq * Area;
+        FJ[1 + a][1 + c] += rx_div(mut * th[a][c], rdij) * Area;
+        FI[1 + a][1 + c] -= rx_div(mut * th[a][c], rdij) * Area;
       }
 #pragma unroll
     for (int c = 0; c < NDIM; ++c) {
-      FJ[RHOE_S][1 + c] += pi[c] * mut / sq * Area;
-      FI[RHOE_S][1 + c] -= pi[c] * mut / sq * Area;
+      FJ[RHOE_S][1 + c] += rx_div(pi[c] * mut, rdij) * Area;
+      FI[RHOE_S][1 + c] -= rx_div(pi[c] * mut, rdij) * Area;
     }
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      FJ[RHOE_S][RHOE_S] += mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
-      FI[RHOE_S][RHOE_S] -= mut / PrT * Cps[q] * Ys[q] * theta / sq * Area;
+      FJ[RHOE_S][RHOE_S] += rx_div(mut_pr * Cps[q] * Ys[q] * theta, rdij) * Area;
+      FI[RHOE_S][RHOE_S] -= rx_div(mut_pr * Cps[q] * Ys[q] * theta, rdij) * Area;
     }
     if (k >= 0) {
       if constexpr (NDIM == 2) {
-        FJ3k += mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_j * theta / sq * Area;
-        FI3k -= mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_i * theta / sq * Area;
+        FJ3k += rx_div(rx_div(mut_prle * hs[kk] * Ys[kk], rrj) * theta, rdij) * Area;
+        FI3k -= rx_div(rx_div(mut_prle * hs[kk] * Ys[kk], rri) * theta, rdij) * Area;
       } else {
-        dsj = mut * Ys[kk] / (PrT * LeT) / rho_j * theta / sq * Area;
-        dsi = mut * Ys[kk] / (PrT * LeT) / rho_i * theta / sq * Area;
-        FJ3k += mut / (PrT * LeT) * hs[kk] / rho_j * theta / sq * Area;
-        FI3k -= mut / (PrT * LeT) * hs[kk] / rho_i * theta / sq * Area;
+        dsj = rx_div(rx_div(rx_div(mut * Ys[kk], rprle), rrj) * theta, rdij) * Area;
+        dsi = rx_div(rx_div(rx_div(mut * Ys[kk], rprle), rri) * theta, rdij) * Area;
+        FJ3k += rx_div(rx_div(mut_prle * hs[kk], rrj) * theta, rdij) * Area;
+        FI3k -= rx_div(rx_div(mut_prle * hs[kk], rri) * theta, rdij) * Area;
       }
     }
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      FJ[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
-      FI[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
+      FJ[RHOE_S][RHOE_S] += mut_prle * Cps[q] * Ys[q] * qaux[q] * Area;
+      FI[RHOE_S][RHOE_S] += mut_prle * Cps[q] * Ys[q] * qaux[q] * Area;
     }
   }
 #pragma unroll
@@ -901,11 +927,11 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) {
     if (b == 0) {
-      ci[d] = -sm[L::VI + d] / rho_i;
-      cj[d] = -sm[L::VJ + d] / rho_j;
+      ci[d] = rx_div(-sm[L::VI + d], rri);
+      cj[d] = rx_div(-sm[L::VJ + d], rrj);
     } else {
-      ci[d] = (b == 1 + d) ? 1.0 / rho_i : 0.0;
-      cj[d] = (b == 1 + d) ? 1.0 / rho_j : 0.0;
+      ci[d] = (b == 1 + d) ? rx_div(1.0, rri) : 0.0;
+      cj[d] = (b == 1 + d) ? rx_div(1.0, rrj) : 0.0;
     }
   }
   const double d0 = (b == 0) ? 1.0 : 0.0;
@@ -973,24 +999,28 @@ __device__ inline void visc_jac_column_own(const DevMech& m, const ViscParams& P
   const SummCRef Ds = Gxn + NS;
   const SummCRef qaux = Ds + NS;
   const double PrT = P.Pr_t, LeT = P.Le_t;
+  // the divisors shared by many quotients below, each with its reciprocal (rx_fdiv.h: the same doubles as `/`)
+  const Recip rdij = rx_recip(dij), rro = rx_recip(rho_o);
   // column-independent part of dJ/drho row a = tl, i-side form on the own data (the j side is its negative)
   double bo = 0.0;
   if (tl < NS) {
     const int a = tl;
-    double v = rho * m.mm[a] * Ds[a] * Xs_o[a] / (totMass * dij * sigma_o * rho_o);
+    const Recip r1 = rx_recip(totMass * dij * sigma_o * rho_o);
+    double v = rx_div(rho * m.mm[a] * Ds[a] * Xs_o[a], r1);
 #pragma unroll
-    for (int q = 0; q < NS; ++q) v -= rho * Ys[a] * m.mm[q] * Ds[q] * Xs_o[q] / (totMass * dij * sigma_o * rho_o);
+    for (int q = 0; q < NS; ++q) v -= rx_div(rho * Ys[a] * m.mm[q] * Ds[q] * Xs_o[q], r1);
     bo = v;
   }
   double col[NS];  // dJ/drho column k = b - RHOS_S, own side (signed)
   const int k = b - RHOS_S;
   const int kk = (k >= 0 && k < NS) ? k : 0;
-  const double dko = rho * Ds[kk] * totMass_o * sigma_o / (dij * totMass * rho_o);
+  const Recip r2 = rx_recip(dij * totMass * rho_o);
+  const double dko = rx_div(rho * Ds[kk] * totMass_o * sigma_o, r2);
 #pragma unroll
   for (int a = 0; a < NS; ++a) {
     double v = __shfl(bo, a, 16);
     if (k >= 0) {
-      v -= rho * Ys[a] * Ds[kk] * totMass_o * sigma_o / (dij * totMass * rho_o);
+      v -= rx_div(rho * Ys[a] * Ds[kk] * totMass_o * sigma_o, r2);
       if (a == k) v += dko;
     }
     col[a] = J ? -v : v;
@@ -998,8 +1028,9 @@ __device__ inline void visc_jac_column_own(const DevMech& m, const ViscParams& P
   if (b >= nVar) return;
   if (k >= 0) {
     double to[NS];
+    const Recip r3 = rx_recip(totMass * rho_o);
 #pragma unroll
-    for (int q = 0; q < NS; ++q) to[q] = 0.5 * rho * m.mm[q] * Ds[q] * Gxn[q] / (totMass * rho_o);
+    for (int q = 0; q < NS; ++q) to[q] = rx_div(0.5 * rho * m.mm[q] * Ds[q] * Gxn[q], r3);
 #pragma unroll
     for (int a = 0; a < NS; ++a)
       if (a == k) {
@@ -1030,10 +1061,10 @@ __device__ inline void visc_jac_column_own(const DevMech& m, const ViscParams& P
 #pragma unroll
   for (int a = 0; a < NDIM; ++a)
 #pragma unroll
-    for (int c = 0; c < NDIM; ++c) F[1 + a][1 + c] = mu * th[a][c] / dij * dS;
+    for (int c = 0; c < NDIM; ++c) F[1 + a][1 + c] = rx_div(mu * th[a][c], rdij) * dS;
 #pragma unroll
-  for (int c = 0; c < NDIM; ++c) F[RHOE_S][1 + c] = pi[c] * mu / dij * dS;
-  F[RHOE_S][RHOE_S] = ktr * theta / dij * dS;
+  for (int c = 0; c < NDIM; ++c) F[RHOE_S][1 + c] = rx_div(pi[c] * mu, rdij) * dS;
+  F[RHOE_S][RHOE_S] = rx_div(ktr * theta, rdij) * dS;
   if (!J) {
 #pragma unroll
     for (int r = 0; r < NF; ++r)
@@ -1053,33 +1084,35 @@ __device__ inline void visc_jac_column_own(const DevMech& m, const ViscParams& P
   double dso = 0.0;  // 3-D species-species diagonal closure term (own side)
   auto pm = [&](double f, double x) { return J ? f + x : f - x; };  // FJ += x / FI -= x
   if (P.rans) {
+    const Recip rprle = rx_recip(PrT * LeT);
+    const double mut_pr = rx_div(mut, rx_recip(PrT)), mut_prle = rx_div(mut, rprle);  // mut / PrT, mut / (PrT LeT)
 #pragma unroll
     for (int a = 0; a < NDIM; ++a)
 #pragma unroll
-      for (int c = 0; c < NDIM; ++c) F[1 + a][1 + c] = pm(F[1 + a][1 + c], mut * th[a][c] / sq * Area);
+      for (int c = 0; c < NDIM; ++c) F[1 + a][1 + c] = pm(F[1 + a][1 + c], rx_div(mut * th[a][c], rdij) * Area);
 #pragma unroll
-    for (int c = 0; c < NDIM; ++c) F[RHOE_S][1 + c] = pm(F[RHOE_S][1 + c], pi[c] * mut / sq * Area);
+    for (int c = 0; c < NDIM; ++c) F[RHOE_S][1 + c] = pm(F[RHOE_S][1 + c], rx_div(pi[c] * mut, rdij) * Area);
 #pragma unroll
     for (int q = 0; q < NS; ++q)
-      F[RHOE_S][RHOE_S] = pm(F[RHOE_S][RHOE_S], mut / PrT * Cps[q] * Ys[q] * theta / sq * Area);
+      F[RHOE_S][RHOE_S] = pm(F[RHOE_S][RHOE_S], rx_div(mut_pr * Cps[q] * Ys[q] * theta, rdij) * Area);
     if (k >= 0) {
       if constexpr (NDIM == 2) {
-        F3k = pm(F3k, mut / (PrT * LeT) * hs[kk] * Ys[kk] / rho_o * theta / sq * Area);
+        F3k = pm(F3k, rx_div(rx_div(mut_prle * hs[kk] * Ys[kk], rro) * theta, rdij) * Area);
       } else {
-        dso = mut * Ys[kk] / (PrT * LeT) / rho_o * theta / sq * Area;
-        F3k = pm(F3k, mut / (PrT * LeT) * hs[kk] / rho_o * theta / sq * Area);
+        dso = rx_div(rx_div(rx_div(mut * Ys[kk], rprle), rro) * theta, rdij) * Area;
+        F3k = pm(F3k, rx_div(rx_div(mut_prle * hs[kk], rro) * theta, rdij) * Area);
       }
     }
 #pragma unroll
-    for (int q = 0; q < NS; ++q) F[RHOE_S][RHOE_S] += mut / (PrT * LeT) * Cps[q] * Ys[q] * qaux[q] * Area;
+    for (int q = 0; q < NS; ++q) F[RHOE_S][RHOE_S] += mut_prle * Cps[q] * Ys[q] * qaux[q] * Area;
   }
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) F[RHOE_S][1 + d] += 0.5 * sm[L::PF + d];
   double co[NDIM];  // dV/dU velocity rows, column b, own node
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) {
-    if (b == 0) co[d] = -sm[(J ? L::VJ : L::VI) + d] / rho_o;
-    else co[d] = (b == 1 + d) ? 1.0 / rho_o : 0.0;
+    if (b == 0) co[d] = rx_div(-sm[(J ? L::VJ : L::VI) + d], rro);
+    else co[d] = (b == 1 + d) ? rx_div(1.0, rro) : 0.0;
   }
   const double d0 = (b == 0) ? 1.0 : 0.0;
 #pragma unroll

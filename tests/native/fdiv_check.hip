@@ -1,0 +1,34 @@
+// Test library (tests/test_gpu_fdiv.py): the compiler's FP64 division against rx_fdiv.h's shared-divisor sequence on
+// the same operands. Not part of the product; built by tests/native/Makefile (__graft_entry__.build()).
+#include <hip/hip_runtime.h>
+
+#include "../../development-of-a-turbulent-numerical-solver-for-reactive-flows-in-su2_amd/csrc/rx_fdiv.h"
+
+__global__ void k_fdiv_check(const double* __restrict__ n, const double* __restrict__ d, double* __restrict__ ref,
+                             double* __restrict__ fast, int count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  ref[i] = n[i] / d[i];
+  fast[i] = rx::rx_div(n[i], rx::rx_recip(d[i]));
+}
+
+extern "C" int fdiv_check(const double* hn, const double* hd, double* href, double* hfast, int count) {
+  if (count <= 0) return 1;
+  double* buf = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)count;
+  if (hipMalloc(&buf, 4 * bytes) != hipSuccess) return 2;
+  int rc = 0;
+  if (hipMemcpy(buf, hn, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(buf + count, hd, bytes, hipMemcpyHostToDevice) != hipSuccess)
+    rc = 3;
+  if (!rc) {
+    k_fdiv_check<<<(count + 255) / 256, 256>>>(buf, buf + count, buf + 2 * (size_t)count, buf + 3 * (size_t)count,
+                                               count);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = 4;
+  }
+  if (!rc && (hipMemcpy(href, buf + 2 * (size_t)count, bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+              hipMemcpy(hfast, buf + 3 * (size_t)count, bytes, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = 5;
+  (void)hipFree(buf);
+  return rc;
+}

@@ -12,13 +12,15 @@ FGMRES(5)+ILU0 step, then the SST step) run
       it), the inner products through ncclAllGather + k_sum_ranks;
   (b) over the synchronous host transport (the same plan through pinned host buffers, eager solve);
 
-and must agree bitwise: gradients, RMS vectors, linear-iteration counts, U and (k, omega) including the halo rows,
-which must hold the values of the owned points they are fed from. Requires an MI355X."""
+and must agree bitwise: gradients, RMS vectors, linear-iteration counts, U, the primitives after the update and
+(k, omega) including the halo rows, which must hold the values of the owned points they are fed from. With RCCL the
+post-update Set_MPI_Solution runs on comm_stream while SetPrimitive_Variables computes the owned points (round 5).
+Requires an MI355X."""
 import numpy as np
 import pytest
 
 from tests.rxpkg import meshgen, rx
-from tests.test_gpu_shard import NS, _case, _set, _step
+from tests.test_gpu_shard import NS, _case, _set
 
 pytestmark = pytest.mark.gpu
 
@@ -63,6 +65,30 @@ class SelfTransport:
         self.desc = rx.HostComm(None, self._cb[0], self._cb[1])
 
 
+def _step(s, t):
+    """One outer iteration in rx.Iterate's order: the flow implicit step, the flow SetPrimitive_Variables on the updated
+    solution (with RCCL its owned points run while the post-update Set_MPI_Solution is in flight on comm_stream, then
+    the halo points), then the SST step."""
+    s.SetPrimitive_Gradient_LS()
+    grad = s.download("GRAD")
+    s.SetStrainMag()
+    s.SetTime_Step()
+    s.Preprocessing_zero()
+    s.Upwind_Residual()
+    s.Viscous_Residual()
+    s.Source_Residual()
+    rms, it = s.ImplicitEuler_Iteration()
+    s.SetPrimitive_Variables(1)
+    V = s.download("V")
+    t.Preprocessing()
+    t.Upwind_Residual()
+    t.Viscous_Residual()
+    t.Source_Residual()
+    trms, tit = t.ImplicitEuler_Iteration()
+    t.Postprocessing()
+    return grad, V, np.r_[rms, trms], (it, tit)
+
+
 def run(transport):
     sh, st_l, mech_arrays, cfg, nd, near = self_halo_shard()
     s = rx.ReactiveNSSolver(sh, rx.Mechanism(mech_arrays), cfg)
@@ -76,8 +102,8 @@ def run(transport):
     _set(s, t, sh, st_l)
     out = []
     for _ in range(2):  # RCCL: the second iteration replays the captured solve graphs
-        g, rms, it = _step(s, t)
-        out.append(dict(grad=g, rms=rms, it=it, U=s.download("U"), T=t.download("U")))
+        g, V, rms, it = _step(s, t)
+        out.append(dict(grad=g, V=V, rms=rms, it=it, U=s.download("U"), T=t.download("U")))
     s.close()
     if tr is not None:
         assert tr.calls > 0
@@ -93,11 +119,14 @@ def test_rccl_self_halo_matches_host_transport():
         assert np.array_equal(a[k]["grad"], b[k]["grad"]), f"iteration {k}: gradients"
         assert np.array_equal(a[k]["rms"], b[k]["rms"]), f"iteration {k}: RMS"
         assert np.array_equal(a[k]["U"], b[k]["U"]), f"iteration {k}: U"
+        assert np.array_equal(a[k]["V"], b[k]["V"]), f"iteration {k}: primitives after the update"
         assert np.array_equal(a[k]["T"], b[k]["T"]), f"iteration {k}: (k, omega)"
         U = a[k]["U"].reshape(-1, nvar)
         T = a[k]["T"].reshape(-1, 2)
         # Set_MPI_Solution after the update: every halo row holds the value of the owned point that feeds it
         assert np.array_equal(U[nd:], U[near]) and np.array_equal(T[nd:], T[near])
+        V = a[k]["V"].reshape(len(sh["l2g"]), -1)
+        assert np.array_equal(V[nd:], V[near])  # the halo points' primitives from the exchanged solution
         assert np.all(np.isfinite(U)) and a[k]["it"][0] >= 1
     G = a[1]["grad"].reshape(len(sh["l2g"]), -1)
     assert np.array_equal(G[nd:], G[near])  # Set_MPI_Primitive_Gradient
