@@ -17,8 +17,7 @@ namespace {
 
 // y[i] = rx_recip(x[i]).y: divisors' reciprocals made by the device's own instructions (rx_fdiv.h)
 __global__ void k_recip_table(const double* __restrict__ x, double* __restrict__ y, int n) {
-  const int i = threadIdx.x;
-  if (i < n) y[i] = rx::rx_recip(x[i]).y;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) y[i] = rx::rx_recip(x[i]).y;
 }
 
 template <typename T>
@@ -652,6 +651,12 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
           dvs[a * ns + b] = std::cbrt(mech->diff_vol[a]) + std::cbrt(mech->diff_vol[b]);
         }
       m.phic = up(phic.data(), phic.size());
+      double* d = nullptr;  // its reciprocals (rx_fdiv.h)
+      RX_HIP(hipMalloc(&d, sizeof(double) * phic.size()));
+      ctx->mech_bufs.push_back(d);
+      if (m.phic) k_recip_table<<<1, 64, 0, ctx->stream>>>(m.phic, d, (int)phic.size());
+      RX_HIP(hipGetLastError());
+      m.rphic = d;
       m.pw25 = up(pw.data(), pw.size());
       m.mij = up(mij.data(), mij.size());
       m.dvs = up(dvs.data(), dvs.size());

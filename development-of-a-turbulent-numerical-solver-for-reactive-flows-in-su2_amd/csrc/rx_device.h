@@ -46,6 +46,7 @@ struct DevMech {
   const double *mij;            // [ns][ns] sqrt(M_a M_b / (M_a + M_b))
   const double *dvs;            // [ns][ns] cbrt(V_a) + cbrt(V_b)
   const double *rmm;            // [ns] rx_recip(mm[s]).y, made on the device (k_recip_table): quotients by M_s
+  const double *rphic;          // [ns][ns] rx_recip(phic).y (Wilke's mixing rule, k_set_primitive)
   uint32_t neg_reac[kMaxNR], neg_prod[kMaxNR];  // species masks with negative rate exponents
 };
 
@@ -55,6 +56,13 @@ __device__ __host__ inline Recip mm_recip(const DevMech& m, int s) {
   return Recip{m.mm[s], m.rmm[s]};
 #else
   return Recip{m.mm[s], 0.0};
+#endif
+}
+__device__ __host__ inline Recip phic_recip(const DevMech& m, int ab) {
+#if RX_FDIV_DEV
+  return Recip{m.phic[ab], m.rphic[ab]};
+#else
+  return Recip{m.phic[ab], 0.0};
 #endif
 }
 

@@ -113,7 +113,7 @@ template <int NS>
 __device__ inline double mix_h(const DevMech& m, double T, const double* Yc, int* err) {
   double h = 0.0;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) h += Yc[s] * (spline(m, P_H, s, T, err) / m.mm[s]);
+  for (int s = 0; s < NS; ++s) h += Yc[s] * rx_div(spline(m, P_H, s, T, err), mm_recip(m, s));
   return h;
 }
 
@@ -137,9 +137,10 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
     V[RHO] = U[0];
   }
   double Ys[NS], Yc[NS];
+  const Recip rrho = rx_recip(U[0]);  // rho's quotients share its reciprocal (rx_fdiv.h: the same doubles as `/`)
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    V[RHOS + s] = U[RHOS_S + s] / U[0];
+    V[RHOS + s] = rx_div(U[RHOS_S + s], rrho);
     Ys[s] = V[RHOS + s];
     Yc[s] = Ys[s] < 0.0 ? 1.0e-30 : Ys[s];
   }
@@ -152,29 +153,30 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
   double sqvel = 0.0;
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) {
-    V[VX + d] = U[RHOVX_S + d] / rho;
+    V[VX + d] = rx_div(U[RHOVX_S + d], rrho);
     sqvel += V[VX + d] * V[VX + d];
   }
   const double Tmin = P.Tmin / P.T_ref, Tmax = P.Tmax / P.T_ref;
   double Rg = 0.0;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) Rg += Yc[s] * (kR / m.mm[s]);
-  const double Rgas = Rg / P.R_ref;
-  const double C1 = (-rhoE + 0.5 * rho * sqvel) / (rho * Rgas);
-  const double C2 = 1.0 / Rgas;
+  for (int s = 0; s < NS; ++s) Rg += Yc[s] * rx_div(kR, mm_recip(m, s));
+  const double Rgas = rx_div(Rg, rx_recip(P.R_ref));
+  const double C1 = rx_div(-rhoE + 0.5 * rho * sqvel, rx_recip(rho * Rgas));
+  const double C2 = rx_div(1.0, rx_recip(Rgas));
+  const Recip rE = rx_recip(P.E_ref);
   const double old_temp = V[0];
   double T = V[0], Told = T + 1.0;
   bool conv = false;
   for (int it = 0; it < 7; ++it) {
     int e1 = ERR_NONE;
-    const double hs_old = mix_h<NS>(m, Told * P.T_ref, Yc, &e1) / P.E_ref;
-    const double hs = mix_h<NS>(m, T * P.T_ref, Yc, &e1) / P.E_ref;
+    const double hs_old = rx_div(mix_h<NS>(m, Told * P.T_ref, Yc, &e1), rE);
+    const double hs = rx_div(mix_h<NS>(m, T * P.T_ref, Yc, &e1), rE);
     if (e1 != ERR_NONE) {  // std::out_of_range inside the secant: bisection on [Tmin, Tmax], 10000 steps
       double Ta = Tmin, Tb = Tmax;
       for (int b = 0; b < 10000; ++b) {
         T = (Ta + Tb) / 2.0;
         int e2 = ERR_NONE;
-        const double h2 = mix_h<NS>(m, T * P.T_ref, Yc, &e2) / P.E_ref;
+        const double h2 = rx_div(mix_h<NS>(m, T * P.T_ref, Yc, &e2), rE);
         const double f = T - C1 - C2 * h2;
         if (fabs(f) < 1.0e-4) {
           conv = true;
@@ -188,7 +190,7 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
     }
     const double f = T - C1 - C2 * hs;
     const double df = T - Told + C2 * (hs_old - hs);
-    const double Tnew = T - f * (T - Told) / df;
+    const double Tnew = T - rx_div(f * (T - Told), rx_recip(df));
     if (fabs(Tnew - T) < 1.0e-6) {
       conv = true;
       break;
@@ -205,7 +207,7 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
     for (int b = 0; b < 32; ++b) {
       T = (Ta + Tb) / 2.0;
       int e2 = ERR_NONE;
-      const double h2 = mix_h<NS>(m, T * P.T_ref, Yc, &e2) / P.E_ref;
+      const double h2 = rx_div(mix_h<NS>(m, T * P.T_ref, Yc, &e2), rE);
       const double f = T - C1 - C2 * h2;
       if (fabs(f) < 1.0e-4) {
         V[0] = T;
@@ -242,14 +244,14 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
   int e3 = ERR_NONE;
   double Cp = 0.0;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) Cp += Yc[s] * (spline(m, P_CP, s, dim_temp, &e3) / m.mm[s]);
-  const double gamma = Cp / (Cp - Rg);
-  V[A_] = sqrt(gamma * V[P_] / rho);
+  for (int s = 0; s < NS; ++s) Cp += Yc[s] * rx_div(spline(m, P_CP, s, dim_temp, &e3), mm_recip(m, s));
+  const double gamma = rx_div(Cp, rx_recip(Cp - Rg));
+  V[A_] = sqrt(rx_div(gamma * V[P_], rrho));
   if (V[A_] < kEPS) {
     V[A_] = kEPS;
     nonPhys = true;
   }
-  V[H_] = (U[RHOE_S] + V[P_]) / rho;
+  V[H_] = rx_div(U[RHOE_S] + V[P_], rrho);
   if (e3 != ERR_NONE) *fail = true;
   return nonPhys;
 }
@@ -300,12 +302,15 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int lo, in
   }
   double Rg = 0.0;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) Rg += Yc[s] * (kR / m.mm[s]);
-  const double Cp = (dim_a * dim_a * Rg) / (dim_a * dim_a - Rg * dim_temp) / P.R_ref;
+  for (int s = 0; s < NS; ++s) Rg += Yc[s] * rx_div(kR, mm_recip(m, s));
+  // the divisors shared by several quotients below, each with its reciprocal (rx_fdiv.h: the same doubles as `/`)
+  const Recip rR = rx_recip(P.R_ref), rE = rx_recip(P.E_ref);
+  const double Cp = rx_div(rx_div(dim_a * dim_a * Rg, rx_recip(dim_a * dim_a - Rg * dim_temp)), rR);
   // CalcdTdU / CalcdPdU
   const double dim_cp = Cp * P.R_ref;
-  const double Cv = (dim_cp - Rg) / P.R_ref;
+  const double Cv = rx_div(dim_cp - Rg, rR);
   const double rhoCv = V[RHO] * Cv;
+  const Recip rcv = rx_recip(rhoCv);
   double sq = 0.0;
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) sq += V[VX + d] * V[VX + d];
@@ -313,22 +318,23 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int lo, in
   double dTdYs[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s)
-    dTdYs[s] = (spline(m, P_H, s, dim_temp, &e4) / m.mm[s] - (kR / m.mm[s]) * dim_temp) / P.E_ref;
+    dTdYs[s] = rx_div(rx_div(spline(m, P_H, s, dim_temp, &e4), mm_recip(m, s)) - rx_div(kR, mm_recip(m, s)) * dim_temp,
+                      rE);
   double* dt = dTdU + (size_t)i * nVar;
-  dt[0] = 0.5 * sq / rhoCv;
+  dt[0] = rx_div(0.5 * sq, rcv);
 #pragma unroll
-  for (int d = 0; d < NDIM; ++d) dt[1 + d] = -V[VX + d] / rhoCv;
-  dt[NDIM + 1] = 1.0 / rhoCv;
+  for (int d = 0; d < NDIM; ++d) dt[1 + d] = rx_div(-V[VX + d], rcv);
+  dt[NDIM + 1] = rx_div(1.0, rcv);
 #pragma unroll
-  for (int s = 0; s < NS; ++s) dt[NDIM + 2 + s] = -dTdYs[s] / rhoCv;
-  const double Gamma = dim_cp / (dim_cp - Rg);
+  for (int s = 0; s < NS; ++s) dt[NDIM + 2 + s] = rx_div(-dTdYs[s], rcv);
+  const double Gamma = rx_div(dim_cp, rx_recip(dim_cp - Rg));
   double* dp = dPdU + (size_t)i * nVar;
   dp[0] = (Gamma - 1.0) * 0.5 * sq;
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) dp[1 + d] = (1.0 - Gamma) * V[VX + d];
   dp[NDIM + 1] = Gamma - 1.0;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) dp[NDIM + 2 + s] = (kR / m.mm[s]) / P.R_ref * V[0] - (Gamma - 1.0) * dTdYs[s];
+  for (int s = 0; s < NS; ++s) dp[NDIM + 2 + s] = rx_div(rx_div(kR, mm_recip(m, s)), rR) * V[0] - (Gamma - 1.0) * dTdYs[s];
   // transport (CReactiveNSVariable::SetPrimVar)
   eddy[i] = P.rans ? mut[i] : 0.0;
   const double dim_press = V[P_] * P.P_ref / 101325.0;
@@ -337,22 +343,25 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int lo, in
   for (int s = 0; s < NS; ++s) {
     visc[s] = spline(m, P_MU, s, dim_temp, &e4);
     cond[s] = spline(m, P_KAPPA, s, dim_temp, &e4);
-    yom[s] = Yc[s] / m.mm[s];
+    yom[s] = rx_div(Yc[s], mm_recip(m, s));
   }
+  Recip rvisc[NS];  // visc[b] divides visc[a] for every a (rx_fdiv.h)
+#pragma unroll
+  for (int b = 0; b < NS; ++b) rvisc[b] = rx_recip(visc[b]);
   double eta = 0.0;
 #pragma unroll RX_PRIM_UNROLL
   for (int a = 0; a < NS; ++a) {
     double phi = 0.0;
 #pragma unroll
     for (int b = 0; b < NS; ++b) {
-      const double f = 1.0 + sqrt(visc[a] / visc[b]) * m.pw25[a * NS + b];
-      phi += yom[b] / m.phic[a * NS + b] * f * f;
+      const double f = 1.0 + sqrt(rx_div(visc[a], rvisc[b])) * m.pw25[a * NS + b];
+      phi += rx_div(yom[b], phic_recip(m, a * NS + b)) * f * f;
     }
-    eta += visc[a] * yom[a] / phi;
+    eta += rx_div(visc[a] * yom[a], rx_recip(phi));
   }
-  mu[i] = eta / P.Visc_ref;
+  mu[i] = rx_div(eta, rx_recip(P.Visc_ref));
 #pragma unroll
-  for (int s = 0; s < NS; ++s) yom[s] = Ys[s] / m.mm[s];  // ComputeLambda: the unclamped argument
+  for (int s = 0; s < NS; ++s) yom[s] = rx_div(Ys[s], mm_recip(m, s));  // ComputeLambda: the unclamped argument
   double lam = 0.0;
 #pragma unroll RX_PRIM_UNROLL
   for (int a = 0; a < NS; ++a) {
@@ -360,24 +369,25 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int lo, in
 #pragma unroll
     for (int b = 0; b < NS; ++b)
       if (b != a) {
-        const double f = 1.0 + sqrt(visc[a] / visc[b]) * m.pw25[a * NS + b];
-        phi += 1.065 * yom[b] / m.phic[a * NS + b] * f * f;
+        const double f = 1.0 + sqrt(rx_div(visc[a], rvisc[b])) * m.pw25[a * NS + b];
+        phi += rx_div(1.065 * yom[b], phic_recip(m, a * NS + b)) * f * f;
       }
     phi += yom[a];
-    lam += cond[a] * yom[a] / phi;
+    lam += rx_div(cond[a] * yom[a], rx_recip(phi));
   }
-  kappa[i] = lam / P.Cond_ref;
+  kappa[i] = rx_div(lam, rx_recip(P.Cond_ref));
   const double pT = 1.0e-3 * pow175_cr(dim_temp);
   const double scale = P.Vel_ref * P.Len_ref * 1.0e4;
+  const Recip rscale = rx_recip(scale);
   double* D = Dij + (size_t)i * NS * NS;
 #pragma unroll RX_PRIM_UNROLL
   for (int a = 0; a < NS; ++a)
 #pragma unroll
     for (int b = a; b < NS; ++b) {
       const double sv = m.dvs[a * NS + b];
-      const double d = pT / (dim_press * m.mij[a * NS + b] * sv * sv);
-      D[a * NS + b] = d / scale;
-      D[b * NS + a] = d / scale;
+      const double d = rx_div(pT, rx_recip(dim_press * m.mij[a * NS + b] * sv * sv));
+      D[a * NS + b] = rx_div(d, rscale);
+      D[b * NS + a] = rx_div(d, rscale);
     }
   if (e4 != ERR_NONE) {
     if (atomicCAS(err, 0, ERR_RANGE) == 0) err[1] = i;

@@ -1784,6 +1784,9 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_wide(const int32_t* __restrict
 // across the barrier. One row per lane group and level (the widest level fits the workgroup's rows); MB blocks of a
 // row come from registers, further ones are loaded when used. Same arithmetic, operation for operation, as the wide
 // sweeps (row_blocks: each block's sum from 0.0, c ascending; blocks ascending).
+#ifndef RX_RING_PROBE
+#define RX_RING_PROBE 0  // timing probes of k_ilu_apply_ring (build variants only; bit 0: no factor-block loads)
+#endif
 template <int NV, int TB>
 constexpr int ring_rpb() {
   return (TB / 64) * (64 / NV);  // rows per pass: whole rows per wavefront (the backward's v exchange is wave-local)
@@ -1842,10 +1845,16 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
 #pragma unroll
       for (int t = 0; t < MB; ++t)
         if (sl.y + t < sl.z) {
+#if RX_RING_PROBE & 1  // timing probe (build variant only): no factor-block loads
+          xo[t] = 0;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) F[t][c] = 0.0;
+#else
           xo[t] = xoff[sl.y + t];
           const double* blk = L + (size_t)(sl.y + t) * NV2 + a * NV;
 #pragma unroll
           for (int c = 0; c < NV; ++c) F[t][c] = blk[c];
+#endif
         }
     };
     bool act = slot_at(g, sl, w);
@@ -1912,10 +1921,16 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
 #pragma unroll
       for (int t = 0; t < MB; ++t)
         if (sl.z + 1 + t < sl.w) {
+#if RX_RING_PROBE & 1
+          xo[t] = 0;
+#pragma unroll
+          for (int c = 0; c < NV; ++c) F[t][c] = 0.0;
+#else
           xo[t] = xoff[sl.z + 1 + t];
           const double* blk = U + (size_t)(sl.z + 1 + t) * NV2 + a * NV;
 #pragma unroll
           for (int c = 0; c < NV; ++c) F[t][c] = blk[c];
+#endif
         }
     };
     bool act = slot_at(g, sl, w);
