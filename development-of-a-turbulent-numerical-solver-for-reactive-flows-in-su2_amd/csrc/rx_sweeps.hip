@@ -555,6 +555,35 @@ __device__ __forceinline__ int lds_row_tied(int off, const double (&v)[NV]) {
   return off;
 }
 
+// acc[e] += S[q + e NV] * v[q] for q ascending (a block product's column, the reference's order: sums from the
+// accumulator, q ascending) with row q + 1's LDS reads issued before row q's products: they are tied to the
+// accumulators after row q - 1, so one row of operands is in flight (the reads are not all hoisted, which spills) and
+// the LDS latency of a row hides behind the previous row's products instead of adding to them.
+template <int NV>
+__device__ __forceinline__ void lds_colprod(const double* S, const double (&v)[NV], double (&acc)[NV]) {
+  double cur[NV];
+  {
+    const int o = lds_row_tied<NV>(0, acc);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) cur[e] = S[o + e * NV];
+  }
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double nxt[NV];
+    if (q + 1 < NV) {
+      const int o = lds_row_tied<NV>(q + 1, acc);
+#pragma unroll
+      for (int e = 0; e < NV; ++e) nxt[e] = S[o + e * NV];
+    }
+#pragma unroll
+    for (int e = 0; e < NV; ++e) acc[e] += cur[e] * v[q];
+    if (q + 1 < NV) {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) cur[e] = nxt[e];
+    }
+  }
+}
+
 // wave_solve_lds with the factorisation stored at row stride NP.
 template <int NV, int NP>
 __device__ __forceinline__ void grp_solve_lds(const double* LU, double (&rhs)[NV]) {
@@ -727,12 +756,16 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
         double w[NV];
 #pragma unroll
         for (int e = 0; e < NV; ++e) w[e] = 0.0;
+#ifdef RX_GRP_TIED1  // A/B: each row's reads wait for the previous row's products
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
           const int o = lds_row_tied<NV>(q, w);
 #pragma unroll
           for (int e = 0; e < NV; ++e) w[e] += S[o + e * NV] * s[q];
         }
+#else
+        lds_colprod<NV>(S, s, w);
+#endif
         if (t < 2) RX_GSTAMP(5 + 2 * t);
         wave_sync();
         if (nu > 0) {
@@ -777,12 +810,16 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
           double x[NV];
 #pragma unroll
           for (int e = 0; e < NV; ++e) x[e] = 0.0;
+#ifdef RX_GRP_TIED1
 #pragma unroll
           for (int q = 0; q < NV; ++q) {
             const int o = lds_row_tied<NV>(q, x);
 #pragma unroll
             for (int e = 0; e < NV; ++e) x[e] += S[o + e * NV] * w[q];
           }
+#else
+          lds_colprod<NV>(S, w, x);
+#endif
 #pragma unroll
           for (int e = 0; e < NV; ++e) d[e] -= x[e];
         }

@@ -446,14 +446,18 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     // row a of Gamma reads), and Gamma is built over them in place row by row: the 2 NS^2 Dij loads are consumed
     // at once instead of being held in registers from the top of the kernel. Dmax is an exact max (order-free).
     const Scr Gt = scr;  // LDS scratch of this lane (NS*NS)
+    // Dij is symmetric at every point (GetDij_SM sets Dij(j, i) = Dij(i, j), reacting_model_library.cpp:761-762;
+    // k_set_primitive stores the one quotient in both places), so the harmonic mean of pair (a, b) is the same double
+    // as that of (b, a): each is made once. Dmax is an exact max (order-free).
     double Dmax = -INFINITY;
 #pragma unroll
     for (int b = 0; b < NS; ++b)
 #pragma unroll
-      for (int a = 0; a < NS; ++a) {
+      for (int a = 0; a <= b; ++a) {
         const double dm = Dm(b * NS + a);
         Dmax = fmax(Dmax, dm);
         Gt[a * NS + b] = dm;
+        if (a != b) Gt[b * NS + a] = dm;
       }
     const double alpha = rx_div(1.0, rx_recip(rho * Dmax));
     double sigma = 0.0, massTot = 0.0;

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-5 cycle l: the grouped ILU build's block products with one row of LDS reads in flight, and k_visc_edge's
+# symmetric harmonic means made once: the whole GPU suite, the build's phase trace, and same-box bench A/B against
+# librx_tied1.so (the products as before) and librx_r5d.so.
+mkdir -p gpurun_out
+PKG=$PWD/development-of-a-turbulent-numerical-solver-for-reactive-flows-in-su2_amd
+T=r05l
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1; rc=$?; echo "gpu tests rc=$rc"; grep -cE "PASSED" gpurun_out/gpu_tests_$T.log; grep -E "FAILED|Error" gpurun_out/gpu_tests_$T.log | head -5; tail -1 gpurun_out/gpu_tests_$T.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python tools/ilu_trace.py 2000 500 256 > gpurun_out/ilu_trace_$T.log 2>&1; echo "trace rc=$?"; tail -12 gpurun_out/ilu_trace_$T.log
+run() { timeout -k 10 300 env $2 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/bench_${T}_$1.log 2>&1 && python tools/ab_table.py $1=gpurun_out/bench_${T}_$1.log && python3 -c "
+import json; l=[x for x in open('gpurun_out/bench_${T}_$1.log') if x.startswith('{')][-1]; k=json.loads(l)['roofline_kernels']
+print('   ', {p: v['avg_launch_us'] for p, v in k.items() if p in ('ILU_APPLY', 'SPMV', 'ILU_BUILD', 'ASSEMBLE', 'VISC')})"; }
+run new RX_LIB=$PKG/librx.so && run tied1 RX_LIB=$PKG/librx_tied1.so && run old RX_LIB=$PKG/librx_r5d.so && \
+run newb RX_LIB=$PKG/librx.so && run tied1b RX_LIB=$PKG/librx_tied1.so || exit 2
+timeout -k 10 400 python bench.py --workload c5 --no-cpu-baseline --steps 8 > gpurun_out/bench_${T}_c5.log 2>&1 && python tools/ab_table.py c5=gpurun_out/bench_${T}_c5.log
