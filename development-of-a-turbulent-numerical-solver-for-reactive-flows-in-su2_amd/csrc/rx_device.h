@@ -339,6 +339,22 @@ __device__ __host__ inline void ausm_jac_entry(const AusmEdge& s, const AusmCol&
   *jj = vj * s.Area;
 }
 
+// The entry of one side only (side 0: Jac_i, 1: Jac_j): the two sides' expressions differ only in the operands
+// (PlL / PlR, MiL / MiR, mLF / mRF, Sib / Sjb, PDL / PDR), so they are selected first and the entry is evaluated once
+// — the same operations as ausm_jac_entry's vi / vj on the same values. Sb: this side's S[b].
+template <int NDIM>
+__device__ __host__ inline double ausm_jac_entry_own(const AusmEdge& s, const AusmCol& c, double phia_i, double phia_j,
+                                                     double Sb, int a, int b, int side) {
+  const double Pl = side ? c.PlR : c.PlL, Mi = side ? c.MiR : c.MiL, mF = side ? s.mRF : s.mLF;
+  const double PD = side ? c.PDR : c.PDL;
+  double v = 0.0;
+  v += s.mss * ((Pl * s.rho_i * phia_i) + (Mi * s.rho_j * phia_j));
+  if (a == b) v += s.mss * mF;
+  if (a == NDIM + 1) v += s.mss * mF * Sb;
+  if (a >= 1 && a <= NDIM) v += s.UN[a - 1] * PD;
+  return v * s.Area;
+}
+
 
 // ---- correctly rounded x^1.75 (x > 0, normal), for ReactingModelLibrary::GetDij_SM's pow(T, 1.75)
 // (reacting_model_library.cpp:751-766). The host libm's pow is correctly rounded for all but ~0.07 % of the

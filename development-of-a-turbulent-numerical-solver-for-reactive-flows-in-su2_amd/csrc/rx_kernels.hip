@@ -1045,11 +1045,12 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     bool bad = false;
 #pragma unroll
     for (int a = 0; a < nVar; ++a) {
-      double ji, jj;
-      ausm_jac_entry<NDIM>(s, cc, ausm_phi<NDIM>(Vsi, Vsi[NDIM + 3], a), ausm_phi<NDIM>(Vsj, Vsj[NDIM + 3], a), sib,
-                           sjb, a, bc, &ji, &jj);
-      bad |= isnan(ji) || isnan(jj);
-      jd[a] = side ? jj : ji;
+      // (k_ausm_edge's NaN check sees both sides' entries; the other side's is the neighbour team's own entry, checked
+      // there, so every entry of the edge is still checked once)
+      const double v = ausm_jac_entry_own<NDIM>(s, cc, ausm_phi<NDIM>(Vsi, Vsi[NDIM + 3], a),
+                                                ausm_phi<NDIM>(Vsj, Vsj[NDIM + 3], a), side ? sjb : sib, a, bc, side);
+      bad |= isnan(v);
+      jd[a] = v;
     }
     return bad;
   };

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-5 cycle m: the grouped ILU build's pipelined block products (librx.so) against RX_GRP_TIED1 (librx_tied1.so):
-# the ILU parity tests, the build's phase trace, same-box bench A/B at C3 and C5.
+# Round-5 cycle m: the grouped ILU build's pipelined block products and the fused assembly's own-side AUSM entries
+# (librx.so) against librx_tied1.so (neither): the whole GPU suite, the build's phase trace, same-box bench A/B at C3
+# and C5.
 mkdir -p gpurun_out
 PKG=$PWD/development-of-a-turbulent-numerical-solver-for-reactive-flows-in-su2_amd
 T=r05m
-timeout -k 10 600 python -u -m pytest tests/test_gpu_partitions.py tests/test_gpu_linsolve.py -x -v \
-  --timeout 170 --timeout-method thread > gpurun_out/ilu_tests_$T.log 2>&1; rc=$?; echo "ilu tests rc=$rc"; grep -cE "PASSED" gpurun_out/ilu_tests_$T.log; grep -E "FAILED|Error" gpurun_out/ilu_tests_$T.log | head -5
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1; rc=$?; echo "gpu tests rc=$rc"; grep -cE "PASSED" gpurun_out/gpu_tests_$T.log; grep -E "FAILED|Error" gpurun_out/gpu_tests_$T.log | head -5; tail -1 gpurun_out/gpu_tests_$T.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python tools/ilu_trace.py 2000 500 256 > gpurun_out/ilu_trace_$T.log 2>&1; echo "trace rc=$?"; tail -12 gpurun_out/ilu_trace_$T.log
 run() { timeout -k 10 300 env $2 python bench.py --no-cpu-baseline --steps 10 $3 > gpurun_out/bench_${T}_$1.log 2>&1 && python tools/ab_table.py $1=gpurun_out/bench_${T}_$1.log && python3 -c "
