@@ -81,7 +81,12 @@ def pmc_fp64_flop(kernel, workload_key):
     return None
 
 
-def ilu_apply_kernels(N, nnzb, nVar, parts):
+def ring_groups():
+    """Wave groups per ring-sweep workgroup (rx_ilu_ring_groups in rx_sweeps.hip: env RX_ILU_RING_G, default 2)."""
+    return 1 if os.environ.get("RX_ILU_RING_G", "").strip() == "1" else 2
+
+
+def ilu_apply_kernels(N, nnzb, nVar, parts, nDim=2):
     """The ILU(0) apply kernels rx_la_ilu_apply launches for this partitioning (rx_sweeps.hip): the LDS-resident
     sweep when a partition's vector, metadata and columns fit the 160 KiB LDS, else the wide global sweeps."""
     rows = -(-N // parts)
@@ -93,7 +98,11 @@ def ilu_apply_kernels(N, nnzb, nVar, parts):
     if nVar >= 5 and not (os.environ.get("RX_ILU_NO_RING") or os.environ.get("RX_NARROW_APPLY")):
         # round 5: both sweeps with the x rows in an LDS ring (when every level has at most 16 * (64 // nVar) rows,
         # as on the C3 / C5 partitions: rocprof shows it there, profiles/r05_c3_kernel_stats.md)
-        return f"k_ilu_apply_ring<{nVar}, 1024, 2>"
+        # template <NV, threads, factor blocks of a row in registers, wave groups>: 3-D rows (up to 7 blocks) take
+        # 768 threads with three blocks in registers (rx_ilu_ring_tb; RX_RING_3D=0: the 2-D shape)
+        if nDim == 3 and os.environ.get("RX_RING_3D", "1") != "0":
+            return f"k_ilu_apply_ring<{nVar}, 768, 3, {ring_groups()}>"
+        return f"k_ilu_apply_ring<{nVar}, 1024, 2, {ring_groups()}>"
     return f"k_ilu_apply_wide<{nVar}, 1024>"  # both sweeps of a partition in one launch (round 4)
 
 
@@ -148,7 +157,7 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         # FGMRES's w = A z (k_fg_spmv_full): every block + its column index once, z gathered, w written
         "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d, "k_fg_spmv_full" + tv),
         # ILU(0) apply: L and U blocks + inv(D_i) (= nnzb blocks) + column indices, b in, x out
-        "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, ilu_apply_kernels(N, nnzb, nVar, parts)),
+        "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, ilu_apply_kernels(N, nnzb, nVar, parts, nDim)),
     }
     if fused:
         del models["CONV"]  # the CONV phase launches no flux kernel (only MUSCL's reconstruction at 2nd order)
@@ -157,11 +166,10 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
 
 def conv_fused(nDim):
     """Whether the implicit AUSM fluxes and Jacobians are made inside k_asm_visc (rx_fuse_conv, rx_kernels.hip):
-    in 2-D by default, RX_ASM_CONV=1 / 0 in both / neither, never with RX_ASM_VISC=0."""
+    by default in 2-D and 3-D (round 5), never with RX_ASM_CONV=0 or RX_ASM_VISC=0."""
     if os.environ.get("RX_ASM_VISC", "1") == "0":
         return False
-    v = os.environ.get("RX_ASM_CONV")
-    return v == "1" if v is not None else nDim == 2
+    return not os.environ.get("RX_ASM_CONV", "").startswith("0")
 
 
 def pmc_traffic(kernel, workload_key, field="hbm_bytes"):

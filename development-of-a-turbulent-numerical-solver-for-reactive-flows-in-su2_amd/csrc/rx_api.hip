@@ -314,7 +314,7 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       // widest sub-level); a block (i, j) of a dependency less than R sub-levels back reads it there, a farther one
       // from j's far row R W + (its index among the partition's far sources), written by j as well
       {
-        const int cap = std::max(1, rx_ilu_ring_rpb(ctx->nVar) / rx_ilu_ring_groups());
+        const int cap = std::max(1, rx_ilu_ring_rpb(ctx->nVar, rx_ilu_ring_tb(ctx)) / rx_ilu_ring_groups());
         std::vector<int32_t> slv(N, 0), spos(N, 0), rpart_lvl(np + 1, 0), rlvl_ptr(1, 0);
         int W = 1;
         S.rmaxlev = 0;

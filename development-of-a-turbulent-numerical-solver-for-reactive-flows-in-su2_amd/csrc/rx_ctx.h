@@ -261,7 +261,8 @@ bool rx_fuse_conv(int nDim);
 // levels of the ILU(0) sweeps' LDS ring (k_ilu_apply_ring): a row's result is read from the ring slot of its level
 // by the rows up to kIluRing - 1 levels later, from a per-partition "far" slot by later ones
 constexpr int kIluRing = 4;
-int rx_ilu_ring_rpb(int nv);  // rows per pass of k_ilu_apply_ring (1024 threads)
+int rx_ilu_ring_rpb(int nv, int tb);  // rows per pass of k_ilu_apply_ring (tb threads)
+int rx_ilu_ring_tb(const rx_ctx* ctx);  // its workgroup size for this context (1 024, or 768 in 3-D)
 int rx_ilu_ring_groups();     // wavefront groups of k_ilu_apply_ring taking turns by level (RX_ILU_RING_G, default 2)
 int rx_launch_visc_edge(rx_ctx* ctx);
 int rx_launch_gather_edge_flux(rx_ctx* ctx, const double* flux, double sign_first);

@@ -989,6 +989,14 @@ struct AusmIn {
 #ifndef RX_WPE_ASMV
 #define RX_WPE_ASMV RX_WPE(NDIM == 2 ? 3 : 2)
 #endif
+#ifndef RX_ASMV_NARROW
+// build knob: 1 (default) = teams of nVar lanes, floor(64 / nVar) nodes per wavefront (5 at nVar 11 / 12, lanes 55..63
+// or 60..63 idle); 0 = 16-lane teams, 4 nodes per wavefront with 5 / 4 of every 16 lanes idle
+#define RX_ASMV_NARROW 1
+#endif
+// a k_asm_visc team's width and the nodes one 256-thread workgroup assembles
+__host__ __device__ constexpr int asmv_team_width(int nVar) { return RX_ASMV_NARROW ? nVar : 16; }
+__host__ __device__ constexpr int asmv_nodes_per_block(int nVar) { return (kBlock / 64) * (64 / asmv_team_width(nVar)); }
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     int N, const int32_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj, const int32_t* __restrict__ edges,
@@ -996,7 +1004,9 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     const double* __restrict__ Fv, const double* __restrict__ Jc, const double* __restrict__ dTdU,
     const double* __restrict__ Summ, const double* __restrict__ Js, const double* __restrict__ Rsrc, DevMech m,
     ViscParams P, double* __restrict__ R, double* __restrict__ A, int src, AusmIn cv) {
-  constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>(), kTeams = kBlock / 16;
+  constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>();
+  constexpr int TW = asmv_team_width(nVar), TPW = 64 / TW, kTeams = asmv_nodes_per_block(nVar);
+  static_assert(TW >= nVar && TW <= 64, "a team holds one lane per column");
   constexpr int nPV = NS + NDIM + 5;
   constexpr int rhos = NDIM + 2, nsv = NS * nVar;
   constexpr int CD = RX_ASMV_CDEG < 0 ? (NDIM == 2 ? 4 : 6) : (RX_ASMV_CDEG > 0 ? RX_ASMV_CDEG : 1);
@@ -1006,11 +1016,13 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   // (RX_ASMV_PARK: at 0, reused by the summary)
   constexpr int SCO = RX_ASMV_PARK ? 0 : SS;
   constexpr int TS = !RX_ASMV_SHS ? SS : (RX_ASMV_PARK ? (CD * kES > SS ? CD * kES : SS) : SS + CD * kES);
-  static_assert(CD <= 16, "the shared edge scalars of the first CD edges are made by team lanes 0..CD-1 (16 lanes)");
+  static_assert(CD <= TW, "the shared edge scalars of the first CD edges are made by team lanes 0..CD-1");
   __shared__ double ssm[kTeams * TS];
-  const int gt = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  const int i = gt / 16, b = gt % 16, team = threadIdx.x / 16;
-  if (i >= N) return;  // whole teams (N * 16 threads)
+  const int lane = threadIdx.x % 64, wv = threadIdx.x / 64, tw = lane / TW;
+  if (tw >= TPW) return;  // the wavefront's lanes past its last whole team
+  const int team = wv * TPW + tw, b = lane - tw * TW, sbase = tw * TW;
+  const int i = xcd_block(blockIdx.x, gridDim.x) * kTeams + team;
+  if (i >= N) return;  // whole teams
   const bool col = b < nVar;
   const int bc = col ? b : 0;
   double* slot = ssm + team * TS;
@@ -1168,7 +1180,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
     {
       const double* tile = Summ + (size_t)(e / kSummTile) * SS * kSummTile + e % kSummTile;
-      for (int q = b; q < SS; q += 16) slot[q] = tile[(size_t)q * kSummTile];
+      for (int q = b; q < SS; q += TW) slot[q] = tile[(size_t)q * kSummTile];
     }
     const double sob = dTdU[(size_t)(side ? n1 : n0) * nVar + bc];  // the own node's dT/dU
     double* Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
@@ -1197,7 +1209,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    visc_jac_column_own<NS, NDIM>(m, P, SummCRef{slot, 1}, sob, side, b, b, [&](int rr, double jv) {
+    visc_jac_column_own<NS, NDIM>(m, P, SummCRef{slot, 1}, sob, side, b, b, sbase, [&](int rr, double jv) {
       D[rr] = side ? D[rr] + jv : D[rr] - jv;
       Ao[rr * nVar + b] = side ? jco[rr] - jv : jco[rr] + jv;
     });
@@ -1635,17 +1647,20 @@ int RX_NSFN(rx_launch_ausm_node)(rx_ctx* ctx) {
 
 #if !RX_NS
 // the implicit convective fluxes and Jacobians are made by the node-centric assembly (k_asm_visc's fused AUSM pass)
-// instead of k_ausm_edge when the assembly also makes the viscous Jacobians, in 2-D by default: C3 (same box) CONV
-// 1.31 + ASSEMBLE 4.89 -> ASSEMBLE 6.79 ms; in 3-D each node's 6 edges and the 2-wave occupancy lose, C5 CONV 2.29 +
-// ASSEMBLE 8.71 -> 12.10 ms (11.76 with the LDS-shared edge scalars). RX_ASM_CONV=1 fuses in both, =0 in neither (A/B); RX_ASM_VISC=0 never fuses
+// instead of k_ausm_edge whenever the assembly also makes the viscous Jacobians. 2-D since round 4: C3 (same box) CONV
+// 1.31 + ASSEMBLE 4.89 -> ASSEMBLE 6.79 ms then, 5.75 ms now. 3-D since round 5: with only the own side's entries
+// evaluated and nVar-lane teams (5 nodes per wavefront), C5 (same box, gpurun_out r05q) CONV 2.01 + ASSEMBLE 7.53 ->
+// ASSEMBLE 9.13 ms, 39.91 -> 39.55 ms per step (round 4: 2.29 + 8.71 -> 11.76 ms, so 3-D kept the edge kernel).
+// RX_ASM_CONV=0 never fuses (A/B, tests/test_gpu_assembly.py); RX_ASM_VISC=0 never fuses
 bool rx_fuse_conv(int nDim) {
+  (void)nDim;
   static const int mode = [] {
     const char* v = getenv("RX_ASM_CONV");
     const char* w = getenv("RX_ASM_VISC");
     if (w && w[0] == '0') return 0;
-    return v ? (v[0] == '1' ? 1 : 0) : 2;
+    return v && v[0] == '0' ? 0 : 1;
   }();
-  return mode == 1 || (mode == 2 && nDim == 2);
+  return mode == 1;
 }
 #endif  // !RX_NS
 
@@ -1738,7 +1753,9 @@ int RX_NSFN(rx_launch_asm_visc)(rx_ctx* ctx, int with_src, int fused_conv) {
     cv.SR = ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
     cv.normal = ctx->normal;
   }
-  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<blocks(ctx->N * 16), kBlock, 0, ctx->stream>>>(
+  RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<(ctx->N + asmv_nodes_per_block(NS_ + ND_ + 2) - 1) /
+                                                                     asmv_nodes_per_block(NS_ + ND_ + 2),
+                                                                 kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
                             ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech,
                             P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv)));

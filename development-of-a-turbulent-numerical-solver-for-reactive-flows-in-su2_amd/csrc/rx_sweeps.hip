@@ -2388,7 +2388,15 @@ int rx_la_ilu_materialize(rx_ctx* ctx) {
 #define RX_ILU_MAX_WAVES 12
 #endif
 int rx_ilu_stage() { return kStage; }
-int rx_ilu_ring_rpb(int nv) { return (1024 / 64) * (64 / nv); }  // ring_rpb<nv, 1024>()
+int rx_ilu_ring_rpb(int nv, int tb) { return (tb / 64) * (64 / nv); }  // ring_rpb<nv, tb>()
+// The ring sweeps' shape: 1 024 threads with two factor blocks of a row in registers (2-D: two lower / upper blocks
+// per row on the quad meshes), or 768 threads (3 waves per SIMD, room for the registers) with three (3-D: the hex
+// meshes' rows have three), so that a row's blocks are all loaded a level ahead instead of the third inside its level.
+// RX_RING_3D=0 gives 3-D the 2-D shape (A/B).
+int rx_ilu_ring_tb(const rx_ctx* ctx) {
+  static const bool off = getenv("RX_RING_3D") && getenv("RX_RING_3D")[0] == '0';
+  return ctx->nDim == 3 && !off ? 768 : 1024;
+}
 int rx_ilu_ring_groups() {  // RX_ILU_RING_G=1: every wavefront at every level (the first ring kernel, A/B)
   static const int g = getenv("RX_ILU_RING_G") && atoi(getenv("RX_ILU_RING_G")) == 1 ? 1 : 2;
   return g;
@@ -2408,6 +2416,10 @@ int rx_la_prepare(rx_ctx* ctx) {
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2, 1>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2, 2>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 768, 3, 1>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 768, 3, 2>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     }
     if constexpr (NV_ >= 5)
@@ -2557,25 +2569,34 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
   // restores the wide sweeps below (A/B)
   static const bool no_ring = getenv("RX_ILU_NO_RING") != nullptr;
   // (its sub-level plan splits the levels wider than one group's rows)
+  const int tb = rx_ilu_ring_tb(ctx);
   const size_t ring_shm = sizeof(double) * ((size_t)std::max(ctx->fs.ring_rows, ctx->bs.ring_rows) * nv +
-                                            (size_t)rx_ilu_ring_rpb(nv) * nv) +
+                                            (size_t)rx_ilu_ring_rpb(nv, tb) * nv) +
                           sizeof(int32_t) * (size_t)(std::max(ctx->fs.rmaxlev, ctx->bs.rmaxlev) + 1);
-  if (!no_ring && !narrow && nv >= 5 && width * nv > 256 && width <= rx_ilu_ring_rpb(nv) &&
+  if (!no_ring && !narrow && nv >= 5 && width * nv > 256 && width <= 2 * rx_ilu_ring_rpb(nv, tb) &&
       ring_shm <= (size_t)ctx->lds_max) {
     const int4* fsl = reinterpret_cast<const int4*>(ctx->fs.slot);
     const int4* bsl = reinterpret_cast<const int4*>(ctx->bs.slot);
     const int2* fr = reinterpret_cast<const int2*>(ctx->fs.ring);
     const int2* br = reinterpret_cast<const int2*>(ctx->bs.ring);
     const int rr = std::max(ctx->fs.ring_rows, ctx->bs.ring_rows);
-    if (rx_ilu_ring_groups() == 1) {
-      RX_NV_SWITCH(nv, (k_ilu_apply_ring<NV_, 1024, 2, 1><<<ctx->npart, 1024, ring_shm, ctx->stream>>>(
-                           ctx->fs.rpart_lvl, ctx->fs.rlvl_ptr, fsl, fr, ctx->bs.rpart_lvl, ctx->bs.rlvl_ptr, bsl, br,
-                           ctx->ring_xoff, ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv, rr)));
+    const int g = rx_ilu_ring_groups();
+#define RX_RING_LAUNCH(TB_, MB_, G_)                                                                                \
+  RX_NV_SWITCH(nv, (k_ilu_apply_ring<NV_, TB_, MB_, G_><<<ctx->npart, TB_, ring_shm, ctx->stream>>>(                \
+                       ctx->fs.rpart_lvl, ctx->fs.rlvl_ptr, fsl, fr, ctx->bs.rpart_lvl, ctx->bs.rlvl_ptr, bsl, br,   \
+                       ctx->ring_xoff, ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv, rr)))
+    if (tb == 768) {
+      if (g == 1) {
+        RX_RING_LAUNCH(768, 3, 1);
+      } else {
+        RX_RING_LAUNCH(768, 3, 2);
+      }
+    } else if (g == 1) {
+      RX_RING_LAUNCH(1024, 2, 1);
     } else {
-      RX_NV_SWITCH(nv, (k_ilu_apply_ring<NV_, 1024, 2, 2><<<ctx->npart, 1024, ring_shm, ctx->stream>>>(
-                           ctx->fs.rpart_lvl, ctx->fs.rlvl_ptr, fsl, fr, ctx->bs.rpart_lvl, ctx->bs.rlvl_ptr, bsl, br,
-                           ctx->ring_xoff, ctx->f[RX_F_ILU], rx_ilu_upper(ctx), rx_invd_buf(ctx), b, x, done, conv, rr)));
+      RX_RING_LAUNCH(1024, 2, 2);
     }
+#undef RX_RING_LAUNCH
     RX_HIP(hipGetLastError());
     return ctx->defer_exchange ? RX_OK : rx_la_exchange(ctx, x, nv);
   }

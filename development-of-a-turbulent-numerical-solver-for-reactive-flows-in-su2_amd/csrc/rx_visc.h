@@ -982,9 +982,10 @@ __device__ inline void visc_jac_column_f(const DevMech& m, const ViscParams& P, 
 // sigma, sum M_s X_s, dT/dU, velocity) and in signs: every j-side quantity is the i-side expression evaluated on the
 // j data with the sign flipped at the same points (-(a - t) = (-a) + t exactly in round-to-nearest), so each entry
 // here is, bitwise, the one visc_jac_column_f hands to put for that side. Sob: dT/dU[b] of the own node.
+// sbase: the wave lane of the team's lane 0 (teams of TW lanes, not necessarily a power of two)
 template <int NS, int NDIM, typename Put>
 __device__ inline void visc_jac_column_own(const DevMech& m, const ViscParams& P, const SummCRef sm, double Sob,
-                                           int side, int b, int tl, Put put) {
+                                           int side, int b, int tl, int sbase, Put put) {
   using L = VSL<NDIM>;
   constexpr int nVar = NS + NDIM + 2, NF = NDIM + 2;
   constexpr int RHOE_S = NDIM + 1, RHOS_S = NDIM + 2;
@@ -1022,7 +1023,7 @@ __device__ inline void visc_jac_column_own(const DevMech& m, const ViscParams& P
   const double dko = rx_div(rho * Ds[kk] * totMass_o * sigma_o, r2);
 #pragma unroll
   for (int a = 0; a < NS; ++a) {
-    double v = __shfl(bo, a, 16);
+    double v = __shfl(bo, sbase + a);
     if (k >= 0) {
       v -= rx_div(rho * Ys[a] * Ds[kk] * totMass_o * sigma_o, r2);
       if (a == k) v += dko;

@@ -11,7 +11,9 @@ def test_ilu_apply_kernel_names(monkeypatch):
     for v in ("RX_ILU_SPLIT", "RX_ILU_NO_RING", "RX_NARROW_APPLY"):
         monkeypatch.delenv(v, raising=False)
     # C3: 1M points, 256 partitions of 3 906 rows -> the vector does not fit LDS: the LDS-ring sweeps (round 5)
-    assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_ring<11, 1024, 2>"
+    assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_ring<11, 1024, 2, 2>"
+    # C5 (3-D, 200x100x100 in 256 partitions): the 3-D ring shape
+    assert bench.ilu_apply_kernels(2_000_000, 13_880_000, 12, 256, nDim=3) == "k_ilu_apply_ring<12, 768, 3, 2>"
     monkeypatch.setenv("RX_ILU_NO_RING", "1")  # the fused wide sweeps (round 4)
     assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_wide<11, 1024>"
     # C4's share per GPU at 2048 partitions: 488-row partitions fit LDS
@@ -30,8 +32,8 @@ def test_kernel_models_cover_the_timed_phases(monkeypatch):
     # the node-centric assembly (default) makes the viscous Jacobians and the AUSM fluxes / Jacobians itself:
     # no k_ausm_edge launch in the CONV phase, and no per-edge convective blocks in the assembly's bytes
     assert m["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>" and "CONV" not in m
-    m3 = bench.kernel_models(8_000_000, 23_580_000, 62_000_000, 7, 3, 5)  # 3-D: the edge kernel by default
-    assert m3["CONV"]["kernel"] == "k_ausm_edge<7, 3>"
+    m3 = bench.kernel_models(8_000_000, 23_580_000, 62_000_000, 7, 3, 5)  # 3-D: fused too (round 5)
+    assert m3["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 3>" and "CONV" not in m3
     monkeypatch.setenv("RX_ASM_CONV", "0")
     u = bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)
     assert u["CONV"]["kernel"] == "k_ausm_edge<7, 2>" and u["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>"

@@ -1,7 +1,7 @@
 """The implicit system's assembly paths: the 2-D node-centric assembly that also evaluates the AUSM
 flux and Jacobians (k_asm_visc's fused pass, the default) against the per-edge convective kernel path
 (k_ausm_edge + k_asm_visc's non-fused pass, RX_ASM_CONV=0), bitwise, for 1st order and both MUSCL branches; the
-3-D fusion forced on (RX_ASM_CONV=1) against its default edge kernel; and a re-assembly of the same residual after
+3-D fused default (round 5) against the edge kernel path, 1st order and MUSCL; and a re-assembly of the same residual after
 an intermediate download (Upwind, Viscous, RES download, then Source) against the straight sequence and the
 reference's golden system. Requires an MI355X."""
 import os
@@ -37,11 +37,12 @@ def test_fused_ausm_assembly_is_bitwise_the_edge_kernel_path(tmp_path, case, ord
     assert np.array_equal(fused["jac"], edge["jac"])
 
 
-def test_fused_ausm_assembly_3d_forced_is_bitwise(tmp_path):
-    forced = run_variant(tmp_path, "mini3d", 0, "1")  # 3-D default is the edge kernel
-    edge = run_variant(tmp_path, "mini3d", 0, None)
-    assert np.array_equal(forced["res"], edge["res"])
-    assert np.array_equal(forced["jac"], edge["jac"])
+@pytest.mark.parametrize("order", [0, 2])
+def test_fused_ausm_assembly_3d_is_bitwise(tmp_path, order):
+    fused = run_variant(tmp_path, "mini3d", order, None)  # 3-D default since round 5: the fused pass
+    edge = run_variant(tmp_path, "mini3d", order, "0")
+    assert np.array_equal(fused["res"], edge["res"])
+    assert np.array_equal(fused["jac"], edge["jac"])
 
 
 @pytest.mark.parametrize("case", ["mini9", "mini3d"])
