@@ -154,8 +154,10 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         "ILU_BUILD": (hbm((nnzb + (nnzb - N) // 2 + 2 * N) * blk, "k_ilu_build_grp" + tv) if ilu_grouped else
                       hbm((2 * nnzb + N) * blk, "k_ilu_build_part" + tv)),
         # SOLVE phase (inside the FGMRES graph; timed by an eager replay of one step after the timed region):
-        # FGMRES's w = A z (k_fg_spmv_full): every block + its column index once, z gathered, w written
-        "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d, "k_fg_spmv_full" + tv),
+        # FGMRES's w = A z (k_fg_spmv_stage for the flow blocks, k_fg_spmv_full for the SST's 2x2): every block + its
+        # column index once, z gathered, w written
+        "SPMV": hbm(nnzb * (blk + 4) + (N + 1) * 4 + 2 * N * nVar * d,
+                    ("k_fg_spmv_stage" if nVar > 4 else "k_fg_spmv_full") + tv),
         # ILU(0) apply: L and U blocks + inv(D_i) (= nnzb blocks) + column indices, b in, x out
         "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, ilu_apply_kernels(N, nnzb, nVar, parts, nDim)),
     }

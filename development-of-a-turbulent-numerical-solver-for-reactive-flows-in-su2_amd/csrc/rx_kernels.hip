@@ -976,12 +976,13 @@ struct AusmIn {
 #define RX_ASMV_FUSE 1  // build knob: 0 compiles k_asm_visc without its fused AUSM pass
 #endif
 #ifndef RX_ASMV_PARK
-// build knob: 1 (default) = the fused pass parks 0 -+ Jc in the off-diagonal block for the viscous pass to finish (each
-// off-diagonal block written twice, read back once); 0 = written once, the column re-evaluated in the viscous pass
-// (VERDICT r04 #3). Same-box A/B at C3 (gpurun_out r05c, two runs each): ASSEMBLE 6.16 / 6.15 ms parked against
-// 6.92 / 6.93 single-write — re-evaluating the AUSM column costs more than the second write of the block; C5 8.81 vs
-// 9.06 ms
-#define RX_ASMV_PARK 1
+// build knob: 0 (default since round 5's cycle r) = each off-diagonal block written once, the own-side AUSM column
+// evaluated again in the viscous pass; 1 = the fused pass parks 0 -+ Jc in the off-diagonal block for
+// the viscous pass to finish (each off-diagonal block written twice, read back once). Same-box A/B at C3, two runs
+// each: first (r05c) ASSEMBLE 6.16 / 6.15 ms parked against 6.92 / 6.93 single-write; once the column evaluates only
+// its own side's entries and the teams are nVar lanes wide (r05r): 5.77 / 5.78 parked against 5.56 / 5.58, C5 9.15
+// against 8.79 ms
+#define RX_ASMV_PARK 0
 #endif
 #ifndef RX_ASMV_CDEG
 #define RX_ASMV_CDEG -1  // build knob: node degree up to which k_asm_visc's convective pass loads everything first

@@ -233,6 +233,112 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv_full(int Nd, const int32_t* 
   if (q < (int64_t)Nd * NV) w[q] = spmv_elem<NV>(q, rp, col, A, z);
 }
 
+// k_fg_spmv_full for the flow blocks (NV > 4) with the blocks staged through LDS (round 5). Element (row i, component
+// a) on one lane reads row a of each block: 88 contiguous bytes per lane, so each of a wavefront's six block loads
+// touched ~44 cache lines for 1 KiB (the kernel's waves were 72 % waiting on instruction issue, r05_c3_stall.json).
+// Here a wavefront owns NN = 64 / NV whole rows of the system and walks their blocks by position s (s-th block of each
+// row at once): the NN blocks are copied to the wavefront's LDS slot by consecutive lanes (each load 512 contiguous
+// bytes but for a row boundary), the NN x columns gathered one double per lane, then lane (row, a) makes its sum from
+// LDS. Every sum is spmv_elem's: the blocks of the row in column order, columns ascending, from +0.0, so w is bitwise
+// k_fg_spmv_full's.
+// Same box at C3 (profiles/r05_ab_s.txt, two runs each): 949 / 963 us per SpMV with k_fg_spmv_full, 918 / 915 staged,
+// 897 / 886 staged with the column indices read once and the next step's blocks loaded during this one (the default);
+// C5 1 448 -> 1 430 -> 1 413 us.
+#ifndef RX_SPMV_STAGE
+#define RX_SPMV_STAGE 2  // build knob: 0 = k_fg_spmv_full for every block size; 1 = staged, one step's loads at a time
+#endif
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_fg_spmv_stage(int Nd, const int32_t* __restrict__ rp,
+                                                          const int32_t* __restrict__ col,
+                                                          const double* __restrict__ A, const double* __restrict__ z,
+                                                          double* __restrict__ w, const KState* __restrict__ s) {
+  constexpr int NN = 64 / NV, B2 = NV * NV, CH = NN * B2, NL = (CH + 63) / 64, WPB = kBlock / 64;
+  __shared__ double sa[WPB][CH];
+  __shared__ double sx[WPB][NN * NV];
+  if (s->done) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i0 = (blockIdx.x * WPB + wv) * NN;  // the wavefront's first row
+  if (i0 >= Nd) return;                          // (uniform over the wavefront)
+  // the rows' block ranges: rp[i0 .. i0 + NN] (clamped at Nd: rows past the end have no blocks)
+  const int rpl = rp[min(i0 + (lane <= NN ? lane : 0), Nd)];
+  int r[NN + 1];
+#pragma unroll
+  for (int j = 0; j <= NN; ++j) r[j] = __builtin_amdgcn_readfirstlane(__shfl(rpl, j));
+  int maxdeg = 0;
+#pragma unroll
+  for (int j = 0; j < NN; ++j) maxdeg = max(maxdeg, r[j + 1] - r[j]);
+  // this lane's share of a step's chunk: element e = u * 64 + lane is entry off of row j's block
+  int64_t base[NL];
+  int deg[NL];
+#pragma unroll
+  for (int u = 0; u < NL; ++u) {
+    const int e = u * 64 + lane, j = e < CH ? e / B2 : 0, off = e < CH ? e - j * B2 : 0;
+    int rj = r[0], dj = r[1] - r[0];
+#pragma unroll
+    for (int q = 1; q < NN; ++q)
+      if (j == q) {
+        rj = r[q];
+        dj = r[q + 1] - r[q];
+      }
+    base[u] = (int64_t)rj * B2 + off;
+    deg[u] = e < CH ? dj : 0;
+  }
+  // the x gather: lane l < NN NV fetches component l % NV of row l / NV's s-th column
+  const int xj = lane < NN * NV ? lane / NV : 0, xc = lane - xj * NV;
+  int xr = r[0], xd = r[1] - r[0];
+#pragma unroll
+  for (int q = 1; q < NN; ++q)
+    if (xj == q) {
+      xr = r[q];
+      xd = r[q + 1] - r[q];
+    }
+  if (lane >= NN * NV) xd = 0;
+  // this lane's element
+  const int n = lane / NV, a = lane - n * NV, i = i0 + n;
+  const bool act = n < NN && i < Nd;
+  int nd = 0;
+#pragma unroll
+  for (int q = 0; q < NN; ++q)
+    if (n == q) nd = r[q + 1] - r[q];
+  double acc = 0.0;
+  double* sw = sa[wv];
+  double* sxw = sx[wv];
+  // RX_SPMV_STAGE=2: the rows' column indices read once up front (the wavefront's rows are one contiguous range of at
+  // most 64 blocks, else from global memory at each step) and each step's blocks loaded during the previous step
+  const int rng = r[NN] - r[0];
+  const int cl = RX_SPMV_STAGE == 2 && lane < rng ? col[r[0] + lane] : 0;
+  const bool cpre = RX_SPMV_STAGE == 2 && rng <= 64;
+  double v[NL];
+  auto load = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < NL; ++u) v[u] = st < deg[u] ? A[base[u] + (int64_t)st * B2] : 0.0;
+  };
+  if (RX_SPMV_STAGE == 2) load(0);
+  for (int st = 0; st < maxdeg; ++st) {
+    if (RX_SPMV_STAGE != 2) load(st);
+    // (the permute runs on every lane, from a lane index kept in range; the global reads only where the row has an
+    // st-th block: a row past the end has xr = rp[Nd], one past the column array)
+    const int xcp = RX_SPMV_STAGE == 2 ? __shfl(cl, min(max(xr + st - r[0], 0), 63)) : 0;
+    const double xv = st < xd ? z[(int64_t)(cpre ? xcp : col[xr + st]) * NV + xc] : 0.0;
+#pragma unroll
+    for (int u = 0; u < NL; ++u)
+      if (u * 64 + lane < CH) sw[u * 64 + lane] = v[u];
+    if (RX_SPMV_STAGE == 2 && st + 1 < maxdeg) load(st + 1);
+    if (lane < NN * NV) sxw[lane] = xv;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (act && st < nd) {
+      const double* ar = sw + n * B2 + a * NV;
+      const double* xr_ = sxw + n * NV;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) acc += ar[c] * xr_[c];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (act) w[(int64_t)i * NV + a] = acc;
+}
+
 // k_fg_spmv_full over a row list (rows[0..n)): the same element arithmetic at the same positions. A distributed
 // solve computes the rows without halo columns while the preconditioned vector's halo is in flight, then the rest.
 template <int NV>
@@ -702,8 +808,13 @@ int prec_spmv(rx_ctx* ctx, const double* in, double* z, double* w, KState* s) {
   if (rc) return rc;
   if (!split) {
     RxPhase ph(ctx, RX_K_SPMV);
-    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_full<NV_><<<blocks(ctx->Nd * NV_), kBlock, 0, st>>>((int)ctx->Nd, ctx->rp,
-                                                                                          ctx->col, A, z, w, s)));
+    if (RX_SPMV_STAGE && ctx->nVar > 4) {
+      RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_stage<NV_><<<blocks(ctx->Nd, (kBlock / 64) * (64 / NV_)), kBlock, 0, st>>>(
+                                  (int)ctx->Nd, ctx->rp, ctx->col, A, z, w, s)));
+    } else {
+      RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_full<NV_><<<blocks(ctx->Nd * NV_), kBlock, 0, st>>>((int)ctx->Nd, ctx->rp,
+                                                                                            ctx->col, A, z, w, s)));
+    }
     return RX_OK;
   }
   const bool overlap = ctx->comm_stream != nullptr && !ctx->has_hcomm;

@@ -42,8 +42,10 @@ def main():
     fe = read_counters(fetch_dir)
     wr = read_counters(write_dir)
     known = 8.0 * nnzb * nv * nv
-    # the FGMRES SpMV (k_fg_spmv before round 3, k_fg_spmv_full since), else the plain SpMV
-    cal = [k for k in (f"k_fg_spmv<{nv}>", f"k_fg_spmv_full<{nv}>", f"k_spmv<{nv}>") if (k, "FETCH_SIZE") in fe][:1]
+    # the FGMRES SpMV (k_fg_spmv before round 3, k_fg_spmv_full since, k_fg_spmv_stage since round 5), else the plain
+    # SpMV
+    cal = [k for k in (f"k_fg_spmv<{nv}>", f"k_fg_spmv_stage<{nv}>", f"k_fg_spmv_full<{nv}>", f"k_spmv<{nv}>")
+           if (k, "FETCH_SIZE") in fe][:1]
     cal_kb = fe.get((cal[0], "FETCH_SIZE")) if cal else None
     factor = known / (cal_kb * 1024.0) if cal_kb else 1.0
     out = {"workload": wkey, "fetch_factor": 2.0,
