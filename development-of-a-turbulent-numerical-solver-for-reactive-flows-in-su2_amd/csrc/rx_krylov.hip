@@ -248,65 +248,74 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv_full(int Nd, const int32_t* 
 #define RX_SPMV_STAGE 2  // build knob: 0 = k_fg_spmv_full for every block size; 1 = staged, one step's loads at a time
 #endif
 template <int NV>
-__global__ __launch_bounds__(kBlock) void k_fg_spmv_stage(int Nd, const int32_t* __restrict__ rp,
+__global__ __launch_bounds__(kBlock) void k_fg_spmv_stage(int n_rows, const int32_t* __restrict__ rows,
+                                                          const int32_t* __restrict__ rp,
                                                           const int32_t* __restrict__ col,
                                                           const double* __restrict__ A, const double* __restrict__ z,
                                                           double* __restrict__ w, const KState* __restrict__ s) {
+  // rows == nullptr: the system's rows 0 .. n_rows - 1; else the row list rows[0 .. n_rows) (a distributed solve's
+  // interior / rank-boundary rows, k_fg_spmv_rows's)
   constexpr int NN = 64 / NV, B2 = NV * NV, CH = NN * B2, NL = (CH + 63) / 64, WPB = kBlock / 64;
   __shared__ double sa[WPB][CH];
   __shared__ double sx[WPB][NN * NV];
   if (s->done) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i0 = (blockIdx.x * WPB + wv) * NN;  // the wavefront's first row
-  if (i0 >= Nd) return;                          // (uniform over the wavefront)
-  // the rows' block ranges: rp[i0 .. i0 + NN] (clamped at Nd: rows past the end have no blocks)
-  const int rpl = rp[min(i0 + (lane <= NN ? lane : 0), Nd)];
-  int r[NN + 1];
+  const int l0 = (blockIdx.x * WPB + wv) * NN;  // the wavefront's first row (of the list)
+  if (l0 >= n_rows) return;                      // (uniform over the wavefront)
+  // lane j < NN: the wavefront's j-th row, its first block and its block count (none past the end)
+  const bool lv = lane < NN && l0 + lane < n_rows;
+  const int rowl = lv ? (rows ? rows[l0 + lane] : l0 + lane) : 0;
+  const int kb = lv ? rp[rowl] : 0, kd = lv ? rp[rowl + 1] - kb : 0;
+  int rb[NN], rd[NN];
 #pragma unroll
-  for (int j = 0; j <= NN; ++j) r[j] = __builtin_amdgcn_readfirstlane(__shfl(rpl, j));
+  for (int j = 0; j < NN; ++j) {
+    rb[j] = __builtin_amdgcn_readfirstlane(__shfl(kb, j));
+    rd[j] = __builtin_amdgcn_readfirstlane(__shfl(kd, j));
+  }
   int maxdeg = 0;
 #pragma unroll
-  for (int j = 0; j < NN; ++j) maxdeg = max(maxdeg, r[j + 1] - r[j]);
+  for (int j = 0; j < NN; ++j) maxdeg = max(maxdeg, rd[j]);
   // this lane's share of a step's chunk: element e = u * 64 + lane is entry off of row j's block
   int64_t base[NL];
   int deg[NL];
 #pragma unroll
   for (int u = 0; u < NL; ++u) {
     const int e = u * 64 + lane, j = e < CH ? e / B2 : 0, off = e < CH ? e - j * B2 : 0;
-    int rj = r[0], dj = r[1] - r[0];
+    int rj = rb[0], dj = rd[0];
 #pragma unroll
     for (int q = 1; q < NN; ++q)
       if (j == q) {
-        rj = r[q];
-        dj = r[q + 1] - r[q];
+        rj = rb[q];
+        dj = rd[q];
       }
     base[u] = (int64_t)rj * B2 + off;
     deg[u] = e < CH ? dj : 0;
   }
   // the x gather: lane l < NN NV fetches component l % NV of row l / NV's s-th column
   const int xj = lane < NN * NV ? lane / NV : 0, xc = lane - xj * NV;
-  int xr = r[0], xd = r[1] - r[0];
+  int xr = rb[0], xd = rd[0];
 #pragma unroll
   for (int q = 1; q < NN; ++q)
     if (xj == q) {
-      xr = r[q];
-      xd = r[q + 1] - r[q];
+      xr = rb[q];
+      xd = rd[q];
     }
   if (lane >= NN * NV) xd = 0;
   // this lane's element
-  const int n = lane / NV, a = lane - n * NV, i = i0 + n;
-  const bool act = n < NN && i < Nd;
+  const int n = lane / NV, a = lane - n * NV;
+  const bool act = n < NN && l0 + n < n_rows;
+  const int i = __shfl(rowl, n < NN ? n : 0);
   int nd = 0;
 #pragma unroll
   for (int q = 0; q < NN; ++q)
-    if (n == q) nd = r[q + 1] - r[q];
+    if (n == q) nd = rd[q];
   double acc = 0.0;
   double* sw = sa[wv];
   double* sxw = sx[wv];
-  // RX_SPMV_STAGE=2: the rows' column indices read once up front (the wavefront's rows are one contiguous range of at
-  // most 64 blocks, else from global memory at each step) and each step's blocks loaded during the previous step
-  const int rng = r[NN] - r[0];
-  const int cl = RX_SPMV_STAGE == 2 && lane < rng ? col[r[0] + lane] : 0;
+  // RX_SPMV_STAGE=2: the rows' column indices read once up front (when the wavefront's rows are one contiguous range
+  // of at most 64 blocks, else from global memory at each step) and each step's blocks loaded during the previous step
+  const int r0 = rb[0], rng = rows ? 65 : rp[min(l0 + NN, n_rows)] - r0;
+  const int cl = RX_SPMV_STAGE == 2 && lane < rng && lane < 64 && !rows ? col[r0 + lane] : 0;
   const bool cpre = RX_SPMV_STAGE == 2 && rng <= 64;
   double v[NL];
   auto load = [&](int st) {
@@ -317,8 +326,8 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv_stage(int Nd, const int32_t*
   for (int st = 0; st < maxdeg; ++st) {
     if (RX_SPMV_STAGE != 2) load(st);
     // (the permute runs on every lane, from a lane index kept in range; the global reads only where the row has an
-    // st-th block: a row past the end has xr = rp[Nd], one past the column array)
-    const int xcp = RX_SPMV_STAGE == 2 ? __shfl(cl, min(max(xr + st - r[0], 0), 63)) : 0;
+    // st-th block)
+    const int xcp = RX_SPMV_STAGE == 2 ? __shfl(cl, min(max(xr + st - r0, 0), 63)) : 0;
     const double xv = st < xd ? z[(int64_t)(cpre ? xcp : col[xr + st]) * NV + xc] : 0.0;
 #pragma unroll
     for (int u = 0; u < NL; ++u)
@@ -810,7 +819,7 @@ int prec_spmv(rx_ctx* ctx, const double* in, double* z, double* w, KState* s) {
     RxPhase ph(ctx, RX_K_SPMV);
     if (RX_SPMV_STAGE && ctx->nVar > 4) {
       RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_stage<NV_><<<blocks(ctx->Nd, (kBlock / 64) * (64 / NV_)), kBlock, 0, st>>>(
-                                  (int)ctx->Nd, ctx->rp, ctx->col, A, z, w, s)));
+                                  (int)ctx->Nd, nullptr, ctx->rp, ctx->col, A, z, w, s)));
     } else {
       RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_full<NV_><<<blocks(ctx->Nd * NV_), kBlock, 0, st>>>((int)ctx->Nd, ctx->rp,
                                                                                             ctx->col, A, z, w, s)));
@@ -828,13 +837,19 @@ int prec_spmv(rx_ctx* ctx, const double* in, double* z, double* w, KState* s) {
   }
   const int ni = (int)ctx->n_spmv_int, nb_rows = (int)(ctx->Nd - ctx->n_spmv_int);
   RxPhase ph(ctx, RX_K_SPMV);
-  if (ni > 0)
-    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)ni * NV_), kBlock, 0, st>>>(
-                                ni, ctx->spmv_rows, ctx->rp, ctx->col, A, z, w, s)));
+  auto rows_spmv = [&](int n, const int32_t* rows) -> int {
+    if (RX_SPMV_STAGE && ctx->nVar > 4) {
+      RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_stage<NV_><<<blocks(n, (kBlock / 64) * (64 / NV_)), kBlock, 0, st>>>(
+                                  n, rows, ctx->rp, ctx->col, A, z, w, s)));
+    } else {
+      RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)n * NV_), kBlock, 0, st>>>(
+                                  n, rows, ctx->rp, ctx->col, A, z, w, s)));
+    }
+    return RX_OK;
+  };
+  if (ni > 0 && (rc = rows_spmv(ni, ctx->spmv_rows))) return rc;
   if (overlap) RX_HIP(hipStreamWaitEvent(st, ctx->comm_join, 0));
-  if (nb_rows > 0)
-    RX_NV_SWITCH(ctx->nVar, (k_fg_spmv_rows<NV_><<<blocks((int64_t)nb_rows * NV_), kBlock, 0, st>>>(
-                                nb_rows, ctx->spmv_rows + ni, ctx->rp, ctx->col, A, z, w, s)));
+  if (nb_rows > 0 && (rc = rows_spmv(nb_rows, ctx->spmv_rows + ni))) return rc;
   return RX_OK;
 }
 
