@@ -247,6 +247,15 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv_full(int Nd, const int32_t* 
 #ifndef RX_SPMV_STAGE
 #define RX_SPMV_STAGE 2  // build knob: 0 = k_fg_spmv_full for every block size; 1 = staged, one step's loads at a time
 #endif
+#ifndef RX_SPMV_XCD
+#define RX_SPMV_XCD 0  // build knob: 1 = consecutive workgroups' rows on one XCD (its L2 then holds their x columns)
+#endif
+__device__ inline int spmv_block(int b, int nb) {  // workgroup b's position: XCD x = b mod 8 takes the x-th eighth
+  if (!RX_SPMV_XCD) return b;
+  constexpr int kXcd = 8;
+  const int x = b % kXcd, idx = b / kXcd, q = nb / kXcd, r = nb % kXcd;
+  return x < r ? x * (q + 1) + idx : r * (q + 1) + (x - r) * q + idx;
+}
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_fg_spmv_stage(int n_rows, const int32_t* __restrict__ rows,
                                                           const int32_t* __restrict__ rp,
@@ -260,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void k_fg_spmv_stage(int n_rows, const int3
   __shared__ double sx[WPB][NN * NV];
   if (s->done) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int l0 = (blockIdx.x * WPB + wv) * NN;  // the wavefront's first row (of the list)
+  const int l0 = (spmv_block(blockIdx.x, gridDim.x) * WPB + wv) * NN;  // the wavefront's first row (of the list)
   if (l0 >= n_rows) return;                      // (uniform over the wavefront)
   // lane j < NN: the wavefront's j-th row, its first block and its block count (none past the end)
   const bool lv = lane < NN && l0 + lane < n_rows;

@@ -1187,6 +1187,9 @@ __global__ __launch_bounds__(256) void k_ilu_build_2(const int32_t* __restrict__
 // Rows with more than kB2 lower blocks (3-D: up to six) take the extra blocks with direct loads. Arithmetic as
 // k_ilu_build_2's gplan branch, operation for operation.
 constexpr int kB2 = 3;
+#ifndef RX_SST_BB2
+#define RX_SST_BB2 2  // build knob: passes of blocks in flight ahead of the pass being factored
+#endif
 struct Plan2 {
   int4 h;        // i, klo, kd, khi
   int j[kB2];    // columns of the first lower blocks
@@ -1265,7 +1268,7 @@ __global__ __launch_bounds__(64) void k_ilu_build_2w(const int32_t* __restrict__
   // pipeline: the plans of passes q .. q + kPB2 - 1 (a register ring shifted every pass) and the blocks of passes
   // q .. q + kBB2 - 1 are in flight while pass q is computed; a pass's blocks are loaded from a plan that arrived
   // passes earlier, so no load waits on another one
-  constexpr int kPB2 = 6, kBB2 = 2;
+  constexpr int kBB2 = RX_SST_BB2, kPB2 = kBB2 + 4 > 6 ? kBB2 + 4 : 6;
   Plan2 Pr[kPB2];
 #pragma unroll
   for (int d = 0; d < kPB2; ++d) Pr[d] = plan2_load(gplan, slot_of(q0 + d));
@@ -1344,7 +1347,10 @@ __global__ __launch_bounds__(64) void k_ilu_build_2w(const int32_t* __restrict__
 // slot, so no load of the pass being computed waits on another load; every load is unconditional (clamped valid
 // addresses) so the wait counts stay static. Rows with more than kB2 blocks on a side take the rest with direct
 // loads. Arithmetic as k_ilu_fwd_wide / k_ilu_bwd_wide, operation for operation.
-constexpr int kS2 = 8, kD2 = 3;
+#ifndef RX_SST_D2
+#define RX_SST_D2 3  // build knob: passes of blocks in flight ahead of the pass being computed
+#endif
+constexpr int kD2 = RX_SST_D2, kS2 = kD2 + 5 > 8 ? kD2 + 5 : 8;
 struct Row2 {
   int c[kB2];        // block columns
   double f[kB2][4];  // blocks
