@@ -159,6 +159,8 @@ def lib():
         _lib.rx_fgmres.argtypes = [C.c_void_p, C.c_double, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         if hasattr(_lib, "rx_linear_solve"):  # an RX_LIB A/B variant built before it may lack it
             _lib.rx_linear_solve.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double)]
+        if hasattr(_lib, "rx_set_system_fold"):  # (an RX_LIB A/B variant built before round 5's cycle v lacks it)
+            _lib.rx_set_system_fold.argtypes = [C.c_void_p, C.c_int]
         _lib.rx_explicit_euler.argtypes = [C.c_void_p, C.c_void_p]
         _lib.rx_implicit_euler.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         _lib.rx_explicit_rk.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p]
@@ -873,6 +875,22 @@ def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=Non
     except the RMS vectors and the linear-solver counts. Returns (rms_flow of the last stage, rms_turb, lin_iters)."""
     if limiter is None:
         limiter = flow.cfg.spatial_order == 2
+    implicit = bool(flow.cfg.implicit)
+    stages = [None] if implicit or not rk_alpha else list(rk_alpha)
+    # nothing reads RES / JAC between the loops and the implicit step here: the assembly may fold the system's V / dt
+    # (rx_set_system_fold; the system is bitwise the same)
+    fold = implicit and hasattr(lib(), "rx_set_system_fold")
+    if fold:
+        _chk(lib().rx_set_system_fold(flow.h, 1), "rx_set_system_fold", flow.h)
+    try:
+        return _iterate_stages(flow, turb, ext_iter, limiter, implicit, stages)
+    finally:
+        if fold:
+            lib().rx_set_system_fold(flow.h, 0)
+
+
+def _iterate_stages(flow, turb, ext_iter, limiter, implicit, stages):
+    """The body of Iterate (below the fold hint)."""
 
     def preprocess(output):
         flow.SetPrimitive_Variables(ext_iter)
@@ -881,8 +899,6 @@ def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=Non
         if limiter and not output:
             flow.SetPrimitive_Limiter()
 
-    implicit = bool(flow.cfg.implicit)
-    stages = [None] if implicit or not rk_alpha else list(rk_alpha)
     it = 0
     for k, alpha in enumerate(stages):
         preprocess(False)

@@ -46,9 +46,29 @@ void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
 
+__global__ void k_fold_mark(int n, const int32_t* __restrict__ rows, int32_t* __restrict__ skip) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) skip[rows[t]] = 1;
+}
+
+// fold_skip for the current boundary markers: the owned boundary points k_bc_apply updates after the assembly
+int fold_prepare(rx_ctx* ctx) {
+  if (ctx->fold_skip && ctx->fold_epoch == ctx->bc_epoch) return RX_OK;
+  if (!ctx->fold_skip) RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->fold_skip), sizeof(int32_t) * (ctx->N + 1)));
+  RX_HIP(hipMemsetAsync(ctx->fold_skip, 0, sizeof(int32_t) * (ctx->N + 1), ctx->stream));
+  if (ctx->bc_on && ctx->bc_nbn > 0)
+    k_fold_mark<<<(int)((ctx->bc_nbn + 255) / 256), 256, 0, ctx->stream>>>((int)ctx->bc_nbn, ctx->bc_bn,
+                                                                          ctx->fold_skip);
+  RX_HIP(hipGetLastError());
+  ctx->fold_epoch = ctx->bc_epoch;
+  return RX_OK;
+}
+
 int ensure_assembled(rx_ctx* ctx) {
   if (!ctx->cfg.implicit || ctx->assembled) return RX_OK;
   if (!ctx->phase_conv) return RX_ERR_STATE;
+  if (ctx->fold_req && ctx->kind == RX_KIND_FLOW)
+    if (int rc0 = fold_prepare(ctx)) return rc0;
   RxPhase ph(ctx, RX_K_ASSEMBLE);
   int rc = rx_launch_assemble(ctx, ctx->phase_visc, ctx->phase_src);
   if (rc) return rc;
@@ -795,7 +815,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
                   ctx->bs.rpart_lvl, ctx->bs.rlvl_ptr, ctx->ring_xoff, ctx->send_idx, ctx->grad_list, ctx->spmv_rows, ctx->sendbuf, ctx->rms_sum,
                   ctx->recon, ctx->uold, ctx->fconv, ctx->fvisc, ctx->jconv, ctx->scratch_in_ilu ? nullptr : ctx->jvisc,
                   ctx->scratch_in_ilu ? nullptr : ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->dlu, ctx->xstar, ctx->jinv,
-                  ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz};
+                  ctx->lim_mn, ctx->lim_mx, ctx->red, ctx->err, ctx->kw, ctx->kz, ctx->fold_skip};
   rx_comm_free(ctx);
   if (ctx->kind == RX_KIND_FLOW) rx_bc_free(ctx);
   rx_la_krylov_free(ctx);
@@ -807,6 +827,13 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+  return RX_OK;
+}
+
+int rx_set_system_fold(rx_ctx* ctx, int on) {
+  if (!ctx) return RX_ERR_ARG;
+  static const bool off = getenv("RX_NO_FOLD") && getenv("RX_NO_FOLD")[0] == '1';  // A/B
+  ctx->fold_req = on && !off && ctx->kind == RX_KIND_FLOW ? 1 : 0;
   return RX_OK;
 }
 

@@ -152,6 +152,13 @@ struct rx_ctx {
   int last_err_phase = 0;    // rx_err_phase of the last RX_ERR_NAN (rx_check_error)
   int conv_deferred = 0;     // implicit AUSM left to the assembly (rx_fuse_conv): k_asm_visc or, without it, k_ausm_edge
   int asm_visc = 0;          // this residual's viscous Jacobians are made by the assembly (k_asm_visc), not k_visc_jac
+  // the implicit system's V / dt folded into the assembly (rx_set_system_fold, round 5): while fold_req is set the
+  // node-centric assembly adds AddVal2Diag's V / dt (or the identity row) to the diagonal of every owned row that no
+  // boundary condition changes afterwards (fold_skip[i] = 0), and the system build then leaves those diagonals alone
+  int fold_req = 0;
+  int sys_folded = 0;                // the last assembly folded (consumed by the next system build)
+  int32_t* fold_skip = nullptr;      // [N] 1: a row the boundary conditions change after the assembly
+  uint64_t fold_epoch = ~0ull;       // the bc_epoch fold_skip was made for
   double* lim_mn = nullptr;  // [N][nL]
   double* lim_mx = nullptr;
   double* red = nullptr;     // reduction scratch

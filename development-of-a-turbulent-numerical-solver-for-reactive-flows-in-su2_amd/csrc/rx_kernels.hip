@@ -969,6 +969,12 @@ struct AusmIn {
   double mInfty;
   int* err;
 };
+// the system build's diagonal folded into k_asm_visc (vol == nullptr: not folded; rx_ctx::fold_req)
+struct SysFold {
+  const double *vol, *dt;
+  const int32_t* skip;
+  int Nd;
+};
 #ifndef RX_ASMV_SHS
 #define RX_ASMV_SHS 1  // build knob: the fused AUSM pass makes each edge's scalars once per team (LDS-shared)
 #endif
@@ -1004,7 +1010,7 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
     const int64_t* __restrict__ edge_blk, const int64_t* __restrict__ diag, const double* __restrict__ Fc,
     const double* __restrict__ Fv, const double* __restrict__ Jc, const double* __restrict__ dTdU,
     const double* __restrict__ Summ, const double* __restrict__ Js, const double* __restrict__ Rsrc, DevMech m,
-    ViscParams P, double* __restrict__ R, double* __restrict__ A, int src, AusmIn cv) {
+    ViscParams P, double* __restrict__ R, double* __restrict__ A, int src, AusmIn cv, SysFold fd) {
   constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>();
   constexpr int TW = asmv_team_width(nVar), TPW = 64 / TW, kTeams = asmv_nodes_per_block(nVar);
   static_assert(TW >= nVar && TW <= 64, "a team holds one lane per column");
@@ -1226,6 +1232,20 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
                                        (size_t)((a - rhos) * nVar + b) * kSrcTile + i % kSrcTile]
                                   : 0.0;
       D[a] += js;
+    }
+  }
+  if (fd.vol && i < fd.Nd && !fd.skip[i]) {
+    // ImplicitEuler_Iteration's AddVal2Diag (k_build_system_elem's operations on this lane's column: the same
+    // quotient added to the diagonal entry, or the identity row with the residual zeroed)
+    if (fd.dt[i] > rx::kEPS) {
+      const double delta = fd.vol[i] / fd.dt[i];
+#pragma unroll
+      for (int a = 0; a < nVar; ++a)
+        if (a == b) D[a] += delta;
+    } else {
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) D[a] = (a == b) ? 1.0 : 0.0;
+      r = 0.0;
     }
   }
   R[(size_t)i * nVar + b] = r;
@@ -1754,13 +1774,20 @@ int RX_NSFN(rx_launch_asm_visc)(rx_ctx* ctx, int with_src, int fused_conv) {
     cv.SR = ctx->cfg.spatial_order ? ctx->recon + 2 * ctx->E * (int64_t)ctx->nPV : nullptr;
     cv.normal = ctx->normal;
   }
+  SysFold fd{nullptr, nullptr, nullptr, (int)ctx->Nd};
+  if (ctx->fold_req && ctx->fold_skip && with_src) {  // (the whole residual: the build follows)
+    fd.vol = ctx->vol;
+    fd.dt = ctx->f[RX_F_DT];
+    fd.skip = ctx->fold_skip;
+  }
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<(ctx->N + asmv_nodes_per_block(NS_ + ND_ + 2) - 1) /
                                                                      asmv_nodes_per_block(NS_ + ND_ + 2),
                                                                  kBlock, 0, ctx->stream>>>(
                             (int)ctx->N, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
                             ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech,
-                            P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv)));
+                            P, ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv, fd)));
   RX_HIP(hipGetLastError());
+  ctx->sys_folded = fd.vol ? 1 : 0;
   return RX_OK;
 }
 #endif  // RX_NS
@@ -1778,6 +1805,7 @@ RX_NS_DISPATCH(rx_launch_grad, (rx_ctx * ctx, const int32_t* list, int64_t n), (
 
 int rx_launch_assemble(rx_ctx* ctx, int with_visc, int with_src) {
   const int nv = ctx->nVar;
+  ctx->sys_folded = 0;  // (set again by a folding k_asm_visc launch)
   const bool fused_conv = ctx->conv_deferred && with_visc && ctx->asm_visc;
   if (ctx->conv_deferred && !fused_conv) {  // deferred, but no viscous pass to fuse it into: the edge kernel now
     const int rc = rx_launch_ausm_edge(ctx);

@@ -83,7 +83,8 @@ __global__ __launch_bounds__(kBlock) void k_build_system_elem(int Nd, int N, con
                                                               const double* __restrict__ vol,
                                                               const double* __restrict__ dt, double* __restrict__ A,
                                                               double* __restrict__ R, double* __restrict__ rhs,
-                                                              double* __restrict__ x) {
+                                                              double* __restrict__ x,
+                                                              const int32_t* __restrict__ skip) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (int64_t)N * NV) return;
   const int i = (int)(q / NV), a = (int)(q - (int64_t)i * NV);
@@ -92,14 +93,19 @@ __global__ __launch_bounds__(kBlock) void k_build_system_elem(int Nd, int N, con
     rhs[q] = 0.0;
     return;
   }
+  // skip != nullptr: the assembly folded the diagonal of the rows with skip[i] == 0 (k_asm_visc, SysFold); their
+  // diagonal and zeroed residual are already this kernel's, only rhs and x are left
+  const bool folded = skip && !skip[i];
   double* D = A + diag[i] * NV * NV + a * NV;
   if (dt[i] > rx::kEPS) {
-    D[a] += vol[i] / dt[i];
+    if (!folded) D[a] += vol[i] / dt[i];
     rhs[q] = -(R[q] + 0.0);
   } else {
+    if (!folded) {
 #pragma unroll
-    for (int c = 0; c < NV; ++c) D[c] = (a == c) ? 1.0 : 0.0;
-    R[q] = 0.0;
+      for (int c = 0; c < NV; ++c) D[c] = (a == c) ? 1.0 : 0.0;
+      R[q] = 0.0;
+    }
     rhs[q] = -(0.0 + 0.0);
   }
 }
@@ -208,14 +214,16 @@ int rx_la_spmv(rx_ctx* ctx, const double* A, const double* x, double* y, const i
 
 int rx_la_build_system(rx_ctx* ctx) {
   static const bool per_node = getenv("RX_BUILD_PER_NODE") != nullptr;  // A/B: the thread-per-node build
-  if (per_node) {
+  const int32_t* skip = ctx->sys_folded ? ctx->fold_skip : nullptr;
+  ctx->sys_folded = 0;
+  if (per_node && !skip) {
     RX_NV_SWITCH(ctx->nVar, (k_build_system<NV_><<<blocks(ctx->N), kBlock, 0, ctx->stream>>>(
                                 (int)ctx->Nd, (int)ctx->N, ctx->diag, ctx->vol, ctx->f[RX_F_DT], ctx->f[RX_F_JAC],
                                 ctx->f[RX_F_RES], ctx->f[RX_F_RHS], ctx->f[RX_F_SOL])));
   } else {
     RX_NV_SWITCH(ctx->nVar, (k_build_system_elem<NV_><<<blocks(ctx->N * NV_), kBlock, 0, ctx->stream>>>(
                                 (int)ctx->Nd, (int)ctx->N, ctx->diag, ctx->vol, ctx->f[RX_F_DT], ctx->f[RX_F_JAC],
-                                ctx->f[RX_F_RES], ctx->f[RX_F_RHS], ctx->f[RX_F_SOL])));
+                                ctx->f[RX_F_RES], ctx->f[RX_F_RHS], ctx->f[RX_F_SOL], skip)));
   }
   RX_HIP(hipGetLastError());
   return RX_OK;

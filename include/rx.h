@@ -185,6 +185,14 @@ int rx_ctx_create(const rx_mesh_desc *mesh, const rx_mech_desc *mech, const rx_c
 int rx_ctx_destroy(rx_ctx *ctx); /* RX_ERR_STATE for a flow context whose SST context (rx_sst_create) is alive:
                                     destroy the SST context first (it runs on the flow's stream / communicator) */
 int rx_field_size(const rx_ctx *ctx, rx_field f, int64_t *count);
+/* Optimisation hint for a caller that runs the whole ImplicitEuler sequence of an iteration (the loops, BC_*, then
+   rx_implicit_euler) with no rx_download / rx_upload of RES or JAC in between (rx.Iterate does): on = 1 lets the
+   node-centric assembly add ImplicitEuler_Iteration's AddVal2Diag V/dt (solver_direct_reactive.cpp:2336-2387) to the
+   rows no boundary condition changes afterwards, so the system build no longer revisits their diagonal blocks.
+   The system is bitwise the same; only the intermediate JAC / RES between the assembly and the implicit step differ
+   from the reference's, which is why it is off by default. Flow contexts only (ignored for SST); RX_NO_FOLD=1
+   disables it. */
+int rx_set_system_fold(rx_ctx *ctx, int on);
 int rx_upload(rx_ctx *ctx, rx_field f, const double *host, int64_t count);
 int rx_download(rx_ctx *ctx, rx_field f, double *host, int64_t count);
 int rx_bsr_pattern(const rx_ctx *ctx, int64_t *row_ptr, int64_t *col); /* host copies, [N+1], [nnzb] */

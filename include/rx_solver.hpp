@@ -209,6 +209,13 @@ inline std::vector<double> Iterate(ReactiveNSSolver& flow, TurbSSTSolver& turb, 
     if (cfg.spatial_order == 2 && !output) flow.SetPrimitive_Limiter();
   };
   const size_t stages = (!cfg.implicit && !rk_alpha.empty()) ? rk_alpha.size() : 1;
+  // nothing reads RES / JAC between the loops and the implicit step here: the assembly may fold the system's V / dt
+  // (rx_set_system_fold; the system is bitwise the same), cleared again on every exit
+  struct Fold {
+    rx_ctx* c;
+    ~Fold() { if (c) rx_set_system_fold(c, 0); }
+  } fold{cfg.implicit ? flow.context() : nullptr};
+  if (fold.c && rx_set_system_fold(fold.c, 1) != RX_OK) throw std::runtime_error("rx_set_system_fold");
   std::vector<double> rms;
   for (size_t k = 0; k < stages; ++k) {
     preprocess(false);
