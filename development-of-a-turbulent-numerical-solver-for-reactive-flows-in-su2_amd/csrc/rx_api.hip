@@ -847,7 +847,10 @@ int rx_upload(rx_ctx* ctx, rx_field f, const double* host, int64_t count) {
   if (!ctx || f < 0 || f >= RX_F_COUNT || count != ctx->fcount[f] || !host) return RX_ERR_ARG;
   if (int rc = rx_settle_u(ctx)) return rc;
   RX_HIP(hipMemcpyAsync(ctx->f[f], host, count * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  if (f == RX_F_ILU) ctx->ilu_valid = 1;  // a caller-provided factor
+  if (f == RX_F_ILU) {  // a caller-provided factor (its diagonal blocks included)
+    ctx->ilu_valid = 1;
+    ctx->ilu_diag_deferred = 0;
+  }
   // a loaded solution is also the Solution_Old (CVariable construction / LoadRestart)
   if (f == RX_F_U && ctx->kind == RX_KIND_FLOW && ctx->uold)
     RX_HIP(hipMemcpyAsync(ctx->uold, ctx->f[f], count * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));

@@ -102,6 +102,7 @@ struct rx_ctx {
   int ilu_waves = 1;            // wavefronts per workgroup of the ILU factorisation
   bool ilu_grp_ok = false;      // every row's plan is compact and updates only its diagonal (k_ilu_build_grp)
   int32_t* ilu_gplan = nullptr; // [N][32] k_ilu_build_grp's row plans (up to 6 lower blocks, one update each)
+  int ilu_diag_deferred = 0;    // the ILU field's diagonal blocks are not stored (k_ilu_build_grp, RX_GRP_DIAG_STORE 0)
   // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
   // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])
   struct Sched {

@@ -610,6 +610,12 @@ __device__ __forceinline__ void grp_solve_lds(const double* LU, double (&rhs)[NV
 #ifndef RX_GRP_WAVES
 #define RX_GRP_WAVES 12
 #endif
+// build knob: 1 = the grouped build stores each row's eliminated diagonal block D_i in the factor (ILU_matrix's
+// diagonal); 0 (default, round 5) = it does not — no sweep reads it (they read inv(D_i)) — and a download of the ILU
+// field remakes it from the matrix and the stored W blocks with the build's arithmetic (k_ilu_diag_materialize)
+#ifndef RX_GRP_DIAG_STORE
+#define RX_GRP_DIAG_STORE 0
+#endif
 #ifndef RX_GRP_WAVES_BIG
 #define RX_GRP_WAVES_BIG 8
 #endif
@@ -824,7 +830,7 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
           for (int e = 0; e < NV; ++e) d[e] -= x[e];
         }
       }
-      if (act) {
+      if (act && RX_GRP_DIAG_STORE) {  // (the sweeps read inv(D_i) only: rx_la_ilu_materialize remakes D_i)
 #pragma unroll
         for (int e = 0; e < NV; ++e) F[(size_t)kd * NV2 + e * NV + al] = d[e];
       }
@@ -2342,6 +2348,7 @@ void launch_ilu_build_grp(rx_ctx* ctx, int gwaves) {
     k_ilu_build_grp<NV><<<ctx->npart, 64 * gwaves, shm, ctx->stream>>>(
         ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_gplan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
         ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)NV * NV, ctx->ilu_trace);
+    ctx->ilu_diag_deferred = RX_GRP_DIAG_STORE ? 0 : 1;
   }
 }
 
@@ -2383,8 +2390,48 @@ __global__ __launch_bounds__(256) void k_ilu_materialize(int N, const int32_t* _
 }
 }  // namespace
 
+// D_i = A_ii - sum_k A_ji W_k over the row's lower blocks in order, each product summed from 0.0 with q ascending and
+// subtracted entry by entry: k_ilu_build_grp's arithmetic on the same operands (the matrix, unchanged since the build,
+// and the W blocks it stored), so the block is bitwise the one the build eliminated. One wavefront per plan slot,
+// lane c = column c.
+template <int NV>
+__global__ __launch_bounds__(256) void k_ilu_diag_materialize(int n, const int32_t* __restrict__ plan,
+                                                              const double* __restrict__ A, double* __restrict__ F) {
+  constexpr int NV2 = NV * NV;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), c = threadIdx.x & 63;
+  if (r >= n || c >= NV) return;
+  const int32_t* rec = plan + (size_t)r * kPlan;
+  const int k0 = rec[1], kd = rec[2];
+  double d[NV];
+#pragma unroll
+  for (int e = 0; e < NV; ++e) d[e] = A[(size_t)kd * NV2 + e * NV + c];
+  for (int k = k0; k < kd; ++k) {
+    const int kk = rec[14 + (k - k0)];
+    if (kk < 0) continue;
+    double x[NV];
+#pragma unroll
+    for (int e = 0; e < NV; ++e) x[e] = 0.0;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const double w = F[(size_t)k * NV2 + q * NV + c];
+#pragma unroll
+      for (int e = 0; e < NV; ++e) x[e] += A[(size_t)kk * NV2 + e * NV + q] * w;
+    }
+#pragma unroll
+    for (int e = 0; e < NV; ++e) d[e] -= x[e];
+  }
+#pragma unroll
+  for (int e = 0; e < NV; ++e) F[(size_t)kd * NV2 + e * NV + c] = d[e];
+}
+
 int rx_la_ilu_materialize(rx_ctx* ctx) {
   if ((!ilu_grouped(ctx) && !ilu2_wave(ctx)) || !ctx->f[RX_F_ILU]) return RX_OK;
+  if (ctx->ilu_diag_deferred && ctx->nVar >= 5) {
+    RX_NV_SWITCH(ctx->nVar, (k_ilu_diag_materialize<NV_><<<(int)((ctx->Nd + 3) / 4), 256, 0, ctx->stream>>>(
+                                (int)ctx->Nd, ctx->ilu_gplan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU])));
+    RX_HIP(hipGetLastError());
+    ctx->ilu_diag_deferred = 0;
+  }
   RX_NV_SWITCH(ctx->nVar, (k_ilu_materialize<NV_><<<(int)((ctx->Nd + 3) / 4), 256, 0, ctx->stream>>>(
                               (int)ctx->Nd, ctx->rp, ctx->klo, ctx->diag, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU])));
   RX_HIP(hipGetLastError());
@@ -2477,6 +2524,7 @@ int rx_la_ilu_build(rx_ctx* ctx) {
 
 static int ilu_build_impl(rx_ctx* ctx) {
   const int nv = ctx->nVar;
+  ctx->ilu_diag_deferred = 0;  // (set again by a grouped build that does not store the diagonal blocks)
   if (ilu2_wave(ctx) && !ctx->ilu_trace) {
     k_ilu_build_2w<<<ctx->npart, 64, (size_t)ctx->maxpart * 4 * sizeof(double), ctx->stream>>>(
         ctx->part_ptr, ctx->fs.part_pass, ctx->fs.pass_lo, ctx->ilu_gplan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
