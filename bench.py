@@ -33,12 +33,15 @@ block of `parts` partitions plus one halo layer (meshgen.shard) and exchanges ha
 calls SendReceive / Set_MPI_*, with every FGMRES inner product and the RMS all-reduced (rx_comm_init; all-gather +
 rank-ordered sum). The first warm-up step runs
 eagerly and must give bitwise the RMS of the next (graph-replayed) one, else the graph is disabled.
-If the communicator cannot be set up, every rank falls back to an independent replica of the
-single-GPU workload and `config.parallelism` says so. Timing = max over ranks; value = all ranks'
-owned cells.
+If the communicator cannot be set up on any rank, the run prints a line with `value: null` and the
+reason, and exits with status 3 (no replica fallback: a scaling point is the decomposed mesh or nothing).
+Timing = max over ranks; value = all ranks' owned cells.
 
-Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel and `cpu_baseline` from the
-CPU restatement (oracle/) timed on one host core over one step of the same mesh.
+Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel and `cpu_baseline`: the reference itself
+(oracle/_ref, compiled from /root/reference) on configs[1]'s 100k-point sample, one serial process per core of the
+host's CPU share at once (`cpu_baseline_reference_1core`: one process alone), beside the CPU restatement (oracle/,
+OpenMP on the same share) over one step of the bench mesh (`cpu_baseline_port`); each names its core count and the
+host's `nproc`.
 """
 from __future__ import annotations
 
@@ -120,6 +123,10 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
     # ~9 kflop per edge (the C3 count is 13.9 kflop per edge, profiles/r02_c3_v2_fp64.json)
     visc_flop = pmc_fp64_flop("k_visc_edge" + te, workload_key) or 9000.0 * E
     fused = conv_fused(nDim)
+    # the node-centric assembly kernel: k_asm_es (round 6: edge-side teams) unless RX_ASMV_ES=0 or a node has more
+    # edges than its workgroup has teams (rx_asmes_teams: 4 * floor(64 / nVar)); else the node-serial k_asm_visc
+    asm_kernel = ("k_asm_es" if os.environ.get("RX_ASMV_ES", "1") != "0" and max_degree <= 4 * (64 // nVar)
+                  else "k_asm_visc") + te
     models = {
         # k_ausm_edge: V (nPV) and dPdU (nVar) per node once; edge (2 int32 + normal); flux + 2 Jacobians
         "CONV": hbm(N * (nPV + nVar) * d + E * (8 + nDim * d) + E * (nVar * d + 2 * blk), "k_ausm_edge" + te),
@@ -137,13 +144,13 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
                      # launched): each edge's two convective blocks, summary record, fluxes and ends' dT/dU in once,
                      # the source rows; the two off-diagonal blocks, the diagonal blocks and the residual out
                      hbm(2 * E * blk + 2 * E * nVar * d + E * summ + N * nVar * d + 24 * E
-                         + N * (ns * nVar + nVar) * d + 2 * E * blk + N * (blk + nVar * d), "k_asm_visc" + te)
+                         + N * (ns * nVar + nVar) * d + 2 * E * blk + N * (blk + nVar * d), asm_kernel)
                      if not fused else
                      # k_asm_visc with the fused AUSM pass (round 4, k_ausm_edge not launched): V and dP/dU per
                      # node and each edge's normal once, the viscous fluxes, summary records, dT/dU and index
                      # arrays, the source rows; the two off-diagonal blocks, the diagonal blocks and the residual out
                      hbm(N * (nPV + nVar) * d + E * nDim * d + E * nVar * d + E * summ + N * nVar * d + 24 * E
-                         + N * (ns * nVar + nVar) * d + 2 * E * blk + N * (blk + nVar * d), "k_asm_visc" + te)),
+                         + N * (ns * nVar + nVar) * d + 2 * E * blk + N * (blk + nVar * d), asm_kernel)),
         "GRAD": hbm(N * ((nDim + nPV) * d + nG * nDim * d) + (N + 1) * 4 + 2 * E * 4, "k_grad_lsq" + te),
         # k_source: V, dT/dU, volume, omega in; residual + the Jacobian's species rows out
         "SOURCE": hbm(N * (nPV + nVar + 2) * d + N * (nVar + ns * nVar) * d, "k_source" + te),
@@ -233,23 +240,40 @@ def cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, bc=None):
         what = "1 outer iteration (flow implicit step + SST step, no boundary conditions)"
     dt = time.perf_counter() - t0
     cores = int(O.lib().orc_num_threads())
+    share, nproc = host_cores()
     return dict(value=N / dt / 1e6, unit="Mcells*iters/s", cores=cores, kind="port",
-                sample=f"{what} of the same {N}-cell mesh, {cores} host threads ({dt:.2f} s)")
+                sample=f"{what} of the same {N}-cell mesh, {cores} host threads ({dt:.2f} s)",
+                host_cpu_share=share, host_nproc=nproc)
 
 
-def cpu_baseline_reference(ns, cfl, nx=500, ny=200):
-    """One outer iteration of the reference itself (SU2's CMeanFlowIteration::Iterate through oracle/ref_harness,
-    compiled from /root/reference's sources by oracle/ref_build.mk into oracle/_ref, serial: one MPI rank, one core)
-    on a bounded sample of the bench workload: the same synthetic jet geometry and interpolated PaSR state
-    (synth.field_at) at nx x ny points — by default configs[1]'s 500 x 200 = 100 000-point mesh (~30 s of CPU; the
-    reference's per-cell cost grows with the mesh: 0.0105 Mcells*iters/s at 300 x 75 (round 4), 0.0033 at 500 x 200, 0.0032 at
-    the C3 mesh itself, profiles/r05_calibration_c{2,3}.json) —, the bench's mechanism (`ns` species), EULER_IMPLICIT
-    with ILU0 FGMRES(5) at the bench's CFL and the jet's boundary conditions. The time is the harness's own clock
-    around Iterate (it1_wall). None when the harness is not built."""
+def host_cores():
+    """(CPU share, nproc): the cores this process may run on (the GPU box grants a 16-CPU share of a larger host and
+    sets OMP_NUM_THREADS to it) and the host's whole count (os.cpu_count(), what `nproc` reports there)."""
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        share = min(share, int(omp))
+    return share, os.cpu_count() or share
+
+
+def cpu_baseline_reference(ns, cfl, nx=500, ny=200, copies=1):
+    """The reference itself (SU2's CMeanFlowIteration::Iterate through oracle/ref_harness, compiled from
+    /root/reference's sources by oracle/ref_build.mk into oracle/_ref; serial: one MPI rank, one core per process) on
+    a bounded sample of the bench workload: the same synthetic jet geometry and interpolated PaSR state
+    (synth.field_at) at nx x ny points — by default configs[1]'s 500 x 200 = 100 000-point mesh —, the bench's
+    mechanism (`ns` species), EULER_IMPLICIT with ILU0 FGMRES(5) at the bench's CFL and the jet's boundary conditions.
+    The time is the harness's own clock around Iterate (it1_wall). On the GPU box one such iteration takes 9-10 s
+    (0.010-0.011 Mcells*iters/s; 0.0105 on the 300 x 75 sample of round 4: the per-cell cost does not depend on the
+    sample there — the container's slower core gives 0.0033, which is what an earlier note compared with).
+    copies > 1: that many independent reference processes at once on as many cores, each on its own copy of the
+    sample, the aggregate throughput copies * points / slowest wall — the all-core reference estimate (the MPI build of
+    the reference cannot be made here: its run on those cores would split one mesh and add communication, so this
+    bounds it from above). None when the harness is not built."""
     harness = os.path.join(ROOT, "oracle", "_ref", "harness")
     if not os.path.exists(harness):
         return None
     import shutil
+    import subprocess
     import tempfile
     from tests.casefiles import unpack
     from tests.rxpkg import meshgen, synth
@@ -268,17 +292,38 @@ def cpu_baseline_reference(ns, cfl, nx=500, ny=200):
             meshgen.write_su2(os.path.join(wd, "mesh.su2"), pts, quads, bnd)
             return "mesh.su2"
 
-        wd = MG.make_workdir("refbase", writer, cfl=cfl, order="1ST_ORDER", prec="ILU0", ns=ns, root=root)
-        MG.write_state(wd, state)
-        a = MG.run_harness(wd, bsr=False, extra=["--iters", "1"])
-        wall = float(np.ravel(a["it1_wall"])[0])
+        wds = []
+        for q in range(copies):
+            wd = MG.make_workdir(f"refbase{q}", writer, cfl=cfl, order="1ST_ORDER", prec="ILU0", ns=ns, root=root)
+            MG.write_state(wd, state)
+            wds.append(wd)
+        if copies == 1:
+            walls = [float(np.ravel(MG.run_harness(wds[0], bsr=False, extra=["--iters", "1"])["it1_wall"])[0])]
+        else:
+            env = dict(os.environ, OMP_NUM_THREADS="1")
+            procs = [subprocess.Popen([harness, "case.cfg", "state.txt", "out", "--iters", "1"], cwd=wd, env=env,
+                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL) for wd in wds]
+            if any(p.wait() != 0 for p in procs):
+                raise RuntimeError("a concurrent reference harness failed")
+            walls = []
+            for wd in wds:
+                man = dict(line.split()[:2] for line in open(os.path.join(wd, "out", "manifest.txt")))
+                walls.append(float(np.fromfile(os.path.join(wd, "out", "it1_wall.bin"),
+                                               dtype="<" + man["it1_wall"])[0]))
     finally:
         shutil.rmtree(root, ignore_errors=True)
     n = len(pts)
-    return dict(value=round(n / wall / 1e6, 6), unit="Mcells*iters/s", cores=1, kind="reference",
-                sample=f"1 outer iteration of the reference itself (oracle/_ref harness, serial, one core) on the "
-                       f"{nx}x{ny} synthetic jet ({n} points, {ns} species, EULER_IMPLICIT ILU0 FGMRES(5), jet BCs): "
-                       f"{wall:.2f} s")
+    wall = max(walls)
+    share, nproc = host_cores()
+    what = (f"1 outer iteration of the reference itself (oracle/_ref harness, serial) on the {nx}x{ny} synthetic jet "
+            f"({n} points, {ns} species, EULER_IMPLICIT ILU0 FGMRES(5), jet BCs)")
+    if copies == 1:
+        return dict(value=round(n / wall / 1e6, 6), unit="Mcells*iters/s", cores=1, kind="reference",
+                    sample=f"{what}, one core: {wall:.2f} s", host_cpu_share=share, host_nproc=nproc)
+    return dict(value=round(copies * n / wall / 1e6, 6), unit="Mcells*iters/s", cores=copies, kind="reference",
+                sample=f"{copies} concurrent copies of {what}, one core each: slowest {wall:.2f} s, fastest "
+                       f"{min(walls):.2f} s (aggregate = copies x points / slowest; an upper bound of the reference's "
+                       f"MPI run on these cores)", host_cpu_share=share, host_nproc=nproc)
 
 
 def setup_sharded(rx, args, nx, ny, ns, world, rank, local, dist, nz=0):
@@ -364,10 +409,19 @@ def main():
         dist.all_gather_object(flags, err)
         bad = [f for f in flags if f]
         if bad:
+            # no scaling point without the domain decomposition: independent replicas would
+            # sum N single-GPU runs into a value a scaling curve must not record, so the line carries no value
             if s is not None:
                 s.close()
-            s = None
-            parallelism = f"replicas x{world} (sharded setup failed: {bad[0]})"
+            if rank == 0:
+                print(json.dumps({"metric": "Mcells*iters/s (reactive RANS)", "value": None, "unit": "Mcells*iters/s",
+                                  "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+                                  "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+                                  "dtype": "f64", "data": "synthetic",
+                                  "config": {"workload": args.workload, "parallelism": "none"},
+                                  "error": f"sharded setup failed on a rank: {bad[0]}"}), flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
         else:
             parallelism = f"sharded x{world} (RCCL halo exchange + all-reduce)"
     if s is None:
@@ -517,7 +571,7 @@ def main():
     if world > 1:
         tot = [None] * world
         dist.all_gather_object(tot, n_owned)
-        cells = int(sum(tot)) if parallelism.startswith("sharded") else N * world
+        cells = int(sum(tot))
     else:
         cells = N
     out = {
@@ -558,13 +612,17 @@ def main():
         # the reference itself on a bounded sample when its harness is built (kind "reference"), beside the
         # restatement on the whole mesh on all host cores (kind "port")
         port = cpu_baseline(mesh, st, mech_arrays, kw, ns, cfg, None if args.no_bc else synth_bc)
-        ref = None
+        ref = ref1 = None
         if nz <= 1 and not args.no_bc:
             try:
-                ref = cpu_baseline_reference(ns, cfg.cfl)
+                ref1 = cpu_baseline_reference(ns, cfg.cfl)
+                share, _ = host_cores()
+                # the reference on every core of the box's CPU share at once, the line's baseline
+                ref = cpu_baseline_reference(ns, cfg.cfl, copies=share) if share > 1 else ref1
             except (SystemExit, Exception) as e:  # noqa: BLE001 - the port line stands
                 port["reference_error"] = repr(e)[:200]
-        out["cpu_baseline"] = ref if ref is not None else port
+        out["cpu_baseline"] = ref if ref is not None else (ref1 if ref1 is not None else port)
+        out["cpu_baseline_reference_1core"] = ref1
         out["cpu_baseline_port"] = port
     else:
         out["cpu_baseline"] = None

@@ -607,6 +607,21 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   CK(dupload(ctx, &ctx->adj_blk, adj_blk.data(), 2 * E));
   CK(dupload(ctx, &ctx->edge_blk, edge_blk.data(), 2 * E));
   for (int64_t i = 0; i < N; ++i) ctx->max_degree = std::max(ctx->max_degree, (int)(adj_ptr[i + 1] - adj_ptr[i]));
+  if (ctx->kind == RX_KIND_FLOW) {  // k_asm_es's node runs: consecutive nodes while their edge sides fit the teams
+    const int T = rx_asmes_teams(ctx->nVar);
+    std::vector<int32_t> wg{0};
+    bool ok = true;
+    for (int64_t n = 0; n < N && ok;) {
+      const int64_t lo = n;
+      while (n < N && n - lo < T && adj_ptr[n + 1] - adj_ptr[lo] <= T) ++n;
+      ok = n > lo;  // a node with more edges than teams
+      wg.push_back((int32_t)n);
+    }
+    if (ok && N > 0) {
+      CK(dupload(ctx, &ctx->asmes_wg, wg.data(), wg.size()));
+      ctx->asmes_nwg = (int)wg.size() - 1;
+    }
+  }
   CK(dupload(ctx, &ctx->nbr_ptr, nptr.data(), N + 1));
   CK(dupload(ctx, &ctx->nbr, nbr.data(), nbr.size()));
   CK(dupload(ctx, &ctx->bv_ptr, bvp.data(), N + 1));
@@ -807,7 +822,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   ctx->solve_exec = nullptr;
   ctx->solve_graph = nullptr;
   if (ctx->kind == RX_KIND_SST && ctx->flow) --ctx->flow->n_children;
-  void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->nbr_ptr,
+  void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->asmes_wg, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.pass_lo, ctx->fs.part_pass, ctx->bs.pass_lo, ctx->bs.part_pass,

@@ -76,6 +76,10 @@ struct rx_ctx {
   int64_t* adj_blk = nullptr;   // [2E] BSR block index of (node, other)
   int64_t* edge_blk = nullptr;  // [E][2] BSR block index of (n0, n1) and (n1, n0)
   int max_degree = 0;           // incident edges of the busiest node
+  // k_asm_es (round 6): workgroup g assembles nodes [asmes_wg[g], asmes_wg[g+1]), whose adjacency entries fit its
+  // rx_asmes_teams(nVar) edge-side teams; null when a node has more edges than that (k_asm_visc then)
+  int32_t* asmes_wg = nullptr;
+  int asmes_nwg = 0;
   int32_t* nbr_ptr = nullptr;   // [N+1] LSQ neighbours in the reference order
   int32_t* nbr = nullptr;
   int32_t* bv_ptr = nullptr;    // [N+1] boundary vertices per node in (marker, vertex) order
@@ -266,6 +270,7 @@ int rx_launch_muscl(rx_ctx* ctx);
 int rx_launch_set_primitive(rx_ctx* ctx, int ext_iter, int64_t lo, int64_t hi);  // points [lo, hi)
 int rx_launch_ausm_edge(rx_ctx* ctx);
 bool rx_fuse_conv(int nDim);
+int rx_asmes_teams(int nVar);  // edge-side teams per k_asm_es workgroup
 // levels of the ILU(0) sweeps' LDS ring (k_ilu_apply_ring): a row's result is read from the ring slot of its level
 // by the rows up to kIluRing - 1 levels later, from a per-partition "far" slot by later ones
 constexpr int kIluRing = 4;

@@ -9,9 +9,17 @@
 //
 // Exactness condition: v_div_scale scales an operand only at the ends of the exponent range — a denormal divisor or
 // quotient, |d| > 2^1022, |n| < 2^-969, or |n / d| >= 2^768 — and there the compiler's sequence rescales while this one
-// does not. The viscous kernels' operands (mass and molar fractions, densities, diffusion coefficients, lengths, areas,
-// mechanism constants) stay far inside that range; tests/test_gpu_fdiv.py checks the two sequences bitwise on random
-// operands across it and on the special values. RX_FDIV=0 at build time turns every rx_div back into `/`.
+// does not (the residual fma(-d, q, n) can go denormal: a 1-ulp difference is possible). The kernels' operands (mass
+// and molar fractions, densities, diffusion coefficients, lengths, areas, mechanism constants) stay inside that range
+// unless a species is depleted below 2^-969 ~ 1e-292. rx_div<true> (build knob RX_FDIV_GUARD=1 for every
+// call site) closes that corner: rx_recip marks a divisor outside [2^-200, 2^52) once (Recip::wide), and rx_div sends
+// such divisors and numerators whose exponent field lies outside [2^-969, 2^560) to the compiler's own `n / d`; inside
+// both windows the quotient lies in [2^-1021, 2^760] and nothing is scaled, so rx_div<true> is `n / d` for every
+// operand pair. It is not the default: the guard splits every division's basic block and the schedulers lose the
+// interleaving of independent divisions — same box, C3 (gpurun_out r06b): VISC 1.83 -> 3.35 ms, ASSEMBLE 5.10 ->
+// 6.44, PRIMITIVE 1.11 -> 1.73, 25.6 -> 29.1 ms per step. tests/test_gpu_fdiv.py checks rx_div against `/` bitwise
+// inside the range and on the special values, and rx_div<true> against `/` over the whole exponent range (denormal and
+// tiny numerators, huge and denormal divisors). RX_FDIV=0 at build time turns every rx_div back into `/`.
 // Divisors that are compile-time constants keep `/` (the compiler may fold its own reciprocal of a constant).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -19,11 +27,15 @@
 #ifndef RX_FDIV
 #define RX_FDIV 1
 #endif
+#ifndef RX_FDIV_GUARD
+#define RX_FDIV_GUARD 0  // build knob: 1 = every rx_div guarded (rx_div<true>, above)
+#endif
 
 namespace rx {
 
 struct Recip {
   double d, y;  // the divisor and its refined reciprocal (the compiler's y)
+  bool wide;    // |d| outside [2^-200, 2^52) (or zero, infinite, NaN): every quotient takes `n / d`
 };
 
 // (host passes — the __host__ __device__ helpers of rx_device.h — keep `/`; the divisor's y is then unused)
@@ -40,14 +52,19 @@ __device__ __host__ __forceinline__ Recip rx_recip(double d) {
   y = __builtin_fma(y, e, y);
   e = __builtin_fma(-d, y, 1.0);
   y = __builtin_fma(y, e, y);
-  return Recip{d, y};
+  const double ad = __builtin_fabs(d);
+  return Recip{d, y, !(ad >= 0x1p-200 && ad < 0x1p52)};
 #else
-  return Recip{d, 0.0};
+  return Recip{d, 0.0, true};
 #endif
 }
 
+template <bool Guard = (RX_FDIV_GUARD != 0)>
 __device__ __host__ __forceinline__ double rx_div(double n, const Recip& r) {
 #if RX_FDIV_DEV
+  // the numerator's biased exponent outside [54, 1583) (|n| < 2^-969, denormal, zero, or |n| >= 2^560)
+  const unsigned en = (unsigned)__double2hiint(n) & 0x7ff00000u;
+  if (Guard && __builtin_expect(r.wide || en - (54u << 20) >= ((1583u - 54u) << 20), 0)) return n / r.d;
   const double q = n * r.y;
   const double e = __builtin_fma(-r.d, q, n);
   return __builtin_amdgcn_div_fixup(__builtin_fma(e, r.y, q), r.d, n);

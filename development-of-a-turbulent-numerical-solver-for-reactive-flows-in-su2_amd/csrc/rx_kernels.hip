@@ -1254,6 +1254,274 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
   for (int a = 0; a < nVar; ++a) Ad[a * nVar] = D[a];
 }
 
+// The same assembly with a node's edges evaluated side by side (round 6). k_asm_visc's team walks its
+// node's edges one after another: per edge a gather of the summary record, a wave barrier, the own-side AUSM column
+// (evaluated twice: once for the diagonal, once more for the off-diagonal block), the viscous column, a second barrier
+// — four dependent rounds per wavefront. Here a team of nVar lanes (lane b = column b) owns one edge side, i.e. one
+// adjacency entry (node i, edge e): a 256-thread workgroup takes a run of consecutive nodes whose adjacency entries fit
+// its 4 * floor(64 / nVar) teams (rx_ctx::asmes_wg, planned on the host), and
+//  - phase A: every team stages its edge's summary record, evaluates the AUSM flux and the own-side Jacobian column
+//    once, the viscous flux and column, writes the neighbour row's off-diagonal block (0 -+ Jc) +- Jv straight from
+//    its lanes, and parks its signed contributions (flux, Jc column, viscous flux, Jv column) in its LDS slot;
+//  - phase B (after one workgroup barrier): the team of the run's j-th node adds its edges' parked contributions in
+//    k_asm_visc's order (the convective ones in edge order, then the viscous ones in edge order; r -+ f is r + (-+f)
+//    exactly), then the source and the folded V / dt, and stores the residual and the diagonal block.
+// Every value and every sum is k_asm_visc's, so the system is bitwise the same (tests/test_gpu_assembly.py).
+// Reference: Upwind_Residual / Viscous_Residual's AddBlock / SubtractBlock (solver_direct_reactive.cpp:2759-2772,
+// :5365-5381), CUpwReactiveAUSM::ComputeResidual (numerics_direct_reactive.cpp:53-378), the viscous Jacobian closure
+// (:1200-1401, :1637-1653).
+#ifndef RX_WPE_ASMES
+#define RX_WPE_ASMES RX_WPE(NDIM == 2 ? 3 : 2)
+#endif
+#ifndef RX_ASMES_WAVES
+#define RX_ASMES_WAVES 4  // build knob: wavefronts per k_asm_es workgroup
+#endif
+#ifndef RX_ASMES_STAGE
+#define RX_ASMES_STAGE 1  // build knob: 0 = phase A gathers its node records per entry and stages the summary first
+#endif
+#ifndef RX_ASMES_PROBE
+// build knob (tools/asm_probe.py, timing only, results wrong): 1 = no summary gather (constant records), 2 = no viscous
+// column, 3 = no AUSM evaluation, 4 = no phase-B sums, 5 = neither column
+#define RX_ASMES_PROBE 0
+#endif
+__host__ __device__ constexpr int asmes_teams(int nVar) { return RX_ASMES_WAVES * (64 / nVar); }
+__host__ __device__ constexpr int asmes_out(int nVar) { return 2 * nVar + 2; }  // parked doubles per lane
+template <int NS, int NDIM>
+__global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
+    const int32_t* __restrict__ wg_node, const int32_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj,
+    const int32_t* __restrict__ edges, const int64_t* __restrict__ edge_blk, const int64_t* __restrict__ diag,
+    const double* __restrict__ Fc, const double* __restrict__ Fv, const double* __restrict__ Jc,
+    const double* __restrict__ dTdU, const double* __restrict__ Summ, const double* __restrict__ Js,
+    const double* __restrict__ Rsrc, DevMech m, ViscParams P, double* __restrict__ R, double* __restrict__ A, int src,
+    AusmIn cv, SysFold fd) {
+  constexpr int nVar = NS + NDIM + 2, nVar2 = nVar * nVar, SS = visc_summary_size<NS, NDIM>();
+  constexpr int TPW = 64 / nVar, kTeams = asmes_teams(nVar), OW = asmes_out(nVar);
+  constexpr int TS = SS > nVar * OW ? SS : nVar * OW;  // a team's slot: the summary record, then its parked outputs
+  constexpr int nPV = NS + NDIM + 5;
+  constexpr int rhos = NDIM + 2, nsv = NS * nVar;
+  __shared__ double ssm[kTeams * TS];
+  const int lane = threadIdx.x % 64, wv = threadIdx.x / 64, tw = lane / nVar;
+  const bool live = tw < TPW;  // lanes past the wavefront's last whole team take no part
+  const int team = wv * TPW + (live ? tw : 0), b = live ? lane - tw * nVar : 0, sbase = tw * nVar;
+  const int g = xcd_block(blockIdx.x, gridDim.x);
+  const int n_lo = wg_node[g], n_hi = wg_node[g + 1];
+  const int kb = adj_ptr[n_lo], ke = adj_ptr[n_hi];
+  double* slot = ssm + team * TS;
+  const bool fused = RX_ASMV_FUSE && cv.V != nullptr;
+  // ---- phase A: edge side kb + team
+  if (live && kb + team < ke) {
+    const int ad = adj[kb + team];
+    const int e = ad >> 1, side = ad & 1;
+    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    const double* tile = Summ + (size_t)(e / kSummTile) * SS * kSummTile + e % kSummTile;
+    double fc, jd[nVar];
+    double sob, fv;
+    double* Ao;
+    if (RX_ASMES_STAGE && fused && RX_ASMES_PROBE != 3 && RX_ASMES_PROBE != 5) {
+      // loads in two groups, in this issue order (vmcnt retires in order): (1) the node records the AUSM pass reads,
+      // one entry per lane, and the per-edge indices; (2) the summary record, into registers. The AUSM pass waits
+      // only for group 1 (through the team's LDS slot: one global load per lane and record instead of one per entry
+      // and lane); the summary lands while it computes, and goes to the slot after it.
+      const double* Vsi = cv.VR ? cv.VR + 2 * (size_t)e * nPV : cv.V + (size_t)n0 * nPV;
+      const double* Vsj = cv.VR ? cv.VR + (2 * (size_t)e + 1) * nPV : cv.V + (size_t)n1 * nPV;
+      const double* Ssi = cv.VR ? cv.SR + 2 * (size_t)e * nVar : cv.dPdU + (size_t)n0 * nVar;
+      const double* Ssj = cv.VR ? cv.SR + (2 * (size_t)e + 1) * nVar : cv.dPdU + (size_t)n1 * nVar;
+      constexpr int kVX = nPV - nVar;  // record entries past the team's width (3 in every instantiation)
+      static_assert(kVX >= 0 && kVX <= nVar, "a record is at most two loads per lane");
+      static_assert(SS + 2 * nPV + 2 * nVar <= TS, "the staged records fit the team's slot beside the summary");
+      const double gvi = Vsi[b], gvj = Vsj[b], gsi = Ssi[b], gsj = Ssj[b];
+      const double gxi = b < kVX ? Vsi[nVar + b] : 0.0, gxj = b < kVX ? Vsj[nVar + b] : 0.0;
+      double nrm[NDIM];
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[(size_t)e * NDIM + d];
+      sob = dTdU[(size_t)(side ? n1 : n0) * nVar + b];
+      fv = Fv[(size_t)e * nVar + b];
+      Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int kSR = (SS + nVar - 1) / nVar;
+      double sreg[kSR];
+#pragma unroll
+      for (int q = 0; q < kSR; ++q) sreg[q] = b + q * nVar < SS ? tile[(size_t)(b + q * nVar) * kSummTile] : 0.0;
+      __builtin_amdgcn_sched_barrier(0);
+      double* vs = slot + SS;  // V_i, V_j, dP/dU_i, dP/dU_j
+      vs[b] = gvi;
+      vs[nPV + b] = gvj;
+      if (b < kVX) {
+        vs[nVar + b] = gxi;
+        vs[nPV + nVar + b] = gxj;
+      }
+      vs[2 * nPV + b] = gsi;
+      vs[2 * nPV + nVar + b] = gsj;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const double* Li = vs;
+      const double* Lj = vs + nPV;
+      AusmEdge s;
+      {
+        double Vi[nPV], Vj[nPV];  // the entries ausm_scalars reads
+#pragma unroll
+        for (int v = 0; v < nPV; ++v) {
+          Vi[v] = v <= NDIM + 2 || v == NDIM + 4 ? Li[v] : 0.0;
+          Vj[v] = v <= NDIM + 2 || v == NDIM + 4 ? Lj[v] : 0.0;
+        }
+        ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+      }
+      bool bad = false;
+      {
+        const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
+        const double pi = b == 0 ? 1.0 : Li[pidx];
+        const double pj = b == 0 ? 1.0 : Lj[pidx];
+        double f = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
+        if (b >= 1 && b <= NDIM) f += s.pLF * pick<NDIM>(s.UN, b - 1) * s.Area;
+        bad |= isnan(f);
+        fc = f;
+      }
+      const AusmCol cc = ausm_col_b<NDIM>(s, gsi, gsj, b);
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) {
+        const double v = ausm_jac_entry_own<NDIM>(s, cc, ausm_phi<NDIM>(Li, Li[NDIM + 3], a),
+                                                  ausm_phi<NDIM>(Lj, Lj[NDIM + 3], a), side ? gsj : gsi, a, b, side);
+        bad |= isnan(v);
+        jd[a] = v;
+      }
+      if (bad) set_err(cv.err, ERR_NAN_UPWIND, (int64_t)e);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < kSR; ++q)
+        if (b + q * nVar < SS) slot[b + q * nVar] = sreg[q];
+    } else {
+      for (int q = b; q < SS; q += nVar) slot[q] = RX_ASMES_PROBE == 1 ? 0.25 + q : tile[(size_t)q * kSummTile];
+      sob = dTdU[(size_t)(side ? n1 : n0) * nVar + b];  // the own node's dT/dU
+      fv = Fv[(size_t)e * nVar + b];
+      Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
+    if (RX_ASMES_PROBE == 3 || RX_ASMES_PROBE == 5) {
+      const double* Vsi = cv.V + (size_t)n0 * nPV;
+      fc = Vsi[b];
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) jd[a] = cv.dPdU[(size_t)n1 * nVar + a];
+    } else if (fused) {
+      // k_asm_visc's fused pass: the edge scalars (every lane of the team makes the same ones: one pass of the
+      // wavefront for its five edges), this lane's flux component and the own side's Jacobian column
+      const double* Vsi = cv.VR ? cv.VR + 2 * (size_t)e * nPV : cv.V + (size_t)n0 * nPV;
+      const double* Vsj = cv.VR ? cv.VR + (2 * (size_t)e + 1) * nPV : cv.V + (size_t)n1 * nPV;
+      const double* Ssi = cv.VR ? cv.SR + 2 * (size_t)e * nVar : cv.dPdU + (size_t)n0 * nVar;
+      const double* Ssj = cv.VR ? cv.SR + (2 * (size_t)e + 1) * nVar : cv.dPdU + (size_t)n1 * nVar;
+      AusmEdge s;
+      {
+        double Vi[nPV], Vj[nPV], nrm[NDIM];  // the entries ausm_scalars reads
+#pragma unroll
+        for (int v = 0; v < nPV; ++v) {
+          Vi[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsi[v] : 0.0;
+          Vj[v] = v <= NDIM + 2 || v == NDIM + 4 ? Vsj[v] : 0.0;
+        }
+#pragma unroll
+        for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[(size_t)e * NDIM + d];
+        ausm_scalars<NDIM>(Vi, Vj, nrm, cv.mInfty, s);
+      }
+      bool bad = false;
+      {
+        const int pidx = (b <= NDIM) ? b : (b == NDIM + 1 ? NDIM + 3 : b + 3);
+        const double pi = b == 0 ? 1.0 : Vsi[pidx];
+        const double pj = b == 0 ? 1.0 : Vsj[pidx];
+        double f = 0.5 * (s.M12 * (pi + pj) + fabs(s.M12) * (pi - pj)) * s.Area;
+        if (b >= 1 && b <= NDIM) f += s.pLF * pick<NDIM>(s.UN, b - 1) * s.Area;
+        bad |= isnan(f);
+        fc = f;
+      }
+      const double sib = Ssi[b], sjb = Ssj[b];
+      const AusmCol cc = ausm_col_b<NDIM>(s, sib, sjb, b);
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) {
+        const double v = ausm_jac_entry_own<NDIM>(s, cc, ausm_phi<NDIM>(Vsi, Vsi[NDIM + 3], a),
+                                                  ausm_phi<NDIM>(Vsj, Vsj[NDIM + 3], a), side ? sjb : sib, a, b, side);
+        bad |= isnan(v);
+        jd[a] = v;
+      }
+      if (bad) set_err(cv.err, ERR_NAN_UPWIND, (int64_t)e);
+    } else {
+      fc = Fc[(size_t)e * nVar + b];
+      const double* J = Jc + ((size_t)e * 2 + side) * nVar2 + b;
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) jd[a] = J[a * nVar];
+    }
+    }
+    double jco[nVar];  // 0 -+ this lane's column of the own-side convective block
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) jco[a] = side ? 0.0 + jd[a] : 0.0 - jd[a];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    double jv[nVar];
+    if (RX_ASMES_PROBE == 2 || RX_ASMES_PROBE == 5) {
+#pragma unroll
+      for (int rr = 0; rr < nVar; ++rr) {
+        jv[rr] = sob * slot[rr];
+        Ao[rr * nVar + b] = side ? jco[rr] - jv[rr] : jco[rr] + jv[rr];
+      }
+    } else {
+      visc_jac_column_own<NS, NDIM>(m, P, SummCRef{slot, 1}, sob, side, b, b, sbase, [&](int rr, double v) {
+        jv[rr] = v;
+        Ao[rr * nVar + b] = side ? jco[rr] - v : jco[rr] + v;
+      });
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // the team has read its summary record: the slot takes the parked outputs
+    double* o = slot + b * OW;
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) {
+      o[a] = side ? -jd[a] : jd[a];
+      o[nVar + 1 + a] = side ? jv[a] : -jv[a];
+    }
+    o[nVar] = side ? -fc : fc;
+    o[2 * nVar + 1] = side ? fv : -fv;
+  }
+  __syncthreads();
+  // ---- phase B: node n_lo + team
+  const int i = n_lo + team;
+  if (!live || i >= n_hi) return;
+  const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  double r = 0.0, D[nVar];
+#pragma unroll
+  for (int a = 0; a < nVar; ++a) D[a] = 0.0;
+  for (int k = k0; k < (RX_ASMES_PROBE == 4 ? k0 + 1 : k1); ++k) {
+    const double* o = ssm + (k - kb) * TS + b * OW;
+    r += o[nVar];
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) D[a] += o[a];
+  }
+  for (int k = k0; k < (RX_ASMES_PROBE == 4 ? k0 : k1); ++k) {
+    const double* o = ssm + (k - kb) * TS + b * OW;
+    r += o[2 * nVar + 1];
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) D[a] += o[nVar + 1 + a];
+  }
+  if (src) {
+    r += Rsrc[(size_t)i * nVar + b];
+#pragma unroll
+    for (int a = 0; a < nVar; ++a) {
+      const double js = a >= rhos ? Js[(size_t)(i / kSrcTile) * nsv * kSrcTile +
+                                       (size_t)((a - rhos) * nVar + b) * kSrcTile + i % kSrcTile]
+                                  : 0.0;
+      D[a] += js;
+    }
+  }
+  if (fd.vol && i < fd.Nd && !fd.skip[i]) {
+    if (fd.dt[i] > rx::kEPS) {
+      const double delta = fd.vol[i] / fd.dt[i];
+#pragma unroll
+      for (int a = 0; a < nVar; ++a)
+        if (a == b) D[a] += delta;
+    } else {
+#pragma unroll
+      for (int a = 0; a < nVar; ++a) D[a] = (a == b) ? 1.0 : 0.0;
+      r = 0.0;
+    }
+  }
+  R[(size_t)i * nVar + b] = r;
+  double* Ad = A + diag[i] * nVar2 + b;
+#pragma unroll
+  for (int a = 0; a < nVar; ++a) Ad[a * nVar] = D[a];
+}
+
 // a12: weighted least-squares gradient of (T, u, v, P, X_s) per node.
 template <int NS, int NDIM>
 __global__ __launch_bounds__(kBlock) void k_grad_lsq(int N, const int32_t* __restrict__ nptr,
@@ -1673,6 +1941,8 @@ int RX_NSFN(rx_launch_ausm_node)(rx_ctx* ctx) {
 // evaluated and nVar-lane teams (5 nodes per wavefront), C5 (same box, gpurun_out r05q) CONV 2.01 + ASSEMBLE 7.53 ->
 // ASSEMBLE 9.13 ms, 39.91 -> 39.55 ms per step (round 4: 2.29 + 8.71 -> 11.76 ms, so 3-D kept the edge kernel).
 // RX_ASM_CONV=0 never fuses (A/B, tests/test_gpu_assembly.py); RX_ASM_VISC=0 never fuses
+int rx_asmes_teams(int nVar) { return asmes_teams(nVar); }
+
 bool rx_fuse_conv(int nDim) {
   (void)nDim;
   static const int mode = [] {
@@ -1689,8 +1959,16 @@ bool rx_fuse_conv(int nDim) {
 int RX_NSFN(rx_launch_ausm_edge)(rx_ctx* ctx) {
   if (!ctx->jconv) {  // allocated at first use: the 2-D fused assembly never needs the per-edge blocks
     if (ctx->capturing) return RX_ERR_STATE;
-    RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->fconv), sizeof(double) * ctx->E * ctx->nVar));
-    RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->jconv), sizeof(double) * ctx->E * 2 * ctx->nVar * ctx->nVar));
+    // both or neither (a failed jconv used to leave fconv allocated, and the next call allocated it again)
+    if (!ctx->fconv) RX_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->fconv), sizeof(double) * ctx->E * ctx->nVar));
+    const hipError_t e =
+        hipMalloc(reinterpret_cast<void**>(&ctx->jconv), sizeof(double) * ctx->E * 2 * ctx->nVar * ctx->nVar);
+    if (e != hipSuccess) {
+      (void)hipFree(ctx->fconv);
+      ctx->fconv = nullptr;
+      ctx->jconv = nullptr;
+      return rx_fail_hip(ctx, e);
+    }
   }
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_ausm_edge<NS_, ND_><<<blocks(ctx->E * kAusmTeam, kAusmBlock), kAusmBlock, 0, ctx->stream>>>(
                             (int)ctx->E, ctx->edges, ctx->normal, ctx->f[RX_F_V], ctx->f[RX_F_DPDU],
@@ -1779,6 +2057,21 @@ int RX_NSFN(rx_launch_asm_visc)(rx_ctx* ctx, int with_src, int fused_conv) {
     fd.vol = ctx->vol;
     fd.dt = ctx->f[RX_F_DT];
     fd.skip = ctx->fold_skip;
+  }
+  // edge-side teams (k_asm_es, round 6) unless a node has more edges than a workgroup has teams, or RX_ASMV_ES=0 (the
+  // node-serial k_asm_visc, for A/B and tests/test_gpu_assembly.py)
+  static const bool es = [] {
+    const char* v = getenv("RX_ASMV_ES");
+    return !(v && v[0] == '0');
+  }();
+  if (es && !RX_ASMV_PARK && ctx->asmes_wg && ctx->asmes_nwg > 0) {
+    RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_es<NS_, ND_><<<ctx->asmes_nwg, RX_ASMES_WAVES * 64, 0, ctx->stream>>>(
+                              ctx->asmes_wg, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
+                              ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech, P,
+                              ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv, fd)));
+    RX_HIP(hipGetLastError());
+    ctx->sys_folded = fd.vol ? 1 : 0;
+    return RX_OK;
   }
   RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_visc<NS_, ND_><<<(ctx->N + asmv_nodes_per_block(NS_ + ND_ + 2) - 1) /
                                                                      asmv_nodes_per_block(NS_ + ND_ + 2),

@@ -1055,8 +1055,11 @@ int rx_la_smoother_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero) {
 // RESTARTED_FGMRES (Solve :662-671): FGMRES cycles of `iter` iterations (the remainder once fewer than `restart`
 // are left) from the previous cycle's x, the tolerance scaled by 1 / |b| after each cycle, until `iter` iterations
 // are spent or |b| < tol. Each cycle's iteration count decides the next, so the cycles synchronise with the host.
-// The reference's loop does not end if a cycle keeps returning 0 iterations with |b| >= tol (its start test meets
-// |r| < eps); this one stops after kMaxCycles and reports RX_ERR_DIVERGED.
+// A cycle that returns 0 iterations has met FGMRES's start test (|r| < eps or |r| < tol |b|, :367-370) and left x as
+// it was, so every later cycle would see the same x: the reference's loop then either spins until the growing
+// tolerance passes |b| (|b| < 1) or never ends (|b| >= 1). This one stops there with RX_OK: the same x and the same
+// iteration count (it used to spin 4096 host-synchronous cycles and report RX_ERR_DIVERGED). kMaxCycles
+// stays as a bound on cycles that keep iterating.
 int rx_la_restarted_fgmres(rx_ctx* ctx, double tol, int iter, int restart, bool x_zero, int* iters, double* resid) {
   constexpr int kMaxCycles = 4096;
   if (iter < 1 || iter > kMaxM) return RX_ERR_ARG;
@@ -1071,6 +1074,7 @@ int rx_la_restarted_fgmres(rx_ctx* ctx, double tol, int iter, int restart, bool 
     total += it;
     // FGMRES updates x over every element, its halo from the exchanged z (:455-457): the next cycle's A x reads it
     if (ctx->distributed() && (rc = rx_la_exchange(ctx, ctx->f[RX_F_SOL], ctx->nVar))) return rc;
+    if (it == 0) break;  // the start test: x is final (above)
     const double bn = static_cast<KState*>(ctx->h_kstate)->bnorm;
     if (bn < stol) break;
     stol = stol * (1.0 / bn);

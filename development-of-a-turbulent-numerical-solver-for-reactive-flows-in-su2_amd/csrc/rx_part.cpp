@@ -232,8 +232,10 @@ std::vector<int> initial_bisection(const Graph& g, int64_t target0, const int64_
   return best;
 }
 
-// Multilevel bisection of g with side 0 holding `frac` of the weight (balance tolerance eps per side).
-std::vector<int> bisect(const Graph& g, double frac, double eps, std::mt19937& rng) {
+// Multilevel bisection of g with side 0 holding `frac` of the weight (balance tolerance eps per side); each side keeps
+// at least min0 / min1 of the weight (its part count: no part comes out empty whatever eps).
+std::vector<int> bisect(const Graph& g, double frac, double eps, std::mt19937& rng, int64_t min0 = 0,
+                        int64_t min1 = 0) {
   const int64_t tot = g.total_vw();
   const int64_t t0 = (int64_t)(frac * (double)tot + 0.5);
   std::vector<Graph> levels{g};
@@ -251,6 +253,8 @@ std::vector<int> bisect(const Graph& g, double frac, double eps, std::mt19937& r
     // the tolerance, widened on coarse levels by one coarse vertex (so a balanced move exists)
     maxw[0] = (int64_t)((double)t0 * (1.0 + eps)) + (h.n == g.n ? 0 : maxv);
     maxw[1] = (int64_t)((double)(tot - t0) * (1.0 + eps)) + (h.n == g.n ? 0 : maxv);
+    maxw[0] = std::min(maxw[0], tot - min1 + (h.n == g.n ? 0 : maxv));
+    maxw[1] = std::min(maxw[1], tot - min0 + (h.n == g.n ? 0 : maxv));
   };
   int64_t maxw[2];
   bounds(levels.back(), maxw);
@@ -294,7 +298,7 @@ void recurse(const Graph& g, const std::vector<int>& verts, int nparts, int p0, 
   }
   const int left = nparts / 2;
   const Graph s = induced(g, verts, local);
-  const std::vector<int> where = bisect(s, (double)left / nparts, eps, rng);
+  const std::vector<int> where = bisect(s, (double)left / nparts, eps, rng, left, nparts - left);
   std::vector<int> a, b;
   for (int i = 0; i < s.n; ++i) (where[i] == 0 ? a : b).push_back(verts[i]);
   recurse(g, a, left, p0, eps, rng, local, part);
@@ -370,6 +374,12 @@ extern "C" int rx_partition_graph(int64_t n, const int64_t* xadj, const int64_t*
   if (n < 0 || n >= (1LL << 31) || nparts < 1 || !part || (n > 0 && (!xadj || !adj)) || imbalance < 0.0)
     return RX_ERR_ARG;
   if (nparts > n && n > 0) return RX_ERR_ARG;
+  // a CSR offset array: starts at 0, never decreases, and its total fits the int32 adjacency
+  if (n > 0) {
+    if (xadj[0] != 0 || xadj[n] >= (1LL << 31)) return RX_ERR_ARG;
+    for (int64_t v = 0; v < n; ++v)
+      if (xadj[v + 1] < xadj[v]) return RX_ERR_ARG;
+  }
   Graph g;
   g.n = (int)n;
   g.xadj.resize(n + 1);
@@ -391,8 +401,14 @@ extern "C" int rx_partition_graph(int64_t n, const int64_t* xadj, const int64_t*
   recurse(g, verts, nparts, 0, eps, rng, local, part);
   if (nparts > 2) {
     const double mean = (double)n / nparts;
-    kway_vcycle(g, part, nparts, (int64_t)std::floor(mean * (1.0 - imbalance)),
+    kway_vcycle(g, part, nparts, std::max<int64_t>(1, (int64_t)std::floor(mean * (1.0 - imbalance))),
                 (int64_t)std::ceil(mean * (1.0 + imbalance)), rng);
+  }
+  {  // every part holds a vertex (the bisection's per-side minimum and the k-way pass's floor of one vertex)
+    std::vector<char> used(nparts, 0);
+    for (int64_t v = 0; v < n; ++v) used[part[v]] = 1;
+    for (int p = 0; p < nparts && n > 0; ++p)
+      if (!used[p]) return RX_ERR_RANGE;
   }
   if (edge_cut) {
     std::vector<int> w(part, part + n);

@@ -200,9 +200,10 @@ int rx_sync(rx_ctx *ctx);
 int64_t rx_last_error_index(const rx_ctx *ctx);
 /* Which reference loop produced the last RX_ERR_NAN that rx_sync / a phase call returned: RX_ERR_PHASE_CALL = the loop
  * of the call itself; RX_ERR_PHASE_UPWIND = Upwind_Residual (solver_direct_reactive.cpp:2746-2757 "NaN found in the
- * upwind residual"): in 2-D the implicit AUSM flux and Jacobians are evaluated by the node-centric assembly, which
- * runs at the first call that needs the system (rx_bc_flow, rx_fgmres, a RES / JAC download), not by
- * rx_edge_flux_conv. */
+ * upwind residual"): in 2-D and in 3-D (round 5) the implicit AUSM flux and Jacobians are evaluated by the
+ * node-centric assembly (k_asm_es / k_asm_visc), which runs at the first call that needs the system (rx_bc_flow,
+ * rx_fgmres, a RES / JAC download), not by rx_edge_flux_conv; with RX_ASM_CONV=0 or RX_ASM_VISC=0 in the environment
+ * the edge kernel k_ausm_edge evaluates them inside rx_edge_flux_conv again. */
 typedef enum { RX_ERR_PHASE_CALL = 0, RX_ERR_PHASE_UPWIND = 1 } rx_err_phase;
 int rx_last_error_phase(const rx_ctx *ctx);
 const char *rx_status_string(int status);

@@ -4,15 +4,17 @@
 
 #include "../../development-of-a-turbulent-numerical-solver-for-reactive-flows-in-su2_amd/csrc/rx_fdiv.h"
 
+template <bool Guard>
 __global__ void k_fdiv_check(const double* __restrict__ n, const double* __restrict__ d, double* __restrict__ ref,
                              double* __restrict__ fast, int count) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   ref[i] = n[i] / d[i];
-  fast[i] = rx::rx_div(n[i], rx::rx_recip(d[i]));
+  fast[i] = rx::rx_div<Guard>(n[i], rx::rx_recip(d[i]));
 }
 
-extern "C" int fdiv_check(const double* hn, const double* hd, double* href, double* hfast, int count) {
+template <bool Guard>
+int fdiv_run(const double* hn, const double* hd, double* href, double* hfast, int count) {
   if (count <= 0) return 1;
   double* buf = nullptr;
   const size_t bytes = sizeof(double) * (size_t)count;
@@ -22,7 +24,7 @@ extern "C" int fdiv_check(const double* hn, const double* hd, double* href, doub
       hipMemcpy(buf + count, hd, bytes, hipMemcpyHostToDevice) != hipSuccess)
     rc = 3;
   if (!rc) {
-    k_fdiv_check<<<(count + 255) / 256, 256>>>(buf, buf + count, buf + 2 * (size_t)count, buf + 3 * (size_t)count,
+    k_fdiv_check<Guard><<<(count + 255) / 256, 256>>>(buf, buf + count, buf + 2 * (size_t)count, buf + 3 * (size_t)count,
                                                count);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = 4;
   }
@@ -31,4 +33,12 @@ extern "C" int fdiv_check(const double* hn, const double* hd, double* href, doub
     rc = 5;
   (void)hipFree(buf);
   return rc;
+}
+
+// rx_div as the kernels use it (the build's RX_FDIV_GUARD, 0 by default) and the guarded rx_div<true>
+extern "C" int fdiv_check(const double* hn, const double* hd, double* href, double* hfast, int count) {
+  return fdiv_run<(RX_FDIV_GUARD != 0)>(hn, hd, href, hfast, count);
+}
+extern "C" int fdiv_check_guarded(const double* hn, const double* hd, double* href, double* hfast, int count) {
+  return fdiv_run<true>(hn, hd, href, hfast, count);
 }

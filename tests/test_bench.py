@@ -25,18 +25,25 @@ def test_ilu_apply_kernel_names(monkeypatch):
 def test_kernel_models_cover_the_timed_phases(monkeypatch):
     monkeypatch.delenv("RX_ASM_CONV", raising=False)
     monkeypatch.delenv("RX_ASM_VISC", raising=False)
+    monkeypatch.delenv("RX_ASMV_ES", raising=False)
     m = bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)
     for k in ("VISC", "VISC_JAC", "ASSEMBLE", "GRAD", "SOURCE", "ILU_BUILD", "SPMV", "ILU_APPLY"):
         assert k in m and m[k]["kernel"] and m[k]["peak"] > 0, k
     assert m["SPMV"]["unit"] == "GB/s" and m["ILU_APPLY"]["kernel"].startswith("k_ilu_apply_")
     # the node-centric assembly (default) makes the viscous Jacobians and the AUSM fluxes / Jacobians itself:
     # no k_ausm_edge launch in the CONV phase, and no per-edge convective blocks in the assembly's bytes
-    assert m["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>" and "CONV" not in m
-    m3 = bench.kernel_models(8_000_000, 23_580_000, 62_000_000, 7, 3, 5)  # 3-D: fused too (round 5)
-    assert m3["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 3>" and "CONV" not in m3
+    # (round 6: with edge-side teams, k_asm_es; the node-serial k_asm_visc with RX_ASMV_ES=0 or a node of more edges
+    # than teams)
+    assert m["ASSEMBLE"]["kernel"] == "k_asm_es<7, 2>" and "CONV" not in m
+    m3 = bench.kernel_models(8_000_000, 23_580_000, 62_000_000, 7, 3, 5, max_degree=6)  # 3-D: fused too (round 5)
+    assert m3["ASSEMBLE"]["kernel"] == "k_asm_es<7, 3>" and "CONV" not in m3
+    assert bench.kernel_models(1_000, 2_000, 5_000, 7, 3, 5, max_degree=24)["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 3>"
+    monkeypatch.setenv("RX_ASMV_ES", "0")
+    assert bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>"
+    monkeypatch.delenv("RX_ASMV_ES")
     monkeypatch.setenv("RX_ASM_CONV", "0")
     u = bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)
-    assert u["CONV"]["kernel"] == "k_ausm_edge<7, 2>" and u["ASSEMBLE"]["kernel"] == "k_asm_visc<7, 2>"
+    assert u["CONV"]["kernel"] == "k_ausm_edge<7, 2>" and u["ASSEMBLE"]["kernel"] == "k_asm_es<7, 2>"
     assert u["ASSEMBLE"]["work"] > m["ASSEMBLE"]["work"]
     monkeypatch.setenv("RX_ASM_VISC", "0")
     assert bench.kernel_models(1_000_000, 1_997_500, 4_995_000, 7, 2, 5)["ASSEMBLE"]["kernel"] == "k_assemble<11, 4>"

@@ -3,7 +3,8 @@ flux and Jacobians (k_asm_visc's fused pass, the default) against the per-edge c
 (k_ausm_edge + k_asm_visc's non-fused pass, RX_ASM_CONV=0), bitwise, for 1st order and both MUSCL branches; the
 3-D fused default (round 5) against the edge kernel path, 1st order and MUSCL; and a re-assembly of the same residual after
 an intermediate download (Upwind, Viscous, RES download, then Source) against the straight sequence and the
-reference's golden system. Requires an MI355X."""
+reference's golden system. Round 6: the edge-side-team assembly (k_asm_es, the default) against the node-serial
+k_asm_visc (RX_ASMV_ES=0), fused and per-edge convective, 2-D and 3-D, every spatial order. Requires an MI355X."""
 import os
 import subprocess
 import sys
@@ -18,12 +19,15 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_variant(tmp_path, case, order, env_val):
+def run_variant(tmp_path, case, order, env_val, es=None):
     env = dict(os.environ)
     env.pop("RX_ASM_CONV", None)
+    env.pop("RX_ASMV_ES", None)
     if env_val is not None:
         env["RX_ASM_CONV"] = env_val
-    out = str(tmp_path / f"{case}_{order}_{env_val}.npz")
+    if es is not None:
+        env["RX_ASMV_ES"] = es
+    out = str(tmp_path / f"{case}_{order}_{env_val}_{es}.npz")
     subprocess.run([sys.executable, os.path.join(HERE, "asm_variant_run.py"), case, str(order), out], env=env,
                    check=True, timeout=300)
     return dict(np.load(out))
@@ -43,6 +47,18 @@ def test_fused_ausm_assembly_3d_is_bitwise(tmp_path, order):
     edge = run_variant(tmp_path, "mini3d", order, "0")
     assert np.array_equal(fused["res"], edge["res"])
     assert np.array_equal(fused["jac"], edge["jac"])
+
+
+@pytest.mark.parametrize("case,order", [("mini9", 0), ("mini9", 1), ("mini9", 2), ("jet9w", 2), ("mini3d", 0),
+                                        ("mini3d", 2)])
+@pytest.mark.parametrize("conv", [None, "0"])
+def test_edge_side_teams_are_bitwise_the_node_serial_assembly(tmp_path, case, order, conv):
+    """k_asm_es (each team one adjacency entry, the node's contributions added in phase B in k_asm_visc's order)
+    against k_asm_visc: residual and every BSR block bitwise, with the fused AUSM pass and with k_ausm_edge's blocks."""
+    es = run_variant(tmp_path, case, order, conv)
+    serial = run_variant(tmp_path, case, order, conv, es="0")
+    assert np.array_equal(es["res"], serial["res"])
+    assert np.array_equal(es["jac"], serial["jac"])
 
 
 @pytest.mark.parametrize("case", ["mini9", "mini3d"])

@@ -14,12 +14,15 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run(tmp_path, nz, no_fold):
+def run(tmp_path, nz, no_fold, es=None):
     env = dict(os.environ)
     env.pop("RX_NO_FOLD", None)
+    env.pop("RX_ASMV_ES", None)
     if no_fold:
         env["RX_NO_FOLD"] = "1"
-    out = str(tmp_path / f"fold_{nz}_{int(no_fold)}.npz")
+    if es is not None:
+        env["RX_ASMV_ES"] = es
+    out = str(tmp_path / f"fold_{nz}_{int(no_fold)}_{es}.npz")
     subprocess.run([sys.executable, os.path.join(HERE, "fold_run.py"), str(nz), out], env=env, check=True,
                    timeout=300)
     return dict(np.load(out))
@@ -30,3 +33,11 @@ def test_folded_system_is_bitwise_the_unfolded_build(tmp_path, nz):
     folded, plain = run(tmp_path, nz, False), run(tmp_path, nz, True)
     for key in ("U", "T", "rms"):
         assert np.array_equal(folded[key], plain[key]), key
+
+
+@pytest.mark.parametrize("nz", [0, 4])
+def test_folded_edge_side_assembly_is_bitwise_the_node_serial_one(tmp_path, nz):
+    """Round 6: the folded k_asm_es (default) against the folded k_asm_visc (RX_ASMV_ES=0), whole outer iterations."""
+    es, serial = run(tmp_path, nz, False), run(tmp_path, nz, False, es="0")
+    for key in ("U", "T", "rms"):
+        assert np.array_equal(es[key], serial[key]), key

@@ -98,3 +98,33 @@ def test_implicit_step_with_solver_vs_oracle(solver, prec):
     assert_close(out[0][2], x_o.ravel(), rtol=0.0, what=f"{solver} step solution vs oracle on the device system")
     assert out[1][1] == out[0][1] and np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][2], out[0][2])
     s.close()
+
+
+def test_restarted_fgmres_stops_when_a_cycle_starts_converged():
+    """a RESTARTED_FGMRES cycle that returns 0 iterations (FGMRES's start test, |r| < eps,
+    linear_solvers_structure.cpp:367-370) leaves x unchanged, so the reference's cycle loop would spin (|b| >= 1: its
+    tolerance only shrinks); the device stops there with RX_OK, x untouched, 0 iterations — it used to spin 4096
+    host-synchronous cycles and report RX_ERR_DIVERGED. System: identity blocks, x0 = b (r = 0 exactly), |b| >> 1."""
+    mesh, st, mech_arrays, kw, rp, col, A, b = system(1)
+    nv = A.shape[1]
+    eye = np.zeros_like(A)
+    for i in range(len(rp) - 1):
+        d = rp[i] + int(np.nonzero(col[rp[i]:rp[i + 1]] == i)[0][0])
+        eye[d] = np.eye(nv)
+    bb = 3.0 + np.arange(b.size, dtype=np.float64) % 7
+    kw.update(lin_tol=1e-6, lin_iter=8)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays),
+                            rx.default_cfg(implicit=1, lin_prec=rx.PREC_ILU, lin_solver=rx.LIN_RESTARTED_FGMRES,
+                                           lin_restart=2, **kw))
+    s.set_state(st)
+    s.Preprocessing_zero()
+    s.Upwind_Residual()
+    s.sync()
+    s.download("RES")
+    s.upload("JAC", eye)
+    s.upload("RHS", bb)
+    s.upload("SOL", bb)
+    it, res = s.linear_solve()
+    assert it == 0 and res == 0.0, (it, res)
+    assert np.array_equal(s.download("SOL"), bb)
+    s.close()
