@@ -609,17 +609,27 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
   for (int64_t i = 0; i < N; ++i) ctx->max_degree = std::max(ctx->max_degree, (int)(adj_ptr[i + 1] - adj_ptr[i]));
   if (ctx->kind == RX_KIND_FLOW) {  // k_asm_es's node runs: consecutive nodes while their edge sides fit the teams
     const int T = rx_asmes_teams(ctx->nVar);
-    std::vector<int32_t> wg{0};
-    bool ok = true;
+    std::vector<int32_t> wg{0, 0};
+    bool ok = ctx->h_rp.back() < (1LL << 31);  // block indices as int32
     for (int64_t n = 0; n < N && ok;) {
       const int64_t lo = n;
       while (n < N && n - lo < T && adj_ptr[n + 1] - adj_ptr[lo] <= T) ++n;
       ok = n > lo;  // a node with more edges than teams
       wg.push_back((int32_t)n);
+      wg.push_back((int32_t)adj_ptr[n]);
     }
     if (ok && N > 0) {
+      std::vector<int32_t> sr(8 * (size_t)E);
+      for (int64_t k = 0; k < 2 * E; ++k) {
+        const int64_t e = adj[k] >> 1, side = adj[k] & 1;
+        sr[4 * k] = (int32_t)((uint32_t)e | ((uint32_t)side << 31));
+        sr[4 * k + 1] = e32[2 * e];
+        sr[4 * k + 2] = e32[2 * e + 1];
+        sr[4 * k + 3] = (int32_t)edge_blk[2 * e + (side ? 0 : 1)];
+      }
       CK(dupload(ctx, &ctx->asmes_wg, wg.data(), wg.size()));
-      ctx->asmes_nwg = (int)wg.size() - 1;
+      CK(dupload(ctx, &ctx->asmes_side, sr.data(), sr.size()));
+      ctx->asmes_nwg = (int)wg.size() / 2 - 1;
     }
   }
   CK(dupload(ctx, &ctx->nbr_ptr, nptr.data(), N + 1));
@@ -822,7 +832,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   ctx->solve_exec = nullptr;
   ctx->solve_graph = nullptr;
   if (ctx->kind == RX_KIND_SST && ctx->flow) --ctx->flow->n_children;
-  void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->asmes_wg, ctx->nbr_ptr,
+  void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->asmes_wg, ctx->asmes_side, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.pass_lo, ctx->fs.part_pass, ctx->bs.pass_lo, ctx->bs.part_pass,

@@ -76,9 +76,12 @@ struct rx_ctx {
   int64_t* adj_blk = nullptr;   // [2E] BSR block index of (node, other)
   int64_t* edge_blk = nullptr;  // [E][2] BSR block index of (n0, n1) and (n1, n0)
   int max_degree = 0;           // incident edges of the busiest node
-  // k_asm_es (round 6): workgroup g assembles nodes [asmes_wg[g], asmes_wg[g+1]), whose adjacency entries fit its
-  // rx_asmes_teams(nVar) edge-side teams; null when a node has more edges than that (k_asm_visc then)
+  // k_asm_es (round 6): workgroup g assembles nodes [asmes_wg[2g], asmes_wg[2g+2]), whose adjacency entries (from
+  // asmes_wg[2g+1] = adj_ptr of its first node) fit its rx_asmes_teams(nVar) edge-side teams; asmes_side [2E][4] per
+  // adjacency entry {edge | side << 31, n0, n1, BSR block of the neighbour row's entry}; null when a node has more
+  // edges than teams (k_asm_visc then)
   int32_t* asmes_wg = nullptr;
+  int32_t* asmes_side = nullptr;
   int asmes_nwg = 0;
   int32_t* nbr_ptr = nullptr;   // [N+1] LSQ neighbours in the reference order
   int32_t* nbr = nullptr;

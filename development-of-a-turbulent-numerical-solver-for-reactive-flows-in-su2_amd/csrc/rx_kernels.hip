@@ -1288,8 +1288,8 @@ __host__ __device__ constexpr int asmes_teams(int nVar) { return RX_ASMES_WAVES 
 __host__ __device__ constexpr int asmes_out(int nVar) { return 2 * nVar + 2; }  // parked doubles per lane
 template <int NS, int NDIM>
 __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
-    const int32_t* __restrict__ wg_node, const int32_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj,
-    const int32_t* __restrict__ edges, const int64_t* __restrict__ edge_blk, const int64_t* __restrict__ diag,
+    const int2* __restrict__ wg_plan, const int4* __restrict__ side_rec, const int32_t* __restrict__ adj_ptr,
+    const int64_t* __restrict__ diag,
     const double* __restrict__ Fc, const double* __restrict__ Fv, const double* __restrict__ Jc,
     const double* __restrict__ dTdU, const double* __restrict__ Summ, const double* __restrict__ Js,
     const double* __restrict__ Rsrc, DevMech m, ViscParams P, double* __restrict__ R, double* __restrict__ A, int src,
@@ -1304,15 +1304,15 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
   const bool live = tw < TPW;  // lanes past the wavefront's last whole team take no part
   const int team = wv * TPW + (live ? tw : 0), b = live ? lane - tw * nVar : 0, sbase = tw * nVar;
   const int g = xcd_block(blockIdx.x, gridDim.x);
-  const int n_lo = wg_node[g], n_hi = wg_node[g + 1];
-  const int kb = adj_ptr[n_lo], ke = adj_ptr[n_hi];
+  const int2 w0 = wg_plan[g], w1 = wg_plan[g + 1];  // {first node, its first adjacency entry}
+  const int n_lo = w0.x, n_hi = w1.x, kb = w0.y, ke = w1.y;
   double* slot = ssm + team * TS;
   const bool fused = RX_ASMV_FUSE && cv.V != nullptr;
   // ---- phase A: edge side kb + team
   if (live && kb + team < ke) {
-    const int ad = adj[kb + team];
-    const int e = ad >> 1, side = ad & 1;
-    const int n0 = edges[2 * e], n1 = edges[2 * e + 1];
+    const int4 sr = side_rec[kb + team];  // {edge | side << 31, n0, n1, BSR block of the neighbour row's entry}
+    const int e = sr.x & 0x7fffffff, side = (int)((unsigned)sr.x >> 31);
+    const int n0 = sr.y, n1 = sr.z;
     const double* tile = Summ + (size_t)(e / kSummTile) * SS * kSummTile + e % kSummTile;
     double fc, jd[nVar];
     double sob, fv;
@@ -1336,7 +1336,7 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
       for (int d = 0; d < NDIM; ++d) nrm[d] = cv.normal[(size_t)e * NDIM + d];
       sob = dTdU[(size_t)(side ? n1 : n0) * nVar + b];
       fv = Fv[(size_t)e * nVar + b];
-      Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
+      Ao = A + (int64_t)sr.w * nVar2;
       __builtin_amdgcn_sched_barrier(0);
       constexpr int kSR = (SS + nVar - 1) / nVar;
       double sreg[kSR];
@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
       for (int q = b; q < SS; q += nVar) slot[q] = RX_ASMES_PROBE == 1 ? 0.25 + q : tile[(size_t)q * kSummTile];
       sob = dTdU[(size_t)(side ? n1 : n0) * nVar + b];  // the own node's dT/dU
       fv = Fv[(size_t)e * nVar + b];
-      Ao = A + edge_blk[2 * e + (side ? 0 : 1)] * nVar2;
+      Ao = A + (int64_t)sr.w * nVar2;
     if (RX_ASMES_PROBE == 3 || RX_ASMES_PROBE == 5) {
       const double* Vsi = cv.V + (size_t)n0 * nPV;
       fc = Vsi[b];
@@ -1474,11 +1474,32 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
     o[nVar] = side ? -fc : fc;
     o[2 * nVar + 1] = side ? fv : -fv;
   }
-  __syncthreads();
-  // ---- phase B: node n_lo + team
+  // ---- phase B: node n_lo + team. Its loads are issued before the barrier (phase A's registers are dead here), so
+  // they are in flight while the other teams finish
   const int i = n_lo + team;
-  if (!live || i >= n_hi) return;
-  const int k0 = adj_ptr[i], k1 = adj_ptr[i + 1];
+  const bool node = live && i < n_hi;
+  int k0 = 0, k1 = 0, fold = 0;
+  double rs = 0.0, js[NS], delta = 0.0;
+  int64_t dblk = 0;
+  if (node) {
+    k0 = adj_ptr[i];
+    k1 = adj_ptr[i + 1];
+    dblk = diag[i];
+    if (src) {
+      rs = Rsrc[(size_t)i * nVar + b];
+#pragma unroll
+      for (int a = 0; a < NS; ++a)
+        js[a] = Js[(size_t)(i / kSrcTile) * nsv * kSrcTile + (size_t)(a * nVar + b) * kSrcTile + i % kSrcTile];
+    }
+    if (fd.vol && i < fd.Nd && !fd.skip[i]) {
+      // ImplicitEuler_Iteration's AddVal2Diag (k_build_system_elem's operations on this lane's column)
+      const double dt = fd.dt[i];
+      fold = dt > rx::kEPS ? 1 : 2;
+      if (fold == 1) delta = fd.vol[i] / dt;
+    }
+  }
+  __syncthreads();
+  if (!node) return;
   double r = 0.0, D[nVar];
 #pragma unroll
   for (int a = 0; a < nVar; ++a) D[a] = 0.0;
@@ -1495,29 +1516,21 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
     for (int a = 0; a < nVar; ++a) D[a] += o[nVar + 1 + a];
   }
   if (src) {
-    r += Rsrc[(size_t)i * nVar + b];
+    r += rs;
 #pragma unroll
-    for (int a = 0; a < nVar; ++a) {
-      const double js = a >= rhos ? Js[(size_t)(i / kSrcTile) * nsv * kSrcTile +
-                                       (size_t)((a - rhos) * nVar + b) * kSrcTile + i % kSrcTile]
-                                  : 0.0;
-      D[a] += js;
-    }
+    for (int a = 0; a < nVar; ++a) D[a] += a >= rhos ? js[a - rhos] : 0.0;
   }
-  if (fd.vol && i < fd.Nd && !fd.skip[i]) {
-    if (fd.dt[i] > rx::kEPS) {
-      const double delta = fd.vol[i] / fd.dt[i];
+  if (fold == 1) {
 #pragma unroll
-      for (int a = 0; a < nVar; ++a)
-        if (a == b) D[a] += delta;
-    } else {
+    for (int a = 0; a < nVar; ++a)
+      if (a == b) D[a] += delta;
+  } else if (fold == 2) {
 #pragma unroll
-      for (int a = 0; a < nVar; ++a) D[a] = (a == b) ? 1.0 : 0.0;
-      r = 0.0;
-    }
+    for (int a = 0; a < nVar; ++a) D[a] = (a == b) ? 1.0 : 0.0;
+    r = 0.0;
   }
   R[(size_t)i * nVar + b] = r;
-  double* Ad = A + diag[i] * nVar2 + b;
+  double* Ad = A + dblk * nVar2 + b;
 #pragma unroll
   for (int a = 0; a < nVar; ++a) Ad[a * nVar] = D[a];
 }
@@ -2066,7 +2079,8 @@ int RX_NSFN(rx_launch_asm_visc)(rx_ctx* ctx, int with_src, int fused_conv) {
   }();
   if (es && !RX_ASMV_PARK && ctx->asmes_wg && ctx->asmes_nwg > 0) {
     RX_DNS_SWITCH(ctx->nDim, ctx->ns, (k_asm_es<NS_, ND_><<<ctx->asmes_nwg, RX_ASMES_WAVES * 64, 0, ctx->stream>>>(
-                              ctx->asmes_wg, ctx->adj_ptr, ctx->adj, ctx->edges, ctx->edge_blk, ctx->diag, ctx->fconv,
+                              reinterpret_cast<const int2*>(ctx->asmes_wg),
+                              reinterpret_cast<const int4*>(ctx->asmes_side), ctx->adj_ptr, ctx->diag, ctx->fconv,
                               ctx->fvisc, ctx->jconv, ctx->f[RX_F_DTDU], ctx->vsumm, ctx->jsrc, ctx->rsrc, ctx->mech, P,
                               ctx->f[RX_F_RES], ctx->f[RX_F_JAC], with_src, cv, fd)));
     RX_HIP(hipGetLastError());
