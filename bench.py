@@ -85,27 +85,32 @@ def pmc_fp64_flop(kernel, workload_key):
 
 
 def ring_groups():
-    """Wave groups per ring-sweep workgroup (rx_ilu_ring_groups in rx_sweeps.hip: env RX_ILU_RING_G, default 2)."""
-    return 1 if os.environ.get("RX_ILU_RING_G", "").strip() == "1" else 2
+    """Wave groups per ring-sweep workgroup (rx_ilu_ring_groups in rx_sweeps.hip: env RX_ILU_RING_G in 1 / 2 / 4 / 8,
+    default 2)."""
+    v = os.environ.get("RX_ILU_RING_G", "").strip()
+    return int(v) if v in ("1", "4", "8") else 2
 
 
 def ilu_apply_kernels(N, nnzb, nVar, parts, nDim=2):
-    """The ILU(0) apply kernels rx_la_ilu_apply launches for this partitioning (rx_sweeps.hip): the LDS-resident
-    sweep when a partition's vector, metadata and columns fit the 160 KiB LDS, else the wide global sweeps."""
+    """The ILU(0) apply kernel rx_la_ilu_apply launches for this partitioning (rx_sweeps.hip), in its order: the LDS-ring
+    sweeps (round 5; since round 6 also where a partition fits the LDS-resident sweep, unless RX_RING_FIRST=0), the
+    LDS-resident sweep when a partition's vector, metadata and columns fit the 160 KiB LDS, else the wide global
+    sweeps."""
     rows = -(-N // parts)
     shm = 8 * (rows * nVar + (256 // nVar) * nVar + 1) + 4 * (8 * rows + rows * nnzb // max(N, 1))
-    if shm <= 160 * 1024:
+    ring = nVar >= 5 and not (os.environ.get("RX_ILU_NO_RING") or os.environ.get("RX_NARROW_APPLY"))
+    ring_first = os.environ.get("RX_RING_FIRST", "1") != "0"
+    if shm <= 160 * 1024 and not (ring and ring_first):
         return f"k_ilu_apply_lds<{nVar}>"
-    if os.environ.get("RX_ILU_SPLIT"):
-        return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
-    if nVar >= 5 and not (os.environ.get("RX_ILU_NO_RING") or os.environ.get("RX_NARROW_APPLY")):
-        # round 5: both sweeps with the x rows in an LDS ring (when every level has at most 16 * (64 // nVar) rows,
-        # as on the C3 / C5 partitions: rocprof shows it there, profiles/r05_c3_kernel_stats.md)
+    if ring:
+        # every level has at most 16 * (64 // nVar) rows on the jet partitions (C3 / C5 / a C4 rank: rocprof shows it)
         # template <NV, threads, factor blocks of a row in registers, wave groups>: 3-D rows (up to 7 blocks) take
         # 768 threads with three blocks in registers (rx_ilu_ring_tb; RX_RING_3D=0: the 2-D shape)
         if nDim == 3 and os.environ.get("RX_RING_3D", "1") != "0":
-            return f"k_ilu_apply_ring<{nVar}, 768, 3, {ring_groups()}>"
+            return f"k_ilu_apply_ring<{nVar}, 768, 3, {min(ring_groups(), 2)}>"
         return f"k_ilu_apply_ring<{nVar}, 1024, 2, {ring_groups()}>"
+    if os.environ.get("RX_ILU_SPLIT"):
+        return f"k_ilu_fwd_wide<{nVar}, 1024>+k_ilu_bwd_wide<{nVar}, 1024>"
     return f"k_ilu_apply_wide<{nVar}, 1024>"  # both sweeps of a partition in one launch (round 4)
 
 

@@ -1281,7 +1281,8 @@ __global__ __launch_bounds__(kBlock) RX_WPE_ASMV void k_asm_visc(
 #endif
 #ifndef RX_ASMES_PROBE
 // build knob (tools/asm_probe.py, timing only, results wrong): 1 = no summary gather (constant records), 2 = no viscous
-// column, 3 = no AUSM evaluation, 4 = no phase-B sums, 5 = neither column
+// column, 3 = no AUSM evaluation, 4 = no phase-B sums, 5 = neither column, 6 = no off-diagonal stores, 7 = no source
+// loads in phase B
 #define RX_ASMES_PROBE 0
 #endif
 __host__ __device__ constexpr int asmes_teams(int nVar) { return RX_ASMES_WAVES * (64 / nVar); }
@@ -1341,7 +1342,8 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
       constexpr int kSR = (SS + nVar - 1) / nVar;
       double sreg[kSR];
 #pragma unroll
-      for (int q = 0; q < kSR; ++q) sreg[q] = b + q * nVar < SS ? tile[(size_t)(b + q * nVar) * kSummTile] : 0.0;
+      for (int q = 0; q < kSR; ++q)
+        sreg[q] = RX_ASMES_PROBE == 1 ? 0.25 + q : b + q * nVar < SS ? tile[(size_t)(b + q * nVar) * kSummTile] : 0.0;
       __builtin_amdgcn_sched_barrier(0);
       double* vs = slot + SS;  // V_i, V_j, dP/dU_i, dP/dU_j
       vs[b] = gvi;
@@ -1460,7 +1462,7 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
     } else {
       visc_jac_column_own<NS, NDIM>(m, P, SummCRef{slot, 1}, sob, side, b, b, sbase, [&](int rr, double v) {
         jv[rr] = v;
-        Ao[rr * nVar + b] = side ? jco[rr] - v : jco[rr] + v;
+        if (RX_ASMES_PROBE != 6) Ao[rr * nVar + b] = side ? jco[rr] - v : jco[rr] + v;
       });
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1485,7 +1487,7 @@ __global__ __launch_bounds__(RX_ASMES_WAVES * 64) RX_WPE_ASMES void k_asm_es(
     k0 = adj_ptr[i];
     k1 = adj_ptr[i + 1];
     dblk = diag[i];
-    if (src) {
+    if (src && RX_ASMES_PROBE != 7) {
       rs = Rsrc[(size_t)i * nVar + b];
 #pragma unroll
       for (int a = 0; a < NS; ++a)

@@ -2450,8 +2450,13 @@ int rx_ilu_ring_tb(const rx_ctx* ctx) {
   static const bool off = getenv("RX_RING_3D") && getenv("RX_RING_3D")[0] == '0';
   return ctx->nDim == 3 && !off ? 768 : 1024;
 }
-int rx_ilu_ring_groups() {  // RX_ILU_RING_G=1: every wavefront at every level (the first ring kernel, A/B)
-  static const int g = getenv("RX_ILU_RING_G") && atoi(getenv("RX_ILU_RING_G")) == 1 ? 1 : 2;
+// RX_ILU_RING_G=1: every wavefront at every level (the first ring kernel, A/B); 4 / 8 (round 6, the 1 024-thread shape):
+// more groups, each a level's loads further ahead, for the small partitions of a C4 rank (levels of ~10-25 rows)
+int rx_ilu_ring_groups() {
+  static const int g = [] {
+    const int v = getenv("RX_ILU_RING_G") ? atoi(getenv("RX_ILU_RING_G")) : 2;
+    return v == 1 || v == 4 || v == 8 ? v : 2;
+  }();
   return g;
 }
 int rx_ilu_max_waves() { return RX_ILU_MAX_WAVES; }
@@ -2473,6 +2478,10 @@ int rx_la_prepare(rx_ctx* ctx) {
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 768, 3, 1>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 768, 3, 2>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2, 4>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2, 8>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     }
     if constexpr (NV_ >= 5)
@@ -2580,6 +2589,16 @@ static bool ilu2_apply_wave(const rx_ctx* ctx) {
   return ctx->nVar == 2 && !old && (size_t)ctx->maxpart * 2 * sizeof(double) <= (size_t)ctx->lds_max;
 }
 
+// whether the ring sweeps take precedence over the LDS-resident apply where both fit (round 6: yes; RX_RING_FIRST=0
+// restores the LDS-resident apply there). At a C4 rank's 490-row partitions (tools/c4_rank_floor.py, gpurun_out r06h,
+// one box) SOLVE 2.28 -> 1.80 ms per step: the LDS-resident apply loads a level's factor blocks one level ahead from
+// 256 threads, the ring two levels ahead per wavefront group from 1 024
+bool rx_ilu_ring_first(const rx_ctx* ctx) {
+  (void)ctx;
+  static const bool on = !(getenv("RX_RING_FIRST") && getenv("RX_RING_FIRST")[0] == '0');
+  return on;
+}
+
 int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const int* conv) {
   const int nv = ctx->nVar;
   if (ilu2_apply_wave(ctx)) {
@@ -2593,7 +2612,7 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
   const size_t shm = sizeof(double) * ((size_t)ctx->maxpart * nv + (size_t)(256 / nv) * nv + 1) +
                      sizeof(int32_t) * (8 * (size_t)ctx->maxpart + (size_t)ctx->maxpart_nnzb);
   static const bool no_lds = getenv("RX_NO_LDS_APPLY") != nullptr;  // diagnosis: force the global sweeps
-  if (shm <= (size_t)ctx->lds_max && !no_lds) {
+  if (shm <= (size_t)ctx->lds_max && !no_lds && !rx_ilu_ring_first(ctx)) {
     RX_NV_SWITCH(nv, (k_ilu_apply_lds<NV_, false><<<ctx->npart, 256, shm, ctx->stream>>>(
                          ctx->part_ptr, ctx->rp, ctx->fs.part_lvl, ctx->fs.lvl_ptr,
                          reinterpret_cast<const int4*>(ctx->fs.slot), ctx->bs.part_lvl, ctx->bs.lvl_ptr,
@@ -2647,6 +2666,10 @@ int rx_la_ilu_apply(rx_ctx* ctx, const double* b, double* x, int* done, const in
       }
     } else if (g == 1) {
       RX_RING_LAUNCH(1024, 2, 1);
+    } else if (g == 4) {
+      RX_RING_LAUNCH(1024, 2, 4);
+    } else if (g == 8) {
+      RX_RING_LAUNCH(1024, 2, 8);
     } else {
       RX_RING_LAUNCH(1024, 2, 2);
     }

@@ -8,15 +8,18 @@ import bench  # noqa: E402
 
 
 def test_ilu_apply_kernel_names(monkeypatch):
-    for v in ("RX_ILU_SPLIT", "RX_ILU_NO_RING", "RX_NARROW_APPLY"):
+    for v in ("RX_ILU_SPLIT", "RX_ILU_NO_RING", "RX_NARROW_APPLY", "RX_RING_FIRST", "RX_ILU_RING_G"):
         monkeypatch.delenv(v, raising=False)
     # C3: 1M points, 256 partitions of 3 906 rows -> the vector does not fit LDS: the LDS-ring sweeps (round 5)
     assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_ring<11, 1024, 2, 2>"
     # C5 (3-D, 200x100x100 in 256 partitions): the 3-D ring shape
     assert bench.ilu_apply_kernels(2_000_000, 13_880_000, 12, 256, nDim=3) == "k_ilu_apply_ring<12, 768, 3, 2>"
+    # C4's share per GPU at 2048 partitions: 488-row partitions fit LDS, but the ring sweeps come first (round 6)
+    assert bench.ilu_apply_kernels(125_000, 624_000, 11, 256) == "k_ilu_apply_ring<11, 1024, 2, 2>"
+    monkeypatch.setenv("RX_RING_FIRST", "0")
+    assert bench.ilu_apply_kernels(125_000, 624_000, 11, 256) == "k_ilu_apply_lds<11>"
     monkeypatch.setenv("RX_ILU_NO_RING", "1")  # the fused wide sweeps (round 4)
     assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_apply_wide<11, 1024>"
-    # C4's share per GPU at 2048 partitions: 488-row partitions fit LDS
     assert bench.ilu_apply_kernels(125_000, 624_000, 11, 256) == "k_ilu_apply_lds<11>"
     monkeypatch.setenv("RX_ILU_SPLIT", "1")
     assert bench.ilu_apply_kernels(1_000_000, 4_995_000, 11, 256) == "k_ilu_fwd_wide<11, 1024>+k_ilu_bwd_wide<11, 1024>"

@@ -1,6 +1,6 @@
 """BASELINE configs[3] (C4): the 1M-point C3 jet (2000 x 500, 7 species, PaSR + SST) decomposed over 8 ranks exactly
 as `bench.py --gpus 8` builds it (strong scaling: 256 partitions per rank = 2048 in all, ~490 rows each, so the ILU(0)
-apply is the LDS-resident k_ilu_apply_lds; 125 000 owned points per rank, one halo layer; meshgen.shard). The 8 ranks share the test box's one MI355X through the host-staged transport over gloo
+apply is the ring sweep k_ilu_apply_ring since round 6 — the LDS-resident k_ilu_apply_lds before; 125 000 owned points per rank, one halo layer; meshgen.shard). The 8 ranks share the test box's one MI355X through the host-staged transport over gloo
 (tests/shard_run.py; RCCL refuses two ranks on one device and runs the same exchange plan and rank-ordered
 all-reduce). Reference: CMeanFlowIteration::Iterate (iteration_structure.cpp:486-560) on 8 MPI ranks of a
 partitioned CGeometry (geometry_structure.cpp:11465-11530).
@@ -57,11 +57,11 @@ def test_c4_implicit_vs_oracle(tmp_path):
     _, state, _, _ = outer_iteration_inputs(mesh, st, cfg, bc)
     shards = write_shards(tmp_path, mesh, st0, mech, kw, WORLD, tg=state["TG"])
     assert [sh["n_domain"] for sh in shards] == [NX * NY // WORLD] * WORLD
-    import bench  # the ILU(0) apply the 8-GPU bench line times at this decomposition: the LDS-resident sweep
+    import bench  # the ILU(0) apply the 8-GPU bench line times at this decomposition: the ring sweeps (round 6)
     for sh in shards:
         assert sh["n_part"] == PARTS // WORLD
         assert bench.ilu_apply_kernels(sh["n_point"], sh["n_point"] + 2 * sh["n_edge"], NS + 4,
-                                       sh["n_part"]).startswith("k_ilu_apply_lds")
+                                       sh["n_part"]).startswith("k_ilu_apply_ring")
     res = run_ranks(tmp_path, WORLD, 1, 1, rx.BENCH_CFL)
     U, T, pre = gather(res, len(st["V"]), st["U"].shape[1])
     check_preprocessing(pre, st, "C4 implicit")

@@ -67,12 +67,23 @@ def main():
     prof = {k: s.profile_read(k) for k in rx.K}
     tprof = {k: t.profile_read(k) for k in rx.K}
     phases = {k: round((prof[k][0] + tprof[k][0]) / a.steps, 4) for k in rx.K if prof[k][1] + tprof[k][1] > 0}
+    s.profile(False)
+    t.profile(False)
+    # the SOLVE phase's kernels per launch (as bench.py: one more step with the solve launched eagerly, flow context)
+    os.environ["RX_NO_GRAPH"] = "1"
+    s.profile(True)
+    step()
+    s.sync()
+    in_solve = {k: round(s.profile_read(k)[0] / max(1, s.profile_read(k)[1]) * 1e3, 1) for k in ("SPMV", "ILU_APPLY")}
+    s.profile(False)
+    os.environ.pop("RX_NO_GRAPH")
     nd = int(sh["n_domain"])
     out = dict(what="C4 rank floor (no communicator: exchanges and all-reduces skipped)", rank=a.rank,
                world=a.world, parts_per_rank=a.parts, owned_points=nd, halo_points=len(sh["l2g"]) - nd,
                neighbours=[int(x) for x in sh["neigh"]], send_points=int(len(sh["send_idx"])),
                ms_per_step=round(el / a.steps * 1e3, 3), mcells_iters_per_s_owned=round(nd * a.steps / el / 1e6, 3),
-               lin_iters=[list(map(int, x)) for x in its[-a.steps:]][:3], phase_ms_per_step=phases)
+               lin_iters=[list(map(int, x)) for x in its[-a.steps:]][:3], phase_ms_per_step=phases,
+               in_solve_us_per_launch=in_solve)
     s.close()
     print(json.dumps(out), flush=True)
 
