@@ -267,6 +267,45 @@ def case_mini9(nx=21, ny=11):
     return a
 
 
+def case_rank9(split=None):
+    """One MPI rank of mini9's implicit system: the reference's own CSysMatrix with domain points
+    [0, P) and halo [P, N) (harness RX_RANK_SPLIT = P), its BuildILUPreconditioner / ComputeILUPreconditioner /
+    ComputeLU_SGSPreconditioner on the system's blocks. The LU-SGS halo preset (halo_x.bin) is the forward-sweep
+    result x* of the other rank, rows [P, N) as their own partition: the oracle's orc_lusgs_fwd_p, the restatement of
+    that rank's (D+L) x* = b — what its SendReceive_Solution hands over. The golden holds the system, P, the preset and
+    the reference's rank-0 outputs (rows [0, P)); tests/test_oracle_golden.py checks the oracle's partitioned
+    ILU build / apply / LU-SGS (struct Parts, part_ptr = [0, P, N]) against them, tests/test_gpu_partitions.py the
+    device's."""
+    oracle = _load("rx_oracle_py", os.path.join(HERE, "oracle.py"))
+    pts, quads, U, writer = mini9_inputs()
+    wd = make_workdir("rank9", writer, cfl=5.0, order="1ST_ORDER", prec="ILU0")
+    write_state(wd, U)
+    a = run_harness(wd, bsr=True)
+    rp, col, A, b = a["bsr_row_ptr"], a["bsr_col"], a["bsr_system"], a["sys_rhs"]
+    N = len(rp) - 1
+    P = split or N // 2
+    xs = oracle.lusgs_forward(rp, col, A, b.ravel(), part_ptr=np.array([0, P, N]))
+    np.ascontiguousarray(xs, dtype="<f8").tofile(os.path.join(wd, "halo_x.bin"))
+    env = dict(os.environ, RX_RANK_SPLIT=str(P))
+    exe = os.path.join(HERE, "_ref", "harness")
+    r = subprocess.run([exe, "case.cfg", "state.txt", "out", "--bsr"], cwd=wd, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout[-4000:] + r.stderr[-4000:])
+        raise SystemExit("harness (RX_RANK_SPLIT) failed")
+    out = {}
+    with open(os.path.join(wd, "out", "manifest.txt")) as f:
+        for line in f:
+            t = line.split()
+            out[t[0]] = np.fromfile(os.path.join(wd, "out", t[0] + ".bin"), dtype="<" + t[1]).reshape(
+                tuple(int(q) for q in t[2:]))
+    assert np.array_equal(out["bsr_system"], A)
+    g = {k: a[k] for k in ("dims", "bsr_row_ptr", "bsr_col", "bsr_system", "sys_rhs")}
+    g.update(rank_split=np.array([P]), rank_halo_x=xs, rank_ilu_factor=out["rank_ilu_factor"],
+             rank_ilu_rhs=out["rank_ilu_rhs"], rank_lusgs_rhs=out["rank_lusgs_rhs"])
+    return g  # the mesh and state are mini9's (the same inputs; the tests use tests/golden/mini9.npz for them)
+
+
 def mini9_inputs(nx=21, ny=11):
     pts, quads, bnd = meshgen.jet_mesh(nx, ny)
     xy, cons = read_plot(os.path.join(CASE_DIR, "PLOT/flow_second_chem.dat"))
@@ -922,7 +961,7 @@ def main():
              "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
              "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d, "fpit2": case_fpit2,
              "fpit2l": lambda: case_fpit2(limiter=True), "it4t": case_it4t,
-             "it4tl": lambda: case_it4t(limiter=True),
+             "it4tl": lambda: case_it4t(limiter=True), "rank9": case_rank9,
              **{k: (lambda k=k: case_lin(k)) for k in LIN_CASES},
              **{f"it{n}s": (lambda n=n: case_itns(n)) for n in (5, 6, 8)}}[case]()
         path = os.path.join(gold, case + ".npz")

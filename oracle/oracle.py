@@ -277,6 +277,16 @@ def lusgs(rp, col, A, b, part_ptr=None):
 
 
 @_keepalive
+def lusgs_forward(rp, col, A, b, part_ptr=None):
+    """The forward sweep of the LU-SGS apply alone, x* per rank ((D+L) x* = b, matrix_structure.cpp:1678-1685)."""
+    N, nb = len(rp) - 1, A.shape[1]
+    x = np.zeros(N * nb)
+    lib().orc_lusgs_fwd_p(C.c_int64(N), C.c_int(nb), _p(rp, np.int64), _p(col, np.int64), _p(A), _p(b),
+                          x.ctypes.data_as(C.c_void_p), *_parts(N, part_ptr))
+    return x.reshape(N, nb)
+
+
+@_keepalive
 def ilu_build(rp, col, A, part_ptr=None):
     N, nb = len(rp) - 1, A.shape[1]
     F = np.empty_like(np.ascontiguousarray(A))  # orc_ilu_build_p copies A first

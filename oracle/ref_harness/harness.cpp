@@ -840,6 +840,52 @@ int main(int argc, char** argv) {
       std::vector<double> info = {(double)it2, resid, tol, (double)m};
       dumpd("fgmres_ilu_info", info, {4});
       }
+      // ---- one MPI rank of the same system. RX_RANK_SPLIT=P: a CSysMatrix whose domain is the
+      // points [0, P) and whose halo is [P, nPoint) — the reference's own per-rank layout, domain points first with
+      // the halo columns present (CSysMatrix::Initialize with nPointDomain = P, matrix_structure.cpp:113-201) —
+      // holding the same blocks; then the reference's BuildILUPreconditioner (:1368-1451, needs the ILU0 cfg: the
+      // ILU matrix is allocated for it, :236-247), ComputeILUPreconditioner (:1453-1515) and
+      // ComputeLU_SGSPreconditioner (:1673-1709) on it. The LU-SGS product's halo entries are preset from
+      // halo_x.bin: what the neighbour ranks' forward sweeps would deliver through SendReceive_Solution (:1687), a
+      // no-op on this serial mesh (no SEND_RECEIVE marker, :794-880), which therefore leaves the preset in place.
+      if (const char* sp = std::getenv("RX_RANK_SPLIT")) {
+        const unsigned long P = std::strtoul(sp, nullptr, 10);
+        CSysMatrix Rk;
+        Rk.Initialize(nPoint, P, nVar, nVar, true, geo, cfg);
+        for (unsigned long i = 0; i < nPoint; ++i)
+          for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) Rk.SetBlock(i, col[k], A.GetBlock(i, col[k]));
+        std::vector<double> zz(P * nVar);
+        if (cfg->GetKind_Linear_Solver_Prec() == ILU) {
+          Rk.BuildILUPreconditioner();
+          std::vector<double> f((size_t)row_ptr[P] * nVar * nVar);
+          for (unsigned long i = 0; i < P; ++i)
+            for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+              su2double* bb = Rk.GetBlock_ILUMatrix(i, col[k]);
+              for (int q = 0; q < nVar * nVar; ++q) f[k * nVar * nVar + q] = bb[q];
+            }
+          dumpd("rank_ilu_factor", f, {(long)row_ptr[P], nVar, nVar});
+          CSysVector zr(nPoint, P, nVar, 0.0);
+          Rk.ComputeILUPreconditioner(rhs, zr, geo, cfg);
+          for (unsigned long q = 0; q < P * nVar; ++q) zz[q] = zr[q];
+          dumpd("rank_ilu_rhs", zz, {(long)P, nVar});
+        }
+        std::vector<double> hx(nPoint * nVar, 0.0);
+        {
+          FILE* hf = std::fopen("halo_x.bin", "rb");
+          if (!hf || std::fread(hx.data(), sizeof(double), hx.size(), hf) != hx.size()) {
+            std::fprintf(stderr, "RX_RANK_SPLIT needs halo_x.bin (%lu x %d doubles)\n", nPoint, nVar);
+            std::exit(4);
+          }
+          std::fclose(hf);
+        }
+        CSysVector zl(nPoint, P, nVar, 0.0);
+        for (unsigned long q = P * nVar; q < nPoint * nVar; ++q) zl[q] = hx[q];
+        Rk.ComputeLU_SGSPreconditioner(rhs, zl, geo, cfg);
+        for (unsigned long q = 0; q < P * nVar; ++q) zz[q] = zl[q];
+        dumpd("rank_lusgs_rhs", zz, {(long)P, nVar});
+        std::vector<double> ps = {(double)P};
+        dumpd("rank_split", ps, {1});
+      }
     }
     // ---- SST loops and the turbulent implicit step (CTurbSSTSolver::Preprocessing :2923-2946,
     //      CTurbSolver::Upwind/Viscous_Residual :429-600, Source_Residual :3018-3080,

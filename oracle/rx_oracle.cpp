@@ -1773,6 +1773,31 @@ void orc_lusgs_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const
   }
 }
 
+// The forward half of orc_lusgs_p alone: x* of every rank, (D+L) x* = b (:1678-1685) — the values a rank's
+// SendReceive_Solution hands its neighbours between the sweeps (:1687). Test infrastructure: the halo preset of the
+// reference's own one-rank LU-SGS (oracle/make_golden.py case_rank9).
+void orc_lusgs_fwd_p(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* b,
+                     double* x, int64_t np, const int64_t* part_ptr) {
+  const std::vector<int64_t> B = part_bounds(N, np, part_ptr);
+  std::vector<double> aux(nb), prv(nb);
+  for (int64_t p = 0; p + 1 < (int64_t)B.size(); ++p)
+    for (int64_t i = B[p]; i < B[p + 1]; ++i) {
+      for (int a = 0; a < nb; ++a) prv[a] = 0.0;
+      for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+        if (col[k] < i && col[k] >= B[p]) {
+          const double* blk = A + k * nb * nb;
+          for (int a = 0; a < nb; ++a) {
+            double pb = 0.0;
+            for (int c = 0; c < nb; ++c) pb += blk[a * nb + c] * x[col[k] * nb + c];
+            prv[a] += pb;
+          }
+        }
+      for (int a = 0; a < nb; ++a) aux[a] = b[i * nb + a] - prv[a];
+      gauss_elim(nb, A + find_diag(rp, col, i) * nb * nb, aux.data());
+      for (int a = 0; a < nb; ++a) x[i * nb + a] = aux[a];
+    }
+}
+
 void orc_lusgs(int64_t N, int nb, const int64_t* rp, const int64_t* col, const double* A, const double* b,
                double* x) {
   orc_lusgs_p(N, nb, rp, col, A, b, x, 1, nullptr);

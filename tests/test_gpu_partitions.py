@@ -187,3 +187,51 @@ def test_ilu_factor_3d_vs_oracle(nx, ny, nz, n_part):
     assert_close(t.download("SOL"), O.ilu_apply(rp, col, F2, b2, part_ptr=pp).ravel(), rtol=0.0,
                  what=f"3-D SST ILU(0) apply nz={nz} P={n_part}")
     s.close()
+
+
+def test_rank_preconditioners_vs_reference_rank():
+    """the device's partition semantics against the reference's own one-rank computation (golden
+    rank9: the reference's CSysMatrix with domain [0, P) and halo columns [P, N), mini9's system; its ILU(0) factor,
+    ILU apply and LU-SGS apply with the halo preset to the other rank's forward sweep). The device runs mini9's mesh
+    cut into the partitions [0, P) and [P, N): rows [0, P) of its factor, ILU apply and LU-SGS apply equal the
+    reference's bitwise (the device's partition [P, N) computes the very forward result the preset holds)."""
+    import os
+
+    import tests.test_gpu_parity as tp
+    g = dict(np.load(os.path.join(tp.GOLD, "rank9.npz")))
+    m = tp.golden("mini9")
+    rp, col, A, b = g["bsr_row_ptr"], g["bsr_col"], g["bsr_system"], g["sys_rhs"].ravel()
+    N, P = len(rp) - 1, int(g["rank_split"][0])
+    nDim, nVar = int(m["dims"][0]), int(m["dims"][1])
+    mesh = {k: m[k] for k in ("edges", "edge_normal", "coord", "volume", "nbr_ptr", "nbr")}
+    mesh["bvertex"] = m.get("bvertex", np.zeros((0, 3), dtype=np.int64))
+    mesh["bvertex_normal"] = m.get("bvertex_normal", np.zeros((0, 2)))
+    mesh["part_ptr"] = np.array([0, P, N], dtype=np.int64)
+    kw = dict(mach_inf=float(m["mach_inf"][0]), prandtl_turb=float(m["visc_params"][1]),
+              lewis_turb=float(m["visc_params"][2]), c_mu=float(m["src_params"][0]),
+              pasr_lb=float(m["src_params"][1]))
+    for prec in ("ilu", "lusgs"):
+        s = rx.ReactiveNSSolver(mesh, rx.Mechanism(m), rx.default_cfg(implicit=1, lin_prec=(1 if prec == "ilu" else 0),
+                                                                      **kw))
+        s.set_state(m)
+        grp, gcol = s.bsr_pattern()
+        assert np.array_equal(grp, rp) and np.array_equal(gcol, col)
+        s.Preprocessing_zero()
+        s.Upwind_Residual()
+        s.sync()
+        s.download("RES")  # the system counts as assembled; then the golden's system replaces it
+        s.upload("JAC", A)
+        s.upload("RHS", b)
+        if prec == "ilu":
+            s.ilu0_build()
+            s.sync()
+            F = s.download("ILU").reshape(-1, nVar, nVar)
+            assert np.array_equal(F[:rp[P]], g["rank_ilu_factor"]), "ILU(0) factor of the rank vs reference"
+            s.ilu0_apply("RHS", "SOL")
+            s.sync()
+            assert np.array_equal(s.download("SOL").reshape(N, nVar)[:P], g["rank_ilu_rhs"]), "ILU apply vs reference"
+        else:
+            s.lusgs_apply("RHS", "SOL")
+            s.sync()
+            assert np.array_equal(s.download("SOL").reshape(N, nVar)[:P], g["rank_lusgs_rhs"]), "LU-SGS vs reference"
+        s.close()

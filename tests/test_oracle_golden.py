@@ -195,3 +195,26 @@ def test_partitioned_ilu_is_block_jacobi():
     assert np.array_equal(O.ilu_apply(rp, col, Fp, b, part_ptr=pp), O.ilu_apply(rp, col, Fbd, b))
     # LU-SGS forward sweeps never see halo columns: with no halo at all both agree with the serial one
     assert np.array_equal(O.lusgs(rp, col, A, b, part_ptr=[0, N]), O.lusgs(rp, col, A, b))
+
+
+def test_partitioned_preconditioners_are_the_references_rank():
+    """the per-rank semantics of the restatement (struct Parts: ILU(0) skipping halo columns, LU-SGS's
+    backward sweep reading the neighbour's forward result x*) pinned by the reference's own code on one rank — golden
+    rank9 (oracle/make_golden.py case_rank9): a CSysMatrix with domain [0, P) and halo columns [P, N) holding mini9's
+    system, the reference's BuildILUPreconditioner / ComputeILUPreconditioner / ComputeLU_SGSPreconditioner on it
+    (matrix_structure.cpp:1368-1515, :1673-1709), the LU-SGS halo preset to the other rank's forward sweep. The
+    oracle on part_ptr = [0, P, N] matches rows [0, P) bitwise."""
+    g, _ = load("rank9")
+    m, _ = load("mini9")
+    rp, col, A, b = g["bsr_row_ptr"], g["bsr_col"], g["bsr_system"], g["sys_rhs"].ravel()
+    assert np.array_equal(A, m["bsr_system"]) and np.array_equal(col, m["bsr_col"])  # mini9's own system
+    N, P = len(rp) - 1, int(g["rank_split"][0])
+    pp = np.array([0, P, N])
+    F = O.ilu_build(rp, col, A, part_ptr=pp)
+    assert np.array_equal(F[:rp[P]], g["rank_ilu_factor"])
+    assert np.array_equal(O.ilu_apply(rp, col, F, b, part_ptr=pp)[:P], g["rank_ilu_rhs"])
+    assert np.array_equal(O.lusgs_forward(rp, col, A, b, part_ptr=pp)[P:], g["rank_halo_x"][P:])
+    assert np.array_equal(O.lusgs(rp, col, A, b, part_ptr=pp)[:P], g["rank_lusgs_rhs"])
+    # the rank is not the serial reference: the halo coupling changes both preconditioners near the cut
+    assert not np.array_equal(g["rank_ilu_rhs"], m["ilu_rhs"][:P])
+    assert not np.array_equal(g["rank_lusgs_rhs"], m["lusgs_rhs"][:P])
