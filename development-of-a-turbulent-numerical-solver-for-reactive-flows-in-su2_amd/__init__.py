@@ -861,7 +861,7 @@ def case_from_cfg(cfg_path):
                 free_stream=dict(rho=fs[0].value, mu=fs[1].value, T=fs[2].value, P=fs[3].value), case=case)
 
 
-def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=None, rk_alpha=None):
+def Iterate(flow: ReactiveNSSolver, turb, ext_iter=0, limiter=None, rk_alpha=None):
     """One reference outer iteration for REACTIVE_RANS on the device, in the reference's order
     (CMeanFlowIteration::Iterate iteration_structure.cpp:486-560; CMultiGridIntegration::MultiGrid_Iteration
     integration_time.cpp:40-140 with MGLEVEL = 0, whose MultiGrid_Cycle pre-smoothing sweep runs iRKLimit stages
@@ -870,7 +870,8 @@ def Iterate(flow: ReactiveNSSolver, turb: TurbSSTSolver, ext_iter=0, limiter=Non
     at stage 0, Space_Integration (loops + BCs), Time_Integration (integration_structure.cpp:325-335):
     ImplicitEuler_Iteration when the flow cfg is implicit, else ExplicitEuler_Iteration (EULER_EXPLICIT, rk_alpha
     None) or one ExplicitRK_Iteration per RK_ALPHA_COEFF entry (RUNGE-KUTTA_EXPLICIT). Then the flow
-    Preprocessing(Output = true) on the updated solution and the SST iteration. limiter None: from
+    Preprocessing(Output = true) on the updated solution and the SST iteration — or, turb None (a flow context with
+    cfg.rans = 0: REACTIVE_NAVIER_STOKES, KIND_TURB_MODEL= NONE), the flow's iteration alone. limiter None: from
     cfg.spatial_order == 2 (SECOND_ORDER_LIMITER, solver_direct_reactive.cpp:4739-4742). Nothing leaves the device
     except the RMS vectors and the linear-solver counts. Returns (rms_flow of the last stage, rms_turb, lin_iters)."""
     if limiter is None:
@@ -915,7 +916,11 @@ def _iterate_stages(flow, turb, ext_iter, limiter, implicit, stages):
             rms = flow.ExplicitEuler_Iteration()
         else:
             rms = flow.ExplicitRK_Iteration(k, alpha)
-    preprocess(True)
+    preprocess(True)  # MultiGrid_Iteration's closing Preprocessing(Output = true) (integration_time.cpp:124-126)
+    if turb is None:
+        # REACTIVE_NAVIER_STOKES without a turbulence model (KIND_TURB_MODEL= NONE, round 6): CMeanFlowIteration::
+        # Iterate runs the flow's MultiGrid_Iteration alone (iteration_structure.cpp:531-534), no SST iteration
+        return rms, None, (it, 0)
     turb.Preprocessing()
     turb.Upwind_Residual()
     turb.Viscous_Residual()

@@ -187,10 +187,12 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
     static const Need need[] = {
         // Kind_Solver (config_structure.cpp:622, default NO_SOLVER); REACTIVE_NAVIER_STOKES + a turbulence model
         // becomes REACTIVE_RANS (:2872-2874), the solver pair driver_structure.cpp:795-822 builds
-        {"PHYSICAL_PROBLEM", "", "REACTIVE_NAVIER_STOKES", "the outer iteration on this path is REACTIVE_RANS"},
-        // :626 (default NONE): SA would build CTurbSASolver (driver_structure.cpp:806-814), NONE a laminar
-        // CReactiveNSSolver without TURB_SOL; rx::Iterate / rx.Iterate always run the SST SingleGrid_Iteration
-        {"KIND_TURB_MODEL", "NONE", "SST", "only the Menter SST turbulence solver is built"},
+        {"PHYSICAL_PROBLEM", "", "REACTIVE_NAVIER_STOKES",
+         "the outer iteration on this path is REACTIVE_RANS (or laminar REACTIVE_NAVIER_STOKES)"},
+        // :626 (default NONE): SA would build CTurbSASolver (driver_structure.cpp:806-814); NONE (round 6) is the
+        // laminar CReactiveNSSolver without TURB_SOL (flow_cfg.rans = 0: rx::Iterate / rx.Iterate without an SST
+        // context run the flow's MultiGrid_Iteration alone, iteration_structure.cpp:531-534)
+        {"KIND_TURB_MODEL", "NONE", "", "SST (REACTIVE_RANS) or NONE (laminar REACTIVE_NAVIER_STOKES)"},
         // :1147 (default WEIGHTED_LEAST_SQUARES): both methods of Gradient_Map (option_structure.hpp:723-725) are
         // built: rx_grad_lsq / rx_grad_gg (SetPrimitive_Gradient_LS / _GG, solver_direct_reactive.cpp:4717) and the
         // SST's SetSolution_Gradient_LS / _GG (solver_direct_turbulent.cpp:2944, 2963)
@@ -211,6 +213,10 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
       if (std::string(n.key) == "NUM_METHOD_GRAD") {
         if (v == "WEIGHTED_LEAST_SQUARES" || v == "GREEN_GAUSS") continue;
         return fail(k, RX_ERR_UNSUPPORTED, "NUM_METHOD_GRAD= " + v + ": " + n.why);
+      }
+      if (std::string(n.key) == "KIND_TURB_MODEL") {
+        if (v == "SST" || v == "NONE") continue;
+        return fail(k, RX_ERR_UNSUPPORTED, "KIND_TURB_MODEL= " + v + ": " + n.why);
       }
       if (std::string(n.key) == "UNSTEADY_SIMULATION" && v == "STEADY") v = "NO";
       if (std::string(n.key) == "PHYSICAL_PROBLEM" && v == "REACTIVE_RANS") v = "REACTIVE_NAVIER_STOKES";

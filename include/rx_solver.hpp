@@ -27,7 +27,8 @@
  *   ImplicitEuler_Iteration       -> rx_sst_implicit_euler       (:615-728)
  *   Postprocessing                -> rx_sst_postprocessing       (:2953-3016)
  *   BC_Inlet / BC_Outlet / BC_Isothermal_Wall -> rx_bc_sst       (:3142-3450)
- * Iterate(flow, turb, ext_iter) is CMeanFlowIteration::Iterate for REACTIVE_RANS (iteration_structure.cpp:486-560).
+ * Iterate(flow, turb, ext_iter) is CMeanFlowIteration::Iterate for REACTIVE_RANS (iteration_structure.cpp:486-560);
+ * IterateFlow(flow, ext_iter) the laminar REACTIVE_NAVIER_STOKES one (no turbulence model, round 6).
  * A spline lookup outside the property tables throws std::out_of_range (MathTools::GetSpline,
  * Common/src/spline.cpp:62-77); any other failure throws std::runtime_error with rx_status_string.
  * Ownership: the solver owns one rx_ctx (device state); host arrays are copied at construction /
@@ -198,9 +199,27 @@ class TurbSSTSolver {
 // (RUNGE-KUTTA_EXPLICIT). SPATIAL_ORDER_FLOW = 2ND_ORDER_LIMITER (cfg.spatial_order == 2) adds
 // SetPrimitive_Limiter to the non-Output Preprocessing (solver_direct_reactive.cpp:4739-4742).
 // Returns the flow RMS (of the last stage); turb_rms gets the SST one.
+// The flow's MultiGrid_Iteration alone: laminar REACTIVE_NAVIER_STOKES (KIND_TURB_MODEL= NONE, a flow context with
+// cfg.rans = 0): CMeanFlowIteration::Iterate runs no turbulence iteration (iteration_structure.cpp:531-534).
+inline std::vector<double> IterateFlow(ReactiveNSSolver& flow, int ext_iter,
+                                       const std::vector<double>& rk_alpha = std::vector<double>());
+
 inline std::vector<double> Iterate(ReactiveNSSolver& flow, TurbSSTSolver& turb, int ext_iter,
                                    std::vector<double>* turb_rms = nullptr,
                                    const std::vector<double>& rk_alpha = std::vector<double>()) {
+  std::vector<double> rms = IterateFlow(flow, ext_iter, rk_alpha);
+  turb.Preprocessing();
+  turb.Upwind_Residual();
+  turb.Viscous_Residual();
+  turb.Source_Residual();
+  turb.BC_Apply();
+  std::vector<double> trms = turb.ImplicitEuler_Iteration();
+  turb.Postprocessing();
+  if (turb_rms) *turb_rms = trms;
+  return rms;
+}
+
+inline std::vector<double> IterateFlow(ReactiveNSSolver& flow, int ext_iter, const std::vector<double>& rk_alpha) {
   const rx_cfg& cfg = flow.config();
   auto preprocess = [&](bool output) {
     flow.SetPrimitive_Variables(ext_iter);
@@ -229,15 +248,7 @@ inline std::vector<double> Iterate(ReactiveNSSolver& flow, TurbSSTSolver& turb, 
     else if (rk_alpha.empty()) rms = flow.ExplicitEuler_Iteration();
     else rms = flow.ExplicitRK_Iteration((int)k, rk_alpha[k]);
   }
-  preprocess(true);  // Preprocessing(Output = true) on the updated solution
-  turb.Preprocessing();
-  turb.Upwind_Residual();
-  turb.Viscous_Residual();
-  turb.Source_Residual();
-  turb.BC_Apply();
-  std::vector<double> trms = turb.ImplicitEuler_Iteration();
-  turb.Postprocessing();
-  if (turb_rms) *turb_rms = trms;
+  preprocess(true);  // MultiGrid_Iteration's Preprocessing(Output = true) on the updated solution (:124-126)
   return rms;
 }
 

@@ -735,6 +735,18 @@ def case_itns(ns):
     return iteration_case(f"it{ns}s", writer, fold_species(U, ns), ns, 2, 1.0, "ILU0", "EULER_IMPLICIT")
 
 
+def case_lam4():
+    """The laminar REACTIVE_NAVIER_STOKES outer iteration (KIND_TURB_MODEL= NONE: CMeanFlowIteration::Iterate runs the
+    flow's MultiGrid_Iteration alone, iteration_structure.cpp:531-534; no SST solver, no eddy viscosity, the laminar
+    PaSR branch): the mini9 jet with the 4-species mechanism (as it4t), implicit ILU0 at CFL 1, two reference outer
+    iterations."""
+    pts, quads, U, writer = mini9_inputs()
+    out = iteration_case("lam4", writer, fold_species(U, 4)[:, :-2], 4, 2, 1.0, "ILU0", "EULER_IMPLICIT",
+                         cfg_edit=lambda t: t.replace("KIND_TURB_MODEL= SST", "KIND_TURB_MODEL= NONE"))
+    out["laminar"] = np.array(1)
+    return out
+
+
 # CSysSolve::Solve's branches (linear_solvers_structure.cpp:626-708) beside the default FGMRES: (LINEAR_SOLVER,
 # LINEAR_SOLVER_PREC, LINEAR_SOLVER_RESTART_FREQUENCY) of each golden
 LIN_CASES = {"lsbc": ("BCGSTAB", "ILU0", 10), "lsbj": ("BCGSTAB", "JACOBI", 10), "lsfj": ("FGMRES", "JACOBI", 10),
@@ -961,7 +973,7 @@ def main():
              "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
              "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d, "fpit2": case_fpit2,
              "fpit2l": lambda: case_fpit2(limiter=True), "it4t": case_it4t,
-             "it4tl": lambda: case_it4t(limiter=True), "rank9": case_rank9,
+             "it4tl": lambda: case_it4t(limiter=True), "rank9": case_rank9, "lam4": case_lam4,
              **{k: (lambda k=k: case_lin(k)) for k in LIN_CASES},
              **{f"it{n}s": (lambda n=n: case_itns(n)) for n in (5, 6, 8)}}[case]()
         path = os.path.join(gold, case + ".npz")

@@ -743,7 +743,14 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
             G = grad_lsq(mech, nDim, np.arange(N), mesh["coord"], o["V"], mesh["nbr_ptr"], mesh["nbr"])
         return o, G, strain_mag(nDim, G)
 
-    T, TG, mut = s["T"], s["TG"], s["mut"]
+    # cfg["rans"] False (round 6): REACTIVE_NAVIER_STOKES without a turbulence model (KIND_TURB_MODEL= NONE) — no
+    # eddy viscosity or turbulent kinetic energy in the flow records, the laminar viscous closure and PaSR branch, and
+    # the flow's MultiGrid_Iteration alone (iteration_structure.cpp:531-534)
+    rans = bool(cfg.get("rans", True))
+    if rans:
+        T, TG, mut = s["T"], s["TG"], s["mut"]
+    else:
+        T, TG, mut = np.zeros((N, 2)), np.zeros((N, 2, nDim)), np.zeros(N)
     scheme = cfg.get("time", "implicit")  # TIME_DISCRE_FLOW: implicit | euler_explicit | rk (RK_ALPHA_COEFF)
     alphas = list(cfg.get("rk_alpha", [1.0])) if scheme == "rk" else [None]
     gk = np.ascontiguousarray(TG[:, 0, :])
@@ -772,9 +779,9 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
             rc, Jci, Jcj = muscl_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], o["V"], o["dPdU"],
                                        G, L, [1.0, 1.0, 1.0], cfg["mach_inf"], imp)
         rv, Jvi, Jvj = visc_edges(mech, nDim, mesh["edges"], mesh["edge_normal"], mesh["coord"], o["V"], G, o["mu"],
-                                  o["kappa"], o["Dij"], o["dTdU"], T[:, 0].copy(), mut, sig, gk, True, imp,
+                                  o["kappa"], o["Dij"], o["dTdU"], T[:, 0].copy(), mut, sig, gk, rans, imp,
                                   [1, 1, 1, cfg["prandtl_turb"], cfg["lewis_turb"]])
-        rs, Js = source_cells(mech, nDim, o["V"], o["dTdU"], vol, T[:, 1].copy(), True, imp,
+        rs, Js = source_cells(mech, nDim, o["V"], o["dTdU"], vol, T[:, 1].copy(), rans, imp,
                               [cfg["c_mu"], cfg["pasr_lb"], 1, 1, 1])
         R, A, _ = assemble(rp, col, mesh["edges"], rc, Jci if imp else None, Jcj, rv, Jvi, Jvj, rs, Js if imp else None,
                            vol, np.full(N, np.inf), nb)
@@ -783,7 +790,7 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
         st = dict(U=U, V=o["V"], dPdU=o["dPdU"], dTdU=o["dTdU"], grad_prim=G, mu=o["mu"], kappa=o["kappa"],
                   Dij=o["Dij"], turb_k=T[:, 0].copy(), mu_t=mut, sigma_k=sig, grad_k=gk, eddy_visc_flow=o["eddy"])
         A_loops, R_loops = (A.copy() if imp else None, R.copy()) if keep else (None, None)
-        charac = bc_flow(mech, nDim, mesh, bc["marker"], bc["prm"], st, rp, col, R, A, Uold, imp, True)
+        charac = bc_flow(mech, nDim, mesh, bc["marker"], bc["prm"], st, rp, col, R, A, Uold, imp, rans)
         if not imp:  # ExplicitEuler_Iteration (solver_direct_reactive.cpp:2414-2449) / ExplicitRK_Iteration (:2456-2493)
             Un = update(Uold, R, nDim, 1, 1.0, vol, dt) if alpha is None else update_rk(Uold, R, nDim, alpha, vol, dt)
             rms = np.maximum(1e-32, np.sqrt(np.sum(R * R, axis=0) / N))
@@ -809,6 +816,9 @@ def outer_iteration(mech, nDim, mesh, s, bc, cfg, ext_iter, pattern, part_ptr=No
     o2, G2, strain2 = preprocess(Un, o["V"], Uold, T, mut)
     Un = o2["U"]
     V2 = o2["V"]
+    if not rans:
+        return dict(U=Un, V=V2, Uold=Uold, rms=rms, lin_iters=it, lin_resid=lres, dt=dt, pre=o, pre_grad=G,
+                    jac_loops=A_loops, res_loops=R_loops, sys=A, rhs=rhs, sol=x)
     rho = np.ascontiguousarray(V2[:, nDim + 2])
     # SST SingleGrid_Iteration: CTurbSSTSolver::Preprocessing (solver_direct_turbulent.cpp:2923-2951): the gradient,
     # SetSolution_Limiter when SPATIAL_ORDER_TURB = 2ND_ORDER_LIMITER, and the flow's SetPrimitive_Limiter again when

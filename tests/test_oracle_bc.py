@@ -126,6 +126,9 @@ def iteration_cfg(g):
     if "ignition" in g:  # IGNITION, IGNITION_ITER, IGNITION_TEMPERATURE, FUEL_INDEX, OXIDIZER_INDEX (ig9)
         cfg["p2v"] = list(cfg["p2v"]) + [float(x) for x in g["ignition"]]
     bc = dict(marker=g["bc_marker"], prm=O.bc_prm(bp, g["mach_inf"][0], g["visc_params"][1], g["visc_params"][2]))
+    if "laminar" in g:  # KIND_TURB_MODEL= NONE (lam4): no SST records
+        cfg["rans"] = False
+        return cfg, bc, dict(U=g["it_U0"], V=g["it_V0"], Uold=g["it_Uold0"])
     state = dict(U=g["it_U0"], V=g["it_V0"], Uold=g["it_Uold0"], T=g["it_sst0"], TG=g["it_sstgrad0"],
                  F1=g["it_F1_0"], F2=g["it_F2_0"], CDkw=g["it_CDkw0"], mut=g["it_mut0"])
     return cfg, bc, state
@@ -203,3 +206,27 @@ def test_ignition_branch_of_set_primitive():
     o2 = O.set_primitive(m, nDim, g["it_U0"], V0, g["it_sst0"][:, 0].copy(), g["it_mut0"], prm_late)
     assert np.array_equal(o2["V"][~hot], V0[~hot]) and np.all(o2["V"][hot, 0] != 1700.0)
     assert np.array_equal(o2["V"][hot, 1:], V0[hot, 1:]) and np.array_equal(o2["dPdU"], o["dPdU"])
+
+
+def test_laminar_outer_iterations_vs_reference():
+    """Round 6: the laminar REACTIVE_NAVIER_STOKES outer iteration (KIND_TURB_MODEL= NONE, golden lam4: the flow's
+    MultiGrid_Iteration alone, iteration_structure.cpp:531-534) restated: each reference iteration from its own state,
+    then both chained."""
+    g = golden("lam4")
+    nDim = int(g["dims"][0])
+    m = O.Mechanism(g)
+    cfg, bc, s0 = iteration_cfg(g)
+    assert cfg["rans"] is False
+    pat = (g["bsr_row_ptr"], g["bsr_col"])
+    for chained in (False, True):
+        s = s0
+        for k in range(2):
+            if not chained and k > 0:
+                p = f"it{k}_"
+                s = dict(U=g[p + "U"], V=g[p + "V"], Uold=g[p + "Uold"])
+            s = O.outer_iteration(m, nDim, g, s, bc, cfg, k, pat)
+            p = f"it{k + 1}_"
+            assert colrel(s["U"], g[p + "U"]) < (1e-12 if not chained else ITER_TOL[k + 1]), (chained, k)
+            assert colrel(s["V"], g[p + "V"]) < (1e-12 if not chained else ITER_TOL[k + 1]), (chained, k)
+            np.testing.assert_allclose(s["rms"], g[p + "rms"], rtol=1e-12)
+            assert "T" not in s
