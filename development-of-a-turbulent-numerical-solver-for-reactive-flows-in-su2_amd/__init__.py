@@ -105,7 +105,7 @@ class BcDesc(C.Structure):
 ERR_PHASE_CALL, ERR_PHASE_UPWIND = 0, 1  # rx_err_phase (rx_last_error_phase)
 LIMITER_VENKATAKRISHNAN, LIMITER_BARTH_JESPERSEN = 0, 1  # rx_slope_limiter
 
-BC_NONE, BC_INLET, BC_OUTLET, BC_ISOTHERMAL, BC_HEATFLUX, BC_EULER = 0, 1, 2, 3, 4, 5
+BC_NONE, BC_INLET, BC_OUTLET, BC_ISOTHERMAL, BC_HEATFLUX, BC_EULER, BC_SUP_INLET, BC_SUP_OUTLET = range(8)
 EULER_WALL_ENUM = 1  # the reference's BC_TYPE value of EULER_WALL (Common/include/option_structure.hpp:750)
 INLET_TOTAL_CONDITIONS, INLET_MASS_FLOW, INLET_TEMPERATURE_IMPOSE = 0, 1, 2
 
@@ -113,12 +113,14 @@ INLET_TOTAL_CONDITIONS, INLET_MASS_FLOW, INLET_TEMPERATURE_IMPOSE = 0, 1, 2
 def bc_from_reference(bc_marker, bc_params, normal_neighbor):
     """rx_bc_desc inputs from the reference's marker table (oracle/ref_harness bc_marker / bc_params: rows
     [KindBC, a, b, dir[3], Y[Ns]]; bc_params[11:18] = the reference's INLET_FLOW, OUTLET_FLOW, ISOTHERMAL,
-    HEAT_FLUX, TOTAL_CONDITIONS, MASS_FLOW, TEMPERATURE_IMPOSE enum values, bc_params[27] EULER_WALL). Other marker
-    kinds (SYMMETRY_PLANE) map to BC_NONE."""
+    HEAT_FLUX, TOTAL_CONDITIONS, MASS_FLOW, TEMPERATURE_IMPOSE enum values, bc_params[27] EULER_WALL,
+    bc_params[28:30] SUPERSONIC_INLET / SUPERSONIC_OUTLET). Other marker kinds (SYMMETRY_PLANE) map to BC_NONE."""
     p = np.asarray(bc_params, dtype=np.float64)
     k_in, k_out, k_iso, k_hf, k_tot, k_mf, k_ti = (int(x) for x in p[11:18])
     k_eu = int(p[27]) if len(p) > 27 else EULER_WALL_ENUM
     kmap = {k_in: BC_INLET, k_out: BC_OUTLET, k_iso: BC_ISOTHERMAL, k_hf: BC_HEATFLUX, k_eu: BC_EULER}
+    if len(p) > 29:
+        kmap.update({int(p[28]): BC_SUP_INLET, int(p[29]): BC_SUP_OUTLET})
     md = np.ascontiguousarray(bc_marker, dtype=np.float64)
     kinds = np.array([kmap.get(int(k), BC_NONE) for k in md[:, 0]], dtype=np.int32)
     inlet = {k_tot: INLET_TOTAL_CONDITIONS, k_mf: INLET_MASS_FLOW, k_ti: INLET_TEMPERATURE_IMPOSE}[int(p[0])]

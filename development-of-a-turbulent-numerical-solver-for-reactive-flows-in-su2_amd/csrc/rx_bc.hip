@@ -128,6 +128,42 @@ __device__ inline bool ghost_state(const DevMech& m, const BCDev& B, int kind, c
   constexpr int T_ = 0, VX = 1, P_ = NDIM + 1, RHO = NDIM + 2, H_ = NDIM + 3, A_ = NDIM + 4, RHOS = NDIM + 5;
   constexpr int nPV = NS + NDIM + 5;
   *sup = false;
+  if (kind == RX_BC_SUP_INLET) {
+    // BC_Supersonic_Inlet (:3014-3055): T, P, velocity and Y from the marker; density from the gas law
+    // (ComputeDensity :457-460), enthalpy (ComputeEnthalpy) and frozen sound speed (ComputeFrozenSoundSpeed :408-411:
+    // sqrt(gamma Rgas T)) at the dimensional temperature, each then non-dimensionalised; no turbulent kinetic energy
+    // in the ghost's enthalpy (the subsonic inlet adds it, :3517)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) Ys[s] = md[6 + s];
+    const double Temperature = md[1], Pressure = md[2];
+    const double Rgas = lib_rgas<NS>(m, Ys);
+    const double Density = Pressure / (Temperature * Rgas);
+    const double Enthalpy = lib_enthalpy<NS>(m, Temperature, Ys, err);
+    const double SoundSpeed = sqrt(lib_gamma<NS>(m, Temperature, Ys, err) * Rgas * Temperature);
+    double Velocity2 = 0.0;
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) {
+      Vg[VX + d] = md[3 + d] / B.vel_ref;
+      Velocity2 += Vg[VX + d] * Vg[VX + d];
+    }
+    Vg[T_] = Temperature / B.T_ref;
+    Vg[P_] = Pressure / B.P_ref;
+    Vg[RHO] = Density / B.rho_ref;
+    Vg[H_] = Enthalpy / B.E_ref + 0.5 * Velocity2;
+    Vg[A_] = SoundSpeed / B.vel_ref;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) Vg[RHOS + s] = Ys[s];
+    // the ghost's dP/dU (:3080-3102) enters only Jacobian_j, which the BC discards: the domain's stands in
+#pragma unroll
+    for (int v = 0; v < NS + NDIM + 2; ++v) Sc[v] = Sd[v];
+    return true;
+  }
+  if (kind == RX_BC_SUP_OUTLET) {  // BC_Supersonic_Outlet (:3708-3717): the ghost is the domain state
+#pragma unroll
+    for (int v = 0; v < nPV; ++v) Vg[v] = Vd[v];
+    *sup = true;
+    return true;
+  }
   if (kind == RX_BC_INLET) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) Ys[s] = md[6 + s];
@@ -504,7 +540,7 @@ __global__ __launch_bounds__(kApplyBlock) void k_bc_apply(const int32_t* __restr
       }
       continue;
     }
-    if (kind != RX_BC_INLET && kind != RX_BC_OUTLET) continue;
+    if (kind != RX_BC_INLET && kind != RX_BC_OUTLET && kind != RX_BC_SUP_INLET && kind != RX_BC_SUP_OUTLET) continue;
     if (q < nVar) {
       r += resc[(size_t)b * nVar + q];
       r -= resv[(size_t)b * nVar + q];
@@ -828,8 +864,13 @@ int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
   if (NB > 0 && !bc->normal_neighbor) return RX_ERR_ARG;
   if (bc->inlet_kind < RX_INLET_TOTAL_CONDITIONS || bc->inlet_kind > RX_INLET_TEMPERATURE_IMPOSE) return RX_ERR_ARG;
   const int nM = bc->n_marker, W = 6 + ctx->ns, nd = ctx->nDim;
-  for (int k = 0; k < nM; ++k)
-    if (bc->kind[k] < RX_BC_NONE || bc->kind[k] > RX_BC_EULER) return RX_ERR_ARG;
+  for (int k = 0; k < nM; ++k) {
+    if (bc->kind[k] < RX_BC_NONE || bc->kind[k] > RX_BC_SUP_OUTLET) return RX_ERR_ARG;
+    // the reference's supersonic BCs give their viscous numerics no turbulence quantities (BC_Inlet's MANGOTURB
+    // add-on, solver_direct_reactive.cpp:3607-3621, has no counterpart at :3131-3203 / :3743-3788): under SST they read
+    // whatever the previous boundary call left in that object, so only laminar contexts take them
+    if ((bc->kind[k] == RX_BC_SUP_INLET || bc->kind[k] == RX_BC_SUP_OUTLET) && ctx->cfg.rans) return RX_ERR_UNSUPPORTED;
+  }
   std::vector<int32_t> node(NB), pn(NB), mark(NB), weak;
   std::vector<uint8_t> wall(ctx->N, 0);
   for (int64_t b = 0; b < NB; ++b) {
@@ -839,7 +880,8 @@ int rx_bc_set(rx_ctx* ctx, const rx_bc_desc* bc) {
     pn[b] = (int32_t)q;
     mark[b] = (int32_t)mk;
     const int kd = bc->kind[mk];
-    if ((kd == RX_BC_INLET || kd == RX_BC_OUTLET) && p < ctx->Nd) weak.push_back((int32_t)b);
+    if ((kd == RX_BC_INLET || kd == RX_BC_OUTLET || kd == RX_BC_SUP_INLET || kd == RX_BC_SUP_OUTLET) && p < ctx->Nd)
+      weak.push_back((int32_t)b);
     if ((kd == RX_BC_ISOTHERMAL || kd == RX_BC_HEATFLUX) && p < ctx->Nd) wall[p] = 1;
   }
   // owned boundary points and their vertices in (marker, vertex) = input order; vertices of RX_BC_NONE markers

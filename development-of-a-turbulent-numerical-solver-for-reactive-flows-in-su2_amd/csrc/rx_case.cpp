@@ -341,16 +341,22 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
     if (k->rk.empty()) k->rk.push_back(1.0);
   }
   // boundary markers (mesh marker order)
-  std::map<std::string, std::vector<double>> inlet, inlet_y;
+  std::map<std::string, std::vector<double>> inlet, inlet_y, sup_in;
   std::map<std::string, double> outlet, iso, hf;
-  std::map<std::string, int> euler, sym;
+  std::map<std::string, int> euler, sym, sup_out;
   {
-    const auto t = list(c.str("MARKER_INLET", ""));
-    for (size_t q = 0; q + 5 < t.size(); q += 6) {
-      std::vector<double> v;
-      for (size_t r = 1; r < 6; ++r) v.push_back(std::strtod(t[q + r].c_str(), nullptr));
-      inlet[t[q]] = v;
-    }
+    // MARKER_INLET= (tag, a, b, dir[3]); MARKER_SUPERSONIC_INLET= (tag, T, P, velocity[3]) (config_structure.cpp's
+    // Marker_Supersonic_Inlet / Inlet_Temperature / Inlet_Pressure / Inlet_Velocity)
+    auto six = [&](const char* key, std::map<std::string, std::vector<double>>& m) {
+      const auto t = list(c.str(key, ""));
+      for (size_t q = 0; q + 5 < t.size(); q += 6) {
+        std::vector<double> v;
+        for (size_t r = 1; r < 6; ++r) v.push_back(std::strtod(t[q + r].c_str(), nullptr));
+        m[t[q]] = v;
+      }
+    };
+    six("MARKER_INLET", inlet);
+    six("MARKER_SUPERSONIC_INLET", sup_in);
     std::string fr = trim(c.str("INLET_MASS_FRAC", ""));
     const size_t a = fr.find_first_not_of("()"), b = fr.find_last_not_of("()");
     fr = a == std::string::npos ? std::string() : fr.substr(a, b - a + 1);
@@ -375,7 +381,11 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
     pairs("MARKER_HEATFLUX", hf);
     for (const auto& u : list(c.str("MARKER_EULER", ""))) euler[u] = 1;
     for (const auto& u : list(c.str("MARKER_SYM", ""))) sym[u] = 1;
+    for (const auto& u : list(c.str("MARKER_SUPERSONIC_OUTLET", ""))) sup_out[u] = 1;
   }
+  // the reference's supersonic BCs give the viscous numerics no turbulence quantities: laminar cases only (rx_bc_set)
+  if ((!sup_in.empty() || !sup_out.empty()) && F.rans)
+    return fail(k, RX_ERR_UNSUPPORTED, "MARKER_SUPERSONIC_INLET / _OUTLET with KIND_TURB_MODEL= SST");
   const int W = 6 + ns;
   std::vector<int32_t> is_wall(nmark, 0);
   k->data.assign((size_t)nmark * W, 0.0);
@@ -388,6 +398,14 @@ int rx_case_read(const char* cfg_path, rx_case** out) {
       for (int q = 0; q < 5; ++q) r[1 + q] = v[q];
       if (inlet_y.count(tag))
         for (size_t s = 0; s < inlet_y[tag].size(); ++s) r[6 + s] = inlet_y[tag][s];
+    } else if (sup_in.count(tag)) {
+      k->kind.push_back(RX_BC_SUP_INLET);
+      const auto& v = sup_in[tag];
+      for (int q = 0; q < 5; ++q) r[1 + q] = v[q];
+      if (inlet_y.count(tag))
+        for (size_t s = 0; s < inlet_y[tag].size(); ++s) r[6 + s] = inlet_y[tag][s];
+    } else if (sup_out.count(tag)) {
+      k->kind.push_back(RX_BC_SUP_OUTLET);
     } else if (outlet.count(tag)) {
       k->kind.push_back(RX_BC_OUTLET);
       r[1] = outlet[tag];

@@ -328,9 +328,15 @@ int rx_sst_postprocessing(rx_ctx *turb);
  *                     row a = the wall heat flux) / CTurbSSTSolver::BC_HeatFlux_Wall solver_direct_turbulent.cpp:
  *                     3087-3140 (the isothermal wall's k = 0, omega = 60 mu / (rho beta_1 d^2))
  *   RX_BC_EULER       CReactiveEulerSolver::BC_Euler_Wall :2881-2966 (weak: momentum += (p + 2/3 rho k) n A, the
- *                     Jacobian's momentum rows += dP/dU n A) / CTurbSolver::BC_Euler_Wall (no action, :608-613) */
+ *                     Jacobian's momentum rows += dP/dU n A) / CTurbSolver::BC_Euler_Wall (no action, :608-613)  *   RX_BC_SUP_INLET   CReactiveEulerSolver::BC_Supersonic_Inlet :2998-3206 (round 6): the whole ghost state imposed,
+ *                     data [kind, T, P, velocity[3], Y[Ns]] (MARKER_SUPERSONIC_INLET + INLET_MASS_FRAC); laminar
+ *                     contexts only (rans = 0: the reference hands its viscous numerics no turbulence quantities)
+ *   RX_BC_SUP_OUTLET  CReactiveEulerSolver::BC_Supersonic_Outlet :3681-3800 (round 6): ghost = the domain state;
+ *                     laminar contexts only
+ */
 typedef enum {
-  RX_BC_NONE = 0, RX_BC_INLET = 1, RX_BC_OUTLET = 2, RX_BC_ISOTHERMAL = 3, RX_BC_HEATFLUX = 4, RX_BC_EULER = 5
+  RX_BC_NONE = 0, RX_BC_INLET = 1, RX_BC_OUTLET = 2, RX_BC_ISOTHERMAL = 3, RX_BC_HEATFLUX = 4, RX_BC_EULER = 5,
+  RX_BC_SUP_INLET = 6, RX_BC_SUP_OUTLET = 7
 } rx_bc_kind;
 typedef enum { RX_INLET_TOTAL_CONDITIONS = 0, RX_INLET_MASS_FLOW = 1, RX_INLET_TEMPERATURE_IMPOSE = 2 } rx_inlet_kind;
 typedef struct {

@@ -747,6 +747,32 @@ def case_lam4():
     return out
 
 
+def case_sup4():
+    """CReactiveEulerSolver::BC_Supersonic_Inlet / BC_Supersonic_Outlet (solver_direct_reactive.cpp:2998-3206,
+    :3681-3800) on the laminar lam4 setup: both inlets MARKER_SUPERSONIC_INLET (oxidizer 300 K, 130 kPa, 20 m/s; fuel
+    800 K, 130 kPa, 0.87 m/s: the whole ghost state imposed; a subsonic MARKER_INLET beside them is not possible —
+    BC_Inlet asserts one INLET_MASS_FRAC entry per MARKER_INLET, :3245, while the supersonic inlet reads its mass
+    fractions from that same list), the outlet a MARKER_SUPERSONIC_OUTLET (ghost = the domain state); two reference
+    outer iterations. Laminar because the reference's two supersonic
+    BCs never hand the turbulence quantities to their viscous numerics (the MANGOTURB add-on of BC_Inlet / BC_Outlet,
+    :3607-3621, is missing there), so under SST they read whatever the previous boundary call left in that object."""
+    pts, quads, U, writer = mini9_inputs()
+
+    def edit(t):
+        t = t.replace("KIND_TURB_MODEL= SST", "KIND_TURB_MODEL= NONE")
+        t = t.replace("MARKER_INLET= ( Oxidizer_Inlet, 300.0, 20.0, 1.0, 0.0, 0.0, Fuel_Inlet, 800.0, 0.87, 0.0, 1.0, 0.0)",
+                      "MARKER_SUPERSONIC_INLET= ( Oxidizer_Inlet, 300.0, 130000.0, 20.0, 0.0, 0.0, "
+                      "Fuel_Inlet, 800.0, 130000.0, 0.0, 0.87, 0.0)")
+        t = t.replace("MARKER_OUTLET= ( Outlet, 101325.0)", "MARKER_SUPERSONIC_OUTLET= ( Outlet )")
+        assert "MARKER_SUPERSONIC_INLET" in t and "MARKER_SUPERSONIC_OUTLET" in t
+        return t
+
+    out = iteration_case("sup4", writer, fold_species(U, 4)[:, :-2], 4, 2, 1.0, "ILU0", "EULER_IMPLICIT",
+                         cfg_edit=edit)
+    out["laminar"] = np.array(1)
+    return out
+
+
 # CSysSolve::Solve's branches (linear_solvers_structure.cpp:626-708) beside the default FGMRES: (LINEAR_SOLVER,
 # LINEAR_SOLVER_PREC, LINEAR_SOLVER_RESTART_FREQUENCY) of each golden
 LIN_CASES = {"lsbc": ("BCGSTAB", "ILU0", 10), "lsbj": ("BCGSTAB", "JACOBI", 10), "lsfj": ("FGMRES", "JACOBI", 10),
@@ -973,7 +999,7 @@ def main():
              "fp3": case_fp3, "jet9k": case_jet9k, "itx9": case_itx9, "itx4": case_itx4, "ig9": case_ig9, "rst9": case_rst9, "fpit": case_fpit, "it7": case_it7,
              "bj9": case_bj9, "gg9": case_gg9, "mix3d": case_mix3d, "fpit2": case_fpit2,
              "fpit2l": lambda: case_fpit2(limiter=True), "it4t": case_it4t,
-             "it4tl": lambda: case_it4t(limiter=True), "rank9": case_rank9, "lam4": case_lam4,
+             "it4tl": lambda: case_it4t(limiter=True), "rank9": case_rank9, "lam4": case_lam4, "sup4": case_sup4,
              **{k: (lambda k=k: case_lin(k)) for k in LIN_CASES},
              **{f"it{n}s": (lambda n=n: case_itns(n)) for n in (5, 6, 8)}}[case]()
         path = os.path.join(gold, case + ".npz")

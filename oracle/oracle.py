@@ -658,12 +658,14 @@ EULER_WALL = 1.0  # the reference's BC_TYPE enum value (Common/include/option_st
 def bc_prm(bc_params, mach_inf, prandtl_turb, lewis_turb):
     """Oracle BC parameter vector: the harness's bc_params[:18] (inlet kind, Tke_Inf, kine_Inf, omega_Inf, beta_1,
     reference values, the reference's marker / inlet enum values) + (Mach_inf, Pr_t, Le_t) + the EULER_WALL enum
-    value (bc_params[27] of the newer harness dumps)."""
+    value (bc_params[27] of the newer harness dumps) + the SUPERSONIC_INLET / SUPERSONIC_OUTLET enum values
+    (bc_params[28:30] of the round-6 dumps; -999, a value no marker row carries, when absent)."""
     bp = np.asarray(bc_params, dtype=np.float64)
-    p = np.zeros(22)
+    p = np.zeros(24)
     p[:18] = bp[:18]
     p[18:21] = (mach_inf, prandtl_turb, lewis_turb)
     p[21] = bp[27] if len(bp) > 27 else EULER_WALL
+    p[22:24] = bp[28:30] if len(bp) > 29 else (-999.0, -999.0)
     return p
 
 

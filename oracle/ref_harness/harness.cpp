@@ -308,6 +308,13 @@ int main(int argc, char** argv) {
         r[1] = cfg->GetIsothermal_Temperature(tag);
       } else if (kind == HEAT_FLUX) {
         r[1] = cfg->GetWall_HeatFlux(tag);
+      } else if (kind == SUPERSONIC_INLET) {  // (T, P, velocity vector, mass fractions)
+        r[1] = cfg->GetInlet_Temperature(tag);
+        r[2] = cfg->GetInlet_Pressure(tag);
+        su2double* vel = cfg->GetInlet_Velocity(tag);
+        for (unsigned short d = 0; d < nDim; ++d) r[3 + d] = vel[d];
+        const su2double* ys = cfg->GetInlet_MassFrac(tag);
+        for (unsigned short s = 0; s < nSpecies; ++s) r[6 + s] = ys[s];
       }
     }
     dumpd("bc_marker", md, {(long)nMarker, W});
@@ -322,7 +329,8 @@ int main(int argc, char** argv) {
                               cfg->GetCFL(MESH_0), cfg->GetLinear_Solver_Error(), (double)cfg->GetLinear_Solver_Iter(),
                               (double)cfg->GetKind_Linear_Solver_Prec(), cfg->GetRelaxation_Factor_Flow(),
                               cfg->GetRelaxation_Factor_Turb(), cfg->GetCFLRedCoeff_Turb(), cfg->GetMax_DeltaTime(),
-                              (double)SYMMETRY_PLANE, (double)EULER_WALL};
+                              (double)SYMMETRY_PLANE, (double)EULER_WALL, (double)SUPERSONIC_INLET,
+                              (double)SUPERSONIC_OUTLET};
     dumpd("bc_params", bp, {(long)bp.size()});
     // the cfg values the other modes dump with their operators, same layouts
     dumpd("mach_inf", std::vector<double>{cfg->GetMach()}, {1});

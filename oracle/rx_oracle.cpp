@@ -3070,6 +3070,7 @@ struct BCPrm {
   int k_inlet, k_outlet, k_iso, k_hf, k_total, k_massflow, k_timpose;  // the reference's enum values
   double mach_inf, Pr_t, Le_t;
   int k_euler;                // EULER_WALL (option_structure.hpp:750)
+  int k_sup_in, k_sup_out;    // SUPERSONIC_INLET / SUPERSONIC_OUTLET (-999: not in the dump)
   int implicit, rans;
 };
 
@@ -3133,7 +3134,36 @@ void flow_weak_vertex(const Mech& m, int nDim, const BCPrm& P, int kind, const d
   const double* Sd = f.dPdU + i * nVar;
   double Sc[32], Sv[32], Ys[32];
   bool sup = false;  // supersonic outlet: the node's own secondaries
-  if (kind == P.k_inlet) {
+  if (kind == P.k_sup_in) {
+    // CReactiveEulerSolver::BC_Supersonic_Inlet (:3014-3055): the marker's T, P, velocity and the inlet mass fractions;
+    // ComputeDensity (P / (T Rgas), :457-460), ComputeEnthalpy and ComputeFrozenSoundSpeed (sqrt(gamma Rgas T),
+    // :408-411) at the dimensional temperature, then non-dimensionalised. The reference divides the CONFIG's velocity
+    // array by Velocity_Ref in place on every call (:3023, :3045-3046); restated once (identical for dimensional runs)
+    for (int s = 0; s < ns; ++s) Ys[s] = md[6 + s];
+    const double Temperature = md[1], Pressure = md[2];
+    const double Rgas = mix_rgas(m, Ys);
+    const double Density = Pressure / (Temperature * Rgas);
+    const double Enthalpy = mix_enthalpy(m, Temperature, Ys);
+    const double SoundSpeed = std::sqrt(frozen_gamma(m, Temperature, Ys) * Rgas * Temperature);
+    double Velocity2 = 0.0;
+    for (int d = 0; d < nDim; ++d) {
+      Vg[VX + d] = md[3 + d] / P.vel_ref;
+      Velocity2 += Vg[VX + d] * Vg[VX + d];
+    }
+    Vg[T_] = Temperature / P.T_ref;
+    Vg[P_] = Pressure / P.P_ref;
+    Vg[RHO] = Density / P.rho_ref;
+    Vg[H_] = Enthalpy / P.E_ref + 0.5 * Velocity2;
+    Vg[A_] = SoundSpeed / P.vel_ref;
+    for (int s = 0; s < ns; ++s) Vg[RHOS + s] = Ys[s];
+    // the ghost's dP/dU (:3080-3102) enters only Jacobian_j, which the BC discards: the domain's stands in
+    for (int v = 0; v < nVar; ++v) Sc[v] = Sd[v];
+  } else if (kind == P.k_sup_out) {
+    // CReactiveEulerSolver::BC_Supersonic_Outlet (:3708-3717, :3753-3755): ghost = domain state, the node's own
+    // secondaries (as the subsonic outlet's supersonic exit)
+    for (int v = 0; v < nPV; ++v) Vg[v] = Vd[v];
+    sup = true;
+  } else if (kind == P.k_inlet) {
     for (int s = 0; s < ns; ++s) Ys[s] = md[6 + s];
     const double* dir = md + 3;
     double Gamma = Sd[nDim + 1] + 1.0, vel_mag = 0.0;
@@ -3454,6 +3484,8 @@ BCPrm bc_params(const double* p, int implicit, int rans) {
   P.Pr_t = p[19];
   P.Le_t = p[20];
   P.k_euler = (int)p[21];
+  P.k_sup_in = (int)p[22];
+  P.k_sup_out = (int)p[23];
   P.implicit = implicit;
   P.rans = rans;
   return P;
@@ -3482,7 +3514,8 @@ int orc_bc_flow(void* h, int nDim, int64_t NB, const int64_t* bvert, const doubl
       for (int mk = 0; mk < nMarker; ++mk) {
         const double* md = mdata + (size_t)mk * W;
         const int kind = (int)md[0];
-        const bool weak = kind == P.k_inlet || kind == P.k_outlet || kind == P.k_euler;
+        const bool weak = kind == P.k_inlet || kind == P.k_outlet || kind == P.k_euler || kind == P.k_sup_in ||
+                          kind == P.k_sup_out;
         const bool strong = kind == P.k_iso || kind == P.k_hf;
         if ((pass == 0 && !weak) || (pass == 1 && !strong)) continue;
         for (int64_t b = 0; b < NB; ++b) {

@@ -81,12 +81,13 @@ def test_cpp_driver_matches_reference(tmp_path, implicit):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["it9", "itx9", "itx4", "lam4"])
+@pytest.mark.parametrize("case", ["it9", "itx9", "itx4", "lam4", "sup4"])
 def test_cpp_driver_reference_iteration(tmp_path, case):
     """rx::Iterate (the reference's outer iteration with the jet's boundary conditions) from the C++ mirror, against
     the reference's own iteration: it9 (implicit, ILU0), itx9 (the shipped cfg: EULER_EXPLICIT flow, LU_SGS SST, the
     whole reference mesh), itx4 (C1: 4 species, RUNGE-KUTTA_EXPLICIT, 3 stages); lam4 (round 6): the laminar
-    REACTIVE_NAVIER_STOKES iteration through rx::IterateFlow."""
+    REACTIVE_NAVIER_STOKES iteration through rx::IterateFlow; sup4 (round 6): the same with the supersonic inlet /
+    outlet markers."""
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", case + ".npz")))
     laminar = "laminar" in g
     if laminar:  # no SST records: zeros stand in for the files the RANS branch reads

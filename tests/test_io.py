@@ -492,3 +492,31 @@ def test_case_from_cfg_laminar(tmp_path, val):
     c = rx.case_from_cfg(os.path.join(wd, "case.cfg"))
     assert c["flow_cfg"]["rans"] == 1
     c["mesh"].close()
+
+
+def test_case_from_cfg_supersonic_markers(tmp_path):
+    """Round 6: MARKER_SUPERSONIC_INLET= (tag, T, P, velocity[3]) with the tag's INLET_MASS_FRAC, and
+    MARKER_SUPERSONIC_OUTLET= (tag) become BC_SUP_INLET / BC_SUP_OUTLET rows (data [kind, T, P, velocity, Y]) in a
+    laminar case; with KIND_TURB_MODEL= SST rx_case_read refuses them (status 9): the reference's supersonic BCs hand
+    their viscous numerics no turbulence quantities (solver_direct_reactive.cpp:3131-3203, :3743-3788)."""
+    wd, base = _jet_cfg(tmp_path)
+    txt = _with_key(base, "MARKER_INLET", None)
+    txt = _with_key(txt, "MARKER_OUTLET", None)
+    txt = _with_key(txt, "MARKER_SUPERSONIC_INLET",
+                    "( Oxidizer_Inlet, 300.0, 130000.0, 20.0, 0.0, 0.0, Fuel_Inlet, 800.0, 130000.0, 0.0, 0.87, 0.0)")
+    txt = _with_key(txt, "MARKER_SUPERSONIC_OUTLET", "( Outlet )")
+    path = os.path.join(wd, "case.cfg")
+    with open(path, "w") as f:
+        f.write(_with_key(txt, "KIND_TURB_MODEL", "NONE"))
+    c = rx.case_from_cfg(path)
+    kinds, data = c["bc"]["kind"], c["bc"]["data"]
+    assert (kinds == rx.BC_SUP_INLET).sum() == 2 and (kinds == rx.BC_SUP_OUTLET).sum() == 1
+    assert not np.isin(kinds, [rx.BC_INLET, rx.BC_OUTLET]).any()
+    rows = data[kinds == rx.BC_SUP_INLET]
+    fuel = rows[np.argmax(rows[:, 1])]
+    assert np.array_equal(fuel[1:6], [800.0, 130000.0, 0.0, 0.87, 0.0]) and fuel[6] == 1.0
+    c["mesh"].close()
+    with open(path, "w") as f:
+        f.write(_with_key(txt, "KIND_TURB_MODEL", "SST"))
+    with pytest.raises(rx.RxError, match="SUPERSONIC.*status 9"):
+        rx.case_from_cfg(path)

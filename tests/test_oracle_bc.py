@@ -208,11 +208,13 @@ def test_ignition_branch_of_set_primitive():
     assert np.array_equal(o2["V"][hot, 1:], V0[hot, 1:]) and np.array_equal(o2["dPdU"], o["dPdU"])
 
 
-def test_laminar_outer_iterations_vs_reference():
+@pytest.mark.parametrize("case", ["lam4", "sup4"])
+def test_laminar_outer_iterations_vs_reference(case):
     """Round 6: the laminar REACTIVE_NAVIER_STOKES outer iteration (KIND_TURB_MODEL= NONE, golden lam4: the flow's
     MultiGrid_Iteration alone, iteration_structure.cpp:531-534) restated: each reference iteration from its own state,
-    then both chained."""
-    g = golden("lam4")
+    then both chained. sup4: both jet inlets MARKER_SUPERSONIC_INLET and the outlet MARKER_SUPERSONIC_OUTLET
+    (BC_Supersonic_Inlet / BC_Supersonic_Outlet, solver_direct_reactive.cpp:2998-3206 / :3681-3800)."""
+    g = golden(case)
     nDim = int(g["dims"][0])
     m = O.Mechanism(g)
     cfg, bc, s0 = iteration_cfg(g)
