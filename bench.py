@@ -172,6 +172,18 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
                     ("k_fg_spmv_stage" if nVar > 4 else "k_fg_spmv_full") + tv),
         # ILU(0) apply: L and U blocks + inv(D_i) (= nnzb blocks) + column indices, b in, x out
         "ILU_APPLY": hbm(nnzb * (blk + 4) + 2 * N * nVar * d, ilu_apply_kernels(N, nnzb, nVar, parts, nDim)),
+        # round 6: k_set_primitive — U, the previous record's temperature, k and mu_t in; the
+        # clamped U, the record (nPV), dP/dU, dT/dU, mu, kappa, D_ij (Ns^2) and the eddy viscosity out
+        "PRIMITIVE": hbm(N * (nVar + 3) * d + N * (nVar + nPV + 2 * nVar + 3 + ns * ns) * d, "k_set_primitive" + te),
+        # k_sst_upwind (first order): per node its velocity + density, (k, omega), residual and diagonal block in / out,
+        # the adjacency pointer; per adjacency entry its index + block position and the off-diagonal 2x2 block in / out;
+        # per edge its ends and normal
+        "SST_UPW": hbm(N * ((nDim + 1) * d + 2 * d + 4 * d + 64 + 4) + 2 * E * (12 + 64) + E * (8 + nDim * d),
+                       f"k_sst_upwind<{nDim}, 0>"),
+        # k_sst_visc: per node F1, mu, eddy viscosity, density, coordinates, (k, omega) and their gradient, residual and
+        # diagonal block in / out; per adjacency entry and edge as the upwind
+        "SST_VISC": hbm(N * ((4 + nDim + 2 + 2 * nDim + 4) * d + 64 + 4) + 2 * E * (12 + 64) + E * (8 + nDim * d),
+                        f"k_sst_visc<{nDim}>"),
     }
     if fused:
         del models["CONV"]  # the CONV phase launches no flux kernel (only MUSCL's reconstruction at 2nd order)
@@ -560,7 +572,7 @@ def main():
             out["traffic"] = None
         return out
 
-    timed = [k for k in models if prof[k][1] > 0]
+    timed = [k for k in models if prof.get(k, (0, 0))[1] > 0]
     kernels = {k: roof(k) for k in timed}
     # GPU time per step of each single-kernel phase (SPMV / ILU_APPLY: average launch of the eager pass x launches per
     # step, i.e. per linear iteration of the flow solve; ILU_APPLY is one kernel, both sweeps, unless RX_ILU_SPLIT)

@@ -304,22 +304,38 @@ __global__ __launch_bounds__(kBlock) void k_sst_upwind(int N, const int32_t* __r
   if (Dp)
 #pragma unroll
     for (int q = 0; q < 4; ++q) D[q] = Dp[q];
+  // first order (round 6): the node's own velocity, density and (k, omega) read once; per edge only the other end's
+  // record is gathered (the same values as the two-sided gather, so the same arithmetic)
+  double uo[NDIM], rhoo = 0.0, ko = 0.0, wo = 0.0;
+  if (ORDER == 0) {
+#pragma unroll
+    for (int d = 0; d < NDIM; ++d) uo[d] = V[(size_t)i * nPV + d + 1];
+    rhoo = V[(size_t)i * nPV + RHO];
+    ko = T[2 * (size_t)i];
+    wo = T[2 * (size_t)i + 1];
+  }
   auto edge = [&](int e, int side, int n0, int n1, int64_t ob) {
     const double* v0 = V + (size_t)n0 * nPV;
     const double* v1 = V + (size_t)n1 * nPV;
     double u0[NDIM], u1[NDIM], rho0, rho1, k0, w0, k1, w1;
     if (ORDER == 0) {
+      const int other = side ? n0 : n1;
+      const double* vx = V + (size_t)other * nPV;
+      double ux[NDIM];
+#pragma unroll
+      for (int d = 0; d < NDIM; ++d) ux[d] = vx[d + 1];
+      const double rhox = vx[RHO], kx = T[2 * (size_t)other], wx = T[2 * (size_t)other + 1];
 #pragma unroll
       for (int d = 0; d < NDIM; ++d) {
-        u0[d] = v0[d + 1];
-        u1[d] = v1[d + 1];
+        u0[d] = side ? ux[d] : uo[d];
+        u1[d] = side ? uo[d] : ux[d];
       }
-      rho0 = v0[RHO];
-      rho1 = v1[RHO];
-      k0 = T[2 * (size_t)n0];
-      w0 = T[2 * (size_t)n0 + 1];
-      k1 = T[2 * (size_t)n1];
-      w1 = T[2 * (size_t)n1 + 1];
+      rho0 = side ? rhox : rhoo;
+      rho1 = side ? rhoo : rhox;
+      k0 = side ? kx : ko;
+      w0 = side ? wx : wo;
+      k1 = side ? ko : kx;
+      w1 = side ? wo : wx;
     } else {
       double vec0[NDIM], vec1[NDIM];
 #pragma unroll
@@ -471,37 +487,54 @@ __global__ __launch_bounds__(kBlock) void k_sst_visc(int N, SSTC c, const int32_
   if (Dp)
 #pragma unroll
     for (int q = 0; q < 4; ++q) D[q] = Dp[q];
+  // round 6: the node's own F1, mu, eddy viscosity, coordinates, (k, omega), their gradient and density read once; per
+  // edge only the other end's are gathered and each operand is selected into its n0 / n1 place (the same values in
+  // the same expressions as the two-sided gather)
+  double TGo[2 * NDIM], cdo[NDIM];
+  const double F1o = F1[i], muo = mu[i], eto = eddy[i], To0 = T[2 * (size_t)i], To1 = T[2 * (size_t)i + 1];
+  const double rhoo = Dp ? V[(size_t)i * nPV + RHO] : 0.0;
+#pragma unroll
+  for (int d = 0; d < NDIM; ++d) cdo[d] = coord[(size_t)i * NDIM + d];
+#pragma unroll
+  for (int q = 0; q < 2 * NDIM; ++q) TGo[q] = TG[(size_t)i * 2 * NDIM + q];
   auto edge = [&](int e, int side, int n0, int n1, int64_t ob) {
-    const double F1i = F1[n0], F1j = F1[n1];
+    const int x = side ? n0 : n1;  // the other end
+    auto pick0 = [&](double own, double oth) { return side ? oth : own; };  // the n0 operand
+    auto pick1 = [&](double own, double oth) { return side ? own : oth; };  // the n1 operand
+    const double F1x = F1[x], mux = mu[x], etx = eddy[x];
+    const double F1i = pick0(F1o, F1x), F1j = pick1(F1o, F1x);
     const double ski = F1i * c.sk1 + (1.0 - F1i) * c.sk2;
     const double skj = F1j * c.sk1 + (1.0 - F1j) * c.sk2;
     const double soi = F1i * c.so1 + (1.0 - F1i) * c.so2;
     const double soj = F1j * c.so1 + (1.0 - F1j) * c.so2;
-    const double mui = mu[n0], muj = mu[n1], eti = eddy[n0], etj = eddy[n1];
+    const double mui = pick0(muo, mux), muj = pick1(muo, mux), eti = pick0(eto, etx), etj = pick1(eto, etx);
     const double dik = mui + ski * eti, djk = muj + skj * etj;
     const double dio = mui + soi * eti, djo = muj + soj * etj;
     const double dk = 0.5 * (dik + djk), dw = 0.5 * (dio + djo);
     double ev[NDIM], nrm[NDIM], dist2 = 0.0, proj = 0.0;
 #pragma unroll
     for (int d = 0; d < NDIM; ++d) {
+      const double cx = coord[(size_t)x * NDIM + d];
       nrm[d] = normal[(size_t)e * NDIM + d];
-      ev[d] = coord[(size_t)n1 * NDIM + d] - coord[(size_t)n0 * NDIM + d];
+      ev[d] = pick1(cdo[d], cx) - pick0(cdo[d], cx);
       dist2 += ev[d] * ev[d];
       proj += ev[d] * nrm[d];
     }
     if (dist2 == 0.0) proj = 0.0; else proj = proj / dist2;
+    const double Tx[2] = {T[2 * (size_t)x], T[2 * (size_t)x + 1]}, To[2] = {To0, To1};
     double corr[2];
 #pragma unroll
     for (int v = 0; v < 2; ++v) {
       double pn = 0.0, pe = 0.0;
 #pragma unroll
       for (int d = 0; d < NDIM; ++d) {
-        const double m = 0.5 * (TG[((size_t)n0 * 2 + v) * NDIM + d] + TG[((size_t)n1 * 2 + v) * NDIM + d]);
+        const double gx = TG[((size_t)x * 2 + v) * NDIM + d], go = TGo[v * NDIM + d];
+        const double m = 0.5 * (pick0(go, gx) + pick1(go, gx));
         pn += m * nrm[d];
         pe += m * ev[d];
       }
       corr[v] = pn;
-      corr[v] -= pe * proj - (T[2 * (size_t)n1 + v] - T[2 * (size_t)n0 + v]) * proj;
+      corr[v] -= pe * proj - (pick1(To[v], Tx[v]) - pick0(To[v], Tx[v])) * proj;
     }
     const double f0 = dk * corr[0], f1 = dw * corr[1];
     if (side == 0) {
@@ -512,7 +545,8 @@ __global__ __launch_bounds__(kBlock) void k_sst_visc(int N, SSTC c, const int32_
       r1 += f1;
     }
     if (Dp) {
-      const double ri = V[(size_t)n0 * nPV + RHO], rj = V[(size_t)n1 * nPV + RHO];
+      const double rx = V[(size_t)(side ? n0 : n1) * nPV + RHO];
+      const double ri = side ? rx : rhoo, rj = side ? rhoo : rx;
       const double Ji[4] = {-dk * proj / ri, 0.0, 0.0, -dw * proj / ri};
       const double Jj[4] = {dk * proj / rj, 0.0, 0.0, dw * proj / rj};
       double* O = A + ob * 4;

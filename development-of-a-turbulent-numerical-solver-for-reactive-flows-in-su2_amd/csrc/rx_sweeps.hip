@@ -619,6 +619,12 @@ __device__ __forceinline__ void grp_solve_lds(const double* LU, double (&rhs)[NV
 #ifndef RX_GRP_WAVES_BIG
 #define RX_GRP_WAVES_BIG 8
 #endif
+// timing probe (build variants only; wrong numerics): bit 0 = every inv(A_jj) load reads row 0's block (an L1/L2 hit
+// instead of the block a group of the previous level just stored), bit 1 = the second and later lower blocks' A_ij /
+// A_ji loads read block 0
+#ifndef RX_GRP_PROBE
+#define RX_GRP_PROBE 0
+#endif
 constexpr int kGrpMaxWaves = RX_GRP_WAVES > RX_GRP_WAVES_BIG ? RX_GRP_WAVES : RX_GRP_WAVES_BIG;
 template <int NV>
 constexpr int grp_waves() { return NV >= 10 ? RX_GRP_WAVES_BIG : RX_GRP_WAVES; }
@@ -739,7 +745,7 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
       load_second(rec, al, bl2, jl2);
 #endif
       if (kd > k0) {
-        const int j0 = rec[8];
+        const int j0 = (RX_GRP_PROBE & 1) ? 0 : rec[8];
 #pragma unroll
         for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)j0 * NV2 + q * NV + ac];
       }
@@ -794,14 +800,15 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
           }
         } else if (k + 1 < kd) {  // further lower blocks' loads (not on quad / hex meshes), into the registers
                                   // just freed (before W's store, so that waiting for them does not wait for it)
-          const int jn = rec[9 + t];
+          const int jn = (RX_GRP_PROBE & 1) ? 0 : rec[9 + t];
 #pragma unroll
           for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)jn * NV2 + q * NV + ac];
+          const size_t kb = (RX_GRP_PROBE & 2) ? 0 : (size_t)(k + 1);
 #pragma unroll
           for (int u = 0; u < PB; ++u)
-            if (16 * u + al < NV2) bl[u] = A[(size_t)(k + 1) * NV2 + 16 * u + al];
+            if (16 * u + al < NV2) bl[u] = A[kb * NV2 + 16 * u + al];
           if (rec[15 + t] >= 0) {
-            const int kk = rec[15 + t];
+            const int kk = (RX_GRP_PROBE & 2) ? 0 : rec[15 + t];
 #pragma unroll
             for (int u = 0; u < PB; ++u)
               if (16 * u + al < NV2) jl[u] = A[(size_t)kk * NV2 + 16 * u + al];
