@@ -1843,6 +1843,12 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_wide(const int32_t* __restrict
 #ifndef RX_RING_PROBE
 #define RX_RING_PROBE 0  // timing probes of k_ilu_apply_ring (build variants only; bit 0: no factor-block loads)
 #endif
+// round 6: a level's global x store issued after the next level's loads (row, factor and slot loads) instead of
+// before them. vmcnt retires loads and stores in issue order, so with the store first, waiting for those loads at
+// the wavefront's next level also waited for the store's write acknowledgement; issued last, it is younger than them.
+#ifndef RX_RING_LATE_STORE
+#define RX_RING_LATE_STORE 1
+#endif
 template <int NV, int TB>
 constexpr int ring_rpb() {
   return (TB / 64) * (64 / NV);  // rows per pass: whole rows per wavefront (the backward's v exchange is wave-local)
@@ -1894,7 +1900,7 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
     };
     int4 sl = make_int4(0, 0, 0, 0), sln = sl;
     int2 w = make_int2(0, -1), wn = w;
-    double F[MB][NV], bi = 0.0;
+    double F[MB][NV], bi = 0.0, xst = 0.0;
     int xo[MB];
     auto issue = [&]() {  // this lane's loads of row sl (its level is the next one computed)
       bi = b[(size_t)sl.x * NV + a];
@@ -1942,13 +1948,17 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
         }
         xs[w.x * NV + a] = xi;
         if (w.y >= 0) xs[w.y * NV + a] = xi;
-        x[(size_t)sl.x * NV + a] = xi;
+        if (!RX_RING_LATE_STORE) x[(size_t)sl.x * NV + a] = xi;
+        xst = xi;
       }
+      const bool st = act;
+      const int xrow = sl.x;
       act = actn;
       sl = sln;
       w = wn;
       if (act) issue();
       actn = slot_at(l + 2 * G, sln, wn);
+      if (RX_RING_LATE_STORE && st) x[(size_t)xrow * NV + a] = xst;
       lds_barrier();
     }
   }
@@ -1968,7 +1978,7 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
     };
     int4 sl = make_int4(0, 0, 0, 0), sln = sl;
     int2 w = make_int2(0, -1), wn = w;
-    double F[MB][NV], inv[NV], xf = 0.0;
+    double F[MB][NV], inv[NV], xf = 0.0, xst = 0.0;
     int xo[MB];
     auto issue = [&]() {
       xf = x[(size_t)sl.x * NV + a];
@@ -2025,13 +2035,17 @@ __global__ __launch_bounds__(TB) void k_ilu_apply_ring(
         for (int c = 0; c < NV; ++c) s += inv[c] * v[vr * NV + c];
         xs[w.x * NV + a] = s;
         if (w.y >= 0) xs[w.y * NV + a] = s;
-        x[(size_t)sl.x * NV + a] = s;
+        if (!RX_RING_LATE_STORE) x[(size_t)sl.x * NV + a] = s;
+        xst = s;
       }
+      const bool st = act;
+      const int xrow = sl.x;
       act = actn;
       sl = sln;
       w = wn;
       if (act) issue();
       actn = slot_at(l + 2 * G, sln, wn);
+      if (RX_RING_LATE_STORE && st) x[(size_t)xrow * NV + a] = xst;
       lds_barrier();
     }
   }
