@@ -449,8 +449,9 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       // order is recomputed exactly as schedule() builds it
       const int64_t Nd = ctx->Nd;
       std::vector<int32_t> fo(Nd);
+      // a row's dependency level in its partition, its place in the level, and the partition's first (global) level
+      std::vector<int32_t> lv(N, 0), lpos(N, 0), lbase(np + 1, 0);
       {
-        std::vector<int32_t> lv(N, 0);
         for (int64_t p = 0; p < np; ++p) {
           const int64_t lo = ctx->h_part_ptr[p], hi = ctx->h_part_ptr[p + 1];
           int32_t maxl = 0;
@@ -463,14 +464,28 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
           std::vector<int32_t> cnt(maxl + 2, 0);
           for (int64_t i = lo; i < hi; ++i) cnt[lv[i] + 1]++;
           for (int32_t l = 0; l <= maxl; ++l) cnt[l + 1] += cnt[l];
-          for (int64_t i = lo; i < hi; ++i) fo[lo + cnt[lv[i]]++] = (int32_t)i;
+          const std::vector<int32_t> start(cnt);
+          for (int64_t i = lo; i < hi; ++i) {
+            lpos[i] = cnt[lv[i]] - start[lv[i]];
+            fo[lo + cnt[lv[i]]++] = (int32_t)i;
+          }
+          lbase[p + 1] = lbase[p] + maxl + 1;  // (schedule()'s part_lvl: a level even for an empty partition)
         }
       }
       std::vector<int32_t> plan((size_t)Nd * 32, 0);
       // k_ilu_build_grp's plans (rx_sweeps.hip): rows with at most six lower blocks, each of whose single update
       // (if any) is the diagonal (triangle-free stencils: quads, hexahedra) — [0..5] as plan, [8 + t] the column j
       // of lower block t, [14 + t] the position of A_ji in row j (-1: the block updates nothing)
+      // round 6, the LDS ring of inv(D) (rx_ilu_grp_ring_w rows per level parity): [6] the row's own ring slot, [20 + t]
+      // the slot of lower block t's inv(A_jj) when row j is in the previous level and in the ring (-1: read from the
+      // factor in memory; its level is then flagged in ilu_gfull, so that the barrier before it waits for the stores)
       std::vector<int32_t> gplan((size_t)Nd * 32, 0);
+      const int32_t rw = rx_ilu_grp_ring_w(ctx);
+      auto ring_slot = [&](int32_t q) { return lpos[q] < rw ? (lv[q] & 1) * rw + lpos[q] : -1; };
+      std::vector<int32_t> gfull((size_t)std::max<int32_t>(lbase[np], 0) + 1, 0);
+      std::vector<int32_t> part_of(N, 0);
+      for (int64_t p = 0; p < np; ++p)
+        for (int64_t i = ctx->h_part_ptr[p]; i < ctx->h_part_ptr[p + 1]; ++i) part_of[i] = (int32_t)p;
       bool grp_ok = true;
       for (int64_t r = 0; r < Nd && grp_ok; ++r) {
         const int32_t i = fo[r];
@@ -483,12 +498,16 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
         g[5] = (int32_t)ctx->h_rp[i + 1];
         const int32_t nlow = (int32_t)diag[i] - klo[i];
         grp_ok = nlow <= 6;
+        g[6] = ring_slot(i);
+        for (int32_t t = 0; t < 6; ++t) g[20 + t] = -1;
         for (int32_t t = 0; t < nlow && grp_ok; ++t) {
           const int32_t k = klo[i] + t;
           const int32_t nu = uptr[k + 1] - uptr[k];
           grp_ok = nu == 0 || (nu == 1 && upd[2 * uptr[k] + 1] == (int32_t)diag[i]);
           g[8 + t] = col32[k];
           g[14 + t] = nu == 1 ? upd[2 * uptr[k]] : -1;  // -1: no update
+          if (lv[col32[k]] == lv[i] - 1) g[20 + t] = ring_slot(col32[k]);
+          if (g[20 + t] < 0) gfull[lbase[part_of[i]] + lv[i]] = 1;
         }
       }
       for (int64_t r = 0; r < Nd; ++r) {
@@ -526,6 +545,8 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       if (grp_ok && rx_ilu_grp_lds(ctx) > (size_t)ctx->lds_max) ctx->ilu_grp_ok = false;
       CK(dupload(ctx, &ctx->ilu_plan, plan.data(), plan.size()));
       if (grp_ok) CK(dupload(ctx, &ctx->ilu_gplan, gplan.data(), gplan.size()));
+      if (grp_ok) CK(dupload(ctx, &ctx->ilu_gfull, gfull.data(), gfull.size()));
+      ctx->ilu_ring_w = rw;
     }
 
     const size_t per_wave = sizeof(double) * ((size_t)(rowmax + 1 + rx_ilu_stage()) * nv * nv + 16);
@@ -833,7 +854,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   ctx->solve_graph = nullptr;
   if (ctx->kind == RX_KIND_SST && ctx->flow) --ctx->flow->n_children;
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->asmes_wg, ctx->asmes_side, ctx->nbr_ptr,
-                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan,
+                  ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan, ctx->ilu_gfull,
                   ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->fs.rows, ctx->bs.part_lvl, ctx->bs.lvl_ptr, ctx->bs.rows,
                   ctx->fs.pass_lo, ctx->fs.part_pass, ctx->bs.pass_lo, ctx->bs.part_pass,
                   ctx->fs.slot, ctx->bs.slot, ctx->fs.ring, ctx->bs.ring, ctx->fs.rpart_lvl, ctx->fs.rlvl_ptr,

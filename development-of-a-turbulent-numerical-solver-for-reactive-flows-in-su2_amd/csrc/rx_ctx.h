@@ -109,6 +109,8 @@ struct rx_ctx {
   int ilu_waves = 1;            // wavefronts per workgroup of the ILU factorisation
   bool ilu_grp_ok = false;      // every row's plan is compact and updates only its diagonal (k_ilu_build_grp)
   int32_t* ilu_gplan = nullptr; // [N][32] k_ilu_build_grp's row plans (up to 6 lower blocks, one update each)
+  int32_t* ilu_gfull = nullptr; // [forward levels + 1] k_ilu_build_grp: 1 = the level reads an inv(A_jj) from memory
+  int ilu_ring_w = 0;           // k_ilu_build_grp's LDS ring of inv(D): rows per level parity (0: no ring)
   int ilu_diag_deferred = 0;    // the ILU field's diagonal blocks are not stored (k_ilu_build_grp, RX_GRP_DIAG_STORE 0)
   // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
   // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])
@@ -332,6 +334,7 @@ int rx_la_build_system(rx_ctx* ctx);
 void rx_bc_free(rx_ctx* ctx);
 int rx_bc_launch_weak(rx_ctx* ctx, hipStream_t st);  // ghost states + boundary fluxes (+ Jacobians)
 size_t rx_ilu_grp_lds(const rx_ctx* ctx);  // grouped ILU build's dynamic LDS (rx_sweeps.hip)
+int rx_ilu_grp_ring_w(const rx_ctx* ctx);  // rows per level parity of the grouped build's inv(D) ring (rx_sweeps.hip)
 int rx_ensure_assembled(rx_ctx* ctx);  // implicit: assemble the residual / BSR Jacobian now (rx_api.hip)
 // SST (rx_sst.hip)
 int rx_sst_build_system(rx_ctx* ctx);

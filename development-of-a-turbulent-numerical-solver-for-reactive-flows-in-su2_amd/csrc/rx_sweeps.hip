@@ -634,22 +634,31 @@ constexpr int grp_np() { return (NV + 1) & ~1; }
 template <int NV>
 constexpr int grp_slot_doubles() { return NV * grp_np<NV>() + kPlan; }  // + two plan records (this row, the next)
 
+// Round 6: an LDS ring of inv(D) (ring_w rows per level parity; the host plan's [6] / [20 + t] slots). A row stores its
+// inv(D_i) to the ring besides the factor, and a row of the next level reads its lower blocks' inv(A_jj) from there
+// instead of from memory. A level none of whose rows reads an inv(A_jj) from memory (gfull[l] = 0) is then entered
+// through an LDS barrier: the global stores of the level before (W, inv(D)) no longer have to be acknowledged first
+// (__syncthreads waits vmcnt(0)), and no inv(A_jj) load queues behind them (vmcnt retires in issue order). A level
+// with such a row (its lower neighbour two or more levels back, or past the ring's width) keeps the full barrier.
+// The same values in the same operations: the factor is bitwise the same.
 template <int NV>
 __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const int32_t* __restrict__ part_lvl,
                                                                     const int32_t* __restrict__ lvl_ptr,
                                                                     const int32_t* __restrict__ plan,
                                                                     const double* __restrict__ A,
                                                                     double* __restrict__ F, double* __restrict__ invD,
-                                                                    long long* __restrict__ trace) {
+                                                                    long long* __restrict__ trace,
+                                                                    const int32_t* __restrict__ gfull, int ring_w) {
   constexpr int NV2 = NV * NV, NP = grp_np<NV>();
   extern __shared__ double lds[];
   const int a = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = blockDim.x >> 4;
   double* S = lds + (size_t)grp * grp_slot_doubles<NV>();  // inv(A_jj), then W, then the LU of D_i
   int* const recb = reinterpret_cast<int*>(S + NV * NP);   // plan records: this row's and the next row's
   const int p = blockIdx.x, l0 = part_lvl[p], l1 = part_lvl[p + 1];
-  // the partition's level pointers in LDS (behind the group slots): the loop bounds and the next-row search read
-  // them every row
-  int* lp = reinterpret_cast<int*>(lds + (size_t)ngrp * grp_slot_doubles<NV>()) - l0;
+  // the inv(D) ring behind the group slots, then the partition's level pointers: the loop bounds and the next-row
+  // search read them every row
+  double* ring = lds + (size_t)ngrp * grp_slot_doubles<NV>();
+  int* lp = reinterpret_cast<int*>(ring + (size_t)2 * ring_w * NV2) - l0;
   for (int l = l0 + (int)threadIdx.x; l <= l1; l += blockDim.x) lp[l] = lvl_ptr[l];
   __syncthreads();
   auto next_slot = [&](int r, int l, int& ln) -> int {  // the group's next row after slot r of level l (its level
@@ -744,10 +753,16 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #ifdef RX_GRP_EARLY2
       load_second(rec, al, bl2, jl2);
 #endif
+      const int rs_own = rec[6];
       if (kd > k0) {
-        const int j0 = (RX_GRP_PROBE & 1) ? 0 : rec[8];
+        const int j0 = (RX_GRP_PROBE & 1) ? 0 : rec[8], rs0 = rec[20];
+        if (rs0 >= 0) {
 #pragma unroll
-        for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)j0 * NV2 + q * NV + ac];
+          for (int q = 0; q < NV; ++q) s[q] = ring[(size_t)rs0 * NV2 + q * NV + ac];
+        } else {
+#pragma unroll
+          for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)j0 * NV2 + q * NV + ac];
+        }
       }
 #ifdef RX_GRP_EARLY2
       if (kd > k0 + 1) {
@@ -800,9 +815,14 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
           }
         } else if (k + 1 < kd) {  // further lower blocks' loads (not on quad / hex meshes), into the registers
                                   // just freed (before W's store, so that waiting for them does not wait for it)
-          const int jn = (RX_GRP_PROBE & 1) ? 0 : rec[9 + t];
+          const int jn = (RX_GRP_PROBE & 1) ? 0 : rec[9 + t], rsn = rec[21 + t];
+          if (rsn >= 0) {
 #pragma unroll
-          for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)jn * NV2 + q * NV + ac];
+            for (int q = 0; q < NV; ++q) s[q] = ring[(size_t)rsn * NV2 + q * NV + ac];
+          } else {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)jn * NV2 + q * NV + ac];
+          }
           const size_t kb = (RX_GRP_PROBE & 2) ? 0 : (size_t)(k + 1);
 #pragma unroll
           for (int u = 0; u < PB; ++u)
@@ -879,11 +899,20 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
       if (act) {
 #pragma unroll
         for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + al] = rhs[rr];
+        if (rs_own >= 0) {
+#pragma unroll
+          for (int rr = 0; rr < NV; ++rr) ring[(size_t)rs_own * NV2 + rr * NV + al] = rhs[rr];
+        }
       }
       RX_GSTAMP(3);
       ++trow;
     }
-    __syncthreads();
+    if (l + 1 >= l1 || gfull[l + 1]) {
+      __syncthreads();
+    } else {  // the next level reads inv(A_jj) from the ring only: an LDS barrier
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     if (trace && blockIdx.x == 0 && threadIdx.x == 0 && l - l0 < kGrpTraceLevels)
       trace[1 + kGrpTraceGroups * kGrpTraceRows * 8 + (l - l0)] = (long long)__builtin_amdgcn_s_memtime();
   }
@@ -2365,10 +2394,11 @@ template <int NV>
 void launch_ilu_build_grp(rx_ctx* ctx, int gwaves) {
   if constexpr (NV >= 5) {
     const size_t shm = sizeof(double) * (size_t)(4 * gwaves) * grp_slot_doubles<NV>() +
+                       sizeof(double) * (size_t)2 * ctx->ilu_ring_w * NV * NV +
                        sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1);
     k_ilu_build_grp<NV><<<ctx->npart, 64 * gwaves, shm, ctx->stream>>>(
         ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_gplan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
-        ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)NV * NV, ctx->ilu_trace);
+        ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)NV * NV, ctx->ilu_trace, ctx->ilu_gfull, ctx->ilu_ring_w);
     ctx->ilu_diag_deferred = RX_GRP_DIAG_STORE ? 0 : 1;
   }
 }
@@ -2521,6 +2551,42 @@ int rx_la_prepare(rx_ctx* ctx) {
   return RX_OK;
 }
 
+// Rows per level parity of the grouped build's inv(D) ring: as many of the widest level's rows as the LDS left by the
+// group slots and the level table holds (RX_GRP_RING=0 or fewer than 8: no ring); 0 when not instantiated.
+#ifndef RX_GRP_RING
+#define RX_GRP_RING 1
+#endif
+static size_t grp_base_lds(const rx_ctx* ctx, int nv, size_t slot_doubles, int waves_cap) {
+  const int gwaves = std::max(1, std::min(waves_cap, (ctx->fs.maxwidth + 3) / 4));
+  (void)nv;
+  return sizeof(double) * (size_t)(4 * gwaves) * slot_doubles + sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1);
+}
+int rx_ilu_grp_ring_w(const rx_ctx* ctx) {
+  int w = 0;
+  auto f = [&](auto nvc) {
+    constexpr int NV = decltype(nvc)::value;
+    if constexpr (NV >= 5) {
+      const size_t base = grp_base_lds(ctx, NV, grp_slot_doubles<NV>(), grp_waves<NV>());
+      const size_t per = sizeof(double) * 2 * (size_t)NV * NV;
+      const size_t room = (size_t)ctx->lds_max > base ? (size_t)ctx->lds_max - base : 0;
+      w = (int)std::min<size_t>((size_t)ctx->fs.maxwidth, room / per);
+      if (!RX_GRP_RING || w < 8) w = 0;
+    }
+  };
+  switch (ctx->nVar) {
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 9: f(std::integral_constant<int, 9>{}); break;
+    case 10: f(std::integral_constant<int, 10>{}); break;
+    case 11: f(std::integral_constant<int, 11>{}); break;
+    case 12: f(std::integral_constant<int, 12>{}); break;
+    case 13: f(std::integral_constant<int, 13>{}); break;
+    case 14: f(std::integral_constant<int, 14>{}); break;
+    default: break;
+  }
+  return w;
+}
+
 // Dynamic LDS of the grouped build at its launch configuration (launch_ilu_build_grp); 0 when not instantiated.
 size_t rx_ilu_grp_lds(const rx_ctx* ctx) {
   size_t shm = 0;
@@ -2528,7 +2594,8 @@ size_t rx_ilu_grp_lds(const rx_ctx* ctx) {
     constexpr int NV = decltype(nvc)::value;
     if constexpr (NV >= 5) {
       const int gwaves = std::max(1, std::min(grp_waves<NV>(), (ctx->fs.maxwidth + 3) / 4));
-      shm = sizeof(double) * (size_t)(4 * gwaves) * grp_slot_doubles<NV>() + sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1);
+      shm = sizeof(double) * (size_t)(4 * gwaves) * grp_slot_doubles<NV>() + sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1) +
+            sizeof(double) * (size_t)2 * ctx->ilu_ring_w * NV * NV;
     }
   };
   switch (ctx->nVar) {
