@@ -1545,7 +1545,10 @@ __global__ __launch_bounds__(kBlock) void k_grad_lsq(int N, const int32_t* __res
                                                      const int32_t* __restrict__ list) {
   constexpr int nPV = NS + NDIM + 5, nG = NS + NDIM + 2, P_P = NDIM + 1, RHOS_P = NDIM + 5, P_G = NDIM + 1,
                 RHOS_G = NDIM + 2;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+#ifndef RX_GRAD_XCD
+#define RX_GRAD_XCD 1  // round 6: workgroups in XCD order (xcd_block), the neighbour records under one L2
+#endif
+  const int t = (RX_GRAD_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= N) return;
   const int i = list ? list[t] : t;  // list: the points of one half of the distributed split (rx_grad_lsq)
   double pi[nG], pj[nG], C[nG][NDIM];

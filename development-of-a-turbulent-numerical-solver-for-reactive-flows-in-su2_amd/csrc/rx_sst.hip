@@ -238,6 +238,18 @@ __global__ __launch_bounds__(kBlock) void k_strain(int N, int nG, const double* 
 // block) is called in edge order.
 template <int NDIM>
 constexpr int sst_pf() { return 2 * NDIM; }
+// Round 6: the node loops' workgroups in XCD order (as rx_kernels.hip's xcd_block): the hardware deals consecutive
+// workgroups round-robin to the 8 XCDs, so a node's neighbours in the previous / next grid line were gathered by
+// other XCDs, each filling its own L2 with the same record lines; remapped, XCD x walks one contiguous node range.
+#ifndef RX_SST_XCD
+#define RX_SST_XCD 1
+#endif
+__device__ inline int sst_node_block(int b, int nb) {
+  if (!RX_SST_XCD) return b;
+  constexpr int kXcd = 8;
+  const int x = b % kXcd, idx = b / kXcd, q = nb / kXcd, r = nb % kXcd;
+  return x < r ? x * (q + 1) + idx : r * (q + 1) + (x - r) * q + idx;
+}
 template <int NDIM, typename Fn>
 __device__ __forceinline__ void sst_edges(int i, const int32_t* __restrict__ adj_ptr, const int32_t* __restrict__ adj,
                                           const int64_t* __restrict__ adj_blk, const int32_t* __restrict__ edges,
@@ -295,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void k_sst_upwind(int N, const int32_t* __r
                                                        const double* __restrict__ V, int nPV,
                                                        const double* __restrict__ T, double* __restrict__ R,
                                                        double* __restrict__ A, SstRecon rc) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = sst_node_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (i >= N) return;
   constexpr int RHO = NDIM + 2, nL = NDIM + 2;
   double r0 = R[2 * (size_t)i], r1 = R[2 * (size_t)i + 1];
@@ -478,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void k_sst_visc(int N, SSTC c, const int32_
                                                      const double* __restrict__ eddy, const double* __restrict__ T,
                                                      const double* __restrict__ TG, const double* __restrict__ F1,
                                                      double* __restrict__ R, double* __restrict__ A) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = sst_node_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (i >= N) return;
   constexpr int RHO = NDIM + 2;
   double r0 = R[2 * (size_t)i], r1 = R[2 * (size_t)i + 1];
