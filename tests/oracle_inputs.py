@@ -17,8 +17,14 @@ def outer_iteration_inputs(mesh, st, cfg, bc):
     nDim = int(np.shape(mesh["coord"])[1])
     bp = np.asarray(dict(np.load(os.path.join(GOLD, "bc9.npz")))["bc_params"])
     md = np.array(bc["data"], dtype=np.float64)
-    md[:, 0] = [{1: bp[11], 2: bp[12], 3: bp[13], 4: bp[14], 5: O.EULER_WALL}.get(int(k), -1.0) for k in bc["kind"]]
-    bco = dict(marker=md, prm=O.bc_prm(bp, cfg.mach_inf, cfg.prandtl_turb, cfg.lewis_turb))
+    # the supersonic kinds (round 6): the reference's SUPERSONIC_INLET / SUPERSONIC_OUTLET enum values (golden sup4's
+    # bc_params[28:30])
+    sup = np.asarray(dict(np.load(os.path.join(GOLD, "sup4.npz")))["bc_params"])[28:30]
+    md[:, 0] = [{1: bp[11], 2: bp[12], 3: bp[13], 4: bp[14], 5: O.EULER_WALL, 6: sup[0], 7: sup[1]}.get(int(k), -1.0)
+                for k in bc["kind"]]
+    prm = O.bc_prm(bp, cfg.mach_inf, cfg.prandtl_turb, cfg.lewis_turb)
+    prm[22:24] = sup
+    bco = dict(marker=md, prm=prm)
     c = dict(cfl=cfg.cfl, max_delta_time=cfg.max_delta_time, prandtl_lam=cfg.prandtl_lam,
              prandtl_turb=cfg.prandtl_turb, lewis_turb=cfg.lewis_turb, mach_inf=cfg.mach_inf, c_mu=cfg.c_mu,
              pasr_lb=cfg.pasr_lb, lin_tol=cfg.lin_tol, lin_iter=cfg.lin_iter, relaxation=cfg.relaxation,

@@ -78,6 +78,65 @@ def test_full_size_iteration_vs_oracle(case):
     assert_close(rms_t, o["sst_rms"], rtol=1e-10, what=f"{case} RMS SST")
 
 
+@pytest.mark.parametrize("variant", ["laminar", "supersonic"])
+def test_full_size_laminar_iteration_vs_oracle(variant):
+    """Round 6: the laminar REACTIVE_NAVIER_STOKES outer iteration (rx.Iterate(flow, None): the flow's
+    MultiGrid_Iteration alone, rans = 0) at configs[1]'s size (500 x 200, 7 species, 256 partitions, implicit ILU0
+    FGMRES(5)), from the laminar start-up preprocessing, against O.outer_iteration(rans=False) in the device's
+    inner-product order; "supersonic": the same with both jet inlets BC_SUP_INLET (T, 101 325 Pa and the velocity
+    the subsonic inlet imposes) and the outlet BC_SUP_OUTLET. Bars as above."""
+    nx, ny, parts, ns = 500, 200, 256, 7
+    mesh, st0, mech, kw = synth.jet_field_case(nx, ny, n_species=ns, n_part=parts)
+    cfg = rx.default_cfg(implicit=1, lin_prec=1, rans=0, **kw)
+    bc = synth.jet_bc(mesh, ns)
+    if variant == "supersonic":
+        data = np.array(bc["data"], dtype=np.float64)
+        kind = np.array(bc["kind"]).copy()
+        for k in range(len(kind)):
+            if kind[k] == rx.BC_INLET:  # [kind, T, |v|, dir, Y] -> [kind, T, P, velocity, Y]
+                vel = data[k, 2] * data[k, 3:6]
+                data[k, 2] = 101325.0
+                data[k, 3:6] = vel
+                kind[k] = rx.BC_SUP_INLET
+            elif kind[k] == rx.BC_OUTLET:
+                kind[k] = rx.BC_SUP_OUTLET
+        bc = dict(bc, kind=kind.astype(np.int32), data=data)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech), cfg)
+    s.set_bc(bc)
+    # the laminar start-up preprocessing: the flow's Preprocessing twice (no turbulence solver between)
+    s.upload("U", st0["U"])
+    s.upload("V", st0["V"])
+    for _ in range(2):
+        s.SetPrimitive_Variables(0)
+        s.SetPrimitive_Gradient()
+        s.SetStrainMag()
+    s.sync()
+    N = len(st0["V"])
+    U0, V0 = s.download("U").reshape(N, -1), s.download("V").reshape(N, -1)
+    rms, rms_t, its = rx.Iterate(s, None, ext_iter=0)
+    s.sync()
+    U = s.download("U").reshape(N, -1)
+    s.close()
+    assert rms_t is None and its[1] == 0
+    zeros = np.zeros(N)
+    st = dict(U=U0, V=V0, sst_sol=np.zeros((N, 2)), sst_F1=zeros, sst_F2=zeros, sst_CDkw=zeros, mu_t=zeros)
+    mesh_o, _, bco, c = outer_iteration_inputs(mesh, st, cfg, bc)
+    c["rans"] = False
+    state = dict(U=U0.copy(), V=V0.copy(), Uold=U0.copy())
+    pat = O.bsr_pattern(N, mesh["edges"])
+    with O.dot_order("device"):
+        o = O.outer_iteration(O.Mechanism(mech), 2, mesh_o, state, bco, c, 0, pat, part_ptr=mesh["part_ptr"],
+                              keep=False)
+    assert its[0] == o["lin_iters"] and "T" not in o
+    cols = [v for v in range(U.shape[1]) if not 1 <= v <= 2]
+    per_column_close(U[:, cols], o["U"][:, cols], rtol=1e-10, floor=1.0, what=f"{variant} U vs oracle")
+    e_sp = species_close(U, o["U"], 2, rtol=1e-10, what=f"{variant} species (elementwise) vs oracle")
+    print(f"{variant}: species elementwise {e_sp:.2e}")
+    mom = np.abs(o["U"][:, 1:3]).max()
+    assert_close(U[:, 1:3], o["U"][:, 1:3], rtol=1e-10, floor=1.0, scale=mom, what=f"{variant} momentum vs oracle")
+    assert_close(rms, o["rms"], rtol=1e-10, what=f"{variant} RMS flow")
+
+
 @pytest.mark.timeout(1200)
 def test_c5_whole_mesh():
     """configs[4] at its stated size on one MI355X: the whole 1000 x 400 x 20 extruded jet (8 000 000 points,
