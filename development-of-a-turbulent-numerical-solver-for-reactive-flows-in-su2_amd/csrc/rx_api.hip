@@ -547,6 +547,14 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
       if (grp_ok) CK(dupload(ctx, &ctx->ilu_gplan, gplan.data(), gplan.size()));
       if (grp_ok) CK(dupload(ctx, &ctx->ilu_gfull, gfull.data(), gfull.size()));
       ctx->ilu_ring_w = rw;
+      // PAIR build (rx_sweeps.hip): meshes whose widest level is at most RX_GRP_PAIR_W rows (the pairs' half as many
+      // rows per round then cost at most two rounds where one did; the C4 rank shape, 490-row partitions with 22-row
+      // levels, takes it, the C3 shape, 62-row levels, does not); RX_GRP_PAIR=0 / 1 forces it off / on
+      {
+        const char* ev = getenv("RX_GRP_PAIR");
+        const int maxw = getenv("RX_GRP_PAIR_W") ? atoi(getenv("RX_GRP_PAIR_W")) : 32;
+        ctx->ilu_pair = grp_ok && (ev ? atoi(ev) != 0 : ctx->fs.maxwidth <= maxw);
+      }
     }
 
     const size_t per_wave = sizeof(double) * ((size_t)(rowmax + 1 + rx_ilu_stage()) * nv * nv + 16);

@@ -111,6 +111,7 @@ struct rx_ctx {
   int32_t* ilu_gplan = nullptr; // [N][32] k_ilu_build_grp's row plans (up to 6 lower blocks, one update each)
   int32_t* ilu_gfull = nullptr; // [forward levels + 1] k_ilu_build_grp: 1 = the level reads an inv(A_jj) from memory
   int ilu_ring_w = 0;           // k_ilu_build_grp's LDS ring of inv(D): rows per level parity (0: no ring)
+  bool ilu_pair = false;        // k_ilu_build_grp with two lane groups per row (PAIR; rows of <= 2 lower blocks)
   int ilu_diag_deferred = 0;    // the ILU field's diagonal blocks are not stored (k_ilu_build_grp, RX_GRP_DIAG_STORE 0)
   // dependency-level schedules of the per-partition lower (fs) / upper (bs) triangular graphs:
   // partition p owns levels [part_lvl[p], part_lvl[p+1]); level l owns rows[lvl_ptr[l] .. lvl_ptr[l+1])

@@ -641,7 +641,14 @@ constexpr int grp_slot_doubles() { return NV * grp_np<NV>() + kPlan; }  // + two
 // (__syncthreads waits vmcnt(0)), and no inv(A_jj) load queues behind them (vmcnt retires in issue order). A level
 // with such a row (its lower neighbour two or more levels back, or past the ring's width) keeps the full barrier.
 // The same values in the same operations: the factor is bitwise the same.
-template <int NV>
+// PAIR (round 6): two groups per row — lane group 2q + role of the workgroup takes row slot q, group `role` makes
+// lower block `role` (W = A_ij inv(A_jj), X = A_ji W) and the helper hands its X to the primary through its LDS slot,
+// which subtracts X_0 then X_1 from D_i in the reference's order and factors D_i alone. The two blocks' products run
+// side by side instead of one after the other (the row's chain is its LDS / FP64 latency, not its loads), for half as
+// many rows per round: the host takes it for the meshes whose rows have at most two lower blocks and whose widest level
+// a round of the pairs covers in at most a few rounds (ctx->ilu_pair, rx_api.hip). The same operations on the same
+// values: the factor is bitwise the same.
+template <int NV, bool PAIR>
 __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const int32_t* __restrict__ part_lvl,
                                                                     const int32_t* __restrict__ lvl_ptr,
                                                                     const int32_t* __restrict__ plan,
@@ -652,6 +659,7 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
   constexpr int NV2 = NV * NV, NP = grp_np<NV>();
   extern __shared__ double lds[];
   const int a = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = blockDim.x >> 4;
+  const int role = PAIR ? (grp & 1) : 0, gslot = PAIR ? (grp >> 1) : grp, nslot = PAIR ? (ngrp >> 1) : ngrp;
   double* S = lds + (size_t)grp * grp_slot_doubles<NV>();  // inv(A_jj), then W, then the LU of D_i
   int* const recb = reinterpret_cast<int*>(S + NV * NP);   // plan records: this row's and the next row's
   const int p = blockIdx.x, l0 = part_lvl[p], l1 = part_lvl[p + 1];
@@ -662,14 +670,14 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
   for (int l = l0 + (int)threadIdx.x; l <= l1; l += blockDim.x) lp[l] = lvl_ptr[l];
   __syncthreads();
   auto next_slot = [&](int r, int l, int& ln) -> int {  // the group's next row after slot r of level l (its level
-    if (r + ngrp < lp[l + 1]) {                         // in ln), -1 if none
+    if (r + nslot < lp[l + 1]) {                        // in ln), -1 if none
       ln = l;
-      return r + ngrp;
+      return r + nslot;
     }
     for (int ll = l + 1; ll < l1; ++ll)
-      if (lp[ll] + grp < lp[ll + 1]) {
+      if (lp[ll] + gslot < lp[ll + 1]) {
         ln = ll;
-        return lp[ll] + grp;
+        return lp[ll] + gslot;
       }
     return -1;
   };
@@ -679,17 +687,17 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
   // stay in flight across the level barrier. Only inv(A_jj) (a row of an earlier level) waits for the barrier.
   auto prefetch = [&](const int* rc, int lane, double (&pd)[NV], double (&pbl)[PB], double (&pjl)[PB]) {
     const int pc = lane < NV ? lane : 0;
-    const int pk0 = rc[1], pkd = rc[2];
+    const int pk0 = rc[1] + role, pkd = rc[2];  // (PAIR: the helper's block is the row's second)
 #pragma unroll
     for (int q = 0; q < NV; ++q) pd[q] = A[(size_t)pkd * NV2 + q * NV + pc];
     if (pkd > pk0) {
 #pragma unroll
       for (int u = 0; u < PB; ++u)
         if (16 * u + lane < NV2) pbl[u] = A[(size_t)pk0 * NV2 + 16 * u + lane];
-      if (rc[14] >= 0) {
+      if (rc[14 + role] >= 0) {
 #pragma unroll
         for (int u = 0; u < PB; ++u)
-          if (16 * u + lane < NV2) pjl[u] = A[(size_t)rc[14] * NV2 + 16 * u + lane];
+          if (16 * u + lane < NV2) pjl[u] = A[(size_t)rc[14 + role] * NV2 + 16 * u + lane];
       }
     }
   };
@@ -714,8 +722,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
   {
     int pr = -1, pl = 0;
     for (int ll = l0; ll < l1 && pr < 0; ++ll)
-      if (lp[ll] + grp < lp[ll + 1]) {
-        pr = lp[ll] + grp;
+      if (lp[ll] + gslot < lp[ll + 1]) {
+        pr = lp[ll] + gslot;
         pl = ll;
       }
     if (pr >= 0) {
@@ -735,7 +743,7 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
     if (tr && trow < kGrpTraceRows) tr[trow * 8 + (ph)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
   for (int l = l0; l < l1; ++l) {
-    for (int r = lp[l] + grp; r < lp[l + 1]; r += ngrp) {
+    for (int r = lp[l] + gslot; r < lp[l + 1]; r += nslot) {
       RX_GSTAMP(0);
       // the lane's column, laundered per row so that nothing derived from it is hoisted out of the row loop
       // (the hoisted unit vectors / addresses otherwise spill)
@@ -754,8 +762,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
       load_second(rec, al, bl2, jl2);
 #endif
       const int rs_own = rec[6];
-      if (kd > k0) {
-        const int j0 = (RX_GRP_PROBE & 1) ? 0 : rec[8], rs0 = rec[20];
+      if (kd > k0 + role) {
+        const int j0 = (RX_GRP_PROBE & 1) ? 0 : rec[8 + role], rs0 = rec[20 + role];
         if (rs0 >= 0) {
 #pragma unroll
           for (int q = 0; q < NV; ++q) s[q] = ring[(size_t)rs0 * NV2 + q * NV + ac];
@@ -771,7 +779,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
         for (int q = 0; q < NV; ++q) s2[q] = invD[(size_t)j1 * NV2 + q * NV + ac];
       }
 #endif
-      for (int k = k0; k < kd; ++k) {
+      constexpr int kstep = PAIR ? 2 : 1;  // PAIR: the primary takes blocks 0, 2, .., the helper 1, 3, ..
+      for (int k = k0 + role; k < kd; k += kstep) {
         const int t = k - k0, nu = rec[14 + t] >= 0 ? 1 : 0;
         wave_sync();
 #pragma unroll
@@ -813,9 +822,10 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
             bl[u] = bl2[u];
             jl[u] = jl2[u];
           }
-        } else if (k + 1 < kd) {  // further lower blocks' loads (not on quad / hex meshes), into the registers
-                                  // just freed (before W's store, so that waiting for them does not wait for it)
-          const int jn = (RX_GRP_PROBE & 1) ? 0 : rec[9 + t], rsn = rec[21 + t];
+        } else if (k + kstep < kd) {  // further lower blocks' loads (not on quad / hex meshes), into the registers
+                                       // just freed (before W's store, so that waiting for them does not wait for it)
+          const int tn = t + kstep;
+          const int jn = (RX_GRP_PROBE & 1) ? 0 : rec[8 + tn], rsn = rec[20 + tn];
           if (rsn >= 0) {
 #pragma unroll
             for (int q = 0; q < NV; ++q) s[q] = ring[(size_t)rsn * NV2 + q * NV + ac];
@@ -823,12 +833,12 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #pragma unroll
             for (int q = 0; q < NV; ++q) s[q] = invD[(size_t)jn * NV2 + q * NV + ac];
           }
-          const size_t kb = (RX_GRP_PROBE & 2) ? 0 : (size_t)(k + 1);
+          const size_t kb = (RX_GRP_PROBE & 2) ? 0 : (size_t)(k + kstep);
 #pragma unroll
           for (int u = 0; u < PB; ++u)
             if (16 * u + al < NV2) bl[u] = A[kb * NV2 + 16 * u + al];
-          if (rec[15 + t] >= 0) {
-            const int kk = (RX_GRP_PROBE & 2) ? 0 : rec[15 + t];
+          if (rec[14 + tn] >= 0) {
+            const int kk = (RX_GRP_PROBE & 2) ? 0 : rec[14 + tn];
 #pragma unroll
             for (int u = 0; u < PB; ++u)
               if (16 * u + al < NV2) jl[u] = A[(size_t)kk * NV2 + 16 * u + al];
@@ -839,8 +849,8 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
           for (int e = 0; e < NV; ++e) F[(size_t)k * NV2 + e * NV + al] = w[e];
         }
         // D_i -= A_ji * W (left-multiply quirk; the block's one update hits the diagonal)
+        double x[NV];
         if (nu > 0) {
-          double x[NV];
 #pragma unroll
           for (int e = 0; e < NV; ++e) x[e] = 0.0;
 #ifdef RX_GRP_TIED1
@@ -853,11 +863,33 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #else
           lds_colprod<NV>(S, w, x);
 #endif
+          if (!PAIR) {
 #pragma unroll
-          for (int e = 0; e < NV; ++e) d[e] -= x[e];
+            for (int e = 0; e < NV; ++e) d[e] -= x[e];
+          }
+        }
+        if (PAIR) {  // blocks t (primary) and t + 1 (helper): the helper's X to its slot, the primary subtracts its
+                     // own X, then the helper's — the reference's block order
+          wave_sync();
+          if (role == 1 && nu > 0 && act) {
+#pragma unroll
+            for (int e = 0; e < NV; ++e) S[e * NV + al] = x[e];
+          }
+          wave_sync();
+          if (role == 0) {
+            if (nu > 0) {
+#pragma unroll
+              for (int e = 0; e < NV; ++e) d[e] -= x[e];
+            }
+            if (k + 1 < kd && rec[15 + t] >= 0) {
+              const double* Sh = S + grp_slot_doubles<NV>();  // the partner's (helper's) slot
+#pragma unroll
+              for (int e = 0; e < NV; ++e) d[e] -= Sh[e * NV + ac];
+            }
+          }
         }
       }
-      if (act && RX_GRP_DIAG_STORE) {  // (the sweeps read inv(D_i) only: rx_la_ilu_materialize remakes D_i)
+      if (act && role == 0 && RX_GRP_DIAG_STORE) {  // (the sweeps read inv(D_i) only: rx_la_ilu_materialize remakes D_i)
 #pragma unroll
         for (int e = 0; e < NV; ++e) F[(size_t)kd * NV2 + e * NV + al] = d[e];
       }
@@ -896,7 +928,7 @@ __global__ __launch_bounds__(64 * grp_waves<NV>()) void k_ilu_build_grp(const in
 #pragma unroll
       for (int rr = 0; rr < NV; ++rr) rhs[rr] = (rr == al) ? 1.0 : 0.0;
       grp_solve_lds<NV, NP>(S, rhs);
-      if (act) {
+      if (act && role == 0) {
 #pragma unroll
         for (int rr = 0; rr < NV; ++rr) invD[(size_t)i * NV2 + rr * NV + al] = rhs[rr];
         if (rs_own >= 0) {
@@ -2396,7 +2428,8 @@ void launch_ilu_build_grp(rx_ctx* ctx, int gwaves) {
     const size_t shm = sizeof(double) * (size_t)(4 * gwaves) * grp_slot_doubles<NV>() +
                        sizeof(double) * (size_t)2 * ctx->ilu_ring_w * NV * NV +
                        sizeof(int32_t) * (size_t)(ctx->fs.maxlev + 1);
-    k_ilu_build_grp<NV><<<ctx->npart, 64 * gwaves, shm, ctx->stream>>>(
+    auto kern = ctx->ilu_pair ? &k_ilu_build_grp<NV, true> : &k_ilu_build_grp<NV, false>;
+    kern<<<ctx->npart, 64 * gwaves, shm, ctx->stream>>>(
         ctx->fs.part_lvl, ctx->fs.lvl_ptr, ctx->ilu_gplan, ctx->f[RX_F_JAC], ctx->f[RX_F_ILU],
         ctx->f[RX_F_ILU] + ctx->nnzb * (int64_t)NV * NV, ctx->ilu_trace, ctx->ilu_gfull, ctx->ilu_ring_w);
     ctx->ilu_diag_deferred = RX_GRP_DIAG_STORE ? 0 : 1;
@@ -2535,9 +2568,12 @@ int rx_la_prepare(rx_ctx* ctx) {
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_apply_ring<NV_, 1024, 2, 8>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
     }
-    if constexpr (NV_ >= 5)
-      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_grp<NV_>),
+    if constexpr (NV_ >= 5) {
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_grp<NV_, false>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+      RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_grp<NV_, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
+    }
     if (NV_ <= 4)
       RX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ilu_build_lds<NV_>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, ctx->lds_max));
