@@ -704,6 +704,13 @@ int create_impl(const rx_mesh_desc* mesh, const rx_mech_desc* mech, const rx_cfg
     m.tx = up(mech->tab_x, (size_t)5 * ns * nt);
     m.ty = up(mech->tab_y, (size_t)5 * ns * nt);
     m.ty2 = up(mech->tab_y2, (size_t)5 * ns * nt);
+    {  // one temperature grid for every (prop, s) row, bitwise: spline_k() shares the interval search (rx_device.h)
+      const double* X = mech->tab_x;
+      bool same = true;
+      for (int r = 1; r < 5 * ns && same; ++r) same = std::memcmp(X, X + (size_t)r * nt, sizeof(double) * nt) == 0;
+      const char* e = getenv("RX_SPLINE_SHARED");  // 0: the per-row search everywhere (the parity tests compare both)
+      m.xshared = (same && !(e && atoi(e) == 0)) ? 1 : 0;
+    }
     {  // the molar masses' reciprocals as the device's division makes them (rx_fdiv.h)
       double* d = nullptr;
       RX_HIP(hipMalloc(&d, sizeof(double) * ns));

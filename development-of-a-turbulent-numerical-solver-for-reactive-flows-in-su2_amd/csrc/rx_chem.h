@@ -24,10 +24,11 @@ struct Kin {
 
 __device__ inline double delta_gibbs(const DevMech& m, int r, double T, double* dnu, int* err) {
   double dG = 0.0, dn = 0.0;
+  const SplineAt k = spline_at(m, T);  // one interval search for every species' H and S rows (rx_device.h)
   for (int s = 0; s < m.ns; ++s) {
     const double dc = m.sp[s * m.nr + r] - m.sr[s * m.nr + r];
     if (dc != 0.0) {
-      dG += dc * (spline(m, P_H, s, T, err) - T * spline(m, P_S, s, T, err));
+      dG += dc * (spline_k(m, P_H, s, T, k, err) - T * spline_k(m, P_S, s, T, k, err));
       dn += dc;
     }
   }

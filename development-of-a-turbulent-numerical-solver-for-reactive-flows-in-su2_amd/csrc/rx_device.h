@@ -39,6 +39,7 @@ struct DevMech {
   const int *rev, *hasb;
   const double *tx, *ty, *ty2;  // [5][ns][ntab]
   double mtot;                  // sum of molar masses
+  int xshared;                  // 1: every tx row is the same grid (spline_at / spline_k)
   // transport constants of the mechanism, evaluated once on the host with the reference's expressions
   // (ComputeEta / ComputeLambda :634-696, GetDij_SM :751-766 of reacting_model_library.cpp):
   const double *phic;           // [ns][ns] sqrt(8 (1 + M_a / M_b))
@@ -85,6 +86,45 @@ __device__ __host__ inline double spline(const DevMech& m, int prop, int s, doub
   const double a = rx_div(x[klo] - T, rh);
   const double b = rx_div(T - x[klo - 1], rh);
   return a * y[klo - 1] + b * y[klo] + ((a * a * a - a) * y2[klo - 1] + (b * b * b - b) * y2[klo]) * (h * h) / 6.0;
+}
+
+// The same spline with the interval search done once per temperature. Every shipped mechanism tabulates all its
+// species and properties on one temperature grid (DevMech::xshared, checked bitwise on the host at upload): then
+// klo, a, b and h of spline() are the same for every (prop, s) row at a given T, and spline_k() returns exactly
+// spline()'s double from them. Without a shared grid spline_k() falls back to spline() row by row.
+struct SplineAt {
+  unsigned long klo;
+  double a, b, hh;
+  bool ok;
+};
+__device__ __host__ inline SplineAt spline_at(const DevMech& m, double T) {
+  SplineAt k{1, 0.0, 0.0, 0.0, false};
+  if (!m.xshared) return k;
+  const double* x = m.tx;
+  const double x0 = x[0], xn = x[m.ntab - 1];
+  if (T < x0 || T > xn) return k;
+  const double h = x[1] - x0;
+  const Recip rh = rx_recip(h);
+  unsigned long klo = (unsigned long)(rx_div(T - x0, rh) + 1);
+  if (klo > (unsigned long)(m.ntab - 1)) klo = m.ntab - 1;
+  k.klo = klo;
+  k.a = rx_div(x[klo] - T, rh);
+  k.b = rx_div(T - x[klo - 1], rh);
+  k.hh = h * h;
+  k.ok = true;
+  return k;
+}
+__device__ __host__ inline double spline_k(const DevMech& m, int prop, int s, double T, const SplineAt& k, int* err) {
+  if (!m.xshared) return spline(m, prop, s, T, err);
+  if (!k.ok) {
+    *err = ERR_RANGE;
+    return 0.0;
+  }
+  const size_t off = (size_t)(prop * m.ns + s) * m.ntab;
+  const double* y = m.ty + off;
+  const double* y2 = m.ty2 + off;
+  const double a = k.a, b = k.b;
+  return a * y[k.klo - 1] + b * y[k.klo] + ((a * a * a - a) * y2[k.klo - 1] + (b * b * b - b) * y2[k.klo]) * k.hh / 6.0;
 }
 
 // ReactingModelLibrary::SetMassFractions + SetMolarFromMass (reacting_model_library.cpp:65-93)

@@ -111,9 +111,10 @@ struct PrimParams {
 
 template <int NS>
 __device__ inline double mix_h(const DevMech& m, double T, const double* Yc, int* err) {
+  const SplineAt k = spline_at(m, T);
   double h = 0.0;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) h += Yc[s] * rx_div(spline(m, P_H, s, T, err), mm_recip(m, s));
+  for (int s = 0; s < NS; ++s) h += Yc[s] * rx_div(spline_k(m, P_H, s, T, k, err), mm_recip(m, s));
   return h;
 }
 
@@ -167,10 +168,14 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
   const double old_temp = V[0];
   double T = V[0], Told = T + 1.0;
   bool conv = false;
+  // h(Told) of an iteration is h(T) of the one before (Told = T there, the same product by T_ref): it is carried
+  // instead of evaluated again; its error flag was the previous iteration's, which went to the bisection if set
+  double hs_prev = 0.0;
   for (int it = 0; it < 7; ++it) {
     int e1 = ERR_NONE;
-    const double hs_old = rx_div(mix_h<NS>(m, Told * P.T_ref, Yc, &e1), rE);
+    const double hs_old = it == 0 ? rx_div(mix_h<NS>(m, Told * P.T_ref, Yc, &e1), rE) : hs_prev;
     const double hs = rx_div(mix_h<NS>(m, T * P.T_ref, Yc, &e1), rE);
+    hs_prev = hs;
     if (e1 != ERR_NONE) {  // std::out_of_range inside the secant: bisection on [Tmin, Tmax], 10000 steps
       double Ta = Tmin, Tb = Tmax;
       for (int b = 0; b < 10000; ++b) {
@@ -243,8 +248,9 @@ __device__ inline bool cons2prim_dev(const DevMech& m, const PrimParams& P, doub
   const double dim_temp = T * P.T_ref;
   int e3 = ERR_NONE;
   double Cp = 0.0;
+  const SplineAt kT = spline_at(m, dim_temp);
 #pragma unroll
-  for (int s = 0; s < NS; ++s) Cp += Yc[s] * rx_div(spline(m, P_CP, s, dim_temp, &e3), mm_recip(m, s));
+  for (int s = 0; s < NS; ++s) Cp += Yc[s] * rx_div(spline_k(m, P_CP, s, dim_temp, kT, &e3), mm_recip(m, s));
   const double gamma = rx_div(Cp, rx_recip(Cp - Rg));
   V[A_] = sqrt(rx_div(gamma * V[P_], rrho));
   if (V[A_] < kEPS) {
@@ -315,10 +321,11 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int lo, in
 #pragma unroll
   for (int d = 0; d < NDIM; ++d) sq += V[VX + d] * V[VX + d];
   int e4 = ERR_NONE;
+  const SplineAt kT = spline_at(m, dim_temp);  // the interval of dim_temp, shared by the H, MU and KAPPA rows below
   double dTdYs[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s)
-    dTdYs[s] = rx_div(rx_div(spline(m, P_H, s, dim_temp, &e4), mm_recip(m, s)) - rx_div(kR, mm_recip(m, s)) * dim_temp,
+    dTdYs[s] = rx_div(rx_div(spline_k(m, P_H, s, dim_temp, kT, &e4), mm_recip(m, s)) - rx_div(kR, mm_recip(m, s)) * dim_temp,
                       rE);
   double* dt = dTdU + (size_t)i * nVar;
   dt[0] = rx_div(0.5 * sq, rcv);
@@ -341,40 +348,33 @@ __global__ __launch_bounds__(kBlock) RX_WPE_PRIM void k_set_primitive(int lo, in
   double visc[NS], cond[NS], yom[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    visc[s] = spline(m, P_MU, s, dim_temp, &e4);
-    cond[s] = spline(m, P_KAPPA, s, dim_temp, &e4);
+    visc[s] = spline_k(m, P_MU, s, dim_temp, kT, &e4);
+    cond[s] = spline_k(m, P_KAPPA, s, dim_temp, kT, &e4);
     yom[s] = rx_div(Yc[s], mm_recip(m, s));
   }
   Recip rvisc[NS];  // visc[b] divides visc[a] for every a (rx_fdiv.h)
 #pragma unroll
   for (int b = 0; b < NS; ++b) rvisc[b] = rx_recip(visc[b]);
-  double eta = 0.0;
+  // ComputeEta and ComputeLambda side by side: Wilke's factor f(a, b) is the same expression in both, so it is
+  // evaluated once per pair; each phi still sums over b, and eta / lam over a, in the reference's order
+  double yoml[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) yoml[s] = rx_div(Ys[s], mm_recip(m, s));  // ComputeLambda: the unclamped argument
+  double eta = 0.0, lam = 0.0;
 #pragma unroll RX_PRIM_UNROLL
   for (int a = 0; a < NS; ++a) {
-    double phi = 0.0;
+    double phi = 0.0, phl = 0.0;
 #pragma unroll
     for (int b = 0; b < NS; ++b) {
       const double f = 1.0 + sqrt(rx_div(visc[a], rvisc[b])) * m.pw25[a * NS + b];
       phi += rx_div(yom[b], phic_recip(m, a * NS + b)) * f * f;
+      if (b != a) phl += rx_div(1.065 * yoml[b], phic_recip(m, a * NS + b)) * f * f;
     }
+    phl += yoml[a];
     eta += rx_div(visc[a] * yom[a], rx_recip(phi));
+    lam += rx_div(cond[a] * yoml[a], rx_recip(phl));
   }
   mu[i] = rx_div(eta, rx_recip(P.Visc_ref));
-#pragma unroll
-  for (int s = 0; s < NS; ++s) yom[s] = rx_div(Ys[s], mm_recip(m, s));  // ComputeLambda: the unclamped argument
-  double lam = 0.0;
-#pragma unroll RX_PRIM_UNROLL
-  for (int a = 0; a < NS; ++a) {
-    double phi = 0.0;
-#pragma unroll
-    for (int b = 0; b < NS; ++b)
-      if (b != a) {
-        const double f = 1.0 + sqrt(rx_div(visc[a], rvisc[b])) * m.pw25[a * NS + b];
-        phi += rx_div(1.065 * yom[b], phic_recip(m, a * NS + b)) * f * f;
-      }
-    phi += yom[a];
-    lam += rx_div(cond[a] * yom[a], rx_recip(phi));
-  }
   kappa[i] = rx_div(lam, rx_recip(P.Cond_ref));
   const double pT = 1.0e-3 * pow175_cr(dim_temp);
   const double scale = P.Vel_ref * P.Len_ref * 1.0e4;

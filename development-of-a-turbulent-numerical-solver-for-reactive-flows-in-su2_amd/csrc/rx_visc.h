@@ -499,8 +499,9 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   double hs[NS];
   {
     const Recip rE = rx_recip(P.E_ref);
+    const SplineAt kT = spline_at(m, dim_temp);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) hs[s] = rx_div(rx_div(spline(m, P_H, s, dim_temp, &err), mm_recip(m, s)), rE);
+    for (int s = 0; s < NS; ++s) hs[s] = rx_div(rx_div(spline_k(m, P_H, s, dim_temp, kT, &err), mm_recip(m, s)), rE);
   }
   double PF[nVar];
 #pragma unroll
@@ -523,8 +524,9 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
     Mean_tke = 0.5 * (ni.tke + nj.tke);
     {
       const Recip rR = rx_recip(P.R_ref);
+      const SplineAt kT = spline_at(m, dim_temp);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) Cps[s] = rx_div(rx_div(spline(m, P_CP, s, dim_temp, &err), mm_recip(m, s)), rR);
+      for (int s = 0; s < NS; ++s) Cps[s] = rx_div(rx_div(spline_k(m, P_CP, s, dim_temp, kT, &err), mm_recip(m, s)), rR);
     }
     {
       const Scr Mt = scr;  // LDS scratch of this lane (NS*NS), Gt is dead here
@@ -668,8 +670,9 @@ __device__ inline int visc_edge(const DevMech& m, const ViscParams& P, const Vis
   for (int d = 0; d < NDIM; ++d) theta += UN[d] * UN[d];
   if (!P.rans) {
     const Recip rR = rx_recip(P.R_ref);
+    const SplineAt kT = spline_at(m, dim_temp);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) Cps[s] = rx_div(rx_div(spline(m, P_CP, s, dim_temp, &err), mm_recip(m, s)), rR);
+    for (int s = 0; s < NS; ++s) Cps[s] = rx_div(rx_div(spline_k(m, P_CP, s, dim_temp, kT, &err), mm_recip(m, s)), rR);
   }
   double totMass = 0.0, totMass_i = 0.0, totMass_j = 0.0, sigma_i = 0.0, sigma_j = 0.0;
 #pragma unroll

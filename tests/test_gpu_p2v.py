@@ -72,3 +72,35 @@ def test_device_resident_iteration_vs_oracle():
         R[j] -= r[e]
     assert np.array_equal(s.download("RES").reshape(N, -1), R)
     s.close()
+
+
+def _iteration_fields(shared, monkeypatch):
+    monkeypatch.setenv("RX_SPLINE_SHARED", "1" if shared else "0")  # read when the mechanism is uploaded
+    mesh, st, mech_arrays, kw = synth.jet_case(40, 16, n_species=7)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), rx.default_cfg(implicit=1, lin_prec=1, cfl=0.5, **kw))
+    s.set_state(st)
+    s.SetPrimitive_Gradient_LS()
+    s.SetTime_Step()
+    s.Preprocessing_zero()
+    s.Upwind_Residual()
+    s.Viscous_Residual()
+    s.Source_Residual()
+    out = {"RES": s.download("RES")}
+    s.ImplicitEuler_Iteration()
+    s.SetPrimitive_Variables()
+    s.sync()
+    for f in ("U", "V", "DPDU", "DTDU", "MU", "KAPPA", "DIJ"):
+        out[f] = s.download(f)
+    s.close()
+    return out
+
+
+def test_shared_grid_spline_matches_per_row(monkeypatch):
+    """The spline interval searched once per temperature (every table on one grid: DevMech::xshared, rx_device.h
+    spline_at / spline_k) against the per-row search (RX_SPLINE_SHARED=0): the secant's enthalpies, Cp, H, mu,
+    kappa, the viscous flux's H and Cp rows and the source's Gibbs energies, through one implicit outer iteration
+    (residual, solve, primitives), bitwise."""
+    a = _iteration_fields(True, monkeypatch)
+    b = _iteration_fields(False, monkeypatch)
+    for f in a:
+        assert np.array_equal(a[f], b[f]), f
