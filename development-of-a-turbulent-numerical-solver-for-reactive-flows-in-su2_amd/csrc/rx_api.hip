@@ -863,10 +863,7 @@ int rx_ctx_destroy(rx_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   // the captured solve first: a graph holding RCCL work keeps the communicator's persistent resources, and
   // ncclCommDestroy waits for them (the self-halo RCCL test hung here with the graph destroyed after the comm)
-  if (ctx->solve_exec) (void)hipGraphExecDestroy(ctx->solve_exec);
-  if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
-  ctx->solve_exec = nullptr;
-  ctx->solve_graph = nullptr;
+  rx_graph_reset(ctx);
   if (ctx->kind == RX_KIND_SST && ctx->flow) --ctx->flow->n_children;
   void* ptrs[] = {ctx->edges, ctx->normal, ctx->coord, ctx->vol, ctx->adj_ptr, ctx->adj, ctx->adj_blk, ctx->edge_blk, ctx->asmes_wg, ctx->asmes_side, ctx->nbr_ptr,
                   ctx->nbr, ctx->bv_ptr, ctx->bv_normal, ctx->rp, ctx->col, ctx->diag, ctx->klo, ctx->khi, ctx->part_ptr, ctx->upd_ptr, ctx->upd, ctx->ilu_plan, ctx->ilu_gplan, ctx->ilu_gfull,
@@ -1184,6 +1181,56 @@ int enqueue_solve(rx_ctx* ctx) {
   return ctx->kind == RX_KIND_SST ? rx_sst_update(ctx) : rx_la_implicit_update(ctx);
 }
 
+// The same sequence as enqueue_solve for FGMRES, in two parts: iterations [0, c), then (split_tail) iterations
+// [i0, m) + finish + RMS + update. An FGMRES that has stopped after c iterations leaves iterations c .. m - 1 as
+// launches that return at their first instruction (≈ 4.4 µs each at the C4 rank shape, one per dependent kernel);
+// the SST solve stops after 2 of its 5, so its 3 x (10-14) empty launches are skipped when the host finds it stopped.
+int enqueue_solve_head(rx_ctx* ctx, int c) {
+  static const bool x_product = getenv("RX_FG_X_PRODUCT") != nullptr;
+  ctx->solve_iters = -1;
+  return rx_la_fgmres_enqueue_part(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter, !x_product, 0, c, false);
+}
+int enqueue_solve_tail(rx_ctx* ctx, int i0) {
+  int rc;
+  if ((rc = rx_la_fgmres_enqueue_part(ctx, ctx->cfg.lin_tol, ctx->cfg.lin_iter, false, i0, ctx->cfg.lin_iter, true)))
+    return rc;
+  if ((rc = rx_la_rms_enqueue(ctx, ctx->f[RX_F_RHS]))) return rc;
+  return ctx->kind == RX_KIND_SST ? rx_sst_update(ctx) : rx_la_implicit_update(ctx);
+}
+
+// The split point of this solve: 0 (whole) unless FGMRES stopped early in the previous solve (or RX_FG_SPLIT=c).
+int solve_split(const rx_ctx* ctx) {
+  if (ctx->cfg.lin_solver != RX_LIN_FGMRES) return 0;
+  const char* e = getenv("RX_FG_SPLIT");
+  const int fixed = (e && e[0]) ? atoi(e) : -1;
+  const int c = fixed >= 0 ? fixed : ctx->fg_split;
+  return (c > 0 && c < ctx->cfg.lin_iter && c < rx_ctx::kSplitMax) ? c : 0;
+}
+
+int enqueue_solve_whole(rx_ctx* ctx, int) { return enqueue_solve(ctx); }
+
+// Run fn(ctx, arg) captured once into (*gr, *ex) and replayed, or eagerly when graphs are off.
+int run_graph(rx_ctx* ctx, bool graphs, hipGraph_t* gr, hipGraphExec_t* ex, int (*fn)(rx_ctx*, int), int arg) {
+  if (!graphs) return fn(ctx, arg);
+  if (!*ex) {
+    RX_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    ctx->capturing = true;
+    const int rc = fn(ctx, arg);
+    ctx->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    if (e != hipSuccess) return rx_fail_hip(ctx, e);
+    *gr = g;
+    RX_HIP(hipGraphInstantiate(ex, g, nullptr, nullptr, 0));
+  }
+  RX_HIP(hipGraphLaunch(*ex, ctx->stream));
+  return RX_OK;
+}
+
 // The solve is replayed as a graph unless RX_NO_GRAPH=1 or a host-staged transport is attached
 // (its exchanges synchronise with the host).
 bool graphs_enabled(const rx_ctx* ctx) {
@@ -1200,6 +1247,13 @@ void rx_graph_reset(rx_ctx* ctx) {
   if (ctx->solve_graph) (void)hipGraphDestroy(ctx->solve_graph);
   ctx->solve_exec = nullptr;
   ctx->solve_graph = nullptr;
+  for (int p = 0; p < 2; ++p)
+    for (int c = 0; c < rx_ctx::kSplitMax; ++c) {
+      if (ctx->split_exec[p][c]) (void)hipGraphExecDestroy(ctx->split_exec[p][c]);
+      if (ctx->split_graph[p][c]) (void)hipGraphDestroy(ctx->split_graph[p][c]);
+      ctx->split_exec[p][c] = nullptr;
+      ctx->split_graph[p][c] = nullptr;
+    }
 }
 
 extern "C" {
@@ -1225,38 +1279,39 @@ int implicit_solve(rx_ctx* ctx, double* res_rms, int* lin_iters) {
   }
   {
     RxPhase ph(ctx, sst ? RX_K_SST_SOLVE : RX_K_SOLVE);
-    if (graphs_enabled(ctx) && rx_la_solve_capturable(ctx)) {
+    const bool graphs = graphs_enabled(ctx) && rx_la_solve_capturable(ctx);
+    if (graphs) {
       const uint64_t epoch = (sst && ctx->flow ? ctx->flow : ctx)->bc_epoch;
-      if (ctx->solve_exec && ctx->graph_epoch != epoch) rx_graph_reset(ctx);
-      if (!ctx->solve_exec) {
+      if (ctx->graph_epoch != epoch) {
+        rx_graph_reset(ctx);
         ctx->graph_epoch = epoch;
-        RX_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-        ctx->capturing = true;
-        rc = enqueue_solve(ctx);
-        ctx->capturing = false;
-        hipGraph_t g = nullptr;
-        const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
-        if (rc) {
-          if (g) (void)hipGraphDestroy(g);
-          return rc;
-        }
-        if (e != hipSuccess) return rx_fail_hip(ctx, e);
-        ctx->solve_graph = g;
-        RX_HIP(hipGraphInstantiate(&ctx->solve_exec, g, nullptr, nullptr, 0));
       }
-      RX_HIP(hipGraphLaunch(ctx->solve_exec, ctx->stream));
-    } else {
-      if ((rc = enqueue_solve(ctx))) return rc;
     }
+    const int c = solve_split(ctx);
+    if (c == 0) {
+      rc = run_graph(ctx, graphs, &ctx->solve_graph, &ctx->solve_exec, enqueue_solve_whole, 0);
+    } else {
+      bool stopped = false;
+      rc = run_graph(ctx, graphs, &ctx->split_graph[0][c], &ctx->split_exec[0][c], enqueue_solve_head, c);
+      if (!rc) rc = rx_la_fgmres_stopped(ctx, &stopped);
+      const int i0 = stopped ? 0 : c;  // [1][0]: finish + RMS + update alone
+      if (!rc)
+        rc = run_graph(ctx, graphs, &ctx->split_graph[1][i0], &ctx->split_exec[1][i0],
+                       enqueue_solve_tail, stopped ? ctx->cfg.lin_iter : c);
+    }
+    if (rc) return rc;
     // the flow's Set_MPI_Solution after the update, on comm_stream (rx_u_exchange_deferred), overlapping the owned
     // points of the next SetPrimitive_Variables
     if (rx_u_exchange_deferred(ctx) && (rc = rx_la_u_exchange_begin(ctx))) return rc;
   }
-  if (res_rms && (rc = rx_la_rms_read(ctx, res_rms))) return rc;
+  if (res_rms && (rc = rx_la_rms_copy(ctx))) return rc;
   int it = 0;
   double resid = 0.0;
-  if ((rc = rx_la_fgmres_result(ctx, &it, &resid))) return rc;
+  rc = rx_la_fgmres_result(ctx, &it, &resid);  // one host wait for both copies
+  if (res_rms && (rc == RX_OK || rc == RX_ERR_DIVERGED)) rx_la_rms_finish(ctx, res_rms);
+  if (rc) return rc;
   if (lin_iters) *lin_iters = ctx->solve_iters >= 0 ? ctx->solve_iters : it;
+  ctx->fg_split = it;  // the next solve's split point (solve_split)
   return RX_OK;
 }
 }  // namespace

@@ -190,6 +190,13 @@ struct rx_ctx {
   uint64_t bc_epoch = 0;
   uint64_t graph_epoch = 0;
   hipGraph_t solve_graph = nullptr;
+  // the FGMRES solve in two captured parts with a host check between them (implicit_solve): [0][c] iterations
+  // [0, c), [1][c] iterations [c, m) + finish + RMS + update, [1][0] finish + RMS + update alone. fg_split: the
+  // split point, the previous solve's iteration count (RX_FG_SPLIT: 0 off, n > 0 fixed)
+  static constexpr int kSplitMax = 65;
+  hipGraphExec_t split_exec[2][kSplitMax] = {};
+  hipGraph_t split_graph[2][kSplitMax] = {};
+  int fg_split = 0;
   bool capturing = false;
 
   // ---- boundary conditions (rx_bc.hip, rx_bc_set); the SST context reads its flow context's
@@ -308,6 +315,11 @@ int rx_la_krylov_alloc(rx_ctx* ctx, int m);
 // Drop the captured solve graph (its kernel arguments point at buffers about to be replaced).
 void rx_graph_reset(rx_ctx* ctx);
 int rx_la_fgmres_enqueue(rx_ctx* ctx, double tol, int m, bool x_zero);  // x_zero: SOL is all +0.0
+int rx_la_fgmres_enqueue_part(rx_ctx* ctx, double tol, int m, bool x_zero, int i0, int i1, bool finish);
+int rx_la_fgmres_stopped(rx_ctx* ctx, bool* stopped);  // synchronises: the partial solve has stopped
+int rx_la_rms_copy(rx_ctx* ctx);                           // rx_la_rms_read's copy to the host (no wait)
+void rx_la_rms_finish(const rx_ctx* ctx, double* rms);  // ... and its RMS from the copied sums
+int rx_la_host_wait(rx_ctx* ctx);  // waits for ctx->stream's work so far
 int rx_la_fgmres_result(rx_ctx* ctx, int* iters, double* resid);
 int rx_la_fgmres(rx_ctx* ctx, double tol, int m, int* iters, double* resid);
 // the other Krylov / smoother branches of CSysSolve::Solve (rx_krylov.hip); results via rx_la_fgmres_result

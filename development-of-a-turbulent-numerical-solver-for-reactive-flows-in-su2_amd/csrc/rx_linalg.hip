@@ -253,13 +253,20 @@ int rx_la_rms_enqueue(rx_ctx* ctx, const double* r) {
 }
 
 int rx_la_rms_read(rx_ctx* ctx, double* rms) {
-  const int nv = ctx->nVar;
+  int rc = rx_la_rms_copy(ctx);
+  if (!rc) rc = rx_la_host_wait(ctx);
+  if (!rc) rx_la_rms_finish(ctx, rms);
+  return rc;
+}
+// the read-back in two halves, so that one host wait covers it and the FGMRES state (implicit_solve)
+int rx_la_rms_copy(rx_ctx* ctx) {
   const double* src = ctx->rms_sum + (ctx->distributed() ? 16 : 0);
-  RX_HIP(hipMemcpyAsync(ctx->h_red, src, sizeof(double) * nv, hipMemcpyDeviceToHost, ctx->stream));
-  RX_HIP(hipStreamSynchronize(ctx->stream));
-  for (int v = 0; v < nv; ++v)
-    rms[v] = std::max(rx::kEPS * rx::kEPS, std::sqrt(ctx->h_red[v] / (double)ctx->n_global));
+  RX_HIP(hipMemcpyAsync(ctx->h_red, src, sizeof(double) * ctx->nVar, hipMemcpyDeviceToHost, ctx->stream));
   return RX_OK;
+}
+void rx_la_rms_finish(const rx_ctx* ctx, double* rms) {
+  for (int v = 0; v < ctx->nVar; ++v)
+    rms[v] = std::max(rx::kEPS * rx::kEPS, std::sqrt(ctx->h_red[v] / (double)ctx->n_global));
 }
 
 // Owned points, then Set_MPI_Solution (solver_direct_reactive.cpp:2403, 2445).

@@ -122,3 +122,53 @@ def test_sst_step_vs_oracle(n_part, prec):
     assert_close(t.download("MUT"), info["mut"], what="mu_t")
     assert_close(t.download("F1"), info["F1"], what="F1")
     s.close()
+
+
+def _split_run(split, monkeypatch):
+    if split is None:
+        monkeypatch.delenv("RX_FG_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("RX_FG_SPLIT", str(split))
+    mesh, st, mech_arrays, kw = synth.jet_case(48, 20, n_species=7, n_part=8)
+    s = rx.ReactiveNSSolver(mesh, rx.Mechanism(mech_arrays), rx.default_cfg(implicit=1, lin_prec=1, **kw))
+    s.set_state(st)
+    t = rx.TurbSSTSolver(mesh, s, rx.sst_cfg(lin_prec=1))
+    t.set_state(st["sst_sol"], mesh["wall_distance"], st["sst_F1"], st["sst_F2"], st["sst_CDkw"])
+    out = []
+    for _ in range(3):
+        s.SetPrimitive_Gradient_LS()
+        s.SetStrainMag()
+        s.SetTime_Step()
+        t.Preprocessing()
+        t.Upwind_Residual()
+        t.Viscous_Residual()
+        t.Source_Residual()
+        rms_t, it_t = t.ImplicitEuler_Iteration()
+        t.Postprocessing()
+        s.Preprocessing_zero()
+        s.Upwind_Residual()
+        s.Viscous_Residual()
+        s.Source_Residual()
+        rms_f, it_f = s.ImplicitEuler_Iteration()
+        s.SetPrimitive_Variables()
+        s.sync()
+        out.append((it_t, it_f, list(rms_t), list(rms_f), t.download("U"), t.download("SOL"), s.download("U"),
+                    s.download("SOL")))
+    s.close()
+    return out
+
+
+def test_fgmres_split_solve_bitwise(monkeypatch):
+    """The FGMRES solve enqueued in two parts with the host's stop check between them (implicit_solve: the split at
+    the previous solve's iteration count, RX_FG_SPLIT=c fixed, 0 off) runs the kernels of the whole solve or skips
+    only launches that would return at once: three flow + SST outer iterations bitwise equal for the whole solve,
+    the adaptive split, a split after 1 iteration (the continuing tail) and after 2."""
+    ref = _split_run(0, monkeypatch)
+    assert any(r[0] < 5 for r in ref), "the SST solve stops early (the split is exercised)"
+    for split in (None, 1, 2):
+        got = _split_run(split, monkeypatch)
+        for a, b in zip(ref, got):
+            assert a[0] == b[0] and a[1] == b[1], (split, a[:2], b[:2])
+            assert a[2] == b[2] and a[3] == b[3], split
+            for x, y in zip(a[4:], b[4:]):
+                assert np.array_equal(x, y), split
