@@ -163,7 +163,9 @@ def kernel_models(N, E, nnzb, ns, nDim, lin_iter, parts=256, workload_key=None, 
         # block of A in once (the lower blocks and the diagonal of row i, the upper blocks as the A_ji of the rows
         # below), the lower factor blocks W, the factored diagonal and inv(D_i) out. k_ilu_build_part (other meshes,
         # RX_ILU_ROWWAVE=1): A in, the whole factor + inv(D) out
-        "ILU_BUILD": (hbm((nnzb + (nnzb - N) // 2 + 2 * N) * blk, "k_ilu_build_grp" + tv) if ilu_grouped else
+        # (<nVar, false>: one lane group per row, the bench meshes' levels are wider than RX_GRP_PAIR_W)
+        "ILU_BUILD": (hbm((nnzb + (nnzb - N) // 2 + 2 * N) * blk, "k_ilu_build_grp" + tv[:-1] + ", false>")
+                      if ilu_grouped else
                       hbm((2 * nnzb + N) * blk, "k_ilu_build_part" + tv)),
         # SOLVE phase (inside the FGMRES graph; timed by an eager replay of one step after the timed region):
         # FGMRES's w = A z (k_fg_spmv_stage for the flow blocks, k_fg_spmv_full for the SST's 2x2): every block + its
