@@ -1422,9 +1422,14 @@ __global__ __launch_bounds__(64) void k_ilu_build_2w(const int32_t* __restrict__
 // addresses) so the wait counts stay static. Rows with more than kB2 blocks on a side take the rest with direct
 // loads. Arithmetic as k_ilu_fwd_wide / k_ilu_bwd_wide, operation for operation.
 #ifndef RX_SST_D2
-#define RX_SST_D2 3  // build knob: passes of blocks in flight ahead of the pass being computed
+#define RX_SST_D2 4  // build knob: passes of blocks in flight ahead of the pass being computed (divides 8: RX_SST_UNROLL)
 #endif
-constexpr int kD2 = RX_SST_D2, kS2 = kD2 + 5 > 8 ? kD2 + 5 : 8;
+#ifndef RX_SST_UNROLL
+#define RX_SST_UNROLL 1  // build knob: unroll the 2x2 sweeps' pass loop by the slot ring's length (8), so that the
+#endif                   // rings of slots and blocks rotate by renaming instead of register moves (kD2 must divide 8;
+                         // SST_SOLVE 0.85 -> 0.68 ms at C3, profiles/r06_ab_ap.txt)
+constexpr int kD2 = RX_SST_D2, kS2 = RX_SST_UNROLL ? 8 : (kD2 + 5 > 8 ? kD2 + 5 : 8);
+static_assert(!RX_SST_UNROLL || (8 % kD2 == 0 && kD2 < 8), "RX_SST_UNROLL: kD2 must divide the slot ring");
 struct Row2 {
   int c[kB2];        // block columns
   double f[kB2][4];  // blocks
@@ -1465,6 +1470,9 @@ __device__ __forceinline__ void sweep2(const int4* __restrict__ slot, const int3
   Row2 R[kD2];  // blocks of passes q .. q + kD2 - 1
 #pragma unroll
   for (int d = 0; d < kD2; ++d) row2_load<BWD>(S[d], col, F, invD, R[d]);
+#if RX_SST_UNROLL
+#pragma unroll 8
+#endif
   for (int q = q0; q < q1; ++q) {
     const bool act = pass_lo[q] + lane < pass_lo[q + 1];
     const int4 sc = S[0];
